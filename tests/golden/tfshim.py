@@ -1,0 +1,264 @@
+"""Eager numpy stand-ins for the TF-1.x / OpenCV calls the reference's hot path makes.
+
+Used ONLY by make_golden.py to execute the reference's own graph-builder code
+(/root/reference/unet.py, unet_simple.py, small.py, refine.py, flow.py,
+train.py loss helpers) verbatim, since TensorFlow and OpenCV are not in this
+image.  Written literally from the library kernels' documented behaviour and
+deliberately independent of oracle/ops.py (different code paths: einsum
+convolution, per-axis interpolation tables, explicit window loops), so the
+golden-vs-oracle test cross-checks two restatements.
+
+Every variable the reference creates is recorded (scope path, shape, values)
+so that tests can check the product's weight construction against the
+reference's draw order.
+"""
+
+import contextlib
+import types
+
+import numpy as np
+
+DTYPE = np.float64
+
+
+class _Registry:
+    def __init__(self):
+        self.scope = []
+        self.variables = []  # (full_name, array)
+
+    def add(self, name, value):
+        full = "/".join(self.scope + [name])
+        self.variables.append((full, np.array(value)))
+        return np.asarray(value)
+
+
+REG = _Registry()
+
+
+@contextlib.contextmanager
+def variable_scope(name, *a, **k):
+    REG.scope.append(name)
+    try:
+        yield
+    finally:
+        REG.scope.pop()
+
+
+def get_variable(name=None, initializer=None, **k):
+    return REG.add(name, initializer)
+
+
+def Variable(value, name=None, **k):
+    return REG.add(name or "Variable", value)
+
+
+def constant(value, name=None, **k):
+    return np.asarray(value)
+
+
+# ------------------------------------------------------------------ nn ops
+
+def conv2d(x, filt, strides, padding, **k):
+    assert list(strides) == [1, 1, 1, 1] and padding == "SAME"
+    x = np.asarray(x, DTYPE)
+    filt = np.asarray(filt, DTYPE)
+    kh, kw, ci, co = filt.shape
+    n, h, w, c = x.shape
+    assert c == ci, (x.shape, filt.shape)
+    ph, pw = (kh - 1) // 2, (kw - 1) // 2  # SAME, stride 1, odd kernel: pad_before = (k-1)//2
+    xp = np.pad(x, ((0, 0), (ph, kh - 1 - ph), (pw, kw - 1 - pw), (0, 0)))
+    out = np.zeros((n, h, w, co), DTYPE)
+    for a in range(kh):
+        for b in range(kw):
+            out += np.einsum("nhwc,co->nhwo", xp[:, a:a + h, b:b + w, :], filt[a, b], optimize=True)
+    return out
+
+
+def bias_add(x, b, **k):
+    return np.asarray(x, DTYPE) + np.asarray(b, DTYPE)
+
+
+def relu(x, name=None):
+    x = np.asarray(x, DTYPE)
+    return np.where(x > 0, x, 0.0)
+
+
+def sigmoid(x, name=None):
+    from scipy.special import expit
+    return expit(np.asarray(x, DTYPE))
+
+
+def softmax(x, axis=-1, name=None):
+    x = np.asarray(x, DTYPE)
+    z = np.exp(x - x.max(axis=axis, keepdims=True))
+    return z / z.sum(axis=axis, keepdims=True)
+
+
+def max_pool(x, ksize, strides, padding, name=None):
+    assert padding == "SAME"
+    x = np.asarray(x, DTYPE)
+    n, h, w, c = x.shape
+    k, s = ksize[1], strides[1]
+    oh, ow = -(-h // s), -(-w // s)
+    pad_h = max((oh - 1) * s + k - h, 0)
+    pad_w = max((ow - 1) * s + k - w, 0)
+    top, left = pad_h // 2, pad_w // 2
+    out = np.full((n, oh, ow, c), -np.inf, DTYPE)
+    for a in range(k):
+        for b in range(k):
+            rows = np.arange(oh) * s - top + a
+            cols = np.arange(ow) * s - left + b
+            rv = (rows >= 0) & (rows < h)
+            cv = (cols >= 0) & (cols < w)
+            tap = np.full((n, oh, ow, c), -np.inf, DTYPE)
+            sub = x[:, np.clip(rows, 0, h - 1)][:, :, np.clip(cols, 0, w - 1)]
+            mask = rv[None, :, None, None] & cv[None, None, :, None]
+            tap = np.where(mask, sub, tap)
+            out = np.maximum(out, tap)
+    return out
+
+
+def _interp_table(out_size, in_size):
+    # tensorflow/core/kernels/resize_bilinear_op.cc, legacy scaler: scale = (float)in/out,
+    # in = (float)i * scale, lower = floor(in), upper = min(ceil(in), in-1), lerp = in - floor(in)
+    scale = np.float32(in_size) / np.float32(out_size)
+    lo = np.empty(out_size, np.int64)
+    hi = np.empty(out_size, np.int64)
+    lerp = np.empty(out_size, np.float32)
+    for i in range(out_size):
+        v = np.float32(i) * scale
+        f = np.floor(v)
+        lo[i] = max(int(f), 0)
+        hi[i] = min(int(np.ceil(v)), in_size - 1)
+        lerp[i] = v - f
+    return lo, hi, lerp
+
+
+def resize_images(images, size, **k):
+    images = np.asarray(images, DTYPE)
+    n, ih, iw, c = images.shape
+    oh, ow = int(size[0]), int(size[1])
+    if (oh, ow) == (ih, iw):
+        return images
+    ylo, yhi, ylerp = _interp_table(oh, ih)
+    xlo, xhi, xlerp = _interp_table(ow, iw)
+    out = np.empty((n, oh, ow, c), DTYPE)
+    for y in range(oh):
+        top_row = images[:, ylo[y]]
+        bot_row = images[:, yhi[y]]
+        tl, tr = top_row[:, xlo], top_row[:, xhi]
+        bl, br = bot_row[:, xlo], bot_row[:, xhi]
+        xl = xlerp.astype(DTYPE)[None, :, None]
+        top = tl + (tr - tl) * xl
+        bot = bl + (br - bl) * xl
+        out[:, y] = top + (bot - top) * DTYPE(ylerp[y])
+    return out
+
+
+def batch_norm(x, center=True, scale=True, is_training=False, scope=None, epsilon=0.001, **k):
+    x = np.asarray(x, DTYPE)
+    c = x.shape[-1]
+    with variable_scope(scope or "BatchNorm"):
+        beta = get_variable("beta", np.zeros(c, np.float32)) if center else np.zeros(c)
+        gamma = get_variable("gamma", np.ones(c, np.float32)) if scale else np.ones(c)
+        mm = get_variable("moving_mean", np.zeros(c, np.float32))
+        mv = get_variable("moving_variance", np.ones(c, np.float32))
+    if bool(is_training):
+        mean = x.reshape(-1, c).mean(axis=0)
+        var = np.square(x.reshape(-1, c) - mean).mean(axis=0)  # fused_batch_norm normalises with the biased variance
+    else:
+        mean, var = mm.astype(DTYPE), mv.astype(DTYPE)
+    return (x - mean) / np.sqrt(var + epsilon) * gamma.astype(DTYPE) + beta.astype(DTYPE)
+
+
+def concat(values=None, axis=0, name=None, **k):
+    return np.concatenate([np.asarray(v, DTYPE) for v in values], axis=axis)
+
+
+def split(value, num_or_size_splits, axis=0, **k):
+    v = np.asarray(value, DTYPE)
+    if isinstance(num_or_size_splits, int):
+        return np.split(v, num_or_size_splits, axis=axis)
+    idx = np.cumsum(num_or_size_splits)[:-1]
+    return np.split(v, idx, axis=axis)
+
+
+def _binary(f):
+    return lambda a, b, name=None: f(np.asarray(a, DTYPE), np.asarray(b, DTYPE))
+
+
+def make_tf():
+    tf = types.ModuleType("tensorflow")
+    tf.variable_scope = variable_scope
+    tf.get_variable = get_variable
+    tf.Variable = Variable
+    tf.constant = constant
+    tf.concat = concat
+    tf.split = split
+    tf.add = _binary(np.add)
+    tf.subtract = _binary(np.subtract)
+    tf.multiply = _binary(np.multiply)
+    tf.square = lambda x, name=None: np.square(np.asarray(x, DTYPE))
+    tf.sqrt = lambda x, name=None: np.sqrt(np.asarray(x, DTYPE))
+    tf.reduce_mean = lambda x, axis=None, name=None: np.mean(np.asarray(x, DTYPE), axis=axis)
+    tf.nn = types.SimpleNamespace(conv2d=conv2d, bias_add=bias_add, relu=relu, sigmoid=sigmoid,
+                                  softmax=softmax, max_pool=max_pool)
+    tf.image = types.SimpleNamespace(resize_images=resize_images)
+    tf.contrib = types.SimpleNamespace(layers=types.SimpleNamespace(batch_norm=batch_norm))
+    return tf
+
+
+# ------------------------------------------------------------------ OpenCV stand-in (remap only)
+
+INTER_LINEAR = 1
+
+
+def remap(src, map1, map2, interpolation):
+    """cv2.remap(src, map1 CV_32FC2, None, INTER_LINEAR), BORDER_CONSTANT 0 — per OpenCV 3.x
+    imgwarp.cpp: X = cvRound(x*32), sx = X>>5, table index (Y&31)*32+(X&31); fully-inside
+    pixels sum S0*w0+S1*w1+S2*w2+S3*w3; border pixels take 0 for every tap outside."""
+    assert map2 is None and interpolation == INTER_LINEAR
+    src = np.asarray(src)
+    h, w = map1.shape[:2]
+    X = np.rint(map1[..., 0].astype(np.float64) * 32).astype(np.int64)
+    Y = np.rint(map1[..., 1].astype(np.float64) * 32).astype(np.int64)
+    sx, sy = X >> 5, Y >> 5
+    ax, ay = X & 31, Y & 31
+    if src.dtype == np.uint8:
+        def wt(fy_lo, fx_lo):  # itab = saturate_cast<short>(tab * INTER_REMAP_COEF_SCALE)
+            t = (np.where(fy_lo, 1 - ay / 32.0, ay / 32.0).astype(np.float32)
+                 * np.where(fx_lo, 1 - ax / 32.0, ax / 32.0).astype(np.float32))
+            return np.rint(t.astype(np.float64) * 32768).astype(np.int64)
+        ws = [wt(True, True), wt(True, False), wt(False, True), wt(False, False)]
+    else:
+        wy0, wy1 = (1 - ay / 32.0).astype(np.float32), (ay / 32.0).astype(np.float32)
+        wx0, wx1 = (1 - ax / 32.0).astype(np.float32), (ax / 32.0).astype(np.float32)
+        ws = [(wy0 * wx0).astype(np.float64), (wy0 * wx1).astype(np.float64),
+              (wy1 * wx0).astype(np.float64), (wy1 * wx1).astype(np.float64)]
+    out = np.zeros((h, w), np.int64 if src.dtype == np.uint8 else np.float64)
+    taps = [(0, 0), (0, 1), (1, 0), (1, 1)]
+    vals = []
+    for dy, dx in taps:
+        yy, xx = sy + dy, sx + dx
+        ok = (yy >= 0) & (yy < src.shape[0]) & (xx >= 0) & (xx < src.shape[1])
+        v = np.zeros((h, w), src.dtype)
+        v[ok] = src[yy[ok], xx[ok]]
+        vals.append(v)
+    if src.dtype == np.uint8:
+        s = sum(vals[i].astype(np.int64) * ws[i] for i in range(4))
+        return np.clip((s + (1 << 14)) >> 15, 0, 255).astype(np.uint8)
+    for i in range(4):
+        out = out + vals[i].astype(np.float64) * ws[i]
+    return out.astype(src.dtype)
+
+
+def make_cv2():
+    cv2 = types.ModuleType("cv2")
+    cv2.INTER_LINEAR = INTER_LINEAR
+    cv2.NORM_MINMAX = 32
+    cv2.IMREAD_UNCHANGED = -1
+    cv2.remap = remap
+    cv2.normalize = lambda *a, **k: None
+    cv2.imshow = lambda *a, **k: None
+    cv2.waitKey = lambda *a, **k: 0
+    return cv2

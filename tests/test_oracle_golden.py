@@ -1,0 +1,145 @@
+"""Pin the CPU oracle against fixtures produced by the reference's own code (CPU only).
+
+The fixtures (tests/golden/*.npz) come from tests/golden/make_golden.py, which
+runs /root/reference's graph builders, flow.correct_alpha, reader.read_flow and
+the train.py loss helpers verbatim (TF/cv2 ops via tests/golden/tfshim.py).
+"""
+
+import os
+import tempfile
+
+import numpy as np
+import pytest
+
+from conftest import golden
+from oracle import flow as oflow
+from oracle import models as om
+from oracle import ops
+
+VGG_MEAN = np.array(ops.VGG_MEAN)
+
+
+def _fresh_weight_vars(g, suffix):
+    names = [str(n) for n in g["var_names"]]
+    idx = [i for i, n in enumerate(names) if n.endswith(suffix)]
+    return [names[i] for i in idx], g["var_sums"][idx], g["var_firsts"][idx]
+
+
+def _close(a, b, rtol, atol):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    assert a.shape == b.shape, (a.shape, b.shape)
+    err = np.abs(a - b)
+    bound = atol + rtol * np.abs(b)
+    assert (err <= bound).all(), "max err %g (worst ratio %g)" % (err.max(), (err / bound).max())
+
+
+@pytest.mark.parametrize("case", ["unet_video_70x90", "unet_video_64x96", "unet_video_70x90_unit", "unet_image_70x90"])
+def test_unet_matches_reference_builder(case, vgg0):
+    g = golden(case)
+    rs = np.random.RandomState(int(g["weight_seed"]))
+    p = om.unet_params(vgg0, rs, video=bool(g["video"]))
+    # draw order: the reference's fresh 'weights' variables, in creation order (unet.py:11-17)
+    names, sums, firsts = _fresh_weight_vars(g, "/weights")
+    assert [n.split("/")[0] for n in names] == [c[0] for c in om.UNET_NEW_CONVS]
+    for n, s, f in zip(names, sums, firsts):
+        w = p[n.split("/")[0]][0].astype(np.float64)
+        assert w.ravel()[0] == f and np.isclose(w.sum(), s, rtol=1e-12, atol=1e-9)
+    r = om.unet_forward(g["x"], p)
+    _close(r["conv1_3"], g["logits"], 1e-9, 1e-9)
+    _close(r["output"], g["output"], 1e-9, 1e-12)
+    for k in ("pool4", "upconv1", "conv2_3"):
+        _close(r[k], g[k], 1e-6, 1e-4)
+
+
+@pytest.mark.parametrize("case", ["unet_simple_256_infer", "unet_simple_64_train"])
+def test_unet_simple_matches_reference_builder(case, vgg0):
+    g = golden(case)
+    rs = np.random.RandomState(int(g["weight_seed"]))
+    p = om.unet_simple_params(rs)
+    names, sums, firsts = _fresh_weight_vars(g, "/weights")
+    assert [n.split("/")[-2] for n in names] == [c[0] for c in om.SIMPLE_NEW_CONVS]
+    for n, s in zip(names, sums):
+        assert np.isclose(p[n.split("/")[-2]][0].astype(np.float64).sum(), s, rtol=1e-12, atol=1e-9)
+    c = g["cmp_u8"].astype(np.float64) - VGG_MEAN
+    b = g["bg_u8"].astype(np.float64) - VGG_MEAN
+    r = om.unet_simple_forward(c, b, c - b, bool(g["phase"]), vgg0, p)
+    _close(r["logits"], g["logits"], 1e-8, 1e-8)
+    _close(r["output"], g["output"], 1e-8, 1e-12)
+    _close(r["upconv4"], g["upconv4"], 1e-5, 1e-4)
+
+
+@pytest.mark.parametrize("case", ["small_70x90_infer", "small_70x90_train"])
+def test_unet_small_matches_reference_builder(case):
+    g = golden(case)
+    p = om.unet_small_params(np.random.RandomState(int(g["weight_seed"])), cin=6)
+    r = om.unet_small_forward(g["x"], bool(g["phase"]), p)
+    _close(r["conv1_3"], g["logits"], 1e-9, 1e-9)
+    _close(r["output"], g["output"], 1e-9, 1e-12)
+    _close(r["upconv2"], g["upconv2"], 1e-5, 1e-5)
+
+
+def test_refine_matches_reference_builder():
+    g = golden("refine_40x56")
+    p = om.refine_params(np.random.RandomState(int(g["weight_seed"])), cin=5)
+    r = om.refine_forward(g["x"], p)
+    _close(r["output"], g["output"], 1e-9, 1e-12)
+    assert np.isclose(r["conv1"].sum(), float(g["conv1_sum"]), rtol=1e-9)
+
+
+def test_read_flow_format_and_roundtrip():
+    g = golden("flow_500x1200")
+    fb = oflow.smooth_flow(500, 1200, seed=int(g["flow_seed_b"]))
+    with tempfile.TemporaryDirectory() as td:
+        p = os.path.join(td, "b.flo")
+        oflow.write_flow(p, fb)
+        head = open(p, "rb").read(len(g["flo_header"]))
+        assert np.array_equal(np.frombuffer(head, np.uint8), g["flo_header"])
+        assert np.array_equal(oflow.read_flow(p), fb)
+
+
+def test_warp_img_matches_reference():
+    g = golden("flow_500x1200")
+    fb = oflow.smooth_flow(500, 1200, seed=int(g["flow_seed_b"]))
+    alpha = g["alpha_u8"] / 255.0
+    w = oflow.warp_img(alpha, fb, mode="opencv")
+    _close(w, g["warped"], 0, 1e-7)
+    assert np.isclose(w.sum(), float(g["warped_f64_sum"]), rtol=1e-12)
+    # the exact-bilinear mode differs from OpenCV's 1/32-pixel quantisation by at most |grad|/64 per axis
+    we = oflow.warp_img(alpha, fb, mode="exact")
+    assert np.abs(we - w).max() < 1.0 / 32 + 1e-9
+
+
+def test_correct_alpha_matches_reference():
+    g = golden("flow_500x1200")
+    fb = oflow.smooth_flow(500, 1200, seed=int(g["flow_seed_b"]))
+    ff = oflow.smooth_flow(500, 1200, seed=int(g["flow_seed_f"]))
+    warped = oflow.warp_img(g["alpha_u8"] / 255.0, fb)
+    out = oflow.correct_alpha(fb, ff, warped.copy(), promote="numpy2")
+    mask = (out == 0) & (warped != 0)
+    assert np.array_equal(np.packbits(mask), g["corrected_zero_mask"])
+    # crafted case: large / negative displacements (numpy-style wrap of negative indices)
+    c2 = oflow.correct_alpha(g["small_backward"], g["small_forward"], g["small_alpha"].copy(), promote="numpy2")
+    assert np.array_equal(c2, g["small_corrected"])
+
+
+def test_warp_bgr_matches_reference():
+    g = golden("flow_500x1200")
+    assert np.array_equal(oflow.warp_bgr(g["bgr_crop"], g["bgr_flow"]), g["bgr_warped"])
+
+
+def test_loss_matches_reference():
+    g = golden("loss_2x32x32")
+    loss, al, cl = ops.matting_loss(g["pred"], g["gt"], g["raw_fg"], g["in_bg"], g["in_cmp"])
+    assert np.isclose(loss, float(g["loss"]), rtol=1e-12)
+    assert np.isclose(al, float(g["alpha_loss"]), rtol=1e-12)
+    assert np.isclose(cl, float(g["cmp_loss"]), rtol=1e-12)
+
+
+def test_oracle_float32_mode_close_to_float64():
+    """The float32 oracle (the timed CPU baseline) tracks the float64 goldens."""
+    g = golden("unet_video_70x90_unit")
+    from oracle.models import synthetic_vgg16
+    p = om.unet_params(synthetic_vgg16(0), np.random.RandomState(int(g["weight_seed"])), video=True)
+    r = om.unet_forward(g["x"], p, dtype=np.float32)
+    _close(r["output"], g["output"], 0, 1e-5)
