@@ -1,0 +1,187 @@
+"""Benchmark: alpha-mattes/sec of unet.UNetVideo at 1920x1080 (BASELINE.json configs[1]; configs[3] at N>1).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--dtype bf16|fp32]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+A step = one UNetVideo forward over B synthetic 1080p 7-channel frames per GPU (inputs resident
+in HBM before timing).  Frame-parallel: every rank runs its own frames, no collective in the data
+path (scaling "weak"); the packed weights are RCCL-broadcast from rank 0 once, before timing.
+Rank 0 prints ONE JSON line (value = frames processed by all ranks / max-over-ranks time).
+"""
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "video-matting_amd"))
+sys.path.insert(0, REPO)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+from vmatting import ops, parallel, unet  # noqa: E402
+from vmatting.weights import synthetic_vgg16  # noqa: E402
+
+METRIC = "alpha-mattes/sec at 1920×1080, 1/2/4/8 MI355X + achieved HBM GB/s"
+PEAK_TFLOPS = {"bf16": 2516.6, "fp32": 157.3}  # MI355X dense MFMA (MI355X_MICROARCH.md chip table)
+PEAK_HBM_GBPS = 8000.0
+VGG_MEAN = (103.939, 116.779, 123.68)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def synth_frames(n, h, w, first, device):
+    """frame f (seed 1234+f): cmp/bg BGR U{0..255} - VGG_MEAN; trimap {0,.5,1} - .5
+    from a random ellipse with an unknown band.  Generated on the device."""
+    out = torch.empty((n, h, w, 7), dtype=torch.float32, device=device)
+    mean = torch.tensor(VGG_MEAN, device=device)
+    yy = torch.arange(h, device=device, dtype=torch.float32)[:, None]
+    xx = torch.arange(w, device=device, dtype=torch.float32)[None, :]
+    for i in range(n):
+        g = torch.Generator(device=device)
+        g.manual_seed(1234 + first + i)
+        out[i, :, :, 0:3] = torch.randint(0, 256, (h, w, 3), generator=g, device=device).float() - mean
+        out[i, :, :, 3:6] = torch.randint(0, 256, (h, w, 3), generator=g, device=device).float() - mean
+        c = torch.rand(4, generator=g, device=device)
+        cy, cx = (0.3 + 0.4 * c[0]) * h, (0.3 + 0.4 * c[1]) * w
+        ry, rx = (0.15 + 0.15 * c[2]) * h, (0.15 + 0.15 * c[3]) * w
+        d = torch.sqrt(((yy - cy) / ry) ** 2 + ((xx - cx) / rx) ** 2)
+        band = 8.0 / float(min(ry, rx))
+        tri = torch.where(d < 1 - band, 1.0, torch.where(d < 1 + band, 0.5, 0.0))
+        out[i, :, :, 6] = tri - 0.5
+    return out
+
+
+def cpu_baseline(h, w, sample_h, sample_w):
+    """The oracle (numpy f32 restatement of unet.py) timed on host cores on a bounded sample."""
+    from oracle import models as om
+    try:
+        from threadpoolctl import threadpool_info
+        threads = max([i.get("num_threads", 1) for i in threadpool_info() if i.get("user_api") == "blas"] or [1])
+    except Exception:
+        threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    vgg = synthetic_vgg16(0)
+    p = om.unet_params(vgg, np.random.RandomState(0), video=True)
+    rs = np.random.RandomState(1234)
+    x = np.concatenate([rs.randint(0, 256, (1, sample_h, sample_w, 6)).astype(np.float32) - np.tile(VGG_MEAN, 2),
+                        rs.choice([-0.5, 0.0, 0.5], (1, sample_h, sample_w, 1))], -1).astype(np.float32)
+    t0 = time.perf_counter()
+    om.unet_forward(x, p, dtype=np.float32)
+    dt = time.perf_counter() - t0
+    scale = (h * w) / float(sample_h * sample_w)  # conv work is linear in pixels
+    return {"value": round(1.0 / (dt * scale), 5), "unit": "frames/s", "cores": int(threads), "kind": "port",
+            "sample": "oracle/ numpy-f32 UNetVideo forward on one %dx%d 7-ch frame (%.1f s), scaled x%.0f to "
+                      "1920x1080 by pixel count" % (sample_w, sample_h, dt, scale)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=1, help="frames per step per GPU")
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample", default="540x960", help="HxW of the CPU-baseline sample frame")
+    ap.add_argument("--no-profile", action="store_true", help="skip per-conv HIP events")
+    ap.add_argument("--layers", action="store_true", help="per-conv timing breakdown on stderr")
+    args = ap.parse_args()
+
+    rank, world, local = parallel.init_from_env("nccl")
+    if world != args.gpus:
+        log("warning: --gpus %d but WORLD_SIZE %d; using WORLD_SIZE" % (args.gpus, world))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    # identical weights everywhere: every rank draws from the same seeds, then rank 0's packed
+    # buffers are broadcast (one RCCL collective) so replicas are bit-identical by construction
+    vgg = synthetic_vgg16(0)
+    np.random.seed(0)
+    model = unet.UNetVideo(vgg, dtype=args.dtype, device=dev)
+    model.params = model._make_params()
+    model._pack()
+    parallel.broadcast_tensors(model.weights_flat(), src=0)
+
+    B, H, W = args.batch, args.height, args.width
+    x = synth_frames(B, H, W, rank * B, dev)
+    flops_per_frame = model.conv_flops(1, H, W)
+
+    for _ in range(args.warmup):
+        model.forward(x)
+    torch.cuda.synchronize()
+
+    prof = None if args.no_profile else ops.conv_profile(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        model.forward(x)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    ops.conv_profile(False)
+
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    frames = world * B * args.steps
+    value = frames / elapsed
+    ms_step = 1000.0 * elapsed / args.steps
+
+    roofline = None
+    if prof:
+        mf = [(f, e0.elapsed_time(e1)) for f, head, e0, e1 in prof if not head]
+        hd = [(f, e0.elapsed_time(e1)) for f, head, e0, e1 in prof if head]
+        fl, ms = sum(f for f, _ in mf), sum(t for _, t in mf)
+        achieved = fl / (ms * 1e-3) / 1e12
+        n_launch = len(mf)
+        roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_TFLOPS[args.dtype],
+                    "unit": "TFLOP/s", "frac": round(achieved / PEAK_TFLOPS[args.dtype], 4), "traffic": None,
+                    "kernel": "conv3x3_mfma (%s)" % args.dtype,
+                    "launches": n_launch, "avg_launch_ms": round(ms / max(1, n_launch), 4),
+                    "flops_per_launch_avg": int(fl / max(1, n_launch))}
+        hfl = sum(t for _, t in hd)
+        per_step = len(prof) // max(1, args.steps)
+        if args.layers and per_step:
+            for i in range(per_step):
+                rows = prof[i::per_step]
+                t_ms = sum(e0.elapsed_time(e1) for _, _, e0, e1 in rows) / len(rows)
+                log("  conv #%2d %s: %.3f ms  %.1f TFLOP/s" % (i, "head" if rows[0][1] else "mfma", t_ms,
+                                                             rows[0][0] / (t_ms * 1e-3) / 1e12))
+        log("conv MFMA: %d launches, %.3f ms total/step, %.1f TFLOP/s; head: %.3f ms/step; step %.3f ms"
+            % (n_launch, ms / args.steps, achieved, hfl / args.steps, ms_step))
+
+    if rank == 0:
+        rec = {"metric": METRIC, "value": round(value, 3), "unit": "frames/s", "n_gpus": world,
+               "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 4),
+               "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
+               "data": "synthetic (seeded 1080p cmp/bg/trimap frames; synthetic VGG16 + init_conv weights)",
+               "config": {"workload": "unet.UNetVideo forward (20 3x3 convs, 3.233 TFLOP/frame), %dx%d 7-ch NHWC"
+                                      % (W, H),
+                          "frames_per_step_per_gpu": B, "height": H, "width": W,
+                          "parallelism": "frame-parallel dp%d" % world},
+               "achieved_tflops_whole_forward": round(value / world * flops_per_frame / 1e12, 2),
+               "roofline": roofline, "cpu_baseline": None}
+        if world == 1 and not args.no_cpu_baseline:
+            sh, sw = (int(v) for v in args.cpu_sample.split("x"))
+            rec["cpu_baseline"] = cpu_baseline(H, W, sh, sw)
+        print(json.dumps(rec), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,128 @@
+/*
+ * vmatting.h — C ABI of the MI355X (gfx950) per-frame alpha-matting path.
+ *
+ * Drop-in boundary for the hot path of tangih/video-matting.  The reference is
+ * TensorFlow-1.x graph code: its "FFI" is the TF op set reached through
+ * sess.run (train.py:81,330).  Each entry point below replaces the TF/OpenCV
+ * op(s) the reference's model builders and flow helpers call, cited per
+ * function.  A Python host (video-matting_amd/vmatting/_lib.py) binds this with
+ * ctypes; INTEGRATION.md shows the binding.
+ *
+ * Conventions
+ *   - All tensor pointers are DEVICE pointers owned by the caller (e.g. from
+ *     torch.Tensor.data_ptr() on ROCm); nothing is allocated inside a call.
+ *   - Activations are NHWC views (vm_tensor): element (n,h,w,c) lives at
+ *     ptr + ((n*H + h)*W + w)*cstride + coff + c, in elements of `dtype`.
+ *     A channel slice of a wider buffer (coff, cstride) is how a tf.concat is
+ *     expressed without a copy (unet.py:62, unet_simple.py:41, small.py:22).
+ *   - `stream` is a hipStream_t (void* here so the header needs no HIP include);
+ *     every call is asynchronous on it and is capturable into a hipGraph.
+ *   - Return value: VM_OK (0) or a negative VM_E* code; vm_last_error() gives a
+ *     per-thread message.  No exception crosses the ABI.
+ *   - Thread-safety: reentrant; calls on different streams may run concurrently.
+ */
+#ifndef VMATTING_H
+#define VMATTING_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VM_ABI_VERSION 1
+
+enum vm_dtype { VM_F32 = 0, VM_BF16 = 1, VM_U8 = 2 };
+
+enum vm_act {
+  VM_ACT_NONE = 0,
+  VM_ACT_RELU = 1,     /* tf.nn.relu            (unet.py:96 ...)            */
+  VM_ACT_SIGMOID = 2,  /* tf.nn.sigmoid         (unet.py:145,205)           */
+  VM_ACT_SOFTMAX = 3   /* tf.nn.softmax, last axis (refine.py:31)           */
+};
+
+enum vm_status {
+  VM_OK = 0,
+  VM_EINVAL = -1,        /* bad argument / shape mismatch (TF: ValueError at build) */
+  VM_EUNSUPPORTED = -2,  /* valid but not supported by this build                    */
+  VM_EHIP = -3,          /* HIP runtime error                                        */
+  VM_EINDEX = -4         /* data-dependent index error (flow.correct_alpha IndexError) */
+};
+
+typedef struct vm_tensor {
+  void* ptr;
+  int32_t n, h, w, c;     /* logical shape                                  */
+  int32_t cstride, coff;  /* channel stride of the pixel row / first channel */
+  int32_t dtype;          /* enum vm_dtype                                   */
+} vm_tensor;
+
+int vm_abi_version(void);
+const char* vm_last_error(void);
+
+/* ---------------------------------------------------------------- 3x3 convolution
+ * Replaces tf.nn.conv2d(x, w, [1,1,1,1], 'SAME') + tf.nn.bias_add + the activation /
+ * inference batch-norm that follows it:
+ *   unet.py:35-42 (new_conv), 44-63 (upconv conv), 65-74 (conv_layer);
+ *   unet_simple.py:19-27, 30-42, 98-107; small.py:13-34; refine.py:18-25.
+ * y = act((conv(x, w) + bias) * scale + shift) per output channel; bias/scale/shift
+ * may be NULL (f32 device arrays of length cout).  Weights are first packed from
+ * TF's HWIO f32 layout into the kernel's [cout_pad][K_pad] layout (K = tap*cin_pad + c).
+ * Computes in x->dtype (bf16 -> MFMA 16x16x32 bf16, f32 -> exact-f32 MFMA 16x16x4),
+ * accumulates in f32.  cout == 1 dispatches the memory-bound head kernel.
+ * act == VM_ACT_SOFTMAX needs cout <= 128 (whole channel row in one tile).
+ */
+size_t vm_conv3x3_packed_bytes(int cin, int cout, int dtype);
+int vm_conv3x3_pack_weights(const float* w_hwio, int cin, int cout, int dtype, void* packed, void* stream);
+int vm_conv3x3_nhwc(const vm_tensor* x, const void* packed, int cin, int cout, const float* bias,
+                    const float* scale, const float* shift, int act, vm_tensor* y, void* stream);
+
+/* tf.nn.max_pool(ksize 2, stride 2, 'SAME') — unet.py:32-33, unet_simple.py:95-96, small.py:40,42 */
+int vm_maxpool2x2_same_nhwc(const vm_tensor* x, vm_tensor* y, void* stream);
+
+/* tf.image.resize_images(x, [H, W]) TF-1.x bilinear legacy — unet.py:58, unet_simple.py:33, small.py:17 */
+int vm_resize_bilinear_tf1_nhwc(const vm_tensor* x, vm_tensor* y, void* stream);
+
+/* dtype / channel-padding copy with optional per-channel affine and activation
+ * (packs the caller's f32 [N,H,W,7] frame into the compute layout; loader.py:76-78 mean/shift
+ * can be folded in via shift).  Channels >= x->c of y are zero-filled. */
+int vm_convert_nhwc(const vm_tensor* x, vm_tensor* y, const float* scale, const float* shift, int act, void* stream);
+
+/* tf.contrib.layers.batch_norm(is_training=True): batch mean / biased variance over N,H,W
+ * (unet_simple.py:25,41; small.py:22,32).  work: vm_bn_workspace_bytes(x) bytes of device scratch. */
+size_t vm_bn_workspace_bytes(const vm_tensor* x);
+int vm_bn_stats_nhwc(const vm_tensor* x, float* mean, float* var, void* work, void* stream);
+/* y = act((x - mean) * rsqrt(var + eps) * gamma + beta); y may alias x. NULL mean/var = 0/1. */
+int vm_bn_apply_nhwc(const vm_tensor* x, vm_tensor* y, const float* mean, const float* var, const float* gamma,
+                     const float* beta, float eps, int act, void* stream);
+
+/* tf.nn.softmax over channels — refine.py:31 */
+int vm_softmax_lastdim_nhwc(const vm_tensor* x, vm_tensor* y, void* stream);
+
+/* flow.warp_img (flow.py:9-18): out[y,x] = bilinear(img, x + flow[y,x,0], y + flow[y,x,1]),
+ * cv2.remap INTER_LINEAR / BORDER_CONSTANT 0.  mode 0 = OpenCV 1/32-pixel fixed point, 1 = exact.
+ * img [ih,iw] f32, flow [h,w,2] f32, out [h,w] f32.  Batched over `n` frames (contiguous). */
+int vm_remap_bilinear_f32(const float* img, int ih, int iw, const float* flow, int h, int w, int n, float* out,
+                          int mode, void* stream);
+/* flow.warp_bgr (flow.py:21-33): uint8 [ih,iw,cn] HWC, OpenCV 15-bit fixed-point weights. */
+int vm_remap_bilinear_u8(const uint8_t* img, int ih, int iw, int cn, const float* flow, int h, int w, uint8_t* out,
+                         void* stream);
+
+/* flow.correct_alpha (flow.py:36-65): forward/backward consistency; alpha [h,w] f32 zeroed IN PLACE
+ * where the round-trip error > thresh.  promote 0 = numpy-1.x float64 index arithmetic, 1 = numpy-2
+ * float32.  *err_flag (device int, zeroed by the caller) is set when an index falls below -dim
+ * (the reference's IndexError); the host turns that into VM_EINDEX. */
+int vm_fb_consistency(const float* backward, const float* forward, int h, int w, float* alpha, float thresh,
+                      int promote, int* err_flag, void* stream);
+
+/* train.py:14-28,42-47 loss: out[0] = mean(0.5*charb(pred,gt) + 0.5*charb(composite(raw_fg,bg,pred), cmp)),
+ * out[1] = mean alpha loss, out[2] = mean compositional loss.  pred/gt [n,h,w,1], others [n,h,w,3] f32.
+ * work: vm_loss_workspace_bytes(n*h*w) bytes. */
+size_t vm_loss_workspace_bytes(long pixels);
+int vm_matting_loss(const float* pred, const float* gt, const float* raw_fg, const float* bg, const float* cmp,
+                    long pixels, float* out, void* work, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VMATTING_H */

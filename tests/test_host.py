@@ -1,0 +1,121 @@
+"""CPU checks of the host logic: weight construction order, .flo I/O, sharding and the
+frame-parallel collectives (gloo, world_size 2)."""
+
+import os
+import tempfile
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from conftest import golden
+from oracle import flow as oflow
+from oracle import models as om
+
+
+def test_synthetic_vgg_matches_oracle_generator():
+    from vmatting.weights import synthetic_vgg16
+    a, b = synthetic_vgg16(0), om.synthetic_vgg16(0)
+    for k in a:
+        assert np.array_equal(a[k][0], b[k][0]) and np.array_equal(a[k][1], b[k][1])
+
+
+@pytest.mark.parametrize("case", ["unet_video_70x90", "unet_image_70x90"])
+def test_unet_weight_draw_order_matches_reference(case, vgg0):
+    """vmatting.unet draws fresh filters from the global numpy RNG in the reference's order."""
+    from vmatting import unet
+    g = golden(case)
+    cls = unet.UNetVideo if int(g["video"]) else unet.UNetImage
+    m = cls.__new__(cls)
+    m.data_dict = vgg0
+    np.random.seed(int(g["weight_seed"]))
+    p = m._make_params()
+    ref = om.unet_params(vgg0, np.random.RandomState(int(g["weight_seed"])), video=bool(g["video"]))
+    assert set(p) == set(ref)
+    for k in ref:
+        assert np.array_equal(p[k][0], ref[k][0]), k
+        assert (p[k][1] is None) == (ref[k][1] is None), k
+        if p[k][1] is not None:
+            assert np.array_equal(p[k][1], ref[k][1]), k
+
+
+def test_unet_flop_count_matches_survey():
+    from vmatting import unet
+    m = unet.UNetVideo.__new__(unet.UNetVideo)
+    m.data_dict = om.synthetic_vgg16(0)
+    np.random.seed(0)
+    m.params = m._make_params()
+    assert m.conv_flops(1, 1080, 1920) == 3_232_595_312_640  # SURVEY.md §8d / BASELINE.md
+
+
+def test_read_flow_roundtrip_and_bad_magic(capsys):
+    from vmatting import reader
+    f = oflow.smooth_flow(37, 53, seed=3)
+    with tempfile.TemporaryDirectory() as td:
+        p = os.path.join(td, "x.flo")
+        reader.write_flow(p, f)
+        assert np.array_equal(reader.read_flow(p), f)
+        assert np.array_equal(oflow.read_flow(p), f)
+        raw = bytearray(open(p, "rb").read())
+        raw[0:4] = np.array([1.0], np.float32).tobytes()
+        open(p, "wb").write(bytes(raw))
+        out = reader.read_flow(p)  # prints, continues (reader.py:25-26)
+        assert "invalid key" in capsys.readouterr().out
+        assert np.array_equal(out, f)
+
+
+def test_composite_matches_reference_formula():
+    from vmatting import reader
+    rs = np.random.RandomState(0)
+    fg = rs.randint(0, 256, (5, 7, 3)).astype(np.uint8)
+    bg = rs.randint(0, 256, (5, 7, 3)).astype(np.uint8)
+    a = rs.uniform(size=(5, 7))
+    ref = a[..., None] * fg + (1 - a[..., None]) * bg
+    assert np.allclose(reader.create_composite_image(fg, bg, a), ref, rtol=0, atol=1e-12)
+
+
+def test_shard_ranges_cover_frames():
+    from vmatting.parallel import shard_range
+    for n in (1, 7, 256, 257):
+        for world in (1, 2, 3, 8):
+            rs = [shard_range(n, r, world) for r in range(world)]
+            assert rs[0][0] == 0 and rs[-1][1] == n
+            assert all(rs[i][1] == rs[i + 1][0] for i in range(world - 1))
+            assert max(b - a for a, b in rs) - min(b - a for a, b in rs) <= 1
+
+
+def _dist_worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    from vmatting import parallel
+    parallel.init_from_env(backend="gloo")
+    try:
+        # weights: rank 0's values win everywhere (one flattened collective)
+        w = [torch.full((5,), float(rank)), torch.arange(6, dtype=torch.float32).reshape(2, 3) * (rank + 1),
+             torch.tensor([rank], dtype=torch.int32)]
+        parallel.broadcast_tensors(w, src=0)
+        ok_b = bool(torch.all(w[0] == 0)) and bool(torch.equal(w[1], torch.arange(6.).reshape(2, 3))) and int(w[2]) == 0
+        # frames: 7 frames sharded 3/4, each rank "computes" frame index * 10, all-gather in order
+        n = 7
+        a, b = parallel.shard_range(n, rank, world)
+        local = torch.arange(a, b, dtype=torch.float32)[:, None, None, None].expand(b - a, 2, 3, 1) * 10
+        full = parallel.gather_frames(local.contiguous(), n)
+        ok_g = full.shape == (7, 2, 3, 1) and bool(torch.equal(full[:, 0, 0, 0], torch.arange(7.) * 10))
+        q.put((rank, ok_b, ok_g))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_frame_parallel_collectives_gloo_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29500 + (os.getpid() % 1000)
+    procs = [ctx.Process(target=_dist_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(60)
+    assert sorted(r for r, _, _ in res) == [0, 1]
+    assert all(b and g for _, b, g in res), res

@@ -1,0 +1,322 @@
+// Memory-bound NHWC kernels: max-pool, TF-1 bilinear resize, dtype/pad conversion,
+// batch-norm statistics + apply, channel softmax.  All vectorised to 16-byte accesses
+// when the view allows (gfx950 Guideline 13), element-wise otherwise.
+
+#include "vm_common.h"
+
+namespace vm {
+
+struct View {
+  char* p;
+  int n, h, w, c, cs, coff, dt;
+};
+
+static View view(const vm_tensor* t) {
+  View v;
+  v.p = reinterpret_cast<char*>(t->ptr);
+  v.n = t->n; v.h = t->h; v.w = t->w; v.c = t->c; v.cs = t->cstride; v.coff = t->coff; v.dt = t->dtype;
+  return v;
+}
+
+__device__ __forceinline__ float ldv(const View& v, long pix, int c) {
+  const long o = pix * v.cs + v.coff + c;
+  return v.dt == VM_F32 ? reinterpret_cast<const float*>(v.p)[o] : bf2f(reinterpret_cast<const uint16_t*>(v.p)[o]);
+}
+
+__device__ __forceinline__ void stv(const View& v, long pix, int c, float x) {
+  const long o = pix * v.cs + v.coff + c;
+  if (v.dt == VM_F32) reinterpret_cast<float*>(v.p)[o] = x;
+  else reinterpret_cast<uint16_t*>(v.p)[o] = f2bf(x);
+}
+
+// 16-byte chunk of CE channels starting at channel c (caller guarantees alignment)
+template <typename T>
+__device__ __forceinline__ void ldc(const View& v, long pix, int c, float* f) {
+  const T* base = reinterpret_cast<const T*>(v.p) + pix * v.cs + v.coff + c;
+  Chunk<T>::unpack(*reinterpret_cast<const uint4*>(base), f);
+}
+template <typename T>
+__device__ __forceinline__ void stc(const View& v, long pix, int c, const float* f) {
+  T* base = reinterpret_cast<T*>(v.p) + pix * v.cs + v.coff + c;
+  *reinterpret_cast<uint4*>(base) = Chunk<T>::pack(f);
+}
+
+// ---------------------------------------------------------------- max pool 2x2 / 2, SAME
+// tf.nn.max_pool SAME (unet.py:33): out = ceil(n/2), pad_before 0, padded taps never win.
+template <typename T, bool VEC>
+__global__ void maxpool2x2_kernel(View x, View y) {
+  constexpr int CE = VEC ? 16 / sizeof(T) : 1;
+  const int cpp = (y.c + CE - 1) / CE;
+  const long total = (long)y.n * y.h * y.w * cpp;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int cc = (int)(i % cpp);
+    const long op = i / cpp;
+    const int ow = (int)(op % y.w);
+    const long t = op / y.w;
+    const int oh = (int)(t % y.h);
+    const int n = (int)(t / y.h);
+    const int ih = 2 * oh, iw = 2 * ow;
+    const long p00 = ((long)n * x.h + ih) * x.w + iw;
+    const bool hasr = iw + 1 < x.w, hasd = ih + 1 < x.h;
+    const int c = cc * CE;
+    if (VEC) {
+      float m[CE], f[CE];
+      ldc<T>(x, p00, c, m);
+      if (hasr) { ldc<T>(x, p00 + 1, c, f); for (int j = 0; j < CE; ++j) m[j] = fmaxf(m[j], f[j]); }
+      if (hasd) { ldc<T>(x, p00 + x.w, c, f); for (int j = 0; j < CE; ++j) m[j] = fmaxf(m[j], f[j]); }
+      if (hasr && hasd) { ldc<T>(x, p00 + x.w + 1, c, f); for (int j = 0; j < CE; ++j) m[j] = fmaxf(m[j], f[j]); }
+      stc<T>(y, op, c, m);
+    } else {
+      float m = ldv(x, p00, c);
+      if (hasr) m = fmaxf(m, ldv(x, p00 + 1, c));
+      if (hasd) m = fmaxf(m, ldv(x, p00 + x.w, c));
+      if (hasr && hasd) m = fmaxf(m, ldv(x, p00 + x.w + 1, c));
+      stv(y, op, c, m);
+    }
+  }
+}
+
+// ---------------------------------------------------------------- TF-1.x legacy bilinear resize
+// tf.image.resize_images (unet.py:58): scale = (float)in/out, src = (float)dst * scale,
+// lo = floor(src), hi = min(lo + 1, in - 1), lerp = src - floor(src);
+// top = tl + (tr - tl) * xl; bot = bl + (br - bl) * xl; out = top + (bot - top) * yl.
+// TF's scaler runs in plain float32; contraction would fuse (float)i*scale into src - floor(src)
+// and produce a MORE precise lerp than TF's — kept off for the coordinate arithmetic.
+__device__ __forceinline__ void tf1_coord(int i, float scale, int in, int& lo, int& hi, float& lerp) {
+#pragma clang fp contract(off)
+  const float src = (float)i * scale;
+  const float fl = floorf(src);
+  lo = (int)fl;
+  hi = min(lo + 1, in - 1);
+  lerp = src - fl;
+}
+
+template <typename T, bool VEC>
+__global__ void resize_tf1_kernel(View x, View y, float sy, float sx) {
+  constexpr int CE = VEC ? 16 / sizeof(T) : 1;
+  const int cpp = (y.c + CE - 1) / CE;
+  const long total = (long)y.n * y.h * y.w * cpp;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int cc = (int)(i % cpp);
+    const long op = i / cpp;
+    const int ow = (int)(op % y.w);
+    const long t = op / y.w;
+    const int oh = (int)(t % y.h);
+    const int n = (int)(t / y.h);
+    int y0, y1, x0, x1;
+    float yl, xl;
+    tf1_coord(oh, sy, x.h, y0, y1, yl);
+    tf1_coord(ow, sx, x.w, x0, x1, xl);
+    const long rb = (long)n * x.h;
+    const long ptl = (rb + y0) * x.w + x0, ptr_ = (rb + y0) * x.w + x1;
+    const long pbl = (rb + y1) * x.w + x0, pbr = (rb + y1) * x.w + x1;
+    const int c = cc * CE;
+    if (VEC) {
+      float tl[CE], tr[CE], bl[CE], br[CE], o[CE];
+      ldc<T>(x, ptl, c, tl); ldc<T>(x, ptr_, c, tr); ldc<T>(x, pbl, c, bl); ldc<T>(x, pbr, c, br);
+#pragma unroll
+      for (int j = 0; j < CE; ++j) {
+        const float top = tl[j] + (tr[j] - tl[j]) * xl;
+        const float bot = bl[j] + (br[j] - bl[j]) * xl;
+        o[j] = top + (bot - top) * yl;
+      }
+      stc<T>(y, op, c, o);
+    } else {
+      const float vtl = ldv(x, ptl, c), vtr = ldv(x, ptr_, c), vbl = ldv(x, pbl, c), vbr = ldv(x, pbr, c);
+      const float top = vtl + (vtr - vtl) * xl;
+      const float bot = vbl + (vbr - vbl) * xl;
+      stv(y, op, c, top + (bot - top) * yl);
+    }
+  }
+}
+
+// ---------------------------------------------------------------- convert / pad / affine
+__global__ void convert_kernel(View x, View y, const float* scale, const float* shift, int act) {
+  const long total = (long)y.n * y.h * y.w * y.c;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % y.c);
+    const long p = i / y.c;
+    float v = 0.f;
+    if (c < x.c) {
+      v = ldv(x, p, c);
+      if (scale) v *= scale[c];
+      if (shift) v += shift[c];
+      v = act == VM_ACT_RELU ? fmaxf(v, 0.f) : act == VM_ACT_SIGMOID ? sigmoid_precise(v) : v;
+    }
+    stv(y, p, c, v);
+  }
+}
+
+// ---------------------------------------------------------------- batch-norm statistics
+// tf.contrib.layers.batch_norm(is_training=True) (unet_simple.py:25): per-channel mean and biased
+// variance over N*H*W.  Pass 1: grid (ceil(C/64), nblk); lane = channel (64 consecutive channels of a
+// pixel per wave -> coalesced), the 4 waves of a block stride over pixels, f64 partial sums,
+// combined across waves in LDS.  Pass 2: one thread per channel folds the nblk partials.
+constexpr int BN_NBLK = 240;
+
+template <typename T>
+__global__ __launch_bounds__(256) void bn_partial_kernel(View x, double* part, int nblk) {
+  __shared__ double sh[2][4][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  const long M = (long)x.n * x.h * x.w;
+  double s = 0.0, ss = 0.0;
+  if (c < x.c) {
+    for (long p = (long)blockIdx.y * 4 + wave; p < M; p += (long)nblk * 4) {
+      const double v = ldv(x, p, c);
+      s += v;
+      ss += v * v;
+    }
+  }
+  sh[0][wave][lane] = s;
+  sh[1][wave][lane] = ss;
+  __syncthreads();
+  if (wave == 0 && c < x.c) {
+    s = sh[0][0][lane] + sh[0][1][lane] + sh[0][2][lane] + sh[0][3][lane];
+    ss = sh[1][0][lane] + sh[1][1][lane] + sh[1][2][lane] + sh[1][3][lane];
+    part[(long)blockIdx.y * x.c + c] = s;
+    part[(long)nblk * x.c + (long)blockIdx.y * x.c + c] = ss;
+  }
+}
+
+__global__ void bn_final_kernel(const double* part, int nblk, int C, long M, float* mean, float* var) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s = 0.0, ss = 0.0;
+  for (int b = 0; b < nblk; ++b) {
+    s += part[(long)b * C + c];
+    ss += part[(long)nblk * C + (long)b * C + c];
+  }
+  const double m = s / (double)M;
+  double v = ss / (double)M - m * m;
+  if (v < 0.0) v = 0.0;
+  mean[c] = (float)m;
+  var[c] = (float)v;
+}
+
+__global__ void bn_apply_kernel(View x, View y, const float* mean, const float* var, const float* gamma,
+                                const float* beta, float eps, int act) {
+  const long total = (long)x.n * x.h * x.w * x.c;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % x.c);
+    const long p = i / x.c;
+    const float m = mean ? mean[c] : 0.f;
+    const float v = var ? var[c] : 1.f;
+    const float g = gamma ? gamma[c] : 1.f;
+    const float b = beta ? beta[c] : 0.f;
+    float t = (ldv(x, p, c) - m) * (1.0f / sqrtf(v + eps)) * g + b;
+    t = act == VM_ACT_RELU ? fmaxf(t, 0.f) : act == VM_ACT_SIGMOID ? sigmoid_precise(t) : t;
+    stv(y, p, c, t);
+  }
+}
+
+// ---------------------------------------------------------------- channel softmax (refine.py:31)
+__global__ void softmax_kernel(View x, View y) {
+  const long M = (long)x.n * x.h * x.w;
+  for (long p = blockIdx.x * (long)blockDim.x + threadIdx.x; p < M; p += (long)gridDim.x * blockDim.x) {
+    float mx = -INFINITY;
+    for (int c = 0; c < x.c; ++c) mx = fmaxf(mx, ldv(x, p, c));
+    float s = 0.f;
+    for (int c = 0; c < x.c; ++c) s += expf(ldv(x, p, c) - mx);
+    const float inv = 1.f / s;
+    for (int c = 0; c < x.c; ++c) stv(y, p, c, expf(ldv(x, p, c) - mx) * inv);
+  }
+}
+
+static bool same_dtype_vec(const vm_tensor* x, const vm_tensor* y) {
+  return x->dtype == y->dtype && x->c == y->c && vec16_ok(x) && vec16_ok(y);
+}
+
+}  // namespace vm
+
+using namespace vm;
+
+extern "C" int vm_maxpool2x2_same_nhwc(const vm_tensor* x, vm_tensor* y, void* stream) {
+  if (!valid_tensor(x) || !valid_tensor(y)) return fail(VM_EINVAL, "maxpool: invalid tensor");
+  if (y->n != x->n || y->h != (x->h + 1) / 2 || y->w != (x->w + 1) / 2 || y->c != x->c)
+    return fail(VM_EINVAL, "maxpool: output must be [%d,%d,%d,%d]", x->n, (x->h + 1) / 2, (x->w + 1) / 2, x->c);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const bool vec = same_dtype_vec(x, y);
+  const int ce = vec ? 16 / elem_bytes(x->dtype) : 1;
+  const long work = (long)y->n * y->h * y->w * ((y->c + ce - 1) / ce);
+  const int grid = grid_for(work, 256);
+  View xv = view(x), yv = view(y);
+  if (vec) {
+    if (x->dtype == VM_BF16) hipLaunchKernelGGL((maxpool2x2_kernel<uint16_t, true>), dim3(grid), dim3(256), 0, st, xv, yv);
+    else hipLaunchKernelGGL((maxpool2x2_kernel<float, true>), dim3(grid), dim3(256), 0, st, xv, yv);
+  } else {
+    hipLaunchKernelGGL((maxpool2x2_kernel<float, false>), dim3(grid), dim3(256), 0, st, xv, yv);
+  }
+  return check_launch("maxpool2x2");
+}
+
+extern "C" int vm_resize_bilinear_tf1_nhwc(const vm_tensor* x, vm_tensor* y, void* stream) {
+  if (!valid_tensor(x) || !valid_tensor(y)) return fail(VM_EINVAL, "resize: invalid tensor");
+  if (y->n != x->n || y->c != x->c) return fail(VM_EINVAL, "resize: batch/channel mismatch");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const float sy = (float)x->h / (float)y->h;
+  const float sx = (float)x->w / (float)y->w;
+  const bool vec = same_dtype_vec(x, y);
+  const int ce = vec ? 16 / elem_bytes(x->dtype) : 1;
+  const long work = (long)y->n * y->h * y->w * ((y->c + ce - 1) / ce);
+  const int grid = grid_for(work, 256);
+  View xv = view(x), yv = view(y);
+  // same size: TF-1 resize_images returns its input; the kernel degenerates to a copy (lerp 0)
+  if (vec) {
+    if (x->dtype == VM_BF16)
+      hipLaunchKernelGGL((resize_tf1_kernel<uint16_t, true>), dim3(grid), dim3(256), 0, st, xv, yv, sy, sx);
+    else hipLaunchKernelGGL((resize_tf1_kernel<float, true>), dim3(grid), dim3(256), 0, st, xv, yv, sy, sx);
+  } else {
+    hipLaunchKernelGGL((resize_tf1_kernel<float, false>), dim3(grid), dim3(256), 0, st, xv, yv, sy, sx);
+  }
+  return check_launch("resize_tf1");
+}
+
+extern "C" int vm_convert_nhwc(const vm_tensor* x, vm_tensor* y, const float* scale, const float* shift, int act,
+                               void* stream) {
+  if (!valid_tensor(x) || !valid_tensor(y)) return fail(VM_EINVAL, "convert: invalid tensor");
+  if (y->n != x->n || y->h != x->h || y->w != x->w || y->c < x->c) return fail(VM_EINVAL, "convert: shape mismatch");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const long work = (long)y->n * y->h * y->w * y->c;
+  hipLaunchKernelGGL(convert_kernel, dim3(grid_for(work, 256)), dim3(256), 0, st, view(x), view(y), scale, shift, act);
+  return check_launch("convert");
+}
+
+extern "C" size_t vm_bn_workspace_bytes(const vm_tensor* x) {
+  if (!x) return 0;
+  return (size_t)2 * BN_NBLK * x->c * sizeof(double);
+}
+
+extern "C" int vm_bn_stats_nhwc(const vm_tensor* x, float* mean, float* var, void* work, void* stream) {
+  if (!valid_tensor(x) || !mean || !var || !work) return fail(VM_EINVAL, "bn_stats: bad argument");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const long M = (long)x->n * x->h * x->w;
+  dim3 grid((x->c + 63) / 64, BN_NBLK);
+  double* part = reinterpret_cast<double*>(work);
+  if (x->dtype == VM_BF16) hipLaunchKernelGGL(bn_partial_kernel<uint16_t>, grid, dim3(256), 0, st, view(x), part, BN_NBLK);
+  else hipLaunchKernelGGL(bn_partial_kernel<float>, grid, dim3(256), 0, st, view(x), part, BN_NBLK);
+  int rc = check_launch("bn_partial");
+  if (rc) return rc;
+  hipLaunchKernelGGL(bn_final_kernel, dim3((x->c + 63) / 64), dim3(64), 0, st, part, BN_NBLK, x->c, M, mean, var);
+  return check_launch("bn_final");
+}
+
+extern "C" int vm_bn_apply_nhwc(const vm_tensor* x, vm_tensor* y, const float* mean, const float* var,
+                                const float* gamma, const float* beta, float eps, int act, void* stream) {
+  if (!valid_tensor(x) || !valid_tensor(y)) return fail(VM_EINVAL, "bn_apply: invalid tensor");
+  if (y->n != x->n || y->h != x->h || y->w != x->w || y->c != x->c) return fail(VM_EINVAL, "bn_apply: shape mismatch");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const long work = (long)x->n * x->h * x->w * x->c;
+  hipLaunchKernelGGL(bn_apply_kernel, dim3(grid_for(work, 256)), dim3(256), 0, st, view(x), view(y), mean, var, gamma,
+                     beta, eps, act);
+  return check_launch("bn_apply");
+}
+
+extern "C" int vm_softmax_lastdim_nhwc(const vm_tensor* x, vm_tensor* y, void* stream) {
+  if (!valid_tensor(x) || !valid_tensor(y)) return fail(VM_EINVAL, "softmax: invalid tensor");
+  if (y->n != x->n || y->h != x->h || y->w != x->w || y->c != x->c) return fail(VM_EINVAL, "softmax: shape mismatch");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const long M = (long)x->n * x->h * x->w;
+  hipLaunchKernelGGL(softmax_kernel, dim3(grid_for(M, 256)), dim3(256), 0, st, view(x), view(y));
+  return check_launch("softmax");
+}

@@ -1,0 +1,124 @@
+// Shared helpers for the gfx950 kernels behind include/vmatting.h.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <cstdarg>
+#include <cstdio>
+
+#include "vmatting.h"
+
+namespace vm {
+
+// per-thread error text for vm_last_error()
+void set_error(const char* fmt, ...);
+
+inline int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  set_error("%s", buf);
+  return code;
+}
+
+inline int check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(VM_EHIP, "%s: %s", what, hipGetErrorString(e));
+  return VM_OK;
+}
+
+inline int elem_bytes(int dtype) { return dtype == VM_F32 ? 4 : dtype == VM_BF16 ? 2 : 1; }
+
+inline bool valid_tensor(const vm_tensor* t) {
+  return t && t->ptr && t->n > 0 && t->h > 0 && t->w > 0 && t->c > 0 && t->coff >= 0 &&
+         t->coff + t->c <= t->cstride && (t->dtype == VM_F32 || t->dtype == VM_BF16);
+}
+
+inline bool vec16_ok(const vm_tensor* t, int extra_elems_multiple = 1) {
+  int ve = 16 / elem_bytes(t->dtype);
+  return (reinterpret_cast<uintptr_t>(t->ptr) % 16 == 0) && (t->cstride % ve == 0) && (t->coff % ve == 0) &&
+         (t->c % (ve * extra_elems_multiple) == 0);
+}
+
+// ---------------------------------------------------------------- device helpers
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float bf2f(uint16_t b) { return __uint_as_float(static_cast<uint32_t>(b) << 16); }
+
+__device__ __forceinline__ uint16_t f2bf(float f) {
+  __bf16 b = static_cast<__bf16>(f);  // v_cvt_pk_bf16_f32 on gfx950: RNE, NaN stays NaN
+  return __builtin_bit_cast(uint16_t, b);
+}
+
+template <typename T>
+__device__ __forceinline__ float ld_elem(const T* p);
+template <>
+__device__ __forceinline__ float ld_elem<float>(const float* p) { return *p; }
+template <>
+__device__ __forceinline__ float ld_elem<uint16_t>(const uint16_t* p) { return bf2f(*p); }
+
+template <typename T>
+__device__ __forceinline__ void st_elem(T* p, float v);
+template <>
+__device__ __forceinline__ void st_elem<float>(float* p, float v) { *p = v; }
+template <>
+__device__ __forceinline__ void st_elem<uint16_t>(uint16_t* p, float v) { *p = f2bf(v); }
+
+// 16-byte chunk <-> floats (4 f32 or 8 bf16)
+template <typename T>
+struct Chunk;
+template <>
+struct Chunk<float> {
+  static constexpr int N = 4;
+  __device__ static void unpack(uint4 u, float* f) {
+    f[0] = __uint_as_float(u.x); f[1] = __uint_as_float(u.y);
+    f[2] = __uint_as_float(u.z); f[3] = __uint_as_float(u.w);
+  }
+  __device__ static uint4 pack(const float* f) {
+    return make_uint4(__float_as_uint(f[0]), __float_as_uint(f[1]), __float_as_uint(f[2]), __float_as_uint(f[3]));
+  }
+};
+template <>
+struct Chunk<uint16_t> {
+  static constexpr int N = 8;
+  __device__ static void unpack(uint4 u, float* f) {
+    uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      f[2 * i] = __uint_as_float(w[i] << 16);
+      f[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+    }
+  }
+  __device__ static uint4 pack(const float* f) {
+    uint32_t w[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) w[i] = uint32_t(f2bf(f[2 * i])) | (uint32_t(f2bf(f[2 * i + 1])) << 16);
+    return make_uint4(w[0], w[1], w[2], w[3]);
+  }
+};
+
+__device__ __forceinline__ float act_apply(float v, int act) {
+  if (act == VM_ACT_RELU) return v > 0.f ? v : 0.f;
+  if (act == VM_ACT_SIGMOID) return 1.f / (1.f + __expf(-v));
+  return v;
+}
+
+// exact-ish sigmoid for the f32 parity path (expf, not the fast approximation)
+__device__ __forceinline__ float sigmoid_precise(float v) {
+  if (v >= 0.f) return 1.f / (1.f + expf(-v));
+  float e = expf(v);
+  return e / (1.f + e);
+}
+
+inline int grid_for(long work, int block, int max_blocks = 256 * 16) {
+  long g = (work + block - 1) / block;
+  if (g > max_blocks) g = max_blocks;
+  if (g < 1) g = 1;
+  return static_cast<int>(g);
+}
+
+}  // namespace vm

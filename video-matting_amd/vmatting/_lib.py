@@ -1,0 +1,94 @@
+"""ctypes binding of include/vmatting.h (libvmatting.so, built in-tree for gfx950).
+
+torch is imported first on purpose: its bundled libamdhip64.so.7 is then the HIP
+runtime the library resolves against (same soname), so device pointers and
+streams from torch are valid inside every vm_* call.
+
+There is no CPU fallback anywhere in the product: if the library is missing or
+no GPU is visible, calls raise.
+"""
+
+import ctypes
+import os
+
+import torch  # noqa: F401  (must precede the CDLL load: shared HIP runtime)
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libvmatting.so")
+
+VM_F32, VM_BF16, VM_U8 = 0, 1, 2
+ACT = {"none": 0, "relu": 1, "sigmoid": 2, "softmax": 3}
+VM_OK, VM_EINVAL, VM_EUNSUPPORTED, VM_EHIP, VM_EINDEX = 0, -1, -2, -3, -4
+ABI_VERSION = 1
+
+c_void_p, c_int, c_float, c_long, c_size_t = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_long, ctypes.c_size_t
+
+
+class VmTensor(ctypes.Structure):
+    _fields_ = [("ptr", c_void_p), ("n", ctypes.c_int32), ("h", ctypes.c_int32), ("w", ctypes.c_int32),
+                ("c", ctypes.c_int32), ("cstride", ctypes.c_int32), ("coff", ctypes.c_int32),
+                ("dtype", ctypes.c_int32)]
+
+
+P = ctypes.POINTER(VmTensor)
+
+# (name, restype, argtypes) — one row per declaration in include/vmatting.h
+SIGNATURES = [
+    ("vm_abi_version", c_int, []),
+    ("vm_last_error", ctypes.c_char_p, []),
+    ("vm_conv3x3_packed_bytes", c_size_t, [c_int, c_int, c_int]),
+    ("vm_conv3x3_pack_weights", c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
+    ("vm_conv3x3_nhwc", c_int, [P, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, P, c_void_p]),
+    ("vm_maxpool2x2_same_nhwc", c_int, [P, P, c_void_p]),
+    ("vm_resize_bilinear_tf1_nhwc", c_int, [P, P, c_void_p]),
+    ("vm_convert_nhwc", c_int, [P, P, c_void_p, c_void_p, c_int, c_void_p]),
+    ("vm_bn_workspace_bytes", c_size_t, [P]),
+    ("vm_bn_stats_nhwc", c_int, [P, c_void_p, c_void_p, c_void_p, c_void_p]),
+    ("vm_bn_apply_nhwc", c_int, [P, P, c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_int, c_void_p]),
+    ("vm_softmax_lastdim_nhwc", c_int, [P, P, c_void_p]),
+    ("vm_remap_bilinear_f32", c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_int, c_void_p, c_int,
+                                      c_void_p]),
+    ("vm_remap_bilinear_u8", c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p]),
+    ("vm_fb_consistency", c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_float, c_int, c_void_p, c_void_p]),
+    ("vm_loss_workspace_bytes", c_size_t, [c_long]),
+    ("vm_matting_loss", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_void_p, c_void_p,
+                                c_void_p]),
+]
+
+_lib = None
+
+
+def lib():
+    """Load libvmatting.so once; raise (never fall back) if it is absent or stale."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError("vmatting: %s not built — run `make -C video-matting_amd` or "
+                               "`python -c 'import __graft_entry__ as g; g.build()'`" % LIB_PATH)
+        l = ctypes.CDLL(LIB_PATH)
+        for name, res, args in SIGNATURES:
+            f = getattr(l, name)
+            f.restype = res
+            f.argtypes = args
+        if l.vm_abi_version() != ABI_VERSION:
+            raise RuntimeError("vmatting: ABI %d != %d, rebuild the library" % (l.vm_abi_version(), ABI_VERSION))
+        _lib = l
+    return _lib
+
+
+def check(rc, what):
+    if rc == VM_OK:
+        return
+    msg = "%s: %s" % (what, lib().vm_last_error().decode(errors="replace"))
+    if rc == VM_EINVAL:
+        raise ValueError(msg)
+    if rc == VM_EINDEX:
+        raise IndexError(msg)
+    if rc == VM_EUNSUPPORTED:
+        raise NotImplementedError(msg)
+    raise RuntimeError(msg)
+
+
+def stream_handle(stream=None):
+    s = torch.cuda.current_stream() if stream is None else stream
+    return c_void_p(s.cuda_stream)

@@ -1,0 +1,265 @@
+"""Tensor-level wrappers over the C ABI (torch tensors on a ROCm device in, out).
+
+Each function is one TF/OpenCV op of the reference (cited in include/vmatting.h).
+NHWC views: any torch tensor whose last dim is contiguous and whose pixel rows
+are evenly strided (stride(1) == W*stride(2), stride(0) == H*stride(1)) — in
+particular a channel slice ``buf[..., a:b]`` of a wider buffer, which is how
+tf.concat is expressed without copies.
+"""
+
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import VmTensor, check, lib, stream_handle
+
+_DT = {torch.float32: _lib.VM_F32, torch.bfloat16: _lib.VM_BF16, torch.uint8: _lib.VM_U8}
+TORCH_DTYPE = {"fp32": torch.float32, "f32": torch.float32, "float32": torch.float32,
+               "bf16": torch.bfloat16, "bfloat16": torch.bfloat16}
+
+
+def _require_gpu(t):
+    if not (isinstance(t, torch.Tensor) and t.is_cuda):
+        raise TypeError("vmatting ops take ROCm device tensors (got %r)" % (type(t) if not isinstance(t, torch.Tensor)
+                                                                          else t.device))
+
+
+def nhwc(t):
+    """Describe a 4-D NHWC torch view as a vm_tensor (by value)."""
+    _require_gpu(t)
+    if t.dim() != 4:
+        raise ValueError("expected NHWC 4-D tensor, got shape %s" % (tuple(t.shape),))
+    n, h, w, c = t.shape
+    s0, s1, s2, s3 = t.stride()
+    if s3 != 1 or (h > 1 and s1 != w * s2) or (n > 1 and s0 != h * s1):
+        raise ValueError("tensor is not an NHWC channel-slice view (strides %s)" % (t.stride(),))
+    if t.dtype not in _DT:
+        raise TypeError("unsupported dtype %s" % t.dtype)
+    return VmTensor(t.data_ptr(), n, h, w, c, s2, 0, _DT[t.dtype])
+
+
+def _ptr(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _f32(t):
+    if t is None:
+        return None
+    _require_gpu(t)
+    assert t.dtype == torch.float32 and t.is_contiguous()
+    return t
+
+
+# ---------------------------------------------------------------------------------------------- conv
+
+class PackedConv:
+    """One 3x3 conv's weights in kernel layout, plus its f32 bias / per-channel affine (folded BN).
+
+    ``w_hwio``: TF-layout filter [3,3,cin,cout] (numpy or tensor).  The reference creates
+    these in unet.py:11-17 (init_conv) / 65-74 (VGG filters).
+    """
+
+    def __init__(self, w_hwio, bias=None, dtype="bf16", device="cuda", scale=None, shift=None):
+        w = torch.as_tensor(np.asarray(w_hwio, np.float32) if not isinstance(w_hwio, torch.Tensor) else w_hwio,
+                            dtype=torch.float32).to(device).contiguous()
+        if w.dim() != 4 or w.shape[0] != 3 or w.shape[1] != 3:
+            raise ValueError("expected a [3,3,cin,cout] filter, got %s" % (tuple(w.shape),))
+        self.cin, self.cout = int(w.shape[2]), int(w.shape[3])
+        self.dtype = TORCH_DTYPE[dtype] if isinstance(dtype, str) else dtype
+        self.w_hwio = w
+        vdt = _DT[self.dtype]
+        nbytes = lib().vm_conv3x3_packed_bytes(self.cin, self.cout, vdt)
+        self.packed = torch.empty(nbytes, dtype=torch.uint8, device=device)
+        check(lib().vm_conv3x3_pack_weights(_ptr(w), self.cin, self.cout, vdt, _ptr(self.packed),
+                                            stream_handle()), "pack_weights")
+        as_f = lambda v: None if v is None else torch.as_tensor(np.asarray(v, np.float32) if not isinstance(  # noqa
+            v, torch.Tensor) else v, dtype=torch.float32).to(device).contiguous()
+        self.bias = as_f(bias)
+        self.scale = as_f(scale)
+        self.shift = as_f(shift)
+
+    def set_affine(self, scale, shift):
+        self.scale = None if scale is None else torch.as_tensor(scale, dtype=torch.float32).to(self.packed.device)
+        self.shift = None if shift is None else torch.as_tensor(shift, dtype=torch.float32).to(self.packed.device)
+
+    def __call__(self, x, act="none", out=None, out_dtype=None, affine=None):
+        return conv3x3(x, self, act, out, out_dtype, affine)
+
+
+def conv3x3(x, pc, act="none", out=None, out_dtype=None, affine=None):
+    """tf.nn.conv2d 3x3 SAME + bias_add (+ folded BN affine) + activation, on MFMA.
+
+    ``affine``: None -> the PackedConv's own scale/shift; False -> none; (scale, shift) -> those.
+    """
+    if x.dtype != pc.dtype:
+        raise TypeError("conv input dtype %s != packed weights dtype %s" % (x.dtype, pc.dtype))
+    if x.shape[-1] != pc.cin:
+        raise ValueError("conv input has %d channels, filter expects %d" % (x.shape[-1], pc.cin))
+    n, h, w, _ = x.shape
+    if out is None:
+        out = torch.empty((n, h, w, pc.cout), dtype=out_dtype or x.dtype, device=x.device)
+    if affine is None:
+        scale, shift = pc.scale, pc.shift
+    elif affine is False:
+        scale = shift = None
+    else:
+        scale, shift = affine
+    xv, yv = nhwc(x), nhwc(out)
+    prof = _CONV_PROFILE
+    if prof is not None:
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev1 = torch.cuda.Event(enable_timing=True)
+        ev0.record()
+    check(lib().vm_conv3x3_nhwc(ctypes.byref(xv), _ptr(pc.packed), pc.cin, pc.cout, _ptr(pc.bias), _ptr(scale),
+                                _ptr(shift), _lib.ACT[act], ctypes.byref(yv), stream_handle()), "conv3x3")
+    if prof is not None:
+        ev1.record()
+        prof.append((2 * n * h * w * 9 * pc.cin * pc.cout, pc.cout == 1, ev0, ev1))
+    return out
+
+
+# When a list, conv3x3 appends (algorithmic FLOPs, is_head, start_event, end_event) per launch —
+# HIP events on the launch stream, used by bench.py for the roofline's achieved TFLOP/s.
+_CONV_PROFILE = None
+
+
+def conv_profile(enable):
+    global _CONV_PROFILE
+    _CONV_PROFILE = [] if enable else None
+    return _CONV_PROFILE
+
+
+# ---------------------------------------------------------------------------------------------- memory-bound ops
+
+def maxpool2x2(x, out=None):
+    """tf.nn.max_pool 2x2/2 SAME."""
+    n, h, w, c = x.shape
+    if out is None:
+        out = torch.empty((n, (h + 1) // 2, (w + 1) // 2, c), dtype=x.dtype, device=x.device)
+    xv, yv = nhwc(x), nhwc(out)
+    check(lib().vm_maxpool2x2_same_nhwc(ctypes.byref(xv), ctypes.byref(yv), stream_handle()), "maxpool2x2")
+    return out
+
+
+def resize_bilinear(x, size, out=None):
+    """tf.image.resize_images(x, size) with TF-1.x defaults (bilinear, legacy coordinates)."""
+    n, h, w, c = x.shape
+    oh, ow = int(size[0]), int(size[1])
+    if out is None:
+        out = torch.empty((n, oh, ow, c), dtype=x.dtype, device=x.device)
+    xv, yv = nhwc(x), nhwc(out)
+    check(lib().vm_resize_bilinear_tf1_nhwc(ctypes.byref(xv), ctypes.byref(yv), stream_handle()), "resize")
+    return out
+
+
+def convert(x, out, scale=None, shift=None, act="none"):
+    """Copy x into out (dtype change, zero-filled extra channels, optional affine + activation)."""
+    xv, yv = nhwc(x), nhwc(out)
+    check(lib().vm_convert_nhwc(ctypes.byref(xv), ctypes.byref(yv), _ptr(_f32(scale)), _ptr(_f32(shift)),
+                                _lib.ACT[act], stream_handle()), "convert")
+    return out
+
+
+_ws_cache = {}
+
+
+def _workspace(nbytes, device):
+    key = (str(device), torch.cuda.current_stream(device).cuda_stream)
+    buf = _ws_cache.get(key)
+    if buf is None or buf.numel() < nbytes:
+        buf = torch.empty(max(nbytes, 1 << 16), dtype=torch.uint8, device=device)
+        _ws_cache[key] = buf
+    return buf
+
+
+def bn_stats(x, mean=None, var=None):
+    """Batch mean / biased variance over N,H,W (tf.contrib batch_norm, is_training=True)."""
+    c = x.shape[-1]
+    mean = torch.empty(c, dtype=torch.float32, device=x.device) if mean is None else mean
+    var = torch.empty(c, dtype=torch.float32, device=x.device) if var is None else var
+    xv = nhwc(x)
+    ws = _workspace(lib().vm_bn_workspace_bytes(ctypes.byref(xv)), x.device)
+    check(lib().vm_bn_stats_nhwc(ctypes.byref(xv), _ptr(mean), _ptr(var), _ptr(ws), stream_handle()), "bn_stats")
+    return mean, var
+
+
+def bn_apply(x, mean, var, gamma, beta, eps=1e-3, act="none", out=None):
+    out = x if out is None else out
+    xv, yv = nhwc(x), nhwc(out)
+    check(lib().vm_bn_apply_nhwc(ctypes.byref(xv), ctypes.byref(yv), _ptr(mean), _ptr(var), _ptr(gamma),
+                                 _ptr(beta), float(eps), _lib.ACT[act], stream_handle()), "bn_apply")
+    return out
+
+
+def softmax_lastdim(x, out=None):
+    out = torch.empty_like(x) if out is None else out
+    xv, yv = nhwc(x), nhwc(out)
+    check(lib().vm_softmax_lastdim_nhwc(ctypes.byref(xv), ctypes.byref(yv), stream_handle()), "softmax")
+    return out
+
+
+# ---------------------------------------------------------------------------------------------- flow
+
+def remap_f32(img, flow, mode="opencv", out=None):
+    """Backward warp of single-channel f32 frames: img [n?,ih,iw], flow [n?,h,w,2] -> [n?,h,w]."""
+    _require_gpu(img)
+    _require_gpu(flow)
+    batched = flow.dim() == 4
+    f = flow if batched else flow[None]
+    im = img if img.dim() == 3 else img[None]
+    n, h, w, two = f.shape
+    if two != 2 or im.shape[0] != n:
+        raise ValueError("flow must be [h,w,2] (or [n,h,w,2]) matching img frames")
+    im = im.contiguous().float()
+    f = f.contiguous().float()
+    if out is None:
+        out = torch.empty((n, h, w), dtype=torch.float32, device=img.device)
+    check(lib().vm_remap_bilinear_f32(_ptr(im), im.shape[1], im.shape[2], _ptr(f), h, w, n, _ptr(out),
+                                      0 if mode == "opencv" else 1, stream_handle()), "remap_f32")
+    return out if batched else out[0]
+
+
+def remap_u8(img, flow):
+    _require_gpu(img)
+    _require_gpu(flow)
+    img = img.contiguous()
+    ih, iw = img.shape[:2]
+    cn = 1 if img.dim() == 2 else img.shape[2]
+    h, w = flow.shape[:2]
+    out = torch.empty((h, w) + (() if img.dim() == 2 else (cn,)), dtype=torch.uint8, device=img.device)
+    f = flow.contiguous().float()
+    check(lib().vm_remap_bilinear_u8(_ptr(img), ih, iw, cn, _ptr(f), h, w, _ptr(out), stream_handle()), "remap_u8")
+    return out
+
+
+def fb_consistency(backward, forward, alpha, thresh=15.0, promote="numpy1"):
+    """flow.correct_alpha on device; alpha (f32 [h,w], contiguous) is modified in place."""
+    for t in (backward, forward, alpha):
+        _require_gpu(t)
+    h, w = backward.shape[:2]
+    if alpha.dtype != torch.float32 or not alpha.is_contiguous() or tuple(alpha.shape) != (h, w):
+        raise ValueError("alpha must be a contiguous f32 [h,w] device tensor")
+    bw = backward.contiguous().float()
+    fw = forward.contiguous().float()
+    err = torch.zeros(1, dtype=torch.int32, device=alpha.device)
+    check(lib().vm_fb_consistency(_ptr(bw), _ptr(fw), h, w, _ptr(alpha), float(thresh),
+                                  0 if promote == "numpy1" else 1, _ptr(err), stream_handle()), "fb_consistency")
+    if int(err.item()) != 0:
+        raise IndexError("correct_alpha: a backward-flow target lies more than one frame outside the image "
+                         "(the reference's numpy IndexError, flow.py:46)")
+    return alpha
+
+
+def matting_loss(pred, gt, raw_fg, in_bg, in_cmp):
+    """train.py:42-47 loss on device -> tensor [loss, alpha_loss, compositional_loss]."""
+    ts = [t.contiguous().float() for t in (pred, gt, raw_fg, in_bg, in_cmp)]
+    for t in ts:
+        _require_gpu(t)
+    pixels = ts[0].numel()
+    out = torch.empty(3, dtype=torch.float32, device=pred.device)
+    ws = _workspace(lib().vm_loss_workspace_bytes(pixels), pred.device)
+    check(lib().vm_matting_loss(*[_ptr(t) for t in ts], pixels, _ptr(out), _ptr(ws), stream_handle()),
+          "matting_loss")
+    return out

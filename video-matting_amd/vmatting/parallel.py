@@ -1,0 +1,63 @@
+"""Frame-parallel execution across the GPUs of a node (one process per GPU, RCCL over xGMI).
+
+Frames are independent at inference (UNetVideo has no BN; BN in inference mode is a
+per-frame affine), so a video batch is split into contiguous per-rank blocks and every
+rank runs the whole network on its block with no communication in the data path.
+Collectives exist only at the edges: one broadcast of the packed weights from rank 0
+(so every replica computes with bit-identical weights) and an optional all-gather of
+the mattes.  backend 'nccl' is RCCL on ROCm; 'gloo' runs the same code on CPU tensors.
+"""
+
+import os
+
+import torch
+import torch.distributed as dist
+
+
+def init_from_env(backend=None):
+    """Initialise torch.distributed from torchrun's env (RANK/WORLD_SIZE/MASTER_*) if present."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 and not dist.is_initialized():
+        if backend is None:
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+        dist.init_process_group(backend=backend)
+    return rank, world, local
+
+
+def shard_range(n_frames, rank, world):
+    """Contiguous block of frames for ``rank``: [start, stop)."""
+    start = (n_frames * rank) // world
+    stop = (n_frames * (rank + 1)) // world
+    return start, stop
+
+
+def broadcast_tensors(tensors, src=0):
+    """Broadcast a list of same-device tensors from ``src`` with ONE collective (flattened byte buffer)."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return tensors
+    flat = torch.cat([t.contiguous().view(-1).view(torch.uint8) for t in tensors])
+    dist.broadcast(flat, src)
+    off = 0
+    for t in tensors:
+        nb = t.numel() * t.element_size()
+        t.view(-1).view(torch.uint8).copy_(flat[off:off + nb])
+        off += nb
+    return tensors
+
+
+def gather_frames(local, n_frames):
+    """All-gather per-rank frame blocks (contiguous, possibly uneven) into the full [n_frames, ...] batch."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return local
+    world = dist.get_world_size()
+    sizes = [shard_range(n_frames, r, world) for r in range(world)]
+    mx = max(b - a for a, b in sizes)
+    pad = torch.zeros((mx,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+    pad[:local.shape[0]] = local
+    parts = [torch.empty_like(pad) for _ in range(world)]
+    dist.all_gather(parts, pad)
+    return torch.cat([p[:b - a] for p, (a, b) in zip(parts, sizes)], dim=0)

@@ -1,0 +1,235 @@
+"""U-Net encoder-decoder (reference unet.py) on gfx950 kernels.
+
+Same construction API as the reference: ``UNetVideo(vgg16_npy_path).build(input)``
+sets ``.output`` (sigmoid alpha) and every intermediate attribute the reference
+sets (conv1_1 ... conv5_2, pool1..4, upconv1..4, conv4_4, conv3_4, conv2_3,
+conv1_3) — unet.py:86-217.  ``input`` is an NHWC [N,H,W,7] (video) / [N,H,W,6]
+(image) float32 frame batch (cmp-VGG_MEAN, bg-VGG_MEAN[, trimap-0.5]); numpy
+arrays are uploaded.  Because the reference's build() only wires a graph that
+sess.run evaluates later, the GPU version also offers ``forward(x)`` to evaluate
+the built network again on new frames with the same weights and buffers.
+
+Data layout in HBM (compute dtype T = bf16 or f32, NHWC, channels innermost):
+  in8   [N,H,W,8]      the 7-ch frame padded to 8 channels (16-byte pixel rows)
+  cat1  [N,H,W,128]    [upconv_4 conv | conv1_2]  = the reference's upconv4 concat
+  cat2  [N,H/2,W/2,256], cat3 [..,512], cat4 [..,1024]: the same for levels 2..4
+so every tf.concat (unet.py:62) is a pair of channel-slice writes, never a copy.
+"""
+
+import numpy as np
+import torch
+
+from . import ops
+from .weights import init_conv, load_vgg16
+
+# fresh convs in graph-build order (unet.py:191-203): scope, cin, cout, keeps bias
+NEW_CONVS = (("upconv_1", 512, 512, False), ("conv4_4", 1024, 512, True),
+             ("upconv_2", 512, 256, False), ("conv3_4", 512, 256, True),
+             ("upconv_3", 256, 128, False), ("conv2_3", 256, 128, True),
+             ("upconv_4", 128, 64, False), ("conv1_5", 128, 1, True))
+
+VGG_USED = ("conv1_1", "conv1_2", "conv2_1", "conv2_2", "conv3_1", "conv3_2", "conv3_3",
+            "conv4_1", "conv4_2", "conv4_3", "conv5_1", "conv5_2")
+
+
+def _levels(h, w):
+    lv = [(h, w)]
+    for _ in range(4):
+        lv.append(((lv[-1][0] + 1) // 2, (lv[-1][1] + 1) // 2))  # SAME 2x2/2 pool: ceil
+    return lv
+
+
+class UNet:
+    """Base class (unet.py:20-83)."""
+
+    IN_CH = None
+
+    def __init__(self, vgg16_npy_path=None, dtype="bf16", device="cuda"):
+        self.data_dict = load_vgg16(vgg16_npy_path)
+        self.dtype = ops.TORCH_DTYPE[dtype] if isinstance(dtype, str) else dtype
+        self.device = torch.device(device)
+        self.params = None       # name -> (w_hwio f32 np, bias f32 np | None)
+        self.convs = None        # name -> ops.PackedConv
+        self._ws = None
+        self._ws_key = None
+
+    # ------------------------------------------------------------------ weights
+    def get_conv_filter(self, name):
+        raise NotImplementedError
+
+    def _make_params(self):
+        """VGG filters from data_dict (unet.py:65-77, 150-157/210-217) and init_conv draws in build order."""
+        p = {}
+        for name in VGG_USED:
+            p[name] = (self.get_conv_filter(name), np.asarray(self.data_dict[name][1], np.float32))
+        for name, cin, cout, keep_bias in NEW_CONVS:
+            w, b = init_conv(cin, cout)
+            p[name] = (w, b if keep_bias else None)
+        return p
+
+    def load_params(self, params):
+        """Install explicit weights {scope: (w_hwio, bias|None)} (e.g. from a checkpoint)."""
+        self.params = {k: (np.asarray(w, np.float32), None if b is None else np.asarray(b, np.float32))
+                       for k, (w, b) in params.items()}
+        self.convs = None
+        return self
+
+    def _pack(self):
+        self.convs = {k: ops.PackedConv(w, b, self.dtype, self.device) for k, (w, b) in self.params.items()}
+
+    def weights_flat(self):
+        """All packed weights as one list of tensors (for an RCCL broadcast from rank 0)."""
+        out = []
+        for k in sorted(self.convs):
+            pc = self.convs[k]
+            out.append(pc.packed)
+            if pc.bias is not None:
+                out.append(pc.bias)
+        return out
+
+    # ------------------------------------------------------------------ buffers
+    def _buffers(self, n, h, w):
+        key = (n, h, w)
+        if self._ws_key == key:
+            return self._ws
+        T, dev = self.dtype, self.device
+        L = _levels(h, w)
+        E = lambda lv, c, dt=T: torch.empty((n, L[lv][0], L[lv][1], c), dtype=dt, device=dev)  # noqa: E731
+        ws = dict(
+            in8=E(0, 8), c11=E(0, 64), cat1=E(0, 128), r4=E(0, 128),
+            p1=E(1, 64), c21=E(1, 128), cat2=E(1, 256), r3=E(1, 256), c23=E(1, 128),
+            p2=E(2, 128), c31=E(2, 256), c32=E(2, 256), cat3=E(2, 512), r2=E(2, 512), c34=E(2, 256),
+            p3=E(3, 256), c41=E(3, 512), c42=E(3, 512), cat4=E(3, 1024), r1=E(3, 512), c44=E(3, 512),
+            p4=E(4, 512), c51=E(4, 512), c52=E(4, 512),
+            logits=E(0, 1, torch.float32), out=E(0, 1, torch.float32))
+        self._ws, self._ws_key = ws, key
+        return ws
+
+    # ------------------------------------------------------------------ graph
+    def build(self, input):
+        """unet.UNet*.build (unet.py:87-148 / 161-208): create weights (first call), run, set attributes."""
+        x = self._as_input(input)
+        if self.params is None:
+            self.params = self._make_params()
+        if self.convs is None:
+            self._pack()
+        self.forward(x)
+        self.data_dict = None  # unet.py:147,207
+        return self.output
+
+    def _as_input(self, input):
+        x = input if isinstance(input, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(input, np.float32))
+        x = x.to(self.device, torch.float32)
+        if x.dim() != 4 or x.shape[-1] != self.IN_CH:
+            raise ValueError("%s.build expects [N,H,W,%d] input, got %s" % (type(self).__name__, self.IN_CH,
+                                                                            tuple(x.shape)))
+        return x
+
+    def forward(self, input):
+        """Evaluate the built network on new frames; returns .output (f32 [N,H,W,1])."""
+        x = self._as_input(input) if not (isinstance(input, torch.Tensor) and input.is_cuda and
+                                          input.dtype == torch.float32) else input
+        if self.convs is None:
+            raise RuntimeError("call build() first")
+        n, h, w, c = x.shape
+        b = self._buffers(n, h, w)
+        L = _levels(h, w)
+        C = self.convs
+        ops.convert(x, b["in8"])
+        xin = b["in8"][..., :c]
+        ops.conv3x3(xin, C["conv1_1"], "relu", out=b["c11"])
+        ops.conv3x3(b["c11"], C["conv1_2"], "relu", out=b["cat1"][..., 64:])
+        ops.maxpool2x2(b["cat1"][..., 64:], out=b["p1"])
+        ops.conv3x3(b["p1"], C["conv2_1"], "relu", out=b["c21"])
+        ops.conv3x3(b["c21"], C["conv2_2"], "relu", out=b["cat2"][..., 128:])
+        ops.maxpool2x2(b["cat2"][..., 128:], out=b["p2"])
+        ops.conv3x3(b["p2"], C["conv3_1"], "relu", out=b["c31"])
+        ops.conv3x3(b["c31"], C["conv3_2"], "relu", out=b["c32"])
+        ops.conv3x3(b["c32"], C["conv3_3"], "relu", out=b["cat3"][..., 256:])
+        ops.maxpool2x2(b["cat3"][..., 256:], out=b["p3"])
+        ops.conv3x3(b["p3"], C["conv4_1"], "relu", out=b["c41"])
+        ops.conv3x3(b["c41"], C["conv4_2"], "relu", out=b["c42"])
+        ops.conv3x3(b["c42"], C["conv4_3"], "relu", out=b["cat4"][..., 512:])
+        ops.maxpool2x2(b["cat4"][..., 512:], out=b["p4"])
+        ops.conv3x3(b["p4"], C["conv5_1"], "relu", out=b["c51"])
+        ops.conv3x3(b["c51"], C["conv5_2"], "relu", out=b["c52"])
+        # decoder: upconv_concat = resize -> conv (no bias, no relu) -> [up, skip] (unet.py:44-63)
+        ops.resize_bilinear(b["c52"], L[3], out=b["r1"])
+        ops.conv3x3(b["r1"], C["upconv_1"], "none", out=b["cat4"][..., :512])
+        ops.conv3x3(b["cat4"], C["conv4_4"], "relu", out=b["c44"])
+        ops.resize_bilinear(b["c44"], L[2], out=b["r2"])
+        ops.conv3x3(b["r2"], C["upconv_2"], "none", out=b["cat3"][..., :256])
+        ops.conv3x3(b["cat3"], C["conv3_4"], "relu", out=b["c34"])
+        ops.resize_bilinear(b["c34"], L[1], out=b["r3"])
+        ops.conv3x3(b["r3"], C["upconv_3"], "none", out=b["cat2"][..., :128])
+        ops.conv3x3(b["cat2"], C["conv2_3"], "relu", out=b["c23"])
+        ops.resize_bilinear(b["c23"], L[0], out=b["r4"])
+        ops.conv3x3(b["r4"], C["upconv_4"], "none", out=b["cat1"][..., :64])
+        ops.conv3x3(b["cat1"], C["conv1_5"], "none", out=b["logits"])
+        ops.convert(b["logits"], b["out"], act="sigmoid")
+        self._publish(b)
+        return self.output
+
+    def _publish(self, b):
+        self.conv1_1 = b["c11"]
+        self.conv1_2 = b["cat1"][..., 64:]
+        self.pool1 = b["p1"]
+        self.conv2_1 = b["c21"]
+        self.conv2_2 = b["cat2"][..., 128:]
+        self.pool2 = b["p2"]
+        self.conv3_1, self.conv3_2 = b["c31"], b["c32"]
+        self.conv3_3 = b["cat3"][..., 256:]
+        self.pool3 = b["p3"]
+        self.conv4_1, self.conv4_2 = b["c41"], b["c42"]
+        self.conv4_3 = b["cat4"][..., 512:]
+        self.pool4 = b["p4"]
+        self.conv5_1, self.conv5_2 = b["c51"], b["c52"]
+        self.upconv1, self.conv4_4 = b["cat4"], b["c44"]
+        self.upconv2, self.conv3_4 = b["cat3"], b["c34"]
+        self.upconv3, self.conv2_3 = b["cat2"], b["c23"]
+        self.upconv4 = b["cat1"]
+        self.conv1_3 = b["logits"]  # scope 'conv1_5' (unet.py:143/203)
+        self.output = b["out"]
+
+    # FLOPs of the 20 convs for an [n,h,w] batch (2 * sum H*W*9*Cin*Cout) — the roofline numerator
+    def conv_flops(self, n, h, w):
+        L = _levels(h, w)
+        lv = {"conv1_1": 0, "conv1_2": 0, "conv2_1": 1, "conv2_2": 1, "conv3_1": 2, "conv3_2": 2, "conv3_3": 2,
+              "conv4_1": 3, "conv4_2": 3, "conv4_3": 3, "conv5_1": 4, "conv5_2": 4, "upconv_1": 3, "conv4_4": 3,
+              "upconv_2": 2, "conv3_4": 2, "upconv_3": 1, "conv2_3": 1, "upconv_4": 0, "conv1_5": 0}
+        tot = 0
+        for k, (wt, _) in self.params.items():
+            hh, ww = L[lv[k]]
+            cin = self.IN_CH if k == "conv1_1" else wt.shape[2]
+            tot += 2 * n * hh * ww * 9 * cin * wt.shape[3]
+        return tot
+
+
+class UNetImage(UNet):
+    """unet.UNetImage (unet.py:86-157): 6-channel input, conv1_1 = [VGG/2, VGG/2]."""
+
+    IN_CH = 6
+
+    def get_conv_filter(self, name):
+        w = np.asarray(self.data_dict[name][0], np.float32)
+        if name == "conv1_1":
+            t = np.zeros((3, 3, 6, 64), dtype=np.float32)
+            t[:, :, :3, :] = w / 2.0
+            t[:, :, 3:6, :] = w / 2.0
+            return t
+        return w
+
+
+class UNetVideo(UNet):
+    """unet.UNetVideo (unet.py:160-217): 7-channel input (cmp, bg, trimap), conv1_1 = [VGG, VGG, 0]."""
+
+    IN_CH = 7
+
+    def get_conv_filter(self, name):
+        w = np.asarray(self.data_dict[name][0], np.float32)
+        if name == "conv1_1":
+            t = np.zeros((3, 3, 7, 64), dtype=np.float32)
+            t[:, :, :3, :] = w
+            t[:, :, 3:6, :] = w
+            return t
+        return w
