@@ -59,6 +59,11 @@ typedef struct vm_tensor {
 
 int vm_abi_version(void);
 const char* vm_last_error(void);
+/* Process-wide tuning knobs (no reference counterpart; TF picks kernels itself):
+ *   "conv_kernel"    0 = auto (default), 1 = register-staged MFMA kernel only, 2 = LDS-DMA kernel when legal
+ *   "conv_min_tiles" grid size (256-wide output tiles) from which auto uses the LDS-DMA kernel (default 128)
+ *   "glds_rb"        K-step bytes of the 256x256 LDS-DMA tile: 128 (2-slot ring, default) or 64 (4-slot) */
+int vm_set_option(const char* key, long value);
 
 /* ---------------------------------------------------------------- 3x3 convolution
  * Replaces tf.nn.conv2d(x, w, [1,1,1,1], 'SAME') + tf.nn.bias_add + the activation /
@@ -67,7 +72,8 @@ const char* vm_last_error(void);
  *   unet_simple.py:19-27, 30-42, 98-107; small.py:13-34; refine.py:18-25.
  * y = act((conv(x, w) + bias) * scale + shift) per output channel; bias/scale/shift
  * may be NULL (f32 device arrays of length cout).  Weights are first packed from
- * TF's HWIO f32 layout into the kernel's [cout_pad][K_pad] layout (K = tap*cin_pad + c).
+ * TF's HWIO f32 layout into the kernel's [cout_pad][K_pad] layout (K ordered channel-chunk-major:
+ * the 9 taps of each 128-byte channel chunk are consecutive, so shared input rows stay L2-resident).
  * Computes in x->dtype (bf16 -> MFMA 16x16x32 bf16, f32 -> exact-f32 MFMA 16x16x4),
  * accumulates in f32.  cout == 1 dispatches the memory-bound head kernel.
  * act == VM_ACT_SOFTMAX needs cout <= 128 (whole channel row in one tile).

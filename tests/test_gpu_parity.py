@@ -55,9 +55,18 @@ CONV_CASES = [  # n, h, w, cin, cout, coff_in, act
 ]
 
 
+@pytest.fixture(params=["regstage", "lds_dma"])
+def conv_kernel(request):
+    """Run a test once per conv kernel: 1 = register-staged, 2 = LDS-DMA pipelined (forced even on small grids)."""
+    from vmatting import _lib
+    _lib.set_option("conv_kernel", 1 if request.param == "regstage" else 2)
+    yield request.param
+    _lib.set_option("conv_kernel", 0)
+
+
 @pytest.mark.parametrize("dtype", ["fp32", "bf16"])
 @pytest.mark.parametrize("case", CONV_CASES)
-def test_conv3x3_vs_oracle(case, dtype):
+def test_conv3x3_vs_oracle(case, dtype, conv_kernel):
     from vmatting import ops
     n, h, w, cin, cout, coff, act = case
     rs = np.random.RandomState(cin * 7 + cout)
@@ -155,6 +164,17 @@ def test_unet_fp32_matches_reference_golden(case, vgg0):
     assert np.all(np.abs(logits - g["logits"]) <= 1e-4 * np.abs(g["logits"]).max() + 1e-4)
     for k in ("pool4", "upconv1", "conv2_3"):
         assert relerr(H(getattr(m, k)), g[k]) < 1e-5, k
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_unet_both_conv_kernels_agree_with_golden(dtype, conv_kernel, vgg0):
+    from vmatting import unet
+    g = golden("unet_video_70x90_unit")
+    np.random.seed(int(g["weight_seed"]))
+    m = unet.UNetVideo(vgg0, dtype=dtype)
+    m.build(g["x"])
+    err = np.abs(H(m.output) - g["output"]).max()
+    assert err <= (1e-4 if dtype == "fp32" else 2e-2), err
 
 
 def test_unet_forward_reuse_and_batch_consistency(vgg0):

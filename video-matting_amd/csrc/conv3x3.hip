@@ -3,19 +3,24 @@
 // Replaces tf.nn.conv2d + tf.nn.bias_add (+ relu / sigmoid / inference BN / softmax) at
 // unet.py:35-42, 44-63, 65-74; unet_simple.py:19-42, 98-107; small.py:13-34; refine.py:18-31.
 //
-// GEMM view: D[cout][pixel] = sum_k Wp[cout][k] * X[pixel][k], k = tap*cin_pad + c,
-// tap = kh*3 + kw, X[pixel][k] = x[n, h+kh-1, w+kw-1, c] (zero outside the frame).
-//   A operand = packed weights (rows = output channels), B operand = activations
-//   (rows = pixels); both K-contiguous, so every MFMA operand fragment is ONE 16-byte
-//   LDS read per lane.  Output of a 16x16 MFMA tile: lane holds 4 consecutive output
-//   channels of one pixel -> 16-byte LDS staging writes, then coalesced 16-byte stores.
-// Tiles: 256 threads = 4 waves, each wave 64 pixels x 64 channels (4x4 MFMA 16x16 tiles);
-//   block tile (BM pixels x BN channels) = (128 x 128) or (256 x 64).
-// K-step: one 128-byte row per operand row (64 bf16 / 32 f32), double-buffered in LDS,
-//   register-staged global loads issued before the MFMAs of the previous step.
-// LDS image: [row][8 x 16-byte chunks], chunk XOR-swizzled by (row>>1)&7 — conflict-free for
-//   the ds_read_b128 lane groups of a 16-row fragment read.
-// bf16: v_mfma_f32_16x16x32_bf16; f32: v_mfma_f32_16x16x4_f32 (exact f32 products, f32 sums).
+// GEMM view: D[cout][pixel] = sum_k Wp[cout][k] * X[pixel][k], k <-> (tap, c), tap = kh*3 + kw,
+// X[pixel][k] = x[n, h+kh-1, w+kw-1, c] (zero outside the frame).
+//   A operand = packed weights (rows = output channels), B operand = activations (rows = pixels);
+//   both K-contiguous, so every MFMA operand fragment is ONE 16-byte LDS read per lane, and a 16x16
+//   MFMA tile leaves 4 consecutive output channels of one pixel in each lane.
+// K layout ("granules" of 64 bytes = GE elements): when cin_pad % GE == 0 the K axis is
+//   channel-chunk-major — granule g covers channels (g/9)*GE .. +GE of tap g%9 — so the 9 taps that
+//   re-read the same input rows are consecutive K-steps and hit L2; otherwise tap-major k = tap*cin_pad+c.
+//
+// Two kernels:
+//   conv3x3_mfma  register-staged, 256 threads, tiles 128x128 / 256x64, 128-byte K-steps, 2-slot LDS.
+//                 Used for small grids, the fused softmax and as the reference implementation.
+//   conv3x3_glds  LDS-DMA pipelined (buffer_load ... lds), 512 threads, tiles 256x256 / 256x128 / 512x64,
+//                 64-byte K-steps in a 4-6 slot ring with counted vmcnt (3-5 stages in flight).
+// bf16: v_mfma_f32_16x16x32_bf16; f32: v_mfma_f32_16x16x4_f32 (exact f32 products; a 2-level sum).
+
+#include <cstdlib>
+#include <cstring>
 
 #include "vm_common.h"
 
@@ -26,6 +31,7 @@ struct ConvArgs {
   int x_cstride, x_coff, H, W;
   long M;  // N*H*W pixels
   int cin_pad, K9, nk;
+  int chunk_major, ng;  // granule layout and number of real granules (chunk-major)
   const void* w;
   int K_pad, cout, cout_pad;
   const float* bias;
@@ -37,9 +43,35 @@ struct ConvArgs {
   int tiles_n, tiles_total;
 };
 
-constexpr int ROWB = 128;  // bytes of one operand row per K-step
+// (K element index k) -> (tap, channel); tap 9 = padding (contributes zero)
+template <int GE>
+__device__ __forceinline__ void k_to_tap(const ConvArgs& a, int k, int& tap, int& c) {
+  if (a.chunk_major) {
+    const int g = k / GE;
+    if (g < a.ng) {
+      const int cc = g / 9;
+      tap = g - cc * 9;
+      c = cc * GE + (k - g * GE);
+    } else {
+      tap = 9;
+      c = 0;
+    }
+  } else if (k < a.K9) {
+    tap = k / a.cin_pad;
+    c = k - tap * a.cin_pad;
+  } else {
+    tap = 9;
+    c = 0;
+  }
+}
 
-__device__ __forceinline__ int swz(int row, int chunk) { return row * ROWB + ((chunk ^ ((row >> 1) & 7)) << 4); }
+// LDS images are [row][RB bytes] with the 16-byte chunk index XOR-swizzled per row; both swizzles
+// make the ds_read_b128 lane groups of a 16-row fragment read conflict-free from ANY starting row.
+template <int RB>
+__device__ __forceinline__ int swz(int row, int chunk) {
+  if constexpr (RB == 128) return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4);
+  else return row * 64 + ((chunk ^ (((row >> 2) & 1) << 1)) << 4);
+}
 
 template <typename T>
 __device__ __forceinline__ void mma16(const uint4& a, const uint4& b, f32x4& c);
@@ -59,52 +91,66 @@ __device__ __forceinline__ void mma16<float>(const uint4& a, const uint4& b, f32
   c = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.w), __uint_as_float(b.w), c, 0, 0, 0);
 }
 
-template <int BM, int BN>
-constexpr int conv_lds_bytes() {
-  return (2 * (BM + BN) * ROWB) > (BM * (BN + 4) * 4) ? (2 * (BM + BN) * ROWB) : (BM * (BN + 4) * 4);
+// XCD-aware bijective remap: blocks b and b+8 share an XCD -> each XCD gets a contiguous tile range
+__device__ __forceinline__ int xcd_tile(int b, int nwg) {
+  const int q = nwg >> 3, r8 = nwg & 7, xcd = b & 7;
+  return (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + (b >> 3);
 }
 
-template <typename T, int BM, int BN, bool FAST>
+// bounds-checked buffer descriptors, rebased per block so 32-bit offsets cover any batch; a lane whose
+// tap leaves the frame gets an out-of-range offset and the hardware returns 0 (SAME zero padding).
+template <typename T>
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t x_rsrc(const ConvArgs& a, long xbase) {
+  const T* Xb = reinterpret_cast<const T*>(a.x) + a.x_coff + xbase * (long)a.x_cstride;
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<T*>(Xb), 0, 0x7ffffff0, 0x00020000);
+}
+template <typename T>
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t w_rsrc(const ConvArgs& a, int n0) {
+  const T* Wb = reinterpret_cast<const T*>(a.w) + (long)n0 * a.K_pad;
+  const uint32_t bytes = (uint32_t)((long)(a.cout_pad - n0) * a.K_pad * (long)sizeof(T));
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<T*>(Wb), 0, bytes, 0x00020000);
+}
+
+constexpr int OOB = (int)0x80000000;
+
+// ================================================================ register-staged kernel
+template <int BM, int BN>
+constexpr int mfma_lds_bytes() {
+  return (2 * (BM + BN) * 128) > (BM * (BN + 4) * 4) ? (2 * (BM + BN) * 128) : (BM * (BN + 4) * 4);
+}
+
+template <typename T, int BM, int BN>
 __global__ __launch_bounds__(256, 2) void conv3x3_mfma(ConvArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int CE = 16 / sizeof(T);      // elements per 16-byte chunk
-  constexpr int BKE = ROWB / sizeof(T);   // K elements per step
-  constexpr int XR = BM / 32;             // X chunks per thread per step
-  constexpr int WR = BN / 32;             // W chunks per thread per step
-  constexpr int WM = BM / 64;
-  constexpr int WN = BN / 64;
+  constexpr int RB = 128;
+  constexpr int CE = 16 / sizeof(T);  // elements per 16-byte chunk
+  constexpr int GE = 64 / sizeof(T);  // elements per 64-byte granule
+  constexpr int BKE = RB / sizeof(T);  // K elements per step
+  constexpr int XR = BM / 32, WR = BN / 32;
+  constexpr int WM = BM / 64, WN = BN / 64;
   static_assert(WM * WN == 4, "4 waves of 64x64");
-  constexpr int STAGE = (BM + BN) * ROWB;
+  constexpr int STAGE = (BM + BN) * RB;
 
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
-  const int wm = wave % WM;
-  const int wn = wave / WM;
-
-  // XCD-aware bijective remap: blocks b and b+8 share an XCD -> give each XCD a contiguous tile range
-  const int nwg = a.tiles_total;
-  const int b = blockIdx.x;
-  const int q = nwg >> 3, r8 = nwg & 7, xcd = b & 7;
-  const int t = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + (b >> 3);
-  const int mt = t / a.tiles_n;
-  const int nt = t - mt * a.tiles_n;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave % WM, wn = wave / WM;
+  const int t = xcd_tile(blockIdx.x, a.tiles_total);
+  const int mt = t / a.tiles_n, nt = t - mt * a.tiles_n;
   const long m0 = (long)mt * BM;
   const int n0 = nt * BN;
-
   const int H = a.H, W = a.W;
   const long HW = (long)H * W;
-  const int chunk = tid & 7;
-  const int rbase = tid >> 3;
+  const int chunk = tid & 7, rbase = tid >> 3;
 
-  long pix[XR];
-  int ph[XR], pw[XR];
+  const long xbase = m0 - W - 1;  // lowest pixel any tap of this tile touches
+  const __amdgpu_buffer_rsrc_t xrs = x_rsrc<T>(a, xbase);
+  const __amdgpu_buffer_rsrc_t wrs = w_rsrc<T>(a, n0);
+  int prow[XR], ph[XR], pw[XR];
 #pragma unroll
   for (int i = 0; i < XR; ++i) {
-    long p = m0 + rbase + 32 * i;
-    pix[i] = p;
+    const long p = m0 + rbase + 32 * i;
+    prow[i] = (int)(p - xbase);
     if (p < a.M) {
-      long rem = p % HW;
+      const long rem = p % HW;
       ph[i] = (int)(rem / W);
       pw[i] = (int)(rem - (long)ph[i] * W);
     } else {
@@ -112,40 +158,18 @@ __global__ __launch_bounds__(256, 2) void conv3x3_mfma(ConvArgs a) {
       pw[i] = 0;
     }
   }
-
-  // Bounds-checked buffer descriptors (wave-uniform, rebased per block so 32-bit offsets suffice for any
-  // batch): a lane whose tap falls outside the frame gets an out-of-range offset and the hardware returns
-  // 0 — the SAME-padding zero fill without a branch or a select on addresses.
-  const long xbase = m0 - W - 1;  // lowest pixel any tap of this tile can touch
-  const T* Xb = reinterpret_cast<const T*>(a.x) + a.x_coff + xbase * (long)a.x_cstride;
-  const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<T*>(Xb), 0, 0x7ffffff0, 0x00020000);
-  const T* Wb = reinterpret_cast<const T*>(a.w) + (long)n0 * a.K_pad;
-  const uint32_t wbytes = (uint32_t)((long)(a.cout_pad - n0) * a.K_pad * (long)sizeof(T));
-  const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<T*>(Wb), 0, wbytes, 0x00020000);
   const int xcs = a.x_cstride;
-  int prow[XR];  // pixel index relative to xbase
-#pragma unroll
-  for (int i = 0; i < XR; ++i) prow[i] = (int)(pix[i] - xbase);
-
   uint4 xr[XR], wr[WR];
 
   auto load = [&](int kt) {
     int tap, c;
-    if (FAST) {
-      const int k0 = kt * BKE;
-      tap = k0 / a.cin_pad;
-      c = k0 - tap * a.cin_pad + chunk * CE;
-    } else {
-      const int k = kt * BKE + chunk * CE;
-      tap = k < a.K9 ? k / a.cin_pad : 9;
-      c = k - tap * a.cin_pad;
-    }
+    k_to_tap<GE>(a, kt * BKE + chunk * CE, tap, c);
     const int dh = tap / 3 - 1, dw = tap - (tap / 3) * 3 - 1;
 #pragma unroll
     for (int i = 0; i < XR; ++i) {
       const int hh = ph[i] + dh, ww = pw[i] + dw;
       const bool ok = tap < 9 && (unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W;
-      const int off = ok ? ((prow[i] + dh * W + dw) * xcs + c) * (int)sizeof(T) : (int)0x80000000;
+      const int off = ok ? ((prow[i] + dh * W + dw) * xcs + c) * (int)sizeof(T) : OOB;
       xr[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0));
     }
 #pragma unroll
@@ -154,13 +178,12 @@ __global__ __launch_bounds__(256, 2) void conv3x3_mfma(ConvArgs a) {
       wr[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(wrs, off, 0, 0));
     }
   };
-
   auto store = [&](int buf) {
     char* s = smem + buf * STAGE;
 #pragma unroll
-    for (int i = 0; i < XR; ++i) *reinterpret_cast<uint4*>(s + swz(rbase + 32 * i, chunk)) = xr[i];
+    for (int i = 0; i < XR; ++i) *reinterpret_cast<uint4*>(s + swz<RB>(rbase + 32 * i, chunk)) = xr[i];
 #pragma unroll
-    for (int i = 0; i < WR; ++i) *reinterpret_cast<uint4*>(s + BM * ROWB + swz(rbase + 32 * i, chunk)) = wr[i];
+    for (int i = 0; i < WR; ++i) *reinterpret_cast<uint4*>(s + BM * RB + swz<RB>(rbase + 32 * i, chunk)) = wr[i];
   };
 
   f32x4 acc[4][4];
@@ -169,9 +192,8 @@ __global__ __launch_bounds__(256, 2) void conv3x3_mfma(ConvArgs a) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // f32 path: the 32 products of one K-step chain into a fresh partial that is then added to the
-  // running sum (two-level summation: error ~ (32 + K/32) ulp instead of K ulp for K up to 9216);
-  // bf16 path: one chain (the bf16 operand rounding dominates).
+  // f32: the products of one K-step chain into a fresh partial added to the running sum (two-level
+  // summation, error ~(32 + K/32) ulp instead of K ulp for K up to 9216); bf16: one chain.
   constexpr bool SPLIT = sizeof(T) == 4;
   auto compute = [&](int buf) {
     const char* s = smem + buf * STAGE;
@@ -187,9 +209,10 @@ __global__ __launch_bounds__(256, 2) void conv3x3_mfma(ConvArgs a) {
       const int ck = kb * 4 + (lane >> 4);
       uint4 av[4], bv[4];
 #pragma unroll
-      for (int f = 0; f < 4; ++f) av[f] = *reinterpret_cast<const uint4*>(s + BM * ROWB + swz(wn * 64 + f * 16 + (lane & 15), ck));
+      for (int f = 0; f < 4; ++f)
+        av[f] = *reinterpret_cast<const uint4*>(s + BM * RB + swz<RB>(wn * 64 + f * 16 + (lane & 15), ck));
 #pragma unroll
-      for (int f = 0; f < 4; ++f) bv[f] = *reinterpret_cast<const uint4*>(s + swz(wm * 64 + f * 16 + (lane & 15), ck));
+      for (int f = 0; f < 4; ++f) bv[f] = *reinterpret_cast<const uint4*>(s + swz<RB>(wm * 64 + f * 16 + (lane & 15), ck));
 #pragma unroll
       for (int fc = 0; fc < 4; ++fc)
 #pragma unroll
@@ -214,7 +237,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_mfma(ConvArgs a) {
     __syncthreads();
   }
 
-  // ---------------------------------------------------------------- epilogue
+  // epilogue: f32 staging in LDS, then coalesced 16-byte stores
   constexpr int SROW = BN + 4;
   float* stg = reinterpret_cast<float*>(smem);
 #pragma unroll
@@ -223,7 +246,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_mfma(ConvArgs a) {
     float bsv[4] = {0.f, 0.f, 0.f, 0.f}, scv[4] = {1.f, 1.f, 1.f, 1.f}, shv[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int co = min(n0 + col + j, a.cout - 1);  // clamped: always a valid address, value unused if padded
+      const int co = min(n0 + col + j, a.cout - 1);  // clamped: always a valid address
       if (a.bias) bsv[j] = a.bias[co];
       if (a.scale) scv[j] = a.scale[co];
       if (a.shift) shv[j] = a.shift[co];
@@ -272,11 +295,9 @@ __global__ __launch_bounds__(256, 2) void conv3x3_mfma(ConvArgs a) {
       if (p >= a.M || co >= a.cout) continue;
       const float* src = stg + rr * SROW + cc * 8;
       uint16_t* dst = Y + p * (long)a.y_cstride + co;
-      if (a.y_vec && co + 8 <= a.cout) {
-        *reinterpret_cast<uint4*>(dst) = Chunk<uint16_t>::pack(src);
-      } else {
+      if (a.y_vec && co + 8 <= a.cout) *reinterpret_cast<uint4*>(dst) = Chunk<uint16_t>::pack(src);
+      else
         for (int j = 0; j < 8 && co + j < a.cout; ++j) dst[j] = f2bf(src[j]);
-      }
     }
   } else {
     constexpr int CPR = BN / 4;
@@ -288,25 +309,302 @@ __global__ __launch_bounds__(256, 2) void conv3x3_mfma(ConvArgs a) {
       if (p >= a.M || co >= a.cout) continue;
       const float* src = stg + rr * SROW + cc * 4;
       float* dst = Y + p * (long)a.y_cstride + co;
-      if (a.y_vec && co + 4 <= a.cout) {
-        *reinterpret_cast<float4*>(dst) = *reinterpret_cast<const float4*>(src);
-      } else {
+      if (a.y_vec && co + 4 <= a.cout) *reinterpret_cast<float4*>(dst) = *reinterpret_cast<const float4*>(src);
+      else
         for (int j = 0; j < 4 && co + j < a.cout; ++j) dst[j] = src[j];
+    }
+  }
+}
+
+// ================================================================ LDS-DMA pipelined kernel
+// Tiles are filled by buffer_load_dwordx4 ... lds (global -> LDS, no VGPRs, 1 KiB = 1024/RB operand rows
+// per wave-instruction, called a "piece"):
+//   * the LDS image is lane-linear, so the XOR swizzle moves to the SOURCE: the lane that fills physical
+//     chunk p of row r fetches logical chunk p ^ f(r) (an involution; the MFMA reads use swz<RB>()).
+//   * SAME padding / pixels past the end get an out-of-range buffer offset -> the DMA writes zeros.
+//   * S-slot ring with 64-byte K-steps: slot kt%S is waited with a COUNTED vmcnt (up to S-2 younger
+//     stages stay in flight), then one raw s_barrier per K-step publishes slot kt and frees slot (kt-1)%S,
+//     which the pieces of K-step kt+S-1 refill while the MFMAs of K-step kt run.
+// 8 waves of (BM/WM) pixels x 64 output channels each.
+template <typename T, int RB, int BM, int BN, int WM, int WN, int S>
+struct GldsCfg {
+  static constexpr int NW = WM * WN, NT = 64 * NW;
+  static constexpr int TPM = BM / WM, TPN = BN / WN;
+  static constexpr int FP = TPM / 16, FC = TPN / 16;
+  static constexpr int RPP = 1024 / RB;           // operand rows per DMA piece
+  static constexpr int XP = BM / RPP, WP = BN / RPP;  // pieces per stage
+  static constexpr int XPW = XP / NW;              // X pieces per wave
+  static constexpr int WPW = (WP + NW - 1) / NW;   // max W pieces per wave
+  static constexpr int STAGE = (BM + BN) * RB;
+  static constexpr int EPI = BM * (64 + 4) * 4;    // one 64-channel f32 slab
+  static constexpr int LDS = (S * STAGE > EPI ? S * STAGE : EPI);
+  static_assert(NW == 8, "8-wave blocks");
+  static_assert(TPN == 64, "epilogue slabs are one wave-column (64 channels) wide");
+  static_assert(XP % NW == 0, "whole X pieces per wave");
+  static_assert(S >= 2 && S <= 8, "ring depth");
+};
+
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+__device__ __forceinline__ uint32_t lds_addr(const char* p) {
+  return (uint32_t)(uintptr_t)(lds_ptr_t)(p);
+}
+
+// One 16-byte-per-lane LDS-DMA (buffer_load_dwordx4 ... offen lds) from inline asm.  Issued through asm on
+// purpose: for a compiler-visible LDS-DMA, hipcc cannot prove the slot being read differs from the slots
+// being filled and emits s_waitcnt vmcnt(0) before the next ds_read — draining every stage in flight.
+// The asm is invisible to that bookkeeping; completion is counted by hand (wait_vm) before the barrier
+// that publishes a slot.  M0 is compiler-reserved: set and restored inside the same statement.
+__device__ __forceinline__ void glds16(__amdgpu_buffer_rsrc_t rsrc, uint32_t lds_dst, int voffset) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %1, %3, 0 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voffset), "s"(lds_dst), "s"(rsrc)
+      : "memory");
+}
+
+// s_waitcnt vmcnt(n) for a wave-uniform runtime n (immediate operand -> one case per value)
+__device__ __forceinline__ void wait_vm(int n) {
+#define VM_W(N) \
+  case N:       \
+    asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); \
+    break;
+  switch (n) {
+    VM_W(0) VM_W(1) VM_W(2) VM_W(3) VM_W(4) VM_W(5) VM_W(6) VM_W(7) VM_W(8) VM_W(9) VM_W(10) VM_W(11) VM_W(12)
+    VM_W(13) VM_W(14) VM_W(15) VM_W(16) VM_W(17) VM_W(18) VM_W(19) VM_W(20) VM_W(21) VM_W(22) VM_W(23) VM_W(24)
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+#undef VM_W
+}
+
+template <typename T, int RB, int BM, int BN, int WM, int WN, int S, bool FAST>
+__global__ __launch_bounds__(512, 1) void conv3x3_glds(ConvArgs a) {
+  using C = GldsCfg<T, RB, BM, BN, WM, WN, S>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int CE = 16 / sizeof(T);
+  constexpr int GE = 64 / sizeof(T);
+  constexpr int BKE = RB / sizeof(T);
+  constexpr int CPR = RB / 16;  // chunks per row
+  constexpr int FP = C::FP, FC = C::FC, XPW = C::XPW, WPW = C::WPW, NT = C::NT, NW = C::NW;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave % WM, wn = wave / WM;
+  const int t = xcd_tile(blockIdx.x, a.tiles_total);
+  const int mt = t / a.tiles_n, nt = t - mt * a.tiles_n;
+  const long m0 = (long)mt * BM;
+  const int n0 = nt * BN;
+  const int H = a.H, W = a.W;
+  const long HW = (long)H * W;
+
+  const long xbase = m0 - W - 1;
+  const __amdgpu_buffer_rsrc_t xrs = x_rsrc<T>(a, xbase);
+  const __amdgpu_buffer_rsrc_t wrs = w_rsrc<T>(a, n0);
+
+  // this lane's DMA rows: X piece i of this wave fills rows (wave + i*NW)*RPP + lane/CPR, physical chunk lane%CPR
+  const int lrow = lane / CPR, lpos = lane % CPR;
+  int prow[XPW], ph[XPW], pw[XPW], xq[XPW];
+#pragma unroll
+  for (int i = 0; i < XPW; ++i) {
+    const int row = (wave + i * NW) * C::RPP + lrow;
+    const long p = m0 + row;
+    xq[i] = (swz<RB>(row, lpos) - row * RB) >> 4;  // logical chunk that belongs in physical chunk lpos
+    prow[i] = (int)(p - xbase);
+    if (p < a.M) {
+      const long rem = p % HW;
+      ph[i] = (int)(rem / W);
+      pw[i] = (int)(rem - (long)ph[i] * W);
+    } else {
+      ph[i] = -0x40000000;
+      pw[i] = 0;
+    }
+  }
+  int woff[WPW];
+  int nwp = 0;  // W pieces of this wave (wave-uniform)
+#pragma unroll
+  for (int i = 0; i < WPW; ++i) {
+    const int piece = wave + i * NW;
+    const int row = piece * C::RPP + lrow;
+    woff[i] = (row * a.K_pad + ((swz<RB>(row, lpos) - row * RB) >> 4) * CE) * (int)sizeof(T);
+    if (piece < C::WP) ++nwp;
+  }
+  const int lps = XPW + nwp;  // DMA pieces this wave issues per stage
+  const int xcs = a.x_cstride;
+
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr(smem));
+  auto issue = [&](int kt, int slot) {
+    const uint32_t sbase = lds0 + slot * C::STAGE;
+    int tapu = 0, c0 = 0;
+    if (FAST && RB == 64) {  // one granule per K-step: tap and channel base are wave-uniform
+      const int cc = kt / 9;
+      tapu = kt - cc * 9;
+      c0 = cc * GE;
+    }
+#pragma unroll
+    for (int i = 0; i < XPW; ++i) {
+      int tap, c;
+      if (FAST && RB == 64) {
+        tap = tapu;
+        c = c0 + xq[i] * CE;
+      } else {
+        k_to_tap<GE>(a, kt * BKE + xq[i] * CE, tap, c);
+      }
+      const int dh = tap / 3 - 1, dw = tap - (tap / 3) * 3 - 1;
+      const int hh = ph[i] + dh, ww = pw[i] + dw;
+      const bool ok = tap < 9 && (unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W;
+      const int off = ok ? ((prow[i] + dh * W + dw) * xcs + c) * (int)sizeof(T) : OOB;
+      glds16(xrs, sbase + (wave + i * NW) * 1024, off);
+    }
+    const int kb = kt * RB;
+#pragma unroll
+    for (int i = 0; i < WPW; ++i)
+      if (wave + i * NW < C::WP) glds16(wrs, sbase + BM * RB + (wave + i * NW) * 1024, woff[i] + kb);
+  };
+
+  f32x4 acc[FC][FP];
+#pragma unroll
+  for (int i = 0; i < FC; ++i)
+#pragma unroll
+    for (int j = 0; j < FP; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  constexpr bool SPLIT = sizeof(T) == 4;
+  auto compute = [&](int slot) {
+    const char* sp = smem + slot * C::STAGE;
+    f32x4 part[SPLIT ? FC : 1][SPLIT ? FP : 1];
+    if constexpr (SPLIT) {
+#pragma unroll
+      for (int i = 0; i < FC; ++i)
+#pragma unroll
+        for (int j = 0; j < FP; ++j) part[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int kb = 0; kb < RB / 64; ++kb) {
+      const int ck = kb * 4 + (lane >> 4);
+      uint4 av[FC], bv[FP];
+#pragma unroll
+      for (int f = 0; f < FC; ++f)
+        av[f] = *reinterpret_cast<const uint4*>(sp + BM * RB + swz<RB>(wn * 64 + f * 16 + (lane & 15), ck));
+#pragma unroll
+      for (int f = 0; f < FP; ++f)
+        bv[f] = *reinterpret_cast<const uint4*>(sp + swz<RB>(wm * C::TPM + f * 16 + (lane & 15), ck));
+#pragma unroll
+      for (int fc = 0; fc < FC; ++fc)
+#pragma unroll
+        for (int fp = 0; fp < FP; ++fp) {
+          if constexpr (SPLIT) mma16<T>(av[fc], bv[fp], part[fc][fp]);
+          else mma16<T>(av[fc], bv[fp], acc[fc][fp]);
+        }
+    }
+    if constexpr (SPLIT) {
+#pragma unroll
+      for (int i = 0; i < FC; ++i)
+#pragma unroll
+        for (int j = 0; j < FP; ++j) acc[i][j] += part[i][j];
+    }
+  };
+
+  const int nk = a.nk;
+#pragma unroll
+  for (int s = 0; s < S - 1; ++s)
+    if (s < nk) issue(s, s);
+  int slot = 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    // stage kt has landed once only the min(S-2, nk-1-kt) younger stages are still in flight
+    wait_vm(min(S - 2, nk - 1 - kt) * lps);
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (kt + S - 1 < nk) {
+      int ns = slot + S - 1;
+      ns -= ns >= S ? S : 0;
+      issue(kt + S - 1, ns);
+    }
+    compute(slot);
+    slot = slot + 1 == S ? 0 : slot + 1;
+  }
+
+  // ---------------------------------------------------------------- epilogue, one 64-channel slab at a time
+  constexpr int SROW = 64 + 4;
+  float* stg = reinterpret_cast<float*>(smem);
+  for (int sl = 0; sl < WN; ++sl) {
+    asm volatile("" ::: "memory");
+    __syncthreads();
+    if (wn == sl) {
+#pragma unroll
+      for (int fc = 0; fc < FC; ++fc) {
+        const int col = fc * 16 + 4 * (lane >> 4);
+        float bsv[4] = {0.f, 0.f, 0.f, 0.f}, scv[4] = {1.f, 1.f, 1.f, 1.f}, shv[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int co = min(n0 + wn * 64 + col + j, a.cout - 1);
+          if (a.bias) bsv[j] = a.bias[co];
+          if (a.scale) scv[j] = a.scale[co];
+          if (a.shift) shv[j] = a.shift[co];
+        }
+#pragma unroll
+        for (int fp = 0; fp < FP; ++fp) {
+          const int row = wm * C::TPM + fp * 16 + (lane & 15);
+          float4 v;
+          float* vv = reinterpret_cast<float*>(&v);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            float tv = (acc[fc][fp][j] + bsv[j]) * scv[j] + shv[j];
+            if (a.act == VM_ACT_RELU) tv = tv > 0.f ? tv : 0.f;
+            else if (a.act == VM_ACT_SIGMOID) tv = sigmoid_precise(tv);
+            vv[j] = tv;
+          }
+          *reinterpret_cast<float4*>(stg + row * SROW + col) = v;
+        }
+      }
+    }
+    __syncthreads();
+    const int nb = n0 + sl * 64;
+    if (a.y_dtype == VM_BF16) {
+      uint16_t* Y = reinterpret_cast<uint16_t*>(a.y) + a.y_coff;
+      for (int idx = tid; idx < BM * 8; idx += NT) {
+        const int rr = idx >> 3, cc = idx & 7;
+        const long p = m0 + rr;
+        const int co = nb + cc * 8;
+        if (p >= a.M || co >= a.cout) continue;
+        const float* src = stg + rr * SROW + cc * 8;
+        uint16_t* dst = Y + p * (long)a.y_cstride + co;
+        if (a.y_vec && co + 8 <= a.cout) *reinterpret_cast<uint4*>(dst) = Chunk<uint16_t>::pack(src);
+        else
+          for (int j = 0; j < 8 && co + j < a.cout; ++j) dst[j] = f2bf(src[j]);
+      }
+    } else {
+      float* Y = reinterpret_cast<float*>(a.y) + a.y_coff;
+      for (int idx = tid; idx < BM * 16; idx += NT) {
+        const int rr = idx >> 4, cc = idx & 15;
+        const long p = m0 + rr;
+        const int co = nb + cc * 4;
+        if (p >= a.M || co >= a.cout) continue;
+        const float* src = stg + rr * SROW + cc * 4;
+        float* dst = Y + p * (long)a.y_cstride + co;
+        if (a.y_vec && co + 4 <= a.cout) *reinterpret_cast<float4*>(dst) = *reinterpret_cast<const float4*>(src);
+        else
+          for (int j = 0; j < 4 && co + j < a.cout; ++j) dst[j] = src[j];
       }
     }
   }
 }
 
-// ---------------------------------------------------------------- Cout == 1 head (conv1_5 + sigmoid)
-// unet.py:203-205 / unet_simple.py:142 / small.py:49-50: a 1-channel 3x3 conv over 128 (or fewer)
-// channels at full resolution is a memory-bound dot product: 16 lanes per pixel, each lane one
-// 16-byte channel chunk per tap (a wave reads 4 pixels x 256 contiguous bytes), a 4-step
-// xor-shuffle reduction inside each 16-lane group, weights staged once per block in LDS.
+// ================================================================ Cout == 1 head (conv1_5 + sigmoid)
+// unet.py:203-205 / unet_simple.py:142 / small.py:49-50: a 1-channel 3x3 conv over <=128 channels at full
+// resolution is a memory-bound dot product: 16 lanes per pixel, each lane one 16-byte channel chunk per
+// tap (a wave reads 4 pixels x 256 contiguous bytes), a 4-step xor-shuffle reduction inside each 16-lane
+// group, weights un-permuted once per block into tap-major order in LDS.
 struct HeadArgs {
   const void* x;
   int x_cstride, x_coff, H, W;
   long M;
-  int cin_pad;
+  int cin_pad, K9, K_pad, chunk_major, ng;
   const void* w;
   const float* bias;
   const float* scale;
@@ -320,10 +618,24 @@ template <typename T>
 __global__ __launch_bounds__(256) void conv3x3_head(HeadArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int CE = 16 / sizeof(T);
+  constexpr int GE = 64 / sizeof(T);
   float* sw = reinterpret_cast<float*>(smem);
-  const int K9 = 9 * a.cin_pad;
   const T* Wt = reinterpret_cast<const T*>(a.w);
-  for (int k = threadIdx.x; k < K9; k += 256) sw[k] = ld_elem<T>(Wt + k);
+  for (int k = threadIdx.x; k < a.K_pad; k += 256) {
+    int tap, c;
+    if (a.chunk_major) {
+      const int g = k / GE;
+      if (g >= a.ng) continue;
+      const int cc = g / 9;
+      tap = g - cc * 9;
+      c = cc * GE + (k - g * GE);
+    } else {
+      if (k >= a.K9) continue;
+      tap = k / a.cin_pad;
+      c = k - tap * a.cin_pad;
+    }
+    sw[tap * a.cin_pad + c] = ld_elem<T>(Wt + k);
+  }
   __syncthreads();
 
   const int sub = threadIdx.x & 15;
@@ -368,16 +680,19 @@ __global__ __launch_bounds__(256) void conv3x3_head(HeadArgs a) {
   }
 }
 
-// ---------------------------------------------------------------- weight packing
-// HWIO f32 [3][3][cin][cout] (unet.py:15 / the VGG npy layout) -> [cout_pad][K_pad] in the compute dtype.
+// ================================================================ weight packing
+// HWIO f32 [3][3][cin][cout] (unet.py:15 / the VGG npy layout) -> [cout_pad][K_pad] in the compute dtype,
+// K in granule order (see the header comment).
 template <typename T>
-__global__ void pack_weights(const float* w, int cin, int cout, int cin_pad, int K_pad, int cout_pad, T* out) {
-  const long total = (long)cout_pad * K_pad;
+__global__ void pack_weights(const float* w, int cin, int cout, ConvArgs g) {
+  constexpr int GE = 64 / sizeof(T);
+  T* out = reinterpret_cast<T*>(const_cast<void*>(g.w));
+  const long total = (long)g.cout_pad * g.K_pad;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const int co = (int)(i / K_pad);
-    const int k = (int)(i - (long)co * K_pad);
-    const int tap = k / cin_pad;
-    const int c = k - tap * cin_pad;
+    const int co = (int)(i / g.K_pad);
+    const int k = (int)(i - (long)co * g.K_pad);
+    int tap, c;
+    k_to_tap<GE>(g, k, tap, c);
     float v = 0.f;
     if (co < cout && tap < 9 && c < cin) v = w[((long)tap * cin + c) * cout + co];
     st_elem<T>(out + i, v);
@@ -385,50 +700,123 @@ __global__ void pack_weights(const float* w, int cin, int cout, int cin_pad, int
 }
 
 struct PackGeom {
-  int cin_pad, bke, K9, K_pad, cout_pad, nk;
+  int cin_pad, ge, K9, K_pad, cout_pad, chunk_major, ng;
 };
 
 static PackGeom geom(int cin, int cout, int dtype) {
   PackGeom g;
-  const int eb = elem_bytes(dtype);
+  g.ge = 64 / elem_bytes(dtype);
   g.cin_pad = (cin + 7) / 8 * 8;
-  g.bke = ROWB / eb;
   g.K9 = 9 * g.cin_pad;
-  g.nk = (g.K9 + g.bke - 1) / g.bke;
-  g.K_pad = g.nk * g.bke;
+  g.chunk_major = g.cin_pad % g.ge == 0;
+  g.ng = g.chunk_major ? g.K9 / g.ge : 0;
+  g.K_pad = (g.K9 + 2 * g.ge - 1) / (2 * g.ge) * (2 * g.ge);  // whole 128-byte steps
   g.cout_pad = (cout + 63) / 64 * 64;
   return g;
 }
 
-template <typename T, int BM, int BN, bool FAST>
-static int launch_mfma(const ConvArgs& a, hipStream_t st) {
-  constexpr int lds = conv_lds_bytes<BM, BN>();
+static void fill_geom(ConvArgs& a, const PackGeom& g) {
+  a.cin_pad = g.cin_pad;
+  a.K9 = g.K9;
+  a.chunk_major = g.chunk_major;
+  a.ng = g.ng;
+  a.K_pad = g.K_pad;
+  a.cout_pad = g.cout_pad;
+}
+
+// ================================================================ dispatch
+template <typename T, int BM, int BN>
+static int launch_mfma(ConvArgs& a, hipStream_t st) {
+  constexpr int lds = mfma_lds_bytes<BM, BN>();
   static bool attr_set = false;  // idempotent; benign race
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3_mfma<T, BM, BN, FAST>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3_mfma<T, BM, BN>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (e != hipSuccess) return fail(VM_EHIP, "hipFuncSetAttribute: %s", hipGetErrorString(e));
     attr_set = true;
   }
-  hipLaunchKernelGGL((conv3x3_mfma<T, BM, BN, FAST>), dim3(a.tiles_total), dim3(256), lds, st, a);
+  a.nk = a.K_pad / (128 / (int)sizeof(T));
+  a.tiles_n = (a.cout + BN - 1) / BN;
+  a.tiles_total = (int)((a.M + BM - 1) / BM) * a.tiles_n;
+  hipLaunchKernelGGL((conv3x3_mfma<T, BM, BN>), dim3(a.tiles_total), dim3(256), lds, st, a);
   return check_launch("conv3x3_mfma");
 }
 
-template <typename T>
-static int dispatch_mfma(ConvArgs& a, bool fast, hipStream_t st) {
-  if (a.cout <= 64) {
-    a.tiles_n = (a.cout + 63) / 64;
-    a.tiles_total = (int)((a.M + 255) / 256) * a.tiles_n;
-    return fast ? launch_mfma<T, 256, 64, true>(a, st) : launch_mfma<T, 256, 64, false>(a, st);
+template <typename T, int RB, int BM, int BN, int WM, int WN, int S, bool FAST>
+static int launch_glds(ConvArgs& a, hipStream_t st) {
+  using C = GldsCfg<T, RB, BM, BN, WM, WN, S>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3_glds<T, RB, BM, BN, WM, WN, S, FAST>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
+    if (e != hipSuccess) return fail(VM_EHIP, "hipFuncSetAttribute(glds): %s", hipGetErrorString(e));
+    attr_set = true;
   }
-  a.tiles_n = (a.cout + 127) / 128;
-  a.tiles_total = (int)((a.M + 127) / 128) * a.tiles_n;
-  return fast ? launch_mfma<T, 128, 128, true>(a, st) : launch_mfma<T, 128, 128, false>(a, st);
+  const int bke = RB / (int)sizeof(T);
+  a.nk = (FAST && RB == 64) ? a.ng : a.K_pad / bke;
+  a.tiles_n = (a.cout + BN - 1) / BN;
+  a.tiles_total = (int)((a.M + BM - 1) / BM) * a.tiles_n;
+  hipLaunchKernelGGL((conv3x3_glds<T, RB, BM, BN, WM, WN, S, FAST>), dim3(a.tiles_total), dim3(C::NT), C::LDS, st,
+                     a);
+  return check_launch("conv3x3_glds");
+}
+
+// tuning knobs (vm_set_option): conv_kernel 0 = auto, 1 = register-staged only, 2 = LDS-DMA whenever legal;
+// conv_min_tiles = smallest grid (in 256-wide output tiles) for which auto picks the LDS-DMA kernel;
+// glds_rb = K-step bytes of the 256x256 LDS-DMA tile (64: 4-slot ring, 128: 2-slot).
+static long g_conv_kernel = 0;
+static long g_conv_min_tiles = 128;
+static long g_glds_rb = 128;
+
+template <typename T, bool FAST>
+static int dispatch_glds(ConvArgs& a, hipStream_t st) {
+  if constexpr (sizeof(T) == 2) {
+    if (a.cout > 128) {
+      if (g_glds_rb == 64) return launch_glds<T, 64, 256, 256, 2, 4, 4, FAST>(a, st);
+      return launch_glds<T, 128, 256, 256, 2, 4, 2, FAST>(a, st);
+    }
+  }
+  if (a.cout > 64) return launch_glds<T, 64, 256, 128, 4, 2, 6, FAST>(a, st);
+  return launch_glds<T, 64, 512, 64, 8, 1, 4, FAST>(a, st);
+}
+
+template <typename T>
+static int dispatch_mfma(ConvArgs& a, hipStream_t st) {
+  if (g_conv_kernel != 1 && a.act != VM_ACT_SOFTMAX) {
+    // measured (tools/convbench.py): the LDS-DMA kernel wins for cout >= 256 (256x256 tiles); for
+    // cout <= 128 its 64-channel-wide waves are DMA-issue-bound and the register-staged kernel is faster
+    const int bm = a.cout > 64 ? 256 : 512;
+    const long tiles = ((a.M + bm - 1) / bm) * ((a.cout + 255) / 256);
+    const bool wide = sizeof(T) == 2 && a.cout > 128;
+    if (g_conv_kernel == 2 || (wide && tiles >= g_conv_min_tiles))
+      return a.chunk_major ? dispatch_glds<T, true>(a, st) : dispatch_glds<T, false>(a, st);
+  }
+  if (a.cout <= 64) return launch_mfma<T, 256, 64>(a, st);
+  return launch_mfma<T, 128, 128>(a, st);
 }
 
 }  // namespace vm
 
 using namespace vm;
+
+extern "C" int vm_set_option(const char* key, long value) {
+  if (!key) return fail(VM_EINVAL, "set_option: NULL key");
+  if (!strcmp(key, "conv_kernel")) {
+    if (value < 0 || value > 2) return fail(VM_EINVAL, "conv_kernel must be 0, 1 or 2");
+    g_conv_kernel = value;
+    return VM_OK;
+  }
+  if (!strcmp(key, "conv_min_tiles")) {
+    g_conv_min_tiles = value;
+    return VM_OK;
+  }
+  if (!strcmp(key, "glds_rb")) {
+    if (value != 64 && value != 128) return fail(VM_EINVAL, "glds_rb must be 64 or 128");
+    g_glds_rb = value;
+    return VM_OK;
+  }
+  return fail(VM_EINVAL, "set_option: unknown key '%s'", key);
+}
 
 extern "C" size_t vm_conv3x3_packed_bytes(int cin, int cout, int dtype) {
   if (cin <= 0 || cout <= 0 || (dtype != VM_F32 && dtype != VM_BF16)) return 0;
@@ -440,15 +828,13 @@ extern "C" int vm_conv3x3_pack_weights(const float* w_hwio, int cin, int cout, i
   if (!w_hwio || !packed || cin <= 0 || cout <= 0) return fail(VM_EINVAL, "pack_weights: bad argument");
   if (dtype != VM_F32 && dtype != VM_BF16) return fail(VM_EINVAL, "pack_weights: dtype %d", dtype);
   PackGeom g = geom(cin, cout, dtype);
+  ConvArgs a{};
+  fill_geom(a, g);
+  a.w = packed;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  const long total = (long)g.cout_pad * g.K_pad;
-  const int grid = grid_for(total, 256);
-  if (dtype == VM_BF16)
-    hipLaunchKernelGGL(pack_weights<uint16_t>, dim3(grid), dim3(256), 0, st, w_hwio, cin, cout, g.cin_pad, g.K_pad,
-                       g.cout_pad, reinterpret_cast<uint16_t*>(packed));
-  else
-    hipLaunchKernelGGL(pack_weights<float>, dim3(grid), dim3(256), 0, st, w_hwio, cin, cout, g.cin_pad, g.K_pad,
-                       g.cout_pad, reinterpret_cast<float*>(packed));
+  const int grid = grid_for((long)g.cout_pad * g.K_pad, 256);
+  if (dtype == VM_BF16) hipLaunchKernelGGL(pack_weights<uint16_t>, dim3(grid), dim3(256), 0, st, w_hwio, cin, cout, a);
+  else hipLaunchKernelGGL(pack_weights<float>, dim3(grid), dim3(256), 0, st, w_hwio, cin, cout, a);
   return check_launch("pack_weights");
 }
 
@@ -474,7 +860,8 @@ extern "C" int vm_conv3x3_nhwc(const vm_tensor* x, const void* packed, int cin, 
   if (cout == 1) {
     HeadArgs h{};
     h.x = x->ptr; h.x_cstride = x->cstride; h.x_coff = x->coff; h.H = x->h; h.W = x->w; h.M = M;
-    h.cin_pad = g.cin_pad; h.w = packed; h.bias = bias; h.scale = scale; h.shift = shift; h.act = act;
+    h.cin_pad = g.cin_pad; h.K9 = g.K9; h.K_pad = g.K_pad; h.chunk_major = g.chunk_major; h.ng = g.ng;
+    h.w = packed; h.bias = bias; h.scale = scale; h.shift = shift; h.act = act;
     h.y = y->ptr; h.y_cstride = y->cstride; h.y_coff = y->coff; h.y_dtype = y->dtype;
     const int grid = grid_for((M + 15) / 16, 1, 256 * 8);
     const size_t lds = (size_t)9 * g.cin_pad * 4;
@@ -485,13 +872,12 @@ extern "C" int vm_conv3x3_nhwc(const vm_tensor* x, const void* packed, int cin, 
 
   ConvArgs a{};
   a.x = x->ptr; a.x_cstride = x->cstride; a.x_coff = x->coff; a.H = x->h; a.W = x->w; a.M = M;
-  a.cin_pad = g.cin_pad; a.K9 = g.K9; a.nk = g.nk;
-  a.w = packed; a.K_pad = g.K_pad; a.cout = cout; a.cout_pad = g.cout_pad;
+  fill_geom(a, g);
+  a.w = packed; a.cout = cout;
   a.bias = bias; a.scale = scale; a.shift = shift; a.act = act;
   a.y = y->ptr; a.y_cstride = y->cstride; a.y_coff = y->coff; a.y_dtype = y->dtype;
   const int yve = 16 / elem_bytes(y->dtype);
   a.y_vec = (reinterpret_cast<uintptr_t>(y->ptr) % 16 == 0) && (y->cstride % yve == 0) && (y->coff % yve == 0);
-  const bool fast = (g.cin_pad % g.bke) == 0;
-  if (dt == VM_BF16) return dispatch_mfma<uint16_t>(a, fast, st);
-  return dispatch_mfma<float>(a, fast, st);
+  if (dt == VM_BF16) return dispatch_mfma<uint16_t>(a, st);
+  return dispatch_mfma<float>(a, st);
 }
