@@ -81,6 +81,58 @@ def cpu_baseline(h, w, sample_h, sample_w):
                       "1920x1080 by pixel count" % (sample_w, sample_h, dt, scale)}
 
 
+def load_traffic(args):
+    """Per-launch HBM bytes per kernel from the committed PMC pass (tools/traffic.py -> profiles/*_traffic.json),
+    used only when it was collected on this exact workload."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*_traffic.json")), reverse=True):
+        try:
+            with open(path) as f:
+                t = json.load(f)
+        except (OSError, ValueError):
+            continue
+        c = t.get("config", {})
+        if (c.get("dtype"), c.get("height"), c.get("width"), c.get("batch")) == (args.dtype, args.height, args.width,
+                                                                               args.batch):
+            return path, t.get("kernels", {})
+    return None, {}
+
+
+def conv_roofline(prof, args):
+    """Roofline of the dominant conv kernel (largest share of conv time): ALGORITHMIC flops per launch
+    (2*H*W*9*cin*cout of each launch) / its average launch duration from HIP events on
+    the launch stream inside the timed region."""
+    per = {}
+    for fl, name, e0, e1 in prof:
+        d = per.setdefault(name, [0, 0.0, 0])
+        d[0] += fl
+        d[1] += e0.elapsed_time(e1)
+        d[2] += 1
+    name, (fl, ms, n) = max(per.items(), key=lambda kv: kv[1][1])
+    achieved = fl / (ms * 1e-3) / 1e12
+    peak = PEAK_TFLOPS[args.dtype]
+    src, traffic = load_traffic(args)
+    tr = traffic.get(name)
+    all_fl = sum(v[0] for k, v in per.items() if "head" not in k)
+    all_ms = sum(v[1] for k, v in per.items() if "head" not in k)
+    if args.layers:
+        per_step = len(prof) // max(1, args.steps)
+        for i in range(per_step):
+            rows = prof[i::per_step]
+            t_ms = sum(e0.elapsed_time(e1) for _, _, e0, e1 in rows) / len(rows)
+            log("  conv #%2d %-55s %.3f ms  %.1f TFLOP/s" % (i, rows[0][1], t_ms, rows[0][0] / (t_ms * 1e-3) / 1e12))
+    for k, (f, t, c) in sorted(per.items(), key=lambda kv: -kv[1][1]):
+        log("%-58s %3d launches %.3f ms/step %.1f TFLOP/s" % (k, c, t / args.steps, f / (t * 1e-3) / 1e12))
+    return {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
+            "frac": round(achieved / peak, 4), "traffic": tr["bytes_per_launch"] if tr else None,
+            "kernel": name, "launches": n, "avg_launch_ms": round(ms / n, 4), "flops_per_launch": int(fl / n),
+            "traffic_source": ("%s (FETCH_SIZE x2 + WRITE_SIZE, per launch)" % os.path.relpath(src, REPO)) if tr
+            else None,
+            "all_mfma_convs": {"tflops": round(all_fl / (all_ms * 1e-3) / 1e12, 2),
+                               "ms_per_step": round(all_ms / args.steps, 4),
+                               "frac": round(all_fl / (all_ms * 1e-3) / 1e12 / peak, 4)}}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -143,27 +195,7 @@ def main():
 
     roofline = None
     if prof:
-        mf = [(f, e0.elapsed_time(e1)) for f, head, e0, e1 in prof if not head]
-        hd = [(f, e0.elapsed_time(e1)) for f, head, e0, e1 in prof if head]
-        fl, ms = sum(f for f, _ in mf), sum(t for _, t in mf)
-        achieved = fl / (ms * 1e-3) / 1e12
-        n_launch = len(mf)
-        roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_TFLOPS[args.dtype],
-                    "unit": "TFLOP/s", "frac": round(achieved / PEAK_TFLOPS[args.dtype], 4), "traffic": None,
-                    "kernel": "conv3x3_mfma (%s)" % args.dtype,
-                    "launches": n_launch, "avg_launch_ms": round(ms / max(1, n_launch), 4),
-                    "flops_per_launch_avg": int(fl / max(1, n_launch))}
-        hfl = sum(t for _, t in hd)
-        per_step = len(prof) // max(1, args.steps)
-        if args.layers and per_step:
-            for i in range(per_step):
-                rows = prof[i::per_step]
-                t_ms = sum(e0.elapsed_time(e1) for _, _, e0, e1 in rows) / len(rows)
-                log("  conv #%2d %s: %.3f ms  %.1f TFLOP/s" % (i, "head" if rows[0][1] else "mfma", t_ms,
-                                                             rows[0][0] / (t_ms * 1e-3) / 1e12))
-        log("conv MFMA: %d launches, %.3f ms total/step, %.1f TFLOP/s; head: %.3f ms/step; step %.3f ms"
-            % (n_launch, ms / args.steps, achieved, hfl / args.steps, ms_step))
-
+        roofline = conv_roofline(prof, args)
     if rank == 0:
         rec = {"metric": METRIC, "value": round(value, 3), "unit": "frames/s", "n_gpus": world,
                "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 4),

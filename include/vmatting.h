@@ -64,6 +64,10 @@ const char* vm_last_error(void);
  *   "conv_min_tiles" grid size (256-wide output tiles) from which auto uses the LDS-DMA kernel (default 128)
  *   "glds_rb"        K-step bytes of the 256x256 LDS-DMA tile: 128 (2-slot ring, default) or 64 (4-slot) */
 int vm_set_option(const char* key, long value);
+/* Name of the conv kernel the calling thread's last vm_conv3x3_nhwc launched, spelled the way
+ * rocprofv3 reports it (e.g. "vm::conv3x3_mfma<unsigned short, 128, 128>"); "" before the first call.
+ * Used to attribute per-kernel profiler counters (bench.py); no reference counterpart. */
+const char* vm_conv3x3_last_kernel(void);
 
 /* ---------------------------------------------------------------- 3x3 convolution
  * Replaces tf.nn.conv2d(x, w, [1,1,1,1], 'SAME') + tf.nn.bias_add + the activation /

@@ -23,6 +23,7 @@ for s in $STEPS; do
     pytest) guard 900 pytest_gpu.log python -m pytest tests -q -m "$PYTEST_SEL" -rf ;;
     slow)   guard 900 pytest_slow.log python -m pytest tests -q -m "gpu and slow" -rf -s ;;
     smoke)  guard 300 smoke.log python -c "import __graft_entry__ as g; g.smoke()" ;;
+    convbench) guard 300 convbench.log python tools/convbench.py --unet-layers --iters 20 ${CONVBENCH_ARGS} ;;
     bench)  guard 600 bench.log python bench.py --steps "${BENCH_STEPS:-10}" --warmup 3 ${BENCH_ARGS} ;;
   esac
 done

@@ -37,6 +37,7 @@ SIGNATURES = [
     ("vm_abi_version", c_int, []),
     ("vm_last_error", ctypes.c_char_p, []),
     ("vm_set_option", c_int, [ctypes.c_char_p, c_long]),
+    ("vm_conv3x3_last_kernel", ctypes.c_char_p, []),
     ("vm_conv3x3_packed_bytes", c_size_t, [c_int, c_int, c_int]),
     ("vm_conv3x3_pack_weights", c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
     ("vm_conv3x3_nhwc", c_int, [P, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, P, c_void_p]),
@@ -93,6 +94,11 @@ def check(rc, what):
 def set_option(key, value):
     """vm_set_option: process-wide kernel-selection knobs ("conv_kernel", "conv_min_tiles")."""
     check(lib().vm_set_option(key.encode(), int(value)), "set_option")
+
+
+def last_conv_kernel():
+    """vm_conv3x3_last_kernel: rocprofv3 spelling of the kernel the last conv call launched."""
+    return lib().vm_conv3x3_last_kernel().decode()
 
 
 def stream_handle(stream=None):

@@ -116,7 +116,7 @@ def conv3x3(x, pc, act="none", out=None, out_dtype=None, affine=None):
                                 _ptr(shift), _lib.ACT[act], ctypes.byref(yv), stream_handle()), "conv3x3")
     if prof is not None:
         ev1.record()
-        prof.append((2 * n * h * w * 9 * pc.cin * pc.cout, pc.cout == 1, ev0, ev1))
+        prof.append((2 * n * h * w * 9 * pc.cin * pc.cout, _lib.last_conv_kernel(), ev0, ev1))
     return out
 
 
