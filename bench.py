@@ -158,9 +158,7 @@ def main():
     # buffers are broadcast (one RCCL collective) so replicas are bit-identical by construction
     vgg = synthetic_vgg16(0)
     np.random.seed(0)
-    model = unet.UNetVideo(vgg, dtype=args.dtype, device=dev)
-    model.params = model._make_params()
-    model._pack()
+    model = unet.UNetVideo(vgg, dtype=args.dtype, device=dev).prepare()
     parallel.broadcast_tensors(model.weights_flat(), src=0)
 
     B, H, W = args.batch, args.height, args.width

@@ -74,6 +74,14 @@ class UNet:
         self.convs = None
         return self
 
+    def prepare(self):
+        """Create (first call) and pack the weights without running a frame, e.g. before an RCCL broadcast."""
+        if self.params is None:
+            self.params = self._make_params()
+        if self.convs is None:
+            self._pack()
+        return self
+
     def _pack(self):
         self.convs = {k: ops.PackedConv(w, b, self.dtype, self.device) for k, (w, b) in self.params.items()}
 
@@ -109,10 +117,7 @@ class UNet:
     def build(self, input):
         """unet.UNet*.build (unet.py:87-148 / 161-208): create weights (first call), run, set attributes."""
         x = self._as_input(input)
-        if self.params is None:
-            self.params = self._make_params()
-        if self.convs is None:
-            self._pack()
+        self.prepare()
         self.forward(x)
         self.data_dict = None  # unet.py:147,207
         return self.output
