@@ -62,7 +62,9 @@ const char* vm_last_error(void);
 /* Process-wide tuning knobs (no reference counterpart; TF picks kernels itself):
  *   "conv_kernel"    0 = auto (default), 1 = register-staged MFMA kernel only, 2 = LDS-DMA kernel when legal
  *   "conv_min_tiles" grid size (256-wide output tiles) from which auto uses the LDS-DMA kernel (default 128)
- *   "glds_rb"        K-step bytes of the 256x256 LDS-DMA tile: 128 (2-slot ring, default) or 64 (4-slot) */
+ *   "glds_rb"        K-step bytes of the 256x256 LDS-DMA tile: 128 (2-slot ring, default) or 64 (4-slot)
+ *   "head_kernel"    cout == 1 convs: 0 = MFMA tap-GEMM kernel (default), 1 = generic per-pixel kernel,
+ *                    2 = register-strip kernel */
 int vm_set_option(const char* key, long value);
 /* Name of the conv kernel the calling thread's last vm_conv3x3_nhwc launched, spelled the way
  * rocprofv3 reports it (e.g. "vm::conv3x3_mfma<unsigned short, 128, 128>"); "" before the first call.

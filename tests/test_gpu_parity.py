@@ -52,6 +52,7 @@ CONV_CASES = [  # n, h, w, cin, cout, coff_in, act
     (1, 5, 7, 1024, 512, 0, "none"), (1, 12, 12, 9, 2, 0, "relu"), (2, 10, 9, 30, 32, 0, "relu"),
     (1, 13, 21, 128, 1, 0, "sigmoid"), (1, 9, 9, 96, 48, 0, "relu"), (1, 7, 5, 256, 128, 128, "relu"),
     (1, 15, 16, 5, 64, 0, "softmax"), (1, 4, 4, 1536, 16, 0, "relu"), (3, 33, 47, 32, 24, 0, "relu"),
+    (2, 10, 17, 128, 1, 8, "sigmoid"), (1, 6, 9, 64, 1, 0, "none"), (1, 3, 8, 256, 1, 0, "relu"),
 ]
 
 
@@ -88,6 +89,36 @@ def test_conv3x3_vs_oracle(case, dtype, conv_kernel):
     ref = {"relu": oops.relu, "sigmoid": oops.sigmoid, "softmax": oops.softmax_lastdim}.get(act, lambda v: v)(ref)
     tol = 1e-5 if dtype == "fp32" else 3e-3
     assert relerr(H(y), ref) < tol, relerr(H(y), ref)
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+@pytest.mark.parametrize("shape", [(2, 19, 37, 128), (1, 9, 70, 64), (1, 17, 130, 8), (1, 5, 11, 256)])
+def test_head_kernels_agree(dtype, shape):
+    """cout == 1: the MFMA tap-GEMM, register-strip and generic per-pixel kernels agree with each other and the
+    oracle (f32: up to summation order)."""
+    from vmatting import _lib, ops
+    tdt = ops.TORCH_DTYPE[dtype]
+    rs = np.random.RandomState(5)
+    xf = rs.normal(size=shape).astype(np.float32)
+    wt = (rs.normal(size=(3, 3, shape[-1], 1)) * 0.03).astype(np.float32)
+    if dtype == "bf16":
+        xf = torch.from_numpy(xf).to(torch.bfloat16).float().numpy()
+        wt = torch.from_numpy(wt).to(torch.bfloat16).float().numpy()
+    x = T(xf, tdt)
+    pc = ops.PackedConv(wt, np.array([0.1], np.float32), tdt, DEV)
+    ref = oops.sigmoid(oops.conv3x3_same(xf.astype(np.float64), wt.astype(np.float64)) + 0.1)
+    outs, names = [], []
+    try:
+        for k in (0, 1, 2):
+            _lib.set_option("head_kernel", k)
+            outs.append(H(ops.conv3x3(x, pc, "sigmoid", out_dtype=torch.float32)))
+            names.append(_lib.last_conv_kernel())
+    finally:
+        _lib.set_option("head_kernel", 0)
+    mfma_ok = shape[-1] <= (128 if dtype == "fp32" else 256)  # MFMA head holds <= 8 k-steps of weights
+    assert ("head_mfma" in names[0]) == mfma_ok and names[1].startswith("vm::conv3x3_head<"), names
+    for y in outs:
+        assert np.abs(y - ref).max() < (2e-6 if dtype == "fp32" else 2e-5), np.abs(y - ref).max()
 
 
 @pytest.mark.parametrize("dtype", ["fp32", "bf16"])

@@ -709,6 +709,234 @@ __global__ __launch_bounds__(256) void conv3x3_head(HeadArgs a) {
   }
 }
 
+// Strip variant for cin_pad == 16 * CE * NCH (conv1_5: 128 channels).  A 16-lane group owns NCH 16-byte channel
+// chunks of P consecutive output pixels of one row: it loads the 3 x (P+2) input pixels once (all loads of a
+// row in flight together), keeps its 9-tap weight slice in registers and reduces the P sums across the group.
+// bf16 uses v_dot2_f32_bf16 on the packed pairs (f32 accumulation, no unpack); f32 uses fma.
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+
+template <typename T, int NCH>
+__device__ __forceinline__ float chunk_dot(const uint4 (&x)[NCH], const uint4 (&w)[NCH], float acc) {
+#pragma unroll
+  for (int q = 0; q < NCH; ++q) {
+    const uint32_t xs[4] = {x[q].x, x[q].y, x[q].z, x[q].w};
+    const uint32_t ws[4] = {w[q].x, w[q].y, w[q].z, w[q].w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if constexpr (sizeof(T) == 2)
+        acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, xs[j]), __builtin_bit_cast(bf16x2_t, ws[j]),
+                                              acc, false);
+      else
+        acc = fmaf(__uint_as_float(xs[j]), __uint_as_float(ws[j]), acc);
+    }
+  }
+  return acc;
+}
+
+template <typename T, int NCH, int P>
+__global__ __launch_bounds__(256) void conv3x3_head_strip(HeadArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int CE = 16 / sizeof(T);
+  constexpr int GE = 64 / sizeof(T);
+  T* sw = reinterpret_cast<T*>(smem);  // [9][cin_pad] tap-major, compute dtype
+  const T* Wt = reinterpret_cast<const T*>(a.w);
+  for (int k = threadIdx.x; k < a.K_pad; k += 256) {
+    int tap, c;
+    if (a.chunk_major) {
+      const int g = k / GE;
+      if (g >= a.ng) continue;
+      const int cc = g / 9;
+      tap = g - cc * 9;
+      c = cc * GE + (k - g * GE);
+    } else {
+      if (k >= a.K9) continue;
+      tap = k / a.cin_pad;
+      c = k - tap * a.cin_pad;
+    }
+    sw[tap * a.cin_pad + c] = Wt[k];
+  }
+  __syncthreads();
+
+  const int sub = threadIdx.x & 15;
+  const int grp = threadIdx.x >> 4;
+  const int H = a.H, W = a.W, cs = a.x_cstride;
+  uint4 wr[9][NCH];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int q = 0; q < NCH; ++q)
+      wr[t][q] = *reinterpret_cast<const uint4*>(sw + t * a.cin_pad + (q * 16 + sub) * CE);
+
+  const T* X = reinterpret_cast<const T*>(a.x) + a.x_coff;
+  const float bias = a.bias ? a.bias[0] : 0.f;
+  const float sc = a.scale ? a.scale[0] : 1.f;
+  const float sh = a.shift ? a.shift[0] : 0.f;
+  const int spr = (W + P - 1) / P;
+  const long rows = a.M / W;
+  const long nstrips = rows * spr;
+  const int rowb = W * cs * (int)sizeof(T);
+  for (long s0 = (long)blockIdx.x * 16; s0 < nstrips; s0 += (long)gridDim.x * 16) {
+    // buffer descriptor rebased on the row above the block's first strip (wave-uniform); halo and
+    // out-of-image taps get an out-of-range offset and read as zero (SAME padding)
+    const long row0 = s0 / spr - 1;
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<T*>(X + row0 * (long)W * cs), 0, 0x7ffffff0, 0x00020000);
+    const long s = s0 + grp;
+    if (s >= nstrips) break;
+    const long row = s / spr;
+    const int w0 = (int)(s - row * spr) * P;
+    const int h = (int)(row % H);
+    const int rel = (int)(row - row0);
+    float acc[P];
+#pragma unroll
+    for (int o = 0; o < P; ++o) acc[o] = 0.f;
+#pragma unroll
+    for (int dh = -1; dh <= 1; ++dh) {
+      const bool rok = (unsigned)(h + dh) < (unsigned)H;
+      const int rbase = (rel + dh) * rowb + sub * CE * (int)sizeof(T);
+      uint4 v[P + 2][NCH];
+#pragma unroll
+      for (int i = 0; i < P + 2; ++i) {
+        const int ww = w0 - 1 + i;
+        const bool ok = rok && (unsigned)ww < (unsigned)W;
+#pragma unroll
+        for (int q = 0; q < NCH; ++q) {
+          const int off = ok ? rbase + ww * cs * (int)sizeof(T) + q * 16 * CE * (int)sizeof(T) : OOB;
+          v[i][q] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);  // keep the row's loads in flight together (the scheduler serialises them)
+#pragma unroll
+      for (int i = 0; i < P + 2; ++i)
+#pragma unroll
+        for (int dw = 0; dw < 3; ++dw) {
+          const int o = i - dw;
+          if (o >= 0 && o < P) acc[o] = chunk_dot<T, NCH>(v[i], wr[(dh + 1) * 3 + dw], acc[o]);
+        }
+    }
+    float mine = 0.f;
+#pragma unroll
+    for (int o = 0; o < P; ++o) {
+      float r = acc[o];
+      r += __shfl_xor(r, 8, 16);
+      r += __shfl_xor(r, 4, 16);
+      r += __shfl_xor(r, 2, 16);
+      r += __shfl_xor(r, 1, 16);
+      if (sub == o) mine = r;
+    }
+    if (sub < P && w0 + sub < W) {
+      float v = (mine + bias) * sc + sh;
+      if (a.act == VM_ACT_RELU) v = v > 0.f ? v : 0.f;
+      else if (a.act == VM_ACT_SIGMOID) v = sigmoid_precise(v);
+      else if (a.act == VM_ACT_SOFTMAX) v = 1.f;
+      const long o = (row * W + w0 + sub) * (long)a.y_cstride + a.y_coff;
+      if (a.y_dtype == VM_BF16) reinterpret_cast<uint16_t*>(a.y)[o] = f2bf(v);
+      else reinterpret_cast<float*>(a.y)[o] = v;
+    }
+  }
+}
+
+// MFMA head: cout == 1 recast as a 1x1 GEMM over the 9 taps.  For a TH x TW output tile the block computes
+// Y[p][t] = sum_c X[p][c] * W[t][c] for every pixel p of the (TH+2) x (TW+2) input window (MFMA: 16 pixels x
+// 16 tap-columns, 9 used), parks Y in LDS, then out(r,c) = sum_t Y[(r+dh_t, c+dw_t)][t].  Every input pixel is
+// read once per tile (plus the halo) straight into MFMA A-fragments; no 3x3 re-reads, no VALU dot products.
+template <typename T, int TH, int TW, int NKS>
+__global__ __launch_bounds__(256) void conv3x3_head_mfma(HeadArgs a) {
+  constexpr int CE = 16 / sizeof(T);
+  constexpr int KS = 4 * CE;  // channels per MFMA k-step
+  constexpr int GE = 64 / sizeof(T);
+  constexpr int IW = TW + 2, NPIX = (TH + 2) * IW, NG = (NPIX + 15) / 16;
+  constexpr int GB = 3;  // pixel groups whose loads are in flight together
+  __shared__ float ys[NG * 16 * 9];
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  T* sw = reinterpret_cast<T*>(smem);  // [9][cin_pad] tap-major
+  const T* Wt = reinterpret_cast<const T*>(a.w);
+  for (int k = threadIdx.x; k < a.K_pad; k += 256) {
+    int tap, c;
+    if (a.chunk_major) {
+      const int g = k / GE;
+      if (g >= a.ng) continue;
+      const int cc = g / 9;
+      tap = g - cc * 9;
+      c = cc * GE + (k - g * GE);
+    } else {
+      if (k >= a.K9) continue;
+      tap = k / a.cin_pad;
+      c = k - tap * a.cin_pad;
+    }
+    sw[tap * a.cin_pad + c] = Wt[k];
+  }
+  __syncthreads();
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int col = lane & 15, ks = lane >> 4;
+  const int H = a.H, W = a.W, cs = a.x_cstride, cin = a.cin_pad;
+  uint4 wf[NKS];
+#pragma unroll
+  for (int s = 0; s < NKS; ++s) {
+    const int c = s * KS + ks * CE;
+    wf[s] = (col < 9 && c < cin) ? *reinterpret_cast<const uint4*>(sw + col * cin + c) : make_uint4(0, 0, 0, 0);
+  }
+
+  const int tw = (W + TW - 1) / TW, th = (H + TH - 1) / TH;
+  const int b = blockIdx.x;
+  const int n = b / (tw * th), rem = b - n * tw * th;
+  const int r0 = (rem / tw) * TH, c0 = (rem % tw) * TW;
+  const T* base = reinterpret_cast<const T*>(a.x) + a.x_coff + ((long)n * H + r0 - 1) * (long)W * cs;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<T*>(base), 0, 0x7ffffff0, 0x00020000);
+
+  for (int g0 = wave * GB; g0 < NG; g0 += 4 * GB) {
+    uint4 xa[GB][NKS];
+#pragma unroll
+    for (int u = 0; u < GB; ++u) {
+      const int j = (g0 + u) * 16 + col;  // input-window pixel of this lane's A row
+      const int lr = j / IW, lc = j - lr * IW;
+      const int hh = r0 - 1 + lr, ww = c0 - 1 + lc;
+      const bool ok = g0 + u < NG && j < NPIX && (unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W;
+      const int pix = (lr * W + ww) * cs;
+#pragma unroll
+      for (int s = 0; s < NKS; ++s) {
+        const int c = s * KS + ks * CE;
+        const int off = (ok && c < cin) ? (pix + c) * (int)sizeof(T) : OOB;
+        xa[u][s] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int u = 0; u < GB; ++u) {
+      if (g0 + u >= NG) break;
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < NKS; ++s) mma16<T>(xa[u][s], wf[s], acc);
+      if (col < 9) {
+        const int p = (g0 + u) * 16 + 4 * ks;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) ys[(p + i) * 9 + col] = acc[i];
+      }
+    }
+  }
+  __syncthreads();
+
+  const float bias = a.bias ? a.bias[0] : 0.f;
+  const float sc = a.scale ? a.scale[0] : 1.f;
+  const float sh = a.shift ? a.shift[0] : 0.f;
+  for (int o = tid; o < TH * TW; o += 256) {
+    const int orow = o / TW, ocol = o - orow * TW;
+    const int h = r0 + orow, w = c0 + ocol;
+    if (h >= H || w >= W) continue;
+    float sum = 0.f;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) sum += ys[((orow + t / 3) * IW + ocol + t % 3) * 9 + t];
+    float v = (sum + bias) * sc + sh;
+    if (a.act == VM_ACT_RELU) v = v > 0.f ? v : 0.f;
+    else if (a.act == VM_ACT_SIGMOID) v = sigmoid_precise(v);
+    else if (a.act == VM_ACT_SOFTMAX) v = 1.f;
+    const long oi = (((long)n * H + h) * W + w) * a.y_cstride + a.y_coff;
+    if (a.y_dtype == VM_BF16) reinterpret_cast<uint16_t*>(a.y)[oi] = f2bf(v);
+    else reinterpret_cast<float*>(a.y)[oi] = v;
+  }
+}
+
 // ================================================================ weight packing
 // HWIO f32 [3][3][cin][cout] (unet.py:15 / the VGG npy layout) -> [cout_pad][K_pad] in the compute dtype,
 // K in granule order (see the header comment).
@@ -805,6 +1033,7 @@ static int launch_glds(ConvArgs& a, hipStream_t st) {
 static long g_conv_kernel = 0;
 static long g_conv_min_tiles = 128;
 static long g_glds_rb = 128;
+static long g_head_kernel = 0;
 
 template <typename T, bool FAST>
 static int dispatch_glds(ConvArgs& a, hipStream_t st) {
@@ -846,6 +1075,11 @@ extern "C" int vm_set_option(const char* key, long value) {
   }
   if (!strcmp(key, "conv_min_tiles")) {
     g_conv_min_tiles = value;
+    return VM_OK;
+  }
+  if (!strcmp(key, "head_kernel")) {
+    if (value < 0 || value > 2) return fail(VM_EINVAL, "head_kernel must be 0, 1 or 2");
+    g_head_kernel = value;
     return VM_OK;
   }
   if (!strcmp(key, "glds_rb")) {
@@ -903,6 +1137,44 @@ extern "C" int vm_conv3x3_nhwc(const vm_tensor* x, const void* packed, int cin, 
     h.cin_pad = g.cin_pad; h.K9 = g.K9; h.K_pad = g.K_pad; h.chunk_major = g.chunk_major; h.ng = g.ng;
     h.w = packed; h.bias = bias; h.scale = scale; h.shift = shift; h.act = act;
     h.y = y->ptr; h.y_cstride = y->cstride; h.y_coff = y->coff; h.y_dtype = y->dtype;
+    const int nks = (g.cin_pad + 4 * ce - 1) / (4 * ce);
+    if (g_head_kernel == 0 && nks <= 8) {
+      constexpr int TH = 8, TW = 64;
+      const long tiles = (long)x->n * ((x->h + TH - 1) / TH) * ((x->w + TW - 1) / TW);
+      if (tiles > 0x7fffffffL) return fail(VM_EUNSUPPORTED, "conv3x3 head: too many tiles");
+      const size_t lds = (size_t)9 * g.cin_pad * elem_bytes(dt);
+      const int nk = nks <= 1 ? 1 : nks <= 2 ? 2 : nks <= 4 ? 4 : 8;
+      snprintf(g_last_kernel, sizeof g_last_kernel, "vm::conv3x3_head_mfma<%s, %d, %d, %d>",
+               dt == VM_BF16 ? "unsigned short" : "float", TH, TW, nk);
+#define VM_HEAD_MFMA(TT, NK) \
+  hipLaunchKernelGGL((conv3x3_head_mfma<TT, TH, TW, NK>), dim3(tiles), dim3(256), lds, st, h)
+      if (dt == VM_BF16) {
+        if (nk == 1) VM_HEAD_MFMA(uint16_t, 1); else if (nk == 2) VM_HEAD_MFMA(uint16_t, 2);
+        else if (nk == 4) VM_HEAD_MFMA(uint16_t, 4); else VM_HEAD_MFMA(uint16_t, 8);
+      } else {
+        if (nk == 1) VM_HEAD_MFMA(float, 1); else if (nk == 2) VM_HEAD_MFMA(float, 2);
+        else if (nk == 4) VM_HEAD_MFMA(float, 4); else VM_HEAD_MFMA(float, 8);
+      }
+#undef VM_HEAD_MFMA
+      return check_launch("conv3x3_head_mfma");
+    }
+    constexpr int P = 8;
+    const int nch = g.cin_pad / (16 * ce);
+    if ((nch == 1 || nch == 2) && g.cin_pad % (16 * ce) == 0 && g_head_kernel != 1) {
+      const long strips = (M / x->w) * ((x->w + P - 1) / P);
+      const int grid = grid_for((strips + 15) / 16, 1, 256 * 8);
+      const size_t lds = (size_t)9 * g.cin_pad * elem_bytes(dt);
+      snprintf(g_last_kernel, sizeof g_last_kernel, "vm::conv3x3_head_strip<%s, %d, %d>",
+               dt == VM_BF16 ? "unsigned short" : "float", nch, P);
+      if (dt == VM_BF16) {
+        if (nch == 1) hipLaunchKernelGGL((conv3x3_head_strip<uint16_t, 1, P>), dim3(grid), dim3(256), lds, st, h);
+        else hipLaunchKernelGGL((conv3x3_head_strip<uint16_t, 2, P>), dim3(grid), dim3(256), lds, st, h);
+      } else {
+        if (nch == 1) hipLaunchKernelGGL((conv3x3_head_strip<float, 1, P>), dim3(grid), dim3(256), lds, st, h);
+        else hipLaunchKernelGGL((conv3x3_head_strip<float, 2, P>), dim3(grid), dim3(256), lds, st, h);
+      }
+      return check_launch("conv3x3_head_strip");
+    }
     const int grid = grid_for((M + 15) / 16, 1, 256 * 8);
     const size_t lds = (size_t)9 * g.cin_pad * 4;
     snprintf(g_last_kernel, sizeof g_last_kernel, "vm::conv3x3_head<%s>", dt == VM_BF16 ? "unsigned short" : "float");

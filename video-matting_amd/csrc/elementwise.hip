@@ -76,6 +76,41 @@ __global__ void maxpool2x2_kernel(View x, View y) {
   }
 }
 
+// Row-blocked vector variant: block b covers chunks [part*256, part*256+256) of output row b / bpr, so the
+// (n, oh) decode is wave-uniform and each lane only splits its chunk index into (ow, channel chunk).
+template <typename T>
+__global__ __launch_bounds__(256) void maxpool2x2_rows(View x, View y, int bpr) {
+  constexpr int CE = 16 / sizeof(T);
+  const int row = blockIdx.x / bpr;
+  const int part = blockIdx.x - row * bpr;
+  const int n = row / y.h, oh = row - n * y.h;
+  const int cpp = y.c / CE;
+  const int i = part * 256 + threadIdx.x;
+  if (i >= y.w * cpp) return;
+  const int ow = i / cpp, c = (i - ow * cpp) * CE;
+  const int ih = 2 * oh, iw = 2 * ow;
+  const long p00 = ((long)n * x.h + ih) * x.w + iw;
+  const bool hasr = iw + 1 < x.w, hasd = ih + 1 < x.h;
+  const T* xb = reinterpret_cast<const T*>(x.p) + x.coff + c;
+  const uint4 a = *reinterpret_cast<const uint4*>(xb + p00 * x.cs);
+  const uint4 b = *reinterpret_cast<const uint4*>(xb + (p00 + (hasr ? 1 : 0)) * x.cs);
+  const uint4 d = *reinterpret_cast<const uint4*>(xb + (p00 + (hasd ? x.w : 0)) * x.cs);
+  const uint4 e = *reinterpret_cast<const uint4*>(xb + (p00 + (hasd ? x.w : 0) + (hasr ? 1 : 0)) * x.cs);
+  float m[CE], f[CE];
+  Chunk<T>::unpack(a, m);
+  Chunk<T>::unpack(b, f);
+#pragma unroll
+  for (int j = 0; j < CE; ++j) m[j] = fmaxf(m[j], f[j]);
+  Chunk<T>::unpack(d, f);
+#pragma unroll
+  for (int j = 0; j < CE; ++j) m[j] = fmaxf(m[j], f[j]);
+  Chunk<T>::unpack(e, f);
+#pragma unroll
+  for (int j = 0; j < CE; ++j) m[j] = fmaxf(m[j], f[j]);
+  T* yb = reinterpret_cast<T*>(y.p) + ((long)row * y.w + ow) * y.cs + y.coff + c;
+  *reinterpret_cast<uint4*>(yb) = Chunk<T>::pack(m);
+}
+
 // ---------------------------------------------------------------- TF-1.x legacy bilinear resize
 // tf.image.resize_images (unet.py:58): scale = (float)in/out, src = (float)dst * scale,
 // lo = floor(src), hi = min(lo + 1, in - 1), lerp = src - floor(src);
@@ -128,6 +163,42 @@ __global__ void resize_tf1_kernel(View x, View y, float sy, float sx) {
       stv(y, op, c, top + (bot - top) * yl);
     }
   }
+}
+
+// Row-blocked vector variant (see maxpool2x2_rows): the vertical taps and weight are wave-uniform.
+template <typename T>
+__global__ __launch_bounds__(256) void resize_tf1_rows(View x, View y, float sy, float sx, int bpr) {
+  constexpr int CE = 16 / sizeof(T);
+  const int row = blockIdx.x / bpr;
+  const int part = blockIdx.x - row * bpr;
+  const int n = row / y.h, oh = row - n * y.h;
+  const int cpp = y.c / CE;
+  const int i = part * 256 + threadIdx.x;
+  if (i >= y.w * cpp) return;
+  const int ow = i / cpp, c = (i - ow * cpp) * CE;
+  int y0, y1, x0, x1;
+  float yl, xl;
+  tf1_coord(oh, sy, x.h, y0, y1, yl);
+  tf1_coord(ow, sx, x.w, x0, x1, xl);
+  const T* xb = reinterpret_cast<const T*>(x.p) + x.coff + c;
+  const long r0 = ((long)n * x.h + y0) * x.w, r1 = ((long)n * x.h + y1) * x.w;
+  const uint4 qtl = *reinterpret_cast<const uint4*>(xb + (r0 + x0) * x.cs);
+  const uint4 qtr = *reinterpret_cast<const uint4*>(xb + (r0 + x1) * x.cs);
+  const uint4 qbl = *reinterpret_cast<const uint4*>(xb + (r1 + x0) * x.cs);
+  const uint4 qbr = *reinterpret_cast<const uint4*>(xb + (r1 + x1) * x.cs);
+  float tl[CE], tr[CE], bl[CE], br[CE], o[CE];
+  Chunk<T>::unpack(qtl, tl);
+  Chunk<T>::unpack(qtr, tr);
+  Chunk<T>::unpack(qbl, bl);
+  Chunk<T>::unpack(qbr, br);
+#pragma unroll
+  for (int j = 0; j < CE; ++j) {
+    const float top = tl[j] + (tr[j] - tl[j]) * xl;
+    const float bot = bl[j] + (br[j] - bl[j]) * xl;
+    o[j] = top + (bot - top) * yl;
+  }
+  T* yb = reinterpret_cast<T*>(y.p) + ((long)row * y.w + ow) * y.cs + y.coff + c;
+  *reinterpret_cast<uint4*>(yb) = Chunk<T>::pack(o);
 }
 
 // ---------------------------------------------------------------- convert / pad / affine
@@ -242,8 +313,11 @@ extern "C" int vm_maxpool2x2_same_nhwc(const vm_tensor* x, vm_tensor* y, void* s
   const int grid = grid_for(work, 256);
   View xv = view(x), yv = view(y);
   if (vec) {
-    if (x->dtype == VM_BF16) hipLaunchKernelGGL((maxpool2x2_kernel<uint16_t, true>), dim3(grid), dim3(256), 0, st, xv, yv);
-    else hipLaunchKernelGGL((maxpool2x2_kernel<float, true>), dim3(grid), dim3(256), 0, st, xv, yv);
+    const int bpr = (int)(((long)y->w * (y->c / ce) + 255) / 256);
+    const long blocks = (long)y->n * y->h * bpr;
+    if (blocks > 0x7fffffffL) return fail(VM_EUNSUPPORTED, "maxpool: output too large");
+    if (x->dtype == VM_BF16) hipLaunchKernelGGL((maxpool2x2_rows<uint16_t>), dim3(blocks), dim3(256), 0, st, xv, yv, bpr);
+    else hipLaunchKernelGGL((maxpool2x2_rows<float>), dim3(blocks), dim3(256), 0, st, xv, yv, bpr);
   } else {
     hipLaunchKernelGGL((maxpool2x2_kernel<float, false>), dim3(grid), dim3(256), 0, st, xv, yv);
   }
@@ -263,9 +337,12 @@ extern "C" int vm_resize_bilinear_tf1_nhwc(const vm_tensor* x, vm_tensor* y, voi
   View xv = view(x), yv = view(y);
   // same size: TF-1 resize_images returns its input; the kernel degenerates to a copy (lerp 0)
   if (vec) {
+    const int bpr = (int)(((long)y->w * (y->c / ce) + 255) / 256);
+    const long blocks = (long)y->n * y->h * bpr;
+    if (blocks > 0x7fffffffL) return fail(VM_EUNSUPPORTED, "resize: output too large");
     if (x->dtype == VM_BF16)
-      hipLaunchKernelGGL((resize_tf1_kernel<uint16_t, true>), dim3(grid), dim3(256), 0, st, xv, yv, sy, sx);
-    else hipLaunchKernelGGL((resize_tf1_kernel<float, true>), dim3(grid), dim3(256), 0, st, xv, yv, sy, sx);
+      hipLaunchKernelGGL((resize_tf1_rows<uint16_t>), dim3(blocks), dim3(256), 0, st, xv, yv, sy, sx, bpr);
+    else hipLaunchKernelGGL((resize_tf1_rows<float>), dim3(blocks), dim3(256), 0, st, xv, yv, sy, sx, bpr);
   } else {
     hipLaunchKernelGGL((resize_tf1_kernel<float, false>), dim3(grid), dim3(256), 0, st, xv, yv, sy, sx);
   }
