@@ -60,7 +60,10 @@ typedef struct vm_tensor {
 int vm_abi_version(void);
 const char* vm_last_error(void);
 /* Process-wide tuning knobs (no reference counterpart; TF picks kernels itself):
- *   "conv_kernel"    0 = auto (default), 1 = register-staged MFMA kernel only, 2 = LDS-DMA kernel when legal
+ *   "conv_kernel"    0 = auto (default: patch kernel when legal, else by shape), 1 = register-staged MFMA kernel
+ *                    only, 2 = LDS-DMA kernel when legal, 3 = patch-reuse kernel when legal (bf16, cin % 32 == 0,
+ *                    bf16 output, no softmax)
+ *   "patch_cfg"      patch-kernel tiling override for tuning (0 = default)
  *   "conv_min_tiles" grid size (256-wide output tiles) from which auto uses the LDS-DMA kernel (default 128)
  *   "glds_rb"        K-step bytes of the 256x256 LDS-DMA tile: 128 (2-slot ring, default) or 64 (4-slot)
  *   "head_kernel"    cout == 1 convs: 0 = MFMA tap-GEMM kernel (default), 1 = generic per-pixel kernel,

@@ -56,13 +56,42 @@ CONV_CASES = [  # n, h, w, cin, cout, coff_in, act
 ]
 
 
-@pytest.fixture(params=["regstage", "lds_dma"])
+@pytest.fixture(params=["regstage", "lds_dma", "patch"])
 def conv_kernel(request):
-    """Run a test once per conv kernel: 1 = register-staged, 2 = LDS-DMA pipelined (forced even on small grids)."""
+    """Run a test once per conv kernel: 1 = register-staged, 2 = LDS-DMA pipelined (forced even on small grids),
+    3 = patch-reuse kernel (bf16 output only; other cases fall back to the auto choice)."""
     from vmatting import _lib
-    _lib.set_option("conv_kernel", 1 if request.param == "regstage" else 2)
+    _lib.set_option("conv_kernel", {"regstage": 1, "lds_dma": 2, "patch": 3}[request.param])
     yield request.param
     _lib.set_option("conv_kernel", 0)
+
+
+@pytest.mark.parametrize("cfg", list(range(1, 11)))
+@pytest.mark.parametrize("case", [(1, 9, 33, 64, 64, "relu"), (2, 17, 70, 128, 128, "none"), (1, 20, 45, 96, 192, "relu"),
+                                  (1, 8, 32, 32, 64, "sigmoid"), (1, 3, 5, 256, 128, "relu")])
+def test_patch_kernel_configs(case, cfg):
+    """Every patch-kernel tiling vs the oracle on bf16-rounded operands (bf16 output), partial tiles included."""
+    from vmatting import _lib, ops
+    n, h, w, cin, cout, act = case
+    rs = np.random.RandomState(cin + cout + h)
+    x = torch.from_numpy(rs.normal(size=(n, h, w, cin)).astype(np.float32)).to(torch.bfloat16)
+    wt = torch.from_numpy((rs.normal(size=(3, 3, cin, cout)) * np.sqrt(2.0 / (9 * cin))).astype(np.float32))
+    wt = wt.to(torch.bfloat16).float().numpy()
+    b = (rs.normal(size=cout) * 0.1).astype(np.float32)
+    pc = ops.PackedConv(wt, b, torch.bfloat16, DEV)
+    _lib.set_option("conv_kernel", 3)
+    _lib.set_option("patch_cfg", cfg)
+    try:
+        y = ops.conv3x3(x.to(DEV), pc, act)
+        name = _lib.last_conv_kernel()
+    finally:
+        _lib.set_option("conv_kernel", 0)
+        _lib.set_option("patch_cfg", 0)
+    assert name.startswith("vm::conv3x3_patch<"), name
+    ref = oops.conv3x3_same(x.float().numpy().astype(np.float64), wt.astype(np.float64)) + b
+    ref = {"relu": oops.relu, "sigmoid": oops.sigmoid}.get(act, lambda v: v)(ref)
+    err = np.abs(y.float().cpu().numpy() - ref).max() / max(1.0, np.abs(ref).max())
+    assert err < 1e-2, err
 
 
 @pytest.mark.parametrize("dtype", ["fp32", "bf16"])

@@ -45,7 +45,8 @@ def run(name, h, w, cin, cout, dtype, iters, n=1):
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / iters
     fl = 2.0 * n * h * w * 9 * cin * cout
-    print("%-10s %4dx%-4d %4d->%-4d  %.4f ms  %7.1f TFLOP/s" % (name, h, w, cin, cout, ms, fl / ms / 1e9), flush=True)
+    print("%-10s %4dx%-4d %4d->%-4d  %.4f ms  %7.1f TFLOP/s  %s" % (name, h, w, cin, cout, ms, fl / ms / 1e9,
+                                                                  _lib.last_conv_kernel()), flush=True)
     return ms
 
 
@@ -53,13 +54,15 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--shape", action="append", default=[], help="HxWxCINxCOUT")
     ap.add_argument("--unet-layers", action="store_true")
-    ap.add_argument("--kernel", type=int, default=0, help="conv_kernel option: 0 auto, 1 regstage, 2 LDS-DMA")
+    ap.add_argument("--kernel", type=int, default=0, help="conv_kernel option: 0 auto, 1 regstage, 2 LDS-DMA, 3 patch")
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--glds-rb", type=int, default=128)
+    ap.add_argument("--patch-cfg", type=int, default=0)
     ap.add_argument("--iters", type=int, default=20)
     args = ap.parse_args()
     _lib.set_option("conv_kernel", args.kernel)
     _lib.set_option("glds_rb", args.glds_rb)
+    _lib.set_option("patch_cfg", args.patch_cfg)
     shapes = [("shape",) + tuple(int(v) for v in s.split("x")) for s in args.shape]
     if args.unet_layers:
         shapes += UNET_1080

@@ -127,8 +127,8 @@ __device__ __forceinline__ TileOrigin tile_origin(long m0, int H, int W) {
   const long q = m0 / W;
   o.w0 = (int)(m0 - q * W);
   o.h0 = (int)(q % H);
-  o.rcp_w = 1.0f / (float)W;
-  o.rcp_h = 1.0f / (float)H;
+  o.rcp_w = __builtin_amdgcn_rcpf((float)W);  // approximate: fast_div corrects the quotient
+  o.rcp_h = __builtin_amdgcn_rcpf((float)H);
   return o;
 }
 
@@ -179,39 +179,66 @@ __global__ __launch_bounds__(256, 2) void conv3x3_mfma(ConvArgs a) {
   const __amdgpu_buffer_rsrc_t xrs = x_rsrc<T>(a, xbase);
   const __amdgpu_buffer_rsrc_t wrs = w_rsrc<T>(a, n0);
   const TileOrigin org = tile_origin(m0, H, W);
-  int prow[XR], ph[XR], pw[XR];
+  const int xcs = a.x_cstride;
+  // per row: byte offset of the pixel relative to xbase, and a 9-bit mask of the taps that stay inside the
+  // frame (bit 9, the K padding "tap", is never set) -> a K-step costs one bit test + add + select per load
+  int pofs[XR], tmask[XR];
+  int ph0, pw0;
+  pixel_hw(org, rbase, H, W, true, ph0, pw0);
+  const int pofs0 = (rbase + W + 1) * xcs * (int)sizeof(T);
 #pragma unroll
   for (int i = 0; i < XR; ++i) {
     const int r = rbase + 32 * i;
-    prow[i] = r + W + 1;  // pixel index relative to xbase
-    pixel_hw(org, r, H, W, m0 + r < a.M, ph[i], pw[i]);
+    int ph, pw;
+    if (W >= 32) {  // rows of a lane are 32 pixels apart: at most one row wrap per step
+      ph = ph0;
+      pw = pw0;
+      pw0 += 32;
+      if (pw0 >= W) {
+        pw0 -= W;
+        ph0 = ph0 + 1 == H ? 0 : ph0 + 1;
+      }
+    } else {
+      pixel_hw(org, r, H, W, true, ph, pw);
+    }
+    if (m0 + r >= a.M) ph = -0x40000000;
+    pofs[i] = pofs0 + i * 32 * xcs * (int)sizeof(T);
+    const int vr = (ph >= 1 && ph <= H) | ((ph >= 0 && ph < H) << 1) | ((ph >= -1 && ph < H - 1) << 2);
+    const int vc = (pw >= 1) | (((unsigned)pw < (unsigned)W) << 1) | ((pw < W - 1) << 2);
+    const int vcc = ((unsigned)pw < (unsigned)W) ? vc : 0;
+    int m = 0;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) m |= (((vr >> (t / 3)) & (vcc >> (t % 3))) & 1) << t;
+    tmask[i] = m;
   }
-  const int xcs = a.x_cstride;
   uint4 xr[XR], wr[WR];
+  const int wofs = (rbase * a.K_pad + chunk * CE) * (int)sizeof(T);
+  const int wstride = 32 * a.K_pad * (int)sizeof(T);
 
   auto load = [&](int kt) {
-    int tap, c;
+    int tap, delta;
     if (a.chunk_major) {  // the step's two granules (chunks 0-3 and 4-7) decoded on the scalar unit
       const int g0 = 2 * kt, g1 = g0 + 1;
       const int cc0 = g0 / 9, cc1 = g1 / 9;
       const int tap0 = g0 < a.ng ? g0 - cc0 * 9 : 9, tap1 = g1 < a.ng ? g1 - cc1 * 9 : 9;
+      const int d0 = (((tap0 / 3 - 1) * W + tap0 % 3 - 1) * xcs + cc0 * GE) * (int)sizeof(T);
+      const int d1 = (((tap1 / 3 - 1) * W + tap1 % 3 - 1) * xcs + cc1 * GE) * (int)sizeof(T);
       const bool hi = chunk >= 4;
       tap = hi ? tap1 : tap0;
-      c = (hi ? cc1 * GE : cc0 * GE) + (chunk & 3) * CE;
+      delta = (hi ? d1 : d0) + (chunk & 3) * 16;
     } else {
+      int c;
       k_to_tap<GE>(a, kt * BKE + chunk * CE, tap, c);
+      delta = (((tap / 3 - 1) * W + tap % 3 - 1) * xcs + c) * (int)sizeof(T);
     }
-    const int dh = tap / 3 - 1, dw = tap - (tap / 3) * 3 - 1;
 #pragma unroll
     for (int i = 0; i < XR; ++i) {
-      const int hh = ph[i] + dh, ww = pw[i] + dw;
-      const bool ok = tap < 9 && (unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W;
-      const int off = ok ? ((prow[i] + dh * W + dw) * xcs + c) * (int)sizeof(T) : OOB;
+      const int off = ((tmask[i] >> tap) & 1) ? pofs[i] + delta : OOB;
       xr[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0));
     }
 #pragma unroll
     for (int i = 0; i < WR; ++i) {
-      const int off = ((rbase + 32 * i) * a.K_pad + kt * BKE + chunk * CE) * (int)sizeof(T);
+      const int off = wofs + i * wstride + kt * RB;
       wr[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(wrs, off, 0, 0));
     }
   };
@@ -274,7 +301,59 @@ __global__ __launch_bounds__(256, 2) void conv3x3_mfma(ConvArgs a) {
     __syncthreads();
   }
 
-  // epilogue: f32 staging in LDS, then coalesced 16-byte stores
+  // fast epilogue (bf16 output, no softmax): y = act(acc * scale' + shift') in registers, bf16 rows staged
+  // in LDS (4 channels = one ds_write_b64 per fragment), then 16-byte buffer stores whose descriptor ends at
+  // the last pixel, so rows past M drop in hardware.
+  if (sizeof(T) == 2 && a.y_dtype == VM_BF16 && a.act != VM_ACT_SOFTMAX && a.y_vec && (a.cout & 7) == 0) {
+    constexpr int SR16 = BN * 2 + 16;  // staging row stride in bytes
+#pragma unroll
+    for (int fc = 0; fc < 4; ++fc) {
+      const int col = wn * 64 + fc * 16 + 4 * (lane >> 4);
+      float mul[4], add[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int co = min(n0 + col + j, a.cout - 1);
+        const float sc = a.scale ? a.scale[co] : 1.f;
+        mul[j] = sc;
+        add[j] = (a.bias ? a.bias[co] : 0.f) * sc + (a.shift ? a.shift[co] : 0.f);
+      }
+#pragma unroll
+      for (int fp = 0; fp < 4; ++fp) {
+        const int row = wm * 64 + fp * 16 + (lane & 15);
+        float v[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          v[j] = fmaf(acc[fc][fp][j], mul[j], add[j]);
+          if (a.act == VM_ACT_RELU) v[j] = fmaxf(v[j], 0.f);
+          else if (a.act == VM_ACT_SIGMOID) v[j] = sigmoid_precise(v[j]);
+        }
+        uint2 pk;
+        pk.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+        pk.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+        *reinterpret_cast<uint2*>(smem + row * SR16 + col * 2) = pk;
+      }
+    }
+    __syncthreads();
+    constexpr int CPR = BN / 8;
+    const int ycs2 = a.y_cstride * 2;
+    const long rows_left = a.M - m0;
+    const long rec = rows_left * (long)ycs2;
+    uint16_t* Yb = reinterpret_cast<uint16_t*>(a.y) + a.y_coff + m0 * (long)a.y_cstride + n0;
+    const __amdgpu_buffer_rsrc_t yrs =
+        __builtin_amdgcn_make_buffer_rsrc(Yb, 0, rec > 0x7ffffff0L ? 0x7ffffff0 : (int)rec, 0x00020000);
+#pragma unroll
+    for (int it = 0; it < BM * CPR / 256; ++it) {
+      const int idx = it * 256 + tid;
+      const int rr = idx / CPR, cc = idx % CPR;
+      const uint4 d = *reinterpret_cast<const uint4*>(smem + rr * SR16 + cc * 16);
+      const int off = (n0 + cc * 8 < a.cout) ? rr * ycs2 + cc * 16 : OOB;
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, d), yrs,
+                                             off, 0, 0);
+    }
+    return;
+  }
+
+  // general epilogue: f32 staging in LDS, then coalesced 16-byte stores
   constexpr int SROW = BN + 4;
   float* stg = reinterpret_cast<float*>(smem);
 #pragma unroll
@@ -620,6 +699,201 @@ __global__ __launch_bounds__(512, 1) void conv3x3_glds(ConvArgs a) {
         else
           for (int j = 0; j < 4 && co + j < a.cout; ++j) dst[j] = src[j];
       }
+    }
+  }
+}
+
+// ================================================================ patch kernel (bf16, chunk-major K)
+// 2-D output tile of 8 x 32 pixels.  Per 64-byte channel granule the (8+2) x (32+2) input patch is DMA'd to
+// LDS ONCE and serves all 9 taps: the MFMA pixel fragments of tap (dh, dw) are the patch rows shifted by
+// (dh+1)*34 + dw+1, so the input costs 1.33x its bytes per granule instead of 9x.  Weights stream per tap
+// (granule order cc*9+tap is exactly the chunk-major packing) through an S-slot ring.  LDS-DMA with the
+// 64-byte-row XOR swizzle applied at the source (conflict-free fragment reads for any start row); counted
+// vmcnt per wave + one barrier per step; dummy (out-of-range) pieces past the end keep the counts uniform.
+template <int BN, int WM, int WN, int S, int TH_ = 8>
+struct PatchCfg {
+  static constexpr int TH = TH_, TW = 32, BM = TH * TW;
+  static constexpr int PW = TW + 2, PPIX = (TH + 2) * PW;  // 340 patch pixels
+  static constexpr int NW = WM * WN, NT = 64 * NW;
+  static constexpr int XP = (PPIX + 15) / 16;                // 22 DMA pieces per patch
+  static constexpr int XPW = (XP + NW - 1) / NW;             // max X pieces per wave
+  static constexpr int PB = XP * 1024;
+  static constexpr int WP = BN / 16;                         // DMA pieces per weight slot
+  static constexpr int WPW = (WP + NW - 1) / NW;
+  static constexpr int WSLOT = BN * 64;
+  static constexpr int TPM = BM / WM, TPN = BN / WN;
+  static constexpr int FP = TPM / 16, FC = TPN / 16;
+  static constexpr int SR = 64 * 2 + 16;                    // epilogue staging row (one 64-channel slab, bf16)
+  static constexpr int EPI = BM * SR;
+  static constexpr int MAIN = 2 * PB + S * WSLOT;
+  static constexpr int LDS = MAIN > EPI ? MAIN : EPI;
+  static_assert(TPN == 64, "one 64-channel epilogue slab per wave column");
+  static_assert(TPM % 32 == 0 || TPM == 16, "pixel fragments stay inside one patch row");
+  static_assert(S >= 3 && S <= 9, "ring depth (the X group is counted in at most one window)");
+};
+
+template <int BN, int WM, int WN, int S, int TH, int MINB, int UNR>
+__global__ __launch_bounds__(64 * WM * WN) __attribute__((amdgpu_waves_per_eu(MINB * WM * WN / 4)))
+void conv3x3_patch(ConvArgs a) {
+  using C = PatchCfg<BN, WM, WN, S, TH>;
+  using T = uint16_t;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int NW = C::NW, NT = C::NT, FP = C::FP, FC = C::FC, XPW = C::XPW, WPW = C::WPW;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave % WM, wn = wave / WM;
+  const int H = a.H, W = a.W, cs = a.x_cstride;
+  const int th = (H + C::TH - 1) / C::TH, tw = (W + C::TW - 1) / C::TW;
+  const int t = xcd_tile(blockIdx.x, a.tiles_total);
+  const int st = t / a.tiles_n, nt = t - st * a.tiles_n;
+  const int n = st / (th * tw), srem = st - n * th * tw;
+  const int r0 = (srem / tw) * C::TH, c0 = (srem - (srem / tw) * tw) * C::TW;
+  const int n0 = nt * BN;
+
+  const T* xb = reinterpret_cast<const T*>(a.x) + a.x_coff + ((long)n * H + r0 - 1) * (long)W * cs;
+  const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<T*>(xb), 0, 0x7ffffff0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wrs = w_rsrc<T>(a, n0);
+
+  // DMA geometry: piece k fills 16 LDS rows (4 lanes x 16 B per row); the lane filling physical chunk lpos of
+  // row r fetches logical chunk swz(r, lpos)
+  const int lrow = lane >> 2, lpos = lane & 3;
+  int xoff[XPW];
+  int x_n = 0;
+#pragma unroll
+  for (int i = 0; i < XPW; ++i) {
+    const int piece = wave + i * NW;
+    const int row = piece * 16 + lrow;
+    const int lq = (swz<64>(row, lpos) - row * 64) >> 4;
+    const int pr = row / C::PW, pc = row - pr * C::PW;
+    const int h = r0 - 1 + pr, w = c0 - 1 + pc;
+    const bool ok = row < C::PPIX && (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
+    xoff[i] = ok ? ((pr * W + w) * cs + lq * 8) * 2 : OOB;
+    if (piece < C::XP) ++x_n;
+  }
+  int woff[WPW];
+  int w_n = 0;
+#pragma unroll
+  for (int i = 0; i < WPW; ++i) {
+    const int piece = wave + i * NW;
+    const int row = piece * 16 + lrow;
+    const int lq = (swz<64>(row, lpos) - row * 64) >> 4;
+    woff[i] = (row * a.K_pad + lq * 8) * 2;
+    if (piece < C::WP) ++w_n;
+  }
+  const int nch = a.cin_pad / 32, nsteps = nch * 9;
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr(smem));
+  const uint32_t wring = lds0 + 2 * C::PB;
+
+  auto issue_x = [&](int cc, int buf) {
+    const bool real = cc < nch;
+#pragma unroll
+    for (int i = 0; i < XPW; ++i)
+      if (wave + i * NW < C::XP) glds16(xrs, lds0 + buf * C::PB + (wave + i * NW) * 1024, real ? xoff[i] + cc * 64 : OOB);
+  };
+  auto issue_w = [&](int s, int slot) {
+    const bool real = s < nsteps;
+#pragma unroll
+    for (int i = 0; i < WPW; ++i)
+      if (wave + i * NW < C::WP) glds16(wrs, wring + slot * C::WSLOT + (wave + i * NW) * 1024, real ? woff[i] + s * 64 : OOB);
+  };
+
+  int boff[FC], abase[FP];
+#pragma unroll
+  for (int f = 0; f < FC; ++f) boff[f] = 2 * C::PB + swz<64>(wn * C::TPN + f * 16 + (lane & 15), lane >> 4);
+#pragma unroll
+  for (int f = 0; f < FP; ++f) {
+    const int p = wm * C::TPM + f * 16;
+    abase[f] = (p / C::TW) * C::PW + (p % C::TW) + (lane & 15);
+  }
+  const int ck = lane >> 4;
+
+  f32x4 acc[FC][FP];
+#pragma unroll
+  for (int i = 0; i < FC; ++i)
+#pragma unroll
+    for (int j = 0; j < FP; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  issue_x(0, 0);
+#pragma unroll
+  for (int j = 0; j < S - 1; ++j) issue_w(j, j);
+  int slot = 0;
+  for (int cc = 0; cc < nch; ++cc) {
+    const char* xp = smem + (cc & 1) * C::PB;
+#pragma unroll UNR
+    for (int tap = 0; tap < 9; ++tap) {
+      const int s = cc * 9 + tap;
+      // in flight after W(s): S-2 younger weight slots, plus the next patch when it was issued inside the window
+      wait_vm((S - 2) * w_n + ((tap >= 1 && tap <= S - 2) ? x_n : 0));
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (tap == 0) issue_x(cc + 1, (cc + 1) & 1);
+      int ns = slot + S - 1;
+      ns -= ns >= S ? S : 0;
+      issue_w(s + S - 1, ns);
+      const char* wp = smem + slot * C::WSLOT;
+      uint4 av[FC], bv[FP];
+#pragma unroll
+      for (int f = 0; f < FC; ++f) av[f] = *reinterpret_cast<const uint4*>(wp + boff[f]);
+      const int toff = (tap / 3) * C::PW + tap % 3;
+#pragma unroll
+      for (int f = 0; f < FP; ++f) bv[f] = *reinterpret_cast<const uint4*>(xp + swz<64>(abase[f] + toff, ck));
+#pragma unroll
+      for (int fc = 0; fc < FC; ++fc)
+#pragma unroll
+        for (int fp = 0; fp < FP; ++fp) mma16<T>(av[fc], bv[fp], acc[fc][fp]);
+      slot = slot + 1 == S ? 0 : slot + 1;
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  // epilogue: one 64-channel slab per wave column, bf16 staged, 16-byte buffer stores (masked by OOB offsets)
+  const int ycs2 = a.y_cstride * 2;
+  T* yb = reinterpret_cast<T*>(a.y) + a.y_coff + (((long)n * H + r0) * W + c0) * (long)a.y_cstride + n0;
+  const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(yb, 0, 0x7ffffff0, 0x00020000);
+  for (int sl = 0; sl < WN; ++sl) {
+    __syncthreads();
+    if (wn == sl) {
+#pragma unroll
+      for (int fc = 0; fc < FC; ++fc) {
+        const int col = fc * 16 + 4 * (lane >> 4);
+        float mul[4], add[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int co = min(n0 + sl * 64 + col + j, a.cout - 1);
+          const float sc = a.scale ? a.scale[co] : 1.f;
+          mul[j] = sc;
+          add[j] = (a.bias ? a.bias[co] : 0.f) * sc + (a.shift ? a.shift[co] : 0.f);
+        }
+#pragma unroll
+        for (int fp = 0; fp < FP; ++fp) {
+          const int row = wm * C::TPM + fp * 16 + (lane & 15);
+          float v[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            v[j] = fmaf(acc[fc][fp][j], mul[j], add[j]);
+            if (a.act == VM_ACT_RELU) v[j] = fmaxf(v[j], 0.f);
+            else if (a.act == VM_ACT_SIGMOID) v[j] = sigmoid_precise(v[j]);
+          }
+          uint2 pk;
+          pk.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+          pk.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+          *reinterpret_cast<uint2*>(smem + row * C::SR + col * 2) = pk;
+        }
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < C::BM * 8 / NT; ++it) {
+      const int idx = it * NT + tid;
+      const int rr = idx >> 3, cq = idx & 7;
+      const uint4 d = *reinterpret_cast<const uint4*>(smem + rr * C::SR + cq * 16);
+      const int pr = rr / C::TW, pc = rr % C::TW;
+      const bool ok = r0 + pr < H && c0 + pc < W && n0 + sl * 64 + cq * 8 < a.cout;
+      const int off = ok ? (pr * W + pc) * ycs2 + (sl * 64 + cq * 8) * 2 : OOB;
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, d), yrs,
+                                             off, 0, 0);
     }
   }
 }
@@ -1027,6 +1301,27 @@ static int launch_glds(ConvArgs& a, hipStream_t st) {
   return check_launch("conv3x3_glds");
 }
 
+template <int BN, int WM, int WN, int S, int TH = 8, int MINB = 1, int UNR = 9>
+static int launch_patch(ConvArgs& a, hipStream_t st) {
+  using C = PatchCfg<BN, WM, WN, S, TH>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3_patch<BN, WM, WN, S, TH, MINB, UNR>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
+    if (e != hipSuccess) return fail(VM_EHIP, "hipFuncSetAttribute(patch): %s", hipGetErrorString(e));
+    attr_set = true;
+  }
+  const long N = a.M / ((long)a.H * a.W);
+  const long sp = N * ((a.H + C::TH - 1) / C::TH) * ((a.W + C::TW - 1) / C::TW);
+  a.tiles_n = (a.cout + BN - 1) / BN;
+  if (sp * a.tiles_n > 0x7fffffffL) return fail(VM_EUNSUPPORTED, "conv3x3: too many tiles");
+  a.tiles_total = (int)(sp * a.tiles_n);
+  snprintf(g_last_kernel, sizeof g_last_kernel, "vm::conv3x3_patch<%d, %d, %d, %d, %d, %d, %d>", BN, WM, WN, S, TH, MINB,
+           UNR);
+  hipLaunchKernelGGL((conv3x3_patch<BN, WM, WN, S, TH, MINB, UNR>), dim3(a.tiles_total), dim3(C::NT), C::LDS, st, a);
+  return check_launch("conv3x3_patch");
+}
+
 // tuning knobs (vm_set_option): conv_kernel 0 = auto, 1 = register-staged only, 2 = LDS-DMA whenever legal;
 // conv_min_tiles = smallest grid (in 256-wide output tiles) for which auto picks the LDS-DMA kernel;
 // glds_rb = K-step bytes of the 256x256 LDS-DMA tile (64: 4-slot ring, 128: 2-slot).
@@ -1034,6 +1329,31 @@ static long g_conv_kernel = 0;
 static long g_conv_min_tiles = 128;
 static long g_glds_rb = 128;
 static long g_head_kernel = 0;
+static long g_patch_cfg = 0;
+
+static bool patch_ok(const ConvArgs& a, size_t tsize) {
+  return tsize == 2 && a.chunk_major && a.cin_pad % 32 == 0 && a.y_dtype == VM_BF16 && a.y_vec &&
+         a.act != VM_ACT_SOFTMAX && (a.cout & 7) == 0;
+}
+
+static int dispatch_patch(ConvArgs& a, hipStream_t st) {
+  switch (g_patch_cfg) {
+    case 1: return launch_patch<64, 4, 1, 6>(a, st);
+    case 2: return launch_patch<128, 2, 2, 6>(a, st);
+    case 3: return launch_patch<128, 4, 2, 4>(a, st);
+    case 4: return launch_patch<128, 4, 2, 6>(a, st);
+    case 5: return launch_patch<64, 8, 1, 6>(a, st);
+    case 6: return launch_patch<128, 4, 2, 4, 8, 2, 1>(a, st);
+    case 7: return launch_patch<128, 4, 2, 4, 8, 1, 1>(a, st);
+    case 8: return launch_patch<64, 8, 1, 4, 8, 1, 1>(a, st);
+    case 9: return launch_patch<64, 8, 1, 4, 8, 2, 1>(a, st);
+    case 10: return launch_patch<64, 4, 1, 4, 8, 2, 1>(a, st);
+    default: break;
+  }
+  // measured (tools/convbench.py --unet-layers, UNetVideo 1080p): 8 waves of 32 px x 64 channels, 64-channel
+  // output tiles, beat every 128-channel tiling on every layer (they run out of registers or occupancy)
+  return launch_patch<64, 8, 1, 6>(a, st);
+}
 
 template <typename T, bool FAST>
 static int dispatch_glds(ConvArgs& a, hipStream_t st) {
@@ -1049,6 +1369,7 @@ static int dispatch_glds(ConvArgs& a, hipStream_t st) {
 
 template <typename T>
 static int dispatch_mfma(ConvArgs& a, hipStream_t st) {
+  if ((g_conv_kernel == 0 || g_conv_kernel == 3) && patch_ok(a, sizeof(T))) return dispatch_patch(a, st);
   if (g_conv_kernel != 1 && a.act != VM_ACT_SOFTMAX) {
     // measured (tools/convbench.py): the LDS-DMA kernel wins for cout >= 256 (256x256 tiles); for
     // cout <= 128 its 64-channel-wide waves are DMA-issue-bound and the register-staged kernel is faster
@@ -1069,12 +1390,17 @@ using namespace vm;
 extern "C" int vm_set_option(const char* key, long value) {
   if (!key) return fail(VM_EINVAL, "set_option: NULL key");
   if (!strcmp(key, "conv_kernel")) {
-    if (value < 0 || value > 2) return fail(VM_EINVAL, "conv_kernel must be 0, 1 or 2");
+    if (value < 0 || value > 3) return fail(VM_EINVAL, "conv_kernel must be 0..3");
     g_conv_kernel = value;
     return VM_OK;
   }
   if (!strcmp(key, "conv_min_tiles")) {
     g_conv_min_tiles = value;
+    return VM_OK;
+  }
+  if (!strcmp(key, "patch_cfg")) {
+    if (value < 0 || value > 10) return fail(VM_EINVAL, "patch_cfg must be 0..10");
+    g_patch_cfg = value;
     return VM_OK;
   }
   if (!strcmp(key, "head_kernel")) {
