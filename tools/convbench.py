@@ -58,11 +58,13 @@ def main():
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--glds-rb", type=int, default=128)
     ap.add_argument("--patch-cfg", type=int, default=0)
+    ap.add_argument("--ablate", type=int, default=0, help="patch kernel timing ablation (1 no MFMA, 2 no DMA, 4 no sync)")
     ap.add_argument("--iters", type=int, default=20)
     args = ap.parse_args()
     _lib.set_option("conv_kernel", args.kernel)
     _lib.set_option("glds_rb", args.glds_rb)
     _lib.set_option("patch_cfg", args.patch_cfg)
+    _lib.set_option("patch_ablate", args.ablate)
     shapes = [("shape",) + tuple(int(v) for v in s.split("x")) for s in args.shape]
     if args.unet_layers:
         shapes += UNET_1080

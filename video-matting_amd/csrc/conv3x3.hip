@@ -727,12 +727,12 @@ struct PatchCfg {
   static constexpr int EPI = BM * SR;
   static constexpr int MAIN = 2 * PB + S * WSLOT;
   static constexpr int LDS = MAIN > EPI ? MAIN : EPI;
-  static_assert(TPN == 64, "one 64-channel epilogue slab per wave column");
+  static_assert(TPN % 64 == 0, "whole 64-channel epilogue slabs per wave column");
   static_assert(TPM % 32 == 0 || TPM == 16, "pixel fragments stay inside one patch row");
   static_assert(S >= 3 && S <= 9, "ring depth (the X group is counted in at most one window)");
 };
 
-template <int BN, int WM, int WN, int S, int TH, int MINB, int UNR>
+template <int BN, int WM, int WN, int S, int TH, int MINB, int UNR, bool PF, int ABL>
 __global__ __launch_bounds__(64 * WM * WN) __attribute__((amdgpu_waves_per_eu(MINB * WM * WN / 4)))
 void conv3x3_patch(ConvArgs a) {
   using C = PatchCfg<BN, WM, WN, S, TH>;
@@ -814,36 +814,88 @@ void conv3x3_patch(ConvArgs a) {
 #pragma unroll
     for (int j = 0; j < FP; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  issue_x(0, 0);
+  auto frags = [&](uint4 (&av)[FC], uint4 (&bv)[FP], int slot, int buf, int tap) {
+    const char* wp = smem + slot * C::WSLOT;
+    const char* xp = smem + buf * C::PB;
 #pragma unroll
-  for (int j = 0; j < S - 1; ++j) issue_w(j, j);
-  int slot = 0;
-  for (int cc = 0; cc < nch; ++cc) {
-    const char* xp = smem + (cc & 1) * C::PB;
+    for (int f = 0; f < FC; ++f) av[f] = *reinterpret_cast<const uint4*>(wp + boff[f]);
+    const int toff = (tap / 3) * C::PW + tap % 3;
+#pragma unroll
+    for (int f = 0; f < FP; ++f) {
+      int row = abase[f] + toff;
+      if constexpr (FC * FP >= 32) asm volatile("" : "+v"(row));  // recompute per step: no 9-tap address table
+      bv[f] = *reinterpret_cast<const uint4*>(xp + swz<64>(row, ck));
+    }
+  };
+  auto sync = [&](int n) {
+    wait_vm(n);
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+
+  if constexpr (PF) {
+    // fragments of step s+1 are read right after the barrier of step s, while step s's MFMAs run; the ring
+    // holds S steps (slot s%S is refilled with step s+S once every wave has its step-s fragments in registers)
+    issue_x(0, 0);
+    issue_x(1, 1);
+#pragma unroll
+    for (int j = 0; j < S; ++j) issue_w(j, j);
+    sync((S - 1) * w_n);
+    uint4 av[FC], bv[FP];
+    frags(av, bv, 0, 0, 0);
+    int slot = 0;
+    for (int cc = 0; cc < nch; ++cc) {
 #pragma unroll UNR
-    for (int tap = 0; tap < 9; ++tap) {
-      const int s = cc * 9 + tap;
-      // in flight after W(s): S-2 younger weight slots, plus the next patch when it was issued inside the window
-      wait_vm((S - 2) * w_n + ((tap >= 1 && tap <= S - 2) ? x_n : 0));
-      asm volatile("" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-      if (tap == 0) issue_x(cc + 1, (cc + 1) & 1);
-      int ns = slot + S - 1;
-      ns -= ns >= S ? S : 0;
-      issue_w(s + S - 1, ns);
-      const char* wp = smem + slot * C::WSLOT;
-      uint4 av[FC], bv[FP];
+      for (int tap = 0; tap < 9; ++tap) {
+        const int s = cc * 9 + tap;
 #pragma unroll
-      for (int f = 0; f < FC; ++f) av[f] = *reinterpret_cast<const uint4*>(wp + boff[f]);
-      const int toff = (tap / 3) * C::PW + tap % 3;
+        for (int fc = 0; fc < FC; ++fc)
 #pragma unroll
-      for (int f = 0; f < FP; ++f) bv[f] = *reinterpret_cast<const uint4*>(xp + swz<64>(abase[f] + toff, ck));
+          for (int fp = 0; fp < FP; ++fp) mma16<T>(av[fc], bv[fp], acc[fc][fp]);
+        if (s + 1 < nsteps) {
+          // in flight after W(s+1): S-2 younger weight steps, plus the patch issued at the end of the last chunk
+          sync((S - 2) * w_n + ((tap <= S - 2 && cc >= 1) ? x_n : 0));
+          issue_w(s + S, slot);
+          if (tap == 8) issue_x(cc + 2, cc & 1);
+          slot = slot + 1 == S ? 0 : slot + 1;
+          frags(av, bv, slot, tap == 8 ? (cc + 1) & 1 : cc & 1, tap == 8 ? 0 : tap + 1);
+        }
+      }
+    }
+  } else {
+    issue_x(0, 0);
 #pragma unroll
-      for (int fc = 0; fc < FC; ++fc)
+    for (int j = 0; j < S - 1; ++j) issue_w(j, j);
+    int slot = 0;
+    for (int cc = 0; cc < nch; ++cc) {
+#pragma unroll UNR
+      for (int tap = 0; tap < 9; ++tap) {
+        const int s = cc * 9 + tap;
+        // in flight after W(s): S-2 younger weight slots, plus the next patch when it was issued inside the window
+        if constexpr (!(ABL & 4)) sync((S - 2) * w_n + ((tap >= 1 && tap <= S - 2) ? x_n : 0));
+        if constexpr (!(ABL & 2)) {
+          if (tap == 0) issue_x(cc + 1, (cc + 1) & 1);
+          int ns = slot + S - 1;
+          ns -= ns >= S ? S : 0;
+          issue_w(s + S - 1, ns);
+        }
+        uint4 av[FC], bv[FP];
+        frags(av, bv, slot, cc & 1, tap);
+        if constexpr (!(ABL & 1)) {
 #pragma unroll
-        for (int fp = 0; fp < FP; ++fp) mma16<T>(av[fc], bv[fp], acc[fc][fp]);
-      slot = slot + 1 == S ? 0 : slot + 1;
+          for (int fc = 0; fc < FC; ++fc)
+#pragma unroll
+            for (int fp = 0; fp < FP; ++fp) mma16<T>(av[fc], bv[fp], acc[fc][fp]);
+        } else {  // keep the fragment reads alive without the MFMAs
+#pragma unroll
+          for (int fc = 0; fc < FC; ++fc) asm volatile("" ::"v"(av[fc].x), "v"(av[fc].w));
+#pragma unroll
+          for (int fp = 0; fp < FP; ++fp) asm volatile("" ::"v"(bv[fp].x), "v"(bv[fp].w));
+        }
+        if constexpr (FC * FP >= 32) __builtin_amdgcn_sched_barrier(0);  // no cross-tap hoisting: registers
+        slot = slot + 1 == S ? 0 : slot + 1;
+      }
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -852,12 +904,14 @@ void conv3x3_patch(ConvArgs a) {
   const int ycs2 = a.y_cstride * 2;
   T* yb = reinterpret_cast<T*>(a.y) + a.y_coff + (((long)n * H + r0) * W + c0) * (long)a.y_cstride + n0;
   const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(yb, 0, 0x7ffffff0, 0x00020000);
-  for (int sl = 0; sl < WN; ++sl) {
+  constexpr int SPW = C::TPN / 64;  // 64-channel slabs per wave column
+  for (int sl = 0; sl < BN / 64; ++sl) {
     __syncthreads();
-    if (wn == sl) {
+    if (wn == sl / SPW) {
 #pragma unroll
       for (int fc = 0; fc < FC; ++fc) {
-        const int col = fc * 16 + 4 * (lane >> 4);
+        if (fc / 4 != sl % SPW) continue;
+        const int col = (fc % 4) * 16 + 4 * (lane >> 4);
         float mul[4], add[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -1301,12 +1355,12 @@ static int launch_glds(ConvArgs& a, hipStream_t st) {
   return check_launch("conv3x3_glds");
 }
 
-template <int BN, int WM, int WN, int S, int TH = 8, int MINB = 1, int UNR = 9>
+template <int BN, int WM, int WN, int S, int TH = 8, int MINB = 1, int UNR = 9, bool PF = false, int ABL = 0>
 static int launch_patch(ConvArgs& a, hipStream_t st) {
   using C = PatchCfg<BN, WM, WN, S, TH>;
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3_patch<BN, WM, WN, S, TH, MINB, UNR>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3_patch<BN, WM, WN, S, TH, MINB, UNR, PF, ABL>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
     if (e != hipSuccess) return fail(VM_EHIP, "hipFuncSetAttribute(patch): %s", hipGetErrorString(e));
     attr_set = true;
@@ -1316,9 +1370,9 @@ static int launch_patch(ConvArgs& a, hipStream_t st) {
   a.tiles_n = (a.cout + BN - 1) / BN;
   if (sp * a.tiles_n > 0x7fffffffL) return fail(VM_EUNSUPPORTED, "conv3x3: too many tiles");
   a.tiles_total = (int)(sp * a.tiles_n);
-  snprintf(g_last_kernel, sizeof g_last_kernel, "vm::conv3x3_patch<%d, %d, %d, %d, %d, %d, %d>", BN, WM, WN, S, TH, MINB,
-           UNR);
-  hipLaunchKernelGGL((conv3x3_patch<BN, WM, WN, S, TH, MINB, UNR>), dim3(a.tiles_total), dim3(C::NT), C::LDS, st, a);
+  snprintf(g_last_kernel, sizeof g_last_kernel, "vm::conv3x3_patch<%d, %d, %d, %d, %d, %d, %d, %s, %d>", BN, WM, WN, S,
+           TH, MINB, UNR, PF ? "true" : "false", ABL);
+  hipLaunchKernelGGL((conv3x3_patch<BN, WM, WN, S, TH, MINB, UNR, PF, ABL>), dim3(a.tiles_total), dim3(C::NT), C::LDS, st, a);
   return check_launch("conv3x3_patch");
 }
 
@@ -1330,6 +1384,7 @@ static long g_conv_min_tiles = 128;
 static long g_glds_rb = 128;
 static long g_head_kernel = 0;
 static long g_patch_cfg = 0;
+static long g_patch_ablate = 0;
 
 static bool patch_ok(const ConvArgs& a, size_t tsize) {
   return tsize == 2 && a.chunk_major && a.cin_pad % 32 == 0 && a.y_dtype == VM_BF16 && a.y_vec &&
@@ -1337,21 +1392,35 @@ static bool patch_ok(const ConvArgs& a, size_t tsize) {
 }
 
 static int dispatch_patch(ConvArgs& a, hipStream_t st) {
+  switch (g_patch_ablate) {  // timing experiments on the default tiling (results are garbage)
+    case 1: return launch_patch<64, 8, 1, 6, 8, 1, 9, false, 1>(a, st);
+    case 2: return launch_patch<64, 8, 1, 6, 8, 1, 9, false, 2>(a, st);
+    case 3: return launch_patch<64, 8, 1, 6, 8, 1, 9, false, 3>(a, st);
+    case 4: return launch_patch<64, 8, 1, 6, 8, 1, 9, false, 4>(a, st);
+    case 6: return launch_patch<64, 8, 1, 6, 8, 1, 9, false, 6>(a, st);
+    case 7: return launch_patch<64, 8, 1, 6, 8, 1, 9, false, 7>(a, st);
+    default: break;
+  }
   switch (g_patch_cfg) {
     case 1: return launch_patch<64, 4, 1, 6>(a, st);
     case 2: return launch_patch<128, 2, 2, 6>(a, st);
     case 3: return launch_patch<128, 4, 2, 4>(a, st);
     case 4: return launch_patch<128, 4, 2, 6>(a, st);
     case 5: return launch_patch<64, 8, 1, 6>(a, st);
-    case 6: return launch_patch<128, 4, 2, 4, 8, 2, 1>(a, st);
-    case 7: return launch_patch<128, 4, 2, 4, 8, 1, 1>(a, st);
-    case 8: return launch_patch<64, 8, 1, 4, 8, 1, 1>(a, st);
-    case 9: return launch_patch<64, 8, 1, 4, 8, 2, 1>(a, st);
-    case 10: return launch_patch<64, 4, 1, 4, 8, 2, 1>(a, st);
+    case 6: return launch_patch<64, 8, 1, 6, 8, 1, 9, true>(a, st);
+    case 7: return launch_patch<64, 8, 1, 4, 8, 1, 9, true>(a, st);
+    case 8: return launch_patch<128, 4, 1, 4, 8, 2>(a, st);
+    case 9: return launch_patch<128, 2, 2, 4, 8, 2>(a, st);
+    case 10: return launch_patch<256, 4, 2, 3, 8, 1>(a, st);
     default: break;
   }
-  // measured (tools/convbench.py --unet-layers, UNetVideo 1080p): 8 waves of 32 px x 64 channels, 64-channel
-  // output tiles, beat every 128-channel tiling on every layer (they run out of registers or occupancy)
+  // measured inside the UNetVideo 1080p forward (bench.py --layers): 4 waves of 64 px x 128 channels (2 blocks
+  // per CU) win for cin >= 256, cout >= 128 when the grid holds >= ~2 full rounds of blocks; otherwise 8 waves of
+  // 32 px x 64 channels (more, smaller blocks)
+  const long N = a.M / ((long)a.H * a.W);
+  const long sp = N * ((a.H + 7) / 8) * ((a.W + 31) / 32);
+  if (a.cout >= 128 && a.cin_pad >= 256 && sp * ((a.cout + 127) / 128) >= 1000)
+    return launch_patch<128, 4, 1, 4, 8, 2>(a, st);
   return launch_patch<64, 8, 1, 6>(a, st);
 }
 
@@ -1396,6 +1465,10 @@ extern "C" int vm_set_option(const char* key, long value) {
   }
   if (!strcmp(key, "conv_min_tiles")) {
     g_conv_min_tiles = value;
+    return VM_OK;
+  }
+  if (!strcmp(key, "patch_ablate")) {
+    g_patch_ablate = value;
     return VM_OK;
   }
   if (!strcmp(key, "patch_cfg")) {
