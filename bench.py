@@ -100,8 +100,8 @@ def load_traffic(args):
 
 def conv_roofline(prof, args):
     """Roofline of the dominant conv kernel (largest share of conv time): ALGORITHMIC flops per launch
-    (2*H*W*9*cin*cout of each launch, DESIGN.md §4) / its average launch duration from HIP events on
-    the launch stream inside the timed region."""
+    (2*H*W*9*cin*cout of each launch, DESIGN.md §3) / its average launch duration from HIP events on
+    the launch stream, recorded over a K-step pass identical to the timed region (run right after it)."""
     per = {}
     for fl, name, e0, e1 in prof:
         d = per.setdefault(name, [0, 0.0, 0])
@@ -169,7 +169,6 @@ def main():
         model.forward(x)
     torch.cuda.synchronize()
 
-    prof = None if args.no_profile else ops.conv_profile(True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -180,7 +179,16 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    ops.conv_profile(False)
+
+    # per-kernel HIP events cost ~10% of the step (a marker between every launch), so the roofline pass is a
+    # second, identical K-step pass with an event pair on the launch stream around every conv
+    prof = None
+    if not args.no_profile:
+        prof = ops.conv_profile(True)
+        for _ in range(args.steps):
+            model.forward(x)
+        torch.cuda.synchronize()
+        ops.conv_profile(False)
 
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)

@@ -91,6 +91,14 @@ size_t vm_conv3x3_packed_bytes(int cin, int cout, int dtype);
 int vm_conv3x3_pack_weights(const float* w_hwio, int cin, int cout, int dtype, void* packed, void* stream);
 int vm_conv3x3_nhwc(const vm_tensor* x, const void* packed, int cin, int cout, const float* bias,
                     const float* scale, const float* shift, int act, vm_tensor* y, void* stream);
+/* Same conv, and additionally the 2x2/2 SAME max-pool of its output written to ypool
+ * ([n, ceil(h/2), ceil(w/2), cout], same dtype) — replaces the conv_layer + max_pool pairs
+ * unet.py:170-187 (conv1_2/pool1 ... conv4_3/pool4; max_pool at unet.py:32-33).
+ * Only the bf16 patch kernel fuses pooling: other cases return VM_EUNSUPPORTED and the caller runs
+ * vm_conv3x3_nhwc + vm_maxpool2x2_same_nhwc instead. */
+int vm_conv3x3_pool_nhwc(const vm_tensor* x, const void* packed, int cin, int cout, const float* bias,
+                         const float* scale, const float* shift, int act, vm_tensor* y, vm_tensor* ypool,
+                         void* stream);
 
 /* tf.nn.max_pool(ksize 2, stride 2, 'SAME') — unet.py:32-33, unet_simple.py:95-96, small.py:40,42 */
 int vm_maxpool2x2_same_nhwc(const vm_tensor* x, vm_tensor* y, void* stream);

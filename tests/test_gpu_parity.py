@@ -150,6 +150,32 @@ def test_head_kernels_agree(dtype, shape):
         assert np.abs(y - ref).max() < (2e-6 if dtype == "fp32" else 2e-5), np.abs(y - ref).max()
 
 
+@pytest.mark.parametrize("shape", [(1, 16, 64, 64, 64), (2, 17, 45, 64, 128), (1, 9, 33, 256, 256),
+                                   (1, 135, 240, 32, 64), (1, 1, 1, 64, 64)])
+@pytest.mark.parametrize("kernel", [0, 1])
+def test_conv_fused_maxpool_matches_separate(shape, kernel):
+    """vm_conv3x3_pool_nhwc: the pooled output equals vm_maxpool2x2 of the conv output bit for bit (odd sizes,
+    batches, channel-slice outputs), and the conv output itself is unchanged; unsupported kernels fall back."""
+    from vmatting import _lib, ops
+    n, h, w, cin, cout = shape
+    rs = np.random.RandomState(h * w + cin)
+    x = torch.from_numpy(rs.normal(size=(n, h, w, cin)).astype(np.float32)).to(torch.bfloat16).to(DEV)
+    wt = (rs.normal(size=(3, 3, cin, cout)) * np.sqrt(2.0 / (9 * cin))).astype(np.float32)
+    pc = ops.PackedConv(wt, (rs.normal(size=cout) * 0.1).astype(np.float32), torch.bfloat16, DEV)
+    _lib.set_option("conv_kernel", kernel)
+    try:
+        cat = torch.zeros((n, h, w, 2 * cout), dtype=torch.bfloat16, device=DEV)
+        pooled = torch.full((n, (h + 1) // 2, (w + 1) // 2, cout), 7.0, dtype=torch.bfloat16, device=DEV)
+        ops.conv3x3(x, pc, "relu", out=cat[..., cout:], pool_out=pooled)
+        y_ref = ops.conv3x3(x, pc, "relu")
+        p_ref = ops.maxpool2x2(y_ref)
+    finally:
+        _lib.set_option("conv_kernel", 0)
+    assert torch.equal(cat[..., cout:], y_ref)
+    assert torch.equal(pooled, p_ref)
+    assert float(cat[..., :cout].abs().max()) == 0.0
+
+
 @pytest.mark.parametrize("dtype", ["fp32", "bf16"])
 def test_conv3x3_writes_channel_slice_only(dtype):
     """Concat-by-slice: a conv writing channels [64,128) of a 128-ch buffer leaves [0,64) untouched."""

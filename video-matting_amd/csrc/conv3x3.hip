@@ -42,6 +42,8 @@ struct ConvArgs {
   void* y;
   int y_cstride, y_coff, y_dtype, y_vec;
   int tiles_n, tiles_total;
+  void* py;  // optional fused 2x2/2 SAME max-pool output (patch kernel only), bf16 view
+  int py_cstride, py_coff;
 };
 
 // (K element index k) -> (tap, channel); tap 9 = padding (contributes zero)
@@ -949,6 +951,45 @@ void conv3x3_patch(ConvArgs a) {
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, d), yrs,
                                              off, 0, 0);
     }
+    if (a.py) {
+      // fused tf.nn.max_pool 2x2/2 SAME (unet.py:32-33) of the staged slab: tiles start on even rows/columns,
+      // so every window lies inside the tile; taps past the frame edge are skipped (never win)
+      const int PH = (H + 1) >> 1, PW = (W + 1) >> 1;
+      const int pr0 = r0 >> 1, pc0 = c0 >> 1;
+      T* pb = reinterpret_cast<T*>(a.py) + a.py_coff + (((long)n * PH + pr0) * PW + pc0) * (long)a.py_cstride + n0;
+      const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(pb, 0, 0x7ffffff0, 0x00020000);
+      constexpr int PTW = C::TW / 2, PITEMS = C::BM / 4 * 8;
+#pragma unroll
+      for (int it = 0; it < (PITEMS + NT - 1) / NT; ++it) {
+        const int idx = it * NT + tid;
+        if (idx >= PITEMS) break;
+        const int pp = idx >> 3, cq = idx & 7;
+        const int pr = pp / PTW, pc = pp % PTW;
+        const int rr = 2 * pr * C::TW + 2 * pc;
+        const bool vh = r0 + 2 * pr + 1 < H, vw = c0 + 2 * pc + 1 < W;
+        float m[8], f[8];
+        Chunk<T>::unpack(*reinterpret_cast<const uint4*>(smem + rr * C::SR + cq * 16), m);
+        if (vw) {
+          Chunk<T>::unpack(*reinterpret_cast<const uint4*>(smem + (rr + 1) * C::SR + cq * 16), f);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) m[j] = fmaxf(m[j], f[j]);
+        }
+        if (vh) {
+          Chunk<T>::unpack(*reinterpret_cast<const uint4*>(smem + (rr + C::TW) * C::SR + cq * 16), f);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) m[j] = fmaxf(m[j], f[j]);
+        }
+        if (vh && vw) {
+          Chunk<T>::unpack(*reinterpret_cast<const uint4*>(smem + (rr + C::TW + 1) * C::SR + cq * 16), f);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) m[j] = fmaxf(m[j], f[j]);
+        }
+        const bool ok = pr0 + pr < PH && pc0 + pc < PW && n0 + sl * 64 + cq * 8 < a.cout;
+        const int off = ok ? ((pr * PW + pc) * a.py_cstride + sl * 64 + cq * 8) * 2 : OOB;
+        __builtin_amdgcn_raw_buffer_store_b128(
+            __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, Chunk<T>::pack(m)), prs, off, 0, 0);
+      }
+    }
   }
 }
 
@@ -1511,8 +1552,26 @@ extern "C" int vm_conv3x3_pack_weights(const float* w_hwio, int cin, int cout, i
   return check_launch("pack_weights");
 }
 
+static int conv_impl(const vm_tensor* x, const void* packed, int cin, int cout, const float* bias, const float* scale,
+                     const float* shift, int act, vm_tensor* y, const vm_tensor* yp, void* stream);
+
 extern "C" int vm_conv3x3_nhwc(const vm_tensor* x, const void* packed, int cin, int cout, const float* bias,
                                const float* scale, const float* shift, int act, vm_tensor* y, void* stream) {
+  return conv_impl(x, packed, cin, cout, bias, scale, shift, act, y, nullptr, stream);
+}
+
+extern "C" int vm_conv3x3_pool_nhwc(const vm_tensor* x, const void* packed, int cin, int cout, const float* bias,
+                                    const float* scale, const float* shift, int act, vm_tensor* y, vm_tensor* ypool,
+                                    void* stream) {
+  if (!valid_tensor(ypool) || !y) return fail(VM_EINVAL, "conv3x3_pool: invalid pool tensor");
+  if (ypool->n != y->n || ypool->h != (y->h + 1) / 2 || ypool->w != (y->w + 1) / 2 || ypool->c != cout ||
+      ypool->dtype != y->dtype)
+    return fail(VM_EINVAL, "conv3x3_pool: pool output must be [n, ceil(h/2), ceil(w/2), cout] in the output dtype");
+  return conv_impl(x, packed, cin, cout, bias, scale, shift, act, y, ypool, stream);
+}
+
+static int conv_impl(const vm_tensor* x, const void* packed, int cin, int cout, const float* bias, const float* scale,
+                     const float* shift, int act, vm_tensor* y, const vm_tensor* yp, void* stream) {
   if (!valid_tensor(x) || !valid_tensor(y) || !packed) return fail(VM_EINVAL, "conv3x3: invalid tensor/weights");
   if (cin <= 0 || cout <= 0 || x->c != cin || y->c != cout)
     return fail(VM_EINVAL, "conv3x3: channel mismatch x.c=%d cin=%d y.c=%d cout=%d", x->c, cin, y->c, cout);
@@ -1529,6 +1588,7 @@ extern "C" int vm_conv3x3_nhwc(const vm_tensor* x, const void* packed, int cin, 
   if (act == VM_ACT_SOFTMAX && cout > 128) return fail(VM_EUNSUPPORTED, "conv3x3: fused softmax needs cout <= 128");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const long M = (long)x->n * x->h * x->w;
+  if (yp && cout == 1) return fail(VM_EUNSUPPORTED, "conv3x3_pool: no fused pooling for cout == 1");
 
   if (cout == 1) {
     HeadArgs h{};
@@ -1590,6 +1650,15 @@ extern "C" int vm_conv3x3_nhwc(const vm_tensor* x, const void* packed, int cin, 
   a.y = y->ptr; a.y_cstride = y->cstride; a.y_coff = y->coff; a.y_dtype = y->dtype;
   const int yve = 16 / elem_bytes(y->dtype);
   a.y_vec = (reinterpret_cast<uintptr_t>(y->ptr) % 16 == 0) && (y->cstride % yve == 0) && (y->coff % yve == 0);
+  if (yp) {
+    const bool pvec = reinterpret_cast<uintptr_t>(yp->ptr) % 16 == 0 && yp->cstride % 8 == 0 && yp->coff % 8 == 0;
+    if (cout == 1 || dt != VM_BF16 || !pvec || !patch_ok(a, 2) || g_conv_kernel == 1 || g_conv_kernel == 2)
+      return fail(VM_EUNSUPPORTED, "conv3x3_pool: fused pooling needs the bf16 patch kernel");
+    a.py = yp->ptr;
+    a.py_cstride = yp->cstride;
+    a.py_coff = yp->coff;
+    return dispatch_patch(a, st);
+  }
   if (dt == VM_BF16) return dispatch_mfma<uint16_t>(a, st);
   return dispatch_mfma<float>(a, st);
 }

@@ -88,10 +88,12 @@ class PackedConv:
         return conv3x3(x, self, act, out, out_dtype, affine)
 
 
-def conv3x3(x, pc, act="none", out=None, out_dtype=None, affine=None):
+def conv3x3(x, pc, act="none", out=None, out_dtype=None, affine=None, pool_out=None):
     """tf.nn.conv2d 3x3 SAME + bias_add (+ folded BN affine) + activation, on MFMA.
 
     ``affine``: None -> the PackedConv's own scale/shift; False -> none; (scale, shift) -> those.
+    ``pool_out``: also write tf.nn.max_pool 2x2/2 SAME of the result there (fused into the conv epilogue when
+    the kernel supports it, else a separate max-pool launch).
     """
     if x.dtype != pc.dtype:
         raise TypeError("conv input dtype %s != packed weights dtype %s" % (x.dtype, pc.dtype))
@@ -112,11 +114,23 @@ def conv3x3(x, pc, act="none", out=None, out_dtype=None, affine=None):
         ev0 = torch.cuda.Event(enable_timing=True)
         ev1 = torch.cuda.Event(enable_timing=True)
         ev0.record()
-    check(lib().vm_conv3x3_nhwc(ctypes.byref(xv), _ptr(pc.packed), pc.cin, pc.cout, _ptr(pc.bias), _ptr(scale),
-                                _ptr(shift), _lib.ACT[act], ctypes.byref(yv), stream_handle()), "conv3x3")
+    fused = False
+    if pool_out is not None:
+        pv = nhwc(pool_out)
+        rc = lib().vm_conv3x3_pool_nhwc(ctypes.byref(xv), _ptr(pc.packed), pc.cin, pc.cout, _ptr(pc.bias),
+                                        _ptr(scale), _ptr(shift), _lib.ACT[act], ctypes.byref(yv), ctypes.byref(pv),
+                                        stream_handle())
+        if rc != _lib.VM_EUNSUPPORTED:
+            check(rc, "conv3x3_pool")
+            fused = True
+    if not fused:
+        check(lib().vm_conv3x3_nhwc(ctypes.byref(xv), _ptr(pc.packed), pc.cin, pc.cout, _ptr(pc.bias), _ptr(scale),
+                                    _ptr(shift), _lib.ACT[act], ctypes.byref(yv), stream_handle()), "conv3x3")
     if prof is not None:
         ev1.record()
         prof.append((2 * n * h * w * 9 * pc.cin * pc.cout, _lib.last_conv_kernel(), ev0, ev1))
+    if pool_out is not None and not fused:
+        maxpool2x2(out, out=pool_out)
     return out
 
 

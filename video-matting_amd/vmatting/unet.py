@@ -143,19 +143,15 @@ class UNet:
         ops.convert(x, b["in8"])
         xin = b["in8"][..., :c]
         ops.conv3x3(xin, C["conv1_1"], "relu", out=b["c11"])
-        ops.conv3x3(b["c11"], C["conv1_2"], "relu", out=b["cat1"][..., 64:])
-        ops.maxpool2x2(b["cat1"][..., 64:], out=b["p1"])
+        ops.conv3x3(b["c11"], C["conv1_2"], "relu", out=b["cat1"][..., 64:], pool_out=b["p1"])
         ops.conv3x3(b["p1"], C["conv2_1"], "relu", out=b["c21"])
-        ops.conv3x3(b["c21"], C["conv2_2"], "relu", out=b["cat2"][..., 128:])
-        ops.maxpool2x2(b["cat2"][..., 128:], out=b["p2"])
+        ops.conv3x3(b["c21"], C["conv2_2"], "relu", out=b["cat2"][..., 128:], pool_out=b["p2"])
         ops.conv3x3(b["p2"], C["conv3_1"], "relu", out=b["c31"])
         ops.conv3x3(b["c31"], C["conv3_2"], "relu", out=b["c32"])
-        ops.conv3x3(b["c32"], C["conv3_3"], "relu", out=b["cat3"][..., 256:])
-        ops.maxpool2x2(b["cat3"][..., 256:], out=b["p3"])
+        ops.conv3x3(b["c32"], C["conv3_3"], "relu", out=b["cat3"][..., 256:], pool_out=b["p3"])
         ops.conv3x3(b["p3"], C["conv4_1"], "relu", out=b["c41"])
         ops.conv3x3(b["c41"], C["conv4_2"], "relu", out=b["c42"])
-        ops.conv3x3(b["c42"], C["conv4_3"], "relu", out=b["cat4"][..., 512:])
-        ops.maxpool2x2(b["cat4"][..., 512:], out=b["p4"])
+        ops.conv3x3(b["c42"], C["conv4_3"], "relu", out=b["cat4"][..., 512:], pool_out=b["p4"])
         ops.conv3x3(b["p4"], C["conv5_1"], "relu", out=b["c51"])
         ops.conv3x3(b["c51"], C["conv5_2"], "relu", out=b["c52"])
         # decoder: upconv_concat = resize -> conv (no bias, no relu) -> [up, skip] (unet.py:44-63)
