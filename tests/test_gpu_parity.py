@@ -66,7 +66,7 @@ def conv_kernel(request):
     _lib.set_option("conv_kernel", 0)
 
 
-@pytest.mark.parametrize("cfg", list(range(1, 11)))
+@pytest.mark.parametrize("cfg", list(range(1, 13)))
 @pytest.mark.parametrize("case", [(1, 9, 33, 64, 64, "relu"), (2, 17, 70, 128, 128, "none"), (1, 20, 45, 96, 192, "relu"),
                                   (1, 8, 32, 32, 64, "sigmoid"), (1, 3, 5, 256, 128, "relu")])
 def test_patch_kernel_configs(case, cfg):
@@ -150,6 +150,28 @@ def test_head_kernels_agree(dtype, shape):
         assert np.abs(y - ref).max() < (2e-6 if dtype == "fp32" else 2e-5), np.abs(y - ref).max()
 
 
+@pytest.mark.parametrize("case", [(1, 9, 13, 3, 64, "relu"), (2, 11, 70, 7, 64, "relu"), (1, 33, 65, 8, 128, "none"),
+                                  (1, 1, 1, 7, 64, "relu"), (1, 16, 32, 6, 64, "sigmoid")])
+def test_first_layer_kernel(case):
+    """cin <= 8 with bf16 output dispatches conv3x3_first (4 taps x 8 channels per MFMA K-step)."""
+    from vmatting import _lib, ops
+    n, h, w, cin, cout, act = case
+    rs = np.random.RandomState(cin * 31 + w)
+    x = torch.from_numpy(rs.normal(size=(n, h, w, cin)).astype(np.float32) * 40).to(torch.bfloat16)
+    wt = torch.from_numpy((rs.normal(size=(3, 3, cin, cout)) * 0.02).astype(np.float32)).to(torch.bfloat16)
+    wt = wt.float().numpy()
+    b = (rs.normal(size=cout) * 0.1).astype(np.float32)
+    pc = ops.PackedConv(wt, b, torch.bfloat16, DEV)
+    buf = torch.zeros((n, h, w, 8), dtype=torch.bfloat16, device=DEV)
+    buf[..., :cin] = x.to(DEV)
+    y = ops.conv3x3(buf[..., :cin], pc, act)
+    assert _lib.last_conv_kernel() == "vm::conv3x3_first"
+    ref = oops.conv3x3_same(x.float().numpy().astype(np.float64), wt.astype(np.float64)) + b
+    ref = {"relu": oops.relu, "sigmoid": oops.sigmoid}.get(act, lambda v: v)(ref)
+    err = np.abs(y.float().cpu().numpy() - ref).max() / max(1.0, np.abs(ref).max())
+    assert err < 1e-2, err
+
+
 @pytest.mark.parametrize("shape", [(1, 16, 64, 64, 64), (2, 17, 45, 64, 128), (1, 9, 33, 256, 256),
                                    (1, 135, 240, 32, 64), (1, 1, 1, 64, 64)])
 @pytest.mark.parametrize("kernel", [0, 1])
@@ -212,6 +234,20 @@ def test_resize_tf1_vs_oracle(dtype, io):
     ref = oops.resize_bilinear_tf1(H(x), oh, ow)
     tol = 1e-6 if dtype == "fp32" else 8e-3
     assert np.abs(H(y) - ref).max() <= tol * max(1.0, np.abs(ref).max())
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+@pytest.mark.parametrize("hw", [(7, 9), (68, 120), (1, 1), (135, 240), (3, 50)])
+def test_resize_2x_bit_exact(dtype, hw):
+    """Exact-2x fast path: identical to the TF-1 legacy formula evaluated in float32 (then rounded to bf16)."""
+    from vmatting import ops
+    tdt = ops.TORCH_DTYPE[dtype]
+    ih, iw = hw
+    x = (torch.randn(2, ih, iw, 32, device=DEV) * 3).to(tdt)
+    y = ops.resize_bilinear(x, (2 * ih, 2 * iw))
+    xf = x.float().cpu().numpy()  # float32 operands: the oracle then evaluates the formula in float32 like TF
+    ref = torch.from_numpy(oops.resize_bilinear_tf1(xf, 2 * ih, 2 * iw)).to(tdt)
+    assert torch.equal(y.cpu(), ref)
 
 
 def test_bn_stats_apply_vs_oracle():

@@ -993,6 +993,111 @@ void conv3x3_patch(ConvArgs a) {
   }
 }
 
+// ================================================================ first layer: cin <= 8 (conv1_1, unet.py:65-74)
+// One 16-byte chunk per pixel, so a 32-deep MFMA K-step covers 4 taps x 8 channels: lane group q of the pixel
+// fragment reads the patch row shifted by tap 4j+q (taps >= 9 read as zero), matching the tap-major packing
+// k = tap*8 + c.  The 10 x 34 patch (5.4 KB) is loaded once; the 64 x 96 weight slice lives in registers.
+// 8 waves of 32 px x 64 channels; same bf16 slab epilogue as the patch kernel.
+__global__ __launch_bounds__(512) void conv3x3_first(ConvArgs a) {
+  using T = uint16_t;
+  constexpr int TH = 8, TW = 32, PW = TW + 2, PPIX = (TH + 2) * PW, BM = TH * TW, SR = 64 * 2 + 16;
+  __shared__ __attribute__((aligned(16))) uint4 patch[PPIX];
+  __shared__ __attribute__((aligned(16))) char stg[BM * SR];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int H = a.H, W = a.W, cs = a.x_cstride;
+  const int th = (H + TH - 1) / TH, tw = (W + TW - 1) / TW;
+  const int t = xcd_tile(blockIdx.x, a.tiles_total);
+  const int st = t / a.tiles_n, nt = t - st * a.tiles_n;
+  const int n = st / (th * tw), srem = st - n * th * tw;
+  const int r0 = (srem / tw) * TH, c0 = (srem - (srem / tw) * tw) * TW;
+  const int n0 = nt * 64;
+
+  const T* xb = reinterpret_cast<const T*>(a.x) + a.x_coff + ((long)n * H + r0 - 1) * (long)W * cs;
+  const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<T*>(xb), 0, 0x7ffffff0, 0x00020000);
+  if (tid < PPIX) {
+    const int pr = tid / PW, pc = tid - pr * PW;
+    const int h = r0 - 1 + pr, w = c0 - 1 + pc;
+    const bool ok = (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
+    const int off = ok ? (pr * W + w) * cs * 2 : OOB;
+    patch[tid] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0));
+  }
+  const int col = lane & 15, q = lane >> 4;
+  const __amdgpu_buffer_rsrc_t wrs = w_rsrc<T>(a, n0);
+  uint4 wf[3][4];
+#pragma unroll
+  for (int j = 0; j < 3; ++j)
+#pragma unroll
+    for (int fc = 0; fc < 4; ++fc)
+      wf[j][fc] = __builtin_bit_cast(
+          uint4, __builtin_amdgcn_raw_buffer_load_b128(wrs, ((fc * 16 + col) * a.K_pad + j * 32 + q * 8) * 2, 0, 0));
+  __syncthreads();
+
+  f32x4 acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int k = 0; k < 2; ++k) acc[i][k] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const int tap = 4 * j + q;
+    const int toff = (tap / 3) * PW + tap % 3;
+    uint4 bv[2];
+#pragma unroll
+    for (int fp = 0; fp < 2; ++fp) {
+      const int p = wave * 32 + fp * 16;  // tile pixel of the fragment's first row: one patch row per wave
+      const uint4 v = patch[(p / TW) * PW + (p % TW) + col + (tap < 9 ? toff : 0)];
+      bv[fp] = tap < 9 ? v : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int fc = 0; fc < 4; ++fc)
+#pragma unroll
+      for (int fp = 0; fp < 2; ++fp) mma16<T>(wf[j][fc], bv[fp], acc[fc][fp]);
+  }
+
+#pragma unroll
+  for (int fc = 0; fc < 4; ++fc) {
+    const int cc = fc * 16 + 4 * q;
+    float mul[4], add[4];
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      const int co = min(n0 + cc + jj, a.cout - 1);
+      const float sc = a.scale ? a.scale[co] : 1.f;
+      mul[jj] = sc;
+      add[jj] = (a.bias ? a.bias[co] : 0.f) * sc + (a.shift ? a.shift[co] : 0.f);
+    }
+#pragma unroll
+    for (int fp = 0; fp < 2; ++fp) {
+      const int row = wave * 32 + fp * 16 + col;
+      float v[4];
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        v[jj] = fmaf(acc[fc][fp][jj], mul[jj], add[jj]);
+        if (a.act == VM_ACT_RELU) v[jj] = fmaxf(v[jj], 0.f);
+        else if (a.act == VM_ACT_SIGMOID) v[jj] = sigmoid_precise(v[jj]);
+      }
+      uint2 pk;
+      pk.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+      pk.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+      *reinterpret_cast<uint2*>(stg + row * SR + cc * 2) = pk;
+    }
+  }
+  __syncthreads();
+  const int ycs2 = a.y_cstride * 2;
+  T* yb = reinterpret_cast<T*>(a.y) + a.y_coff + (((long)n * H + r0) * W + c0) * (long)a.y_cstride + n0;
+  const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(yb, 0, 0x7ffffff0, 0x00020000);
+#pragma unroll
+  for (int it = 0; it < BM * 8 / 512; ++it) {
+    const int idx = it * 512 + tid;
+    const int rr = idx >> 3, cq = idx & 7;
+    const uint4 d = *reinterpret_cast<const uint4*>(stg + rr * SR + cq * 16);
+    const int pr = rr / TW, pc = rr % TW;
+    const bool ok = r0 + pr < H && c0 + pc < W && n0 + cq * 8 < a.cout;
+    const int off = ok ? (pr * W + pc) * ycs2 + cq * 16 : OOB;
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, d), yrs,
+                                           off, 0, 0);
+  }
+}
+
 // ================================================================ Cout == 1 head (conv1_5 + sigmoid)
 // unet.py:203-205 / unet_simple.py:142 / small.py:49-50: a 1-channel 3x3 conv over <=128 channels at full
 // resolution is a memory-bound dot product: 16 lanes per pixel, each lane one 16-byte channel chunk per
@@ -1453,6 +1558,8 @@ static int dispatch_patch(ConvArgs& a, hipStream_t st) {
     case 8: return launch_patch<128, 4, 1, 4, 8, 2>(a, st);
     case 9: return launch_patch<128, 2, 2, 4, 8, 2>(a, st);
     case 10: return launch_patch<256, 4, 2, 3, 8, 1>(a, st);
+    case 11: return launch_patch<64, 8, 1, 6, 4>(a, st);
+    case 12: return launch_patch<64, 4, 1, 6, 4>(a, st);
     default: break;
   }
   // measured inside the UNetVideo 1080p forward (bench.py --layers): 4 waves of 64 px x 128 channels (2 blocks
@@ -1462,6 +1569,7 @@ static int dispatch_patch(ConvArgs& a, hipStream_t st) {
   const long sp = N * ((a.H + 7) / 8) * ((a.W + 31) / 32);
   if (a.cout >= 128 && a.cin_pad >= 256 && sp * ((a.cout + 127) / 128) >= 1000)
     return launch_patch<128, 4, 1, 4, 8, 2>(a, st);
+  if (sp * ((a.cout + 63) / 64) < 512) return launch_patch<64, 4, 1, 6, 4>(a, st);  // small grids: 8 x 4 px tiles
   return launch_patch<64, 8, 1, 6>(a, st);
 }
 
@@ -1477,8 +1585,22 @@ static int dispatch_glds(ConvArgs& a, hipStream_t st) {
   return launch_glds<T, 64, 512, 64, 8, 1, 4, FAST>(a, st);
 }
 
+static int launch_first(ConvArgs& a, hipStream_t st) {
+  const long N = a.M / ((long)a.H * a.W);
+  const long sp = N * ((a.H + 7) / 8) * ((a.W + 31) / 32);
+  a.tiles_n = (a.cout + 63) / 64;
+  if (sp * a.tiles_n > 0x7fffffffL) return fail(VM_EUNSUPPORTED, "conv3x3: too many tiles");
+  a.tiles_total = (int)(sp * a.tiles_n);
+  snprintf(g_last_kernel, sizeof g_last_kernel, "vm::conv3x3_first");
+  hipLaunchKernelGGL(conv3x3_first, dim3(a.tiles_total), dim3(512), 0, st, a);
+  return check_launch("conv3x3_first");
+}
+
 template <typename T>
 static int dispatch_mfma(ConvArgs& a, hipStream_t st) {
+  if (sizeof(T) == 2 && g_conv_kernel != 1 && g_conv_kernel != 2 && a.cin_pad == 8 && !a.chunk_major &&
+      a.y_dtype == VM_BF16 && a.y_vec && a.act != VM_ACT_SOFTMAX && (a.cout & 7) == 0 && a.K_pad == 128)
+    return launch_first(a, st);
   if ((g_conv_kernel == 0 || g_conv_kernel == 3) && patch_ok(a, sizeof(T))) return dispatch_patch(a, st);
   if (g_conv_kernel != 1 && a.act != VM_ACT_SOFTMAX) {
     // measured (tools/convbench.py): the LDS-DMA kernel wins for cout >= 256 (256x256 tiles); for
@@ -1513,7 +1635,7 @@ extern "C" int vm_set_option(const char* key, long value) {
     return VM_OK;
   }
   if (!strcmp(key, "patch_cfg")) {
-    if (value < 0 || value > 10) return fail(VM_EINVAL, "patch_cfg must be 0..10");
+    if (value < 0 || value > 12) return fail(VM_EINVAL, "patch_cfg must be 0..12");
     g_patch_cfg = value;
     return VM_OK;
   }

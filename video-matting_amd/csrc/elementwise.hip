@@ -151,12 +151,14 @@ __global__ void resize_tf1_kernel(View x, View y, float sy, float sx) {
       ldc<T>(x, ptl, c, tl); ldc<T>(x, ptr_, c, tr); ldc<T>(x, pbl, c, bl); ldc<T>(x, pbr, c, br);
 #pragma unroll
       for (int j = 0; j < CE; ++j) {
+#pragma clang fp contract(off)
         const float top = tl[j] + (tr[j] - tl[j]) * xl;
         const float bot = bl[j] + (br[j] - bl[j]) * xl;
         o[j] = top + (bot - top) * yl;
       }
       stc<T>(y, op, c, o);
     } else {
+#pragma clang fp contract(off)
       const float vtl = ldv(x, ptl, c), vtr = ldv(x, ptr_, c), vbl = ldv(x, pbl, c), vbr = ldv(x, pbr, c);
       const float top = vtl + (vtr - vtl) * xl;
       const float bot = vbl + (vbr - vbl) * xl;
@@ -193,12 +195,65 @@ __global__ __launch_bounds__(256) void resize_tf1_rows(View x, View y, float sy,
   Chunk<T>::unpack(qbr, br);
 #pragma unroll
   for (int j = 0; j < CE; ++j) {
+#pragma clang fp contract(off)
     const float top = tl[j] + (tr[j] - tl[j]) * xl;
     const float bot = bl[j] + (br[j] - bl[j]) * xl;
     o[j] = top + (bot - top) * yl;
   }
   T* yb = reinterpret_cast<T*>(y.p) + ((long)row * y.w + ow) * y.cs + y.coff + c;
   *reinterpret_cast<uint4*>(yb) = Chunk<T>::pack(o);
+}
+
+// Exact 2x upsampling (y = 2 * x in both dims, scale 0.5): every output pixel's taps are the low-res pixels
+// (i|i+1, j|j+1) of its 2x2 quad, so one lane loads those 4 chunks once and writes the 4 outputs of the quad —
+// the same float32 arithmetic as resize_tf1_kernel (lerp 0 or 0.5), bit-identical results.
+template <typename T>
+__global__ __launch_bounds__(256) void resize2x_tf1_rows(View x, View y, int bpr) {
+  constexpr int CE = 16 / sizeof(T);
+  const int row = blockIdx.x / bpr;  // low-res row n*x.h + i
+  const int part = blockIdx.x - row * bpr;
+  const int n = row / x.h, i = row - n * x.h;
+  const int cpp = y.c / CE;
+  const int t = part * 256 + threadIdx.x;
+  if (t >= x.w * cpp) return;
+  const int j = t / cpp, c = (t - j * cpp) * CE;
+  const int i1 = min(i + 1, x.h - 1), j1 = min(j + 1, x.w - 1);
+  const T* xb = reinterpret_cast<const T*>(x.p) + x.coff + c;
+  const long r0 = ((long)n * x.h + i) * x.w, r1 = ((long)n * x.h + i1) * x.w;
+  float a00[CE], a01[CE], a10[CE], a11[CE];
+  Chunk<T>::unpack(*reinterpret_cast<const uint4*>(xb + (r0 + j) * x.cs), a00);
+  Chunk<T>::unpack(*reinterpret_cast<const uint4*>(xb + (r0 + j1) * x.cs), a01);
+  Chunk<T>::unpack(*reinterpret_cast<const uint4*>(xb + (r1 + j) * x.cs), a10);
+  Chunk<T>::unpack(*reinterpret_cast<const uint4*>(xb + (r1 + j1) * x.cs), a11);
+  T* yb = reinterpret_cast<T*>(y.p) + y.coff + c;
+#pragma unroll
+  for (int dy = 0; dy < 2; ++dy) {
+    const int oy = 2 * i + dy;
+    if (oy >= y.h) break;
+#pragma unroll
+    for (int dx = 0; dx < 2; ++dx) {
+      const int ox = 2 * j + dx;
+      if (ox >= y.w) break;
+      int ly0, ly1, lx0, lx1;
+      float fy, fx;
+      tf1_coord(oy, 0.5f, x.h, ly0, ly1, fy);
+      tf1_coord(ox, 0.5f, x.w, lx0, lx1, fx);
+      // taps: (ly0, lx0) = (i, j); ly1 / lx1 are i1 / j1 when the lerp is nonzero, else they equal i / j
+      const float* tl = a00;
+      const float* tr = (lx1 == lx0) ? a00 : a01;
+      const float* bl = (ly1 == ly0) ? a00 : a10;
+      const float* br = (ly1 == ly0) ? tr : ((lx1 == lx0) ? a10 : a11);
+      float o[CE];
+#pragma unroll
+      for (int e = 0; e < CE; ++e) {
+#pragma clang fp contract(off)
+        const float top = tl[e] + (tr[e] - tl[e]) * fx;
+        const float bot = bl[e] + (br[e] - bl[e]) * fx;
+        o[e] = top + (bot - top) * fy;
+      }
+      *reinterpret_cast<uint4*>(yb + (((long)n * y.h + oy) * y.w + ox) * y.cs) = Chunk<T>::pack(o);
+    }
+  }
 }
 
 // ---------------------------------------------------------------- convert / pad / affine
@@ -336,7 +391,13 @@ extern "C" int vm_resize_bilinear_tf1_nhwc(const vm_tensor* x, vm_tensor* y, voi
   const int grid = grid_for(work, 256);
   View xv = view(x), yv = view(y);
   // same size: TF-1 resize_images returns its input; the kernel degenerates to a copy (lerp 0)
-  if (vec) {
+  if (vec && y->h == 2 * x->h && y->w == 2 * x->w) {
+    const int bpr = (int)(((long)x->w * (y->c / ce) + 255) / 256);
+    const long blocks = (long)x->n * x->h * bpr;
+    if (blocks > 0x7fffffffL) return fail(VM_EUNSUPPORTED, "resize: output too large");
+    if (x->dtype == VM_BF16) hipLaunchKernelGGL((resize2x_tf1_rows<uint16_t>), dim3(blocks), dim3(256), 0, st, xv, yv, bpr);
+    else hipLaunchKernelGGL((resize2x_tf1_rows<float>), dim3(blocks), dim3(256), 0, st, xv, yv, bpr);
+  } else if (vec) {
     const int bpr = (int)(((long)y->w * (y->c / ce) + 255) / 256);
     const long blocks = (long)y->n * y->h * bpr;
     if (blocks > 0x7fffffffL) return fail(VM_EUNSUPPORTED, "resize: output too large");
