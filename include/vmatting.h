@@ -100,6 +100,22 @@ int vm_conv3x3_pool_nhwc(const vm_tensor* x, const void* packed, int cin, int co
                          const float* scale, const float* shift, int act, vm_tensor* y, vm_tensor* ypool,
                          void* stream);
 
+/* tf.image.resize_images(x, [2h, 2w]) (TF-1 legacy bilinear, exact 2x) followed by the 3x3 SAME conv, without
+ * materialising the resized tensor — unet.py:44-63 (upconv_concat: resize_images at :58, conv2d at :60) for the
+ * levels whose skip tensor is exactly twice the input's size.  Bilinear 2x is linear, so every output pixel
+ * (2i+a, 2j+b) is a 3x3 conv of the low-res frame at (i, j) with one of four "phase" filters:
+ * vm_conv3x3_fold_up2x_weights folds the HWIO f32 filter [3,3,cin,cout] into [3,3,cin,4*cout] (channel
+ * p*cout + co = phase p = 2a+b of channel co); pack that with vm_conv3x3_pack_weights(cin, 4*cout) as packed_up
+ * and the plain filter as packed.  The frame border (output rows 0 and 2h-1, columns 0 and 2w-1), where the
+ * resized image's zero padding breaks the folding, is recomputed from packed the unfused way.
+ * x: low-res [n,h,w,cin]; y: [n,2h,2w,cout].  bf16 only (f32 callers use resize + conv3x3: VM_EUNSUPPORTED),
+ * cout % 64 == 0, 16-byte aligned channel views.  Numerics: the folded filter is rounded to bf16 instead of the
+ * resized activations (same bf16 tolerance class as the unfused path). */
+int vm_conv3x3_fold_up2x_weights(const float* w_hwio, int cin, int cout, float* w_up_hwio, void* stream);
+int vm_conv3x3_up2x_nhwc(const vm_tensor* x, const void* packed_up, const void* packed, int cin, int cout,
+                         const float* bias, const float* scale, const float* shift, int act, vm_tensor* y,
+                         void* stream);
+
 /* tf.nn.max_pool(ksize 2, stride 2, 'SAME') — unet.py:32-33, unet_simple.py:95-96, small.py:40,42 */
 int vm_maxpool2x2_same_nhwc(const vm_tensor* x, vm_tensor* y, void* stream);
 

@@ -198,6 +198,59 @@ def test_conv_fused_maxpool_matches_separate(shape, kernel):
     assert float(cat[..., :cout].abs().max()) == 0.0
 
 
+UP_CASES = [(1, 9, 13, 128, 64), (2, 7, 33, 256, 128), (1, 1, 1, 64, 64), (1, 3, 2, 32, 64), (1, 34, 60, 512, 256),
+            (1, 17, 30, 64, 192), (1, 68, 120, 128, 64)]
+
+
+@pytest.mark.parametrize("cfg", [0, 1, 5, 8, 10, 12])
+@pytest.mark.parametrize("case", UP_CASES)
+def test_upconv_folded_resize(case, cfg):
+    """vm_conv3x3_up2x_nhwc (resize folded into four phase filters + exact border recompute) vs the oracle's
+    resize_images -> conv2d on the same bf16 operands (bf16 tolerance), vs the unfused GPU path (resize kernel +
+    conv kernel), with bias + relu through the phase-indexed epilogue and a channel-slice (concat) output."""
+    from vmatting import _lib, ops
+    n, h, w, cin, cout = case
+    rs = np.random.RandomState(h * 31 + cin + cout)
+    x = torch.from_numpy(rs.normal(size=(n, h, w, cin)).astype(np.float32)).to(torch.bfloat16).to(DEV)
+    wt = torch.from_numpy((rs.normal(size=(3, 3, cin, cout)) * np.sqrt(2.0 / (9 * cin))).astype(np.float32))
+    wt = wt.to(torch.bfloat16).float().numpy()
+    b = (rs.normal(size=cout) * 0.1).astype(np.float32)
+    pc = ops.PackedConv(wt, b, torch.bfloat16, DEV)
+    cat = torch.full((n, 2 * h, 2 * w, 2 * cout), 7.0, dtype=torch.bfloat16, device=DEV)
+    _lib.set_option("patch_cfg", cfg)
+    try:
+        ops.upconv3x3(x, pc, "relu", out=cat[..., :cout])
+        name = _lib.last_conv_kernel()
+    finally:
+        _lib.set_option("patch_cfg", 0)
+    assert name.startswith("vm::conv3x3_patch<"), name
+    assert bool(torch.all(cat[..., cout:] == 7.0))
+    y = cat[..., :cout].float().cpu().numpy()
+    r = oops.resize_bilinear_tf1(x.float().cpu().numpy(), 2 * h, 2 * w)
+    r = torch.from_numpy(r.astype(np.float32)).to(torch.bfloat16).float().numpy().astype(np.float64)
+    ref = oops.relu(oops.conv3x3_same(r, wt.astype(np.float64)) + b)
+    err = np.abs(y - ref).max() / max(1.0, np.abs(ref).max())
+    assert err < 1e-2, err
+    unfused = ops.upconv3x3(x, pc, "relu", fold=False).float().cpu().numpy()
+    assert np.abs(y - unfused).max() / max(1.0, np.abs(unfused).max()) < 1e-2
+    # border pixels take the unfused arithmetic (bf16 resized taps, plain filter)
+    for sl in (np.s_[:, 0], np.s_[:, -1], np.s_[:, :, 0], np.s_[:, :, -1]):
+        assert np.abs(y[sl] - unfused[sl]).max() <= 1e-2 * max(1.0, np.abs(unfused[sl]).max())
+
+
+def test_upconv_fold_f32_uses_unfused_path():
+    """f32 has no folded kernel: upconv3x3 runs resize + conv and stays within the f32 parity bound."""
+    from vmatting import ops
+    rs = np.random.RandomState(3)
+    x = torch.from_numpy(rs.normal(size=(1, 5, 7, 64)).astype(np.float32)).to(DEV)
+    wt = (rs.normal(size=(3, 3, 64, 64)) * 0.05).astype(np.float32)
+    pc = ops.PackedConv(wt, None, torch.float32, DEV)
+    assert pc.up2x() is None
+    y = ops.upconv3x3(x, pc, "none")
+    ref = oops.conv3x3_same(oops.resize_bilinear_tf1(H(x), 10, 14), wt.astype(np.float64))
+    assert relerr(H(y), ref) < 1e-5
+
+
 @pytest.mark.parametrize("dtype", ["fp32", "bf16"])
 def test_conv3x3_writes_channel_slice_only(dtype):
     """Concat-by-slice: a conv writing channels [64,128) of a 128-ch buffer leaves [0,64) untouched."""

@@ -11,12 +11,14 @@ mkdir -p "$OUT"
 PASSES=(
   "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE"
   "SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_SALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD SQ_BUSY_CU_CYCLES"
-  "TA_TA_BUSY TA_BUFFER_READ_LDS_WAVEFRONTS TA_ADDR_STALLED_BY_TC_CYCLES TA_DATA_STALLED_BY_TC_CYCLES"
+  "TA_TA_BUSY TA_BUFFER_READ_LDS_WAVEFRONTS"
+  "TA_ADDR_STALLED_BY_TC_CYCLES TA_DATA_STALLED_BY_TC_CYCLES"
   "TCP_TCC_READ_REQ_LATENCY TCP_TCC_READ_REQ TCP_PENDING_STALL_CYCLES TD_TD_BUSY"
   "TCC_HIT_sum TCC_MISS_sum"
   "FETCH_SIZE"
   "WRITE_SIZE"
 )
+[ -n "$PMC_SHORT" ] && PASSES=("${PASSES[@]:0:2}")
 i=0
 for p in "${PASSES[@]}"; do
   i=$((i+1))

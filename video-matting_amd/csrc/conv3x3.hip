@@ -44,6 +44,7 @@ struct ConvArgs {
   int tiles_n, tiles_total;
   void* py;  // optional fused 2x2/2 SAME max-pool output (patch kernel only), bf16 view
   int py_cstride, py_coff;
+  int up, up_cout;  // folded 2x resize (patch kernel only): cout = 4 phases x up_cout, y is [N,2H,2W,up_cout]
 };
 
 // (K element index k) -> (tap, channel); tap 9 = padding (contributes zero)
@@ -768,9 +769,13 @@ void conv3x3_patch(ConvArgs a) {
     const int row = piece * 16 + lrow;
     const int lq = (swz<64>(row, lpos) - row * 64) >> 4;
     const int pr = row / C::PW, pc = row - pr * C::PW;
-    const int h = r0 - 1 + pr, w = c0 - 1 + pc;
+    int h = r0 - 1 + pr, w = c0 - 1 + pc;
+    if (a.up) {  // folded 2x resize: past the bottom/right edge the low-res frame is replicated (TF1 clamp)
+      h = min(h, H - 1);
+      w = min(w, W - 1);
+    }
     const bool ok = row < C::PPIX && (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
-    xoff[i] = ok ? ((pr * W + w) * cs + lq * 8) * 2 : OOB;
+    xoff[i] = ok ? (((h - r0 + 1) * W + w) * cs + lq * 8) * 2 : OOB;
     if (piece < C::XP) ++x_n;
   }
   int woff[WPW];
@@ -903,11 +908,18 @@ void conv3x3_patch(ConvArgs a) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
   // epilogue: one 64-channel slab per wave column, bf16 staged, 16-byte buffer stores (masked by OOB offsets)
+  // a.up (folded 2x resize, vm_conv3x3_up2x_nhwc): output channel n0+sl*64+c is phase p = (a,b) of channel
+  // c' = (n0+sl*64) - p*up_cout + c, stored at full-res pixel (2*h+a, 2*w+b) of the [N,2H,2W,up_cout] view
   const int ycs2 = a.y_cstride * 2;
-  T* yb = reinterpret_cast<T*>(a.y) + a.y_coff + (((long)n * H + r0) * W + c0) * (long)a.y_cstride + n0;
+  const int YW = a.up ? 2 * W : W;
+  T* yb = reinterpret_cast<T*>(a.y) + a.y_coff +
+          (a.up ? (((long)n * 2 * H + 2 * r0) * YW + 2 * c0) : (((long)n * H + r0) * W + c0)) * (long)a.y_cstride;
   const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(yb, 0, 0x7ffffff0, 0x00020000);
   constexpr int SPW = C::TPN / 64;  // 64-channel slabs per wave column
   for (int sl = 0; sl < BN / 64; ++sl) {
+    const int phase = a.up ? (n0 + sl * 64) / a.up_cout : 0;
+    const int cb = n0 + sl * 64 - phase * a.up_cout;  // first (per-phase) output channel of the slab
+    const int ccap = a.up ? a.up_cout : a.cout;
     __syncthreads();
     if (wn == sl / SPW) {
 #pragma unroll
@@ -917,7 +929,7 @@ void conv3x3_patch(ConvArgs a) {
         float mul[4], add[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const int co = min(n0 + sl * 64 + col + j, a.cout - 1);
+          const int co = min(cb + col + j, ccap - 1);
           const float sc = a.scale ? a.scale[co] : 1.f;
           mul[j] = sc;
           add[j] = (a.bias ? a.bias[co] : 0.f) * sc + (a.shift ? a.shift[co] : 0.f);
@@ -946,8 +958,9 @@ void conv3x3_patch(ConvArgs a) {
       const int rr = idx >> 3, cq = idx & 7;
       const uint4 d = *reinterpret_cast<const uint4*>(smem + rr * C::SR + cq * 16);
       const int pr = rr / C::TW, pc = rr % C::TW;
-      const bool ok = r0 + pr < H && c0 + pc < W && n0 + sl * 64 + cq * 8 < a.cout;
-      const int off = ok ? (pr * W + pc) * ycs2 + (sl * 64 + cq * 8) * 2 : OOB;
+      const bool ok = r0 + pr < H && c0 + pc < W && cb + cq * 8 < ccap;
+      const int pix = a.up ? (2 * pr + (phase >> 1)) * YW + 2 * pc + (phase & 1) : pr * W + pc;
+      const int off = ok ? pix * ycs2 + (cb + cq * 8) * 2 : OOB;
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, d), yrs,
                                              off, 0, 0);
     }
@@ -1455,6 +1468,139 @@ static void fill_geom(ConvArgs& a, const PackGeom& g) {
   a.cout_pad = g.cout_pad;
 }
 
+// ================================================================ folded 2x resize (unet.py:44-63 upconv_concat)
+// conv3x3(resize2x(x)) with TF1 legacy bilinear (scale 0.5) is linear in x: resized row 2i = x[i], row 2i+1 =
+// (x[i] + x[i+1]) / 2.  So output pixel (2i+a, 2j+b) is a 3x3 conv of the LOW-RES frame at (i, j) with a phase
+// filter W'_ab[u][v] = sum_{kh,kw} R_a[u][kh] R_b[v][kw] W[kh][kw], u,v in {-1,0,+1}:
+//   R_0 = [[.5,0,0],[.5,1,.5],[0,0,.5]]  (rows u, columns kh)      R_1 = [[0,0,0],[1,.5,0],[0,.5,1]]
+// Output channel p*cout + co of the folded conv is phase p = 2a+b of channel co.  Exact in the interior and, with
+// the low-res frame replicated past its bottom/right edge, at output rows/columns 2H-2; output row/column 0 and
+// 2H-1 / 2W-1 see the resized image's zero padding instead and are recomputed by conv3x3_up2x_border.
+__global__ void fold_up2x_weights(const float* w, int cin, int cout, float* wu) {
+  const long total = 9L * cin * cout;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int co = (int)(i % cout);
+    const long r = i / cout;
+    const int ci = (int)(r % cin);
+    const int tap = (int)(r / cin), u = tap / 3, v = tap % 3;  // low-res tap (u, v) = offset (u-1, v-1)
+    constexpr float R[2][3][3] = {{{.5f, 0.f, 0.f}, {.5f, 1.f, .5f}, {0.f, 0.f, .5f}},
+                                  {{0.f, 0.f, 0.f}, {1.f, .5f, 0.f}, {0.f, .5f, 1.f}}};
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int pa = p >> 1, pb = p & 1;
+      double s = 0.0;
+      for (int kh = 0; kh < 3; ++kh)
+        for (int kw = 0; kw < 3; ++kw) {
+          const float c = R[pa][u][kh] * R[pb][v][kw];
+          if (c != 0.f) s += (double)c * (double)w[((long)(kh * 3 + kw) * cin + ci) * cout + co];
+        }
+      wu[((long)tap * cin + ci) * (4L * cout) + (long)p * cout + co] = (float)s;
+    }
+  }
+}
+
+struct BorderArgs {
+  const void* x;  // low-res [N,H,W,cin] bf16 view
+  int x_cstride, x_coff, H, W, nframes;
+  const void* w;  // plain packed filter (chunk-major bf16)
+  int K_pad, cout, nch;
+  const float* bias;
+  const float* scale;
+  const float* shift;
+  int act;
+  void* y;  // [N,2H,2W,cout] bf16 view
+  int y_cstride, y_coff;
+  int nb;  // border pixels per frame
+};
+
+// Border pixels of the folded upconv, computed the unfused way: the 9 resized taps (TF1 legacy bilinear in f32,
+// rounded to bf16 as vm_resize_bilinear_tf1_nhwc stores them; zero outside the 2H x 2W frame) of 16 pixels are
+// staged per 32-channel granule, and each wave runs 9 MFMAs (one per tap) for its 16 output channels.
+__global__ __launch_bounds__(256) void conv3x3_up2x_border(BorderArgs a) {
+  using T = uint16_t;
+  __shared__ __attribute__((aligned(16))) char stg[9 * 16 * 64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int OH = 2 * a.H, OW = 2 * a.W;
+  const long total = (long)a.nframes * a.nb, b0 = (long)blockIdx.x * 16;
+  const int co0 = blockIdx.y * 64 + wave * 16;
+  auto decode = [&](long b, int& n, int& oy, int& ox) {
+    n = (int)(b / a.nb);
+    const int r = (int)(b - (long)n * a.nb);
+    if (r < OW) { oy = 0; ox = r; }
+    else if (r < 2 * OW) { oy = OH - 1; ox = r - OW; }
+    else if (r < 2 * OW + OH - 2) { oy = r - 2 * OW + 1; ox = 0; }
+    else { oy = r - 2 * OW - (OH - 2) + 1; ox = OW - 1; }
+  };
+  const T* xb = reinterpret_cast<const T*>(a.x) + a.x_coff;
+  const T* wb = reinterpret_cast<const T*>(a.w);
+  f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int cc = 0; cc < a.nch; ++cc) {
+    uint4 wf[9];
+    const bool wok = co0 + (lane & 15) < a.cout;
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap)
+      wf[tap] = wok ? *reinterpret_cast<const uint4*>(wb + (long)(co0 + (lane & 15)) * a.K_pad + (cc * 9 + tap) * 32 +
+                                                      (lane >> 4) * 8)
+                    : make_uint4(0, 0, 0, 0);
+    for (int it = tid; it < 9 * 64; it += 256) {
+      const int tap = it >> 6, px = (it >> 2) & 15, q = it & 3;
+      float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      if (b0 + px < total) {
+        int n, oy, ox;
+        decode(b0 + px, n, oy, ox);
+        const int yy = oy + tap / 3 - 1, xx = ox + tap % 3 - 1;
+        if ((unsigned)yy < (unsigned)OH && (unsigned)xx < (unsigned)OW) {
+#pragma clang fp contract(off)
+          const float sy = (float)yy * 0.5f, sx = (float)xx * 0.5f;
+          const float fy0 = floorf(sy), fx0 = floorf(sx);
+          const int y0 = (int)fy0, x0 = (int)fx0, y1 = min(y0 + 1, a.H - 1), x1 = min(x0 + 1, a.W - 1);
+          const float ly = sy - fy0, lx = sx - fx0;
+          const int c = cc * 32 + q * 8;
+          const long r0 = ((long)n * a.H + y0) * a.W, r1 = ((long)n * a.H + y1) * a.W;
+          float tl[8], tr[8], bl[8], br[8];
+          Chunk<T>::unpack(*reinterpret_cast<const uint4*>(xb + (r0 + x0) * a.x_cstride + c), tl);
+          Chunk<T>::unpack(*reinterpret_cast<const uint4*>(xb + (r0 + x1) * a.x_cstride + c), tr);
+          Chunk<T>::unpack(*reinterpret_cast<const uint4*>(xb + (r1 + x0) * a.x_cstride + c), bl);
+          Chunk<T>::unpack(*reinterpret_cast<const uint4*>(xb + (r1 + x1) * a.x_cstride + c), br);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float top = tl[e] + (tr[e] - tl[e]) * lx;
+            const float bot = bl[e] + (br[e] - bl[e]) * lx;
+            o[e] = top + (bot - top) * ly;
+          }
+        }
+      }
+      *reinterpret_cast<uint4*>(stg + (tap * 16 + px) * 64 + q * 16) = Chunk<T>::pack(o);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap)
+      mma16<T>(wf[tap], *reinterpret_cast<const uint4*>(stg + (tap * 16 + (lane & 15)) * 64 + (lane >> 4) * 16), acc);
+    __syncthreads();
+  }
+  // lane holds output channels co0 + 4*(lane>>4) + j of border pixel b0 + (lane&15)
+  const long b = b0 + (lane & 15);
+  if (b >= total) return;
+  int n, oy, ox;
+  decode(b, n, oy, ox);
+  const int cq = co0 + 4 * (lane >> 4);
+  if (cq >= a.cout) return;
+  float v[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int co = min(cq + j, a.cout - 1);
+    const float sc = a.scale ? a.scale[co] : 1.f;
+    v[j] = fmaf(acc[j], sc, (a.bias ? a.bias[co] : 0.f) * sc + (a.shift ? a.shift[co] : 0.f));
+    if (a.act == VM_ACT_RELU) v[j] = fmaxf(v[j], 0.f);
+    else if (a.act == VM_ACT_SIGMOID) v[j] = sigmoid_precise(v[j]);
+  }
+  T* yp = reinterpret_cast<T*>(a.y) + (((long)n * OH + oy) * OW + ox) * (long)a.y_cstride + a.y_coff + cq;
+  uint2 pk;
+  pk.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+  pk.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+  *reinterpret_cast<uint2*>(yp) = pk;
+}
+
 // ================================================================ dispatch
 // name of the kernel the last conv call on this thread launched, spelled as rocprofv3 reports it
 // (bench.py matches its per-launch PMC traffic by this name)
@@ -1690,6 +1836,56 @@ extern "C" int vm_conv3x3_pool_nhwc(const vm_tensor* x, const void* packed, int 
       ypool->dtype != y->dtype)
     return fail(VM_EINVAL, "conv3x3_pool: pool output must be [n, ceil(h/2), ceil(w/2), cout] in the output dtype");
   return conv_impl(x, packed, cin, cout, bias, scale, shift, act, y, ypool, stream);
+}
+
+extern "C" int vm_conv3x3_fold_up2x_weights(const float* w_hwio, int cin, int cout, float* w_up_hwio, void* stream) {
+  if (!w_hwio || !w_up_hwio || cin <= 0 || cout <= 0) return fail(VM_EINVAL, "fold_up2x: bad argument");
+  hipLaunchKernelGGL(fold_up2x_weights, dim3(grid_for(9L * cin * cout, 256)), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), w_hwio, cin, cout, w_up_hwio);
+  return check_launch("fold_up2x_weights");
+}
+
+extern "C" int vm_conv3x3_up2x_nhwc(const vm_tensor* x, const void* packed_up, const void* packed, int cin, int cout,
+                                    const float* bias, const float* scale, const float* shift, int act, vm_tensor* y,
+                                    void* stream) {
+  if (!valid_tensor(x) || !valid_tensor(y) || !packed_up || !packed)
+    return fail(VM_EINVAL, "conv3x3_up2x: invalid tensor/weights");
+  if (cin <= 0 || cout <= 0 || x->c != cin || y->c != cout)
+    return fail(VM_EINVAL, "conv3x3_up2x: channel mismatch x.c=%d cin=%d y.c=%d cout=%d", x->c, cin, y->c, cout);
+  if (y->n != x->n || y->h != 2 * x->h || y->w != 2 * x->w)
+    return fail(VM_EINVAL, "conv3x3_up2x: output must be [%d,%d,%d,%d]", x->n, 2 * x->h, 2 * x->w, cout);
+  if (act < VM_ACT_NONE || act > VM_ACT_SOFTMAX) return fail(VM_EINVAL, "conv3x3_up2x: act %d", act);
+  const PackGeom g = geom(cin, 4 * cout, x->dtype), g1 = geom(cin, cout, x->dtype);
+  const bool xvec = reinterpret_cast<uintptr_t>(x->ptr) % 16 == 0 && x->cstride % 8 == 0 && x->coff % 8 == 0 &&
+                    x->coff + g.cin_pad <= x->cstride;
+  const bool yvec = reinterpret_cast<uintptr_t>(y->ptr) % 16 == 0 && y->cstride % 8 == 0 && y->coff % 8 == 0;
+  if (x->dtype != VM_BF16 || y->dtype != VM_BF16 || cout % 64 || !xvec || !yvec || act == VM_ACT_SOFTMAX ||
+      g_conv_kernel == 1 || g_conv_kernel == 2)
+    return fail(VM_EUNSUPPORTED, "conv3x3_up2x: folded resize needs the bf16 patch kernel (cout %% 64 == 0, "
+                                 "16-byte channel views)");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  ConvArgs a{};
+  a.x = x->ptr; a.x_cstride = x->cstride; a.x_coff = x->coff; a.H = x->h; a.W = x->w;
+  a.M = (long)x->n * x->h * x->w;
+  fill_geom(a, g);
+  a.w = packed_up; a.cout = 4 * cout;
+  a.bias = bias; a.scale = scale; a.shift = shift; a.act = act;
+  a.y = y->ptr; a.y_cstride = y->cstride; a.y_coff = y->coff; a.y_dtype = y->dtype; a.y_vec = 1;
+  a.up = 1; a.up_cout = cout;
+  if (!patch_ok(a, 2)) return fail(VM_EUNSUPPORTED, "conv3x3_up2x: shape not supported by the patch kernel");
+  int rc = dispatch_patch(a, st);
+  if (rc != VM_OK) return rc;
+  BorderArgs b{};
+  b.x = x->ptr; b.x_cstride = x->cstride; b.x_coff = x->coff; b.H = x->h; b.W = x->w; b.nframes = x->n;
+  b.w = packed; b.K_pad = g1.K_pad; b.cout = cout; b.nch = g1.cin_pad / 32;
+  b.bias = bias; b.scale = scale; b.shift = shift; b.act = act;
+  b.y = y->ptr; b.y_cstride = y->cstride; b.y_coff = y->coff;
+  const int OH = 2 * x->h, OW = 2 * x->w;
+  b.nb = 2 * OW + 2 * (OH - 2);
+  const long nblk = ((long)x->n * b.nb + 15) / 16;
+  if (nblk > 0x7fffffffL) return fail(VM_EUNSUPPORTED, "conv3x3_up2x: too many border pixels");
+  hipLaunchKernelGGL(conv3x3_up2x_border, dim3((unsigned)nblk, cout / 64), dim3(256), 0, st, b);
+  return check_launch("conv3x3_up2x_border");
 }
 
 static int conv_impl(const vm_tensor* x, const void* packed, int cin, int cout, const float* bias, const float* scale,

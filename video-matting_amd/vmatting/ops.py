@@ -80,6 +80,22 @@ class PackedConv:
         self.scale = as_f(scale)
         self.shift = as_f(shift)
 
+    def up2x(self):
+        """The folded-resize weights of this filter (vm_conv3x3_fold_up2x_weights + pack, cout' = 4*cout),
+        built once on first use; None when the compute dtype has no folded path (f32)."""
+        if self.dtype != torch.bfloat16 or self.cout % 64:
+            return None
+        if getattr(self, "_up", None) is None:
+            dev = self.packed.device
+            wu = torch.empty((3, 3, self.cin, 4 * self.cout), dtype=torch.float32, device=dev)
+            check(lib().vm_conv3x3_fold_up2x_weights(_ptr(self.w_hwio), self.cin, self.cout, _ptr(wu),
+                                                     stream_handle()), "fold_up2x_weights")
+            nbytes = lib().vm_conv3x3_packed_bytes(self.cin, 4 * self.cout, _DT[self.dtype])
+            self._up = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+            check(lib().vm_conv3x3_pack_weights(_ptr(wu), self.cin, 4 * self.cout, _DT[self.dtype], _ptr(self._up),
+                                                stream_handle()), "pack_weights(up2x)")
+        return self._up
+
     def set_affine(self, scale, shift):
         self.scale = None if scale is None else torch.as_tensor(scale, dtype=torch.float32).to(self.packed.device)
         self.shift = None if shift is None else torch.as_tensor(shift, dtype=torch.float32).to(self.packed.device)
@@ -132,6 +148,37 @@ def conv3x3(x, pc, act="none", out=None, out_dtype=None, affine=None, pool_out=N
     if pool_out is not None and not fused:
         maxpool2x2(out, out=pool_out)
     return out
+
+
+def upconv3x3(x, pc, act="none", out=None, size=None, rbuf=None, fold=True):
+    """tf.image.resize_images(x, size) -> conv3x3 (unet.py:44-63, the upconv half of upconv_concat).
+
+    Exact 2x upsampling in bf16 runs as ONE folded conv on the low-res frame (vm_conv3x3_up2x_nhwc, no resized
+    tensor in HBM) when ``fold``; any other case is the resize kernel (into ``rbuf`` if given) followed by the
+    conv kernel."""
+    n, h, w, _ = x.shape
+    oh, ow = (2 * h, 2 * w) if size is None else (int(size[0]), int(size[1]))
+    if out is None:
+        out = torch.empty((n, oh, ow, pc.cout), dtype=x.dtype, device=x.device)
+    up = pc.up2x() if fold and (oh, ow) == (2 * h, 2 * w) and x.dtype == pc.dtype else None
+    if up is not None:
+        xv, yv = nhwc(x), nhwc(out)
+        prof = _CONV_PROFILE
+        if prof is not None:
+            ev0 = torch.cuda.Event(enable_timing=True)
+            ev1 = torch.cuda.Event(enable_timing=True)
+            ev0.record()
+        rc = lib().vm_conv3x3_up2x_nhwc(ctypes.byref(xv), _ptr(up), _ptr(pc.packed), pc.cin, pc.cout, _ptr(pc.bias),
+                                        _ptr(pc.scale), _ptr(pc.shift), _lib.ACT[act], ctypes.byref(yv),
+                                        stream_handle())
+        if rc != _lib.VM_EUNSUPPORTED:
+            check(rc, "conv3x3_up2x")
+            if prof is not None:
+                ev1.record()
+                prof.append((2 * n * oh * ow * 9 * pc.cin * pc.cout, _lib.last_conv_kernel(), ev0, ev1))
+            return out
+    r = resize_bilinear(x, (oh, ow), out=rbuf)
+    return conv3x3(r, pc, act, out=out)
 
 
 # When a list, conv3x3 appends (algorithmic FLOPs, is_head, start_event, end_event) per launch —

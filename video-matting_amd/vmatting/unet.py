@@ -43,6 +43,8 @@ class UNet:
     """Base class (unet.py:20-83)."""
 
     IN_CH = None
+    # upconvs whose exact-2x resize is folded into the conv (ops.upconv3x3; bf16 only, others resize + conv)
+    fold_upconv = ("upconv_3", "upconv_4")  # upconv_2 folded would run on the 135x240 grid: slower (measured)
 
     def __init__(self, vgg16_npy_path=None, dtype="bf16", device="cuda"):
         self.data_dict = load_vgg16(vgg16_npy_path)
@@ -91,6 +93,8 @@ class UNet:
         for k in sorted(self.convs):
             pc = self.convs[k]
             out.append(pc.packed)
+            if k in self.fold_upconv and pc.up2x() is not None:
+                out.append(pc.up2x())
             if pc.bias is not None:
                 out.append(pc.bias)
         return out
@@ -155,17 +159,15 @@ class UNet:
         ops.conv3x3(b["p4"], C["conv5_1"], "relu", out=b["c51"])
         ops.conv3x3(b["c51"], C["conv5_2"], "relu", out=b["c52"])
         # decoder: upconv_concat = resize -> conv (no bias, no relu) -> [up, skip] (unet.py:44-63)
-        ops.resize_bilinear(b["c52"], L[3], out=b["r1"])
-        ops.conv3x3(b["r1"], C["upconv_1"], "none", out=b["cat4"][..., :512])
+        up = lambda src, scope, lv, out, rkey: ops.upconv3x3(  # noqa: E731
+            src, C[scope], "none", out=out, size=L[lv], rbuf=b[rkey], fold=scope in self.fold_upconv)
+        up(b["c52"], "upconv_1", 3, b["cat4"][..., :512], "r1")
         ops.conv3x3(b["cat4"], C["conv4_4"], "relu", out=b["c44"])
-        ops.resize_bilinear(b["c44"], L[2], out=b["r2"])
-        ops.conv3x3(b["r2"], C["upconv_2"], "none", out=b["cat3"][..., :256])
+        up(b["c44"], "upconv_2", 2, b["cat3"][..., :256], "r2")
         ops.conv3x3(b["cat3"], C["conv3_4"], "relu", out=b["c34"])
-        ops.resize_bilinear(b["c34"], L[1], out=b["r3"])
-        ops.conv3x3(b["r3"], C["upconv_3"], "none", out=b["cat2"][..., :128])
+        up(b["c34"], "upconv_3", 1, b["cat2"][..., :128], "r3")
         ops.conv3x3(b["cat2"], C["conv2_3"], "relu", out=b["c23"])
-        ops.resize_bilinear(b["c23"], L[0], out=b["r4"])
-        ops.conv3x3(b["r4"], C["upconv_4"], "none", out=b["cat1"][..., :64])
+        up(b["c23"], "upconv_4", 0, b["cat1"][..., :64], "r4")
         ops.conv3x3(b["cat1"], C["conv1_5"], "none", out=b["logits"])
         ops.convert(b["logits"], b["out"], act="sigmoid")
         self._publish(b)
