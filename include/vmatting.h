@@ -100,6 +100,16 @@ int vm_conv3x3_pool_nhwc(const vm_tensor* x, const void* packed, int cin, int co
                          const float* scale, const float* shift, int act, vm_tensor* y, vm_tensor* ypool,
                          void* stream);
 
+/* Two chained convs whose 64-channel intermediate never leaves the chip: y = act2(conv3x3(relu(conv3x3(x, w1) + bias1),
+ * w2) + bias2 ...), optionally with the fused 2x2 SAME max-pool of y into ypool (NULL = none) — replaces
+ * unet.py:170-172 (conv1_1 -> conv1_2 -> pool1; conv_layer at :65-74) and the VGG towers' first pair
+ * (unet_simple.py:60-62).  x: [n,h,w,cin1 <= 8] bf16 view whose 8-element pixel row from coff is readable (the
+ * channels >= cin1 meet zero weights); packed1 = vm_conv3x3_pack_weights(cin1, 64), packed2 = (64, cout2).
+ * bf16 only: other dtypes return VM_EUNSUPPORTED and the caller runs the two convs separately. */
+int vm_conv3x3_pair_first_nhwc(const vm_tensor* x, const void* packed1, int cin1, const float* bias1,
+                               const void* packed2, int cout2, const float* bias2, const float* scale2,
+                               const float* shift2, int act2, vm_tensor* y, vm_tensor* ypool, void* stream);
+
 /* tf.image.resize_images(x, [2h, 2w]) (TF-1 legacy bilinear, exact 2x) followed by the 3x3 SAME conv, without
  * materialising the resized tensor — unet.py:44-63 (upconv_concat: resize_images at :58, conv2d at :60) for the
  * levels whose skip tensor is exactly twice the input's size.  Bilinear 2x is linear, so every output pixel

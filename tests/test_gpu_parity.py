@@ -198,6 +198,33 @@ def test_conv_fused_maxpool_matches_separate(shape, kernel):
     assert float(cat[..., :cout].abs().max()) == 0.0
 
 
+@pytest.mark.parametrize("shape", [(1, 16, 64, 64), (2, 17, 45, 64), (1, 1, 1, 64), (1, 135, 240, 64), (1, 9, 33, 128),
+                                   (1, 40, 70, 64)])
+@pytest.mark.parametrize("pool", [False, True])
+def test_conv_pair_first_bit_exact(shape, pool):
+    """vm_conv3x3_pair_first_nhwc (conv1_1 evaluated into LDS, then conv1_2 [+ pool1]) equals the two separate
+    kernels bit for bit: same bf16 rounding of the 64-channel intermediate, same accumulation order."""
+    from vmatting import _lib, ops
+    n, h, w, cout2 = shape
+    rs = np.random.RandomState(h * w + cout2)
+    x8 = torch.zeros((n, h, w, 8), dtype=torch.bfloat16, device=DEV)
+    x8[..., :7] = torch.from_numpy((rs.normal(size=(n, h, w, 7)) * 50).astype(np.float32)).to(torch.bfloat16).to(DEV)
+    w1 = (rs.normal(size=(3, 3, 7, 64)) * np.sqrt(2.0 / 63)).astype(np.float32)
+    w2 = (rs.normal(size=(3, 3, 64, cout2)) * np.sqrt(2.0 / 576)).astype(np.float32)
+    pc1 = ops.PackedConv(w1, (rs.normal(size=64) * 0.1).astype(np.float32), torch.bfloat16, DEV)
+    pc2 = ops.PackedConv(w2, (rs.normal(size=cout2) * 0.1).astype(np.float32), torch.bfloat16, DEV)
+    cat = torch.full((n, h, w, 2 * cout2), 7.0, dtype=torch.bfloat16, device=DEV)
+    pooled = torch.zeros((n, (h + 1) // 2, (w + 1) // 2, cout2), dtype=torch.bfloat16, device=DEV) if pool else None
+    ops.conv_pair_first(x8[..., :7], pc1, pc2, "relu", out=cat[..., cout2:], pool_out=pooled)
+    assert _lib.last_conv_kernel().endswith("true>"), _lib.last_conv_kernel()
+    m = ops.conv3x3(x8[..., :7], pc1, "relu")
+    y = ops.conv3x3(m, pc2, "relu")
+    assert torch.equal(cat[..., cout2:], y)
+    assert bool(torch.all(cat[..., :cout2] == 7.0))
+    if pool:
+        assert torch.equal(pooled, ops.maxpool2x2(y))
+
+
 UP_CASES = [(1, 9, 13, 128, 64), (2, 7, 33, 256, 128), (1, 1, 1, 64, 64), (1, 3, 2, 32, 64), (1, 34, 60, 512, 256),
             (1, 17, 30, 64, 192), (1, 68, 120, 128, 64)]
 
@@ -376,6 +403,33 @@ def test_unet_bf16_close_to_reference(vgg0):
     lerr = relerr(H(m.conv1_3), g["logits"])
     print("bf16 UNetVideo 70x90 unit: alpha max-abs err %.3e, logits rel err %.3e" % (err, lerr))
     assert err < 2e-2 and lerr < 5e-2
+
+
+def test_unet_bf16_fused_and_unfused_forward_agree(vgg0):
+    """bf16 forward: fusing conv1_1->conv1_2 changes nothing (bit for bit, the lazily evaluated .conv1_1 included);
+    folding the upconv resizes stays in the bf16 error class of the resize + conv path (logits; alpha of saturated
+    He-init logits is not a useful measure here — test_unet_bf16_close_to_reference checks alpha on unit weights)."""
+    from vmatting import unet
+    rs = np.random.RandomState(11)
+    x = np.concatenate([rs.uniform(-120, 130, (1, 66, 130, 6)), rs.choice([-0.5, 0.0, 0.5], (1, 66, 130, 1))], -1)
+    xt = torch.from_numpy(x.astype(np.float32)).to(DEV)
+    np.random.seed(1)
+    m = unet.UNetVideo(vgg0, dtype="bf16")
+    m.build(x.astype(np.float32))
+
+    def variant(fuse, fold):
+        v = unet.UNetVideo(vgg0, dtype="bf16").load_params(m.params)
+        v.fuse_first, v.fold_upconv = fuse, fold
+        v.prepare()
+        v.forward(xt)
+        return v
+
+    m2 = variant(False, m.fold_upconv)
+    assert torch.equal(m.conv1_1, m2.conv1_1)
+    assert torch.equal(m.conv1_2, m2.conv1_2) and torch.equal(m.pool1, m2.pool1)
+    assert torch.equal(m.output, m2.output)
+    m3 = variant(True, ())
+    assert relerr(H(m.conv1_3), H(m3.conv1_3)) < 2e-2, relerr(H(m.conv1_3), H(m3.conv1_3))
 
 
 @pytest.mark.parametrize("case", ["unet_simple_256_infer", "unet_simple_64_train"])

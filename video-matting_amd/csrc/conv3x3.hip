@@ -45,6 +45,8 @@ struct ConvArgs {
   void* py;  // optional fused 2x2/2 SAME max-pool output (patch kernel only), bf16 view
   int py_cstride, py_coff;
   int up, up_cout;  // folded 2x resize (patch kernel only): cout = 4 phases x up_cout, y is [N,2H,2W,up_cout]
+  const void* w1;   // FIRST patch kernel: packed cin<=8 -> 64 first conv (tap-major, K_pad 128) and its bias
+  const float* bias1;
 };
 
 // (K element index k) -> (tap, channel); tap 9 = padding (contributes zero)
@@ -730,12 +732,82 @@ struct PatchCfg {
   static constexpr int EPI = BM * SR;
   static constexpr int MAIN = 2 * PB + S * WSLOT;
   static constexpr int LDS = MAIN > EPI ? MAIN : EPI;
+  static constexpr int IW = TW + 4, IPIX = (TH + 4) * IW;   // FIRST: 8-channel input patch (16 B per pixel)
+  static constexpr int LDS_FIRST = MAIN + IPIX * 16 > EPI ? MAIN + IPIX * 16 : EPI;
   static_assert(TPN % 64 == 0, "whole 64-channel epilogue slabs per wave column");
   static_assert(TPM % 32 == 0 || TPM == 16, "pixel fragments stay inside one patch row");
   static_assert(S >= 3 && S <= 9, "ring depth (the X group is counted in at most one window)");
 };
 
-template <int BN, int WM, int WN, int S, int TH, int MINB, int UNR, bool PF, int ABL>
+// First conv (cin <= 8 -> 64 channels, + bias + relu) of the patch pixels, for the FIRST patch kernel.  The 8-channel
+// input patch (TH+4) x (TW+4) is staged at ip; 16-pixel fragments of the (TH+2) x (TW+2) patch are spread over the
+// waves; a 32-deep K-step covers 4 taps x 8 channels (tap-major packing k = tap*8 + c, like conv3x3_first).
+template <class C>
+__device__ __forceinline__ void first_layer_patch(const ConvArgs& a, char* smem, int pb, char* ip, int n, int r0, int c0,
+                                                  int wave, int lane, int tid) {
+  using T = uint16_t;
+  const int H = a.H, W = a.W;
+  const T* x8 = reinterpret_cast<const T*>(a.x) + a.x_coff;
+  for (int i = tid; i < C::IPIX; i += C::NT) {
+    const int ir = i / C::IW, ic = i - ir * C::IW;
+    const int h = r0 - 2 + ir, w = c0 - 2 + ic;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if ((unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W)
+      v = *reinterpret_cast<const uint4*>(x8 + (((long)n * H + h) * W + w) * (long)a.x_cstride);
+    *reinterpret_cast<uint4*>(ip + i * 16) = v;
+  }
+  const int col = lane & 15, q = lane >> 4;
+  const T* w1 = reinterpret_cast<const T*>(a.w1);
+  uint4 wf[3][4];
+#pragma unroll
+  for (int j = 0; j < 3; ++j)
+#pragma unroll
+    for (int fc = 0; fc < 4; ++fc) wf[j][fc] = *reinterpret_cast<const uint4*>(w1 + (fc * 16 + col) * 128 + j * 32 + q * 8);
+  float b1[4][4];
+#pragma unroll
+  for (int fc = 0; fc < 4; ++fc)
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) b1[fc][jj] = a.bias1 ? a.bias1[fc * 16 + 4 * q + jj] : 0.f;
+  __syncthreads();
+  constexpr int NF = (C::PPIX + 15) / 16;
+  for (int f = wave; f < NF; f += C::NW) {
+    const int p = f * 16 + col;
+    const int pr = p / C::PW, pc = p - pr * C::PW;
+    f32x4 acc[4];
+#pragma unroll
+    for (int fc = 0; fc < 4; ++fc) acc[fc] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const int tap = 4 * j + q;
+      uint4 bv = make_uint4(0, 0, 0, 0);
+      if (tap < 9 && p < C::PPIX) bv = *reinterpret_cast<const uint4*>(ip + ((pr + tap / 3) * C::IW + pc + tap % 3) * 16);
+#pragma unroll
+      for (int fc = 0; fc < 4; ++fc) mma16<T>(wf[j][fc], bv, acc[fc]);
+    }
+    const int h = r0 - 1 + pr, w = c0 - 1 + pc;
+    const bool inside = (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
+    if (p < C::PPIX) {
+#pragma unroll
+      for (int fc = 0; fc < 4; ++fc) {
+        float v[4];
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) v[jj] = inside ? fmaxf(acc[fc][jj] + b1[fc][jj], 0.f) : 0.f;
+        uint2 pk;
+        pk.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+        pk.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+        // channel fc*16 + 4q: granule fc/2, 16-byte chunk (fc&1)*2 + q/2, half q&1
+        *reinterpret_cast<uint2*>(smem + (fc >> 1) * pb + swz<64>(p, (fc & 1) * 2 + (q >> 1)) + (q & 1) * 8) = pk;
+      }
+    }
+  }
+  __syncthreads();
+}
+
+// FIRST: the conv's 64-channel input is itself conv3x3(x8) + bias + relu of an 8-channel frame (unet.py:170-171,
+// conv1_1 -> conv1_2): the prologue evaluates that first conv on the (TH+2) x (TW+2) patch straight into the two
+// granule buffers (zero outside the frame = the second conv's SAME padding), so the 64-channel activation never
+// touches HBM; the main loop then streams only weights.
+template <int BN, int WM, int WN, int S, int TH, int MINB, int UNR, bool PF, int ABL, bool FIRST>
 __global__ __launch_bounds__(64 * WM * WN) __attribute__((amdgpu_waves_per_eu(MINB * WM * WN / 4)))
 void conv3x3_patch(ConvArgs a) {
   using C = PatchCfg<BN, WM, WN, S, TH>;
@@ -764,7 +836,7 @@ void conv3x3_patch(ConvArgs a) {
   int xoff[XPW];
   int x_n = 0;
 #pragma unroll
-  for (int i = 0; i < XPW; ++i) {
+  for (int i = 0; i < XPW && !FIRST; ++i) {
     const int piece = wave + i * NW;
     const int row = piece * 16 + lrow;
     const int lq = (swz<64>(row, lpos) - row * 64) >> 4;
@@ -793,6 +865,7 @@ void conv3x3_patch(ConvArgs a) {
   const uint32_t wring = lds0 + 2 * C::PB;
 
   auto issue_x = [&](int cc, int buf) {
+    if constexpr (FIRST) return;
     const bool real = cc < nch;
 #pragma unroll
     for (int i = 0; i < XPW; ++i)
@@ -874,6 +947,7 @@ void conv3x3_patch(ConvArgs a) {
     issue_x(0, 0);
 #pragma unroll
     for (int j = 0; j < S - 1; ++j) issue_w(j, j);
+    if constexpr (FIRST) first_layer_patch<C>(a, smem, C::PB, smem + C::MAIN, n, r0, c0, wave, lane, tid);
     int slot = 0;
     for (int cc = 0; cc < nch; ++cc) {
 #pragma unroll UNR
@@ -1647,13 +1721,17 @@ static int launch_glds(ConvArgs& a, hipStream_t st) {
   return check_launch("conv3x3_glds");
 }
 
-template <int BN, int WM, int WN, int S, int TH = 8, int MINB = 1, int UNR = 9, bool PF = false, int ABL = 0>
+template <int BN, int WM, int WN, int S, int TH = 8, int MINB = 1, int UNR = 9, bool PF = false, int ABL = 0,
+          bool FIRST = false>
 static int launch_patch(ConvArgs& a, hipStream_t st) {
   using C = PatchCfg<BN, WM, WN, S, TH>;
+  static_assert(!(FIRST && PF), "FIRST uses the plain pipeline");
+  constexpr int lds = FIRST ? C::LDS_FIRST : C::LDS;
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3_patch<BN, WM, WN, S, TH, MINB, UNR, PF, ABL>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
+    hipError_t e = hipFuncSetAttribute(
+        reinterpret_cast<const void*>(&conv3x3_patch<BN, WM, WN, S, TH, MINB, UNR, PF, ABL, FIRST>),
+        hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (e != hipSuccess) return fail(VM_EHIP, "hipFuncSetAttribute(patch): %s", hipGetErrorString(e));
     attr_set = true;
   }
@@ -1662,9 +1740,10 @@ static int launch_patch(ConvArgs& a, hipStream_t st) {
   a.tiles_n = (a.cout + BN - 1) / BN;
   if (sp * a.tiles_n > 0x7fffffffL) return fail(VM_EUNSUPPORTED, "conv3x3: too many tiles");
   a.tiles_total = (int)(sp * a.tiles_n);
-  snprintf(g_last_kernel, sizeof g_last_kernel, "vm::conv3x3_patch<%d, %d, %d, %d, %d, %d, %d, %s, %d>", BN, WM, WN, S,
-           TH, MINB, UNR, PF ? "true" : "false", ABL);
-  hipLaunchKernelGGL((conv3x3_patch<BN, WM, WN, S, TH, MINB, UNR, PF, ABL>), dim3(a.tiles_total), dim3(C::NT), C::LDS, st, a);
+  snprintf(g_last_kernel, sizeof g_last_kernel, "vm::conv3x3_patch<%d, %d, %d, %d, %d, %d, %d, %s, %d, %s>", BN, WM, WN,
+           S, TH, MINB, UNR, PF ? "true" : "false", ABL, FIRST ? "true" : "false");
+  hipLaunchKernelGGL((conv3x3_patch<BN, WM, WN, S, TH, MINB, UNR, PF, ABL, FIRST>), dim3(a.tiles_total), dim3(C::NT), lds,
+                     st, a);
   return check_launch("conv3x3_patch");
 }
 
@@ -1886,6 +1965,41 @@ extern "C" int vm_conv3x3_up2x_nhwc(const vm_tensor* x, const void* packed_up, c
   if (nblk > 0x7fffffffL) return fail(VM_EUNSUPPORTED, "conv3x3_up2x: too many border pixels");
   hipLaunchKernelGGL(conv3x3_up2x_border, dim3((unsigned)nblk, cout / 64), dim3(256), 0, st, b);
   return check_launch("conv3x3_up2x_border");
+}
+
+extern "C" int vm_conv3x3_pair_first_nhwc(const vm_tensor* x, const void* packed1, int cin1, const float* bias1,
+                                          const void* packed2, int cout2, const float* bias2, const float* scale2,
+                                          const float* shift2, int act2, vm_tensor* y, vm_tensor* ypool, void* stream) {
+  if (!valid_tensor(x) || !valid_tensor(y) || !packed1 || !packed2)
+    return fail(VM_EINVAL, "conv3x3_pair_first: invalid tensor/weights");
+  if (cin1 <= 0 || cin1 > 8 || x->c != cin1 || cout2 <= 0 || y->c != cout2)
+    return fail(VM_EINVAL, "conv3x3_pair_first: x.c=%d cin1=%d (<= 8) y.c=%d cout2=%d", x->c, cin1, y->c, cout2);
+  if (x->n != y->n || x->h != y->h || x->w != y->w) return fail(VM_EINVAL, "conv3x3_pair_first: spatial mismatch");
+  if (act2 < VM_ACT_NONE || act2 > VM_ACT_SOFTMAX) return fail(VM_EINVAL, "conv3x3_pair_first: act %d", act2);
+  if (ypool && (!valid_tensor(ypool) || ypool->n != y->n || ypool->h != (y->h + 1) / 2 || ypool->w != (y->w + 1) / 2 ||
+                ypool->c != cout2 || ypool->dtype != y->dtype))
+    return fail(VM_EINVAL, "conv3x3_pair_first: pool output must be [n, ceil(h/2), ceil(w/2), cout2]");
+  const bool xvec = reinterpret_cast<uintptr_t>(x->ptr) % 16 == 0 && x->cstride % 8 == 0 && x->coff % 8 == 0 &&
+                    x->coff + 8 <= x->cstride;
+  const bool yvec = reinterpret_cast<uintptr_t>(y->ptr) % 16 == 0 && y->cstride % 8 == 0 && y->coff % 8 == 0;
+  const bool pvec = !ypool || (reinterpret_cast<uintptr_t>(ypool->ptr) % 16 == 0 && ypool->cstride % 8 == 0 &&
+                               ypool->coff % 8 == 0);
+  if (x->dtype != VM_BF16 || y->dtype != VM_BF16 || !xvec || !yvec || !pvec || cout2 % 8 || act2 == VM_ACT_SOFTMAX ||
+      g_conv_kernel == 1 || g_conv_kernel == 2)
+    return fail(VM_EUNSUPPORTED, "conv3x3_pair_first: needs bf16 16-byte channel views (x: 8-channel pixels)");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  ConvArgs a{};
+  a.x = x->ptr; a.x_cstride = x->cstride; a.x_coff = x->coff; a.H = x->h; a.W = x->w;
+  a.M = (long)x->n * x->h * x->w;
+  fill_geom(a, geom(64, cout2, VM_BF16));
+  a.w = packed2; a.cout = cout2;
+  a.bias = bias2; a.scale = scale2; a.shift = shift2; a.act = act2;
+  a.y = y->ptr; a.y_cstride = y->cstride; a.y_coff = y->coff; a.y_dtype = y->dtype; a.y_vec = 1;
+  a.w1 = packed1; a.bias1 = bias1;
+  if (ypool) { a.py = ypool->ptr; a.py_cstride = ypool->cstride; a.py_coff = ypool->coff; }
+  const long sp = (long)x->n * ((x->h + 7) / 8) * ((x->w + 31) / 32);
+  if (sp * ((cout2 + 63) / 64) < 512) return launch_patch<64, 4, 1, 6, 4, 1, 9, false, 0, true>(a, st);
+  return launch_patch<64, 8, 1, 6, 8, 1, 9, false, 0, true>(a, st);
 }
 
 static int conv_impl(const vm_tensor* x, const void* packed, int cin, int cout, const float* bias, const float* scale,

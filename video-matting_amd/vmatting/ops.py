@@ -150,6 +150,36 @@ def conv3x3(x, pc, act="none", out=None, out_dtype=None, affine=None, pool_out=N
     return out
 
 
+def conv_pair_first(x, pc1, pc2, act2="relu", out=None, pool_out=None, mid=None):
+    """conv3x3(relu(conv3x3(x, pc1)), pc2) (+ 2x2 SAME max-pool into pool_out): unet.py:170-172, conv1_1 -> conv1_2
+    (-> pool1).  bf16 runs ONE kernel whose 64-channel intermediate stays in LDS (vm_conv3x3_pair_first_nhwc); any
+    other case runs the two convs through ``mid`` (the intermediate, allocated when None)."""
+    n, h, w, _ = x.shape
+    if out is None:
+        out = torch.empty((n, h, w, pc2.cout), dtype=x.dtype, device=x.device)
+    if x.dtype == torch.bfloat16 and pc1.dtype == pc2.dtype == torch.bfloat16 and pc1.cout == 64 and pc2.cin == 64:
+        xv, yv = nhwc(x), nhwc(out)
+        pv = nhwc(pool_out) if pool_out is not None else None
+        prof = _CONV_PROFILE
+        if prof is not None:
+            ev0 = torch.cuda.Event(enable_timing=True)
+            ev1 = torch.cuda.Event(enable_timing=True)
+            ev0.record()
+        rc = lib().vm_conv3x3_pair_first_nhwc(ctypes.byref(xv), _ptr(pc1.packed), pc1.cin, _ptr(pc1.bias),
+                                              _ptr(pc2.packed), pc2.cout, _ptr(pc2.bias), _ptr(pc2.scale),
+                                              _ptr(pc2.shift), _lib.ACT[act2], ctypes.byref(yv),
+                                              ctypes.byref(pv) if pv is not None else None, stream_handle())
+        if rc != _lib.VM_EUNSUPPORTED:
+            check(rc, "conv3x3_pair_first")
+            if prof is not None:
+                ev1.record()
+                prof.append((2 * n * h * w * 9 * (pc1.cin * pc1.cout + pc2.cin * pc2.cout), _lib.last_conv_kernel(),
+                             ev0, ev1))
+            return out
+    m = conv3x3(x, pc1, "relu", out=mid)
+    return conv3x3(m, pc2, act2, out=out, pool_out=pool_out)
+
+
 def upconv3x3(x, pc, act="none", out=None, size=None, rbuf=None, fold=True):
     """tf.image.resize_images(x, size) -> conv3x3 (unet.py:44-63, the upconv half of upconv_concat).
 

@@ -44,6 +44,8 @@ class UNet:
 
     IN_CH = None
     # upconvs whose exact-2x resize is folded into the conv (ops.upconv3x3; bf16 only, others resize + conv)
+    # conv1_1 -> conv1_2 as one kernel (ops.conv_pair_first; bf16 only, others run them separately)
+    fuse_first = True
     fold_upconv = ("upconv_3", "upconv_4")  # upconv_2 folded would run on the 135x240 grid: slower (measured)
 
     def __init__(self, vgg16_npy_path=None, dtype="bf16", device="cuda"):
@@ -54,6 +56,8 @@ class UNet:
         self.convs = None        # name -> ops.PackedConv
         self._ws = None
         self._ws_key = None
+        self._c11 = None
+        self._xin = None
 
     # ------------------------------------------------------------------ weights
     def get_conv_filter(self, name):
@@ -146,8 +150,14 @@ class UNet:
         C = self.convs
         ops.convert(x, b["in8"])
         xin = b["in8"][..., :c]
-        ops.conv3x3(xin, C["conv1_1"], "relu", out=b["c11"])
-        ops.conv3x3(b["c11"], C["conv1_2"], "relu", out=b["cat1"][..., 64:], pool_out=b["p1"])
+        if self.fuse_first:  # conv1_1 stays on chip; .conv1_1 is evaluated on first access
+            ops.conv_pair_first(xin, C["conv1_1"], C["conv1_2"], "relu", out=b["cat1"][..., 64:], pool_out=b["p1"],
+                                mid=b["c11"])
+            self._c11 = None
+        else:
+            self._c11 = ops.conv3x3(xin, C["conv1_1"], "relu", out=b["c11"])
+            ops.conv3x3(b["c11"], C["conv1_2"], "relu", out=b["cat1"][..., 64:], pool_out=b["p1"])
+        self._xin = xin
         ops.conv3x3(b["p1"], C["conv2_1"], "relu", out=b["c21"])
         ops.conv3x3(b["c21"], C["conv2_2"], "relu", out=b["cat2"][..., 128:], pool_out=b["p2"])
         ops.conv3x3(b["p2"], C["conv3_1"], "relu", out=b["c31"])
@@ -173,8 +183,14 @@ class UNet:
         self._publish(b)
         return self.output
 
+    @property
+    def conv1_1(self):
+        """unet.py:170 conv1_1 — with fuse_first the forward never writes it to HBM, so it is evaluated here."""
+        if self._c11 is None and self._ws is not None:
+            self._c11 = ops.conv3x3(self._xin, self.convs["conv1_1"], "relu", out=self._ws["c11"])
+        return self._c11
+
     def _publish(self, b):
-        self.conv1_1 = b["c11"]
         self.conv1_2 = b["cat1"][..., 64:]
         self.pool1 = b["p1"]
         self.conv2_1 = b["c21"]
