@@ -100,12 +100,20 @@ int vm_conv3x3_pool_nhwc(const vm_tensor* x, const void* packed, int cin, int co
                          const float* scale, const float* shift, int act, vm_tensor* y, vm_tensor* ypool,
                          void* stream);
 
+/* cout == 1 head conv, y = act(conv(x, w) + bias ...), and optionally alpha = sigmoid of the pre-activation value
+ * (f32, contiguous [n*h*w]) from the same pass — unet.py:203-205 (conv1_5 = self.conv1_3 logits, then
+ * tf.nn.sigmoid -> self.output; unet_simple.py:142, small.py:49-50).  alpha may be NULL. */
+int vm_conv3x3_head_nhwc(const vm_tensor* x, const void* packed, int cin, const float* bias, const float* scale,
+                         const float* shift, int act, vm_tensor* y, float* alpha, void* stream);
+
 /* Two chained convs whose 64-channel intermediate never leaves the chip: y = act2(conv3x3(relu(conv3x3(x, w1) + bias1),
  * w2) + bias2 ...), optionally with the fused 2x2 SAME max-pool of y into ypool (NULL = none) — replaces
  * unet.py:170-172 (conv1_1 -> conv1_2 -> pool1; conv_layer at :65-74) and the VGG towers' first pair
- * (unet_simple.py:60-62).  x: [n,h,w,cin1 <= 8] bf16 view whose 8-element pixel row from coff is readable (the
- * channels >= cin1 meet zero weights); packed1 = vm_conv3x3_pack_weights(cin1, 64), packed2 = (64, cout2).
- * bf16 only: other dtypes return VM_EUNSUPPORTED and the caller runs the two convs separately. */
+ * (unet_simple.py:60-62).  x: [n,h,w,cin1 <= 8], either a bf16 view whose 8-element pixel row from coff is
+ * readable (the channels >= cin1 meet zero weights) or the caller's f32 frame itself (any channel stride; rounded
+ * to bf16 on load, which replaces the vm_convert_nhwc pass); packed1 = vm_conv3x3_pack_weights(cin1, 64, bf16),
+ * packed2 = (64, cout2, bf16).  bf16 compute only: an f32 y returns VM_EUNSUPPORTED and the caller runs the two
+ * convs separately. */
 int vm_conv3x3_pair_first_nhwc(const vm_tensor* x, const void* packed1, int cin1, const float* bias1,
                                const void* packed2, int cout2, const float* bias2, const float* scale2,
                                const float* shift2, int act2, vm_tensor* y, vm_tensor* ypool, void* stream);

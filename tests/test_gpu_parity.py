@@ -201,21 +201,25 @@ def test_conv_fused_maxpool_matches_separate(shape, kernel):
 @pytest.mark.parametrize("shape", [(1, 16, 64, 64), (2, 17, 45, 64), (1, 1, 1, 64), (1, 135, 240, 64), (1, 9, 33, 128),
                                    (1, 40, 70, 64)])
 @pytest.mark.parametrize("pool", [False, True])
-def test_conv_pair_first_bit_exact(shape, pool):
+@pytest.mark.parametrize("xdtype", ["bf16", "fp32"])
+def test_conv_pair_first_bit_exact(shape, pool, xdtype):
     """vm_conv3x3_pair_first_nhwc (conv1_1 evaluated into LDS, then conv1_2 [+ pool1]) equals the two separate
-    kernels bit for bit: same bf16 rounding of the 64-channel intermediate, same accumulation order."""
+    kernels bit for bit: same bf16 rounding of the 64-channel intermediate, same accumulation order; an f32 frame is
+    rounded on load exactly like vm_convert_nhwc."""
     from vmatting import _lib, ops
     n, h, w, cout2 = shape
     rs = np.random.RandomState(h * w + cout2)
+    xf = torch.from_numpy((rs.normal(size=(n, h, w, 7)) * 50).astype(np.float32)).to(DEV)
     x8 = torch.zeros((n, h, w, 8), dtype=torch.bfloat16, device=DEV)
-    x8[..., :7] = torch.from_numpy((rs.normal(size=(n, h, w, 7)) * 50).astype(np.float32)).to(torch.bfloat16).to(DEV)
+    ops.convert(xf, x8)
     w1 = (rs.normal(size=(3, 3, 7, 64)) * np.sqrt(2.0 / 63)).astype(np.float32)
     w2 = (rs.normal(size=(3, 3, 64, cout2)) * np.sqrt(2.0 / 576)).astype(np.float32)
     pc1 = ops.PackedConv(w1, (rs.normal(size=64) * 0.1).astype(np.float32), torch.bfloat16, DEV)
     pc2 = ops.PackedConv(w2, (rs.normal(size=cout2) * 0.1).astype(np.float32), torch.bfloat16, DEV)
     cat = torch.full((n, h, w, 2 * cout2), 7.0, dtype=torch.bfloat16, device=DEV)
     pooled = torch.zeros((n, (h + 1) // 2, (w + 1) // 2, cout2), dtype=torch.bfloat16, device=DEV) if pool else None
-    ops.conv_pair_first(x8[..., :7], pc1, pc2, "relu", out=cat[..., cout2:], pool_out=pooled)
+    ops.conv_pair_first(x8[..., :7] if xdtype == "bf16" else xf, pc1, pc2, "relu", out=cat[..., cout2:],
+                        pool_out=pooled)
     assert _lib.last_conv_kernel().endswith("true>"), _lib.last_conv_kernel()
     m = ops.conv3x3(x8[..., :7], pc1, "relu")
     y = ops.conv3x3(m, pc2, "relu")
@@ -223,6 +227,30 @@ def test_conv_pair_first_bit_exact(shape, pool):
     assert bool(torch.all(cat[..., :cout2] == 7.0))
     if pool:
         assert torch.equal(pooled, ops.maxpool2x2(y))
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+@pytest.mark.parametrize("head_kernel", [0, 1, 2])
+def test_conv_head_alpha_output(dtype, head_kernel):
+    """vm_conv3x3_head_nhwc: the alpha output equals sigmoid of the stored logits exactly as the separate
+    vm_convert_nhwc(sigmoid) pass computes it; the logits are unchanged."""
+    from vmatting import _lib, ops
+    tdt = ops.TORCH_DTYPE[dtype]
+    rs = np.random.RandomState(9)
+    x = torch.from_numpy(rs.normal(size=(2, 19, 70, 128)).astype(np.float32)).to(tdt).to(DEV)
+    pc = ops.PackedConv((rs.normal(size=(3, 3, 128, 1)) * 0.05).astype(np.float32), np.array([0.3], np.float32), tdt)
+    _lib.set_option("head_kernel", head_kernel)
+    try:
+        logits = torch.empty((2, 19, 70, 1), dtype=torch.float32, device=DEV)
+        alpha = torch.empty((2, 19, 70, 1), dtype=torch.float32, device=DEV)
+        ops.conv_head(x, pc, "none", out=logits, alpha=alpha)
+        ref_logits = ops.conv3x3(x, pc, "none", out_dtype=torch.float32)
+    finally:
+        _lib.set_option("head_kernel", 0)
+    assert torch.equal(logits, ref_logits)
+    ref_alpha = torch.empty_like(alpha)
+    ops.convert(logits, ref_alpha, act="sigmoid")
+    assert torch.equal(alpha, ref_alpha)
 
 
 UP_CASES = [(1, 9, 13, 128, 64), (2, 7, 33, 256, 128), (1, 1, 1, 64, 64), (1, 3, 2, 32, 64), (1, 34, 60, 512, 256),

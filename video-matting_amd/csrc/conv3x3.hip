@@ -47,6 +47,7 @@ struct ConvArgs {
   int up, up_cout;  // folded 2x resize (patch kernel only): cout = 4 phases x up_cout, y is [N,2H,2W,up_cout]
   const void* w1;   // FIRST patch kernel: packed cin<=8 -> 64 first conv (tap-major, K_pad 128) and its bias
   const float* bias1;
+  int x_f32, x_c;   // FIRST: the frame is f32 with x_c channels (converted to bf16 in the prologue)
 };
 
 // (K element index k) -> (tap, channel); tap 9 = padding (contributes zero)
@@ -748,12 +749,23 @@ __device__ __forceinline__ void first_layer_patch(const ConvArgs& a, char* smem,
   using T = uint16_t;
   const int H = a.H, W = a.W;
   const T* x8 = reinterpret_cast<const T*>(a.x) + a.x_coff;
+  const float* xf = reinterpret_cast<const float*>(a.x) + a.x_coff;
   for (int i = tid; i < C::IPIX; i += C::NT) {
     const int ir = i / C::IW, ic = i - ir * C::IW;
     const int h = r0 - 2 + ir, w = c0 - 2 + ic;
     uint4 v = make_uint4(0, 0, 0, 0);
-    if ((unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W)
-      v = *reinterpret_cast<const uint4*>(x8 + (((long)n * H + h) * W + w) * (long)a.x_cstride);
+    if ((unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W) {
+      const long pix = (((long)n * H + h) * W + w) * (long)a.x_cstride;
+      if (a.x_f32) {  // the caller's f32 frame (loader.py:76-78 layout), rounded to bf16 like vm_convert_nhwc
+        // (measured: one pixel per lane beats a coalesced channel-pair sweep, whose extra LDS stores cost more)
+        float f[8];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) f[c] = c < a.x_c ? xf[pix + c] : 0.f;
+        v = Chunk<T>::pack(f);
+      } else {
+        v = *reinterpret_cast<const uint4*>(x8 + pix);
+      }
+    }
     *reinterpret_cast<uint4*>(ip + i * 16) = v;
   }
   const int col = lane & 15, q = lane >> 4;
@@ -1202,6 +1214,7 @@ struct HeadArgs {
   int act;
   void* y;
   int y_cstride, y_coff, y_dtype;
+  float* y2;  // optional: sigmoid of the pre-activation value, f32 [M] (unet.py:204-205 output beside conv1_3)
 };
 
 template <typename T>
@@ -1260,6 +1273,7 @@ __global__ __launch_bounds__(256) void conv3x3_head(HeadArgs a) {
     acc += __shfl_xor(acc, 1, 16);
     if (sub == 0) {
       float v = (acc + bias) * sc + sh;
+      if (a.y2) a.y2[p] = sigmoid_precise(v);
       if (a.act == VM_ACT_RELU) v = v > 0.f ? v : 0.f;
       else if (a.act == VM_ACT_SIGMOID) v = sigmoid_precise(v);
       else if (a.act == VM_ACT_SOFTMAX) v = 1.f;  // softmax over a single channel
@@ -1387,6 +1401,7 @@ __global__ __launch_bounds__(256) void conv3x3_head_strip(HeadArgs a) {
     }
     if (sub < P && w0 + sub < W) {
       float v = (mine + bias) * sc + sh;
+      if (a.y2) a.y2[row * W + w0 + sub] = sigmoid_precise(v);
       if (a.act == VM_ACT_RELU) v = v > 0.f ? v : 0.f;
       else if (a.act == VM_ACT_SIGMOID) v = sigmoid_precise(v);
       else if (a.act == VM_ACT_SOFTMAX) v = 1.f;
@@ -1489,6 +1504,7 @@ __global__ __launch_bounds__(256) void conv3x3_head_mfma(HeadArgs a) {
 #pragma unroll
     for (int t = 0; t < 9; ++t) sum += ys[((orow + t / 3) * IW + ocol + t % 3) * 9 + t];
     float v = (sum + bias) * sc + sh;
+    if (a.y2) a.y2[((long)n * H + h) * W + w] = sigmoid_precise(v);
     if (a.act == VM_ACT_RELU) v = v > 0.f ? v : 0.f;
     else if (a.act == VM_ACT_SIGMOID) v = sigmoid_precise(v);
     else if (a.act == VM_ACT_SOFTMAX) v = 1.f;
@@ -1900,7 +1916,8 @@ extern "C" int vm_conv3x3_pack_weights(const float* w_hwio, int cin, int cout, i
 }
 
 static int conv_impl(const vm_tensor* x, const void* packed, int cin, int cout, const float* bias, const float* scale,
-                     const float* shift, int act, vm_tensor* y, const vm_tensor* yp, void* stream);
+                     const float* shift, int act, vm_tensor* y, const vm_tensor* yp, void* stream,
+                     float* y2 = nullptr);
 
 extern "C" int vm_conv3x3_nhwc(const vm_tensor* x, const void* packed, int cin, int cout, const float* bias,
                                const float* scale, const float* shift, int act, vm_tensor* y, void* stream) {
@@ -1979,14 +1996,16 @@ extern "C" int vm_conv3x3_pair_first_nhwc(const vm_tensor* x, const void* packed
   if (ypool && (!valid_tensor(ypool) || ypool->n != y->n || ypool->h != (y->h + 1) / 2 || ypool->w != (y->w + 1) / 2 ||
                 ypool->c != cout2 || ypool->dtype != y->dtype))
     return fail(VM_EINVAL, "conv3x3_pair_first: pool output must be [n, ceil(h/2), ceil(w/2), cout2]");
-  const bool xvec = reinterpret_cast<uintptr_t>(x->ptr) % 16 == 0 && x->cstride % 8 == 0 && x->coff % 8 == 0 &&
-                    x->coff + 8 <= x->cstride;
+  const bool xf32 = x->dtype == VM_F32;
+  const bool xvec = xf32 || (reinterpret_cast<uintptr_t>(x->ptr) % 16 == 0 && x->cstride % 8 == 0 &&
+                             x->coff % 8 == 0 && x->coff + 8 <= x->cstride);
   const bool yvec = reinterpret_cast<uintptr_t>(y->ptr) % 16 == 0 && y->cstride % 8 == 0 && y->coff % 8 == 0;
   const bool pvec = !ypool || (reinterpret_cast<uintptr_t>(ypool->ptr) % 16 == 0 && ypool->cstride % 8 == 0 &&
                                ypool->coff % 8 == 0);
-  if (x->dtype != VM_BF16 || y->dtype != VM_BF16 || !xvec || !yvec || !pvec || cout2 % 8 || act2 == VM_ACT_SOFTMAX ||
-      g_conv_kernel == 1 || g_conv_kernel == 2)
-    return fail(VM_EUNSUPPORTED, "conv3x3_pair_first: needs bf16 16-byte channel views (x: 8-channel pixels)");
+  if (y->dtype != VM_BF16 || !xvec || !yvec || !pvec || cout2 % 8 || act2 == VM_ACT_SOFTMAX || g_conv_kernel == 1 ||
+      g_conv_kernel == 2)
+    return fail(VM_EUNSUPPORTED, "conv3x3_pair_first: needs a bf16 output and 16-byte channel views (bf16 x: "
+                                 "8-channel pixels)");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   ConvArgs a{};
   a.x = x->ptr; a.x_cstride = x->cstride; a.x_coff = x->coff; a.H = x->h; a.W = x->w;
@@ -1995,15 +2014,21 @@ extern "C" int vm_conv3x3_pair_first_nhwc(const vm_tensor* x, const void* packed
   a.w = packed2; a.cout = cout2;
   a.bias = bias2; a.scale = scale2; a.shift = shift2; a.act = act2;
   a.y = y->ptr; a.y_cstride = y->cstride; a.y_coff = y->coff; a.y_dtype = y->dtype; a.y_vec = 1;
-  a.w1 = packed1; a.bias1 = bias1;
+  a.w1 = packed1; a.bias1 = bias1; a.x_f32 = xf32; a.x_c = cin1;
   if (ypool) { a.py = ypool->ptr; a.py_cstride = ypool->cstride; a.py_coff = ypool->coff; }
   const long sp = (long)x->n * ((x->h + 7) / 8) * ((x->w + 31) / 32);
   if (sp * ((cout2 + 63) / 64) < 512) return launch_patch<64, 4, 1, 6, 4, 1, 9, false, 0, true>(a, st);
   return launch_patch<64, 8, 1, 6, 8, 1, 9, false, 0, true>(a, st);
 }
 
+extern "C" int vm_conv3x3_head_nhwc(const vm_tensor* x, const void* packed, int cin, const float* bias,
+                                    const float* scale, const float* shift, int act, vm_tensor* y, float* alpha,
+                                    void* stream) {
+  return conv_impl(x, packed, cin, 1, bias, scale, shift, act, y, nullptr, stream, alpha);
+}
+
 static int conv_impl(const vm_tensor* x, const void* packed, int cin, int cout, const float* bias, const float* scale,
-                     const float* shift, int act, vm_tensor* y, const vm_tensor* yp, void* stream) {
+                     const float* shift, int act, vm_tensor* y, const vm_tensor* yp, void* stream, float* y2) {
   if (!valid_tensor(x) || !valid_tensor(y) || !packed) return fail(VM_EINVAL, "conv3x3: invalid tensor/weights");
   if (cin <= 0 || cout <= 0 || x->c != cin || y->c != cout)
     return fail(VM_EINVAL, "conv3x3: channel mismatch x.c=%d cin=%d y.c=%d cout=%d", x->c, cin, y->c, cout);
@@ -2027,7 +2052,7 @@ static int conv_impl(const vm_tensor* x, const void* packed, int cin, int cout, 
     h.x = x->ptr; h.x_cstride = x->cstride; h.x_coff = x->coff; h.H = x->h; h.W = x->w; h.M = M;
     h.cin_pad = g.cin_pad; h.K9 = g.K9; h.K_pad = g.K_pad; h.chunk_major = g.chunk_major; h.ng = g.ng;
     h.w = packed; h.bias = bias; h.scale = scale; h.shift = shift; h.act = act;
-    h.y = y->ptr; h.y_cstride = y->cstride; h.y_coff = y->coff; h.y_dtype = y->dtype;
+    h.y = y->ptr; h.y_cstride = y->cstride; h.y_coff = y->coff; h.y_dtype = y->dtype; h.y2 = y2;
     const int nks = (g.cin_pad + 4 * ce - 1) / (4 * ce);
     if (g_head_kernel == 0 && nks <= 8) {
       constexpr int TH = 8, TW = 64;

@@ -150,6 +150,35 @@ def conv3x3(x, pc, act="none", out=None, out_dtype=None, affine=None, pool_out=N
     return out
 
 
+def conv_head(x, pc, act="none", out=None, alpha=None):
+    """cout == 1 conv (unet.py:203-204 conv1_5) into ``out``; with ``alpha`` (contiguous f32, one value per pixel)
+    also tf.nn.sigmoid of the pre-activation from the same pass (unet.py:205), saving a separate elementwise launch."""
+    if pc.cout != 1:
+        raise ValueError("conv_head needs a cout == 1 filter")
+    if x.dtype != pc.dtype:
+        raise TypeError("conv input dtype %s != packed weights dtype %s" % (x.dtype, pc.dtype))
+    n, h, w, _ = x.shape
+    if out is None:
+        out = torch.empty((n, h, w, 1), dtype=torch.float32, device=x.device)
+    if alpha is not None:
+        _require_gpu(alpha)
+        if alpha.dtype != torch.float32 or not alpha.is_contiguous() or alpha.numel() != n * h * w:
+            raise ValueError("alpha must be a contiguous f32 tensor of n*h*w elements")
+    xv, yv = nhwc(x), nhwc(out)
+    prof = _CONV_PROFILE
+    if prof is not None:
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev1 = torch.cuda.Event(enable_timing=True)
+        ev0.record()
+    check(lib().vm_conv3x3_head_nhwc(ctypes.byref(xv), _ptr(pc.packed), pc.cin, _ptr(pc.bias), _ptr(pc.scale),
+                                     _ptr(pc.shift), _lib.ACT[act], ctypes.byref(yv), _ptr(alpha), stream_handle()),
+          "conv3x3_head")
+    if prof is not None:
+        ev1.record()
+        prof.append((2 * n * h * w * 9 * pc.cin, _lib.last_conv_kernel(), ev0, ev1))
+    return out
+
+
 def conv_pair_first(x, pc1, pc2, act2="relu", out=None, pool_out=None, mid=None):
     """conv3x3(relu(conv3x3(x, pc1)), pc2) (+ 2x2 SAME max-pool into pool_out): unet.py:170-172, conv1_1 -> conv1_2
     (-> pool1).  bf16 runs ONE kernel whose 64-channel intermediate stays in LDS (vm_conv3x3_pair_first_nhwc); any
@@ -157,7 +186,8 @@ def conv_pair_first(x, pc1, pc2, act2="relu", out=None, pool_out=None, mid=None)
     n, h, w, _ = x.shape
     if out is None:
         out = torch.empty((n, h, w, pc2.cout), dtype=x.dtype, device=x.device)
-    if x.dtype == torch.bfloat16 and pc1.dtype == pc2.dtype == torch.bfloat16 and pc1.cout == 64 and pc2.cin == 64:
+    if x.dtype in (torch.bfloat16, torch.float32) and pc1.dtype == pc2.dtype == torch.bfloat16 and pc1.cout == 64 \
+            and pc2.cin == 64:
         xv, yv = nhwc(x), nhwc(out)
         pv = nhwc(pool_out) if pool_out is not None else None
         prof = _CONV_PROFILE
@@ -176,6 +206,10 @@ def conv_pair_first(x, pc1, pc2, act2="relu", out=None, pool_out=None, mid=None)
                 prof.append((2 * n * h * w * 9 * (pc1.cin * pc1.cout + pc2.cin * pc2.cout), _lib.last_conv_kernel(),
                              ev0, ev1))
             return out
+    if x.dtype != pc1.dtype:  # the unfused path takes the frame in the compute dtype, channels padded to 8
+        c = x.shape[-1]
+        xb = torch.empty((n, h, w, (c + 7) // 8 * 8), dtype=pc1.dtype, device=x.device)
+        x = convert(x, xb)[..., :c]
     m = conv3x3(x, pc1, "relu", out=mid)
     return conv3x3(m, pc2, act2, out=out, pool_out=pool_out)
 

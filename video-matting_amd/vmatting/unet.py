@@ -57,7 +57,8 @@ class UNet:
         self._ws = None
         self._ws_key = None
         self._c11 = None
-        self._xin = None
+        self._x = None
+        self._in8_valid = False
 
     # ------------------------------------------------------------------ weights
     def get_conv_filter(self, name):
@@ -148,16 +149,19 @@ class UNet:
         b = self._buffers(n, h, w)
         L = _levels(h, w)
         C = self.convs
-        ops.convert(x, b["in8"])
-        xin = b["in8"][..., :c]
-        if self.fuse_first:  # conv1_1 stays on chip; .conv1_1 is evaluated on first access
-            ops.conv_pair_first(xin, C["conv1_1"], C["conv1_2"], "relu", out=b["cat1"][..., 64:], pool_out=b["p1"],
-                                mid=b["c11"])
+        if self.fuse_first and self.dtype == torch.bfloat16:
+            # conv1_1 stays on chip and reads the f32 frame itself (bf16 rounding on load); .conv1_1 is evaluated
+            # on first access
+            ops.conv_pair_first(x, C["conv1_1"], C["conv1_2"], "relu", out=b["cat1"][..., 64:], pool_out=b["p1"])
             self._c11 = None
+            self._in8_valid = False
         else:
+            ops.convert(x, b["in8"])
+            xin = b["in8"][..., :c]
+            self._in8_valid = True
             self._c11 = ops.conv3x3(xin, C["conv1_1"], "relu", out=b["c11"])
             ops.conv3x3(b["c11"], C["conv1_2"], "relu", out=b["cat1"][..., 64:], pool_out=b["p1"])
-        self._xin = xin
+        self._x = x
         ops.conv3x3(b["p1"], C["conv2_1"], "relu", out=b["c21"])
         ops.conv3x3(b["c21"], C["conv2_2"], "relu", out=b["cat2"][..., 128:], pool_out=b["p2"])
         ops.conv3x3(b["p2"], C["conv3_1"], "relu", out=b["c31"])
@@ -178,8 +182,7 @@ class UNet:
         up(b["c34"], "upconv_3", 1, b["cat2"][..., :128], "r3")
         ops.conv3x3(b["cat2"], C["conv2_3"], "relu", out=b["c23"])
         up(b["c23"], "upconv_4", 0, b["cat1"][..., :64], "r4")
-        ops.conv3x3(b["cat1"], C["conv1_5"], "none", out=b["logits"])
-        ops.convert(b["logits"], b["out"], act="sigmoid")
+        ops.conv_head(b["cat1"], C["conv1_5"], "none", out=b["logits"], alpha=b["out"])  # conv1_5 + sigmoid
         self._publish(b)
         return self.output
 
@@ -187,7 +190,11 @@ class UNet:
     def conv1_1(self):
         """unet.py:170 conv1_1 — with fuse_first the forward never writes it to HBM, so it is evaluated here."""
         if self._c11 is None and self._ws is not None:
-            self._c11 = ops.conv3x3(self._xin, self.convs["conv1_1"], "relu", out=self._ws["c11"])
+            if not self._in8_valid:
+                ops.convert(self._x, self._ws["in8"])
+                self._in8_valid = True
+            xin = self._ws["in8"][..., :self.IN_CH]
+            self._c11 = ops.conv3x3(xin, self.convs["conv1_1"], "relu", out=self._ws["c11"])
         return self._c11
 
     def _publish(self, b):
