@@ -202,7 +202,8 @@ def test_conv_fused_maxpool_matches_separate(shape, kernel):
                                    (1, 40, 70, 64)])
 @pytest.mark.parametrize("pool", [False, True])
 @pytest.mark.parametrize("xdtype", ["bf16", "fp32"])
-def test_conv_pair_first_bit_exact(shape, pool, xdtype):
+@pytest.mark.parametrize("pair_kernel", [0, 1])
+def test_conv_pair_first_bit_exact(shape, pool, xdtype, pair_kernel):
     """vm_conv3x3_pair_first_nhwc (conv1_1 evaluated into LDS, then conv1_2 [+ pool1]) equals the two separate
     kernels bit for bit: same bf16 rounding of the 64-channel intermediate, same accumulation order; an f32 frame is
     rounded on load exactly like vm_convert_nhwc."""
@@ -218,9 +219,15 @@ def test_conv_pair_first_bit_exact(shape, pool, xdtype):
     pc2 = ops.PackedConv(w2, (rs.normal(size=cout2) * 0.1).astype(np.float32), torch.bfloat16, DEV)
     cat = torch.full((n, h, w, 2 * cout2), 7.0, dtype=torch.bfloat16, device=DEV)
     pooled = torch.zeros((n, (h + 1) // 2, (w + 1) // 2, cout2), dtype=torch.bfloat16, device=DEV) if pool else None
-    ops.conv_pair_first(x8[..., :7] if xdtype == "bf16" else xf, pc1, pc2, "relu", out=cat[..., cout2:],
-                        pool_out=pooled)
-    assert _lib.last_conv_kernel().endswith("true>"), _lib.last_conv_kernel()
+    _lib.set_option("pair_kernel", pair_kernel)
+    try:
+        ops.conv_pair_first(x8[..., :7] if xdtype == "bf16" else xf, pc1, pc2, "relu", out=cat[..., cout2:],
+                            pool_out=pooled)
+        name = _lib.last_conv_kernel()
+    finally:
+        _lib.set_option("pair_kernel", 0)
+    persist = pair_kernel == 0 and cout2 == 64
+    assert name == "vm::conv3x3_pair_persist" if persist else name.endswith("true>"), name
     m = ops.conv3x3(x8[..., :7], pc1, "relu")
     y = ops.conv3x3(m, pc2, "relu")
     assert torch.equal(cat[..., cout2:], y)

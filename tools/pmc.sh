@@ -23,7 +23,7 @@ i=0
 for p in "${PASSES[@]}"; do
   i=$((i+1))
   (cd /tmp && timeout -k 10 240 rocprofv3 --pmc $p --kernel-trace --output-format csv -d "$OUT/pass$i" -o run \
-      -- python3 "$REPO/tools/convbench.py" "$@" > "$OUT/pass$i.log" 2>&1)
+      -- python3 "$REPO/tools/${PMC_TOOL:-convbench.py}" "$@" > "$OUT/pass$i.log" 2>&1)
   rc=$?
   if [ $rc -ne 0 ]; then echo "[pmc $TAG pass$i] rc=$rc"; tail -5 "$OUT/pass$i.log"; exit $rc; fi
 done

@@ -1092,6 +1092,247 @@ void conv3x3_patch(ConvArgs a) {
   }
 }
 
+// ================================================================ persistent first pair (conv1_1 -> conv1_2 [-> pool1])
+// unet.py:170-172 at full resolution.  conv1_2 has only 2 channel granules (18 K-steps), so in the streaming patch
+// kernel the per-tile fixed costs (input latency, the first conv, the epilogue) dominate.  Here ONE 512-thread block
+// per CU keeps all of conv1_2's weights in LDS (18 K-step slots x 64 couts x 64 B = 72 KB, loaded once) and walks
+// the 8 x 32 tiles t = blockIdx.x, +gridDim.x, ...: the main loop has no barrier and no DMA, and the next tile's
+// input pixels are loaded into registers while the current tile's MFMAs run.
+struct PairCfg {
+  static constexpr int TH = 8, TW = 32, BM = TH * TW, PW = TW + 2, PPIX = (TH + 2) * PW;
+  static constexpr int IW = TW + 4, IPIX = (TH + 4) * IW;  // 8-channel input patch, origin (r0-2, c0-2)
+  static constexpr int NW = 8, NT = 512, NSTEP = 18;
+  static constexpr int PB = ((PPIX + 15) / 16) * 1024;     // one 32-channel granule of the patch (64-B rows)
+  static constexpr int WSLOT = 64 * 64;
+  static constexpr int PBU = PPIX * 64;                   // bytes of a granule buffer actually addressed
+  static constexpr int SR = 64 * 2 + 16;                   // epilogue staging row
+  static constexpr int P_OFF = NSTEP * WSLOT, I_OFF = P_OFF + 2 * PBU, S_OFF = I_OFF + IPIX * 16;
+  static constexpr int LDS = S_OFF + BM * SR;
+};
+static_assert(PairCfg::LDS <= 163840, "weights + patch + input + staging in one CU's LDS");
+static_assert(PairCfg::IPIX <= PairCfg::NT, "one input pixel per thread");
+
+__global__ __launch_bounds__(512) void conv3x3_pair_persist(ConvArgs a) {
+  using C = PairCfg;
+  using T = uint16_t;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int H = a.H, W = a.W;
+  const int th = (H + C::TH - 1) / C::TH, tw = (W + C::TW - 1) / C::TW;
+  const int ntiles = (int)(a.M / ((long)H * W)) * th * tw;
+  const int col = lane & 15, q = lane >> 4;
+
+  // conv1_2 weights: slot s = K-step s of the chunk-major packing (granule cc*9 + tap), swizzled 64-B rows
+  const T* wg = reinterpret_cast<const T*>(a.w);
+  for (int i = tid; i < C::NSTEP * 64 * 4; i += C::NT) {
+    const int st = i >> 8, row = (i >> 2) & 63, ch = i & 3;
+    *reinterpret_cast<uint4*>(smem + st * C::WSLOT + swz<64>(row, ch)) =
+        *reinterpret_cast<const uint4*>(wg + (long)row * a.K_pad + st * 32 + ch * 8);
+  }
+  // conv1_1 (tap-major, K_pad 128) weight fragments and bias stay in registers
+  const T* w1 = reinterpret_cast<const T*>(a.w1);
+  uint4 wf[3][4];
+#pragma unroll
+  for (int j = 0; j < 3; ++j)
+#pragma unroll
+    for (int fc = 0; fc < 4; ++fc) wf[j][fc] = *reinterpret_cast<const uint4*>(w1 + (fc * 16 + col) * 128 + j * 32 + q * 8);
+  float b1[4][4];
+#pragma unroll
+  for (int fc = 0; fc < 4; ++fc)
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) b1[fc][jj] = a.bias1 ? a.bias1[fc * 16 + 4 * q + jj] : 0.f;
+  float mul[4][4], add[4][4];
+#pragma unroll
+  for (int fc = 0; fc < 4; ++fc)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int co = min(fc * 16 + 4 * q + j, a.cout - 1);
+      const float sc = a.scale ? a.scale[co] : 1.f;
+      mul[fc][j] = sc;
+      add[fc][j] = (a.bias ? a.bias[co] : 0.f) * sc + (a.shift ? a.shift[co] : 0.f);
+    }
+
+  // input pixel of this thread (one per thread): raw registers while in flight, bf16 chunk in LDS
+  const T* x8 = reinterpret_cast<const T*>(a.x) + a.x_coff;
+  const float* xf = reinterpret_cast<const float*>(a.x) + a.x_coff;
+  uint4 xq = make_uint4(0, 0, 0, 0);
+  float xr[8];
+  bool xin = false;
+  auto load_in = [&](int t) {
+    const int n = t / (th * tw), rem = t - n * th * tw;
+    const int ir = tid / C::IW, ic = tid - ir * C::IW;
+    const int h = (rem / tw) * C::TH - 2 + ir, w = (rem % tw) * C::TW - 2 + ic;
+    xin = tid < C::IPIX && (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
+    if (xin) {
+      const long pix = (((long)n * H + h) * W + w) * (long)a.x_cstride;
+      if (a.x_f32) {
+#pragma unroll
+        for (int c = 0; c < 8; ++c) xr[c] = c < a.x_c ? xf[pix + c] : 0.f;
+      } else {
+        xq = *reinterpret_cast<const uint4*>(x8 + pix);
+      }
+    }
+  };
+  auto store_in = [&]() {
+    if (tid < C::IPIX)
+      *reinterpret_cast<uint4*>(smem + C::I_OFF + tid * 16) =
+          !xin ? make_uint4(0, 0, 0, 0) : a.x_f32 ? Chunk<T>::pack(xr) : xq;
+  };
+
+  int t = blockIdx.x;
+  if (t < ntiles) {
+    load_in(t);
+    store_in();
+  }
+  __syncthreads();
+  const int ycs2 = a.y_cstride * 2;
+  for (; t < ntiles; t += gridDim.x) {
+    const int n = t / (th * tw), rem = t - n * th * tw;
+    const int r0 = (rem / tw) * C::TH, c0 = (rem % tw) * C::TW;
+    // (1) conv1_1 + bias + relu of the (TH+2) x (TW+2) patch into both granule buffers (zero outside the frame)
+    for (int f = wave; f < (C::PPIX + 15) / 16; f += C::NW) {
+      const int p = f * 16 + col;
+      const int pr = p / C::PW, pc = p - pr * C::PW;
+      f32x4 acc1[4];
+#pragma unroll
+      for (int fc = 0; fc < 4; ++fc) acc1[fc] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        const int tap = 4 * j + q;
+        uint4 bv = make_uint4(0, 0, 0, 0);
+        if (tap < 9 && p < C::PPIX)
+          bv = *reinterpret_cast<const uint4*>(smem + C::I_OFF + ((pr + tap / 3) * C::IW + pc + tap % 3) * 16);
+#pragma unroll
+        for (int fc = 0; fc < 4; ++fc) mma16<T>(wf[j][fc], bv, acc1[fc]);
+      }
+      const int h = r0 - 1 + pr, w = c0 - 1 + pc;
+      const bool inside = (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
+      if (p < C::PPIX) {
+#pragma unroll
+        for (int fc = 0; fc < 4; ++fc) {
+          float v[4];
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) v[jj] = inside ? fmaxf(acc1[fc][jj] + b1[fc][jj], 0.f) : 0.f;
+          uint2 pk;
+          pk.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+          pk.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+          *reinterpret_cast<uint2*>(smem + C::P_OFF + (fc >> 1) * C::PBU + swz<64>(p, (fc & 1) * 2 + (q >> 1)) +
+                                    (q & 1) * 8) = pk;
+        }
+      }
+    }
+    __syncthreads();
+    // (2) next tile's input in flight during the main loop
+    const int tn = t + gridDim.x;
+    if (tn < ntiles) load_in(tn);
+    // (3) conv1_2: 2 granules x 9 taps, operands straight from LDS, no barrier
+    f32x4 acc[4][2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int k = 0; k < 2; ++k) acc[i][k] = f32x4{0.f, 0.f, 0.f, 0.f};
+    int abase[2];
+#pragma unroll
+    for (int fp = 0; fp < 2; ++fp) {
+      const int p = wave * 32 + fp * 16;
+      abase[fp] = (p / C::TW) * C::PW + (p % C::TW) + col;
+    }
+#pragma unroll
+    for (int cc = 0; cc < 2; ++cc)
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        const char* wp = smem + (cc * 9 + tap) * C::WSLOT;
+        const char* xp = smem + C::P_OFF + cc * C::PBU;
+        const int toff = (tap / 3) * C::PW + tap % 3;
+        uint4 av[4], bv[2];
+#pragma unroll
+        for (int fc = 0; fc < 4; ++fc) av[fc] = *reinterpret_cast<const uint4*>(wp + swz<64>(fc * 16 + col, q));
+#pragma unroll
+        for (int fp = 0; fp < 2; ++fp) bv[fp] = *reinterpret_cast<const uint4*>(xp + swz<64>(abase[fp] + toff, q));
+#pragma unroll
+        for (int fc = 0; fc < 4; ++fc)
+#pragma unroll
+          for (int fp = 0; fp < 2; ++fp) mma16<T>(av[fc], bv[fp], acc[fc][fp]);
+      }
+    if (tn < ntiles) store_in();  // ip was last read by this tile's first conv, before the barrier above
+    // (4) epilogue: bias/affine/act -> bf16 staging -> 16-byte stores (+ fused 2x2 SAME max-pool)
+#pragma unroll
+    for (int fc = 0; fc < 4; ++fc) {
+      const int cl = fc * 16 + 4 * q;
+#pragma unroll
+      for (int fp = 0; fp < 2; ++fp) {
+        const int row = wave * 32 + fp * 16 + col;
+        float v[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          v[j] = fmaf(acc[fc][fp][j], mul[fc][j], add[fc][j]);
+          if (a.act == VM_ACT_RELU) v[j] = fmaxf(v[j], 0.f);
+          else if (a.act == VM_ACT_SIGMOID) v[j] = sigmoid_precise(v[j]);
+        }
+        uint2 pk;
+        pk.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+        pk.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+        *reinterpret_cast<uint2*>(smem + C::S_OFF + row * C::SR + cl * 2) = pk;
+      }
+    }
+    // one barrier publishes the staging, the next tile's input and (for the next first conv) the end of this
+    // tile's patch reads; the stores below then overlap the next tile's first conv (staging is rewritten only
+    // after the next tile's first barrier)
+    __syncthreads();
+    T* yb = reinterpret_cast<T*>(a.y) + a.y_coff + (((long)n * H + r0) * W + c0) * (long)a.y_cstride;
+    const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(yb, 0, 0x7ffffff0, 0x00020000);
+#pragma unroll
+    for (int it = 0; it < C::BM * 8 / C::NT; ++it) {
+      const int idx = it * C::NT + tid;
+      const int rr = idx >> 3, cq = idx & 7;
+      const uint4 d = *reinterpret_cast<const uint4*>(smem + C::S_OFF + rr * C::SR + cq * 16);
+      const int pr = rr / C::TW, pc = rr % C::TW;
+      const bool ok = r0 + pr < H && c0 + pc < W && cq * 8 < a.cout;
+      const int off = ok ? (pr * W + pc) * ycs2 + cq * 16 : OOB;
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, d), yrs,
+                                             off, 0, 0);
+    }
+    if (a.py) {
+      const int PH = (H + 1) >> 1, PWd = (W + 1) >> 1;
+      const int pr0 = r0 >> 1, pc0 = c0 >> 1;
+      T* pb = reinterpret_cast<T*>(a.py) + a.py_coff + (((long)n * PH + pr0) * PWd + pc0) * (long)a.py_cstride;
+      const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(pb, 0, 0x7ffffff0, 0x00020000);
+      constexpr int PTW = C::TW / 2, PITEMS = C::BM / 4 * 8;
+#pragma unroll
+      for (int it = 0; it < (PITEMS + C::NT - 1) / C::NT; ++it) {
+        const int idx = it * C::NT + tid;
+        if (idx >= PITEMS) break;
+        const int pp = idx >> 3, cq = idx & 7;
+        const int pr = pp / PTW, pc = pp % PTW;
+        const int rr = 2 * pr * C::TW + 2 * pc;
+        const bool vh = r0 + 2 * pr + 1 < H, vw = c0 + 2 * pc + 1 < W;
+        float m[8], f[8];
+        Chunk<T>::unpack(*reinterpret_cast<const uint4*>(smem + C::S_OFF + rr * C::SR + cq * 16), m);
+        if (vw) {
+          Chunk<T>::unpack(*reinterpret_cast<const uint4*>(smem + C::S_OFF + (rr + 1) * C::SR + cq * 16), f);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) m[j] = fmaxf(m[j], f[j]);
+        }
+        if (vh) {
+          Chunk<T>::unpack(*reinterpret_cast<const uint4*>(smem + C::S_OFF + (rr + C::TW) * C::SR + cq * 16), f);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) m[j] = fmaxf(m[j], f[j]);
+        }
+        if (vh && vw) {
+          Chunk<T>::unpack(*reinterpret_cast<const uint4*>(smem + C::S_OFF + (rr + C::TW + 1) * C::SR + cq * 16), f);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) m[j] = fmaxf(m[j], f[j]);
+        }
+        const bool ok = pr0 + pr < PH && pc0 + pc < PWd && cq * 8 < a.cout;
+        const int off = ok ? ((pr * PWd + pc) * a.py_cstride + cq * 8) * 2 : OOB;
+        __builtin_amdgcn_raw_buffer_store_b128(
+            __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, Chunk<T>::pack(m)), prs, off, 0, 0);
+      }
+    }
+  }
+}
+
 // ================================================================ first layer: cin <= 8 (conv1_1, unet.py:65-74)
 // One 16-byte chunk per pixel, so a 32-deep MFMA K-step covers 4 taps x 8 channels: lane group q of the pixel
 // fragment reads the patch row shifted by tap 4j+q (taps >= 9 read as zero), matching the tap-major packing
@@ -1772,6 +2013,8 @@ static long g_glds_rb = 128;
 static long g_head_kernel = 0;
 static long g_patch_cfg = 0;
 static long g_patch_ablate = 0;
+static long g_pair_kernel = 0;  // vm_conv3x3_pair_first_nhwc: 0 = persistent weights-resident kernel when cout == 64,
+                                // 1 = streaming patch kernel
 
 static bool patch_ok(const ConvArgs& a, size_t tsize) {
   return tsize == 2 && a.chunk_major && a.cin_pad % 32 == 0 && a.y_dtype == VM_BF16 && a.y_vec &&
@@ -1878,6 +2121,11 @@ extern "C" int vm_set_option(const char* key, long value) {
   if (!strcmp(key, "patch_cfg")) {
     if (value < 0 || value > 12) return fail(VM_EINVAL, "patch_cfg must be 0..12");
     g_patch_cfg = value;
+    return VM_OK;
+  }
+  if (!strcmp(key, "pair_kernel")) {
+    if (value < 0 || value > 1) return fail(VM_EINVAL, "pair_kernel must be 0 or 1");
+    g_pair_kernel = value;
     return VM_OK;
   }
   if (!strcmp(key, "head_kernel")) {
@@ -2017,6 +2265,22 @@ extern "C" int vm_conv3x3_pair_first_nhwc(const vm_tensor* x, const void* packed
   a.w1 = packed1; a.bias1 = bias1; a.x_f32 = xf32; a.x_c = cin1;
   if (ypool) { a.py = ypool->ptr; a.py_cstride = ypool->cstride; a.py_coff = ypool->coff; }
   const long sp = (long)x->n * ((x->h + 7) / 8) * ((x->w + 31) / 32);
+  if (cout2 == 64 && g_pair_kernel == 0 && sp <= 0x7fffffffL) {
+    static int attr_dev = -1, n_cu = 0;
+    int dev = 0;
+    hipGetDevice(&dev);
+    if (attr_dev != dev) {
+      hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3_pair_persist),
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, PairCfg::LDS);
+      if (e == hipSuccess) e = hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
+      if (e != hipSuccess) return fail(VM_EHIP, "conv3x3_pair_persist setup: %s", hipGetErrorString(e));
+      attr_dev = dev;
+    }
+    const int grid = (int)(sp < n_cu ? sp : n_cu);
+    snprintf(g_last_kernel, sizeof g_last_kernel, "vm::conv3x3_pair_persist");
+    hipLaunchKernelGGL(conv3x3_pair_persist, dim3(grid), dim3(PairCfg::NT), PairCfg::LDS, st, a);
+    return check_launch("conv3x3_pair_persist");
+  }
   if (sp * ((cout2 + 63) / 64) < 512) return launch_patch<64, 4, 1, 6, 4, 1, 9, false, 0, true>(a, st);
   return launch_patch<64, 8, 1, 6, 8, 1, 9, false, 0, true>(a, st);
 }
