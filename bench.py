@@ -81,7 +81,7 @@ def cpu_baseline(h, w, sample_h, sample_w):
                       "1920x1080 by pixel count" % (sample_w, sample_h, dt, scale)}
 
 
-def load_traffic(args):
+def load_traffic(args, full=False):
     """Per-launch HBM bytes per kernel from the committed PMC pass (tools/traffic.py -> profiles/*_traffic.json),
     used only when it was collected on this exact workload."""
     import glob
@@ -94,8 +94,8 @@ def load_traffic(args):
         c = t.get("config", {})
         if (c.get("dtype"), c.get("height"), c.get("width"), c.get("batch")) == (args.dtype, args.height, args.width,
                                                                                args.batch):
-            return path, t.get("kernels", {})
-    return None, {}
+            return (path, t) if full else (path, t.get("kernels", {}))
+    return None, ({} if not full else None)
 
 
 def conv_roofline(prof, args):
@@ -146,6 +146,7 @@ def main():
     ap.add_argument("--cpu-sample", default="540x960", help="HxW of the CPU-baseline sample frame")
     ap.add_argument("--no-profile", action="store_true", help="skip per-conv HIP events")
     ap.add_argument("--layers", action="store_true", help="per-conv timing breakdown on stderr")
+    ap.add_argument("--no-graph", action="store_true", help="time eager launches instead of the captured HIP graph")
     args = ap.parse_args()
 
     rank, world, local = parallel.init_from_env("nccl")
@@ -165,8 +166,11 @@ def main():
     x = synth_frames(B, H, W, rank * B, dev)
     flops_per_frame = model.conv_flops(1, H, W)
 
+    # the timed step is the whole forward replayed from a HIP graph (captured once: one host call per step, no
+    # per-launch host cost); --no-graph times the eager launch sequence instead
+    step = model.capture(x).replay if not args.no_graph else (lambda: model.forward(x))
     for _ in range(args.warmup):
-        model.forward(x)
+        step()
     torch.cuda.synchronize()
 
     if world > 1:
@@ -174,7 +178,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        model.forward(x)
+        step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -210,9 +214,19 @@ def main():
                "config": {"workload": "unet.UNetVideo forward (20 3x3 convs, 3.233 TFLOP/frame), %dx%d 7-ch NHWC"
                                       % (W, H),
                           "frames_per_step_per_gpu": B, "height": H, "width": W,
+                          "launch": "eager" if args.no_graph else "hip-graph replay",
                           "parallelism": "frame-parallel dp%d" % world},
                "achieved_tflops_whole_forward": round(value / world * flops_per_frame / 1e12, 2),
                "roofline": roofline, "cpu_baseline": None}
+        src, tr = load_traffic(args, full=True)
+        if tr and tr.get("bytes_per_forward"):
+            # whole-forward HBM traffic (PMC FETCH_SIZE x2 + WRITE_SIZE summed over every kernel of one forward,
+            # one-time weight packing excluded) at this run's frame rate
+            bpf = tr["bytes_per_forward"] / float(args.batch)
+            rec["achieved_hbm_gbps"] = round(bpf * value / world / 1e9, 1)
+            rec["hbm"] = {"bytes_per_frame": int(bpf), "achieved_gbps_per_gpu": rec["achieved_hbm_gbps"],
+                          "peak_gbps": PEAK_HBM_GBPS, "frac": round(bpf * value / world / 1e9 / PEAK_HBM_GBPS, 4),
+                          "source": os.path.relpath(src, REPO)}
         if world == 1 and not args.no_cpu_baseline:
             sh, sw = (int(v) for v in args.cpu_sample.split("x"))
             rec["cpu_baseline"] = cpu_baseline(H, W, sh, sw)

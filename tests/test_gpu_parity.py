@@ -467,6 +467,23 @@ def test_unet_bf16_fused_and_unfused_forward_agree(vgg0):
     assert relerr(H(m.conv1_3), H(m3.conv1_3)) < 2e-2, relerr(H(m.conv1_3), H(m3.conv1_3))
 
 
+@pytest.mark.parametrize("dtype", ["bf16", "fp32"])
+def test_unet_graph_replay_matches_eager(dtype, vgg0):
+    """UNet.capture: the HIP-graph replay reproduces the eager forward bit for bit, also on new frames copied in."""
+    from vmatting import unet
+    rs = np.random.RandomState(5)
+    xs = [np.concatenate([rs.uniform(-120, 130, (2, 40, 72, 6)), rs.choice([-0.5, 0.0, 0.5], (2, 40, 72, 1))],
+                         -1).astype(np.float32) for _ in range(2)]
+    np.random.seed(1)
+    m = unet.UNetVideo(vgg0, dtype=dtype)
+    m.build(xs[0])
+    g = m.capture(xs[0])
+    for x in xs:
+        ya = g(x).clone()
+        yb = m.forward(torch.from_numpy(x).to(DEV)).clone()
+        assert torch.equal(ya, yb)
+
+
 @pytest.mark.parametrize("case", ["unet_simple_256_infer", "unet_simple_64_train"])
 def test_unet_simple_fp32_matches_reference_golden(case, vgg0):
     from vmatting import unet_simple

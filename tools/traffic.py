@@ -39,9 +39,13 @@ def main():
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--batch", type=int, default=1)
     ap.add_argument("--match", default="vm::", help="only kernels whose name contains this")
+    ap.add_argument("--forwards", type=int, default=3, help="forwards in the profiled run (warmup + steps)")
+    ap.add_argument("--setup", default="pack_weights,fold_up2x", help="one-time kernels left out of the per-frame sum")
     a = ap.parse_args()
     fe, wr = read(a.fetch, "FETCH_SIZE"), read(a.write, "WRITE_SIZE")
     kernels = {}
+    per_forward = 0.0
+    setup = [k for k in a.setup.split(",") if k]
     for name in sorted(set(fe) & set(wr)):
         if a.match not in name:
             continue
@@ -50,9 +54,12 @@ def main():
         wb = 1024 * sum(w) / len(w)
         kernels[name] = {"launches": len(f), "fetch_bytes_per_launch": int(fb), "write_bytes_per_launch": int(wb),
                          "bytes_per_launch": int(fb + wb)}
+        if not any(k in name for k in setup):
+            per_forward += (2 * 1024 * sum(f) + 1024 * sum(w)) / a.forwards
     rec = {"config": {"dtype": a.dtype, "height": a.height, "width": a.width, "batch": a.batch},
            "method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes, --kernel-trace), "
-                     "FETCH_SIZE x2 (gfx950), KB -> bytes", "kernels": kernels}
+                     "FETCH_SIZE x2 (gfx950), KB -> bytes", "forwards": a.forwards,
+           "bytes_per_forward": int(per_forward), "kernels": kernels}
     with open(a.out, "w") as f:
         json.dump(rec, f, indent=1)
     for k, v in kernels.items():

@@ -186,6 +186,12 @@ class UNet:
         self._publish(b)
         return self.output
 
+    def capture(self, x):
+        """Record one forward over frames shaped like ``x`` into a HIP graph (torch.cuda.CUDAGraph over the same
+        C-ABI launches) and return a GraphedForward: replaying it re-runs the whole forward with one host call, so
+        throughput no longer depends on the host's per-launch cost.  New frames are copied into ``.input``."""
+        return GraphedForward(self, x)
+
     @property
     def conv1_1(self):
         """unet.py:170 conv1_1 — with fuse_first the forward never writes it to HBM, so it is evaluated here."""
@@ -259,3 +265,35 @@ class UNetVideo(UNet):
             t[:, :, 3:6, :] = w
             return t
         return w
+
+
+class GraphedForward:
+    """A UNet forward captured once into a HIP graph (see UNet.capture).
+
+    ``input`` is the static frame buffer the graph reads ([N,H,W,C] f32 on the device) and ``output`` the static
+    alpha buffer it writes; ``replay()`` launches the graph on the current stream, ``__call__(frames)`` copies frames
+    in first.  The model's weights and activation buffers are the ones captured: do not change the model's shape or
+    weights afterwards (capture again instead)."""
+
+    def __init__(self, model, x):
+        x = model._as_input(x)
+        self.model = model
+        self.input = torch.empty_like(x)
+        self.input.copy_(x)
+        side = torch.cuda.Stream(device=self.input.device)
+        side.wait_stream(torch.cuda.current_stream(self.input.device))
+        with torch.cuda.stream(side):  # lazily built kernels/weights (folded filters, attributes) before capture
+            model.forward(self.input)
+        torch.cuda.current_stream(self.input.device).wait_stream(side)
+        torch.cuda.synchronize(self.input.device)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.output = model.forward(self.input)
+
+    def replay(self):
+        self.graph.replay()
+        return self.output
+
+    def __call__(self, frames):
+        self.input.copy_(self.model._as_input(frames))
+        return self.replay()
