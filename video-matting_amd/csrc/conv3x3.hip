@@ -2044,6 +2044,13 @@ static int dispatch_patch(ConvArgs& a, hipStream_t st) {
     case 10: return launch_patch<256, 4, 2, 3, 8, 1>(a, st);
     case 11: return launch_patch<64, 8, 1, 6, 4>(a, st);
     case 12: return launch_patch<64, 4, 1, 6, 4>(a, st);
+    case 13: return launch_patch<128, 4, 1, 4, 8, 2, 9, true>(a, st);
+    case 14: return launch_patch<128, 4, 1, 5, 8, 2, 9, true>(a, st);
+    case 15: return launch_patch<128, 4, 1, 6, 8, 2, 9, false>(a, st);
+    // 16 x 32 px tiles: half the weight-stream DMA per pixel of the 8 x 32 tiles
+    case 16: return launch_patch<64, 8, 1, 6, 16>(a, st);
+    case 17: return launch_patch<128, 8, 1, 4, 16>(a, st);
+    case 18: return launch_patch<128, 4, 2, 4, 16>(a, st);
     default: break;
   }
   // measured inside the UNetVideo 1080p forward (bench.py --layers): 4 waves of 64 px x 128 channels (2 blocks
@@ -2119,7 +2126,7 @@ extern "C" int vm_set_option(const char* key, long value) {
     return VM_OK;
   }
   if (!strcmp(key, "patch_cfg")) {
-    if (value < 0 || value > 12) return fail(VM_EINVAL, "patch_cfg must be 0..12");
+    if (value < 0 || value > 18) return fail(VM_EINVAL, "patch_cfg must be 0..18");
     g_patch_cfg = value;
     return VM_OK;
   }
