@@ -33,7 +33,7 @@ extern "C" {
 
 #define VM_ABI_VERSION 1
 
-enum vm_dtype { VM_F32 = 0, VM_BF16 = 1, VM_U8 = 2 };
+enum vm_dtype { VM_F32 = 0, VM_BF16 = 1, VM_U8 = 2, VM_F64 = 3 /* loader outputs only */ };
 
 enum vm_act {
   VM_ACT_NONE = 0,
@@ -178,6 +178,49 @@ int vm_fb_consistency(const float* backward, const float* forward, int h, int w,
 size_t vm_loss_workspace_bytes(long pixels);
 int vm_matting_loss(const float* pred, const float* gt, const float* raw_fg, const float* bg, const float* cmp,
                     long pixels, float* out, void* work, void* stream);
+
+/* ---------------------------------------------------------------- training-sample loader
+ * Replaces the per-pixel part of loader.py's sample builders after decoding: load_and_crop (loader.py:39-85),
+ * simple_load_crop (:119-157), video_load_crop (:285-330) and their batch loops get_batch / simple_batch /
+ * video_batch (:93-116, 160-171, 333-345) — get_padded_img canvases (:10-36), crops, flow.warp_img of the
+ * previous alpha (:291-293), cv2.resize(INTER_LINEAR) of fg / alpha / warped alpha / bg to the network size
+ * (:70-73, 146-148, 316-319), reader.create_composite_image and the VGG_MEAN subtraction (:75-77).
+ * The random draws stay on the host (same np.random calls, same order); the host passes their outcome as
+ * window maps.  One axis of a padded + cropped source: resize-source index u in [0, n) is canvas index
+ * t = u + off; the canvas holds image data on [lo, hi) at image index t + shift, zeros elsewhere. */
+typedef struct vm_crop_axis {
+  int32_t n, off, lo, hi, shift;
+} vm_crop_axis;
+
+typedef struct vm_loader_sample {
+  const uint8_t* fg;   /* foreground BGRA u8 [fg_h, fg_w, 4] (reader.read_fg_img: BGR + alpha), 4-byte aligned */
+  const uint8_t* prev; /* previous frame BGRA u8 [prev_h, prev_w, 4] (its alpha is warped) or NULL */
+  const float* flow;   /* backward flow f32 [fg_h, fg_w, 2] (reader.read_flow), 8-byte aligned, or NULL */
+  const uint8_t* bg;   /* background BGR u8 [bg_h, bg_w, 3] (cv2.imread) */
+  int32_t fg_h, fg_w, prev_h, prev_w, bg_h, bg_w;
+  vm_crop_axis fg_rows, fg_cols, bg_rows, bg_cols;
+  int32_t mirror;      /* get_batch rd_mirror: flip this sample's outputs left-right (loader.py:105-109) */
+  int32_t reserved;
+} vm_loader_sample;
+
+enum vm_loader_plane { VM_LOADER_CMP = 0, VM_LOADER_BG = 1, VM_LOADER_LABEL = 2, VM_LOADER_WARPED = 3,
+                       VM_LOADER_FG = 4 };
+
+/* Output planes [n, out_h, out_w, *] (NULL = not produced); element (i, y, x, k) of plane p is at
+ * ptr[p][((i*out_h + y)*out_w + x)*pixstride[p] + k].  cmp, bg: 3 channels, mean-subtracted; label: 1 channel
+ * (alpha); warped: 3 identical channels (loader.py:293); fg: 3 channels, the resized raw foreground. */
+typedef struct vm_loader_outputs {
+  void* ptr[5];
+  int32_t pixstride[5];
+  int32_t reserved;
+} vm_loader_outputs;
+
+/* samples: HOST array of n descriptors whose image pointers are device pointers; validated, then uploaded into
+ * work (device, vm_loader_workspace_bytes(n) bytes) on `stream`.  dtype VM_F32 or VM_F64 (float64 = the
+ * reference's values bit for bit).  Output size (out_h, out_w) = (input_size[1], input_size[0]). */
+size_t vm_loader_workspace_bytes(int n);
+int vm_loader_compose(const vm_loader_sample* samples, int n, int out_h, int out_w, int dtype,
+                      const vm_loader_outputs* out, void* work, void* stream);
 
 #ifdef __cplusplus
 }

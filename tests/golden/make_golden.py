@@ -262,16 +262,96 @@ def gen_loss(R, out):
                                cmp_loss=float(np.mean(cmp_loss)))
 
 
+# loader entries: (seed, fg_hw, bg_hw, video).  E2's 300 x 700 foreground takes both branches of
+# get_padded_img for the 320 crop (rows padded, columns cropped into a zero-tailed canvas).
+LOADER_ENTRIES = [(41, (330, 340), (250, 300), True), (42, (330, 340), (640, 640), True),
+                  (43, (300, 700), (500, 375), False), (44, (520, 360), (330, 420), False)]
+# calls: (fn, entry indices, global np.random seed, input_size, rd_mirror)
+LOADER_CALLS = [("video_load_crop", [0], 0, (320, 320), 0), ("video_load_crop", [0], 1, (320, 320), 0),
+                ("video_load_crop", [1], 2, (320, 320), 0), ("video_load_crop", [1], 5, (320, 320), 0),
+                ("video_load_crop", [0], 3, (200, 200), 0), ("video_load_crop", [1], 4, (160, 160), 0),
+                ("simple_load_crop", [2], 6, (320, 320), 0), ("simple_load_crop", [2], 7, (96, 96), 0),
+                ("simple_load_crop", [3], 8, (320, 320), 0),
+                ("get_batch", [2, 3, 2], 9, (64, 64), 1), ("video_batch", [0, 1], 10, (96, 96), 0)]
+LOADER_OUTS = {"video_load_crop": ("cmp", "bg", "label", "warped", "fg"),
+               "simple_load_crop": ("cmp", "bg", "label", "fg"),
+               "get_batch": ("input", "label", "fg"),
+               "video_batch": ("cmp", "bg", "label", "warped", "fg")}
+
+
+def _write_loader_entry(td, idx):
+    from PIL import Image
+    from oracle.loader import synthetic_entry
+    seed, fg_hw, bg_hw, video = LOADER_ENTRIES[idx]
+    ent = synthetic_entry(seed, fg_hw, bg_hw, video)
+    p = lambda s: os.path.join(td, "e%d_%s" % (idx, s))  # noqa: E731
+    Image.fromarray(np.ascontiguousarray(ent[0][:, :, [2, 1, 0, 3]])).save(p("fg.png"))  # BGRA -> RGBA file
+    Image.fromarray(np.ascontiguousarray(ent[1][:, :, ::-1])).save(p("bg.png"))
+    if video:
+        Image.fromarray(np.ascontiguousarray(ent[2][:, :, [2, 1, 0, 3]])).save(p("prev.png"))
+        write_flow(p("flow.flo"), ent[3])
+        return (p("fg.png"), p("bg.png"), p("prev.png"), p("flow.flo"))
+    a = ent[0][:, :, 3]
+    tri = np.where(a == 255, 255, np.where(a == 0, 0, 128)).astype(np.uint8)
+    Image.fromarray(tri).save(p("trimap.png"))
+    return (p("fg.png"), p("trimap.png"), p("bg.png"))
+
+
+def gen_loader(R, out):
+    """Run the reference's loader.py (load_and_crop via get_batch, simple_load_crop, video_load_crop,
+    video_batch) on synthetic PNG / .flo files; keep 1024 sampled pixels of every output plane
+    (float64, exact), float64 plane sums, and the next global np.random draw (draw-count check)."""
+    sys.path.insert(0, REF)
+    import loader  # the reference module, for real
+    d = {"entries": np.array([[s, f[0], f[1], b[0], b[1], int(v)] for s, f, b, v in LOADER_ENTRIES]),
+         "n_calls": len(LOADER_CALLS)}
+    with tempfile.TemporaryDirectory() as td:
+        paths = [_write_loader_entry(td, i) for i in range(len(LOADER_ENTRIES))]
+        for ci, (fn, ents, seed, size, mirror) in enumerate(LOADER_CALLS):
+            np.random.seed(seed)
+            if fn == "get_batch":
+                res = loader.get_batch([list(paths[e]) for e in ents], size, rd_scale=False, rd_mirror=bool(mirror))
+            elif fn.endswith("_batch"):
+                res = getattr(loader, fn)([paths[e] for e in ents], size)
+            else:
+                res = getattr(loader, fn)(paths[ents[0]], size)
+            nxt = np.random.randint(0, 2 ** 31 - 1)
+            res = [np.asarray(r, np.float64) for r in res]
+            if not fn.endswith("batch"):
+                res = [r[None] for r in res]
+            n, oh, ow = res[0].shape[:3]
+            rs = np.random.RandomState(1000 + ci)
+            pn, py, px = rs.randint(0, n, 1024), rs.randint(0, oh, 1024), rs.randint(0, ow, 1024)
+            pre = "c%d_" % ci
+            d[pre + "meta"] = np.array([seed, size[0], size[1], mirror, nxt])
+            d[pre + "fn"] = np.array(fn)
+            d[pre + "entries"] = np.array(ents)
+            d[pre + "pos"] = np.stack([pn, py, px])
+            for name, r in zip(LOADER_OUTS[fn], res):
+                d[pre + name + "_vals"] = r[pn, py, px]
+                d[pre + name + "_sum"] = np.array(float(r.sum()))
+            print("loader call", ci, fn, "crop type", [np.random.RandomState(seed).randint(0, 3)], "shape", res[0].shape)
+    out["loader_calls"] = d
+
+
 def main():
     np.load = _fake_load
     R = load_reference()
     out = {}
+    if len(sys.argv) > 1:  # regenerate only the named fixtures: make_golden.py loader
+        for name in sys.argv[1:]:
+            globals()["gen_" + name](R, out)
+        for name, d in out.items():
+            np.savez_compressed(os.path.join(HERE, name + ".npz"), **d)
+            print("wrote", name, os.path.getsize(os.path.join(HERE, name + ".npz")))
+        return
     gen_unet(R, out)
     gen_refine(R, out)
     gen_small(R, out)
     gen_flow(R, out)
     gen_loss(R, out)
     gen_unet_simple(R, out)
+    gen_loader(R, out)
     for name, d in out.items():
         np.savez_compressed(os.path.join(HERE, name + ".npz"), **d)
         print("wrote", name, os.path.getsize(os.path.join(HERE, name + ".npz")))

@@ -252,12 +252,102 @@ def remap(src, map1, map2, interpolation):
     return out.astype(src.dtype)
 
 
+def resize(src, dsize, interpolation=INTER_LINEAR, **k):
+    """cv2.resize(src, dsize, interpolation=INTER_LINEAR) for float64 sources, written after the
+    structure of OpenCV 3.x imgproc/resize.cpp: dsize == ssize copies; an exact 2x reduction in both
+    axes switches to the INTER_AREA fast path (sum += S[ofs0]+S[ofs1]+S[ofs2]+S[ofs3]; D = sum*scale);
+    otherwise resizeGeneric_ with HResizeLinear<double,double,float> / VResizeLinear: per-column
+    (xofs, alpha) and per-row (yofs, beta) tables built one entry at a time in float32, rows fetched
+    through clip(sy, 0, ssize.height)."""
+    src = np.asarray(src)
+    assert interpolation == INTER_LINEAR and src.dtype == np.float64
+    if src.ndim == 3 and src.shape[2] == 1:
+        src = src[:, :, 0]
+    sh, sw = src.shape[:2]
+    dw, dh = int(dsize[0]), int(dsize[1])
+    if (sh, sw) == (dh, dw):
+        return src.copy()
+    inv_x, inv_y = float(dw) / sw, float(dh) / sh
+    scale_x, scale_y = 1.0 / inv_x, 1.0 / inv_y
+    ix, iy = int(round(scale_x)), int(round(scale_y))
+    eps = np.finfo(np.float64).eps
+    if abs(scale_x - ix) < eps and abs(scale_y - iy) < eps and ix == 2 and iy == 2:
+        dst = np.zeros((dh, dw) + src.shape[2:], np.float64)
+        scale = float(np.float32(1.0) / np.float32(4))
+        for dy in range(dh):
+            for dx in range(dw):
+                S = [src[2 * dy + a, 2 * dx + b] for a in range(2) for b in range(2)]
+                total = 0.0 + (((S[0] + S[1]) + S[2]) + S[3])
+                dst[dy, dx] = total * scale
+        return dst
+    xofs, alpha, xmax = [], [], dw
+    for dx in range(dw):
+        fx = np.float32((dx + 0.5) * scale_x - 0.5)
+        sx = int(np.floor(fx))
+        fx = np.float32(fx - np.float32(sx))
+        if sx < 0:
+            fx, sx = np.float32(0), 0
+        if sx + 1 >= sw:
+            xmax = min(xmax, dx)
+            if sx >= sw - 1:
+                fx, sx = np.float32(0), sw - 1
+        xofs.append(sx)
+        alpha.append((float(np.float32(1) - fx), float(fx)))
+    yofs, beta = [], []
+    for dy in range(dh):
+        fy = np.float32((dy + 0.5) * scale_y - 0.5)
+        sy = int(np.floor(fy))
+        fy = np.float32(fy - np.float32(sy))
+        yofs.append(sy)
+        beta.append((float(np.float32(1) - fy), float(fy)))
+
+    def hresize(row):
+        out = np.empty((dw,) + row.shape[1:], np.float64)
+        for dx in range(dw):
+            sx = xofs[dx]
+            if dx < xmax:
+                out[dx] = row[sx] * alpha[dx][0] + row[sx + 1] * alpha[dx][1]
+            else:
+                out[dx] = row[sx] * 1.0
+        return out
+
+    dst = np.empty((dh, dw) + src.shape[2:], np.float64)
+    cache = {}
+    for dy in range(dh):
+        rows = []
+        for k in range(2):
+            sy = min(max(yofs[dy] + k, 0), sh - 1)
+            if sy not in cache:
+                cache[sy] = hresize(src[sy])
+            rows.append(cache[sy])
+        dst[dy] = rows[0] * beta[dy][0] + rows[1] * beta[dy][1]
+    return dst
+
+
+def imread(path, flags=1):
+    """cv2.imread via PIL: flags -1 (IMREAD_UNCHANGED) keeps BGRA / 16-bit, 0 = grayscale, else BGR u8."""
+    from PIL import Image
+    im = Image.open(path)
+    if flags == 0:
+        return np.asarray(im.convert("L"))
+    if flags == -1:
+        a = np.asarray(im)
+        if a.ndim == 3 and a.shape[2] == 4:
+            return a[:, :, [2, 1, 0, 3]]
+        if a.ndim == 3:
+            return a[:, :, ::-1]
+        return a
+    return np.ascontiguousarray(np.asarray(im.convert("RGB"))[:, :, ::-1])
+
+
 def make_cv2():
     cv2 = types.ModuleType("cv2")
     cv2.INTER_LINEAR = INTER_LINEAR
     cv2.NORM_MINMAX = 32
     cv2.IMREAD_UNCHANGED = -1
     cv2.remap = remap
+    cv2.resize = resize
+    cv2.imread = imread
     cv2.normalize = lambda *a, **k: None
     cv2.imshow = lambda *a, **k: None
     cv2.waitKey = lambda *a, **k: 0

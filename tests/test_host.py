@@ -119,3 +119,55 @@ def test_frame_parallel_collectives_gloo_world2():
         p.join(60)
     assert sorted(r for r, _, _ in res) == [0, 1]
     assert all(b and g for _, b, g in res), res
+
+
+# ---------------------------------------------------------------- loader host logic (no GPU)
+
+@pytest.mark.parametrize("fg_hw,bg_hw", [((330, 340), (250, 300)), ((300, 700), (500, 375)), ((1080, 1920), (720, 1280)),
+                                         ((200, 200), (640, 640)), ((700, 310), (90, 1300))])
+def test_loader_plan_replays_reference_draws(fg_hw, bg_hw):
+    """The product's host planning consumes np.random exactly like the oracle restatement of loader.py."""
+    from oracle import loader as ol
+    from vmatting import loader as vl
+    for seed in range(12):
+        np.random.seed(seed)
+        want = ol.plan_crop(fg_hw, bg_hw)
+        a = np.random.randint(0, 1 << 30)
+        np.random.seed(seed)
+        got = vl.plan_crop(fg_hw, bg_hw)
+        b = np.random.randint(0, 1 << 30)
+        assert a == b
+        assert [tuple(x) for x in got] == [x.astuple() for x in want[1:]]
+
+
+def test_loader_get_padded_img_matches_oracle_maps():
+    from oracle import loader as ol
+    from vmatting import loader as vl
+    img = np.arange(7 * 9 * 2).reshape(7, 9, 2)
+    for seed in range(6):
+        for crop in ((5, 12), (9, 4), (7, 9)):
+            np.random.seed(seed)
+            got = vl.get_padded_img(img, *crop)
+            np.random.seed(seed)
+            rows, cols = ol.pad_axis(7, crop[0]), ol.pad_axis(9, crop[1])
+            want = ol.Axis(rows[0], 0, *rows[1:]).gather(ol.Axis(cols[0], 0, *cols[1:]).gather(img, 1), 0)
+            assert np.array_equal(got, want)
+
+
+def test_loader_struct_layout():
+    import ctypes
+    from vmatting import _lib
+    assert ctypes.sizeof(_lib.VmCropAxis) == 20
+    assert ctypes.sizeof(_lib.VmLoaderSample) == 144
+    assert ctypes.sizeof(_lib.VmLoaderOutputs) == 64
+
+
+def test_loader_file_helpers(tmp_path):
+    from vmatting import loader as vl
+    lst = tmp_path / "list.txt"
+    lst.write_text("a/fg.png a/tr.png b/bg.jpg\nc/fg.png c/tr.png d/bg.jpg\n")
+    files = vl.get_file_list("/data", str(lst))
+    assert files[1] == ["/data/c/fg.png", "/data/c/tr.png", "/data/d/bg.jpg"]
+    assert not vl.epoch_is_over(files, 2)
+    assert vl.get_batch_list(files, 1) == [["/data/c/fg.png", "/data/c/tr.png", "/data/d/bg.jpg"]]
+    assert vl.epoch_is_over(files, 2)

@@ -143,3 +143,93 @@ def test_oracle_float32_mode_close_to_float64():
     p = om.unet_params(synthetic_vgg16(0), np.random.RandomState(int(g["weight_seed"])), video=True)
     r = om.unet_forward(g["x"], p, dtype=np.float32)
     _close(r["output"], g["output"], 0, 1e-5)
+
+
+# ---------------------------------------------------------------- training-sample loader (loader.py)
+
+def _loader_entry(g, i):
+    from oracle import loader as ol
+    s, fh, fw, bh, bw, v = (int(x) for x in g["entries"][i])
+    return ol.synthetic_entry(s, (fh, fw), (bh, bw), bool(v))
+
+
+def loader_call_outputs(g, ci, entry_fn):
+    """Replay golden call ci through entry_fn(entries, seed, input_size, mirror, fn) -> dict of [n,h,w,c]
+    arrays; returns (outputs, next global draw)."""
+    p = "c%d_" % ci
+    seed, sw, sh, mirror, _ = (int(x) for x in g[p + "meta"])
+    ents = [int(e) for e in g[p + "entries"]]
+    np.random.seed(seed)
+    out = entry_fn(ents, (sw, sh), bool(mirror), str(g[p + "fn"]))
+    return out, np.random.randint(0, 2 ** 31 - 1)
+
+
+def check_loader_call(g, ci, out, nxt):
+    p = "c%d_" % ci
+    assert nxt == int(g[p + "meta"][4]), "np.random draw count differs from the reference's"
+    pn, py, px = g[p + "pos"]
+    names = [k[len(p):-5] for k in g if k.startswith(p) and k.endswith("_vals")]
+    assert names
+    for k in names:
+        v = np.asarray(out[k], np.float64)[pn, py, px]
+        assert np.array_equal(v, g[p + k + "_vals"]), "%s: max diff %g" % (k, np.abs(v - g[p + k + "_vals"]).max())
+        s = float(np.asarray(out[k], np.float64).sum())
+        assert abs(s - float(g[p + k + "_sum"])) <= 1e-10 * max(1.0, abs(s)), k
+
+
+@pytest.mark.parametrize("ci", range(11))
+def test_loader_oracle_matches_reference_loader(ci):
+    """oracle/loader.py reproduces loader.py's outputs bit for bit (float64) and consumes the same draws."""
+    from oracle import loader as ol
+    g = golden("loader_calls")
+    assert int(g["n_calls"]) == 11
+
+    def run(ents, size, mirror, fn):
+        out = ol.batch([_loader_entry(g, e) for e in ents], size, mirror=mirror)
+        if fn == "get_batch":
+            out["input"] = np.concatenate([out["cmp"], out["bg"]], axis=3)
+        return out
+
+    out, nxt = loader_call_outputs(g, ci, run)
+    check_loader_call(g, ci, out, nxt)
+
+
+def test_loader_golden_covers_crop_paths():
+    """The golden calls exercise every resize path and both get_padded_img branches."""
+    from oracle import loader as ol
+    g = golden("loader_calls")
+    seen = set()
+    for ci in range(int(g["n_calls"])):
+        p = "c%d_" % ci
+        seed, sw, sh = (int(x) for x in g[p + "meta"][:3])
+        np.random.seed(seed)
+        e = _loader_entry(g, int(g[p + "entries"][0]))
+        (ch, _), fr, fc, br, bc = ol.plan_crop(e[0].shape[:2], e[1].shape[:2])
+        for ax, img_n in ((fr, e[0].shape[0]), (fc, e[0].shape[1])):
+            if ax.shift < 0:
+                seen.add("pad-offset")
+            elif ax.hi < img_n:
+                seen.add("pad-zero-tail")
+        seen.add("copy" if ch == sw else ("area" if ch == 2 * sw else "linear"))
+        if (br.n, bc.n) == (2 * sh, 2 * sw):
+            seen.add("bg-area")
+    assert {"pad-offset", "pad-zero-tail", "copy", "area", "linear", "bg-area"} <= seen, seen
+
+
+@pytest.mark.parametrize("shape", [(37, 23), (640, 640), (480, 320), (5, 3), (64, 64, 3), (300, 700, 3), (41, 1)])
+@pytest.mark.parametrize("dsize", [(320, 320), (64, 48), (20, 2), (1, 1)])
+def test_cv_resize_restatements_agree(shape, dsize):
+    """oracle.loader.resize_linear (vectorised) == tfshim.resize (loop form, OpenCV structure) bit for bit."""
+    import sys
+
+    from conftest import GOLDEN
+    if GOLDEN not in sys.path:
+        sys.path.insert(0, GOLDEN)
+    import tfshim
+    from oracle import loader as ol
+    if shape[:2] == (640, 640) and dsize != (320, 320):
+        pytest.skip("large source only for the area path")
+    img = np.random.RandomState(sum(shape)).uniform(0, 255, shape)
+    a = ol.resize_linear(img, dsize)
+    b = tfshim.resize(img, dsize)
+    assert a.shape == b.shape and np.array_equal(a, b)

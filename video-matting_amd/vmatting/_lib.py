@@ -16,7 +16,7 @@ import torch  # noqa: F401  (must precede the CDLL load: shared HIP runtime)
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libvmatting.so")
 
-VM_F32, VM_BF16, VM_U8 = 0, 1, 2
+VM_F32, VM_BF16, VM_U8, VM_F64 = 0, 1, 2, 3
 ACT = {"none": 0, "relu": 1, "sigmoid": 2, "softmax": 3}
 VM_OK, VM_EINVAL, VM_EUNSUPPORTED, VM_EHIP, VM_EINDEX = 0, -1, -2, -3, -4
 ABI_VERSION = 1
@@ -31,6 +31,26 @@ class VmTensor(ctypes.Structure):
 
 
 P = ctypes.POINTER(VmTensor)
+
+
+class VmCropAxis(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_int32), ("off", ctypes.c_int32), ("lo", ctypes.c_int32), ("hi", ctypes.c_int32),
+                ("shift", ctypes.c_int32)]
+
+
+class VmLoaderSample(ctypes.Structure):
+    _fields_ = [("fg", c_void_p), ("prev", c_void_p), ("flow", c_void_p), ("bg", c_void_p),
+                ("fg_h", ctypes.c_int32), ("fg_w", ctypes.c_int32), ("prev_h", ctypes.c_int32),
+                ("prev_w", ctypes.c_int32), ("bg_h", ctypes.c_int32), ("bg_w", ctypes.c_int32),
+                ("fg_rows", VmCropAxis), ("fg_cols", VmCropAxis), ("bg_rows", VmCropAxis), ("bg_cols", VmCropAxis),
+                ("mirror", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+
+class VmLoaderOutputs(ctypes.Structure):
+    _fields_ = [("ptr", c_void_p * 5), ("pixstride", ctypes.c_int32 * 5), ("reserved", ctypes.c_int32)]
+
+
+LOADER_PLANES = {"cmp": 0, "bg": 1, "label": 2, "warped": 3, "fg": 4}
 
 # (name, restype, argtypes) — one row per declaration in include/vmatting.h
 SIGNATURES = [
@@ -64,6 +84,9 @@ SIGNATURES = [
     ("vm_loss_workspace_bytes", c_size_t, [c_long]),
     ("vm_matting_loss", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_void_p, c_void_p,
                                 c_void_p]),
+    ("vm_loader_workspace_bytes", c_size_t, [c_int]),
+    ("vm_loader_compose", c_int, [ctypes.POINTER(VmLoaderSample), c_int, c_int, c_int, c_int,
+                                  ctypes.POINTER(VmLoaderOutputs), c_void_p, c_void_p]),
 ]
 
 _lib = None
