@@ -112,11 +112,15 @@ def test_loader_device_resident_inputs_and_input_layout():
     np.random.seed(3)
     plan = vl.plan_crop(fg.shape[:2], bg.shape[:2])
     s = {"fg": torch.from_numpy(fg).cuda(), "bg": torch.from_numpy(bg).cuda(), "plan": plan}
-    r = vl.compose_batch([s], (96, 96), ("input", "label", "fg", "cmp", "bg"), dtype=torch.float64)
+    r = vl.compose_batch([s], (96, 96), ("input", "label", "fg"), dtype=torch.float64)
+    r2 = vl.compose_batch([s], (96, 96), ("cmp", "bg"), dtype=torch.float64)
     torch.cuda.synchronize()
     want = _oracle_batch([{"fg": fg, "bg": bg, "plan": plan}], (96, 96), [False])
     assert np.array_equal(H(r["input"]), np.concatenate([want["cmp"], want["bg"]], axis=3))
-    assert np.array_equal(H(r["cmp"]), want["cmp"]) and np.array_equal(H(r["label"]), want["label"])
+    assert np.array_equal(H(r["label"]), want["label"]) and np.array_equal(H(r["fg"]), want["fg"])
+    assert np.array_equal(H(r2["cmp"]), want["cmp"]) and np.array_equal(H(r2["bg"]), want["bg"])
+    with pytest.raises(ValueError):
+        vl.compose_batch([s], (96, 96), ("input", "cmp"))
 
 
 def test_loader_rejects_bad_windows():

@@ -131,6 +131,8 @@ def compose_batch(samples, input_size, outputs=("cmp", "bg", "label", "fg"), mir
     n = len(samples)
     if n == 0:
         raise ValueError("empty batch")
+    if "input" in outputs and ("cmp" in outputs or "bg" in outputs):
+        raise ValueError("'input' already holds cmp and bg (channels 0-2 / 3-5)")
     ow, oh = int(input_size[0]), int(input_size[1])
     keep = []
     desc = (_lib.VmLoaderSample * n)()
