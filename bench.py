@@ -81,6 +81,69 @@ def cpu_baseline(h, w, sample_h, sample_w):
                       "1920x1080 by pixel count" % (sample_w, sample_h, dt, scale)}
 
 
+def loader_inputs(n, h, w, seed=0):
+    """Decoded video-loader entries (fg/prev BGRA, bg BGR u8, piecewise-constant f32 flow) at h x w."""
+    rs = np.random.RandomState(seed)
+    out = []
+    for _ in range(n):
+        lo = rs.uniform(-12, 12, ((h + 63) // 64, (w + 63) // 64, 2)).astype(np.float32)
+        flow = np.repeat(np.repeat(lo, 64, 0), 64, 1)[:h, :w]  # |u|, |v| <= 12 px
+        out.append({"fg": rs.randint(0, 256, (h, w, 4), dtype=np.uint8),
+                    "bg": rs.randint(0, 256, (h, w, 3), dtype=np.uint8),
+                    "prev": rs.randint(0, 256, (h, w, 4), dtype=np.uint8), "flow": np.ascontiguousarray(flow)})
+    return out
+
+
+def loader_bench(dev, steps, cpu=True, n=8, size=320, h=1080, w=1920):
+    """video_batch's per-pixel work (csrc/loader.hip) on a batch of n 1080p video entries resized
+    to size x size; inputs resident in HBM, the host's np.random draws replayed once outside the timed region."""
+    from vmatting import loader as vl
+    host = loader_inputs(n, h, w)
+    np.random.seed(0)
+    for s in host:
+        s["plan"] = vl.plan_crop((h, w), (h, w))
+    samples = [dict(s, **{k: torch.from_numpy(s[k]).to(dev) for k in ("fg", "bg", "prev", "flow")}) for s in host]
+    names = ("cmp", "bg", "label", "warped", "fg")
+    for _ in range(3):
+        vl.compose_batch(samples, (size, size), names, device=dev)
+    torch.cuda.synchronize()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    t0 = time.perf_counter()
+    ev[0].record()
+    for _ in range(steps):
+        vl.compose_batch(samples, (size, size), names, device=dev)
+    ev[1].record()
+    torch.cuda.synchronize()
+    wall = (time.perf_counter() - t0) / steps
+    dev_ms = ev[0].elapsed_time(ev[1]) / steps
+    # algorithmic bytes per batch: the f32 outputs (13 channels) + each source byte the resize can touch, once
+    # (min(window area, 4 taps per output pixel) per plane: fg BGRA 4 B, flow 8 B, prev BGRA 4 B, bg 3 B)
+    taps = 4 * size * size
+    src = 0
+    for s in host:
+        fr, fc, br, bc = s["plan"]
+        src += min(fr[0] * fc[0], taps) * (4 + 8 + 4) + min(br[0] * bc[0], taps) * 3
+    algo = n * size * size * 13 * 4 + src
+    rec = {"workload": "loader.video_batch per-pixel work: %d entries %dx%d -> %dx%d, f32 out" % (n, w, h, size, size),
+           "samples_per_s": round(n / wall, 1), "ms_per_batch": round(1000 * wall, 4),
+           "device_ms_per_batch": round(dev_ms, 4), "algorithmic_bytes_per_batch": int(algo),
+           "achieved_gbps": round(algo / (dev_ms * 1e-3) / 1e9, 1), "peak_gbps": PEAK_HBM_GBPS,
+           "crops": [int(s["plan"][0][0]) for s in host]}
+    if cpu:
+        from oracle import loader as ol  # the CPU-baseline leg only
+        k = 2
+        t0 = time.perf_counter()
+        for s in host[:k]:
+            fr, fc, br, bc = (ol.Axis(*a) for a in s["plan"])
+            srcs = ol.crop_sources(s["fg"], s["bg"], fr, fc, br, bc, s["prev"], s["flow"])
+            ol.compose(srcs[0], srcs[1], srcs[3], (size, size), srcs[2])
+        dt = (time.perf_counter() - t0) / k
+        rec["cpu_baseline"] = {"value": round(1.0 / dt, 3), "unit": "samples/s", "cores": 1, "kind": "port",
+                               "sample": "oracle/loader.py (numpy float64, with the reference's full-frame warp) on "
+                                         "%d of the %d entries (%.2f s each)" % (k, n, dt)}
+    return rec
+
+
 def load_traffic(args, full=False):
     """Per-launch HBM bytes per kernel from the committed PMC pass (tools/traffic.py -> profiles/*_traffic.json),
     used only when it was collected on this exact workload."""
@@ -147,6 +210,7 @@ def main():
     ap.add_argument("--no-profile", action="store_true", help="skip per-conv HIP events")
     ap.add_argument("--layers", action="store_true", help="per-conv timing breakdown on stderr")
     ap.add_argument("--no-graph", action="store_true", help="time eager launches instead of the captured HIP graph")
+    ap.add_argument("--no-loader", action="store_true", help="skip the training-sample loader record (rank 0, N=1)")
     args = ap.parse_args()
 
     rank, world, local = parallel.init_from_env("nccl")
@@ -230,6 +294,8 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             sh, sw = (int(v) for v in args.cpu_sample.split("x"))
             rec["cpu_baseline"] = cpu_baseline(H, W, sh, sw)
+        if world == 1 and not args.no_loader:
+            rec["loader"] = loader_bench(dev, max(args.steps, 10), cpu=not args.no_cpu_baseline)
         print(json.dumps(rec), flush=True)
     if world > 1:
         dist.destroy_process_group()
