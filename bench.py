@@ -211,6 +211,8 @@ def main():
     ap.add_argument("--layers", action="store_true", help="per-conv timing breakdown on stderr")
     ap.add_argument("--no-graph", action="store_true", help="time eager launches instead of the captured HIP graph")
     ap.add_argument("--no-loader", action="store_true", help="skip the training-sample loader record (rank 0, N=1)")
+    ap.add_argument("--option", action="append", default=[], metavar="KEY=VALUE",
+                    help="vm_set_option kernel knob before the run (A/B comparisons), repeatable")
     args = ap.parse_args()
 
     rank, world, local = parallel.init_from_env("nccl")
@@ -218,6 +220,10 @@ def main():
         log("warning: --gpus %d but WORLD_SIZE %d; using WORLD_SIZE" % (args.gpus, world))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    for kv in args.option:
+        k, v = kv.split("=")
+        from vmatting import _lib
+        _lib.set_option(k, int(v))
 
     # identical weights everywhere: every rank draws from the same seeds, then rank 0's packed
     # buffers are broadcast (one RCCL collective) so replicas are bit-identical by construction

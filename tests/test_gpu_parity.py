@@ -66,7 +66,7 @@ def conv_kernel(request):
     _lib.set_option("conv_kernel", 0)
 
 
-@pytest.mark.parametrize("cfg", list(range(1, 13)))
+@pytest.mark.parametrize("cfg", list(range(1, 23)))
 @pytest.mark.parametrize("case", [(1, 9, 33, 64, 64, "relu"), (2, 17, 70, 128, 128, "none"), (1, 20, 45, 96, 192, "relu"),
                                   (1, 8, 32, 32, 64, "sigmoid"), (1, 3, 5, 256, 128, "relu")])
 def test_patch_kernel_configs(case, cfg):
@@ -264,7 +264,7 @@ UP_CASES = [(1, 9, 13, 128, 64), (2, 7, 33, 256, 128), (1, 1, 1, 64, 64), (1, 3,
             (1, 17, 30, 64, 192), (1, 68, 120, 128, 64)]
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 5, 8, 10, 12])
+@pytest.mark.parametrize("cfg", [0, 1, 5, 8, 10, 12, 19, 21])
 @pytest.mark.parametrize("case", UP_CASES)
 def test_upconv_folded_resize(case, cfg):
     """vm_conv3x3_up2x_nhwc (resize folded into four phase filters + exact border recompute) vs the oracle's

@@ -716,8 +716,9 @@ __global__ __launch_bounds__(512, 1) void conv3x3_glds(ConvArgs a) {
 // (granule order cc*9+tap is exactly the chunk-major packing) through an S-slot ring.  LDS-DMA with the
 // 64-byte-row XOR swizzle applied at the source (conflict-free fragment reads for any start row); counted
 // vmcnt per wave + one barrier per step; dummy (out-of-range) pieces past the end keep the counts uniform.
-template <int BN, int WM, int WN, int S, int TH_ = 8>
+template <int BN, int WM, int WN, int S, int TH_ = 8, int G_ = 1>
 struct PatchCfg {
+  static constexpr int G = G_;                               // taps per weight-ring slot (one barrier per slot)
   static constexpr int TH = TH_, TW = 32, BM = TH * TW;
   static constexpr int PW = TW + 2, PPIX = (TH + 2) * PW;  // 340 patch pixels
   static constexpr int NW = WM * WN, NT = 64 * NW;
@@ -731,13 +732,14 @@ struct PatchCfg {
   static constexpr int FP = TPM / 16, FC = TPN / 16;
   static constexpr int SR = 64 * 2 + 16;                    // epilogue staging row (one 64-channel slab, bf16)
   static constexpr int EPI = BM * SR;
-  static constexpr int MAIN = 2 * PB + S * WSLOT;
+  static constexpr int MAIN = 2 * PB + S * G * WSLOT;
   static constexpr int LDS = MAIN > EPI ? MAIN : EPI;
   static constexpr int IW = TW + 4, IPIX = (TH + 4) * IW;   // FIRST: 8-channel input patch (16 B per pixel)
   static constexpr int LDS_FIRST = MAIN + IPIX * 16 > EPI ? MAIN + IPIX * 16 : EPI;
   static_assert(TPN % 64 == 0, "whole 64-channel epilogue slabs per wave column");
   static_assert(TPM % 32 == 0 || TPM == 16, "pixel fragments stay inside one patch row");
-  static_assert(S >= 3 && S <= 9, "ring depth (the X group is counted in at most one window)");
+  static_assert(G == 1 || G == 3, "a slot holds one tap or one kernel row");
+  static_assert(G == 1 ? (S >= 3 && S <= 9) : (S >= 2 && S <= 4), "ring depth (the X group is counted in at most one window)");
 };
 
 // First conv (cin <= 8 -> 64 channels, + bias + relu) of the patch pixels, for the FIRST patch kernel.  The 8-channel
@@ -819,10 +821,10 @@ __device__ __forceinline__ void first_layer_patch(const ConvArgs& a, char* smem,
 // conv1_1 -> conv1_2): the prologue evaluates that first conv on the (TH+2) x (TW+2) patch straight into the two
 // granule buffers (zero outside the frame = the second conv's SAME padding), so the 64-channel activation never
 // touches HBM; the main loop then streams only weights.
-template <int BN, int WM, int WN, int S, int TH, int MINB, int UNR, bool PF, int ABL, bool FIRST>
+template <int BN, int WM, int WN, int S, int TH, int MINB, int UNR, bool PF, int ABL, bool FIRST, int G = 1>
 __global__ __launch_bounds__(64 * WM * WN) __attribute__((amdgpu_waves_per_eu(MINB * WM * WN / 4)))
 void conv3x3_patch(ConvArgs a) {
-  using C = PatchCfg<BN, WM, WN, S, TH>;
+  using C = PatchCfg<BN, WM, WN, S, TH, G>;
   using T = uint16_t;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int NW = C::NW, NT = C::NT, FP = C::FP, FC = C::FC, XPW = C::XPW, WPW = C::WPW;
@@ -883,11 +885,15 @@ void conv3x3_patch(ConvArgs a) {
     for (int i = 0; i < XPW; ++i)
       if (wave + i * NW < C::XP) glds16(xrs, lds0 + buf * C::PB + (wave + i * NW) * 1024, real ? xoff[i] + cc * 64 : OOB);
   };
-  auto issue_w = [&](int s, int slot) {
-    const bool real = s < nsteps;
+  auto issue_w = [&](int s, int slot) {  // ring step s = taps s*G .. s*G+G-1 (chunk-major K: consecutive 64 B)
 #pragma unroll
-    for (int i = 0; i < WPW; ++i)
-      if (wave + i * NW < C::WP) glds16(wrs, wring + slot * C::WSLOT + (wave + i * NW) * 1024, real ? woff[i] + s * 64 : OOB);
+    for (int g = 0; g < G; ++g) {
+      const bool real = s * G + g < nsteps;
+#pragma unroll
+      for (int i = 0; i < WPW; ++i)
+        if (wave + i * NW < C::WP)
+          glds16(wrs, wring + (slot * G + g) * C::WSLOT + (wave + i * NW) * 1024, real ? woff[i] + (s * G + g) * 64 : OOB);
+    }
   };
 
   int boff[FC], abase[FP];
@@ -907,7 +913,7 @@ void conv3x3_patch(ConvArgs a) {
     for (int j = 0; j < FP; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   auto frags = [&](uint4 (&av)[FC], uint4 (&bv)[FP], int slot, int buf, int tap) {
-    const char* wp = smem + slot * C::WSLOT;
+    const char* wp = smem + (slot * G + (G == 1 ? 0 : tap % G)) * C::WSLOT;
     const char* xp = smem + buf * C::PB;
 #pragma unroll
     for (int f = 0; f < FC; ++f) av[f] = *reinterpret_cast<const uint4*>(wp + boff[f]);
@@ -926,7 +932,39 @@ void conv3x3_patch(ConvArgs a) {
     asm volatile("" ::: "memory");
   };
 
-  if constexpr (PF) {
+  if constexpr (G > 1) {
+    // one ring slot = one kernel row (G = 3 taps): one barrier per row; inside the row the fragments of tap g+1 are
+    // read while tap g's MFMAs run (same slot and patch, no synchronisation needed)
+    static_assert(!PF && !FIRST && ABL == 0, "row-slot pipeline: plain configuration only");
+    constexpr int R = 9 / G;
+    issue_x(0, 0);
+#pragma unroll
+    for (int j = 0; j < S - 1; ++j) issue_w(j, j);
+    int slot = 0;
+    for (int cc = 0; cc < nch; ++cc) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int k = cc * R + r;
+        // in flight after W(k): S-2 younger row slots, plus the next patch when it was issued inside that window
+        sync((S - 2) * G * w_n + ((r >= 1 && r <= S - 2) ? x_n : 0));
+        if (r == 0) issue_x(cc + 1, (cc + 1) & 1);
+        int ns = slot + S - 1;
+        ns -= ns >= S ? S : 0;
+        issue_w(k + S - 1, ns);
+        uint4 av[2][FC], bv[2][FP];
+        frags(av[0], bv[0], slot, cc & 1, r * G);
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+          if (g + 1 < G) frags(av[(g + 1) & 1], bv[(g + 1) & 1], slot, cc & 1, r * G + g + 1);
+#pragma unroll
+          for (int fc = 0; fc < FC; ++fc)
+#pragma unroll
+            for (int fp = 0; fp < FP; ++fp) mma16<T>(av[g & 1][fc], bv[g & 1][fp], acc[fc][fp]);
+        }
+        slot = slot + 1 == S ? 0 : slot + 1;
+      }
+    }
+  } else if constexpr (PF) {
     // fragments of step s+1 are read right after the barrier of step s, while step s's MFMAs run; the ring
     // holds S steps (slot s%S is refilled with step s+S once every wave has its step-s fragments in registers)
     issue_x(0, 0);
@@ -1979,15 +2017,15 @@ static int launch_glds(ConvArgs& a, hipStream_t st) {
 }
 
 template <int BN, int WM, int WN, int S, int TH = 8, int MINB = 1, int UNR = 9, bool PF = false, int ABL = 0,
-          bool FIRST = false>
+          bool FIRST = false, int G = 1>
 static int launch_patch(ConvArgs& a, hipStream_t st) {
-  using C = PatchCfg<BN, WM, WN, S, TH>;
+  using C = PatchCfg<BN, WM, WN, S, TH, G>;
   static_assert(!(FIRST && PF), "FIRST uses the plain pipeline");
   constexpr int lds = FIRST ? C::LDS_FIRST : C::LDS;
   static bool attr_set = false;
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute(
-        reinterpret_cast<const void*>(&conv3x3_patch<BN, WM, WN, S, TH, MINB, UNR, PF, ABL, FIRST>),
+        reinterpret_cast<const void*>(&conv3x3_patch<BN, WM, WN, S, TH, MINB, UNR, PF, ABL, FIRST, G>),
         hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (e != hipSuccess) return fail(VM_EHIP, "hipFuncSetAttribute(patch): %s", hipGetErrorString(e));
     attr_set = true;
@@ -1997,10 +2035,10 @@ static int launch_patch(ConvArgs& a, hipStream_t st) {
   a.tiles_n = (a.cout + BN - 1) / BN;
   if (sp * a.tiles_n > 0x7fffffffL) return fail(VM_EUNSUPPORTED, "conv3x3: too many tiles");
   a.tiles_total = (int)(sp * a.tiles_n);
-  snprintf(g_last_kernel, sizeof g_last_kernel, "vm::conv3x3_patch<%d, %d, %d, %d, %d, %d, %d, %s, %d, %s>", BN, WM, WN,
-           S, TH, MINB, UNR, PF ? "true" : "false", ABL, FIRST ? "true" : "false");
-  hipLaunchKernelGGL((conv3x3_patch<BN, WM, WN, S, TH, MINB, UNR, PF, ABL, FIRST>), dim3(a.tiles_total), dim3(C::NT), lds,
-                     st, a);
+  snprintf(g_last_kernel, sizeof g_last_kernel, "vm::conv3x3_patch<%d, %d, %d, %d, %d, %d, %d, %s, %d, %s, %d>", BN, WM,
+           WN, S, TH, MINB, UNR, PF ? "true" : "false", ABL, FIRST ? "true" : "false", G);
+  hipLaunchKernelGGL((conv3x3_patch<BN, WM, WN, S, TH, MINB, UNR, PF, ABL, FIRST, G>), dim3(a.tiles_total), dim3(C::NT),
+                     lds, st, a);
   return check_launch("conv3x3_patch");
 }
 
@@ -2012,6 +2050,7 @@ static long g_conv_min_tiles = 128;
 static long g_glds_rb = 128;
 static long g_head_kernel = 0;
 static long g_patch_cfg = 0;
+static long g_patch_rowslot = 1;  // 0 = the per-tap-barrier dispatch of r01 (A/B runs)
 static long g_patch_ablate = 0;
 static long g_pair_kernel = 0;  // vm_conv3x3_pair_first_nhwc: 0 = persistent weights-resident kernel when cout == 64,
                                 // 1 = streaming patch kernel
@@ -2051,17 +2090,35 @@ static int dispatch_patch(ConvArgs& a, hipStream_t st) {
     case 16: return launch_patch<64, 8, 1, 6, 16>(a, st);
     case 17: return launch_patch<128, 8, 1, 4, 16>(a, st);
     case 18: return launch_patch<128, 4, 2, 4, 16>(a, st);
+    // one barrier per kernel row (3 taps per ring slot), tap g+1's fragments read under tap g's MFMAs
+    case 19: return launch_patch<64, 8, 1, 3, 8, 1, 9, false, 0, false, 3>(a, st);
+    case 20: return launch_patch<64, 4, 1, 3, 8, 2, 9, false, 0, false, 3>(a, st);
+    case 21: return launch_patch<128, 4, 1, 2, 4, 2, 9, false, 0, false, 3>(a, st);
+    case 22: return launch_patch<64, 8, 1, 2, 8, 1, 9, false, 0, false, 3>(a, st);
+    case 23: return launch_patch<128, 8, 1, 2, 8, 1, 9, false, 0, false, 3>(a, st);
+    case 24: return launch_patch<128, 4, 2, 2, 8, 1, 9, false, 0, false, 3>(a, st);
+    case 25: return launch_patch<64, 4, 1, 2, 4, 2, 9, false, 0, false, 3>(a, st);
     default: break;
   }
-  // measured inside the UNetVideo 1080p forward (bench.py --layers): 4 waves of 64 px x 128 channels (2 blocks
-  // per CU) win for cin >= 256, cout >= 128 when the grid holds >= ~2 full rounds of blocks; otherwise 8 waves of
-  // 32 px x 64 channels (more, smaller blocks)
+  // measured per layer inside the UNetVideo 1080p forward (scripts/sweep.sh, profiles/r01_patch_cfg_sweep.txt):
+  // 8 waves of 32 px x 64 channels with one barrier per kernel row (3 taps per ring slot) everywhere, except
+  // 4 waves of 64 px x 128 channels (2 blocks per CU, one barrier per tap) for cin >= 512, cout >= 128 on grids
+  // of >= ~2 full rounds of blocks, a 3-slot ring for the largest grids, 4 x 32 px tiles for grids under 2 rounds.
+  // Same-box A/B of the whole forward (bench.py --option patch_rowslot=0|1): 292.4 -> 306.8 frames/s
   const long N = a.M / ((long)a.H * a.W);
   const long sp = N * ((a.H + 7) / 8) * ((a.W + 31) / 32);
-  if (a.cout >= 128 && a.cin_pad >= 256 && sp * ((a.cout + 127) / 128) >= 1000)
+  const long blocks64 = sp * ((a.cout + 63) / 64);
+  if (!g_patch_rowslot) {
+    if (a.cout >= 128 && a.cin_pad >= 256 && sp * ((a.cout + 127) / 128) >= 1000)
+      return launch_patch<128, 4, 1, 4, 8, 2>(a, st);
+    if (blocks64 < 512) return launch_patch<64, 4, 1, 6, 4>(a, st);
+    return launch_patch<64, 8, 1, 6>(a, st);
+  }
+  if (a.cout >= 128 && a.cin_pad >= 512 && sp * ((a.cout + 127) / 128) >= 1000)
     return launch_patch<128, 4, 1, 4, 8, 2>(a, st);
-  if (sp * ((a.cout + 63) / 64) < 512) return launch_patch<64, 4, 1, 6, 4>(a, st);  // small grids: 8 x 4 px tiles
-  return launch_patch<64, 8, 1, 6>(a, st);
+  if (blocks64 >= 8000) return launch_patch<64, 8, 1, 3, 8, 1, 9, false, 0, false, 3>(a, st);
+  if (blocks64 < 512) return launch_patch<64, 4, 1, 2, 4, 2, 9, false, 0, false, 3>(a, st);  // L5: 4 x 32 px tiles
+  return launch_patch<64, 8, 1, 2, 8, 1, 9, false, 0, false, 3>(a, st);
 }
 
 template <typename T, bool FAST>
@@ -2126,8 +2183,13 @@ extern "C" int vm_set_option(const char* key, long value) {
     return VM_OK;
   }
   if (!strcmp(key, "patch_cfg")) {
-    if (value < 0 || value > 18) return fail(VM_EINVAL, "patch_cfg must be 0..18");
+    if (value < 0 || value > 25) return fail(VM_EINVAL, "patch_cfg must be 0..25");
     g_patch_cfg = value;
+    return VM_OK;
+  }
+  if (!strcmp(key, "patch_rowslot")) {
+    if (value < 0 || value > 1) return fail(VM_EINVAL, "patch_rowslot must be 0 or 1");
+    g_patch_rowslot = value;
     return VM_OK;
   }
   if (!strcmp(key, "pair_kernel")) {
