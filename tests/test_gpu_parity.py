@@ -66,7 +66,7 @@ def conv_kernel(request):
     _lib.set_option("conv_kernel", 0)
 
 
-@pytest.mark.parametrize("cfg", list(range(1, 23)))
+@pytest.mark.parametrize("cfg", list(range(1, 27)))
 @pytest.mark.parametrize("case", [(1, 9, 33, 64, 64, "relu"), (2, 17, 70, 128, 128, "none"), (1, 20, 45, 96, 192, "relu"),
                                   (1, 8, 32, 32, 64, "sigmoid"), (1, 3, 5, 256, 128, "relu")])
 def test_patch_kernel_configs(case, cfg):

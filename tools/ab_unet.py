@@ -1,0 +1,43 @@
+"""Same-box A/B of UNetVideo forward variants (graph replay, 1080p bf16): python tools/ab_unet.py"""
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(REPO, "video-matting_amd"), REPO]
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+from vmatting import unet  # noqa: E402
+from vmatting.weights import synthetic_vgg16  # noqa: E402
+
+VARIANTS = {
+    "default": {},
+    "fold_up2": {"fold_upconv": ("upconv_2", "upconv_3", "upconv_4")},
+}
+
+
+def run(name, steps=30):
+    np.random.seed(0)
+    m = unet.UNetVideo(synthetic_vgg16(0), dtype="bf16", device="cuda")
+    for k, v in VARIANTS[name].items():
+        setattr(m, k, v)
+    m.prepare()
+    x = bench.synth_frames(1, 1080, 1920, 0, "cuda")
+    g = m.capture(x)
+    for _ in range(3):
+        g.replay()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        g.replay()
+    torch.cuda.synchronize()
+    return 1000 * (time.perf_counter() - t0) / steps
+
+
+if __name__ == "__main__":
+    names = sys.argv[1:] or list(VARIANTS)
+    for rep in range(2):
+        for n in names:
+            print("%-10s %.4f ms/frame" % (n, run(n)), flush=True)

@@ -1884,14 +1884,21 @@ struct BorderArgs {
 
 // Border pixels of the folded upconv, computed the unfused way: the 9 resized taps (TF1 legacy bilinear in f32,
 // rounded to bf16 as vm_resize_bilinear_tf1_nhwc stores them; zero outside the 2H x 2W frame) of 16 pixels are
-// staged per 32-channel granule, and each wave runs 9 MFMAs (one per tap) for its 16 output channels.
+// staged per 32-channel granule, and 36 MFMAs (9 taps x 4 groups of 16 output channels) consume them.  The granule
+// loop is spread over the 4 waves (wave w takes granules w, w+4, ...; its own staging buffer, so no block barrier
+// per granule), and the 4 partial sums are added in LDS at the end: the work per block is a few microseconds of
+// latency, so splitting K across waves is what shortens it.
+__device__ __forceinline__ uint4 sel3(int i, uint4 a, uint4 b, uint4 c) { return i == 0 ? a : (i == 1 ? b : c); }
+
 __global__ __launch_bounds__(256) void conv3x3_up2x_border(BorderArgs a) {
   using T = uint16_t;
-  __shared__ __attribute__((aligned(16))) char stg[9 * 16 * 64];
+  constexpr int RS = 64 + 4;  // reduction row (f32)
+  __shared__ __attribute__((aligned(16))) char stg[4][9 * 16 * 64];
+  __shared__ __attribute__((aligned(16))) float red[4][16 * RS];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int OH = 2 * a.H, OW = 2 * a.W;
   const long total = (long)a.nframes * a.nb, b0 = (long)blockIdx.x * 16;
-  const int co0 = blockIdx.y * 64 + wave * 16;
+  const int cob = blockIdx.y * 64;
   auto decode = [&](long b, int& n, int& oy, int& ox) {
     n = (int)(b / a.nb);
     const int r = (int)(b - (long)n * a.nb);
@@ -1902,68 +1909,95 @@ __global__ __launch_bounds__(256) void conv3x3_up2x_border(BorderArgs a) {
   };
   const T* xb = reinterpret_cast<const T*>(a.x) + a.x_coff;
   const T* wb = reinterpret_cast<const T*>(a.w);
-  f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int cc = 0; cc < a.nch; ++cc) {
-    uint4 wf[9];
-    const bool wok = co0 + (lane & 15) < a.cout;
+  char* my = stg[wave];
+  f32x4 acc[4];
 #pragma unroll
-    for (int tap = 0; tap < 9; ++tap)
-      wf[tap] = wok ? *reinterpret_cast<const uint4*>(wb + (long)(co0 + (lane & 15)) * a.K_pad + (cc * 9 + tap) * 32 +
-                                                      (lane >> 4) * 8)
-                    : make_uint4(0, 0, 0, 0);
-    for (int it = tid; it < 9 * 64; it += 256) {
-      const int tap = it >> 6, px = (it >> 2) & 15, q = it & 3;
+  for (int g = 0; g < 4; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // lane -> (pixel, 8-channel quarter of the granule); its 9 taps are the 3 x 3 neighbourhood of the border pixel
+  // in the resized frame, which reads at most a 3 x 3 block of the low-res frame: 9 gathers, all in flight at once
+  const int px = (lane >> 2) & 15, q = lane & 3;
+  const bool live = b0 + px < total;
+  int pn = 0, oy = 0, ox = 0;
+  if (live) decode(b0 + px, pn, oy, ox);
+  const int ry0 = max(oy - 1, 0) >> 1, cx0 = max(ox - 1, 0) >> 1;
+  for (int cc = wave; cc < a.nch; cc += 4) {  // wave-uniform trip count: no block barrier inside
+    const T* xr = xb + ((long)pn * a.H) * a.W * (long)a.x_cstride + cc * 32 + q * 8;
+    auto ld = [&](int i, int j) -> uint4 {
+      const int yy = min(ry0 + i, a.H - 1), xx = min(cx0 + j, a.W - 1);
+      return live ? *reinterpret_cast<const uint4*>(xr + ((long)yy * a.W + xx) * a.x_cstride) : make_uint4(0, 0, 0, 0);
+    };
+    const uint4 b00 = ld(0, 0), b01 = ld(0, 1), b02 = ld(0, 2);
+    const uint4 b10 = ld(1, 0), b11 = ld(1, 1), b12 = ld(1, 2);
+    const uint4 b20 = ld(2, 0), b21 = ld(2, 1), b22 = ld(2, 2);
+    auto pick = [=](int i, int j) -> uint4 {  // the 3 x 3 block entry (i, j) for runtime i, j: selects, no indexing
+      return sel3(i, sel3(j, b00, b01, b02), sel3(j, b10, b11, b12), sel3(j, b20, b21, b22));
+    };
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
       float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-      if (b0 + px < total) {
-        int n, oy, ox;
-        decode(b0 + px, n, oy, ox);
-        const int yy = oy + tap / 3 - 1, xx = ox + tap % 3 - 1;
-        if ((unsigned)yy < (unsigned)OH && (unsigned)xx < (unsigned)OW) {
+      const int yy = oy + tap / 3 - 1, xx = ox + tap % 3 - 1;
+      if (live && (unsigned)yy < (unsigned)OH && (unsigned)xx < (unsigned)OW) {
 #pragma clang fp contract(off)
-          const float sy = (float)yy * 0.5f, sx = (float)xx * 0.5f;
-          const float fy0 = floorf(sy), fx0 = floorf(sx);
-          const int y0 = (int)fy0, x0 = (int)fx0, y1 = min(y0 + 1, a.H - 1), x1 = min(x0 + 1, a.W - 1);
-          const float ly = sy - fy0, lx = sx - fx0;
-          const int c = cc * 32 + q * 8;
-          const long r0 = ((long)n * a.H + y0) * a.W, r1 = ((long)n * a.H + y1) * a.W;
-          float tl[8], tr[8], bl[8], br[8];
-          Chunk<T>::unpack(*reinterpret_cast<const uint4*>(xb + (r0 + x0) * a.x_cstride + c), tl);
-          Chunk<T>::unpack(*reinterpret_cast<const uint4*>(xb + (r0 + x1) * a.x_cstride + c), tr);
-          Chunk<T>::unpack(*reinterpret_cast<const uint4*>(xb + (r1 + x0) * a.x_cstride + c), bl);
-          Chunk<T>::unpack(*reinterpret_cast<const uint4*>(xb + (r1 + x1) * a.x_cstride + c), br);
+        const float sy = (float)yy * 0.5f, sx = (float)xx * 0.5f;
+        const float fy0 = floorf(sy), fx0 = floorf(sx);
+        const int y0 = (int)fy0, x0 = (int)fx0, y1 = min(y0 + 1, a.H - 1), x1 = min(x0 + 1, a.W - 1);
+        const float ly = sy - fy0, lx = sx - fx0;
+        float tl[8], tr[8], bl[8], br[8];
+        Chunk<T>::unpack(pick(y0 - ry0, x0 - cx0), tl);
+        Chunk<T>::unpack(pick(y0 - ry0, x1 - cx0), tr);
+        Chunk<T>::unpack(pick(y1 - ry0, x0 - cx0), bl);
+        Chunk<T>::unpack(pick(y1 - ry0, x1 - cx0), br);
 #pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const float top = tl[e] + (tr[e] - tl[e]) * lx;
-            const float bot = bl[e] + (br[e] - bl[e]) * lx;
-            o[e] = top + (bot - top) * ly;
-          }
+        for (int e = 0; e < 8; ++e) {
+          const float top = tl[e] + (tr[e] - tl[e]) * lx;
+          const float bot = bl[e] + (br[e] - bl[e]) * lx;
+          o[e] = top + (bot - top) * ly;
         }
       }
-      *reinterpret_cast<uint4*>(stg + (tap * 16 + px) * 64 + q * 16) = Chunk<T>::pack(o);
+      *reinterpret_cast<uint4*>(my + (tap * 16 + px) * 64 + q * 16) = Chunk<T>::pack(o);
     }
-    __syncthreads();
+    // the wave reads what its own lanes wrote: complete the LDS stores before the fragment loads
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
-    for (int tap = 0; tap < 9; ++tap)
-      mma16<T>(wf[tap], *reinterpret_cast<const uint4*>(stg + (tap * 16 + (lane & 15)) * 64 + (lane >> 4) * 16), acc);
-    __syncthreads();
+    for (int g = 0; g < 4; ++g) {
+      const T* wrow = wb + (long)(cob + g * 16 + (lane & 15)) * a.K_pad + cc * 9 * 32 + (lane >> 4) * 8;
+      uint4 wf[9];
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) wf[tap] = *reinterpret_cast<const uint4*>(wrow + tap * 32);
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap)
+        mma16<T>(wf[tap], *reinterpret_cast<const uint4*>(my + (tap * 16 + (lane & 15)) * 64 + (lane >> 4) * 16),
+                 acc[g]);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
-  // lane holds output channels co0 + 4*(lane>>4) + j of border pixel b0 + (lane&15)
-  const long b = b0 + (lane & 15);
+  // lane holds output channels cob + g*16 + 4*(lane>>4) + j of border pixel b0 + (lane&15)
+#pragma unroll
+  for (int g = 0; g < 4; ++g)
+    *reinterpret_cast<float4*>(&red[wave][(lane & 15) * RS + g * 16 + 4 * (lane >> 4)]) =
+        make_float4(acc[g][0], acc[g][1], acc[g][2], acc[g][3]);
+  __syncthreads();
+  const int ep = tid >> 4, cq = (tid & 15) * 4;
+  const long b = b0 + ep;
   if (b >= total) return;
-  int n, oy, ox;
-  decode(b, n, oy, ox);
-  const int cq = co0 + 4 * (lane >> 4);
-  if (cq >= a.cout) return;
+  int n, ey, ex;
+  decode(b, n, ey, ex);
   float v[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const int co = min(cq + j, a.cout - 1);
+    const int co = cob + cq + j;
+    const float sum = ((red[0][ep * RS + cq + j] + red[1][ep * RS + cq + j]) + red[2][ep * RS + cq + j]) +
+                      red[3][ep * RS + cq + j];
     const float sc = a.scale ? a.scale[co] : 1.f;
-    v[j] = fmaf(acc[j], sc, (a.bias ? a.bias[co] : 0.f) * sc + (a.shift ? a.shift[co] : 0.f));
+    v[j] = fmaf(sum, sc, (a.bias ? a.bias[co] : 0.f) * sc + (a.shift ? a.shift[co] : 0.f));
     if (a.act == VM_ACT_RELU) v[j] = fmaxf(v[j], 0.f);
     else if (a.act == VM_ACT_SIGMOID) v[j] = sigmoid_precise(v[j]);
   }
-  T* yp = reinterpret_cast<T*>(a.y) + (((long)n * OH + oy) * OW + ox) * (long)a.y_cstride + a.y_coff + cq;
+  T* yp = reinterpret_cast<T*>(a.y) + (((long)n * OH + ey) * OW + ex) * (long)a.y_cstride + a.y_coff + cob + cq;
   uint2 pk;
   pk.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
   pk.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
@@ -2098,6 +2132,8 @@ static int dispatch_patch(ConvArgs& a, hipStream_t st) {
     case 23: return launch_patch<128, 8, 1, 2, 8, 1, 9, false, 0, false, 3>(a, st);
     case 24: return launch_patch<128, 4, 2, 2, 8, 1, 9, false, 0, false, 3>(a, st);
     case 25: return launch_patch<64, 4, 1, 2, 4, 2, 9, false, 0, false, 3>(a, st);
+    // one 8 x 32 px patch shared by 256 output channels (8 waves of 64 px x 128 channels, one block per CU)
+    case 26: return launch_patch<256, 4, 2, 2, 8, 1, 9, false, 0, false, 3>(a, st);
     default: break;
   }
   // measured per layer inside the UNetVideo 1080p forward (scripts/sweep.sh, profiles/r01_patch_cfg_sweep.txt):
@@ -2183,7 +2219,7 @@ extern "C" int vm_set_option(const char* key, long value) {
     return VM_OK;
   }
   if (!strcmp(key, "patch_cfg")) {
-    if (value < 0 || value > 25) return fail(VM_EINVAL, "patch_cfg must be 0..25");
+    if (value < 0 || value > 26) return fail(VM_EINVAL, "patch_cfg must be 0..26");
     g_patch_cfg = value;
     return VM_OK;
   }
