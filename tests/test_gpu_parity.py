@@ -227,7 +227,9 @@ def test_conv_pair_first_bit_exact(shape, pool, xdtype, pair_kernel):
     finally:
         _lib.set_option("pair_kernel", 0)
     persist = pair_kernel == 0 and cout2 == 64
-    assert name == "vm::conv3x3_pair_persist" if persist else name.endswith("true>"), name
+    # conv3x3_patch<BN, WM, WN, S, TH, MINB, UNR, PF, ABL, FIRST, G>: the fused pair has FIRST = true
+    first = name.split("<", 1)[-1].rstrip(">").split(",")[9].strip() if "<" in name else ""
+    assert name == "vm::conv3x3_pair_persist" if persist else first == "true", name
     m = ops.conv3x3(x8[..., :7], pc1, "relu")
     y = ops.conv3x3(m, pc2, "relu")
     assert torch.equal(cat[..., cout2:], y)
