@@ -59,6 +59,44 @@ def synth_frames(n, h, w, first, device):
     return out
 
 
+def video_batch(graphed, n_frames, h, w, rank, world, dev):
+    """BASELINE config 4: ``n_frames`` synthetic 1080p frames (seeds 1234..) sharded frame-parallel in contiguous
+    blocks, each rank runs its block through the captured forward, then ONE all-gather (RCCL ring over xGMI) hands
+    every rank the whole [n_frames, H, W, 1] fp32 matte batch.  Timed between barriers, max over ranks."""
+    a, b = parallel.shard_range(n_frames, rank, world)
+    frames = synth_frames(b - a, h, w, a, dev)
+    out_shape = tuple(graphed.output.shape[1:])
+    local = torch.empty((b - a,) + out_shape, dtype=graphed.output.dtype, device=dev)
+    mx = max(q - p for p, q in (parallel.shard_range(n_frames, r, world) for r in range(world)))
+    recv = torch.empty((world * mx,) + out_shape, dtype=local.dtype, device=dev) if world > 1 else None
+    graphed(frames[:1])  # warm
+    if world > 1:
+        parallel.gather_frames(local, n_frames, out=recv)  # warm the communicator
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(b - a):
+        local[i].copy_(graphed(frames[i:i + 1])[0])
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    full = parallel.gather_frames(local, n_frames, out=recv)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t2 = time.perf_counter()
+    ts = torch.tensor([t2 - t0, t1 - t0, t2 - t1], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(ts, op=dist.ReduceOp.MAX)
+    total, comp, gath = (float(v) for v in ts.tolist())
+    assert full.shape[0] == n_frames
+    return {"workload": "config 4: %d synthetic %dx%d frames sharded frame-parallel, mattes all-gathered to every rank"
+                        % (n_frames, w, h),
+            "frames": n_frames, "frames_per_s": round(n_frames / total, 3), "ms_total": round(1e3 * total, 3),
+            "ms_compute_max_rank": round(1e3 * comp, 3), "ms_all_gather": round(1e3 * gath, 3),
+            "all_gather_bytes": int(full.numel() * full.element_size()),
+            "includes": "per-frame input copy into the graph's static buffer + graph replay + matte copy-out"}
+
+
 def cpu_baseline(h, w, sample_h, sample_w):
     """The oracle (numpy f32 restatement of unet.py) timed on host cores on a bounded sample."""
     from oracle import models as om
@@ -211,6 +249,8 @@ def main():
     ap.add_argument("--layers", action="store_true", help="per-conv timing breakdown on stderr")
     ap.add_argument("--no-graph", action="store_true", help="time eager launches instead of the captured HIP graph")
     ap.add_argument("--no-loader", action="store_true", help="skip the training-sample loader record (rank 0, N=1)")
+    ap.add_argument("--video-frames", type=int, default=256,
+                    help="config-4 record: frames sharded over the ranks + matte all-gather (0 = skip)")
     ap.add_argument("--option", action="append", default=[], metavar="KEY=VALUE",
                     help="vm_set_option kernel knob before the run (A/B comparisons), repeatable")
     args = ap.parse_args()
@@ -238,7 +278,8 @@ def main():
 
     # the timed step is the whole forward replayed from a HIP graph (captured once: one host call per step, no
     # per-launch host cost); --no-graph times the eager launch sequence instead
-    step = model.capture(x).replay if not args.no_graph else (lambda: model.forward(x))
+    graphed = model.capture(x) if not args.no_graph else None
+    step = graphed.replay if graphed is not None else (lambda: model.forward(x))
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -263,6 +304,10 @@ def main():
             model.forward(x)
         torch.cuda.synchronize()
         ops.conv_profile(False)
+
+    video = None
+    if args.video_frames > 0 and graphed is not None and args.batch == 1:
+        video = video_batch(graphed, args.video_frames, H, W, rank, world, dev)
 
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -297,6 +342,8 @@ def main():
             rec["hbm"] = {"bytes_per_frame": int(bpf), "achieved_gbps_per_gpu": rec["achieved_hbm_gbps"],
                           "peak_gbps": PEAK_HBM_GBPS, "frac": round(bpf * value / world / 1e9 / PEAK_HBM_GBPS, 4),
                           "source": os.path.relpath(src, REPO)}
+        if video:
+            rec["video_batch"] = video
         if world == 1 and not args.no_cpu_baseline:
             sh, sw = (int(v) for v in args.cpu_sample.split("x"))
             rec["cpu_baseline"] = cpu_baseline(H, W, sh, sw)

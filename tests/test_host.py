@@ -102,6 +102,11 @@ def _dist_worker(rank, world, port, q):
         local = torch.arange(a, b, dtype=torch.float32)[:, None, None, None].expand(b - a, 2, 3, 1) * 10
         full = parallel.gather_frames(local.contiguous(), n)
         ok_g = full.shape == (7, 2, 3, 1) and bool(torch.equal(full[:, 0, 0, 0], torch.arange(7.) * 10))
+        # even split (config 4's 256 frames / P): gathered straight into the receive buffer
+        a, b = parallel.shard_range(8, rank, world)
+        local = torch.arange(a, b, dtype=torch.float32)[:, None, None, None].expand(b - a, 2, 3, 1) * 10
+        full = parallel.gather_frames(local.contiguous(), 8)
+        ok_g = ok_g and full.shape == (8, 2, 3, 1) and bool(torch.equal(full[:, 1, 2, 0], torch.arange(8.) * 10))
         q.put((rank, ok_b, ok_g))
     finally:
         dist.destroy_process_group()

@@ -49,15 +49,25 @@ def broadcast_tensors(tensors, src=0):
     return tensors
 
 
-def gather_frames(local, n_frames):
-    """All-gather per-rank frame blocks (contiguous, possibly uneven) into the full [n_frames, ...] batch."""
+def gather_frames(local, n_frames, out=None):
+    """All-gather per-rank frame blocks (contiguous, possibly uneven) into the full [n_frames, ...] batch.
+
+    One ``all_gather_into_tensor`` (RCCL ring over xGMI) into a [world * max_block, ...] buffer; with an even
+    split the result is that buffer itself (no extra copy), otherwise the padded rows are squeezed out.
+    ``out`` may pass a preallocated [world * max_block, ...] receive buffer."""
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
         return local
     world = dist.get_world_size()
     sizes = [shard_range(n_frames, r, world) for r in range(world)]
     mx = max(b - a for a, b in sizes)
-    pad = torch.zeros((mx,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
-    pad[:local.shape[0]] = local
-    parts = [torch.empty_like(pad) for _ in range(world)]
-    dist.all_gather(parts, pad)
-    return torch.cat([p[:b - a] for p, (a, b) in zip(parts, sizes)], dim=0)
+    if local.shape[0] != mx:
+        pad = torch.zeros((mx,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+        pad[:local.shape[0]] = local
+    else:
+        pad = local.contiguous()
+    if out is None:
+        out = torch.empty((world * mx,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+    dist.all_gather_into_tensor(out, pad)
+    if all(b - a == mx for a, b in sizes):
+        return out
+    return torch.cat([out[r * mx:r * mx + (b - a)] for r, (a, b) in enumerate(sizes)], dim=0)
