@@ -45,9 +45,9 @@ def load_reference():
     np.float = float  # numpy<1.24 aliases used by reader.py:74, flow.py:38, loader.py:43
     np.int = int
     sys.path.insert(0, REF)
-    import unet, unet_simple, small, refine, flow, reader, train  # noqa: E401
+    import unet, unet_simple, small, refine, flow, reader, train, tps, augmentation  # noqa: E401
     return types.SimpleNamespace(unet=unet, unet_simple=unet_simple, small=small, refine=refine,
-                                 flow=flow, reader=reader, train=train)
+                                 flow=flow, reader=reader, train=train, tps=tps, augmentation=augmentation)
 
 
 _VGG = {}
@@ -334,6 +334,63 @@ def gen_loader(R, out):
     out["loader_calls"] = d
 
 
+def gen_tps(R, out):
+    """tps.warp_images / tps.deform run for REAL (numpy + scipy 1.15.3 ndimage.map_coordinates; only the unused
+    `import cv2` of tps.py resolves to the shim)."""
+    d = {}
+    fgimg = load_png_bgra(os.path.join(REF, "test_data", "in0062.png"))
+    img = resize_u8(np.ascontiguousarray(fgimg[:, :, :3]), 70, 45)          # [45, 70, 3] u8
+    alpha = resize_u8(np.ascontiguousarray(fgimg[:, :, 3]), 70, 45) / 255.  # [45, 70] f64
+    rs = np.random.RandomState(11)
+    cases = [  # (name, region, approximate_grid, order, grid seed, grid h/w)
+        ("a", (0, 0, 45, 70), 2, 1, 3),
+        ("b", (0, 0, 33, 47), 1, 1, 4),
+        ("c", (5, 3, 40, 60), 3, 0, 5),
+        ("d", (0, 0, 45, 70), 2.5, 1, 6),
+    ]
+    for name, region, ag, order, seed in cases:
+        np.random.seed(seed)
+        h, w = region[2], region[3]
+        grid, new_grid = R.augmentation.deform_grid(h, w)
+        planes = [img[:, :, 0], img[:, :, 1], img[:, :, 2], alpha, (rs.rand(45, 70) * 4 - 1).astype(np.float32)]
+        res = R.tps.warp_images(grid, new_grid, planes, region, interpolation_order=order, approximate_grid=ag)
+        d[name + "_from"], d[name + "_to"] = grid, new_grid
+        d[name + "_region"], d[name + "_ag"], d[name + "_order"] = np.array(region), np.array(ag), np.array(order)
+        d[name + "_f32_in"] = planes[4]
+        d[name + "_u8"] = np.stack(res[:3], axis=-1)
+        d[name + "_f64"] = res[3]
+        d[name + "_f32"] = res[4]
+    np.random.seed(21)
+    d["deform_out"] = R.tps.deform(img)
+    d["img"], d["alpha"] = img, alpha
+    out["tps"] = d
+
+
+def gen_augment(R, out):
+    """augmentation.augment (augmentation.py:101-135) run verbatim: its np.random draws, deform_grid, tps.py
+    (real scipy) and the cv2 calls (warpAffine / getRotationMatrix2D / cvtColor HSV from tfshim)."""
+    d = {}
+    fgimg = load_png_bgra(os.path.join(REF, "test_data", "in0062.png"))
+    bgimg = load_png_bgra(os.path.join(REF, "test_data", "cmp1.png"))
+    for i, (h, w, seed) in enumerate([(48, 64, 31), (57, 83, 32)]):
+        fg = resize_u8(np.ascontiguousarray(fgimg[:, :, :3]), w, h)
+        alpha = resize_u8(np.ascontiguousarray(fgimg[:, :, 3]), w, h) / 255.
+        bg = resize_u8(np.ascontiguousarray(bgimg[:, :, :3]), w, h)
+        np.random.seed(seed)
+        nfg, nbg, nal = R.augmentation.augment(fg, bg, alpha)
+        d["fg%d" % i], d["bg%d" % i], d["alpha%d" % i], d["seed%d" % i] = fg, bg, alpha, np.array(seed)
+        d["new_fg%d" % i], d["new_bg%d" % i], d["new_alpha%d" % i] = nfg, nbg, nal
+        d["next_draw%d" % i] = np.array(np.random.randint(0, 1 << 30))
+    # change_illumination alone over every HSV corner case
+    rs = np.random.RandomState(5)
+    px = rs.randint(0, 256, (16, 40, 3)).astype(np.uint8)
+    px[0, :6] = [[0, 0, 0], [255, 255, 255], [7, 7, 7], [0, 0, 255], [255, 0, 0], [3, 250, 3]]
+    d["illum_in"] = px
+    d["illum_abc"] = np.array([1.03, 0.81, -0.05])
+    d["illum_out"] = R.augmentation.change_illumination(px, 1.03, 0.81, -0.05)
+    out["augment"] = d
+
+
 def main():
     np.load = _fake_load
     R = load_reference()
@@ -352,6 +409,8 @@ def main():
     gen_loss(R, out)
     gen_unet_simple(R, out)
     gen_loader(R, out)
+    gen_tps(R, out)
+    gen_augment(R, out)
     for name, d in out.items():
         np.savez_compressed(os.path.join(HERE, name + ".npz"), **d)
         print("wrote", name, os.path.getsize(os.path.join(HERE, name + ".npz")))

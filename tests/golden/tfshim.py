@@ -208,7 +208,7 @@ def make_tf():
     return tf
 
 
-# ------------------------------------------------------------------ OpenCV stand-in (remap only)
+# ------------------------------------------------------------------ OpenCV stand-in (remap, resize, imread, warpAffine, cvtColor HSV)
 
 INTER_LINEAR = 1
 
@@ -340,6 +340,128 @@ def imread(path, flags=1):
     return np.ascontiguousarray(np.asarray(im.convert("RGB"))[:, :, ::-1])
 
 
+# warpAffine / getRotationMatrix2D / cvtColor(HSV) — written after OpenCV 3.x imgwarp.cpp (WarpAffineInvoker +
+# remapBilinear) and color.cpp (RGB2HSV_b, HSV2RGB_b/_f), per pixel in C order; independent of oracle/augment.py.
+
+def _cv_round(v):
+    return int(np.rint(v))  # cvRound: round half to even
+
+
+def warpAffine(src, M, dsize, flags=INTER_LINEAR):
+    assert flags == INTER_LINEAR
+    src = np.asarray(src)
+    assert src.dtype in (np.uint8, np.float64, np.float32), src.dtype
+    m = [float(v) for v in np.asarray(M, np.float64).reshape(6)]
+    D = m[0] * m[4] - m[1] * m[3]
+    D = 1. / D if D != 0 else 0.
+    A11, A22 = m[4] * D, m[0] * D
+    m[0] = A11
+    m[1] *= -D
+    m[3] *= -D
+    m[4] = A22
+    b1 = -m[0] * m[2] - m[1] * m[5]
+    b2 = -m[3] * m[2] - m[4] * m[5]
+    m[2], m[5] = b1, b2
+    W, H = dsize
+    sh, sw = src.shape[:2]
+    cn = 1 if src.ndim == 2 else src.shape[2]
+    S = src.reshape(sh, sw, cn)
+    dst = np.zeros((H, W, cn), src.dtype)
+    adelta = [_cv_round(m[0] * x * 1024) for x in range(W)]
+    bdelta = [_cv_round(m[3] * x * 1024) for x in range(W)]
+    for y in range(H):
+        X0 = _cv_round((m[1] * y + m[2]) * 1024) + 16
+        Y0 = _cv_round((m[4] * y + m[5]) * 1024) + 16
+        for x in range(W):
+            X = (X0 + adelta[x]) >> 5
+            Y = (Y0 + bdelta[x]) >> 5
+            sx = max(-32768, min(32767, X >> 5))
+            sy = max(-32768, min(32767, Y >> 5))
+            fx, fy = X & 31, Y & 31
+            if sx >= sw or sx + 1 < 0 or sy >= sh or sy + 1 < 0:
+                continue  # BORDER_CONSTANT: the whole pixel is the border value 0
+            for k in range(cn):
+                v = [S[yy, xx, k] if (0 <= yy < sh and 0 <= xx < sw) else 0
+                     for yy, xx in ((sy, sx), (sy, sx + 1), (sy + 1, sx), (sy + 1, sx + 1))]
+                if src.dtype == np.uint8:
+                    wt = [(32 - fy) * (32 - fx) * 32, (32 - fy) * fx * 32, fy * (32 - fx) * 32, fy * fx * 32]
+                    t = int(v[0]) * wt[0] + int(v[1]) * wt[1] + int(v[2]) * wt[2] + int(v[3]) * wt[3]
+                    dst[y, x, k] = max(0, min(255, (t + (1 << 14)) >> 15))
+                else:
+                    ty = (np.float32(1 - fy / 32.), np.float32(fy / 32.))
+                    tx = (np.float32(1 - fx / 32.), np.float32(fx / 32.))
+                    wt = [float(ty[0] * tx[0]), float(ty[0] * tx[1]), float(ty[1] * tx[0]), float(ty[1] * tx[1])]
+                    dst[y, x, k] = float(v[0]) * wt[0] + float(v[1]) * wt[1] + float(v[2]) * wt[2] + float(v[3]) * wt[3]
+    return dst[..., 0] if src.ndim == 2 else dst
+
+
+def getRotationMatrix2D(center, angle, scale):
+    import math
+    cx, cy = float(np.float32(center[0])), float(np.float32(center[1]))
+    angle = angle * (math.pi / 180)
+    alpha = math.cos(angle) * scale
+    beta = math.sin(angle) * scale
+    return np.array([[alpha, beta, (1 - alpha) * cx - beta * cy], [-beta, alpha, beta * cx + (1 - alpha) * cy]])
+
+
+COLOR_BGR2HSV = 40
+COLOR_HSV2BGR = 54
+
+
+def _hsv_tables():
+    sdiv = [0] * 256
+    hdiv = [0] * 256
+    for i in range(1, 256):
+        sdiv[i] = _cv_round((255 << 12) / (1. * i))
+        hdiv[i] = _cv_round((180 << 12) / (6. * i))
+    return sdiv, hdiv
+
+
+def cvtColor(src, code):
+    src = np.asarray(src)
+    assert src.dtype == np.uint8 and src.ndim == 3 and src.shape[2] == 3
+    out = np.zeros_like(src)
+    if code == COLOR_BGR2HSV:
+        sdiv, hdiv = _hsv_tables()
+        for (y, x), _ in np.ndenumerate(src[..., 0]):
+            b, g, r = (int(v) for v in src[y, x])
+            v = max(b, g, r)
+            vmin = min(b, g, r)
+            diff = v - vmin
+            vr = -1 if v == r else 0
+            vg = -1 if v == g else 0
+            s = (diff * sdiv[v] + (1 << 11)) >> 12
+            h = (vr & (g - b)) + (~vr & ((vg & (b - r + 2 * diff)) + ((~vg) & (r - g + 4 * diff))))
+            h = (h * hdiv[diff] + (1 << 11)) >> 12
+            h += 180 if h < 0 else 0
+            out[y, x] = (h, s, v)
+        return out
+    assert code == COLOR_HSV2BGR
+    f = np.float32
+    hscale = f(6.) / f(180.)
+    sector_data = ((1, 3, 0), (1, 0, 2), (3, 0, 1), (0, 2, 1), (0, 1, 3), (2, 1, 0))
+    for (y, x), _ in np.ndenumerate(src[..., 0]):
+        h = f(src[y, x, 0])
+        s = f(src[y, x, 1]) * f(1. / 255.)
+        v = f(src[y, x, 2]) * f(1. / 255.)
+        if s == 0:
+            b = g = r = v
+        else:
+            h = f(h * hscale)
+            while h < 0:
+                h = f(h + f(6))
+            while h >= 6:
+                h = f(h - f(6))
+            sector = int(np.floor(h))
+            h = f(h - f(sector))
+            if not 0 <= sector < 6:
+                sector, h = 0, f(0)
+            tab = (v, f(v * f(f(1) - s)), f(v * f(f(1) - f(s * h))), f(v * f(f(1) - f(s * f(f(1) - h)))))
+            b, g, r = (tab[sector_data[sector][k]] for k in range(3))
+        out[y, x] = [max(0, min(255, int(np.rint(f(c * f(255)))))) for c in (b, g, r)]
+    return out
+
+
 def make_cv2():
     cv2 = types.ModuleType("cv2")
     cv2.INTER_LINEAR = INTER_LINEAR
@@ -348,6 +470,11 @@ def make_cv2():
     cv2.remap = remap
     cv2.resize = resize
     cv2.imread = imread
+    cv2.warpAffine = warpAffine
+    cv2.getRotationMatrix2D = getRotationMatrix2D
+    cv2.cvtColor = cvtColor
+    cv2.COLOR_BGR2HSV = COLOR_BGR2HSV
+    cv2.COLOR_HSV2BGR = COLOR_HSV2BGR
     cv2.normalize = lambda *a, **k: None
     cv2.imshow = lambda *a, **k: None
     cv2.waitKey = lambda *a, **k: 0

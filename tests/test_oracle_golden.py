@@ -233,3 +233,86 @@ def test_cv_resize_restatements_agree(shape, dsize):
     a = ol.resize_linear(img, dsize)
     b = tfshim.resize(img, dsize)
     assert a.shape == b.shape and np.array_equal(a, b)
+
+
+# ---------------------------------------------------------------- augmentation row
+
+def _tps_case(g, n):
+    from oracle import augment as oa
+    reg = tuple(int(v) for v in g[n + "_region"])
+    ag = float(g[n + "_ag"])
+    ag = int(ag) if ag == int(ag) else ag
+    planes = [g["img"][:, :, 0], g["img"][:, :, 1], g["img"][:, :, 2], g["alpha"], g[n + "_f32_in"]]
+    return oa.warp_images(g[n + "_from"], g[n + "_to"], planes, reg, int(g[n + "_order"]), ag)
+
+
+@pytest.mark.parametrize("case", ["a", "b", "c", "d"])
+def test_tps_oracle_matches_reference_tps(case):
+    """oracle.augment.warp_images == the reference's tps.warp_images (run for real on scipy) bit for bit:
+    approximate_grid 2 / 1 / 3 / 2.5, order 1 and 0, an offset output region, u8 / f64 / f32 planes."""
+    g = golden("tps")
+    r = _tps_case(g, case)
+    assert np.array_equal(np.stack(r[:3], axis=-1), g[case + "_u8"])
+    assert np.array_equal(r[3], g[case + "_f64"])
+    assert np.array_equal(r[4], g[case + "_f32"])
+
+
+def test_tps_deform_matches_reference():
+    from oracle import augment as oa
+    g = golden("tps")
+    np.random.seed(21)
+    assert np.array_equal(oa.deform(g["img"]), g["deform_out"])
+
+
+@pytest.mark.parametrize("dt", [np.uint8, np.float32, np.float64])
+@pytest.mark.parametrize("order", [0, 1])
+def test_map_coordinates_restatement_matches_scipy(dt, order):
+    """scipy (the reference's dependency, present here) vs the restatement on coordinates around every edge."""
+    from scipy import ndimage
+    from oracle import augment as oa
+    rs = np.random.RandomState(order * 7 + len(np.dtype(dt).name))
+    img = (rs.rand(7, 9) * 255).astype(dt)
+    cr = rs.uniform(-2, 8, size=(40, 50))
+    cc = rs.uniform(-2, 10, size=(40, 50))
+    cr[::3] = np.round(cr[::3])
+    cc[::4] = np.round(cc[::4])
+    cr[0, :10] = [0, 6, -0.0, 6.0, -1e-12, 6 + 1e-12, 3, -0.5, 6.5, 1e-7]
+    cc[1, :6] = [1e-9, 8 - 1e-9, 8, 8 + 1e-9, -1e-9, 0.5]
+    assert np.array_equal(ndimage.map_coordinates(img, [cr, cc], order=order), oa.map_coordinates(img, cr, cc, order))
+
+
+@pytest.mark.parametrize("i", [0, 1])
+def test_augment_oracle_matches_reference(i):
+    """augmentation.augment run verbatim (its draws, deform_grid, real tps.py; cv2 from tfshim)."""
+    from oracle import augment as oa
+    a = golden("augment")
+    np.random.seed(int(a["seed%d" % i]))
+    fg, bg, al = oa.augment(a["fg%d" % i], a["bg%d" % i], a["alpha%d" % i])
+    assert np.array_equal(fg, a["new_fg%d" % i])
+    assert np.array_equal(bg, a["new_bg%d" % i])
+    assert np.array_equal(al, a["new_alpha%d" % i])
+    assert np.random.randint(0, 1 << 30) == int(a["next_draw%d" % i])  # same number of draws consumed
+    a2 = golden("augment")
+    assert np.array_equal(oa.change_illumination(a2["illum_in"], *a2["illum_abc"]), a2["illum_out"])
+
+
+def test_cv_warp_affine_and_hsv_restatements_agree():
+    """tfshim's per-pixel cv2 restatement (imgwarp.cpp / color.cpp order) == the oracle's vectorised one."""
+    import sys
+
+    from conftest import GOLDEN
+    if GOLDEN not in sys.path:
+        sys.path.insert(0, GOLDEN)
+    import tfshim
+    from oracle import augment as oa
+    cv2 = tfshim.make_cv2()
+    rs = np.random.RandomState(1)
+    for src in [(rs.rand(23, 31, 3) * 255).astype(np.uint8), rs.rand(23, 31)]:
+        for M in [np.float32([[1, 0, 3], [0, 1, -2]]), cv2.getRotationMatrix2D((15, 11), 7.3, 1.1),
+                  cv2.getRotationMatrix2D((16, 8), -9.9, 1.02)]:
+            assert np.array_equal(cv2.warpAffine(src, M, (31, 23)), oa.warp_affine(src, M, (31, 23)))
+    hsv = np.stack(np.meshgrid(np.arange(180), np.arange(0, 256, 3), np.arange(0, 256, 7), indexing="ij"),
+                   -1).reshape(-1, 1, 3).astype(np.uint8)[::7]
+    assert np.array_equal(cv2.cvtColor(hsv, cv2.COLOR_HSV2BGR), oa.hsv2bgr(hsv))
+    bgr = (rs.rand(30, 40, 3) * 255).astype(np.uint8)
+    assert np.array_equal(cv2.cvtColor(bgr, cv2.COLOR_BGR2HSV), oa.bgr2hsv(bgr))
