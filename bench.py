@@ -182,6 +182,50 @@ def loader_bench(dev, steps, cpu=True, n=8, size=320, h=1080, w=1920):
     return rec
 
 
+def augment_bench(dev, steps, cpu=True, h=1080, w=1920):
+    """augmentation.augment on one 1080p (fg, bg, alpha) sample resident in HBM: host draws +
+    TPS solve + one stats sync + the csrc/augment.hip kernels.  Device time from HIP events on the launch stream."""
+    from vmatting import augmentation as va
+    rs = np.random.RandomState(9)
+    yy, xx = np.mgrid[0:h, 0:w]
+    alpha_h = np.clip(1.2 - np.sqrt(((yy - 0.46 * h) / (0.28 * h)) ** 2 + ((xx - 0.47 * w) / (0.21 * w)) ** 2), 0, 1)
+    fg_h = (rs.rand(h, w, 3) * 255).astype(np.uint8)
+    bg_h = (rs.rand(h, w, 3) * 255).astype(np.uint8)
+    fg, bg, alpha = (torch.from_numpy(a).to(dev) for a in (fg_h, bg_h, alpha_h))
+    np.random.seed(0)
+    for _ in range(3):
+        va.augment(fg, bg, alpha)
+    torch.cuda.synchronize()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    t0 = time.perf_counter()
+    ev[0].record()
+    for _ in range(steps):
+        va.augment(fg, bg, alpha)
+    ev[1].record()
+    torch.cuda.synchronize()
+    wall = (time.perf_counter() - t0) / steps
+    dev_ms = ev[0].elapsed_time(ev[1]) / steps
+    # algorithmic bytes per sample (per pixel): alpha stats 8; bg 2 warps 2*(3+3); TPS grid (h/2)(w/2)*16 = 4;
+    # fg TPS 3+3, alpha TPS 8+8; fg 2 warps 2*(3+3); alpha 2 warps 2*(8+8); illumination fg+bg 2*(3+3)
+    algo = h * w * (8 + 12 + 4 + 6 + 16 + 12 + 32 + 12)
+    rec = {"workload": "augmentation.augment: one %dx%d sample (u8 fg/bg, f64 alpha), inputs in HBM" % (w, h),
+           "samples_per_s": round(1.0 / wall, 1), "ms_per_sample": round(1000 * wall, 4),
+           "device_ms_per_sample": round(dev_ms, 4), "algorithmic_bytes_per_sample": int(algo),
+           "achieved_gbps": round(algo / (dev_ms * 1e-3) / 1e9, 1), "peak_gbps": PEAK_HBM_GBPS}
+    if cpu:
+        from oracle import augment as oa  # the CPU-baseline leg only
+        sh, sw = h // 2, w // 2
+        np.random.seed(0)
+        t0 = time.perf_counter()
+        oa.augment(fg_h[:sh, :sw].copy(), bg_h[:sh, :sw].copy(), alpha_h[::2, ::2].copy())
+        dt = (time.perf_counter() - t0) * (h * w) / float(sh * sw)
+        rec["cpu_baseline"] = {"value": round(1.0 / dt, 3), "unit": "samples/s", "cores": 1, "kind": "port",
+                               "sample": "oracle/augment.py (numpy, scipy-order TPS + OpenCV restatement) on one "
+                                         "%dx%d sample, scaled x%d to %dx%d by pixel count" % (sw, sh, (h * w) // (sh * sw),
+                                                                                         w, h)}
+    return rec
+
+
 def load_traffic(args, full=False):
     """Per-launch HBM bytes per kernel from the committed PMC pass (tools/traffic.py -> profiles/*_traffic.json),
     used only when it was collected on this exact workload."""
@@ -249,6 +293,7 @@ def main():
     ap.add_argument("--layers", action="store_true", help="per-conv timing breakdown on stderr")
     ap.add_argument("--no-graph", action="store_true", help="time eager launches instead of the captured HIP graph")
     ap.add_argument("--no-loader", action="store_true", help="skip the training-sample loader record (rank 0, N=1)")
+    ap.add_argument("--no-augment", action="store_true", help="skip the augmentation record (rank 0, N=1)")
     ap.add_argument("--video-frames", type=int, default=256,
                     help="config-4 record: frames sharded over the ranks + matte all-gather (0 = skip)")
     ap.add_argument("--option", action="append", default=[], metavar="KEY=VALUE",
@@ -349,6 +394,8 @@ def main():
             rec["cpu_baseline"] = cpu_baseline(H, W, sh, sw)
         if world == 1 and not args.no_loader:
             rec["loader"] = loader_bench(dev, max(args.steps, 10), cpu=not args.no_cpu_baseline)
+        if world == 1 and not args.no_augment:
+            rec["augment"] = augment_bench(dev, max(args.steps, 10), cpu=not args.no_cpu_baseline)
         print(json.dumps(rec), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -222,6 +222,51 @@ size_t vm_loader_workspace_bytes(int n);
 int vm_loader_compose(const vm_loader_sample* samples, int n, int out_h, int out_w, int dtype,
                       const vm_loader_outputs* out, void* work, void* stream);
 
+/* ---------------------------------------------------------------- augmentation
+ * tps.py (thin-plate-spline warp) and augmentation.py (augment's per-pixel work).  The TPS coefficient solve
+ * (tps._make_warp's 28x28 pinv, tps.py:110-115) and the np.random draws stay on the host, as in the reference;
+ * the per-pixel evaluation, resampling and colour work run here. */
+
+/* tps._make_inverse_warp's grid evaluation (tps.py:41-51 with tps._calculate_f, tps.py:100-108):
+ * grid[c][i][j] = a1_c + ax_c*x_i + ay_c*y_j + sum_k w_kc * U(|(x_i, y_j) - P_k|), U(r) = (r*r)*log(r) (0 below
+ * 1e-100, tps.py:80-81), x_i = i*x_step + x_lo, y_j = j*y_step + y_lo (np.mgrid).  points [npts,2] and coeffs
+ * [npts+3,2] (w_k rows, then a1, ax, ay) are DEVICE f64; grid is DEVICE f64 [2, nx, ny]. */
+int vm_tps_grid(const double* points, const double* coeffs, int npts, int nx, int ny, double x_lo, double x_step,
+                double y_lo, double y_step, double* grid, void* stream);
+
+/* The inverse map tps.warp_images samples with.  upsample = 0 (approximate_grid == 1): the grid is the map and the
+ * output is nx x ny.  upsample = 1: the output is (x_span+1) x (y_span+1) (x_span = x_max - x_min) and each pixel's
+ * map is the bilinear upsampling of tps.py:55-74 with x_steps = (x_max - x_min) / approximate_grid. */
+typedef struct vm_tps_map {
+  const double* grid;
+  int32_t nx, ny;
+  int32_t upsample;
+  int32_t x_span, y_span;
+  int32_t reserved;
+  double x_steps, y_steps;
+} vm_tps_map;
+
+/* tps.warp_images' resampling (tps.py:34): scipy.ndimage.map_coordinates(plane, map, order) with mode 'constant'
+ * (cval 0) on `cn` interleaved planes.  img [ih, iw, cn] and out [oh, ow, cn] of dtype VM_U8 / VM_F32 / VM_F64
+ * (integer outputs round as scipy does: (type)(t + 0.5)).  order 0 or 1. */
+int vm_tps_sample(const vm_tps_map* map, const void* img, int ih, int iw, int cn, int dtype, int order, void* out,
+                  void* stream);
+
+/* cv2.warpAffine(src, M, (w, h)) with INTER_LINEAR, BORDER_CONSTANT 0 (augmentation.py:58-61): m is the FORWARD
+ * 2x3 matrix (HOST, 6 doubles), inverted in double as warpAffine does.  src [ih, iw, cn], dst [h, w, cn], dtype
+ * VM_U8 (15-bit fixed-point weights), VM_F32 or VM_F64 (float table weights). */
+int vm_warp_affine(const void* src, int ih, int iw, int cn, int dtype, const double* m, void* dst, int h, int w,
+                   void* stream);
+
+/* augmentation.change_illumination (augmentation.py:86-98): cvtColor BGR2HSV (uint8, hrange 180), S and V through
+ * lut (HOST, 256 bytes: lut[u] = uint8(255 * clip(a * (u/255.)**b + c, 0, 1)), built by the caller with the
+ * reference's float64 arithmetic), cvtColor HSV2BGR.  bgr / out: device uint8 [pixels, 3]. */
+int vm_change_illumination_u8(const uint8_t* bgr, long pixels, const uint8_t* lut, uint8_t* out, void* stream);
+
+/* augmentation.object_size / fg_center (augmentation.py:10-20): stats (device int64[3]) = number of nonzero
+ * alpha pixels, sum of their row indices, sum of their column indices.  alpha [h, w] VM_F64 / VM_F32 / VM_U8. */
+int vm_nonzero_stats(const void* alpha, int h, int w, int dtype, long long* stats, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,464 @@
+// Augmentation path: tps.py's thin-plate-spline warp and augmentation.py's
+// per-pixel work (warpAffine, HSV illumination change, the foreground statistics).  All of it is gather- or
+// HBM-bound integer/f64 work: one thread per output pixel, rows of consecutive threads write consecutive
+// pixels (coalesced stores), taps are L2-served gathers.  Built with -ffp-contract=off: every expression is
+// evaluated in the reference's order with IEEE rounding at each step (numpy / scipy / OpenCV do not fuse).
+
+#include "vm_common.h"
+
+namespace vm {
+
+// ---------------------------------------------------------------------------------------------------- tps.py
+
+// uint8 HWC outputs: a block's run of 256 consecutive pixels (cn bytes each) is staged in LDS and written back as
+// 4-byte stores (one lane per dword) instead of cn scattered byte stores per lane.
+constexpr int kRun = 256;
+
+__device__ __forceinline__ void flush_run(uint8_t* __restrict__ dst, const uint8_t* stage, int nbytes) {
+  if ((reinterpret_cast<uintptr_t>(dst) & 3) == 0) {
+    const int nw = nbytes >> 2;
+    for (int t = threadIdx.x; t < nw; t += blockDim.x)
+      reinterpret_cast<uint32_t*>(dst)[t] = reinterpret_cast<const uint32_t*>(stage)[t];
+    for (int t = (nw << 2) + threadIdx.x; t < nbytes; t += blockDim.x) dst[t] = stage[t];
+  } else {
+    for (int t = threadIdx.x; t < nbytes; t += blockDim.x) dst[t] = stage[t];
+  }
+}
+
+// (row, col) of flat pixel i in a row-major [*, w] image: 32-bit unsigned division (callers check total < 2^31);
+// a 64-bit divide is a long emulated sequence on CDNA.
+__device__ __forceinline__ int row_of(long i, int w) { return (int)((unsigned)i / (unsigned)w); }
+
+// One output pixel per lane.  uint8 outputs go through the LDS run (blockDim.x == kRun, cn <= 8); wider types
+// store straight from the lane (consecutive lanes, consecutive pixels).
+template <typename T, class F>
+__device__ __forceinline__ void for_pixels(long total, int cn, T* __restrict__ out, F&& pixel) {
+  if constexpr (sizeof(T) == 1) {
+    __shared__ __attribute__((aligned(16))) uint8_t stage[kRun * 8];
+    for (long base = (long)blockIdx.x * kRun; base < total; base += (long)gridDim.x * kRun) {
+      const long i = base + threadIdx.x;
+      if (i < total) pixel(i, reinterpret_cast<T*>(stage) + threadIdx.x * cn);
+      __syncthreads();
+      const long n = total - base < kRun ? total - base : kRun;
+      flush_run(reinterpret_cast<uint8_t*>(out) + base * cn, stage, (int)(n * cn));
+      __syncthreads();
+    }
+  } else {
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x)
+      pixel(i, out + i * cn);
+  }
+}
+
+// tps._calculate_f (tps.py:100-108) on the approximate grid of tps._make_inverse_warp (tps.py:41-51):
+// x_i = i*x_step + x_lo (np.mgrid), f = a1 + ax*x + ay*y + sum_k w_k * U(r_k), U(r) = (r*r)*log(r), 0 below
+// 1e-100 (tps.py:80-81).  Both coordinates share the distance evaluation; each keeps its own accumulator in the
+// reference's order.
+__global__ void tps_grid_kernel(const double* __restrict__ pts, const double* __restrict__ coef, int npts, int nx,
+                                int ny, double x_lo, double x_step, double y_lo, double y_step,
+                                double* __restrict__ grid) {
+  const long total = (long)nx * ny;
+  const double a1x = coef[2 * npts], a1y = coef[2 * npts + 1];
+  const double axx = coef[2 * npts + 2], axy = coef[2 * npts + 3];
+  const double ayx = coef[2 * npts + 4], ayy = coef[2 * npts + 5];
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int ix = row_of(i, ny), iy = (int)(i - (long)ix * ny);
+    const double x = (double)ix * x_step + x_lo;
+    const double y = (double)iy * y_step + y_lo;
+    double sx = 0.0, sy = 0.0;
+    for (int k = 0; k < npts; ++k) {
+      const double dx = x - pts[2 * k], dy = y - pts[2 * k + 1];
+      const double r = sqrt(dx * dx + dy * dy);
+      const double u = (r * r) * (r < 1e-100 ? 0.0 : log(r));
+      sx += coef[2 * k] * u;
+      sy += coef[2 * k + 1] * u;
+    }
+    grid[i] = a1x + axx * x + ayx * y + sx;
+    grid[total + i] = a1y + axy * x + ayy * y + sy;
+  }
+}
+
+// One axis of the grid upsampling (tps.py:55-63): frac, idx = modf((steps - 1) * u / span); idx1 =
+// int(clip(idx + 1, 0, steps - 1)).
+struct UpAxis {
+  int i0, i1;
+  double f, f1;
+};
+
+__device__ __forceinline__ UpAxis up_axis(int u, double steps, int span) {
+  const double v = (steps - 1.0) * (double)u / (double)span;
+  const double ip = trunc(v);
+  UpAxis a;
+  a.i0 = (int)ip;
+  a.f = v - ip;
+  a.f1 = 1.0 - a.f;
+  double c = (double)(a.i0 + 1);
+  c = c < 0.0 ? 0.0 : c;
+  c = c > steps - 1.0 ? steps - 1.0 : c;
+  a.i1 = (int)c;
+  return a;
+}
+
+template <typename T>
+__device__ __forceinline__ double to_f64(T v) {
+  return (double)v;
+}
+
+template <typename T>
+__device__ __forceinline__ T from_f64(double t);
+template <>
+__device__ __forceinline__ uint8_t from_f64<uint8_t>(double t) {  // scipy CASE_INTERP_OUT_UINT: (type)(t + 0.5)
+  return (uint8_t)(t + 0.5);
+}
+template <>
+__device__ __forceinline__ float from_f64<float>(double t) {
+  return (float)t;
+}
+template <>
+__device__ __forceinline__ double from_f64<double>(double t) {
+  return t;
+}
+
+// tps.warp_images' sampling (tps.py:34): the per-pixel source coordinate is the grid (UP = false) or its bilinear
+// upsampling t00*x1*y1 + t01*x1*yf + t10*xf*y1 + t11*xf*yf (tps.py:64-74); then scipy.ndimage.map_coordinates
+// (order 0 / 1, mode 'constant', cval 0): a coordinate outside [0, n-1] gives 0; order 1 sums
+// t += (v * w_row) * w_col over the taps (r0,c0) (r0,c1) (r1,c0) (r1,c1), weights (1 - f, 1 - (1 - f)).
+template <typename T, int ORDER, bool UP>
+__global__ void tps_sample_kernel(const double* __restrict__ grid, int nx, int ny, double x_steps, int x_span,
+                                  double y_steps, int y_span, const T* __restrict__ img, int ih, int iw, int cn,
+                                  T* __restrict__ out, int oh, int ow) {
+  const long total = (long)oh * ow;
+  const long gsz = (long)nx * ny;
+  for_pixels(total, cn, out, [&](long i, T* o) {
+    const int oy = row_of(i, ow), ox = (int)(i - (long)oy * ow);
+    double tr, tc;
+    if (UP) {
+      const UpAxis ax = up_axis(oy, x_steps, x_span);
+      const UpAxis ay = up_axis(ox, y_steps, y_span);
+      const long a00 = (long)ax.i0 * ny + ay.i0, a01 = (long)ax.i0 * ny + ay.i1;
+      const long a10 = (long)ax.i1 * ny + ay.i0, a11 = (long)ax.i1 * ny + ay.i1;
+      tr = grid[a00] * ax.f1 * ay.f1 + grid[a01] * ax.f1 * ay.f + grid[a10] * ax.f * ay.f1 + grid[a11] * ax.f * ay.f;
+      tc = grid[gsz + a00] * ax.f1 * ay.f1 + grid[gsz + a01] * ax.f1 * ay.f + grid[gsz + a10] * ax.f * ay.f1 +
+           grid[gsz + a11] * ax.f * ay.f;
+    } else {
+      tr = grid[i];
+      tc = grid[gsz + i];
+    }
+    const bool inside = tr >= 0.0 && tr <= (double)(ih - 1) && tc >= 0.0 && tc <= (double)(iw - 1);
+    if (!inside) {
+      for (int k = 0; k < cn; ++k) o[k] = from_f64<T>(0.0);
+      return;
+    }
+    if (ORDER == 0) {
+      const int r = (int)floor(tr + 0.5), c = (int)floor(tc + 0.5);
+      const T* p = img + ((long)r * iw + c) * cn;
+      for (int k = 0; k < cn; ++k) o[k] = from_f64<T>(to_f64(p[k]));
+    } else {
+      const double fr0 = floor(tr), fc0 = floor(tc);
+      const int r0 = (int)fr0, c0 = (int)fc0;
+      const double fr = tr - fr0, fc = tc - fc0;
+      const double wr0 = 1.0 - fr, wr1 = 1.0 - wr0, wc0 = 1.0 - fc, wc1 = 1.0 - wc0;
+      const bool r1ok = r0 + 1 < ih, c1ok = c0 + 1 < iw;
+      const T* p00 = img + ((long)r0 * iw + c0) * cn;
+      for (int k = 0; k < cn; ++k) {
+        const double v00 = to_f64(p00[k]);
+        const double v01 = c1ok ? to_f64(p00[cn + k]) : 0.0;
+        const double v10 = r1ok ? to_f64(p00[(long)iw * cn + k]) : 0.0;
+        const double v11 = (r1ok && c1ok) ? to_f64(p00[((long)iw + 1) * cn + k]) : 0.0;
+        double t = 0.0;
+        t += (v00 * wr0) * wc0;
+        t += (v01 * wr0) * wc1;
+        t += (v10 * wr1) * wc0;
+        t += (v11 * wr1) * wc1;
+        o[k] = from_f64<T>(t);
+      }
+    }
+  });
+}
+
+// ---------------------------------------------------------------------------------------------------- OpenCV
+
+struct Affine {
+  double m[6];  // the inverted matrix (dst -> src), as WarpAffineInvoker uses it
+};
+
+__device__ __forceinline__ int cv_round(double v) { return (int)rint(v); }  // cvRound: round half to even
+
+// cv2.warpAffine INTER_LINEAR, BORDER_CONSTANT 0 (OpenCV 3.x imgwarp.cpp WarpAffineInvoker + remapBilinear):
+// X = (cvRound((M1*y + M2)*1024) + 16 + cvRound(M0*x*1024)) >> 5, tap (X>>5, Y>>5) saturated to short, fraction
+// (X&31, Y&31) into the 32x32 bilinear table.  uint8: 15-bit weights (32-ay)(32-ax)*32 ..., (s + 2^14) >> 15;
+// float: the exact float table weights, v0*w0 + v1*w1 + v2*w2 + v3*w3 in the source type's arithmetic.
+template <typename T>
+__global__ void warp_affine_kernel(const T* __restrict__ src, int ih, int iw, int cn, Affine a, T* __restrict__ dst,
+                                   int h, int w) {
+  const long total = (long)h * w;
+  for_pixels(total, cn, dst, [&](long i, T* o) {
+    const int y = row_of(i, w), x = (int)(i - (long)y * w);
+    const int adelta = cv_round(a.m[0] * (double)x * 1024.0);
+    const int bdelta = cv_round(a.m[3] * (double)x * 1024.0);
+    const int X0 = cv_round((a.m[1] * (double)y + a.m[2]) * 1024.0) + 16;
+    const int Y0 = cv_round((a.m[4] * (double)y + a.m[5]) * 1024.0) + 16;
+    const int X = (X0 + adelta) >> 5, Y = (Y0 + bdelta) >> 5;
+    int sx = X >> 5, sy = Y >> 5;
+    sx = sx < -32768 ? -32768 : (sx > 32767 ? 32767 : sx);
+    sy = sy < -32768 ? -32768 : (sy > 32767 ? 32767 : sy);
+    const int ax = X & 31, ay = Y & 31;
+    const bool y0ok = (unsigned)sy < (unsigned)ih, y1ok = (unsigned)(sy + 1) < (unsigned)ih;
+    const bool x0ok = (unsigned)sx < (unsigned)iw, x1ok = (unsigned)(sx + 1) < (unsigned)iw;
+    const T* p = src + ((long)sy * iw + sx) * cn;
+    for (int k = 0; k < cn; ++k) {
+      const T v0 = (y0ok && x0ok) ? p[k] : T(0);
+      const T v1 = (y0ok && x1ok) ? p[cn + k] : T(0);
+      const T v2 = (y1ok && x0ok) ? p[(long)iw * cn + k] : T(0);
+      const T v3 = (y1ok && x1ok) ? p[((long)iw + 1) * cn + k] : T(0);
+      if constexpr (sizeof(T) == 1) {
+        const int s = (int)v0 * ((32 - ay) * (32 - ax) * 32) + (int)v1 * ((32 - ay) * ax * 32) +
+                      (int)v2 * (ay * (32 - ax) * 32) + (int)v3 * (ay * ax * 32);
+        int r = (s + (1 << 14)) >> 15;
+        o[k] = (T)(r < 0 ? 0 : (r > 255 ? 255 : r));
+      } else {
+        const float wy0 = 1.f - (float)ay * (1.f / 32.f), wy1 = (float)ay * (1.f / 32.f);
+        const float wx0 = 1.f - (float)ax * (1.f / 32.f), wx1 = (float)ax * (1.f / 32.f);
+        const T w0 = (T)(wy0 * wx0), w1 = (T)(wy0 * wx1), w2 = (T)(wy1 * wx0), w3 = (T)(wy1 * wx1);
+        o[k] = v0 * w0 + v1 * w1 + v2 * w2 + v3 * w3;
+      }
+    }
+  });
+}
+
+struct Lut256 {
+  uint8_t t[256];
+};
+
+// augmentation.change_illumination (augmentation.py:86-98): cvtColor BGR2HSV (RGB2HSV_b, hsv_shift 12, hrange
+// 180), S and V through the host-built map lut[u] = uint8(255 * clip(a * (u/255)^b + c, 0, 1)), cvtColor HSV2BGR
+// (HSV2RGB_b: float32 HSV2RGB_f, then cvRound(x * 255) saturated).  The division tables live in LDS.
+__global__ void __launch_bounds__(256) illumination_kernel(const uint8_t* __restrict__ bgr, long pixels, Lut256 lut,
+                                                           uint8_t* __restrict__ out) {
+  __shared__ int sdiv[256], hdiv[256];
+  {
+    const int t = threadIdx.x;
+    sdiv[t] = t ? (int)rint((double)(255 << 12) / (1.0 * t)) : 0;
+    hdiv[t] = t ? (int)rint((double)(180 << 12) / (6.0 * t)) : 0;
+  }
+  __syncthreads();
+  const float hscale = 6.f / 180.f;
+  const float inv255 = 1.f / 255.f;
+  for_pixels(pixels, 3, out, [&](long i, uint8_t* o) {
+    const int b = bgr[3 * i], g = bgr[3 * i + 1], r = bgr[3 * i + 2];
+    int v = b > g ? b : g;
+    v = v > r ? v : r;
+    int vmin = b < g ? b : g;
+    vmin = vmin < r ? vmin : r;
+    const int diff = v - vmin;
+    const int vr = v == r ? -1 : 0, vg = v == g ? -1 : 0;
+    const int s = (diff * sdiv[v] + (1 << 11)) >> 12;
+    int hh = (vr & (g - b)) + (~vr & ((vg & (b - r + 2 * diff)) + ((~vg) & (r - g + 4 * diff))));
+    hh = (hh * hdiv[diff] + (1 << 11)) >> 12;
+    hh += hh < 0 ? 180 : 0;
+    // new_hsv = (h, lut[s], lut[v]) -> HSV2RGB_b
+    float hf = (float)(uint8_t)hh;
+    const float sf = (float)lut.t[s] * inv255;
+    const float vf = (float)lut.t[v] * inv255;
+    float ob, og, orr;
+    if (sf == 0.f) {
+      ob = og = orr = vf;
+    } else {
+      hf *= hscale;
+      while (hf < 0.f) hf += 6.f;
+      while (hf >= 6.f) hf -= 6.f;
+      int sector = (int)floorf(hf);
+      hf -= (float)sector;
+      if ((unsigned)sector >= 6u) {
+        sector = 0;
+        hf = 0.f;
+      }
+      float tab[4];
+      tab[0] = vf;
+      tab[1] = vf * (1.f - sf);
+      tab[2] = vf * (1.f - sf * hf);
+      tab[3] = vf * (1.f - sf * (1.f - hf));
+      const int sd[6][3] = {{1, 3, 0}, {1, 0, 2}, {3, 0, 1}, {0, 2, 1}, {0, 1, 3}, {2, 1, 0}};
+      ob = tab[sd[sector][0]];
+      og = tab[sd[sector][1]];
+      orr = tab[sd[sector][2]];
+    }
+    auto sat = [](float x) -> uint8_t {
+      const int q = (int)rintf(x * 255.f);
+      return (uint8_t)(q < 0 ? 0 : (q > 255 ? 255 : q));
+    };
+    o[0] = sat(ob);
+    o[1] = sat(og);
+    o[2] = sat(orr);
+  });
+}
+
+// augmentation.object_size / fg_center (augmentation.py:10-20): count, row-index sum and column-index sum of the
+// nonzero alpha pixels (exact integers; the host forms sqrt(count) and int(sum / count) like numpy).
+template <typename T>
+__global__ void __launch_bounds__(256) nonzero_stats_kernel(const T* __restrict__ a, int h, int w,
+                                                            unsigned long long* __restrict__ stats) {
+  unsigned long long cnt = 0, sr = 0, sc = 0;
+  for (int r = blockIdx.x; r < h; r += gridDim.x) {
+    const T* row = a + (long)r * w;
+    for (int c = threadIdx.x; c < w; c += blockDim.x) {
+      if (row[c] != T(0)) {
+        ++cnt;
+        sr += (unsigned long long)r;
+        sc += (unsigned long long)c;
+      }
+    }
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    cnt += __shfl_xor(cnt, off, 64);
+    sr += __shfl_xor(sr, off, 64);
+    sc += __shfl_xor(sc, off, 64);
+  }
+  // one set of atomics per block (not per wave): the three counters are single addresses
+  __shared__ unsigned long long part[3][4];
+  const int wv = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    part[0][wv] = cnt;
+    part[1][wv] = sr;
+    part[2][wv] = sc;
+  }
+  __syncthreads();
+  if (threadIdx.x < 3) {
+    unsigned long long v = 0;
+    for (int k = 0; k < (int)(blockDim.x >> 6); ++k) v += part[threadIdx.x][k];
+    if (v) atomicAdd(&stats[threadIdx.x], v);
+  }
+}
+
+}  // namespace vm
+
+using namespace vm;
+
+extern "C" int vm_tps_grid(const double* points, const double* coeffs, int npts, int nx, int ny, double x_lo,
+                           double x_step, double y_lo, double y_step, double* grid, void* stream) {
+  if (!points || !coeffs || !grid || npts <= 0 || nx <= 0 || ny <= 0) return fail(VM_EINVAL, "tps_grid: bad argument");
+  if ((long)nx * ny >= (1L << 31)) return fail(VM_EUNSUPPORTED, "tps_grid: more than 2^31 grid points");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const long total = (long)nx * ny;
+  hipLaunchKernelGGL(tps_grid_kernel, dim3(grid_for(total, 256)), dim3(256), 0, st, points, coeffs, npts, nx, ny, x_lo,
+                     x_step, y_lo, y_step, grid);
+  return check_launch("tps_grid");
+}
+
+template <typename T>
+static void launch_tps_sample(const vm_tps_map* m, const void* img, int ih, int iw, int cn, int order, void* out,
+                              int oh, int ow, hipStream_t st) {
+  const dim3 g(grid_for((long)oh * ow, 256)), b(256);
+  const T* s = static_cast<const T*>(img);
+  T* o = static_cast<T*>(out);
+#define VM_TPS_LAUNCH(ORD, UP)                                                                                      \
+  hipLaunchKernelGGL((tps_sample_kernel<T, ORD, UP>), g, b, 0, st, m->grid, m->nx, m->ny, m->x_steps, m->x_span,    \
+                     m->y_steps, m->y_span, s, ih, iw, cn, o, oh, ow)
+  if (order == 0) {
+    if (m->upsample) VM_TPS_LAUNCH(0, true);
+    else VM_TPS_LAUNCH(0, false);
+  } else {
+    if (m->upsample) VM_TPS_LAUNCH(1, true);
+    else VM_TPS_LAUNCH(1, false);
+  }
+#undef VM_TPS_LAUNCH
+}
+
+extern "C" int vm_tps_sample(const vm_tps_map* map, const void* img, int ih, int iw, int cn, int dtype, int order,
+                             void* out, void* stream) {
+  if (!map || !map->grid || !img || !out || ih <= 0 || iw <= 0 || cn <= 0 || map->nx <= 0 || map->ny <= 0 ||
+      (order != 0 && order != 1))
+    return fail(VM_EINVAL, "tps_sample: bad argument");
+  if (dtype == VM_U8 && cn > 8) return fail(VM_EUNSUPPORTED, "tps_sample: uint8 images with more than 8 planes");
+  if ((long)map->nx * map->ny >= (1L << 31) || ((long)map->x_span + 1) * (map->y_span + 1) >= (1L << 31))
+    return fail(VM_EUNSUPPORTED, "tps_sample: more than 2^31 pixels");
+  int oh = map->nx, ow = map->ny;
+  if (map->upsample) {
+    if (map->x_span <= 0 || map->y_span <= 0) return fail(VM_EINVAL, "tps_sample: empty output region");
+    // every grid index the upsampling can form must lie inside the grid
+    if (!(map->x_steps - 1.0 < (double)map->nx) || !(map->y_steps - 1.0 < (double)map->ny) || map->x_steps < 1.0 ||
+        map->y_steps < 1.0)
+      return fail(VM_EINVAL, "tps_sample: grid %dx%d too small for steps %g x %g", map->nx, map->ny, map->x_steps,
+                  map->y_steps);
+    oh = map->x_span + 1;
+    ow = map->y_span + 1;
+  }
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  switch (dtype) {
+    case VM_U8: launch_tps_sample<uint8_t>(map, img, ih, iw, cn, order, out, oh, ow, st); break;
+    case VM_F32: launch_tps_sample<float>(map, img, ih, iw, cn, order, out, oh, ow, st); break;
+    case VM_F64: launch_tps_sample<double>(map, img, ih, iw, cn, order, out, oh, ow, st); break;
+    default: return fail(VM_EUNSUPPORTED, "tps_sample: dtype %d", dtype);
+  }
+  return check_launch("tps_sample");
+}
+
+extern "C" int vm_warp_affine(const void* src, int ih, int iw, int cn, int dtype, const double* m, void* dst, int h,
+                              int w, void* stream) {
+  if (!src || !dst || !m || ih <= 0 || iw <= 0 || cn <= 0 || h <= 0 || w <= 0)
+    return fail(VM_EINVAL, "warp_affine: bad argument");
+  if (dtype == VM_U8 && cn > 8) return fail(VM_EUNSUPPORTED, "warp_affine: uint8 images with more than 8 channels");
+  if ((long)h * w >= (1L << 31)) return fail(VM_EUNSUPPORTED, "warp_affine: more than 2^31 pixels");
+  // warpAffine without WARP_INVERSE_MAP inverts the forward matrix in double (imgwarp.cpp)
+  Affine a;
+  for (int i = 0; i < 6; ++i) a.m[i] = m[i];
+  double d = a.m[0] * a.m[4] - a.m[1] * a.m[3];
+  d = d != 0 ? 1. / d : 0.;
+  const double a11 = a.m[4] * d, a22 = a.m[0] * d;
+  a.m[0] = a11;
+  a.m[1] *= -d;
+  a.m[3] *= -d;
+  a.m[4] = a22;
+  const double b1 = -a.m[0] * a.m[2] - a.m[1] * a.m[5];
+  const double b2 = -a.m[3] * a.m[2] - a.m[4] * a.m[5];
+  a.m[2] = b1;
+  a.m[5] = b2;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const dim3 g(grid_for((long)h * w, 256)), b(256);
+  switch (dtype) {
+    case VM_U8:
+      hipLaunchKernelGGL(warp_affine_kernel<uint8_t>, g, b, 0, st, static_cast<const uint8_t*>(src), ih, iw, cn, a,
+                         static_cast<uint8_t*>(dst), h, w);
+      break;
+    case VM_F32:
+      hipLaunchKernelGGL(warp_affine_kernel<float>, g, b, 0, st, static_cast<const float*>(src), ih, iw, cn, a,
+                         static_cast<float*>(dst), h, w);
+      break;
+    case VM_F64:
+      hipLaunchKernelGGL(warp_affine_kernel<double>, g, b, 0, st, static_cast<const double*>(src), ih, iw, cn, a,
+                         static_cast<double*>(dst), h, w);
+      break;
+    default: return fail(VM_EUNSUPPORTED, "warp_affine: dtype %d", dtype);
+  }
+  return check_launch("warp_affine");
+}
+
+extern "C" int vm_change_illumination_u8(const uint8_t* bgr, long pixels, const uint8_t* lut, uint8_t* out,
+                                         void* stream) {
+  if (!bgr || !lut || !out || pixels <= 0) return fail(VM_EINVAL, "change_illumination: bad argument");
+  Lut256 l;
+  for (int i = 0; i < 256; ++i) l.t[i] = lut[i];
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(illumination_kernel, dim3(grid_for(pixels, 256)), dim3(256), 0, st, bgr, pixels, l, out);
+  return check_launch("change_illumination");
+}
+
+extern "C" int vm_nonzero_stats(const void* alpha, int h, int w, int dtype, long long* stats, void* stream) {
+  if (!alpha || !stats || h <= 0 || w <= 0) return fail(VM_EINVAL, "nonzero_stats: bad argument");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (hipMemsetAsync(stats, 0, 3 * sizeof(long long), st) != hipSuccess) return fail(VM_EHIP, "nonzero_stats: memset");
+  auto* s = reinterpret_cast<unsigned long long*>(stats);
+  const dim3 g(h < 1024 ? h : 1024), b(256);
+  switch (dtype) {
+    case VM_F64:
+      hipLaunchKernelGGL(nonzero_stats_kernel<double>, g, b, 0, st, static_cast<const double*>(alpha), h, w, s);
+      break;
+    case VM_F32:
+      hipLaunchKernelGGL(nonzero_stats_kernel<float>, g, b, 0, st, static_cast<const float*>(alpha), h, w, s);
+      break;
+    case VM_U8:
+      hipLaunchKernelGGL(nonzero_stats_kernel<uint8_t>, g, b, 0, st, static_cast<const uint8_t*>(alpha), h, w, s);
+      break;
+    default: return fail(VM_EUNSUPPORTED, "nonzero_stats: dtype %d", dtype);
+  }
+  return check_launch("nonzero_stats");
+}

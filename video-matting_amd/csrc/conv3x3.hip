@@ -2373,7 +2373,7 @@ extern "C" int vm_conv3x3_pair_first_nhwc(const vm_tensor* x, const void* packed
   if (cout2 == 64 && g_pair_kernel == 0 && sp <= 0x7fffffffL) {
     static int attr_dev = -1, n_cu = 0;
     int dev = 0;
-    hipGetDevice(&dev);
+    (void)hipGetDevice(&dev);
     if (attr_dev != dev) {
       hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3_pair_persist),
                                          hipFuncAttributeMaxDynamicSharedMemorySize, PairCfg::LDS);

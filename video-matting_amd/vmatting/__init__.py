@@ -8,4 +8,5 @@ C ABI in include/vmatting.h).  No CPU fallback: a missing library or GPU raises.
 from . import _lib, ops, weights  # noqa: F401
 from .params import VGG_MEAN  # noqa: F401
 
-__all__ = ["unet", "unet_simple", "small", "refine", "flow", "reader", "parallel", "ops", "weights"]
+__all__ = ["unet", "unet_simple", "small", "refine", "flow", "reader", "tps", "augmentation", "loader", "parallel", "ops",
+           "weights"]

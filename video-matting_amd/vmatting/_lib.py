@@ -50,6 +50,12 @@ class VmLoaderOutputs(ctypes.Structure):
     _fields_ = [("ptr", c_void_p * 5), ("pixstride", ctypes.c_int32 * 5), ("reserved", ctypes.c_int32)]
 
 
+class VmTpsMap(ctypes.Structure):
+    _fields_ = [("grid", c_void_p), ("nx", ctypes.c_int32), ("ny", ctypes.c_int32), ("upsample", ctypes.c_int32),
+                ("x_span", ctypes.c_int32), ("y_span", ctypes.c_int32), ("reserved", ctypes.c_int32),
+                ("x_steps", ctypes.c_double), ("y_steps", ctypes.c_double)]
+
+
 LOADER_PLANES = {"cmp": 0, "bg": 1, "label": 2, "warped": 3, "fg": 4}
 
 # (name, restype, argtypes) — one row per declaration in include/vmatting.h
@@ -87,6 +93,14 @@ SIGNATURES = [
     ("vm_loader_workspace_bytes", c_size_t, [c_int]),
     ("vm_loader_compose", c_int, [ctypes.POINTER(VmLoaderSample), c_int, c_int, c_int, c_int,
                                   ctypes.POINTER(VmLoaderOutputs), c_void_p, c_void_p]),
+    ("vm_tps_grid", c_int, [c_void_p, c_void_p, c_int, c_int, c_int, ctypes.c_double, ctypes.c_double,
+                            ctypes.c_double, ctypes.c_double, c_void_p, c_void_p]),
+    ("vm_tps_sample", c_int, [ctypes.POINTER(VmTpsMap), c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p,
+                              c_void_p]),
+    ("vm_warp_affine", c_int, [c_void_p, c_int, c_int, c_int, c_int, ctypes.POINTER(ctypes.c_double), c_void_p,
+                               c_int, c_int, c_void_p]),
+    ("vm_change_illumination_u8", c_int, [c_void_p, c_long, ctypes.POINTER(ctypes.c_uint8), c_void_p, c_void_p]),
+    ("vm_nonzero_stats", c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
 ]
 
 _lib = None

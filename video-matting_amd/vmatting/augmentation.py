@@ -1,0 +1,144 @@
+"""augmentation.py (synthetic video-matting samples) on gfx950 kernels — SURVEY.md §8(f) rank 3.
+
+Same names and call shapes as the reference's augmentation.py:10-135.  The np.random draws stay on the host in
+the reference's order (so a seeded run draws the same parameters); everything per pixel runs on the device:
+the foreground statistics behind object_size / fg_center (vm_nonzero_stats), the TPS deformation (tps.py via
+vm_tps_grid / vm_tps_sample), cv2.warpAffine (vm_warp_affine) and the HSV illumination change
+(vm_change_illumination_u8, whose 256-entry S/V map is built on the host with the reference's float64
+arithmetic).  numpy in -> numpy out; torch device tensors stay on the device.  The dataset-writing driver
+augmentation() (file listing, imread/imwrite, progress bar) is I/O and out of scope.
+"""
+
+import math
+
+import numpy as np
+import torch
+
+from . import ops
+from . import tps
+from .tps import deform_grid  # noqa: F401  (augmentation.deform_grid, augmentation.py:23-39)
+
+
+def _device(a):
+    if isinstance(a, torch.Tensor):
+        return a if a.is_cuda else a.cuda()
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def _out(t, like):
+    return t if isinstance(like, torch.Tensor) else t.cpu().numpy()
+
+
+def _stats(alpha):
+    return [int(v) for v in ops.nonzero_stats(_device(alpha)).cpu().tolist()]
+
+
+def object_size(alpha):
+    """augmentation.object_size (augmentation.py:10-14): sqrt of the number of nonzero alpha pixels."""
+    return np.sqrt(_stats(alpha)[0])
+
+
+def fg_center(alpha):
+    """augmentation.fg_center (augmentation.py:17-20): (int(mean column), int(mean row)) of the nonzero pixels.
+    An all-zero alpha raises ValueError, as int(np.mean([])) does in the reference."""
+    cnt, sr, sc = _stats(alpha)
+    if cnt == 0:
+        raise ValueError("cannot convert float NaN to integer")
+    return int(sc / cnt), int(sr / cnt)  # exact integer sums, one float64 division (numpy's mean)
+
+
+def rotation_matrix(center, angle, scale):
+    """cv2.getRotationMatrix2D(center, angle, scale) (center is a Point2f)."""
+    cx, cy = float(np.float32(center[0])), float(np.float32(center[1]))
+    a = angle * (math.pi / 180)
+    alpha = math.cos(a) * scale
+    beta = math.sin(a) * scale
+    return np.array([[alpha, beta, (1 - alpha) * cx - beta * cy],
+                     [-beta, alpha, beta * cx + (1 - alpha) * cy]])
+
+
+def _warp_image_dev(img, params, inv=None):
+    (tu, tv), rot, scale, center = params
+    h, w = img.shape[:2]
+    if inv is not None:
+        img = inv.sample(img, 1)
+        if img.shape[2] == 1:
+            img = img[:, :, 0]
+    mt = np.float32([[1, 0, tu], [0, 1, tv]])
+    translated = ops.warp_affine(img, mt, (w, h))
+    return ops.warp_affine(translated, rotation_matrix(center, rot, scale), (w, h))
+
+
+def warp_image(img, params, thin=None):
+    """augmentation.warp_image (augmentation.py:42-61): optional TPS deformation thin = (grid, def_grid)
+    (output (h+1, w+1)), then cv2.warpAffine by the translation (tu, tv) and by getRotationMatrix2D(center, rot,
+    scale), both to (w, h)."""
+    d = _device(img)
+    h, w = d.shape[:2]
+    inv = None
+    if thin is not None:
+        grid, def_grid = thin
+        inv = tps.InverseWarp(grid, def_grid, (0, 0, h, w), 2, d.device)
+    return _out(_warp_image_dev(d, params, inv), img)
+
+
+def identity(m, n):
+    """augmentation.identity (augmentation.py:64-68): arr[i, j] = [i+1, j+1] (int64, host)."""
+    vec1 = np.arange(1, n + 1)
+    vec2 = np.arange(1, m + 1)
+    return np.transpose([np.repeat(vec2, n), np.tile(vec1, m)]).reshape(m, n, 2)
+
+
+def synthetize_flow(fg_params, bg_params, grids, warped_alpha):
+    """augmentation.synthetize_flow (augmentation.py:71-83) passes int64 identity() maps to cv2.warpAffine,
+    which OpenCV rejects (no 64-bit integer depth); the reference therefore always raises here, and so does
+    this drop-in.  It has no caller in the reference."""
+    raise TypeError("src data type = 9 is not supported (cv2.warpAffine on the int64 identity map, "
+                    "augmentation.py:78)")
+
+
+def illumination_lut(a, b, c):
+    """change_illumination's S/V map (augmentation.py:89-95) for every uint8 value, float64 like the reference."""
+    x = np.arange(256, dtype=np.uint8)
+    return (255. * np.clip(a * np.power(x / 255., b) + c, 0., 1.)).astype(np.uint8)
+
+
+def change_illumination(bgr, a, b, c):
+    """augmentation.change_illumination (augmentation.py:86-98): HSV round trip with S, V -> a * x**b + c."""
+    return _out(ops.change_illumination(_device(bgr), illumination_lut(a, b, c)), bgr)
+
+
+def augment(fg, bg, alpha):
+    """augmentation.augment (augmentation.py:101-135): camera motion on bg, TPS + similarity motion on fg and
+    alpha, one illumination change for both.  Returns (new_fg u8, new_bg u8, new_alpha f64)."""
+    bound_translate, bound_rotate, bound_scale = 0.05, 10, 0.15
+    dfg, dbg, dal = _device(fg), _device(bg), _device(alpha)
+    h, w = dfg.shape[:2]
+    cnt, sr, sc = _stats(dal)
+    fg_size = np.sqrt(cnt)
+    # camera motion (bg)
+    tu_bg = int(np.random.uniform(-w * bound_translate, w * bound_translate))
+    tv_bg = int(np.random.uniform(-h * bound_translate, h * bound_translate))
+    rot_bg = 0.
+    scale_bg = np.random.uniform(1., 1. + bound_scale)
+    new_bg = _warp_image_dev(dbg, ((tu_bg, tv_bg), rot_bg, scale_bg, (w // 2, h // 2)))
+    # object motion (fg): TPS deformation + similarity
+    grid, def_grid = deform_grid(h, w)
+    tu_fg = int(np.random.uniform(-fg_size * bound_translate, fg_size * bound_translate))
+    tv_fg = int(np.random.uniform(-fg_size * bound_translate, fg_size * bound_translate))
+    rot_fg = np.random.uniform(-bound_rotate, bound_rotate)
+    scale_fg = np.random.uniform(1., 1. + bound_scale)
+    if cnt == 0:
+        raise ValueError("cannot convert float NaN to integer")
+    params_fg = (tu_fg, tv_fg), rot_fg, scale_fg, (int(sc / cnt), int(sr / cnt))
+    # one TPS map serves fg and alpha (the reference evaluates the same map twice)
+    inv = tps.InverseWarp(grid, def_grid, (0, 0, h, w), 2, dfg.device)
+    new_fg = _warp_image_dev(dfg, params_fg, inv)
+    new_alpha = _warp_image_dev(dal, params_fg, inv)
+    a = np.random.uniform(1. - 0.05, 1. + 0.05)
+    b = np.random.uniform(1. - 0.3, 1. + 0.3)
+    c = np.random.uniform(-0.07, 0.07)
+    lut = illumination_lut(a, b, c)
+    new_fg = ops.change_illumination(new_fg, lut)
+    new_bg = ops.change_illumination(new_bg, lut)
+    return _out(new_fg, fg), _out(new_bg, bg), _out(new_alpha, alpha)

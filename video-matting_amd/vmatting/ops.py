@@ -388,3 +388,102 @@ def matting_loss(pred, gt, raw_fg, in_bg, in_cmp):
     check(lib().vm_matting_loss(*[_ptr(t) for t in ts], pixels, _ptr(out), _ptr(ws), stream_handle()),
           "matting_loss")
     return out
+
+
+# ---------------------------------------------------------------- augmentation row (tps.py / augmentation.py)
+
+_AUG_DT = {torch.uint8: _lib.VM_U8, torch.float32: _lib.VM_F32, torch.float64: _lib.VM_F64}
+
+
+def _dtype_code(t, what):
+    if t.dtype not in _AUG_DT:
+        raise TypeError("%s: unsupported dtype %s (uint8, float32, float64)" % (what, t.dtype))
+    return _AUG_DT[t.dtype]
+
+
+def tps_grid(points, coeffs, nx, ny, x_lo, x_step, y_lo, y_step, out=None):
+    """vm_tps_grid: the TPS map evaluated on an nx x ny np.mgrid lattice -> f64 [2, nx, ny] on the device."""
+    _require_gpu(points)
+    _require_gpu(coeffs)
+    p = points.contiguous().double()
+    c = coeffs.contiguous().double()
+    if p.dim() != 2 or p.shape[1] != 2 or c.shape != (p.shape[0] + 3, 2):
+        raise ValueError("tps_grid: points [n,2] and coeffs [n+3,2], got %s %s" % (tuple(p.shape), tuple(c.shape)))
+    if out is None:
+        out = torch.empty((2, nx, ny), dtype=torch.float64, device=p.device)
+    check(lib().vm_tps_grid(_ptr(p), _ptr(c), p.shape[0], nx, ny, float(x_lo), float(x_step), float(y_lo),
+                            float(y_step), _ptr(out), stream_handle()), "tps_grid")
+    return out
+
+
+def tps_sample(grid, img, order=1, upsample=None, out=None):
+    """vm_tps_sample: map_coordinates of img [ih, iw, cn] (u8/f32/f64) through the grid (or its upsampling:
+    upsample = (x_steps, x_span, y_steps, y_span)) -> [oh, ow, cn] of img's dtype."""
+    _require_gpu(grid)
+    _require_gpu(img)
+    img = img.contiguous()
+    if img.dim() == 2:
+        img = img[:, :, None]
+    ih, iw, cn = img.shape
+    nx, ny = grid.shape[1:]
+    m = _lib.VmTpsMap()
+    m.grid = _ptr(grid)
+    m.nx, m.ny = nx, ny
+    if upsample is None:
+        m.upsample = 0
+        oh, ow = nx, ny
+    else:
+        xs, xspan, ys, yspan = upsample
+        m.upsample, m.x_steps, m.x_span, m.y_steps, m.y_span = 1, float(xs), int(xspan), float(ys), int(yspan)
+        oh, ow = int(xspan) + 1, int(yspan) + 1
+    if out is None:
+        out = torch.empty((oh, ow, cn), dtype=img.dtype, device=img.device)
+    check(lib().vm_tps_sample(ctypes.byref(m), _ptr(img), ih, iw, cn, _dtype_code(img, "tps_sample"), int(order),
+                              _ptr(out), stream_handle()), "tps_sample")
+    return out
+
+
+def warp_affine(src, M, dsize, out=None):
+    """vm_warp_affine: cv2.warpAffine(src, M, dsize=(w, h)), INTER_LINEAR, BORDER_CONSTANT 0."""
+    _require_gpu(src)
+    src = src.contiguous()
+    two_d = src.dim() == 2
+    ih, iw = src.shape[:2]
+    cn = 1 if two_d else src.shape[2]
+    w, h = int(dsize[0]), int(dsize[1])
+    m = (ctypes.c_double * 6)(*[float(v) for v in np.asarray(M, np.float64).reshape(6)])
+    if out is None:
+        out = torch.empty((h, w) if two_d else (h, w, cn), dtype=src.dtype, device=src.device)
+    check(lib().vm_warp_affine(_ptr(src), ih, iw, cn, _dtype_code(src, "warp_affine"), m, _ptr(out), h, w,
+                               stream_handle()), "warp_affine")
+    return out
+
+
+def change_illumination(bgr, lut, out=None):
+    """vm_change_illumination_u8: BGR u8 -> HSV -> (h, lut[s], lut[v]) -> BGR u8."""
+    _require_gpu(bgr)
+    if bgr.dtype != torch.uint8 or bgr.shape[-1] != 3:
+        raise TypeError("change_illumination: uint8 [..., 3] expected")
+    bgr = bgr.contiguous()
+    lut = np.ascontiguousarray(lut, np.uint8)
+    if lut.shape != (256,):
+        raise ValueError("change_illumination: lut must have 256 entries")
+    if out is None:
+        out = torch.empty_like(bgr)
+    check(lib().vm_change_illumination_u8(_ptr(bgr), bgr.numel() // 3,
+                                          lut.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), _ptr(out),
+                                          stream_handle()), "change_illumination")
+    return out
+
+
+def nonzero_stats(alpha, out=None):
+    """vm_nonzero_stats: (count, row-index sum, column-index sum) of alpha != 0, int64[3] on the device."""
+    _require_gpu(alpha)
+    alpha = alpha.contiguous()
+    if alpha.dim() != 2:
+        raise ValueError("nonzero_stats: alpha must be [h, w]")
+    if out is None:
+        out = torch.empty(3, dtype=torch.int64, device=alpha.device)
+    check(lib().vm_nonzero_stats(_ptr(alpha), alpha.shape[0], alpha.shape[1], _dtype_code(alpha, "nonzero_stats"),
+                                 _ptr(out), stream_handle()), "nonzero_stats")
+    return out
