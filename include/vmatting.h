@@ -267,6 +267,12 @@ int vm_change_illumination_u8(const uint8_t* bgr, long pixels, const uint8_t* lu
  * alpha pixels, sum of their row indices, sum of their column indices.  alpha [h, w] VM_F64 / VM_F32 / VM_U8. */
 int vm_nonzero_stats(const void* alpha, int h, int w, int dtype, long long* stats, void* stream);
 
+/* data.trimap_from_matte (data.py:37-67; the reference uses dilate 1, crop 3): trimap u8 [h, w] from a float64
+ * matte [h, w] (device), 255 / 0 where the matte is exactly 1 / 0, 128 elsewhere and — reproducing the reference's
+ * raster-order overwrites — on 1-pixels (0-pixels) with a non-0/1 pixel later in raster order within crop (dilate)
+ * in the max-norm.  dilate, crop <= 8. */
+int vm_trimap_from_matte(const double* matte, int h, int w, int dilate, int crop, uint8_t* trimap, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -45,9 +45,10 @@ def load_reference():
     np.float = float  # numpy<1.24 aliases used by reader.py:74, flow.py:38, loader.py:43
     np.int = int
     sys.path.insert(0, REF)
-    import unet, unet_simple, small, refine, flow, reader, train, tps, augmentation  # noqa: E401
+    import unet, unet_simple, small, refine, flow, reader, train, tps, augmentation, data  # noqa: E401
     return types.SimpleNamespace(unet=unet, unet_simple=unet_simple, small=small, refine=refine,
-                                 flow=flow, reader=reader, train=train, tps=tps, augmentation=augmentation)
+                                 flow=flow, reader=reader, train=train, tps=tps, augmentation=augmentation,
+                                 data=data)
 
 
 _VGG = {}
@@ -391,6 +392,25 @@ def gen_augment(R, out):
     out["augment"] = d
 
 
+def gen_trimap(R, out):
+    """data.trimap_from_matte (data.py:37-67) run verbatim (pure-Python raster loop) on the in0062.png alpha
+    (resized), on a matte with isolated unknown pixels next to 0 and 1, and on image-border cases."""
+    d = {}
+    fgimg = load_png_bgra(os.path.join(REF, "test_data", "in0062.png"))
+    m0 = resize_u8(np.ascontiguousarray(fgimg[:, :, 3]), 60, 144) / 255.
+    rs = np.random.RandomState(13)
+    m1 = np.where(rs.rand(37, 41) < 0.5, 0., 1.)
+    m1[rs.rand(37, 41) < 0.05] = 0.5
+    m1[0, 0] = m1[-1, -1] = m1[0, -1] = m1[-1, 0] = 0.25
+    m2 = np.zeros((9, 11))
+    m2[4, 5] = 0.7
+    m2[:, 7:] = 1.
+    for i, m in enumerate([m0, m1, m2]):
+        d["matte%d" % i] = m
+        d["trimap%d" % i] = R.data.trimap_from_matte(m)
+    out["trimap"] = d
+
+
 def main():
     np.load = _fake_load
     R = load_reference()
@@ -411,6 +431,7 @@ def main():
     gen_loader(R, out)
     gen_tps(R, out)
     gen_augment(R, out)
+    gen_trimap(R, out)
     for name, d in out.items():
         np.savez_compressed(os.path.join(HERE, name + ".npz"), **d)
         print("wrote", name, os.path.getsize(os.path.join(HERE, name + ".npz")))

@@ -237,3 +237,28 @@ def test_augment_1080p_vs_oracle():
     assert np.array_equal(got[1], want[1])
     _u8_close(got[0], want[0], 2e-3)
     _f_close(got[2], want[2], 1e-9)
+
+
+# ---------------------------------------------------------------- data.py
+
+@pytest.mark.parametrize("i", [0, 1, 2])
+def test_trimap_matches_reference(i):
+    from vmatting import data as vd
+    g = golden("trimap")
+    assert np.array_equal(vd.trimap_from_matte(g["matte%d" % i]), g["trimap%d" % i])
+
+
+@pytest.mark.parametrize("shape", [(1, 1), (3, 200), (17, 65), (300, 517), (1080, 1920)])
+@pytest.mark.parametrize("dc", [(1, 3), (0, 0), (3, 1), (8, 2)])
+def test_trimap_bit_exact_vs_oracle(shape, dc):
+    from oracle import data as od
+    from vmatting import data as vd
+    rs = np.random.RandomState(shape[0] + 7 * dc[0] + dc[1])
+    h, w = shape
+    m = np.where(rs.rand(h, w) < 0.5, 0., 1.)
+    m[rs.rand(h, w) < 0.03] = rs.rand()
+    m[rs.rand(h, w) < 0.001] = np.nan
+    got = vd.trimap_from_matte(m, *dc)
+    assert np.array_equal(got, od.trimap_from_matte(m, *dc))
+    with pytest.raises(AssertionError):
+        vd.trimap_from_matte(m.astype(np.float32))

@@ -316,3 +316,11 @@ def test_cv_warp_affine_and_hsv_restatements_agree():
     assert np.array_equal(cv2.cvtColor(hsv, cv2.COLOR_HSV2BGR), oa.hsv2bgr(hsv))
     bgr = (rs.rand(30, 40, 3) * 255).astype(np.uint8)
     assert np.array_equal(cv2.cvtColor(bgr, cv2.COLOR_BGR2HSV), oa.bgr2hsv(bgr))
+
+
+@pytest.mark.parametrize("i", [0, 1, 2])
+def test_trimap_oracle_matches_reference(i):
+    """data.trimap_from_matte's raster loop (run verbatim for the fixture) == the half-window restatement."""
+    from oracle import data as od
+    g = golden("trimap")
+    assert np.array_equal(od.trimap_from_matte(g["matte%d" % i]), g["trimap%d" % i])

@@ -329,6 +329,53 @@ __global__ void __launch_bounds__(256) nonzero_stats_kernel(const T* __restrict_
   }
 }
 
+
+// ---------------------------------------------------------------------------------------------------- data.py
+
+// data.trimap_from_matte (data.py:37-67).  The reference's raster loop lets a known pixel's own assignment (255 for
+// matte 1, 0 for matte 0) overwrite every earlier 128-mark, so the result is 128 for unknown pixels and for known
+// pixels with an unknown pixel LATER in raster order within radius crop (matte 1) / dilate (matte 0).  A 16x64
+// tile's classes (0 / 1 / unknown / outside) are staged in LDS with the half-window halo below and to the sides.
+constexpr int kTriH = 16, kTriW = 64, kTriMaxSide = 8;
+
+__global__ void __launch_bounds__(256) trimap_kernel(const double* __restrict__ m, int h, int w, int dilate, int crop,
+                                                     uint8_t* __restrict__ out) {
+  __shared__ uint8_t cls[(kTriH + kTriMaxSide) * (kTriW + 2 * kTriMaxSide)];
+  const int side = dilate > crop ? dilate : crop;
+  const int r0 = blockIdx.y * kTriH, c0 = blockIdx.x * kTriW;
+  const int lw = kTriW + 2 * side, lh = kTriH + side;
+  for (int t = threadIdx.x; t < lh * lw; t += blockDim.x) {
+    const int rr = r0 + t / lw, cc = c0 - side + t % lw;
+    uint8_t k = 3;  // outside the image
+    if (rr < h && cc >= 0 && cc < w) {
+      const double v = m[(long)rr * w + cc];
+      k = v == 1. ? 1 : (v == 0. ? 0 : 2);
+    }
+    cls[t] = k;
+  }
+  __syncthreads();
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int c = c0 + tx;
+  if (c >= w) return;
+  for (int j = 0; j < kTriH / 4; ++j) {
+    const int lr = ty * (kTriH / 4) + j, r = r0 + lr;
+    if (r >= h) break;
+    const uint8_t own = cls[lr * lw + tx + side];
+    uint8_t v = 128;
+    if (own <= 1) {
+      v = own ? 255 : 0;
+      const int rad = own ? crop : dilate;
+      for (int dk = 0; dk <= rad && v != 128; ++dk)
+        for (int dl = (dk == 0 ? 1 : -rad); dl <= rad; ++dl)
+          if (cls[(lr + dk) * lw + tx + side + dl] == 2) {
+            v = 128;
+            break;
+          }
+    }
+    out[(long)r * w + c] = v;
+  }
+}
+
 }  // namespace vm
 
 using namespace vm;
@@ -461,4 +508,16 @@ extern "C" int vm_nonzero_stats(const void* alpha, int h, int w, int dtype, long
     default: return fail(VM_EUNSUPPORTED, "nonzero_stats: dtype %d", dtype);
   }
   return check_launch("nonzero_stats");
+}
+
+extern "C" int vm_trimap_from_matte(const double* matte, int h, int w, int dilate, int crop, uint8_t* trimap,
+                                    void* stream) {
+  if (!matte || !trimap || h <= 0 || w <= 0 || dilate < 0 || crop < 0)
+    return fail(VM_EINVAL, "trimap_from_matte: bad argument");
+  if (dilate > kTriMaxSide || crop > kTriMaxSide)
+    return fail(VM_EUNSUPPORTED, "trimap_from_matte: dilate/crop above %d", kTriMaxSide);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const dim3 g((w + kTriW - 1) / kTriW, (h + kTriH - 1) / kTriH), b(256);
+  hipLaunchKernelGGL(trimap_kernel, g, b, 0, st, matte, h, w, dilate, crop, trimap);
+  return check_launch("trimap_from_matte");
 }

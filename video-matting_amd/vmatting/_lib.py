@@ -101,6 +101,7 @@ SIGNATURES = [
                                c_int, c_int, c_void_p]),
     ("vm_change_illumination_u8", c_int, [c_void_p, c_long, ctypes.POINTER(ctypes.c_uint8), c_void_p, c_void_p]),
     ("vm_nonzero_stats", c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
+    ("vm_trimap_from_matte", c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
 ]
 
 _lib = None

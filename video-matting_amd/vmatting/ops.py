@@ -487,3 +487,16 @@ def nonzero_stats(alpha, out=None):
     check(lib().vm_nonzero_stats(_ptr(alpha), alpha.shape[0], alpha.shape[1], _dtype_code(alpha, "nonzero_stats"),
                                  _ptr(out), stream_handle()), "nonzero_stats")
     return out
+
+
+def trimap_from_matte(matte, dilate=1, crop=3, out=None):
+    """vm_trimap_from_matte: data.trimap_from_matte on a float64 [h, w] device matte -> uint8 [h, w]."""
+    _require_gpu(matte)
+    if matte.dtype != torch.float64 or matte.dim() != 2:
+        raise AssertionError("trimap_from_matte: float64 [h, w] matte expected (data.py:42)")
+    matte = matte.contiguous()
+    if out is None:
+        out = torch.empty(matte.shape, dtype=torch.uint8, device=matte.device)
+    check(lib().vm_trimap_from_matte(_ptr(matte), matte.shape[0], matte.shape[1], int(dilate), int(crop), _ptr(out),
+                                     stream_handle()), "trimap_from_matte")
+    return out
