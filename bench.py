@@ -226,6 +226,100 @@ def augment_bench(dev, steps, cpu=True, h=1080, w=1920):
     return rec
 
 
+def train_flops(n, h, w):
+    """Algorithmic FLOPs of one config-5 step: 3 frozen VGG16 towers + UNetSimple forward (unet_simple.py:45-171),
+    the filter gradient of every trainable conv and the data gradient of the convs whose input is trainable."""
+    from vmatting.train import DGRAD, LEVELS
+    from vmatting.unet_simple import NEW_CONVS, _levels
+    L = _levels(h, w)
+    vgg = [(0, 3, 64), (0, 64, 64), (1, 64, 128), (1, 128, 128), (2, 128, 256), (2, 256, 256), (2, 256, 256),
+           (3, 256, 512), (3, 512, 512), (3, 512, 512), (4, 512, 512), (4, 512, 512), (4, 512, 512)]
+    f = lambda lv, ci, co: 2.0 * n * L[lv][0] * L[lv][1] * 9 * ci * co  # noqa: E731
+    fwd = 3 * sum(f(*v) for v in vgg)
+    lvl = {"output": 0}
+    for lv, _, _, sels, up, _, conv, _ in LEVELS:
+        for s, _ in sels:
+            lvl[s] = lv
+        lvl[up] = lvl[conv] = lv
+    head = sum(f(lvl[s], ci, co) for s, ci, co in NEW_CONVS)
+    dgrad = sum(f(lvl[s], ci, co) for s, ci, co in NEW_CONVS if s in DGRAD)
+    return fwd + head, head + dgrad
+
+
+def train_bench(dev, steps, warmup, world, rank, cpu=True, n=8, size=320, dtype="bf16"):
+    """BASELINE config 5: one train.py video_procedure iteration per step (train.py:288-343) — batch of 8 320x320
+    samples per GPU (params.py:8-9) resident in HBM: 3 VGG16 towers + UNetSimple (batch-statistics BN) forward,
+    loss, backward through the trainable layers, one RCCL all-reduce of the gradients (DDP), TF-Adam, re-pack.
+    Device time per phase from HIP events on the launch stream; step time = max over ranks."""
+    from vmatting.train import VideoTrainer
+    from vmatting.weights import synthetic_vgg16
+    rs = np.random.RandomState(100 + rank)
+    mean = np.array([103.939, 116.779, 123.68])
+    fg = rs.uniform(0, 255, (n, size, size, 3))
+    bg = rs.uniform(0, 255, (n, size, size, 3))
+    yy, xx = np.mgrid[:size, :size]
+    gt = np.clip(1.2 - np.hypot((yy - size / 2) / (size / 3), (xx - size / 2) / (size / 4)), 0, 1)
+    gt = np.repeat(gt[None, :, :, None], n, 0)
+    cmp = gt * fg + (1 - gt) * bg - mean
+    warped = np.repeat(gt, 3, -1)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.float32)).to(dev)  # noqa: E731
+    cmp_d, bg_d, warped_d, gt_d, fg_d = T(cmp), T(bg - mean), T(warped), T(gt), T(fg)
+    np.random.seed(1)
+    trn = VideoTrainer(synthetic_vgg16(0), dtype, dev)
+    for _ in range(warmup):
+        trn.step(cmp_d, bg_d, warped_d, gt_d, fg_d)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+    fwd_ms = bwd_ms = upd_ms = 0.0
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        ev[0].record()
+        trn.forward(cmp_d, bg_d, warped_d)
+        from vmatting import ops
+        trn._tb["loss"].copy_(ops.matting_loss(trn._tb["alpha"], gt_d, fg_d, bg_d, cmp_d))
+        ev[1].record()
+        trn.grad.zero_()
+        trn.backward(gt_d, fg_d, bg_d, cmp_d)
+        ev[2].record()
+        trn.apply_gradients()
+        ev[3].record()
+        torch.cuda.synchronize()
+        fwd_ms += ev[0].elapsed_time(ev[1])
+        bwd_ms += ev[1].elapsed_time(ev[2])
+        upd_ms += ev[2].elapsed_time(ev[3])
+    wall = torch.tensor([(time.perf_counter() - t0) / steps], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(wall, op=dist.ReduceOp.MAX)
+    wall = float(wall)
+    fwd_f, bwd_f = train_flops(n, size, size)
+    rec = {"workload": "train.py video_procedure step (config 5): %d x %dx%d per GPU, 3 VGG16 towers + UNetSimple "
+                       "fwd/bwd, loss, DDP all-reduce, TF-Adam" % (n, size, size),
+           "dtype": dtype + " forward, f32 gradients/optimizer", "n_gpus": world,
+           "samples_per_s": round(n * world / wall, 1), "ms_per_step": round(1000 * wall, 3),
+           "device_ms": {"forward_loss": round(fwd_ms / steps, 3), "backward": round(bwd_ms / steps, 3),
+                         "allreduce_adam_repack": round(upd_ms / steps, 3)},
+           "flops_per_step_per_gpu": {"forward": fwd_f, "backward": bwd_f},
+           "achieved_tflops_per_gpu": round((fwd_f + bwd_f) / wall / 1e12, 1),
+           "loss_last": [round(float(v), 5) for v in trn._tb["loss"].cpu()]}
+    if cpu and world == 1:
+        from oracle import models as om  # the CPU-baseline leg only
+        from oracle import train_ref as tr
+        sh = 128
+        p = om.unet_simple_params(np.random.RandomState(1))
+        sl = lambda a: np.asarray(a[:1, :sh, :sh], np.float64)  # noqa: E731
+        t0 = time.perf_counter()
+        tr.train_step_grads(sl(cmp), sl(bg - mean), sl(warped), sl(gt), sl(fg), synthetic_vgg16(0), p)
+        dt = (time.perf_counter() - t0) * (size * size) / float(sh * sh)
+        rec["cpu_baseline"] = {"value": round(1.0 / dt, 4), "unit": "samples/s", "cores": torch.get_num_threads(),
+                               "kind": "port",
+                               "sample": "oracle/train_ref.py (numpy-f64 VGG towers + torch-f64 autograd head) on one "
+                                         "%dx%d sample, scaled x%.2f to %dx%d by pixel count" %
+                                         (sh, sh, (size * size) / float(sh * sh), size, size)}
+    return rec
+
+
 def load_traffic(args, full=False):
     """Per-launch HBM bytes per kernel from the committed PMC pass (tools/traffic.py -> profiles/*_traffic.json),
     used only when it was collected on this exact workload."""
@@ -294,6 +388,7 @@ def main():
     ap.add_argument("--no-graph", action="store_true", help="time eager launches instead of the captured HIP graph")
     ap.add_argument("--no-loader", action="store_true", help="skip the training-sample loader record (rank 0, N=1)")
     ap.add_argument("--no-augment", action="store_true", help="skip the augmentation record (rank 0, N=1)")
+    ap.add_argument("--no-train", action="store_true", help="skip the config-5 training-step record (all ranks)")
     ap.add_argument("--video-frames", type=int, default=256,
                     help="config-4 record: frames sharded over the ranks + matte all-gather (0 = skip)")
     ap.add_argument("--option", action="append", default=[], metavar="KEY=VALUE",
@@ -354,6 +449,10 @@ def main():
     if args.video_frames > 0 and graphed is not None and args.batch == 1:
         video = video_batch(graphed, args.video_frames, H, W, rank, world, dev)
 
+    train = None
+    if not args.no_train:  # every rank: the DDP all-reduce is part of the step
+        train = train_bench(dev, max(args.steps // 2, 5), 2, world, rank, cpu=not args.no_cpu_baseline)
+
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -389,6 +488,8 @@ def main():
                           "source": os.path.relpath(src, REPO)}
         if video:
             rec["video_batch"] = video
+        if train:
+            rec["train"] = train
         if world == 1 and not args.no_cpu_baseline:
             sh, sw = (int(v) for v in args.cpu_sample.split("x"))
             rec["cpu_baseline"] = cpu_baseline(H, W, sh, sw)

@@ -273,6 +273,48 @@ int vm_nonzero_stats(const void* alpha, int h, int w, int dtype, long long* stat
  * in the max-norm.  dilate, crop <= 8. */
 int vm_trimap_from_matte(const double* matte, int h, int w, int dilate, int crop, uint8_t* trimap, void* stream);
 
+/* ---------------------------------------------------------------- training step (config 5)
+ * Backward of train.py's loss through UNetSimple's trainable layers and tf.train.AdamOptimizer
+ * (train.py:288-343 video_procedure, 176-227 simple_procedure; unet_simple.py:19-42,116-142).  Gradients are f32;
+ * forward activations (x, y views) may be f32 or bf16. */
+
+/* dL/dlogits for alpha = sigmoid(logits) (unet_simple.py:142) under train.py:294-298's loss
+ * (regular_l1 train.py:21-28, composite :14-18); pred/gt [P], raw_fg/bg/cmp [P,3] f32 device; dlogits [P]. */
+int vm_matting_loss_backward(const float* pred, const float* gt, const float* raw_fg, const float* bg, const float* cmp,
+                             long pixels, float* dlogits, void* stream);
+
+/* Workspace of vm_bn_backward_nhwc for a c-channel view. */
+size_t vm_bn_backward_workspace_bytes(int channels);
+
+/* Gradient of tf.contrib.layers.batch_norm(is_training=True) (unet_simple.py:25,41) w.r.t. its input x, gamma and
+ * beta, given dy (f32) = dL/d(BN output); y (optional) = the relu output that followed the BN (unet_simple.py:120-141:
+ * tf.nn.relu(new_conv(...))), so g = dy * (y > 0).  mean/var: the batch statistics the forward normalised with.
+ * x == NULL: only dbeta = sum(g) (a bias gradient: the channel sum of dy).  dx / dgamma / dbeta may be NULL. */
+int vm_bn_backward_nhwc(const vm_tensor* x, const vm_tensor* dy, const vm_tensor* y, const float* mean,
+                        const float* var, const float* gamma, float eps, vm_tensor* dx, float* dgamma, float* dbeta,
+                        void* work, void* stream);
+
+/* tf.nn.relu gradient: dx = dy * (y > 0); dx f32. */
+int vm_relu_backward_nhwc(const vm_tensor* dy, const vm_tensor* y, vm_tensor* dx, void* stream);
+
+/* Adjoint of vm_resize_bilinear_tf1_nhwc (tf.image.resize_images, unet_simple.py:33): dy [n,oh,ow,c] (f32 view) ->
+ * dx contiguous f32 [n,ih,iw,c] (overwritten). */
+int vm_resize_bilinear_tf1_backward(const vm_tensor* dy, float* dx, int ih, int iw, void* stream);
+
+/* Weight gradient of the 3x3 SAME conv (tf.nn.conv2d, unet_simple.py:23,35): dw[3][3][cin][cout] (HWIO, f32) +=
+ * sum over pixels of x (view, cin = x->c) patch x dy (f32 view [n,h,w,cout]); cout <= 48.  Accumulates. */
+int vm_conv3x3_wgrad_nhwc(const vm_tensor* x, const vm_tensor* dy, float* dw, void* stream);
+
+/* The data-gradient filter of a 3x3 SAME conv: w_flipped[kh][kw][co][ci] = w[2-kh][2-kw][ci][co]; dx is then
+ * vm_conv3x3_nhwc(dy, pack(w_flipped)). */
+int vm_conv3x3_flip_weights(const float* w_hwio, int cin, int cout, float* w_flipped, void* stream);
+
+/* tf.train.AdamOptimizer's ApplyAdam (train.py:302-304) over n f32 values, g = grad * grad_scale:
+ * m += (g - m)(1 - beta1); v += (g^2 - v)(1 - beta2); var -= m * lr_t / (sqrt(v) + eps), with the caller's
+ * lr_t = lr * sqrt(1 - beta2^t) / (1 - beta1^t). */
+int vm_adam_tf(float* var, float* m, float* v, const float* grad, long n, float lr_t, float beta1, float beta2,
+               float eps, float grad_scale, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

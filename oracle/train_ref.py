@@ -1,0 +1,132 @@
+"""CPU restatement of the config-5 training step (TEST INFRASTRUCTURE — only tests/, smoke() and bench.py's
+cpu_baseline may use it; the product never does).
+
+  train_step_grads  one iteration of train.py's video_procedure / simple_procedure (train.py:288-343 / 176-227):
+                    create_model(cmp, bg, warped, phase=True) (unet_simple.py:145-171) with the frozen VGG towers
+                    taken from the numpy oracle (models.vgg16_tower), then UNetSimple restated in torch float64 so
+                    that autograd gives d loss / d every variable of 'model/simple_unet' (train.py:289)
+  adam_tf           tf.train.AdamOptimizer's ApplyAdam (train.py:302-304) in numpy float32, including TF's f32
+                    beta-power variables and lr_t = lr*sqrt(1-beta2^t)/(1-beta1^t)
+
+The forward is the same op sequence as models.unet_simple_forward (pinned by the reference builders' goldens,
+tests/golden/unet_simple_64_train.npz); tests check the two agree before trusting the gradients.  No TF gradient
+goldens exist (TF is absent), so the backward is pinned by autograd on that forward: "parity unpinned" against
+real TF 1.x gradients.
+"""
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from . import models as om
+
+BN_EPS = 1e-3
+
+LEVELS = (
+    ("conv4", ("select4_1", "select4_2", "select4_3"), "upconv4", "conv4"),
+    ("conv3", ("select3_1", "select3_2", "select3_3"), "upconv3", "conv3"),
+    ("conv2", ("select2_1", "select2_2"), "upconv2", "conv2"),
+    ("conv1", ("select1_1", "select1_2", "select1_3"), "upconv1", "conv1"),
+)
+
+
+def _conv(x, w, b=None):
+    """tf.nn.conv2d 3x3 SAME (+ bias_add) on NHWC with an HWIO filter."""
+    y = F.conv2d(x.permute(0, 3, 1, 2).contiguous(), w.permute(3, 2, 0, 1).contiguous(), b, padding=1)
+    return y.permute(0, 2, 3, 1)
+
+
+def _bn(x, gamma, beta):
+    mean = x.mean(dim=(0, 1, 2))
+    var = ((x - mean) ** 2).mean(dim=(0, 1, 2))
+    return (x - mean) * (gamma / torch.sqrt(var + BN_EPS)) + beta
+
+
+def _resize(x, oh, ow):
+    """TF-1 legacy bilinear (models/ops.resize_bilinear_tf1) as differentiable gathers."""
+    n, ih, iw, c = x.shape
+    if (ih, iw) == (oh, ow):
+        return x
+    sy = np.float32(ih) / np.float32(oh)
+    sx = np.float32(iw) / np.float32(ow)
+    ys = np.arange(oh, dtype=np.float32) * sy
+    xs = np.arange(ow, dtype=np.float32) * sx
+    y0 = np.floor(ys).astype(np.int64)
+    x0 = np.floor(xs).astype(np.int64)
+    y1 = np.minimum(y0 + 1, ih - 1)
+    x1 = np.minimum(x0 + 1, iw - 1)
+    fy = torch.from_numpy((ys - np.floor(ys)).astype(np.float64))[None, :, None, None]
+    fx = torch.from_numpy((xs - np.floor(xs)).astype(np.float64))[None, None, :, None]
+    T = lambda a: torch.from_numpy(a)  # noqa: E731
+    tl = x[:, T(y0)][:, :, T(x0)]
+    tr = x[:, T(y0)][:, :, T(x1)]
+    bl = x[:, T(y1)][:, :, T(x0)]
+    br = x[:, T(y1)][:, :, T(x1)]
+    top = tl + (tr - tl) * fx
+    bot = bl + (br - bl) * fx
+    return top + (bot - top) * fy
+
+
+def train_step_grads(cmp, bg, warped, gt, raw_fg, vgg, params, bn=None):
+    """-> (loss terms (loss, alpha_loss, cmp_loss), alpha, grads {(scope, kind): ndarray})
+
+    params: {scope: (w_hwio, bias|None)} (models.unet_simple_params); bn: {scope: (gamma, beta)} or fresh (1, 0).
+    kinds: 'w', 'b' (new_conv scopes), 'gamma', 'beta' — the trainable variables of unet_simple.py:19-42."""
+    f64 = lambda a: np.asarray(a, np.float64)  # noqa: E731
+    cmp, bg, warped = f64(cmp), f64(bg), f64(warped)
+    towers = [om.vgg16_tower(t, vgg) for t in (cmp, bg, warped)]
+    cat = lambda k: torch.from_numpy(np.concatenate([t[k] for t in towers], -1))  # noqa: E731
+    layers = {
+        "conv1": [torch.from_numpy(np.concatenate([cmp, bg, warped], -1)), cat("conv1_1"), cat("conv1_2")],
+        "conv2": [cat("conv2_1"), cat("conv2_2")],
+        "conv3": [cat("conv3_1"), cat("conv3_2"), cat("conv3_3")],
+        "conv4": [cat("conv4_1"), cat("conv4_2"), cat("conv4_3")],
+        "conv5": [cat("conv5_1"), cat("conv5_2"), cat("conv5_3")],
+    }
+    V = {}
+    for scope, (w, b) in params.items():
+        V[scope, "w"] = torch.tensor(f64(w), requires_grad=True)
+        if not scope.startswith("upconv"):
+            V[scope, "b"] = torch.tensor(f64(b), requires_grad=True)
+    widths = {"upconv4": 96, "upconv3": 48, "upconv2": 32, "upconv1": 30}
+    for scope, (w, b) in params.items():
+        c = widths.get(scope, w.shape[3])
+        g, be = (np.ones(c), np.zeros(c)) if bn is None or scope not in bn else bn[scope]
+        V[scope, "gamma"] = torch.tensor(f64(g), requires_grad=True)
+        V[scope, "beta"] = torch.tensor(f64(be), requires_grad=True)
+
+    def new_conv(x, s):
+        return _bn(_conv(x, V[s, "w"], V[s, "b"]), V[s, "gamma"], V[s, "beta"])
+
+    prev = layers["conv5"][-1]
+    for key, sels, up, conv in LEVELS:
+        srcs = layers[key]
+        outs = [torch.relu(new_conv(srcs[i], s)) for i, s in enumerate(sels)]
+        h, w = outs[0].shape[1:3]
+        u = torch.relu(_conv(_resize(prev, h, w), V[up, "w"]))
+        catn = _bn(torch.cat(outs + [u], -1), V[up, "gamma"], V[up, "beta"])
+        prev = torch.relu(new_conv(catn, conv))
+    alpha = torch.sigmoid(new_conv(prev, "output"))
+    gt_t, fg_t, bg_t, cmp_t = (torch.from_numpy(f64(a)) for a in (gt, raw_fg, bg, cmp))
+    eps2 = np.float64(np.float32(1e-6) ** 2)
+    la = torch.sqrt((alpha - gt_t) ** 2 + eps2)
+    lc = torch.sqrt((alpha * fg_t + (1 - alpha) * bg_t - cmp_t) ** 2 + eps2)
+    loss = (0.5 * la + 0.5 * lc).mean()
+    loss.backward()
+    grads = {k: v.grad.numpy().copy() for k, v in V.items()}
+    terms = (float(loss), float(la.mean()), float(lc.mean()))
+    return terms, alpha.detach().numpy(), grads
+
+
+def adam_tf(var, m, v, grad, t, lr=1e-3, beta1=0.9, beta2=0.999, eps=1e-8):
+    """ApplyAdam after ``t`` steps' beta-power updates (t >= 1), numpy float32 -> (var, m, v)."""
+    f = np.float32
+    b1p, b2p = f(1.0), f(1.0)
+    for _ in range(t):
+        b1p, b2p = f(b1p * f(beta1)), f(b2p * f(beta2))
+    lr_t = f(f(lr) * np.sqrt(f(1) - b2p) / (f(1) - b1p))
+    g = np.asarray(grad, f)
+    m = (m + (g - m) * (f(1) - f(beta1))).astype(f)
+    v = (v + (g * g - v) * (f(1) - f(beta2))).astype(f)
+    var = (var - (m * lr_t) / (np.sqrt(v) + f(eps))).astype(f)
+    return var, m, v

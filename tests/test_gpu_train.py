@@ -1,0 +1,288 @@
+"""GPU parity of the config-5 training step (train.py:288-343) against the CPU restatement oracle/train_ref.py.
+
+Tolerances (f32 kernels vs the float64 autograd restatement):
+  * single backward kernels (wgrad, BN backward, resize adjoint, loss backward): max-abs error <= 1e-4 of the
+    reference's max-abs (f32 accumulation order only);
+  * whole step, fp32 path: loss terms within 1e-5 relative, alpha within 1e-4 max-abs, every gradient tensor
+    within 2e-3 of its max-abs (BN over tiny spatial levels amplifies f32 rounding); conv-bias gradients, which
+    BN makes exactly zero in real arithmetic, within 2e-3 of the same scope's filter-gradient scale;
+  * Adam: the kernel's update equals numpy-f32 ApplyAdam on the same gradients to 1e-6 relative.
+Gradients are "parity unpinned" against real TF 1.x (absent); they are pinned by autograd on the oracle forward.
+"""
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import gpu_available
+from oracle import models as om
+from oracle import train_ref as tr
+
+pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not gpu_available(), reason="needs a ROCm GPU")]
+
+DEV = "cuda"
+
+
+def T(a, dtype=torch.float32):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(DEV, dtype)
+
+
+def H(t):
+    return t.detach().float().cpu().numpy().astype(np.float64)
+
+
+def scaled_err(a, b):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    return np.abs(a - b).max() / max(np.abs(b).max(), 1e-30)
+
+
+# ----------------------------------------------------------------------------- single kernels
+
+@pytest.mark.parametrize("cout", [1, 2, 4, 8, 16, 24, 32, 48])
+@pytest.mark.parametrize("xdtype", ["f32", "bf16"])
+def test_conv_wgrad(cout, xdtype):
+    from vmatting import ops
+    rs = np.random.RandomState(cout)
+    n, h, w, cin = 2, 13, 37, 70
+    x = rs.normal(size=(n, h, w, cin + 6)).astype(np.float32)
+    dy = rs.normal(size=(n, h, w, cout)).astype(np.float32)
+    tdt = torch.float32 if xdtype == "f32" else torch.bfloat16
+    xd = T(x, tdt)
+    xs = xd[..., 3:3 + cin]  # a channel-slice view, like the concat buffers
+    dw = torch.zeros((3, 3, cin, cout), dtype=torch.float32, device=DEV)
+    dyp = torch.zeros((n, h, w, cout + 2), device=DEV)
+    dyp[..., 1:1 + cout] = T(dy)
+    ops.conv_wgrad(xs, dyp[..., 1:1 + cout], dw)  # both operands as channel-slice views
+    xr = torch.from_numpy(H(xs)).requires_grad_(False)
+    wr = torch.zeros((3, 3, cin, cout), dtype=torch.float64, requires_grad=True)
+    y = tr._conv(xr, wr)
+    (y * torch.from_numpy(dy.astype(np.float64))).sum().backward()
+    assert scaled_err(H(dw), wr.grad.numpy()) <= 1e-4
+
+
+def test_conv_wgrad_accumulates_and_large_cin():
+    from vmatting import ops
+    rs = np.random.RandomState(3)
+    x = rs.normal(size=(1, 6, 9, 1536)).astype(np.float32)
+    dy = rs.normal(size=(1, 6, 9, 16)).astype(np.float32)
+    dw = torch.ones((3, 3, 1536, 16), dtype=torch.float32, device=DEV)
+    ops.conv_wgrad(T(x), T(dy), dw)
+    wr = torch.zeros((3, 3, 1536, 16), dtype=torch.float64, requires_grad=True)
+    (tr._conv(torch.from_numpy(x.astype(np.float64)), wr) * torch.from_numpy(dy.astype(np.float64))).sum().backward()
+    assert scaled_err(H(dw) - 1.0, wr.grad.numpy()) <= 1e-4
+
+
+def test_conv_wgrad_rejects_wide_cout():
+    from vmatting import ops
+    x = torch.zeros((1, 4, 4, 8), device=DEV)
+    with pytest.raises(NotImplementedError):
+        ops.conv_wgrad(x, torch.zeros((1, 4, 4, 64), device=DEV), torch.zeros((3, 3, 8, 64), device=DEV))
+
+
+@pytest.mark.parametrize("cin,cout", [(1, 32), (24, 48), (32, 24), (48, 96)])
+def test_conv_dgrad_through_flipped_filter(cin, cout):
+    """dx of y = conv(x, w) equals the forward conv of dy with flip_weights(w) (f32 MFMA path)."""
+    from vmatting import ops
+    rs = np.random.RandomState(cin)
+    n, h, w = 2, 11, 19
+    wt = rs.normal(size=(3, 3, cout, cin)).astype(np.float32)  # forward filter cout -> cin (dgrad maps cin -> cout)
+    dy = rs.normal(size=(n, h, w, cin)).astype(np.float32)
+    wf = torch.empty((3, 3, cin, cout), dtype=torch.float32, device=DEV)
+    ops.flip_weights(T(wt), wf)
+    pc = ops.PackedConv(wf, None, "fp32", DEV)
+    dyp = torch.zeros((n, h, w, (cin + 7) // 8 * 8), device=DEV)  # conv input views: channels padded to 8
+    dyp[..., :cin] = T(dy)
+    dx = ops.conv3x3(dyp[..., :cin], pc, "none", affine=False)
+    xr = torch.zeros((n, h, w, cout), dtype=torch.float64, requires_grad=True)
+    (tr._conv(xr, torch.from_numpy(wt.astype(np.float64))) * torch.from_numpy(dy.astype(np.float64))).sum().backward()
+    assert scaled_err(H(dx), xr.grad.numpy()) <= 1e-4
+
+
+@pytest.mark.parametrize("mask", [False, True])
+def test_bn_backward(mask):
+    from vmatting import ops
+    rs = np.random.RandomState(5)
+    n, h, w, c = 2, 9, 14, 20
+    x = (rs.normal(size=(n, h, w, c)) * 3 + 1).astype(np.float32)
+    gamma = rs.uniform(0.5, 1.5, c).astype(np.float32)
+    beta = rs.normal(size=c).astype(np.float32)
+    dy = rs.normal(size=(n, h, w, c)).astype(np.float32)
+    xd = T(x)
+    mean, var = ops.bn_stats(xd)
+    y = ops.bn_apply(xd, mean, var, T(gamma), T(beta), 1e-3, "relu" if mask else "none", out=torch.empty_like(xd))
+    dx = torch.empty_like(xd)
+    dg = torch.empty(c, device=DEV)
+    db = torch.empty(c, device=DEV)
+    ops.bn_backward(xd, T(dy), y if mask else None, mean, var, T(gamma), 1e-3, dx=dx, dgamma=dg, dbeta=db)
+    xr = torch.tensor(x.astype(np.float64), requires_grad=True)
+    gr = torch.tensor(gamma.astype(np.float64), requires_grad=True)
+    br = torch.tensor(beta.astype(np.float64), requires_grad=True)
+    out = tr._bn(xr, gr, br)
+    if mask:
+        out = torch.relu(out)
+    (out * torch.from_numpy(dy.astype(np.float64))).sum().backward()
+    assert scaled_err(H(dx), xr.grad.numpy()) <= 1e-4
+    assert scaled_err(H(dg), gr.grad.numpy()) <= 1e-4
+    assert scaled_err(H(db), br.grad.numpy()) <= 1e-4
+    # bias-gradient mode: channel sums only
+    s = torch.empty(c, device=DEV)
+    ops.bn_backward(None, T(dy), None, None, None, None, dbeta=s)
+    assert scaled_err(H(s), dy.astype(np.float64).sum(axis=(0, 1, 2))) <= 1e-5
+
+
+@pytest.mark.parametrize("ih,iw,oh,ow", [(5, 7, 10, 14), (3, 4, 5, 7), (17, 30, 34, 60), (8, 8, 8, 8)])
+def test_resize_backward(ih, iw, oh, ow):
+    from vmatting import ops
+    rs = np.random.RandomState(ih)
+    dy = rs.normal(size=(2, oh, ow, 6)).astype(np.float32)
+    dx = torch.empty((2, ih, iw, 6), dtype=torch.float32, device=DEV)
+    ops.resize_backward(T(dy), dx)
+    xr = torch.zeros((2, ih, iw, 6), dtype=torch.float64, requires_grad=True)
+    (tr._resize(xr, oh, ow) * torch.from_numpy(dy.astype(np.float64))).sum().backward()
+    assert scaled_err(H(dx), xr.grad.numpy()) <= 1e-5
+
+
+def test_relu_backward():
+    from vmatting import ops
+    rs = np.random.RandomState(2)
+    y = np.maximum(rs.normal(size=(1, 5, 6, 7)), 0).astype(np.float32)
+    dy = rs.normal(size=(1, 5, 6, 7)).astype(np.float32)
+    dx = torch.empty((1, 5, 6, 7), device=DEV)
+    ops.relu_backward(T(dy), T(y), dx)
+    assert np.array_equal(H(dx), np.where(y > 0, dy, 0).astype(np.float64))
+
+
+def test_loss_backward():
+    from vmatting import ops
+    rs = np.random.RandomState(9)
+    P = 3000
+    a = rs.uniform(0.01, 0.99, (P, 1)).astype(np.float32)
+    gt = rs.uniform(0, 1, (P, 1)).astype(np.float32)
+    fg, bg, cmp = (rs.uniform(-120, 150, (P, 3)).astype(np.float32) for _ in range(3))
+    g = ops.matting_loss_backward(T(a), T(gt), T(fg), T(bg), T(cmp))
+    lg = torch.tensor(np.log(a / (1 - a)).astype(np.float64), requires_grad=True)
+    al = torch.sigmoid(lg)
+    eps2 = np.float64(np.float32(1e-6) ** 2)
+    t = lambda v: torch.from_numpy(v.astype(np.float64))  # noqa: E731
+    loss = (0.5 * torch.sqrt((al - t(gt)) ** 2 + eps2) + 0.5 * torch.sqrt((al * t(fg) + (1 - al) * t(bg) - t(cmp)) ** 2
+                                                                           + eps2)).mean()
+    loss.backward()
+    assert scaled_err(H(g), lg.grad.numpy()) <= 1e-4
+
+
+def test_adam_matches_tf_applyadam():
+    from vmatting import ops
+    rs = np.random.RandomState(4)
+    n = 10007
+    var = rs.normal(size=n).astype(np.float32)
+    g1, g2 = (rs.normal(size=n).astype(np.float32) for _ in range(2))
+    vd, md, vvd = T(var), torch.zeros(n, device=DEV), torch.zeros(n, device=DEV)
+    ref = (var, np.zeros(n, np.float32), np.zeros(n, np.float32))
+    for t, g in ((1, g1), (2, g2)):
+        f = np.float32
+        b1p = f(1)
+        b2p = f(1)
+        for _ in range(t):
+            b1p, b2p = f(b1p * f(0.9)), f(b2p * f(0.999))
+        lr_t = f(f(1e-3) * np.sqrt(f(1) - b2p) / (f(1) - b1p))
+        ops.adam_tf(vd, md, vvd, T(g * 2), lr_t, 0.9, 0.999, 1e-8, grad_scale=0.5)
+        ref = tr.adam_tf(*ref, g, t)
+    assert np.abs(H(vd) - ref[0]).max() <= 1e-6 * max(1.0, np.abs(ref[0]).max())
+    assert scaled_err(H(md), ref[1]) <= 1e-6
+
+
+# ----------------------------------------------------------------------------- whole step
+
+def _batch(n, h, w, seed=11):
+    rs = np.random.RandomState(seed)
+    mean = np.array([103.939, 116.779, 123.68])
+    fg = rs.uniform(0, 255, (n, h, w, 3))
+    bg = rs.uniform(0, 255, (n, h, w, 3))
+    yy, xx = np.mgrid[:h, :w]
+    gt = np.clip(1.2 - np.hypot((yy - h / 2) / (h / 3), (xx - w / 2) / (w / 3)), 0, 1)[None, :, :, None]
+    gt = np.repeat(gt, n, 0)
+    cmp = gt * fg + (1 - gt) * bg - mean
+    warped = np.repeat(np.clip(gt + rs.normal(0, 0.05, gt.shape), 0, 1), 3, -1)
+    f = lambda a: a.astype(np.float32)  # noqa: E731
+    return f(cmp), f(bg - mean), f(warped), f(gt), f(fg)
+
+
+@pytest.fixture(scope="module")
+def step_case():
+    from vmatting.train import VideoTrainer
+    from vmatting.weights import synthetic_vgg16
+    vgg = synthetic_vgg16(0)
+    params = om.unet_simple_params(np.random.RandomState(1))
+    rs = np.random.RandomState(2)
+    bn = {s: (rs.uniform(0.5, 1.5, c).astype(np.float32), rs.normal(0, 0.2, c).astype(np.float32))
+          for s, c in [(k, (w.shape[3] if not k.startswith("upconv") else {"upconv4": 96, "upconv3": 48,
+                                                                          "upconv2": 32, "upconv1": 30}[k]))
+                       for k, (w, _) in params.items()]}
+    cmp, bg, warped, gt, fg = _batch(2, 64, 80)
+    trn = VideoTrainer(vgg, "fp32", DEV, params=params, bn=bn)
+    p0 = H(trn.flat).astype(np.float32)
+    loss = H(trn.step(cmp, bg, warped, gt, fg))
+    torch.cuda.synchronize()
+    terms, alpha, grads = tr.train_step_grads(cmp, bg, warped, gt, fg, vgg, params, bn)
+    return dict(trn=trn, p0=p0, loss=loss, terms=terms, alpha=alpha, grads=grads, alpha_gpu=H(trn.output))
+
+
+def test_train_step_loss_and_alpha(step_case):
+    c = step_case
+    np.testing.assert_allclose(c["loss"], c["terms"], rtol=1e-5)
+    assert np.abs(c["alpha_gpu"] - c["alpha"]).max() <= 1e-4
+
+
+def test_train_step_gradients(step_case):
+    """Relative L2 error <= 2e-3 and max-abs <= 1.5e-2 of each tensor's max-abs.  The f32 forward flips a few relu
+    / max-pool decisions of the f64 restatement on near-zero values; at the deep levels (a few hundred pixels per
+    channel) one flipped pixel moves a filter gradient by ~1/M of its scale, so max-abs is looser than L2."""
+    c = step_case
+    trn, grads = c["trn"], c["grads"]
+    bad, worst = [], 0.0
+    for (scope, kind), g_ref in grads.items():
+        g = H(trn.G[scope, kind])
+        # conv biases are exactly zero in real arithmetic (BN removes them): bound by the filter-gradient scale
+        scale = np.abs(grads[scope, "w"]).max() if kind == "b" else np.abs(g_ref).max()
+        l2 = np.linalg.norm(g - g_ref) / max(np.linalg.norm(grads[scope, "w"] if kind == "b" else g_ref), 1e-30)
+        mx = np.abs(g - g_ref).max() / scale
+        worst = max(worst, l2)
+        if not (mx <= 1.5e-2 and (kind == "b" or l2 <= 2e-3)):
+            bad.append((scope, kind, round(float(l2), 5), round(float(mx), 5)))
+    print("worst relative L2 gradient error %.2e" % worst)
+    assert not bad, bad
+
+
+def test_train_step_adam_update(step_case):
+    c = step_case
+    trn = c["trn"]
+    g = H(trn.grad).astype(np.float32)
+    want, _, _ = tr.adam_tf(c["p0"], np.zeros_like(g), np.zeros_like(g), g, 1)
+    assert np.abs(H(trn.flat) - want).max() <= 1e-6 * max(1.0, np.abs(want).max())
+    # the packed forward filters follow the updated flat buffer
+    from vmatting import ops
+    pc = trn.model.convs["conv2"]
+    x = torch.randn((1, 6, 7, pc.cin), device=DEV)
+    fresh = ops.PackedConv(trn.P["conv2", "w"].clone(), trn.P["conv2", "b"].clone(), "fp32", DEV)
+    assert torch.equal(ops.conv3x3(x, pc, "none", affine=False), ops.conv3x3(x, fresh, "none", affine=False))
+
+
+def test_train_second_step_decreases_nothing_nan(step_case):
+    c = step_case
+    trn = c["trn"]
+    cmp, bg, warped, gt, fg = _batch(2, 40, 56)
+    loss2 = H(trn.step(cmp, bg, warped, gt, fg))
+    assert np.all(np.isfinite(loss2)) and np.all(np.isfinite(H(trn.flat)))
+    assert trn.t == 2
+
+
+def test_train_step_bf16_runs():
+    from vmatting.train import VideoTrainer
+    from vmatting.weights import synthetic_vgg16
+    params = om.unet_simple_params(np.random.RandomState(1))
+    cmp, bg, warped, gt, fg = _batch(2, 64, 64)
+    trn = VideoTrainer(synthetic_vgg16(0), "bf16", DEV, params=params)
+    losses = [H(trn.step(cmp, bg, warped, gt, fg))[0] for _ in range(3)]
+    assert np.all(np.isfinite(losses)) and np.all(np.isfinite(H(trn.grad)))
+    terms, _, grads = tr.train_step_grads(cmp, bg, warped, gt, fg, synthetic_vgg16(0), params)
+    assert abs(losses[0] - terms[0]) <= 0.05 * terms[0]

@@ -1,0 +1,109 @@
+"""CPU checks of the config-5 training step's host side and its oracle (no GPU):
+the torch-f64 restatement's forward equals the numpy oracle (pinned by the reference builders' goldens), its
+gradients pass a finite-difference probe, the flat parameter layout covers the trainable variables, TF-Adam's
+oracle behaves as ApplyAdam, and the DDP gradient all-reduce is correct at world size 2 (gloo)."""
+
+import multiprocessing as mp
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import models as om
+from oracle import ops as oops
+from oracle import train_ref as tr
+from vmatting.train import param_layout
+
+
+def _case(n=1, h=20, w=24, seed=3):
+    rs = np.random.RandomState(seed)
+    mean = np.array([103.939, 116.779, 123.68])
+    fg = rs.uniform(0, 255, (n, h, w, 3))
+    bg = rs.uniform(0, 255, (n, h, w, 3))
+    gt = rs.uniform(0, 1, (n, h, w, 1))
+    cmp = gt * fg + (1 - gt) * bg - mean
+    warped = np.repeat(gt, 3, -1)
+    return cmp, bg - mean, warped, gt, fg
+
+
+@pytest.fixture(scope="module")
+def small_vgg():
+    return om.synthetic_vgg16(0)
+
+
+def test_restatement_forward_matches_numpy_oracle(small_vgg):
+    cmp, bg, warped, gt, fg = _case()
+    p = om.unet_simple_params(np.random.RandomState(1))
+    terms, alpha, grads = tr.train_step_grads(cmp, bg, warped, gt, fg, small_vgg, p)
+    ref = om.unet_simple_forward(cmp, bg, warped, True, small_vgg, p)
+    assert np.abs(alpha - ref["output"]).max() <= 1e-10
+    np.testing.assert_allclose(terms, oops.matting_loss(ref["output"], gt, fg, bg, cmp), rtol=1e-9)
+    assert set(grads) == {(s, k) for s, k, _, _ in param_layout()[0]}
+
+
+def test_restatement_gradient_finite_difference(small_vgg):
+    """Central differences on a few filter/gamma entries of the deepest and shallowest layers."""
+    cmp, bg, warped, gt, fg = _case(h=16, w=16, seed=4)
+    p = om.unet_simple_params(np.random.RandomState(2))
+    _, _, grads = tr.train_step_grads(cmp, bg, warped, gt, fg, small_vgg, p)
+    for scope, idx in (("output", (1, 1, 3, 0)), ("conv2", (0, 2, 5, 7)), ("upconv3", (2, 1, 10, 4))):
+        h = 1e-4
+        w = p[scope][0].astype(np.float64)
+        vals = []
+        for s in (h, -h):
+            q = dict(p)
+            w2 = w.copy()
+            w2[idx] += s
+            q[scope] = (w2, p[scope][1])
+            vals.append(tr.train_step_grads(cmp, bg, warped, gt, fg, small_vgg, q)[0][0])
+        fd = (vals[0] - vals[1]) / (2 * h)
+        assert abs(fd - grads[scope, "w"][idx]) <= 1e-5 * max(1.0, abs(fd)) + 1e-7, (scope, fd, grads[scope, "w"][idx])
+
+
+def test_param_layout_is_the_trainable_set():
+    from vmatting.train import param_layout
+    from vmatting.unet_simple import NEW_CONVS
+    lay, n = param_layout()
+    conv = sum(9 * ci * co for _, ci, co in NEW_CONVS)
+    bias = sum(co for s, _, co in NEW_CONVS if not s.startswith("upconv"))
+    bnw = sum({"upconv4": 96, "upconv3": 48, "upconv2": 32, "upconv1": 30}.get(s, co) for s, _, co in NEW_CONVS)
+    assert n == conv + bias + 2 * bnw
+    assert 1.5e6 < n < 1.7e6  # ~1.62M trainable simple_unet parameters
+    offs = [o for _, _, o, _ in lay]
+    assert offs == sorted(offs) and len(set(offs)) == len(offs)
+    assert not any(s.startswith("upconv") and k == "b" for s, k, _, _ in lay)
+
+
+def test_adam_oracle_first_step_is_lr_sign():
+    g = np.array([3.0, -0.5, 1e-3, -20.0], np.float32)
+    var, m, v = tr.adam_tf(np.zeros(4, np.float32), np.zeros(4, np.float32), np.zeros(4, np.float32), g, 1)
+    np.testing.assert_allclose(var, -1e-3 * np.sign(g), rtol=1e-3)  # eps costs 3e-4 at |g| = 1e-3
+    np.testing.assert_allclose(m, 0.1 * g, rtol=1e-6)
+
+
+def _ddp_worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    from vmatting import parallel
+    parallel.init_from_env(backend="gloo")
+    try:
+        g = torch.arange(10, dtype=torch.float32) * (rank + 1)
+        scale = parallel.allreduce_grads(g)
+        ok = scale == 0.5 and torch.equal(g * scale, torch.arange(10, dtype=torch.float32) * 1.5)
+        q.put((rank, bool(ok)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gradient_allreduce_gloo_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 30500 + (os.getpid() % 1000)
+    procs = [ctx.Process(target=_ddp_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(60)
+    assert sorted(r for r, _ in res) == [0, 1] and all(ok for _, ok in res), res

@@ -1,0 +1,430 @@
+// Backward pass + optimizer of the config-5 training step (train.py:288-343, video_procedure; the same graph
+// as simple_procedure, train.py:176-227): the gradient of
+//   loss = mean(0.5*regular_l1(pred, gt) + 0.5*regular_l1(composite(raw_fg, bg, pred), cmp))   (train.py:294-298)
+// through UNetSimple's trainable layers (unet_simple.py:116-142: conv + bias -> batch_norm(is_training) -> relu,
+// upconv_concat's resize -> conv -> relu -> concat -> batch_norm), and tf.train.AdamOptimizer's update
+// (train.py:302-304).  The frozen VGG towers (tf.constant weights, unet_simple.py:109-113) need no gradient.
+//
+//   loss_backward   dL/dlogits of sigmoid(logits) under the Charbonnier alpha + compositional loss
+//   bn_backward     fused-BN gradient (batch statistics), optional relu mask from the BN+relu output:
+//                   dx = gamma*rstd*(g - sum(g)/M - xhat*sum(g*xhat)/M), dgamma = sum(g*xhat), dbeta = sum(g)
+//   conv_wgrad      dW[kh,kw,ci,co] = sum_p x[p + (kh-1, kw-1), ci] * dy[p, co]: per block an LDS patch of
+//                   (4+2) x (32+2) pixels x CC channels and the 4 x 32 dy tile; each thread owns one (kh, ci,
+//                   4-channel co group) and slides the three kw taps along a pixel row (1 new LDS x read and one
+//                   float4 dy read per 12 FMAs); blocks walk tiles persistently, one atomic flush per block
+//   conv dgrad      the forward conv kernels on flipped, transposed weights (flip_weights here)
+//   resize_backward adjoint of the TF-1 legacy bilinear resize (4 atomic taps per output element)
+//   relu_backward   dy * (y > 0)
+//   adam            TF ApplyAdam: m += (g-m)(1-b1); v += (g^2-v)(1-b2); var -= m*lr_t/(sqrt(v)+eps)
+
+#include "vm_common.h"
+
+namespace vm {
+namespace trn {
+
+struct V {
+  char* p;
+  int n, h, w, c, cs, coff, dt;
+};
+
+static V mk(const vm_tensor* t) {
+  V v;
+  v.p = reinterpret_cast<char*>(t->ptr);
+  v.n = t->n; v.h = t->h; v.w = t->w; v.c = t->c; v.cs = t->cstride; v.coff = t->coff; v.dt = t->dtype;
+  return v;
+}
+
+__device__ __forceinline__ float ld(const V& v, long pix, int c) {
+  const long o = pix * v.cs + v.coff + c;
+  return v.dt == VM_F32 ? reinterpret_cast<const float*>(v.p)[o] : bf2f(reinterpret_cast<const uint16_t*>(v.p)[o]);
+}
+
+__device__ __forceinline__ void st(const V& v, long pix, int c, float x) {
+  const long o = pix * v.cs + v.coff + c;
+  if (v.dt == VM_F32) reinterpret_cast<float*>(v.p)[o] = x;
+  else reinterpret_cast<uint16_t*>(v.p)[o] = f2bf(x);
+}
+
+// ---------------------------------------------------------------- loss backward (train.py:21-28, 294-298)
+// s_loss is [N,H,W,3] (the [N,H,W,1] alpha term broadcast), so with P pixels
+//   dL/dpred = 0.5/(3P) * (3*(a-g)/La + sum_k e_k/Lc_k * (fg_k - bg_k)),   e_k = a*fg_k + (1-a)*bg_k - cmp_k
+// and dL/dlogits = dL/dpred * a*(1-a) (tf.nn.sigmoid's gradient in terms of its output).
+__global__ __launch_bounds__(256) void loss_backward_kernel(const float* __restrict__ pred, const float* __restrict__ gt,
+                                                            const float* __restrict__ fg, const float* __restrict__ bg,
+                                                            const float* __restrict__ cmp, long P, float* dlogit) {
+  const float eps2 = 1e-6f * 1e-6f;
+  const float k = 0.5f / (3.0f * (float)P);
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < P; i += (long)gridDim.x * blockDim.x) {
+    const float a = pred[i];
+    const float d = a - gt[i];
+    float s = 3.f * d / sqrtf(d * d + eps2);
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const float f = fg[i * 3 + j], b = bg[i * 3 + j];
+      const float e = a * f + (1.f - a) * b - cmp[i * 3 + j];
+      s += e / sqrtf(e * e + eps2) * (f - b);
+    }
+    dlogit[i] = k * s * a * (1.f - a);
+  }
+}
+
+// ---------------------------------------------------------------- batch-norm backward (training statistics)
+constexpr int BN_NBLK = 240;
+
+template <bool MASK>
+__device__ __forceinline__ float grad_in(const V& dy, const V& y, long p, int c) {
+  const float g = ld(dy, p, c);
+  if (MASK) return ld(y, p, c) > 0.f ? g : 0.f;
+  return g;
+}
+
+// per (64-channel group, pixel block): double partial sums of g and g*xhat (x == NULL: g only)
+template <bool MASK>
+__global__ __launch_bounds__(256) void bn_bwd_partial(V x, V dy, V y, const float* mean, const float* var, float eps,
+                                                      double* part, int nblk) {
+  __shared__ double sh[2][4][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  const long M = (long)dy.n * dy.h * dy.w;
+  double s1 = 0.0, s2 = 0.0;
+  if (c < dy.c) {
+    const float m = x.p ? mean[c] : 0.f;
+    const float r = x.p ? 1.0f / sqrtf(var[c] + eps) : 0.f;
+    for (long p = (long)blockIdx.y * 4 + wave; p < M; p += (long)nblk * 4) {
+      const float g = grad_in<MASK>(dy, y, p, c);
+      s1 += g;
+      if (x.p) s2 += (double)g * (double)((ld(x, p, c) - m) * r);
+    }
+  }
+  sh[0][wave][lane] = s1;
+  sh[1][wave][lane] = s2;
+  __syncthreads();
+  if (wave == 0 && c < dy.c) {
+    s1 = sh[0][0][lane] + sh[0][1][lane] + sh[0][2][lane] + sh[0][3][lane];
+    s2 = sh[1][0][lane] + sh[1][1][lane] + sh[1][2][lane] + sh[1][3][lane];
+    part[(long)blockIdx.y * dy.c + c] = s1;
+    part[(long)nblk * dy.c + (long)blockIdx.y * dy.c + c] = s2;
+  }
+}
+
+__global__ void bn_bwd_final(const double* part, int nblk, int C, float* sum_g, float* sum_gx) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s1 = 0.0, s2 = 0.0;
+  for (int b = 0; b < nblk; ++b) {
+    s1 += part[(long)b * C + c];
+    s2 += part[(long)nblk * C + (long)b * C + c];
+  }
+  if (sum_g) sum_g[c] = (float)s1;
+  if (sum_gx) sum_gx[c] = (float)s2;
+}
+
+template <bool MASK>
+__global__ void bn_bwd_apply(V x, V dy, V y, const float* mean, const float* var, const float* gamma, float eps,
+                             const float* sum_g, const float* sum_gx, V dx) {
+  const long M = (long)dy.n * dy.h * dy.w;
+  const long total = M * dy.c;
+  const float invM = 1.0f / (float)M;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % dy.c);
+    const long p = i / dy.c;
+    const float r = 1.0f / sqrtf(var[c] + eps);
+    const float xh = (ld(x, p, c) - mean[c]) * r;
+    const float g = grad_in<MASK>(dy, y, p, c);
+    const float gm = gamma ? gamma[c] : 1.f;
+    st(dx, p, c, gm * r * (g - sum_g[c] * invM - xh * sum_gx[c] * invM));
+  }
+}
+
+__global__ void relu_bwd_kernel(V dy, V y, V dx) {
+  const long total = (long)dy.n * dy.h * dy.w * dy.c;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % dy.c);
+    const long p = i / dy.c;
+    st(dx, p, c, ld(y, p, c) > 0.f ? ld(dy, p, c) : 0.f);
+  }
+}
+
+// ---------------------------------------------------------------- resize backward (adjoint of resize_tf1)
+__device__ __forceinline__ void tf1c(int i, float scale, int in, int& lo, int& hi, float& lerp) {
+#pragma clang fp contract(off)
+  const float src = (float)i * scale;
+  const float fl = floorf(src);
+  lo = (int)fl;
+  hi = min(lo + 1, in - 1);
+  lerp = src - fl;
+}
+
+__global__ void resize_bwd_kernel(V dy, float* dx, int ih, int iw, float sy, float sx) {
+  const long total = (long)dy.n * dy.h * dy.w * dy.c;
+  const int C = dy.c;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    const long op = i / C;
+    const int ow = (int)(op % dy.w);
+    const long t = op / dy.w;
+    const int oh = (int)(t % dy.h);
+    const int n = (int)(t / dy.h);
+    int y0, y1, x0, x1;
+    float yl, xl;
+    tf1c(oh, sy, ih, y0, y1, yl);
+    tf1c(ow, sx, iw, x0, x1, xl);
+    const float g = ld(dy, op, c);
+    const float gt = g * (1.f - yl), gb = g * yl;
+    const long rb = (long)n * ih;
+    atomicAdd(dx + ((rb + y0) * iw + x0) * C + c, gt * (1.f - xl));
+    atomicAdd(dx + ((rb + y0) * iw + x1) * C + c, gt * xl);
+    atomicAdd(dx + ((rb + y1) * iw + x0) * C + c, gb * (1.f - xl));
+    atomicAdd(dx + ((rb + y1) * iw + x1) * C + c, gb * xl);
+  }
+}
+
+// ---------------------------------------------------------------- conv weight gradient
+constexpr int WG_TH = 4, WG_TW = 32, WG_PH = WG_TH + 2, WG_PW = WG_TW + 2, WG_NT = 256;
+
+template <int CC, int CO4>
+__global__ __launch_bounds__(WG_NT) void wgrad_kernel(V x, V dy, float* dw,
+                                                      int tiles_h, int tiles_w, long ntiles) {
+  constexpr int TASKS = 3 * CC * CO4;
+  constexpr int TPT = (TASKS + WG_NT - 1) / WG_NT;
+  __shared__ float xs[WG_PH * WG_PW * CC];
+  __shared__ float4 ds[WG_TH * WG_TW * CO4];
+  const int tid = threadIdx.x;
+  const int c0 = blockIdx.y * CC;
+  const int cin = x.c, cout = dy.c;
+  float acc[TPT][3][4];
+#pragma unroll
+  for (int k = 0; k < TPT; ++k)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) acc[k][j][0] = acc[k][j][1] = acc[k][j][2] = acc[k][j][3] = 0.f;
+
+  for (long tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int tx = (int)(tile % tiles_w);
+    const long t2 = tile / tiles_w;
+    const int ty = (int)(t2 % tiles_h);
+    const int n = (int)(t2 / tiles_h);
+    const int y0 = ty * WG_TH, x0 = tx * WG_TW;
+    for (int e = tid; e < WG_PH * WG_PW * CC; e += WG_NT) {
+      const int ci = e % CC;
+      const int pc = e / CC;
+      const int col = pc % WG_PW, r = pc / WG_PW;
+      const int gy = y0 + r - 1, gx = x0 + col - 1, c = c0 + ci;
+      float v = 0.f;
+      if (gy >= 0 && gy < x.h && gx >= 0 && gx < x.w && c < cin) v = ld(x, ((long)n * x.h + gy) * x.w + gx, c);
+      xs[e] = v;
+    }
+    float* dsf = reinterpret_cast<float*>(ds);
+    for (int e = tid; e < WG_TH * WG_TW * CO4 * 4; e += WG_NT) {
+      const int co = e % (CO4 * 4);
+      const int pp = e / (CO4 * 4);
+      const int gy = y0 + pp / WG_TW, gx = x0 + pp % WG_TW;
+      float v = 0.f;
+      if (gy < x.h && gx < x.w && co < cout) v = ld(dy, ((long)n * x.h + gy) * x.w + gx, co);
+      dsf[e] = v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < TPT; ++k) {
+      const int t = tid + k * WG_NT;
+      if (TASKS % WG_NT == 0 || t < TASKS) {
+        const int ci = t % CC;
+        const int cg = (t / CC) % CO4;
+        const int kh = t / (CC * CO4);
+        for (int py = 0; py < WG_TH; ++py) {
+          const float* row = xs + ((py + kh) * WG_PW) * CC + ci;
+          const float4* drow = ds + py * WG_TW * CO4 + cg;
+          float xa = row[0], xb = row[CC];
+#pragma unroll 8
+          for (int px = 0; px < WG_TW; ++px) {
+            const float xc = row[(px + 2) * CC];
+            const float4 d = drow[px * CO4];
+            acc[k][0][0] += xa * d.x; acc[k][0][1] += xa * d.y; acc[k][0][2] += xa * d.z; acc[k][0][3] += xa * d.w;
+            acc[k][1][0] += xb * d.x; acc[k][1][1] += xb * d.y; acc[k][1][2] += xb * d.z; acc[k][1][3] += xb * d.w;
+            acc[k][2][0] += xc * d.x; acc[k][2][1] += xc * d.y; acc[k][2][2] += xc * d.z; acc[k][2][3] += xc * d.w;
+            xa = xb;
+            xb = xc;
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int k = 0; k < TPT; ++k) {
+    const int t = tid + k * WG_NT;
+    if (TASKS % WG_NT == 0 || t < TASKS) {
+      const int ci = t % CC;
+      const int cg = (t / CC) % CO4;
+      const int kh = t / (CC * CO4);
+      const int c = c0 + ci;
+      if (c < cin) {
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int co = cg * 4 + j;
+            if (co < cout) atomicAdd(dw + (((long)(kh * 3 + kw) * cin + c) * cout + co), acc[k][kw][j]);
+          }
+      }
+    }
+  }
+}
+
+// HWIO [3][3][cin][cout] -> the dgrad filter [3][3][cout][cin], spatially flipped
+__global__ void flip_weights_kernel(const float* w, int cin, int cout, float* wt) {
+  const long total = 9L * cin * cout;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int co = (int)(i % cout);
+    const long r = i / cout;
+    const int ci = (int)(r % cin);
+    const int tap = (int)(r / cin);
+    wt[((long)(8 - tap) * cout + co) * cin + ci] = w[i];
+  }
+}
+
+// ---------------------------------------------------------------- Adam (tf.train.AdamOptimizer, train.py:302-304)
+__global__ void adam_kernel(float* var, float* m, float* v, const float* grad, long n, float lr_t, float beta1,
+                            float beta2, float eps, float grad_scale) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+#pragma clang fp contract(off)
+    const float g = grad[i] * grad_scale;
+    const float mi = m[i] + (g - m[i]) * (1.f - beta1);
+    const float vi = v[i] + (g * g - v[i]) * (1.f - beta2);
+    m[i] = mi;
+    v[i] = vi;
+    var[i] = var[i] - (mi * lr_t) / (sqrtf(vi) + eps);
+  }
+}
+
+template <int CC, int CO4>
+static void launch_wgrad(const V& xv, const V& dy, float* dw, hipStream_t st) {
+  const int tiles_h = (xv.h + WG_TH - 1) / WG_TH, tiles_w = (xv.w + WG_TW - 1) / WG_TW;
+  const long ntiles = (long)xv.n * tiles_h * tiles_w;
+  const int ncc = (xv.c + CC - 1) / CC;
+  long gx = (2048 + ncc - 1) / ncc;
+  if (gx > ntiles) gx = ntiles;
+  if (gx < 1) gx = 1;
+  hipLaunchKernelGGL((wgrad_kernel<CC, CO4>), dim3((unsigned)gx, ncc), dim3(WG_NT), 0, st, xv, dy, dw, tiles_h,
+                     tiles_w, ntiles);
+}
+
+static bool ok_view(const vm_tensor* t) { return valid_tensor(t); }
+
+static bool same_shape(const vm_tensor* a, const vm_tensor* b) {
+  return a->n == b->n && a->h == b->h && a->w == b->w && a->c == b->c;
+}
+
+}  // namespace trn
+}  // namespace vm
+
+using namespace vm;
+using namespace vm::trn;
+
+extern "C" int vm_matting_loss_backward(const float* pred, const float* gt, const float* raw_fg, const float* bg,
+                                        const float* cmp, long pixels, float* dlogits, void* stream) {
+  if (!pred || !gt || !raw_fg || !bg || !cmp || !dlogits || pixels <= 0)
+    return fail(VM_EINVAL, "matting_loss_backward: bad argument");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(loss_backward_kernel, dim3(grid_for(pixels, 256)), dim3(256), 0, st, pred, gt, raw_fg, bg, cmp,
+                     pixels, dlogits);
+  return check_launch("matting_loss_backward");
+}
+
+extern "C" size_t vm_bn_backward_workspace_bytes(int channels) {
+  return channels <= 0 ? 0 : (size_t)2 * BN_NBLK * channels * sizeof(double) + (size_t)2 * channels * sizeof(float);
+}
+
+extern "C" int vm_bn_backward_nhwc(const vm_tensor* x, const vm_tensor* dy, const vm_tensor* y, const float* mean,
+                                   const float* var, const float* gamma, float eps, vm_tensor* dx, float* dgamma,
+                                   float* dbeta, void* work, void* stream) {
+  if (!ok_view(dy) || dy->dtype != VM_F32 || !work) return fail(VM_EINVAL, "bn_backward: bad dy / workspace");
+  if (x && (!ok_view(x) || !same_shape(x, dy) || !mean || !var)) return fail(VM_EINVAL, "bn_backward: bad x");
+  if (y && (!ok_view(y) || !same_shape(y, dy))) return fail(VM_EINVAL, "bn_backward: bad relu mask y");
+  if (dx && (!x || !ok_view(dx) || !same_shape(dx, dy) || dx->dtype != VM_F32))
+    return fail(VM_EINVAL, "bn_backward: dx needs x and an f32 [n,h,w,c] view");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  V xv{}, yv{}, dyv = mk(dy);
+  if (x) xv = mk(x);
+  if (y) yv = mk(y);
+  const int C = dy->c;
+  double* part = reinterpret_cast<double*>(work);
+  // the two channel sums land in dbeta / dgamma when given, else in the float tail of the workspace
+  float* tail = reinterpret_cast<float*>(part + 2L * BN_NBLK * C);
+  float* sg = dbeta ? dbeta : tail;
+  float* sgx = dgamma ? dgamma : tail + C;
+  dim3 grid((C + 63) / 64, BN_NBLK);
+  if (y) hipLaunchKernelGGL(bn_bwd_partial<true>, grid, dim3(256), 0, st, xv, dyv, yv, mean, var, eps, part, BN_NBLK);
+  else hipLaunchKernelGGL(bn_bwd_partial<false>, grid, dim3(256), 0, st, xv, dyv, yv, mean, var, eps, part, BN_NBLK);
+  int rc = check_launch("bn_backward_partial");
+  if (rc) return rc;
+  hipLaunchKernelGGL(bn_bwd_final, dim3((C + 63) / 64), dim3(64), 0, st, part, BN_NBLK, C, sg, x ? sgx : nullptr);
+  rc = check_launch("bn_backward_final");
+  if (rc || !dx) return rc;
+  const long work_n = (long)dy->n * dy->h * dy->w * C;
+  if (y)
+    hipLaunchKernelGGL(bn_bwd_apply<true>, dim3(grid_for(work_n, 256)), dim3(256), 0, st, xv, dyv, yv, mean, var,
+                       gamma, eps, sg, sgx, mk(dx));
+  else
+    hipLaunchKernelGGL(bn_bwd_apply<false>, dim3(grid_for(work_n, 256)), dim3(256), 0, st, xv, dyv, yv, mean, var,
+                       gamma, eps, sg, sgx, mk(dx));
+  return check_launch("bn_backward_apply");
+}
+
+extern "C" int vm_relu_backward_nhwc(const vm_tensor* dy, const vm_tensor* y, vm_tensor* dx, void* stream) {
+  if (!ok_view(dy) || !ok_view(y) || !ok_view(dx) || !same_shape(dy, y) || !same_shape(dy, dx))
+    return fail(VM_EINVAL, "relu_backward: bad tensors");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const long n = (long)dy->n * dy->h * dy->w * dy->c;
+  hipLaunchKernelGGL(relu_bwd_kernel, dim3(grid_for(n, 256)), dim3(256), 0, st, mk(dy), mk(y), mk(dx));
+  return check_launch("relu_backward");
+}
+
+extern "C" int vm_resize_bilinear_tf1_backward(const vm_tensor* dy, float* dx, int ih, int iw, void* stream) {
+  if (!ok_view(dy) || !dx || ih <= 0 || iw <= 0) return fail(VM_EINVAL, "resize_backward: bad argument");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  hipError_t e = hipMemsetAsync(dx, 0, (size_t)dy->n * ih * iw * dy->c * sizeof(float), st);
+  if (e != hipSuccess) return fail(VM_EHIP, "resize_backward: %s", hipGetErrorString(e));
+  const float sy = (float)ih / (float)dy->h, sx = (float)iw / (float)dy->w;
+  const long n = (long)dy->n * dy->h * dy->w * dy->c;
+  hipLaunchKernelGGL(resize_bwd_kernel, dim3(grid_for(n, 256)), dim3(256), 0, st, mk(dy), dx, ih, iw, sy, sx);
+  return check_launch("resize_backward");
+}
+
+extern "C" int vm_conv3x3_wgrad_nhwc(const vm_tensor* x, const vm_tensor* dy, float* dw, void* stream) {
+  if (!ok_view(x) || !ok_view(dy) || !dw || dy->dtype != VM_F32 || dy->n != x->n || dy->h != x->h || dy->w != x->w)
+    return fail(VM_EINVAL, "conv3x3_wgrad: bad argument");
+  const int cout = dy->c;
+  if (cout > 48) return fail(VM_EUNSUPPORTED, "conv3x3_wgrad: cout %d > 48", cout);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  V xv = mk(x), dv = mk(dy);
+  const int co4 = (cout + 3) / 4;
+  switch (co4) {
+    case 1: launch_wgrad<64, 1>(xv, dv, dw, st); break;
+    case 2: launch_wgrad<64, 2>(xv, dv, dw, st); break;
+    case 3:
+    case 4: launch_wgrad<32, 4>(xv, dv, dw, st); break;
+    case 5:
+    case 6: launch_wgrad<32, 6>(xv, dv, dw, st); break;
+    case 7:
+    case 8: launch_wgrad<32, 8>(xv, dv, dw, st); break;
+    default: launch_wgrad<32, 12>(xv, dv, dw, st); break;
+  }
+  return check_launch("conv3x3_wgrad");
+}
+
+extern "C" int vm_conv3x3_flip_weights(const float* w_hwio, int cin, int cout, float* w_flipped, void* stream) {
+  if (!w_hwio || !w_flipped || cin <= 0 || cout <= 0) return fail(VM_EINVAL, "flip_weights: bad argument");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(flip_weights_kernel, dim3(grid_for(9L * cin * cout, 256)), dim3(256), 0, st, w_hwio, cin, cout,
+                     w_flipped);
+  return check_launch("flip_weights");
+}
+
+extern "C" int vm_adam_tf(float* var, float* m, float* v, const float* grad, long n, float lr_t, float beta1,
+                          float beta2, float eps, float grad_scale, void* stream) {
+  if (!var || !m || !v || !grad || n <= 0) return fail(VM_EINVAL, "adam: bad argument");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n, 256)), dim3(256), 0, st, var, m, v, grad, n, lr_t, beta1, beta2,
+                     eps, grad_scale);
+  return check_launch("adam");
+}

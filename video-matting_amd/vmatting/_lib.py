@@ -102,6 +102,17 @@ SIGNATURES = [
     ("vm_change_illumination_u8", c_int, [c_void_p, c_long, ctypes.POINTER(ctypes.c_uint8), c_void_p, c_void_p]),
     ("vm_nonzero_stats", c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
     ("vm_trimap_from_matte", c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
+    ("vm_matting_loss_backward", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_void_p,
+                                         c_void_p]),
+    ("vm_bn_backward_workspace_bytes", c_size_t, [c_int]),
+    ("vm_bn_backward_nhwc", c_int, [P, P, P, c_void_p, c_void_p, c_void_p, c_float, P, c_void_p, c_void_p, c_void_p,
+                                    c_void_p]),
+    ("vm_relu_backward_nhwc", c_int, [P, P, P, c_void_p]),
+    ("vm_resize_bilinear_tf1_backward", c_int, [P, c_void_p, c_int, c_int, c_void_p]),
+    ("vm_conv3x3_wgrad_nhwc", c_int, [P, P, c_void_p, c_void_p]),
+    ("vm_conv3x3_flip_weights", c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p]),
+    ("vm_adam_tf", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_float, c_float, c_float, c_float,
+                           c_float, c_void_p]),
 ]
 
 _lib = None

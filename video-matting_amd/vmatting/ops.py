@@ -96,6 +96,13 @@ class PackedConv:
                                                 stream_handle()), "pack_weights(up2x)")
         return self._up
 
+    def repack(self):
+        """Re-pack after the f32 HWIO filter changed in place (the optimizer step of train.VideoTrainer)."""
+        check(lib().vm_conv3x3_pack_weights(_ptr(self.w_hwio), self.cin, self.cout, _DT[self.dtype],
+                                            _ptr(self.packed), stream_handle()), "pack_weights")
+        self._up = None
+        return self
+
     def set_affine(self, scale, shift):
         self.scale = None if scale is None else torch.as_tensor(scale, dtype=torch.float32).to(self.packed.device)
         self.shift = None if shift is None else torch.as_tensor(shift, dtype=torch.float32).to(self.packed.device)
@@ -500,3 +507,75 @@ def trimap_from_matte(matte, dilate=1, crop=3, out=None):
     check(lib().vm_trimap_from_matte(_ptr(matte), matte.shape[0], matte.shape[1], int(dilate), int(crop), _ptr(out),
                                      stream_handle()), "trimap_from_matte")
     return out
+
+
+# ---------------------------------------------------------------- training step (train.py:288-343, config 5)
+
+def matting_loss_backward(pred, gt, raw_fg, in_bg, in_cmp, out=None):
+    """dL/dlogits of train.py:294-298's loss for pred = sigmoid(logits) (all contiguous f32 device tensors)."""
+    ts = [_f32(t) for t in (pred, gt, raw_fg, in_bg, in_cmp)]
+    pixels = ts[0].numel()
+    if ts[1].numel() != pixels or any(t.numel() != 3 * pixels for t in ts[2:]):
+        raise ValueError("matting_loss_backward: pred/gt [P], raw_fg/bg/cmp [P,3]")
+    out = torch.empty_like(ts[0]) if out is None else _f32(out)
+    check(lib().vm_matting_loss_backward(*[_ptr(t) for t in ts], pixels, _ptr(out), stream_handle()),
+          "matting_loss_backward")
+    return out
+
+
+def bn_backward(x, dy, y, mean, var, gamma, eps=1e-3, dx=None, dgamma=None, dbeta=None):
+    """Gradient of tf.contrib batch_norm(is_training=True) (+ the relu after it when ``y`` is given).
+    x None: only dbeta = channel sum of dy (a bias gradient)."""
+    c = dy.shape[-1]
+    views = [None if t is None else nhwc(t) for t in (x, dy, y, dx)]
+    ref = lambda v: None if v is None else ctypes.byref(v)  # noqa: E731
+    ws = _workspace(lib().vm_bn_backward_workspace_bytes(c), dy.device)
+    check(lib().vm_bn_backward_nhwc(ref(views[0]), ref(views[1]), ref(views[2]), _ptr(mean), _ptr(var), _ptr(gamma),
+                                    float(eps), ref(views[3]), _ptr(dgamma), _ptr(dbeta), _ptr(ws), stream_handle()),
+          "bn_backward")
+    return dx
+
+
+def relu_backward(dy, y, dx):
+    dv, yv, xv = nhwc(dy), nhwc(y), nhwc(dx)
+    check(lib().vm_relu_backward_nhwc(ctypes.byref(dv), ctypes.byref(yv), ctypes.byref(xv), stream_handle()),
+          "relu_backward")
+    return dx
+
+
+def resize_backward(dy, dx):
+    """Adjoint of resize_bilinear: dy [n,oh,ow,c] -> dx contiguous f32 [n,ih,iw,c] (overwritten)."""
+    _f32(dx)
+    if dx.shape[0] != dy.shape[0] or dx.shape[3] != dy.shape[3]:
+        raise ValueError("resize_backward: batch/channel mismatch")
+    dv = nhwc(dy)
+    check(lib().vm_resize_bilinear_tf1_backward(ctypes.byref(dv), _ptr(dx), dx.shape[1], dx.shape[2],
+                                                stream_handle()), "resize_backward")
+    return dx
+
+
+def conv_wgrad(x, dy, dw):
+    """dw[3,3,cin,cout] += 3x3 SAME conv weight gradient of input view x and f32 output-gradient view dy."""
+    _f32(dw)
+    n, h, w, cin = x.shape
+    cout = dy.shape[-1]
+    if tuple(dy.shape) != (n, h, w, cout) or dw.numel() != 9 * cin * cout:
+        raise ValueError("conv_wgrad: x %s, dy %s, dw %s" % (tuple(x.shape), tuple(dy.shape), tuple(dw.shape)))
+    xv, dv = nhwc(x), nhwc(dy)
+    check(lib().vm_conv3x3_wgrad_nhwc(ctypes.byref(xv), ctypes.byref(dv), _ptr(dw), stream_handle()), "conv_wgrad")
+    return dw
+
+
+def flip_weights(w_hwio, out):
+    cin, cout = int(w_hwio.shape[2]), int(w_hwio.shape[3])
+    check(lib().vm_conv3x3_flip_weights(_ptr(_f32(w_hwio)), cin, cout, _ptr(_f32(out)), stream_handle()),
+          "flip_weights")
+    return out
+
+
+def adam_tf(var, m, v, grad, lr_t, beta1, beta2, eps, grad_scale=1.0):
+    for t in (var, m, v, grad):
+        _f32(t)
+    check(lib().vm_adam_tf(_ptr(var), _ptr(m), _ptr(v), _ptr(grad), var.numel(), float(lr_t), float(beta1),
+                           float(beta2), float(eps), float(grad_scale), stream_handle()), "adam")
+    return var

@@ -71,3 +71,13 @@ def gather_frames(local, n_frames, out=None):
     if all(b - a == mx for a, b in sizes):
         return out
     return torch.cat([out[r * mx:r * mx + (b - a)] for r, (a, b) in enumerate(sizes)], dim=0)
+
+
+def allreduce_grads(flat):
+    """Data-parallel gradient exchange of the training step (train.py:302-304 under DDP): ONE all-reduce (sum) of
+    the flat f32 gradient buffer (≈6.5 MB for UNetSimple).  Returns the scale (1/world) the optimizer applies, so
+    the averaging costs no extra pass over the buffer."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return 1.0
+    dist.all_reduce(flat, op=dist.ReduceOp.SUM)
+    return 1.0 / dist.get_world_size()

@@ -1,0 +1,252 @@
+"""Config-5 training step on gfx950 kernels: train.py's video_procedure / simple_procedure iteration.
+
+One ``VideoTrainer.step(cmp, bg, warped, gt, raw_fg)`` is one ``sess.run([train_merged, train_op], feed_dict)``
+of the reference (train.py:325-327; simple_procedure train.py:205-208 feeds ``diff = cmp - bg`` instead of the
+warped previous alpha, train.py:245):
+
+  forward   unet_simple.create_model(cmp, bg, warped, phase=True) (unet_simple.py:145-171) — the frozen VGG16
+            towers, then UNetSimple with batch-statistics BN (is_training=True); pre-BN tensors and batch
+            statistics are kept for the backward pass
+  loss      loss = mean(0.5*regular_l1(pred, gt) + 0.5*regular_l1(composite(raw_fg, bg, pred), cmp))
+            (train.py:294-298; the summary scalars [loss, alpha_loss, cmp_loss] are returned)
+  backward  through the trainable 'model/simple_unet' variables only (train.py:289: TRAINABLE_VARIABLES of that
+            scope — conv weights and biases, BN gamma/beta); hand-written kernels (csrc/train.hip): BN backward
+            with the relu mask, conv weight gradient, conv data gradient (forward kernels on flipped weights),
+            TF-1 resize adjoint.  The upconv biases (unet_simple.py:34, drawn but unused) get no gradient, so
+            TF's apply_gradients skips them; here they are simply not parameters
+  exchange  DDP: one RCCL all-reduce of the flat gradient buffer (parallel.allreduce_grads); BN statistics stay
+            per replica (each rank normalises over its own batch of 8, as the single-device reference does)
+  update    tf.train.AdamOptimizer(lr, beta1=0.9, beta2=0.999, epsilon=1e-8) (train.py:300-304) over the flat
+            parameter buffer in one launch, then the forward / data-gradient filters are re-packed
+
+The moving BN statistics are never updated, as in the reference (UPDATE_OPS is not wired, train.py:304).
+"""
+
+import numpy as np
+import torch
+
+from . import ops, parallel
+from .layers import EPS
+from .unet_simple import NEW_CONVS, UNetSimple, Vgg16, _levels
+
+# UNetSimple levels from the bottom up (unet_simple.py:119-141):
+# (level, concat buffer, width, [(select scope, source)], upconv scope, upconv input, conv scope, conv output)
+LEVELS = (
+    (3, "up4", 96, (("select4_1", "cat_conv4_1"), ("select4_2", "cat_conv4_2"), ("select4_3", "cat_conv4_3")),
+     "upconv4", "cat_conv5_3", "conv4", "c4"),
+    (2, "up3", 48, (("select3_1", "cat_conv3_1"), ("select3_2", "cat_conv3_2"), ("select3_3", "cat_conv3_3")),
+     "upconv3", "c4", "conv3", "c3"),
+    (1, "up2", 32, (("select2_1", "cat_conv2_1"), ("select2_2", "cat_conv2_2")), "upconv2", "c3", "conv2", "c2"),
+    (0, "up1", 30, (("select1_1", "in9"), ("select1_2", "cat_conv1_1"), ("select1_3", "cat_conv1_2")),
+     "upconv1", "c2", "conv1", "c1"),
+)
+RBUF = {"upconv4": "r4", "upconv3": "r3", "upconv2": "r2", "upconv1": "r1"}
+# convs whose input is itself trainable: they need a data gradient (the select convs and upconv4 read frozen
+# VGG features / the network input)
+DGRAD = ("output", "conv1", "conv2", "conv3", "conv4", "upconv1", "upconv2", "upconv3")
+BN_WIDTH = {lv[4]: lv[2] for lv in LEVELS}
+
+
+def param_layout():
+    """Flat f32 layout of the trainable variables in TF creation order (unet_simple.py:119-142): per scope the
+    filter [3,3,cin,cout], the bias (new_conv only), then bn/beta and bn/gamma.  -> [(scope, kind, offset, shape)]"""
+    out, off = [], 0
+    for name, cin, cout in NEW_CONVS:
+        ents = [("w", (3, 3, cin, cout))]
+        if not name.startswith("upconv"):
+            ents.append(("b", (cout,)))
+        c = BN_WIDTH.get(name, cout)
+        ents += [("beta", (c,)), ("gamma", (c,))]
+        for kind, shape in ents:
+            out.append((name, kind, off, shape))
+            off += int(np.prod(shape))
+    return out, off
+
+
+class VideoTrainer:
+    """train.video_procedure's iteration on device (also simple_procedure's: pass diff = cmp - bg as ``warped``)."""
+
+    def __init__(self, vgg16_npy_path=None, dtype="fp32", device="cuda", params=None, bn=None, lr=1e-3,
+                 beta1=0.9, beta2=0.999, epsilon=1e-8):
+        self.vgg = vgg16_npy_path if isinstance(vgg16_npy_path, Vgg16) else Vgg16(vgg16_npy_path, dtype, device)
+        self.model = UNetSimple(self.vgg, True, dtype, device, params)
+        self.device = self.model.device
+        self.lr, self.beta1, self.beta2, self.epsilon = lr, beta1, beta2, epsilon
+        self.layout, n = param_layout()
+        dev = self.device
+        self.flat = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.grad = torch.zeros_like(self.flat)
+        self.m = torch.zeros_like(self.flat)
+        self.v = torch.zeros_like(self.flat)
+        self.P, self.G = {}, {}
+        for scope, kind, off, shape in self.layout:
+            self.P[scope, kind] = self.flat[off:off + int(np.prod(shape))].view(shape)
+            self.G[scope, kind] = self.grad[off:off + int(np.prod(shape))].view(shape)
+        # move the freshly drawn variables into the flat buffer and alias every consumer onto it
+        for scope, pc in self.model.convs.items():
+            self.P[scope, "w"].copy_(pc.w_hwio)
+            pc.w_hwio = self.P[scope, "w"]
+            if (scope, "b") in self.P:
+                self.P[scope, "b"].copy_(pc.bias)
+                pc.bias = self.P[scope, "b"]
+        for scope, bnl in self.model.bn.items():
+            if bn is not None and scope in bn:
+                bnl.set(*bn[scope])
+            self.P[scope, "gamma"].copy_(bnl.gamma)
+            self.P[scope, "beta"].copy_(bnl.beta)
+            bnl.gamma, bnl.beta = self.P[scope, "gamma"], self.P[scope, "beta"]
+        # data-gradient filters: flipped / transposed f32 copies, packed for the forward conv kernels
+        self.dconv, self._wflip = {}, {}
+        for scope in DGRAD:
+            pc = self.model.convs[scope]
+            self._wflip[scope] = torch.empty((3, 3, pc.cout, pc.cin), dtype=torch.float32, device=dev)
+            ops.flip_weights(pc.w_hwio, self._wflip[scope])
+            self.dconv[scope] = ops.PackedConv(self._wflip[scope], None, "fp32", dev)
+        self.t = 0
+        self._b1p = np.float32(1.0)
+        self._b2p = np.float32(1.0)
+        self._tb, self._key = None, None
+
+    # ------------------------------------------------------------------------------------------- buffers
+    def _train_buffers(self, n, h, w):
+        if self._key == (n, h, w):
+            return self._tb
+        L = _levels(h, w)
+        dev = self.device
+        F = lambda lv, c: torch.empty((n, L[lv][0], L[lv][1], c), dtype=torch.float32, device=dev)  # noqa: E731
+        tb = {"alpha": F(0, 1), "dlogit": F(0, 1), "loss": torch.zeros(3, dtype=torch.float32, device=dev)}
+        st = lambda c: (torch.empty(c, dtype=torch.float32, device=dev),  # noqa: E731
+                        torch.empty(c, dtype=torch.float32, device=dev))
+        for lv, cat, width, sels, up, prev, conv, cout_key in LEVELS:
+            for s, _ in sels + ((conv, None),):
+                c = self.model.convs[s].cout
+                tb["z_" + s], tb["dz_" + s], tb["st_" + s] = F(lv, c), F(lv, c), st(c)
+            tb["st_" + up] = st(width)
+            tb["dcatn_" + up] = F(lv, width)
+            tb["dcat_" + up] = F(lv, width)
+            tb["du_" + up] = F(lv, self.model.convs[up].cout)
+            if up in DGRAD:
+                tb["dr_" + up] = F(lv, self.model.convs[up].cin)
+                tb["dprev_" + up] = F(lv + 1, self.model.convs[up].cin)
+            tb["dout_" + conv] = F(lv, self.model.convs[conv].cout)
+        # the output conv's dz feeds the data-gradient conv, whose input views need channels padded to 8
+        tb["z_output"], tb["st_output"] = F(0, 1), st(1)
+        tb["dz_output"] = torch.zeros((n, h, w, 8), dtype=torch.float32, device=dev)[..., :1]
+        self._tb, self._key = tb, (n, h, w)
+        return tb
+
+    @staticmethod
+    def _src(b, key):
+        return b["in9"][..., :9] if key == "in9" else b[key]
+
+    # ------------------------------------------------------------------------------------------- forward
+    def _new_conv(self, x, scope, act, out, tb):
+        """new_conv (unet_simple.py:19-27) with batch statistics, then ``act``; keeps z and (mean, var)."""
+        z, (mean, var) = tb["z_" + scope], tb["st_" + scope]
+        ops.conv3x3(x, self.model.convs[scope], "none", out=z, affine=False)
+        ops.bn_stats(z, mean, var)
+        bnl = self.model.bn[scope]
+        ops.bn_apply(z, mean, var, bnl.gamma, bnl.beta, EPS, act, out=out)
+
+    def forward(self, cmp, bg, warped):
+        m = self.model
+        xs = [t if isinstance(t, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(t, np.float32))
+              for t in (cmp, bg, warped)]
+        xs = [t.to(self.device, torch.float32) for t in xs]
+        n, h, w, _ = xs[0].shape
+        b = m._buffers(n, h, w)
+        tb = self._train_buffers(n, h, w)
+        L = _levels(h, w)
+        for t in range(3):
+            ops.convert(xs[t], b["in"][t])
+            ops.convert(xs[t], b["in9"][..., 3 * t:3 * t + 3])
+            m._tower(b, t)
+        for lv, cat, width, sels, up, prev, conv, out_key in LEVELS:
+            c, off = b[cat][..., :width], 0
+            for s, src in sels:
+                co = m.convs[s].cout
+                self._new_conv(self._src(b, src), s, "relu", c[..., off:off + co], tb)
+                off += co
+            # upconv_concat (unet_simple.py:30-42): resize -> conv (no bias) -> relu -> concat -> BN
+            r = ops.resize_bilinear(b[prev], L[lv], out=b[RBUF[up]])
+            ops.conv3x3(r, m.convs[up], "relu", out=c[..., off:width], affine=False)
+            mean, var = tb["st_" + up]
+            ops.bn_stats(c, mean, var)
+            ops.bn_apply(c, mean, var, m.bn[up].gamma, m.bn[up].beta, EPS, "none", out=b[cat + "n"][..., :width])
+            self._new_conv(b[cat + "n"][..., :width], conv, "relu", b[out_key], tb)
+        self._new_conv(b["c1"], "output", "sigmoid", tb["alpha"], tb)
+        self.output = tb["alpha"]
+        return self.output
+
+    # ------------------------------------------------------------------------------------------- backward
+    def _conv_backward(self, scope, x_in, dy, mask, tb, dgrad_out=None):
+        """BN(+relu) backward into dz, then bias / filter gradients, optionally the data gradient of x_in."""
+        z, dz, (mean, var) = tb["z_" + scope], tb["dz_" + scope], tb["st_" + scope]
+        ops.bn_backward(z, dy, mask, mean, var, self.P[scope, "gamma"], EPS, dx=dz,
+                        dgamma=self.G[scope, "gamma"], dbeta=self.G[scope, "beta"])
+        ops.bn_backward(None, dz, None, None, None, None, dbeta=self.G[scope, "b"])
+        ops.conv_wgrad(x_in, dz, self.G[scope, "w"])
+        if dgrad_out is not None:
+            ops.conv3x3(dz, self.dconv[scope], "none", out=dgrad_out, affine=False)
+        return dz
+
+    def backward(self, gt, raw_fg, bg, cmp):
+        m, tb = self.model, self._tb
+        b = m._ws
+        ops.matting_loss_backward(tb["alpha"], gt, raw_fg, bg, cmp, out=tb["dlogit"])
+        dout = tb["dout_conv1"]
+        self._conv_backward("output", b["c1"], tb["dlogit"], None, tb, dgrad_out=dout)
+        for lv, cat, width, sels, up, prev, conv, out_key in reversed(LEVELS):
+            c, cn = b[cat][..., :width], b[cat + "n"][..., :width]
+            self._conv_backward(conv, cn, dout, b[out_key], tb, dgrad_out=tb["dcatn_" + up])
+            mean, var = tb["st_" + up]
+            ops.bn_backward(c, tb["dcatn_" + up], None, mean, var, self.P[up, "gamma"], EPS, dx=tb["dcat_" + up],
+                            dgamma=self.G[up, "gamma"], dbeta=self.G[up, "beta"])
+            dcat, off = tb["dcat_" + up], 0
+            for s, src in sels:
+                co = m.convs[s].cout
+                self._conv_backward(s, self._src(b, src), dcat[..., off:off + co], c[..., off:off + co], tb)
+                off += co
+            du = ops.relu_backward(dcat[..., off:width], c[..., off:width], tb["du_" + up])
+            ops.conv_wgrad(b[RBUF[up]], du, self.G[up, "w"])
+            if up in DGRAD:
+                ops.conv3x3(du, self.dconv[up], "none", out=tb["dr_" + up], affine=False)
+                dout = ops.resize_backward(tb["dr_" + up], tb["dprev_" + up])
+
+    # ------------------------------------------------------------------------------------------- update
+    def apply_gradients(self):
+        """DDP gradient all-reduce + tf.train.AdamOptimizer step over the flat buffer, then re-pack the filters."""
+        scale = parallel.allreduce_grads(self.grad)
+        self.t += 1
+        # TF keeps beta1_power / beta2_power as f32 variables multiplied once per step (adam.py _finish)
+        self._b1p = np.float32(self._b1p * np.float32(self.beta1))
+        self._b2p = np.float32(self._b2p * np.float32(self.beta2))
+        one = np.float32(1.0)
+        lr_t = np.float32(np.float32(self.lr) * np.sqrt(one - self._b2p) / (one - self._b1p))
+        ops.adam_tf(self.flat, self.m, self.v, self.grad, lr_t, self.beta1, self.beta2, self.epsilon, scale)
+        for scope, pc in self.model.convs.items():
+            pc.repack()
+        for scope in DGRAD:
+            ops.flip_weights(self.model.convs[scope].w_hwio, self._wflip[scope])
+            self.dconv[scope].repack()
+
+    def step(self, cmp, bg, warped, gt, raw_fg):
+        """One training iteration; returns the device tensor [loss, alpha_loss, compositional_loss] (pre-update)."""
+        self.forward(cmp, bg, warped)
+        dev = lambda t: (t if isinstance(t, torch.Tensor) else torch.from_numpy(  # noqa: E731
+            np.ascontiguousarray(t, np.float32))).to(self.device, torch.float32).contiguous()
+        gt, raw_fg, bg_d, cmp_d = dev(gt), dev(raw_fg), dev(bg), dev(cmp)
+        tb = self._tb
+        loss = ops.matting_loss(tb["alpha"], gt, raw_fg, bg_d, cmp_d)
+        tb["loss"].copy_(loss)
+        self.grad.zero_()
+        self.backward(gt, raw_fg, bg_d, cmp_d)
+        self.apply_gradients()
+        return tb["loss"]
+
+    def params_numpy(self):
+        """{scope: (w, b|None)} and {scope: (gamma, beta)} on the host (checkpointing / inference hand-off)."""
+        conv = {s: (self.P[s, "w"].cpu().numpy(), self.P[s, "b"].cpu().numpy() if (s, "b") in self.P else None)
+                for s, _, _ in NEW_CONVS}
+        bn = {s: (self.P[s, "gamma"].cpu().numpy(), self.P[s, "beta"].cpu().numpy()) for s in self.model.bn}
+        return conv, bn
