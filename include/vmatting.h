@@ -301,9 +301,13 @@ int vm_relu_backward_nhwc(const vm_tensor* dy, const vm_tensor* y, vm_tensor* dx
  * dx contiguous f32 [n,ih,iw,c] (overwritten). */
 int vm_resize_bilinear_tf1_backward(const vm_tensor* dy, float* dx, int ih, int iw, void* stream);
 
+/* Workspace of vm_conv3x3_wgrad_nhwc (per-block partial filter gradients, <= 64 MiB). */
+size_t vm_conv3x3_wgrad_workspace_bytes(int n, int h, int w, int cin, int cout);
+
 /* Weight gradient of the 3x3 SAME conv (tf.nn.conv2d, unet_simple.py:23,35): dw[3][3][cin][cout] (HWIO, f32) +=
- * sum over pixels of x (view, cin = x->c) patch x dy (f32 view [n,h,w,cout]); cout <= 48.  Accumulates. */
-int vm_conv3x3_wgrad_nhwc(const vm_tensor* x, const vm_tensor* dy, float* dw, void* stream);
+ * sum over pixels of x (view, cin = x->c) patch x dy (f32 view [n,h,w,cout]); cout <= 48.  Accumulates;
+ * deterministic (fixed-order two-pass sum through ``work``). */
+int vm_conv3x3_wgrad_nhwc(const vm_tensor* x, const vm_tensor* dy, float* dw, void* work, void* stream);
 
 /* The data-gradient filter of a 3x3 SAME conv: w_flipped[kh][kw][co][ci] = w[2-kh][2-kw][ci][co]; dx is then
  * vm_conv3x3_nhwc(dy, pack(w_flipped)). */

@@ -17,12 +17,12 @@ run() {  # run <limit> <log> cmd...
   [ $rc -eq 0 ] || exit $rc
 }
 run 400 stats.log rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/stats" -o run \
-    -- python3 "$REPO/bench.py" --steps 10 --warmup 3 --no-cpu-baseline "$@"
+    -- python3 "$REPO/bench.py" --steps 10 --warmup 3 --no-cpu-baseline --no-train "$@"
 cp "$(find "$OUT/stats" -name '*kernel_stats.csv' | head -n 1)" "$REPO/profiles/${TAG}_kernel_stats.csv"
 run 400 fetch.log rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$OUT/fetch" -o run \
-    -- python3 "$REPO/bench.py" --steps 2 --warmup 1 --no-cpu-baseline --no-profile --no-loader --no-augment --video-frames 0 "$@"
+    -- python3 "$REPO/bench.py" --steps 2 --warmup 1 --no-cpu-baseline --no-profile --no-loader --no-augment --no-train --video-frames 0 "$@"
 run 400 write.log rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/write" -o run \
-    -- python3 "$REPO/bench.py" --steps 2 --warmup 1 --no-cpu-baseline --no-profile --no-loader --no-augment --video-frames 0 "$@"
+    -- python3 "$REPO/bench.py" --steps 2 --warmup 1 --no-cpu-baseline --no-profile --no-loader --no-augment --no-train --video-frames 0 "$@"
 python3 "$REPO/tools/traffic.py" --fetch "$OUT/fetch" --write "$OUT/write" --out "$REPO/profiles/${TAG}_traffic.json" --forwards 4  # capture warm-up + 1 warmup + 2 steps
 cp "$REPO/profiles/${TAG}_traffic.json" "$REPO/profiles/${TAG}_kernel_stats.csv" "$REPO/gpurun_out/"
 run 600 bench.log python3 "$REPO/bench.py" --layers "$@"

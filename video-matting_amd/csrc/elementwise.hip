@@ -278,17 +278,20 @@ __global__ void convert_kernel(View x, View y, const float* scale, const float* 
 // variance over N*H*W.  Pass 1: grid (ceil(C/64), nblk); lane = channel (64 consecutive channels of a
 // pixel per wave -> coalesced), the 4 waves of a block stride over pixels, f64 partial sums,
 // combined across waves in LDS.  Pass 2: one thread per channel folds the nblk partials.
-constexpr int BN_NBLK = 240;
+constexpr int BN_NBLK = 1024;  // pixel blocks (max); launches use min(BN_NBLK, M / 256)
 
-template <typename T>
+// CP = lanes per pixel: 64 for c > 32 (a block covers 64 channels of each pixel, blockIdx.x picks the group);
+// for narrow tensors CP = next power of two >= c, so one wave reads 64 / CP pixels per step instead of idling lanes.
+template <typename T, int CP>
 __global__ __launch_bounds__(256) void bn_partial_kernel(View x, double* part, int nblk) {
+  constexpr int PPW = 64 / CP;
   __shared__ double sh[2][4][64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + lane;
+  const int c = blockIdx.x * CP + (lane % CP);
   const long M = (long)x.n * x.h * x.w;
   double s = 0.0, ss = 0.0;
   if (c < x.c) {
-    for (long p = (long)blockIdx.y * 4 + wave; p < M; p += (long)nblk * 4) {
+    for (long p = ((long)blockIdx.y * 4 + wave) * PPW + lane / CP; p < M; p += (long)nblk * 4 * PPW) {
       const double v = ldv(x, p, c);
       s += v;
       ss += v * v;
@@ -297,27 +300,58 @@ __global__ __launch_bounds__(256) void bn_partial_kernel(View x, double* part, i
   sh[0][wave][lane] = s;
   sh[1][wave][lane] = ss;
   __syncthreads();
-  if (wave == 0 && c < x.c) {
-    s = sh[0][0][lane] + sh[0][1][lane] + sh[0][2][lane] + sh[0][3][lane];
-    ss = sh[1][0][lane] + sh[1][1][lane] + sh[1][2][lane] + sh[1][3][lane];
+  if ((int)threadIdx.x < CP && c < x.c) {
+    s = ss = 0.0;
+    for (int w = 0; w < 4; ++w)
+      for (int k = 0; k < PPW; ++k) {
+        s += sh[0][w][k * CP + threadIdx.x];
+        ss += sh[1][w][k * CP + threadIdx.x];
+      }
     part[(long)blockIdx.y * x.c + c] = s;
     part[(long)nblk * x.c + (long)blockIdx.y * x.c + c] = ss;
   }
 }
 
-__global__ void bn_final_kernel(const double* part, int nblk, int C, long M, float* mean, float* var) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+// one wave per channel folds the nblk partials (lane-strided, then a shuffle tree)
+__global__ __launch_bounds__(64) void bn_final_kernel(const double* part, int nblk, int C, long M, float* mean,
+                                                      float* var) {
+  const int c = blockIdx.x, lane = threadIdx.x;
   double s = 0.0, ss = 0.0;
-  for (int b = 0; b < nblk; ++b) {
+  for (int b = lane; b < nblk; b += 64) {
     s += part[(long)b * C + c];
     ss += part[(long)nblk * C + (long)b * C + c];
   }
-  const double m = s / (double)M;
-  double v = ss / (double)M - m * m;
-  if (v < 0.0) v = 0.0;
-  mean[c] = (float)m;
-  var[c] = (float)v;
+  for (int o = 32; o > 0; o >>= 1) {
+    s += __shfl_down(s, o);
+    ss += __shfl_down(ss, o);
+  }
+  if (lane == 0) {
+    const double m = s / (double)M;
+    double v = ss / (double)M - m * m;
+    if (v < 0.0) v = 0.0;
+    mean[c] = (float)m;
+    var[c] = (float)v;
+  }
+}
+
+static int bn_blocks(long M) { return (int)(M / 256 < 1 ? 1 : M / 256 > BN_NBLK ? BN_NBLK : M / 256); }
+
+template <typename T>
+static int launch_bn_partial(const View& xv, double* part, hipStream_t st) {
+  const int C = xv.c;
+  const int nb = bn_blocks((long)xv.n * xv.h * xv.w);
+  const int cp = C > 32 ? 64 : C > 16 ? 32 : C > 8 ? 16 : C > 4 ? 8 : C > 2 ? 4 : C > 1 ? 2 : 1;
+  dim3 grid(cp == 64 ? (C + 63) / 64 : 1, nb);
+  switch (cp) {
+    case 1: hipLaunchKernelGGL((bn_partial_kernel<T, 1>), grid, dim3(256), 0, st, xv, part, nb); break;
+    case 2: hipLaunchKernelGGL((bn_partial_kernel<T, 2>), grid, dim3(256), 0, st, xv, part, nb); break;
+    case 4: hipLaunchKernelGGL((bn_partial_kernel<T, 4>), grid, dim3(256), 0, st, xv, part, nb); break;
+    case 8: hipLaunchKernelGGL((bn_partial_kernel<T, 8>), grid, dim3(256), 0, st, xv, part, nb); break;
+    case 16: hipLaunchKernelGGL((bn_partial_kernel<T, 16>), grid, dim3(256), 0, st, xv, part, nb); break;
+    case 32: hipLaunchKernelGGL((bn_partial_kernel<T, 32>), grid, dim3(256), 0, st, xv, part, nb); break;
+    default: hipLaunchKernelGGL((bn_partial_kernel<T, 64>), grid, dim3(256), 0, st, xv, part, nb); break;
+  }
+  return nb;
 }
 
 __global__ void bn_apply_kernel(View x, View y, const float* mean, const float* var, const float* gamma,
@@ -429,13 +463,12 @@ extern "C" int vm_bn_stats_nhwc(const vm_tensor* x, float* mean, float* var, voi
   if (!valid_tensor(x) || !mean || !var || !work) return fail(VM_EINVAL, "bn_stats: bad argument");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const long M = (long)x->n * x->h * x->w;
-  dim3 grid((x->c + 63) / 64, BN_NBLK);
   double* part = reinterpret_cast<double*>(work);
-  if (x->dtype == VM_BF16) hipLaunchKernelGGL(bn_partial_kernel<uint16_t>, grid, dim3(256), 0, st, view(x), part, BN_NBLK);
-  else hipLaunchKernelGGL(bn_partial_kernel<float>, grid, dim3(256), 0, st, view(x), part, BN_NBLK);
+  const int nb = x->dtype == VM_BF16 ? launch_bn_partial<uint16_t>(view(x), part, st)
+                                     : launch_bn_partial<float>(view(x), part, st);
   int rc = check_launch("bn_partial");
   if (rc) return rc;
-  hipLaunchKernelGGL(bn_final_kernel, dim3((x->c + 63) / 64), dim3(64), 0, st, part, BN_NBLK, x->c, M, mean, var);
+  hipLaunchKernelGGL(bn_final_kernel, dim3(x->c), dim3(64), 0, st, part, nb, x->c, M, mean, var);
   return check_launch("bn_final");
 }
 

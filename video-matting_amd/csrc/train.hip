@@ -11,9 +11,10 @@
 //   conv_wgrad      dW[kh,kw,ci,co] = sum_p x[p + (kh-1, kw-1), ci] * dy[p, co]: per block an LDS patch of
 //                   (4+2) x (32+2) pixels x CC channels and the 4 x 32 dy tile; each thread owns one (kh, ci,
 //                   4-channel co group) and slides the three kw taps along a pixel row (1 new LDS x read and one
-//                   float4 dy read per 12 FMAs); blocks walk tiles persistently, one atomic flush per block
+//                   float4 dy read per 12 FMAs); blocks walk tiles persistently and store one partial filter
+//                   gradient each, summed in fixed order by a second pass (deterministic, no atomics)
 //   conv dgrad      the forward conv kernels on flipped, transposed weights (flip_weights here)
-//   resize_backward adjoint of the TF-1 legacy bilinear resize (4 atomic taps per output element)
+//   resize_backward adjoint of the TF-1 legacy bilinear resize, gathered per input element (no atomics)
 //   relu_backward   dy * (y > 0)
 //   adam            TF ApplyAdam: m += (g-m)(1-b1); v += (g^2-v)(1-b2); var -= m*lr_t/(sqrt(v)+eps)
 
@@ -69,7 +70,7 @@ __global__ __launch_bounds__(256) void loss_backward_kernel(const float* __restr
 }
 
 // ---------------------------------------------------------------- batch-norm backward (training statistics)
-constexpr int BN_NBLK = 240;
+constexpr int BN_NBLK = 1024;  // pixel blocks (max); launches use min(BN_NBLK, M / 256)
 
 template <bool MASK>
 __device__ __forceinline__ float grad_in(const V& dy, const V& y, long p, int c) {
@@ -78,19 +79,21 @@ __device__ __forceinline__ float grad_in(const V& dy, const V& y, long p, int c)
   return g;
 }
 
-// per (64-channel group, pixel block): double partial sums of g and g*xhat (x == NULL: g only)
-template <bool MASK>
+// per (channel group, pixel block): double partial sums of g and g*xhat (x == NULL: g only).  CP lanes per pixel as
+// in elementwise.hip's bn_partial_kernel: narrow tensors put 64 / CP pixels in flight per wave.
+template <bool MASK, int CP>
 __global__ __launch_bounds__(256) void bn_bwd_partial(V x, V dy, V y, const float* mean, const float* var, float eps,
                                                       double* part, int nblk) {
+  constexpr int PPW = 64 / CP;
   __shared__ double sh[2][4][64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + lane;
+  const int c = blockIdx.x * CP + (lane % CP);
   const long M = (long)dy.n * dy.h * dy.w;
   double s1 = 0.0, s2 = 0.0;
   if (c < dy.c) {
     const float m = x.p ? mean[c] : 0.f;
     const float r = x.p ? 1.0f / sqrtf(var[c] + eps) : 0.f;
-    for (long p = (long)blockIdx.y * 4 + wave; p < M; p += (long)nblk * 4) {
+    for (long p = ((long)blockIdx.y * 4 + wave) * PPW + lane / CP; p < M; p += (long)nblk * 4 * PPW) {
       const float g = grad_in<MASK>(dy, y, p, c);
       s1 += g;
       if (x.p) s2 += (double)g * (double)((ld(x, p, c) - m) * r);
@@ -99,24 +102,50 @@ __global__ __launch_bounds__(256) void bn_bwd_partial(V x, V dy, V y, const floa
   sh[0][wave][lane] = s1;
   sh[1][wave][lane] = s2;
   __syncthreads();
-  if (wave == 0 && c < dy.c) {
-    s1 = sh[0][0][lane] + sh[0][1][lane] + sh[0][2][lane] + sh[0][3][lane];
-    s2 = sh[1][0][lane] + sh[1][1][lane] + sh[1][2][lane] + sh[1][3][lane];
+  if ((int)threadIdx.x < CP && c < dy.c) {
+    s1 = s2 = 0.0;
+    for (int w = 0; w < 4; ++w)
+      for (int k = 0; k < PPW; ++k) {
+        s1 += sh[0][w][k * CP + threadIdx.x];
+        s2 += sh[1][w][k * CP + threadIdx.x];
+      }
     part[(long)blockIdx.y * dy.c + c] = s1;
     part[(long)nblk * dy.c + (long)blockIdx.y * dy.c + c] = s2;
   }
 }
 
-__global__ void bn_bwd_final(const double* part, int nblk, int C, float* sum_g, float* sum_gx) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+__global__ __launch_bounds__(64) void bn_bwd_final(const double* part, int nblk, int C, float* sum_g, float* sum_gx) {
+  const int c = blockIdx.x, lane = threadIdx.x;
   double s1 = 0.0, s2 = 0.0;
-  for (int b = 0; b < nblk; ++b) {
+  for (int b = lane; b < nblk; b += 64) {
     s1 += part[(long)b * C + c];
     s2 += part[(long)nblk * C + (long)b * C + c];
   }
-  if (sum_g) sum_g[c] = (float)s1;
-  if (sum_gx) sum_gx[c] = (float)s2;
+  for (int o = 32; o > 0; o >>= 1) {
+    s1 += __shfl_down(s1, o);
+    s2 += __shfl_down(s2, o);
+  }
+  if (lane == 0) {
+    if (sum_g) sum_g[c] = (float)s1;
+    if (sum_gx) sum_gx[c] = (float)s2;
+  }
+}
+
+template <bool MASK>
+static void launch_bn_bwd_partial(const V& x, const V& dy, const V& y, const float* mean, const float* var, float eps,
+                                  double* part, int nb, hipStream_t st) {
+  const int C = dy.c;
+  const int cp = C > 32 ? 64 : C > 16 ? 32 : C > 8 ? 16 : C > 4 ? 8 : C > 2 ? 4 : C > 1 ? 2 : 1;
+  dim3 g(cp == 64 ? (C + 63) / 64 : 1, nb), b(256);
+  switch (cp) {
+    case 1: hipLaunchKernelGGL((bn_bwd_partial<MASK, 1>), g, b, 0, st, x, dy, y, mean, var, eps, part, nb); break;
+    case 2: hipLaunchKernelGGL((bn_bwd_partial<MASK, 2>), g, b, 0, st, x, dy, y, mean, var, eps, part, nb); break;
+    case 4: hipLaunchKernelGGL((bn_bwd_partial<MASK, 4>), g, b, 0, st, x, dy, y, mean, var, eps, part, nb); break;
+    case 8: hipLaunchKernelGGL((bn_bwd_partial<MASK, 8>), g, b, 0, st, x, dy, y, mean, var, eps, part, nb); break;
+    case 16: hipLaunchKernelGGL((bn_bwd_partial<MASK, 16>), g, b, 0, st, x, dy, y, mean, var, eps, part, nb); break;
+    case 32: hipLaunchKernelGGL((bn_bwd_partial<MASK, 32>), g, b, 0, st, x, dy, y, mean, var, eps, part, nb); break;
+    default: hipLaunchKernelGGL((bn_bwd_partial<MASK, 64>), g, b, 0, st, x, dy, y, mean, var, eps, part, nb); break;
+  }
 }
 
 template <bool MASK>
@@ -155,35 +184,51 @@ __device__ __forceinline__ void tf1c(int i, float scale, int in, int& lo, int& h
   lerp = src - fl;
 }
 
+// Gather form (deterministic, no atomics): input pixel (iy, ix) collects the output pixels whose taps hit it.  With
+// scale = in/out <= ~1 those lie in rows [floor((iy-1)/sy)-1, ceil((iy+1)/sy)+1] (likewise columns); each candidate's
+// taps are recomputed with the forward's exact f32 coordinate arithmetic, so the weights match it bit for bit.
+__device__ __forceinline__ float tap_w(int o, float scale, int in, int i) {
+  int lo, hi;
+  float l;
+  tf1c(o, scale, in, lo, hi, l);
+  return (lo == i ? 1.f - l : 0.f) + (hi == i ? l : 0.f);
+}
+
 __global__ void resize_bwd_kernel(V dy, float* dx, int ih, int iw, float sy, float sx) {
-  const long total = (long)dy.n * dy.h * dy.w * dy.c;
+  const long total = (long)dy.n * ih * iw * dy.c;
   const int C = dy.c;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
     const int c = (int)(i % C);
-    const long op = i / C;
-    const int ow = (int)(op % dy.w);
-    const long t = op / dy.w;
-    const int oh = (int)(t % dy.h);
-    const int n = (int)(t / dy.h);
-    int y0, y1, x0, x1;
-    float yl, xl;
-    tf1c(oh, sy, ih, y0, y1, yl);
-    tf1c(ow, sx, iw, x0, x1, xl);
-    const float g = ld(dy, op, c);
-    const float gt = g * (1.f - yl), gb = g * yl;
-    const long rb = (long)n * ih;
-    atomicAdd(dx + ((rb + y0) * iw + x0) * C + c, gt * (1.f - xl));
-    atomicAdd(dx + ((rb + y0) * iw + x1) * C + c, gt * xl);
-    atomicAdd(dx + ((rb + y1) * iw + x0) * C + c, gb * (1.f - xl));
-    atomicAdd(dx + ((rb + y1) * iw + x1) * C + c, gb * xl);
+    const long ip = i / C;
+    const int ix = (int)(ip % iw);
+    const long t = ip / iw;
+    const int iy = (int)(t % ih);
+    const int n = (int)(t / ih);
+    const int r0 = max(0, (int)floorf((iy - 1) / sy) - 1), r1 = min(dy.h - 1, (int)ceilf((iy + 1) / sy) + 1);
+    const int q0 = max(0, (int)floorf((ix - 1) / sx) - 1), q1 = min(dy.w - 1, (int)ceilf((ix + 1) / sx) + 1);
+    float acc = 0.f;
+    for (int oh = r0; oh <= r1; ++oh) {
+      const float wy = tap_w(oh, sy, ih, iy);
+      if (wy == 0.f) continue;
+      float row = 0.f;
+      for (int ow = q0; ow <= q1; ++ow) {
+        const float wx = tap_w(ow, sx, iw, ix);
+        if (wx != 0.f) row += wx * ld(dy, ((long)n * dy.h + oh) * dy.w + ow, c);
+      }
+      acc += wy * row;
+    }
+    dx[i] = acc;
   }
 }
 
 // ---------------------------------------------------------------- conv weight gradient
 constexpr int WG_TH = 4, WG_TW = 32, WG_PH = WG_TH + 2, WG_PW = WG_TW + 2, WG_NT = 256;
 
-template <int CC, int CO4>
-__global__ __launch_bounds__(WG_NT) void wgrad_kernel(V x, V dy, float* dw,
+// XV: x is T-typed with 16-byte aligned channel vectors (cin, coff, cstride multiples of the vector width), so a
+// pixel's CC channels arrive as CC/VE 16-byte loads, all of a thread's loads issued before any LDS store.
+// DV: likewise dy as float4 (cout % 4 == 0).  Otherwise element loads.
+template <int CC, int CO4, typename T, bool XV, bool DV>
+__global__ __launch_bounds__(WG_NT) void wgrad_kernel(V x, V dy, float* partials,
                                                       int tiles_h, int tiles_w, long ntiles) {
   constexpr int TASKS = 3 * CC * CO4;
   constexpr int TPT = (TASKS + WG_NT - 1) / WG_NT;
@@ -192,6 +237,8 @@ __global__ __launch_bounds__(WG_NT) void wgrad_kernel(V x, V dy, float* dw,
   const int tid = threadIdx.x;
   const int c0 = blockIdx.y * CC;
   const int cin = x.c, cout = dy.c;
+  // this block's partial filter gradient: row blockIdx.x of the [gridDim.x][3][3][cin][cout] workspace
+  float* part = partials + (long)blockIdx.x * 9 * cin * cout;
   float acc[TPT][3][4];
 #pragma unroll
   for (int k = 0; k < TPT; ++k)
@@ -204,23 +251,73 @@ __global__ __launch_bounds__(WG_NT) void wgrad_kernel(V x, V dy, float* dw,
     const int ty = (int)(t2 % tiles_h);
     const int n = (int)(t2 / tiles_h);
     const int y0 = ty * WG_TH, x0 = tx * WG_TW;
-    for (int e = tid; e < WG_PH * WG_PW * CC; e += WG_NT) {
-      const int ci = e % CC;
-      const int pc = e / CC;
-      const int col = pc % WG_PW, r = pc / WG_PW;
-      const int gy = y0 + r - 1, gx = x0 + col - 1, c = c0 + ci;
-      float v = 0.f;
-      if (gy >= 0 && gy < x.h && gx >= 0 && gx < x.w && c < cin) v = ld(x, ((long)n * x.h + gy) * x.w + gx, c);
-      xs[e] = v;
+    if constexpr (XV) {
+      constexpr int VE = 16 / sizeof(T), NVP = CC / VE, NV = WG_PH * WG_PW * NVP, VPT = (NV + WG_NT - 1) / WG_NT;
+      uint4 buf[VPT];
+#pragma unroll
+      for (int k = 0; k < VPT; ++k) {
+        const int e = tid + k * WG_NT;
+        buf[k] = make_uint4(0, 0, 0, 0);
+        if (NV % WG_NT == 0 || e < NV) {
+          const int j = e % NVP, pc = e / NVP;
+          const int gy = y0 + pc / WG_PW - 1, gx = x0 + pc % WG_PW - 1, c = c0 + j * VE;
+          if (gy >= 0 && gy < x.h && gx >= 0 && gx < x.w && c < cin)
+            buf[k] = *reinterpret_cast<const uint4*>(reinterpret_cast<const T*>(x.p) +
+                                                     (((long)n * x.h + gy) * x.w + gx) * x.cs + x.coff + c);
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < VPT; ++k) {
+        const int e = tid + k * WG_NT;
+        if (NV % WG_NT == 0 || e < NV) {
+          float f[VE];
+          Chunk<T>::unpack(buf[k], f);
+          float4* d = reinterpret_cast<float4*>(xs + (e / NVP) * CC + (e % NVP) * VE);
+#pragma unroll
+          for (int i = 0; i < VE / 4; ++i) d[i] = make_float4(f[4 * i], f[4 * i + 1], f[4 * i + 2], f[4 * i + 3]);
+        }
+      }
+    } else {
+      for (int e = tid; e < WG_PH * WG_PW * CC; e += WG_NT) {
+        const int ci = e % CC;
+        const int pc = e / CC;
+        const int col = pc % WG_PW, r = pc / WG_PW;
+        const int gy = y0 + r - 1, gx = x0 + col - 1, c = c0 + ci;
+        float v = 0.f;
+        if (gy >= 0 && gy < x.h && gx >= 0 && gx < x.w && c < cin) v = ld(x, ((long)n * x.h + gy) * x.w + gx, c);
+        xs[e] = v;
+      }
     }
-    float* dsf = reinterpret_cast<float*>(ds);
-    for (int e = tid; e < WG_TH * WG_TW * CO4 * 4; e += WG_NT) {
-      const int co = e % (CO4 * 4);
-      const int pp = e / (CO4 * 4);
-      const int gy = y0 + pp / WG_TW, gx = x0 + pp % WG_TW;
-      float v = 0.f;
-      if (gy < x.h && gx < x.w && co < cout) v = ld(dy, ((long)n * x.h + gy) * x.w + gx, co);
-      dsf[e] = v;
+    if constexpr (DV) {
+      constexpr int ND = WG_TH * WG_TW * CO4, DPT = (ND + WG_NT - 1) / WG_NT;
+      float4 buf[DPT];
+#pragma unroll
+      for (int k = 0; k < DPT; ++k) {
+        const int e = tid + k * WG_NT;
+        buf[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (ND % WG_NT == 0 || e < ND) {
+          const int cg = e % CO4, pp = e / CO4;
+          const int gy = y0 + pp / WG_TW, gx = x0 + pp % WG_TW;
+          if (gy < x.h && gx < x.w && cg * 4 < cout)
+            buf[k] = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(dy.p) +
+                                                      (((long)n * x.h + gy) * x.w + gx) * dy.cs + dy.coff + cg * 4);
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < DPT; ++k) {
+        const int e = tid + k * WG_NT;
+        if (ND % WG_NT == 0 || e < ND) ds[e] = buf[k];
+      }
+    } else {
+      float* dsf = reinterpret_cast<float*>(ds);
+      for (int e = tid; e < WG_TH * WG_TW * CO4 * 4; e += WG_NT) {
+        const int co = e % (CO4 * 4);
+        const int pp = e / (CO4 * 4);
+        const int gy = y0 + pp / WG_TW, gx = x0 + pp % WG_TW;
+        float v = 0.f;
+        if (gy < x.h && gx < x.w && co < cout) v = ld(dy, ((long)n * x.h + gy) * x.w + gx, co);
+        dsf[e] = v;
+      }
     }
     __syncthreads();
 #pragma unroll
@@ -263,7 +360,7 @@ __global__ __launch_bounds__(WG_NT) void wgrad_kernel(V x, V dy, float* dw,
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             const int co = cg * 4 + j;
-            if (co < cout) atomicAdd(dw + (((long)(kh * 3 + kw) * cin + c) * cout + co), acc[k][kw][j]);
+            if (co < cout) part[(((long)(kh * 3 + kw) * cin + c) * cout + co)] = acc[k][kw][j];
           }
       }
     }
@@ -296,16 +393,71 @@ __global__ void adam_kernel(float* var, float* m, float* v, const float* grad, l
   }
 }
 
-template <int CC, int CO4>
-static void launch_wgrad(const V& xv, const V& dy, float* dw, hipStream_t st) {
+// dw[i] += sum over the gx block rows of the partials (fixed order: deterministic).  A block owns 64 columns; its
+// 16 waves stride the rows (independent loads in flight), then fold through LDS.
+__global__ __launch_bounds__(1024) void wgrad_reduce_kernel(const float* part, int rows, long S, float* dw) {
+  __shared__ float sh[16][64];
+  const int col = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  const long i = (long)blockIdx.x * 64 + col;
+  float s = 0.f;
+  if (i < S) {
+#pragma unroll 8
+    for (int b = rg; b < rows; b += 16) s += part[(long)b * S + i];
+  }
+  sh[rg][col] = s;
+  __syncthreads();
+  if (rg == 0 && i < S) {
+    float t = 0.f;
+    for (int g = 0; g < 16; ++g) t += sh[g][col];
+    dw[i] += t;
+  }
+}
+
+constexpr size_t WG_WS_CAP = 64ull << 20;  // workspace bytes
+
+// pixel-tile blocks per channel chunk: ~1024 blocks in all (4 per CU), fewer when the partial rows would pass
+// WG_WS_CAP
+static long wgrad_rows(int n, int h, int w, int cin, int cout, int cc) {
+  const long ntiles = (long)n * ((h + WG_TH - 1) / WG_TH) * ((w + WG_TW - 1) / WG_TW);
+  const int ncc = (cin + cc - 1) / cc;
+  long gx = (1024 + ncc - 1) / ncc;
+  const long cap = (long)(WG_WS_CAP / (9ull * cin * cout * sizeof(float)));
+  if (gx > cap) gx = cap;
+  if (gx > ntiles) gx = ntiles;
+  return gx < 1 ? 1 : gx;
+}
+
+static int wgrad_cc(int cout) { return (cout + 3) / 4 <= 2 ? 64 : 32; }
+
+template <int CC, int CO4, typename T, bool XV, bool DV>
+static void launch_wgrad_t(const V& xv, const V& dy, float* dw, float* ws, hipStream_t st) {
   const int tiles_h = (xv.h + WG_TH - 1) / WG_TH, tiles_w = (xv.w + WG_TW - 1) / WG_TW;
   const long ntiles = (long)xv.n * tiles_h * tiles_w;
   const int ncc = (xv.c + CC - 1) / CC;
-  long gx = (2048 + ncc - 1) / ncc;
-  if (gx > ntiles) gx = ntiles;
-  if (gx < 1) gx = 1;
-  hipLaunchKernelGGL((wgrad_kernel<CC, CO4>), dim3((unsigned)gx, ncc), dim3(WG_NT), 0, st, xv, dy, dw, tiles_h,
-                     tiles_w, ntiles);
+  const long gx = wgrad_rows(xv.n, xv.h, xv.w, xv.c, dy.c, CC);
+  hipLaunchKernelGGL((wgrad_kernel<CC, CO4, T, XV, DV>), dim3((unsigned)gx, ncc), dim3(WG_NT), 0, st, xv, dy, ws,
+                     tiles_h, tiles_w, ntiles);
+  const long S = 9L * xv.c * dy.c;
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((S + 63) / 64)), dim3(1024), 0, st, ws, (int)gx, S, dw);
+}
+
+static bool vec_ok(const V& v, int ve) {
+  return reinterpret_cast<uintptr_t>(v.p) % 16 == 0 && v.c % ve == 0 && v.coff % ve == 0 && v.cs % ve == 0;
+}
+
+template <int CC, int CO4>
+static void launch_wgrad(const V& xv, const V& dy, float* dw, float* ws, hipStream_t st) {
+  const bool dv = vec_ok(dy, 4);
+  if (xv.dt == VM_BF16 && vec_ok(xv, 8)) {
+    if (dv) launch_wgrad_t<CC, CO4, uint16_t, true, true>(xv, dy, dw, ws, st);
+    else launch_wgrad_t<CC, CO4, uint16_t, true, false>(xv, dy, dw, ws, st);
+  } else if (xv.dt == VM_F32 && vec_ok(xv, 4)) {
+    if (dv) launch_wgrad_t<CC, CO4, float, true, true>(xv, dy, dw, ws, st);
+    else launch_wgrad_t<CC, CO4, float, true, false>(xv, dy, dw, ws, st);
+  } else {
+    if (dv) launch_wgrad_t<CC, CO4, float, false, true>(xv, dy, dw, ws, st);
+    else launch_wgrad_t<CC, CO4, float, false, false>(xv, dy, dw, ws, st);
+  }
 }
 
 static bool ok_view(const vm_tensor* t) { return valid_tensor(t); }
@@ -352,12 +504,13 @@ extern "C" int vm_bn_backward_nhwc(const vm_tensor* x, const vm_tensor* dy, cons
   float* tail = reinterpret_cast<float*>(part + 2L * BN_NBLK * C);
   float* sg = dbeta ? dbeta : tail;
   float* sgx = dgamma ? dgamma : tail + C;
-  dim3 grid((C + 63) / 64, BN_NBLK);
-  if (y) hipLaunchKernelGGL(bn_bwd_partial<true>, grid, dim3(256), 0, st, xv, dyv, yv, mean, var, eps, part, BN_NBLK);
-  else hipLaunchKernelGGL(bn_bwd_partial<false>, grid, dim3(256), 0, st, xv, dyv, yv, mean, var, eps, part, BN_NBLK);
+  const long M = (long)dy->n * dy->h * dy->w;
+  const int nb = (int)(M / 256 < 1 ? 1 : M / 256 > BN_NBLK ? BN_NBLK : M / 256);
+  if (y) launch_bn_bwd_partial<true>(xv, dyv, yv, mean, var, eps, part, nb, st);
+  else launch_bn_bwd_partial<false>(xv, dyv, yv, mean, var, eps, part, nb, st);
   int rc = check_launch("bn_backward_partial");
   if (rc) return rc;
-  hipLaunchKernelGGL(bn_bwd_final, dim3((C + 63) / 64), dim3(64), 0, st, part, BN_NBLK, C, sg, x ? sgx : nullptr);
+  hipLaunchKernelGGL(bn_bwd_final, dim3(C), dim3(64), 0, st, part, nb, C, sg, x ? sgx : nullptr);
   rc = check_launch("bn_backward_final");
   if (rc || !dx) return rc;
   const long work_n = (long)dy->n * dy->h * dy->w * C;
@@ -382,32 +535,40 @@ extern "C" int vm_relu_backward_nhwc(const vm_tensor* dy, const vm_tensor* y, vm
 extern "C" int vm_resize_bilinear_tf1_backward(const vm_tensor* dy, float* dx, int ih, int iw, void* stream) {
   if (!ok_view(dy) || !dx || ih <= 0 || iw <= 0) return fail(VM_EINVAL, "resize_backward: bad argument");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  hipError_t e = hipMemsetAsync(dx, 0, (size_t)dy->n * ih * iw * dy->c * sizeof(float), st);
-  if (e != hipSuccess) return fail(VM_EHIP, "resize_backward: %s", hipGetErrorString(e));
+  if (dy->h > 4 * ih || dy->w > 4 * iw || ih > 2 * dy->h || iw > 2 * dy->w)
+    return fail(VM_EUNSUPPORTED, "resize_backward: scale %dx%d -> %dx%d outside the upsampling range", ih, iw, dy->h,
+                dy->w);
   const float sy = (float)ih / (float)dy->h, sx = (float)iw / (float)dy->w;
-  const long n = (long)dy->n * dy->h * dy->w * dy->c;
+  const long n = (long)dy->n * ih * iw * dy->c;
   hipLaunchKernelGGL(resize_bwd_kernel, dim3(grid_for(n, 256)), dim3(256), 0, st, mk(dy), dx, ih, iw, sy, sx);
   return check_launch("resize_backward");
 }
 
-extern "C" int vm_conv3x3_wgrad_nhwc(const vm_tensor* x, const vm_tensor* dy, float* dw, void* stream) {
-  if (!ok_view(x) || !ok_view(dy) || !dw || dy->dtype != VM_F32 || dy->n != x->n || dy->h != x->h || dy->w != x->w)
+extern "C" size_t vm_conv3x3_wgrad_workspace_bytes(int n, int h, int w, int cin, int cout) {
+  if (n <= 0 || h <= 0 || w <= 0 || cin <= 0 || cout <= 0) return 0;
+  return (size_t)wgrad_rows(n, h, w, cin, cout, wgrad_cc(cout)) * 9 * cin * cout * sizeof(float);
+}
+
+extern "C" int vm_conv3x3_wgrad_nhwc(const vm_tensor* x, const vm_tensor* dy, float* dw, void* work, void* stream) {
+  if (!ok_view(x) || !ok_view(dy) || !dw || !work || dy->dtype != VM_F32 || dy->n != x->n || dy->h != x->h ||
+      dy->w != x->w)
     return fail(VM_EINVAL, "conv3x3_wgrad: bad argument");
   const int cout = dy->c;
   if (cout > 48) return fail(VM_EUNSUPPORTED, "conv3x3_wgrad: cout %d > 48", cout);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   V xv = mk(x), dv = mk(dy);
+  float* ws = reinterpret_cast<float*>(work);
   const int co4 = (cout + 3) / 4;
   switch (co4) {
-    case 1: launch_wgrad<64, 1>(xv, dv, dw, st); break;
-    case 2: launch_wgrad<64, 2>(xv, dv, dw, st); break;
+    case 1: launch_wgrad<64, 1>(xv, dv, dw, ws, st); break;
+    case 2: launch_wgrad<64, 2>(xv, dv, dw, ws, st); break;
     case 3:
-    case 4: launch_wgrad<32, 4>(xv, dv, dw, st); break;
+    case 4: launch_wgrad<32, 4>(xv, dv, dw, ws, st); break;
     case 5:
-    case 6: launch_wgrad<32, 6>(xv, dv, dw, st); break;
+    case 6: launch_wgrad<32, 6>(xv, dv, dw, ws, st); break;
     case 7:
-    case 8: launch_wgrad<32, 8>(xv, dv, dw, st); break;
-    default: launch_wgrad<32, 12>(xv, dv, dw, st); break;
+    case 8: launch_wgrad<32, 8>(xv, dv, dw, ws, st); break;
+    default: launch_wgrad<32, 12>(xv, dv, dw, ws, st); break;
   }
   return check_launch("conv3x3_wgrad");
 }

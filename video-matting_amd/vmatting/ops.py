@@ -562,7 +562,9 @@ def conv_wgrad(x, dy, dw):
     if tuple(dy.shape) != (n, h, w, cout) or dw.numel() != 9 * cin * cout:
         raise ValueError("conv_wgrad: x %s, dy %s, dw %s" % (tuple(x.shape), tuple(dy.shape), tuple(dw.shape)))
     xv, dv = nhwc(x), nhwc(dy)
-    check(lib().vm_conv3x3_wgrad_nhwc(ctypes.byref(xv), ctypes.byref(dv), _ptr(dw), stream_handle()), "conv_wgrad")
+    ws = _workspace(lib().vm_conv3x3_wgrad_workspace_bytes(n, h, w, cin, cout), x.device)
+    check(lib().vm_conv3x3_wgrad_nhwc(ctypes.byref(xv), ctypes.byref(dv), _ptr(dw), _ptr(ws), stream_handle()),
+          "conv_wgrad")
     return dw
 
 
