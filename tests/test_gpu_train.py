@@ -60,6 +60,24 @@ def test_conv_wgrad(cout, xdtype):
     assert scaled_err(H(dw), wr.grad.numpy()) <= 1e-4
 
 
+@pytest.mark.parametrize("cin,cs,cout,xdtype", [(30, 32, 32, "bf16"), (9, 16, 2, "bf16"), (30, 32, 24, "f32"),
+                                                (9, 16, 2, "f32"), (192, 192, 2, "bf16")])
+def test_conv_wgrad_padded_views(cin, cs, cout, xdtype):
+    """16-byte x loads straddling the view's last channel (up1n[..., :30], in9[..., :9]): the pad lanes hold
+    garbage that must not reach dw."""
+    from vmatting import ops
+    rs = np.random.RandomState(cin + cout)
+    n, h, w = 2, 21, 45
+    x = rs.normal(size=(n, h, w, cs)).astype(np.float32)
+    dy = rs.normal(size=(n, h, w, cout)).astype(np.float32)
+    xd = T(x, torch.float32 if xdtype == "f32" else torch.bfloat16)
+    dw = torch.zeros((3, 3, cin, cout), dtype=torch.float32, device=DEV)
+    ops.conv_wgrad(xd[..., :cin], T(dy), dw)
+    wr = torch.zeros((3, 3, cin, cout), dtype=torch.float64, requires_grad=True)
+    (tr._conv(torch.from_numpy(H(xd[..., :cin])), wr) * torch.from_numpy(dy.astype(np.float64))).sum().backward()
+    assert scaled_err(H(dw), wr.grad.numpy()) <= 1e-4
+
+
 def test_conv_wgrad_accumulates_and_large_cin():
     from vmatting import ops
     rs = np.random.RandomState(3)

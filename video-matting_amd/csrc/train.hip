@@ -232,6 +232,9 @@ __global__ __launch_bounds__(WG_NT) void wgrad_kernel(V x, V dy, float* partials
                                                       int tiles_h, int tiles_w, long ntiles) {
   constexpr int TASKS = 3 * CC * CO4;
   constexpr int TPT = (TASKS + WG_NT - 1) / WG_NT;
+  constexpr int VE = 16 / sizeof(T), NVP = CC / VE, NV = WG_PH * WG_PW * NVP;
+  constexpr int VPT = XV ? (NV + WG_NT - 1) / WG_NT : 1;
+  constexpr int ND = WG_TH * WG_TW * CO4, DPT = DV ? (ND + WG_NT - 1) / WG_NT : 1;
   __shared__ float xs[WG_PH * WG_PW * CC];
   __shared__ float4 ds[WG_TH * WG_TW * CO4];
   const int tid = threadIdx.x;
@@ -245,33 +248,63 @@ __global__ __launch_bounds__(WG_NT) void wgrad_kernel(V x, V dy, float* partials
 #pragma unroll
     for (int j = 0; j < 3; ++j) acc[k][j][0] = acc[k][j][1] = acc[k][j][2] = acc[k][j][3] = 0.f;
 
-  for (long tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+  // vector paths: the next tile's 16-byte loads are issued into registers before the current tile's FMAs,
+  // so their latency hides under the compute (register double buffer; LDS holds the current tile)
+  uint4 xb[VPT];
+  float4 db[DPT];
+  auto coords = [&](long tile, int& n, int& y0, int& x0) {
     const int tx = (int)(tile % tiles_w);
     const long t2 = tile / tiles_w;
-    const int ty = (int)(t2 % tiles_h);
-    const int n = (int)(t2 / tiles_h);
-    const int y0 = ty * WG_TH, x0 = tx * WG_TW;
+    y0 = (int)(t2 % tiles_h) * WG_TH;
+    n = (int)(t2 / tiles_h);
+    x0 = tx * WG_TW;
+  };
+  auto issue = [&](long tile) {
+    int n, y0, x0;
+    coords(tile, n, y0, x0);
     if constexpr (XV) {
-      constexpr int VE = 16 / sizeof(T), NVP = CC / VE, NV = WG_PH * WG_PW * NVP, VPT = (NV + WG_NT - 1) / WG_NT;
-      uint4 buf[VPT];
 #pragma unroll
       for (int k = 0; k < VPT; ++k) {
         const int e = tid + k * WG_NT;
-        buf[k] = make_uint4(0, 0, 0, 0);
+        xb[k] = make_uint4(0, 0, 0, 0);
         if (NV % WG_NT == 0 || e < NV) {
           const int j = e % NVP, pc = e / NVP;
           const int gy = y0 + pc / WG_PW - 1, gx = x0 + pc % WG_PW - 1, c = c0 + j * VE;
           if (gy >= 0 && gy < x.h && gx >= 0 && gx < x.w && c < cin)
-            buf[k] = *reinterpret_cast<const uint4*>(reinterpret_cast<const T*>(x.p) +
-                                                     (((long)n * x.h + gy) * x.w + gx) * x.cs + x.coff + c);
+            xb[k] = *reinterpret_cast<const uint4*>(reinterpret_cast<const T*>(x.p) +
+                                                    (((long)n * x.h + gy) * x.w + gx) * x.cs + x.coff + c);
         }
       }
+    }
+    if constexpr (DV) {
+#pragma unroll
+      for (int k = 0; k < DPT; ++k) {
+        const int e = tid + k * WG_NT;
+        db[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (ND % WG_NT == 0 || e < ND) {
+          const int cg = e % CO4, pp = e / CO4;
+          const int gy = y0 + pp / WG_TW, gx = x0 + pp % WG_TW;
+          if (gy < x.h && gx < x.w && cg * 4 < cout)
+            db[k] = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(dy.p) +
+                                                     (((long)n * x.h + gy) * x.w + gx) * dy.cs + dy.coff + cg * 4);
+        }
+      }
+    }
+  };
+  auto commit = [&](long tile) {
+    int n, y0, x0;
+    coords(tile, n, y0, x0);
+    if constexpr (XV) {
 #pragma unroll
       for (int k = 0; k < VPT; ++k) {
         const int e = tid + k * WG_NT;
         if (NV % WG_NT == 0 || e < NV) {
           float f[VE];
-          Chunk<T>::unpack(buf[k], f);
+          Chunk<T>::unpack(xb[k], f);
+          const int c = c0 + (e % NVP) * VE;  // a vector straddling cin (padded views): zero the lanes past it
+#pragma unroll
+          for (int i = 0; i < VE; ++i)
+            if (c + i >= cin) f[i] = 0.f;
           float4* d = reinterpret_cast<float4*>(xs + (e / NVP) * CC + (e % NVP) * VE);
 #pragma unroll
           for (int i = 0; i < VE / 4; ++i) d[i] = make_float4(f[4 * i], f[4 * i + 1], f[4 * i + 2], f[4 * i + 3]);
@@ -281,32 +314,17 @@ __global__ __launch_bounds__(WG_NT) void wgrad_kernel(V x, V dy, float* partials
       for (int e = tid; e < WG_PH * WG_PW * CC; e += WG_NT) {
         const int ci = e % CC;
         const int pc = e / CC;
-        const int col = pc % WG_PW, r = pc / WG_PW;
-        const int gy = y0 + r - 1, gx = x0 + col - 1, c = c0 + ci;
+        const int gy = y0 + pc / WG_PW - 1, gx = x0 + pc % WG_PW - 1, c = c0 + ci;
         float v = 0.f;
         if (gy >= 0 && gy < x.h && gx >= 0 && gx < x.w && c < cin) v = ld(x, ((long)n * x.h + gy) * x.w + gx, c);
         xs[e] = v;
       }
     }
     if constexpr (DV) {
-      constexpr int ND = WG_TH * WG_TW * CO4, DPT = (ND + WG_NT - 1) / WG_NT;
-      float4 buf[DPT];
 #pragma unroll
       for (int k = 0; k < DPT; ++k) {
         const int e = tid + k * WG_NT;
-        buf[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (ND % WG_NT == 0 || e < ND) {
-          const int cg = e % CO4, pp = e / CO4;
-          const int gy = y0 + pp / WG_TW, gx = x0 + pp % WG_TW;
-          if (gy < x.h && gx < x.w && cg * 4 < cout)
-            buf[k] = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(dy.p) +
-                                                      (((long)n * x.h + gy) * x.w + gx) * dy.cs + dy.coff + cg * 4);
-        }
-      }
-#pragma unroll
-      for (int k = 0; k < DPT; ++k) {
-        const int e = tid + k * WG_NT;
-        if (ND % WG_NT == 0 || e < ND) ds[e] = buf[k];
+        if (ND % WG_NT == 0 || e < ND) ds[e] = db[k];
       }
     } else {
       float* dsf = reinterpret_cast<float*>(ds);
@@ -319,7 +337,13 @@ __global__ __launch_bounds__(WG_NT) void wgrad_kernel(V x, V dy, float* partials
         dsf[e] = v;
       }
     }
+  };
+
+  if (blockIdx.x < ntiles) issue(blockIdx.x);
+  for (long tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    commit(tile);
     __syncthreads();
+    if (tile + gridDim.x < ntiles) issue(tile + gridDim.x);
 #pragma unroll
     for (int k = 0; k < TPT; ++k) {
       const int t = tid + k * WG_NT;
@@ -445,13 +469,20 @@ static bool vec_ok(const V& v, int ve) {
   return reinterpret_cast<uintptr_t>(v.p) % 16 == 0 && v.c % ve == 0 && v.coff % ve == 0 && v.cs % ve == 0;
 }
 
+// x may also be read in 16-byte vectors past its last channel when the row stride holds them (the padded
+// concat / input buffers: up1n[..., :30] of a 32-wide row, in9[..., :9] of a 16-wide row); the extra lanes are zeroed
+static bool xvec_ok(const V& v, int ve) {
+  return reinterpret_cast<uintptr_t>(v.p) % 16 == 0 && v.coff % ve == 0 && v.cs % ve == 0 &&
+         v.coff + (v.c + ve - 1) / ve * ve <= v.cs;
+}
+
 template <int CC, int CO4>
 static void launch_wgrad(const V& xv, const V& dy, float* dw, float* ws, hipStream_t st) {
   const bool dv = vec_ok(dy, 4);
-  if (xv.dt == VM_BF16 && vec_ok(xv, 8)) {
+  if (xv.dt == VM_BF16 && xvec_ok(xv, 8)) {
     if (dv) launch_wgrad_t<CC, CO4, uint16_t, true, true>(xv, dy, dw, ws, st);
     else launch_wgrad_t<CC, CO4, uint16_t, true, false>(xv, dy, dw, ws, st);
-  } else if (xv.dt == VM_F32 && vec_ok(xv, 4)) {
+  } else if (xv.dt == VM_F32 && xvec_ok(xv, 4)) {
     if (dv) launch_wgrad_t<CC, CO4, float, true, true>(xv, dy, dw, ws, st);
     else launch_wgrad_t<CC, CO4, float, true, false>(xv, dy, dw, ws, st);
   } else {
