@@ -102,10 +102,27 @@ class VideoTrainer:
             self._wflip[scope] = torch.empty((3, 3, pc.cout, pc.cin), dtype=torch.float32, device=dev)
             ops.flip_weights(pc.w_hwio, self._wflip[scope])
             self.dconv[scope] = ops.PackedConv(self._wflip[scope], None, "fp32", dev)
+        # bf16: the patch-reuse conv kernel needs cout % 8 == 0, so the narrow new_convs (select2_* cout 4,
+        # select1_* cout 2, output cout 1) run on zero-padded copies of their filters into 8-channel buffers
+        self._padconv = {}
+        if self.model.dtype == torch.bfloat16:
+            for scope, cin, cout in NEW_CONVS:
+                if cout % 8 and not scope.startswith("upconv"):
+                    cp = (cout + 7) // 8 * 8
+                    wp = torch.zeros((3, 3, cin, cp), dtype=torch.float32, device=dev)
+                    bp = torch.zeros(cp, dtype=torch.float32, device=dev)
+                    self._padconv[scope] = (ops.PackedConv(wp, bp, self.model.dtype, dev), wp, bp, cout)
+            self._sync_padded()
         self.t = 0
         self._b1p = np.float32(1.0)
         self._b2p = np.float32(1.0)
         self._tb, self._key = None, None
+
+    def _sync_padded(self):
+        for scope, (pc, wp, bp, cout) in self._padconv.items():
+            wp[..., :cout].copy_(self.P[scope, "w"])
+            bp[:cout].copy_(self.P[scope, "b"])
+            pc.repack()
 
     # ------------------------------------------------------------------------------------------- buffers
     def _train_buffers(self, n, h, w):
@@ -117,10 +134,17 @@ class VideoTrainer:
         tb = {"alpha": F(0, 1), "dlogit": F(0, 1), "loss": torch.zeros(3, dtype=torch.float32, device=dev)}
         st = lambda c: (torch.empty(c, dtype=torch.float32, device=dev),  # noqa: E731
                         torch.empty(c, dtype=torch.float32, device=dev))
+        # pre-BN conv outputs in the compute dtype: bf16 lets the patch-reuse conv kernel write them
+        Z = lambda lv, c: torch.empty((n, L[lv][0], L[lv][1], c), dtype=self.model.dtype, device=dev)  # noqa: E731
         for lv, cat, width, sels, up, prev, conv, cout_key in LEVELS:
             for s, _ in sels + ((conv, None),):
                 c = self.model.convs[s].cout
-                tb["z_" + s], tb["dz_" + s], tb["st_" + s] = F(lv, c), F(lv, c), st(c)
+                if s in self._padconv:
+                    tb["zfull_" + s] = Z(lv, (c + 7) // 8 * 8)
+                    tb["z_" + s] = tb["zfull_" + s][..., :c]
+                else:
+                    tb["z_" + s] = Z(lv, c)
+                tb["dz_" + s], tb["st_" + s] = F(lv, c), st(c)
             tb["st_" + up] = st(width)
             tb["dcatn_" + up] = F(lv, width)
             tb["dcat_" + up] = F(lv, width)
@@ -130,7 +154,12 @@ class VideoTrainer:
                 tb["dprev_" + up] = F(lv + 1, self.model.convs[up].cin)
             tb["dout_" + conv] = F(lv, self.model.convs[conv].cout)
         # the output conv's dz feeds the data-gradient conv, whose input views need channels padded to 8
-        tb["z_output"], tb["st_output"] = F(0, 1), st(1)
+        if "output" in self._padconv:
+            tb["zfull_output"] = Z(0, 8)
+            tb["z_output"] = tb["zfull_output"][..., :1]
+        else:
+            tb["z_output"] = F(0, 1)
+        tb["st_output"] = st(1)
         tb["dz_output"] = torch.zeros((n, h, w, 8), dtype=torch.float32, device=dev)[..., :1]
         self._tb, self._key = tb, (n, h, w)
         return tb
@@ -143,7 +172,10 @@ class VideoTrainer:
     def _new_conv(self, x, scope, act, out, tb):
         """new_conv (unet_simple.py:19-27) with batch statistics, then ``act``; keeps z and (mean, var)."""
         z, (mean, var) = tb["z_" + scope], tb["st_" + scope]
-        ops.conv3x3(x, self.model.convs[scope], "none", out=z, affine=False)
+        if scope in self._padconv:
+            ops.conv3x3(x, self._padconv[scope][0], "none", out=tb["zfull_" + scope], affine=False)
+        else:
+            ops.conv3x3(x, self.model.convs[scope], "none", out=z, affine=False)
         ops.bn_stats(z, mean, var)
         bnl = self.model.bn[scope]
         ops.bn_apply(z, mean, var, bnl.gamma, bnl.beta, EPS, act, out=out)
@@ -229,6 +261,7 @@ class VideoTrainer:
         for scope in DGRAD:
             ops.flip_weights(self.model.convs[scope].w_hwio, self._wflip[scope])
             self.dconv[scope].repack()
+        self._sync_padded()
 
     def step(self, cmp, bg, warped, gt, raw_fg):
         """One training iteration; returns the device tensor [loss, alpha_loss, compositional_loss] (pre-update)."""
