@@ -8,11 +8,17 @@ A step = one UNetVideo forward over B synthetic 1080p 7-channel frames per GPU (
 in HBM before timing).  Frame-parallel: every rank runs its own frames, no collective in the data
 path (scaling "weak"); the packed weights are RCCL-broadcast from rank 0 once, before timing.
 Rank 0 prints ONE JSON line (value = frames processed by all ranks / max-over-ranks time).
+
+Sub-records on the same line: video_batch (config 4: 256 frames sharded + all-gathered), temporal
+(config 3: warp + occlusion + refine), fp32 (the path that meets north_star's 1e-4 bound), parity
+(bf16 vs fp32 vs the CPU oracle on the timed frame), train (config 5), loader and augment.
 """
 
 import argparse
 import json
 import os
+import platform
+import statistics
 import sys
 import time
 
@@ -24,62 +30,78 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-from vmatting import ops, parallel, unet  # noqa: E402
+from vmatting import ops, parallel, unet, video  # noqa: E402
 from vmatting.weights import synthetic_vgg16  # noqa: E402
 
 METRIC = "alpha-mattes/sec at 1920×1080, 1/2/4/8 MI355X + achieved HBM GB/s"
 PEAK_TFLOPS = {"bf16": 2516.6, "fp32": 157.3}  # MI355X dense MFMA (MI355X_MICROARCH.md chip table)
 PEAK_HBM_GBPS = 8000.0
-VGG_MEAN = (103.939, 116.779, 123.68)
+VGG_MEAN = video.VGG_MEAN
+N_SIMD = 1024  # 256 CUs x 4 SIMDs
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def synth_frames(n, h, w, first, device):
-    """frame f (seed 1234+f): cmp/bg BGR U{0..255} - VGG_MEAN; trimap {0,.5,1} - .5
-    from a random ellipse with an unknown band.  Generated on the device."""
-    out = torch.empty((n, h, w, 7), dtype=torch.float32, device=device)
-    mean = torch.tensor(VGG_MEAN, device=device)
-    yy = torch.arange(h, device=device, dtype=torch.float32)[:, None]
-    xx = torch.arange(w, device=device, dtype=torch.float32)[None, :]
-    for i in range(n):
-        g = torch.Generator(device=device)
-        g.manual_seed(1234 + first + i)
-        out[i, :, :, 0:3] = torch.randint(0, 256, (h, w, 3), generator=g, device=device).float() - mean
-        out[i, :, :, 3:6] = torch.randint(0, 256, (h, w, 3), generator=g, device=device).float() - mean
-        c = torch.rand(4, generator=g, device=device)
-        cy, cx = (0.3 + 0.4 * c[0]) * h, (0.3 + 0.4 * c[1]) * w
-        ry, rx = (0.15 + 0.15 * c[2]) * h, (0.15 + 0.15 * c[3]) * w
-        d = torch.sqrt(((yy - cy) / ry) ** 2 + ((xx - cx) / rx) ** 2)
-        band = 8.0 / float(min(ry, rx))
-        tri = torch.where(d < 1 - band, 1.0, torch.where(d < 1 + band, 0.5, 0.0))
-        out[i, :, :, 6] = tri - 0.5
-    return out
+def host_info():
+    """Host CPU model and the thread count the CPU baselines use (BLAS pool; OMP_NUM_THREADS on the box)."""
+    model = platform.processor() or "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        from threadpoolctl import threadpool_info
+        threads = max([i.get("num_threads", 1) for i in threadpool_info() if i.get("user_api") == "blas"] or [1])
+    except Exception:
+        threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    return model, int(threads)
 
 
-def video_batch(graphed, n_frames, h, w, rank, world, dev):
-    """BASELINE config 4: ``n_frames`` synthetic 1080p frames (seeds 1234..) sharded frame-parallel in contiguous
-    blocks, each rank runs its block through the captured forward, then ONE all-gather (RCCL ring over xGMI) hands
-    every rank the whole [n_frames, H, W, 1] fp32 matte batch.  Timed between barriers, max over ranks."""
-    a, b = parallel.shard_range(n_frames, rank, world)
-    frames = synth_frames(b - a, h, w, a, dev)
-    out_shape = tuple(graphed.output.shape[1:])
-    local = torch.empty((b - a,) + out_shape, dtype=graphed.output.dtype, device=dev)
+class Events:
+    """HIP events on the CURRENT stream (the one every vm_* launch of this process uses)."""
+
+    def __init__(self):
+        self.e = []
+
+    def mark(self):
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record()
+        self.e.append(ev)
+        return ev
+
+
+def ms(e0, e1):
+    return e0.elapsed_time(e1)
+
+
+# ------------------------------------------------------------------------------------------------ config 4
+
+def video_batch(model, value_per_gpu, n_frames, h, w, rank, world, dev, chunk):
+    """BASELINE config 4 through the product path (vmatting/video.py): n_frames synthetic 1080p frames sharded
+    frame-parallel in contiguous blocks, each rank's block replayed in HIP graphs of `chunk` frames (input read
+    in place, alpha written in place), then ONE all-gather (RCCL ring over xGMI) hands every rank the whole
+    [n_frames, H, W, 1] f32 matte batch.  Timed between barriers, max over ranks."""
+    a, b = video.shard(n_frames, rank, world)
+    frames = video.synthetic_frames(b - a, h, w, first=a, device=dev)
+    vm = video.VideoMatter(model, frames, chunk=chunk)
     mx = max(q - p for p, q in (parallel.shard_range(n_frames, r, world) for r in range(world)))
-    recv = torch.empty((world * mx,) + out_shape, dtype=local.dtype, device=dev) if world > 1 else None
-    graphed(frames[:1])  # warm
+    recv = torch.empty((world * mx, h, w, 1), dtype=torch.float32, device=dev) if world > 1 else None
+    vm.run()  # warm
     if world > 1:
-        parallel.gather_frames(local, n_frames, out=recv)  # warm the communicator
+        parallel.gather_frames(vm.alpha, n_frames, out=recv)  # warm the communicator
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(b - a):
-        local[i].copy_(graphed(frames[i:i + 1])[0])
+    vm.run()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
-    full = parallel.gather_frames(local, n_frames, out=recv)
+    full = parallel.gather_frames(vm.alpha, n_frames, out=recv)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -89,35 +111,171 @@ def video_batch(graphed, n_frames, h, w, rank, world, dev):
         dist.all_reduce(ts, op=dist.ReduceOp.MAX)
     total, comp, gath = (float(v) for v in ts.tolist())
     assert full.shape[0] == n_frames
-    return {"workload": "config 4: %d synthetic %dx%d frames sharded frame-parallel, mattes all-gathered to every rank"
-                        % (n_frames, w, h),
-            "frames": n_frames, "frames_per_s": round(n_frames / total, 3), "ms_total": round(1e3 * total, 3),
+    fps = n_frames / total
+    return {"workload": "config 4: %d synthetic %dx%d frames sharded frame-parallel over %d GPU(s), mattes "
+                        "all-gathered to every rank (vmatting/video.py)" % (n_frames, w, h, world),
+            "frames": n_frames, "frames_per_s": round(fps, 3), "ms_total": round(1e3 * total, 3),
             "ms_compute_max_rank": round(1e3 * comp, 3), "ms_all_gather": round(1e3 * gath, 3),
-            "all_gather_bytes": int(full.numel() * full.element_size()),
-            "includes": "per-frame input copy into the graph's static buffer + graph replay + matte copy-out"}
+            "all_gather_bytes": int(full.numel() * full.element_size()), "chunk_frames": chunk,
+            "graphs_per_rank": len(vm.spans),
+            # this run's own single-GPU reference: the headline step rate per GPU (batch-1 graph replay)
+            "parallel_efficiency": round(fps / (world * value_per_gpu), 4),
+            "parallel_efficiency_def": "frames_per_s / (n_gpus x the headline value per GPU of this run)",
+            "includes": "chunked HIP-graph replay reading the frames in place + the matte all-gather"}
 
 
-def cpu_baseline(h, w, sample_h, sample_w):
-    """The oracle (numpy f32 restatement of unet.py) timed on host cores on a bounded sample."""
-    from oracle import models as om
-    try:
-        from threadpoolctl import threadpool_info
-        threads = max([i.get("num_threads", 1) for i in threadpool_info() if i.get("user_api") == "blas"] or [1])
-    except Exception:
-        threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-    vgg = synthetic_vgg16(0)
-    p = om.unet_params(vgg, np.random.RandomState(0), video=True)
-    rs = np.random.RandomState(1234)
-    x = np.concatenate([rs.randint(0, 256, (1, sample_h, sample_w, 6)).astype(np.float32) - np.tile(VGG_MEAN, 2),
-                        rs.choice([-0.5, 0.0, 0.5], (1, sample_h, sample_w, 1))], -1).astype(np.float32)
+# ------------------------------------------------------------------------------------------------ config 3
+
+def synthetic_flow(h, w, seed, modes=8, amp=20.0):
+    """smooth random flow, sum of `modes` Gaussian modes scaled to |u|,|v| <= amp (seed 7)."""
+    rs = np.random.RandomState(seed)
+    yy, xx = np.mgrid[0:h, 0:w].astype(np.float32)
+    out = np.zeros((h, w, 2), np.float32)
+    for _ in range(modes):
+        cy, cx = rs.uniform(0, h), rs.uniform(0, w)
+        s = rs.uniform(0.1, 0.4) * max(h, w)
+        g = np.exp(-((yy - cy) ** 2 + (xx - cx) ** 2) / np.float32(2 * s * s))
+        out[..., 0] += np.float32(rs.uniform(-1, 1)) * g
+        out[..., 1] += np.float32(rs.uniform(-1, 1)) * g
+    out *= np.float32(amp / max(1e-9, float(np.abs(out).max())))
+    return out
+
+
+def temporal_case(h, w, seed=7):
+    rs = np.random.RandomState(seed)
+    bw = synthetic_flow(h, w, seed)
+    fw = -bw
+    yy, xx = np.mgrid[0:h, 0:w]
+    fw[((yy - 0.4 * h) ** 2 + (xx - 0.6 * w) ** 2) < (0.15 * min(h, w)) ** 2] += 40.0  # an occluded disk
+    prev = np.clip(1.3 - np.hypot((yy - h / 2) / (h / 3), (xx - w / 2) / (w / 4)), 0, 1).astype(np.float32)
+    cur = np.clip(prev + rs.normal(0, 0.02, prev.shape), 0, 1).astype(np.float32)
+    cmp = (rs.uniform(0, 255, (h, w, 3)) - np.array(VGG_MEAN)).astype(np.float32)
+    return prev, cur, cmp, bw, fw
+
+
+def temporal_bench(dev, steps, dtype, sizes, cpu, threads):
+    """BASELINE config 3: flow warp (flow.py:9-18) + occlusion check (flow.py:36-65) + RefineNet (refine.py:27-32,
+    Cin 5) on synthetic smooth flows, inputs resident in HBM.  Device ms per stage from HIP events on the launch
+    stream; both stages are HBM-bound (algorithmic bytes below), the refine conv is also reported in TFLOP/s."""
+    from vmatting import temporal
+    recs = []
+    for h, w in sizes:
+        prev, cur, cmp, bw, fw = temporal_case(h, w)
+        T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+        args = [T(a) for a in (prev, cur, cmp, bw, fw)]
+        np.random.seed(3)
+        tp = temporal.TemporalRefiner(dtype=dtype, device=dev)
+        for _ in range(3):
+            tp(*args, check_index=False)
+        torch.cuda.synchronize()
+        ev = Events()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            ev.mark()
+            x = tp.prepare_input(*args, check_index=False)
+            ev.mark()
+            tp.refine.forward_prepared(x, out=tp._bufs[(h, w)]["out"])
+            ev.mark()
+        torch.cuda.synchronize()
+        wall = (time.perf_counter() - t0) / steps
+        assert int(tp._bufs[(h, w)]["err"].item()) == 0
+        e = ev.e
+        t_in = sum(ms(e[3 * i], e[3 * i + 1]) for i in range(steps)) / steps
+        t_rf = sum(ms(e[3 * i + 1], e[3 * i + 2]) for i in range(steps)) / steps
+        px = h * w
+        ob = 2 if dtype == "bf16" else 4
+        # input pass: flow_b 8 + flow_f gather 8 + prev gather 4 + cmp 12 + alpha_t 4 + warped out 4 + row 8*ob
+        b_in = px * (8 + 8 + 4 + 12 + 4 + 4 + 8 * ob)
+        # refine: input row 8*ob + f32 64-ch softmax out 256; FLOPs of conv4 at the reference's Cin = 5
+        b_rf = px * (8 * ob + 256)
+        f_rf = 2.0 * px * 9 * 5 * 64
+        rec = {"workload": "config 3: warp + correct_alpha + RefineNet(Cin 5) at %dx%d, %s" % (w, h, dtype),
+               "pairs_per_s": round(1.0 / wall, 1), "ms_per_pair": round(1e3 * wall, 4),
+               "device_ms": {"warp_occlusion_input": round(t_in, 4), "refine_conv_softmax": round(t_rf, 4)},
+               "roofline": {
+                   "warp_occlusion_input": {"bound": "hbm", "algorithmic_bytes": int(b_in),
+                                            "achieved_gbps": round(b_in / (t_in * 1e-3) / 1e9, 1),
+                                            "peak_gbps": PEAK_HBM_GBPS,
+                                            "frac": round(b_in / (t_in * 1e-3) / 1e9 / PEAK_HBM_GBPS, 4)},
+                   "refine_conv_softmax": {"bound": "hbm", "algorithmic_bytes": int(b_rf),
+                                           "achieved_gbps": round(b_rf / (t_rf * 1e-3) / 1e9, 1),
+                                           "peak_gbps": PEAK_HBM_GBPS,
+                                           "frac": round(b_rf / (t_rf * 1e-3) / 1e9 / PEAK_HBM_GBPS, 4),
+                                           "tflops": round(f_rf / (t_rf * 1e-3) / 1e12, 2)}},
+               "occluded_px": int((tp.warped == 0).sum().item())}
+        if cpu and (h, w) == sizes[0]:
+            from oracle import flow as oflow  # the CPU-baseline leg only
+            from oracle import ops as oops
+            p4 = tp.refine.params["conv4"]
+            times = []
+            for _ in range(2):
+                t0 = time.perf_counter()
+                a = oflow.correct_alpha(bw, fw, oflow.warp_img(prev, bw), promote="numpy1")
+                xin = np.concatenate([cmp, cur[..., None], a[..., None].astype(np.float32)], -1)[None]
+                oops.softmax_lastdim(oops.conv3x3_same(xin, p4[0], p4[1]))
+                times.append(time.perf_counter() - t0)
+            dt = min(times)
+            rec["cpu_baseline"] = {"value": round(1.0 / dt, 3), "unit": "pairs/s", "cores": threads, "kind": "port",
+                                   "sample": "oracle/flow.py warp_img + vectorised correct_alpha + oracle/ops.py "
+                                             "conv3x3 + softmax (RefineNet conv4, f32) on one %dx%d pair, best of 2"
+                                             % (w, h)}
+        recs.append(rec)
+    return recs
+
+
+# ------------------------------------------------------------------------------------------------ CPU baseline + parity
+
+def cpu_baseline(x_host, params, frames, threads, model_name):
+    """The oracle (numpy f32 restatement of unet.py, the reference's op sequence) on the host cores: 1 warm-up
+    frame at 270x480, then `frames` full 1920x1080 frames timed, median.  Returns (record, oracle output of the
+    first timed frame) — the latter is the fp32 parity check of the timed frame."""
+    from oracle import models as om  # the CPU-baseline leg only
+    om.unet_forward(np.ascontiguousarray(x_host[:, :270, :480]), params, dtype=np.float32)
+    times, ref = [], None
+    for _ in range(frames):
+        t0 = time.perf_counter()
+        r = om.unet_forward(x_host, params, dtype=np.float32)
+        times.append(time.perf_counter() - t0)
+        if ref is None:
+            ref = r
+    med = statistics.median(times)
+    rec = {"value": round(1.0 / med, 5), "unit": "frames/s", "cores": threads, "kind": "port",
+           "host_cpu": model_name,
+           "sample": "oracle/models.py numpy-f32 UNetVideo forward (the reference's op sequence) on the timed "
+                     "1920x1080 frame: 1 warm-up (270x480), median of %d full frames (%s s)"
+                     % (frames, ", ".join("%.1f" % t for t in times))}
+    return rec, ref
+
+
+def fp32_record(model, x, steps, vgg, params):
+    """The fp32 path (exact-f32 MFMA, the one north_star's 1e-4 alpha bound holds for) at 1080p: graph-replayed
+    forward timed over `steps` frames, plus per-conv events for its roofline against the f32 MFMA peak."""
+    m32 = unet.UNetVideo(vgg, dtype="fp32", device=x.device).load_params(params).prepare()
+    g = m32.capture(x)
+    g.replay()
+    torch.cuda.synchronize()
     t0 = time.perf_counter()
-    om.unet_forward(x, p, dtype=np.float32)
-    dt = time.perf_counter() - t0
-    scale = (h * w) / float(sample_h * sample_w)  # conv work is linear in pixels
-    return {"value": round(1.0 / (dt * scale), 5), "unit": "frames/s", "cores": int(threads), "kind": "port",
-            "sample": "oracle/ numpy-f32 UNetVideo forward on one %dx%d 7-ch frame (%.1f s), scaled x%.0f to "
-                      "1920x1080 by pixel count" % (sample_w, sample_h, dt, scale)}
+    for _ in range(steps):
+        g.replay()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    prof = ops.conv_profile(True)
+    m32.forward(x)
+    torch.cuda.synchronize()
+    ops.conv_profile(False)
+    fl = sum(p[0] for p in prof)
+    t = sum(ms(p[2], p[3]) for p in prof)
+    flops = m32.conv_flops(x.shape[0], x.shape[1], x.shape[2])
+    rec = {"workload": "unet.UNetVideo forward, fp32 (v_mfma_f32_16x16x4_f32), 1920x1080, hip-graph replay",
+           "frames_per_s": round(x.shape[0] / dt, 3), "ms_per_frame": round(1e3 * dt / x.shape[0], 3),
+           "tflops_whole_forward": round(flops / dt / 1e12, 2),
+           "roofline": {"bound": "mfma", "achieved": round(fl / (t * 1e-3) / 1e12, 2), "peak": PEAK_TFLOPS["fp32"],
+                        "unit": "TFLOP/s", "frac": round(fl / (t * 1e-3) / 1e12 / PEAK_TFLOPS["fp32"], 4),
+                        "scope": "all convs of one forward (HIP events per launch)"}}
+    return rec, m32
 
+
+# ------------------------------------------------------------------------------------------------ loader / augment
 
 def loader_inputs(n, h, w, seed=0):
     """Decoded video-loader entries (fg/prev BGRA, bg BGR u8, piecewise-constant f32 flow) at h x w."""
@@ -132,7 +290,16 @@ def loader_inputs(n, h, w, seed=0):
     return out
 
 
-def loader_bench(dev, steps, cpu=True, n=8, size=320, h=1080, w=1920):
+def _pool_rate(fn, items, threads):
+    """Wall-clock rate of fn over items on a pool of `threads` host threads (numpy releases the GIL)."""
+    from concurrent.futures import ThreadPoolExecutor
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(max_workers=threads) as ex:
+        list(ex.map(fn, items))
+    return len(items) / (time.perf_counter() - t0)
+
+
+def loader_bench(dev, steps, threads, cpu=True, n=8, size=320, h=1080, w=1920):
     """video_batch's per-pixel work (csrc/loader.hip) on a batch of n 1080p video entries resized
     to size x size; inputs resident in HBM, the host's np.random draws replayed once outside the timed region."""
     from vmatting import loader as vl
@@ -145,15 +312,15 @@ def loader_bench(dev, steps, cpu=True, n=8, size=320, h=1080, w=1920):
     for _ in range(3):
         vl.compose_batch(samples, (size, size), names, device=dev)
     torch.cuda.synchronize()
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    ev = Events()
     t0 = time.perf_counter()
-    ev[0].record()
+    ev.mark()
     for _ in range(steps):
         vl.compose_batch(samples, (size, size), names, device=dev)
-    ev[1].record()
+    ev.mark()
     torch.cuda.synchronize()
     wall = (time.perf_counter() - t0) / steps
-    dev_ms = ev[0].elapsed_time(ev[1]) / steps
+    dev_ms = ms(*ev.e) / steps
     # algorithmic bytes per batch: the f32 outputs (13 channels) + each source byte the resize can touch, once
     # (min(window area, 4 taps per output pixel) per plane: fg BGRA 4 B, flow 8 B, prev BGRA 4 B, bg 3 B)
     taps = 4 * size * size
@@ -169,20 +336,20 @@ def loader_bench(dev, steps, cpu=True, n=8, size=320, h=1080, w=1920):
            "crops": [int(s["plan"][0][0]) for s in host]}
     if cpu:
         from oracle import loader as ol  # the CPU-baseline leg only
-        k = 2
-        t0 = time.perf_counter()
-        for s in host[:k]:
+
+        def one(s):
             fr, fc, br, bc = (ol.Axis(*a) for a in s["plan"])
             srcs = ol.crop_sources(s["fg"], s["bg"], fr, fc, br, bc, s["prev"], s["flow"])
             ol.compose(srcs[0], srcs[1], srcs[3], (size, size), srcs[2])
-        dt = (time.perf_counter() - t0) / k
-        rec["cpu_baseline"] = {"value": round(1.0 / dt, 3), "unit": "samples/s", "cores": 1, "kind": "port",
-                               "sample": "oracle/loader.py (numpy float64, with the reference's full-frame warp) on "
-                                         "%d of the %d entries (%.2f s each)" % (k, n, dt)}
+        items = [host[i % n] for i in range(threads)]
+        rate = _pool_rate(one, items, threads)
+        rec["cpu_baseline"] = {"value": round(rate, 3), "unit": "samples/s", "cores": threads, "kind": "port",
+                               "sample": "oracle/loader.py (numpy float64, with the reference's full-frame warp), "
+                                         "%d entries on a pool of %d host threads" % (len(items), threads)}
     return rec
 
 
-def augment_bench(dev, steps, cpu=True, h=1080, w=1920):
+def augment_bench(dev, steps, threads, cpu=True, h=1080, w=1920):
     """augmentation.augment on one 1080p (fg, bg, alpha) sample resident in HBM: host draws +
     TPS solve + one stats sync + the csrc/augment.hip kernels.  Device time from HIP events on the launch stream."""
     from vmatting import augmentation as va
@@ -196,15 +363,15 @@ def augment_bench(dev, steps, cpu=True, h=1080, w=1920):
     for _ in range(3):
         va.augment(fg, bg, alpha)
     torch.cuda.synchronize()
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    ev = Events()
     t0 = time.perf_counter()
-    ev[0].record()
+    ev.mark()
     for _ in range(steps):
         va.augment(fg, bg, alpha)
-    ev[1].record()
+    ev.mark()
     torch.cuda.synchronize()
     wall = (time.perf_counter() - t0) / steps
-    dev_ms = ev[0].elapsed_time(ev[1]) / steps
+    dev_ms = ms(*ev.e) / steps
     # algorithmic bytes per sample (per pixel): alpha stats 8; bg 2 warps 2*(3+3); TPS grid (h/2)(w/2)*16 = 4;
     # fg TPS 3+3, alpha TPS 8+8; fg 2 warps 2*(3+3); alpha 2 warps 2*(8+8); illumination fg+bg 2*(3+3)
     algo = h * w * (8 + 12 + 4 + 6 + 16 + 12 + 32 + 12)
@@ -215,16 +382,17 @@ def augment_bench(dev, steps, cpu=True, h=1080, w=1920):
     if cpu:
         from oracle import augment as oa  # the CPU-baseline leg only
         sh, sw = h // 2, w // 2
+        args = (fg_h[:sh, :sw].copy(), bg_h[:sh, :sw].copy(), alpha_h[::2, ::2].copy())
         np.random.seed(0)
-        t0 = time.perf_counter()
-        oa.augment(fg_h[:sh, :sw].copy(), bg_h[:sh, :sw].copy(), alpha_h[::2, ::2].copy())
-        dt = (time.perf_counter() - t0) * (h * w) / float(sh * sw)
-        rec["cpu_baseline"] = {"value": round(1.0 / dt, 3), "unit": "samples/s", "cores": 1, "kind": "port",
-                               "sample": "oracle/augment.py (numpy, scipy-order TPS + OpenCV restatement) on one "
-                                         "%dx%d sample, scaled x%d to %dx%d by pixel count" % (sw, sh, (h * w) // (sh * sw),
-                                                                                         w, h)}
+        rate = _pool_rate(lambda _: oa.augment(*args), list(range(threads)), threads) * (sh * sw) / float(h * w)
+        rec["cpu_baseline"] = {"value": round(rate, 3), "unit": "samples/s", "cores": threads, "kind": "port",
+                               "sample": "oracle/augment.py (numpy, scipy-order TPS + OpenCV restatement): %d "
+                                         "%dx%d samples on a pool of %d host threads, scaled x%d to %dx%d by pixel "
+                                         "count" % (threads, sw, sh, threads, (h * w) // (sh * sw), w, h)}
     return rec
 
+
+# ------------------------------------------------------------------------------------------------ config 5
 
 def train_flops(n, h, w):
     """Algorithmic FLOPs of one config-5 step: 3 frozen VGG16 towers + UNetSimple forward (unet_simple.py:45-171),
@@ -246,15 +414,14 @@ def train_flops(n, h, w):
     return fwd + head, head + dgrad
 
 
-def train_bench(dev, steps, warmup, world, rank, cpu=True, n=8, size=320, dtype="bf16"):
+def train_bench(dev, steps, warmup, world, rank, threads, cpu=True, n=8, size=320, dtype="bf16"):
     """BASELINE config 5: one train.py video_procedure iteration per step (train.py:288-343) — batch of 8 320x320
     samples per GPU (params.py:8-9) resident in HBM: 3 VGG16 towers + UNetSimple (batch-statistics BN) forward,
     loss, backward through the trainable layers, one RCCL all-reduce of the gradients (DDP), TF-Adam, re-pack.
     Device time per phase from HIP events on the launch stream; step time = max over ranks."""
     from vmatting.train import VideoTrainer
-    from vmatting.weights import synthetic_vgg16
     rs = np.random.RandomState(100 + rank)
-    mean = np.array([103.939, 116.779, 123.68])
+    mean = np.array(VGG_MEAN)
     fg = rs.uniform(0, 255, (n, size, size, 3))
     bg = rs.uniform(0, 255, (n, size, size, 3))
     yy, xx = np.mgrid[:size, :size]
@@ -271,35 +438,32 @@ def train_bench(dev, steps, warmup, world, rank, cpu=True, n=8, size=320, dtype=
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
-    fwd_ms = bwd_ms = upd_ms = 0.0
+    ev = Events()
     t0 = time.perf_counter()
     for _ in range(steps):
-        ev[0].record()
+        ev.mark()
         trn.forward(cmp_d, bg_d, warped_d)
-        from vmatting import ops
         trn._tb["loss"].copy_(ops.matting_loss(trn._tb["alpha"], gt_d, fg_d, bg_d, cmp_d))
-        ev[1].record()
+        ev.mark()
         trn.grad.zero_()
         trn.backward(gt_d, fg_d, bg_d, cmp_d)
-        ev[2].record()
+        ev.mark()
         trn.apply_gradients()
-        ev[3].record()
-        torch.cuda.synchronize()
-        fwd_ms += ev[0].elapsed_time(ev[1])
-        bwd_ms += ev[1].elapsed_time(ev[2])
-        upd_ms += ev[2].elapsed_time(ev[3])
+        ev.mark()
+    torch.cuda.synchronize()
     wall = torch.tensor([(time.perf_counter() - t0) / steps], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(wall, op=dist.ReduceOp.MAX)
     wall = float(wall)
+    e = ev.e
+    ph = [sum(ms(e[4 * i + k], e[4 * i + k + 1]) for i in range(steps)) / steps for k in range(3)]
     fwd_f, bwd_f = train_flops(n, size, size)
     rec = {"workload": "train.py video_procedure step (config 5): %d x %dx%d per GPU, 3 VGG16 towers + UNetSimple "
                        "fwd/bwd, loss, DDP all-reduce, TF-Adam" % (n, size, size),
            "dtype": dtype + " forward, f32 gradients/optimizer", "n_gpus": world,
            "samples_per_s": round(n * world / wall, 1), "ms_per_step": round(1000 * wall, 3),
-           "device_ms": {"forward_loss": round(fwd_ms / steps, 3), "backward": round(bwd_ms / steps, 3),
-                         "allreduce_adam_repack": round(upd_ms / steps, 3)},
+           "device_ms": {"forward_loss": round(ph[0], 3), "backward": round(ph[1], 3),
+                         "allreduce_adam_repack": round(ph[2], 3)},
            "flops_per_step_per_gpu": {"forward": fwd_f, "backward": bwd_f},
            "achieved_tflops_per_gpu": round((fwd_f + bwd_f) / wall / 1e12, 1),
            "loss_last": [round(float(v), 5) for v in trn._tb["loss"].cpu()]}
@@ -312,7 +476,7 @@ def train_bench(dev, steps, warmup, world, rank, cpu=True, n=8, size=320, dtype=
         t0 = time.perf_counter()
         tr.train_step_grads(sl(cmp), sl(bg - mean), sl(warped), sl(gt), sl(fg), synthetic_vgg16(0), p)
         dt = (time.perf_counter() - t0) * (size * size) / float(sh * sh)
-        rec["cpu_baseline"] = {"value": round(1.0 / dt, 4), "unit": "samples/s", "cores": torch.get_num_threads(),
+        rec["cpu_baseline"] = {"value": round(1.0 / dt, 4), "unit": "samples/s", "cores": threads,
                                "kind": "port",
                                "sample": "oracle/train_ref.py (numpy-f64 VGG towers + torch-f64 autograd head) on one "
                                          "%dx%d sample, scaled x%.2f to %dx%d by pixel count" %
@@ -320,11 +484,13 @@ def train_bench(dev, steps, warmup, world, rank, cpu=True, n=8, size=320, dtype=
     return rec
 
 
-def load_traffic(args, full=False):
-    """Per-launch HBM bytes per kernel from the committed PMC pass (tools/traffic.py -> profiles/*_traffic.json),
-    used only when it was collected on this exact workload."""
+# ------------------------------------------------------------------------------------------------ roofline
+
+def load_profile(kind, args):
+    """Per-launch PMC values per kernel from the committed rocprofv3 passes (tools/pmc_passes.py ->
+    profiles/*_<kind>.json), used only when collected on this exact workload."""
     import glob
-    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*_traffic.json")), reverse=True):
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*_%s.json" % kind)), reverse=True):
         try:
             with open(path) as f:
                 t = json.load(f)
@@ -333,8 +499,8 @@ def load_traffic(args, full=False):
         c = t.get("config", {})
         if (c.get("dtype"), c.get("height"), c.get("width"), c.get("batch")) == (args.dtype, args.height, args.width,
                                                                                args.batch):
-            return (path, t) if full else (path, t.get("kernels", {}))
-    return None, ({} if not full else None)
+            return os.path.relpath(path, REPO), t
+    return None, None
 
 
 def conv_roofline(prof, args):
@@ -345,52 +511,69 @@ def conv_roofline(prof, args):
     for fl, name, e0, e1 in prof:
         d = per.setdefault(name, [0, 0.0, 0])
         d[0] += fl
-        d[1] += e0.elapsed_time(e1)
+        d[1] += ms(e0, e1)
         d[2] += 1
-    name, (fl, ms, n) = max(per.items(), key=lambda kv: kv[1][1])
-    achieved = fl / (ms * 1e-3) / 1e12
+    name, (fl, t, n) = max(per.items(), key=lambda kv: kv[1][1])
+    achieved = fl / (t * 1e-3) / 1e12
     peak = PEAK_TFLOPS[args.dtype]
-    src, traffic = load_traffic(args)
-    tr = traffic.get(name)
+    src_t, traffic = load_profile("traffic", args)
+    tr = (traffic or {}).get("kernels", {}).get(name)
+    src_m, mf = load_profile("mfma", args)
+    mk = (mf or {}).get("kernels", {}).get(name)
     all_fl = sum(v[0] for k, v in per.items() if "head" not in k)
     all_ms = sum(v[1] for k, v in per.items() if "head" not in k)
     if args.layers:
         per_step = len(prof) // max(1, args.steps)
         for i in range(per_step):
             rows = prof[i::per_step]
-            t_ms = sum(e0.elapsed_time(e1) for _, _, e0, e1 in rows) / len(rows)
+            t_ms = sum(ms(e0, e1) for _, _, e0, e1 in rows) / len(rows)
             log("  conv #%2d %-55s %.3f ms  %.1f TFLOP/s" % (i, rows[0][1], t_ms, rows[0][0] / (t_ms * 1e-3) / 1e12))
-    for k, (f, t, c) in sorted(per.items(), key=lambda kv: -kv[1][1]):
-        log("%-58s %3d launches %.3f ms/step %.1f TFLOP/s" % (k, c, t / args.steps, f / (t * 1e-3) / 1e12))
-    return {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
-            "frac": round(achieved / peak, 4), "traffic": tr["bytes_per_launch"] if tr else None,
-            "kernel": name, "launches": n, "avg_launch_ms": round(ms / n, 4), "flops_per_launch": int(fl / n),
-            "traffic_source": ("%s (FETCH_SIZE x2 + WRITE_SIZE, per launch)" % os.path.relpath(src, REPO)) if tr
-            else None,
-            "all_mfma_convs": {"tflops": round(all_fl / (all_ms * 1e-3) / 1e12, 2),
-                               "ms_per_step": round(all_ms / args.steps, 4),
-                               "frac": round(all_fl / (all_ms * 1e-3) / 1e12 / peak, 4)}}
+    for k, (f, tt, c) in sorted(per.items(), key=lambda kv: -kv[1][1]):
+        log("%-58s %3d launches %.3f ms/step %.1f TFLOP/s" % (k, c, tt / args.steps, f / (tt * 1e-3) / 1e12))
+    rec = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
+           "frac": round(achieved / peak, 4), "traffic": tr["bytes_per_launch"] if tr else None,
+           "kernel": name, "launches": n, "avg_launch_ms": round(t / n, 4), "flops_per_launch": int(fl / n),
+           "traffic_source": ("%s (FETCH_SIZE x2 + WRITE_SIZE, per launch)" % src_t) if tr else None,
+           "all_mfma_convs": {"tflops": round(all_fl / (all_ms * 1e-3) / 1e12, 2),
+                              "ms_per_step": round(all_ms / args.steps, 4),
+                              "frac": round(all_fl / (all_ms * 1e-3) / 1e12 / peak, 4)}}
+    if mk:
+        # SQ_VALU_MFMA_BUSY_CYCLES: SIMD-cycles the matrix pipes were busy (all SIMDs, one launch);
+        # GRBM_GUI_ACTIVE / 8: the launch's GPU cycles (summed over the 8 XCDs by rocprofv3)
+        cyc = mk["GRBM_GUI_ACTIVE"] / 8.0
+        rec["mfma_util"] = round(mk["SQ_VALU_MFMA_BUSY_CYCLES"] / (N_SIMD * cyc), 4)
+        rec["mfma_counters"] = {"source": src_m, "SQ_VALU_MFMA_BUSY_CYCLES": mk["SQ_VALU_MFMA_BUSY_CYCLES"],
+                                "GRBM_GUI_ACTIVE": mk["GRBM_GUI_ACTIVE"], "SQ_BUSY_CYCLES": mk.get("SQ_BUSY_CYCLES"),
+                                "effective_clock_ghz": round(cyc / (t / n * 1e-3) / 1e9, 3),
+                                "def": "mfma_util = SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE/8): "
+                                       "matrix-pipe busy fraction at the clock the chip actually held"}
+    return rec
 
+
+# ------------------------------------------------------------------------------------------------ main
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=1, help="frames per step per GPU")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample", default="540x960", help="HxW of the CPU-baseline sample frame")
+    ap.add_argument("--cpu-frames", type=int, default=2, help="full 1080p frames timed for the CPU baseline (median)")
     ap.add_argument("--no-profile", action="store_true", help="skip per-conv HIP events")
     ap.add_argument("--layers", action="store_true", help="per-conv timing breakdown on stderr")
     ap.add_argument("--no-graph", action="store_true", help="time eager launches instead of the captured HIP graph")
     ap.add_argument("--no-loader", action="store_true", help="skip the training-sample loader record (rank 0, N=1)")
     ap.add_argument("--no-augment", action="store_true", help="skip the augmentation record (rank 0, N=1)")
     ap.add_argument("--no-train", action="store_true", help="skip the config-5 training-step record (all ranks)")
+    ap.add_argument("--no-temporal", action="store_true", help="skip the config-3 record (rank 0)")
+    ap.add_argument("--no-fp32", action="store_true", help="skip the fp32 record and the parity block (rank 0)")
     ap.add_argument("--video-frames", type=int, default=256,
                     help="config-4 record: frames sharded over the ranks + matte all-gather (0 = skip)")
+    ap.add_argument("--video-chunk", type=int, default=8, help="frames per HIP graph in the config-4 record")
     ap.add_argument("--option", action="append", default=[], metavar="KEY=VALUE",
                     help="vm_set_option kernel knob before the run (A/B comparisons), repeatable")
     args = ap.parse_args()
@@ -404,6 +587,7 @@ def main():
         k, v = kv.split("=")
         from vmatting import _lib
         _lib.set_option(k, int(v))
+    cpu_model, threads = host_info()
 
     # identical weights everywhere: every rank draws from the same seeds, then rank 0's packed
     # buffers are broadcast (one RCCL collective) so replicas are bit-identical by construction
@@ -413,7 +597,7 @@ def main():
     parallel.broadcast_tensors(model.weights_flat(), src=0)
 
     B, H, W = args.batch, args.height, args.width
-    x = synth_frames(B, H, W, rank * B, dev)
+    x = video.synthetic_frames(B, H, W, first=rank * B, device=dev)
     flops_per_frame = model.conv_flops(1, H, W)
 
     # the timed step is the whole forward replayed from a HIP graph (captured once: one host call per step, no
@@ -434,6 +618,8 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    alpha_timed = (graphed.output if graphed is not None else model.output).clone()
+    logits_timed = model.conv1_3.clone()
 
     # per-kernel HIP events cost ~10% of the step (a marker between every launch), so the roofline pass is a
     # second, identical K-step pass with an event pair on the launch stream around every conv
@@ -445,26 +631,23 @@ def main():
         torch.cuda.synchronize()
         ops.conv_profile(False)
 
-    video = None
-    if args.video_frames > 0 and graphed is not None and args.batch == 1:
-        video = video_batch(graphed, args.video_frames, H, W, rank, world, dev)
-
-    train = None
-    if not args.no_train:  # every rank: the DDP all-reduce is part of the step
-        train = train_bench(dev, max(args.steps // 2, 5), 2, world, rank, cpu=not args.no_cpu_baseline)
-
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-
     frames = world * B * args.steps
     value = frames / elapsed
     ms_step = 1000.0 * elapsed / args.steps
 
-    roofline = None
-    if prof:
-        roofline = conv_roofline(prof, args)
+    vrec = None
+    if args.video_frames > 0:
+        vrec = video_batch(model, value / world, args.video_frames, H, W, rank, world, dev, args.video_chunk)
+
+    train = None
+    if not args.no_train:  # every rank: the DDP all-reduce is part of the step
+        train = train_bench(dev, max(args.steps // 4, 10), 3, world, rank, threads, cpu=not args.no_cpu_baseline)
+
+    roofline = conv_roofline(prof, args) if prof else None
     if rank == 0:
         rec = {"metric": METRIC, "value": round(value, 3), "unit": "frames/s", "n_gpus": world,
                "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 4),
@@ -477,7 +660,7 @@ def main():
                           "parallelism": "frame-parallel dp%d" % world},
                "achieved_tflops_whole_forward": round(value / world * flops_per_frame / 1e12, 2),
                "roofline": roofline, "cpu_baseline": None}
-        src, tr = load_traffic(args, full=True)
+        src, tr = load_profile("traffic", args)
         if tr and tr.get("bytes_per_forward"):
             # whole-forward HBM traffic (PMC FETCH_SIZE x2 + WRITE_SIZE summed over every kernel of one forward,
             # one-time weight packing excluded) at this run's frame rate
@@ -485,18 +668,42 @@ def main():
             rec["achieved_hbm_gbps"] = round(bpf * value / world / 1e9, 1)
             rec["hbm"] = {"bytes_per_frame": int(bpf), "achieved_gbps_per_gpu": rec["achieved_hbm_gbps"],
                           "peak_gbps": PEAK_HBM_GBPS, "frac": round(bpf * value / world / 1e9 / PEAK_HBM_GBPS, 4),
-                          "source": os.path.relpath(src, REPO)}
-        if video:
-            rec["video_batch"] = video
+                          "source": src}
+        if world == 1 and not args.no_fp32:
+            params = model.params
+            fp32, m32 = fp32_record(model, x, 10, vgg, params)
+            rec["fp32"] = fp32
+            a32 = m32.output.clone()
+            l32 = m32.conv1_3.clone()
+            par = {"frame": "the timed %dx%d frame (seed 1234)" % (W, H),
+                   "bf16_vs_fp32_alpha_maxabs": float((alpha_timed - a32).abs().max()) if args.dtype == "bf16"
+                   else 0.0,
+                   "bf16_logits_rel": float((logits_timed - l32).abs().max() / l32.abs().max())
+                   if args.dtype == "bf16" else 0.0,
+                   "bound": 1e-4, "bound_applies_to": "fp32 alpha vs the reference CPU forward (north_star)"}
+            if not args.no_cpu_baseline:
+                crec, ref = cpu_baseline(x[:1].cpu().numpy(), params, args.cpu_frames, threads, cpu_model)
+                rec["cpu_baseline"] = crec
+                par["fp32_vs_oracle_alpha_maxabs"] = float(np.abs(a32[:1].cpu().numpy() - ref["output"]).max())
+                par["fp32_vs_oracle_logits_rel"] = float(np.abs(l32[:1].cpu().numpy() - ref["conv1_3"]).max()
+                                                         / np.abs(ref["conv1_3"]).max())
+                par["bf16_vs_oracle_alpha_maxabs"] = float(np.abs(alpha_timed[:1].cpu().numpy()
+                                                                  - ref["output"]).max())
+                par["fp32_meets_bound"] = par["fp32_vs_oracle_alpha_maxabs"] <= 1e-4
+                par["bf16_meets_bound"] = par["bf16_vs_oracle_alpha_maxabs"] <= 1e-4
+            rec["parity"] = par
+            del m32
+        if vrec:
+            rec["video_batch"] = vrec
+        if world == 1 and not args.no_temporal:
+            rec["temporal"] = temporal_bench(dev, 20, args.dtype, [(500, 1200), (1080, 1920)],
+                                             not args.no_cpu_baseline, threads)
         if train:
             rec["train"] = train
-        if world == 1 and not args.no_cpu_baseline:
-            sh, sw = (int(v) for v in args.cpu_sample.split("x"))
-            rec["cpu_baseline"] = cpu_baseline(H, W, sh, sw)
         if world == 1 and not args.no_loader:
-            rec["loader"] = loader_bench(dev, max(args.steps, 10), cpu=not args.no_cpu_baseline)
+            rec["loader"] = loader_bench(dev, max(args.steps // 4, 10), threads, cpu=not args.no_cpu_baseline)
         if world == 1 and not args.no_augment:
-            rec["augment"] = augment_bench(dev, max(args.steps, 10), cpu=not args.no_cpu_baseline)
+            rec["augment"] = augment_bench(dev, max(args.steps // 4, 10), threads, cpu=not args.no_cpu_baseline)
         print(json.dumps(rec), flush=True)
     if world > 1:
         dist.destroy_process_group()

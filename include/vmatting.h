@@ -172,6 +172,17 @@ int vm_remap_bilinear_u8(const uint8_t* img, int ih, int iw, int cn, const float
 int vm_fb_consistency(const float* backward, const float* forward, int h, int w, float* alpha, float thresh,
                       int promote, int* err_flag, void* stream);
 
+/* BASELINE config 3 in one pass (flow.py:69-77 chain, refine.py:27 input): per pixel
+ *   alpha_w = warp_img(prev_alpha, backward)      (as vm_remap_bilinear_f32 mode 0, flow.py:9-18)
+ *   correct_alpha(backward, forward, alpha_w)     (as vm_fb_consistency, flow.py:36-65, threshold thresh)
+ *   out[pixel] = [cmp B, G, R, alpha, alpha_w, 0, 0, 0]   (the RefineNet input, Cin 5 padded to 8)
+ * prev_alpha / alpha [h,w] f32, backward / forward [h,w,2] f32, cmp [h,w,3] f32 (BGR - VGG_MEAN), out [h,w,8]
+ * in out_dtype (VM_F32 or VM_BF16), warped [h,w] f32 or NULL.  *err_flag (zeroed by the caller) is set where
+ * the reference raises IndexError; the output is then undefined. */
+int vm_temporal_refine_input(const float* prev_alpha, const float* backward, const float* forward, const float* cmp,
+                             const float* alpha, int h, int w, float thresh, int promote, void* out, int out_dtype,
+                             float* warped, int* err_flag, void* stream);
+
 /* train.py:14-28,42-47 loss: out[0] = mean(0.5*charb(pred,gt) + 0.5*charb(composite(raw_fg,bg,pred), cmp)),
  * out[1] = mean alpha loss, out[2] = mean compositional loss.  pred/gt [n,h,w,1], others [n,h,w,3] f32.
  * work: vm_loss_workspace_bytes(n*h*w) bytes. */

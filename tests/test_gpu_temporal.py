@@ -1,0 +1,105 @@
+"""BASELINE config 3 on the GPU: the fused warp + occlusion + refine-input pass (temporal.TemporalRefiner) against
+the separate-op API and the CPU oracle.
+
+* the fused pass's warped / corrected alpha is bit-identical to flow.warp_img -> flow.correct_alpha on the GPU,
+  which the golden tests pin to the reference's own flow.py outputs (test_gpu_parity.py);
+* the refine input channels are exactly [cmp, alpha, warped] (f32) or their bf16 rounding;
+* 500x1200 (the flow.py demo size) and 1080p: the fp32 refine output (64-ch softmax) within 1e-5 max-abs of the
+  numpy oracle (oracle.models.refine_forward on the same input) — the chain's size-independent properties
+  (softmax rows sum to 1, occluded pixels carry warped alpha 0) at full size.
+"""
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import gpu_available
+
+pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not gpu_available(), reason="needs a ROCm GPU")]
+
+DEV = "cuda"
+
+
+def _case(h, w, seed=7):
+    from oracle.flow import smooth_flow
+    rs = np.random.RandomState(seed)
+    bw = smooth_flow(h, w, seed=seed)
+    fw = -smooth_flow(h, w, seed=seed)  # round trip closes ...
+    yy, xx = np.mgrid[0:h, 0:w]
+    occ = ((yy - 0.4 * h) ** 2 + (xx - 0.6 * w) ** 2) < (0.15 * min(h, w)) ** 2
+    fw[occ] += 40.0  # ... except inside a disk: occluded (err > 15 px)
+    yy, xx = np.mgrid[0:h, 0:w]
+    prev = np.clip(1.3 - np.hypot((yy - h / 2) / (h / 3), (xx - w / 2) / (w / 4)), 0, 1).astype(np.float32)
+    cur = np.clip(prev + rs.normal(0, 0.02, prev.shape), 0, 1).astype(np.float32)
+    cmp = (rs.uniform(0, 255, (h, w, 3)) - np.array([103.939, 116.779, 123.68])).astype(np.float32)
+    return prev, cur, cmp, bw.astype(np.float32), fw.astype(np.float32), occ
+
+
+def T(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+
+
+@pytest.mark.parametrize("h,w", [(64, 96), (500, 1200)])
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_fused_input_equals_separate_ops(h, w, dtype):
+    from vmatting import flow, temporal
+    prev, cur, cmp, bw, fw, _ = _case(h, w)
+    np.random.seed(3)
+    tp = temporal.TemporalRefiner(dtype=dtype)
+    x = tp.prepare_input(T(prev), T(cur), T(cmp), T(bw), T(fw))
+    warped = flow.warp_img(T(prev), T(bw))
+    flow.correct_alpha(T(bw), T(fw), warped)
+    assert torch.equal(tp.warped, warped)
+    want = torch.cat([T(cmp), T(cur)[..., None], warped[..., None]], -1)[None]
+    want = want.to(x.dtype)
+    assert torch.equal(x, want)
+    pad = tp._bufs[(h, w)]["xin"][..., 5:]
+    assert torch.count_nonzero(pad) == 0
+
+
+@pytest.mark.parametrize("h,w", [(500, 1200), (1080, 1920)])
+def test_temporal_refine_fp32_vs_oracle(h, w):
+    from oracle import flow as oflow
+    from oracle import models as om
+    from vmatting import temporal
+    prev, cur, cmp, bw, fw, occ = _case(h, w)
+    np.random.seed(3)
+    tp = temporal.TemporalRefiner(dtype="fp32")
+    out = tp(T(prev), T(cur), T(cmp), T(bw), T(fw))
+    torch.cuda.synchronize()
+    warped = oflow.correct_alpha(bw, fw, oflow.warp_img(prev, bw), promote="numpy1").astype(np.float32)
+    gw = tp.warped.cpu().numpy()
+    assert np.abs(gw - warped).max() <= 1e-6  # the remap golden bound (test_gpu_parity.py)
+    # occluded where the backward target lands in the disk where forward flow was perturbed
+    assert np.array_equal(gw == 0, warped == 0) and (gw == 0).sum() > (occ.sum() // 2)
+    x = np.concatenate([cmp, cur[..., None], warped[..., None]], -1)[None]
+    ref = om.refine_forward(x, tp.refine.params, dtype=np.float32)["output"]
+    got = out.cpu().numpy()
+    err = float(np.abs(got - ref).max())
+    print("config 3 %dx%d: fp32 refine softmax max-abs err vs oracle %.2e" % (h, w, err))
+    assert err <= 1e-5
+    np.testing.assert_allclose(got.sum(-1), 1.0, atol=1e-5)
+
+
+def test_temporal_refine_bf16_close_to_fp32():
+    from vmatting import temporal
+    prev, cur, cmp, bw, fw, _ = _case(540, 960)
+    np.random.seed(3)
+    tb = temporal.TemporalRefiner(dtype="bf16")
+    ob = tb(T(prev), T(cur), T(cmp), T(bw), T(fw)).clone()
+    np.random.seed(3)
+    tf = temporal.TemporalRefiner(dtype="fp32")
+    of = tf(T(prev), T(cur), T(cmp), T(bw), T(fw))
+    err = float((ob - of).abs().max())
+    print("config 3 bf16 vs fp32 softmax max-abs diff %.2e" % err)
+    assert err < 5e-2
+    assert torch.equal(tb.warped, tf.warped)
+
+
+def test_temporal_index_error():
+    from vmatting import temporal
+    prev, cur, cmp, bw, fw, _ = _case(16, 20)
+    bw[3, 4, 1] = -40.0  # i0 = 3 - 40 < -h: the reference's IndexError (flow.py:46)
+    tp = temporal.TemporalRefiner(dtype="fp32")
+    with pytest.raises(IndexError):
+        tp(T(prev), T(cur), T(cmp), T(bw), T(fw))

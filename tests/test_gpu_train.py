@@ -148,7 +148,10 @@ def test_bn_backward(mask):
     assert scaled_err(H(s), dy.astype(np.float64).sum(axis=(0, 1, 2))) <= 1e-5
 
 
-@pytest.mark.parametrize("ih,iw,oh,ow", [(5, 7, 10, 14), (3, 4, 5, 7), (17, 30, 34, 60), (8, 8, 8, 8)])
+@pytest.mark.parametrize("ih,iw,oh,ow", [(5, 7, 10, 14), (3, 4, 5, 7), (17, 30, 34, 60), (8, 8, 8, 8),
+                                         # near the launcher's limits (oh <= 4*ih) and the 1080p level sizes
+                                         (3, 5, 12, 20), (7, 9, 25, 31), (68, 120, 135, 240),
+                                         (135, 240, 270, 480), (4, 3, 13, 11), (5, 6, 19, 23)])
 def test_resize_backward(ih, iw, oh, ow):
     from vmatting import ops
     rs = np.random.RandomState(ih)
@@ -304,3 +307,101 @@ def test_train_step_bf16_runs():
     assert np.all(np.isfinite(losses)) and np.all(np.isfinite(H(trn.grad)))
     terms, _, grads = tr.train_step_grads(cmp, bg, warped, gt, fg, synthetic_vgg16(0), params)
     assert abs(losses[0] - terms[0]) <= 0.05 * terms[0]
+
+
+def test_train_step_bf16_gradients():
+    """The bf16 path (bf16 pre-BN buffers, padded narrow convs) against the f64 autograd restatement.
+    Bound: relative L2 <= 5e-2 per gradient tensor (bf16 forward activations; the f32 path meets 2e-3)."""
+    from vmatting.train import VideoTrainer
+    from vmatting.weights import synthetic_vgg16
+    params = om.unet_simple_params(np.random.RandomState(1))
+    cmp, bg, warped, gt, fg = _batch(2, 64, 80)
+    vgg = synthetic_vgg16(0)
+    trn = VideoTrainer(vgg, "bf16", DEV, params=params)
+    trn.forward(cmp, bg, warped)
+    from vmatting import ops
+    d = lambda a: T(a)  # noqa: E731
+    trn.grad.zero_()
+    trn.backward(d(gt), d(fg), d(bg), d(cmp))
+    torch.cuda.synchronize()
+    _, _, grads = tr.train_step_grads(cmp, bg, warped, gt, fg, vgg, params)
+    bad, worst = [], 0.0
+    for (scope, kind), g_ref in grads.items():
+        if kind == "b":  # exactly zero in real arithmetic (BN removes conv biases)
+            continue
+        g = H(trn.G[scope, kind])
+        l2 = np.linalg.norm(g - g_ref) / max(np.linalg.norm(g_ref), 1e-30)
+        worst = max(worst, l2)
+        if not l2 <= 5e-2:
+            bad.append((scope, kind, round(float(l2), 4)))
+    print("bf16 step: worst relative L2 gradient error %.2e" % worst)
+    assert not bad, bad
+
+
+def test_train_bf16_padded_convs_track_the_filters():
+    """After an Adam step, each zero-padded narrow conv (select2_*, select1_*, output) computes the updated filter
+    on its first cout channels and exactly zero in the padded ones."""
+    from vmatting import ops
+    from vmatting.train import VideoTrainer
+    from vmatting.weights import synthetic_vgg16
+    params = om.unet_simple_params(np.random.RandomState(1))
+    cmp, bg, warped, gt, fg = _batch(2, 32, 48)
+    trn = VideoTrainer(synthetic_vgg16(0), "bf16", DEV, params=params)
+    trn.step(cmp, bg, warped, gt, fg)
+    assert trn._padconv, "the bf16 trainer pads the narrow convs"
+    for scope, (pc, wp, bp, cout) in trn._padconv.items():
+        x = torch.randn((1, 9, 13, pc.cin), device=DEV).to(torch.bfloat16)
+        y = ops.conv3x3(x, pc, "none", affine=False, out_dtype=torch.float32)
+        fresh = ops.PackedConv(trn.P[scope, "w"].clone(), trn.P[scope, "b"].clone(), "fp32", DEV)
+        want = ops.conv3x3(x.float(), fresh, "none", affine=False)
+        assert torch.count_nonzero(y[..., cout:]) == 0, scope
+        err = (y[..., :cout] - want).abs().max().item() / max(want.abs().max().item(), 1e-30)
+        assert err <= 2e-2, (scope, err)
+
+
+def _ddp_init_worker(rank, world, port, q):
+    import os
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    try:
+        from vmatting import parallel
+        from vmatting.train import VideoTrainer
+        from vmatting.weights import synthetic_vgg16
+        parallel.init_from_env(backend="gloo")  # gloo moves the cuda tensors; both ranks share cuda:0
+        torch.cuda.set_device(0)
+        np.random.seed(100 + rank)  # different init_conv draws per rank: the trainer must replicate rank 0's
+        trn = VideoTrainer(synthetic_vgg16(0), "fp32", "cuda:0")
+        cmp, bg, warped, gt, fg = _batch(1, 32, 32, seed=11 + rank)  # different data per rank
+        trn.step(cmp, bg, warped, gt, fg)
+        torch.cuda.synchronize()
+        flat = trn.flat.cpu()
+        pk = trn.model.convs["conv2"].packed.cpu()
+        both = [torch.empty_like(flat) for _ in range(world)]
+        dist.all_gather(both, flat)
+        pks = [torch.empty_like(pk) for _ in range(world)]
+        dist.all_gather(pks, pk)
+        q.put((rank, bool(torch.equal(both[0], both[1])), bool(torch.equal(pks[0], pks[1]))))
+    except Exception as e:  # report instead of hanging the parent
+        q.put((rank, False, repr(e)))
+    finally:
+        import torch.distributed as dist
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def test_ddp_replicas_start_identical_and_stay_identical():
+    """with world > 1 the trainer broadcasts rank 0's variables before the first step, so after one
+    DDP step (averaged gradients) the replicas hold bit-identical parameters and packed filters."""
+    import multiprocessing as mp
+    import os
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29700 + (os.getpid() % 500)
+    procs = [ctx.Process(target=_ddp_init_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=100) for _ in procs]
+    for p in procs:
+        p.join(30)
+    assert sorted(r[0] for r in res) == [0, 1]
+    assert all(r[1] is True and r[2] is True for r in res), res

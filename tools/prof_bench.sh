@@ -1,29 +1,40 @@
 #!/bin/bash
 # rocprofv3 evidence for bench.py (run on the GPU box):  bash tools/prof_bench.sh <round-tag> [bench args]
-#   1. --kernel-trace --stats of a short bench run      -> profiles/<tag>_kernel_stats.csv
-#   2. --pmc FETCH_SIZE, 3. --pmc WRITE_SIZE (own passes) -> profiles/<tag>_traffic.json
-#   4. the bench itself (reads the traffic file)         -> gpurun_out/<tag>_bench.json
+#   1. --kernel-trace --stats of the FORWARD ONLY (the headline loop + its roofline pass)  -> profiles/<tag>_kernel_stats.csv
+#   2. --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE (own pass)          -> profiles/<tag>_mfma.json
+#   3. --pmc FETCH_SIZE, 4. --pmc WRITE_SIZE (own passes)                                 -> profiles/<tag>_traffic.json
+#   5. --kernel-trace --stats of the config-3 record (temporal)                           -> profiles/<tag>_temporal_kernel_stats.csv
+#   6. the full bench (reads the profiles of 2-4)                                         -> gpurun_out/<tag>_bench.json
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 REPO=$(pwd)
 TAG=$1; shift
 export TMPDIR=/tmp
 OUT=$REPO/gpurun_out/prof_$TAG
 mkdir -p "$OUT" "$REPO/profiles"
+FWD="--no-cpu-baseline --no-train --no-loader --no-augment --no-temporal --no-fp32 --video-frames 0"
 run() {  # run <limit> <log> cmd...
   local lim=$1 log=$2; shift 2
   (cd /tmp && timeout -k 10 "$lim" "$@" > "$OUT/$log" 2>&1)
   local rc=$?
-  echo "[$log] rc=$rc"; tail -n 4 "$OUT/$log"
+  echo "[$log] rc=$rc"; tail -n 3 "$OUT/$log"
   [ $rc -eq 0 ] || exit $rc
 }
-run 400 stats.log rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/stats" -o run \
-    -- python3 "$REPO/bench.py" --steps 10 --warmup 3 --no-cpu-baseline --no-train "$@"
+run 300 stats.log rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/stats" -o run \
+    -- python3 "$REPO/bench.py" --steps 50 --warmup 5 $FWD "$@"
 cp "$(find "$OUT/stats" -name '*kernel_stats.csv' | head -n 1)" "$REPO/profiles/${TAG}_kernel_stats.csv"
-run 400 fetch.log rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$OUT/fetch" -o run \
-    -- python3 "$REPO/bench.py" --steps 2 --warmup 1 --no-cpu-baseline --no-profile --no-loader --no-augment --no-train --video-frames 0 "$@"
-run 400 write.log rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/write" -o run \
-    -- python3 "$REPO/bench.py" --steps 2 --warmup 1 --no-cpu-baseline --no-profile --no-loader --no-augment --no-train --video-frames 0 "$@"
+tail -n 1 "$OUT/stats.log" > "$REPO/profiles/${TAG}_stats_bench.json"
+run 300 mfma.log timeout -s KILL 240 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace \
+    --output-format csv -d "$OUT/mfma" -o run -- python3 "$REPO/bench.py" --steps 3 --warmup 1 --no-profile $FWD "$@"
+python3 "$REPO/tools/mfma.py" --pmc "$OUT/mfma" --out "$REPO/profiles/${TAG}_mfma.json"
+run 300 fetch.log timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$OUT/fetch" -o run \
+    -- python3 "$REPO/bench.py" --steps 2 --warmup 1 --no-profile $FWD "$@"
+run 300 write.log timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/write" -o run \
+    -- python3 "$REPO/bench.py" --steps 2 --warmup 1 --no-profile $FWD "$@"
 python3 "$REPO/tools/traffic.py" --fetch "$OUT/fetch" --write "$OUT/write" --out "$REPO/profiles/${TAG}_traffic.json" --forwards 4  # capture warm-up + 1 warmup + 2 steps
-cp "$REPO/profiles/${TAG}_traffic.json" "$REPO/profiles/${TAG}_kernel_stats.csv" "$REPO/gpurun_out/"
+run 300 temporal.log rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/temporal" -o run \
+    -- python3 "$REPO/bench.py" --steps 2 --warmup 1 --no-profile --no-cpu-baseline --no-train --no-loader --no-augment --no-fp32 --video-frames 0 "$@"
+cp "$(find "$OUT/temporal" -name '*kernel_stats.csv' | head -n 1)" "$REPO/profiles/${TAG}_temporal_kernel_stats.csv"
+cp "$REPO"/profiles/${TAG}_* "$REPO/gpurun_out/"
 run 600 bench.log python3 "$REPO/bench.py" --layers "$@"
 tail -n 1 "$OUT/bench.log" > "$REPO/gpurun_out/${TAG}_bench.json"
+grep -E "conv #|launches" "$OUT/bench.log" > "$REPO/gpurun_out/${TAG}_bench_layers.log" || true

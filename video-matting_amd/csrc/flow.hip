@@ -118,6 +118,62 @@ __global__ void fb_consistency_kernel(const float* __restrict__ bw, const float*
   }
 }
 
+// ---------------------------------------------------------------- config 3: warp + occlusion + refine input
+// One pass per pixel of the two-frame chain flow.py's demo runs (flow.py:69-77): alpha_w = warp_img(prev, flow_b)
+// (the remap_f32 mode-0 arithmetic above), correct_alpha(flow_b, flow_f, alpha_w) (fb_consistency above: one
+// gather of flow_f at the backward target), and the RefineNet input row [cmp B,G,R, alpha_t, alpha_w, 0, 0, 0]
+// (refine.py:27, Cin = 5 padded to 8, the concat of SURVEY.md 8(a) a14) written as one 16- or 32-byte NHWC pixel.
+// Every value is bit-identical to the separate kernels; the IndexError flag is raised as in fb_check (the caller
+// raises before using the output).
+template <typename T, int PROMOTE>
+__global__ __launch_bounds__(256) void temporal_input_kernel(const float* __restrict__ prev,
+                                                             const float* __restrict__ bw,
+                                                             const float* __restrict__ fw,
+                                                             const float* __restrict__ cmp,
+                                                             const float* __restrict__ cur, int h, int w,
+                                                             double thresh, T* __restrict__ out,
+                                                             float* __restrict__ warped, int* err) {
+  const long total = (long)h * w;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int y = (int)(i / w), x = (int)(i - (long)y * w);
+    const float2 fl = reinterpret_cast<const float2*>(bw)[i];
+    // warp_img: cv2.remap 1/32-pixel fixed point (remap_f32_kernel, mode 0)
+    const int X = (int)rintf(((float)x + fl.x) * 32.f);
+    const int Y = (int)rintf(((float)y + fl.y) * 32.f);
+    const int x0 = X >> 5, y0 = Y >> 5;
+    const float fx = (float)(X & 31) * (1.f / 32.f), fy = (float)(Y & 31) * (1.f / 32.f);
+    auto tap = [&](int yy, int xx) -> float {
+      return ((unsigned)yy < (unsigned)h && (unsigned)xx < (unsigned)w) ? prev[(long)yy * w + xx] : 0.f;
+    };
+    const float w00 = (1.f - fy) * (1.f - fx), w01 = (1.f - fy) * fx, w10 = fy * (1.f - fx), w11 = fy * fx;
+    float a = tap(y0, x0) * w00;
+    a += tap(y0, x0 + 1) * w01;
+    a += tap(y0 + 1, x0) * w10;
+    a += tap(y0 + 1, x0 + 1) * w11;
+    // correct_alpha (fb_consistency_kernel)
+    const long j0 = step_index<PROMOTE>(fl.x, x, w);
+    const long i0 = step_index<PROMOTE>(fl.y, y, h);
+    if (j0 < -(long)w || i0 < -(long)h) {
+      atomicOr(err, 1);
+    } else {
+      const long ji = j0 < 0 ? j0 + w : j0, ii = i0 < 0 ? i0 + h : i0;
+      const float2 f = reinterpret_cast<const float2*>(fw)[ii * w + ji];
+      const long j1 = step_index<PROMOTE>(f.x, j0, w);
+      const long i1 = step_index<PROMOTE>(f.y, i0, h);
+      const double di = (double)(i1 - y), dj = (double)(j1 - x);
+      if (sqrt(di * di + dj * dj) > thresh) a = 0.f;
+    }
+    if (warped) warped[i] = a;
+    float v[8] = {cmp[i * 3], cmp[i * 3 + 1], cmp[i * 3 + 2], cur[i], a, 0.f, 0.f, 0.f};
+    if constexpr (sizeof(T) == 2) {
+      reinterpret_cast<uint4*>(out)[i] = Chunk<T>::pack(v);
+    } else {
+      reinterpret_cast<float4*>(out)[2 * i] = make_float4(v[0], v[1], v[2], v[3]);
+      reinterpret_cast<float4*>(out)[2 * i + 1] = make_float4(v[4], 0.f, 0.f, 0.f);
+    }
+  }
+}
+
 // ---------------------------------------------------------------- training loss (train.py:14-28, 42-47)
 constexpr int LOSS_NBLK = 512;
 
@@ -212,6 +268,29 @@ extern "C" int vm_fb_consistency(const float* backward, const float* forward, in
                        (double)thresh, err_flag);
   }
   return check_launch("fb_consistency");
+}
+
+extern "C" int vm_temporal_refine_input(const float* prev_alpha, const float* backward, const float* forward,
+                                        const float* cmp, const float* alpha, int h, int w, float thresh, int promote,
+                                        void* out, int out_dtype, float* warped, int* err_flag, void* stream) {
+  if (!prev_alpha || !backward || !forward || !cmp || !alpha || !out || !err_flag || h <= 0 || w <= 0 ||
+      (promote != 0 && promote != 1) || (out_dtype != VM_F32 && out_dtype != VM_BF16))
+    return fail(VM_EINVAL, "temporal_refine_input: bad argument");
+  if ((reinterpret_cast<uintptr_t>(backward) | reinterpret_cast<uintptr_t>(forward)) % 8 ||
+      reinterpret_cast<uintptr_t>(out) % 16)
+    return fail(VM_EUNSUPPORTED, "temporal_refine_input: flows 8-byte and out 16-byte aligned");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int grid = grid_for((long)h * w, 256);
+#define VM_TEMPORAL(TT, PR)                                                                                           \
+  hipLaunchKernelGGL((temporal_input_kernel<TT, PR>), dim3(grid), dim3(256), 0, st, prev_alpha, backward, forward, cmp, \
+                     alpha, h, w, (double)thresh, reinterpret_cast<TT*>(out), warped, err_flag)
+  if (out_dtype == VM_BF16) {
+    if (promote == 0) VM_TEMPORAL(uint16_t, 0); else VM_TEMPORAL(uint16_t, 1);
+  } else {
+    if (promote == 0) VM_TEMPORAL(float, 0); else VM_TEMPORAL(float, 1);
+  }
+#undef VM_TEMPORAL
+  return check_launch("temporal_refine_input");
 }
 
 extern "C" size_t vm_loss_workspace_bytes(long pixels) {

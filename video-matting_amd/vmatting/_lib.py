@@ -87,6 +87,8 @@ SIGNATURES = [
                                       c_void_p]),
     ("vm_remap_bilinear_u8", c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p]),
     ("vm_fb_consistency", c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_float, c_int, c_void_p, c_void_p]),
+    ("vm_temporal_refine_input", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_float,
+                                         c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
     ("vm_loss_workspace_bytes", c_size_t, [c_long]),
     ("vm_matting_loss", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_void_p, c_void_p,
                                 c_void_p]),

@@ -28,6 +28,13 @@ def init_from_env(backend=None):
     return rank, world, local
 
 
+def world_size():
+    """Number of ranks of the default process group (1 when torch.distributed is not initialised)."""
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_world_size()
+    return 1
+
+
 def shard_range(n_frames, rank, world):
     """Contiguous block of frames for ``rank``: [start, stop)."""
     start = (n_frames * rank) // world

@@ -40,9 +40,22 @@ class RefineNet:
         cpad = (c + 7) // 8 * 8
         xin = torch.empty((n, h, w, cpad), dtype=self.dtype, device=self.device)
         ops.convert(x, xin)
-        self._x = xin[..., :c]
+        return self.forward_prepared(xin[..., :c])
+
+    def prepare(self, cin):
+        """Draw (refine.py:28-31 order) and pack the four filters for a ``cin``-channel input without a frame."""
+        if self.params is None:
+            self.params = {k: init_conv(cin, 64) for k in ("conv1", "conv2", "conv3", "conv4")}
+        if self.convs is None:
+            self.convs = {k: ops.PackedConv(w, b, self.dtype, self.device) for k, (w, b) in self.params.items()}
+        return self
+
+    def forward_prepared(self, x, out=None):
+        """Forward on an input already in the compute dtype with channels padded to 8 (a channel view such as
+        the one vm_temporal_refine_input writes); ``out`` optionally receives the f32 [N,H,W,64] softmax."""
+        self._x = x
         self._lazy = {}
-        self.conv4 = ops.conv3x3(self._x, self.convs["conv4"], "softmax", out_dtype=torch.float32)
+        self.conv4 = ops.conv3x3(x, self.convs["conv4"], "softmax", out=out, out_dtype=torch.float32)
         self.output = self.conv4
         return self.output
 

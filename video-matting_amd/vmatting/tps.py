@@ -1,3 +1,9 @@
+# The host-side TPS solve below (_U, _interpoint_distances, _make_L_matrix, _coefficients and the
+# deform_grid draw sequence) follows the reference's tps.py, which is
+#   Copyright 2007 Zachary Pincus, part of CellTool,
+#   free software under version 2 of the GNU General Public License (tps.py:1-6).
+# Those ~30 lines stay close to the original so that numpy's pinv solve and np.random draw order are
+# reproduced bit for bit; they are distributed under the same GPLv2 terms as the original.
 """tps.py (thin-plate-spline warp, Bookstein) on gfx950 kernels — SURVEY.md §8(f) rank 3.
 
 Same names and call shapes as the reference's tps.py:14-149.  The host keeps what the reference does once per

@@ -95,6 +95,12 @@ class VideoTrainer:
             self.P[scope, "gamma"].copy_(bnl.gamma)
             self.P[scope, "beta"].copy_(bnl.beta)
             bnl.gamma, bnl.beta = self.P[scope, "gamma"], self.P[scope, "beta"]
+        # DDP: every replica starts from rank 0's variables.  init_conv draws from each process's global numpy RNG
+        # (unet_simple.py:10-16), so without this the ranks would apply the averaged gradient to different models
+        if parallel.world_size() > 1:
+            parallel.broadcast_tensors([self.flat], src=0)
+            for pc in self.model.convs.values():
+                pc.repack()
         # data-gradient filters: flipped / transposed f32 copies, packed for the forward conv kernels
         self.dconv, self._wflip = {}, {}
         for scope in DGRAD:
@@ -264,7 +270,8 @@ class VideoTrainer:
         self._sync_padded()
 
     def step(self, cmp, bg, warped, gt, raw_fg):
-        """One training iteration; returns the device tensor [loss, alpha_loss, compositional_loss] (pre-update)."""
+        """One training iteration; returns a new device tensor [loss, alpha_loss, compositional_loss] (pre-update),
+        not aliased to the trainer's buffers."""
         self.forward(cmp, bg, warped)
         dev = lambda t: (t if isinstance(t, torch.Tensor) else torch.from_numpy(  # noqa: E731
             np.ascontiguousarray(t, np.float32))).to(self.device, torch.float32).contiguous()
@@ -275,7 +282,7 @@ class VideoTrainer:
         self.grad.zero_()
         self.backward(gt, raw_fg, bg_d, cmp_d)
         self.apply_gradients()
-        return tb["loss"]
+        return tb["loss"].clone()
 
     def params_numpy(self):
         """{scope: (w, b|None)} and {scope: (gamma, beta)} on the host (checkpointing / inference hand-off)."""

@@ -39,6 +39,21 @@ def _levels(h, w):
     return lv
 
 
+class _LazyBuffers(dict):
+    """Buffer dict whose listed entries are allocated on first access."""
+
+    def __init__(self, lazy, make):
+        super().__init__()
+        self._lazy, self._make = lazy, make
+
+    def __missing__(self, key):
+        if key not in self._lazy:
+            raise KeyError(key)
+        t = self._make(*self._lazy[key])
+        self[key] = t
+        return t
+
+
 class UNet:
     """Base class (unet.py:20-83)."""
 
@@ -56,6 +71,7 @@ class UNet:
         self.convs = None        # name -> ops.PackedConv
         self._ws = None
         self._ws_key = None
+        self._ws_all = {}
         self._c11 = None
         self._x = None
         self._in8_valid = False
@@ -106,20 +122,29 @@ class UNet:
 
     # ------------------------------------------------------------------ buffers
     def _buffers(self, n, h, w):
+        """Activation buffers for an [n,h,w] batch.  Every shape's set is kept (a HIP graph captured on one set
+        keeps pointing at it, e.g. video.py's full chunks and its shorter last chunk)."""
         key = (n, h, w)
         if self._ws_key == key:
+            return self._ws
+        if key in self._ws_all:
+            self._ws, self._ws_key = self._ws_all[key], key
             return self._ws
         T, dev = self.dtype, self.device
         L = _levels(h, w)
         E = lambda lv, c, dt=T: torch.empty((n, L[lv][0], L[lv][1], c), dtype=dt, device=dev)  # noqa: E731
-        ws = dict(
-            in8=E(0, 8), c11=E(0, 64), cat1=E(0, 128), r4=E(0, 128),
-            p1=E(1, 64), c21=E(1, 128), cat2=E(1, 256), r3=E(1, 256), c23=E(1, 128),
-            p2=E(2, 128), c31=E(2, 256), c32=E(2, 256), cat3=E(2, 512), r2=E(2, 512), c34=E(2, 256),
-            p3=E(3, 256), c41=E(3, 512), c42=E(3, 512), cat4=E(3, 1024), r1=E(3, 512), c44=E(3, 512),
+        # in8 / c11 (unfused first pair, the lazily evaluated .conv1_1) and the resize targets r1..r4 (unfolded
+        # upconvs) are allocated on first use only: the bf16 fused/folded forward never touches in8, c11, r3, r4
+        ws = _LazyBuffers(dict(in8=(0, 8), c11=(0, 64), r4=(0, 128), r3=(1, 256), r2=(2, 512), r1=(3, 512)), E)
+        ws.update(
+            cat1=E(0, 128),
+            p1=E(1, 64), c21=E(1, 128), cat2=E(1, 256), c23=E(1, 128),
+            p2=E(2, 128), c31=E(2, 256), c32=E(2, 256), cat3=E(2, 512), c34=E(2, 256),
+            p3=E(3, 256), c41=E(3, 512), c42=E(3, 512), cat4=E(3, 1024), c44=E(3, 512),
             p4=E(4, 512), c51=E(4, 512), c52=E(4, 512),
             logits=E(0, 1, torch.float32), out=E(0, 1, torch.float32))
         self._ws, self._ws_key = ws, key
+        self._ws_all[key] = ws
         return ws
 
     # ------------------------------------------------------------------ graph
@@ -139,8 +164,10 @@ class UNet:
                                                                             tuple(x.shape)))
         return x
 
-    def forward(self, input):
-        """Evaluate the built network on new frames; returns .output (f32 [N,H,W,1])."""
+    def forward(self, input, out=None):
+        """Evaluate the built network on new frames; returns .output (f32 [N,H,W,1]).  ``out`` (contiguous f32
+        [N,H,W,1] on the device) receives the alpha instead of the model's own buffer (video.py writes each chunk
+        of frames straight into its slice of the result)."""
         x = self._as_input(input) if not (isinstance(input, torch.Tensor) and input.is_cuda and
                                           input.dtype == torch.float32) else input
         if self.convs is None:
@@ -182,15 +209,19 @@ class UNet:
         up(b["c34"], "upconv_3", 1, b["cat2"][..., :128], "r3")
         ops.conv3x3(b["cat2"], C["conv2_3"], "relu", out=b["c23"])
         up(b["c23"], "upconv_4", 0, b["cat1"][..., :64], "r4")
-        ops.conv_head(b["cat1"], C["conv1_5"], "none", out=b["logits"], alpha=b["out"])  # conv1_5 + sigmoid
+        alpha = b["out"] if out is None else out
+        ops.conv_head(b["cat1"], C["conv1_5"], "none", out=b["logits"], alpha=alpha)  # conv1_5 + sigmoid
         self._publish(b)
+        self.output = alpha
         return self.output
 
-    def capture(self, x):
+    def capture(self, x, static=False, out=None):
         """Record one forward over frames shaped like ``x`` into a HIP graph (torch.cuda.CUDAGraph over the same
         C-ABI launches) and return a GraphedForward: replaying it re-runs the whole forward with one host call, so
-        throughput no longer depends on the host's per-launch cost.  New frames are copied into ``.input``."""
-        return GraphedForward(self, x)
+        throughput no longer depends on the host's per-launch cost.  New frames are copied into ``.input``;
+        ``static=True`` records ``x`` itself as the input (no copy; x must stay allocated and in place) and ``out``
+        the alpha destination."""
+        return GraphedForward(self, x, static, out)
 
     @property
     def conv1_1(self):
@@ -275,20 +306,23 @@ class GraphedForward:
     in first.  The model's weights and activation buffers are the ones captured: do not change the model's shape or
     weights afterwards (capture again instead)."""
 
-    def __init__(self, model, x):
+    def __init__(self, model, x, static=False, out=None):
         x = model._as_input(x)
         self.model = model
-        self.input = torch.empty_like(x)
-        self.input.copy_(x)
+        if static:
+            self.input = x
+        else:
+            self.input = torch.empty_like(x)
+            self.input.copy_(x)
         side = torch.cuda.Stream(device=self.input.device)
         side.wait_stream(torch.cuda.current_stream(self.input.device))
         with torch.cuda.stream(side):  # lazily built kernels/weights (folded filters, attributes) before capture
-            model.forward(self.input)
+            model.forward(self.input, out)
         torch.cuda.current_stream(self.input.device).wait_stream(side)
         torch.cuda.synchronize(self.input.device)
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
-            self.output = model.forward(self.input)
+            self.output = model.forward(self.input, out)
 
     def replay(self):
         self.graph.replay()

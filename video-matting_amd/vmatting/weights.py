@@ -38,15 +38,52 @@ def synthetic_vgg16(seed=0, scale=1.0):
     return out
 
 
-def load_vgg16(path_or_dict):
-    """Accept a data_dict, or a path to a vgg16.npy (a pickled dict, like the reference loads)."""
+def save_vgg16_npz(data_dict, path):
+    """Write a data_dict as a plain-array .npz ("<layer>/W", "<layer>/b"): no pickle, loadable with
+    allow_pickle=False by load_vgg16."""
+    arrays = {}
+    for name, (w, b) in data_dict.items():
+        arrays[name + "/W"] = np.asarray(w, np.float32)
+        arrays[name + "/b"] = np.asarray(b, np.float32)
+    np.savez(path, **arrays)
+
+
+def _load_npz(path):
+    out = {}
+    with np.load(path, allow_pickle=False) as z:
+        for key in z.files:
+            name, kind = key.rsplit("/", 1)
+            ent = out.setdefault(name, [None, None])
+            ent[0 if kind == "W" else 1] = z[key]
+    bad = [k for k, (w, b) in out.items() if w is None or b is None]
+    if bad:
+        raise ValueError("%s: layers without both W and b: %s" % (path, bad))
+    return out
+
+
+def load_vgg16(path_or_dict, allow_pickle=None):
+    """Accept a data_dict, a weights-only ``.npz`` (save_vgg16_npz / tools/vgg_npy_to_npz.py), or a pickled
+    ``vgg16.npy`` as unet.py:29 / unet_simple.py:54 load it.
+
+    A pickled .npy can execute code when loaded, so it is refused unless the caller opts in with
+    ``allow_pickle=True`` or VMATTING_ALLOW_PICKLE=1 (trusted files only).  With the default path, a
+    ``weights/vgg16.npz`` next to the reference's ``weights/vgg16.npy`` is preferred."""
     if isinstance(path_or_dict, dict):
         return path_or_dict
-    path = DEFAULT_VGG_PATH if path_or_dict is None else path_or_dict
+    path = DEFAULT_VGG_PATH if path_or_dict is None else os.fspath(path_or_dict)
+    if path.endswith(".npy") and os.path.exists(path[:-4] + ".npz"):
+        path = path[:-4] + ".npz"
     if not os.path.exists(path):
         raise FileNotFoundError("[Errno 2] No such file or directory: %r (pass a data_dict, e.g. "
-                                "vmatting.weights.synthetic_vgg16(0), or a real vgg16.npy)" % path)
-    # the user's own checkpoint file: the reference loads it the same way (unet.py:29)
+                                "vmatting.weights.synthetic_vgg16(0), or a vgg16 .npz / .npy)" % path)
+    if path.endswith(".npz"):
+        return _load_npz(path)
+    if allow_pickle is None:
+        allow_pickle = os.environ.get("VMATTING_ALLOW_PICKLE", "") == "1"
+    if not allow_pickle:
+        raise ValueError("%s is a pickled data_dict, which can run code when loaded.  Convert it once with "
+                         "tools/vgg_npy_to_npz.py (weights-only .npz), or pass allow_pickle=True / set "
+                         "VMATTING_ALLOW_PICKLE=1 for a file you trust" % path)
     return np.load(path, encoding="latin1", allow_pickle=True).item()
 
 
