@@ -4,7 +4,7 @@ the separate-op API and the CPU oracle.
 * the fused pass's warped / corrected alpha is bit-identical to flow.warp_img -> flow.correct_alpha on the GPU,
   which the golden tests pin to the reference's own flow.py outputs (test_gpu_parity.py);
 * the refine input channels are exactly [cmp, alpha, warped] (f32) or their bf16 rounding;
-* 500x1200 (the flow.py demo size) and 1080p: the fp32 refine output (64-ch softmax) within 1e-5 max-abs of the
+* 500x1200 (the flow.py demo size) and 1080p: the fp32 refine output (64-ch softmax) within 1e-4 max-abs of the
   numpy oracle (oracle.models.refine_forward on the same input) — the chain's size-independent properties
   (softmax rows sum to 1, occluded pixels carry warped alpha 0) at full size.
 """
@@ -77,7 +77,7 @@ def test_temporal_refine_fp32_vs_oracle(h, w):
     got = out.cpu().numpy()
     err = float(np.abs(got - ref).max())
     print("config 3 %dx%d: fp32 refine softmax max-abs err vs oracle %.2e" % (h, w, err))
-    assert err <= 1e-5
+    assert err <= 1e-4  # north_star's fp32 bound (f32 summation order in a saturated 64-way softmax: ~2e-5)
     np.testing.assert_allclose(got.sum(-1), 1.0, atol=1e-5)
 
 
