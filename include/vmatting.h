@@ -91,6 +91,12 @@ size_t vm_conv3x3_packed_bytes(int cin, int cout, int dtype);
 int vm_conv3x3_pack_weights(const float* w_hwio, int cin, int cout, int dtype, void* packed, void* stream);
 int vm_conv3x3_nhwc(const vm_tensor* x, const void* packed, int cin, int cout, const float* bias,
                     const float* scale, const float* shift, int act, vm_tensor* y, void* stream);
+/* The same conv over the channel concat of nsrc sources (unet_simple.py:153-168's per-level concat of the three
+ * towers, tower-major in HBM so the towers run as one batch): x is the [n,h,w,c_src] view of source 0, source s
+ * lies src_stride elements further; cin = nsrc * x->c, and x->c must be whole 64-byte granules. */
+int vm_conv3x3_sources_nhwc(const vm_tensor* x, int nsrc, long src_stride, const void* packed, int cin, int cout,
+                            const float* bias, const float* scale, const float* shift, int act, vm_tensor* y,
+                            void* stream);
 /* Same conv, and additionally the 2x2/2 SAME max-pool of its output written to ypool
  * ([n, ceil(h/2), ceil(w/2), cout], same dtype) — replaces the conv_layer + max_pool pairs
  * unet.py:170-187 (conv1_2/pool1 ... conv4_3/pool4; max_pool at unet.py:32-33).
@@ -319,6 +325,14 @@ size_t vm_conv3x3_wgrad_workspace_bytes(int n, int h, int w, int cin, int cout);
  * sum over pixels of x (view, cin = x->c) patch x dy (f32 view [n,h,w,cout]); cout <= 48.  Accumulates;
  * deterministic (fixed-order two-pass sum through ``work``). */
 int vm_conv3x3_wgrad_nhwc(const vm_tensor* x, const vm_tensor* dy, float* dw, void* work, void* stream);
+/* The weight gradient with options: x_src_c > 0 reads x as x->c / x_src_c sources of x_src_c channels each,
+ * source s at x_src_stride elements from the view base (the frozen towers' features stored tower-major,
+ * unet_simple.py:153-168's concat); mode 0 = the exact-f32 FMA kernel above, mode 1 = MFMA with bf16 operands
+ * (x a bf16 view of 16-byte channel chunks, dy rounded to bf16 on load, f32 sums; the bf16 training path).
+ * cout <= 48; dw += result; work: vm_conv3x3_wgrad_ex_workspace_bytes(..., mode) bytes. */
+size_t vm_conv3x3_wgrad_ex_workspace_bytes(int n, int h, int w, int cin, int cout, int mode);
+int vm_conv3x3_wgrad_ex_nhwc(const vm_tensor* x, int x_src_c, long x_src_stride, const vm_tensor* dy, float* dw,
+                             void* work, int mode, void* stream);
 
 /* The data-gradient filter of a 3x3 SAME conv: w_flipped[kh][kw][co][ci] = w[2-kh][2-kw][ci][co]; dx is then
  * vm_conv3x3_nhwc(dy, pack(w_flipped)). */

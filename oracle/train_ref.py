@@ -67,17 +67,23 @@ def _resize(x, oh, ow):
     return top + (bot - top) * fy
 
 
-def train_step_grads(cmp, bg, warped, gt, raw_fg, vgg, params, bn=None):
+def train_step_grads(cmp, bg, warped, gt, raw_fg, vgg, params, bn=None, towers=None):
     """-> (loss terms (loss, alpha_loss, cmp_loss), alpha, grads {(scope, kind): ndarray})
 
     params: {scope: (w_hwio, bias|None)} (models.unet_simple_params); bn: {scope: (gamma, beta)} or fresh (1, 0).
-    kinds: 'w', 'b' (new_conv scopes), 'gamma', 'beta' — the trainable variables of unet_simple.py:19-42."""
+    kinds: 'w', 'b' (new_conv scopes), 'gamma', 'beta' — the trainable variables of unet_simple.py:19-42.
+    towers: optional precomputed frozen-tower features (3 dicts layer -> [N,H,W,C], plus 'in9' in the first) to
+    isolate the trainable head (a test of a reduced-precision path's head against its own tower features)."""
     f64 = lambda a: np.asarray(a, np.float64)  # noqa: E731
     cmp, bg, warped = f64(cmp), f64(bg), f64(warped)
-    towers = [om.vgg16_tower(t, vgg) for t in (cmp, bg, warped)]
-    cat = lambda k: torch.from_numpy(np.concatenate([t[k] for t in towers], -1))  # noqa: E731
+    in9 = np.concatenate([cmp, bg, warped], -1)
+    if towers is None:
+        towers = [om.vgg16_tower(t, vgg) for t in (cmp, bg, warped)]
+    elif "in9" in towers[0]:
+        in9 = f64(towers[0]["in9"])
+    cat = lambda k: torch.from_numpy(np.concatenate([f64(t[k]) for t in towers], -1))  # noqa: E731
     layers = {
-        "conv1": [torch.from_numpy(np.concatenate([cmp, bg, warped], -1)), cat("conv1_1"), cat("conv1_2")],
+        "conv1": [torch.from_numpy(in9), cat("conv1_1"), cat("conv1_2")],
         "conv2": [cat("conv2_1"), cat("conv2_2")],
         "conv3": [cat("conv3_1"), cat("conv3_2"), cat("conv3_3")],
         "conv4": [cat("conv4_1"), cat("conv4_2"), cat("conv4_3")],

@@ -309,9 +309,22 @@ def test_train_step_bf16_runs():
     assert abs(losses[0] - terms[0]) <= 0.05 * terms[0]
 
 
+def _gpu_towers(trn, n):
+    """The bf16 trainer's own frozen-tower features (tower-major buffers) as 3 per-tower dicts + its in9 input."""
+    b = trn.model._ws
+    towers = [{k[2:]: H(v[t * n:(t + 1) * n]) for k, v in b.items() if k.startswith("t_conv")} for t in range(3)]
+    towers[0]["in9"] = H(b["in9"][..., :9])
+    return towers
+
+
 def test_train_step_bf16_gradients():
-    """The bf16 path (bf16 pre-BN buffers, padded narrow convs) against the f64 autograd restatement.
-    Bound: relative L2 <= 5e-2 per gradient tensor (bf16 forward activations; the f32 path meets 2e-3)."""
+    """The bf16 path (bf16 activations, f32 pre-BN buffers, padded narrow convs, MFMA filter gradients with dy
+    rounded to bf16) against the f64 autograd restatement evaluated on the SAME bf16 tower features, so the
+    comparison isolates the trainable head.  BN with batch statistics over few pixels makes these gradients
+    ill-conditioned: the exact f64 gradients themselves move by several % when only the trainable filters are
+    perturbed by bf16-sized relative noise (2^-9).  Bound, self-calibrated: per tensor, relative L2 error <= 4x that
+    f64 sensitivity + 2e-2 (measured: <= 2.6x); the whole gradient vector's cosine with the reference >= 0.95
+    (measured 0.979)."""
     from vmatting.train import VideoTrainer
     from vmatting.weights import synthetic_vgg16
     params = om.unet_simple_params(np.random.RandomState(1))
@@ -319,23 +332,32 @@ def test_train_step_bf16_gradients():
     vgg = synthetic_vgg16(0)
     trn = VideoTrainer(vgg, "bf16", DEV, params=params)
     trn.forward(cmp, bg, warped)
-    from vmatting import ops
-    d = lambda a: T(a)  # noqa: E731
     trn.grad.zero_()
-    trn.backward(d(gt), d(fg), d(bg), d(cmp))
+    trn.backward(T(gt), T(fg), T(bg), T(cmp))
     torch.cuda.synchronize()
-    _, _, grads = tr.train_step_grads(cmp, bg, warped, gt, fg, vgg, params)
-    bad, worst = [], 0.0
+    towers = _gpu_towers(trn, 2)
+    _, _, grads = tr.train_step_grads(cmp, bg, warped, gt, fg, vgg, params, towers=towers)
+    rs = np.random.RandomState(7)
+    p2 = {k: (w * (1 + 2.0 ** -9 * rs.normal(size=w.shape)).astype(np.float32), b) for k, (w, b) in params.items()}
+    _, _, g2 = tr.train_step_grads(cmp, bg, warped, gt, fg, vgg, p2, towers=towers)
+    bad, got_all, ref_all, rows = [], [], [], []
     for (scope, kind), g_ref in grads.items():
         if kind == "b":  # exactly zero in real arithmetic (BN removes conv biases)
             continue
         g = H(trn.G[scope, kind])
-        l2 = np.linalg.norm(g - g_ref) / max(np.linalg.norm(g_ref), 1e-30)
-        worst = max(worst, l2)
-        if not l2 <= 5e-2:
-            bad.append((scope, kind, round(float(l2), 4)))
-    print("bf16 step: worst relative L2 gradient error %.2e" % worst)
+        nrm = max(np.linalg.norm(g_ref), 1e-30)
+        l2 = np.linalg.norm(g - g_ref) / nrm
+        sens = np.linalg.norm(g2[scope, kind] - g_ref) / nrm
+        got_all.append(g.ravel())
+        ref_all.append(g_ref.ravel())
+        rows.append("%s/%s %.3e (sens %.3e)" % (scope, kind, l2, sens))
+        if not l2 <= 4 * sens + 2e-2:
+            bad.append((scope, kind, round(float(l2), 4), round(float(sens), 4)))
+    a, b = np.concatenate(got_all), np.concatenate(ref_all)
+    cos = float(a @ b / (np.linalg.norm(a) * np.linalg.norm(b)))
+    print("bf16 step: gradient cosine %.4f\n  %s" % (cos, "\n  ".join(rows)))
     assert not bad, bad
+    assert cos >= 0.95
 
 
 def test_train_bf16_padded_convs_track_the_filters():
@@ -350,10 +372,13 @@ def test_train_bf16_padded_convs_track_the_filters():
     trn.step(cmp, bg, warped, gt, fg)
     assert trn._padconv, "the bf16 trainer pads the narrow convs"
     for scope, (pc, wp, bp, cout) in trn._padconv.items():
-        x = torch.randn((1, 9, 13, pc.cin), device=DEV).to(torch.bfloat16)
+        cpad = (pc.cin + 31) // 32 * 32
+        x = torch.randn((1, 9, 13, cpad), device=DEV).to(torch.bfloat16)[..., :pc.cin]
         y = ops.conv3x3(x, pc, "none", affine=False, out_dtype=torch.float32)
         fresh = ops.PackedConv(trn.P[scope, "w"].clone(), trn.P[scope, "b"].clone(), "fp32", DEV)
-        want = ops.conv3x3(x.float(), fresh, "none", affine=False)
+        xf = torch.zeros((1, 9, 13, cpad), device=DEV)
+        xf[..., :pc.cin] = x.float()
+        want = ops.conv3x3(xf[..., :pc.cin], fresh, "none", affine=False)
         assert torch.count_nonzero(y[..., cout:]) == 0, scope
         err = (y[..., :cout] - want).abs().max().item() / max(want.abs().max().item(), 1e-30)
         assert err <= 2e-2, (scope, err)
@@ -405,3 +430,78 @@ def test_ddp_replicas_start_identical_and_stay_identical():
         p.join(30)
     assert sorted(r[0] for r in res) == [0, 1]
     assert all(r[1] is True and r[2] is True for r in res), res
+
+
+# ----------------------------------------------------------------------------- MFMA weight gradient (bf16 path)
+
+def _bf16(a):
+    return torch.from_numpy(np.ascontiguousarray(a, np.float32)).to(torch.bfloat16).float().numpy()
+
+
+@pytest.mark.parametrize("cout", [1, 2, 4, 8, 16, 24, 32, 48])
+@pytest.mark.parametrize("cin,cs", [(9, 16), (30, 32), (64, 72), (192, 192), (70, 80)])
+def test_conv_wgrad_mfma(cin, cs, cout):
+    """vm_conv3x3_wgrad_bf16_nhwc: bf16 x and dy rounded to bf16, f32 sums — against float64 autograd on the same
+    bf16-rounded operands (so only the summation order differs): max-abs error <= 1e-4 of scale."""
+    from vmatting import ops
+    rs = np.random.RandomState(cin * 100 + cout)
+    n, h, w = 2, 13, 70
+    x = rs.normal(size=(n, h, w, cs)).astype(np.float32)
+    dy = rs.normal(size=(n, h, w, cout)).astype(np.float32)
+    xd = T(x, torch.bfloat16)
+    dw = torch.zeros((3, 3, cin, cout), dtype=torch.float32, device=DEV)
+    ops.conv_wgrad(xd[..., :cin], T(dy), dw, mfma=True)
+    wr = torch.zeros((3, 3, cin, cout), dtype=torch.float64, requires_grad=True)
+    xr = torch.from_numpy(H(xd[..., :cin]))
+    (tr._conv(xr, wr) * torch.from_numpy(_bf16(dy).astype(np.float64))).sum().backward()
+    assert scaled_err(H(dw), wr.grad.numpy()) <= 1e-4
+
+
+@pytest.mark.parametrize("cin,cout,hw", [(1536, 16, (9, 40)), (768, 8, (19, 33)), (384, 4, (7, 100))])
+def test_conv_wgrad_mfma_wide_cin_accumulates(cin, cout, hw):
+    from vmatting import ops
+    rs = np.random.RandomState(cout)
+    x = rs.normal(size=(1,) + hw + (cin,)).astype(np.float32)
+    dy = rs.normal(size=(1,) + hw + (cout,)).astype(np.float32)
+    dw = torch.ones((3, 3, cin, cout), dtype=torch.float32, device=DEV)
+    xd = T(x, torch.bfloat16)
+    ops.conv_wgrad(xd, T(dy), dw, mfma=True)
+    wr = torch.zeros((3, 3, cin, cout), dtype=torch.float64, requires_grad=True)
+    (tr._conv(torch.from_numpy(H(xd)), wr) * torch.from_numpy(_bf16(dy).astype(np.float64))).sum().backward()
+    assert scaled_err(H(dw) - 1.0, wr.grad.numpy()) <= 1e-4
+
+
+def test_conv_wgrad_mfma_tower_major_sources():
+    """x read from 3 tower-major sources ([3N,h,w,c] buffer, the batched frozen towers): equals the wgrad of the
+    channel concat [tower0 | tower1 | tower2] per pixel (unet_simple.py:153-168)."""
+    from vmatting import ops
+    rs = np.random.RandomState(5)
+    n, h, w, c, cout = 2, 11, 37, 64, 16
+    feats = rs.normal(size=(3 * n, h, w, c)).astype(np.float32)
+    fd = T(feats, torch.bfloat16)
+    dy = rs.normal(size=(n, h, w, cout)).astype(np.float32)
+    cat = np.concatenate([H(fd[t * n:(t + 1) * n]) for t in range(3)], -1)
+    for mfma in (False, True):  # exact-f32 kernel (dy as is) and MFMA kernel (dy rounded to bf16)
+        dw = torch.zeros((3, 3, 3 * c, cout), dtype=torch.float32, device=DEV)
+        ops.conv_wgrad(ops.SourceConcat(fd, 3), T(dy), dw, mfma=mfma)
+        wr = torch.zeros((3, 3, 3 * c, cout), dtype=torch.float64, requires_grad=True)
+        dref = _bf16(dy) if mfma else dy
+        (tr._conv(torch.from_numpy(cat), wr) * torch.from_numpy(dref.astype(np.float64))).sum().backward()
+        assert scaled_err(H(dw), wr.grad.numpy()) <= 1e-4, mfma
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+@pytest.mark.parametrize("c,cout", [(64, 2), (128, 4), (256, 8), (512, 16), (512, 48)])
+def test_conv_over_tower_major_sources_equals_concat(dtype, c, cout):
+    """vm_conv3x3_sources_nhwc (the batched towers' concat read as 3 sources) equals the conv of the materialised
+    concat bit for bit (same kernel, same K order)."""
+    from vmatting import ops
+    tdt = ops.TORCH_DTYPE[dtype]
+    n, h, w = 2, 9, 37
+    base = (torch.randn(3 * n, h, w, c, device=DEV) * 0.5).to(tdt)
+    sc = ops.SourceConcat(base, 3)
+    wt = (np.random.RandomState(c + cout).normal(size=(3, 3, 3 * c, cout)) * 0.05).astype(np.float32)
+    pc = ops.PackedConv(wt, np.zeros(cout, np.float32), dtype)
+    a = ops.conv3x3(sc, pc, "relu")
+    b = ops.conv3x3(sc.materialize().contiguous(), pc, "relu")
+    assert torch.equal(a, b)

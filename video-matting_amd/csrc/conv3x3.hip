@@ -48,7 +48,18 @@ struct ConvArgs {
   const void* w1;   // FIRST patch kernel: packed cin<=8 -> 64 first conv (tap-major, K_pad 128) and its bias
   const float* bias1;
   int x_f32, x_c;   // FIRST: the frame is f32 with x_c channels (converted to bf16 in the prologue)
+  // x_src_c > 0: the input channels come from cin / x_src_c sources of x_src_c channels each, source s at
+  // x_src_stride elements from the view base (tower-major features: unet_simple.py:153-168's concat, never built)
+  int x_src_c;
+  long x_src_stride;
 };
+
+// element offset of input channel c (relative to the view's channel 0) under the source split
+__device__ __forceinline__ long src_chan(const ConvArgs& a, int c) {
+  if (a.x_src_c <= 0) return c;
+  const int s = c / a.x_src_c;
+  return (long)s * a.x_src_stride + (c - s * a.x_src_c);
+}
 
 // (K element index k) -> (tap, channel); tap 9 = padding (contributes zero)
 template <int GE>
@@ -227,15 +238,15 @@ __global__ __launch_bounds__(256, 2) void conv3x3_mfma(ConvArgs a) {
       const int g0 = 2 * kt, g1 = g0 + 1;
       const int cc0 = g0 / 9, cc1 = g1 / 9;
       const int tap0 = g0 < a.ng ? g0 - cc0 * 9 : 9, tap1 = g1 < a.ng ? g1 - cc1 * 9 : 9;
-      const int d0 = (((tap0 / 3 - 1) * W + tap0 % 3 - 1) * xcs + cc0 * GE) * (int)sizeof(T);
-      const int d1 = (((tap1 / 3 - 1) * W + tap1 % 3 - 1) * xcs + cc1 * GE) * (int)sizeof(T);
+      const int d0 = (int)(((tap0 / 3 - 1) * W + tap0 % 3 - 1) * xcs + src_chan(a, cc0 * GE)) * (int)sizeof(T);
+      const int d1 = (int)(((tap1 / 3 - 1) * W + tap1 % 3 - 1) * xcs + src_chan(a, cc1 * GE)) * (int)sizeof(T);
       const bool hi = chunk >= 4;
       tap = hi ? tap1 : tap0;
       delta = (hi ? d1 : d0) + (chunk & 3) * 16;
     } else {
       int c;
       k_to_tap<GE>(a, kt * BKE + chunk * CE, tap, c);
-      delta = (((tap / 3 - 1) * W + tap % 3 - 1) * xcs + c) * (int)sizeof(T);
+      delta = (int)(((tap / 3 - 1) * W + tap % 3 - 1) * xcs + src_chan(a, c)) * (int)sizeof(T);
     }
 #pragma unroll
     for (int i = 0; i < XR; ++i) {
@@ -731,7 +742,8 @@ struct PatchCfg {
   static constexpr int TPM = BM / WM, TPN = BN / WN;
   static constexpr int FP = TPM / 16, FC = TPN / 16;
   static constexpr int SR = 64 * 2 + 16;                    // epilogue staging row (one 64-channel slab, bf16)
-  static constexpr int EPI = BM * SR;
+  static constexpr int SR32 = 64 * 4 + 16;                  // the same slab in f32 (f32 output views)
+  static constexpr int EPI = BM * SR32;
   static constexpr int MAIN = 2 * PB + S * G * WSLOT;
   static constexpr int LDS = MAIN > EPI ? MAIN : EPI;
   static constexpr int IW = TW + 4, IPIX = (TH + 4) * IW;   // FIRST: 8-channel input patch (16 B per pixel)
@@ -883,7 +895,8 @@ void conv3x3_patch(ConvArgs a) {
     const bool real = cc < nch;
 #pragma unroll
     for (int i = 0; i < XPW; ++i)
-      if (wave + i * NW < C::XP) glds16(xrs, lds0 + buf * C::PB + (wave + i * NW) * 1024, real ? xoff[i] + cc * 64 : OOB);
+      if (wave + i * NW < C::XP)
+        glds16(xrs, lds0 + buf * C::PB + (wave + i * NW) * 1024, real ? xoff[i] + (int)src_chan(a, cc * 32) * 2 : OOB);
   };
   auto issue_w = [&](int s, int slot) {  // ring step s = taps s*G .. s*G+G-1 (chunk-major K: consecutive 64 B)
 #pragma unroll
@@ -1040,6 +1053,57 @@ void conv3x3_patch(ConvArgs a) {
           (a.up ? (((long)n * 2 * H + 2 * r0) * YW + 2 * c0) : (((long)n * H + r0) * W + c0)) * (long)a.y_cstride;
   const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(yb, 0, 0x7ffffff0, 0x00020000);
   constexpr int SPW = C::TPN / 64;  // 64-channel slabs per wave column
+  if (a.y_dtype == VM_F32) {
+    // f32 output (the training step's pre-BN buffers, unet_simple.py:19-27): f32 slab staging, 4 channels per
+    // 16-byte store; no fused pool / folded resize on this path (host-checked)
+    float* yf = reinterpret_cast<float*>(a.y) + a.y_coff + (((long)n * H + r0) * W + c0) * (long)a.y_cstride;
+    const __amdgpu_buffer_rsrc_t yfr = __builtin_amdgcn_make_buffer_rsrc(yf, 0, 0x7ffffff0, 0x00020000);
+    const int ycs4 = a.y_cstride * 4;
+    for (int sl = 0; sl < BN / 64; ++sl) {
+      const int cb = n0 + sl * 64;
+      __syncthreads();
+      if (wn == sl / SPW) {
+#pragma unroll
+        for (int fc = 0; fc < FC; ++fc) {
+          if (fc / 4 != sl % SPW) continue;
+          const int col = (fc % 4) * 16 + 4 * (lane >> 4);
+          float mul[4], add[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int co = min(cb + col + j, a.cout - 1);
+            const float sc = a.scale ? a.scale[co] : 1.f;
+            mul[j] = sc;
+            add[j] = (a.bias ? a.bias[co] : 0.f) * sc + (a.shift ? a.shift[co] : 0.f);
+          }
+#pragma unroll
+          for (int fp = 0; fp < FP; ++fp) {
+            const int row = wm * C::TPM + fp * 16 + (lane & 15);
+            float v[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              v[j] = fmaf(acc[fc][fp][j], mul[j], add[j]);
+              if (a.act == VM_ACT_RELU) v[j] = fmaxf(v[j], 0.f);
+              else if (a.act == VM_ACT_SIGMOID) v[j] = sigmoid_precise(v[j]);
+            }
+            *reinterpret_cast<float4*>(smem + row * C::SR32 + col * 4) = make_float4(v[0], v[1], v[2], v[3]);
+          }
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int it = 0; it < C::BM * 16 / NT; ++it) {
+        const int idx = it * NT + tid;
+        const int rr = idx >> 4, cq = idx & 15;
+        const uint4 d = *reinterpret_cast<const uint4*>(smem + rr * C::SR32 + cq * 16);
+        const int pr = rr / C::TW, pc = rr % C::TW;
+        const bool ok = r0 + pr < H && c0 + pc < W && cb + cq * 4 < a.cout;
+        const int off = ok ? (pr * W + pc) * ycs4 + (cb + cq * 4) * 4 : OOB;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, d), yfr,
+                                               off, 0, 0);
+      }
+    }
+    return;
+  }
   for (int sl = 0; sl < BN / 64; ++sl) {
     const int phase = a.up ? (n0 + sl * 64) / a.up_cout : 0;
     const int cb = n0 + sl * 64 - phase * a.up_cout;  // first (per-phase) output channel of the slab
@@ -2090,8 +2154,10 @@ static long g_pair_kernel = 0;  // vm_conv3x3_pair_first_nhwc: 0 = persistent we
                                 // 1 = streaming patch kernel
 
 static bool patch_ok(const ConvArgs& a, size_t tsize) {
-  return tsize == 2 && a.chunk_major && a.cin_pad % 32 == 0 && a.y_dtype == VM_BF16 && a.y_vec &&
-         a.act != VM_ACT_SOFTMAX && (a.cout & 7) == 0;
+  // bf16 output, or f32 output without the fused pool / folded resize (cout multiple of 4 for 16-byte stores)
+  const bool yok = a.y_dtype == VM_BF16 ? (a.cout & 7) == 0 : (a.y_dtype == VM_F32 && !a.py && !a.up && (a.cout & 3) == 0);
+  return tsize == 2 && a.chunk_major && a.cin_pad % 32 == 0 && yok && a.y_vec && a.act != VM_ACT_SOFTMAX &&
+         (a.x_src_c <= 0 || a.x_src_c % 32 == 0);
 }
 
 static int dispatch_patch(ConvArgs& a, hipStream_t st) {
@@ -2182,11 +2248,11 @@ static int launch_first(ConvArgs& a, hipStream_t st) {
 
 template <typename T>
 static int dispatch_mfma(ConvArgs& a, hipStream_t st) {
-  if (sizeof(T) == 2 && g_conv_kernel != 1 && g_conv_kernel != 2 && a.cin_pad == 8 && !a.chunk_major &&
+  if (sizeof(T) == 2 && g_conv_kernel != 1 && g_conv_kernel != 2 && a.cin_pad == 8 && !a.chunk_major && a.x_src_c <= 0 &&
       a.y_dtype == VM_BF16 && a.y_vec && a.act != VM_ACT_SOFTMAX && (a.cout & 7) == 0 && a.K_pad == 128)
     return launch_first(a, st);
   if ((g_conv_kernel == 0 || g_conv_kernel == 3) && patch_ok(a, sizeof(T))) return dispatch_patch(a, st);
-  if (g_conv_kernel != 1 && a.act != VM_ACT_SOFTMAX) {
+  if (g_conv_kernel != 1 && a.act != VM_ACT_SOFTMAX && a.x_src_c <= 0) {
     // measured (tools/convbench.py): the LDS-DMA kernel wins for cout >= 256 (256x256 tiles); for
     // cout <= 128 its 64-channel-wide waves are DMA-issue-bound and the register-staged kernel is faster
     const int bm = a.cout > 64 ? 256 : 512;
@@ -2270,11 +2336,19 @@ extern "C" int vm_conv3x3_pack_weights(const float* w_hwio, int cin, int cout, i
 
 static int conv_impl(const vm_tensor* x, const void* packed, int cin, int cout, const float* bias, const float* scale,
                      const float* shift, int act, vm_tensor* y, const vm_tensor* yp, void* stream,
-                     float* y2 = nullptr);
+                     float* y2 = nullptr, int nsrc = 0, long src_stride = 0);
 
 extern "C" int vm_conv3x3_nhwc(const vm_tensor* x, const void* packed, int cin, int cout, const float* bias,
                                const float* scale, const float* shift, int act, vm_tensor* y, void* stream) {
   return conv_impl(x, packed, cin, cout, bias, scale, shift, act, y, nullptr, stream);
+}
+
+extern "C" int vm_conv3x3_sources_nhwc(const vm_tensor* x, int nsrc, long src_stride, const void* packed, int cin,
+                                       int cout, const float* bias, const float* scale, const float* shift, int act,
+                                       vm_tensor* y, void* stream) {
+  if (nsrc < 1 || (nsrc > 1 && src_stride <= 0)) return fail(VM_EINVAL, "conv3x3_sources: nsrc %d stride %ld", nsrc,
+                                                            src_stride);
+  return conv_impl(x, packed, cin, cout, bias, scale, shift, act, y, nullptr, stream, nullptr, nsrc, src_stride);
 }
 
 extern "C" int vm_conv3x3_pool_nhwc(const vm_tensor* x, const void* packed, int cin, int cout, const float* bias,
@@ -2397,17 +2471,22 @@ extern "C" int vm_conv3x3_head_nhwc(const vm_tensor* x, const void* packed, int 
 }
 
 static int conv_impl(const vm_tensor* x, const void* packed, int cin, int cout, const float* bias, const float* scale,
-                     const float* shift, int act, vm_tensor* y, const vm_tensor* yp, void* stream, float* y2) {
+                     const float* shift, int act, vm_tensor* y, const vm_tensor* yp, void* stream, float* y2, int nsrc,
+                     long src_stride) {
   if (!valid_tensor(x) || !valid_tensor(y) || !packed) return fail(VM_EINVAL, "conv3x3: invalid tensor/weights");
-  if (cin <= 0 || cout <= 0 || x->c != cin || y->c != cout)
-    return fail(VM_EINVAL, "conv3x3: channel mismatch x.c=%d cin=%d y.c=%d cout=%d", x->c, cin, y->c, cout);
+  const int xc = nsrc > 1 ? nsrc * x->c : x->c;  // sources: x is the view of source 0
+  if (cin <= 0 || cout <= 0 || xc != cin || y->c != cout)
+    return fail(VM_EINVAL, "conv3x3: channel mismatch x.c=%d cin=%d y.c=%d cout=%d", xc, cin, y->c, cout);
+  if (nsrc > 1 && (cout == 1 || yp || x->c % (x->dtype == VM_BF16 ? 32 : 16) || src_stride % 8))
+    return fail(VM_EUNSUPPORTED, "conv3x3: split sources need whole 64-byte granules per source (x.c=%d)", x->c);
   if (x->n != y->n || x->h != y->h || x->w != y->w)
     return fail(VM_EINVAL, "conv3x3: spatial mismatch [%d,%d,%d] vs [%d,%d,%d]", x->n, x->h, x->w, y->n, y->h, y->w);
   if (act < VM_ACT_NONE || act > VM_ACT_SOFTMAX) return fail(VM_EINVAL, "conv3x3: act %d", act);
   const int dt = x->dtype;
   PackGeom g = geom(cin, cout, dt);
   const int ce = 16 / elem_bytes(dt);
-  if (reinterpret_cast<uintptr_t>(x->ptr) % 16 || x->cstride % ce || x->coff % ce || x->coff + g.cin_pad > x->cstride)
+  if (reinterpret_cast<uintptr_t>(x->ptr) % 16 || x->cstride % ce || x->coff % ce ||
+      x->coff + (nsrc > 1 ? x->c : g.cin_pad) > x->cstride)
     return fail(VM_EUNSUPPORTED,
                 "conv3x3: input view must be 16-byte aligned with channel padding to %d (coff=%d cstride=%d)",
                 g.cin_pad, x->coff, x->cstride);
@@ -2471,6 +2550,10 @@ static int conv_impl(const vm_tensor* x, const void* packed, int cin, int cout, 
   ConvArgs a{};
   a.x = x->ptr; a.x_cstride = x->cstride; a.x_coff = x->coff; a.H = x->h; a.W = x->w; a.M = M;
   fill_geom(a, g);
+  if (nsrc > 1) {
+    a.x_src_c = x->c;
+    a.x_src_stride = src_stride;
+  }
   a.w = packed; a.cout = cout;
   a.bias = bias; a.scale = scale; a.shift = shift; a.act = act;
   a.y = y->ptr; a.y_cstride = y->cstride; a.y_coff = y->coff; a.y_dtype = y->dtype;

@@ -26,17 +26,26 @@ namespace trn {
 struct V {
   char* p;
   int n, h, w, c, cs, coff, dt;
+  int sc;     // > 0: channel c lives in source c / sc (tower-major features), sources ss elements apart
+  long ss;
 };
 
 static V mk(const vm_tensor* t) {
   V v;
   v.p = reinterpret_cast<char*>(t->ptr);
   v.n = t->n; v.h = t->h; v.w = t->w; v.c = t->c; v.cs = t->cstride; v.coff = t->coff; v.dt = t->dtype;
+  v.sc = 0; v.ss = 0;
   return v;
 }
 
+__device__ __forceinline__ long vchan(const V& v, int c) {
+  if (v.sc <= 0) return c;
+  const int s = c / v.sc;
+  return (long)s * v.ss + (c - s * v.sc);
+}
+
 __device__ __forceinline__ float ld(const V& v, long pix, int c) {
-  const long o = pix * v.cs + v.coff + c;
+  const long o = pix * v.cs + v.coff + vchan(v, c);
   return v.dt == VM_F32 ? reinterpret_cast<const float*>(v.p)[o] : bf2f(reinterpret_cast<const uint16_t*>(v.p)[o]);
 }
 
@@ -272,7 +281,7 @@ __global__ __launch_bounds__(WG_NT) void wgrad_kernel(V x, V dy, float* partials
           const int gy = y0 + pc / WG_PW - 1, gx = x0 + pc % WG_PW - 1, c = c0 + j * VE;
           if (gy >= 0 && gy < x.h && gx >= 0 && gx < x.w && c < cin)
             xb[k] = *reinterpret_cast<const uint4*>(reinterpret_cast<const T*>(x.p) +
-                                                    (((long)n * x.h + gy) * x.w + gx) * x.cs + x.coff + c);
+                                                    (((long)n * x.h + gy) * x.w + gx) * x.cs + x.coff + vchan(x, c));
         }
       }
     }
@@ -391,6 +400,285 @@ __global__ __launch_bounds__(WG_NT) void wgrad_kernel(V x, V dy, float* partials
   }
 }
 
+// ---------------------------------------------------------------- conv weight gradient on MFMA (bf16 operands)
+// dW_t[ci][co] = sum_p X[p + off_t][ci] * DY[p][co] (t = kh*3 + kw, off_t = (kh-1, kw-1)) as 9 GEMMs whose K axis is
+// the pixels: v_mfma_f32_16x16x32_bf16 with A = X^T (16 input channels x 32 pixels), B = DY (32 pixels x 16 output
+// channels), f32 accumulation.  Both operands sit in LDS in their natural NHWC order ([pixel][channel] rows) and are
+// read k-major with ds_read_b64_tr_b16, so no transpose pass exists anywhere.  One of the two operands carries the
+// 1-pixel halo and is read at the 9 tap offsets; the other is read once per K-step and reused by the 9 taps:
+//   SX  (shift x):  X patch (TH+2) x (TW+2) x CIB, DY tile TH x TW x COP        — wide cout (upconv*, conv*)
+//   !SX (shift dy): X tile TH x TW x CIB, DY patch (TH+2) x (TW+2) x COP       — narrow cout (select*, output):
+//                   dW_t = sum_q X[q] * DY[q - off_t], with DY zero outside the frame
+// Block = 4 waves on one TH(4) x TW(32) pixel tile, wave w owns tile row w (one 32-pixel K-step); blocks walk tiles
+// (split-K over gridDim.x, one partial per block, the fixed-order wgrad_reduce_kernel sums them: deterministic).
+// DY arrives f32 and is rounded to bf16 when staged (the bf16 training path's precision: bf16 operands, f32 sums).
+// The LDS images are swizzled so every transposed read (two 16-lane groups 8 rows apart per 32-lane half) is
+// conflict-free for any row base (tap shifts move it by 0..2 rows/pixels).
+constexpr int WM_TH = 4, WM_TW = 32, WM_PW = WM_TW + 2, WM_PPIX = (WM_TH + 2) * WM_PW;  // 204 patch pixels
+constexpr int WM_PROWS = (WM_PPIX + 15) / 16 * 16;                                   // 208: swizzle stays in range
+
+struct WgArgs {
+  const uint16_t* x;  // bf16 input view base (pixel 0, channel coff applied)
+  int n, h, w, cin, xcs, x_src_c;  // x_src_c > 0: channel c lives in source c / x_src_c at + x_src_stride elements
+  long x_src_stride;
+  const float* dy;  // f32 output-gradient view base (coff applied)
+  int cout, dcs;
+  float* part;      // [gridDim.x][9][cin][cout]
+  int tiles_h, tiles_w;
+  long ntiles;
+};
+
+// byte offset of 32-byte piece c (16 bf16 channels) of image row r, rows of RB bytes (32, 64 or 128)
+template <int RB>
+__device__ __forceinline__ int wm_off(int r, int c) {
+  if constexpr (RB == 32) return 32 * (r ^ (((r >> 3) & 1) << 2));
+  else if constexpr (RB == 64) return 64 * r + 32 * (c ^ ((r >> 3) & 1));
+  else return 128 * r + 32 * (c ^ ((r >> 1) & 1) ^ (((r >> 3) & 1) << 1));
+}
+
+typedef short v4s __attribute__((ext_vector_type(4)));
+
+// the 16x16x32 operand fragment whose k rows are image rows rk(0..7) (8 consecutive pixels of one image row band),
+// columns = 16-channel piece c: two transposed 4-row reads
+template <int RB>
+__device__ __forceinline__ bf16x8 wm_frag(const char* img, int r0, int c, int lane) {
+  const int q = (lane >> 2) & 3, p = lane & 3;
+  typedef __attribute__((address_space(3))) v4s* lp;
+  const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(img + wm_off<RB>(r0 + q, c) + 8 * p));
+  const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(img + wm_off<RB>(r0 + 4 + q, c) + 8 * p));
+  v4s v[2] = {lo, hi};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+template <int NCI, int NCO, bool SX>
+__global__ __launch_bounds__(256, 2) void wgrad_mfma_kernel(WgArgs a) {
+  constexpr int CIB = NCI * 16, COP = NCO * 16;
+  constexpr int RBX = NCI == 1 ? 32 : NCI == 2 ? 64 : 128;
+  constexpr int RBD = NCO == 1 ? 32 : NCO == 2 ? 64 : 128;
+  constexpr int XROWS = SX ? WM_PROWS : WM_TH * WM_TW, DROWS = SX ? WM_TH * WM_TW : WM_PROWS;
+  constexpr int XBYTES = XROWS * RBX, DBYTES = DROWS * RBD;
+  constexpr int XPIX = SX ? WM_PPIX : WM_TH * WM_TW, DPIX = SX ? WM_TH * WM_TW : WM_PPIX;
+  constexpr int XCH = CIB / 8, DCH = COP / 8;                    // 16-byte chunks per pixel row
+  constexpr int NXC = XPIX * XCH, NDC = DPIX * DCH;
+  constexpr int XPT = (NXC + 255) / 256, DPT = (NDC + 255) / 256;
+  constexpr int RED = 9 * NCI * NCO * 4 * 64 * 4;                // one wave's accumulators in bytes
+  constexpr int MAIN = XBYTES + DBYTES;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  (void)RED;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int c0 = blockIdx.y * CIB;
+  char* ximg = smem;
+  char* dimg = smem + XBYTES;
+
+  f32x4 acc[9][NCI][NCO];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int i = 0; i < NCI; ++i)
+#pragma unroll
+      for (int o = 0; o < NCO; ++o) acc[t][i][o] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  uint4 xb[XPT];
+  float4 db[DPT][2];
+  auto coords = [&](long tile, int& n, int& y0, int& x0) {
+    const int tx = (int)(tile % a.tiles_w);
+    const long t2 = tile / a.tiles_w;
+    y0 = (int)(t2 % a.tiles_h) * WM_TH;
+    n = (int)(t2 / a.tiles_h);
+    x0 = tx * WM_TW;
+  };
+  // image pixel e of the patch (halo: origin (y0-1, x0-1), 34 wide) or the tile (origin (y0, x0), 32 wide)
+  auto pix = [&](int e, bool halo, int y0, int x0, int& gy, int& gx) {
+    if (halo) {
+      gy = y0 - 1 + e / WM_PW;
+      gx = x0 - 1 + e % WM_PW;
+    } else {
+      gy = y0 + e / WM_TW;
+      gx = x0 + e % WM_TW;
+    }
+  };
+  auto issue = [&](long tile) {
+    int n, y0, x0;
+    coords(tile, n, y0, x0);
+#pragma unroll
+    for (int k = 0; k < XPT; ++k) {
+      const int e = tid + k * 256;
+      xb[k] = make_uint4(0, 0, 0, 0);
+      if (NXC % 256 == 0 || e < NXC) {
+        const int pe = e / XCH, j = e % XCH;
+        int gy, gx;
+        pix(pe, SX, y0, x0, gy, gx);
+        const int c = c0 + j * 8;
+        if ((unsigned)gy < (unsigned)a.h && (unsigned)gx < (unsigned)a.w && c < a.cin) {
+          long off = (((long)n * a.h + gy) * a.w + gx) * a.xcs;
+          if (a.x_src_c > 0) off += (long)(c / a.x_src_c) * a.x_src_stride + c % a.x_src_c;
+          else off += c;
+          xb[k] = *reinterpret_cast<const uint4*>(a.x + off);
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < DPT; ++k) {
+      const int e = tid + k * 256;
+      db[k][0] = db[k][1] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (NDC % 256 == 0 || e < NDC) {
+        const int pe = e / DCH, j = e % DCH;
+        int gy, gx;
+        pix(pe, !SX, y0, x0, gy, gx);
+        const int co = j * 8;
+        if ((unsigned)gy < (unsigned)a.h && (unsigned)gx < (unsigned)a.w && co < a.cout) {
+          const float* src = a.dy + (((long)n * a.h + gy) * a.w + gx) * a.dcs + co;
+          if (co + 8 <= a.cout && (reinterpret_cast<uintptr_t>(src) & 15) == 0) {
+            db[k][0] = *reinterpret_cast<const float4*>(src);
+            db[k][1] = *reinterpret_cast<const float4*>(src + 4);
+          } else {
+            float f[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) f[i] = co + i < a.cout ? src[i] : 0.f;
+            db[k][0] = make_float4(f[0], f[1], f[2], f[3]);
+            db[k][1] = make_float4(f[4], f[5], f[6], f[7]);
+          }
+        }
+      }
+    }
+  };
+  auto commit = [&]() {
+#pragma unroll
+    for (int k = 0; k < XPT; ++k) {
+      const int e = tid + k * 256;
+      if (NXC % 256 == 0 || e < NXC) {
+        const int pe = e / XCH, j = e % XCH;
+        uint4 v = xb[k];
+        const int c = c0 + j * 8;
+        if (c + 8 > a.cin) {  // a chunk straddling cin (padded views): zero the lanes past it
+          uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            if (c + 2 * i >= a.cin) w4[i] = 0u;
+            else if (c + 2 * i + 1 >= a.cin) w4[i] &= 0xffffu;
+          }
+          v = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+        }
+        *reinterpret_cast<uint4*>(ximg + wm_off<RBX>(pe, j >> 1) + (j & 1) * 16) = v;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < DPT; ++k) {
+      const int e = tid + k * 256;
+      if (NDC % 256 == 0 || e < NDC) {
+        const int pe = e / DCH, j = e % DCH;
+        const float f[8] = {db[k][0].x, db[k][0].y, db[k][0].z, db[k][0].w,
+                            db[k][1].x, db[k][1].y, db[k][1].z, db[k][1].w};
+        *reinterpret_cast<uint4*>(dimg + wm_off<RBD>(pe, j >> 1) + (j & 1) * 16) = Chunk<uint16_t>::pack(f);
+      }
+    }
+  };
+
+  const int g = lane >> 4;
+  if (blockIdx.x < a.ntiles) issue(blockIdx.x);
+  for (long tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
+    commit();
+    __syncthreads();
+    if (tile + gridDim.x < a.ntiles) issue(tile + gridDim.x);
+    // K-step: the 32 pixels of tile row `wave`; group g of the fragment holds pixels 8g..8g+7
+    if constexpr (SX) {
+      bf16x8 bd[NCO];
+#pragma unroll
+      for (int o = 0; o < NCO; ++o) bd[o] = wm_frag<RBD>(dimg, wave * WM_TW + 8 * g, o, lane);
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int r0 = (wave + t / 3) * WM_PW + t % 3 + 8 * g;
+#pragma unroll
+        for (int i = 0; i < NCI; ++i) {
+          const bf16x8 ax = wm_frag<RBX>(ximg, r0, i, lane);
+#pragma unroll
+          for (int o = 0; o < NCO; ++o)
+            acc[t][i][o] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ax, bd[o], acc[t][i][o], 0, 0, 0);
+        }
+      }
+    } else {
+      bf16x8 ax[NCI];
+#pragma unroll
+      for (int i = 0; i < NCI; ++i) ax[i] = wm_frag<RBX>(ximg, wave * WM_TW + 8 * g, i, lane);
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        // DY[q - off_t]: patch coordinates (row + 2 - kh, col + 2 - kw)
+        const int r0 = (wave + 2 - t / 3) * WM_PW + 2 - t % 3 + 8 * g;
+#pragma unroll
+        for (int o = 0; o < NCO; ++o) {
+          const bf16x8 bd = wm_frag<RBD>(dimg, r0, o, lane);
+#pragma unroll
+          for (int i = 0; i < NCI; ++i)
+            acc[t][i][o] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ax[i], bd, acc[t][i][o], 0, 0, 0);
+        }
+      }
+    }
+    __syncthreads();
+  }
+
+  // fold the 4 waves' accumulators (LDS, two rounds), wave 0 stores the block's partial
+  float* red = reinterpret_cast<float*>(smem);
+  constexpr int NA = 9 * NCI * NCO * 4;
+  auto put = [&](int slot) {
+    int k = 0;
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int i = 0; i < NCI; ++i)
+#pragma unroll
+        for (int o = 0; o < NCO; ++o)
+#pragma unroll
+          for (int j = 0; j < 4; ++j, ++k) red[(slot * NA + k) * 64 + lane] = acc[t][i][o][j];
+  };
+  auto add = [&](int slot) {
+    int k = 0;
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int i = 0; i < NCI; ++i)
+#pragma unroll
+        for (int o = 0; o < NCO; ++o)
+#pragma unroll
+          for (int j = 0; j < 4; ++j, ++k) acc[t][i][o][j] += red[(slot * NA + k) * 64 + lane];
+  };
+  if (wave >= 2) put(wave - 2);
+  __syncthreads();
+  if (wave < 2) add(wave);
+  __syncthreads();
+  if (wave == 1) put(0);
+  __syncthreads();
+  if (wave == 0) {
+    add(0);
+    float* part = a.part + (long)blockIdx.x * 9 * a.cin * a.cout;
+    const int co_l = lane & 15, ci_l = 4 * (lane >> 4);
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int i = 0; i < NCI; ++i)
+#pragma unroll
+        for (int o = 0; o < NCO; ++o) {
+          const int co = o * 16 + co_l;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int ci = c0 + i * 16 + ci_l + j;
+            if (ci < a.cin && co < a.cout) part[((long)t * a.cin + ci) * a.cout + co] = acc[t][i][o][j];
+          }
+        }
+  }
+  (void)MAIN;
+}
+
+template <int NCI, int NCO, bool SX>
+constexpr int wgrad_mfma_lds() {
+  constexpr int RBX = NCI == 1 ? 32 : NCI == 2 ? 64 : 128;
+  constexpr int RBD = NCO == 1 ? 32 : NCO == 2 ? 64 : 128;
+  constexpr int XROWS = SX ? WM_PROWS : WM_TH * WM_TW, DROWS = SX ? WM_TH * WM_TW : WM_PROWS;
+  constexpr int MAIN = XROWS * RBX + DROWS * RBD;
+  constexpr int RED = 2 * 9 * NCI * NCO * 4 * 64 * 4;
+  return MAIN > RED ? MAIN : RED;
+}
+
 // HWIO [3][3][cin][cout] -> the dgrad filter [3][3][cout][cin], spatially flipped
 __global__ void flip_weights_kernel(const float* w, int cin, int cout, float* wt) {
   const long total = 9L * cin * cout;
@@ -472,6 +760,9 @@ static bool vec_ok(const V& v, int ve) {
 // x may also be read in 16-byte vectors past its last channel when the row stride holds them (the padded
 // concat / input buffers: up1n[..., :30] of a 32-wide row, in9[..., :9] of a 16-wide row); the extra lanes are zeroed
 static bool xvec_ok(const V& v, int ve) {
+  if (v.sc > 0)  // split sources: a vector never straddles two sources
+    return reinterpret_cast<uintptr_t>(v.p) % 16 == 0 && v.coff % ve == 0 && v.cs % ve == 0 && v.sc % ve == 0 &&
+           v.ss % ve == 0 && v.coff + v.sc <= v.cs;
   return reinterpret_cast<uintptr_t>(v.p) % 16 == 0 && v.coff % ve == 0 && v.cs % ve == 0 &&
          v.coff + (v.c + ve - 1) / ve * ve <= v.cs;
 }
@@ -489,6 +780,51 @@ static void launch_wgrad(const V& xv, const V& dy, float* dw, float* ws, hipStre
     if (dv) launch_wgrad_t<CC, CO4, float, false, true>(xv, dy, dw, ws, st);
     else launch_wgrad_t<CC, CO4, float, false, false>(xv, dy, dw, ws, st);
   }
+}
+
+struct WmCfg {
+  int nci, nco;
+  bool sx;
+};
+
+// operand tiling of the MFMA weight gradient: cout -> NCO 16-wide fragments, the input-channel fragments per block
+// as wide as 144 accumulator registers allow; the operand with fewer fragments per K-step carries the tap shift
+static WmCfg wgrad_mfma_cfg(int cin, int cout) {
+  WmCfg c;
+  c.nco = cout <= 16 ? 1 : cout <= 32 ? 2 : 3;
+  if (c.nco == 1) c.nci = cin > 32 ? 4 : cin > 16 ? 2 : 1;
+  else if (c.nco == 2) c.nci = cin > 16 ? 2 : 1;
+  else c.nci = 1;
+  c.sx = c.nco >= c.nci;
+  return c;
+}
+
+template <int NCI, int NCO, bool SX>
+static int launch_wgrad_mfma_t(WgArgs& a, float* dw, hipStream_t st) {
+  constexpr int lds = wgrad_mfma_lds<NCI, NCO, SX>();
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_mfma_kernel<NCI, NCO, SX>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    if (e != hipSuccess) return fail(VM_EHIP, "hipFuncSetAttribute(wgrad_mfma): %s", hipGetErrorString(e));
+    attr = true;
+  }
+  const int ncc = (a.cin + NCI * 16 - 1) / (NCI * 16);
+  const long gx = wgrad_rows(a.n, a.h, a.w, a.cin, a.cout, NCI * 16);
+  hipLaunchKernelGGL((wgrad_mfma_kernel<NCI, NCO, SX>), dim3((unsigned)gx, ncc), dim3(256), lds, st, a);
+  const long S = 9L * a.cin * a.cout;
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((S + 63) / 64)), dim3(1024), 0, st, a.part, (int)gx, S, dw);
+  return VM_OK;
+}
+
+static int launch_wgrad_mfma(WgArgs& a, float* dw, hipStream_t st) {
+  const WmCfg c = wgrad_mfma_cfg(a.cin, a.cout);
+  if (c.nci == 4) return launch_wgrad_mfma_t<4, 1, false>(a, dw, st);
+  if (c.nci == 2 && c.nco == 1) return launch_wgrad_mfma_t<2, 1, false>(a, dw, st);
+  if (c.nci == 1 && c.nco == 1) return launch_wgrad_mfma_t<1, 1, true>(a, dw, st);
+  if (c.nci == 2 && c.nco == 2) return launch_wgrad_mfma_t<2, 2, true>(a, dw, st);
+  if (c.nci == 1 && c.nco == 2) return launch_wgrad_mfma_t<1, 2, true>(a, dw, st);
+  return launch_wgrad_mfma_t<1, 3, true>(a, dw, st);
 }
 
 static bool ok_view(const vm_tensor* t) { return valid_tensor(t); }
@@ -602,6 +938,58 @@ extern "C" int vm_conv3x3_wgrad_nhwc(const vm_tensor* x, const vm_tensor* dy, fl
     default: launch_wgrad<32, 12>(xv, dv, dw, ws, st); break;
   }
   return check_launch("conv3x3_wgrad");
+}
+
+extern "C" size_t vm_conv3x3_wgrad_ex_workspace_bytes(int n, int h, int w, int cin, int cout, int mode) {
+  if (n <= 0 || h <= 0 || w <= 0 || cin <= 0 || cout <= 0 || cout > 48) return 0;
+  if (mode != 1) return (size_t)wgrad_rows(n, h, w, cin, cout, wgrad_cc(cout)) * 9 * cin * cout * sizeof(float);
+  const WmCfg c = wgrad_mfma_cfg(cin, cout);
+  return (size_t)wgrad_rows(n, h, w, cin, cout, c.nci * 16) * 9 * cin * cout * sizeof(float);
+}
+
+extern "C" int vm_conv3x3_wgrad_ex_nhwc(const vm_tensor* x, int x_src_c, long x_src_stride, const vm_tensor* dy,
+                                        float* dw, void* work, int mode, void* stream) {
+  vm_tensor xs = x ? *x : vm_tensor{};
+  if (x_src_c > 0) xs.c = x_src_c;  // the view of source 0 must be valid; the others follow at x_src_stride
+  if (!x || !ok_view(&xs) || !ok_view(dy) || !dw || !work || dy->dtype != VM_F32 || dy->n != x->n || dy->h != x->h ||
+      dy->w != x->w || x_src_c < 0 || (x_src_c > 0 && (x_src_stride <= 0 || x->c % x_src_c)) ||
+      (mode != 0 && mode != 1))
+    return fail(VM_EINVAL, "conv3x3_wgrad_ex: bad argument");
+  if (dy->c > 48) return fail(VM_EUNSUPPORTED, "conv3x3_wgrad_ex: cout %d > 48", dy->c);
+  if (mode == 0) {  // exact f32 FMA kernel, optionally over split sources
+    V xv = mk(x), dv = mk(dy);
+    xv.sc = x_src_c;
+    xv.ss = x_src_stride;
+    float* ws = reinterpret_cast<float*>(work);
+    switch ((dy->c + 3) / 4) {
+      case 1: launch_wgrad<64, 1>(xv, dv, dw, ws, reinterpret_cast<hipStream_t>(stream)); break;
+      case 2: launch_wgrad<64, 2>(xv, dv, dw, ws, reinterpret_cast<hipStream_t>(stream)); break;
+      case 3:
+      case 4: launch_wgrad<32, 4>(xv, dv, dw, ws, reinterpret_cast<hipStream_t>(stream)); break;
+      case 5:
+      case 6: launch_wgrad<32, 6>(xv, dv, dw, ws, reinterpret_cast<hipStream_t>(stream)); break;
+      case 7:
+      case 8: launch_wgrad<32, 8>(xv, dv, dw, ws, reinterpret_cast<hipStream_t>(stream)); break;
+      default: launch_wgrad<32, 12>(xv, dv, dw, ws, reinterpret_cast<hipStream_t>(stream)); break;
+    }
+    return check_launch("conv3x3_wgrad_ex");
+  }
+  if (x->dtype != VM_BF16 || reinterpret_cast<uintptr_t>(x->ptr) % 16 || x->coff % 8 || x->cstride % 8 ||
+      (x_src_c > 0 ? (x_src_c % 8 || x->c % x_src_c || x->coff + x_src_c > x->cstride || x_src_stride % 8)
+                   : x->coff + (x->c + 7) / 8 * 8 > x->cstride))
+    return fail(VM_EUNSUPPORTED, "conv3x3_wgrad_ex: the MFMA mode needs a bf16 x of 16-byte channel chunks");
+  WgArgs a{};
+  a.x = reinterpret_cast<const uint16_t*>(x->ptr) + x->coff;
+  a.n = x->n; a.h = x->h; a.w = x->w; a.cin = x->c; a.xcs = x->cstride;
+  a.x_src_c = x_src_c; a.x_src_stride = x_src_stride;
+  a.dy = reinterpret_cast<const float*>(dy->ptr) + dy->coff;
+  a.cout = dy->c; a.dcs = dy->cstride;
+  a.part = reinterpret_cast<float*>(work);
+  a.tiles_h = (x->h + WM_TH - 1) / WM_TH; a.tiles_w = (x->w + WM_TW - 1) / WM_TW;
+  a.ntiles = (long)x->n * a.tiles_h * a.tiles_w;
+  int rc = launch_wgrad_mfma(a, dw, reinterpret_cast<hipStream_t>(stream));
+  if (rc) return rc;
+  return check_launch("conv3x3_wgrad_ex");
 }
 
 extern "C" int vm_conv3x3_flip_weights(const float* w_hwio, int cin, int cout, float* w_flipped, void* stream) {

@@ -111,6 +111,29 @@ class PackedConv:
         return conv3x3(x, self, act, out, out_dtype, affine)
 
 
+class SourceConcat:
+    """The channel concat of ``nsrc`` equally shaped feature maps stored one after another in ``base``
+    ([nsrc*N, H, W, C], contiguous) — unet_simple.py:153-168's per-level concat of the three VGG towers, which
+    run as ONE batch-3N pass here.  Never materialised: conv3x3 / conv_wgrad read it as split sources."""
+
+    def __init__(self, base, nsrc):
+        if base.dim() != 4 or base.shape[0] % nsrc or not base.is_contiguous():
+            raise ValueError("SourceConcat: base must be a contiguous [nsrc*N,H,W,C] tensor")
+        self.base, self.nsrc = base, int(nsrc)
+        n = base.shape[0] // nsrc
+        self.src0 = base[:n]
+        self.stride = n * base.shape[1] * base.shape[2] * base.shape[3]
+        self.shape = (n, base.shape[1], base.shape[2], nsrc * base.shape[3])
+        self.dtype, self.device, self.is_cuda = base.dtype, base.device, base.is_cuda
+
+    def source(self, i):
+        n = self.shape[0]
+        return self.base[i * n:(i + 1) * n]
+
+    def materialize(self):
+        return torch.cat([self.source(i) for i in range(self.nsrc)], -1)
+
+
 def conv3x3(x, pc, act="none", out=None, out_dtype=None, affine=None, pool_out=None):
     """tf.nn.conv2d 3x3 SAME + bias_add (+ folded BN affine) + activation, on MFMA.
 
@@ -131,6 +154,14 @@ def conv3x3(x, pc, act="none", out=None, out_dtype=None, affine=None, pool_out=N
         scale = shift = None
     else:
         scale, shift = affine
+    if isinstance(x, SourceConcat):
+        if pool_out is not None:
+            raise ValueError("conv3x3: no fused pooling over split sources")
+        xv, yv = nhwc(x.src0), nhwc(out)
+        check(lib().vm_conv3x3_sources_nhwc(ctypes.byref(xv), x.nsrc, x.stride, _ptr(pc.packed), pc.cin, pc.cout,
+                                            _ptr(pc.bias), _ptr(scale), _ptr(shift), _lib.ACT[act], ctypes.byref(yv),
+                                            stream_handle()), "conv3x3_sources")
+        return out
     xv, yv = nhwc(x), nhwc(out)
     prof = _CONV_PROFILE
     if prof is not None:
@@ -554,14 +585,33 @@ def resize_backward(dy, dx):
     return dx
 
 
-def conv_wgrad(x, dy, dw):
-    """dw[3,3,cin,cout] += 3x3 SAME conv weight gradient of input view x and f32 output-gradient view dy."""
+def conv_wgrad(x, dy, dw, mfma=False, sources=None):
+    """dw[3,3,cin,cout] += 3x3 SAME conv weight gradient of input view x and f32 output-gradient view dy.
+
+    ``mfma``: bf16 x only — the MFMA kernel with dy rounded to bf16 (the bf16 training path); else the exact-f32
+    FMA kernel.  ``sources`` = (number of sources, element stride between sources): x is the [n,h,w,c] view of
+    source 0 and the conv input is the channel concat of the sources (tower-major features, MFMA kernel only)."""
     _f32(dw)
+    if isinstance(x, SourceConcat):
+        x, sources = x.src0, (x.nsrc, x.stride)
     n, h, w, cin = x.shape
     cout = dy.shape[-1]
-    if tuple(dy.shape) != (n, h, w, cout) or dw.numel() != 9 * cin * cout:
+    src_c = cin
+    if sources is not None:
+        cin = src_c * int(sources[0])
+    if tuple(dy.shape[:3]) != (n, h, w) or dw.numel() != 9 * cin * cout:
         raise ValueError("conv_wgrad: x %s, dy %s, dw %s" % (tuple(x.shape), tuple(dy.shape), tuple(dw.shape)))
-    xv, dv = nhwc(x), nhwc(dy)
+    dv = nhwc(dy)
+    if mfma or sources is not None:
+        xv = nhwc(x)
+        xv.c = cin
+        src_c, stride = (src_c, int(sources[1])) if sources is not None else (0, 0)
+        mode = 1 if mfma else 0
+        ws = _workspace(lib().vm_conv3x3_wgrad_ex_workspace_bytes(n, h, w, cin, cout, mode), x.device)
+        check(lib().vm_conv3x3_wgrad_ex_nhwc(ctypes.byref(xv), src_c, stride, ctypes.byref(dv), _ptr(dw), _ptr(ws),
+                                             mode, stream_handle()), "conv_wgrad_ex")
+        return dw
+    xv = nhwc(x)
     ws = _workspace(lib().vm_conv3x3_wgrad_workspace_bytes(n, h, w, cin, cout), x.device)
     check(lib().vm_conv3x3_wgrad_nhwc(ctypes.byref(xv), ctypes.byref(dv), _ptr(dw), _ptr(ws), stream_handle()),
           "conv_wgrad")

@@ -119,6 +119,8 @@ class VideoTrainer:
                     bp = torch.zeros(cp, dtype=torch.float32, device=dev)
                     self._padconv[scope] = (ops.PackedConv(wp, bp, self.model.dtype, dev), wp, bp, cout)
             self._sync_padded()
+        # filter gradients: bf16 operands on MFMA in the bf16 path, the exact-f32 kernel in the fp32 (parity) path
+        self._mfma_wgrad = self.model.dtype == torch.bfloat16
         self.t = 0
         self._b1p = np.float32(1.0)
         self._b2p = np.float32(1.0)
@@ -140,8 +142,10 @@ class VideoTrainer:
         tb = {"alpha": F(0, 1), "dlogit": F(0, 1), "loss": torch.zeros(3, dtype=torch.float32, device=dev)}
         st = lambda c: (torch.empty(c, dtype=torch.float32, device=dev),  # noqa: E731
                         torch.empty(c, dtype=torch.float32, device=dev))
-        # pre-BN conv outputs in the compute dtype: bf16 lets the patch-reuse conv kernel write them
-        Z = lambda lv, c: torch.empty((n, L[lv][0], L[lv][1], c), dtype=self.model.dtype, device=dev)  # noqa: E731
+        # pre-BN conv outputs stay f32 in both modes (the patch-reuse kernel writes f32 views): BN's x-hat = (z -
+        # mean) * rstd loses most of bf16's 8 bits when a channel's mean is large against its spread, and the
+        # gamma gradients (sum g * x-hat) with it (measured: 40-90 % error on the select1_* gammas with bf16 z)
+        Z = lambda lv, c: torch.empty((n, L[lv][0], L[lv][1], c), dtype=torch.float32, device=dev)  # noqa: E731
         for lv, cat, width, sels, up, prev, conv, cout_key in LEVELS:
             for s, _ in sels + ((conv, None),):
                 c = self.model.convs[s].cout
@@ -195,10 +199,8 @@ class VideoTrainer:
         b = m._buffers(n, h, w)
         tb = self._train_buffers(n, h, w)
         L = _levels(h, w)
-        for t in range(3):
-            ops.convert(xs[t], b["in"][t])
-            ops.convert(xs[t], b["in9"][..., 3 * t:3 * t + 3])
-            m._tower(b, t)
+        m.load_inputs(b, xs)
+        m._towers(b)
         for lv, cat, width, sels, up, prev, conv, out_key in LEVELS:
             c, off = b[cat][..., :width], 0
             for s, src in sels:
@@ -206,7 +208,11 @@ class VideoTrainer:
                 self._new_conv(self._src(b, src), s, "relu", c[..., off:off + co], tb)
                 off += co
             # upconv_concat (unet_simple.py:30-42): resize -> conv (no bias) -> relu -> concat -> BN
-            r = ops.resize_bilinear(b[prev], L[lv], out=b[RBUF[up]])
+            r = b[RBUF[up]]
+            if isinstance(r, ops.SourceConcat):  # upconv4 on the towers' conv5_3 (tower-major)
+                ops.resize_bilinear(b[prev].base, L[lv], out=r.base)
+            else:
+                ops.resize_bilinear(b[prev], L[lv], out=r)
             ops.conv3x3(r, m.convs[up], "relu", out=c[..., off:width], affine=False)
             mean, var = tb["st_" + up]
             ops.bn_stats(c, mean, var)
@@ -223,7 +229,7 @@ class VideoTrainer:
         ops.bn_backward(z, dy, mask, mean, var, self.P[scope, "gamma"], EPS, dx=dz,
                         dgamma=self.G[scope, "gamma"], dbeta=self.G[scope, "beta"])
         ops.bn_backward(None, dz, None, None, None, None, dbeta=self.G[scope, "b"])
-        ops.conv_wgrad(x_in, dz, self.G[scope, "w"])
+        ops.conv_wgrad(x_in, dz, self.G[scope, "w"], mfma=self._mfma_wgrad)
         if dgrad_out is not None:
             ops.conv3x3(dz, self.dconv[scope], "none", out=dgrad_out, affine=False)
         return dz
@@ -246,7 +252,7 @@ class VideoTrainer:
                 self._conv_backward(s, self._src(b, src), dcat[..., off:off + co], c[..., off:off + co], tb)
                 off += co
             du = ops.relu_backward(dcat[..., off:width], c[..., off:width], tb["du_" + up])
-            ops.conv_wgrad(b[RBUF[up]], du, self.G[up, "w"])
+            ops.conv_wgrad(b[RBUF[up]], du, self.G[up, "w"], mfma=self._mfma_wgrad)
             if up in DGRAD:
                 ops.conv3x3(du, self.dconv[up], "none", out=tb["dr_" + up], affine=False)
                 dout = ops.resize_backward(tb["dr_" + up], tb["dprev_" + up])

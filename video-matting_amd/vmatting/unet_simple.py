@@ -71,49 +71,62 @@ class UNetSimple:
         self._ws, self._key = None, None
 
     def _buffers(self, n, h, w):
+        """Activation buffers for an [n,h,w] batch.  The three towers run as ONE batch of 3n frames (tower t =
+        frames t*n .. t*n+n-1 of every t_* buffer); the per-level concats of create_model (unet_simple.py:153-168)
+        are ops.SourceConcat views of those tower-major buffers, read as three sources by the select convs."""
         if self._key == (n, h, w):
             return self._ws
         L = _levels(h, w)
         T, dev = self.dtype, self.device
-        Z = lambda lv, c, dt=T: torch.zeros((n, L[lv][0], L[lv][1], c), dtype=dt, device=dev)  # noqa: E731
-        b = {"in": [Z(0, 8) for _ in range(3)], "in9": Z(0, 16)}
+        Z = lambda lv, c, dt=T, k=1: torch.zeros((k * n, L[lv][0], L[lv][1], c), dtype=dt, device=dev)  # noqa: E731
+        b = {"tin": Z(0, 8, k=3), "in9": Z(0, 16)}
         widths = {"conv1_1": (0, 64), "conv1_2": (0, 64), "conv2_1": (1, 128), "conv2_2": (1, 128),
                   "conv3_1": (2, 256), "conv3_2": (2, 256), "conv3_3": (2, 256), "conv4_1": (3, 512),
                   "conv4_2": (3, 512), "conv4_3": (3, 512), "conv5_1": (4, 512), "conv5_2": (4, 512),
                   "conv5_3": (4, 512)}
         for k, (lv, c) in widths.items():
-            b["cat_" + k] = Z(lv, 3 * c)
+            b["t_" + k] = Z(lv, c, k=3)
+            b["cat_" + k] = ops.SourceConcat(b["t_" + k], 3)
         for i, c in enumerate((64, 128, 256, 512)):
-            b["pool%d" % (i + 1)] = [Z(i + 1, c) for _ in range(3)]
-        b.update(up4=Z(3, 96), up4n=Z(3, 96), r4=Z(3, 1536), c4=Z(3, 48),
-                 up3=Z(2, 48), up3n=Z(2, 48), r3=Z(2, 48), c3=Z(2, 24),
-                 up2=Z(1, 32), up2n=Z(1, 32), r2=Z(1, 24), c2=Z(1, 32),
-                 up1=Z(0, 32), up1n=Z(0, 32), r1=Z(0, 32), c1=Z(0, 32),
+            b["tpool%d" % (i + 1)] = Z(i + 1, c, k=3)
+        # the upconv_concat buffers (select outputs + upconv relu, the input of the upconv BN) are f32: with batch
+        # statistics, bf16 rounding of them feeds the BN backward's x-hat projection and costs the select gammas'
+        # gradients 4-14x their f64 sensitivity (tests/test_gpu_train.py::test_train_step_bf16_gradients)
+        F = torch.float32
+        b.update(up4=Z(3, 96, F), up4n=Z(3, 96), r4=ops.SourceConcat(Z(3, 512, k=3), 3), c4=Z(3, 48),
+                 up3=Z(2, 48, F), up3n=Z(2, 48), r3=Z(2, 48), c3=Z(2, 24),
+                 up2=Z(1, 32, F), up2n=Z(1, 32), r2=Z(1, 24), c2=Z(1, 32),
+                 up1=Z(0, 32, F), up1n=Z(0, 32), r1=Z(0, 32), c1=Z(0, 32),
                  logits=Z(0, 1, torch.float32), out=Z(0, 1, torch.float32))
         self._ws, self._key = b, (n, h, w)
         return b
 
-    def _tower(self, b, t):
-        """Tower t of create_model (vgg1/2/3 on cmp/bg/diff) into slice t of every concat buffer."""
+    def _towers(self, b):
+        """The three frozen towers of create_model (vgg1/2/3 on cmp/bg/diff, unet_simple.py:57-89, 148-152) as one
+        batch-3n VGG16 pass over b['tin'] (the towers share weights); 2x2 pools fused into the conv epilogue."""
         V = self.vgg.convs
-        sl = lambda k, c: b["cat_" + k][..., t * c:(t + 1) * c]  # noqa: E731
-        ops.conv3x3(b["in"][t][..., :3], V["conv1_1"], "relu", out=sl("conv1_1", 64))
-        ops.conv3x3(sl("conv1_1", 64), V["conv1_2"], "relu", out=sl("conv1_2", 64))
-        ops.maxpool2x2(sl("conv1_2", 64), out=b["pool1"][t])
-        ops.conv3x3(b["pool1"][t], V["conv2_1"], "relu", out=sl("conv2_1", 128))
-        ops.conv3x3(sl("conv2_1", 128), V["conv2_2"], "relu", out=sl("conv2_2", 128))
-        ops.maxpool2x2(sl("conv2_2", 128), out=b["pool2"][t])
-        ops.conv3x3(b["pool2"][t], V["conv3_1"], "relu", out=sl("conv3_1", 256))
-        ops.conv3x3(sl("conv3_1", 256), V["conv3_2"], "relu", out=sl("conv3_2", 256))
-        ops.conv3x3(sl("conv3_2", 256), V["conv3_3"], "relu", out=sl("conv3_3", 256))
-        ops.maxpool2x2(sl("conv3_3", 256), out=b["pool3"][t])
-        ops.conv3x3(b["pool3"][t], V["conv4_1"], "relu", out=sl("conv4_1", 512))
-        ops.conv3x3(sl("conv4_1", 512), V["conv4_2"], "relu", out=sl("conv4_2", 512))
-        ops.conv3x3(sl("conv4_2", 512), V["conv4_3"], "relu", out=sl("conv4_3", 512))
-        ops.maxpool2x2(sl("conv4_3", 512), out=b["pool4"][t])
-        ops.conv3x3(b["pool4"][t], V["conv5_1"], "relu", out=sl("conv5_1", 512))
-        ops.conv3x3(sl("conv5_1", 512), V["conv5_2"], "relu", out=sl("conv5_2", 512))
-        ops.conv3x3(sl("conv5_2", 512), V["conv5_3"], "relu", out=sl("conv5_3", 512))
+        t = lambda k: b["t_" + k]  # noqa: E731
+        ops.conv3x3(b["tin"][..., :3], V["conv1_1"], "relu", out=t("conv1_1"))
+        ops.conv3x3(t("conv1_1"), V["conv1_2"], "relu", out=t("conv1_2"), pool_out=b["tpool1"])
+        ops.conv3x3(b["tpool1"], V["conv2_1"], "relu", out=t("conv2_1"))
+        ops.conv3x3(t("conv2_1"), V["conv2_2"], "relu", out=t("conv2_2"), pool_out=b["tpool2"])
+        ops.conv3x3(b["tpool2"], V["conv3_1"], "relu", out=t("conv3_1"))
+        ops.conv3x3(t("conv3_1"), V["conv3_2"], "relu", out=t("conv3_2"))
+        ops.conv3x3(t("conv3_2"), V["conv3_3"], "relu", out=t("conv3_3"), pool_out=b["tpool3"])
+        ops.conv3x3(b["tpool3"], V["conv4_1"], "relu", out=t("conv4_1"))
+        ops.conv3x3(t("conv4_1"), V["conv4_2"], "relu", out=t("conv4_2"))
+        ops.conv3x3(t("conv4_2"), V["conv4_3"], "relu", out=t("conv4_3"), pool_out=b["tpool4"])
+        ops.conv3x3(b["tpool4"], V["conv5_1"], "relu", out=t("conv5_1"))
+        ops.conv3x3(t("conv5_1"), V["conv5_2"], "relu", out=t("conv5_2"))
+        ops.conv3x3(t("conv5_2"), V["conv5_3"], "relu", out=t("conv5_3"))
+
+    def load_inputs(self, b, xs):
+        """cmp / bg / diff (f32 device tensors) into the towers' batch (tower t = frames t*n..) and into the 9-channel
+        layers['conv1'][0] = concat(cmp, bg, diff) (unet_simple.py:148-152)."""
+        n = xs[0].shape[0]
+        for t in range(3):
+            ops.convert(xs[t], b["tin"][t * n:(t + 1) * n])
+            ops.convert(xs[t], b["in9"][..., 3 * t:3 * t + 3])
 
     def forward(self, cmp, bg, diff, phase=None):
         ph = self.phase if phase is None else bool(phase)
@@ -124,10 +137,8 @@ class UNetSimple:
         b = self._buffers(n, h, w)
         L = _levels(h, w)
         C, B = self.convs, self.bn
-        for t in range(3):
-            ops.convert(xs[t], b["in"][t])
-            ops.convert(xs[t], b["in9"][..., 3 * t:3 * t + 3])  # layers['conv1'][0] = concat(cmp, bg, diff)
-            self._tower(b, t)
+        self.load_inputs(b, xs)
+        self._towers(b)
         R = lambda x, k, out: conv_bn(x, C[k], B[k], ph, "relu", out)  # noqa: E731
         # level 4
         for i in range(3):
@@ -158,7 +169,10 @@ class UNetSimple:
 
     def _upconv(self, prev, size, scope, rbuf, up_slice, cat, catn, phase):
         """upconv_concat (unet_simple.py:30-42): resize -> conv (no bias) -> relu -> concat -> BN."""
-        ops.resize_bilinear(prev, size, out=rbuf)
+        if isinstance(prev, ops.SourceConcat):  # upconv4 on the towers' conv5_3: resize the tower-major batch
+            ops.resize_bilinear(prev.base, size, out=rbuf.base)
+        else:
+            ops.resize_bilinear(prev, size, out=rbuf)
         ops.conv3x3(rbuf, self.convs[scope], "relu", out=up_slice, affine=False)
         self.bn[scope](cat, phase, out=catn)
 
