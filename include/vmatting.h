@@ -310,9 +310,16 @@ size_t vm_bn_backward_workspace_bytes(int channels);
 int vm_bn_backward_nhwc(const vm_tensor* x, const vm_tensor* dy, const vm_tensor* y, const float* mean,
                         const float* var, const float* gamma, float eps, vm_tensor* dx, float* dgamma, float* dbeta,
                         void* work, void* stream);
+/* The same with dx2 (optional, may be NULL): a second copy of dx in dx2's dtype (the bf16 operand of the
+ * data-gradient conv in the bf16 training path, written in the same pass). */
+int vm_bn_backward_ex_nhwc(const vm_tensor* x, const vm_tensor* dy, const vm_tensor* y, const float* mean,
+                           const float* var, const float* gamma, float eps, vm_tensor* dx, vm_tensor* dx2,
+                           float* dgamma, float* dbeta, void* work, void* stream);
 
 /* tf.nn.relu gradient: dx = dy * (y > 0); dx f32. */
 int vm_relu_backward_nhwc(const vm_tensor* dy, const vm_tensor* y, vm_tensor* dx, void* stream);
+/* The same with an optional second (e.g. bf16) copy of dx. */
+int vm_relu_backward_ex_nhwc(const vm_tensor* dy, const vm_tensor* y, vm_tensor* dx, vm_tensor* dx2, void* stream);
 
 /* Adjoint of vm_resize_bilinear_tf1_nhwc (tf.image.resize_images, unet_simple.py:33): dy [n,oh,ow,c] (f32 view) ->
  * dx contiguous f32 [n,ih,iw,c] (overwritten). */

@@ -159,7 +159,7 @@ static void launch_bn_bwd_partial(const V& x, const V& dy, const V& y, const flo
 
 template <bool MASK>
 __global__ void bn_bwd_apply(V x, V dy, V y, const float* mean, const float* var, const float* gamma, float eps,
-                             const float* sum_g, const float* sum_gx, V dx) {
+                             const float* sum_g, const float* sum_gx, V dx, V dx2) {
   const long M = (long)dy.n * dy.h * dy.w;
   const long total = M * dy.c;
   const float invM = 1.0f / (float)M;
@@ -170,16 +170,20 @@ __global__ void bn_bwd_apply(V x, V dy, V y, const float* mean, const float* var
     const float xh = (ld(x, p, c) - mean[c]) * r;
     const float g = grad_in<MASK>(dy, y, p, c);
     const float gm = gamma ? gamma[c] : 1.f;
-    st(dx, p, c, gm * r * (g - sum_g[c] * invM - xh * sum_gx[c] * invM));
+    const float v = gm * r * (g - sum_g[c] * invM - xh * sum_gx[c] * invM);
+    st(dx, p, c, v);
+    if (dx2.p) st(dx2, p, c, v);  // the bf16 copy the data-gradient conv reads
   }
 }
 
-__global__ void relu_bwd_kernel(V dy, V y, V dx) {
+__global__ void relu_bwd_kernel(V dy, V y, V dx, V dx2) {
   const long total = (long)dy.n * dy.h * dy.w * dy.c;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
     const int c = (int)(i % dy.c);
     const long p = i / dy.c;
-    st(dx, p, c, ld(y, p, c) > 0.f ? ld(dy, p, c) : 0.f);
+    const float v = ld(y, p, c) > 0.f ? ld(dy, p, c) : 0.f;
+    st(dx, p, c, v);
+    if (dx2.p) st(dx2, p, c, v);
   }
 }
 
@@ -839,6 +843,12 @@ static bool same_shape(const vm_tensor* a, const vm_tensor* b) {
 using namespace vm;
 using namespace vm::trn;
 
+extern "C" int vm_bn_backward_ex_nhwc(const vm_tensor* x, const vm_tensor* dy, const vm_tensor* y, const float* mean,
+                                      const float* var, const float* gamma, float eps, vm_tensor* dx, vm_tensor* dx2,
+                                      float* dgamma, float* dbeta, void* work, void* stream);
+extern "C" int vm_relu_backward_ex_nhwc(const vm_tensor* dy, const vm_tensor* y, vm_tensor* dx, vm_tensor* dx2,
+                                        void* stream);
+
 extern "C" int vm_matting_loss_backward(const float* pred, const float* gt, const float* raw_fg, const float* bg,
                                         const float* cmp, long pixels, float* dlogits, void* stream) {
   if (!pred || !gt || !raw_fg || !bg || !cmp || !dlogits || pixels <= 0)
@@ -856,6 +866,14 @@ extern "C" size_t vm_bn_backward_workspace_bytes(int channels) {
 extern "C" int vm_bn_backward_nhwc(const vm_tensor* x, const vm_tensor* dy, const vm_tensor* y, const float* mean,
                                    const float* var, const float* gamma, float eps, vm_tensor* dx, float* dgamma,
                                    float* dbeta, void* work, void* stream) {
+  return vm_bn_backward_ex_nhwc(x, dy, y, mean, var, gamma, eps, dx, nullptr, dgamma, dbeta, work, stream);
+}
+
+extern "C" int vm_bn_backward_ex_nhwc(const vm_tensor* x, const vm_tensor* dy, const vm_tensor* y, const float* mean,
+                                      const float* var, const float* gamma, float eps, vm_tensor* dx, vm_tensor* dx2,
+                                      float* dgamma, float* dbeta, void* work, void* stream) {
+  if (dx2 && (!dx || !ok_view(dx2) || !same_shape(dx2, dy)))
+    return fail(VM_EINVAL, "bn_backward: dx2 needs dx and an [n,h,w,c] view");
   if (!ok_view(dy) || dy->dtype != VM_F32 || !work) return fail(VM_EINVAL, "bn_backward: bad dy / workspace");
   if (x && (!ok_view(x) || !same_shape(x, dy) || !mean || !var)) return fail(VM_EINVAL, "bn_backward: bad x");
   if (y && (!ok_view(y) || !same_shape(y, dy))) return fail(VM_EINVAL, "bn_backward: bad relu mask y");
@@ -883,19 +901,26 @@ extern "C" int vm_bn_backward_nhwc(const vm_tensor* x, const vm_tensor* dy, cons
   const long work_n = (long)dy->n * dy->h * dy->w * C;
   if (y)
     hipLaunchKernelGGL(bn_bwd_apply<true>, dim3(grid_for(work_n, 256)), dim3(256), 0, st, xv, dyv, yv, mean, var,
-                       gamma, eps, sg, sgx, mk(dx));
+                       gamma, eps, sg, sgx, mk(dx), dx2 ? mk(dx2) : V{});
   else
     hipLaunchKernelGGL(bn_bwd_apply<false>, dim3(grid_for(work_n, 256)), dim3(256), 0, st, xv, dyv, yv, mean, var,
-                       gamma, eps, sg, sgx, mk(dx));
+                       gamma, eps, sg, sgx, mk(dx), dx2 ? mk(dx2) : V{});
   return check_launch("bn_backward_apply");
 }
 
 extern "C" int vm_relu_backward_nhwc(const vm_tensor* dy, const vm_tensor* y, vm_tensor* dx, void* stream) {
-  if (!ok_view(dy) || !ok_view(y) || !ok_view(dx) || !same_shape(dy, y) || !same_shape(dy, dx))
+  return vm_relu_backward_ex_nhwc(dy, y, dx, nullptr, stream);
+}
+
+extern "C" int vm_relu_backward_ex_nhwc(const vm_tensor* dy, const vm_tensor* y, vm_tensor* dx, vm_tensor* dx2,
+                                        void* stream) {
+  if (!ok_view(dy) || !ok_view(y) || !ok_view(dx) || !same_shape(dy, y) || !same_shape(dy, dx) ||
+      (dx2 && (!ok_view(dx2) || !same_shape(dy, dx2))))
     return fail(VM_EINVAL, "relu_backward: bad tensors");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const long n = (long)dy->n * dy->h * dy->w * dy->c;
-  hipLaunchKernelGGL(relu_bwd_kernel, dim3(grid_for(n, 256)), dim3(256), 0, st, mk(dy), mk(y), mk(dx));
+  hipLaunchKernelGGL(relu_bwd_kernel, dim3(grid_for(n, 256)), dim3(256), 0, st, mk(dy), mk(y), mk(dx),
+                     dx2 ? mk(dx2) : V{});
   return check_launch("relu_backward");
 }
 

@@ -554,22 +554,23 @@ def matting_loss_backward(pred, gt, raw_fg, in_bg, in_cmp, out=None):
     return out
 
 
-def bn_backward(x, dy, y, mean, var, gamma, eps=1e-3, dx=None, dgamma=None, dbeta=None):
+def bn_backward(x, dy, y, mean, var, gamma, eps=1e-3, dx=None, dgamma=None, dbeta=None, dx2=None):
     """Gradient of tf.contrib batch_norm(is_training=True) (+ the relu after it when ``y`` is given).
-    x None: only dbeta = channel sum of dy (a bias gradient)."""
+    x None: only dbeta = channel sum of dy (a bias gradient).  dx2: optional second copy of dx (e.g. bf16)."""
     c = dy.shape[-1]
-    views = [None if t is None else nhwc(t) for t in (x, dy, y, dx)]
+    views = [None if t is None else nhwc(t) for t in (x, dy, y, dx, dx2)]
     ref = lambda v: None if v is None else ctypes.byref(v)  # noqa: E731
     ws = _workspace(lib().vm_bn_backward_workspace_bytes(c), dy.device)
-    check(lib().vm_bn_backward_nhwc(ref(views[0]), ref(views[1]), ref(views[2]), _ptr(mean), _ptr(var), _ptr(gamma),
-                                    float(eps), ref(views[3]), _ptr(dgamma), _ptr(dbeta), _ptr(ws), stream_handle()),
-          "bn_backward")
+    check(lib().vm_bn_backward_ex_nhwc(ref(views[0]), ref(views[1]), ref(views[2]), _ptr(mean), _ptr(var),
+                                       _ptr(gamma), float(eps), ref(views[3]), ref(views[4]), _ptr(dgamma),
+                                       _ptr(dbeta), _ptr(ws), stream_handle()), "bn_backward")
     return dx
 
 
-def relu_backward(dy, y, dx):
+def relu_backward(dy, y, dx, dx2=None):
     dv, yv, xv = nhwc(dy), nhwc(y), nhwc(dx)
-    check(lib().vm_relu_backward_nhwc(ctypes.byref(dv), ctypes.byref(yv), ctypes.byref(xv), stream_handle()),
+    x2 = ctypes.byref(nhwc(dx2)) if dx2 is not None else None
+    check(lib().vm_relu_backward_ex_nhwc(ctypes.byref(dv), ctypes.byref(yv), ctypes.byref(xv), x2, stream_handle()),
           "relu_backward")
     return dx
 

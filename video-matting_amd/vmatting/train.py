@@ -101,13 +101,22 @@ class VideoTrainer:
             parallel.broadcast_tensors([self.flat], src=0)
             for pc in self.model.convs.values():
                 pc.repack()
-        # data-gradient filters: flipped / transposed f32 copies, packed for the forward conv kernels
-        self.dconv, self._wflip = {}, {}
+        # data-gradient filters: flipped / transposed f32 copies, packed for the forward conv kernels (fp32 path); the
+        # bf16 path packs them bf16 with the gradient channels padded to 32, so the data-gradient convs run on the
+        # patch-reuse MFMA kernel from bf16 copies of the gradients (bn_backward / relu_backward write them)
+        self.dconv, self._wflip, self.dconv16 = {}, {}, {}
+        bf16 = self.model.dtype == torch.bfloat16
         for scope in DGRAD:
             pc = self.model.convs[scope]
             self._wflip[scope] = torch.empty((3, 3, pc.cout, pc.cin), dtype=torch.float32, device=dev)
             ops.flip_weights(pc.w_hwio, self._wflip[scope])
-            self.dconv[scope] = ops.PackedConv(self._wflip[scope], None, "fp32", dev)
+            if bf16:
+                cp = (pc.cout + 31) // 32 * 32
+                wpad = torch.zeros((3, 3, cp, pc.cin), dtype=torch.float32, device=dev)
+                wpad[:, :, :pc.cout].copy_(self._wflip[scope])
+                self.dconv16[scope] = (ops.PackedConv(wpad, None, "bf16", dev), wpad)
+            else:
+                self.dconv[scope] = ops.PackedConv(self._wflip[scope], None, "fp32", dev)
         # bf16: the patch-reuse conv kernel needs cout % 8 == 0, so the narrow new_convs (select2_* cout 4,
         # select1_* cout 2, output cout 1) run on zero-padded copies of their filters into 8-channel buffers
         self._padconv = {}
@@ -171,6 +180,11 @@ class VideoTrainer:
             tb["z_output"] = F(0, 1)
         tb["st_output"] = st(1)
         tb["dz_output"] = torch.zeros((n, h, w, 8), dtype=torch.float32, device=dev)[..., :1]
+        # bf16 copies of the gradients the data-gradient convs read, channels zero-padded to 32
+        for scope, (pc16, _) in self.dconv16.items():
+            lv = 0 if scope == "output" else {"conv1": 0, "conv2": 1, "conv3": 2, "conv4": 3, "upconv1": 0,
+                                              "upconv2": 1, "upconv3": 2}[scope]
+            tb["g16_" + scope] = torch.zeros((n, L[lv][0], L[lv][1], pc16.cin), dtype=torch.bfloat16, device=dev)
         self._tb, self._key = tb, (n, h, w)
         return tb
 
@@ -226,12 +240,17 @@ class VideoTrainer:
     def _conv_backward(self, scope, x_in, dy, mask, tb, dgrad_out=None):
         """BN(+relu) backward into dz, then bias / filter gradients, optionally the data gradient of x_in."""
         z, dz, (mean, var) = tb["z_" + scope], tb["dz_" + scope], tb["st_" + scope]
+        g16 = tb["g16_" + scope] if dgrad_out is not None and scope in self.dconv16 else None
         ops.bn_backward(z, dy, mask, mean, var, self.P[scope, "gamma"], EPS, dx=dz,
-                        dgamma=self.G[scope, "gamma"], dbeta=self.G[scope, "beta"])
+                        dgamma=self.G[scope, "gamma"], dbeta=self.G[scope, "beta"],
+                        dx2=None if g16 is None else g16[..., :dz.shape[-1]])
         ops.bn_backward(None, dz, None, None, None, None, dbeta=self.G[scope, "b"])
         ops.conv_wgrad(x_in, dz, self.G[scope, "w"], mfma=self._mfma_wgrad)
         if dgrad_out is not None:
-            ops.conv3x3(dz, self.dconv[scope], "none", out=dgrad_out, affine=False)
+            if g16 is not None:
+                ops.conv3x3(g16, self.dconv16[scope][0], "none", out=dgrad_out, affine=False)
+            else:
+                ops.conv3x3(dz, self.dconv[scope], "none", out=dgrad_out, affine=False)
         return dz
 
     def backward(self, gt, raw_fg, bg, cmp):
@@ -251,10 +270,15 @@ class VideoTrainer:
                 co = m.convs[s].cout
                 self._conv_backward(s, self._src(b, src), dcat[..., off:off + co], c[..., off:off + co], tb)
                 off += co
-            du = ops.relu_backward(dcat[..., off:width], c[..., off:width], tb["du_" + up])
+            g16 = tb.get("g16_" + up)
+            du = ops.relu_backward(dcat[..., off:width], c[..., off:width], tb["du_" + up],
+                                   dx2=None if g16 is None else g16[..., :width - off])
             ops.conv_wgrad(b[RBUF[up]], du, self.G[up, "w"], mfma=self._mfma_wgrad)
             if up in DGRAD:
-                ops.conv3x3(du, self.dconv[up], "none", out=tb["dr_" + up], affine=False)
+                if g16 is not None:
+                    ops.conv3x3(g16, self.dconv16[up][0], "none", out=tb["dr_" + up], affine=False)
+                else:
+                    ops.conv3x3(du, self.dconv[up], "none", out=tb["dr_" + up], affine=False)
                 dout = ops.resize_backward(tb["dr_" + up], tb["dprev_" + up])
 
     # ------------------------------------------------------------------------------------------- update
@@ -272,7 +296,12 @@ class VideoTrainer:
             pc.repack()
         for scope in DGRAD:
             ops.flip_weights(self.model.convs[scope].w_hwio, self._wflip[scope])
-            self.dconv[scope].repack()
+            if scope in self.dconv16:
+                pc16, wpad = self.dconv16[scope]
+                wpad[:, :, :self._wflip[scope].shape[2]].copy_(self._wflip[scope])
+                pc16.repack()
+            else:
+                self.dconv[scope].repack()
         self._sync_padded()
 
     def step(self, cmp, bg, warped, gt, raw_fg):
