@@ -311,10 +311,12 @@ int vm_bn_backward_nhwc(const vm_tensor* x, const vm_tensor* dy, const vm_tensor
                         const float* var, const float* gamma, float eps, vm_tensor* dx, float* dgamma, float* dbeta,
                         void* work, void* stream);
 /* The same with dx2 (optional, may be NULL): a second copy of dx in dx2's dtype (the bf16 operand of the
- * data-gradient conv in the bf16 training path, written in the same pass). */
+ * data-gradient conv in the bf16 training path, written in the same pass); dbias (optional, needs x): the
+ * gradient of a bias added before the BN (new_conv's conv bias, unet_simple.py:23-25) = sum of dx over the
+ * pixels, from the same double sums (zero in exact arithmetic). */
 int vm_bn_backward_ex_nhwc(const vm_tensor* x, const vm_tensor* dy, const vm_tensor* y, const float* mean,
                            const float* var, const float* gamma, float eps, vm_tensor* dx, vm_tensor* dx2,
-                           float* dgamma, float* dbeta, void* work, void* stream);
+                           float* dgamma, float* dbeta, float* dbias, void* work, void* stream);
 
 /* tf.nn.relu gradient: dx = dy * (y > 0); dx f32. */
 int vm_relu_backward_nhwc(const vm_tensor* dy, const vm_tensor* y, vm_tensor* dx, void* stream);

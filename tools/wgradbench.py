@@ -19,6 +19,9 @@ SHAPES = [("select4", 40, 1536, 16), ("upconv4", 40, 1536, 48), ("conv4", 40, 96
 
 def main():
     iters = int(sys.argv[1]) if len(sys.argv) > 1 else 10
+    if os.environ.get("WGRAD_VARIANT"):
+        from vmatting import _lib
+        _lib.set_option("wgrad_variant", int(os.environ["WGRAD_VARIANT"]))
     tot = [0.0, 0.0]
     for name, s, cin, cout in SHAPES:
         cs = (cin + 15) // 16 * 16

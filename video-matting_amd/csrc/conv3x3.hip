@@ -2309,6 +2309,7 @@ extern "C" int vm_set_option(const char* key, long value) {
     g_glds_rb = value;
     return VM_OK;
   }
+  if (train_set_option(key, value)) return VM_OK;
   return fail(VM_EINVAL, "set_option: unknown key '%s'", key);
 }
 

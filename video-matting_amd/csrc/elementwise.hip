@@ -354,17 +354,22 @@ static int launch_bn_partial(const View& xv, double* part, hipStream_t st) {
   return nb;
 }
 
-__global__ void bn_apply_kernel(View x, View y, const float* mean, const float* var, const float* gamma,
-                                const float* beta, float eps, int act) {
-  const long total = (long)x.n * x.h * x.w * x.c;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const int c = (int)(i % x.c);
-    const long p = i / x.c;
-    const float m = mean ? mean[c] : 0.f;
-    const float v = var ? var[c] : 1.f;
-    const float g = gamma ? gamma[c] : 1.f;
-    const float b = beta ? beta[c] : 0.f;
-    float t = (ldv(x, p, c) - m) * (1.0f / sqrtf(v + eps)) * g + b;
+// CP (power of two >= C, at most 64) lanes per pixel, channel block blockIdx.y: each lane keeps one channel's
+// constants in registers and no element index is divided
+template <int CP>
+__global__ __launch_bounds__(256) void bn_apply_kernel(View x, View y, const float* mean, const float* var,
+                                                       const float* gamma, const float* beta, float eps, int act) {
+  const long M = (long)x.n * x.h * x.w;
+  const int c = blockIdx.y * CP + (threadIdx.x & (CP - 1));
+  if (c >= x.c) return;
+  const float m = mean ? mean[c] : 0.f;
+  const float v = var ? var[c] : 1.f;
+  const float g = gamma ? gamma[c] : 1.f;
+  const float b = beta ? beta[c] : 0.f;
+  const float r = 1.0f / sqrtf(v + eps);
+  const long step = (long)gridDim.x * (blockDim.x / CP);
+  for (long p = (long)blockIdx.x * (blockDim.x / CP) + threadIdx.x / CP; p < M; p += step) {
+    float t = (ldv(x, p, c) - m) * r * g + b;
     t = act == VM_ACT_RELU ? fmaxf(t, 0.f) : act == VM_ACT_SIGMOID ? sigmoid_precise(t) : t;
     stv(y, p, c, t);
   }
@@ -477,9 +482,18 @@ extern "C" int vm_bn_apply_nhwc(const vm_tensor* x, vm_tensor* y, const float* m
   if (!valid_tensor(x) || !valid_tensor(y)) return fail(VM_EINVAL, "bn_apply: invalid tensor");
   if (y->n != x->n || y->h != x->h || y->w != x->w || y->c != x->c) return fail(VM_EINVAL, "bn_apply: shape mismatch");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  const long work = (long)x->n * x->h * x->w * x->c;
-  hipLaunchKernelGGL(bn_apply_kernel, dim3(grid_for(work, 256)), dim3(256), 0, st, view(x), view(y), mean, var, gamma,
-                     beta, eps, act);
+  const long M = (long)x->n * x->h * x->w;
+  const int C = x->c;
+  const int cp = C > 32 ? 64 : C > 16 ? 32 : C > 8 ? 16 : C > 4 ? 8 : C > 2 ? 4 : C > 1 ? 2 : 1;
+  const long px = (M + 256 / cp - 1) / (256 / cp);
+  const dim3 grid((unsigned)(px < 4096 ? px : 4096), (unsigned)((C + cp - 1) / cp));
+  const View xv = view(x), yv = view(y);
+  switch (cp) {
+#define VM_BA(CP) \
+  case CP: hipLaunchKernelGGL((bn_apply_kernel<CP>), grid, dim3(256), 0, st, xv, yv, mean, var, gamma, beta, eps, act); break;
+    VM_BA(1) VM_BA(2) VM_BA(4) VM_BA(8) VM_BA(16) VM_BA(32) VM_BA(64)
+#undef VM_BA
+  }
   return check_launch("bn_apply");
 }
 

@@ -18,6 +18,8 @@
 //   relu_backward   dy * (y > 0)
 //   adam            TF ApplyAdam: m += (g-m)(1-b1); v += (g^2-v)(1-b2); var -= m*lr_t/(sqrt(v)+eps)
 
+#include <cstring>
+
 #include "vm_common.h"
 
 namespace vm {
@@ -94,49 +96,67 @@ template <bool MASK, int CP>
 __global__ __launch_bounds__(256) void bn_bwd_partial(V x, V dy, V y, const float* mean, const float* var, float eps,
                                                       double* part, int nblk) {
   constexpr int PPW = 64 / CP;
-  __shared__ double sh[2][4][64];
+  __shared__ double sh[3][4][64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int c = blockIdx.x * CP + (lane % CP);
   const long M = (long)dy.n * dy.h * dy.w;
-  double s1 = 0.0, s2 = 0.0;
+  double s1 = 0.0, s2 = 0.0, s3 = 0.0;
   if (c < dy.c) {
     const float m = x.p ? mean[c] : 0.f;
     const float r = x.p ? 1.0f / sqrtf(var[c] + eps) : 0.f;
     for (long p = ((long)blockIdx.y * 4 + wave) * PPW + lane / CP; p < M; p += (long)nblk * 4 * PPW) {
       const float g = grad_in<MASK>(dy, y, p, c);
       s1 += g;
-      if (x.p) s2 += (double)g * (double)((ld(x, p, c) - m) * r);
+      if (x.p) {
+        const float xh = (ld(x, p, c) - m) * r;
+        s2 += (double)g * (double)xh;
+        s3 += (double)xh;
+      }
     }
   }
   sh[0][wave][lane] = s1;
   sh[1][wave][lane] = s2;
+  sh[2][wave][lane] = s3;
   __syncthreads();
   if ((int)threadIdx.x < CP && c < dy.c) {
-    s1 = s2 = 0.0;
+    s1 = s2 = s3 = 0.0;
     for (int w = 0; w < 4; ++w)
       for (int k = 0; k < PPW; ++k) {
         s1 += sh[0][w][k * CP + threadIdx.x];
         s2 += sh[1][w][k * CP + threadIdx.x];
+        s3 += sh[2][w][k * CP + threadIdx.x];
       }
     part[(long)blockIdx.y * dy.c + c] = s1;
     part[(long)nblk * dy.c + (long)blockIdx.y * dy.c + c] = s2;
+    part[2L * nblk * dy.c + (long)blockIdx.y * dy.c + c] = s3;
   }
 }
 
-__global__ __launch_bounds__(64) void bn_bwd_final(const double* part, int nblk, int C, float* sum_g, float* sum_gx) {
+// folds the partials; with dbias also the gradient of a bias added before the BN (new_conv's conv bias,
+// unet_simple.py:23-25): sum_p dx = gamma*rstd*(sum g - M*mean g - sum xhat * sum(g*xhat)/M), zero in exact
+// arithmetic (BN removes the bias), evaluated from the same double sums instead of a pass over dx
+__global__ __launch_bounds__(64) void bn_bwd_final(const double* part, int nblk, int C, float* sum_g, float* sum_gx,
+                                                   float* dbias, const float* gamma, const float* var, float eps,
+                                                   long M) {
   const int c = blockIdx.x, lane = threadIdx.x;
-  double s1 = 0.0, s2 = 0.0;
+  double s1 = 0.0, s2 = 0.0, s3 = 0.0;
   for (int b = lane; b < nblk; b += 64) {
     s1 += part[(long)b * C + c];
     s2 += part[(long)nblk * C + (long)b * C + c];
+    if (dbias) s3 += part[2L * nblk * C + (long)b * C + c];
   }
   for (int o = 32; o > 0; o >>= 1) {
     s1 += __shfl_down(s1, o);
     s2 += __shfl_down(s2, o);
+    s3 += __shfl_down(s3, o);
   }
   if (lane == 0) {
     if (sum_g) sum_g[c] = (float)s1;
     if (sum_gx) sum_gx[c] = (float)s2;
+    if (dbias) {
+      const double r = 1.0 / sqrt((double)var[c] + (double)eps), g = gamma ? gamma[c] : 1.0;
+      dbias[c] = (float)(g * r * (s1 - (double)M * (s1 / (double)M) - s3 * s2 / (double)M));
+    }
   }
 }
 
@@ -157,35 +177,62 @@ static void launch_bn_bwd_partial(const V& x, const V& dy, const V& y, const flo
   }
 }
 
-template <bool MASK>
-__global__ void bn_bwd_apply(V x, V dy, V y, const float* mean, const float* var, const float* gamma, float eps,
-                             const float* sum_g, const float* sum_gx, V dx, V dx2) {
+// elementwise passes over [M pixels x C channels]: CP (power of two >= C, at most 64) lanes per pixel, channel
+// block blockIdx.y, so a lane keeps one channel (its per-channel constants in registers) and no element index is
+// ever divided
+template <bool MASK, int CP>
+__global__ __launch_bounds__(256) void bn_bwd_apply(V x, V dy, V y, const float* mean, const float* var,
+                                                    const float* gamma, float eps, const float* sum_g,
+                                                    const float* sum_gx, V dx, V dx2) {
   const long M = (long)dy.n * dy.h * dy.w;
-  const long total = M * dy.c;
+  const int c = blockIdx.y * CP + (threadIdx.x & (CP - 1));
+  if (c >= dy.c) return;
   const float invM = 1.0f / (float)M;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const int c = (int)(i % dy.c);
-    const long p = i / dy.c;
-    const float r = 1.0f / sqrtf(var[c] + eps);
-    const float xh = (ld(x, p, c) - mean[c]) * r;
+  const float r = 1.0f / sqrtf(var[c] + eps);
+  const float m = mean[c];
+  const float k = (gamma ? gamma[c] : 1.f) * r;
+  const float sg = sum_g[c] * invM, sgx = sum_gx[c] * invM;
+  const long step = (long)gridDim.x * (blockDim.x / CP);
+  for (long p = (long)blockIdx.x * (blockDim.x / CP) + threadIdx.x / CP; p < M; p += step) {
+    const float xh = (ld(x, p, c) - m) * r;
     const float g = grad_in<MASK>(dy, y, p, c);
-    const float gm = gamma ? gamma[c] : 1.f;
-    const float v = gm * r * (g - sum_g[c] * invM - xh * sum_gx[c] * invM);
+    const float v = k * (g - sg - xh * sgx);
     st(dx, p, c, v);
     if (dx2.p) st(dx2, p, c, v);  // the bf16 copy the data-gradient conv reads
   }
 }
 
-__global__ void relu_bwd_kernel(V dy, V y, V dx, V dx2) {
-  const long total = (long)dy.n * dy.h * dy.w * dy.c;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const int c = (int)(i % dy.c);
-    const long p = i / dy.c;
+template <int CP>
+__global__ __launch_bounds__(256) void relu_bwd_kernel(V dy, V y, V dx, V dx2) {
+  const long M = (long)dy.n * dy.h * dy.w;
+  const int c = blockIdx.y * CP + (threadIdx.x & (CP - 1));
+  if (c >= dy.c) return;
+  const long step = (long)gridDim.x * (blockDim.x / CP);
+  for (long p = (long)blockIdx.x * (blockDim.x / CP) + threadIdx.x / CP; p < M; p += step) {
     const float v = ld(y, p, c) > 0.f ? ld(dy, p, c) : 0.f;
     st(dx, p, c, v);
     if (dx2.p) st(dx2, p, c, v);
   }
 }
+
+static int lanes_for(int C) { return C > 32 ? 64 : C > 16 ? 32 : C > 8 ? 16 : C > 4 ? 8 : C > 2 ? 4 : C > 1 ? 2 : 1; }
+
+// grid of an [M x C] packed-lane pass: x = pixel blocks (256/CP pixels each, capped), y = channel blocks
+static dim3 lanes_grid(long M, int C, int cp) {
+  const long px = (M + 256 / cp - 1) / (256 / cp);
+  return dim3((unsigned)(px < 4096 ? px : 4096), (unsigned)((C + cp - 1) / cp));
+}
+
+#define VM_CP_SWITCH(CP_, CALL) \
+  switch (CP_) {                \
+    case 1: CALL(1); break;     \
+    case 2: CALL(2); break;     \
+    case 4: CALL(4); break;     \
+    case 8: CALL(8); break;     \
+    case 16: CALL(16); break;   \
+    case 32: CALL(32); break;   \
+    default: CALL(64); break;   \
+  }
 
 // ---------------------------------------------------------------- resize backward (adjoint of resize_tf1)
 __device__ __forceinline__ void tf1c(int i, float scale, int in, int& lo, int& hi, float& lerp) {
@@ -418,8 +465,13 @@ __global__ __launch_bounds__(WG_NT) void wgrad_kernel(V x, V dy, float* partials
 // DY arrives f32 and is rounded to bf16 when staged (the bf16 training path's precision: bf16 operands, f32 sums).
 // The LDS images are swizzled so every transposed read (two 16-lane groups 8 rows apart per 32-lane half) is
 // conflict-free for any row base (tap shifts move it by 0..2 rows/pixels).
-constexpr int WM_TH = 4, WM_TW = 32, WM_PW = WM_TW + 2, WM_PPIX = (WM_TH + 2) * WM_PW;  // 204 patch pixels
-constexpr int WM_PROWS = (WM_PPIX + 15) / 16 * 16;                                   // 208: swizzle stays in range
+constexpr int WM_TW = 32, WM_PW = WM_TW + 2;
+// patch pixels of a TH x 32 tile with its halo, and the image rows allocated for them (a multiple of 16, so the row
+// swizzle stays in range)
+template <int TH>
+constexpr int wm_ppix() { return (TH + 2) * WM_PW; }
+template <int TH>
+constexpr int wm_prows() { return (wm_ppix<TH>() + 15) / 16 * 16; }
 
 struct WgArgs {
   const uint16_t* x;  // bf16 input view base (pixel 0, channel coff applied)
@@ -454,8 +506,9 @@ __device__ __forceinline__ bf16x8 wm_frag(const char* img, int r0, int c, int la
   return __builtin_bit_cast(bf16x8, v);
 }
 
-template <int NCI, int NCO, bool SX>
+template <int NCI, int NCO, bool SX, int TH>
 __global__ __launch_bounds__(256, 2) void wgrad_mfma_kernel(WgArgs a) {
+  constexpr int WM_TH = TH, WM_PPIX = wm_ppix<TH>(), WM_PROWS = wm_prows<TH>();
   constexpr int CIB = NCI * 16, COP = NCO * 16;
   constexpr int RBX = NCI == 1 ? 32 : NCI == 2 ? 64 : 128;
   constexpr int RBD = NCO == 1 ? 32 : NCO == 2 ? 64 : 128;
@@ -585,36 +638,40 @@ __global__ __launch_bounds__(256, 2) void wgrad_mfma_kernel(WgArgs a) {
     commit();
     __syncthreads();
     if (tile + gridDim.x < a.ntiles) issue(tile + gridDim.x);
-    // K-step: the 32 pixels of tile row `wave`; group g of the fragment holds pixels 8g..8g+7
-    if constexpr (SX) {
-      bf16x8 bd[NCO];
+    // K-steps: the 32 pixels of tile rows wave, wave+4, ...; group g of a fragment holds pixels 8g..8g+7
 #pragma unroll
-      for (int o = 0; o < NCO; ++o) bd[o] = wm_frag<RBD>(dimg, wave * WM_TW + 8 * g, o, lane);
+    for (int rr = 0; rr < TH / 4; ++rr) {
+      const int row = wave + 4 * rr;
+      if constexpr (SX) {
+        bf16x8 bd[NCO];
 #pragma unroll
-      for (int t = 0; t < 9; ++t) {
-        const int r0 = (wave + t / 3) * WM_PW + t % 3 + 8 * g;
+        for (int o = 0; o < NCO; ++o) bd[o] = wm_frag<RBD>(dimg, row * WM_TW + 8 * g, o, lane);
 #pragma unroll
-        for (int i = 0; i < NCI; ++i) {
-          const bf16x8 ax = wm_frag<RBX>(ximg, r0, i, lane);
+        for (int t = 0; t < 9; ++t) {
+          const int r0 = (row + t / 3) * WM_PW + t % 3 + 8 * g;
 #pragma unroll
-          for (int o = 0; o < NCO; ++o)
-            acc[t][i][o] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ax, bd[o], acc[t][i][o], 0, 0, 0);
+          for (int i = 0; i < NCI; ++i) {
+            const bf16x8 ax = wm_frag<RBX>(ximg, r0, i, lane);
+#pragma unroll
+            for (int o = 0; o < NCO; ++o)
+              acc[t][i][o] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ax, bd[o], acc[t][i][o], 0, 0, 0);
+          }
         }
-      }
-    } else {
-      bf16x8 ax[NCI];
+      } else {
+        bf16x8 ax[NCI];
 #pragma unroll
-      for (int i = 0; i < NCI; ++i) ax[i] = wm_frag<RBX>(ximg, wave * WM_TW + 8 * g, i, lane);
+        for (int i = 0; i < NCI; ++i) ax[i] = wm_frag<RBX>(ximg, row * WM_TW + 8 * g, i, lane);
 #pragma unroll
-      for (int t = 0; t < 9; ++t) {
-        // DY[q - off_t]: patch coordinates (row + 2 - kh, col + 2 - kw)
-        const int r0 = (wave + 2 - t / 3) * WM_PW + 2 - t % 3 + 8 * g;
+        for (int t = 0; t < 9; ++t) {
+          // DY[q - off_t]: patch coordinates (row + 2 - kh, col + 2 - kw)
+          const int r0 = (row + 2 - t / 3) * WM_PW + 2 - t % 3 + 8 * g;
 #pragma unroll
-        for (int o = 0; o < NCO; ++o) {
-          const bf16x8 bd = wm_frag<RBD>(dimg, r0, o, lane);
+          for (int o = 0; o < NCO; ++o) {
+            const bf16x8 bd = wm_frag<RBD>(dimg, r0, o, lane);
 #pragma unroll
-          for (int i = 0; i < NCI; ++i)
-            acc[t][i][o] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ax[i], bd, acc[t][i][o], 0, 0, 0);
+            for (int i = 0; i < NCI; ++i)
+              acc[t][i][o] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ax[i], bd, acc[t][i][o], 0, 0, 0);
+          }
         }
       }
     }
@@ -673,11 +730,11 @@ __global__ __launch_bounds__(256, 2) void wgrad_mfma_kernel(WgArgs a) {
   (void)MAIN;
 }
 
-template <int NCI, int NCO, bool SX>
+template <int NCI, int NCO, bool SX, int TH>
 constexpr int wgrad_mfma_lds() {
   constexpr int RBX = NCI == 1 ? 32 : NCI == 2 ? 64 : 128;
   constexpr int RBD = NCO == 1 ? 32 : NCO == 2 ? 64 : 128;
-  constexpr int XROWS = SX ? WM_PROWS : WM_TH * WM_TW, DROWS = SX ? WM_TH * WM_TW : WM_PROWS;
+  constexpr int XROWS = SX ? wm_prows<TH>() : TH * WM_TW, DROWS = SX ? TH * WM_TW : wm_prows<TH>();
   constexpr int MAIN = XROWS * RBX + DROWS * RBD;
   constexpr int RED = 2 * 9 * NCI * NCO * 4 * 64 * 4;
   return MAIN > RED ? MAIN : RED;
@@ -793,42 +850,68 @@ struct WmCfg {
 
 // operand tiling of the MFMA weight gradient: cout -> NCO 16-wide fragments, the input-channel fragments per block
 // as wide as 144 accumulator registers allow; the operand with fewer fragments per K-step carries the tap shift
+// blocks per channel chunk of the MFMA weight gradient: ~1024 in all, at most one per tile (tiles of the smallest
+// variant, so the workspace query, which cannot know the variant, is an upper bound), capped by the workspace
+static long wgrad_mfma_rows(const WgArgs& a, int cib) {
+  return wgrad_rows(a.n, a.h, a.w, a.cin, a.cout, cib) < a.ntiles ? wgrad_rows(a.n, a.h, a.w, a.cin, a.cout, cib)
+                                                                  : (a.ntiles < 1 ? 1 : a.ntiles);
+}
+
+// (at most 72-108 accumulator registers: the 144-register tilings spill next to the staging registers)
 static WmCfg wgrad_mfma_cfg(int cin, int cout) {
   WmCfg c;
   c.nco = cout <= 16 ? 1 : cout <= 32 ? 2 : 3;
-  if (c.nco == 1) c.nci = cin > 32 ? 4 : cin > 16 ? 2 : 1;
-  else if (c.nco == 2) c.nci = cin > 16 ? 2 : 1;
-  else c.nci = 1;
+  c.nci = (c.nco == 1 && cin > 16) ? 2 : 1;
   c.sx = c.nco >= c.nci;
   return c;
 }
 
-template <int NCI, int NCO, bool SX>
+template <int NCI, int NCO, bool SX, int TH>
 static int launch_wgrad_mfma_t(WgArgs& a, float* dw, hipStream_t st) {
-  constexpr int lds = wgrad_mfma_lds<NCI, NCO, SX>();
+  constexpr int lds = wgrad_mfma_lds<NCI, NCO, SX, TH>();
   static bool attr = false;
   if (!attr) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_mfma_kernel<NCI, NCO, SX>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_mfma_kernel<NCI, NCO, SX, TH>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (e != hipSuccess) return fail(VM_EHIP, "hipFuncSetAttribute(wgrad_mfma): %s", hipGetErrorString(e));
     attr = true;
   }
+  a.tiles_h = (a.h + TH - 1) / TH;
+  a.tiles_w = (a.w + WM_TW - 1) / WM_TW;
+  a.ntiles = (long)a.n * a.tiles_h * a.tiles_w;
   const int ncc = (a.cin + NCI * 16 - 1) / (NCI * 16);
-  const long gx = wgrad_rows(a.n, a.h, a.w, a.cin, a.cout, NCI * 16);
-  hipLaunchKernelGGL((wgrad_mfma_kernel<NCI, NCO, SX>), dim3((unsigned)gx, ncc), dim3(256), lds, st, a);
+  const long gx = wgrad_mfma_rows(a, NCI * 16);
+  hipLaunchKernelGGL((wgrad_mfma_kernel<NCI, NCO, SX, TH>), dim3((unsigned)gx, ncc), dim3(256), lds, st, a);
   const long S = 9L * a.cin * a.cout;
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((S + 63) / 64)), dim3(1024), 0, st, a.part, (int)gx, S, dw);
   return VM_OK;
 }
 
+static long g_wgrad_variant = 0;  // A/B knob (vm_set_option "wgrad_variant"): 0/1 4-row tiles, 2 8-row tiles
+}  // namespace trn
+
+int train_set_option(const char* key, long value) {
+  if (!strcmp(key, "wgrad_variant")) {
+    trn::g_wgrad_variant = value;
+    return 1;
+  }
+  return 0;
+}
+
+namespace trn {
+
 static int launch_wgrad_mfma(WgArgs& a, float* dw, hipStream_t st) {
   const WmCfg c = wgrad_mfma_cfg(a.cin, a.cout);
-  if (c.nci == 4) return launch_wgrad_mfma_t<4, 1, false>(a, dw, st);
-  if (c.nci == 2 && c.nco == 1) return launch_wgrad_mfma_t<2, 1, false>(a, dw, st);
-  if (c.nci == 1 && c.nco == 1) return launch_wgrad_mfma_t<1, 1, true>(a, dw, st);
-  if (c.nci == 2 && c.nco == 2) return launch_wgrad_mfma_t<2, 2, true>(a, dw, st);
-  if (c.nci == 1 && c.nco == 2) return launch_wgrad_mfma_t<1, 2, true>(a, dw, st);
-  return launch_wgrad_mfma_t<1, 3, true>(a, dw, st);
+  const bool th8 = g_wgrad_variant == 2;
+  if (c.nco == 1 && c.nci >= 2)
+    return th8 ? launch_wgrad_mfma_t<2, 1, false, 8>(a, dw, st) : launch_wgrad_mfma_t<2, 1, false, 4>(a, dw, st);
+  if (c.nci == 1 && c.nco == 1)
+    return th8 ? launch_wgrad_mfma_t<1, 1, true, 8>(a, dw, st) : launch_wgrad_mfma_t<1, 1, true, 4>(a, dw, st);
+  if (c.nci == 2 && c.nco == 2)
+    return th8 ? launch_wgrad_mfma_t<2, 2, true, 8>(a, dw, st) : launch_wgrad_mfma_t<2, 2, true, 4>(a, dw, st);
+  if (c.nci == 1 && c.nco == 2)
+    return th8 ? launch_wgrad_mfma_t<1, 2, true, 8>(a, dw, st) : launch_wgrad_mfma_t<1, 2, true, 4>(a, dw, st);
+  return th8 ? launch_wgrad_mfma_t<1, 3, true, 8>(a, dw, st) : launch_wgrad_mfma_t<1, 3, true, 4>(a, dw, st);
 }
 
 static bool ok_view(const vm_tensor* t) { return valid_tensor(t); }
@@ -845,7 +928,7 @@ using namespace vm::trn;
 
 extern "C" int vm_bn_backward_ex_nhwc(const vm_tensor* x, const vm_tensor* dy, const vm_tensor* y, const float* mean,
                                       const float* var, const float* gamma, float eps, vm_tensor* dx, vm_tensor* dx2,
-                                      float* dgamma, float* dbeta, void* work, void* stream);
+                                      float* dgamma, float* dbeta, float* dbias, void* work, void* stream);
 extern "C" int vm_relu_backward_ex_nhwc(const vm_tensor* dy, const vm_tensor* y, vm_tensor* dx, vm_tensor* dx2,
                                         void* stream);
 
@@ -860,20 +943,21 @@ extern "C" int vm_matting_loss_backward(const float* pred, const float* gt, cons
 }
 
 extern "C" size_t vm_bn_backward_workspace_bytes(int channels) {
-  return channels <= 0 ? 0 : (size_t)2 * BN_NBLK * channels * sizeof(double) + (size_t)2 * channels * sizeof(float);
+  return channels <= 0 ? 0 : (size_t)3 * BN_NBLK * channels * sizeof(double) + (size_t)2 * channels * sizeof(float);
 }
 
 extern "C" int vm_bn_backward_nhwc(const vm_tensor* x, const vm_tensor* dy, const vm_tensor* y, const float* mean,
                                    const float* var, const float* gamma, float eps, vm_tensor* dx, float* dgamma,
                                    float* dbeta, void* work, void* stream) {
-  return vm_bn_backward_ex_nhwc(x, dy, y, mean, var, gamma, eps, dx, nullptr, dgamma, dbeta, work, stream);
+  return vm_bn_backward_ex_nhwc(x, dy, y, mean, var, gamma, eps, dx, nullptr, dgamma, dbeta, nullptr, work, stream);
 }
 
 extern "C" int vm_bn_backward_ex_nhwc(const vm_tensor* x, const vm_tensor* dy, const vm_tensor* y, const float* mean,
                                       const float* var, const float* gamma, float eps, vm_tensor* dx, vm_tensor* dx2,
-                                      float* dgamma, float* dbeta, void* work, void* stream) {
+                                      float* dgamma, float* dbeta, float* dbias, void* work, void* stream) {
   if (dx2 && (!dx || !ok_view(dx2) || !same_shape(dx2, dy)))
     return fail(VM_EINVAL, "bn_backward: dx2 needs dx and an [n,h,w,c] view");
+  if (dbias && !x) return fail(VM_EINVAL, "bn_backward: dbias needs x");
   if (!ok_view(dy) || dy->dtype != VM_F32 || !work) return fail(VM_EINVAL, "bn_backward: bad dy / workspace");
   if (x && (!ok_view(x) || !same_shape(x, dy) || !mean || !var)) return fail(VM_EINVAL, "bn_backward: bad x");
   if (y && (!ok_view(y) || !same_shape(y, dy))) return fail(VM_EINVAL, "bn_backward: bad relu mask y");
@@ -886,7 +970,7 @@ extern "C" int vm_bn_backward_ex_nhwc(const vm_tensor* x, const vm_tensor* dy, c
   const int C = dy->c;
   double* part = reinterpret_cast<double*>(work);
   // the two channel sums land in dbeta / dgamma when given, else in the float tail of the workspace
-  float* tail = reinterpret_cast<float*>(part + 2L * BN_NBLK * C);
+  float* tail = reinterpret_cast<float*>(part + 3L * BN_NBLK * C);
   float* sg = dbeta ? dbeta : tail;
   float* sgx = dgamma ? dgamma : tail + C;
   const long M = (long)dy->n * dy->h * dy->w;
@@ -895,16 +979,20 @@ extern "C" int vm_bn_backward_ex_nhwc(const vm_tensor* x, const vm_tensor* dy, c
   else launch_bn_bwd_partial<false>(xv, dyv, yv, mean, var, eps, part, nb, st);
   int rc = check_launch("bn_backward_partial");
   if (rc) return rc;
-  hipLaunchKernelGGL(bn_bwd_final, dim3(C), dim3(64), 0, st, part, nb, C, sg, x ? sgx : nullptr);
+  hipLaunchKernelGGL(bn_bwd_final, dim3(C), dim3(64), 0, st, part, nb, C, sg, x ? sgx : nullptr, dbias, gamma, var,
+                     eps, M);
   rc = check_launch("bn_backward_final");
   if (rc || !dx) return rc;
-  const long work_n = (long)dy->n * dy->h * dy->w * C;
-  if (y)
-    hipLaunchKernelGGL(bn_bwd_apply<true>, dim3(grid_for(work_n, 256)), dim3(256), 0, st, xv, dyv, yv, mean, var,
-                       gamma, eps, sg, sgx, mk(dx), dx2 ? mk(dx2) : V{});
-  else
-    hipLaunchKernelGGL(bn_bwd_apply<false>, dim3(grid_for(work_n, 256)), dim3(256), 0, st, xv, dyv, yv, mean, var,
-                       gamma, eps, sg, sgx, mk(dx), dx2 ? mk(dx2) : V{});
+  const int cp = lanes_for(C);
+  const dim3 grid = lanes_grid(M, C, cp);
+  const V dxv = mk(dx), dx2v = dx2 ? mk(dx2) : V{};
+#define VM_BNA(CP)                                                                                                    \
+  if (y) hipLaunchKernelGGL((bn_bwd_apply<true, CP>), grid, dim3(256), 0, st, xv, dyv, yv, mean, var, gamma, eps, sg, \
+                            sgx, dxv, dx2v);                                                                          \
+  else hipLaunchKernelGGL((bn_bwd_apply<false, CP>), grid, dim3(256), 0, st, xv, dyv, yv, mean, var, gamma, eps, sg,  \
+                          sgx, dxv, dx2v)
+  VM_CP_SWITCH(cp, VM_BNA)
+#undef VM_BNA
   return check_launch("bn_backward_apply");
 }
 
@@ -918,9 +1006,13 @@ extern "C" int vm_relu_backward_ex_nhwc(const vm_tensor* dy, const vm_tensor* y,
       (dx2 && (!ok_view(dx2) || !same_shape(dy, dx2))))
     return fail(VM_EINVAL, "relu_backward: bad tensors");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  const long n = (long)dy->n * dy->h * dy->w * dy->c;
-  hipLaunchKernelGGL(relu_bwd_kernel, dim3(grid_for(n, 256)), dim3(256), 0, st, mk(dy), mk(y), mk(dx),
-                     dx2 ? mk(dx2) : V{});
+  const long M = (long)dy->n * dy->h * dy->w;
+  const int cp = lanes_for(dy->c);
+  const dim3 grid = lanes_grid(M, dy->c, cp);
+  const V a = mk(dy), b = mk(y), c = mk(dx), d = dx2 ? mk(dx2) : V{};
+#define VM_RB(CP) hipLaunchKernelGGL((relu_bwd_kernel<CP>), grid, dim3(256), 0, st, a, b, c, d)
+  VM_CP_SWITCH(cp, VM_RB)
+#undef VM_RB
   return check_launch("relu_backward");
 }
 
@@ -1010,8 +1102,6 @@ extern "C" int vm_conv3x3_wgrad_ex_nhwc(const vm_tensor* x, int x_src_c, long x_
   a.dy = reinterpret_cast<const float*>(dy->ptr) + dy->coff;
   a.cout = dy->c; a.dcs = dy->cstride;
   a.part = reinterpret_cast<float*>(work);
-  a.tiles_h = (x->h + WM_TH - 1) / WM_TH; a.tiles_w = (x->w + WM_TW - 1) / WM_TW;
-  a.ntiles = (long)x->n * a.tiles_h * a.tiles_w;
   int rc = launch_wgrad_mfma(a, dw, reinterpret_cast<hipStream_t>(stream));
   if (rc) return rc;
   return check_launch("conv3x3_wgrad_ex");

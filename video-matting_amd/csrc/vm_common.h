@@ -14,6 +14,9 @@ namespace vm {
 // per-thread error text for vm_last_error()
 void set_error(const char* fmt, ...);
 
+// tuning knobs of the training kernels (train.hip), reached through vm_set_option: 1 = handled, 0 = unknown key
+int train_set_option(const char* key, long value);
+
 inline int fail(int code, const char* fmt, ...) {
   char buf[512];
   va_list ap;

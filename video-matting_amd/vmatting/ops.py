@@ -554,16 +554,17 @@ def matting_loss_backward(pred, gt, raw_fg, in_bg, in_cmp, out=None):
     return out
 
 
-def bn_backward(x, dy, y, mean, var, gamma, eps=1e-3, dx=None, dgamma=None, dbeta=None, dx2=None):
+def bn_backward(x, dy, y, mean, var, gamma, eps=1e-3, dx=None, dgamma=None, dbeta=None, dx2=None, dbias=None):
     """Gradient of tf.contrib batch_norm(is_training=True) (+ the relu after it when ``y`` is given).
-    x None: only dbeta = channel sum of dy (a bias gradient).  dx2: optional second copy of dx (e.g. bf16)."""
+    x None: only dbeta = channel sum of dy (a bias gradient).  dx2: optional second copy of dx (e.g. bf16).
+    dbias: the gradient of a conv bias added before the BN (= channel sum of dx) from the same reduction."""
     c = dy.shape[-1]
     views = [None if t is None else nhwc(t) for t in (x, dy, y, dx, dx2)]
     ref = lambda v: None if v is None else ctypes.byref(v)  # noqa: E731
     ws = _workspace(lib().vm_bn_backward_workspace_bytes(c), dy.device)
     check(lib().vm_bn_backward_ex_nhwc(ref(views[0]), ref(views[1]), ref(views[2]), _ptr(mean), _ptr(var),
                                        _ptr(gamma), float(eps), ref(views[3]), ref(views[4]), _ptr(dgamma),
-                                       _ptr(dbeta), _ptr(ws), stream_handle()), "bn_backward")
+                                       _ptr(dbeta), _ptr(dbias), _ptr(ws), stream_handle()), "bn_backward")
     return dx
 
 

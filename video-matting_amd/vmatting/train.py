@@ -243,8 +243,7 @@ class VideoTrainer:
         g16 = tb["g16_" + scope] if dgrad_out is not None and scope in self.dconv16 else None
         ops.bn_backward(z, dy, mask, mean, var, self.P[scope, "gamma"], EPS, dx=dz,
                         dgamma=self.G[scope, "gamma"], dbeta=self.G[scope, "beta"],
-                        dx2=None if g16 is None else g16[..., :dz.shape[-1]])
-        ops.bn_backward(None, dz, None, None, None, None, dbeta=self.G[scope, "b"])
+                        dx2=None if g16 is None else g16[..., :dz.shape[-1]], dbias=self.G[scope, "b"])
         ops.conv_wgrad(x_in, dz, self.G[scope, "w"], mfma=self._mfma_wgrad)
         if dgrad_out is not None:
             if g16 is not None:
