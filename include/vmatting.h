@@ -94,6 +94,13 @@ int vm_conv3x3_nhwc(const vm_tensor* x, const void* packed, int cin, int cout, c
 /* The same conv over the channel concat of nsrc sources (unet_simple.py:153-168's per-level concat of the three
  * towers, tower-major in HBM so the towers run as one batch): x is the [n,h,w,c_src] view of source 0, source s
  * lies src_stride elements further; cin = nsrc * x->c, and x->c must be whole 64-byte granules. */
+/* vm_conv3x3_nhwc / vm_conv3x3_sources_nhwc with a caller workspace: small-grid bf16 convs with a long K loop
+ * (the deep levels of unet_simple's towers and heads) split their channel granules over ~1024 blocks and reduce the
+ * f32 partial sums in a fixed order (deterministic).  nsrc 0/1 = one source.  work: vm_conv3x3_workspace_bytes. */
+size_t vm_conv3x3_workspace_bytes(const vm_tensor* x, int cin, int cout);
+int vm_conv3x3_ex_nhwc(const vm_tensor* x, int nsrc, long src_stride, const void* packed, int cin, int cout,
+                       const float* bias, const float* scale, const float* shift, int act, vm_tensor* y, void* work,
+                       size_t work_bytes, void* stream);
 int vm_conv3x3_sources_nhwc(const vm_tensor* x, int nsrc, long src_stride, const void* packed, int cin, int cout,
                             const float* bias, const float* scale, const float* shift, int act, vm_tensor* y,
                             void* stream);

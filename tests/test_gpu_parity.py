@@ -185,6 +185,7 @@ def test_conv_fused_maxpool_matches_separate(shape, kernel):
     wt = (rs.normal(size=(3, 3, cin, cout)) * np.sqrt(2.0 / (9 * cin))).astype(np.float32)
     pc = ops.PackedConv(wt, (rs.normal(size=cout) * 0.1).astype(np.float32), torch.bfloat16, DEV)
     _lib.set_option("conv_kernel", kernel)
+    _lib.set_option("splitk_tiles", 0)  # the reference conv without split-K (same summation order as the fused one)
     try:
         cat = torch.zeros((n, h, w, 2 * cout), dtype=torch.bfloat16, device=DEV)
         pooled = torch.full((n, (h + 1) // 2, (w + 1) // 2, cout), 7.0, dtype=torch.bfloat16, device=DEV)
@@ -193,6 +194,7 @@ def test_conv_fused_maxpool_matches_separate(shape, kernel):
         p_ref = ops.maxpool2x2(y_ref)
     finally:
         _lib.set_option("conv_kernel", 0)
+        _lib.set_option("splitk_tiles", 512)
     assert torch.equal(cat[..., cout:], y_ref)
     assert torch.equal(pooled, p_ref)
     assert float(cat[..., :cout].abs().max()) == 0.0

@@ -505,3 +505,33 @@ def test_conv_over_tower_major_sources_equals_concat(dtype, c, cout):
     a = ops.conv3x3(sc, pc, "relu")
     b = ops.conv3x3(sc.materialize().contiguous(), pc, "relu")
     assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("n,h,w,cin,cout,odt", [(6, 20, 20, 512, 512, "bf16"), (2, 40, 40, 1536, 16, "f32"),
+                                                (2, 40, 40, 192, 48, "f32"), (3, 9, 33, 256, 64, "bf16")])
+def test_conv_split_k_matches_unsplit(n, h, w, cin, cout, odt):
+    """Small-grid bf16 convs split their channel granules (vm_conv3x3_ex_nhwc + workspace): same result as the
+    unsplit kernel up to f32 summation order (and one bf16 output rounding)."""
+    from vmatting import _lib, ops
+    x = (torch.randn(n, h, w, cin, device=DEV) * 0.5).to(torch.bfloat16)
+    wt = (np.random.RandomState(cin + cout).normal(size=(3, 3, cin, cout)) * np.sqrt(2.0 / (9 * cin))).astype(
+        np.float32)
+    pc = ops.PackedConv(wt, np.random.RandomState(1).normal(size=cout).astype(np.float32), "bf16")
+    tdt = torch.bfloat16 if odt == "bf16" else torch.float32
+    assert lib_ws(x, cin, cout) > 0, "this shape should split"
+    a = ops.conv3x3(x, pc, "relu", out_dtype=tdt, splitk=True).float()
+    try:
+        _lib.set_option("splitk_tiles", 0)
+        b = ops.conv3x3(x, pc, "relu", out_dtype=tdt, splitk=True).float()
+    finally:
+        _lib.set_option("splitk_tiles", 512)
+    tol = 1e-2 if odt == "bf16" else 1e-5
+    assert float((a - b).abs().max()) <= tol * float(b.abs().max())
+
+
+def lib_ws(x, cin, cout):
+    import ctypes
+    from vmatting import ops
+    from vmatting._lib import lib
+    xv = ops.nhwc(x)
+    return lib().vm_conv3x3_workspace_bytes(ctypes.byref(xv), cin, cout)

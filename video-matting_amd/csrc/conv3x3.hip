@@ -52,6 +52,10 @@ struct ConvArgs {
   // x_src_stride elements from the view base (tower-major features: unet_simple.py:153-168's concat, never built)
   int x_src_c;
   long x_src_stride;
+  // split-K (patch kernel, row-slot pipeline): ksplit > 1 splits the channel granules over gridDim.y; each split
+  // writes raw f32 sums to part[split][pixel][cout] and splitk_reduce_kernel applies bias/affine/act (fixed order)
+  int ksplit;
+  float* part;
 };
 
 // element offset of input channel c (relative to the view's channel 0) under the source split
@@ -886,7 +890,11 @@ void conv3x3_patch(ConvArgs a) {
     woff[i] = (row * a.K_pad + lq * 8) * 2;
     if (piece < C::WP) ++w_n;
   }
-  const int nch = a.cin_pad / 32, nsteps = nch * 9;
+  const int nch_all = a.cin_pad / 32;
+  const int ksp = a.ksplit > 1 ? a.ksplit : 1;
+  const int per_split = (nch_all + ksp - 1) / ksp;  // host: every split non-empty
+  const int cc_beg = (int)blockIdx.y * per_split;
+  const int nch = min(nch_all, cc_beg + per_split), nsteps = nch * 9;  // end granule / step of this split
   const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr(smem));
   const uint32_t wring = lds0 + 2 * C::PB;
 
@@ -950,11 +958,11 @@ void conv3x3_patch(ConvArgs a) {
     // read while tap g's MFMAs run (same slot and patch, no synchronisation needed)
     static_assert(!PF && !FIRST && ABL == 0, "row-slot pipeline: plain configuration only");
     constexpr int R = 9 / G;
-    issue_x(0, 0);
+    issue_x(cc_beg, cc_beg & 1);
 #pragma unroll
-    for (int j = 0; j < S - 1; ++j) issue_w(j, j);
+    for (int j = 0; j < S - 1; ++j) issue_w(cc_beg * R + j, j);
     int slot = 0;
-    for (int cc = 0; cc < nch; ++cc) {
+    for (int cc = cc_beg; cc < nch; ++cc) {
 #pragma unroll
       for (int r = 0; r < R; ++r) {
         const int k = cc * R + r;
@@ -1053,12 +1061,15 @@ void conv3x3_patch(ConvArgs a) {
           (a.up ? (((long)n * 2 * H + 2 * r0) * YW + 2 * c0) : (((long)n * H + r0) * W + c0)) * (long)a.y_cstride;
   const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(yb, 0, 0x7ffffff0, 0x00020000);
   constexpr int SPW = C::TPN / 64;  // 64-channel slabs per wave column
-  if (a.y_dtype == VM_F32) {
-    // f32 output (the training step's pre-BN buffers, unet_simple.py:19-27): f32 slab staging, 4 channels per
-    // 16-byte store; no fused pool / folded resize on this path (host-checked)
-    float* yf = reinterpret_cast<float*>(a.y) + a.y_coff + (((long)n * H + r0) * W + c0) * (long)a.y_cstride;
+  const bool splitk = a.ksplit > 1;
+  if (a.y_dtype == VM_F32 || splitk) {
+    // f32 output (the training step's pre-BN buffers, unet_simple.py:19-27) or a split-K partial: f32 slab staging,
+    // 4 channels per 16-byte store; no fused pool / folded resize on this path (host-checked)
+    const int ycs = splitk ? a.cout : a.y_cstride;
+    float* yf = splitk ? a.part + (long)blockIdx.y * a.M * a.cout + (((long)n * H + r0) * W + c0) * (long)ycs
+                       : reinterpret_cast<float*>(a.y) + a.y_coff + (((long)n * H + r0) * W + c0) * (long)ycs;
     const __amdgpu_buffer_rsrc_t yfr = __builtin_amdgcn_make_buffer_rsrc(yf, 0, 0x7ffffff0, 0x00020000);
-    const int ycs4 = a.y_cstride * 4;
+    const int ycs4 = ycs * 4;
     for (int sl = 0; sl < BN / 64; ++sl) {
       const int cb = n0 + sl * 64;
       __syncthreads();
@@ -1071,9 +1082,9 @@ void conv3x3_patch(ConvArgs a) {
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             const int co = min(cb + col + j, a.cout - 1);
-            const float sc = a.scale ? a.scale[co] : 1.f;
+            const float sc = (a.scale && !splitk) ? a.scale[co] : 1.f;
             mul[j] = sc;
-            add[j] = (a.bias ? a.bias[co] : 0.f) * sc + (a.shift ? a.shift[co] : 0.f);
+            add[j] = splitk ? 0.f : (a.bias ? a.bias[co] : 0.f) * sc + (a.shift ? a.shift[co] : 0.f);
           }
 #pragma unroll
           for (int fp = 0; fp < FP; ++fp) {
@@ -1082,8 +1093,8 @@ void conv3x3_patch(ConvArgs a) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
               v[j] = fmaf(acc[fc][fp][j], mul[j], add[j]);
-              if (a.act == VM_ACT_RELU) v[j] = fmaxf(v[j], 0.f);
-              else if (a.act == VM_ACT_SIGMOID) v[j] = sigmoid_precise(v[j]);
+              if (!splitk && a.act == VM_ACT_RELU) v[j] = fmaxf(v[j], 0.f);
+              else if (!splitk && a.act == VM_ACT_SIGMOID) v[j] = sigmoid_precise(v[j]);
             }
             *reinterpret_cast<float4*>(smem + row * C::SR32 + col * 4) = make_float4(v[0], v[1], v[2], v[3]);
           }
@@ -2068,6 +2079,37 @@ __global__ __launch_bounds__(256) void conv3x3_up2x_border(BorderArgs a) {
   *reinterpret_cast<uint2*>(yp) = pk;
 }
 
+// ================================================================ split-K reduction
+// out[p][c] = act((sum_s part[s][p][c]) * scale + bias*scale + shift), the splits summed in order (deterministic);
+// one thread per 4 output channels of a pixel
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ part, int ks, long M, int cout,
+                                                            const float* bias, const float* scale, const float* shift,
+                                                            int act, void* y, int y_dtype, int ycs, int ycoff) {
+  const int c4 = (cout + 3) / 4;
+  const long total = M * c4;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long p = i / c4;
+    const int c = (int)(i - p * c4) * 4;
+    float4 s = *reinterpret_cast<const float4*>(part + p * cout + c);
+    for (int k = 1; k < ks; ++k) {
+      const float4 t = *reinterpret_cast<const float4*>(part + (long)k * M * cout + p * cout + c);
+      s.x += t.x; s.y += t.y; s.z += t.z; s.w += t.w;
+    }
+    float v[4] = {s.x, s.y, s.z, s.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (c + j >= cout) break;
+      const float sc = scale ? scale[c + j] : 1.f;
+      float t = fmaf(v[j], sc, (bias ? bias[c + j] : 0.f) * sc + (shift ? shift[c + j] : 0.f));
+      if (act == VM_ACT_RELU) t = fmaxf(t, 0.f);
+      else if (act == VM_ACT_SIGMOID) t = sigmoid_precise(t);
+      const long o = p * ycs + ycoff + c + j;
+      if (y_dtype == VM_F32) reinterpret_cast<float*>(y)[o] = t;
+      else reinterpret_cast<uint16_t*>(y)[o] = f2bf(t);
+    }
+  }
+}
+
 // ================================================================ dispatch
 // name of the kernel the last conv call on this thread launched, spelled as rocprofv3 reports it
 // (bench.py matches its per-launch PMC traffic by this name)
@@ -2135,9 +2177,24 @@ static int launch_patch(ConvArgs& a, hipStream_t st) {
   a.tiles_total = (int)(sp * a.tiles_n);
   snprintf(g_last_kernel, sizeof g_last_kernel, "vm::conv3x3_patch<%d, %d, %d, %d, %d, %d, %d, %s, %d, %s, %d>", BN, WM,
            WN, S, TH, MINB, UNR, PF ? "true" : "false", ABL, FIRST ? "true" : "false", G);
-  hipLaunchKernelGGL((conv3x3_patch<BN, WM, WN, S, TH, MINB, UNR, PF, ABL, FIRST, G>), dim3(a.tiles_total), dim3(C::NT),
-                     lds, st, a);
+  hipLaunchKernelGGL((conv3x3_patch<BN, WM, WN, S, TH, MINB, UNR, PF, ABL, FIRST, G>),
+                     dim3(a.tiles_total, a.ksplit > 1 ? a.ksplit : 1), dim3(C::NT), lds, st, a);
   return check_launch("conv3x3_patch");
+}
+
+// split-K plan of a patch-kernel conv: small grids (under g_splitk_tiles 4 x 32 pixel x 64 channel tiles) with a
+// long K loop split the channel granules so that ~1024 blocks run; 1 = no split.  Deterministic in the geometry,
+// so vm_conv3x3_workspace_bytes and the launch agree.
+static long g_splitk_tiles = 512;
+static int splitk_plan(long n, int h, int w, int cin_pad, int cout) {
+  const long tiles = n * ((h + 3) / 4) * ((w + 31) / 32) * ((cout + 63) / 64);
+  const int nch = cin_pad / 32;
+  if (tiles >= g_splitk_tiles || nch < 4 || tiles <= 0) return 1;
+  int ks = (int)((1024 + tiles - 1) / tiles);
+  if (ks > nch / 2) ks = nch / 2;
+  if (ks < 2) return 1;
+  const int per = (nch + ks - 1) / ks;
+  return (nch + per - 1) / per;  // every split non-empty
 }
 
 // tuning knobs (vm_set_option): conv_kernel 0 = auto, 1 = register-staged only, 2 = LDS-DMA whenever legal;
@@ -2161,6 +2218,14 @@ static bool patch_ok(const ConvArgs& a, size_t tsize) {
 }
 
 static int dispatch_patch(ConvArgs& a, hipStream_t st) {
+  if (a.ksplit > 1) {  // split-K: the 4 x 32-pixel row-slot config, then the fixed-order reduction
+    int rc = launch_patch<64, 4, 1, 2, 4, 2, 9, false, 0, false, 3>(a, st);
+    if (rc) return rc;
+    const long work = a.M * ((a.cout + 3) / 4);
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(grid_for(work, 256)), dim3(256), 0, st, a.part, a.ksplit, a.M,
+                       a.cout, a.bias, a.scale, a.shift, a.act, a.y, a.y_dtype, a.y_cstride, a.y_coff);
+    return check_launch("splitk_reduce");
+  }
   switch (g_patch_ablate) {  // timing experiments on the default tiling (results are garbage)
     case 1: return launch_patch<64, 8, 1, 6, 8, 1, 9, false, 1>(a, st);
     case 2: return launch_patch<64, 8, 1, 6, 8, 1, 9, false, 2>(a, st);
@@ -2304,6 +2369,10 @@ extern "C" int vm_set_option(const char* key, long value) {
     g_head_kernel = value;
     return VM_OK;
   }
+  if (!strcmp(key, "splitk_tiles")) {
+    g_splitk_tiles = value;
+    return VM_OK;
+  }
   if (!strcmp(key, "glds_rb")) {
     if (value != 64 && value != 128) return fail(VM_EINVAL, "glds_rb must be 64 or 128");
     g_glds_rb = value;
@@ -2337,7 +2406,8 @@ extern "C" int vm_conv3x3_pack_weights(const float* w_hwio, int cin, int cout, i
 
 static int conv_impl(const vm_tensor* x, const void* packed, int cin, int cout, const float* bias, const float* scale,
                      const float* shift, int act, vm_tensor* y, const vm_tensor* yp, void* stream,
-                     float* y2 = nullptr, int nsrc = 0, long src_stride = 0);
+                     float* y2 = nullptr, int nsrc = 0, long src_stride = 0, void* work = nullptr,
+                     size_t work_bytes = 0);
 
 extern "C" int vm_conv3x3_nhwc(const vm_tensor* x, const void* packed, int cin, int cout, const float* bias,
                                const float* scale, const float* shift, int act, vm_tensor* y, void* stream) {
@@ -2473,7 +2543,7 @@ extern "C" int vm_conv3x3_head_nhwc(const vm_tensor* x, const void* packed, int 
 
 static int conv_impl(const vm_tensor* x, const void* packed, int cin, int cout, const float* bias, const float* scale,
                      const float* shift, int act, vm_tensor* y, const vm_tensor* yp, void* stream, float* y2, int nsrc,
-                     long src_stride) {
+                     long src_stride, void* work, size_t work_bytes) {
   if (!valid_tensor(x) || !valid_tensor(y) || !packed) return fail(VM_EINVAL, "conv3x3: invalid tensor/weights");
   const int xc = nsrc > 1 ? nsrc * x->c : x->c;  // sources: x is the view of source 0
   if (cin <= 0 || cout <= 0 || xc != cin || y->c != cout)
@@ -2555,6 +2625,7 @@ static int conv_impl(const vm_tensor* x, const void* packed, int cin, int cout, 
     a.x_src_c = x->c;
     a.x_src_stride = src_stride;
   }
+  a.ksplit = 1;
   a.w = packed; a.cout = cout;
   a.bias = bias; a.scale = scale; a.shift = shift; a.act = act;
   a.y = y->ptr; a.y_cstride = y->cstride; a.y_coff = y->coff; a.y_dtype = y->dtype;
@@ -2569,6 +2640,32 @@ static int conv_impl(const vm_tensor* x, const void* packed, int cin, int cout, 
     a.py_coff = yp->coff;
     return dispatch_patch(a, st);
   }
+  if (dt == VM_BF16 && work && g_conv_kernel == 0 && patch_ok(a, 2) && (cout & 3) == 0) {
+    const int ks = splitk_plan(x->n, x->h, x->w, a.cin_pad, cout);
+    if (ks > 1 && work_bytes >= (size_t)ks * M * cout * sizeof(float)) {
+      a.ksplit = ks;
+      a.part = reinterpret_cast<float*>(work);
+      return dispatch_patch(a, st);
+    }
+  }
   if (dt == VM_BF16) return dispatch_mfma<uint16_t>(a, st);
   return dispatch_mfma<float>(a, st);
+}
+
+// workspace of vm_conv3x3_ex_nhwc: the split-K partial sums of a small-grid bf16 conv, else 0
+extern "C" size_t vm_conv3x3_workspace_bytes(const vm_tensor* x, int cin, int cout) {
+  if (!x || x->dtype != VM_BF16 || cin <= 0 || cout <= 0 || (cout & 3)) return 0;
+  const PackGeom g = geom(cin, cout, VM_BF16);
+  if (!g.chunk_major || g.cin_pad % 32) return 0;
+  const int ks = splitk_plan(x->n, x->h, x->w, g.cin_pad, cout);
+  return ks > 1 ? (size_t)ks * x->n * x->h * x->w * cout * sizeof(float) : 0;
+}
+
+extern "C" int vm_conv3x3_ex_nhwc(const vm_tensor* x, int nsrc, long src_stride, const void* packed, int cin, int cout,
+                                  const float* bias, const float* scale, const float* shift, int act, vm_tensor* y,
+                                  void* work, size_t work_bytes, void* stream) {
+  if (nsrc < 0 || (nsrc > 1 && src_stride <= 0)) return fail(VM_EINVAL, "conv3x3_ex: nsrc %d stride %ld", nsrc,
+                                                            src_stride);
+  return conv_impl(x, packed, cin, cout, bias, scale, shift, act, y, nullptr, stream, nullptr, nsrc, src_stride, work,
+                   work_bytes);
 }

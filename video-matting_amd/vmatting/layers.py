@@ -47,6 +47,6 @@ class BatchNorm:
 def conv_bn(x, pc, bn, phase, act, out):
     """new_conv (conv + bias -> BN) followed by ``act`` (unet_simple.py:19-27 + the relu at the call site)."""
     if not phase:
-        return ops.conv3x3(x, pc, act, out=out, affine=(bn.inf_scale, bn.inf_shift))
-    ops.conv3x3(x, pc, "none", out=out, affine=False)
+        return ops.conv3x3(x, pc, act, out=out, affine=(bn.inf_scale, bn.inf_shift), splitk=True)
+    ops.conv3x3(x, pc, "none", out=out, affine=False, splitk=True)
     return bn(out, True, act)

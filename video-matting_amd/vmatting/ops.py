@@ -134,12 +134,14 @@ class SourceConcat:
         return torch.cat([self.source(i) for i in range(self.nsrc)], -1)
 
 
-def conv3x3(x, pc, act="none", out=None, out_dtype=None, affine=None, pool_out=None):
+def conv3x3(x, pc, act="none", out=None, out_dtype=None, affine=None, pool_out=None, splitk=False):
     """tf.nn.conv2d 3x3 SAME + bias_add (+ folded BN affine) + activation, on MFMA.
 
     ``affine``: None -> the PackedConv's own scale/shift; False -> none; (scale, shift) -> those.
     ``pool_out``: also write tf.nn.max_pool 2x2/2 SAME of the result there (fused into the conv epilogue when
     the kernel supports it, else a separate max-pool launch).
+    ``splitk``: allow split-K on small grids (a workspace is passed; the per-pixel summation order then depends
+    on the batch size, so the inference nets, whose frames must not depend on their batch, leave it off).
     """
     if x.dtype != pc.dtype:
         raise TypeError("conv input dtype %s != packed weights dtype %s" % (x.dtype, pc.dtype))
@@ -154,13 +156,28 @@ def conv3x3(x, pc, act="none", out=None, out_dtype=None, affine=None, pool_out=N
         scale = shift = None
     else:
         scale, shift = affine
-    if isinstance(x, SourceConcat):
-        if pool_out is not None:
-            raise ValueError("conv3x3: no fused pooling over split sources")
-        xv, yv = nhwc(x.src0), nhwc(out)
-        check(lib().vm_conv3x3_sources_nhwc(ctypes.byref(xv), x.nsrc, x.stride, _ptr(pc.packed), pc.cin, pc.cout,
-                                            _ptr(pc.bias), _ptr(scale), _ptr(shift), _lib.ACT[act], ctypes.byref(yv),
-                                            stream_handle()), "conv3x3_sources")
+    if isinstance(x, SourceConcat) or pool_out is None:
+        # the general entry: split sources and/or a workspace for split-K on small grids
+        if isinstance(x, SourceConcat):
+            xv, nsrc, stride = nhwc(x.src0), x.nsrc, x.stride
+            if pool_out is not None:
+                raise ValueError("conv3x3: no fused pooling over split sources")
+        else:
+            xv, nsrc, stride = nhwc(x), 1, 0
+        yv = nhwc(out)
+        wsz = lib().vm_conv3x3_workspace_bytes(ctypes.byref(xv), pc.cin, pc.cout) if splitk else 0
+        ws = _workspace(wsz, x.device) if wsz else None
+        prof = _CONV_PROFILE
+        if prof is not None:
+            ev0 = torch.cuda.Event(enable_timing=True)
+            ev1 = torch.cuda.Event(enable_timing=True)
+            ev0.record()
+        check(lib().vm_conv3x3_ex_nhwc(ctypes.byref(xv), nsrc, stride, _ptr(pc.packed), pc.cin, pc.cout,
+                                       _ptr(pc.bias), _ptr(scale), _ptr(shift), _lib.ACT[act], ctypes.byref(yv),
+                                       _ptr(ws), wsz, stream_handle()), "conv3x3")
+        if prof is not None:
+            ev1.record()
+            prof.append((2 * n * h * w * 9 * pc.cin * pc.cout, _lib.last_conv_kernel(), ev0, ev1))
         return out
     xv, yv = nhwc(x), nhwc(out)
     prof = _CONV_PROFILE

@@ -197,9 +197,9 @@ class VideoTrainer:
         """new_conv (unet_simple.py:19-27) with batch statistics, then ``act``; keeps z and (mean, var)."""
         z, (mean, var) = tb["z_" + scope], tb["st_" + scope]
         if scope in self._padconv:
-            ops.conv3x3(x, self._padconv[scope][0], "none", out=tb["zfull_" + scope], affine=False)
+            ops.conv3x3(x, self._padconv[scope][0], "none", out=tb["zfull_" + scope], affine=False, splitk=True)
         else:
-            ops.conv3x3(x, self.model.convs[scope], "none", out=z, affine=False)
+            ops.conv3x3(x, self.model.convs[scope], "none", out=z, affine=False, splitk=True)
         ops.bn_stats(z, mean, var)
         bnl = self.model.bn[scope]
         ops.bn_apply(z, mean, var, bnl.gamma, bnl.beta, EPS, act, out=out)
@@ -227,7 +227,7 @@ class VideoTrainer:
                 ops.resize_bilinear(b[prev].base, L[lv], out=r.base)
             else:
                 ops.resize_bilinear(b[prev], L[lv], out=r)
-            ops.conv3x3(r, m.convs[up], "relu", out=c[..., off:width], affine=False)
+            ops.conv3x3(r, m.convs[up], "relu", out=c[..., off:width], affine=False, splitk=True)
             mean, var = tb["st_" + up]
             ops.bn_stats(c, mean, var)
             ops.bn_apply(c, mean, var, m.bn[up].gamma, m.bn[up].beta, EPS, "none", out=b[cat + "n"][..., :width])

@@ -113,12 +113,12 @@ class UNetSimple:
         ops.conv3x3(b["tpool2"], V["conv3_1"], "relu", out=t("conv3_1"))
         ops.conv3x3(t("conv3_1"), V["conv3_2"], "relu", out=t("conv3_2"))
         ops.conv3x3(t("conv3_2"), V["conv3_3"], "relu", out=t("conv3_3"), pool_out=b["tpool3"])
-        ops.conv3x3(b["tpool3"], V["conv4_1"], "relu", out=t("conv4_1"))
-        ops.conv3x3(t("conv4_1"), V["conv4_2"], "relu", out=t("conv4_2"))
+        ops.conv3x3(b["tpool3"], V["conv4_1"], "relu", out=t("conv4_1"), splitk=True)
+        ops.conv3x3(t("conv4_1"), V["conv4_2"], "relu", out=t("conv4_2"), splitk=True)
         ops.conv3x3(t("conv4_2"), V["conv4_3"], "relu", out=t("conv4_3"), pool_out=b["tpool4"])
-        ops.conv3x3(b["tpool4"], V["conv5_1"], "relu", out=t("conv5_1"))
-        ops.conv3x3(t("conv5_1"), V["conv5_2"], "relu", out=t("conv5_2"))
-        ops.conv3x3(t("conv5_2"), V["conv5_3"], "relu", out=t("conv5_3"))
+        ops.conv3x3(b["tpool4"], V["conv5_1"], "relu", out=t("conv5_1"), splitk=True)
+        ops.conv3x3(t("conv5_1"), V["conv5_2"], "relu", out=t("conv5_2"), splitk=True)
+        ops.conv3x3(t("conv5_2"), V["conv5_3"], "relu", out=t("conv5_3"), splitk=True)
 
     def load_inputs(self, b, xs):
         """cmp / bg / diff (f32 device tensors) into the towers' batch (tower t = frames t*n..) and into the 9-channel
@@ -173,7 +173,7 @@ class UNetSimple:
             ops.resize_bilinear(prev.base, size, out=rbuf.base)
         else:
             ops.resize_bilinear(prev, size, out=rbuf)
-        ops.conv3x3(rbuf, self.convs[scope], "relu", out=up_slice, affine=False)
+        ops.conv3x3(rbuf, self.convs[scope], "relu", out=up_slice, affine=False, splitk=True)
         self.bn[scope](cat, phase, out=catn)
 
     def _publish(self, b):
