@@ -89,6 +89,17 @@ const char* vm_conv3x3_last_kernel(void);
  */
 size_t vm_conv3x3_packed_bytes(int cin, int cout, int dtype);
 int vm_conv3x3_pack_weights(const float* w_hwio, int cin, int cout, int dtype, void* packed, void* stream);
+
+/* Many packs in ONE launch (the optimizer step re-packs every trainable filter, train.py:302-304).  A job packs the
+ * conv geometry (cin, cout, dtype) from an f32 HWIO source filter of (w_cin, w_cout) channels, zero outside it
+ * (a cout-padded narrow conv); flip = 1 packs the data-gradient filter of that source instead (spatially flipped,
+ * in/out transposed: cin = the source's output channels (padded), cout = its input channels). */
+typedef struct vm_pack_job {
+  const float* w;
+  void* packed;
+  int32_t cin, cout, dtype, flip, w_cin, w_cout;
+} vm_pack_job;
+int vm_conv3x3_pack_weights_batch(int njobs, const vm_pack_job* jobs, void* stream);
 int vm_conv3x3_nhwc(const vm_tensor* x, const void* packed, int cin, int cout, const float* bias,
                     const float* scale, const float* shift, int act, vm_tensor* y, void* stream);
 /* The same conv over the channel concat of nsrc sources (unet_simple.py:153-168's per-level concat of the three

@@ -116,6 +116,38 @@ def test_conv_dgrad_through_flipped_filter(cin, cout):
     assert scaled_err(H(dx), xr.grad.numpy()) <= 1e-4
 
 
+def test_pack_weights_batch_matches_single_packs():
+    """vm_conv3x3_pack_weights_batch: plain, cout-padded and flipped (data-gradient) jobs in one launch give the
+    same bytes as single packs of the explicitly padded / flip_weights filters."""
+    from vmatting import ops
+    rs = np.random.RandomState(11)
+    cases = []
+    for cin, cout, dt in [(64, 64, "bf16"), (30, 2, "bf16"), (9, 16, "fp32"), (96, 30, "bf16"), (30, 24, "fp32")]:
+        cases.append((T(rs.normal(size=(3, 3, cin, cout)).astype(np.float32)), cin, cout, dt))
+    convs, refs = [], []
+    for w, cin, cout, dt in cases:
+        convs.append(ops.PackedConv(w.clone(), None, dt, DEV))
+        refs.append(ops.PackedConv(w, None, dt, DEV))
+        cp = (cout + 7) // 8 * 8  # cout-padded copy
+        wp = torch.zeros((3, 3, cin, cp), device=DEV)
+        wp[..., :cout] = w
+        convs.append(ops.PackedConv.from_source(w, cin, cp, dt))
+        refs.append(ops.PackedConv(wp, None, dt, DEV))
+        cq = (cout + 31) // 32 * 32  # flipped, input channels padded to 32
+        wf = torch.empty((3, 3, cout, cin), device=DEV)
+        ops.flip_weights(w, wf)
+        wfp = torch.zeros((3, 3, cq, cin), device=DEV)
+        wfp[:, :, :cout] = wf
+        convs.append(ops.PackedConv.from_source(w, cq, cin, dt, flip=True))
+        refs.append(ops.PackedConv(wfp, None, dt, DEV))
+    for pc in convs:
+        pc.packed.fill_(0xA5)
+    ops.PackBatch(convs)()
+    torch.cuda.synchronize()
+    for pc, ref in zip(convs, refs):
+        assert torch.equal(pc.packed, ref.packed)
+
+
 @pytest.mark.parametrize("mask", [False, True])
 def test_bn_backward(mask):
     from vmatting import ops
@@ -371,7 +403,7 @@ def test_train_bf16_padded_convs_track_the_filters():
     trn = VideoTrainer(synthetic_vgg16(0), "bf16", DEV, params=params)
     trn.step(cmp, bg, warped, gt, fg)
     assert trn._padconv, "the bf16 trainer pads the narrow convs"
-    for scope, (pc, wp, bp, cout) in trn._padconv.items():
+    for scope, (pc, bp, cout) in trn._padconv.items():
         cpad = (pc.cin + 31) // 32 * 32
         x = torch.randn((1, 9, 13, cpad), device=DEV).to(torch.bfloat16)[..., :pc.cin]
         y = ops.conv3x3(x, pc, "none", affine=False, out_dtype=torch.float32)

@@ -1887,6 +1887,44 @@ __global__ void pack_weights(const float* w, int cin, int cout, ConvArgs g) {
   }
 }
 
+constexpr int PACK_MAX_JOBS = 48;
+struct PackBatch {
+  int n;
+  vm_pack_job j[PACK_MAX_JOBS];
+  int K_pad[PACK_MAX_JOBS], cout_pad[PACK_MAX_JOBS], cin_pad[PACK_MAX_JOBS];
+};
+
+// job blockIdx.y: k_to_tap's decode of the conv geometry (as pack_weights), value from the (flipped) source filter
+__global__ void pack_weights_batch(PackBatch b) {
+  const vm_pack_job& j = b.j[blockIdx.y];
+  const bool bf = j.dtype == VM_BF16;
+  const int GE = bf ? 32 : 16;
+  ConvArgs g{};
+  g.cin_pad = b.cin_pad[blockIdx.y];
+  g.K9 = 9 * g.cin_pad;
+  g.chunk_major = g.cin_pad % GE == 0;
+  g.ng = g.chunk_major ? g.K9 / GE : 0;
+  const int K_pad = b.K_pad[blockIdx.y];
+  const long total = (long)b.cout_pad[blockIdx.y] * K_pad;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int co = (int)(i / K_pad);
+    const int k = (int)(i - (long)co * K_pad);
+    int tap, c;
+    if (bf) k_to_tap<32>(g, k, tap, c);
+    else k_to_tap<16>(g, k, tap, c);
+    float v = 0.f;
+    if (tap < 9 && co < j.cout && c < j.cin) {
+      if (!j.flip) {
+        if (co < j.w_cout && c < j.w_cin) v = j.w[((long)tap * j.w_cin + c) * j.w_cout + co];
+      } else if (c < j.w_cout && co < j.w_cin) {
+        v = j.w[((long)(8 - tap) * j.w_cin + co) * j.w_cout + c];
+      }
+    }
+    if (bf) reinterpret_cast<uint16_t*>(j.packed)[i] = f2bf(v);
+    else reinterpret_cast<float*>(j.packed)[i] = v;
+  }
+}
+
 struct PackGeom {
   int cin_pad, ge, K9, K_pad, cout_pad, chunk_major, ng;
 };
@@ -2402,6 +2440,33 @@ extern "C" int vm_conv3x3_pack_weights(const float* w_hwio, int cin, int cout, i
   if (dtype == VM_BF16) hipLaunchKernelGGL(pack_weights<uint16_t>, dim3(grid), dim3(256), 0, st, w_hwio, cin, cout, a);
   else hipLaunchKernelGGL(pack_weights<float>, dim3(grid), dim3(256), 0, st, w_hwio, cin, cout, a);
   return check_launch("pack_weights");
+}
+
+extern "C" int vm_conv3x3_pack_weights_batch(int njobs, const vm_pack_job* jobs, void* stream) {
+  if (njobs < 0 || (njobs > 0 && !jobs)) return fail(VM_EINVAL, "pack_weights_batch: bad argument");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  for (int base = 0; base < njobs; base += PACK_MAX_JOBS) {
+    PackBatch b{};
+    b.n = njobs - base < PACK_MAX_JOBS ? njobs - base : PACK_MAX_JOBS;
+    long mx = 1;
+    for (int i = 0; i < b.n; ++i) {
+      const vm_pack_job& j = jobs[base + i];
+      if (!j.w || !j.packed || j.cin <= 0 || j.cout <= 0 || j.w_cin <= 0 || j.w_cout <= 0 ||
+          (j.dtype != VM_F32 && j.dtype != VM_BF16))
+        return fail(VM_EINVAL, "pack_weights_batch: bad job %d", base + i);
+      b.j[i] = j;
+      const PackGeom g = geom(j.cin, j.cout, j.dtype);
+      b.K_pad[i] = g.K_pad;
+      b.cout_pad[i] = g.cout_pad;
+      b.cin_pad[i] = g.cin_pad;
+      const long t = (long)g.cout_pad * g.K_pad;
+      if (t > mx) mx = t;
+    }
+    hipLaunchKernelGGL(pack_weights_batch, dim3(grid_for(mx, 256, 256), b.n), dim3(256), 0, st, b);
+    int rc = check_launch("pack_weights_batch");
+    if (rc) return rc;
+  }
+  return VM_OK;
 }
 
 static int conv_impl(const vm_tensor* x, const void* packed, int cin, int cout, const float* bias, const float* scale,

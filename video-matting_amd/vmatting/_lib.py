@@ -50,6 +50,12 @@ class VmLoaderOutputs(ctypes.Structure):
     _fields_ = [("ptr", c_void_p * 5), ("pixstride", ctypes.c_int32 * 5), ("reserved", ctypes.c_int32)]
 
 
+class VmPackJob(ctypes.Structure):
+    _fields_ = [("w", c_void_p), ("packed", c_void_p), ("cin", ctypes.c_int32), ("cout", ctypes.c_int32),
+                ("dtype", ctypes.c_int32), ("flip", ctypes.c_int32), ("w_cin", ctypes.c_int32),
+                ("w_cout", ctypes.c_int32)]
+
+
 class VmTpsMap(ctypes.Structure):
     _fields_ = [("grid", c_void_p), ("nx", ctypes.c_int32), ("ny", ctypes.c_int32), ("upsample", ctypes.c_int32),
                 ("x_span", ctypes.c_int32), ("y_span", ctypes.c_int32), ("reserved", ctypes.c_int32),
@@ -119,6 +125,7 @@ SIGNATURES = [
     ("vm_conv3x3_workspace_bytes", c_size_t, [P, c_int, c_int]),
     ("vm_conv3x3_ex_nhwc", c_int, [P, c_int, c_long, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, P,
                                    c_void_p, c_size_t, c_void_p]),
+    ("vm_conv3x3_pack_weights_batch", c_int, [c_int, ctypes.POINTER(VmPackJob), c_void_p]),
     ("vm_conv3x3_sources_nhwc", c_int, [P, c_int, c_long, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p,
                                         c_int, P, c_void_p]),
     ("vm_conv3x3_wgrad_ex_workspace_bytes", c_size_t, [c_int, c_int, c_int, c_int, c_int, c_int]),

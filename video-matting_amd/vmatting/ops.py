@@ -80,6 +80,27 @@ class PackedConv:
         self.scale = as_f(scale)
         self.shift = as_f(shift)
 
+    @classmethod
+    def from_source(cls, src, cin, cout, dtype="bf16", flip=False, bias=None):
+        """A (cin, cout) conv packed from the f32 HWIO filter ``src`` with zeros outside it: a cout-padded copy of a
+        narrow conv (flip=False), or the data-gradient conv of ``src`` (flip=True: spatially flipped, in/out
+        transposed, so cin >= src's cout and cout = src's cin).  ``src`` is read again by every pack_batch."""
+        self = cls.__new__(cls)
+        self.cin, self.cout = int(cin), int(cout)
+        self.dtype = TORCH_DTYPE[dtype] if isinstance(dtype, str) else dtype
+        self.w_hwio, self._src, self._flip = None, src, bool(flip)
+        nbytes = lib().vm_conv3x3_packed_bytes(self.cin, self.cout, _DT[self.dtype])
+        self.packed = torch.empty(nbytes, dtype=torch.uint8, device=src.device)
+        self.bias, self.scale, self.shift = bias, None, None
+        pack_batch([self])
+        return self
+
+    def pack_job(self):
+        src = self.w_hwio if self.w_hwio is not None else self._src
+        flip = getattr(self, "_flip", False)
+        return _lib.VmPackJob(_ptr(src), _ptr(self.packed), self.cin, self.cout, _DT[self.dtype], int(flip),
+                              int(src.shape[2]), int(src.shape[3]))
+
     def up2x(self):
         """The folded-resize weights of this filter (vm_conv3x3_fold_up2x_weights + pack, cout' = 4*cout),
         built once on first use; None when the compute dtype has no folded path (f32)."""
@@ -98,9 +119,7 @@ class PackedConv:
 
     def repack(self):
         """Re-pack after the f32 HWIO filter changed in place (the optimizer step of train.VideoTrainer)."""
-        check(lib().vm_conv3x3_pack_weights(_ptr(self.w_hwio), self.cin, self.cout, _DT[self.dtype],
-                                            _ptr(self.packed), stream_handle()), "pack_weights")
-        self._up = None
+        pack_batch([self])
         return self
 
     def set_affine(self, scale, shift):
@@ -109,6 +128,24 @@ class PackedConv:
 
     def __call__(self, x, act="none", out=None, out_dtype=None, affine=None):
         return conv3x3(x, self, act, out, out_dtype, affine)
+
+
+class PackBatch:
+    """Re-pack many PackedConvs in one launch (vm_conv3x3_pack_weights_batch); the job array is built once, so the
+    sources and packed buffers must stay where they are (the trainer's flat parameter buffer does)."""
+
+    def __init__(self, convs):
+        self.convs = list(convs)
+        self.jobs = (_lib.VmPackJob * max(1, len(self.convs)))(*[pc.pack_job() for pc in self.convs])
+
+    def __call__(self):
+        check(lib().vm_conv3x3_pack_weights_batch(len(self.convs), self.jobs, stream_handle()), "pack_weights_batch")
+        for pc in self.convs:
+            pc._up = None
+
+
+def pack_batch(convs):
+    PackBatch(convs)()
 
 
 class SourceConcat:

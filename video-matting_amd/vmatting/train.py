@@ -101,45 +101,37 @@ class VideoTrainer:
             parallel.broadcast_tensors([self.flat], src=0)
             for pc in self.model.convs.values():
                 pc.repack()
-        # data-gradient filters: flipped / transposed f32 copies, packed for the forward conv kernels (fp32 path); the
-        # bf16 path packs them bf16 with the gradient channels padded to 32, so the data-gradient convs run on the
-        # patch-reuse MFMA kernel from bf16 copies of the gradients (bn_backward / relu_backward write them)
-        self.dconv, self._wflip, self.dconv16 = {}, {}, {}
+        # data-gradient filters: flipped / transposed packs of the forward filters (fp32 path); the bf16 path packs
+        # them bf16 with the gradient channels padded to 32, so the data-gradient convs run on the patch-reuse MFMA
+        # kernel from bf16 copies of the gradients (bn_backward / relu_backward write them)
+        self.dconv, self.dconv16 = {}, {}
         bf16 = self.model.dtype == torch.bfloat16
         for scope in DGRAD:
             pc = self.model.convs[scope]
-            self._wflip[scope] = torch.empty((3, 3, pc.cout, pc.cin), dtype=torch.float32, device=dev)
-            ops.flip_weights(pc.w_hwio, self._wflip[scope])
             if bf16:
                 cp = (pc.cout + 31) // 32 * 32
-                wpad = torch.zeros((3, 3, cp, pc.cin), dtype=torch.float32, device=dev)
-                wpad[:, :, :pc.cout].copy_(self._wflip[scope])
-                self.dconv16[scope] = (ops.PackedConv(wpad, None, "bf16", dev), wpad)
+                self.dconv16[scope] = ops.PackedConv.from_source(pc.w_hwio, cp, pc.cin, "bf16", flip=True)
             else:
-                self.dconv[scope] = ops.PackedConv(self._wflip[scope], None, "fp32", dev)
+                self.dconv[scope] = ops.PackedConv.from_source(pc.w_hwio, pc.cout, pc.cin, "fp32", flip=True)
         # bf16: the patch-reuse conv kernel needs cout % 8 == 0, so the narrow new_convs (select2_* cout 4,
-        # select1_* cout 2, output cout 1) run on zero-padded copies of their filters into 8-channel buffers
+        # select1_* cout 2, output cout 1) run on zero-padded packs of their filters into 8-channel buffers
         self._padconv = {}
         if self.model.dtype == torch.bfloat16:
             for scope, cin, cout in NEW_CONVS:
                 if cout % 8 and not scope.startswith("upconv"):
-                    cp = (cout + 7) // 8 * 8
-                    wp = torch.zeros((3, 3, cin, cp), dtype=torch.float32, device=dev)
-                    bp = torch.zeros(cp, dtype=torch.float32, device=dev)
-                    self._padconv[scope] = (ops.PackedConv(wp, bp, self.model.dtype, dev), wp, bp, cout)
-            self._sync_padded()
+                    bp = torch.zeros((cout + 7) // 8 * 8, dtype=torch.float32, device=dev)
+                    bp[:cout].copy_(self.P[scope, "b"])
+                    pc = ops.PackedConv.from_source(self.P[scope, "w"], cin, bp.numel(), self.model.dtype, bias=bp)
+                    self._padconv[scope] = (pc, bp, cout)
+        # every filter re-pack of the optimizer step in one launch
+        self._repack = ops.PackBatch(list(self.model.convs.values()) + list(self.dconv16.values()) +
+                                     list(self.dconv.values()) + [v[0] for v in self._padconv.values()])
         # filter gradients: bf16 operands on MFMA in the bf16 path, the exact-f32 kernel in the fp32 (parity) path
         self._mfma_wgrad = self.model.dtype == torch.bfloat16
         self.t = 0
         self._b1p = np.float32(1.0)
         self._b2p = np.float32(1.0)
         self._tb, self._key = None, None
-
-    def _sync_padded(self):
-        for scope, (pc, wp, bp, cout) in self._padconv.items():
-            wp[..., :cout].copy_(self.P[scope, "w"])
-            bp[:cout].copy_(self.P[scope, "b"])
-            pc.repack()
 
     # ------------------------------------------------------------------------------------------- buffers
     def _train_buffers(self, n, h, w):
@@ -181,7 +173,7 @@ class VideoTrainer:
         tb["st_output"] = st(1)
         tb["dz_output"] = torch.zeros((n, h, w, 8), dtype=torch.float32, device=dev)[..., :1]
         # bf16 copies of the gradients the data-gradient convs read, channels zero-padded to 32
-        for scope, (pc16, _) in self.dconv16.items():
+        for scope, pc16 in self.dconv16.items():
             lv = 0 if scope == "output" else {"conv1": 0, "conv2": 1, "conv3": 2, "conv4": 3, "upconv1": 0,
                                               "upconv2": 1, "upconv3": 2}[scope]
             tb["g16_" + scope] = torch.zeros((n, L[lv][0], L[lv][1], pc16.cin), dtype=torch.bfloat16, device=dev)
@@ -247,7 +239,7 @@ class VideoTrainer:
         ops.conv_wgrad(x_in, dz, self.G[scope, "w"], mfma=self._mfma_wgrad)
         if dgrad_out is not None:
             if g16 is not None:
-                ops.conv3x3(g16, self.dconv16[scope][0], "none", out=dgrad_out, affine=False)
+                ops.conv3x3(g16, self.dconv16[scope], "none", out=dgrad_out, affine=False)
             else:
                 ops.conv3x3(dz, self.dconv[scope], "none", out=dgrad_out, affine=False)
         return dz
@@ -275,7 +267,7 @@ class VideoTrainer:
             ops.conv_wgrad(b[RBUF[up]], du, self.G[up, "w"], mfma=self._mfma_wgrad)
             if up in DGRAD:
                 if g16 is not None:
-                    ops.conv3x3(g16, self.dconv16[up][0], "none", out=tb["dr_" + up], affine=False)
+                    ops.conv3x3(g16, self.dconv16[up], "none", out=tb["dr_" + up], affine=False)
                 else:
                     ops.conv3x3(du, self.dconv[up], "none", out=tb["dr_" + up], affine=False)
                 dout = ops.resize_backward(tb["dr_" + up], tb["dprev_" + up])
@@ -291,17 +283,9 @@ class VideoTrainer:
         one = np.float32(1.0)
         lr_t = np.float32(np.float32(self.lr) * np.sqrt(one - self._b2p) / (one - self._b1p))
         ops.adam_tf(self.flat, self.m, self.v, self.grad, lr_t, self.beta1, self.beta2, self.epsilon, scale)
-        for scope, pc in self.model.convs.items():
-            pc.repack()
-        for scope in DGRAD:
-            ops.flip_weights(self.model.convs[scope].w_hwio, self._wflip[scope])
-            if scope in self.dconv16:
-                pc16, wpad = self.dconv16[scope]
-                wpad[:, :, :self._wflip[scope].shape[2]].copy_(self._wflip[scope])
-                pc16.repack()
-            else:
-                self.dconv[scope].repack()
-        self._sync_padded()
+        self._repack()
+        for scope, (pc, bp, cout) in self._padconv.items():
+            bp[:cout].copy_(self.P[scope, "b"])
 
     def step(self, cmp, bg, warped, gt, raw_fg):
         """One training iteration; returns a new device tensor [loss, alpha_loss, compositional_loss] (pre-update),
