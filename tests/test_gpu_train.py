@@ -404,13 +404,15 @@ def test_train_bf16_padded_convs_track_the_filters():
     trn.step(cmp, bg, warped, gt, fg)
     assert trn._padconv, "the bf16 trainer pads the narrow convs"
     for scope, (pc, bp, cout) in trn._padconv.items():
+        cin = trn.P[scope, "w"].shape[2]  # pc.cin may be channel-padded (select1_1: 9 -> 32, zero pad channels)
         cpad = (pc.cin + 31) // 32 * 32
-        x = torch.randn((1, 9, 13, cpad), device=DEV).to(torch.bfloat16)[..., :pc.cin]
-        y = ops.conv3x3(x, pc, "none", affine=False, out_dtype=torch.float32)
+        x = torch.zeros((1, 9, 13, cpad), device=DEV, dtype=torch.bfloat16)
+        x[..., :cin] = torch.randn((1, 9, 13, cin), device=DEV).to(torch.bfloat16)
+        y = ops.conv3x3(x[..., :pc.cin], pc, "none", affine=False, out_dtype=torch.float32)
         fresh = ops.PackedConv(trn.P[scope, "w"].clone(), trn.P[scope, "b"].clone(), "fp32", DEV)
-        xf = torch.zeros((1, 9, 13, cpad), device=DEV)
-        xf[..., :pc.cin] = x.float()
-        want = ops.conv3x3(xf[..., :pc.cin], fresh, "none", affine=False)
+        xf = torch.zeros((1, 9, 13, (cin + 7) // 8 * 8), device=DEV)
+        xf[..., :cin] = x[..., :cin].float()
+        want = ops.conv3x3(xf[..., :cin], fresh, "none", affine=False)
         assert torch.count_nonzero(y[..., cout:]) == 0, scope
         err = (y[..., :cout] - want).abs().max().item() / max(want.abs().max().item(), 1e-30)
         assert err <= 2e-2, (scope, err)

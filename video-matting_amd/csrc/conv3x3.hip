@@ -1109,8 +1109,15 @@ void conv3x3_patch(ConvArgs a) {
         const int pr = rr / C::TW, pc = rr % C::TW;
         const bool ok = r0 + pr < H && c0 + pc < W && cb + cq * 4 < a.cout;
         const int off = ok ? (pr * W + pc) * ycs4 + (cb + cq * 4) * 4 : OOB;
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, d), yfr,
-                                               off, 0, 0);
+        if (splitk || a.y_vec) {
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, d),
+                                                 yfr, off, 0, 0);
+        } else {  // a view whose channel offset / stride is not a multiple of 4 (up1[..., 6:30]): dword stores
+          __builtin_amdgcn_raw_buffer_store_b32(d.x, yfr, off, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b32(d.y, yfr, off + 4, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b32(d.z, yfr, off + 8, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b32(d.w, yfr, off + 12, 0, 0);
+        }
       }
     }
     return;
@@ -2249,9 +2256,11 @@ static long g_pair_kernel = 0;  // vm_conv3x3_pair_first_nhwc: 0 = persistent we
                                 // 1 = streaming patch kernel
 
 static bool patch_ok(const ConvArgs& a, size_t tsize) {
-  // bf16 output, or f32 output without the fused pool / folded resize (cout multiple of 4 for 16-byte stores)
-  const bool yok = a.y_dtype == VM_BF16 ? (a.cout & 7) == 0 : (a.y_dtype == VM_F32 && !a.py && !a.up && (a.cout & 3) == 0);
-  return tsize == 2 && a.chunk_major && a.cin_pad % 32 == 0 && yok && a.y_vec && a.act != VM_ACT_SOFTMAX &&
+  // bf16 output (16-byte aligned view), or f32 output without the fused pool / folded resize (cout multiple of 4;
+  // dword stores when the view is not 16-byte aligned)
+  const bool yok = a.y_dtype == VM_BF16 ? (a.cout & 7) == 0 && a.y_vec
+                                        : (a.y_dtype == VM_F32 && !a.py && !a.up && (a.cout & 3) == 0);
+  return tsize == 2 && a.chunk_major && a.cin_pad % 32 == 0 && yok && a.act != VM_ACT_SOFTMAX &&
          (a.x_src_c <= 0 || a.x_src_c % 32 == 0);
 }
 

@@ -88,15 +88,19 @@ class PackedConv:
         self = cls.__new__(cls)
         self.cin, self.cout = int(cin), int(cout)
         self.dtype = TORCH_DTYPE[dtype] if isinstance(dtype, str) else dtype
-        self.w_hwio, self._src, self._flip = None, src, bool(flip)
+        self.w_hwio, self._src, self._flip = None, src, bool(flip)  # src: a tensor, or a PackedConv (its filter)
         nbytes = lib().vm_conv3x3_packed_bytes(self.cin, self.cout, _DT[self.dtype])
-        self.packed = torch.empty(nbytes, dtype=torch.uint8, device=src.device)
+        self.packed = torch.empty(nbytes, dtype=torch.uint8, device=self._source().device)
         self.bias, self.scale, self.shift = bias, None, None
         pack_batch([self])
         return self
 
-    def pack_job(self):
+    def _source(self):
         src = self.w_hwio if self.w_hwio is not None else self._src
+        return src.w_hwio if isinstance(src, PackedConv) else src
+
+    def pack_job(self):
+        src = self._source()
         flip = getattr(self, "_flip", False)
         return _lib.VmPackJob(_ptr(src), _ptr(self.packed), self.cin, self.cout, _DT[self.dtype], int(flip),
                               int(src.shape[2]), int(src.shape[3]))
@@ -358,6 +362,17 @@ def maxpool2x2(x, out=None):
     xv, yv = nhwc(x), nhwc(out)
     check(lib().vm_maxpool2x2_same_nhwc(ctypes.byref(xv), ctypes.byref(yv), stream_handle()), "maxpool2x2")
     return out
+
+
+def widen(x, c):
+    """The channel view ``x`` widened to ``c`` channels over the same storage: the zero pad channels of a padded
+    buffer, read by a conv whose pack is channel-padded (UNetSimple.padded).  x's channel stride must cover c."""
+    if x.shape[-1] == c:
+        return x
+    cs = x.stride(-2)
+    if x.dim() != 4 or x.stride(-1) != 1 or (x.storage_offset() % cs) + c > cs:
+        raise ValueError("widen: a [N,H,W,%d] view needs %d channels of stride, has %d" % (x.shape[-1], c, cs))
+    return x.as_strided(tuple(x.shape[:-1]) + (c,), x.stride(), x.storage_offset())
 
 
 def resize_bilinear(x, size, out=None):

@@ -27,7 +27,7 @@ import torch
 
 from . import ops, parallel
 from .layers import EPS
-from .unet_simple import NEW_CONVS, UNetSimple, Vgg16, _levels
+from .unet_simple import CIN_PAD, NEW_CONVS, UNetSimple, Vgg16, _levels
 
 # UNetSimple levels from the bottom up (unet_simple.py:119-141):
 # (level, concat buffer, width, [(select scope, source)], upconv scope, upconv input, conv scope, conv output)
@@ -95,6 +95,7 @@ class VideoTrainer:
             self.P[scope, "gamma"].copy_(bnl.gamma)
             self.P[scope, "beta"].copy_(bnl.beta)
             bnl.gamma, bnl.beta = self.P[scope, "gamma"], self.P[scope, "beta"]
+        self.model.relink_padded()
         # DDP: every replica starts from rank 0's variables.  init_conv draws from each process's global numpy RNG
         # (unet_simple.py:10-16), so without this the ranks would apply the averaged gradient to different models
         if parallel.world_size() > 1:
@@ -108,9 +109,10 @@ class VideoTrainer:
         bf16 = self.model.dtype == torch.bfloat16
         for scope in DGRAD:
             pc = self.model.convs[scope]
-            if bf16:
+            if bf16:  # f32 outputs of a multiple of 4 channels (the patch kernel's f32 epilogue): conv1's 30 -> 32
                 cp = (pc.cout + 31) // 32 * 32
-                self.dconv16[scope] = ops.PackedConv.from_source(pc.w_hwio, cp, pc.cin, "bf16", flip=True)
+                self.dconv16[scope] = ops.PackedConv.from_source(pc.w_hwio, cp, (pc.cin + 3) // 4 * 4, "bf16",
+                                                                 flip=True)
             else:
                 self.dconv[scope] = ops.PackedConv.from_source(pc.w_hwio, pc.cout, pc.cin, "fp32", flip=True)
         # bf16: the patch-reuse conv kernel needs cout % 8 == 0, so the narrow new_convs (select2_* cout 4,
@@ -121,11 +123,13 @@ class VideoTrainer:
                 if cout % 8 and not scope.startswith("upconv"):
                     bp = torch.zeros((cout + 7) // 8 * 8, dtype=torch.float32, device=dev)
                     bp[:cout].copy_(self.P[scope, "b"])
-                    pc = ops.PackedConv.from_source(self.P[scope, "w"], cin, bp.numel(), self.model.dtype, bias=bp)
+                    pc = ops.PackedConv.from_source(self.P[scope, "w"], CIN_PAD.get(scope, cin), bp.numel(),
+                                                    self.model.dtype, bias=bp)
                     self._padconv[scope] = (pc, bp, cout)
         # every filter re-pack of the optimizer step in one launch
         self._repack = ops.PackBatch(list(self.model.convs.values()) + list(self.dconv16.values()) +
-                                     list(self.dconv.values()) + [v[0] for v in self._padconv.values()])
+                                     list(self.dconv.values()) + [v[0] for v in self._padconv.values()] +
+                                     list(self.model.padded.values()))
         # filter gradients: bf16 operands on MFMA in the bf16 path, the exact-f32 kernel in the fp32 (parity) path
         self._mfma_wgrad = self.model.dtype == torch.bfloat16
         self.t = 0
@@ -157,7 +161,7 @@ class VideoTrainer:
                     tb["z_" + s] = Z(lv, c)
                 tb["dz_" + s], tb["st_" + s] = F(lv, c), st(c)
             tb["st_" + up] = st(width)
-            tb["dcatn_" + up] = F(lv, width)
+            tb["dcatn_" + up] = F(lv, (width + 3) // 4 * 4)[..., :width]  # conv1's dgrad writes 32 (padded)
             tb["dcat_" + up] = F(lv, width)
             tb["du_" + up] = F(lv, self.model.convs[up].cout)
             if up in DGRAD:
@@ -189,9 +193,11 @@ class VideoTrainer:
         """new_conv (unet_simple.py:19-27) with batch statistics, then ``act``; keeps z and (mean, var)."""
         z, (mean, var) = tb["z_" + scope], tb["st_" + scope]
         if scope in self._padconv:
-            ops.conv3x3(x, self._padconv[scope][0], "none", out=tb["zfull_" + scope], affine=False, splitk=True)
+            pc = self._padconv[scope][0]
+            ops.conv3x3(ops.widen(x, pc.cin), pc, "none", out=tb["zfull_" + scope], affine=False, splitk=True)
         else:
-            ops.conv3x3(x, self.model.convs[scope], "none", out=z, affine=False, splitk=True)
+            pc, x = self.model.conv(scope, x)
+            ops.conv3x3(x, pc, "none", out=z, affine=False, splitk=True)
         ops.bn_stats(z, mean, var)
         bnl = self.model.bn[scope]
         ops.bn_apply(z, mean, var, bnl.gamma, bnl.beta, EPS, act, out=out)
@@ -219,7 +225,8 @@ class VideoTrainer:
                 ops.resize_bilinear(b[prev].base, L[lv], out=r.base)
             else:
                 ops.resize_bilinear(b[prev], L[lv], out=r)
-            ops.conv3x3(r, m.convs[up], "relu", out=c[..., off:width], affine=False, splitk=True)
+            pc, rx = m.conv(up, r)
+            ops.conv3x3(rx, pc, "relu", out=c[..., off:width], affine=False, splitk=True)
             mean, var = tb["st_" + up]
             ops.bn_stats(c, mean, var)
             ops.bn_apply(c, mean, var, m.bn[up].gamma, m.bn[up].beta, EPS, "none", out=b[cat + "n"][..., :width])
@@ -239,7 +246,8 @@ class VideoTrainer:
         ops.conv_wgrad(x_in, dz, self.G[scope, "w"], mfma=self._mfma_wgrad)
         if dgrad_out is not None:
             if g16 is not None:
-                ops.conv3x3(g16, self.dconv16[scope], "none", out=dgrad_out, affine=False)
+                pc = self.dconv16[scope]
+                ops.conv3x3(g16, pc, "none", out=ops.widen(dgrad_out, pc.cout), affine=False)
             else:
                 ops.conv3x3(dz, self.dconv[scope], "none", out=dgrad_out, affine=False)
         return dz

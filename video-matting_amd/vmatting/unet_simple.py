@@ -31,6 +31,9 @@ NEW_CONVS = (("select4_1", 1536, 16), ("select4_2", 1536, 16), ("select4_3", 153
              ("upconv1", 32, 24), ("conv1", 30, 32),
              ("output", 32, 1))
 BN_SCOPES = {"upconv4": 96, "upconv3": 48, "upconv2": 32, "upconv1": 30}
+# bf16: convs whose input width is not a multiple of 32 read a zero-padded buffer through a channel-padded pack,
+# so they run on the patch-reuse MFMA kernel (cin % 32 == 0) instead of the generic one
+CIN_PAD = {"select1_1": 32, "upconv2": 32, "upconv3": 64, "conv3": 64}
 
 
 def _levels(h, w):
@@ -66,6 +69,10 @@ class UNetSimple:
                 params[name] = (w, None if name.startswith("upconv") else b)
         self.params = params
         self.convs = {k: ops.PackedConv(w, b, self.dtype, self.device) for k, (w, b) in params.items()}
+        self.padded = {}
+        if self.dtype == torch.bfloat16:
+            self.padded = {k: ops.PackedConv.from_source(self.convs[k], c, self.convs[k].cout, self.dtype,
+                                                         bias=self.convs[k].bias) for k, c in CIN_PAD.items()}
         self.bn = {k: BatchNorm(c, self.device) for k, _, c in NEW_CONVS if not k.startswith("upconv")}
         self.bn.update({k: BatchNorm(c, self.device) for k, c in BN_SCOPES.items()})
         self._ws, self._key = None, None
@@ -79,7 +86,7 @@ class UNetSimple:
         L = _levels(h, w)
         T, dev = self.dtype, self.device
         Z = lambda lv, c, dt=T, k=1: torch.zeros((k * n, L[lv][0], L[lv][1], c), dtype=dt, device=dev)  # noqa: E731
-        b = {"tin": Z(0, 8, k=3), "in9": Z(0, 16)}
+        b = {"tin": Z(0, 8, k=3), "in9": Z(0, 32)}
         widths = {"conv1_1": (0, 64), "conv1_2": (0, 64), "conv2_1": (1, 128), "conv2_2": (1, 128),
                   "conv3_1": (2, 256), "conv3_2": (2, 256), "conv3_3": (2, 256), "conv4_1": (3, 512),
                   "conv4_2": (3, 512), "conv4_3": (3, 512), "conv5_1": (4, 512), "conv5_2": (4, 512),
@@ -94,12 +101,25 @@ class UNetSimple:
         # gradients 4-14x their f64 sensitivity (tests/test_gpu_train.py::test_train_step_bf16_gradients)
         F = torch.float32
         b.update(up4=Z(3, 96, F), up4n=Z(3, 96), r4=ops.SourceConcat(Z(3, 512, k=3), 3), c4=Z(3, 48),
-                 up3=Z(2, 48, F), up3n=Z(2, 48), r3=Z(2, 48), c3=Z(2, 24),
-                 up2=Z(1, 32, F), up2n=Z(1, 32), r2=Z(1, 24), c2=Z(1, 32),
+                 up3=Z(2, 48, F), up3n=Z(2, 64)[..., :48], r3=Z(2, 64)[..., :48], c3=Z(2, 24),
+                 up2=Z(1, 32, F), up2n=Z(1, 32), r2=Z(1, 32)[..., :24], c2=Z(1, 32),
                  up1=Z(0, 32, F), up1n=Z(0, 32), r1=Z(0, 32), c1=Z(0, 32),
                  logits=Z(0, 1, torch.float32), out=Z(0, 1, torch.float32))
         self._ws, self._key = b, (n, h, w)
         return b
+
+    def conv(self, scope, x):
+        """(pack, input) for conv ``scope`` on the logical view x: the channel-padded pack on x widened to its
+        buffer's zero pad channels (bf16, CIN_PAD), else the conv itself on x."""
+        pc = self.padded.get(scope)
+        if pc is None:
+            return self.convs[scope], x
+        return pc, ops.widen(x, pc.cin)
+
+    def relink_padded(self):
+        """Point the padded packs' biases at their convs' (after VideoTrainer aliases them onto its flat buffer)."""
+        for k, pc in self.padded.items():
+            pc.bias = self.convs[k].bias
 
     def _towers(self, b):
         """The three frozen towers of create_model (vgg1/2/3 on cmp/bg/diff, unet_simple.py:57-89, 148-152) as one
@@ -139,7 +159,7 @@ class UNetSimple:
         C, B = self.convs, self.bn
         self.load_inputs(b, xs)
         self._towers(b)
-        R = lambda x, k, out: conv_bn(x, C[k], B[k], ph, "relu", out)  # noqa: E731
+        R = lambda x, k, out: conv_bn(*self.conv(k, x)[::-1], B[k], ph, "relu", out)  # noqa: E731
         # level 4
         for i in range(3):
             R(b["cat_conv4_%d" % (i + 1)], "select4_%d" % (i + 1), b["up4"][..., 16 * i:16 * (i + 1)])
@@ -173,7 +193,8 @@ class UNetSimple:
             ops.resize_bilinear(prev.base, size, out=rbuf.base)
         else:
             ops.resize_bilinear(prev, size, out=rbuf)
-        ops.conv3x3(rbuf, self.convs[scope], "relu", out=up_slice, affine=False, splitk=True)
+        pc, x = self.conv(scope, rbuf)
+        ops.conv3x3(x, pc, "relu", out=up_slice, affine=False, splitk=True)
         self.bn[scope](cat, phase, out=catn)
 
     def _publish(self, b):
