@@ -2127,6 +2127,128 @@ __global__ __launch_bounds__(256) void conv3x3_up2x_border(BorderArgs a) {
 // ================================================================ split-K reduction
 // out[p][c] = act((sum_s part[s][p][c]) * scale + bias*scale + shift), the splits summed in order (deterministic);
 // one thread per 4 output channels of a pixel
+// ---------------------------------------------------------------- narrow convs (2 <= cout <= 16)
+// The select convs of unet_simple.py:153-168 map 192..1536 channels onto 2..16: a 64-wide output tile would spend
+// 4-32x the MFMA work on zero weights, and the conv is really a stream over its input.  One 16-column MFMA tile
+// (A = the packed weights' first 16 output channels, B = 16 patch pixels), the (TH+2) x 34 input patch of one
+// 32-channel chunk staged in LDS (swizzled 64-byte pixel rows), the next chunk's patch and filter held in registers
+// while this one is consumed.  Output lane l: pixel l % 16, channels 4 (l / 16) .. +3.  ksplit > 1 splits the
+// chunks over gridDim.y into raw f32 partials (splitk_reduce_kernel, fixed order).
+template <int TH>
+__global__ __launch_bounds__(256) void conv3x3_thin(ConvArgs a) {
+  constexpr int TW = 32, PW = TW + 2, PPIX = (TH + 2) * PW, PIECES = PPIX * 4, PPT = (PIECES + 255) / 256;
+  constexpr int RPW = TH / 4;    // patch rows per wave
+  constexpr int WPIECES = 9 * 16 * 4, WPT = (WPIECES + 255) / 256;  // the chunk's filter: [tap][k/8][co 16]
+  __shared__ uint4 xs[PPIX * 4];
+  __shared__ uint4 ws[WPT * 256];  // tail slots hold clamped duplicates (unconditional stores)
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int tw = (a.W + TW - 1) / TW, th = (a.H + TH - 1) / TH;
+  int t = blockIdx.x;
+  const int tx = t % tw;
+  t /= tw;
+  const int ty = t % th;
+  const int n = t / th;
+  const int r0 = ty * TH, c0 = tx * TW;
+  const int nch = a.cin_pad / 32;
+  int cb = 0, ce = nch;
+  if (a.ksplit > 1) {
+    const int per = (nch + a.ksplit - 1) / a.ksplit;
+    cb = blockIdx.y * per;
+    ce = min(nch, cb + per);
+  }
+  // byte offsets of this thread's patch pieces inside image n (out of the frame: out of range -> the hardware
+  // returns 0, SAME padding); the host guarantees H*W*cstride*2 < 2^31
+  int xoff[PPT];
+#pragma unroll
+  for (int i = 0; i < PPT; ++i) {
+    const int id = tid + i * 256;
+    const int p = id >> 2, q = id & 3;
+    const int pr = p / PW, pc = p - pr * PW;
+    const int yy = r0 - 1 + pr, xx = c0 - 1 + pc;
+    const bool ok = id < PIECES && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W;
+    xoff[i] = ok ? ((yy * a.W + xx) * a.x_cstride + q * 8) * 2 : OOB;
+  }
+  const uint16_t* Xn = reinterpret_cast<const uint16_t*>(a.x) + a.x_coff + (long)n * a.H * a.W * a.x_cstride;
+  const __amdgpu_buffer_rsrc_t wrs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.w), 0, 0x7ffffff0, 0x00020000);  // 16 x K_pad bf16 used
+  uint4 xr[PPT], wr[WPT];
+  // the chunk's patch pieces and filter pieces (tap, k/8, co: the A operand's lane order) into registers
+#define VM_THIN_FETCH(CC)                                                                                          \
+  {                                                                                                                \
+    const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(                                          \
+        const_cast<uint16_t*>(Xn + src_chan(a, (CC) * 32)), 0, 0x7ffffff0, 0x00020000);                            \
+    _Pragma("unroll") for (int i = 0; i < PPT; ++i) xr[i] =                                                        \
+        __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xrs, xoff[i], 0, 0));                      \
+    _Pragma("unroll") for (int i = 0; i < WPT; ++i) {                                                              \
+      const int id = min(tid + i * 256, WPIECES - 1);                                                              \
+      wr[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(                                     \
+          wrs, ((id & 15) * a.K_pad + ((CC) * 9 + (id >> 6)) * 32 + ((id >> 4) & 3) * 8) * 2, 0, 0));              \
+    }                                                                                                              \
+  }
+  f32x4 acc[2 * RPW];
+#pragma unroll
+  for (int f = 0; f < 2 * RPW; ++f) acc[f] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (cb < ce) VM_THIN_FETCH(cb);
+  for (int cc = cb; cc < ce; ++cc) {
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < PPT; ++i) {
+      const int id = tid + i * 256;
+      const int p = id >> 2, q = id & 3;
+      if (id < PIECES) xs[p * 4 + (q ^ (((p >> 2) & 1) << 1))] = xr[i];
+    }
+#pragma unroll
+    for (int i = 0; i < WPT; ++i) ws[tid + i * 256] = wr[i];
+    __syncthreads();
+    if (cc + 1 < ce) VM_THIN_FETCH(cc + 1);
+#pragma unroll
+    for (int tp = 0; tp < 9; ++tp) {
+      const uint4 w = ws[tp * 64 + lane];  // A operand: output channel lane % 16, k = 8 (lane / 16) .. +7
+#pragma unroll
+      for (int f = 0; f < 2 * RPW; ++f) {
+        const int rr = wv * RPW + (f >> 1), c = (f & 1) * 16 + (lane & 15);
+        const int pp = (rr + tp / 3) * PW + c + tp % 3;
+        const uint4 b = xs[pp * 4 + ((lane >> 4) ^ (((pp >> 2) & 1) << 1))];
+        mma16<uint16_t>(w, b, acc[f]);
+      }
+    }
+  }
+  const int co0 = 4 * (lane >> 4);
+  if (co0 >= a.cout) return;
+  const bool splitk = a.ksplit > 1;
+  float mul[4], add[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int co = min(co0 + j, a.cout - 1);
+    const float sc = (a.scale && !splitk) ? a.scale[co] : 1.f;
+    mul[j] = sc;
+    add[j] = splitk ? 0.f : (a.bias ? a.bias[co] : 0.f) * sc + (a.shift ? a.shift[co] : 0.f);
+  }
+#pragma unroll
+  for (int f = 0; f < 2 * RPW; ++f) {
+    const int row = r0 + wv * RPW + (f >> 1), col = c0 + (f & 1) * 16 + (lane & 15);
+    if (row >= a.H || col >= a.W) continue;
+    const long m = ((long)n * a.H + row) * a.W + col;
+    if (splitk) {
+      float* d = a.part + ((long)blockIdx.y * a.M + m) * a.cout + co0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (co0 + j < a.cout) d[j] = acc[f][j];
+      continue;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (co0 + j >= a.cout) break;
+      float v = fmaf(acc[f][j], mul[j], add[j]);
+      if (a.act == VM_ACT_RELU) v = fmaxf(v, 0.f);
+      else if (a.act == VM_ACT_SIGMOID) v = sigmoid_precise(v);
+      const long o = m * a.y_cstride + a.y_coff + co0 + j;
+      if (a.y_dtype == VM_BF16) reinterpret_cast<uint16_t*>(a.y)[o] = f2bf(v);
+      else reinterpret_cast<float*>(a.y)[o] = v;
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ part, int ks, long M, int cout,
                                                             const float* bias, const float* scale, const float* shift,
                                                             int act, void* y, int y_dtype, int ycs, int ycoff) {
@@ -2240,6 +2362,42 @@ static int splitk_plan(long n, int h, int w, int cin_pad, int cout) {
   if (ks < 2) return 1;
   const int per = (nch + ks - 1) / ks;
   return (nch + per - 1) / per;  // every split non-empty
+}
+
+// narrow-cout convs (conv3x3_thin): bf16, chunk-major 32-channel granules, 2..16 output channels, no pool / resize
+static long g_thin_kernel = 1;
+static bool thin_ok(int dt, const PackGeom& g, int cout, int x_src_c, int act, const vm_tensor* x) {
+  return g_thin_kernel && dt == VM_BF16 && cout >= 2 && cout <= 16 && g.chunk_major && g.cin_pad % 32 == 0 &&
+         (x_src_c <= 0 || x_src_c % 32 == 0) && act != VM_ACT_SOFTMAX &&
+         (long)x->h * x->w * x->cstride * 2 < 0x7ffffff0L;  // 32-bit byte offsets inside one image
+}
+// split-K plan: below 1024 blocks of 8 x 32 pixels, split the 32-channel chunks over ~thin_blocks (512) blocks
+static long g_thin_th = 8, g_thin_blocks = 512;
+static int thin_splitk_plan(long n, int h, int w, int cin_pad) {
+  const long tiles = n * ((h + 7) / 8) * ((w + 31) / 32);  // in 8-row units whatever the tile height
+  const int nch = cin_pad / 32;
+  if (tiles <= 0 || tiles >= 1024 || nch < 4) return 1;
+  int ks = (int)((g_thin_blocks + tiles - 1) / tiles);
+  if (ks > nch / 2) ks = nch / 2;
+  if (ks < 2) return 1;
+  const int per = (nch + ks - 1) / ks;
+  return (nch + per - 1) / per;
+}
+static int dispatch_thin(ConvArgs& a, long n, hipStream_t st) {
+  const int th = (int)g_thin_th;
+  const long tiles = n * ((a.H + th - 1) / th) * ((a.W + 31) / 32);
+  if (tiles > 0x7fffffffL) return fail(VM_EUNSUPPORTED, "conv3x3_thin: too many tiles");
+  snprintf(g_last_kernel, sizeof g_last_kernel, "vm::conv3x3_thin<%d>", th);
+  const dim3 grid(tiles, a.ksplit > 1 ? a.ksplit : 1);
+  if (th == 16) hipLaunchKernelGGL(conv3x3_thin<16>, grid, dim3(256), 0, st, a);
+  else if (th == 4) hipLaunchKernelGGL(conv3x3_thin<4>, grid, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL(conv3x3_thin<8>, grid, dim3(256), 0, st, a);
+  int rc = check_launch("conv3x3_thin");
+  if (rc || a.ksplit <= 1) return rc;
+  const long work = a.M * ((a.cout + 3) / 4);
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3(grid_for(work, 256)), dim3(256), 0, st, a.part, a.ksplit, a.M, a.cout,
+                     a.bias, a.scale, a.shift, a.act, a.y, a.y_dtype, a.y_cstride, a.y_coff);
+  return check_launch("splitk_reduce");
 }
 
 // tuning knobs (vm_set_option): conv_kernel 0 = auto, 1 = register-staged only, 2 = LDS-DMA whenever legal;
@@ -2386,6 +2544,20 @@ extern "C" int vm_set_option(const char* key, long value) {
   if (!strcmp(key, "conv_kernel")) {
     if (value < 0 || value > 3) return fail(VM_EINVAL, "conv_kernel must be 0..3");
     g_conv_kernel = value;
+    return VM_OK;
+  }
+  if (!strcmp(key, "thin_blocks")) {
+    g_thin_blocks = value;
+    return VM_OK;
+  }
+  if (!strcmp(key, "thin_th")) {
+    if (value != 4 && value != 8 && value != 16) return fail(VM_EINVAL, "thin_th must be 4, 8 or 16");
+    g_thin_th = value;
+    return VM_OK;
+  }
+  if (!strcmp(key, "thin_kernel")) {
+    if (value < 0 || value > 1) return fail(VM_EINVAL, "thin_kernel must be 0 or 1");
+    g_thin_kernel = value;
     return VM_OK;
   }
   if (!strcmp(key, "conv_min_tiles")) {
@@ -2714,6 +2886,14 @@ static int conv_impl(const vm_tensor* x, const void* packed, int cin, int cout, 
     a.py_coff = yp->coff;
     return dispatch_patch(a, st);
   }
+  if (g_conv_kernel == 0 && thin_ok(dt, g, cout, a.x_src_c, act, x)) {
+    const int ks = work ? thin_splitk_plan(x->n, x->h, x->w, a.cin_pad) : 1;
+    if (ks > 1 && work_bytes >= (size_t)ks * M * cout * sizeof(float)) {
+      a.ksplit = ks;
+      a.part = reinterpret_cast<float*>(work);
+    }
+    return dispatch_thin(a, x->n, st);
+  }
   if (dt == VM_BF16 && work && g_conv_kernel == 0 && patch_ok(a, 2) && (cout & 3) == 0) {
     const int ks = splitk_plan(x->n, x->h, x->w, a.cin_pad, cout);
     if (ks > 1 && work_bytes >= (size_t)ks * M * cout * sizeof(float)) {
@@ -2728,8 +2908,13 @@ static int conv_impl(const vm_tensor* x, const void* packed, int cin, int cout, 
 
 // workspace of vm_conv3x3_ex_nhwc: the split-K partial sums of a small-grid bf16 conv, else 0
 extern "C" size_t vm_conv3x3_workspace_bytes(const vm_tensor* x, int cin, int cout) {
-  if (!x || x->dtype != VM_BF16 || cin <= 0 || cout <= 0 || (cout & 3)) return 0;
+  if (!x || x->dtype != VM_BF16 || cin <= 0 || cout <= 0) return 0;
   const PackGeom g = geom(cin, cout, VM_BF16);
+  if (g_conv_kernel == 0 && thin_ok(VM_BF16, g, cout, cin == x->c ? 0 : x->c, VM_ACT_NONE, x)) {
+    const int ks = thin_splitk_plan(x->n, x->h, x->w, g.cin_pad);
+    return ks > 1 ? (size_t)ks * x->n * x->h * x->w * cout * sizeof(float) : 0;
+  }
+  if (cout & 3) return 0;
   if (!g.chunk_major || g.cin_pad % 32) return 0;
   const int ks = splitk_plan(x->n, x->h, x->w, g.cin_pad, cout);
   return ks > 1 ? (size_t)ks * x->n * x->h * x->w * cout * sizeof(float) : 0;
