@@ -319,7 +319,7 @@ __global__ __launch_bounds__(WG_NT) void wgrad_kernel(V x, V dy, float* partials
     n = (int)(t2 / tiles_h);
     x0 = tx * WG_TW;
   };
-  auto issue = [&](long tile) {
+  auto issue = [&](int tile) {
     int n, y0, x0;
     coords(tile, n, y0, x0);
     if constexpr (XV) {
@@ -538,11 +538,11 @@ __global__ __launch_bounds__(256, 2) void wgrad_mfma_kernel(WgArgs a) {
 
   uint4 xb[XPT];
   float4 db[DPT][2];
-  auto coords = [&](long tile, int& n, int& y0, int& x0) {
-    const int tx = (int)(tile % a.tiles_w);
-    const long t2 = tile / a.tiles_w;
-    y0 = (int)(t2 % a.tiles_h) * WM_TH;
-    n = (int)(t2 / a.tiles_h);
+  auto coords = [&](int tile, int& n, int& y0, int& x0) {
+    const int tx = tile % a.tiles_w;
+    const int t2 = tile / a.tiles_w;
+    y0 = (t2 % a.tiles_h) * WM_TH;
+    n = t2 / a.tiles_h;
     x0 = tx * WM_TW;
   };
   // image pixel e of the patch (halo: origin (y0-1, x0-1), 34 wide) or the tile (origin (y0, x0), 32 wide)
@@ -555,7 +555,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_mfma_kernel(WgArgs a) {
       gx = x0 + e % WM_TW;
     }
   };
-  auto issue = [&](long tile) {
+  auto issue = [&](int tile) {
     int n, y0, x0;
     coords(tile, n, y0, x0);
 #pragma unroll
@@ -633,11 +633,15 @@ __global__ __launch_bounds__(256, 2) void wgrad_mfma_kernel(WgArgs a) {
   };
 
   const int g = lane >> 4;
-  if (blockIdx.x < a.ntiles) issue(blockIdx.x);
-  for (long tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
+  // a contiguous run of tiles per block: consecutive K-steps stay on neighbouring rows of the same pages (a
+  // gridDim-strided walk jumps megabytes per step and pays TLB misses on every one)
+  const int t_beg = (int)((long)blockIdx.x * a.ntiles / gridDim.x);
+  const int t_end = (int)((long)(blockIdx.x + 1) * a.ntiles / gridDim.x);
+  if (t_beg < t_end) issue(t_beg);
+  for (int tile = t_beg; tile < t_end; ++tile) {
     commit();
     __syncthreads();
-    if (tile + gridDim.x < a.ntiles) issue(tile + gridDim.x);
+    if (tile + 1 < t_end) issue(tile + 1);
     // K-steps: the 32 pixels of tile rows wave, wave+4, ...; group g of a fragment holds pixels 8g..8g+7
 #pragma unroll
     for (int rr = 0; rr < TH / 4; ++rr) {
@@ -879,6 +883,7 @@ static int launch_wgrad_mfma_t(WgArgs& a, float* dw, hipStream_t st) {
   a.tiles_h = (a.h + TH - 1) / TH;
   a.tiles_w = (a.w + WM_TW - 1) / WM_TW;
   a.ntiles = (long)a.n * a.tiles_h * a.tiles_w;
+  if (a.ntiles > 0x7fffffffL) return fail(VM_EUNSUPPORTED, "conv_wgrad: too many pixel tiles");
   const int ncc = (a.cin + NCI * 16 - 1) / (NCI * 16);
   const long gx = wgrad_mfma_rows(a, NCI * 16);
   hipLaunchKernelGGL((wgrad_mfma_kernel<NCI, NCO, SX, TH>), dim3((unsigned)gx, ncc), dim3(256), lds, st, a);
