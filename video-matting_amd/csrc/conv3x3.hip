@@ -942,7 +942,7 @@ void conv3x3_patch(ConvArgs a) {
 #pragma unroll
     for (int f = 0; f < FP; ++f) {
       int row = abase[f] + toff;
-      if constexpr (FC * FP >= 32) asm volatile("" : "+v"(row));  // recompute per step: no 9-tap address table
+      if constexpr (FC * FP >= 16) asm volatile("" : "+v"(row));  // recompute per step: no 9-tap address table
       bv[f] = *reinterpret_cast<const uint4*>(xp + swz<64>(row, ck));
     }
   };
@@ -956,7 +956,7 @@ void conv3x3_patch(ConvArgs a) {
   if constexpr (G > 1) {
     // one ring slot = one kernel row (G = 3 taps): one barrier per row; inside the row the fragments of tap g+1 are
     // read while tap g's MFMAs run (same slot and patch, no synchronisation needed)
-    static_assert(!PF && !FIRST && ABL == 0, "row-slot pipeline: plain configuration only");
+    static_assert(!PF && !FIRST, "row-slot pipeline: plain configuration only");
     constexpr int R = 9 / G;
     issue_x(cc_beg, cc_beg & 1);
 #pragma unroll
@@ -967,20 +967,55 @@ void conv3x3_patch(ConvArgs a) {
       for (int r = 0; r < R; ++r) {
         const int k = cc * R + r;
         // in flight after W(k): S-2 younger row slots, plus the next patch when it was issued inside that window
-        sync((S - 2) * G * w_n + ((r >= 1 && r <= S - 2) ? x_n : 0));
-        if (r == 0) issue_x(cc + 1, (cc + 1) & 1);
-        int ns = slot + S - 1;
-        ns -= ns >= S ? S : 0;
-        issue_w(k + S - 1, ns);
+        // timing ablations (results are garbage): ABL&4 no synchronisation, ABL&8 barrier without the DMA wait,
+        // ABL&2 no DMA, ABL&1 no MFMA
+        if constexpr (ABL & 8) {
+          asm volatile("" ::: "memory");
+          __builtin_amdgcn_s_barrier();
+          asm volatile("" ::: "memory");
+        } else if constexpr (!(ABL & 4)) {
+          sync((S - 2) * G * w_n + ((r >= 1 && r <= S - 2) ? x_n : 0));
+        }
+        if constexpr (!(ABL & 2)) {
+          if (r == 0) issue_x(cc + 1, (cc + 1) & 1);
+          int ns = slot + S - 1;
+          ns -= ns >= S ? S : 0;
+          issue_w(k + S - 1, ns);
+        }
         uint4 av[2][FC], bv[2][FP];
         frags(av[0], bv[0], slot, cc & 1, r * G);
 #pragma unroll
         for (int g = 0; g < G; ++g) {
           if (g + 1 < G) frags(av[(g + 1) & 1], bv[(g + 1) & 1], slot, cc & 1, r * G + g + 1);
+          if constexpr (ABL & 1) {
 #pragma unroll
-          for (int fc = 0; fc < FC; ++fc)
+            for (int fc = 0; fc < FC; ++fc) asm volatile("" ::"v"(av[g & 1][fc].x), "v"(av[g & 1][fc].w));
 #pragma unroll
-            for (int fp = 0; fp < FP; ++fp) mma16<T>(av[g & 1][fc], bv[g & 1][fp], acc[fc][fp]);
+            for (int fp = 0; fp < FP; ++fp) asm volatile("" ::"v"(bv[g & 1][fp].x), "v"(bv[g & 1][fp].w));
+          } else {
+#pragma unroll
+            for (int fc = 0; fc < FC; ++fc)
+#pragma unroll
+              for (int fp = 0; fp < FP; ++fp) mma16<T>(av[g & 1][fc], bv[g & 1][fp], acc[fc][fp]);
+          }
+        }
+        // schedule experiments (ABL 16 / 32): pin the order of the row's fragment reads and MFMAs
+        if constexpr (ABL & 16) {  // all reads of tap g+1 issued ahead of tap g's MFMAs
+          __builtin_amdgcn_sched_group_barrier(0x100, FC + FP, 0);
+#pragma unroll
+          for (int g = 0; g < G; ++g) {
+            if (g + 1 < G) __builtin_amdgcn_sched_group_barrier(0x100, FC + FP, 0);
+            __builtin_amdgcn_sched_group_barrier(0x8, FC * FP, 0);
+          }
+        } else if constexpr (ABL & 32) {  // tap g+1's reads spread one per MFMA of tap g
+          __builtin_amdgcn_sched_group_barrier(0x100, FC + FP, 0);
+#pragma unroll
+          for (int g = 0; g < G; ++g)
+#pragma unroll
+            for (int i = 0; i < FC * FP; ++i) {
+              __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);
+              if (g + 1 < G && i < FC + FP) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+            }
         }
         slot = slot + 1 == S ? 0 : slot + 1;
       }
@@ -1218,6 +1253,21 @@ void conv3x3_patch(ConvArgs a) {
 // per CU keeps all of conv1_2's weights in LDS (18 K-step slots x 64 couts x 64 B = 72 KB, loaded once) and walks
 // the 8 x 32 tiles t = blockIdx.x, +gridDim.x, ...: the main loop has no barrier and no DMA, and the next tile's
 // input pixels are loaded into registers while the current tile's MFMAs run.
+// The pair kernel's own patch images use a 2-bit chunk swizzle: like swz<64>, conflict-free for the ds_read_b128
+// fragment reads from any start row, and also for ds_write_b128 of 8 consecutive rows (swz<64> is 2-way there)
+__device__ __forceinline__ int swz2(int row, int chunk) { return row * 64 + ((chunk ^ ((row >> 1) & 3)) << 4); }
+
+// MFMA 16x16 output -> whole 16-byte channel chunks: lane (col, q) holds channels 4q..4q+3 of fragment pair member
+// lo (channels 0..15 of a 32-channel group) and hi (16..31).  One v_permlane16_swap per dword trades the odd rows'
+// lo with the even rows' hi, so even q holds channels 4q..4q+7 (chunk q/2) and odd q channels 16+4(q-1)..+7
+// (chunk 2 + q/2) of the 32-channel group.
+__device__ __forceinline__ uint4 chunk_pair(uint2 lo, uint2 hi, int q) {
+  const auto sx = __builtin_amdgcn_permlane16_swap(lo.x, hi.x, false, false);
+  const auto sy = __builtin_amdgcn_permlane16_swap(lo.y, hi.y, false, false);
+  (void)q;
+  return make_uint4(sx[0], sy[0], sx[1], sy[1]);
+}
+
 struct PairCfg {
   static constexpr int TH = 8, TW = 32, BM = TH * TW, PW = TW + 2, PPIX = (TH + 2) * PW;
   static constexpr int IW = TW + 4, IPIX = (TH + 4) * IW;  // 8-channel input patch, origin (r0-2, c0-2)
@@ -1227,11 +1277,25 @@ struct PairCfg {
   static constexpr int PBU = PPIX * 64;                   // bytes of a granule buffer actually addressed
   static constexpr int SR = 64 * 2 + 16;                   // epilogue staging row
   static constexpr int P_OFF = NSTEP * WSLOT, I_OFF = P_OFF + 2 * PBU, S_OFF = I_OFF + IPIX * 16;
-  static constexpr int LDS = S_OFF + BM * SR;
+  static constexpr int R_OFF = S_OFF + BM * SR;             // per-channel epilogue constants: mul[64], add[64], b1[64]
+  static constexpr int LDS = R_OFF + 3 * 64 * 4;
 };
 static_assert(PairCfg::LDS <= 163840, "weights + patch + input + staging in one CU's LDS");
 static_assert(PairCfg::IPIX <= PairCfg::NT, "one input pixel per thread");
 
+// PABL: timing ablations (results are garbage): 1 no first-conv MFMAs, 2 no conv1_2 MFMAs, 4 no output stores,
+// 8 no input loads
+// XF32: the input frame is f32 (x_f32, the UNetVideo path) — a compile-time choice, so the input loads carry no
+// runtime branch (a branch join made hipcc wait for the loads right after issuing them, before conv1_2)
+// a workgroup barrier that orders LDS only (no vmcnt(0) as __syncthreads emits): global stores and loads stay in
+// flight across it
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <int PABL = 0, bool XF32 = true>
 __global__ __launch_bounds__(512) void conv3x3_pair_persist(ConvArgs a) {
   using C = PairCfg;
   using T = uint16_t;
@@ -1257,21 +1321,15 @@ __global__ __launch_bounds__(512) void conv3x3_pair_persist(ConvArgs a) {
   for (int j = 0; j < 3; ++j)
 #pragma unroll
     for (int fc = 0; fc < 4; ++fc) wf[j][fc] = *reinterpret_cast<const uint4*>(w1 + (fc * 16 + col) * 128 + j * 32 + q * 8);
-  float b1[4][4];
-#pragma unroll
-  for (int fc = 0; fc < 4; ++fc)
-#pragma unroll
-    for (int jj = 0; jj < 4; ++jj) b1[fc][jj] = a.bias1 ? a.bias1[fc * 16 + 4 * q + jj] : 0.f;
-  float mul[4][4], add[4][4];
-#pragma unroll
-  for (int fc = 0; fc < 4; ++fc)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int co = min(fc * 16 + 4 * q + j, a.cout - 1);
-      const float sc = a.scale ? a.scale[co] : 1.f;
-      mul[fc][j] = sc;
-      add[fc][j] = (a.bias ? a.bias[co] : 0.f) * sc + (a.shift ? a.shift[co] : 0.f);
-    }
+  // per-channel constants live in LDS (registers go to the conv1_2 fragment prefetch)
+  float* rmul = reinterpret_cast<float*>(smem + C::R_OFF);
+  if (tid < 64) {
+    const int co = min(tid, a.cout - 1);
+    const float sc = a.scale ? a.scale[co] : 1.f;
+    rmul[tid] = sc;
+    rmul[64 + tid] = (a.bias ? a.bias[co] : 0.f) * sc + (a.shift ? a.shift[co] : 0.f);
+    rmul[128 + tid] = a.bias1 ? a.bias1[tid] : 0.f;
+  }
 
   // input pixel of this thread (one per thread): raw registers while in flight, bf16 chunk in LDS
   const T* x8 = reinterpret_cast<const T*>(a.x) + a.x_coff;
@@ -1284,20 +1342,29 @@ __global__ __launch_bounds__(512) void conv3x3_pair_persist(ConvArgs a) {
     const int ir = tid / C::IW, ic = tid - ir * C::IW;
     const int h = (rem / tw) * C::TH - 2 + ir, w = (rem % tw) * C::TW - 2 + ic;
     xin = tid < C::IPIX && (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
-    if (xin) {
-      const long pix = (((long)n * H + h) * W + w) * (long)a.x_cstride;
-      if (a.x_f32) {
+    if (PABL & 8) return;
+    // branch-free: out-of-frame lanes read pixel (0,0) and channels past x_c re-read the last one, so all loads
+    // issue back to back and are waited for once, at store_in (a per-element conditional load makes hipcc wait
+    // for each load in turn)
+    const long pix = xin ? (((long)n * H + h) * W + w) * (long)a.x_cstride : 0;
+    if constexpr (XF32) {
 #pragma unroll
-        for (int c = 0; c < 8; ++c) xr[c] = c < a.x_c ? xf[pix + c] : 0.f;
-      } else {
-        xq = *reinterpret_cast<const uint4*>(x8 + pix);
-      }
+      for (int c = 0; c < 8; ++c) xr[c] = xf[pix + min(c, a.x_c - 1)];
+    } else {
+      xq = *reinterpret_cast<const uint4*>(x8 + pix);
     }
   };
   auto store_in = [&]() {
-    if (tid < C::IPIX)
-      *reinterpret_cast<uint4*>(smem + C::I_OFF + tid * 16) =
-          !xin ? make_uint4(0, 0, 0, 0) : a.x_f32 ? Chunk<T>::pack(xr) : xq;
+    if (tid < C::IPIX) {
+      uint4 v = xq;
+      if constexpr (XF32) {
+        float xz[8];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) xz[c] = c < a.x_c ? xr[c] : 0.f;
+        v = Chunk<T>::pack(xz);
+      }
+      *reinterpret_cast<uint4*>(smem + C::I_OFF + tid * 16) = xin ? v : make_uint4(0, 0, 0, 0);
+    }
   };
 
   int t = blockIdx.x;
@@ -1323,26 +1390,35 @@ __global__ __launch_bounds__(512) void conv3x3_pair_persist(ConvArgs a) {
         uint4 bv = make_uint4(0, 0, 0, 0);
         if (tap < 9 && p < C::PPIX)
           bv = *reinterpret_cast<const uint4*>(smem + C::I_OFF + ((pr + tap / 3) * C::IW + pc + tap % 3) * 16);
+        if constexpr (PABL & 1) {
+          asm volatile("" ::"v"(bv.x), "v"(bv.w));
+        } else {
 #pragma unroll
-        for (int fc = 0; fc < 4; ++fc) mma16<T>(wf[j][fc], bv, acc1[fc]);
+          for (int fc = 0; fc < 4; ++fc) mma16<T>(wf[j][fc], bv, acc1[fc]);
+        }
       }
       const int h = r0 - 1 + pr, w = c0 - 1 + pc;
       const bool inside = (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
-      if (p < C::PPIX) {
+      uint2 pk[4];
 #pragma unroll
-        for (int fc = 0; fc < 4; ++fc) {
-          float v[4];
+      for (int fc = 0; fc < 4; ++fc) {
+        const float4 bb = *reinterpret_cast<const float4*>(rmul + 128 + fc * 16 + 4 * q);
+        const float b1[4] = {bb.x, bb.y, bb.z, bb.w};
+        float v[4];
 #pragma unroll
-          for (int jj = 0; jj < 4; ++jj) v[jj] = inside ? fmaxf(acc1[fc][jj] + b1[fc][jj], 0.f) : 0.f;
-          uint2 pk;
-          pk.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-          pk.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-          *reinterpret_cast<uint2*>(smem + C::P_OFF + (fc >> 1) * C::PBU + swz<64>(p, (fc & 1) * 2 + (q >> 1)) +
-                                    (q & 1) * 8) = pk;
-        }
+        for (int jj = 0; jj < 4; ++jj) v[jj] = inside ? fmaxf(acc1[fc][jj] + b1[jj], 0.f) : 0.f;
+        pk[fc].x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+        pk[fc].y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+      }
+      // whole 16-byte chunks per lane (conflict-free ds_write_b128 under swz2) instead of 8-byte halves
+#pragma unroll
+      for (int g = 0; g < 2; ++g) {
+        const uint4 ck = chunk_pair(pk[2 * g], pk[2 * g + 1], q);
+        if (p < C::PPIX)
+          *reinterpret_cast<uint4*>(smem + C::P_OFF + g * C::PBU + swz2(p, (q & 1) ? 2 + (q >> 1) : q >> 1)) = ck;
       }
     }
-    __syncthreads();
+    lds_barrier();  // LDS only: the previous tile's output stores stay in flight across it
     // (2) next tile's input in flight during the main loop
     const int tn = t + gridDim.x;
     if (tn < ntiles) load_in(tn);
@@ -1358,48 +1434,74 @@ __global__ __launch_bounds__(512) void conv3x3_pair_persist(ConvArgs a) {
       const int p = wave * 32 + fp * 16;
       abase[fp] = (p / C::TW) * C::PW + (p % C::TW) + col;
     }
+    // K-step s = (granule s / 9, tap s % 9); the fragments of step s + 1 are read while step s's MFMAs run
+    auto frags = [&](uint4 (&av)[4], uint4 (&bv)[2], int s) {
+      const int cc = s / 9, tap = s - cc * 9;
+      const char* wp = smem + s * C::WSLOT;
+      const char* xp = smem + C::P_OFF + cc * C::PBU;
+      const int toff = (tap / 3) * C::PW + tap % 3;
 #pragma unroll
-    for (int cc = 0; cc < 2; ++cc)
+      for (int fc = 0; fc < 4; ++fc) av[fc] = *reinterpret_cast<const uint4*>(wp + swz<64>(fc * 16 + col, q));
 #pragma unroll
-      for (int tap = 0; tap < 9; ++tap) {
-        const char* wp = smem + (cc * 9 + tap) * C::WSLOT;
-        const char* xp = smem + C::P_OFF + cc * C::PBU;
-        const int toff = (tap / 3) * C::PW + tap % 3;
-        uint4 av[4], bv[2];
+      for (int fp = 0; fp < 2; ++fp) bv[fp] = *reinterpret_cast<const uint4*>(xp + swz2(abase[fp] + toff, q));
+    };
+    uint4 av[2][4], bv[2][2];
+    frags(av[0], bv[0], 0);
 #pragma unroll
-        for (int fc = 0; fc < 4; ++fc) av[fc] = *reinterpret_cast<const uint4*>(wp + swz<64>(fc * 16 + col, q));
+    for (int s = 0; s < C::NSTEP; ++s) {
+      if (s + 1 < C::NSTEP) frags(av[(s + 1) & 1], bv[(s + 1) & 1], s + 1);
+      if constexpr (PABL & 2) {
 #pragma unroll
-        for (int fp = 0; fp < 2; ++fp) bv[fp] = *reinterpret_cast<const uint4*>(xp + swz<64>(abase[fp] + toff, q));
+        for (int fc = 0; fc < 4; ++fc) asm volatile("" ::"v"(av[s & 1][fc].x), "v"(av[s & 1][fc].w));
+#pragma unroll
+        for (int fp = 0; fp < 2; ++fp) asm volatile("" ::"v"(bv[s & 1][fp].x), "v"(bv[s & 1][fp].w));
+      } else {
 #pragma unroll
         for (int fc = 0; fc < 4; ++fc)
 #pragma unroll
-          for (int fp = 0; fp < 2; ++fp) mma16<T>(av[fc], bv[fp], acc[fc][fp]);
+          for (int fp = 0; fp < 2; ++fp) mma16<T>(av[s & 1][fc], bv[s & 1][fp], acc[fc][fp]);
       }
+    }
+    if constexpr (!(PABL & 2)) {  // pin the order: step s+1's 6 reads ahead of step s's 8 MFMAs
+      __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);
+#pragma unroll
+      for (int s = 0; s < C::NSTEP; ++s) {
+        if (s + 1 < C::NSTEP) __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);
+        __builtin_amdgcn_sched_group_barrier(0x8, 8, 0);
+      }
+    }
     if (tn < ntiles) store_in();  // ip was last read by this tile's first conv, before the barrier above
     // (4) epilogue: bias/affine/act -> bf16 staging -> 16-byte stores (+ fused 2x2 SAME max-pool)
 #pragma unroll
-    for (int fc = 0; fc < 4; ++fc) {
-      const int cl = fc * 16 + 4 * q;
+    for (int fp = 0; fp < 2; ++fp) {
+      const int row = wave * 32 + fp * 16 + col;
+      uint2 pk[4];
 #pragma unroll
-      for (int fp = 0; fp < 2; ++fp) {
-        const int row = wave * 32 + fp * 16 + col;
+      for (int fc = 0; fc < 4; ++fc) {
+        const int cl = fc * 16 + 4 * q;
+        const float4 m4 = *reinterpret_cast<const float4*>(rmul + cl);
+        const float4 a4 = *reinterpret_cast<const float4*>(rmul + 64 + cl);
+        const float mul[4] = {m4.x, m4.y, m4.z, m4.w}, add[4] = {a4.x, a4.y, a4.z, a4.w};
         float v[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          v[j] = fmaf(acc[fc][fp][j], mul[fc][j], add[fc][j]);
+          v[j] = fmaf(acc[fc][fp][j], mul[j], add[j]);
           if (a.act == VM_ACT_RELU) v[j] = fmaxf(v[j], 0.f);
           else if (a.act == VM_ACT_SIGMOID) v[j] = sigmoid_precise(v[j]);
         }
-        uint2 pk;
-        pk.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-        pk.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-        *reinterpret_cast<uint2*>(smem + C::S_OFF + row * C::SR + cl * 2) = pk;
+        pk[fc].x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+        pk[fc].y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
       }
+      // 16-byte chunks: rows of 144 B make 8 consecutive rows hit 8 distinct 4-bank groups (conflict-free b128)
+#pragma unroll
+      for (int g = 0; g < 2; ++g)
+        *reinterpret_cast<uint4*>(smem + C::S_OFF + row * C::SR + 64 * g +
+                                  16 * ((q & 1) ? 2 + (q >> 1) : q >> 1)) = chunk_pair(pk[2 * g], pk[2 * g + 1], q);
     }
     // one barrier publishes the staging, the next tile's input and (for the next first conv) the end of this
     // tile's patch reads; the stores below then overlap the next tile's first conv (staging is rewritten only
     // after the next tile's first barrier)
-    __syncthreads();
+    lds_barrier();  // LDS only: the previous tile's output stores stay in flight across it
     T* yb = reinterpret_cast<T*>(a.y) + a.y_coff + (((long)n * H + r0) * W + c0) * (long)a.y_cstride;
     const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(yb, 0, 0x7ffffff0, 0x00020000);
 #pragma unroll
@@ -1408,7 +1510,7 @@ __global__ __launch_bounds__(512) void conv3x3_pair_persist(ConvArgs a) {
       const int rr = idx >> 3, cq = idx & 7;
       const uint4 d = *reinterpret_cast<const uint4*>(smem + C::S_OFF + rr * C::SR + cq * 16);
       const int pr = rr / C::TW, pc = rr % C::TW;
-      const bool ok = r0 + pr < H && c0 + pc < W && cq * 8 < a.cout;
+      const bool ok = r0 + pr < H && c0 + pc < W && cq * 8 < a.cout && !(PABL & 4);
       const int off = ok ? (pr * W + pc) * ycs2 + cq * 16 : OOB;
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, d), yrs,
                                              off, 0, 0);
@@ -1444,7 +1546,7 @@ __global__ __launch_bounds__(512) void conv3x3_pair_persist(ConvArgs a) {
 #pragma unroll
           for (int j = 0; j < 8; ++j) m[j] = fmaxf(m[j], f[j]);
         }
-        const bool ok = pr0 + pr < PH && pc0 + pc < PWd && cq * 8 < a.cout;
+        const bool ok = pr0 + pr < PH && pc0 + pc < PWd && cq * 8 < a.cout && !(PABL & 4);
         const int off = ok ? ((pr * PWd + pc) * a.py_cstride + cq * 8) * 2 : OOB;
         __builtin_amdgcn_raw_buffer_store_b128(
             __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, Chunk<T>::pack(m)), prs, off, 0, 0);
@@ -2438,6 +2540,16 @@ static int dispatch_patch(ConvArgs& a, hipStream_t st) {
     case 4: return launch_patch<64, 8, 1, 6, 8, 1, 9, false, 4>(a, st);
     case 6: return launch_patch<64, 8, 1, 6, 8, 1, 9, false, 6>(a, st);
     case 7: return launch_patch<64, 8, 1, 6, 8, 1, 9, false, 7>(a, st);
+    // the same ablations on the row-slot default (64 x 8 waves, 2-slot ring of kernel rows)
+    case 11: return launch_patch<64, 8, 1, 2, 8, 1, 9, false, 1, false, 3>(a, st);
+    case 12: return launch_patch<64, 8, 1, 2, 8, 1, 9, false, 2, false, 3>(a, st);
+    case 14: return launch_patch<64, 8, 1, 2, 8, 1, 9, false, 4, false, 3>(a, st);
+    case 16: return launch_patch<64, 8, 1, 2, 8, 1, 9, false, 6, false, 3>(a, st);
+    case 18: return launch_patch<64, 8, 1, 2, 8, 1, 9, false, 8, false, 3>(a, st);
+    case 19: return launch_patch<64, 8, 1, 2, 8, 1, 9, false, 5, false, 3>(a, st);
+    case 20: return launch_patch<64, 8, 1, 2, 8, 1, 9, false, 16, false, 3>(a, st);
+    case 21: return launch_patch<64, 8, 1, 2, 8, 1, 9, false, 32, false, 3>(a, st);
+    case 22: return launch_patch<64, 8, 1, 2, 8, 2, 9, false, 16, false, 3>(a, st);
     default: break;
   }
   switch (g_patch_cfg) {
@@ -2470,6 +2582,14 @@ static int dispatch_patch(ConvArgs& a, hipStream_t st) {
     case 25: return launch_patch<64, 4, 1, 2, 4, 2, 9, false, 0, false, 3>(a, st);
     // one 8 x 32 px patch shared by 256 output channels (8 waves of 64 px x 128 channels, one block per CU)
     case 26: return launch_patch<256, 4, 2, 2, 8, 1, 9, false, 0, false, 3>(a, st);
+    // 64 px x 64 channel wave tiles, 4 waves (two 256 px x 64 channel blocks per CU)
+    case 27: return launch_patch<64, 4, 1, 2, 8, 2, 9, false, 0, false, 3>(a, st);
+    // 16 x 32 px tiles on 16 waves of 32 px x 64 channels (1024 threads, one block per CU): half the weight DMA per MFMA
+    case 28: return launch_patch<64, 16, 1, 2, 16, 1, 9, false, 0, false, 3>(a, st);
+    case 29: return launch_patch<64, 16, 1, 3, 16, 1, 9, false, 0, false, 3>(a, st);
+    // 64 px x 64 channel wave tiles at 4 waves per SIMD (8 waves of 256 px x 128 channels, two blocks per CU)
+    case 30: return launch_patch<128, 4, 2, 3, 8, 2>(a, st);
+    case 31: return launch_patch<128, 4, 2, 4, 8, 2>(a, st);
     default: break;
   }
   // measured per layer inside the UNetVideo 1080p forward (scripts/sweep.sh, profiles/r01_patch_cfg_sweep.txt):
@@ -2487,7 +2607,7 @@ static int dispatch_patch(ConvArgs& a, hipStream_t st) {
     return launch_patch<64, 8, 1, 6>(a, st);
   }
   if (a.cout >= 128 && a.cin_pad >= 512 && sp * ((a.cout + 127) / 128) >= 1000)
-    return launch_patch<128, 4, 1, 4, 8, 2>(a, st);
+    return launch_patch<128, 4, 2, 3, 8, 2>(a, st);  // 64 px x 64 channel waves, 4 per SIMD (r02: -5% vs 4x1 waves)
   if (blocks64 >= 8000) return launch_patch<64, 8, 1, 3, 8, 1, 9, false, 0, false, 3>(a, st);
   if (blocks64 < 512) return launch_patch<64, 4, 1, 2, 4, 2, 9, false, 0, false, 3>(a, st);  // L5: 4 x 32 px tiles
   return launch_patch<64, 8, 1, 2, 8, 1, 9, false, 0, false, 3>(a, st);
@@ -2569,7 +2689,7 @@ extern "C" int vm_set_option(const char* key, long value) {
     return VM_OK;
   }
   if (!strcmp(key, "patch_cfg")) {
-    if (value < 0 || value > 26) return fail(VM_EINVAL, "patch_cfg must be 0..26");
+    if (value < 0 || value > 31) return fail(VM_EINVAL, "patch_cfg must be 0..31");
     g_patch_cfg = value;
     return VM_OK;
   }
@@ -2579,7 +2699,7 @@ extern "C" int vm_set_option(const char* key, long value) {
     return VM_OK;
   }
   if (!strcmp(key, "pair_kernel")) {
-    if (value < 0 || value > 1) return fail(VM_EINVAL, "pair_kernel must be 0 or 1");
+    if (value < 0 || (value > 1 && value < 10) || value > 18) return fail(VM_EINVAL, "pair_kernel must be 0, 1 or 10..18");
     g_pair_kernel = value;
     return VM_OK;
   }
@@ -2728,6 +2848,25 @@ extern "C" int vm_conv3x3_up2x_nhwc(const vm_tensor* x, const void* packed_up, c
   return check_launch("conv3x3_up2x_border");
 }
 
+template <int PABL, bool XF32 = true>
+static int launch_pair_persist(ConvArgs& a, long sp, hipStream_t st) {
+  if (!a.x_f32 && XF32) return launch_pair_persist<PABL, false>(a, sp, st);
+  static int attr_dev = -1, n_cu = 0;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (attr_dev != dev) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3_pair_persist<PABL, XF32>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, PairCfg::LDS);
+    if (e == hipSuccess) e = hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
+    if (e != hipSuccess) return fail(VM_EHIP, "conv3x3_pair_persist setup: %s", hipGetErrorString(e));
+    attr_dev = dev;
+  }
+  const int grid = (int)(sp < n_cu ? sp : n_cu);
+  snprintf(g_last_kernel, sizeof g_last_kernel, "vm::conv3x3_pair_persist");
+  hipLaunchKernelGGL((conv3x3_pair_persist<PABL, XF32>), dim3(grid), dim3(PairCfg::NT), PairCfg::LDS, st, a);
+  return check_launch("conv3x3_pair_persist");
+}
+
 extern "C" int vm_conv3x3_pair_first_nhwc(const vm_tensor* x, const void* packed1, int cin1, const float* bias1,
                                           const void* packed2, int cout2, const float* bias2, const float* scale2,
                                           const float* shift2, int act2, vm_tensor* y, vm_tensor* ypool, void* stream) {
@@ -2761,21 +2900,15 @@ extern "C" int vm_conv3x3_pair_first_nhwc(const vm_tensor* x, const void* packed
   a.w1 = packed1; a.bias1 = bias1; a.x_f32 = xf32; a.x_c = cin1;
   if (ypool) { a.py = ypool->ptr; a.py_cstride = ypool->cstride; a.py_coff = ypool->coff; }
   const long sp = (long)x->n * ((x->h + 7) / 8) * ((x->w + 31) / 32);
-  if (cout2 == 64 && g_pair_kernel == 0 && sp <= 0x7fffffffL) {
-    static int attr_dev = -1, n_cu = 0;
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    if (attr_dev != dev) {
-      hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3_pair_persist),
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, PairCfg::LDS);
-      if (e == hipSuccess) e = hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
-      if (e != hipSuccess) return fail(VM_EHIP, "conv3x3_pair_persist setup: %s", hipGetErrorString(e));
-      attr_dev = dev;
+  if (cout2 == 64 && (g_pair_kernel == 0 || g_pair_kernel >= 10) && sp <= 0x7fffffffL) {
+    switch (g_pair_kernel) {  // >= 10: timing ablations (garbage results)
+      case 11: return launch_pair_persist<1>(a, sp, st);
+      case 12: return launch_pair_persist<2>(a, sp, st);
+      case 14: return launch_pair_persist<4>(a, sp, st);
+      case 18: return launch_pair_persist<8>(a, sp, st);
+      case 13: return launch_pair_persist<3>(a, sp, st);
+      default: return launch_pair_persist<0>(a, sp, st);
     }
-    const int grid = (int)(sp < n_cu ? sp : n_cu);
-    snprintf(g_last_kernel, sizeof g_last_kernel, "vm::conv3x3_pair_persist");
-    hipLaunchKernelGGL(conv3x3_pair_persist, dim3(grid), dim3(PairCfg::NT), PairCfg::LDS, st, a);
-    return check_launch("conv3x3_pair_persist");
   }
   if (sp * ((cout2 + 63) / 64) < 512) return launch_patch<64, 4, 1, 6, 4, 1, 9, false, 0, true>(a, st);
   return launch_patch<64, 8, 1, 6, 8, 1, 9, false, 0, true>(a, st);

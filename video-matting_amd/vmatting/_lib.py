@@ -14,7 +14,8 @@ import os
 import torch  # noqa: F401  (must precede the CDLL load: shared HIP runtime)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libvmatting.so")
+# VM_LIB_PATH: an alternative build of the same library (same-box A/B timing runs); never a fallback
+LIB_PATH = os.environ.get("VM_LIB_PATH") or os.path.join(HERE, "libvmatting.so")
 
 VM_F32, VM_BF16, VM_U8, VM_F64 = 0, 1, 2, 3
 ACT = {"none": 0, "relu": 1, "sigmoid": 2, "softmax": 3}
