@@ -264,6 +264,71 @@ def test_conv_head_alpha_output(dtype, head_kernel):
     assert torch.equal(alpha, ref_alpha)
 
 
+ROWS_CASES = [(1, 9, 33, 64, 64, "relu"), (2, 17, 70, 128, 128, "none"), (1, 20, 45, 96, 192, "relu"),
+              (1, 8, 32, 32, 64, "sigmoid"), (1, 3, 5, 256, 128, "relu"), (1, 37, 70, 512, 256, "relu"),
+              (1, 33, 66, 64, 24, "relu"), (3, 16, 32, 160, 64, "none")]
+
+
+@pytest.mark.parametrize("th", [16, 8])
+@pytest.mark.parametrize("case", ROWS_CASES)
+def test_rows_kernel(case, th):
+    """conv3x3_rows (row-stationary register reuse, conv_rows.hip) vs the oracle on bf16-rounded operands, and
+    BIT-identical to the patch kernel (same per-accumulator MFMA sequence: granules in order, taps 0..8), with the
+    fused 2x2 SAME max-pool of the same launch, partial tiles and a channel-slice output."""
+    from vmatting import _lib, ops
+    n, h, w, cin, cout, act = case
+    rs = np.random.RandomState(cin + cout + h + th)
+    x = torch.from_numpy(rs.normal(size=(n, h, w, cin)).astype(np.float32)).to(torch.bfloat16)
+    wt = torch.from_numpy((rs.normal(size=(3, 3, cin, cout)) * np.sqrt(2.0 / (9 * cin))).astype(np.float32))
+    wt = wt.to(torch.bfloat16).float().numpy()
+    b = (rs.normal(size=cout) * 0.1).astype(np.float32)
+    pc = ops.PackedConv(wt, b, torch.bfloat16, DEV)
+    outs, pools, names = [], [], []
+    for opt in (th, 0):
+        cat = torch.full((n, h, w, cout + 16), 7.0, dtype=torch.bfloat16, device=DEV)
+        pool = torch.empty((n, (h + 1) // 2, (w + 1) // 2, cout), dtype=torch.bfloat16, device=DEV)
+        _lib.set_option("rows_kernel", opt)
+        try:
+            ops.conv3x3(x.to(DEV), pc, act, out=cat[..., 8:8 + cout], pool_out=pool)
+            names.append(_lib.last_conv_kernel())
+        finally:
+            _lib.set_option("rows_kernel", 1)
+        assert bool(torch.all(cat[..., :8] == 7.0)) and bool(torch.all(cat[..., 8 + cout:] == 7.0))
+        outs.append(cat[..., 8:8 + cout].clone())
+        pools.append(pool)
+    assert names[0] == "vm::conv3x3_rows<%d>" % th and names[1].startswith("vm::conv3x3_patch<"), names
+    ref = oops.conv3x3_same(x.float().numpy().astype(np.float64), wt.astype(np.float64)) + b
+    ref = {"relu": oops.relu, "sigmoid": oops.sigmoid}.get(act, lambda v: v)(ref)
+    y = outs[0].float().cpu().numpy()
+    assert np.abs(y - ref).max() / max(1.0, np.abs(ref).max()) < 1e-2
+    assert torch.equal(outs[0], outs[1])
+    assert torch.equal(pools[0], pools[1])
+    assert np.array_equal(H(pools[0]), oops.max_pool_2x2_same(H(outs[0])))
+
+
+@pytest.mark.parametrize("case", [(1, 9, 13, 128, 64), (2, 7, 33, 256, 128), (1, 34, 60, 512, 256), (1, 1, 1, 64, 64)])
+def test_rows_kernel_folded_upconv(case):
+    """The folded 2x upconv (4 phase filters, phase-indexed epilogue scatter) on conv3x3_rows: bit-identical to the
+    patch kernel's result."""
+    from vmatting import _lib, ops
+    n, h, w, cin, cout = case
+    rs = np.random.RandomState(h * 7 + cin)
+    x = torch.from_numpy(rs.normal(size=(n, h, w, cin)).astype(np.float32)).to(torch.bfloat16).to(DEV)
+    wt = (rs.normal(size=(3, 3, cin, cout)) * np.sqrt(2.0 / (9 * cin))).astype(np.float32)
+    pc = ops.PackedConv(wt, (rs.normal(size=cout) * 0.1).astype(np.float32), torch.bfloat16, DEV)
+    res = []
+    for opt in (16, 0):
+        _lib.set_option("rows_kernel", opt)
+        try:
+            res.append(ops.upconv3x3(x, pc, "relu"))
+            name = _lib.last_conv_kernel()
+        finally:
+            _lib.set_option("rows_kernel", 1)
+        if opt:
+            assert name in ("vm::conv3x3_rows<16>", "vm::conv3x3_up2x_border"), name
+    assert torch.equal(res[0], res[1])
+
+
 UP_CASES = [(1, 9, 13, 128, 64), (2, 7, 33, 256, 128), (1, 1, 1, 64, 64), (1, 3, 2, 32, 64), (1, 34, 60, 512, 256),
             (1, 17, 30, 64, 192), (1, 68, 120, 128, 64)]
 

@@ -60,7 +60,13 @@ def main():
     ap.add_argument("--patch-cfg", type=int, default=0)
     ap.add_argument("--ablate", type=int, default=0, help="patch kernel timing ablation (1 no MFMA, 2 no DMA, 4 no sync)")
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--option", action="append", default=[], help="extra vm_set_option key=value")
+    ap.add_argument("--ab", default="", help="key=v1,v2,...: time every value per shape, interleaved in rounds")
+    ap.add_argument("--rounds", type=int, default=3)
     args = ap.parse_args()
+    for kv in args.option:
+        k, v = kv.split("=")
+        _lib.set_option(k, int(v))
     _lib.set_option("conv_kernel", args.kernel)
     _lib.set_option("glds_rb", args.glds_rb)
     _lib.set_option("patch_cfg", args.patch_cfg)
@@ -68,6 +74,21 @@ def main():
     shapes = [("shape",) + tuple(int(v) for v in s.split("x")) for s in args.shape]
     if args.unet_layers:
         shapes += UNET_1080
+    if args.ab:  # same-process interleaved A/B (one variant after the other, several rounds; median per variant)
+        key, vals = args.ab.split("=")
+        vals = [int(v) for v in vals.split(",")]
+        tot = {v: 0.0 for v in vals}
+        for s in shapes:
+            t = {v: [] for v in vals}
+            for _ in range(args.rounds):
+                for v in vals:
+                    _lib.set_option(key, v)
+                    t[v].append(run(*s, dtype=args.dtype, iters=args.iters))
+            for v in vals:
+                tot[v] += float(np.median(t[v]))
+            print("AB %-10s " % s[0] + "  ".join("%s=%d: %.4f ms" % (key, v, np.median(t[v])) for v in vals), flush=True)
+        print("AB total " + "  ".join("%s=%d: %.3f ms" % (key, v, tot[v]) for v in vals))
+        return
     tot = 0.0
     for s in shapes:
         tot += run(*s, dtype=args.dtype, iters=args.iters)

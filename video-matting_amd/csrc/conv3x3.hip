@@ -23,48 +23,11 @@
 #include <cstring>
 #include <cstdio>
 
-#include "vm_common.h"
+#include "conv_common.h"
 
 namespace vm {
 
-struct ConvArgs {
-  const void* x;
-  int x_cstride, x_coff, H, W;
-  long M;  // N*H*W pixels
-  int cin_pad, K9, nk;
-  int chunk_major, ng;  // granule layout and number of real granules (chunk-major)
-  const void* w;
-  int K_pad, cout, cout_pad;
-  const float* bias;
-  const float* scale;
-  const float* shift;
-  int act;
-  void* y;
-  int y_cstride, y_coff, y_dtype, y_vec;
-  int tiles_n, tiles_total;
-  void* py;  // optional fused 2x2/2 SAME max-pool output (patch kernel only), bf16 view
-  int py_cstride, py_coff;
-  int up, up_cout;  // folded 2x resize (patch kernel only): cout = 4 phases x up_cout, y is [N,2H,2W,up_cout]
-  const void* w1;   // FIRST patch kernel: packed cin<=8 -> 64 first conv (tap-major, K_pad 128) and its bias
-  const float* bias1;
-  int x_f32, x_c;   // FIRST: the frame is f32 with x_c channels (converted to bf16 in the prologue)
-  // x_src_c > 0: the input channels come from cin / x_src_c sources of x_src_c channels each, source s at
-  // x_src_stride elements from the view base (tower-major features: unet_simple.py:153-168's concat, never built)
-  int x_src_c;
-  long x_src_stride;
-  // split-K (patch kernel, row-slot pipeline): ksplit > 1 splits the channel granules over gridDim.y; each split
-  // writes raw f32 sums to part[split][pixel][cout] and splitk_reduce_kernel applies bias/affine/act (fixed order)
-  int ksplit;
-  float* part;
-};
-
-// element offset of input channel c (relative to the view's channel 0) under the source split
-__device__ __forceinline__ long src_chan(const ConvArgs& a, int c) {
-  if (a.x_src_c <= 0) return c;
-  const int s = c / a.x_src_c;
-  return (long)s * a.x_src_stride + (c - s * a.x_src_c);
-}
-
+// ConvArgs, swizzles, MFMA wrappers, LDS-DMA helpers: conv_common.h
 // (K element index k) -> (tap, channel); tap 9 = padding (contributes zero)
 template <int GE>
 __device__ __forceinline__ void k_to_tap(const ConvArgs& a, int k, int& tap, int& c) {
@@ -86,54 +49,6 @@ __device__ __forceinline__ void k_to_tap(const ConvArgs& a, int k, int& tap, int
     c = 0;
   }
 }
-
-// LDS images are [row][RB bytes] with the 16-byte chunk index XOR-swizzled per row; both swizzles
-// make the ds_read_b128 lane groups of a 16-row fragment read conflict-free from ANY starting row.
-template <int RB>
-__device__ __forceinline__ int swz(int row, int chunk) {
-  if constexpr (RB == 128) return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4);
-  else return row * 64 + ((chunk ^ (((row >> 2) & 1) << 1)) << 4);
-}
-
-template <typename T>
-__device__ __forceinline__ void mma16(const uint4& a, const uint4& b, f32x4& c);
-
-template <>
-__device__ __forceinline__ void mma16<uint16_t>(const uint4& a, const uint4& b, f32x4& c) {
-  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0, 0,
-                                               0);
-}
-
-template <>
-__device__ __forceinline__ void mma16<float>(const uint4& a, const uint4& b, f32x4& c) {
-  // lane k-slot s = lane>>4 holds k = 4s..4s+3 of the 16-wide k-block; MFMA t consumes element t.
-  c = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.x), __uint_as_float(b.x), c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.y), __uint_as_float(b.y), c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.z), __uint_as_float(b.z), c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.w), __uint_as_float(b.w), c, 0, 0, 0);
-}
-
-// XCD-aware bijective remap: blocks b and b+8 share an XCD -> each XCD gets a contiguous tile range
-__device__ __forceinline__ int xcd_tile(int b, int nwg) {
-  const int q = nwg >> 3, r8 = nwg & 7, xcd = b & 7;
-  return (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + (b >> 3);
-}
-
-// bounds-checked buffer descriptors, rebased per block so 32-bit offsets cover any batch; a lane whose
-// tap leaves the frame gets an out-of-range offset and the hardware returns 0 (SAME zero padding).
-template <typename T>
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t x_rsrc(const ConvArgs& a, long xbase) {
-  const T* Xb = reinterpret_cast<const T*>(a.x) + a.x_coff + xbase * (long)a.x_cstride;
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<T*>(Xb), 0, 0x7ffffff0, 0x00020000);
-}
-template <typename T>
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t w_rsrc(const ConvArgs& a, int n0) {
-  const T* Wb = reinterpret_cast<const T*>(a.w) + (long)n0 * a.K_pad;
-  const uint32_t bytes = (uint32_t)((long)(a.cout_pad - n0) * a.K_pad * (long)sizeof(T));
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<T*>(Wb), 0, bytes, 0x00020000);
-}
-
-constexpr int OOB = (int)0x80000000;
 
 // Decode (h, w) of the pixels m0 + r of a tile without per-lane 64-bit division: the tile origin is decoded
 // once (wave-uniform), a row offset r < BM + W is split by a float reciprocal (exact after one fix-up for
@@ -480,44 +395,6 @@ struct GldsCfg {
   static_assert(XP % NW == 0, "whole X pieces per wave");
   static_assert(S >= 2 && S <= 8, "ring depth");
 };
-
-typedef __attribute__((address_space(3))) void* lds_ptr_t;
-
-__device__ __forceinline__ uint32_t lds_addr(const char* p) {
-  return (uint32_t)(uintptr_t)(lds_ptr_t)(p);
-}
-
-// One 16-byte-per-lane LDS-DMA (buffer_load_dwordx4 ... offen lds) from inline asm.  Issued through asm on
-// purpose: for a compiler-visible LDS-DMA, hipcc cannot prove the slot being read differs from the slots
-// being filled and emits s_waitcnt vmcnt(0) before the next ds_read — draining every stage in flight.
-// The asm is invisible to that bookkeeping; completion is counted by hand (wait_vm) before the barrier
-// that publishes a slot.  M0 is compiler-reserved: set and restored inside the same statement.
-__device__ __forceinline__ void glds16(__amdgpu_buffer_rsrc_t rsrc, uint32_t lds_dst, int voffset) {
-  unsigned keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\t"
-      "s_mov_b32 m0, %2\n\t"
-      "s_nop 0\n\t"
-      "buffer_load_dwordx4 %1, %3, 0 offen lds\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(voffset), "s"(lds_dst), "s"(rsrc)
-      : "memory");
-}
-
-// s_waitcnt vmcnt(n) for a wave-uniform runtime n (immediate operand -> one case per value)
-__device__ __forceinline__ void wait_vm(int n) {
-#define VM_W(N) \
-  case N:       \
-    asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); \
-    break;
-  switch (n) {
-    VM_W(0) VM_W(1) VM_W(2) VM_W(3) VM_W(4) VM_W(5) VM_W(6) VM_W(7) VM_W(8) VM_W(9) VM_W(10) VM_W(11) VM_W(12)
-    VM_W(13) VM_W(14) VM_W(15) VM_W(16) VM_W(17) VM_W(18) VM_W(19) VM_W(20) VM_W(21) VM_W(22) VM_W(23) VM_W(24)
-    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-#undef VM_W
-}
 
 template <typename T, int RB, int BM, int BN, int WM, int WN, int S, bool FAST>
 __global__ __launch_bounds__(512, 1) void conv3x3_glds(ConvArgs a) {
@@ -2382,7 +2259,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
 // ================================================================ dispatch
 // name of the kernel the last conv call on this thread launched, spelled as rocprofv3 reports it
 // (bench.py matches its per-launch PMC traffic by this name)
-static thread_local char g_last_kernel[128];
+thread_local char g_last_kernel[128];
 template <typename T>
 static const char* tname() { return sizeof(T) == 2 ? "unsigned short" : "float"; }
 
@@ -2512,6 +2389,9 @@ static long g_head_kernel = 0;
 static long g_patch_cfg = 0;
 static long g_patch_rowslot = 1;  // 0 = the per-tap-barrier dispatch of r01 (A/B runs)
 static long g_patch_ablate = 0;
+static long g_rows_kernel = 1;        // conv_rows.hip: 0 = off, 1 = auto (grid size), 8 / 16 = forced tile height
+static long g_rows_min_blocks = 900;
+static long g_rows_min_cin = 256;      // short K loops: the 2-blocks-per-CU patch kernel hides prologue/epilogue better
 static long g_pair_kernel = 0;  // vm_conv3x3_pair_first_nhwc: 0 = persistent weights-resident kernel when cout == 64,
                                 // 1 = streaming patch kernel
 
@@ -2592,6 +2472,18 @@ static int dispatch_patch(ConvArgs& a, hipStream_t st) {
     case 31: return launch_patch<128, 4, 2, 4, 8, 2>(a, st);
     default: break;
   }
+  // row-stationary kernel (conv_rows.hip) on grids of >= g_rows_min_blocks 16 x 32 px x 64 channel blocks (one block
+  // per CU: ~4 full rounds); rows_kernel 8 / 16 forces that tile height wherever it is legal
+  if (g_rows_kernel && rows_ok(a)) {
+    if (g_rows_kernel == 8 || g_rows_kernel == 16) return launch_rows(a, st, (int)g_rows_kernel);
+    const long N16 = a.M / ((long)a.H * a.W);
+    const long blocks16 = N16 * ((a.H + 15) / 16) * ((a.W + 31) / 32) * ((a.cout + 63) / 64);
+    // measured in the 1080p forward (scripts/opt_ab.sh): a win for cin >= 512 (upconv_2, conv3_4) and for cin 256 on
+    // >= 2 x 900 blocks (conv2_3); a loss for the folded upconvs (8-byte phase-scattered stores) and shorter K loops
+    if (!a.up && blocks16 >= g_rows_min_blocks && a.cin_pad >= g_rows_min_cin &&
+        (a.cin_pad >= 2 * g_rows_min_cin || blocks16 >= 2 * g_rows_min_blocks))
+      return launch_rows(a, st, 16);
+  }
   // measured per layer inside the UNetVideo 1080p forward (scripts/sweep.sh, profiles/r01_patch_cfg_sweep.txt):
   // 8 waves of 32 px x 64 channels with one barrier per kernel row (3 taps per ring slot) everywhere, except
   // 4 waves of 64 px x 128 channels (2 blocks per CU, one barrier per tap) for cin >= 512, cout >= 128 on grids
@@ -2664,6 +2556,19 @@ extern "C" int vm_set_option(const char* key, long value) {
   if (!strcmp(key, "conv_kernel")) {
     if (value < 0 || value > 3) return fail(VM_EINVAL, "conv_kernel must be 0..3");
     g_conv_kernel = value;
+    return VM_OK;
+  }
+  if (!strcmp(key, "rows_kernel")) {
+    if (value != 0 && value != 1 && value != 8 && value != 16) return fail(VM_EINVAL, "rows_kernel must be 0, 1, 8 or 16");
+    g_rows_kernel = value;
+    return VM_OK;
+  }
+  if (!strcmp(key, "rows_min_cin")) {
+    g_rows_min_cin = value;
+    return VM_OK;
+  }
+  if (!strcmp(key, "rows_min_blocks")) {
+    g_rows_min_blocks = value;
     return VM_OK;
   }
   if (!strcmp(key, "thin_blocks")) {
