@@ -1134,17 +1134,6 @@ void conv3x3_patch(ConvArgs a) {
 // fragment reads from any start row, and also for ds_write_b128 of 8 consecutive rows (swz<64> is 2-way there)
 __device__ __forceinline__ int swz2(int row, int chunk) { return row * 64 + ((chunk ^ ((row >> 1) & 3)) << 4); }
 
-// MFMA 16x16 output -> whole 16-byte channel chunks: lane (col, q) holds channels 4q..4q+3 of fragment pair member
-// lo (channels 0..15 of a 32-channel group) and hi (16..31).  One v_permlane16_swap per dword trades the odd rows'
-// lo with the even rows' hi, so even q holds channels 4q..4q+7 (chunk q/2) and odd q channels 16+4(q-1)..+7
-// (chunk 2 + q/2) of the 32-channel group.
-__device__ __forceinline__ uint4 chunk_pair(uint2 lo, uint2 hi, int q) {
-  const auto sx = __builtin_amdgcn_permlane16_swap(lo.x, hi.x, false, false);
-  const auto sy = __builtin_amdgcn_permlane16_swap(lo.y, hi.y, false, false);
-  (void)q;
-  return make_uint4(sx[0], sy[0], sx[1], sy[1]);
-}
-
 struct PairCfg {
   static constexpr int TH = 8, TW = 32, BM = TH * TW, PW = TW + 2, PPIX = (TH + 2) * PW;
   static constexpr int IW = TW + 4, IPIX = (TH + 4) * IW;  // 8-channel input patch, origin (r0-2, c0-2)
@@ -1290,7 +1279,7 @@ __global__ __launch_bounds__(512) void conv3x3_pair_persist(ConvArgs a) {
       // whole 16-byte chunks per lane (conflict-free ds_write_b128 under swz2) instead of 8-byte halves
 #pragma unroll
       for (int g = 0; g < 2; ++g) {
-        const uint4 ck = chunk_pair(pk[2 * g], pk[2 * g + 1], q);
+        const uint4 ck = chunk_pair(pk[2 * g], pk[2 * g + 1]);
         if (p < C::PPIX)
           *reinterpret_cast<uint4*>(smem + C::P_OFF + g * C::PBU + swz2(p, (q & 1) ? 2 + (q >> 1) : q >> 1)) = ck;
       }
@@ -1373,7 +1362,7 @@ __global__ __launch_bounds__(512) void conv3x3_pair_persist(ConvArgs a) {
 #pragma unroll
       for (int g = 0; g < 2; ++g)
         *reinterpret_cast<uint4*>(smem + C::S_OFF + row * C::SR + 64 * g +
-                                  16 * ((q & 1) ? 2 + (q >> 1) : q >> 1)) = chunk_pair(pk[2 * g], pk[2 * g + 1], q);
+                                  16 * ((q & 1) ? 2 + (q >> 1) : q >> 1)) = chunk_pair(pk[2 * g], pk[2 * g + 1]);
     }
     // one barrier publishes the staging, the next tile's input and (for the next first conv) the end of this
     // tile's patch reads; the stores below then overlap the next tile's first conv (staging is rewritten only
@@ -2391,6 +2380,7 @@ static long g_patch_rowslot = 1;  // 0 = the per-tap-barrier dispatch of r01 (A/
 static long g_patch_ablate = 0;
 static long g_rows_kernel = 1;        // conv_rows.hip: 0 = off, 1 = auto (grid size), 8 / 16 = forced tile height
 static long g_rows_min_blocks = 900;
+static long g_rows_up = 0;            // 1: the folded upconvs too
 static long g_rows_min_cin = 256;      // short K loops: the 2-blocks-per-CU patch kernel hides prologue/epilogue better
 static long g_pair_kernel = 0;  // vm_conv3x3_pair_first_nhwc: 0 = persistent weights-resident kernel when cout == 64,
                                 // 1 = streaming patch kernel
@@ -2480,7 +2470,7 @@ static int dispatch_patch(ConvArgs& a, hipStream_t st) {
     const long blocks16 = N16 * ((a.H + 15) / 16) * ((a.W + 31) / 32) * ((a.cout + 63) / 64);
     // measured in the 1080p forward (scripts/opt_ab.sh): a win for cin >= 512 (upconv_2, conv3_4) and for cin 256 on
     // >= 2 x 900 blocks (conv2_3); a loss for the folded upconvs (8-byte phase-scattered stores) and shorter K loops
-    if (!a.up && blocks16 >= g_rows_min_blocks && a.cin_pad >= g_rows_min_cin &&
+    if ((!a.up || g_rows_up) && blocks16 >= g_rows_min_blocks && a.cin_pad >= g_rows_min_cin &&
         (a.cin_pad >= 2 * g_rows_min_cin || blocks16 >= 2 * g_rows_min_blocks))
       return launch_rows(a, st, 16);
   }
@@ -2561,6 +2551,10 @@ extern "C" int vm_set_option(const char* key, long value) {
   if (!strcmp(key, "rows_kernel")) {
     if (value != 0 && value != 1 && value != 8 && value != 16) return fail(VM_EINVAL, "rows_kernel must be 0, 1, 8 or 16");
     g_rows_kernel = value;
+    return VM_OK;
+  }
+  if (!strcmp(key, "rows_up")) {
+    g_rows_up = value;
     return VM_OK;
   }
   if (!strcmp(key, "rows_min_cin")) {

@@ -129,6 +129,16 @@ __device__ __forceinline__ void wait_vm(int n) {
 #undef VM_W
 }
 
+// MFMA 16x16 output -> whole 16-byte channel chunks: lane (col, q) holds channels 4q..4q+3 of fragment pair member
+// lo (channels 0..15 of a 32-channel group) and hi (16..31).  One v_permlane16_swap per dword trades the odd rows'
+// lo with the even rows' hi, so even q holds channels 4q..4q+7 (chunk q/2) and odd q channels 16+4(q-1)..+7
+// (chunk 2 + q/2) of the 32-channel group.
+__device__ __forceinline__ uint4 chunk_pair(uint2 lo, uint2 hi) {
+  const auto sx = __builtin_amdgcn_permlane16_swap(lo.x, hi.x, false, false);
+  const auto sy = __builtin_amdgcn_permlane16_swap(lo.y, hi.y, false, false);
+  return make_uint4(sx[0], sy[0], sx[1], sy[1]);
+}
+
 // name of the kernel the last conv call on this thread launched, spelled as rocprofv3 reports it (conv3x3.hip)
 extern thread_local char g_last_kernel[128];
 

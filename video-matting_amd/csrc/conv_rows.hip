@@ -278,61 +278,88 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
     const int PH = (H + 1) >> 1, PWo = (W + 1) >> 1;
     T* pbp = uniform_ptr(a.py ? reinterpret_cast<T*>(a.py) + a.py_coff + (long)tt.n * PH * PWo * a.py_cstride : nullptr);
     const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(pbp, 0, 0x7ffffff0, 0x00020000);
+    float mul[FC][4], add[FC][4];
 #pragma unroll
-    for (int f = 0; f < FC; ++f) {
-      const int chn = cg * C::CW + f * 16 + 4 * ck;
-      const bool cok = cb + chn < ccap;
-      float mul[4], add[4];
+    for (int f = 0; f < FC; ++f)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int co = min(cb + chn + j, ccap - 1);
+        const int co = min(cb + cg * C::CW + f * 16 + 4 * ck + j, ccap - 1);
         const float sc = a.scale ? a.scale[co] : 1.f;
-        mul[j] = sc;
-        add[j] = (a.bias ? a.bias[co] : 0.f) * sc + (a.shift ? a.shift[co] : 0.f);
+        mul[f][j] = sc;
+        add[f][j] = (a.bias ? a.bias[co] : 0.f) * sc + (a.shift ? a.shift[co] : 0.f);
       }
+    auto pack4 = [](const float (&v)[4]) __attribute__((always_inline)) {
+      return make_uint2((uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16), (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16));
+    };
+    // FC == 2: the two 16-channel fragments form one 32-channel group, and chunk_pair turns the lanes' 4-channel quads
+    // into whole 16-byte chunks (chunk c16 of the group): one 16-byte store per pixel row instead of two 8-byte ones
+    const int c16 = (ck & 1) ? 2 + (ck >> 1) : ck >> 1;
 #pragma unroll
-      for (int pf = 0; pf < 2; ++pf) {
-        const int c = tt.c0 + pf * 16 + col;
-        float v[R][4];
+    for (int pf = 0; pf < 2; ++pf) {
+      const int c = tt.c0 + pf * 16 + col;
+      float v[R][FC][4];
 #pragma unroll
-        for (int o = 0; o < R; ++o) {
-          const int r = tt.r0 + rg * R + o;
+      for (int o = 0; o < R; ++o) {
+        const int r = tt.r0 + rg * R + o;
+#pragma unroll
+        for (int f = 0; f < FC; ++f)
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            float t = fmaf(acc[o][f][pf][j], mul[j], add[j]);
+            float t = fmaf(acc[o][f][pf][j], mul[f][j], add[f][j]);
             if (a.act == VM_ACT_RELU) t = fmaxf(t, 0.f);
             else if (a.act == VM_ACT_SIGMOID) t = sigmoid_precise(t);
-            v[o][j] = t;
+            v[o][f][j] = t;
           }
-          const bool ok = r < H && c < W && cok;
-          const int pix = a.up ? (2 * r + (phase >> 1)) * YW + 2 * c + (phase & 1) : r * W + c;
-          const uint32_t lo2 = (uint32_t)f2bf(v[o][0]) | ((uint32_t)f2bf(v[o][1]) << 16);
-          const uint32_t hi2 = (uint32_t)f2bf(v[o][2]) | ((uint32_t)f2bf(v[o][3]) << 16);
-          __builtin_amdgcn_raw_buffer_store_b64(
-              __builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, make_uint2(lo2, hi2)), yrs,
-              ok ? (pix * a.y_cstride + cb + chn) * 2 : OOB, 0, 0);
-        }
-        if (a.py) {
+        const int pix = a.up ? (2 * r + (phase >> 1)) * YW + 2 * c + (phase & 1) : r * W + c;
+        if constexpr (FC == 2) {
+          const int chan = cb + cg * C::CW + c16 * 8;
+          const uint4 d = chunk_pair(pack4(v[o][0]), pack4(v[o][1]));
+          const bool ok = r < H && c < W && chan < ccap;
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, d),
+                                                 yrs, ok ? (pix * a.y_cstride + chan) * 2 : OOB, 0, 0);
+        } else {
 #pragma unroll
-          for (int op = 0; op < R / 2; ++op) {
-            const int r = tt.r0 + rg * R + 2 * op;  // even: the window's top row
-            const bool v0 = r < H && c < W, v1 = r + 1 < H && c < W;
-            float m[4];
+          for (int f = 0; f < FC; ++f) {
+            const int chan = cb + cg * C::CW + f * 16 + 4 * ck;
+            const bool ok = r < H && c < W && chan < ccap;
+            __builtin_amdgcn_raw_buffer_store_b64(
+                __builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, pack4(v[o][f])), yrs,
+                ok ? (pix * a.y_cstride + chan) * 2 : OOB, 0, 0);
+          }
+        }
+      }
+      if (a.py) {
+#pragma unroll
+        for (int op = 0; op < R / 2; ++op) {
+          const int r = tt.r0 + rg * R + 2 * op;  // even: the window's top row
+          const bool v0 = r < H && c < W, v1 = r + 1 < H && c < W;
+          float m[FC][4];
+#pragma unroll
+          for (int f = 0; f < FC; ++f)
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-              float t = v0 ? v[2 * op][j] : -INFINITY;
-              if (v1) t = fmaxf(t, v[2 * op + 1][j]);
+              float t = v0 ? v[2 * op][f][j] : -INFINITY;
+              if (v1) t = fmaxf(t, v[2 * op + 1][f][j]);
               // column partner: lane col ^ 1 (DPP quad_perm [1,0,3,2])
               const float u = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(t), 0xB1, 0xF, 0xF, false));
-              m[j] = fmaxf(t, u);
+              m[f][j] = fmaxf(t, u);
             }
-            const int pr = r >> 1, pc = c >> 1;
-            const bool ok = (col & 1) == 0 && pr < PH && pc < PWo && tt.n0 + chn < a.cout;
-            const uint32_t lo2 = (uint32_t)f2bf(m[0]) | ((uint32_t)f2bf(m[1]) << 16);
-            const uint32_t hi2 = (uint32_t)f2bf(m[2]) | ((uint32_t)f2bf(m[3]) << 16);
-            __builtin_amdgcn_raw_buffer_store_b64(
-                __builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, make_uint2(lo2, hi2)), prs,
-                ok ? ((pr * PWo + pc) * a.py_cstride + tt.n0 + chn) * 2 : OOB, 0, 0);
+          const int pr = r >> 1, pc = c >> 1;
+          const bool pok = (col & 1) == 0 && pr < PH && pc < PWo;
+          if constexpr (FC == 2) {
+            const int chan = tt.n0 + cg * C::CW + c16 * 8;
+            const uint4 d = chunk_pair(pack4(m[0]), pack4(m[1]));
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, d),
+                                                   prs, pok && chan < a.cout ? ((pr * PWo + pc) * a.py_cstride + chan) * 2 : OOB,
+                                                   0, 0);
+          } else {
+#pragma unroll
+            for (int f = 0; f < FC; ++f) {
+              const int chan = tt.n0 + cg * C::CW + f * 16 + 4 * ck;
+              __builtin_amdgcn_raw_buffer_store_b64(
+                  __builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, pack4(m[f])), prs,
+                  pok && chan < a.cout ? ((pr * PWo + pc) * a.py_cstride + chan) * 2 : OOB, 0, 0);
+            }
           }
         }
       }
@@ -439,7 +466,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // dummy DMAs past the end must land before the block exits
 }
 
-// the row-stationary kernel takes: bf16 in / bf16 out (8-byte aligned view), chunk-major 32-channel granules, no
+// the row-stationary kernel takes: bf16 in / bf16 out (16-byte aligned views), chunk-major 32-channel granules, no
 // split-K, no softmax epilogue, 32-bit byte offsets inside one image (conv3x3_patch covers everything else)
 bool rows_ok(const ConvArgs& a) {
   const long img_in = (long)a.H * a.W * a.x_cstride * 2;
@@ -447,7 +474,7 @@ bool rows_ok(const ConvArgs& a) {
   return a.chunk_major && a.cin_pad % 32 == 0 && a.y_dtype == VM_BF16 && a.y_vec && (a.cout & 7) == 0 &&
          a.act != VM_ACT_SOFTMAX && a.ksplit <= 1 && (a.x_src_c <= 0 || a.x_src_c % 32 == 0) &&
          (!a.up || a.up_cout % 64 == 0) && img_in < 0x7ffffff0L && img_out < 0x7ffffff0L &&
-         (!a.py || (a.py_cstride % 4 == 0 && a.py_coff % 4 == 0));
+         (!a.py || (a.py_cstride % 8 == 0 && a.py_coff % 8 == 0));
 }
 
 static int g_num_cu = 0;
