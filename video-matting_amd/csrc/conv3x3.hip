@@ -1187,6 +1187,9 @@ __global__ __launch_bounds__(512) void conv3x3_pair_persist(ConvArgs a) {
   for (int j = 0; j < 3; ++j)
 #pragma unroll
     for (int fc = 0; fc < 4; ++fc) wf[j][fc] = *reinterpret_cast<const uint4*>(w1 + (fc * 16 + col) * 128 + j * 32 + q * 8);
+  // consume the fragments here: otherwise hipcc's wait for these loads sits inside the tile loop (it cannot tell the
+  // first iteration from the rest), where every tile then waits vmcnt(3..0) for the PREVIOUS tile's output stores
+  __builtin_amdgcn_s_waitcnt(0xF70);  // vmcnt(0) (expcnt / lgkmcnt at max): a real S_WAITCNT the wait pass accounts for
   // per-channel constants live in LDS (registers go to the conv1_2 fragment prefetch)
   float* rmul = reinterpret_cast<float*>(smem + C::R_OFF);
   if (tid < 64) {
@@ -1237,6 +1240,8 @@ __global__ __launch_bounds__(512) void conv3x3_pair_persist(ConvArgs a) {
   if (t < ntiles) {
     load_in(t);
     store_in();
+    // the input of the block's second tile is in flight from here on (a whole tile ahead of its store_in)
+    if (t + (int)gridDim.x < ntiles) load_in(t + gridDim.x);
   }
   __syncthreads();
   const int ycs2 = a.y_cstride * 2;
@@ -1285,9 +1290,7 @@ __global__ __launch_bounds__(512) void conv3x3_pair_persist(ConvArgs a) {
       }
     }
     lds_barrier();  // LDS only: the previous tile's output stores stay in flight across it
-    // (2) next tile's input in flight during the main loop
     const int tn = t + gridDim.x;
-    if (tn < ntiles) load_in(tn);
     // (3) conv1_2: 2 granules x 9 taps, operands straight from LDS, no barrier
     f32x4 acc[4][2];
 #pragma unroll
@@ -1337,6 +1340,9 @@ __global__ __launch_bounds__(512) void conv3x3_pair_persist(ConvArgs a) {
       }
     }
     if (tn < ntiles) store_in();  // ip was last read by this tile's first conv, before the barrier above
+    // (2') the input of the tile after next goes in flight now, in the registers store_in just freed: one whole tile
+    // of work (its epilogue, first conv and conv1_2) covers the HBM latency of the f32 frame reads
+    if (tn + (int)gridDim.x < ntiles) load_in(tn + gridDim.x);
     // (4) epilogue: bias/affine/act -> bf16 staging -> 16-byte stores (+ fused 2x2 SAME max-pool)
 #pragma unroll
     for (int fp = 0; fp < 2; ++fp) {
