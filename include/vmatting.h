@@ -180,6 +180,13 @@ int vm_bn_apply_nhwc(const vm_tensor* x, vm_tensor* y, const float* mean, const 
 /* tf.nn.softmax over channels — refine.py:31 */
 int vm_softmax_lastdim_nhwc(const vm_tensor* x, vm_tensor* y, void* stream);
 
+/* reader.create_composite_image (reader.py:72-79): out = a*fg + (1-a)*bg on channels 0..2 (channels >= 3: bg),
+ * over `pixels` pixels of `cn` interleaved channels.  fg/bg: img_dtype VM_U8 / VM_F32 / VM_F64; alpha: one
+ * VM_F32 / VM_F64 value per pixel; out: VM_F32 / VM_F64.  Computed in float64 (numpy's promotion), rounded to
+ * out_dtype, so a VM_F64 output is bit-identical to the reference's numpy expression. */
+int vm_composite_image(const void* fg, const void* bg, int img_dtype, const void* alpha, int alpha_dtype,
+                       long pixels, int cn, void* out, int out_dtype, void* stream);
+
 /* flow.warp_img (flow.py:9-18): out[y,x] = bilinear(img, x + flow[y,x,0], y + flow[y,x,1]),
  * cv2.remap INTER_LINEAR / BORDER_CONSTANT 0.  mode 0 = OpenCV 1/32-pixel fixed point, 1 = exact.
  * img [ih,iw] f32, flow [h,w,2] f32, out [h,w] f32.  Batched over `n` frames (contiguous). */

@@ -262,3 +262,32 @@ def test_trimap_bit_exact_vs_oracle(shape, dc):
     assert np.array_equal(got, od.trimap_from_matte(m, *dc))
     with pytest.raises(AssertionError):
         vd.trimap_from_matte(m.astype(np.float32))
+
+
+@pytest.mark.parametrize("shape,cn,idt,adt", [((37, 53), 3, np.uint8, np.float64), ((1080, 1920), 3, np.uint8, np.float32),
+                                               ((16, 9), 4, np.float64, np.float64), ((5, 7), 3, np.float32, np.float32),
+                                               ((0, 4), 3, np.uint8, np.float64)])
+def test_composite_image_matches_numpy(shape, cn, idt, adt):
+    """vm_composite_image vs the reference's own numpy expression (reader.py:72-79): tri_alpha = zeros_like(fg)
+    with channels 0..2 = alpha (a 4th channel keeps alpha 0 -> bg), tri*fg + (1-tri)*bg in float64; f64 output
+    bit-identical, f32 output = its f32 rounding."""
+    from vmatting import reader
+    rs = np.random.RandomState(sum(shape) + cn)
+    if idt == np.uint8:
+        fg, bg = (rs.randint(0, 256, size=shape + (cn,)).astype(np.uint8) for _ in range(2))
+    else:
+        fg, bg = (rs.uniform(0, 255, size=shape + (cn,)).astype(idt) for _ in range(2))
+    alpha = rs.uniform(0, 1, size=shape).astype(adt)
+    if alpha.size:
+        alpha.flat[::7] = 0.0
+        alpha.flat[3::11] = 1.0
+    tri = np.zeros(fg.shape, np.float64)
+    for c in range(min(cn, 3)):
+        tri[..., c] = alpha
+    ref = np.multiply(tri, fg) + np.multiply(1.0 - tri, bg)
+    dev = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    out = reader.create_composite_image(dev(fg), dev(bg), dev(alpha))
+    assert out.dtype == torch.float64
+    assert np.array_equal(H(out), ref)
+    out32 = reader.create_composite_image(dev(fg), dev(bg), dev(alpha), out_dtype=torch.float32)
+    assert np.array_equal(H(out32), ref.astype(np.float32))

@@ -505,3 +505,60 @@ extern "C" int vm_softmax_lastdim_nhwc(const vm_tensor* x, vm_tensor* y, void* s
   hipLaunchKernelGGL(softmax_kernel, dim3(grid_for(M, 256)), dim3(256), 0, st, view(x), view(y));
   return check_launch("softmax");
 }
+
+// ---------------------------------------------------------------- compositing
+// reader.create_composite_image (reader.py:72-79): tri_alpha = zeros_like(fg) with channels 0..2 set to alpha,
+// composite = tri_alpha * fg + (1 - tri_alpha) * bg, in float64 like numpy (channels >= 3 get alpha 0, i.e. bg).
+// Each element is computed in double, products and sum rounded separately (no fma), then rounded to the
+// output dtype, so an f64 output is bit-identical to the numpy expression and an f32 output is its f32 rounding.
+template <typename TI, typename TA, typename TO>
+__global__ void __launch_bounds__(256) composite_kernel(const TI* __restrict__ fg, const TI* __restrict__ bg,
+                                                        const TA* __restrict__ alpha, long elems, int cn,
+                                                        TO* __restrict__ out) {
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < elems; i += stride) {
+    const long p = i / cn;
+    const int c = (int)(i - p * cn);
+    const double a = c < 3 ? (double)alpha[p] : 0.0;
+    double p0 = a * (double)fg[i], p1 = (1.0 - a) * (double)bg[i];
+    asm volatile("" : "+v"(p0), "+v"(p1));  // opaque: the products stay rounded (hipcc would fuse them into v_fmac_f64)
+    const double v = p0 + p1;
+    out[i] = (TO)v;
+  }
+}
+
+template <typename TI, typename TA>
+static void launch_composite(const void* fg, const void* bg, const void* alpha, long elems, int cn, void* out,
+                             int out_dtype, hipStream_t st) {
+  const dim3 grid(grid_for(elems, 256, 256 * 32)), block(256);
+  if (out_dtype == VM_F64)
+    hipLaunchKernelGGL((composite_kernel<TI, TA, double>), grid, block, 0, st, (const TI*)fg, (const TI*)bg,
+                       (const TA*)alpha, elems, cn, (double*)out);
+  else
+    hipLaunchKernelGGL((composite_kernel<TI, TA, float>), grid, block, 0, st, (const TI*)fg, (const TI*)bg,
+                       (const TA*)alpha, elems, cn, (float*)out);
+}
+
+template <typename TI>
+static void launch_composite_a(const void* fg, const void* bg, const void* alpha, int alpha_dtype, long elems, int cn,
+                               void* out, int out_dtype, hipStream_t st) {
+  if (alpha_dtype == VM_F64) launch_composite<TI, double>(fg, bg, alpha, elems, cn, out, out_dtype, st);
+  else launch_composite<TI, float>(fg, bg, alpha, elems, cn, out, out_dtype, st);
+}
+
+extern "C" int vm_composite_image(const void* fg, const void* bg, int img_dtype, const void* alpha, int alpha_dtype,
+                                  long pixels, int cn, void* out, int out_dtype, void* stream) {
+  if (pixels < 0 || cn < 1) return fail(VM_EINVAL, "composite: bad size");
+  if (img_dtype != VM_U8 && img_dtype != VM_F32 && img_dtype != VM_F64)
+    return fail(VM_EUNSUPPORTED, "composite: image dtype must be u8, f32 or f64");
+  if ((alpha_dtype != VM_F32 && alpha_dtype != VM_F64) || (out_dtype != VM_F32 && out_dtype != VM_F64))
+    return fail(VM_EUNSUPPORTED, "composite: alpha / output dtype must be f32 or f64");
+  if (pixels == 0) return VM_OK;
+  if (!fg || !bg || !alpha || !out) return fail(VM_EINVAL, "composite: null pointer");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const long elems = pixels * cn;
+  if (img_dtype == VM_U8) launch_composite_a<uint8_t>(fg, bg, alpha, alpha_dtype, elems, cn, out, out_dtype, st);
+  else if (img_dtype == VM_F32) launch_composite_a<float>(fg, bg, alpha, alpha_dtype, elems, cn, out, out_dtype, st);
+  else launch_composite_a<double>(fg, bg, alpha, alpha_dtype, elems, cn, out, out_dtype, st);
+  return check_launch("composite");
+}

@@ -90,6 +90,8 @@ SIGNATURES = [
     ("vm_bn_stats_nhwc", c_int, [P, c_void_p, c_void_p, c_void_p, c_void_p]),
     ("vm_bn_apply_nhwc", c_int, [P, P, c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_int, c_void_p]),
     ("vm_softmax_lastdim_nhwc", c_int, [P, P, c_void_p]),
+    ("vm_composite_image", c_int, [c_void_p, c_void_p, c_int, c_void_p, c_int, c_long, c_int, c_void_p, c_int,
+                                   c_void_p]),
     ("vm_remap_bilinear_f32", c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_int, c_void_p, c_int,
                                       c_void_p]),
     ("vm_remap_bilinear_u8", c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p]),

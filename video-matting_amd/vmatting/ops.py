@@ -432,6 +432,34 @@ def softmax_lastdim(x, out=None):
     return out
 
 
+
+def composite_image(fg, bg, alpha, out_dtype=torch.float64, out=None):
+    """vm_composite_image: reader.create_composite_image (reader.py:72-79) on the device.
+
+    fg, bg: [..., cn] uint8 / float32 / float64 (same dtype); alpha: [...] float32 / float64.  Computed in
+    float64 like numpy; out_dtype float64 (bit-identical to the reference) or float32.
+    """
+    _require_gpu(fg)
+    if bg.shape != fg.shape or bg.dtype != fg.dtype or bg.device != fg.device:
+        raise ValueError("composite_image: fg and bg must have the same shape, dtype and device")
+    if fg.dim() < 1 or tuple(alpha.shape) != tuple(fg.shape[:-1]):
+        raise ValueError("composite_image: alpha must be fg.shape[:-1], got %s vs %s" % (tuple(alpha.shape), tuple(fg.shape)))
+    if fg.dtype not in (torch.uint8, torch.float32, torch.float64) or alpha.dtype not in (torch.float32, torch.float64):
+        raise TypeError("composite_image: u8/f32/f64 images and f32/f64 alpha expected")
+    if out_dtype not in (torch.float32, torch.float64):
+        raise TypeError("composite_image: out_dtype must be float32 or float64")
+    fg, bg, alpha = fg.contiguous(), bg.contiguous(), alpha.contiguous()
+    if out is None:
+        out = torch.empty(fg.shape, dtype=out_dtype, device=fg.device)
+    elif out.shape != fg.shape or out.dtype != out_dtype or not out.is_contiguous():
+        raise ValueError("composite_image: out must be a contiguous %s tensor of fg's shape" % out_dtype)
+    cn = fg.shape[-1]
+    check(lib().vm_composite_image(_ptr(fg), _ptr(bg), _AUG_DT[fg.dtype], _ptr(alpha), _AUG_DT[alpha.dtype],
+                                   fg.numel() // max(cn, 1), cn, _ptr(out), _AUG_DT[out_dtype], stream_handle()),
+          "composite_image")
+    return out
+
+
 # ---------------------------------------------------------------------------------------------- flow
 
 def remap_f32(img, flow, mode="opencv", out=None):

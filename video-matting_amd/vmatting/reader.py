@@ -39,15 +39,16 @@ def write_flow(flow_path, flow):
         flow.tofile(f)
 
 
-def create_composite_image(fg, bg, alpha):
+def create_composite_image(fg, bg, alpha, out_dtype=torch.float64):
     """reader.create_composite_image (reader.py:72-79): alpha*fg + (1-alpha)*bg per channel.
 
-    numpy in -> float64 numpy out (like the reference); device tensors -> device tensor.
+    numpy in -> float64 numpy out (like the reference); device tensors -> float64 device tensor from the
+    vm_composite_image kernel (bit-identical to the numpy expression; pass out_dtype=torch.float32 to halve
+    the write).
     """
     if isinstance(fg, torch.Tensor):
-        a = alpha.to(torch.float32)
-        a = a[..., None] if a.dim() == fg.dim() - 1 else a
-        return a * fg.to(torch.float32) + (1.0 - a) * bg.to(torch.float32)
+        from vmatting import ops
+        return ops.composite_image(fg, bg, alpha, out_dtype=out_dtype)
     a = np.asarray(alpha, np.float64)[..., None]
     return a * np.asarray(fg) + (1.0 - a) * np.asarray(bg)
 
