@@ -108,3 +108,36 @@ def test_temporal_index_error():
     tp = temporal.TemporalRefiner(dtype="fp32")
     with pytest.raises(IndexError):
         tp(T(prev), T(cur), T(cmp), T(bw), T(fw))
+
+
+@pytest.mark.parametrize("n,h,w", [(1, 37, 70), (2, 8, 32), (1, 1, 1), (1, 135, 240), (1, 17, 33)])
+def test_refine_softmax_kernel_matches_generic_epilogue(n, h, w):
+    """conv3x3_first_softmax (register softmax over the 4 lanes holding a pixel's 64 logits, plain and
+    nontemporal stores) against the generic conv kernel's LDS softmax epilogue on the same bf16 refine input:
+    same bf16 products, f32 sums in another order -> probabilities within 1e-5, rows sum to 1, ragged tiles."""
+    from vmatting import _lib, ops
+    rs = np.random.RandomState(h * 131 + w)
+    x = rs.uniform(-1, 1, size=(n, h, w, 8)).astype(np.float32)
+    x[..., 5:] = 0.0
+    pc = ops.PackedConv((rs.normal(size=(3, 3, 5, 64)) * 0.3).astype(np.float32),
+                        rs.normal(size=64).astype(np.float32), "bf16")
+    xb = T(x).to(torch.bfloat16)[..., :5]  # 5 channels in an 8-channel buffer, as the temporal input
+    outs = {}
+    try:
+        for k in (0, 1, 2):
+            _lib.set_option("softmax_kernel", k)
+            outs[k] = ops.conv3x3(xb, pc, "softmax", out_dtype=torch.float32)
+            name = _lib.last_conv_kernel()
+            assert ("first_softmax" in name) == (k != 0), name
+        for blocks in (1, 3, 7):  # persistent walks with partial last rounds
+            _lib.set_option("softmax_blocks", blocks)
+            assert torch.equal(ops.conv3x3(xb, pc, "softmax", out_dtype=torch.float32), outs[2]), blocks
+    finally:
+        _lib.set_option("softmax_kernel", 1)
+        _lib.set_option("softmax_blocks", 1024)
+    ref = outs[0].cpu().numpy()
+    for k in (1, 2):
+        got = outs[k].cpu().numpy()
+        assert np.abs(got - ref).max() <= 1e-5, (k, np.abs(got - ref).max())
+        np.testing.assert_allclose(got.sum(-1), 1.0, atol=1e-5)
+    assert torch.equal(outs[1], outs[2])

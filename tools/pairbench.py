@@ -21,7 +21,9 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--xdtype", default="fp32")
     ap.add_argument("--hw", default="1080x1920")
+    ap.add_argument("--xin-wide", type=int, default=1)
     a = ap.parse_args()
+    _lib.set_option("pair_xin_wide", a.xin_wide)
     h, w = (int(v) for v in a.hw.split("x"))
     _lib.set_option("pair_kernel", a.pair_kernel)
     rs = np.random.RandomState(0)

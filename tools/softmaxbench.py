@@ -1,0 +1,37 @@
+"""Refine conv4 + softmax (refine.py:27-32) at 1080p bf16: vm softmax_kernel variants side by side.
+
+0 = generic conv kernel + LDS softmax epilogue, 1 = conv3x3_first_softmax, 2 = its nontemporal-store form.
+Algorithmic bytes: 16 B/px bf16 input chunk (8 channels) + 256 B/px f32 softmax out.
+"""
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, __file__.rsplit("/tools/", 1)[0] + "/video-matting_amd")
+from vmatting import _lib, ops  # noqa: E402
+
+h, w = (int(v) for v in (sys.argv[1:3] if len(sys.argv) > 2 else (1080, 1920)))
+rs = np.random.RandomState(0)
+x = torch.from_numpy(rs.uniform(-1, 1, size=(1, h, w, 8)).astype(np.float32)).cuda().to(torch.bfloat16)
+pc = ops.PackedConv((rs.normal(size=(3, 3, 5, 64)) * 0.3).astype(np.float32), rs.normal(size=64).astype(np.float32),
+                    "bf16")
+out = torch.empty((1, h, w, 64), dtype=torch.float32, device="cuda")
+nbytes = h * w * (16 + 256)
+for k, blocks in ((0, 1024), (1, 1024), (2, 1024), (2, 512), (2, 2048), (2, 4096), (2, 100000)):
+    _lib.set_option("softmax_kernel", k)
+    _lib.set_option("softmax_blocks", blocks)
+    fn = lambda: ops.conv3x3(x[..., :5], pc, "softmax", out=out)  # noqa: E731
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(50):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / 50
+    print("softmax_kernel %d blocks %6d  %-40s %.1f us  %.2f TB/s algorithmic" % (k, blocks, _lib.last_conv_kernel(), ms * 1e3,
+                                                                      nbytes / ms / 1e9), flush=True)
+_lib.set_option("softmax_kernel", 1)

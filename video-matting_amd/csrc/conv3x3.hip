@@ -1151,8 +1151,10 @@ static_assert(PairCfg::IPIX <= PairCfg::NT, "one input pixel per thread");
 
 // PABL: timing ablations (results are garbage): 1 no first-conv MFMAs, 2 no conv1_2 MFMAs, 4 no output stores,
 // 8 no input loads
-// XF32: the input frame is f32 (x_f32, the UNetVideo path) — a compile-time choice, so the input loads carry no
-// runtime branch (a branch join made hipcc wait for the loads right after issuing them, before conv1_2)
+// XIN: the input dtype/load form — a compile-time choice, so the input loads carry no runtime branch (a branch join
+// made hipcc wait for the loads right after issuing them, before conv1_2).  0: bf16 8-channel chunks; 1: f32 frame,
+// one dword load per channel; 2: f32 frame with 4 <= x_c <= 8 channels (the UNetVideo path), two 16-byte loads per
+// pixel (channels 0..3 and x_c-4..x_c-1, dword-aligned) instead of 8 dword loads
 // a workgroup barrier that orders LDS only (no vmcnt(0) as __syncthreads emits): global stores and loads stay in
 // flight across it
 __device__ __forceinline__ void lds_barrier() {
@@ -1161,7 +1163,7 @@ __device__ __forceinline__ void lds_barrier() {
   asm volatile("" ::: "memory");
 }
 
-template <int PABL = 0, bool XF32 = true>
+template <int PABL = 0, int XIN = 2>
 __global__ __launch_bounds__(512) void conv3x3_pair_persist(ConvArgs a) {
   using C = PairCfg;
   using T = uint16_t;
@@ -1205,6 +1207,7 @@ __global__ __launch_bounds__(512) void conv3x3_pair_persist(ConvArgs a) {
   const float* xf = reinterpret_cast<const float*>(a.x) + a.x_coff;
   uint4 xq = make_uint4(0, 0, 0, 0);
   float xr[8];
+  f32x4 xlo = f32x4{0.f, 0.f, 0.f, 0.f}, xhi = xlo;
   bool xin = false;
   auto load_in = [&](int t) {
     const int n = t / (th * tw), rem = t - n * th * tw;
@@ -1216,7 +1219,10 @@ __global__ __launch_bounds__(512) void conv3x3_pair_persist(ConvArgs a) {
     // issue back to back and are waited for once, at store_in (a per-element conditional load makes hipcc wait
     // for each load in turn)
     const long pix = xin ? (((long)n * H + h) * W + w) * (long)a.x_cstride : 0;
-    if constexpr (XF32) {
+    if constexpr (XIN == 2) {  // unaligned 16-byte loads (4-byte aligned): memcpy keeps hipcc from assuming 16
+      __builtin_memcpy(&xlo, xf + pix, 16);
+      __builtin_memcpy(&xhi, xf + pix + (a.x_c - 4), 16);
+    } else if constexpr (XIN == 1) {
 #pragma unroll
       for (int c = 0; c < 8; ++c) xr[c] = xf[pix + min(c, a.x_c - 1)];
     } else {
@@ -1226,7 +1232,19 @@ __global__ __launch_bounds__(512) void conv3x3_pair_persist(ConvArgs a) {
   auto store_in = [&]() {
     if (tid < C::IPIX) {
       uint4 v = xq;
-      if constexpr (XF32) {
+      if constexpr (XIN == 2) {
+        float xz[8];
+        const int sh = a.x_c - 4;  // xhi[k] = channel sh + k
+#pragma unroll
+        for (int c = 0; c < 4; ++c) xz[c] = xlo[c];
+#pragma unroll
+        for (int c = 4; c < 8; ++c) {
+          const int k = c - sh;
+          const float h = k == 0 ? xhi[0] : k == 1 ? xhi[1] : k == 2 ? xhi[2] : xhi[3];
+          xz[c] = c < a.x_c ? h : 0.f;
+        }
+        v = Chunk<T>::pack(xz);
+      } else if constexpr (XIN == 1) {
         float xz[8];
 #pragma unroll
         for (int c = 0; c < 8; ++c) xz[c] = c < a.x_c ? xr[c] : 0.f;
@@ -1529,6 +1547,129 @@ __global__ __launch_bounds__(512) void conv3x3_first(ConvArgs a) {
     const int off = ok ? (pr * W + pc) * ycs2 + cq * 16 : OOB;
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, d), yrs,
                                            off, 0, 0);
+  }
+}
+
+// ================================================================ refine conv4 + softmax (refine.py:27-32)
+// RefineNet's only live layer: a cin <= 8 -> 64 3x3 conv whose 64 logits per pixel go straight into
+// tf.nn.softmax and out as f32.  The conv is conv3x3_first's (one 16-byte chunk per pixel, 4 taps x 8 channels
+// per K-step, the 64 x 96 weight slice in registers); the softmax never leaves registers: a pixel's 64 logits
+// sit in the 4 lanes col, col+16, col+32, col+48 (16 each), so two xor-shuffles give the row max and the row
+// sum.  Every lane then stores its four 16-byte channel quads (a wave store covers 16 pixels x 64 contiguous
+// bytes).  The kernel writes 256 B per pixel and reads 16: HBM-write-bound.  NT: nontemporal stores (the
+// 531 MB 1080p output is never re-read by this pass).
+template <bool NT>
+__global__ __launch_bounds__(512) void conv3x3_first_softmax(ConvArgs a) {
+  using T = uint16_t;
+  constexpr int TH = 8, TW = 32, PW = TW + 2, PPIX = (TH + 2) * PW;
+  __shared__ __attribute__((aligned(16))) uint4 patch[PPIX];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int H = a.H, W = a.W, cs = a.x_cstride;
+  const int th = (H + TH - 1) / TH, tw = (W + TW - 1) / TW;
+  const int ntiles = a.tiles_total;
+  // persistent: the block walks tiles blockIdx.x, +gridDim.x, ... (bands of consecutive tiles per XCD); the next
+  // tile's patch pixel is loaded into a register while the current tile computes and stores
+  auto tile_of = [&](int i) {  // a partial last round keeps block order (the band remap is a bijection of a full one)
+    const int base = (i / a.tiles_n) * a.tiles_n;
+    return base + a.tiles_n <= ntiles ? base + xcd_tile(i - base, a.tiles_n) : i;
+  };
+  auto load_patch = [&](int t) {
+    const int n = t / (th * tw), srem = t - n * th * tw;
+    const int r0 = (srem / tw) * TH, c0 = (srem - (srem / tw) * tw) * TW;
+    const int pr = tid / PW, pc = tid - pr * PW;
+    const int h = r0 - 1 + pr, w = c0 - 1 + pc;
+    const bool ok = tid < PPIX && (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
+    const T* xb = reinterpret_cast<const T*>(a.x) + a.x_coff + ((long)n * H + (ok ? h : 0)) * (long)W * cs;
+    return ok ? *reinterpret_cast<const uint4*>(xb + (long)w * cs) : make_uint4(0, 0, 0, 0);
+  };
+  const int col = lane & 15, q = lane >> 4;
+  const __amdgpu_buffer_rsrc_t wrs = w_rsrc<T>(a, 0);
+  uint4 wf[3][4];
+#pragma unroll
+  for (int j = 0; j < 3; ++j)
+#pragma unroll
+    for (int fc = 0; fc < 4; ++fc)
+      wf[j][fc] = __builtin_bit_cast(
+          uint4, __builtin_amdgcn_raw_buffer_load_b128(wrs, ((fc * 16 + col) * a.K_pad + j * 32 + q * 8) * 2, 0, 0));
+  float mul[4][4], add[4][4];
+#pragma unroll
+  for (int fc = 0; fc < 4; ++fc)
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      const int co = fc * 16 + 4 * q + jj;
+      const float sc = a.scale ? a.scale[co] : 1.f;
+      mul[fc][jj] = sc;
+      add[fc][jj] = (a.bias ? a.bias[co] : 0.f) * sc + (a.shift ? a.shift[co] : 0.f);
+    }
+  int i = blockIdx.x;
+  uint4 nxt = i < ntiles ? load_patch(tile_of(i)) : make_uint4(0, 0, 0, 0);
+  for (; i < ntiles; i += gridDim.x) {
+    const int t = tile_of(i);
+    const int n = t / (th * tw), srem = t - n * th * tw;
+    const int r0 = (srem / tw) * TH, c0 = (srem - (srem / tw) * tw) * TW;
+    __syncthreads();  // the previous tile's patch reads are done
+    if (tid < PPIX) patch[tid] = nxt;
+    __syncthreads();
+    if (i + (int)gridDim.x < ntiles) nxt = load_patch(tile_of(i + gridDim.x));
+
+    f32x4 acc[4][2];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int fp = 0; fp < 2; ++fp) acc[k][fp] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const int tap = 4 * j + q;
+      const int toff = (tap / 3) * PW + tap % 3;
+      uint4 bv[2];
+#pragma unroll
+      for (int fp = 0; fp < 2; ++fp) {
+        const uint4 v = patch[wave * PW + fp * 16 + col + (tap < 9 ? toff : 0)];  // patch row `wave` + kernel row
+        bv[fp] = tap < 9 ? v : make_uint4(0, 0, 0, 0);
+      }
+#pragma unroll
+      for (int fc = 0; fc < 4; ++fc)
+#pragma unroll
+        for (int fp = 0; fp < 2; ++fp) mma16<T>(wf[j][fc], bv[fp], acc[fc][fp]);
+    }
+
+    const int ycs = a.y_cstride;
+    float* yb = reinterpret_cast<float*>(a.y) + a.y_coff + (((long)n * H + r0 + wave) * W + c0) * (long)ycs;
+#pragma unroll
+    for (int fp = 0; fp < 2; ++fp) {
+      float v[4][4];
+      float mx = -INFINITY;
+#pragma unroll
+      for (int fc = 0; fc < 4; ++fc)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          v[fc][jj] = fmaf(acc[fc][fp][jj], mul[fc][jj], add[fc][jj]);
+          mx = fmaxf(mx, v[fc][jj]);
+        }
+      mx = fmaxf(mx, __shfl_xor(mx, 16));
+      mx = fmaxf(mx, __shfl_xor(mx, 32));
+      float sum = 0.f;
+#pragma unroll
+      for (int fc = 0; fc < 4; ++fc)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          v[fc][jj] = expf(v[fc][jj] - mx);
+          sum += v[fc][jj];
+        }
+      sum += __shfl_xor(sum, 16);
+      sum += __shfl_xor(sum, 32);
+      const float inv = 1.f / sum;
+      const int pc = fp * 16 + col;
+      if (r0 + wave < H && c0 + pc < W) {
+        float* yp = yb + (long)pc * ycs + 4 * q;
+#pragma unroll
+        for (int fc = 0; fc < 4; ++fc) {
+          const f32x4 o = f32x4{v[fc][0] * inv, v[fc][1] * inv, v[fc][2] * inv, v[fc][3] * inv};
+          if constexpr (NT) __builtin_nontemporal_store(o, reinterpret_cast<f32x4*>(yp + fc * 16));
+          else *reinterpret_cast<f32x4*>(yp + fc * 16) = o;
+        }
+      }
+    }
   }
 }
 
@@ -2525,8 +2666,35 @@ static int launch_first(ConvArgs& a, hipStream_t st) {
   return check_launch("conv3x3_first");
 }
 
+static int g_softmax_kernel = 1;  // 0: the generic kernels' softmax epilogue, 1: conv3x3_first_softmax, 2: its NT form
+static long g_softmax_blocks = 1024;  // persistent grid of conv3x3_first_softmax
+static long g_pair_xin_wide = 1;  // pair kernel, f32 frames with >= 4 channels: two 16-byte loads per pixel (XIN 2)
+
+static int launch_first_softmax(ConvArgs& a, hipStream_t st) {
+  const long N = a.M / ((long)a.H * a.W);
+  const long sp = N * ((a.H + 7) / 8) * ((a.W + 31) / 32);
+  if (sp > 0x7fffffffL) return fail(VM_EUNSUPPORTED, "conv3x3: too many tiles");
+  a.tiles_total = (int)sp;
+  // persistent grid of g_softmax_blocks; tile_of() maps block-order indices in rounds of tiles_n = grid onto
+  // contiguous per-XCD bands (xcd_tile within a round)
+  const int grid = (int)std::min<long>(sp, g_softmax_blocks);
+  a.tiles_n = grid;
+  if (g_softmax_kernel == 2) {
+    snprintf(g_last_kernel, sizeof g_last_kernel, "vm::conv3x3_first_softmax<true>");
+    hipLaunchKernelGGL(conv3x3_first_softmax<true>, dim3(grid), dim3(512), 0, st, a);
+  } else {
+    snprintf(g_last_kernel, sizeof g_last_kernel, "vm::conv3x3_first_softmax<false>");
+    hipLaunchKernelGGL(conv3x3_first_softmax<false>, dim3(grid), dim3(512), 0, st, a);
+  }
+  return check_launch("conv3x3_first_softmax");
+}
+
 template <typename T>
 static int dispatch_mfma(ConvArgs& a, hipStream_t st) {
+  if (sizeof(T) == 2 && g_softmax_kernel != 0 && g_conv_kernel != 1 && g_conv_kernel != 2 && a.cin_pad == 8 &&
+      !a.chunk_major && a.x_src_c <= 0 && a.y_dtype == VM_F32 && a.y_vec && a.act == VM_ACT_SOFTMAX && a.cout == 64 &&
+      a.K_pad == 128)
+    return launch_first_softmax(a, st);
   if (sizeof(T) == 2 && g_conv_kernel != 1 && g_conv_kernel != 2 && a.cin_pad == 8 && !a.chunk_major && a.x_src_c <= 0 &&
       a.y_dtype == VM_BF16 && a.y_vec && a.act != VM_ACT_SOFTMAX && (a.cout & 7) == 0 && a.K_pad == 128)
     return launch_first(a, st);
@@ -2553,6 +2721,16 @@ extern "C" int vm_set_option(const char* key, long value) {
   if (!strcmp(key, "conv_kernel")) {
     if (value < 0 || value > 3) return fail(VM_EINVAL, "conv_kernel must be 0..3");
     g_conv_kernel = value;
+    return VM_OK;
+  }
+  if (!strcmp(key, "softmax_kernel")) {
+    if (value < 0 || value > 2) return fail(VM_EINVAL, "softmax_kernel must be 0..2");
+    g_softmax_kernel = value;
+    return VM_OK;
+  }
+  if (!strcmp(key, "softmax_blocks")) {
+    if (value < 1 || value > (1 << 20)) return fail(VM_EINVAL, "softmax_blocks must be 1..2^20");
+    g_softmax_blocks = value;
     return VM_OK;
   }
   if (!strcmp(key, "head_th")) {
@@ -2607,6 +2785,11 @@ extern "C" int vm_set_option(const char* key, long value) {
   if (!strcmp(key, "patch_rowslot")) {
     if (value < 0 || value > 1) return fail(VM_EINVAL, "patch_rowslot must be 0 or 1");
     g_patch_rowslot = value;
+    return VM_OK;
+  }
+  if (!strcmp(key, "pair_xin_wide")) {
+    if (value < 0 || value > 1) return fail(VM_EINVAL, "pair_xin_wide must be 0 or 1");
+    g_pair_xin_wide = value;
     return VM_OK;
   }
   if (!strcmp(key, "pair_kernel")) {
@@ -2759,14 +2942,17 @@ extern "C" int vm_conv3x3_up2x_nhwc(const vm_tensor* x, const void* packed_up, c
   return check_launch("conv3x3_up2x_border");
 }
 
-template <int PABL, bool XF32 = true>
+template <int PABL, int XIN = 2>
 static int launch_pair_persist(ConvArgs& a, long sp, hipStream_t st) {
-  if (!a.x_f32 && XF32) return launch_pair_persist<PABL, false>(a, sp, st);
+  if constexpr (XIN == 2) {
+    if (!a.x_f32) return launch_pair_persist<PABL, 0>(a, sp, st);
+    if (a.x_c < 4 || !g_pair_xin_wide) return launch_pair_persist<PABL, 1>(a, sp, st);
+  }
   static int attr_dev = -1, n_cu = 0;
   int dev = 0;
   (void)hipGetDevice(&dev);
   if (attr_dev != dev) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3_pair_persist<PABL, XF32>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3_pair_persist<PABL, XIN>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, PairCfg::LDS);
     if (e == hipSuccess) e = hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
     if (e != hipSuccess) return fail(VM_EHIP, "conv3x3_pair_persist setup: %s", hipGetErrorString(e));
@@ -2774,7 +2960,7 @@ static int launch_pair_persist(ConvArgs& a, long sp, hipStream_t st) {
   }
   const int grid = (int)(sp < n_cu ? sp : n_cu);
   snprintf(g_last_kernel, sizeof g_last_kernel, "vm::conv3x3_pair_persist");
-  hipLaunchKernelGGL((conv3x3_pair_persist<PABL, XF32>), dim3(grid), dim3(PairCfg::NT), PairCfg::LDS, st, a);
+  hipLaunchKernelGGL((conv3x3_pair_persist<PABL, XIN>), dim3(grid), dim3(PairCfg::NT), PairCfg::LDS, st, a);
   return check_launch("conv3x3_pair_persist");
 }
 
