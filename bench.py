@@ -566,6 +566,8 @@ def main():
     ap.add_argument("--no-profile", action="store_true", help="skip per-conv HIP events")
     ap.add_argument("--layers", action="store_true", help="per-conv timing breakdown on stderr")
     ap.add_argument("--no-graph", action="store_true", help="time eager launches instead of the captured HIP graph")
+    ap.add_argument("--no-split-head", action="store_true",
+                    help="conv1_5 over the whole cat1 instead of the pair kernel's head split (A/B)")
     ap.add_argument("--no-loader", action="store_true", help="skip the training-sample loader record (rank 0, N=1)")
     ap.add_argument("--no-augment", action="store_true", help="skip the augmentation record (rank 0, N=1)")
     ap.add_argument("--no-train", action="store_true", help="skip the config-5 training-step record (all ranks)")
@@ -593,7 +595,9 @@ def main():
     # buffers are broadcast (one RCCL collective) so replicas are bit-identical by construction
     vgg = synthetic_vgg16(0)
     np.random.seed(0)
-    model = unet.UNetVideo(vgg, dtype=args.dtype, device=dev).prepare()
+    model = unet.UNetVideo(vgg, dtype=args.dtype, device=dev)
+    model.split_head = not args.no_split_head
+    model.prepare()
     parallel.broadcast_tensors(model.weights_flat(), src=0)
 
     B, H, W = args.batch, args.height, args.width

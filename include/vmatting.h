@@ -142,6 +142,22 @@ int vm_conv3x3_pair_first_nhwc(const vm_tensor* x, const void* packed1, int cin1
                                const void* packed2, int cout2, const float* bias2, const float* scale2,
                                const float* shift2, int act2, vm_tensor* y, vm_tensor* ypool, void* stream);
 
+/* The pair kernel with the head split (unet.py:170-172 + 203-205): conv1_5 over cat1 = [up, skip] is linear in
+ * its input channels, so the skip half's share is taken where conv1_2's output is made.  Besides y/ypool the pair
+ * kernel writes partial[pixel][12] (f32, n*h*w*12 floats): taps 0..8 of sum_c y[pixel][c] * head_w[tap][head_coff+c]
+ * (head_w = conv1_5's HWIO f32 filter [3,3,head_cin,1], bf16-rounded like the packed head; 9..11 = 0).  store_y = 0
+ * leaves y unwritten (only the pool and the partials leave the chip).  vm_conv3x3_head_partial_nhwc then runs the
+ * head over the other channels (x = the up half, packed for that many channels) and adds
+ * sum_tap partial[pixel + offset(tap)][tap] (zero outside the frame) before bias / act / alpha. */
+int vm_conv3x3_pair_first_head_nhwc(const vm_tensor* x, const void* packed1, int cin1, const float* bias1,
+                                    const void* packed2, int cout2, const float* bias2, const float* scale2,
+                                    const float* shift2, int act2, vm_tensor* y, vm_tensor* ypool,
+                                    const float* head_w, int head_cin, int head_coff, float* partial, int store_y,
+                                    void* stream);
+int vm_conv3x3_head_partial_nhwc(const vm_tensor* x, const void* packed, int cin, const float* bias,
+                                 const float* scale, const float* shift, int act, vm_tensor* y, float* alpha,
+                                 const float* partial, void* stream);
+
 /* tf.image.resize_images(x, [2h, 2w]) (TF-1 legacy bilinear, exact 2x) followed by the 3x3 SAME conv, without
  * materialising the resized tensor — unet.py:44-63 (upconv_concat: resize_images at :58, conv2d at :60) for the
  * levels whose skip tensor is exactly twice the input's size.  Bilinear 2x is linear, so every output pixel

@@ -509,6 +509,56 @@ def test_unet_bf16_close_to_reference(vgg0):
     assert err < 2e-2 and lerr < 5e-2
 
 
+@pytest.mark.parametrize("shape", [(1, 16, 64), (2, 17, 45), (1, 1, 1), (1, 135, 240), (1, 40, 70)])
+@pytest.mark.parametrize("store_y", [False, True])
+def test_conv_pair_first_head_partials(shape, store_y):
+    """vm_conv3x3_pair_first_head_nhwc: pool1 (and y when store_y) bit-identical to the plain pair kernel; the head
+    partials partial[p][t] = sum_c y[p][c] * bf16(w)[t][64 + c] of the kernel's own bf16 outputs (f32 MFMA sums vs an
+    f64 restatement); taps 9..11 zero; y untouched when not stored.  Then conv_head over the other 64 channels +
+    the partials equals the full 128-channel head within f32 summation order."""
+    from vmatting import ops
+    n, h, w = shape
+    rs = np.random.RandomState(h * w + 3)
+    xf = torch.from_numpy((rs.normal(size=(n, h, w, 7)) * 50).astype(np.float32)).to(DEV)
+    w1 = (rs.normal(size=(3, 3, 7, 64)) * np.sqrt(2.0 / 63)).astype(np.float32)
+    w2 = (rs.normal(size=(3, 3, 64, 64)) * np.sqrt(2.0 / 576)).astype(np.float32)
+    wh = (rs.normal(size=(3, 3, 128, 1)) * np.sqrt(2.0 / 1152)).astype(np.float32)
+    bh = np.array([0.25], np.float32)
+    pc1 = ops.PackedConv(w1, (rs.normal(size=64) * 0.1).astype(np.float32), torch.bfloat16, DEV)
+    pc2 = ops.PackedConv(w2, (rs.normal(size=64) * 0.1).astype(np.float32), torch.bfloat16, DEV)
+    cat = torch.zeros((n, h, w, 128), dtype=torch.bfloat16, device=DEV)
+    cat[..., :64] = torch.from_numpy(rs.uniform(0, 2, (n, h, w, 64)).astype(np.float32)).to(DEV).to(torch.bfloat16)
+    pooled = torch.zeros((n, (h + 1) // 2, (w + 1) // 2, 64), dtype=torch.bfloat16, device=DEV)
+    ops.conv_pair_first(xf, pc1, pc2, "relu", out=cat[..., 64:], pool_out=pooled)
+    cat2 = cat.clone()
+    cat2[..., 64:] = 7.0
+    pooled2 = torch.zeros_like(pooled)
+    part = torch.full((n, h, w, 12), 3.0, dtype=torch.float32, device=DEV)
+    whd = T(wh)
+    ops.conv_pair_first_head(xf, pc1, pc2, whd, 64, part, "relu", out=cat2[..., 64:], pool_out=pooled2,
+                             store_y=store_y)
+    assert torch.equal(pooled2, pooled)
+    if store_y:
+        assert torch.equal(cat2, cat)
+    else:
+        assert float((cat2[..., 64:].float() - 7.0).abs().max()) == 0.0
+    y = H(cat[..., 64:].float()).astype(np.float64)
+    wb = H(whd.to(torch.bfloat16).float()).astype(np.float64).reshape(9, 128)[:, 64:]
+    want = np.einsum("nhwc,tc->nhwt", y, wb)
+    got = H(part)
+    assert np.abs(got[..., 9:]).max() == 0.0
+    assert relerr(got[..., :9], want) < 1e-5, relerr(got[..., :9], want)
+    # the split head vs the full head
+    full = ops.PackedConv(wh, bh, torch.bfloat16, DEV)
+    upper = ops.PackedConv(np.ascontiguousarray(wh[:, :, :64, :]), bh, torch.bfloat16, DEV)
+    a_full = torch.empty((n, h, w), dtype=torch.float32, device=DEV)
+    a_split = torch.empty_like(a_full)
+    l_full = ops.conv_head(cat, full, "none", alpha=a_full)
+    l_split = ops.conv_head(cat[..., :64], upper, "none", alpha=a_split, partial=part)
+    assert relerr(H(l_split), H(l_full)) < 1e-5, relerr(H(l_split), H(l_full))
+    assert float((a_split - a_full).abs().max()) < 1e-5
+
+
 def test_unet_bf16_fused_and_unfused_forward_agree(vgg0):
     """bf16 forward: fusing conv1_1->conv1_2 changes nothing (bit for bit, the lazily evaluated .conv1_1 included);
     folding the upconv resizes stays in the bf16 error class of the resize + conv path (logits; alpha of saturated
@@ -521,17 +571,22 @@ def test_unet_bf16_fused_and_unfused_forward_agree(vgg0):
     m = unet.UNetVideo(vgg0, dtype="bf16")
     m.build(x.astype(np.float32))
 
-    def variant(fuse, fold):
+    def variant(fuse, fold, split=True):
         v = unet.UNetVideo(vgg0, dtype="bf16").load_params(m.params)
-        v.fuse_first, v.fold_upconv = fuse, fold
+        v.fuse_first, v.fold_upconv, v.split_head = fuse, fold, split
         v.prepare()
         v.forward(xt)
         return v
 
     m2 = variant(False, m.fold_upconv)
+    m4 = variant(True, m.fold_upconv, split=False)
     assert torch.equal(m.conv1_1, m2.conv1_1)
-    assert torch.equal(m.conv1_2, m2.conv1_2) and torch.equal(m.pool1, m2.pool1)
-    assert torch.equal(m.output, m2.output)
+    assert torch.equal(m.pool1, m2.pool1) and torch.equal(m.conv1_2, m2.conv1_2)  # .conv1_2 lazily evaluated (split)
+    assert torch.equal(m4.output, m2.output)
+    assert torch.equal(m.upconv4, m4.upconv4)
+    # the split head (pair-kernel shares of conv1_2's half) only reorders f32 sums
+    assert relerr(H(m.conv1_3), H(m4.conv1_3)) < 1e-5, relerr(H(m.conv1_3), H(m4.conv1_3))
+    assert float((m.output - m4.output).abs().max()) < 1e-5
     m3 = variant(True, ())
     assert relerr(H(m.conv1_3), H(m3.conv1_3)) < 2e-2, relerr(H(m.conv1_3), H(m3.conv1_3))
 

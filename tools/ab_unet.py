@@ -8,23 +8,23 @@ sys.path[:0] = [os.path.join(REPO, "video-matting_amd"), REPO]
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
-import bench  # noqa: E402
-from vmatting import unet  # noqa: E402
+from vmatting import unet, video  # noqa: E402
 from vmatting.weights import synthetic_vgg16  # noqa: E402
 
 VARIANTS = {
     "default": {},
     "fold_up2": {"fold_upconv": ("upconv_2", "upconv_3", "upconv_4")},
+    "nosplit": {"split_head": False},
 }
 
 
-def run(name, steps=30):
+def run(name, steps=100):
     np.random.seed(0)
     m = unet.UNetVideo(synthetic_vgg16(0), dtype="bf16", device="cuda")
     for k, v in VARIANTS[name].items():
         setattr(m, k, v)
     m.prepare()
-    x = bench.synth_frames(1, 1080, 1920, 0, "cuda")
+    x = video.synthetic_frames(1, 1080, 1920, first=0, device="cuda")
     g = m.capture(x)
     for _ in range(3):
         g.replay()
@@ -38,6 +38,6 @@ def run(name, steps=30):
 
 if __name__ == "__main__":
     names = sys.argv[1:] or list(VARIANTS)
-    for rep in range(2):
+    for rep in range(3):
         for n in names:
             print("%-10s %.4f ms/frame" % (n, run(n)), flush=True)

@@ -1201,6 +1201,24 @@ __global__ __launch_bounds__(512) void conv3x3_pair_persist(ConvArgs a) {
     rmul[64 + tid] = (a.bias ? a.bias[co] : 0.f) * sc + (a.shift ? a.shift[co] : 0.f);
     rmul[128 + tid] = a.bias1 ? a.bias1[tid] : 0.f;
   }
+  // head split: A fragments of the skip half's head filter, rows = taps (9 of 16), k = 8q + j <-> conv1_2 channel
+  // (2kk + j/4)*16 + 4q + j%4 — the channel order in which the epilogue's lane holds its bf16 outputs (B operand)
+  uint4 hwf[2] = {make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};
+  if (a.hd) {
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      uint32_t u[4];
+#pragma unroll
+      for (int jp = 0; jp < 4; ++jp) {
+        const int j0 = 2 * jp, j1 = 2 * jp + 1;
+        const int c0 = (2 * kk + j0 / 4) * 16 + 4 * q + j0 % 4, c1 = (2 * kk + j1 / 4) * 16 + 4 * q + j1 % 4;
+        const float w0 = col < 9 ? a.hw[col * a.hw_cin + a.hw_coff + c0] : 0.f;
+        const float w1 = col < 9 ? a.hw[col * a.hw_cin + a.hw_coff + c1] : 0.f;
+        u[jp] = (uint32_t)f2bf(w0) | ((uint32_t)f2bf(w1) << 16);
+      }
+      hwf[kk] = make_uint4(u[0], u[1], u[2], u[3]);
+    }
+  }
 
   // input pixel of this thread (one per thread): raw registers while in flight, bf16 chunk in LDS
   const T* x8 = reinterpret_cast<const T*>(a.x) + a.x_coff;
@@ -1382,6 +1400,14 @@ __global__ __launch_bounds__(512) void conv3x3_pair_persist(ConvArgs a) {
         pk[fc].x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
         pk[fc].y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
       }
+      if (a.hd) {  // the skip half's head partials of this lane's pixel: 2 MFMAs on the bf16 outputs just made
+        f32x4 dacc = f32x4{0.f, 0.f, 0.f, 0.f};
+        mma16<T>(hwf[0], make_uint4(pk[0].x, pk[0].y, pk[1].x, pk[1].y), dacc);
+        mma16<T>(hwf[1], make_uint4(pk[2].x, pk[2].y, pk[3].x, pk[3].y), dacc);
+        const int pc = fp * 16 + col;
+        if (q < 3 && r0 + wave < H && c0 + pc < W)
+          *reinterpret_cast<f32x4*>(a.hd + (((long)n * H + r0 + wave) * W + c0 + pc) * 12 + 4 * q) = dacc;
+      }
       // 16-byte chunks: rows of 144 B make 8 consecutive rows hit 8 distinct 4-bank groups (conflict-free b128)
 #pragma unroll
       for (int g = 0; g < 2; ++g)
@@ -1396,6 +1422,7 @@ __global__ __launch_bounds__(512) void conv3x3_pair_persist(ConvArgs a) {
     const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(yb, 0, 0x7ffffff0, 0x00020000);
 #pragma unroll
     for (int it = 0; it < C::BM * 8 / C::NT; ++it) {
+      if (a.y_skip) break;
       const int idx = it * C::NT + tid;
       const int rr = idx >> 3, cq = idx & 7;
       const uint4 d = *reinterpret_cast<const uint4*>(smem + C::S_OFF + rr * C::SR + cq * 16);
@@ -1559,10 +1586,11 @@ __global__ __launch_bounds__(512) void conv3x3_first(ConvArgs a) {
 // bytes).  The kernel writes 256 B per pixel and reads 16: HBM-write-bound.  NT: nontemporal stores (the
 // 531 MB 1080p output is never re-read by this pass).
 template <bool NT>
-__global__ __launch_bounds__(512) void conv3x3_first_softmax(ConvArgs a) {
+__global__ __launch_bounds__(512, 2) void conv3x3_first_softmax(ConvArgs a) {
   using T = uint16_t;
   constexpr int TH = 8, TW = 32, PW = TW + 2, PPIX = (TH + 2) * PW;
   __shared__ __attribute__((aligned(16))) uint4 patch[PPIX];
+  __shared__ __attribute__((aligned(16))) float rmul[2 * 64];  // per-channel scale, bias*scale + shift
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int H = a.H, W = a.W, cs = a.x_cstride;
   const int th = (H + TH - 1) / TH, tw = (W + TW - 1) / TW;
@@ -1591,16 +1619,11 @@ __global__ __launch_bounds__(512) void conv3x3_first_softmax(ConvArgs a) {
     for (int fc = 0; fc < 4; ++fc)
       wf[j][fc] = __builtin_bit_cast(
           uint4, __builtin_amdgcn_raw_buffer_load_b128(wrs, ((fc * 16 + col) * a.K_pad + j * 32 + q * 8) * 2, 0, 0));
-  float mul[4][4], add[4][4];
-#pragma unroll
-  for (int fc = 0; fc < 4; ++fc)
-#pragma unroll
-    for (int jj = 0; jj < 4; ++jj) {
-      const int co = fc * 16 + 4 * q + jj;
-      const float sc = a.scale ? a.scale[co] : 1.f;
-      mul[fc][jj] = sc;
-      add[fc][jj] = (a.bias ? a.bias[co] : 0.f) * sc + (a.shift ? a.shift[co] : 0.f);
-    }
+  if (tid < 64) {  // constants in LDS (read per tile): 2 blocks per CU fit the register file
+    const float sc = a.scale ? a.scale[tid] : 1.f;
+    rmul[tid] = sc;
+    rmul[64 + tid] = (a.bias ? a.bias[tid] : 0.f) * sc + (a.shift ? a.shift[tid] : 0.f);
+  }
   int i = blockIdx.x;
   uint4 nxt = i < ntiles ? load_patch(tile_of(i)) : make_uint4(0, 0, 0, 0);
   for (; i < ntiles; i += gridDim.x) {
@@ -1640,12 +1663,16 @@ __global__ __launch_bounds__(512) void conv3x3_first_softmax(ConvArgs a) {
       float v[4][4];
       float mx = -INFINITY;
 #pragma unroll
-      for (int fc = 0; fc < 4; ++fc)
+      for (int fc = 0; fc < 4; ++fc) {
+        const float4 m4 = *reinterpret_cast<const float4*>(rmul + fc * 16 + 4 * q);
+        const float4 a4 = *reinterpret_cast<const float4*>(rmul + 64 + fc * 16 + 4 * q);
+        const float mul[4] = {m4.x, m4.y, m4.z, m4.w}, add[4] = {a4.x, a4.y, a4.z, a4.w};
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj) {
-          v[fc][jj] = fmaf(acc[fc][fp][jj], mul[fc][jj], add[fc][jj]);
+          v[fc][jj] = fmaf(acc[fc][fp][jj], mul[jj], add[jj]);
           mx = fmaxf(mx, v[fc][jj]);
         }
+      }
       mx = fmaxf(mx, __shfl_xor(mx, 16));
       mx = fmaxf(mx, __shfl_xor(mx, 32));
       float sum = 0.f;
@@ -1691,6 +1718,7 @@ struct HeadArgs {
   void* y;
   int y_cstride, y_coff, y_dtype;
   float* y2;  // optional: sigmoid of the pre-activation value, f32 [M] (unet.py:204-205 output beside conv1_3)
+  const float* part;  // optional: per-tap partials [M][12] of the channels x does not carry (the pair kernel's hd)
 };
 
 template <typename T>
@@ -1939,6 +1967,18 @@ __global__ __launch_bounds__(256) void conv3x3_head_mfma(HeadArgs a) {
 
   for (int g0 = wave * GB; g0 < NG; g0 += 4 * GB) {
     uint4 xa[GB][NKS];
+    float pv[GB][4];  // head split: the partials this lane adds (issued with the input loads, used after the MFMAs)
+#pragma unroll
+    for (int u = 0; u < GB; ++u) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int j = (g0 + u) * 16 + 4 * ks + i, lr = j / IW, lc = j - lr * IW;
+        const int hh = r0 - 1 + lr, ww = c0 - 1 + lc;
+        const bool ok = a.part && col < 9 && g0 + u < NG && j < NPIX && (unsigned)hh < (unsigned)H &&
+                        (unsigned)ww < (unsigned)W;
+        pv[u][i] = ok ? a.part[(((long)n * H + hh) * W + ww) * 12 + col] : 0.f;
+      }
+    }
 #pragma unroll
     for (int u = 0; u < GB; ++u) {
       const int j = (g0 + u) * 16 + col;  // input-window pixel of this lane's A row
@@ -1963,7 +2003,7 @@ __global__ __launch_bounds__(256) void conv3x3_head_mfma(HeadArgs a) {
       if (col < 9) {
         const int p = (g0 + u) * 16 + 4 * ks;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) ys[(p + i) * 9 + col] = acc[i];
+        for (int i = 0; i < 4; ++i) ys[(p + i) * 9 + col] = acc[i] + pv[u][i];  // + the other channels' share
       }
     }
   }
@@ -2867,7 +2907,7 @@ extern "C" int vm_conv3x3_pack_weights_batch(int njobs, const vm_pack_job* jobs,
 static int conv_impl(const vm_tensor* x, const void* packed, int cin, int cout, const float* bias, const float* scale,
                      const float* shift, int act, vm_tensor* y, const vm_tensor* yp, void* stream,
                      float* y2 = nullptr, int nsrc = 0, long src_stride = 0, void* work = nullptr,
-                     size_t work_bytes = 0);
+                     size_t work_bytes = 0, const float* head_part = nullptr);
 
 extern "C" int vm_conv3x3_nhwc(const vm_tensor* x, const void* packed, int cin, int cout, const float* bias,
                                const float* scale, const float* shift, int act, vm_tensor* y, void* stream) {
@@ -2964,9 +3004,41 @@ static int launch_pair_persist(ConvArgs& a, long sp, hipStream_t st) {
   return check_launch("conv3x3_pair_persist");
 }
 
+static int pair_first_impl(const vm_tensor* x, const void* packed1, int cin1, const float* bias1, const void* packed2,
+                           int cout2, const float* bias2, const float* scale2, const float* shift2, int act2,
+                           vm_tensor* y, vm_tensor* ypool, const float* head_w, int head_cin, int head_coff,
+                           float* partial, int store_y, void* stream);
+
 extern "C" int vm_conv3x3_pair_first_nhwc(const vm_tensor* x, const void* packed1, int cin1, const float* bias1,
                                           const void* packed2, int cout2, const float* bias2, const float* scale2,
                                           const float* shift2, int act2, vm_tensor* y, vm_tensor* ypool, void* stream) {
+  return pair_first_impl(x, packed1, cin1, bias1, packed2, cout2, bias2, scale2, shift2, act2, y, ypool, nullptr, 0, 0,
+                         nullptr, 1, stream);
+}
+
+extern "C" int vm_conv3x3_pair_first_head_nhwc(const vm_tensor* x, const void* packed1, int cin1, const float* bias1,
+                                               const void* packed2, int cout2, const float* bias2,
+                                               const float* scale2, const float* shift2, int act2, vm_tensor* y,
+                                               vm_tensor* ypool, const float* head_w, int head_cin, int head_coff,
+                                               float* partial, int store_y, void* stream) {
+  if (!head_w || !partial || head_cin <= 0 || head_coff < 0 || head_coff + cout2 > head_cin)
+    return fail(VM_EINVAL, "conv3x3_pair_first_head: head filter [3,3,%d,1] with the pair's %d channels at %d",
+                head_cin, cout2, head_coff);
+  return pair_first_impl(x, packed1, cin1, bias1, packed2, cout2, bias2, scale2, shift2, act2, y, ypool, head_w,
+                         head_cin, head_coff, partial, store_y, stream);
+}
+
+extern "C" int vm_conv3x3_head_partial_nhwc(const vm_tensor* x, const void* packed, int cin, const float* bias,
+                                            const float* scale, const float* shift, int act, vm_tensor* y,
+                                            float* alpha, const float* partial, void* stream) {
+  if (!partial) return fail(VM_EINVAL, "conv3x3_head_partial: partial is NULL");
+  return conv_impl(x, packed, cin, 1, bias, scale, shift, act, y, nullptr, stream, alpha, 0, 0, nullptr, 0, partial);
+}
+
+static int pair_first_impl(const vm_tensor* x, const void* packed1, int cin1, const float* bias1, const void* packed2,
+                           int cout2, const float* bias2, const float* scale2, const float* shift2, int act2,
+                           vm_tensor* y, vm_tensor* ypool, const float* head_w, int head_cin, int head_coff,
+                           float* partial, int store_y, void* stream) {
   if (!valid_tensor(x) || !valid_tensor(y) || !packed1 || !packed2)
     return fail(VM_EINVAL, "conv3x3_pair_first: invalid tensor/weights");
   if (cin1 <= 0 || cin1 > 8 || x->c != cin1 || cout2 <= 0 || y->c != cout2)
@@ -2997,6 +3069,12 @@ extern "C" int vm_conv3x3_pair_first_nhwc(const vm_tensor* x, const void* packed
   a.w1 = packed1; a.bias1 = bias1; a.x_f32 = xf32; a.x_c = cin1;
   if (ypool) { a.py = ypool->ptr; a.py_cstride = ypool->cstride; a.py_coff = ypool->coff; }
   const long sp = (long)x->n * ((x->h + 7) / 8) * ((x->w + 31) / 32);
+  if (partial) {  // the head split lives in the persistent pair kernel only
+    if (cout2 != 64 || g_pair_kernel != 0 || sp > 0x7fffffffL)
+      return fail(VM_EUNSUPPORTED, "conv3x3_pair_first_head: needs the persistent pair kernel (cout2 64)");
+    a.hd = partial; a.hw = head_w; a.hw_cin = head_cin; a.hw_coff = head_coff; a.y_skip = store_y ? 0 : 1;
+    return launch_pair_persist<0>(a, sp, st);
+  }
   if (cout2 == 64 && (g_pair_kernel == 0 || g_pair_kernel >= 10) && sp <= 0x7fffffffL) {
     switch (g_pair_kernel) {  // >= 10: timing ablations (garbage results)
       case 11: return launch_pair_persist<1>(a, sp, st);
@@ -3019,8 +3097,9 @@ extern "C" int vm_conv3x3_head_nhwc(const vm_tensor* x, const void* packed, int 
 
 static int conv_impl(const vm_tensor* x, const void* packed, int cin, int cout, const float* bias, const float* scale,
                      const float* shift, int act, vm_tensor* y, const vm_tensor* yp, void* stream, float* y2, int nsrc,
-                     long src_stride, void* work, size_t work_bytes) {
+                     long src_stride, void* work, size_t work_bytes, const float* head_part) {
   if (!valid_tensor(x) || !valid_tensor(y) || !packed) return fail(VM_EINVAL, "conv3x3: invalid tensor/weights");
+  if (head_part && cout != 1) return fail(VM_EINVAL, "conv3x3: head partials need cout == 1");
   const int xc = nsrc > 1 ? nsrc * x->c : x->c;  // sources: x is the view of source 0
   if (cin <= 0 || cout <= 0 || xc != cin || y->c != cout)
     return fail(VM_EINVAL, "conv3x3: channel mismatch x.c=%d cin=%d y.c=%d cout=%d", xc, cin, y->c, cout);
@@ -3048,12 +3127,15 @@ static int conv_impl(const vm_tensor* x, const void* packed, int cin, int cout, 
     h.cin_pad = g.cin_pad; h.K9 = g.K9; h.K_pad = g.K_pad; h.chunk_major = g.chunk_major; h.ng = g.ng;
     h.w = packed; h.bias = bias; h.scale = scale; h.shift = shift; h.act = act;
     h.y = y->ptr; h.y_cstride = y->cstride; h.y_coff = y->coff; h.y_dtype = y->dtype; h.y2 = y2;
+    h.part = head_part;
+    if (head_part && (g_head_kernel != 0 || (g.cin_pad + 4 * ce - 1) / (4 * ce) > 8))
+      return fail(VM_EUNSUPPORTED, "conv3x3 head: partials need the MFMA head kernel");
     const int nks = (g.cin_pad + 4 * ce - 1) / (4 * ce);
     if (g_head_kernel == 0 && nks <= 8) {
       constexpr int TW = 64;
       // 16-row tiles for the bf16 128-channel head (cat1 of UNetVideo): input window 18 x 66 per 16 x 64 outputs
       // (1.16x the tile's bytes instead of 1.29x for 8 rows)
-      const int TH = (dt == VM_BF16 && nks == 4 && g_head_th == 16) ? 16 : 8;
+      const int TH = (dt == VM_BF16 && (nks == 4 || (nks == 2 && head_part)) && g_head_th == 16) ? 16 : 8;
       const long tiles = (long)x->n * ((x->h + TH - 1) / TH) * ((x->w + TW - 1) / TW);
       if (tiles > 0x7fffffffL) return fail(VM_EUNSUPPORTED, "conv3x3 head: too many tiles");
       const size_t lds = (size_t)9 * g.cin_pad * elem_bytes(dt);
@@ -3062,7 +3144,9 @@ static int conv_impl(const vm_tensor* x, const void* packed, int cin, int cout, 
                dt == VM_BF16 ? "unsigned short" : "float", TH, TW, nk);
 #define VM_HEAD_MFMA(TT, NK) \
   hipLaunchKernelGGL((conv3x3_head_mfma<TT, 8, TW, NK>), dim3(tiles), dim3(256), lds, st, h)
-      if (TH == 16) {
+      if (TH == 16 && nk == 2) {  // the split head's 64-channel half
+        hipLaunchKernelGGL((conv3x3_head_mfma<uint16_t, 16, TW, 2>), dim3(tiles), dim3(256), lds, st, h);
+      } else if (TH == 16) {
         hipLaunchKernelGGL((conv3x3_head_mfma<uint16_t, 16, TW, 4>), dim3(tiles), dim3(256), lds, st, h);
       } else if (dt == VM_BF16) {
         if (nk == 1) VM_HEAD_MFMA(uint16_t, 1); else if (nk == 2) VM_HEAD_MFMA(uint16_t, 2);

@@ -34,6 +34,12 @@ struct ConvArgs {
   // writes raw f32 sums to part[split][pixel][cout] and splitk_reduce_kernel applies bias/affine/act (fixed order)
   int ksplit;
   float* part;
+  // pair kernel + head split (unet.py:203 conv1_5 over cat1 = [up, skip]): hd != nullptr makes the pair kernel also
+  // write the skip half's per-tap head partials hd[pixel][12] (taps 0..8 of sum_c y[pixel][c] * hw[tap][hw_coff + c],
+  // hw = the head's HWIO f32 filter with hw_cin input channels); y_skip = 1 leaves conv1_2's output unwritten
+  float* hd;
+  const float* hw;
+  int hw_cin, hw_coff, y_skip;
 };
 
 // element offset of input channel c (relative to the view's channel 0) under the source split

@@ -80,6 +80,11 @@ SIGNATURES = [
                                      c_void_p]),
     ("vm_conv3x3_pair_first_nhwc", c_int, [P, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p,
                                            c_void_p, c_int, P, P, c_void_p]),
+    ("vm_conv3x3_pair_first_head_nhwc", c_int, [P, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p,
+                                                c_void_p, c_int, P, P, c_void_p, c_int, c_int, c_void_p, c_int,
+                                                c_void_p]),
+    ("vm_conv3x3_head_partial_nhwc", c_int, [P, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, P, c_void_p,
+                                             c_void_p, c_void_p]),
     ("vm_conv3x3_fold_up2x_weights", c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p]),
     ("vm_conv3x3_up2x_nhwc", c_int, [P, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, P,
                                      c_void_p]),

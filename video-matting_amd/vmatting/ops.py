@@ -246,7 +246,7 @@ def conv3x3(x, pc, act="none", out=None, out_dtype=None, affine=None, pool_out=N
     return out
 
 
-def conv_head(x, pc, act="none", out=None, alpha=None):
+def conv_head(x, pc, act="none", out=None, alpha=None, partial=None):
     """cout == 1 conv (unet.py:203-204 conv1_5) into ``out``; with ``alpha`` (contiguous f32, one value per pixel)
     also tf.nn.sigmoid of the pre-activation from the same pass (unet.py:205), saving a separate elementwise launch."""
     if pc.cout != 1:
@@ -266,12 +266,59 @@ def conv_head(x, pc, act="none", out=None, alpha=None):
         ev0 = torch.cuda.Event(enable_timing=True)
         ev1 = torch.cuda.Event(enable_timing=True)
         ev0.record()
-    check(lib().vm_conv3x3_head_nhwc(ctypes.byref(xv), _ptr(pc.packed), pc.cin, _ptr(pc.bias), _ptr(pc.scale),
-                                     _ptr(pc.shift), _lib.ACT[act], ctypes.byref(yv), _ptr(alpha), stream_handle()),
-          "conv3x3_head")
+    if partial is not None:  # + the per-tap shares of the channels x does not carry (conv_pair_first_head)
+        if partial.dtype != torch.float32 or not partial.is_contiguous() or tuple(partial.shape) != (n, h, w, 12):
+            raise ValueError("partial must be a contiguous f32 [n,h,w,12] tensor")
+        check(lib().vm_conv3x3_head_partial_nhwc(ctypes.byref(xv), _ptr(pc.packed), pc.cin, _ptr(pc.bias),
+                                                 _ptr(pc.scale), _ptr(pc.shift), _lib.ACT[act], ctypes.byref(yv),
+                                                 _ptr(alpha), _ptr(partial), stream_handle()), "conv3x3_head_partial")
+    else:
+        check(lib().vm_conv3x3_head_nhwc(ctypes.byref(xv), _ptr(pc.packed), pc.cin, _ptr(pc.bias), _ptr(pc.scale),
+                                         _ptr(pc.shift), _lib.ACT[act], ctypes.byref(yv), _ptr(alpha),
+                                         stream_handle()), "conv3x3_head")
     if prof is not None:
         ev1.record()
         prof.append((2 * n * h * w * 9 * pc.cin, _lib.last_conv_kernel(), ev0, ev1))
+    return out
+
+
+def conv_pair_first_head(x, pc1, pc2, head_w, head_coff, partial, act2="relu", out=None, pool_out=None,
+                         store_y=False, fallback=False):
+    """conv_pair_first with the head split (vm_conv3x3_pair_first_head_nhwc): besides pool_out (and ``out`` when
+    store_y) the pair kernel writes ``partial`` [n,h,w,12] f32 = per-tap shares of the cout == 1 head filter
+    ``head_w`` (device f32 HWIO [3,3,cin_head,1]) over its output channels, which sit at head_coff of the head's
+    input (unet.py:203: conv1_5 over cat1 = [upconv_4, conv1_2]).  conv_head(..., partial=partial) finishes it.
+    ``fallback``: return None instead of raising when the kernel cannot take the case (the caller runs the
+    unsplit path)."""
+    n, h, w, _ = x.shape
+    if pc1.dtype != torch.bfloat16 or pc2.dtype != torch.bfloat16 or pc1.cout != 64 or pc2.cin != 64:
+        raise NotImplementedError("conv_pair_first_head: bf16 64-channel pair only")
+    if head_w.dtype != torch.float32 or not head_w.is_contiguous() or head_w.dim() != 4 or head_w.shape[3] != 1:
+        raise ValueError("head_w must be a contiguous f32 [3,3,cin,1] filter")
+    if partial.dtype != torch.float32 or not partial.is_contiguous() or tuple(partial.shape) != (n, h, w, 12):
+        raise ValueError("partial must be a contiguous f32 [n,h,w,12] tensor")
+    _require_gpu(head_w)
+    _require_gpu(partial)
+    if out is None:
+        out = torch.empty((n, h, w, pc2.cout), dtype=torch.bfloat16, device=x.device)
+    xv, yv = nhwc(x), nhwc(out)
+    pv = nhwc(pool_out) if pool_out is not None else None
+    prof = _CONV_PROFILE
+    if prof is not None:
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev1 = torch.cuda.Event(enable_timing=True)
+        ev0.record()
+    rc = lib().vm_conv3x3_pair_first_head_nhwc(
+        ctypes.byref(xv), _ptr(pc1.packed), pc1.cin, _ptr(pc1.bias), _ptr(pc2.packed), pc2.cout, _ptr(pc2.bias),
+        _ptr(pc2.scale), _ptr(pc2.shift), _lib.ACT[act2], ctypes.byref(yv),
+        ctypes.byref(pv) if pv is not None else None, _ptr(head_w), int(head_w.shape[2]), head_coff, _ptr(partial),
+        int(bool(store_y)), stream_handle())
+    if rc == _lib.VM_EUNSUPPORTED and fallback:
+        return None  # e.g. a kernel-selection override (vm_set_option "conv_kernel"/"pair_kernel") rules it out
+    check(rc, "conv3x3_pair_first_head")
+    if prof is not None:
+        ev1.record()
+        prof.append((2 * n * h * w * 9 * (pc1.cin * pc1.cout + pc2.cin * pc2.cout), _lib.last_conv_kernel(), ev0, ev1))
     return out
 
 

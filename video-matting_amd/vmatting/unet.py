@@ -61,6 +61,10 @@ class UNet:
     # upconvs whose exact-2x resize is folded into the conv (ops.upconv3x3; bf16 only, others resize + conv)
     # conv1_1 -> conv1_2 as one kernel (ops.conv_pair_first; bf16 only, others run them separately)
     fuse_first = True
+    # head split (bf16 + fuse_first): the pair kernel takes conv1_5's share of the skip half of cat1 in its epilogue
+    # (vm_conv3x3_pair_first_head_nhwc), so conv1_2's 64-channel output never reaches HBM and the head reads only
+    # the upconv_4 half; .conv1_2 / .upconv4 are then evaluated on first access
+    split_head = True
     fold_upconv = ("upconv_3", "upconv_4")  # upconv_2 folded would run on the 135x240 grid: slower (measured)
 
     def __init__(self, vgg16_npy_path=None, dtype="bf16", device="cuda"):
@@ -75,6 +79,8 @@ class UNet:
         self._c11 = None
         self._x = None
         self._in8_valid = False
+        self._skip_valid = True
+        self._head_up = None     # split head: (conv1_5 HWIO f32 on the device, PackedConv of its upconv_4 half)
 
     # ------------------------------------------------------------------ weights
     def get_conv_filter(self, name):
@@ -107,6 +113,14 @@ class UNet:
 
     def _pack(self):
         self.convs = {k: ops.PackedConv(w, b, self.dtype, self.device) for k, (w, b) in self.params.items()}
+        self._head_up = None
+        if self._lean():
+            w, b = self.params["conv1_5"]
+            self._head_up = (torch.as_tensor(np.ascontiguousarray(w, np.float32)).to(self.device),
+                             ops.PackedConv(np.ascontiguousarray(w[:, :, :64, :]), b, self.dtype, self.device))
+
+    def _lean(self):
+        return self.split_head and self.fuse_first and self.dtype == torch.bfloat16
 
     def weights_flat(self):
         """All packed weights as one list of tensors (for an RCCL broadcast from rank 0)."""
@@ -118,6 +132,8 @@ class UNet:
                 out.append(pc.up2x())
             if pc.bias is not None:
                 out.append(pc.bias)
+        if self._head_up is not None:
+            out += [self._head_up[0], self._head_up[1].packed, self._head_up[1].bias]
         return out
 
     # ------------------------------------------------------------------ buffers
@@ -135,7 +151,8 @@ class UNet:
         E = lambda lv, c, dt=T: torch.empty((n, L[lv][0], L[lv][1], c), dtype=dt, device=dev)  # noqa: E731
         # in8 / c11 (unfused first pair, the lazily evaluated .conv1_1) and the resize targets r1..r4 (unfolded
         # upconvs) are allocated on first use only: the bf16 fused/folded forward never touches in8, c11, r3, r4
-        ws = _LazyBuffers(dict(in8=(0, 8), c11=(0, 64), r4=(0, 128), r3=(1, 256), r2=(2, 512), r1=(3, 512)), E)
+        ws = _LazyBuffers(dict(in8=(0, 8), c11=(0, 64), r4=(0, 128), r3=(1, 256), r2=(2, 512), r1=(3, 512),
+                               hpart=(0, 12, torch.float32)), E)
         ws.update(
             cat1=E(0, 128),
             p1=E(1, 64), c21=E(1, 128), cat2=E(1, 256), c23=E(1, 128),
@@ -176,7 +193,16 @@ class UNet:
         b = self._buffers(n, h, w)
         L = _levels(h, w)
         C = self.convs
-        if self.fuse_first and self.dtype == torch.bfloat16:
+        lean = self._lean() and self._head_up is not None
+        # conv1_1 and conv1_2 stay on chip: only pool1 and the head's per-tap shares of conv1_2 leave the kernel
+        lean = lean and ops.conv_pair_first_head(x, C["conv1_1"], C["conv1_2"], self._head_up[0], 64, b["hpart"],
+                                                 "relu", out=b["cat1"][..., 64:], pool_out=b["p1"], store_y=False,
+                                                 fallback=True) is not None
+        self._skip_valid = not lean
+        if lean:
+            self._c11 = None
+            self._in8_valid = False
+        elif self.fuse_first and self.dtype == torch.bfloat16:
             # conv1_1 stays on chip and reads the f32 frame itself (bf16 rounding on load); .conv1_1 is evaluated
             # on first access
             ops.conv_pair_first(x, C["conv1_1"], C["conv1_2"], "relu", out=b["cat1"][..., 64:], pool_out=b["p1"])
@@ -210,7 +236,11 @@ class UNet:
         ops.conv3x3(b["cat2"], C["conv2_3"], "relu", out=b["c23"])
         up(b["c23"], "upconv_4", 0, b["cat1"][..., :64], "r4")
         alpha = b["out"] if out is None else out
-        ops.conv_head(b["cat1"], C["conv1_5"], "none", out=b["logits"], alpha=alpha)  # conv1_5 + sigmoid
+        if lean:  # conv1_5 + sigmoid over the upconv_4 half + the pair kernel's shares of the conv1_2 half
+            ops.conv_head(b["cat1"][..., :64], self._head_up[1], "none", out=b["logits"], alpha=alpha,
+                          partial=b["hpart"])
+        else:
+            ops.conv_head(b["cat1"], C["conv1_5"], "none", out=b["logits"], alpha=alpha)  # conv1_5 + sigmoid
         self._publish(b)
         self.output = alpha
         return self.output
@@ -234,8 +264,23 @@ class UNet:
             self._c11 = ops.conv3x3(xin, self.convs["conv1_1"], "relu", out=self._ws["c11"])
         return self._c11
 
+    @property
+    def conv1_2(self):
+        """unet.py:171 conv1_2 — with the head split the forward never writes it to HBM, so it is evaluated here
+        (conv1_1 -> conv1_2 unfused: bit-identical to the pair kernel's values)."""
+        if self._ws is None:
+            return None
+        if not self._skip_valid:
+            ops.conv3x3(self.conv1_1, self.convs["conv1_2"], "relu", out=self._ws["cat1"][..., 64:])
+            self._skip_valid = True
+        return self._ws["cat1"][..., 64:]
+
+    @property
+    def upconv4(self):
+        """unet.py:200 upconv4 = concat([upconv_4, conv1_2]) (the skip half evaluated on first access)."""
+        return None if self.conv1_2 is None else self._ws["cat1"]
+
     def _publish(self, b):
-        self.conv1_2 = b["cat1"][..., 64:]
         self.pool1 = b["p1"]
         self.conv2_1 = b["c21"]
         self.conv2_2 = b["cat2"][..., 128:]
@@ -250,7 +295,6 @@ class UNet:
         self.upconv1, self.conv4_4 = b["cat4"], b["c44"]
         self.upconv2, self.conv3_4 = b["cat3"], b["c34"]
         self.upconv3, self.conv2_3 = b["cat2"], b["c23"]
-        self.upconv4 = b["cat1"]
         self.conv1_3 = b["logits"]  # scope 'conv1_5' (unet.py:143/203)
         self.output = b["out"]
 
