@@ -129,11 +129,15 @@ def test_refine_softmax_kernel_matches_generic_epilogue(n, h, w):
             outs[k] = ops.conv3x3(xb, pc, "softmax", out_dtype=torch.float32)
             name = _lib.last_conv_kernel()
             assert ("first_softmax" in name) == (k != 0), name
+        for k in (3, 4):  # the per-wave LDS transpose store forms: same values
+            _lib.set_option("softmax_kernel", k)
+            assert torch.equal(ops.conv3x3(xb, pc, "softmax", out_dtype=torch.float32), outs[1]), k
+        _lib.set_option("softmax_kernel", 2)
         for blocks in (1, 3, 7):  # persistent walks with partial last rounds
             _lib.set_option("softmax_blocks", blocks)
             assert torch.equal(ops.conv3x3(xb, pc, "softmax", out_dtype=torch.float32), outs[2]), blocks
     finally:
-        _lib.set_option("softmax_kernel", 1)
+        _lib.set_option("softmax_kernel", 4)
         _lib.set_option("softmax_blocks", 1024)
     ref = outs[0].cpu().numpy()
     for k in (1, 2):

@@ -18,7 +18,8 @@ pc = ops.PackedConv((rs.normal(size=(3, 3, 5, 64)) * 0.3).astype(np.float32), rs
                     "bf16")
 out = torch.empty((1, h, w, 64), dtype=torch.float32, device="cuda")
 nbytes = h * w * (16 + 256)
-for k, blocks in ((0, 1024), (1, 1024), (2, 1024), (2, 512), (2, 2048), (2, 4096), (2, 100000)):
+for k, blocks in ((0, 1024), (1, 1024), (4, 1024), (4, 256), (4, 512), (4, 768), (4, 1024), (4, 512), (1, 512),
+                  (2, 512)):
     _lib.set_option("softmax_kernel", k)
     _lib.set_option("softmax_blocks", blocks)
     fn = lambda: ops.conv3x3(x[..., :5], pc, "softmax", out=out)  # noqa: E731
@@ -34,4 +35,4 @@ for k, blocks in ((0, 1024), (1, 1024), (2, 1024), (2, 512), (2, 2048), (2, 4096
     ms = e0.elapsed_time(e1) / 50
     print("softmax_kernel %d blocks %6d  %-40s %.1f us  %.2f TB/s algorithmic" % (k, blocks, _lib.last_conv_kernel(), ms * 1e3,
                                                                       nbytes / ms / 1e9), flush=True)
-_lib.set_option("softmax_kernel", 1)
+_lib.set_option("softmax_kernel", 4)

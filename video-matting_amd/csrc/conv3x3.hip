@@ -1585,11 +1585,15 @@ __global__ __launch_bounds__(512) void conv3x3_first(ConvArgs a) {
 // sum.  Every lane then stores its four 16-byte channel quads (a wave store covers 16 pixels x 64 contiguous
 // bytes).  The kernel writes 256 B per pixel and reads 16: HBM-write-bound.  NT: nontemporal stores (the
 // 531 MB 1080p output is never re-read by this pass).
-template <bool NT>
+// STG: each wave transposes its 16 pixels x 64 channels through a private LDS slab so that every store instruction
+// writes 4 whole pixels (1 KB contiguous when the output is dense) instead of 16 pixels x 64 bytes.
+template <bool NT, bool STG = false>
 __global__ __launch_bounds__(512, 2) void conv3x3_first_softmax(ConvArgs a) {
   using T = uint16_t;
   constexpr int TH = 8, TW = 32, PW = TW + 2, PPIX = (TH + 2) * PW;
+  constexpr int SRF = 68;  // staging row: 64 floats + 4 (rows 272 B apart)
   __shared__ __attribute__((aligned(16))) uint4 patch[PPIX];
+  __shared__ __attribute__((aligned(16))) float stg[STG ? 8 * 16 * SRF : 4];
   __shared__ __attribute__((aligned(16))) float rmul[2 * 64];  // per-channel scale, bias*scale + shift
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int H = a.H, W = a.W, cs = a.x_cstride;
@@ -1686,14 +1690,39 @@ __global__ __launch_bounds__(512, 2) void conv3x3_first_softmax(ConvArgs a) {
       sum += __shfl_xor(sum, 16);
       sum += __shfl_xor(sum, 32);
       const float inv = 1.f / sum;
-      const int pc = fp * 16 + col;
-      if (r0 + wave < H && c0 + pc < W) {
-        float* yp = yb + (long)pc * ycs + 4 * q;
+      if constexpr (STG) {
+        float* ws = stg + wave * 16 * SRF;
 #pragma unroll
-        for (int fc = 0; fc < 4; ++fc) {
-          const f32x4 o = f32x4{v[fc][0] * inv, v[fc][1] * inv, v[fc][2] * inv, v[fc][3] * inv};
-          if constexpr (NT) __builtin_nontemporal_store(o, reinterpret_cast<f32x4*>(yp + fc * 16));
-          else *reinterpret_cast<f32x4*>(yp + fc * 16) = o;
+        for (int fc = 0; fc < 4; ++fc)
+          *reinterpret_cast<f32x4*>(ws + col * SRF + fc * 16 + 4 * q) =
+              f32x4{v[fc][0] * inv, v[fc][1] * inv, v[fc][2] * inv, v[fc][3] * inv};
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+        for (int it = 0; it < 4; ++it) {  // lane l: pixel 4*it + l/16, channels 4*(l%16) .. +3
+          const int px = 4 * it + (lane >> 4), ch = 4 * (lane & 15);
+          const f32x4 o = *reinterpret_cast<const f32x4*>(ws + px * SRF + ch);
+          const int pc = fp * 16 + px;
+          if (r0 + wave < H && c0 + pc < W) {
+            float* yp = yb + (long)pc * ycs + ch;
+            if constexpr (NT) __builtin_nontemporal_store(o, reinterpret_cast<f32x4*>(yp));
+            else *reinterpret_cast<f32x4*>(yp) = o;
+          }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // reads done before the next fragment's writes
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      } else {
+        const int pc = fp * 16 + col;
+        if (r0 + wave < H && c0 + pc < W) {
+          float* yp = yb + (long)pc * ycs + 4 * q;
+#pragma unroll
+          for (int fc = 0; fc < 4; ++fc) {
+            const f32x4 o = f32x4{v[fc][0] * inv, v[fc][1] * inv, v[fc][2] * inv, v[fc][3] * inv};
+            if constexpr (NT) __builtin_nontemporal_store(o, reinterpret_cast<f32x4*>(yp + fc * 16));
+            else *reinterpret_cast<f32x4*>(yp + fc * 16) = o;
+          }
         }
       }
     }
@@ -2706,7 +2735,8 @@ static int launch_first(ConvArgs& a, hipStream_t st) {
   return check_launch("conv3x3_first");
 }
 
-static int g_softmax_kernel = 1;  // 0: the generic kernels' softmax epilogue, 1: conv3x3_first_softmax, 2: its NT form
+static int g_softmax_kernel = 4;  // 0: the generic kernels' softmax epilogue, 1: conv3x3_first_softmax, 2: its NT form,
+                                  // 3 / 4: plain / NT with the per-wave LDS transpose (whole-pixel stores)
 static long g_softmax_blocks = 1024;  // persistent grid of conv3x3_first_softmax
 static long g_pair_xin_wide = 1;  // pair kernel, f32 frames with >= 4 channels: two 16-byte loads per pixel (XIN 2)
 
@@ -2719,7 +2749,13 @@ static int launch_first_softmax(ConvArgs& a, hipStream_t st) {
   // contiguous per-XCD bands (xcd_tile within a round)
   const int grid = (int)std::min<long>(sp, g_softmax_blocks);
   a.tiles_n = grid;
-  if (g_softmax_kernel == 2) {
+  if (g_softmax_kernel == 3) {
+    snprintf(g_last_kernel, sizeof g_last_kernel, "vm::conv3x3_first_softmax<false, true>");
+    hipLaunchKernelGGL((conv3x3_first_softmax<false, true>), dim3(grid), dim3(512), 0, st, a);
+  } else if (g_softmax_kernel == 4) {
+    snprintf(g_last_kernel, sizeof g_last_kernel, "vm::conv3x3_first_softmax<true, true>");
+    hipLaunchKernelGGL((conv3x3_first_softmax<true, true>), dim3(grid), dim3(512), 0, st, a);
+  } else if (g_softmax_kernel == 2) {
     snprintf(g_last_kernel, sizeof g_last_kernel, "vm::conv3x3_first_softmax<true>");
     hipLaunchKernelGGL(conv3x3_first_softmax<true>, dim3(grid), dim3(512), 0, st, a);
   } else {
@@ -2764,7 +2800,7 @@ extern "C" int vm_set_option(const char* key, long value) {
     return VM_OK;
   }
   if (!strcmp(key, "softmax_kernel")) {
-    if (value < 0 || value > 2) return fail(VM_EINVAL, "softmax_kernel must be 0..2");
+    if (value < 0 || value > 4) return fail(VM_EINVAL, "softmax_kernel must be 0..4");
     g_softmax_kernel = value;
     return VM_OK;
   }
