@@ -67,7 +67,13 @@ const char* vm_last_error(void);
  *   "conv_min_tiles" grid size (256-wide output tiles) from which auto uses the LDS-DMA kernel (default 128)
  *   "glds_rb"        K-step bytes of the 256x256 LDS-DMA tile: 128 (2-slot ring, default) or 64 (4-slot)
  *   "head_kernel"    cout == 1 convs: 0 = MFMA tap-GEMM kernel (default), 1 = generic per-pixel kernel,
- *                    2 = register-strip kernel */
+ *                    2 = register-strip kernel
+ *   "softmax_kernel" bf16 cin <= 8 -> 64 conv + softmax (refine.py conv4): 0 = generic kernels' epilogue,
+ *                    1 = conv3x3_first_softmax (register stores), 2 = its nontemporal form, 3 / 4 = per-wave LDS
+ *                    transpose with whole-pixel plain / nontemporal stores (4 = default)
+ *   "softmax_blocks" persistent grid of conv3x3_first_softmax (default 1024)
+ *   "pair_xin_wide"  pair kernel, f32 frames with 4..8 channels: 1 = two 16-byte loads per pixel (default),
+ *                    0 = one dword load per channel */
 int vm_set_option(const char* key, long value);
 /* Name of the conv kernel the calling thread's last vm_conv3x3_nhwc launched, spelled the way
  * rocprofv3 reports it (e.g. "vm::conv3x3_mfma<unsigned short, 128, 128>"); "" before the first call.
