@@ -82,11 +82,27 @@ def ms(e0, e1):
 
 # ------------------------------------------------------------------------------------------------ config 4
 
-def video_batch(model, value_per_gpu, n_frames, h, w, rank, world, dev, chunk):
+def video_batch(model, n_frames, h, w, rank, world, dev, chunk, solo_frames=32):
     """BASELINE config 4 through the product path (vmatting/video.py): n_frames synthetic 1080p frames sharded
     frame-parallel in contiguous blocks, each rank's block replayed in HIP graphs of `chunk` frames (input read
     in place, alpha written in place), then ONE all-gather (RCCL ring over xGMI) hands every rank the whole
-    [n_frames, H, W, 1] f32 matte batch.  Timed between barriers, max over ranks."""
+    [n_frames, H, W, 1] f32 matte batch.  Timed between barriers, max over ranks.
+
+    parallel_efficiency (N > 1) = frames/s / (N x the same video path's frames/s on ONE GPU, measured in this run:
+    rank 0 alone replays `solo_frames` frames' chunk graphs while the other ranks wait at a barrier)."""
+    solo = None
+    if world > 1:
+        if rank == 0:
+            sf = video.synthetic_frames(solo_frames, h, w, first=0, device=dev)
+            svm = video.VideoMatter(model, sf, chunk=chunk)
+            svm.run()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            svm.run()
+            torch.cuda.synchronize()
+            solo = solo_frames / (time.perf_counter() - t0)
+            del svm, sf
+        dist.barrier()
     a, b = video.shard(n_frames, rank, world)
     frames = video.synthetic_frames(b - a, h, w, first=a, device=dev)
     vm = video.VideoMatter(model, frames, chunk=chunk)
@@ -112,16 +128,22 @@ def video_batch(model, value_per_gpu, n_frames, h, w, rank, world, dev, chunk):
     total, comp, gath = (float(v) for v in ts.tolist())
     assert full.shape[0] == n_frames
     fps = n_frames / total
-    return {"workload": "config 4: %d synthetic %dx%d frames sharded frame-parallel over %d GPU(s), mattes "
-                        "all-gathered to every rank (vmatting/video.py)" % (n_frames, w, h, world),
-            "frames": n_frames, "frames_per_s": round(fps, 3), "ms_total": round(1e3 * total, 3),
-            "ms_compute_max_rank": round(1e3 * comp, 3), "ms_all_gather": round(1e3 * gath, 3),
-            "all_gather_bytes": int(full.numel() * full.element_size()), "chunk_frames": chunk,
-            "graphs_per_rank": len(vm.spans),
-            # this run's own single-GPU reference: the headline step rate per GPU (batch-1 graph replay)
-            "parallel_efficiency": round(fps / (world * value_per_gpu), 4),
-            "parallel_efficiency_def": "frames_per_s / (n_gpus x the headline value per GPU of this run)",
-            "includes": "chunked HIP-graph replay reading the frames in place + the matte all-gather"}
+    rec = {"workload": "config 4: %d synthetic %dx%d frames sharded frame-parallel over %d GPU(s), mattes "
+                       "all-gathered to every rank (vmatting/video.py)" % (n_frames, w, h, world),
+           "frames": n_frames, "frames_per_s": round(fps, 3), "ms_total": round(1e3 * total, 3),
+           "ms_compute_max_rank": round(1e3 * comp, 3), "chunk_frames": chunk, "graphs_per_rank": len(vm.spans),
+           "includes": "chunked HIP-graph replay reading the frames in place" + (" + the matte all-gather"
+                                                                                 if world > 1 else "")}
+    if world > 1 and solo is not None:  # rank 0 (the one that prints)
+        rec.update({"ms_all_gather": round(1e3 * gath, 3),
+                    "all_gather_bytes": int(full.numel() * full.element_size()),
+                    "solo_frames_per_s": round(solo, 3), "parallel_efficiency": round(fps / (world * solo), 4),
+                    "parallel_efficiency_def": "frames_per_s / (n_gpus x the same chunked video path's frames/s on "
+                                               "rank 0 alone, %d frames, measured in this run)" % solo_frames})
+    else:
+        rec["parallel_efficiency_def"] = ("N = 1: this record IS the single-GPU reference of the video path; "
+                                          "efficiency is defined at N > 1 against it")
+    return rec
 
 
 # ------------------------------------------------------------------------------------------------ config 3
@@ -153,13 +175,15 @@ def temporal_case(h, w, seed=7):
     return prev, cur, cmp, bw, fw
 
 
-def temporal_bench(dev, steps, dtype, sizes, cpu, threads):
+def temporal_bench(dev, steps, dtypes, sizes, cpu, threads):
     """BASELINE config 3: flow warp (flow.py:9-18) + occlusion check (flow.py:36-65) + RefineNet (refine.py:27-32,
-    Cin 5) on synthetic smooth flows, inputs resident in HBM.  Device ms per stage from HIP events on the launch
-    stream; both stages are HBM-bound (algorithmic bytes below), the refine conv is also reported in TFLOP/s."""
+    Cin 5) on synthetic smooth flows, inputs resident in HBM, for each compute dtype: fp32 is the reference's
+    precision (the config-3 number), bf16 the throughput variant.  Device ms per stage from HIP events on the
+    launch stream; the refine stage's roofline is the larger of its HBM time (algorithmic bytes) and its MFMA time
+    (algorithmic FLOPs at the dtype's dense peak)."""
     from vmatting import temporal
-    recs = []
-    for h, w in sizes:
+    recs, cpu_rec = [], None
+    for dtype, (h, w) in [(d, hw) for d in dtypes for hw in sizes]:
         prev, cur, cmp, bw, fw = temporal_case(h, w)
         T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
         args = [T(a) for a in (prev, cur, cmp, bw, fw)]
@@ -189,21 +213,29 @@ def temporal_bench(dev, steps, dtype, sizes, cpu, threads):
         # refine: input row 8*ob + f32 64-ch softmax out 256; FLOPs of conv4 at the reference's Cin = 5
         b_rf = px * (8 * ob + 256)
         f_rf = 2.0 * px * 9 * 5 * 64
+        pk = PEAK_TFLOPS[dtype]
+        t_hbm, t_mfma = b_rf / (PEAK_HBM_GBPS * 1e9), f_rf / (pk * 1e12)
+        rf = {"bound": "hbm" if t_hbm >= t_mfma else "mfma", "algorithmic_bytes": int(b_rf),
+              "algorithmic_flops": int(f_rf), "achieved_gbps": round(b_rf / (t_rf * 1e-3) / 1e9, 1),
+              "peak_gbps": PEAK_HBM_GBPS, "tflops": round(f_rf / (t_rf * 1e-3) / 1e12, 2), "peak_tflops": pk,
+              "roofline_ms": round(1e3 * max(t_hbm, t_mfma), 4),
+              "frac": round(1e3 * max(t_hbm, t_mfma) / t_rf, 4),
+              "frac_def": "roofline time (max of HBM bytes / 8 TB/s and FLOPs / dense peak) / measured device time"}
         rec = {"workload": "config 3: warp + correct_alpha + RefineNet(Cin 5) at %dx%d, %s" % (w, h, dtype),
+               "dtype": dtype,
+               "role": "reference precision (fp32, the config-3 number)" if dtype == "fp32" else
+                       "throughput variant (bf16 operands, f32 accumulate and softmax)",
                "pairs_per_s": round(1.0 / wall, 1), "ms_per_pair": round(1e3 * wall, 4),
                "device_ms": {"warp_occlusion_input": round(t_in, 4), "refine_conv_softmax": round(t_rf, 4)},
+               "refine_kernel": _lib_last_kernel(),
                "roofline": {
                    "warp_occlusion_input": {"bound": "hbm", "algorithmic_bytes": int(b_in),
                                             "achieved_gbps": round(b_in / (t_in * 1e-3) / 1e9, 1),
                                             "peak_gbps": PEAK_HBM_GBPS,
                                             "frac": round(b_in / (t_in * 1e-3) / 1e9 / PEAK_HBM_GBPS, 4)},
-                   "refine_conv_softmax": {"bound": "hbm", "algorithmic_bytes": int(b_rf),
-                                           "achieved_gbps": round(b_rf / (t_rf * 1e-3) / 1e9, 1),
-                                           "peak_gbps": PEAK_HBM_GBPS,
-                                           "frac": round(b_rf / (t_rf * 1e-3) / 1e9 / PEAK_HBM_GBPS, 4),
-                                           "tflops": round(f_rf / (t_rf * 1e-3) / 1e12, 2)}},
+                   "refine_conv_softmax": rf},
                "occluded_px": int((tp.warped == 0).sum().item())}
-        if cpu and (h, w) == sizes[0]:
+        if cpu and (h, w) == sizes[0] and cpu_rec is None:
             from oracle import flow as oflow  # the CPU-baseline leg only
             from oracle import ops as oops
             p4 = tp.refine.params["conv4"]
@@ -215,17 +247,23 @@ def temporal_bench(dev, steps, dtype, sizes, cpu, threads):
                 oops.softmax_lastdim(oops.conv3x3_same(xin, p4[0], p4[1]))
                 times.append(time.perf_counter() - t0)
             dt = min(times)
-            rec["cpu_baseline"] = {"value": round(1.0 / dt, 3), "unit": "pairs/s", "cores": threads, "kind": "port",
-                                   "sample": "oracle/flow.py warp_img + vectorised correct_alpha + oracle/ops.py "
-                                             "conv3x3 + softmax (RefineNet conv4, f32) on one %dx%d pair, best of 2"
-                                             % (w, h)}
+            cpu_rec = {"value": round(1.0 / dt, 3), "unit": "pairs/s", "cores": threads, "kind": "port",
+                       "sample": "oracle/flow.py warp_img + vectorised correct_alpha + oracle/ops.py "
+                                 "conv3x3 + softmax (RefineNet conv4, f32) on one %dx%d pair, best of 2" % (w, h)}
+        if cpu_rec is not None and (h, w) == sizes[0]:
+            rec["cpu_baseline"] = cpu_rec
         recs.append(rec)
     return recs
 
 
+def _lib_last_kernel():
+    from vmatting import _lib
+    return _lib.last_conv_kernel()
+
+
 # ------------------------------------------------------------------------------------------------ CPU baseline + parity
 
-def cpu_baseline(x_host, params, frames, threads, model_name):
+def cpu_baseline(x_host, params, frames, threads, model_name, flops_per_frame):
     """The oracle (numpy f32 restatement of unet.py, the reference's op sequence) on the host cores: 1 warm-up
     frame at 270x480, then `frames` full 1920x1080 frames timed, median.  Returns (record, oracle output of the
     first timed frame) — the latter is the fp32 parity check of the timed frame."""
@@ -240,7 +278,11 @@ def cpu_baseline(x_host, params, frames, threads, model_name):
             ref = r
     med = statistics.median(times)
     rec = {"value": round(1.0 / med, 5), "unit": "frames/s", "cores": threads, "kind": "port",
-           "host_cpu": model_name,
+           "host_cpu": model_name, "implied_tflops": round(flops_per_frame / med / 1e12, 3),
+           "affinity_cpus": len(os.sched_getaffinity(0)),
+           "threads_def": "cores = BLAS pool threads the oracle ran on (numpy's OpenBLAS, OMP_NUM_THREADS on the box); "
+                          "affinity_cpus = CPUs in this process's affinity mask; the loader / augment / train / "
+                          "temporal CPU legs use the same thread count",
            "sample": "oracle/models.py numpy-f32 UNetVideo forward (the reference's op sequence) on the timed "
                      "1920x1080 frame: 1 warm-up (270x480), median of %d full frames (%s s)"
                      % (frames, ", ".join("%.1f" % t for t in times))}
@@ -484,6 +526,73 @@ def train_bench(dev, steps, warmup, world, rank, threads, cpu=True, n=8, size=32
     return rec
 
 
+def train_chain_bench(dev, steps, warmup, n=8, size=320, h=1080, w=1920, dtype="bf16"):
+    """BASELINE config 5 as ONE pipeline per step (rank 0, N=1): augmentation.augment makes frame t of each of n
+    1080p source samples resident in HBM (augmentation.py:102-135, host np.random draws + TPS solve + one stats
+    readback per sample), the video loader's crops / warp / resize / composite turn the n (frame t, bg, frame t-1,
+    flow) entries into an n x size^2 batch (loader.py:285-330, host crop draws), then one VideoTrainer step
+    (train.py:318-332).  No decoding: the source images are synthetic device tensors (PNG/JPEG decode is host I/O
+    outside the path).  Wall ms per phase and device ms per phase (HIP events on the launch stream)."""
+    from vmatting import augmentation as va
+    from vmatting import loader as vl
+    from vmatting.train import VideoTrainer
+    rs = np.random.RandomState(12)
+    yy, xx = np.mgrid[0:h, 0:w]
+    src = []
+    for i in range(n):
+        al = np.clip(1.2 - np.sqrt(((yy - (0.4 + 0.02 * i) * h) / (0.28 * h)) ** 2 +
+                                   ((xx - 0.47 * w) / (0.21 * w)) ** 2), 0, 1)
+        src.append(tuple(torch.from_numpy(np.ascontiguousarray(a)).to(dev) for a in
+                         ((rs.rand(h, w, 3) * 255).astype(np.uint8), (rs.rand(h, w, 3) * 255).astype(np.uint8), al)))
+    flow = torch.from_numpy(synthetic_flow(h, w, 11, amp=12.0)).to(dev)
+    np.random.seed(7)
+    trn = VideoTrainer(synthetic_vgg16(0), dtype, dev)
+    names = ("cmp", "bg", "label", "warped", "fg")
+
+    def one(ev=None, wall=None):
+        t0 = time.perf_counter()
+        ev and ev.mark()
+        samples = []
+        for fg, bg, al in src:
+            smp = va.video_sample(fg, bg, al, flow)
+            smp["plan"] = vl.plan_crop((h, w), (h, w))
+            samples.append(smp)
+        t1 = time.perf_counter()
+        ev and ev.mark()
+        r = vl.compose_batch(samples, (size, size), names, device=dev)
+        t2 = time.perf_counter()
+        ev and ev.mark()
+        loss = trn.step(r["cmp"], r["bg"], r["warped"], r["label"], r["fg"])
+        ev and ev.mark()
+        t3 = time.perf_counter()
+        if wall is not None:
+            wall.append((t1 - t0, t2 - t1, t3 - t2))
+        return loss
+
+    for _ in range(warmup):
+        one()
+    torch.cuda.synchronize()
+    ev, wall = Events(), []
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        loss = one(ev, wall)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    e = ev.e
+    dev_ms = [sum(ms(e[4 * i + k], e[4 * i + k + 1]) for i in range(steps)) / steps for k in range(3)]
+    host_ms = [1e3 * sum(wl[k] for wl in wall) / steps for k in range(3)]
+    return {"workload": "config 5 chained: augmentation.augment on %d 1080p sources -> loader video_batch per-pixel "
+                        "work -> %dx%d -> VideoTrainer step (%s forward, f32 gradients / Adam)" % (n, size, size, dtype),
+            "samples_per_s": round(n / dt, 1), "ms_per_step": round(1e3 * dt, 3),
+            "device_ms": {"augment": round(dev_ms[0], 3), "loader": round(dev_ms[1], 3),
+                          "train_step": round(dev_ms[2], 3)},
+            "host_issue_ms": {"augment_draws_tps_solve_stats_sync": round(host_ms[0], 3),
+                              "loader_crop_draws_and_launch": round(host_ms[1], 3),
+                              "train_step_launches": round(host_ms[2], 3)},
+            "decode": "none: synthetic source images resident in HBM (PNG/JPEG decoding is host I/O outside the path)",
+            "loss_last": [round(float(v), 5) for v in loss.cpu()]}
+
+
 # ------------------------------------------------------------------------------------------------ roofline
 
 def load_profile(kind, args):
@@ -562,7 +671,7 @@ def main():
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-frames", type=int, default=2, help="full 1080p frames timed for the CPU baseline (median)")
+    ap.add_argument("--cpu-frames", type=int, default=3, help="full 1080p frames timed for the CPU baseline (median)")
     ap.add_argument("--no-profile", action="store_true", help="skip per-conv HIP events")
     ap.add_argument("--layers", action="store_true", help="per-conv timing breakdown on stderr")
     ap.add_argument("--no-graph", action="store_true", help="time eager launches instead of the captured HIP graph")
@@ -645,11 +754,13 @@ def main():
 
     vrec = None
     if args.video_frames > 0:
-        vrec = video_batch(model, value / world, args.video_frames, H, W, rank, world, dev, args.video_chunk)
+        vrec = video_batch(model, args.video_frames, H, W, rank, world, dev, args.video_chunk)
 
     train = None
     if not args.no_train:  # every rank: the DDP all-reduce is part of the step
         train = train_bench(dev, max(args.steps // 4, 10), 3, world, rank, threads, cpu=not args.no_cpu_baseline)
+        if world == 1:
+            train["chained"] = train_chain_bench(dev, 5, 2)
 
     roofline = conv_roofline(prof, args) if prof else None
     if rank == 0:
@@ -693,7 +804,8 @@ def main():
                    "fp32_logits_absmax": float(l32.abs().max()),
                    "bound": 1e-4, "bound_applies_to": "fp32 alpha vs the reference CPU forward (north_star)"}
             if not args.no_cpu_baseline:
-                crec, ref = cpu_baseline(x[:1].cpu().numpy(), params, args.cpu_frames, threads, cpu_model)
+                crec, ref = cpu_baseline(x[:1].cpu().numpy(), params, args.cpu_frames, threads, cpu_model,
+                                         flops_per_frame)
                 rec["cpu_baseline"] = crec
                 par["fp32_vs_oracle_alpha_maxabs"] = float(np.abs(a32[:1].cpu().numpy() - ref["output"]).max())
                 par["fp32_vs_oracle_logits_rel"] = float(np.abs(l32[:1].cpu().numpy() - ref["conv1_3"]).max()
@@ -707,7 +819,7 @@ def main():
         if vrec:
             rec["video_batch"] = vrec
         if world == 1 and not args.no_temporal:
-            rec["temporal"] = temporal_bench(dev, 20, args.dtype, [(500, 1200), (1080, 1920)],
+            rec["temporal"] = temporal_bench(dev, 20, ["fp32", "bf16"], [(500, 1200), (1080, 1920)],
                                              not args.no_cpu_baseline, threads)
         if train:
             rec["train"] = train

@@ -63,7 +63,11 @@ const char* vm_last_error(void);
  *   "conv_kernel"    0 = auto (default: patch kernel when legal, else by shape), 1 = register-staged MFMA kernel
  *                    only, 2 = LDS-DMA kernel when legal, 3 = patch-reuse kernel when legal (bf16, cin % 32 == 0,
  *                    bf16 output, no softmax)
- *   "patch_cfg"      patch-kernel tiling override for tuning (0 = default)
+ *   "patch_cfg"      patch-kernel tiling override (0 = dispatcher's choice; 19, 22, 25, 30 = one of the tilings it
+ *                    picks); the other sweep tilings and the timing-only ablations ("patch_ablate", "patch_rowslot",
+ *                    "pair_kernel" 10..18, garbage results) exist only in the study build (`make study`), never here
+ *   "src_span_limit" byte span of split sources the 32-bit-offset conv kernels take (default 0x7ffffff0; wider
+ *                    spans return VM_EUNSUPPORTED and the caller materialises the concat); lowered by tests
  *   "conv_min_tiles" grid size (256-wide output tiles) from which auto uses the LDS-DMA kernel (default 128)
  *   "glds_rb"        K-step bytes of the 256x256 LDS-DMA tile: 128 (2-slot ring, default) or 64 (4-slot)
  *   "head_kernel"    cout == 1 convs: 0 = MFMA tap-GEMM kernel (default), 1 = generic per-pixel kernel,
@@ -364,6 +368,14 @@ int vm_bn_backward_nhwc(const vm_tensor* x, const vm_tensor* dy, const vm_tensor
 int vm_bn_backward_ex_nhwc(const vm_tensor* x, const vm_tensor* dy, const vm_tensor* y, const float* mean,
                            const float* var, const float* gamma, float eps, vm_tensor* dx, vm_tensor* dx2,
                            float* dgamma, float* dbeta, float* dbias, void* work, void* stream);
+
+/* The input-gradient pass of vm_bn_backward_ex_nhwc alone, with the two channel sums given: sum_g = sum(g),
+ * sum_gx = sum(g * xhat) over `count` pixels.  SyncBN (DDP with statistics over the global batch, the single-device
+ * reference's unet_simple.py:25,41 normalisation): each replica takes its local sums (vm_bn_backward_ex_nhwc with
+ * dx NULL), all-reduces them, and applies them here with count = all replicas' pixels. */
+int vm_bn_backward_apply_nhwc(const vm_tensor* x, const vm_tensor* dy, const vm_tensor* y, const float* mean,
+                              const float* var, const float* gamma, float eps, const float* sum_g,
+                              const float* sum_gx, long count, vm_tensor* dx, vm_tensor* dx2, void* stream);
 
 /* tf.nn.relu gradient: dx = dy * (y > 0); dx f32. */
 int vm_relu_backward_nhwc(const vm_tensor* dy, const vm_tensor* y, vm_tensor* dx, void* stream);

@@ -66,7 +66,7 @@ def conv_kernel(request):
     _lib.set_option("conv_kernel", 0)
 
 
-@pytest.mark.parametrize("cfg", list(range(1, 27)))
+@pytest.mark.parametrize("cfg", [19, 22, 25, 30])  # every tiling the shipped dispatcher can pick
 @pytest.mark.parametrize("case", [(1, 9, 33, 64, 64, "relu"), (2, 17, 70, 128, 128, "none"), (1, 20, 45, 96, 192, "relu"),
                                   (1, 8, 32, 32, 64, "sigmoid"), (1, 3, 5, 256, 128, "relu")])
 def test_patch_kernel_configs(case, cfg):
@@ -333,7 +333,7 @@ UP_CASES = [(1, 9, 13, 128, 64), (2, 7, 33, 256, 128), (1, 1, 1, 64, 64), (1, 3,
             (1, 17, 30, 64, 192), (1, 68, 120, 128, 64)]
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 5, 8, 10, 12, 19, 21])
+@pytest.mark.parametrize("cfg", [0, 19, 22, 25, 30])
 @pytest.mark.parametrize("case", UP_CASES)
 def test_upconv_folded_resize(case, cfg):
     """vm_conv3x3_up2x_nhwc (resize folded into four phase filters + exact border recompute) vs the oracle's
@@ -606,6 +606,79 @@ def test_unet_graph_replay_matches_eager(dtype, vgg0):
         ya = g(x).clone()
         yb = m.forward(torch.from_numpy(x).to(DEV)).clone()
         assert torch.equal(ya, yb)
+
+
+def test_unet_graph_replay_restores_lazy_attributes(vgg0):
+    """After another shape's eager forward and a lazy .conv1_2 evaluation, a replay leaves the model's attributes on
+    the replayed frames: .output / .conv1_2 equal a fresh eager forward of the same frames (head split: conv1_2 is
+    re-evaluated, not the stale skip half)."""
+    from vmatting import unet
+    rs = np.random.RandomState(6)
+    mk = lambda n, h, w: np.concatenate([rs.uniform(-120, 130, (n, h, w, 6)),  # noqa: E731
+                                         rs.choice([-0.5, 0.0, 0.5], (n, h, w, 1))], -1).astype(np.float32)
+    x0, x1, other = mk(1, 40, 72), mk(1, 40, 72), mk(2, 24, 40)
+    np.random.seed(1)
+    m = unet.UNetVideo(vgg0, dtype="bf16")
+    m.build(x0)
+    g = m.capture(x0)
+    g(x1)
+    c12_a = m.conv1_2.clone()  # lazily evaluated on x1
+    m.forward(torch.from_numpy(other).to(DEV))
+    _ = m.conv1_2  # evaluated on the other shape's set
+    g(x0)
+    out_g, c12_g = m.output.clone(), m.conv1_2.clone()
+    m.forward(torch.from_numpy(x0).to(DEV))
+    assert torch.equal(out_g, m.output) and torch.equal(c12_g, m.conv1_2)
+    assert not torch.equal(c12_a, c12_g)
+
+
+def test_split_sources_past_the_offset_limit_fall_back():
+    """split sources (tower-major SourceConcat) whose byte span passes the 32-bit offsets of the patch
+    kernel are refused by the library (VM_EUNSUPPORTED) and ops.conv3x3 runs the materialised concat instead —
+    same kernel, same arithmetic: bit-identical to the split-source result, and the oracle within bf16 tolerance."""
+    from vmatting import _lib, ops
+    rs = np.random.RandomState(17)
+    n, h, w, c, cout = 2, 21, 70, 64, 64
+    base = T(rs.normal(size=(3 * n, h, w, c)).astype(np.float32), torch.bfloat16)
+    sc = ops.SourceConcat(base, 3)
+    wt = torch.from_numpy((rs.normal(size=(3, 3, 3 * c, cout)) * 0.05).astype(np.float32))
+    wt = wt.to(torch.bfloat16).float().numpy()
+    b = (rs.normal(size=cout) * 0.1).astype(np.float32)
+    pc = ops.PackedConv(wt, b, torch.bfloat16, DEV)
+    split = ops.conv3x3(sc, pc, "relu").clone()
+    span = (2 * sc.stride + h * w * c) * 2
+    try:
+        _lib.set_option("src_span_limit", span)  # exactly at the limit: refused
+        xv = ops.nhwc(sc.src0)
+        y = torch.empty_like(split)
+        yv = ops.nhwc(y)
+        import ctypes
+        rc = _lib.lib().vm_conv3x3_ex_nhwc(ctypes.byref(xv), 3, sc.stride, ops._ptr(pc.packed), pc.cin, pc.cout,
+                                           ops._ptr(pc.bias), None, None, _lib.ACT["relu"], ctypes.byref(yv), None, 0,
+                                           _lib.stream_handle())
+        assert rc == _lib.VM_EUNSUPPORTED
+        fell = ops.conv3x3(sc, pc, "relu").clone()
+    finally:
+        _lib.set_option("src_span_limit", 0x7ffffff0)
+    assert torch.equal(fell, split)
+    cat = np.concatenate([H(sc.source(i)) for i in range(3)], -1).astype(np.float64)
+    ref = oops.relu(oops.conv3x3_same(cat, wt.astype(np.float64)) + b)
+    assert np.abs(H(split) - ref).max() <= 1e-2 * max(1.0, np.abs(ref).max())
+
+
+def test_unet_simple_inference_is_batch_invariant(vgg0):
+    """UNetSimple inference (phase False, folded BN affine) runs without split-K, so a frame's alpha
+    does not depend on the batch it is evaluated in (bf16 path)."""
+    from vmatting import unet_simple
+    rs = np.random.RandomState(3)
+    c = rs.uniform(-120, 130, (3, 64, 96, 3)).astype(np.float32)
+    b = rs.uniform(-120, 130, (3, 64, 96, 3)).astype(np.float32)
+    np.random.seed(2)
+    m = unet_simple.create_model(c, b, c - b, False, vgg16_npy_path=vgg0, dtype="bf16")
+    full = m.output.clone()
+    for i in range(3):
+        one = m.forward(c[i:i + 1], b[i:i + 1], c[i:i + 1] - b[i:i + 1]).clone()
+        assert torch.equal(one[0], full[i]), i
 
 
 @pytest.mark.parametrize("case", ["unet_simple_256_infer", "unet_simple_64_train"])

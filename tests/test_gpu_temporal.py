@@ -101,6 +101,31 @@ def test_temporal_refine_bf16_close_to_fp32():
     assert torch.equal(tb.warped, tf.warped)
 
 
+@pytest.mark.parametrize("h,w", [(500, 1200), (1080, 1920)])
+def test_temporal_refine_bf16_kernel_vs_oracle(h, w):
+    """The TIMED bf16 config-3 refine (conv3x3_first_softmax<true, true>: refine conv4 + the 64-way softmax fused)
+    against the oracle's conv + softmax in float64 on the same bf16-rounded input row and bf16-rounded filter (f32
+    bias): only the f32 summation order and the device exp differ, so the probabilities stay within 1e-4 max-abs
+    (north_star's bound) at full size; rows sum to 1."""
+    from oracle import ops as oops
+    from vmatting import _lib, temporal
+    prev, cur, cmp, bw, fw, _ = _case(h, w)
+    np.random.seed(3)
+    tp = temporal.TemporalRefiner(dtype="bf16")
+    out = tp(T(prev), T(cur), T(cmp), T(bw), T(fw))
+    torch.cuda.synchronize()
+    assert _lib.last_conv_kernel() == "vm::conv3x3_first_softmax<true, true>", _lib.last_conv_kernel()
+    x = tp._bufs[(h, w)]["xin"][..., :5].float().cpu().numpy().astype(np.float64)  # the bf16 input row
+    w4, b4 = tp.refine.params["conv4"]
+    w4 = torch.from_numpy(np.ascontiguousarray(w4, np.float32)).to(torch.bfloat16).double().numpy()
+    ref = oops.softmax_lastdim(oops.conv3x3_same(x, w4, np.asarray(b4, np.float64)))
+    got = out.cpu().numpy()
+    err = float(np.abs(got - ref).max())
+    print("config 3 %dx%d: bf16 refine kernel max-abs err vs oracle (bf16 operands) %.2e" % (h, w, err))
+    assert err <= 1e-4
+    np.testing.assert_allclose(got.sum(-1), 1.0, atol=1e-5)
+
+
 def test_temporal_index_error():
     from vmatting import temporal
     prev, cur, cmp, bw, fw, _ = _case(16, 20)
@@ -129,7 +154,7 @@ def test_refine_softmax_kernel_matches_generic_epilogue(n, h, w):
             outs[k] = ops.conv3x3(xb, pc, "softmax", out_dtype=torch.float32)
             name = _lib.last_conv_kernel()
             assert ("first_softmax" in name) == (k != 0), name
-        for k in (3, 4):  # the per-wave LDS transpose store forms: same values
+        for k in (3, 4, 5):  # the per-wave LDS transpose store forms (5: weights staged in LDS): same values
             _lib.set_option("softmax_kernel", k)
             assert torch.equal(ops.conv3x3(xb, pc, "softmax", out_dtype=torch.float32), outs[1]), k
         _lib.set_option("softmax_kernel", 2)
@@ -145,3 +170,37 @@ def test_refine_softmax_kernel_matches_generic_epilogue(n, h, w):
         assert np.abs(got - ref).max() <= 1e-5, (k, np.abs(got - ref).max())
         np.testing.assert_allclose(got.sum(-1), 1.0, atol=1e-5)
     assert torch.equal(outs[1], outs[2])
+
+
+@pytest.mark.parametrize("cin", [1, 3, 5, 8])
+@pytest.mark.parametrize("n,h,w", [(1, 37, 70), (2, 8, 32), (1, 1, 1), (1, 135, 240)])
+def test_refine_softmax_f32_kernel(n, h, w, cin):
+    """conv3x3_first_softmax_f32 (compact-K exact-f32 MFMA conv + register softmax, the fp32 config-3 refine) against
+    the generic f32 kernel's softmax epilogue and the float64 oracle: exact f32 products, f32 sums in another order
+    -> within 1e-5 of both; rows sum to 1; ragged tiles and partial persistent rounds."""
+    from oracle import ops as oops
+    from vmatting import _lib, ops
+    rs = np.random.RandomState(h * 7 + w + cin)
+    x = np.zeros((n, h, w, 8), np.float32)
+    x[..., :cin] = rs.uniform(-30, 30, size=(n, h, w, cin))
+    wt = (rs.normal(size=(3, 3, cin, 64)) * 0.3).astype(np.float32)
+    b = rs.normal(size=64).astype(np.float32)
+    pc = ops.PackedConv(wt, b, "fp32")
+    xd = T(x)[..., :cin]
+    try:
+        got = ops.conv3x3(xd, pc, "softmax").clone()
+        assert _lib.last_conv_kernel() == "vm::conv3x3_first_softmax_f32<%d>" % cin, _lib.last_conv_kernel()
+        _lib.set_option("softmax_blocks", 3)
+        assert torch.equal(ops.conv3x3(xd, pc, "softmax"), got)  # persistent walk, partial last round
+        _lib.set_option("softmax_kernel", 0)
+        gen = ops.conv3x3(xd, pc, "softmax").clone()
+        assert "first_softmax" not in _lib.last_conv_kernel()
+    finally:
+        _lib.set_option("softmax_kernel", 4)
+        _lib.set_option("softmax_blocks", 1024)
+    ref = oops.softmax_lastdim(oops.conv3x3_same(x[..., :cin].astype(np.float64), wt.astype(np.float64),
+                                                 b.astype(np.float64)))
+    g = got.cpu().numpy()
+    assert np.abs(g - gen.cpu().numpy()).max() <= 1e-5
+    assert np.abs(g - ref).max() <= 1e-5, np.abs(g - ref).max()
+    np.testing.assert_allclose(g.sum(-1), 1.0, atol=1e-5)

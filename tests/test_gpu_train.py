@@ -418,7 +418,7 @@ def test_train_bf16_padded_convs_track_the_filters():
         assert err <= 2e-2, (scope, err)
 
 
-def _ddp_init_worker(rank, world, port, q):
+def _ddp_init_worker(rank, world, port, q, dtype="fp32"):
     import os
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
@@ -429,17 +429,26 @@ def _ddp_init_worker(rank, world, port, q):
         parallel.init_from_env(backend="gloo")  # gloo moves the cuda tensors; both ranks share cuda:0
         torch.cuda.set_device(0)
         np.random.seed(100 + rank)  # different init_conv draws per rank: the trainer must replicate rank 0's
-        trn = VideoTrainer(synthetic_vgg16(0), "fp32", "cuda:0")
+        trn = VideoTrainer(synthetic_vgg16(0), dtype, "cuda:0")
+        torch.cuda.synchronize()
+
+        def packs():  # every kernel-layout copy the step reads: forward, channel-padded, padded-cout, data-gradient
+            ts = [pc.packed for pc in trn.model.convs.values()] + [pc.packed for pc in trn.model.padded.values()]
+            ts += [v[0].packed for v in trn._padconv.values()] + [v[1] for v in trn._padconv.values()]
+            ts += [pc.packed for pc in list(trn.dconv16.values()) + list(trn.dconv.values())]
+            return torch.cat([t.reshape(-1).view(torch.uint8) for t in ts]).cpu()
+
+        def same(t):
+            got = [torch.empty_like(t) for _ in range(world)]
+            dist.all_gather(got, t)
+            return all(torch.equal(got[0], g) for g in got)
+
+        ok_init = same(packs())  # before the first step: the padded bf16 packs too
         cmp, bg, warped, gt, fg = _batch(1, 32, 32, seed=11 + rank)  # different data per rank
         trn.step(cmp, bg, warped, gt, fg)
         torch.cuda.synchronize()
-        flat = trn.flat.cpu()
-        pk = trn.model.convs["conv2"].packed.cpu()
-        both = [torch.empty_like(flat) for _ in range(world)]
-        dist.all_gather(both, flat)
-        pks = [torch.empty_like(pk) for _ in range(world)]
-        dist.all_gather(pks, pk)
-        q.put((rank, bool(torch.equal(both[0], both[1])), bool(torch.equal(pks[0], pks[1]))))
+        ok_flat = same(trn.flat.cpu())
+        q.put((rank, ok_flat, ok_init and same(packs())))
     except Exception as e:  # report instead of hanging the parent
         q.put((rank, False, repr(e)))
     finally:
@@ -448,15 +457,17 @@ def _ddp_init_worker(rank, world, port, q):
             dist.destroy_process_group()
 
 
-def test_ddp_replicas_start_identical_and_stay_identical():
-    """with world > 1 the trainer broadcasts rank 0's variables before the first step, so after one
-    DDP step (averaged gradients) the replicas hold bit-identical parameters and packed filters."""
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_ddp_replicas_start_identical_and_stay_identical(dtype):
+    """with world > 1 the trainer broadcasts rank 0's variables before the first step and re-makes
+    every pack from them (the bf16 channel-padded packs included), so the replicas hold bit-identical packs before
+    the first step and bit-identical parameters and packs after one DDP step (averaged gradients)."""
     import multiprocessing as mp
     import os
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = 29700 + (os.getpid() % 500)
-    procs = [ctx.Process(target=_ddp_init_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_ddp_init_worker, args=(r, 2, port + (dtype == "bf16"), q, dtype)) for r in range(2)]
     for p in procs:
         p.start()
     res = [q.get(timeout=100) for _ in procs]
@@ -569,3 +580,107 @@ def lib_ws(x, cin, cout):
     from vmatting._lib import lib
     xv = ops.nhwc(x)
     return lib().vm_conv3x3_workspace_bytes(ctypes.byref(xv), cin, cout)
+
+
+# ----------------------------------------------------------------------------- config 5 chained
+
+def test_config5_chain_augment_loader_step():
+    """BASELINE config 5 as one pipeline on the device: augmentation.augment (augmentation.py:102-135) makes frame t
+    of each of 2 small source samples (frame t-1 = the source, as augmentation.augmentation writes them), the video
+    loader's per-pixel work (loader.py:285-330) crops / warps / resizes / composites them into a 64x64 batch, and
+    one fp32 VideoTrainer.step (train.py:318-332) trains on it.  The step's loss terms equal oracle/train_ref.py's
+    float64 restatement evaluated on the loader's own outputs (1e-5 relative), alpha within 1e-4."""
+    from oracle.flow import smooth_flow
+    from vmatting import augmentation as va
+    from vmatting import loader as vl
+    from vmatting.train import VideoTrainer
+    from vmatting.weights import synthetic_vgg16
+    h, w = 120, 160
+    rs = np.random.RandomState(21)
+    yy, xx = np.mgrid[0:h, 0:w]
+    np.random.seed(5)
+    samples = []
+    for i in range(2):
+        al = np.clip(1.2 - np.hypot((yy - (0.45 + 0.1 * i) * h) / (0.3 * h), (xx - 0.5 * w) / (0.25 * w)), 0, 1)
+        fg = rs.randint(0, 256, (h, w, 3)).astype(np.uint8)
+        bg = rs.randint(0, 256, (h, w, 3)).astype(np.uint8)
+        s = va.video_sample(T(fg, torch.uint8), T(bg, torch.uint8), T(al, torch.float64),
+                            T(smooth_flow(h, w, seed=30 + i, amp=6.0).astype(np.float32)))
+        assert s["fg"].shape == (h, w, 4) and s["prev"].dtype == torch.uint8 and s["fg"].is_cuda
+        assert torch.equal(s["prev"][..., 3], (255.0 * T(al, torch.float64)).to(torch.uint8))
+        s["plan"] = vl.plan_crop((h, w), (h, w))
+        samples.append(s)
+    r = vl.compose_batch(samples, (64, 64), ("cmp", "bg", "label", "warped", "fg"))
+    vgg = synthetic_vgg16(0)
+    params = om.unet_simple_params(np.random.RandomState(1))
+    trn = VideoTrainer(vgg, "fp32", DEV, params=params)
+    loss = H(trn.step(r["cmp"], r["bg"], r["warped"], r["label"], r["fg"]))
+    torch.cuda.synchronize()
+    terms, alpha, _ = tr.train_step_grads(H(r["cmp"]), H(r["bg"]), H(r["warped"]), H(r["label"]), H(r["fg"]), vgg,
+                                          params)
+    np.testing.assert_allclose(loss, terms, rtol=1e-5)
+    assert np.abs(H(trn.output) - alpha).max() <= 1e-4
+    assert np.isfinite(loss).all() and loss[0] > 0
+
+
+def _syncbn_worker(rank, world, port, q):
+    import os
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    try:
+        from vmatting import parallel
+        from vmatting.train import VideoTrainer
+        from vmatting.weights import synthetic_vgg16
+        parallel.init_from_env(backend="gloo")
+        torch.cuda.set_device(0)
+        params = om.unet_simple_params(np.random.RandomState(1))
+        trn = VideoTrainer(synthetic_vgg16(0), "fp32", "cuda:0", params=params, sync_bn=True)
+        assert trn.sync_bn
+        cmp, bg, warped, gt, fg = (a[rank:rank + 1] for a in _batch(2, 48, 64, seed=13))
+        loss = trn.step(cmp, bg, warped, gt, fg).cpu().numpy()
+        torch.cuda.synchronize()
+        q.put((rank, loss, trn.grad.cpu().numpy(), None))
+    except Exception as e:  # report instead of hanging the parent
+        import traceback
+        q.put((rank, None, None, traceback.format_exc()[-1500:]))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def test_syncbn_two_replicas_match_one_replica_with_both_samples():
+    """SyncBN (VideoTrainer(sync_bn=True), unet_simple.py:25,41 over the global batch): two replicas with one sample
+    each (gloo, both on cuda:0) produce the gradient one replica computes on both samples (the DDP-averaged
+    gradient vs the single-device one) to f32 tolerance, and the mean of their losses is its loss."""
+    import multiprocessing as mp
+    import os
+    from vmatting.train import VideoTrainer
+    from vmatting.weights import synthetic_vgg16
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29650 + (os.getpid() % 40)
+    procs = [ctx.Process(target=_syncbn_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted((q.get(timeout=110) for _ in procs), key=lambda r: r[0])
+    for p in procs:
+        p.join(30)
+    assert all(r[3] is None for r in res), [r[3] for r in res]
+    params = om.unet_simple_params(np.random.RandomState(1))
+    ref = VideoTrainer(synthetic_vgg16(0), "fp32", DEV, params=params)
+    loss = H(ref.step(*_batch(2, 48, 64, seed=13)))
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(0.5 * (res[0][1] + res[1][1]), loss, rtol=2e-5)
+    g_ref = H(ref.grad)
+    np.testing.assert_array_equal(res[0][2], res[1][2])  # the all-reduced gradient is the same on both ranks
+    g = 0.5 * res[0][2].astype(np.float64)  # DDP averages the summed replica gradients
+    bad = []
+    for scope, kind, off, shape in ref.layout:
+        if kind == "b":  # conv biases: zero in exact arithmetic (BN removes them)
+            continue
+        n = int(np.prod(shape))
+        a, b = g[off:off + n], g_ref[off:off + n]
+        l2 = np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30)
+        if l2 > 1e-3:
+            bad.append((scope, kind, float(l2)))
+    assert not bad, bad

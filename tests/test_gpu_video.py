@@ -5,7 +5,8 @@ all-gather) over synthetic 1080p frames, checked frame by frame.
   graph-replayed, batched path changes nothing about a frame's arithmetic);
 * fp32: one sampled frame's alpha within 1e-4 max-abs of the numpy f32 oracle (north_star's bound), its logits
   within 1e-4 of their scale.
-World 1 here (the box has one GPU); the world-2 sharding / gather arithmetic is covered with gloo in test_host.py.
+World 1 here, plus world 2 as two processes sharing the one GPU over gloo (the real model, broadcast, graphs and
+the uneven gather); the sharding / gather arithmetic alone is covered with gloo on CPU in test_host.py.
 """
 
 import numpy as np
@@ -71,3 +72,65 @@ def test_video_batch_fp32_frame_vs_oracle(vgg0):
     assert err <= 1e-4
     lg = m.conv1_3[1].cpu().numpy()  # logits of the last chunk's frames (the model's buffer)
     assert np.abs(lg - r["conv1_3"][0]).max() <= 1e-4 * np.abs(r["conv1_3"]).max() + 1e-4
+
+
+def _world2_worker(rank, world, port, q, n_frames, h, w, chunk):
+    """One rank of the real frame-parallel path on the shared cuda:0 (gloo moves the device tensors): its own
+    init_conv draws, rank 0's packed weights broadcast into them, its uneven shard through video.matte_video (chunked
+    graph replay), the all-gather of the mattes; then every gathered matte against a standalone forward() with the
+    broadcast weights."""
+    import os
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    try:
+        from vmatting import parallel, unet, video
+        from vmatting.weights import synthetic_vgg16
+        parallel.init_from_env(backend="gloo")
+        torch.cuda.set_device(0)
+        np.random.seed(100 + rank)  # each rank draws different init_conv filters: the broadcast must replace them
+        model = unet.UNetVideo(synthetic_vgg16(0), dtype="bf16", device="cuda:0").prepare()
+        mine = torch.cat([t.reshape(-1).view(torch.uint8) for t in model.weights_flat()]).clone()
+        parallel.broadcast_tensors(model.weights_flat(), src=0)
+        flat = torch.cat([t.reshape(-1).view(torch.uint8) for t in model.weights_flat()])
+        a, b = video.shard(n_frames)
+        frames = video.synthetic_frames(b - a, h, w, first=a, device="cuda:0")
+        full, vm = video.matte_video(model, frames, n_frames, chunk=chunk)
+        torch.cuda.synchronize()
+        got = full.clone()
+        # replicas: identical weights after the broadcast (rank 1's own draws differed before it)
+        sums = [torch.empty(2, dtype=torch.float64) for _ in range(world)]
+        dist.all_gather(sums, torch.tensor([float(flat.double().sum()), float(mine.double().sum())],
+                                           dtype=torch.float64))
+        ok_w = all(float(s[0]) == float(sums[0][0]) for s in sums) and float(sums[1][1]) != float(sums[0][1])
+        ok_shape = tuple(got.shape) == (n_frames, h, w, 1)
+        allf = video.synthetic_frames(n_frames, h, w, first=0, device="cuda:0")
+        bad = [i for i in range(n_frames)
+               if not torch.equal(model.forward(allf[i:i + 1].clone())[0], got[i])]
+        q.put((rank, ok_w, ok_shape, bad, len(vm.spans)))
+    except Exception as e:  # report instead of hanging the parent
+        import traceback
+        q.put((rank, False, False, [repr(e), traceback.format_exc()[-800:]], 0))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def test_frame_parallel_world2_real_model():
+    """Config 4's product path at world 2 on the one GPU (two processes on cuda:0, gloo): rank-0 weight broadcast
+    into captured graphs, an uneven 4/3 split of 7 frames, graph replay on rank 1, the matte all-gather — every
+    gathered matte bit-equal to rank 0's standalone forward() of that frame (train.py:318-332's frame loop)."""
+    import multiprocessing as mp
+    import os
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29200 + (os.getpid() % 500)
+    procs = [ctx.Process(target=_world2_worker, args=(r, 2, port, q, 7, 270, 480, 2)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=110) for _ in procs)
+    for p in procs:
+        p.join(30)
+    assert [r[0] for r in res] == [0, 1], res
+    for rank, ok_w, ok_shape, bad, spans in res:
+        assert ok_w and ok_shape and bad == [], (rank, ok_w, ok_shape, bad)
+    assert [r[4] for r in res] == [2, 2]  # 4 frames -> 2 chunks of 2; 3 frames -> 2 + 1

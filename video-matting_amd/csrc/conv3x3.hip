@@ -1587,8 +1587,9 @@ __global__ __launch_bounds__(512) void conv3x3_first(ConvArgs a) {
 // 531 MB 1080p output is never re-read by this pass).
 // STG: each wave transposes its 16 pixels x 64 channels through a private LDS slab so that every store instruction
 // writes 4 whole pixels (1 KB contiguous when the output is dense) instead of 16 pixels x 64 bytes.
-template <bool NT, bool STG = false>
-__global__ __launch_bounds__(512, 2) void conv3x3_first_softmax(ConvArgs a) {
+// WL: the weight fragments staged once per block in LDS instead of 48 registers (4 waves per SIMD without spills)
+template <bool NT, bool STG = false, bool WL = false>
+__global__ __launch_bounds__(512, WL ? 4 : 2) void conv3x3_first_softmax(ConvArgs a) {
   using T = uint16_t;
   constexpr int TH = 8, TW = 32, PW = TW + 2, PPIX = (TH + 2) * PW;
   constexpr int SRF = 68;  // staging row: 64 floats + 4 (rows 272 B apart)
@@ -1616,13 +1617,22 @@ __global__ __launch_bounds__(512, 2) void conv3x3_first_softmax(ConvArgs a) {
   };
   const int col = lane & 15, q = lane >> 4;
   const __amdgpu_buffer_rsrc_t wrs = w_rsrc<T>(a, 0);
-  uint4 wf[3][4];
+  __shared__ __attribute__((aligned(16))) uint4 wlds[WL ? 3 * 4 * 64 : 1];
+  uint4 wf[WL ? 1 : 3][4];
+  if constexpr (WL) {
+    for (int e = tid; e < 3 * 4 * 64; e += 512) {  // [j][fc][lane]
+      const int j = e >> 8, fc = (e >> 6) & 3, l = e & 63;
+      wlds[e] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
+                                              wrs, ((fc * 16 + (l & 15)) * a.K_pad + j * 32 + (l >> 4) * 8) * 2, 0, 0));
+    }
+  } else {
 #pragma unroll
-  for (int j = 0; j < 3; ++j)
+    for (int j = 0; j < 3; ++j)
 #pragma unroll
-    for (int fc = 0; fc < 4; ++fc)
-      wf[j][fc] = __builtin_bit_cast(
-          uint4, __builtin_amdgcn_raw_buffer_load_b128(wrs, ((fc * 16 + col) * a.K_pad + j * 32 + q * 8) * 2, 0, 0));
+      for (int fc = 0; fc < 4; ++fc)
+        wf[j][fc] = __builtin_bit_cast(
+            uint4, __builtin_amdgcn_raw_buffer_load_b128(wrs, ((fc * 16 + col) * a.K_pad + j * 32 + q * 8) * 2, 0, 0));
+  }
   if (tid < 64) {  // constants in LDS (read per tile): 2 blocks per CU fit the register file
     const float sc = a.scale ? a.scale[tid] : 1.f;
     rmul[tid] = sc;
@@ -1655,9 +1665,11 @@ __global__ __launch_bounds__(512, 2) void conv3x3_first_softmax(ConvArgs a) {
         bv[fp] = tap < 9 ? v : make_uint4(0, 0, 0, 0);
       }
 #pragma unroll
-      for (int fc = 0; fc < 4; ++fc)
+      for (int fc = 0; fc < 4; ++fc) {
+        const uint4 wv = WL ? wlds[(j * 4 + fc) * 64 + lane] : wf[WL ? 0 : j][fc];
 #pragma unroll
-        for (int fp = 0; fp < 2; ++fp) mma16<T>(wf[j][fc], bv[fp], acc[fc][fp]);
+        for (int fp = 0; fp < 2; ++fp) mma16<T>(wv, bv[fp], acc[fc][fp]);
+      }
     }
 
     const int ycs = a.y_cstride;
@@ -1725,6 +1737,157 @@ __global__ __launch_bounds__(512, 2) void conv3x3_first_softmax(ConvArgs a) {
           }
         }
       }
+    }
+  }
+}
+
+// ================================================================ refine conv4 + softmax in f32 (refine.py:27-32)
+// The reference's precision for config 3: f32 input row [cmp, alpha, warped] (CIN <= 8 of an 8-channel pixel), exact
+// f32 products on v_mfma_f32_16x16x4_f32, f32 sums, f32 softmax.  K is COMPACT: k = tap * CIN + c over the 9 * CIN
+// real taps (45 for the refine's CIN 5 -> 12 four-deep MFMA steps instead of the 18 of the padded 72); the lane in
+// k-slot q of step s reads tap (4s+q) / CIN, channel (4s+q) % CIN.  The patch lives in LDS as channel planes, so the
+// 16 lanes of a k-slot read 16 consecutive pixels (conflict-free).  The weights and the per-lane patch offsets are
+// staged once per block in LDS ([step][lane] records: one ds_read_b128 of the 4 cout fragments + one offset per
+// step), which keeps the kernel at 4 waves per SIMD (2 blocks per CU) without spilling.  Softmax + per-wave LDS
+// transpose + whole-pixel nontemporal stores as in conv3x3_first_softmax.  Per 8 x 32 tile a wave issues NS x 8
+// MFMAs (32 cycles each): at NS = 12 the chip's f32 matrix time for a 1080p frame (~80 us) is on par with its 531 MB
+// of f32 output at HBM speed.
+template <int CIN>
+__global__ __launch_bounds__(512, 4) void conv3x3_first_softmax_f32(ConvArgs a) {
+  constexpr int NS = (9 * CIN + 3) / 4;
+  constexpr int TH = 8, TW = 32, PW = TW + 2, PPIX = (TH + 2) * PW;
+  constexpr int SRF = 68;  // staging row: 64 floats + 4
+  constexpr int ZERO = CIN * PPIX;  // a zero slot: k >= 9 * CIN reads it
+  __shared__ __attribute__((aligned(16))) float patch[CIN * PPIX + 4];
+  __shared__ __attribute__((aligned(16))) float stg[8 * 16 * SRF];
+  __shared__ __attribute__((aligned(16))) f32x4 wl[NS * 64];
+  __shared__ int pl[NS * 4];
+  __shared__ __attribute__((aligned(16))) float rmul[2 * 64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int H = a.H, W = a.W, cs = a.x_cstride;
+  const int th = (H + TH - 1) / TH, tw = (W + TW - 1) / TW;
+  const int ntiles = a.tiles_total;
+  auto tile_of = [&](int i) {
+    const int base = (i / a.tiles_n) * a.tiles_n;
+    return base + a.tiles_n <= ntiles ? base + xcd_tile(i - base, a.tiles_n) : i;
+  };
+  auto load_patch = [&](int t, float4& lo, float4& hi) {
+    const int n = t / (th * tw), srem = t - n * th * tw;
+    const int r0 = (srem / tw) * TH, c0 = (srem - (srem / tw) * tw) * TW;
+    const int pr = tid / PW, pc = tid - pr * PW;
+    const int h = r0 - 1 + pr, w = c0 - 1 + pc;
+    const bool ok = tid < PPIX && (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
+    const float* xp = reinterpret_cast<const float*>(a.x) + a.x_coff + ((long)n * H + (ok ? h : 0)) * (long)W * cs +
+                      (long)(ok ? w : 0) * cs;
+    lo = ok ? *reinterpret_cast<const float4*>(xp) : make_float4(0.f, 0.f, 0.f, 0.f);
+    hi = ok && CIN > 4 ? *reinterpret_cast<const float4*>(xp + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+  };
+  const int col = lane & 15, q = lane >> 4;
+  const float* Wt = reinterpret_cast<const float*>(a.w);
+  for (int e = tid; e < NS * 64; e += 512) {  // wl[s][l] = the 4 cout fragments of lane l's (tap, c) at step s
+    const int st = e >> 6, l = e & 63;
+    const int kk = 4 * st + (l >> 4), co = l & 15;
+    const int tap = kk / CIN, c = kk - tap * CIN;
+    f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (kk < 9 * CIN)
+#pragma unroll
+      for (int fc = 0; fc < 4; ++fc) v[fc] = Wt[(long)(fc * 16 + co) * a.K_pad + tap * 8 + c];
+    wl[e] = v;
+  }
+  if (tid < NS * 4) {
+    const int kk = tid;  // step tid / 4, k-slot tid % 4
+    const int tap = kk / CIN, c = kk - tap * CIN;
+    pl[tid] = kk < 9 * CIN ? c * PPIX + (tap / 3) * PW + tap % 3 : -1;
+  }
+  if (tid < 4) patch[ZERO + tid] = 0.f;
+  if (tid < 64) {
+    const float sc = a.scale ? a.scale[tid] : 1.f;
+    rmul[tid] = sc;
+    rmul[64 + tid] = (a.bias ? a.bias[tid] : 0.f) * sc + (a.shift ? a.shift[tid] : 0.f);
+  }
+  int i = blockIdx.x;
+  float4 nlo = make_float4(0.f, 0.f, 0.f, 0.f), nhi = nlo;
+  if (i < ntiles) load_patch(tile_of(i), nlo, nhi);
+  for (; i < ntiles; i += gridDim.x) {
+    const int t = tile_of(i);
+    const int n = t / (th * tw), srem = t - n * th * tw;
+    const int r0 = (srem / tw) * TH, c0 = (srem - (srem / tw) * tw) * TW;
+    __syncthreads();  // the previous tile's patch reads are done (first tile: the staged tables are written)
+    if (tid < PPIX) {
+      const float v[8] = {nlo.x, nlo.y, nlo.z, nlo.w, nhi.x, nhi.y, nhi.z, nhi.w};
+#pragma unroll
+      for (int c = 0; c < CIN; ++c) patch[c * PPIX + tid] = v[c];
+    }
+    __syncthreads();
+    if (i + (int)gridDim.x < ntiles) load_patch(tile_of(i + gridDim.x), nlo, nhi);
+
+    f32x4 acc[4][2];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int fp = 0; fp < 2; ++fp) acc[k][fp] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int prow = wave * PW + col;  // patch row `wave` (+ the tap's kernel row in the offset)
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const f32x4 w4 = wl[s * 64 + lane];
+      const int po = pl[s * 4 + q];
+      const float b0 = patch[po < 0 ? ZERO : po + prow], b1 = patch[po < 0 ? ZERO : po + prow + 16];
+#pragma unroll
+      for (int fc = 0; fc < 4; ++fc) {
+        acc[fc][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(w4[fc], b0, acc[fc][0], 0, 0, 0);
+        acc[fc][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(w4[fc], b1, acc[fc][1], 0, 0, 0);
+      }
+    }
+
+    const int ycs = a.y_cstride;
+    float* yb = reinterpret_cast<float*>(a.y) + a.y_coff + (((long)n * H + r0 + wave) * W + c0) * (long)ycs;
+#pragma unroll
+    for (int fp = 0; fp < 2; ++fp) {
+      float v[4][4];
+      float mx = -INFINITY;
+#pragma unroll
+      for (int fc = 0; fc < 4; ++fc) {
+        const float4 m4 = *reinterpret_cast<const float4*>(rmul + fc * 16 + 4 * q);
+        const float4 a4 = *reinterpret_cast<const float4*>(rmul + 64 + fc * 16 + 4 * q);
+        const float mul[4] = {m4.x, m4.y, m4.z, m4.w}, add[4] = {a4.x, a4.y, a4.z, a4.w};
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          v[fc][jj] = fmaf(acc[fc][fp][jj], mul[jj], add[jj]);
+          mx = fmaxf(mx, v[fc][jj]);
+        }
+      }
+      mx = fmaxf(mx, __shfl_xor(mx, 16));
+      mx = fmaxf(mx, __shfl_xor(mx, 32));
+      float sum = 0.f;
+#pragma unroll
+      for (int fc = 0; fc < 4; ++fc)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          v[fc][jj] = expf(v[fc][jj] - mx);
+          sum += v[fc][jj];
+        }
+      sum += __shfl_xor(sum, 16);
+      sum += __shfl_xor(sum, 32);
+      const float inv = 1.f / sum;
+      float* ws = stg + wave * 16 * SRF;
+#pragma unroll
+      for (int fc = 0; fc < 4; ++fc)
+        *reinterpret_cast<f32x4*>(ws + col * SRF + fc * 16 + 4 * q) =
+            f32x4{v[fc][0] * inv, v[fc][1] * inv, v[fc][2] * inv, v[fc][3] * inv};
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+      for (int it = 0; it < 4; ++it) {  // lane l: pixel 4*it + l/16, channels 4*(l%16) .. +3
+        const int px = 4 * it + (lane >> 4), ch = 4 * (lane & 15);
+        const f32x4 o = *reinterpret_cast<const f32x4*>(ws + px * SRF + ch);
+        const int pc = fp * 16 + px;
+        if (r0 + wave < H && c0 + pc < W)
+          __builtin_nontemporal_store(o, reinterpret_cast<f32x4*>(yb + (long)pc * ycs + ch));
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
   }
 }
@@ -2593,12 +2756,16 @@ static long g_glds_rb = 128;
 static long g_head_kernel = 0;
 static long g_head_th = 16;  // conv3x3_head_mfma tile height for the bf16 128-channel head (8 or 16)
 static long g_patch_cfg = 0;
+#ifdef VM_STUDY
 static long g_patch_rowslot = 1;  // 0 = the per-tap-barrier dispatch of r01 (A/B runs)
 static long g_patch_ablate = 0;
+#endif
 static long g_rows_kernel = 1;        // conv_rows.hip: 0 = off, 1 = auto (grid size), 8 / 16 = forced tile height
 static long g_rows_min_blocks = 900;
 static long g_rows_up = 0;            // 1: the folded upconvs too
 static long g_rows_min_cin = 256;      // short K loops: the 2-blocks-per-CU patch kernel hides prologue/epilogue better
+static long g_src_span_limit = 0x7ffffff0L;  // split-source byte span the 32-bit offset kernels take (option
+                                              // "src_span_limit" lowers it for the fallback tests)
 static long g_pair_kernel = 0;  // vm_conv3x3_pair_first_nhwc: 0 = persistent weights-resident kernel when cout == 64,
                                 // 1 = streaming patch kernel
 
@@ -2620,6 +2787,7 @@ static int dispatch_patch(ConvArgs& a, hipStream_t st) {
                        a.cout, a.bias, a.scale, a.shift, a.act, a.y, a.y_dtype, a.y_cstride, a.y_coff);
     return check_launch("splitk_reduce");
   }
+#ifdef VM_STUDY
   switch (g_patch_ablate) {  // timing experiments on the default tiling (results are garbage)
     case 1: return launch_patch<64, 8, 1, 6, 8, 1, 9, false, 1>(a, st);
     case 2: return launch_patch<64, 8, 1, 6, 8, 1, 9, false, 2>(a, st);
@@ -2639,7 +2807,15 @@ static int dispatch_patch(ConvArgs& a, hipStream_t st) {
     case 22: return launch_patch<64, 8, 1, 2, 8, 2, 9, false, 16, false, 3>(a, st);
     default: break;
   }
+#endif
   switch (g_patch_cfg) {
+    // the tilings the dispatcher below picks (the only ones in the shipped library)
+    case 19: return launch_patch<64, 8, 1, 3, 8, 1, 9, false, 0, false, 3>(a, st);
+    case 22: return launch_patch<64, 8, 1, 2, 8, 1, 9, false, 0, false, 3>(a, st);
+    case 25: return launch_patch<64, 4, 1, 2, 4, 2, 9, false, 0, false, 3>(a, st);
+    case 30: return launch_patch<128, 4, 2, 3, 8, 2>(a, st);
+#ifdef VM_STUDY
+    // study build only (make study): every tiling of the r01/r02 sweeps (scripts/sweep.sh, scripts/conv_study.sh)
     case 1: return launch_patch<64, 4, 1, 6>(a, st);
     case 2: return launch_patch<128, 2, 2, 6>(a, st);
     case 3: return launch_patch<128, 4, 2, 4>(a, st);
@@ -2660,13 +2836,10 @@ static int dispatch_patch(ConvArgs& a, hipStream_t st) {
     case 17: return launch_patch<128, 8, 1, 4, 16>(a, st);
     case 18: return launch_patch<128, 4, 2, 4, 16>(a, st);
     // one barrier per kernel row (3 taps per ring slot), tap g+1's fragments read under tap g's MFMAs
-    case 19: return launch_patch<64, 8, 1, 3, 8, 1, 9, false, 0, false, 3>(a, st);
     case 20: return launch_patch<64, 4, 1, 3, 8, 2, 9, false, 0, false, 3>(a, st);
     case 21: return launch_patch<128, 4, 1, 2, 4, 2, 9, false, 0, false, 3>(a, st);
-    case 22: return launch_patch<64, 8, 1, 2, 8, 1, 9, false, 0, false, 3>(a, st);
     case 23: return launch_patch<128, 8, 1, 2, 8, 1, 9, false, 0, false, 3>(a, st);
     case 24: return launch_patch<128, 4, 2, 2, 8, 1, 9, false, 0, false, 3>(a, st);
-    case 25: return launch_patch<64, 4, 1, 2, 4, 2, 9, false, 0, false, 3>(a, st);
     // one 8 x 32 px patch shared by 256 output channels (8 waves of 64 px x 128 channels, one block per CU)
     case 26: return launch_patch<256, 4, 2, 2, 8, 1, 9, false, 0, false, 3>(a, st);
     // 64 px x 64 channel wave tiles, 4 waves (two 256 px x 64 channel blocks per CU)
@@ -2674,9 +2847,9 @@ static int dispatch_patch(ConvArgs& a, hipStream_t st) {
     // 16 x 32 px tiles on 16 waves of 32 px x 64 channels (1024 threads, one block per CU): half the weight DMA per MFMA
     case 28: return launch_patch<64, 16, 1, 2, 16, 1, 9, false, 0, false, 3>(a, st);
     case 29: return launch_patch<64, 16, 1, 3, 16, 1, 9, false, 0, false, 3>(a, st);
-    // 64 px x 64 channel wave tiles at 4 waves per SIMD (8 waves of 256 px x 128 channels, two blocks per CU)
-    case 30: return launch_patch<128, 4, 2, 3, 8, 2>(a, st);
+    // 64 px x 64 channel wave tiles at 4 waves per SIMD, 4-slot ring
     case 31: return launch_patch<128, 4, 2, 4, 8, 2>(a, st);
+#endif
     default: break;
   }
   // row-stationary kernel (conv_rows.hip) on grids of >= g_rows_min_blocks 16 x 32 px x 64 channel blocks (one block
@@ -2699,12 +2872,14 @@ static int dispatch_patch(ConvArgs& a, hipStream_t st) {
   const long N = a.M / ((long)a.H * a.W);
   const long sp = N * ((a.H + 7) / 8) * ((a.W + 31) / 32);
   const long blocks64 = sp * ((a.cout + 63) / 64);
+#ifdef VM_STUDY
   if (!g_patch_rowslot) {
     if (a.cout >= 128 && a.cin_pad >= 256 && sp * ((a.cout + 127) / 128) >= 1000)
       return launch_patch<128, 4, 1, 4, 8, 2>(a, st);
     if (blocks64 < 512) return launch_patch<64, 4, 1, 6, 4>(a, st);
     return launch_patch<64, 8, 1, 6>(a, st);
   }
+#endif
   if (a.cout >= 128 && a.cin_pad >= 512 && sp * ((a.cout + 127) / 128) >= 1000)
     return launch_patch<128, 4, 2, 3, 8, 2>(a, st);  // 64 px x 64 channel waves, 4 per SIMD (r02: -5% vs 4x1 waves)
   if (blocks64 >= 8000) return launch_patch<64, 8, 1, 3, 8, 1, 9, false, 0, false, 3>(a, st);
@@ -2755,6 +2930,9 @@ static int launch_first_softmax(ConvArgs& a, hipStream_t st) {
   } else if (g_softmax_kernel == 4) {
     snprintf(g_last_kernel, sizeof g_last_kernel, "vm::conv3x3_first_softmax<true, true>");
     hipLaunchKernelGGL((conv3x3_first_softmax<true, true>), dim3(grid), dim3(512), 0, st, a);
+  } else if (g_softmax_kernel == 5) {
+    snprintf(g_last_kernel, sizeof g_last_kernel, "vm::conv3x3_first_softmax<true, true, true>");
+    hipLaunchKernelGGL((conv3x3_first_softmax<true, true, true>), dim3(grid), dim3(512), 0, st, a);
   } else if (g_softmax_kernel == 2) {
     snprintf(g_last_kernel, sizeof g_last_kernel, "vm::conv3x3_first_softmax<true>");
     hipLaunchKernelGGL(conv3x3_first_softmax<true>, dim3(grid), dim3(512), 0, st, a);
@@ -2765,8 +2943,34 @@ static int launch_first_softmax(ConvArgs& a, hipStream_t st) {
   return check_launch("conv3x3_first_softmax");
 }
 
+static int launch_first_softmax_f32(ConvArgs& a, int cin, hipStream_t st) {
+  const long N = a.M / ((long)a.H * a.W);
+  const long sp = N * ((a.H + 7) / 8) * ((a.W + 31) / 32);
+  if (sp > 0x7fffffffL) return fail(VM_EUNSUPPORTED, "conv3x3: too many tiles");
+  a.tiles_total = (int)sp;
+  const int grid = (int)std::min<long>(sp, g_softmax_blocks);
+  a.tiles_n = grid;
+#define VM_SMF(C)                                                                            \
+  case C:                                                                                   \
+    snprintf(g_last_kernel, sizeof g_last_kernel, "vm::conv3x3_first_softmax_f32<%d>", C); \
+    hipLaunchKernelGGL(conv3x3_first_softmax_f32<C>, dim3(grid), dim3(512), 0, st, a);      \
+    break;
+  switch (cin) {
+    VM_SMF(1) VM_SMF(2) VM_SMF(3) VM_SMF(4) VM_SMF(5) VM_SMF(6) VM_SMF(7) VM_SMF(8)
+    default: return fail(VM_EINVAL, "conv3x3_first_softmax_f32: cin %d", cin);
+  }
+#undef VM_SMF
+  return check_launch("conv3x3_first_softmax_f32");
+}
+
 template <typename T>
-static int dispatch_mfma(ConvArgs& a, hipStream_t st) {
+static int dispatch_mfma(ConvArgs& a, hipStream_t st, int cin = 0) {
+  // f32 refine conv + softmax (cin <= 8 of a 16-byte-aligned 8-float pixel, 64 outputs, f32 out)
+  if (sizeof(T) == 4 && g_softmax_kernel != 0 && g_conv_kernel != 1 && g_conv_kernel != 2 && cin > 0 && cin <= 8 &&
+      a.cin_pad == 8 && !a.chunk_major && a.x_src_c <= 0 && a.y_dtype == VM_F32 && a.y_vec && a.act == VM_ACT_SOFTMAX &&
+      a.cout == 64 && a.K_pad == 96 && a.x_cstride % 4 == 0 && a.x_coff % 4 == 0 &&
+      reinterpret_cast<uintptr_t>(a.x) % 16 == 0)
+    return launch_first_softmax_f32(a, cin, st);
   if (sizeof(T) == 2 && g_softmax_kernel != 0 && g_conv_kernel != 1 && g_conv_kernel != 2 && a.cin_pad == 8 &&
       !a.chunk_major && a.x_src_c <= 0 && a.y_dtype == VM_F32 && a.y_vec && a.act == VM_ACT_SOFTMAX && a.cout == 64 &&
       a.K_pad == 128)
@@ -2800,7 +3004,7 @@ extern "C" int vm_set_option(const char* key, long value) {
     return VM_OK;
   }
   if (!strcmp(key, "softmax_kernel")) {
-    if (value < 0 || value > 4) return fail(VM_EINVAL, "softmax_kernel must be 0..4");
+    if (value < 0 || value > 5) return fail(VM_EINVAL, "softmax_kernel must be 0..5");
     g_softmax_kernel = value;
     return VM_OK;
   }
@@ -2831,6 +3035,11 @@ extern "C" int vm_set_option(const char* key, long value) {
     g_rows_min_blocks = value;
     return VM_OK;
   }
+  if (!strcmp(key, "src_span_limit")) {
+    if (value < 1 || value > 0x7ffffff0L) return fail(VM_EINVAL, "src_span_limit must be 1..0x7ffffff0");
+    g_src_span_limit = value;
+    return VM_OK;
+  }
   if (!strcmp(key, "thin_blocks")) {
     g_thin_blocks = value;
     return VM_OK;
@@ -2849,13 +3058,19 @@ extern "C" int vm_set_option(const char* key, long value) {
     g_conv_min_tiles = value;
     return VM_OK;
   }
-  if (!strcmp(key, "patch_ablate")) {
-    g_patch_ablate = value;
+  if (!strcmp(key, "patch_cfg")) {
+#ifdef VM_STUDY
+    if (value < 0 || value > 31) return fail(VM_EINVAL, "patch_cfg must be 0..31");
+#else
+    if (value != 0 && value != 19 && value != 22 && value != 25 && value != 30)
+      return fail(VM_EINVAL, "patch_cfg must be 0, 19, 22, 25 or 30 (other tilings: the study build, make study)");
+#endif
+    g_patch_cfg = value;
     return VM_OK;
   }
-  if (!strcmp(key, "patch_cfg")) {
-    if (value < 0 || value > 31) return fail(VM_EINVAL, "patch_cfg must be 0..31");
-    g_patch_cfg = value;
+#ifdef VM_STUDY
+  if (!strcmp(key, "patch_ablate")) {  // timing-only ablations: garbage results
+    g_patch_ablate = value;
     return VM_OK;
   }
   if (!strcmp(key, "patch_rowslot")) {
@@ -2863,13 +3078,18 @@ extern "C" int vm_set_option(const char* key, long value) {
     g_patch_rowslot = value;
     return VM_OK;
   }
+#endif
   if (!strcmp(key, "pair_xin_wide")) {
     if (value < 0 || value > 1) return fail(VM_EINVAL, "pair_xin_wide must be 0 or 1");
     g_pair_xin_wide = value;
     return VM_OK;
   }
   if (!strcmp(key, "pair_kernel")) {
+#ifdef VM_STUDY
     if (value < 0 || (value > 1 && value < 10) || value > 18) return fail(VM_EINVAL, "pair_kernel must be 0, 1 or 10..18");
+#else
+    if (value < 0 || value > 1) return fail(VM_EINVAL, "pair_kernel must be 0 or 1 (ablations: the study build)");
+#endif
     g_pair_kernel = value;
     return VM_OK;
   }
@@ -3112,14 +3332,17 @@ static int pair_first_impl(const vm_tensor* x, const void* packed1, int cin1, co
     return launch_pair_persist<0>(a, sp, st);
   }
   if (cout2 == 64 && (g_pair_kernel == 0 || g_pair_kernel >= 10) && sp <= 0x7fffffffL) {
-    switch (g_pair_kernel) {  // >= 10: timing ablations (garbage results)
+#ifdef VM_STUDY
+    switch (g_pair_kernel) {  // >= 10: timing ablations (garbage results), study build only
       case 11: return launch_pair_persist<1>(a, sp, st);
       case 12: return launch_pair_persist<2>(a, sp, st);
       case 14: return launch_pair_persist<4>(a, sp, st);
       case 18: return launch_pair_persist<8>(a, sp, st);
       case 13: return launch_pair_persist<3>(a, sp, st);
-      default: return launch_pair_persist<0>(a, sp, st);
+      default: break;
     }
+#endif
+    return launch_pair_persist<0>(a, sp, st);
   }
   if (sp * ((cout2 + 63) / 64) < 512) return launch_patch<64, 4, 1, 6, 4, 1, 9, false, 0, true>(a, st);
   return launch_patch<64, 8, 1, 6, 8, 1, 9, false, 0, true>(a, st);
@@ -3249,6 +3472,15 @@ static int conv_impl(const vm_tensor* x, const void* packed, int cin, int cout, 
     }
     return dispatch_thin(a, x->n, st);
   }
+  if (nsrc > 1) {
+    // the patch / row-stationary / generic kernels add source s's offset (s * src_stride elements) into 32-bit
+    // byte offsets inside one image's buffer resource: the whole span must stay below it (the thin kernel above
+    // forms 64-bit source pointers).  Callers materialise the concat instead (ops.conv3x3)
+    const long span = ((long)(nsrc - 1) * src_stride + (long)x->h * x->w * x->cstride) * elem_bytes(dt);
+    if (span >= g_src_span_limit)
+      return fail(VM_EUNSUPPORTED, "conv3x3: split sources span %ld bytes (limit %ld): materialise the concat", span,
+                  g_src_span_limit);
+  }
   if (dt == VM_BF16 && work && g_conv_kernel == 0 && patch_ok(a, 2) && (cout & 3) == 0) {
     const int ks = splitk_plan(x->n, x->h, x->w, a.cin_pad, cout);
     if (ks > 1 && work_bytes >= (size_t)ks * M * cout * sizeof(float)) {
@@ -3258,7 +3490,7 @@ static int conv_impl(const vm_tensor* x, const void* packed, int cin, int cout, 
     }
   }
   if (dt == VM_BF16) return dispatch_mfma<uint16_t>(a, st);
-  return dispatch_mfma<float>(a, st);
+  return dispatch_mfma<float>(a, st, cin);
 }
 
 // workspace of vm_conv3x3_ex_nhwc: the split-K partial sums of a small-grid bf16 conv, else 0

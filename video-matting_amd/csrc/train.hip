@@ -180,14 +180,15 @@ static void launch_bn_bwd_partial(const V& x, const V& dy, const V& y, const flo
 // elementwise passes over [M pixels x C channels]: CP (power of two >= C, at most 64) lanes per pixel, channel
 // block blockIdx.y, so a lane keeps one channel (its per-channel constants in registers) and no element index is
 // ever divided
+// count > 0: the sums are over `count` pixels (SyncBN: all replicas' pixels), else over this view's M
 template <bool MASK, int CP>
 __global__ __launch_bounds__(256) void bn_bwd_apply(V x, V dy, V y, const float* mean, const float* var,
                                                     const float* gamma, float eps, const float* sum_g,
-                                                    const float* sum_gx, V dx, V dx2) {
+                                                    const float* sum_gx, V dx, V dx2, long count = 0) {
   const long M = (long)dy.n * dy.h * dy.w;
   const int c = blockIdx.y * CP + (threadIdx.x & (CP - 1));
   if (c >= dy.c) return;
-  const float invM = 1.0f / (float)M;
+  const float invM = 1.0f / (float)(count > 0 ? count : M);
   const float r = 1.0f / sqrtf(var[c] + eps);
   const float m = mean[c];
   const float k = (gamma ? gamma[c] : 1.f) * r;
@@ -996,6 +997,29 @@ extern "C" int vm_bn_backward_ex_nhwc(const vm_tensor* x, const vm_tensor* dy, c
                             sgx, dxv, dx2v);                                                                          \
   else hipLaunchKernelGGL((bn_bwd_apply<false, CP>), grid, dim3(256), 0, st, xv, dyv, yv, mean, var, gamma, eps, sg,  \
                           sgx, dxv, dx2v)
+  VM_CP_SWITCH(cp, VM_BNA)
+#undef VM_BNA
+  return check_launch("bn_backward_apply");
+}
+
+extern "C" int vm_bn_backward_apply_nhwc(const vm_tensor* x, const vm_tensor* dy, const vm_tensor* y,
+                                         const float* mean, const float* var, const float* gamma, float eps,
+                                         const float* sum_g, const float* sum_gx, long count, vm_tensor* dx,
+                                         vm_tensor* dx2, void* stream) {
+  if (!ok_view(x) || !ok_view(dy) || dy->dtype != VM_F32 || !same_shape(x, dy) || !mean || !var || !sum_g ||
+      !sum_gx || count <= 0 || !dx || !ok_view(dx) || !same_shape(dx, dy) || dx->dtype != VM_F32 ||
+      (y && (!ok_view(y) || !same_shape(y, dy))) || (dx2 && (!ok_view(dx2) || !same_shape(dx2, dy))))
+    return fail(VM_EINVAL, "bn_backward_apply: bad argument");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const long M = (long)dy->n * dy->h * dy->w;
+  const V xv = mk(x), dyv = mk(dy), yv = y ? mk(y) : V{}, dxv = mk(dx), dx2v = dx2 ? mk(dx2) : V{};
+  const int cp = lanes_for(dy->c);
+  const dim3 grid = lanes_grid(M, dy->c, cp);
+#define VM_BNA(CP)                                                                                                    \
+  if (y) hipLaunchKernelGGL((bn_bwd_apply<true, CP>), grid, dim3(256), 0, st, xv, dyv, yv, mean, var, gamma, eps,     \
+                            sum_g, sum_gx, dxv, dx2v, count);                                                         \
+  else hipLaunchKernelGGL((bn_bwd_apply<false, CP>), grid, dim3(256), 0, st, xv, dyv, yv, mean, var, gamma, eps,      \
+                          sum_g, sum_gx, dxv, dx2v, count)
   VM_CP_SWITCH(cp, VM_BNA)
 #undef VM_BNA
   return check_launch("bn_backward_apply");

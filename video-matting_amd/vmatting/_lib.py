@@ -125,6 +125,8 @@ SIGNATURES = [
                                     c_void_p]),
     ("vm_bn_backward_ex_nhwc", c_int, [P, P, P, c_void_p, c_void_p, c_void_p, c_float, P, P, c_void_p, c_void_p,
                                        c_void_p, c_void_p, c_void_p]),
+    ("vm_bn_backward_apply_nhwc", c_int, [P, P, P, c_void_p, c_void_p, c_void_p, c_float, c_void_p, c_void_p, c_long,
+                                          P, P, c_void_p]),
     ("vm_relu_backward_nhwc", c_int, [P, P, P, c_void_p]),
     ("vm_relu_backward_ex_nhwc", c_int, [P, P, P, P, c_void_p]),
     ("vm_resize_bilinear_tf1_backward", c_int, [P, c_void_p, c_int, c_int, c_void_p]),

@@ -142,3 +142,22 @@ def augment(fg, bg, alpha):
     new_fg = ops.change_illumination(new_fg, lut)
     new_bg = ops.change_illumination(new_bg, lut)
     return _out(new_fg, fg), _out(new_bg, bg), _out(new_alpha, alpha)
+
+
+def bgra(fg, alpha):
+    """The BGRA image augmentation.augmentation writes for a (fg, alpha) pair (augmentation.py:152-153,163-164):
+    concat(fg u8, (255. * alpha).astype(uint8)) — on the device for device tensors (float64 product, truncation)."""
+    dfg, dal = _device(fg), _device(alpha)
+    a8 = (255.0 * dal.to(torch.float64)).to(torch.uint8)
+    return _out(torch.cat([dfg, a8.reshape(dal.shape[0], dal.shape[1], 1)], 2), fg)
+
+
+def video_sample(fg, bg, alpha, flow):
+    """One training entry of loader.video_batch made in memory the way augmentation.augmentation makes it on disk
+    (augmentation.py:141-168): frame t-1 = the reference BGRA (fg + alpha), frame t = augment(fg, bg, alpha) as
+    BGRA with its augmented background.  ``flow`` is the entry's .flo (the reference computes it offline with an
+    optical-flow estimator between the two frames; any [h, w, 2] f32).  Returns the dict loader.compose_batch takes
+    (fg, bg, prev, flow; add "plan" = loader.plan_crop(...)), all on the device."""
+    nfg, nbg, nal = augment(_device(fg), _device(bg), _device(alpha))
+    return {"fg": bgra(nfg, nal), "bg": nbg, "prev": bgra(_device(fg), _device(alpha)), "flow": _device(flow)}
+

@@ -46,7 +46,7 @@ class BatchNorm:
 
 def conv_bn(x, pc, bn, phase, act, out):
     """new_conv (conv + bias -> BN) followed by ``act`` (unet_simple.py:19-27 + the relu at the call site)."""
-    if not phase:
-        return ops.conv3x3(x, pc, act, out=out, affine=(bn.inf_scale, bn.inf_shift), splitk=True)
+    if not phase:  # inference: no split-K, so a frame's result does not depend on its batch (ops.conv3x3)
+        return ops.conv3x3(x, pc, act, out=out, affine=(bn.inf_scale, bn.inf_shift))
     ops.conv3x3(x, pc, "none", out=out, affine=False, splitk=True)
     return bn(out, True, act)

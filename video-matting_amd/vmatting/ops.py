@@ -213,9 +213,17 @@ def conv3x3(x, pc, act="none", out=None, out_dtype=None, affine=None, pool_out=N
             ev0 = torch.cuda.Event(enable_timing=True)
             ev1 = torch.cuda.Event(enable_timing=True)
             ev0.record()
-        check(lib().vm_conv3x3_ex_nhwc(ctypes.byref(xv), nsrc, stride, _ptr(pc.packed), pc.cin, pc.cout,
-                                       _ptr(pc.bias), _ptr(scale), _ptr(shift), _lib.ACT[act], ctypes.byref(yv),
-                                       _ptr(ws), wsz, stream_handle()), "conv3x3")
+        rc = lib().vm_conv3x3_ex_nhwc(ctypes.byref(xv), nsrc, stride, _ptr(pc.packed), pc.cin, pc.cout,
+                                      _ptr(pc.bias), _ptr(scale), _ptr(shift), _lib.ACT[act], ctypes.byref(yv),
+                                      _ptr(ws), wsz, stream_handle())
+        if rc == _lib.VM_EUNSUPPORTED and nsrc > 1:
+            # sources spread wider than the kernels' 32-bit offsets reach (large batches): one materialised concat
+            xm = x.materialize()
+            xv = nhwc(xm)
+            rc = lib().vm_conv3x3_ex_nhwc(ctypes.byref(xv), 1, 0, _ptr(pc.packed), pc.cin, pc.cout, _ptr(pc.bias),
+                                          _ptr(scale), _ptr(shift), _lib.ACT[act], ctypes.byref(yv), _ptr(ws), wsz,
+                                          stream_handle())
+        check(rc, "conv3x3")
         if prof is not None:
             ev1.record()
             prof.append((2 * n * h * w * 9 * pc.cin * pc.cout, _lib.last_conv_kernel(), ev0, ev1))
@@ -709,6 +717,17 @@ def bn_backward(x, dy, y, mean, var, gamma, eps=1e-3, dx=None, dgamma=None, dbet
     check(lib().vm_bn_backward_ex_nhwc(ref(views[0]), ref(views[1]), ref(views[2]), _ptr(mean), _ptr(var),
                                        _ptr(gamma), float(eps), ref(views[3]), ref(views[4]), _ptr(dgamma),
                                        _ptr(dbeta), _ptr(dbias), _ptr(ws), stream_handle()), "bn_backward")
+    return dx
+
+
+def bn_backward_apply(x, dy, y, mean, var, gamma, sum_g, sum_gx, count, dx, eps=1e-3, dx2=None):
+    """The input-gradient pass of bn_backward with given channel sums over ``count`` pixels (SyncBN: the sums
+    all-reduced over the replicas, count = their pixels)."""
+    views = [None if t is None else nhwc(t) for t in (x, dy, y, dx, dx2)]
+    ref = lambda v: None if v is None else ctypes.byref(v)  # noqa: E731
+    check(lib().vm_bn_backward_apply_nhwc(ref(views[0]), ref(views[1]), ref(views[2]), _ptr(mean), _ptr(var),
+                                          _ptr(gamma), float(eps), _ptr(_f32(sum_g)), _ptr(_f32(sum_gx)), int(count),
+                                          ref(views[3]), ref(views[4]), stream_handle()), "bn_backward_apply")
     return dx
 
 

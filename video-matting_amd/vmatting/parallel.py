@@ -74,7 +74,10 @@ def gather_frames(local, n_frames, out=None):
         pad = local.contiguous()
     if out is None:
         out = torch.empty((world * mx,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
-    dist.all_gather_into_tensor(out, pad)
+    if dist.get_backend() == "gloo":  # gloo's collective is the list form (host-staged for device tensors)
+        dist.all_gather(list(out.view((world, mx) + tuple(local.shape[1:])).unbind(0)), pad)
+    else:
+        dist.all_gather_into_tensor(out, pad)
     if all(b - a == mx for a, b in sizes):
         return out
     return torch.cat([out[r * mx:r * mx + (b - a)] for r, (a, b) in enumerate(sizes)], dim=0)
@@ -88,3 +91,11 @@ def allreduce_grads(flat):
         return 1.0
     dist.all_reduce(flat, op=dist.ReduceOp.SUM)
     return 1.0 / dist.get_world_size()
+
+
+def allreduce_sum(t):
+    """In-place sum over the ranks (SyncBN's per-channel moments and gradient sums: a few KB per BN layer)."""
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return t
+

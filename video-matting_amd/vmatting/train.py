@@ -15,7 +15,9 @@ warped previous alpha, train.py:245):
             TF-1 resize adjoint.  The upconv biases (unet_simple.py:34, drawn but unused) get no gradient, so
             TF's apply_gradients skips them; here they are simply not parameters
   exchange  DDP: one RCCL all-reduce of the flat gradient buffer (parallel.allreduce_grads); BN statistics stay
-            per replica (each rank normalises over its own batch of 8, as the single-device reference does)
+            per replica by default (each rank normalises over its own batch of 8); ``sync_bn=True`` normalises
+            over the global batch instead (one small all-reduce of per-channel moments per BN layer, forward and
+            backward), the single-device reference's semantics for a batch split over replicas
   update    tf.train.AdamOptimizer(lr, beta1=0.9, beta2=0.999, epsilon=1e-8) (train.py:300-304) over the flat
             parameter buffer in one launch, then the forward / data-gradient filters are re-packed
 
@@ -67,11 +69,15 @@ class VideoTrainer:
     """train.video_procedure's iteration on device (also simple_procedure's: pass diff = cmp - bg as ``warped``)."""
 
     def __init__(self, vgg16_npy_path=None, dtype="fp32", device="cuda", params=None, bn=None, lr=1e-3,
-                 beta1=0.9, beta2=0.999, epsilon=1e-8):
+                 beta1=0.9, beta2=0.999, epsilon=1e-8, sync_bn=False):
         self.vgg = vgg16_npy_path if isinstance(vgg16_npy_path, Vgg16) else Vgg16(vgg16_npy_path, dtype, device)
         self.model = UNetSimple(self.vgg, True, dtype, device, params)
         self.device = self.model.device
         self.lr, self.beta1, self.beta2, self.epsilon = lr, beta1, beta2, epsilon
+        # SyncBN: batch statistics (and their gradient sums) over every replica's batch, as the single-device
+        # reference normalises its whole batch (unet_simple.py:25,41; params.py:8); one small all-reduce per BN
+        # layer in the forward and one in the backward.  Off: per-replica statistics (plain DDP)
+        self.sync_bn = bool(sync_bn) and parallel.world_size() > 1
         self.layout, n = param_layout()
         dev = self.device
         self.flat = torch.zeros(n, dtype=torch.float32, device=dev)
@@ -97,11 +103,11 @@ class VideoTrainer:
             bnl.gamma, bnl.beta = self.P[scope, "gamma"], self.P[scope, "beta"]
         self.model.relink_padded()
         # DDP: every replica starts from rank 0's variables.  init_conv draws from each process's global numpy RNG
-        # (unet_simple.py:10-16), so without this the ranks would apply the averaged gradient to different models
+        # (unet_simple.py:10-16), so without this the ranks would apply the averaged gradient to different models.
+        # Every pack below is made from the broadcast buffer; the model's own packs (convs and the channel-padded
+        # bf16 packs of UNetSimple.padded, drawn in UNetSimple.__init__) are re-made from it by _refresh_packs()
         if parallel.world_size() > 1:
             parallel.broadcast_tensors([self.flat], src=0)
-            for pc in self.model.convs.values():
-                pc.repack()
         # data-gradient filters: flipped / transposed packs of the forward filters (fp32 path); the bf16 path packs
         # them bf16 with the gradient channels padded to 32, so the data-gradient convs run on the patch-reuse MFMA
         # kernel from bf16 copies of the gradients (bn_backward / relu_backward write them)
@@ -130,6 +136,8 @@ class VideoTrainer:
         self._repack = ops.PackBatch(list(self.model.convs.values()) + list(self.dconv16.values()) +
                                      list(self.dconv.values()) + [v[0] for v in self._padconv.values()] +
                                      list(self.model.padded.values()))
+        if parallel.world_size() > 1:
+            self._refresh_packs()
         # filter gradients: bf16 operands on MFMA in the bf16 path, the exact-f32 kernel in the fp32 (parity) path
         self._mfma_wgrad = self.model.dtype == torch.bfloat16
         self.t = 0
@@ -198,7 +206,7 @@ class VideoTrainer:
         else:
             pc, x = self.model.conv(scope, x)
             ops.conv3x3(x, pc, "none", out=z, affine=False, splitk=True)
-        ops.bn_stats(z, mean, var)
+        self._stats(z, mean, var)
         bnl = self.model.bn[scope]
         ops.bn_apply(z, mean, var, bnl.gamma, bnl.beta, EPS, act, out=out)
 
@@ -228,21 +236,50 @@ class VideoTrainer:
             pc, rx = m.conv(up, r)
             ops.conv3x3(rx, pc, "relu", out=c[..., off:width], affine=False, splitk=True)
             mean, var = tb["st_" + up]
-            ops.bn_stats(c, mean, var)
+            self._stats(c, mean, var)
             ops.bn_apply(c, mean, var, m.bn[up].gamma, m.bn[up].beta, EPS, "none", out=b[cat + "n"][..., :width])
             self._new_conv(b[cat + "n"][..., :width], conv, "relu", b[out_key], tb)
         self._new_conv(b["c1"], "output", "sigmoid", tb["alpha"], tb)
         self.output = tb["alpha"]
         return self.output
 
+    def _stats(self, x, mean, var):
+        """Batch mean / biased variance of x's channels; SyncBN: over every replica's pixels (count-weighted, the
+        second moment combined in float64 so the per-replica variances do not cancel)."""
+        ops.bn_stats(x, mean, var)
+        if self.sync_bn:
+            m = float(x.shape[0] * x.shape[1] * x.shape[2])
+            md = mean.double()
+            t = torch.stack([md * m, (var.double() + md * md) * m, torch.full_like(md, m)])
+            parallel.allreduce_sum(t)
+            gm = t[0] / t[2]
+            mean.copy_(gm)
+            var.copy_((t[1] / t[2] - gm * gm).clamp_min(0.0))
+
+    def _bn_backward(self, x, dy, mask, mean, var, scope, dx, dx2=None, dbias=None):
+        """BN(+relu mask) backward: dx, dgamma / dbeta (local sums, DDP averages them) and optionally the conv-bias
+        gradient.  SyncBN: the local channel sums are all-reduced and the input gradient uses the global ones."""
+        gamma, dgamma, dbeta = self.P[scope, "gamma"], self.G[scope, "gamma"], self.G[scope, "beta"]
+        if not self.sync_bn:
+            return ops.bn_backward(x, dy, mask, mean, var, gamma, EPS, dx=dx, dgamma=dgamma, dbeta=dbeta, dx2=dx2,
+                                   dbias=dbias)
+        ops.bn_backward(x, dy, mask, mean, var, gamma, EPS, dgamma=dgamma, dbeta=dbeta)
+        sums = torch.cat([dbeta, dgamma])
+        parallel.allreduce_sum(sums)
+        c = dbeta.numel()
+        count = x.shape[0] * x.shape[1] * x.shape[2] * parallel.world_size()
+        ops.bn_backward_apply(x, dy, mask, mean, var, gamma, sums[:c], sums[c:], count, dx, EPS, dx2=dx2)
+        if dbias is not None:  # the conv bias's gradient = channel sum of this replica's dx
+            ops.bn_backward(None, dx, None, None, None, None, EPS, dbeta=dbias)
+        return dx
+
     # ------------------------------------------------------------------------------------------- backward
     def _conv_backward(self, scope, x_in, dy, mask, tb, dgrad_out=None):
         """BN(+relu) backward into dz, then bias / filter gradients, optionally the data gradient of x_in."""
         z, dz, (mean, var) = tb["z_" + scope], tb["dz_" + scope], tb["st_" + scope]
         g16 = tb["g16_" + scope] if dgrad_out is not None and scope in self.dconv16 else None
-        ops.bn_backward(z, dy, mask, mean, var, self.P[scope, "gamma"], EPS, dx=dz,
-                        dgamma=self.G[scope, "gamma"], dbeta=self.G[scope, "beta"],
-                        dx2=None if g16 is None else g16[..., :dz.shape[-1]], dbias=self.G[scope, "b"])
+        self._bn_backward(z, dy, mask, mean, var, scope, dz, dx2=None if g16 is None else g16[..., :dz.shape[-1]],
+                          dbias=self.G[scope, "b"])
         ops.conv_wgrad(x_in, dz, self.G[scope, "w"], mfma=self._mfma_wgrad)
         if dgrad_out is not None:
             if g16 is not None:
@@ -262,8 +299,7 @@ class VideoTrainer:
             c, cn = b[cat][..., :width], b[cat + "n"][..., :width]
             self._conv_backward(conv, cn, dout, b[out_key], tb, dgrad_out=tb["dcatn_" + up])
             mean, var = tb["st_" + up]
-            ops.bn_backward(c, tb["dcatn_" + up], None, mean, var, self.P[up, "gamma"], EPS, dx=tb["dcat_" + up],
-                            dgamma=self.G[up, "gamma"], dbeta=self.G[up, "beta"])
+            self._bn_backward(c, tb["dcatn_" + up], None, mean, var, up, tb["dcat_" + up])
             dcat, off = tb["dcat_" + up], 0
             for s, src in sels:
                 co = m.convs[s].cout
@@ -291,6 +327,11 @@ class VideoTrainer:
         one = np.float32(1.0)
         lr_t = np.float32(np.float32(self.lr) * np.sqrt(one - self._b2p) / (one - self._b1p))
         ops.adam_tf(self.flat, self.m, self.v, self.grad, lr_t, self.beta1, self.beta2, self.epsilon, scale)
+        self._refresh_packs()
+
+    def _refresh_packs(self):
+        """Re-make every kernel-layout copy of the flat parameters (forward, data-gradient and channel-padded packs,
+        the padded biases) after the flat buffer changed: the optimizer step, or rank 0's DDP broadcast."""
         self._repack()
         for scope, (pc, bp, cout) in self._padconv.items():
             bp[:cout].copy_(self.P[scope, "b"])

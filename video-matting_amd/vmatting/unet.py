@@ -16,6 +16,8 @@ Data layout in HBM (compute dtype T = bf16 or f32, NHWC, channels innermost):
 so every tf.concat (unet.py:62) is a pair of channel-slice writes, never a copy.
 """
 
+import weakref
+
 import numpy as np
 import torch
 
@@ -75,7 +77,7 @@ class UNet:
         self.convs = None        # name -> ops.PackedConv
         self._ws = None
         self._ws_key = None
-        self._ws_all = {}
+        self._ws_all = weakref.WeakValueDictionary()  # (n,h,w) -> buffer set, while something holds it
         self._c11 = None
         self._x = None
         self._in8_valid = False
@@ -138,8 +140,9 @@ class UNet:
 
     # ------------------------------------------------------------------ buffers
     def _buffers(self, n, h, w):
-        """Activation buffers for an [n,h,w] batch.  Every shape's set is kept (a HIP graph captured on one set
-        keeps pointing at it, e.g. video.py's full chunks and its shorter last chunk)."""
+        """Activation buffers for an [n,h,w] batch.  The model holds the current shape's set; a HIP graph captured
+        on a set holds that one (GraphedForward), e.g. video.py's full chunks and its shorter last chunk.  A set
+        nobody holds any more is freed, so a model that sees many frame sizes does not accumulate buffers."""
         key = (n, h, w)
         if self._ws_key == key:
             return self._ws
@@ -367,9 +370,18 @@ class GraphedForward:
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
             self.output = model.forward(self.input, out)
+        # the buffer set the graph writes stays alive with the graph; so does the forward's host-side state
+        self._ws, self._ws_key = model._ws, model._ws_key
+        self._skip_valid = model._skip_valid
 
     def replay(self):
         self.graph.replay()
+        m = self.model
+        if m._ws is not self._ws:  # the model ran another shape since: its attributes follow this replay
+            m._ws, m._ws_key = self._ws, self._ws_key
+            m._publish(self._ws)
+        m._x, m._c11, m._in8_valid, m._skip_valid = self.input, None, False, self._skip_valid
+        m.output = self.output
         return self.output
 
     def __call__(self, frames):

@@ -121,9 +121,11 @@ class UNetSimple:
         for k, pc in self.padded.items():
             pc.bias = self.convs[k].bias
 
-    def _towers(self, b):
+    def _towers(self, b, splitk=True):
         """The three frozen towers of create_model (vgg1/2/3 on cmp/bg/diff, unet_simple.py:57-89, 148-152) as one
-        batch-3n VGG16 pass over b['tin'] (the towers share weights); 2x2 pools fused into the conv epilogue."""
+        batch-3n VGG16 pass over b['tin'] (the towers share weights); 2x2 pools fused into the conv epilogue.
+        ``splitk``: split-K on the small L4/L5 grids (training); inference leaves it off so frames are
+        batch-invariant."""
         V = self.vgg.convs
         t = lambda k: b["t_" + k]  # noqa: E731
         ops.conv3x3(b["tin"][..., :3], V["conv1_1"], "relu", out=t("conv1_1"))
@@ -133,12 +135,12 @@ class UNetSimple:
         ops.conv3x3(b["tpool2"], V["conv3_1"], "relu", out=t("conv3_1"))
         ops.conv3x3(t("conv3_1"), V["conv3_2"], "relu", out=t("conv3_2"))
         ops.conv3x3(t("conv3_2"), V["conv3_3"], "relu", out=t("conv3_3"), pool_out=b["tpool3"])
-        ops.conv3x3(b["tpool3"], V["conv4_1"], "relu", out=t("conv4_1"), splitk=True)
-        ops.conv3x3(t("conv4_1"), V["conv4_2"], "relu", out=t("conv4_2"), splitk=True)
+        ops.conv3x3(b["tpool3"], V["conv4_1"], "relu", out=t("conv4_1"), splitk=splitk)
+        ops.conv3x3(t("conv4_1"), V["conv4_2"], "relu", out=t("conv4_2"), splitk=splitk)
         ops.conv3x3(t("conv4_2"), V["conv4_3"], "relu", out=t("conv4_3"), pool_out=b["tpool4"])
-        ops.conv3x3(b["tpool4"], V["conv5_1"], "relu", out=t("conv5_1"), splitk=True)
-        ops.conv3x3(t("conv5_1"), V["conv5_2"], "relu", out=t("conv5_2"), splitk=True)
-        ops.conv3x3(t("conv5_2"), V["conv5_3"], "relu", out=t("conv5_3"), splitk=True)
+        ops.conv3x3(b["tpool4"], V["conv5_1"], "relu", out=t("conv5_1"), splitk=splitk)
+        ops.conv3x3(t("conv5_1"), V["conv5_2"], "relu", out=t("conv5_2"), splitk=splitk)
+        ops.conv3x3(t("conv5_2"), V["conv5_3"], "relu", out=t("conv5_3"), splitk=splitk)
 
     def load_inputs(self, b, xs):
         """cmp / bg / diff (f32 device tensors) into the towers' batch (tower t = frames t*n..) and into the 9-channel
@@ -158,7 +160,7 @@ class UNetSimple:
         L = _levels(h, w)
         C, B = self.convs, self.bn
         self.load_inputs(b, xs)
-        self._towers(b)
+        self._towers(b, splitk=ph)
         R = lambda x, k, out: conv_bn(*self.conv(k, x)[::-1], B[k], ph, "relu", out)  # noqa: E731
         # level 4
         for i in range(3):
@@ -194,7 +196,7 @@ class UNetSimple:
         else:
             ops.resize_bilinear(prev, size, out=rbuf)
         pc, x = self.conv(scope, rbuf)
-        ops.conv3x3(x, pc, "relu", out=up_slice, affine=False, splitk=True)
+        ops.conv3x3(x, pc, "relu", out=up_slice, affine=False, splitk=bool(phase))
         self.bn[scope](cat, phase, out=catn)
 
     def _publish(self, b):

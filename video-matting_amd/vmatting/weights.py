@@ -71,7 +71,8 @@ def load_vgg16(path_or_dict, allow_pickle=None):
     if isinstance(path_or_dict, dict):
         return path_or_dict
     path = DEFAULT_VGG_PATH if path_or_dict is None else os.fspath(path_or_dict)
-    if path.endswith(".npy") and os.path.exists(path[:-4] + ".npz"):
+    # only the default location is redirected to its converted sibling: a path the caller named is loaded as named
+    if path_or_dict is None and os.path.exists(path[:-4] + ".npz"):
         path = path[:-4] + ".npz"
     if not os.path.exists(path):
         raise FileNotFoundError("[Errno 2] No such file or directory: %r (pass a data_dict, e.g. "
