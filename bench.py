@@ -456,7 +456,7 @@ def train_flops(n, h, w):
     return fwd + head, head + dgrad
 
 
-def train_bench(dev, steps, warmup, world, rank, threads, cpu=True, n=8, size=320, dtype="bf16"):
+def train_bench(dev, steps, warmup, world, rank, threads, cpu=True, n=8, size=320, dtype="bf16", graph=True):
     """BASELINE config 5: one train.py video_procedure iteration per step (train.py:288-343) — batch of 8 320x320
     samples per GPU (params.py:8-9) resident in HBM: 3 VGG16 towers + UNetSimple (batch-statistics BN) forward,
     loss, backward through the trainable layers, one RCCL all-reduce of the gradients (DDP), TF-Adam, re-pack.
@@ -475,8 +475,13 @@ def train_bench(dev, steps, warmup, world, rank, threads, cpu=True, n=8, size=32
     cmp_d, bg_d, warped_d, gt_d, fg_d = T(cmp), T(bg - mean), T(warped), T(gt), T(fg)
     np.random.seed(1)
     trn = VideoTrainer(synthetic_vgg16(0), dtype, dev)
+    # forward + loss and backward replayed from HIP graphs (VideoTrainer.capture), DDP exchange + Adam eager
+    g = trn.capture(cmp_d, bg_d, warped_d, gt_d, fg_d) if graph else None
     for _ in range(warmup):
-        trn.step(cmp_d, bg_d, warped_d, gt_d, fg_d)
+        if g is not None:
+            g.step()
+        else:
+            trn.step(cmp_d, bg_d, warped_d, gt_d, fg_d)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -484,11 +489,17 @@ def train_bench(dev, steps, warmup, world, rank, threads, cpu=True, n=8, size=32
     t0 = time.perf_counter()
     for _ in range(steps):
         ev.mark()
-        trn.forward(cmp_d, bg_d, warped_d)
-        trn._tb["loss"].copy_(ops.matting_loss(trn._tb["alpha"], gt_d, fg_d, bg_d, cmp_d))
+        if g is not None:
+            g.g_fwd.replay()
+        else:
+            trn.forward(cmp_d, bg_d, warped_d)
+            trn._tb["loss"].copy_(ops.matting_loss(trn._tb["alpha"], gt_d, fg_d, bg_d, cmp_d))
         ev.mark()
-        trn.grad.zero_()
-        trn.backward(gt_d, fg_d, bg_d, cmp_d)
+        if g is not None:
+            g.g_bwd.replay()
+        else:
+            trn.grad.zero_()
+            trn.backward(gt_d, fg_d, bg_d, cmp_d)
         ev.mark()
         trn.apply_gradients()
         ev.mark()
@@ -503,6 +514,8 @@ def train_bench(dev, steps, warmup, world, rank, threads, cpu=True, n=8, size=32
     rec = {"workload": "train.py video_procedure step (config 5): %d x %dx%d per GPU, 3 VGG16 towers + UNetSimple "
                        "fwd/bwd, loss, DDP all-reduce, TF-Adam" % (n, size, size),
            "dtype": dtype + " forward, f32 gradients/optimizer", "n_gpus": world,
+           "launch": "hip-graph replay of forward+loss and of backward, eager all-reduce + Adam + re-pack" if graph
+                     else "eager",
            "samples_per_s": round(n * world / wall, 1), "ms_per_step": round(1000 * wall, 3),
            "device_ms": {"forward_loss": round(ph[0], 3), "backward": round(ph[1], 3),
                          "allreduce_adam_repack": round(ph[2], 3)},
@@ -548,6 +561,7 @@ def train_chain_bench(dev, steps, warmup, n=8, size=320, h=1080, w=1920, dtype="
     np.random.seed(7)
     trn = VideoTrainer(synthetic_vgg16(0), dtype, dev)
     names = ("cmp", "bg", "label", "warped", "fg")
+    tg = [None]
 
     def one(ev=None, wall=None):
         t0 = time.perf_counter()
@@ -562,7 +576,10 @@ def train_chain_bench(dev, steps, warmup, n=8, size=320, h=1080, w=1920, dtype="
         r = vl.compose_batch(samples, (size, size), names, device=dev)
         t2 = time.perf_counter()
         ev and ev.mark()
-        loss = trn.step(r["cmp"], r["bg"], r["warped"], r["label"], r["fg"])
+        batch = (r["cmp"], r["bg"], r["warped"], r["label"], r["fg"])
+        if tg[0] is None:  # the step's forward / backward as HIP graphs (VideoTrainer.capture), captured once
+            tg[0] = trn.capture(*batch)
+        loss = tg[0].step(*batch)
         ev and ev.mark()
         t3 = time.perf_counter()
         if wall is not None:
@@ -687,7 +704,13 @@ def main():
     ap.add_argument("--video-chunk", type=int, default=8, help="frames per HIP graph in the config-4 record")
     ap.add_argument("--option", action="append", default=[], metavar="KEY=VALUE",
                     help="vm_set_option kernel knob before the run (A/B comparisons), repeatable")
+    ap.add_argument("--only", choices=["train", "train_chain", "temporal"],
+                    help="profiling passes: run just this record (rank 0 / N=1) and print it")
+    ap.add_argument("--temporal-sizes", default="500x1200,1080x1920", help="config-3 sizes HxW, comma separated")
+    ap.add_argument("--temporal-dtypes", default="fp32,bf16", help="config-3 compute dtypes, comma separated")
     args = ap.parse_args()
+    t_sizes = [tuple(int(v) for v in hw.split("x")) for hw in args.temporal_sizes.split(",")]
+    t_dtypes = args.temporal_dtypes.split(",")
 
     rank, world, local = parallel.init_from_env("nccl")
     if world != args.gpus:
@@ -699,6 +722,18 @@ def main():
         from vmatting import _lib
         _lib.set_option(k, int(v))
     cpu_model, threads = host_info()
+    if args.only:  # one record alone (rocprofv3 passes per record: tools/prof_bench.sh)
+        if args.only == "train":
+            rec = train_bench(dev, args.steps, args.warmup, world, rank, threads, cpu=False, graph=not args.no_graph)
+        elif args.only == "train_chain":
+            rec = train_chain_bench(dev, args.steps, args.warmup)
+        else:
+            rec = temporal_bench(dev, args.steps, t_dtypes, t_sizes, False, threads)
+        if rank == 0:
+            print(json.dumps({"only": args.only, "record": rec}), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
 
     # identical weights everywhere: every rank draws from the same seeds, then rank 0's packed
     # buffers are broadcast (one RCCL collective) so replicas are bit-identical by construction
@@ -758,7 +793,8 @@ def main():
 
     train = None
     if not args.no_train:  # every rank: the DDP all-reduce is part of the step
-        train = train_bench(dev, max(args.steps // 4, 10), 3, world, rank, threads, cpu=not args.no_cpu_baseline)
+        train = train_bench(dev, max(args.steps // 4, 10), 3, world, rank, threads, cpu=not args.no_cpu_baseline,
+                            graph=not args.no_graph)
         if world == 1:
             train["chained"] = train_chain_bench(dev, 5, 2)
 
@@ -819,8 +855,7 @@ def main():
         if vrec:
             rec["video_batch"] = vrec
         if world == 1 and not args.no_temporal:
-            rec["temporal"] = temporal_bench(dev, 20, ["fp32", "bf16"], [(500, 1200), (1080, 1920)],
-                                             not args.no_cpu_baseline, threads)
+            rec["temporal"] = temporal_bench(dev, 20, t_dtypes, t_sizes, not args.no_cpu_baseline, threads)
         if train:
             rec["train"] = train
         if world == 1 and not args.no_loader:

@@ -72,10 +72,11 @@ const char* vm_last_error(void);
  *   "glds_rb"        K-step bytes of the 256x256 LDS-DMA tile: 128 (2-slot ring, default) or 64 (4-slot)
  *   "head_kernel"    cout == 1 convs: 0 = MFMA tap-GEMM kernel (default), 1 = generic per-pixel kernel,
  *                    2 = register-strip kernel
- *   "softmax_kernel" bf16 cin <= 8 -> 64 conv + softmax (refine.py conv4): 0 = generic kernels' epilogue,
- *                    1 = conv3x3_first_softmax (register stores), 2 = its nontemporal form, 3 / 4 = per-wave LDS
- *                    transpose with whole-pixel plain / nontemporal stores (4 = default)
- *   "softmax_blocks" persistent grid of conv3x3_first_softmax (default 1024)
+ *   "softmax_kernel" cin <= 8 -> 64 conv + softmax (refine.py conv4): 0 = generic kernels' epilogue; bf16: 1 =
+ *                    conv3x3_first_softmax (register stores), 2 = its nontemporal form, 3 / 4 = per-wave LDS transpose
+ *                    with whole-pixel plain / nontemporal stores, 5 = 4 with the weights in LDS, 6 = wave-private
+ *                    strips, no per-tile block barrier (default); f32: any value but 0 = conv3x3_first_softmax_f32
+ *   "softmax_blocks" persistent grid of the conv3x3_first_softmax kernels (default 2048)
  *   "pair_xin_wide"  pair kernel, f32 frames with 4..8 channels: 1 = two 16-byte loads per pixel (default),
  *                    0 = one dword load per channel */
 int vm_set_option(const char* key, long value);

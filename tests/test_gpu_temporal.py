@@ -103,7 +103,7 @@ def test_temporal_refine_bf16_close_to_fp32():
 
 @pytest.mark.parametrize("h,w", [(500, 1200), (1080, 1920)])
 def test_temporal_refine_bf16_kernel_vs_oracle(h, w):
-    """The TIMED bf16 config-3 refine (conv3x3_first_softmax<true, true>: refine conv4 + the 64-way softmax fused)
+    """The TIMED bf16 config-3 refine (conv3x3_first_softmax_strip: refine conv4 + the 64-way softmax fused)
     against the oracle's conv + softmax in float64 on the same bf16-rounded input row and bf16-rounded filter (f32
     bias): only the f32 summation order and the device exp differ, so the probabilities stay within 1e-4 max-abs
     (north_star's bound) at full size; rows sum to 1."""
@@ -114,7 +114,7 @@ def test_temporal_refine_bf16_kernel_vs_oracle(h, w):
     tp = temporal.TemporalRefiner(dtype="bf16")
     out = tp(T(prev), T(cur), T(cmp), T(bw), T(fw))
     torch.cuda.synchronize()
-    assert _lib.last_conv_kernel() == "vm::conv3x3_first_softmax<true, true>", _lib.last_conv_kernel()
+    assert _lib.last_conv_kernel() == "vm::conv3x3_first_softmax_strip", _lib.last_conv_kernel()
     x = tp._bufs[(h, w)]["xin"][..., :5].float().cpu().numpy().astype(np.float64)  # the bf16 input row
     w4, b4 = tp.refine.params["conv4"]
     w4 = torch.from_numpy(np.ascontiguousarray(w4, np.float32)).to(torch.bfloat16).double().numpy()
@@ -154,18 +154,25 @@ def test_refine_softmax_kernel_matches_generic_epilogue(n, h, w):
             outs[k] = ops.conv3x3(xb, pc, "softmax", out_dtype=torch.float32)
             name = _lib.last_conv_kernel()
             assert ("first_softmax" in name) == (k != 0), name
-        for k in (3, 4, 5):  # the per-wave LDS transpose store forms (5: weights staged in LDS): same values
+        for k in (3, 4, 5):  # the per-wave LDS transpose store forms (5: weights in LDS): same values
             _lib.set_option("softmax_kernel", k)
             assert torch.equal(ops.conv3x3(xb, pc, "softmax", out_dtype=torch.float32), outs[1]), k
+        _lib.set_option("softmax_kernel", 6)  # wave strips (the default): bias-initialised sums, v_exp_f32
+        outs[6] = ops.conv3x3(xb, pc, "softmax", out_dtype=torch.float32)
+        assert _lib.last_conv_kernel() == "vm::conv3x3_first_softmax_strip"
+        for blocks in (1, 3, 7):
+            _lib.set_option("softmax_blocks", blocks)
+            assert torch.equal(ops.conv3x3(xb, pc, "softmax", out_dtype=torch.float32), outs[6]), blocks
+        _lib.set_option("softmax_blocks", 2048)
         _lib.set_option("softmax_kernel", 2)
         for blocks in (1, 3, 7):  # persistent walks with partial last rounds
             _lib.set_option("softmax_blocks", blocks)
             assert torch.equal(ops.conv3x3(xb, pc, "softmax", out_dtype=torch.float32), outs[2]), blocks
     finally:
-        _lib.set_option("softmax_kernel", 4)
-        _lib.set_option("softmax_blocks", 1024)
+        _lib.set_option("softmax_kernel", 6)
+        _lib.set_option("softmax_blocks", 2048)
     ref = outs[0].cpu().numpy()
-    for k in (1, 2):
+    for k in (1, 2, 6):
         got = outs[k].cpu().numpy()
         assert np.abs(got - ref).max() <= 1e-5, (k, np.abs(got - ref).max())
         np.testing.assert_allclose(got.sum(-1), 1.0, atol=1e-5)
@@ -177,7 +184,8 @@ def test_refine_softmax_kernel_matches_generic_epilogue(n, h, w):
 def test_refine_softmax_f32_kernel(n, h, w, cin):
     """conv3x3_first_softmax_f32 (compact-K exact-f32 MFMA conv + register softmax, the fp32 config-3 refine) against
     the generic f32 kernel's softmax epilogue and the float64 oracle: exact f32 products, f32 sums in another order
-    -> within 1e-5 of both; rows sum to 1; ragged tiles and partial persistent rounds."""
+    -> within 5e-5 of the generic kernel and 1e-4 (north_star's bound) of float64; rows sum to 1; ragged tiles and
+    partial persistent rounds."""
     from oracle import ops as oops
     from vmatting import _lib, ops
     rs = np.random.RandomState(h * 7 + w + cin)
@@ -196,11 +204,12 @@ def test_refine_softmax_f32_kernel(n, h, w, cin):
         gen = ops.conv3x3(xd, pc, "softmax").clone()
         assert "first_softmax" not in _lib.last_conv_kernel()
     finally:
-        _lib.set_option("softmax_kernel", 4)
-        _lib.set_option("softmax_blocks", 1024)
+        _lib.set_option("softmax_kernel", 6)
+        _lib.set_option("softmax_blocks", 2048)
     ref = oops.softmax_lastdim(oops.conv3x3_same(x[..., :cin].astype(np.float64), wt.astype(np.float64),
                                                  b.astype(np.float64)))
     g = got.cpu().numpy()
-    assert np.abs(g - gen.cpu().numpy()).max() <= 1e-5
-    assert np.abs(g - ref).max() <= 1e-5, np.abs(g - ref).max()
+    # logits reach |100| here (inputs +-30, 9*cin taps): f32 sums of either order sit ~1e-5 from the f64 softmax
+    assert np.abs(g - gen.cpu().numpy()).max() <= 5e-5
+    assert np.abs(g - ref).max() <= 1e-4, np.abs(g - ref).max()
     np.testing.assert_allclose(g.sum(-1), 1.0, atol=1e-5)

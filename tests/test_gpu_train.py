@@ -684,3 +684,23 @@ def test_syncbn_two_replicas_match_one_replica_with_both_samples():
         if l2 > 1e-3:
             bad.append((scope, kind, float(l2)))
     assert not bad, bad
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_train_graph_step_equals_eager(dtype):
+    """VideoTrainer.capture: two steps replayed from the forward / backward HIP graphs (new batches copied in, Adam
+    eager in between) leave bit-identical parameters, packs and losses to two eager VideoTrainer.step calls."""
+    from vmatting.train import VideoTrainer
+    from vmatting.weights import synthetic_vgg16
+    vgg = synthetic_vgg16(0)
+    params = om.unet_simple_params(np.random.RandomState(1))
+    b1, b2 = _batch(2, 48, 64, seed=3), _batch(2, 48, 64, seed=4)
+    eager = VideoTrainer(vgg, dtype, DEV, params=params)
+    le = [H(eager.step(*b)) for b in (b1, b2)]
+    graphed = VideoTrainer(vgg, dtype, DEV, params=params)
+    g = graphed.capture(*b1)
+    lg = [H(g.step(*b)) for b in (b1, b2)]
+    torch.cuda.synchronize()
+    assert all(np.array_equal(a, b) for a, b in zip(le, lg)), (le, lg)
+    assert torch.equal(eager.flat, graphed.flat)
+    assert torch.equal(eager.model.convs["conv2"].packed, graphed.model.convs["conv2"].packed)

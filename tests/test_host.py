@@ -176,3 +176,16 @@ def test_loader_file_helpers(tmp_path):
     assert not vl.epoch_is_over(files, 2)
     assert vl.get_batch_list(files, 1) == [["/data/c/fg.png", "/data/c/tr.png", "/data/d/bg.jpg"]]
     assert vl.epoch_is_over(files, 2)
+
+
+def test_load_vgg16_explicit_npy_is_not_redirected(tmp_path):
+    """an explicitly named .npy is loaded as named (here: refused as a pickle) even when a sibling .npz
+    exists; only the default location prefers its converted .npz."""
+    from vmatting import weights
+    d = weights.synthetic_vgg16(0)
+    np.save(tmp_path / "vgg16.npy", np.array(d, dtype=object), allow_pickle=True)
+    weights.save_vgg16_npz({"conv1_1": d["conv1_1"]}, str(tmp_path / "vgg16.npz"))
+    with pytest.raises(ValueError, match="pickled"):
+        weights.load_vgg16(str(tmp_path / "vgg16.npy"))
+    got = weights.load_vgg16(str(tmp_path / "vgg16.npz"))
+    assert list(got) == ["conv1_1"] and np.array_equal(got["conv1_1"][0], d["conv1_1"][0])

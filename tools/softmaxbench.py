@@ -1,6 +1,8 @@
-"""Refine conv4 + softmax (refine.py:27-32) at 1080p bf16: vm softmax_kernel variants side by side.
+"""Refine conv4 + softmax (refine.py:27-32) at 1080p, bf16 and fp32: vm softmax_kernel variants side by side.
 
-0 = generic conv kernel + LDS softmax epilogue, 1 = conv3x3_first_softmax, 2 = its nontemporal-store form.
+0 = generic conv kernel + LDS softmax epilogue, 1 = conv3x3_first_softmax, 2 = its nontemporal-store form,
+4 = + per-wave LDS transpose (default), 5 = weights in LDS, 6 = wave-private strips (conv3x3_first_softmax_strip);
+fp32: 0 = generic f32 kernel, else conv3x3_first_softmax_f32.
 Algorithmic bytes: 16 B/px bf16 input chunk (8 channels) + 256 B/px f32 softmax out.
 """
 import sys
@@ -13,15 +15,18 @@ from vmatting import _lib, ops  # noqa: E402
 
 h, w = (int(v) for v in (sys.argv[1:3] if len(sys.argv) > 2 else (1080, 1920)))
 rs = np.random.RandomState(0)
-x = torch.from_numpy(rs.uniform(-1, 1, size=(1, h, w, 8)).astype(np.float32)).cuda().to(torch.bfloat16)
-pc = ops.PackedConv((rs.normal(size=(3, 3, 5, 64)) * 0.3).astype(np.float32), rs.normal(size=64).astype(np.float32),
-                    "bf16")
+xf = torch.from_numpy(rs.uniform(-1, 1, size=(1, h, w, 8)).astype(np.float32)).cuda()
+wt, bias = (rs.normal(size=(3, 3, 5, 64)) * 0.3).astype(np.float32), rs.normal(size=64).astype(np.float32)
+pcs = {"bf16": ops.PackedConv(wt, bias, "bf16"), "fp32": ops.PackedConv(wt, bias, "fp32")}
+xs = {"bf16": xf.to(torch.bfloat16), "fp32": xf}
 out = torch.empty((1, h, w, 64), dtype=torch.float32, device="cuda")
-nbytes = h * w * (16 + 256)
-for k, blocks in ((0, 1024), (1, 1024), (4, 1024), (4, 256), (4, 512), (4, 768), (4, 1024), (4, 512), (1, 512),
-                  (2, 512)):
+CFGS = [("bf16", 4, 1024), ("bf16", 5, 1024), ("bf16", 6, 1024), ("bf16", 6, 2048), ("bf16", 6, 4096),
+        ("fp32", 0, 1024), ("fp32", 6, 1024), ("fp32", 6, 2048), ("fp32", 6, 4096), ("bf16", 6, 2048)]
+for dt, k, blocks in CFGS:
     _lib.set_option("softmax_kernel", k)
     _lib.set_option("softmax_blocks", blocks)
+    x, pc = xs[dt], pcs[dt]
+    nbytes = h * w * ((16 if dt == "bf16" else 32) + 256)
     fn = lambda: ops.conv3x3(x[..., :5], pc, "softmax", out=out)  # noqa: E731
     for _ in range(3):
         fn()
@@ -33,6 +38,7 @@ for k, blocks in ((0, 1024), (1, 1024), (4, 1024), (4, 256), (4, 512), (4, 768),
     e1.record()
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / 50
-    print("softmax_kernel %d blocks %6d  %-40s %.1f us  %.2f TB/s algorithmic" % (k, blocks, _lib.last_conv_kernel(), ms * 1e3,
-                                                                      nbytes / ms / 1e9), flush=True)
-_lib.set_option("softmax_kernel", 4)
+    print("%s softmax_kernel %d blocks %5d  %-42s %.1f us  %.2f TB/s algorithmic" % (
+        dt, k, blocks, _lib.last_conv_kernel(), ms * 1e3, nbytes / ms / 1e9), flush=True)
+_lib.set_option("softmax_kernel", 6)
+_lib.set_option("softmax_blocks", 2048)

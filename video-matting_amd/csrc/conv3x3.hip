@@ -1741,28 +1741,93 @@ __global__ __launch_bounds__(512, WL ? 4 : 2) void conv3x3_first_softmax(ConvArg
   }
 }
 
-// ================================================================ refine conv4 + softmax in f32 (refine.py:27-32)
-// The reference's precision for config 3: f32 input row [cmp, alpha, warped] (CIN <= 8 of an 8-channel pixel), exact
-// f32 products on v_mfma_f32_16x16x4_f32, f32 sums, f32 softmax.  K is COMPACT: k = tap * CIN + c over the 9 * CIN
-// real taps (45 for the refine's CIN 5 -> 12 four-deep MFMA steps instead of the 18 of the padded 72); the lane in
-// k-slot q of step s reads tap (4s+q) / CIN, channel (4s+q) % CIN.  The patch lives in LDS as channel planes, so the
-// 16 lanes of a k-slot read 16 consecutive pixels (conflict-free).  The weights and the per-lane patch offsets are
-// staged once per block in LDS ([step][lane] records: one ds_read_b128 of the 4 cout fragments + one offset per
-// step), which keeps the kernel at 4 waves per SIMD (2 blocks per CU) without spilling.  Softmax + per-wave LDS
-// transpose + whole-pixel nontemporal stores as in conv3x3_first_softmax.  Per 8 x 32 tile a wave issues NS x 8
-// MFMAs (32 cycles each): at NS = 12 the chip's f32 matrix time for a 1080p frame (~80 us) is on par with its 531 MB
-// of f32 output at HBM speed.
-template <int CIN>
-__global__ __launch_bounds__(512, 4) void conv3x3_first_softmax_f32(ConvArgs a) {
-  constexpr int NS = (9 * CIN + 3) / 4;
-  constexpr int TH = 8, TW = 32, PW = TW + 2, PPIX = (TH + 2) * PW;
-  constexpr int SRF = 68;  // staging row: 64 floats + 4
-  constexpr int ZERO = CIN * PPIX;  // a zero slot: k >= 9 * CIN reads it
-  __shared__ __attribute__((aligned(16))) float patch[CIN * PPIX + 4];
-  __shared__ __attribute__((aligned(16))) float stg[8 * 16 * SRF];
-  __shared__ __attribute__((aligned(16))) f32x4 wl[NS * 64];
-  __shared__ int pl[NS * 4];
+// The refine softmax of one wave's 32-pixel x 64-channel accumulator strip (acc[fc][fp]: MFMA 16x16 layout, pixel
+// fp*16 + col, channels fc*16 + 4q .. +3), its per-channel affine from rmul ([scale | bias*scale + shift]), and the
+// whole-pixel nontemporal stores through the wave's private 16 x 68-float LDS slab `ws`: every store instruction
+// writes 4 whole pixels.  `valid` = pixels of the strip inside the frame.
+// strip accumulators: zero (the epilogue applies the affine), or the bias (no scale / shift: rmul[64..] = bias)
+__device__ __forceinline__ void init_strip_acc(f32x4 (&acc)[4][2], const float* rmul, bool aff, int q) {
+#pragma unroll
+  for (int fc = 0; fc < 4; ++fc) {
+    const f32x4 b = aff ? f32x4{0.f, 0.f, 0.f, 0.f} : *reinterpret_cast<const f32x4*>(rmul + 64 + fc * 16 + 4 * q);
+    acc[fc][0] = b;
+    acc[fc][1] = b;
+  }
+}
+
+// AFF: apply rmul's per-channel affine; without it the accumulators already hold the logits (the kernel started
+// them at the bias: the refine conv has no BN, scale/shift are absent).  The exponential is v_exp_f32 on x*log2(e)
+// (__expf): for the softmax of logits bounded by max-subtraction its relative error (~1e-6 near 0, below 1e-5
+// absolute on every probability) is far inside the 1e-4 bound, at a third of expf's instructions — this epilogue is
+// the VALU-bound half of the kernel.
+template <bool AFF>
+__device__ __forceinline__ void softmax_store_strip(const f32x4 (&acc)[4][2], const float* rmul, float* ws, float* yb,
+                                                    int ycs, int valid, int lane) {
+  constexpr int SRF = 68;
+  const int col = lane & 15, q = lane >> 4;
+#pragma unroll
+  for (int fp = 0; fp < 2; ++fp) {
+    float v[4][4];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int fc = 0; fc < 4; ++fc) {
+      if constexpr (AFF) {
+        const float4 m4 = *reinterpret_cast<const float4*>(rmul + fc * 16 + 4 * q);
+        const float4 a4 = *reinterpret_cast<const float4*>(rmul + 64 + fc * 16 + 4 * q);
+        const float mul[4] = {m4.x, m4.y, m4.z, m4.w}, add[4] = {a4.x, a4.y, a4.z, a4.w};
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) v[fc][jj] = fmaf(acc[fc][fp][jj], mul[jj], add[jj]);
+      } else {
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) v[fc][jj] = acc[fc][fp][jj];
+      }
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) mx = fmaxf(mx, v[fc][jj]);
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 16));
+    mx = fmaxf(mx, __shfl_xor(mx, 32));
+    float sum = 0.f;
+#pragma unroll
+    for (int fc = 0; fc < 4; ++fc)
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        v[fc][jj] = __expf(v[fc][jj] - mx);
+        sum += v[fc][jj];
+      }
+    sum += __shfl_xor(sum, 16);
+    sum += __shfl_xor(sum, 32);
+    const float inv = 1.f / sum;
+#pragma unroll
+    for (int fc = 0; fc < 4; ++fc)
+      *reinterpret_cast<f32x4*>(ws + col * SRF + fc * 16 + 4 * q) =
+          f32x4{v[fc][0] * inv, v[fc][1] * inv, v[fc][2] * inv, v[fc][3] * inv};
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {  // lane l: pixel 4*it + l/16, channels 4*(l%16) .. +3
+      const int px = 4 * it + (lane >> 4), ch = 4 * (lane & 15);
+      const f32x4 o = *reinterpret_cast<const f32x4*>(ws + px * SRF + ch);
+      const int pc = fp * 16 + px;
+      if (pc < valid) __builtin_nontemporal_store(o, reinterpret_cast<f32x4*>(yb + (long)pc * ycs + ch));
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+}
+
+// bf16 refine conv4 + softmax on wave-private strips (see conv3x3_first_softmax_f32 below for the strip scheme): the
+// conv is conv3x3_first's (one 16-byte pixel chunk per lane, 4 taps x 8 channels per 32-deep K-step, 3 steps); each
+// wave stages its 3 x 34-pixel patch, the weight fragments live in LDS ([step][fc][lane]), no block barrier per tile.
+__global__ __launch_bounds__(512, 4) void conv3x3_first_softmax_strip(ConvArgs a) {
+  using T = uint16_t;
+  constexpr int TH = 8, TW = 32, PW = TW + 2, SP = 3 * PW;
+  constexpr int SRF = 68;
+  __shared__ __attribute__((aligned(16))) uint4 wlds[3 * 4 * 64];
   __shared__ __attribute__((aligned(16))) float rmul[2 * 64];
+  __shared__ __attribute__((aligned(16))) uint4 pat[8 * SP];
+  __shared__ __attribute__((aligned(16))) float stg[8 * 16 * SRF];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int H = a.H, W = a.W, cs = a.x_cstride;
   const int th = (H + TH - 1) / TH, tw = (W + TW - 1) / TW;
@@ -1771,16 +1836,123 @@ __global__ __launch_bounds__(512, 4) void conv3x3_first_softmax_f32(ConvArgs a) 
     const int base = (i / a.tiles_n) * a.tiles_n;
     return base + a.tiles_n <= ntiles ? base + xcd_tile(i - base, a.tiles_n) : i;
   };
-  auto load_patch = [&](int t, float4& lo, float4& hi) {
+  auto load_strip = [&](int t, uint4 (&v)[2]) {
     const int n = t / (th * tw), srem = t - n * th * tw;
-    const int r0 = (srem / tw) * TH, c0 = (srem - (srem / tw) * tw) * TW;
-    const int pr = tid / PW, pc = tid - pr * PW;
-    const int h = r0 - 1 + pr, w = c0 - 1 + pc;
-    const bool ok = tid < PPIX && (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
-    const float* xp = reinterpret_cast<const float*>(a.x) + a.x_coff + ((long)n * H + (ok ? h : 0)) * (long)W * cs +
-                      (long)(ok ? w : 0) * cs;
-    lo = ok ? *reinterpret_cast<const float4*>(xp) : make_float4(0.f, 0.f, 0.f, 0.f);
-    hi = ok && CIN > 4 ? *reinterpret_cast<const float4*>(xp + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+    const int r = (srem / tw) * TH + wave, c0 = (srem - (srem / tw) * tw) * TW;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int e = lane + 64 * k;
+      const int pr = e / PW, pc = e - pr * PW;
+      const int h = r - 1 + pr, w = c0 - 1 + pc;
+      const bool ok = e < SP && (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
+      const T* xp = reinterpret_cast<const T*>(a.x) + a.x_coff + ((long)n * H + (ok ? h : 0)) * (long)W * cs +
+                    (long)(ok ? w : 0) * cs;
+      v[k] = ok ? *reinterpret_cast<const uint4*>(xp) : make_uint4(0, 0, 0, 0);
+    }
+  };
+  const int col = lane & 15, q = lane >> 4;
+  const __amdgpu_buffer_rsrc_t wrs = w_rsrc<T>(a, 0);
+  for (int e = tid; e < 3 * 4 * 64; e += 512) {  // [j][fc][lane]
+    const int j = e >> 8, fc = (e >> 6) & 3, l = e & 63;
+    wlds[e] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
+                                            wrs, ((fc * 16 + (l & 15)) * a.K_pad + j * 32 + (l >> 4) * 8) * 2, 0, 0));
+  }
+  if (tid < 64) {
+    const float sc = a.scale ? a.scale[tid] : 1.f;
+    rmul[tid] = sc;
+    rmul[64 + tid] = (a.bias ? a.bias[tid] : 0.f) * sc + (a.shift ? a.shift[tid] : 0.f);
+  }
+  uint4* P = pat + wave * SP;
+  const bool aff = a.scale || a.shift;  // else the accumulators start at the bias and hold the logits
+  __syncthreads();  // the only block-wide barrier: the staged tables
+  int i = blockIdx.x;
+  uint4 nv[2];
+  if (i < ntiles) load_strip(tile_of(i), nv);
+  for (; i < ntiles; i += gridDim.x) {
+    const int t = tile_of(i);
+    const int n = t / (th * tw), srem = t - n * th * tw;
+    const int r = (srem / tw) * TH + wave, c0 = (srem - (srem / tw) * tw) * TW;
+    P[lane] = nv[0];
+    if (lane + 64 < SP) P[lane + 64] = nv[1];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (i + (int)gridDim.x < ntiles) load_strip(tile_of(i + gridDim.x), nv);
+    if (r >= H) continue;
+    f32x4 acc[4][2];
+    init_strip_acc(acc, rmul, aff, q);
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const int tap = 4 * j + q;
+      const int toff = (tap / 3) * PW + tap % 3;
+      uint4 bv[2];
+#pragma unroll
+      for (int fp = 0; fp < 2; ++fp) {
+        const uint4 v = P[fp * 16 + col + (tap < 9 ? toff : 0)];
+        bv[fp] = tap < 9 ? v : make_uint4(0, 0, 0, 0);
+      }
+#pragma unroll
+      for (int fc = 0; fc < 4; ++fc) {
+        const uint4 wv = wlds[(j * 4 + fc) * 64 + lane];
+#pragma unroll
+        for (int fp = 0; fp < 2; ++fp) mma16<T>(wv, bv[fp], acc[fc][fp]);
+      }
+    }
+    float* yb = reinterpret_cast<float*>(a.y) + a.y_coff + (((long)n * H + r) * W + c0) * (long)a.y_cstride;
+    if (aff) softmax_store_strip<true>(acc, rmul, stg + wave * 16 * SRF, yb, a.y_cstride, W - c0, lane);
+    else softmax_store_strip<false>(acc, rmul, stg + wave * 16 * SRF, yb, a.y_cstride, W - c0, lane);
+  }
+}
+
+// ================================================================ refine conv4 + softmax in f32 (refine.py:27-32)
+// The reference's precision for config 3: f32 input row [cmp, alpha, warped] (CIN <= 8 of an 8-channel pixel), exact
+// f32 products on v_mfma_f32_16x16x4_f32, f32 sums, f32 softmax.  K is COMPACT: k = tap * CIN + c over the 9 * CIN
+// real taps (45 for the refine's CIN 5 -> 12 four-deep MFMA steps instead of the 18 of the padded 72); the lane in
+// k-slot q of step s reads tap (4s+q) / CIN, channel (4s+q) % CIN.
+// Work unit = one wave's STRIP (1 output row x 32 px x 64 channels): the wave stages its own 3 x 34 px patch in LDS as
+// channel planes (the 16 lanes of a k-slot read 16 consecutive pixels: conflict-free) and never waits for the other
+// waves, so one wave's MFMA phase (12 steps x 8 MFMAs of 32 cycles) runs under another's softmax + store phase; a
+// block-wide barrier per tile had serialised the two (0.225 ms at 1080p).  The 8 waves of a block take the 8 rows of
+// one 8 x 32 tile (their halo rows meet in L1/L2), tiles walk persistently in XCD bands.  Weights and per-lane patch
+// offsets are staged once per block ([step][lane] records: one ds_read_b128 for the 4 cout fragments + one offset);
+// the next strip's pixels are prefetched into registers.  Softmax + per-wave LDS transpose + whole-pixel nontemporal
+// stores as in conv3x3_first_softmax.
+template <int CIN>
+__global__ __launch_bounds__(512, 4) void conv3x3_first_softmax_f32(ConvArgs a) {
+  constexpr int NS = (9 * CIN + 3) / 4;
+  constexpr int TH = 8, TW = 32, PW = TW + 2, SP = 3 * PW;  // strip patch: 3 rows x 34 px
+  constexpr int WPF = (CIN * SP + 32 + 3) / 4 * 4;            // per-wave patch floats (+ 32 zeros)
+  constexpr int ZERO = CIN * SP;
+  constexpr int SRF = 68;  // staging row: 64 floats + 4
+  __shared__ __attribute__((aligned(16))) f32x4 wl[NS * 64];
+  __shared__ int pl[NS * 4];
+  __shared__ __attribute__((aligned(16))) float rmul[2 * 64];
+  __shared__ __attribute__((aligned(16))) float pat[8 * WPF];
+  __shared__ __attribute__((aligned(16))) float stg[8 * 16 * SRF];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int H = a.H, W = a.W, cs = a.x_cstride;
+  const int th = (H + TH - 1) / TH, tw = (W + TW - 1) / TW;
+  const int ntiles = a.tiles_total;
+  auto tile_of = [&](int i) {
+    const int base = (i / a.tiles_n) * a.tiles_n;
+    return base + a.tiles_n <= ntiles ? base + xcd_tile(i - base, a.tiles_n) : i;
+  };
+  // this wave's strip of tile t: rows r - 1 .. r + 1 (r = tile row 0 + wave), pixels c0 - 1 .. c0 + 32; lane e (and
+  // e + 64) fetch patch pixel e
+  auto load_strip = [&](int t, float4 (&v)[2][2]) {
+    const int n = t / (th * tw), srem = t - n * th * tw;
+    const int r = (srem / tw) * TH + wave, c0 = (srem - (srem / tw) * tw) * TW;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int e = lane + 64 * k;
+      const int pr = e / PW, pc = e - pr * PW;
+      const int h = r - 1 + pr, w = c0 - 1 + pc;
+      const bool ok = e < SP && (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
+      const float* xp = reinterpret_cast<const float*>(a.x) + a.x_coff + ((long)n * H + (ok ? h : 0)) * (long)W * cs +
+                        (long)(ok ? w : 0) * cs;
+      v[k][0] = ok ? *reinterpret_cast<const float4*>(xp) : make_float4(0.f, 0.f, 0.f, 0.f);
+      v[k][1] = ok && CIN > 4 ? *reinterpret_cast<const float4*>(xp + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
   };
   const int col = lane & 15, q = lane >> 4;
   const float* Wt = reinterpret_cast<const float*>(a.w);
@@ -1797,41 +1969,45 @@ __global__ __launch_bounds__(512, 4) void conv3x3_first_softmax_f32(ConvArgs a) 
   if (tid < NS * 4) {
     const int kk = tid;  // step tid / 4, k-slot tid % 4
     const int tap = kk / CIN, c = kk - tap * CIN;
-    pl[tid] = kk < 9 * CIN ? c * PPIX + (tap / 3) * PW + tap % 3 : -1;
+    pl[tid] = kk < 9 * CIN ? c * SP + (tap / 3) * PW + tap % 3 : ZERO;  // k past 9 * CIN: 32 zeros
   }
-  if (tid < 4) patch[ZERO + tid] = 0.f;
+  float* P = pat + wave * WPF;
+  if (lane < 32) P[ZERO + lane] = 0.f;
   if (tid < 64) {
     const float sc = a.scale ? a.scale[tid] : 1.f;
     rmul[tid] = sc;
     rmul[64 + tid] = (a.bias ? a.bias[tid] : 0.f) * sc + (a.shift ? a.shift[tid] : 0.f);
   }
+  const bool aff = a.scale || a.shift;  // else the accumulators start at the bias and hold the logits
+  __syncthreads();  // the only block-wide barrier: the staged tables
   int i = blockIdx.x;
-  float4 nlo = make_float4(0.f, 0.f, 0.f, 0.f), nhi = nlo;
-  if (i < ntiles) load_patch(tile_of(i), nlo, nhi);
+  float4 nv[2][2];
+  if (i < ntiles) load_strip(tile_of(i), nv);
   for (; i < ntiles; i += gridDim.x) {
     const int t = tile_of(i);
     const int n = t / (th * tw), srem = t - n * th * tw;
-    const int r0 = (srem / tw) * TH, c0 = (srem - (srem / tw) * tw) * TW;
-    __syncthreads();  // the previous tile's patch reads are done (first tile: the staged tables are written)
-    if (tid < PPIX) {
-      const float v[8] = {nlo.x, nlo.y, nlo.z, nlo.w, nhi.x, nhi.y, nhi.z, nhi.w};
+    const int r = (srem / tw) * TH + wave, c0 = (srem - (srem / tw) * tw) * TW;
 #pragma unroll
-      for (int c = 0; c < CIN; ++c) patch[c * PPIX + tid] = v[c];
+    for (int k = 0; k < 2; ++k) {
+      const int e = lane + 64 * k;
+      const float v[8] = {nv[k][0].x, nv[k][0].y, nv[k][0].z, nv[k][0].w, nv[k][1].x, nv[k][1].y, nv[k][1].z, nv[k][1].w};
+      if (e < SP)
+#pragma unroll
+        for (int c = 0; c < CIN; ++c) P[c * SP + e] = v[c];
     }
-    __syncthreads();
-    if (i + (int)gridDim.x < ntiles) load_patch(tile_of(i + gridDim.x), nlo, nhi);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (i + (int)gridDim.x < ntiles) load_strip(tile_of(i + gridDim.x), nv);
+    if (r >= H) continue;  // a strip below the frame (wave-uniform): nothing to compute or store
 
     f32x4 acc[4][2];
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-#pragma unroll
-      for (int fp = 0; fp < 2; ++fp) acc[k][fp] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const int prow = wave * PW + col;  // patch row `wave` (+ the tap's kernel row in the offset)
+    init_strip_acc(acc, rmul, aff, q);
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
       const f32x4 w4 = wl[s * 64 + lane];
       const int po = pl[s * 4 + q];
-      const float b0 = patch[po < 0 ? ZERO : po + prow], b1 = patch[po < 0 ? ZERO : po + prow + 16];
+      const float b0 = P[po + col], b1 = P[po + 16 + col];
 #pragma unroll
       for (int fc = 0; fc < 4; ++fc) {
         acc[fc][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(w4[fc], b0, acc[fc][0], 0, 0, 0);
@@ -1839,56 +2015,9 @@ __global__ __launch_bounds__(512, 4) void conv3x3_first_softmax_f32(ConvArgs a) 
       }
     }
 
-    const int ycs = a.y_cstride;
-    float* yb = reinterpret_cast<float*>(a.y) + a.y_coff + (((long)n * H + r0 + wave) * W + c0) * (long)ycs;
-#pragma unroll
-    for (int fp = 0; fp < 2; ++fp) {
-      float v[4][4];
-      float mx = -INFINITY;
-#pragma unroll
-      for (int fc = 0; fc < 4; ++fc) {
-        const float4 m4 = *reinterpret_cast<const float4*>(rmul + fc * 16 + 4 * q);
-        const float4 a4 = *reinterpret_cast<const float4*>(rmul + 64 + fc * 16 + 4 * q);
-        const float mul[4] = {m4.x, m4.y, m4.z, m4.w}, add[4] = {a4.x, a4.y, a4.z, a4.w};
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj) {
-          v[fc][jj] = fmaf(acc[fc][fp][jj], mul[jj], add[jj]);
-          mx = fmaxf(mx, v[fc][jj]);
-        }
-      }
-      mx = fmaxf(mx, __shfl_xor(mx, 16));
-      mx = fmaxf(mx, __shfl_xor(mx, 32));
-      float sum = 0.f;
-#pragma unroll
-      for (int fc = 0; fc < 4; ++fc)
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj) {
-          v[fc][jj] = expf(v[fc][jj] - mx);
-          sum += v[fc][jj];
-        }
-      sum += __shfl_xor(sum, 16);
-      sum += __shfl_xor(sum, 32);
-      const float inv = 1.f / sum;
-      float* ws = stg + wave * 16 * SRF;
-#pragma unroll
-      for (int fc = 0; fc < 4; ++fc)
-        *reinterpret_cast<f32x4*>(ws + col * SRF + fc * 16 + 4 * q) =
-            f32x4{v[fc][0] * inv, v[fc][1] * inv, v[fc][2] * inv, v[fc][3] * inv};
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-      for (int it = 0; it < 4; ++it) {  // lane l: pixel 4*it + l/16, channels 4*(l%16) .. +3
-        const int px = 4 * it + (lane >> 4), ch = 4 * (lane & 15);
-        const f32x4 o = *reinterpret_cast<const f32x4*>(ws + px * SRF + ch);
-        const int pc = fp * 16 + px;
-        if (r0 + wave < H && c0 + pc < W)
-          __builtin_nontemporal_store(o, reinterpret_cast<f32x4*>(yb + (long)pc * ycs + ch));
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    }
+    float* yb = reinterpret_cast<float*>(a.y) + a.y_coff + (((long)n * H + r) * W + c0) * (long)a.y_cstride;
+    if (aff) softmax_store_strip<true>(acc, rmul, stg + wave * 16 * SRF, yb, a.y_cstride, W - c0, lane);
+    else softmax_store_strip<false>(acc, rmul, stg + wave * 16 * SRF, yb, a.y_cstride, W - c0, lane);
   }
 }
 
@@ -2910,9 +3039,10 @@ static int launch_first(ConvArgs& a, hipStream_t st) {
   return check_launch("conv3x3_first");
 }
 
-static int g_softmax_kernel = 4;  // 0: the generic kernels' softmax epilogue, 1: conv3x3_first_softmax, 2: its NT form,
-                                  // 3 / 4: plain / NT with the per-wave LDS transpose (whole-pixel stores)
-static long g_softmax_blocks = 1024;  // persistent grid of conv3x3_first_softmax
+static int g_softmax_kernel = 6;  // 0: the generic kernels' softmax epilogue, 1: conv3x3_first_softmax, 2: its NT form,
+                                  // 3 / 4: plain / NT with the per-wave LDS transpose (whole-pixel stores), 5: 4 with
+                                  // LDS weights, 6: wave-private strips (conv3x3_first_softmax_strip, default)
+static long g_softmax_blocks = 2048;  // persistent grid of conv3x3_first_softmax*
 static long g_pair_xin_wide = 1;  // pair kernel, f32 frames with >= 4 channels: two 16-byte loads per pixel (XIN 2)
 
 static int launch_first_softmax(ConvArgs& a, hipStream_t st) {
@@ -2930,6 +3060,9 @@ static int launch_first_softmax(ConvArgs& a, hipStream_t st) {
   } else if (g_softmax_kernel == 4) {
     snprintf(g_last_kernel, sizeof g_last_kernel, "vm::conv3x3_first_softmax<true, true>");
     hipLaunchKernelGGL((conv3x3_first_softmax<true, true>), dim3(grid), dim3(512), 0, st, a);
+  } else if (g_softmax_kernel == 6) {
+    snprintf(g_last_kernel, sizeof g_last_kernel, "vm::conv3x3_first_softmax_strip");
+    hipLaunchKernelGGL(conv3x3_first_softmax_strip, dim3(grid), dim3(512), 0, st, a);
   } else if (g_softmax_kernel == 5) {
     snprintf(g_last_kernel, sizeof g_last_kernel, "vm::conv3x3_first_softmax<true, true, true>");
     hipLaunchKernelGGL((conv3x3_first_softmax<true, true, true>), dim3(grid), dim3(512), 0, st, a);
@@ -3004,7 +3137,7 @@ extern "C" int vm_set_option(const char* key, long value) {
     return VM_OK;
   }
   if (!strcmp(key, "softmax_kernel")) {
-    if (value < 0 || value > 5) return fail(VM_EINVAL, "softmax_kernel must be 0..5");
+    if (value < 0 || value > 6) return fail(VM_EINVAL, "softmax_kernel must be 0..6");
     g_softmax_kernel = value;
     return VM_OK;
   }

@@ -351,9 +351,68 @@ class VideoTrainer:
         self.apply_gradients()
         return tb["loss"].clone()
 
+    def capture(self, cmp, bg, warped, gt, raw_fg):
+        """Record one step's forward + loss and its backward over batches shaped like these as two HIP graphs
+        (torch.cuda.CUDAGraph over the same C-ABI launches) -> a TrainGraph.  Its step() copies a batch in, replays
+        both and runs the DDP exchange + Adam + re-pack eagerly (their host-side bias correction changes every
+        step), so the ~300 launches of a step cost one host call each way.  The graphs read the trainer's
+        parameters, packs and buffers in place, so updates made by apply_gradients are seen by the next replay."""
+        return TrainGraph(self, cmp, bg, warped, gt, raw_fg)
+
     def params_numpy(self):
         """{scope: (w, b|None)} and {scope: (gamma, beta)} on the host (checkpointing / inference hand-off)."""
         conv = {s: (self.P[s, "w"].cpu().numpy(), self.P[s, "b"].cpu().numpy() if (s, "b") in self.P else None)
                 for s, _, _ in NEW_CONVS}
         bn = {s: (self.P[s, "gamma"].cpu().numpy(), self.P[s, "beta"].cpu().numpy()) for s in self.model.bn}
         return conv, bn
+
+
+class TrainGraph:
+    """VideoTrainer.capture's result: ``step(cmp, bg, warped, gt, raw_fg)`` = VideoTrainer.step on graph replays;
+    ``inputs`` are the static batch buffers the graphs read."""
+
+    def __init__(self, trn, *batch):
+        if trn.sync_bn and torch.distributed.get_backend() != "nccl":
+            raise NotImplementedError("capture with sync_bn needs the nccl (RCCL) backend: gloo collectives are not "
+                                      "graph-capturable")
+        dev = trn.device
+        self.trn = trn
+        self.inputs = [(t if isinstance(t, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(t, np.float32)))
+                       .to(dev, torch.float32).contiguous().clone() for t in batch]
+        side = torch.cuda.Stream(device=dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):  # lazily built buffers / workspaces, no parameter update
+            self._forward()
+            self._backward()
+        torch.cuda.current_stream(dev).wait_stream(side)
+        torch.cuda.synchronize(dev)
+        self.g_fwd, self.g_bwd = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.g_fwd):
+            self._forward()
+        with torch.cuda.graph(self.g_bwd):
+            self._backward()
+
+    def _forward(self):
+        cmp, bg, warped, gt, fg = self.inputs
+        t = self.trn
+        t.forward(cmp, bg, warped)
+        t._tb["loss"].copy_(ops.matting_loss(t._tb["alpha"], gt, fg, bg, cmp))
+
+    def _backward(self):
+        cmp, bg, warped, gt, fg = self.inputs
+        self.trn.grad.zero_()
+        self.trn.backward(gt, fg, bg, cmp)
+
+    def load(self, *batch):
+        for dst, src in zip(self.inputs, batch):
+            dst.copy_(src if isinstance(src, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(src, np.float32)))
+
+    def step(self, *batch):
+        """One training iteration on graph replays; returns [loss, alpha_loss, compositional_loss] (pre-update)."""
+        if batch:
+            self.load(*batch)
+        self.g_fwd.replay()
+        self.g_bwd.replay()
+        self.trn.apply_gradients()
+        return self.trn._tb["loss"].clone()
+
