@@ -66,6 +66,8 @@ const char* vm_last_error(void);
  *   "patch_cfg"      patch-kernel tiling override (0 = dispatcher's choice; 19, 22, 25, 30 = one of the tilings it
  *                    picks); the other sweep tilings and the timing-only ablations ("patch_ablate", "patch_rowslot",
  *                    "pair_kernel" 10..18, garbage results) exist only in the study build (`make study`), never here
+ *   "up_skip"        folded 2x upconvs: 1 = skip the exact-zero taps of the odd phases' filters (25 of 36 taps run,
+ *                    bit-identical, default), 0 = run all 36
  *   "src_span_limit" byte span of split sources the 32-bit-offset conv kernels take (default 0x7ffffff0; wider
  *                    spans return VM_EUNSUPPORTED and the caller materialises the concat); lowered by tests
  *   "conv_min_tiles" grid size (256-wide output tiles) from which auto uses the LDS-DMA kernel (default 128)

@@ -55,9 +55,10 @@ def _resize(x, oh, ow):
     x0 = np.floor(xs).astype(np.int64)
     y1 = np.minimum(y0 + 1, ih - 1)
     x1 = np.minimum(x0 + 1, iw - 1)
-    fy = torch.from_numpy((ys - np.floor(ys)).astype(np.float64))[None, :, None, None]
-    fx = torch.from_numpy((xs - np.floor(xs)).astype(np.float64))[None, None, :, None]
-    T = lambda a: torch.from_numpy(a)  # noqa: E731
+    dev = x.device
+    fy = torch.from_numpy((ys - np.floor(ys)).astype(np.float64))[None, :, None, None].to(dev)
+    fx = torch.from_numpy((xs - np.floor(xs)).astype(np.float64))[None, None, :, None].to(dev)
+    T = lambda a: torch.from_numpy(a).to(dev)  # noqa: E731
     tl = x[:, T(y0)][:, :, T(x0)]
     tr = x[:, T(y0)][:, :, T(x1)]
     bl = x[:, T(y1)][:, :, T(x0)]
@@ -67,8 +68,11 @@ def _resize(x, oh, ow):
     return top + (bot - top) * fy
 
 
-def train_step_grads(cmp, bg, warped, gt, raw_fg, vgg, params, bn=None, towers=None):
+def train_step_grads(cmp, bg, warped, gt, raw_fg, vgg, params, bn=None, towers=None, device="cpu"):
     """-> (loss terms (loss, alpha_loss, cmp_loss), alpha, grads {(scope, kind): ndarray})
+
+    device: where the float64 autograd runs ("cpu"; a GPU only for large test shapes — float64 there too, the
+    checker, not the product).
 
     params: {scope: (w_hwio, bias|None)} (models.unet_simple_params); bn: {scope: (gamma, beta)} or fresh (1, 0).
     kinds: 'w', 'b' (new_conv scopes), 'gamma', 'beta' — the trainable variables of unet_simple.py:19-42.
@@ -80,10 +84,12 @@ def train_step_grads(cmp, bg, warped, gt, raw_fg, vgg, params, bn=None, towers=N
     if towers is None:
         towers = [om.vgg16_tower(t, vgg) for t in (cmp, bg, warped)]
     elif "in9" in towers[0]:
-        in9 = f64(towers[0]["in9"])
-    cat = lambda k: torch.from_numpy(np.concatenate([f64(t[k]) for t in towers], -1))  # noqa: E731
+        in9 = towers[0]["in9"]
+    # tower features may be numpy arrays or tensors (a device test hands over the trainer's own, already on device)
+    dd = lambda a: a.to(device, torch.float64) if isinstance(a, torch.Tensor) else torch.from_numpy(f64(a)).to(device)  # noqa: E731,E501
+    cat = lambda k: torch.cat([dd(t[k]) for t in towers], -1)  # noqa: E731
     layers = {
-        "conv1": [torch.from_numpy(in9), cat("conv1_1"), cat("conv1_2")],
+        "conv1": [dd(in9), cat("conv1_1"), cat("conv1_2")],
         "conv2": [cat("conv2_1"), cat("conv2_2")],
         "conv3": [cat("conv3_1"), cat("conv3_2"), cat("conv3_3")],
         "conv4": [cat("conv4_1"), cat("conv4_2"), cat("conv4_3")],
@@ -91,15 +97,15 @@ def train_step_grads(cmp, bg, warped, gt, raw_fg, vgg, params, bn=None, towers=N
     }
     V = {}
     for scope, (w, b) in params.items():
-        V[scope, "w"] = torch.tensor(f64(w), requires_grad=True)
+        V[scope, "w"] = torch.tensor(f64(w), requires_grad=True, device=device)
         if not scope.startswith("upconv"):
-            V[scope, "b"] = torch.tensor(f64(b), requires_grad=True)
+            V[scope, "b"] = torch.tensor(f64(b), requires_grad=True, device=device)
     widths = {"upconv4": 96, "upconv3": 48, "upconv2": 32, "upconv1": 30}
     for scope, (w, b) in params.items():
         c = widths.get(scope, w.shape[3])
         g, be = (np.ones(c), np.zeros(c)) if bn is None or scope not in bn else bn[scope]
-        V[scope, "gamma"] = torch.tensor(f64(g), requires_grad=True)
-        V[scope, "beta"] = torch.tensor(f64(be), requires_grad=True)
+        V[scope, "gamma"] = torch.tensor(f64(g), requires_grad=True, device=device)
+        V[scope, "beta"] = torch.tensor(f64(be), requires_grad=True, device=device)
 
     def new_conv(x, s):
         return _bn(_conv(x, V[s, "w"], V[s, "b"]), V[s, "gamma"], V[s, "beta"])
@@ -113,15 +119,15 @@ def train_step_grads(cmp, bg, warped, gt, raw_fg, vgg, params, bn=None, towers=N
         catn = _bn(torch.cat(outs + [u], -1), V[up, "gamma"], V[up, "beta"])
         prev = torch.relu(new_conv(catn, conv))
     alpha = torch.sigmoid(new_conv(prev, "output"))
-    gt_t, fg_t, bg_t, cmp_t = (torch.from_numpy(f64(a)) for a in (gt, raw_fg, bg, cmp))
+    gt_t, fg_t, bg_t, cmp_t = (torch.from_numpy(f64(a)).to(device) for a in (gt, raw_fg, bg, cmp))
     eps2 = np.float64(np.float32(1e-6) ** 2)
     la = torch.sqrt((alpha - gt_t) ** 2 + eps2)
     lc = torch.sqrt((alpha * fg_t + (1 - alpha) * bg_t - cmp_t) ** 2 + eps2)
     loss = (0.5 * la + 0.5 * lc).mean()
     loss.backward()
-    grads = {k: v.grad.numpy().copy() for k, v in V.items()}
+    grads = {k: v.grad.cpu().numpy().copy() for k, v in V.items()}
     terms = (float(loss), float(la.mean()), float(lc.mean()))
-    return terms, alpha.detach().numpy(), grads
+    return terms, alpha.detach().cpu().numpy(), grads
 
 
 def adam_tf(var, m, v, grad, t, lr=1e-3, beta1=0.9, beta2=0.999, eps=1e-8):

@@ -369,6 +369,30 @@ def test_upconv_folded_resize(case, cfg):
         assert np.abs(y[sl] - unfused[sl]).max() <= 1e-2 * max(1.0, np.abs(unfused[sl]).max())
 
 
+@pytest.mark.parametrize("cfg", [0, 19, 22, 25])
+@pytest.mark.parametrize("case", [(1, 9, 13, 128, 64), (2, 7, 33, 256, 128), (1, 68, 120, 128, 64), (1, 3, 2, 32, 64)])
+def test_upconv_folded_zero_tap_skip_bit_identical(case, cfg):
+    """The folded upconv's odd phases have exactly-zero filter rows / columns (TF1 legacy 2x bilinear): skipping
+    those taps (up_skip 1, the default: 25 of 36 taps) gives bit-identical outputs to running all of them."""
+    from vmatting import _lib, ops
+    n, h, w, cin, cout = case
+    rs = np.random.RandomState(h * 7 + cin)
+    x = torch.from_numpy(rs.normal(size=(n, h, w, cin)).astype(np.float32)).to(torch.bfloat16).to(DEV)
+    wt = (rs.normal(size=(3, 3, cin, cout)) * np.sqrt(2.0 / (9 * cin))).astype(np.float32)
+    pc = ops.PackedConv(wt, (rs.normal(size=cout) * 0.1).astype(np.float32), torch.bfloat16, DEV)
+    outs = []
+    try:
+        _lib.set_option("patch_cfg", cfg)
+        for skip in (1, 0):
+            _lib.set_option("up_skip", skip)
+            outs.append(ops.upconv3x3(x, pc, "relu").clone())
+            assert _lib.last_conv_kernel().endswith("true>" if skip else "false>"), _lib.last_conv_kernel()
+    finally:
+        _lib.set_option("up_skip", 1)
+        _lib.set_option("patch_cfg", 0)
+    assert torch.equal(outs[0], outs[1])
+
+
 def test_upconv_fold_f32_uses_unfused_path():
     """f32 has no folded kernel: upconv3x3 runs resize + conv and stays within the f32 parity bound."""
     from vmatting import ops

@@ -704,3 +704,47 @@ def test_train_graph_step_equals_eager(dtype):
     assert all(np.array_equal(a, b) for a, b in zip(le, lg)), (le, lg)
     assert torch.equal(eager.flat, graphed.flat)
     assert torch.equal(eager.model.convs["conv2"].packed, graphed.model.convs["conv2"].packed)
+
+
+@pytest.mark.slow
+def test_train_step_bf16_gradients_bench_shape():
+    """the bf16 step's gradients at the bench's 8 x 320^2 batch, where the BN statistics run over
+    many pixels per channel, against float64 autograd (run on the GPU: test infrastructure) on the trainer's own bf16
+    tower features.  Bound, self-calibrated as in test_train_step_bf16_gradients but 2x tighter: per tensor relative
+    L2 <= 2x the f64 sensitivity to bf16-sized filter noise + 1e-2, gradient cosine >= 0.99."""
+    from vmatting.train import VideoTrainer
+    from vmatting.weights import synthetic_vgg16
+    n, h, w = 8, 320, 320
+    params = om.unet_simple_params(np.random.RandomState(1))
+    cmp, bg, warped, gt, fg = _batch(n, h, w, seed=17)
+    vgg = synthetic_vgg16(0)
+    trn = VideoTrainer(vgg, "bf16", DEV, params=params)
+    trn.forward(cmp, bg, warped)
+    trn.grad.zero_()
+    trn.backward(T(gt), T(fg), T(bg), T(cmp))
+    torch.cuda.synchronize()
+    b = trn.model._ws
+    towers = [{k[2:]: v[t * n:(t + 1) * n] for k, v in b.items() if k.startswith("t_conv")} for t in range(3)]
+    towers[0]["in9"] = b["in9"][..., :9]
+    _, _, grads = tr.train_step_grads(cmp, bg, warped, gt, fg, vgg, params, towers=towers, device=DEV)
+    rs = np.random.RandomState(7)
+    p2 = {k: (w_ * (1 + 2.0 ** -9 * rs.normal(size=w_.shape)).astype(np.float32), b_) for k, (w_, b_) in params.items()}
+    _, _, g2 = tr.train_step_grads(cmp, bg, warped, gt, fg, vgg, p2, towers=towers, device=DEV)
+    bad, got_all, ref_all, rows = [], [], [], []
+    for (scope, kind), g_ref in grads.items():
+        if kind == "b":
+            continue
+        g = H(trn.G[scope, kind])
+        nrm = max(np.linalg.norm(g_ref), 1e-30)
+        l2 = np.linalg.norm(g - g_ref) / nrm
+        sens = np.linalg.norm(g2[scope, kind] - g_ref) / nrm
+        got_all.append(g.ravel())
+        ref_all.append(g_ref.ravel())
+        rows.append("%s/%s %.3e (sens %.3e)" % (scope, kind, l2, sens))
+        if not l2 <= 2 * sens + 1e-2:
+            bad.append((scope, kind, round(float(l2), 4), round(float(sens), 4)))
+    a, b_ = np.concatenate(got_all), np.concatenate(ref_all)
+    cos = float(a @ b_ / (np.linalg.norm(a) * np.linalg.norm(b_)))
+    print("bf16 step 8x320^2: gradient cosine %.5f\n  %s" % (cos, "\n  ".join(rows)))
+    assert not bad, bad
+    assert cos >= 0.99

@@ -8,21 +8,27 @@ sys.path[:0] = [os.path.join(REPO, "video-matting_amd"), REPO]
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
-from vmatting import unet, video  # noqa: E402
+from vmatting import _lib, unet, video  # noqa: E402
 from vmatting.weights import synthetic_vgg16  # noqa: E402
 
 VARIANTS = {
     "default": {},
     "fold_up2": {"fold_upconv": ("upconv_2", "upconv_3", "upconv_4")},
     "nosplit": {"split_head": False},
+    "noskip": {"_opt": {"up_skip": 0}},  # folded upconvs without the zero-tap skipping
+    "fold_up2_noskip": {"fold_upconv": ("upconv_2", "upconv_3", "upconv_4"), "_opt": {"up_skip": 0}},
 }
 
 
 def run(name, steps=100):
     np.random.seed(0)
     m = unet.UNetVideo(synthetic_vgg16(0), dtype="bf16", device="cuda")
+    opts = VARIANTS[name].get("_opt", {})
     for k, v in VARIANTS[name].items():
-        setattr(m, k, v)
+        if k != "_opt":
+            setattr(m, k, v)
+    for k, v in opts.items():
+        _lib.set_option(k, v)
     m.prepare()
     x = video.synthetic_frames(1, 1080, 1920, first=0, device="cuda")
     g = m.capture(x)
@@ -33,7 +39,10 @@ def run(name, steps=100):
     for _ in range(steps):
         g.replay()
     torch.cuda.synchronize()
-    return 1000 * (time.perf_counter() - t0) / steps
+    ms = 1000 * (time.perf_counter() - t0) / steps
+    for k in opts:
+        _lib.set_option(k, {"up_skip": 1}.get(k, 0))
+    return ms
 
 
 if __name__ == "__main__":

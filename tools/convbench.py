@@ -69,8 +69,10 @@ def main():
         _lib.set_option(k, int(v))
     _lib.set_option("conv_kernel", args.kernel)
     _lib.set_option("glds_rb", args.glds_rb)
-    _lib.set_option("patch_cfg", args.patch_cfg)
-    _lib.set_option("patch_ablate", args.ablate)
+    if args.patch_cfg:
+        _lib.set_option("patch_cfg", args.patch_cfg)  # sweep tilings other than 19/22/25/30: the study build
+    if args.ablate:  # timing-only ablations exist in the study build only:
+        _lib.set_option("patch_ablate", args.ablate)  # VM_LIB_PATH=video-matting_amd/study/libvmatting_study.so
     shapes = [("shape",) + tuple(int(v) for v in s.split("x")) for s in args.shape]
     if args.unet_layers:
         shapes += UNET_1080

@@ -21,6 +21,7 @@
 
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
 #include <cstdio>
 
 #include "conv_common.h"
@@ -714,7 +715,9 @@ __device__ __forceinline__ void first_layer_patch(const ConvArgs& a, char* smem,
 // conv1_1 -> conv1_2): the prologue evaluates that first conv on the (TH+2) x (TW+2) patch straight into the two
 // granule buffers (zero outside the frame = the second conv's SAME padding), so the 64-channel activation never
 // touches HBM; the main loop then streams only weights.
-template <int BN, int WM, int WN, int S, int TH, int MINB, int UNR, bool PF, int ABL, bool FIRST, int G = 1>
+// UPSKIP: the folded-upconv instantiation (vm_conv3x3_up2x_nhwc), which skips its phase filters' zero taps
+template <int BN, int WM, int WN, int S, int TH, int MINB, int UNR, bool PF, int ABL, bool FIRST, int G = 1,
+          bool UPSKIP = false>
 __global__ __launch_bounds__(64 * WM * WN) __attribute__((amdgpu_waves_per_eu(MINB * WM * WN / 4)))
 void conv3x3_patch(ConvArgs a) {
   using C = PatchCfg<BN, WM, WN, S, TH, G>;
@@ -829,6 +832,13 @@ void conv3x3_patch(ConvArgs a) {
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
   };
+  // folded 2x resize: the TF1 legacy upsampling makes an odd output row (phase a = 1) a blend of low-res rows i and
+  // i+1 only, so its phase filter's kernel row 0 (offset -1) is exactly zero; likewise kernel column 0 for odd
+  // output columns (b = 1).  A block whose channels are one phase skips those taps' fragment reads and MFMAs:
+  // phases (0,0) / (0,1) / (1,0) / (1,1) run 9 / 6 / 6 / 4 of the 9 taps (25 of 36, bit-identical: the skipped
+  // products are exact zeros).  The weight DMA and the barriers keep their schedule.
+  const int up_phase = UPSKIP && a.up && n0 / a.up_cout == (n0 + BN - 1) / a.up_cout ? n0 / a.up_cout : 0;
+  const bool skip_r0 = (up_phase >> 1) != 0, skip_c0 = (up_phase & 1) != 0;
 
   if constexpr (G > 1) {
     // one ring slot = one kernel row (G = 3 taps): one barrier per row; inside the row the fragments of tap g+1 are
@@ -859,21 +869,23 @@ void conv3x3_patch(ConvArgs a) {
           ns -= ns >= S ? S : 0;
           issue_w(k + S - 1, ns);
         }
-        uint4 av[2][FC], bv[2][FP];
-        frags(av[0], bv[0], slot, cc & 1, r * G);
+        if (!(UPSKIP && skip_r0 && r == 0)) {  // (a folded upconv's zero kernel row: no reads, no MFMAs)
+          uint4 av[2][FC], bv[2][FP];
+          frags(av[0], bv[0], slot, cc & 1, r * G);
 #pragma unroll
-        for (int g = 0; g < G; ++g) {
-          if (g + 1 < G) frags(av[(g + 1) & 1], bv[(g + 1) & 1], slot, cc & 1, r * G + g + 1);
-          if constexpr (ABL & 1) {
+          for (int g = 0; g < G; ++g) {
+            if (g + 1 < G) frags(av[(g + 1) & 1], bv[(g + 1) & 1], slot, cc & 1, r * G + g + 1);
+            if constexpr (ABL & 1) {
 #pragma unroll
-            for (int fc = 0; fc < FC; ++fc) asm volatile("" ::"v"(av[g & 1][fc].x), "v"(av[g & 1][fc].w));
+              for (int fc = 0; fc < FC; ++fc) asm volatile("" ::"v"(av[g & 1][fc].x), "v"(av[g & 1][fc].w));
 #pragma unroll
-            for (int fp = 0; fp < FP; ++fp) asm volatile("" ::"v"(bv[g & 1][fp].x), "v"(bv[g & 1][fp].w));
-          } else {
+              for (int fp = 0; fp < FP; ++fp) asm volatile("" ::"v"(bv[g & 1][fp].x), "v"(bv[g & 1][fp].w));
+            } else if (!(UPSKIP && skip_c0 && g == 0)) {  // (its zero kernel column: no MFMAs)
 #pragma unroll
-            for (int fc = 0; fc < FC; ++fc)
+              for (int fc = 0; fc < FC; ++fc)
 #pragma unroll
-              for (int fp = 0; fp < FP; ++fp) mma16<T>(av[g & 1][fc], bv[g & 1][fp], acc[fc][fp]);
+                for (int fp = 0; fp < FP; ++fp) mma16<T>(av[g & 1][fc], bv[g & 1][fp], acc[fc][fp]);
+            }
           }
         }
         // schedule experiments (ABL 16 / 32): pin the order of the row's fragment reads and MFMAs
@@ -946,7 +958,7 @@ void conv3x3_patch(ConvArgs a) {
         }
         uint4 av[FC], bv[FP];
         frags(av, bv, slot, cc & 1, tap);
-        if constexpr (!(ABL & 1)) {
+        if constexpr (!(ABL & 1)) {  // (no zero-tap skipping here: it made this pipeline spill)
 #pragma unroll
           for (int fc = 0; fc < FC; ++fc)
 #pragma unroll
@@ -2800,7 +2812,7 @@ static int launch_glds(ConvArgs& a, hipStream_t st) {
 }
 
 template <int BN, int WM, int WN, int S, int TH = 8, int MINB = 1, int UNR = 9, bool PF = false, int ABL = 0,
-          bool FIRST = false, int G = 1>
+          bool FIRST = false, int G = 1, bool UPSKIP = false>
 static int launch_patch(ConvArgs& a, hipStream_t st) {
   using C = PatchCfg<BN, WM, WN, S, TH, G>;
   static_assert(!(FIRST && PF), "FIRST uses the plain pipeline");
@@ -2808,7 +2820,7 @@ static int launch_patch(ConvArgs& a, hipStream_t st) {
   static bool attr_set = false;
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute(
-        reinterpret_cast<const void*>(&conv3x3_patch<BN, WM, WN, S, TH, MINB, UNR, PF, ABL, FIRST, G>),
+        reinterpret_cast<const void*>(&conv3x3_patch<BN, WM, WN, S, TH, MINB, UNR, PF, ABL, FIRST, G, UPSKIP>),
         hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (e != hipSuccess) return fail(VM_EHIP, "hipFuncSetAttribute(patch): %s", hipGetErrorString(e));
     attr_set = true;
@@ -2818,11 +2830,22 @@ static int launch_patch(ConvArgs& a, hipStream_t st) {
   a.tiles_n = (a.cout + BN - 1) / BN;
   if (sp * a.tiles_n > 0x7fffffffL) return fail(VM_EUNSUPPORTED, "conv3x3: too many tiles");
   a.tiles_total = (int)(sp * a.tiles_n);
-  snprintf(g_last_kernel, sizeof g_last_kernel, "vm::conv3x3_patch<%d, %d, %d, %d, %d, %d, %d, %s, %d, %s, %d>", BN, WM,
-           WN, S, TH, MINB, UNR, PF ? "true" : "false", ABL, FIRST ? "true" : "false", G);
-  hipLaunchKernelGGL((conv3x3_patch<BN, WM, WN, S, TH, MINB, UNR, PF, ABL, FIRST, G>),
+  snprintf(g_last_kernel, sizeof g_last_kernel, "vm::conv3x3_patch<%d, %d, %d, %d, %d, %d, %d, %s, %d, %s, %d, %s>", BN,
+           WM, WN, S, TH, MINB, UNR, PF ? "true" : "false", ABL, FIRST ? "true" : "false", G, UPSKIP ? "true" : "false");
+  hipLaunchKernelGGL((conv3x3_patch<BN, WM, WN, S, TH, MINB, UNR, PF, ABL, FIRST, G, UPSKIP>),
                      dim3(a.tiles_total, a.ksplit > 1 ? a.ksplit : 1), dim3(C::NT), lds, st, a);
   return check_launch("conv3x3_patch");
+}
+
+static long g_up_skip = 1;  // vm_set_option "up_skip": 0 runs the folded upconvs without the zero-tap skipping (A/B)
+
+// a shipped tiling: the folded-upconv instantiation (zero phase taps skipped, row-slot pipeline G = 3) for a.up,
+// else the plain one
+template <int BN, int WM, int WN, int S, int TH = 8, int MINB = 1, int UNR = 9, bool PF = false, int ABL = 0,
+          bool FIRST = false, int G = 1>
+static int launch_patch_up(ConvArgs& a, hipStream_t st) {
+  if (G > 1 && a.up && g_up_skip) return launch_patch<BN, WM, WN, S, TH, MINB, UNR, PF, ABL, FIRST, G, (G > 1)>(a, st);
+  return launch_patch<BN, WM, WN, S, TH, MINB, UNR, PF, ABL, FIRST, G, false>(a, st);
 }
 
 // split-K plan of a patch-kernel conv: small grids (under g_splitk_tiles 4 x 32 pixel x 64 channel tiles) with a
@@ -2939,10 +2962,10 @@ static int dispatch_patch(ConvArgs& a, hipStream_t st) {
 #endif
   switch (g_patch_cfg) {
     // the tilings the dispatcher below picks (the only ones in the shipped library)
-    case 19: return launch_patch<64, 8, 1, 3, 8, 1, 9, false, 0, false, 3>(a, st);
-    case 22: return launch_patch<64, 8, 1, 2, 8, 1, 9, false, 0, false, 3>(a, st);
-    case 25: return launch_patch<64, 4, 1, 2, 4, 2, 9, false, 0, false, 3>(a, st);
-    case 30: return launch_patch<128, 4, 2, 3, 8, 2>(a, st);
+    case 19: return launch_patch_up<64, 8, 1, 3, 8, 1, 9, false, 0, false, 3>(a, st);
+    case 22: return launch_patch_up<64, 8, 1, 2, 8, 1, 9, false, 0, false, 3>(a, st);
+    case 25: return launch_patch_up<64, 4, 1, 2, 4, 2, 9, false, 0, false, 3>(a, st);
+    case 30: return launch_patch_up<128, 4, 2, 3, 8, 2>(a, st);
 #ifdef VM_STUDY
     // study build only (make study): every tiling of the r01/r02 sweeps (scripts/sweep.sh, scripts/conv_study.sh)
     case 1: return launch_patch<64, 4, 1, 6>(a, st);
@@ -3009,11 +3032,12 @@ static int dispatch_patch(ConvArgs& a, hipStream_t st) {
     return launch_patch<64, 8, 1, 6>(a, st);
   }
 #endif
-  if (a.cout >= 128 && a.cin_pad >= 512 && sp * ((a.cout + 127) / 128) >= 1000)
-    return launch_patch<128, 4, 2, 3, 8, 2>(a, st);  // 64 px x 64 channel waves, 4 per SIMD (r02: -5% vs 4x1 waves)
-  if (blocks64 >= 8000) return launch_patch<64, 8, 1, 3, 8, 1, 9, false, 0, false, 3>(a, st);
-  if (blocks64 < 512) return launch_patch<64, 4, 1, 2, 4, 2, 9, false, 0, false, 3>(a, st);  // L5: 4 x 32 px tiles
-  return launch_patch<64, 8, 1, 2, 8, 1, 9, false, 0, false, 3>(a, st);
+  // (a folded upconv takes the row-slot configs below, whose instantiation skips its phases' zero taps)
+  if (!(a.up && g_up_skip) && a.cout >= 128 && a.cin_pad >= 512 && sp * ((a.cout + 127) / 128) >= 1000)
+    return launch_patch_up<128, 4, 2, 3, 8, 2>(a, st);  // 64 px x 64 channel waves, 4 per SIMD (r02: -5% vs 4x1)
+  if (blocks64 >= 8000) return launch_patch_up<64, 8, 1, 3, 8, 1, 9, false, 0, false, 3>(a, st);
+  if (blocks64 < 512) return launch_patch_up<64, 4, 1, 2, 4, 2, 9, false, 0, false, 3>(a, st);  // L5: 4 x 32 px tiles
+  return launch_patch_up<64, 8, 1, 2, 8, 1, 9, false, 0, false, 3>(a, st);
 }
 
 template <typename T, bool FAST>
@@ -3166,6 +3190,11 @@ extern "C" int vm_set_option(const char* key, long value) {
   }
   if (!strcmp(key, "rows_min_blocks")) {
     g_rows_min_blocks = value;
+    return VM_OK;
+  }
+  if (!strcmp(key, "up_skip")) {
+    if (value < 0 || value > 1) return fail(VM_EINVAL, "up_skip must be 0 or 1");
+    g_up_skip = value;
     return VM_OK;
   }
   if (!strcmp(key, "src_span_limit")) {
