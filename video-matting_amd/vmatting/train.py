@@ -69,7 +69,7 @@ class VideoTrainer:
     """train.video_procedure's iteration on device (also simple_procedure's: pass diff = cmp - bg as ``warped``)."""
 
     def __init__(self, vgg16_npy_path=None, dtype="fp32", device="cuda", params=None, bn=None, lr=1e-3,
-                 beta1=0.9, beta2=0.999, epsilon=1e-8, sync_bn=False):
+                 beta1=0.9, beta2=0.999, epsilon=1e-8, sync_bn=False, streams=3):
         self.vgg = vgg16_npy_path if isinstance(vgg16_npy_path, Vgg16) else Vgg16(vgg16_npy_path, dtype, device)
         self.model = UNetSimple(self.vgg, True, dtype, device, params)
         self.device = self.model.device
@@ -78,6 +78,14 @@ class VideoTrainer:
         # reference normalises its whole batch (unet_simple.py:25,41; params.py:8); one small all-reduce per BN
         # layer in the forward and one in the backward.  Off: per-replica statistics (plain DDP)
         self.sync_bn = bool(sync_bn) and parallel.world_size() > 1
+        # the select convs (unet_simple.py:120-139) read only the frozen towers' features and feed only their
+        # level's concat: their chains (conv -> BN forward; BN backward -> filter gradient) run on `streams` side
+        # streams beside the decoder chain, whose small deep-level kernels leave most of the chip idle.  Same
+        # kernels, same arithmetic (bit-identical); events order them, also inside a captured graph.  SyncBN keeps
+        # one stream (its collectives stay in one issue order)
+        dev_ = torch.device(device)
+        self._side = [] if self.sync_bn or streams < 1 or dev_.type != "cuda" else \
+            [torch.cuda.Stream(device=dev_) for _ in range(int(streams))]
         self.layout, n = param_layout()
         dev = self.device
         self.flat = torch.zeros(n, dtype=torch.float32, device=dev)
@@ -221,11 +229,28 @@ class VideoTrainer:
         L = _levels(h, w)
         m.load_inputs(b, xs)
         m._towers(b)
+        main = torch.cuda.current_stream(self.device) if self._side else None
+        done = {}
+        if self._side:  # every level's select chains, queued on the side streams right after the towers
+            for st in self._side:
+                st.wait_stream(main)
+            for lv, cat, width, sels, up, prev, conv, out_key in LEVELS:
+                c, off, done[lv] = b[cat][..., :width], 0, []
+                for i, (s, src) in enumerate(sels):
+                    co = m.convs[s].cout
+                    st = self._side[i % len(self._side)]
+                    with torch.cuda.stream(st):
+                        self._new_conv(self._src(b, src), s, "relu", c[..., off:off + co], tb)
+                    ev = torch.cuda.Event()
+                    ev.record(st)
+                    done[lv].append(ev)
+                    off += co
         for lv, cat, width, sels, up, prev, conv, out_key in LEVELS:
             c, off = b[cat][..., :width], 0
             for s, src in sels:
                 co = m.convs[s].cout
-                self._new_conv(self._src(b, src), s, "relu", c[..., off:off + co], tb)
+                if not self._side:
+                    self._new_conv(self._src(b, src), s, "relu", c[..., off:off + co], tb)
                 off += co
             # upconv_concat (unet_simple.py:30-42): resize -> conv (no bias) -> relu -> concat -> BN
             r = b[RBUF[up]]
@@ -235,6 +260,8 @@ class VideoTrainer:
                 ops.resize_bilinear(b[prev], L[lv], out=r)
             pc, rx = m.conv(up, r)
             ops.conv3x3(rx, pc, "relu", out=c[..., off:width], affine=False, splitk=True)
+            for ev in done.get(lv, ()):
+                main.wait_event(ev)
             mean, var = tb["st_" + up]
             self._stats(c, mean, var)
             ops.bn_apply(c, mean, var, m.bn[up].gamma, m.bn[up].beta, EPS, "none", out=b[cat + "n"][..., :width])
@@ -292,6 +319,7 @@ class VideoTrainer:
     def backward(self, gt, raw_fg, bg, cmp):
         m, tb = self.model, self._tb
         b = m._ws
+        main = torch.cuda.current_stream(self.device) if self._side else None
         ops.matting_loss_backward(tb["alpha"], gt, raw_fg, bg, cmp, out=tb["dlogit"])
         dout = tb["dout_conv1"]
         self._conv_backward("output", b["c1"], tb["dlogit"], None, tb, dgrad_out=dout)
@@ -301,9 +329,15 @@ class VideoTrainer:
             mean, var = tb["st_" + up]
             self._bn_backward(c, tb["dcatn_" + up], None, mean, var, up, tb["dcat_" + up])
             dcat, off = tb["dcat_" + up], 0
-            for s, src in sels:
+            for i, (s, src) in enumerate(sels):
                 co = m.convs[s].cout
-                self._conv_backward(s, self._src(b, src), dcat[..., off:off + co], c[..., off:off + co], tb)
+                if self._side:  # leaves of the backward graph: beside the decoder chain, joined before the update
+                    st = self._side[i % len(self._side)]
+                    st.wait_stream(main)
+                    with torch.cuda.stream(st):
+                        self._conv_backward(s, self._src(b, src), dcat[..., off:off + co], c[..., off:off + co], tb)
+                else:
+                    self._conv_backward(s, self._src(b, src), dcat[..., off:off + co], c[..., off:off + co], tb)
                 off += co
             g16 = tb.get("g16_" + up)
             du = ops.relu_backward(dcat[..., off:width], c[..., off:width], tb["du_" + up],
@@ -315,6 +349,8 @@ class VideoTrainer:
                 else:
                     ops.conv3x3(du, self.dconv[up], "none", out=tb["dr_" + up], affine=False)
                 dout = ops.resize_backward(tb["dr_" + up], tb["dprev_" + up])
+        for st in self._side:  # every gradient is in place before the all-reduce / Adam that read them
+            main.wait_stream(st)
 
     # ------------------------------------------------------------------------------------------- update
     def apply_gradients(self):
