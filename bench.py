@@ -456,7 +456,7 @@ def train_flops(n, h, w):
     return fwd + head, head + dgrad
 
 
-def train_bench(dev, steps, warmup, world, rank, threads, cpu=True, n=8, size=320, dtype="bf16", graph=True):
+def train_bench(dev, steps, warmup, world, rank, threads, cpu=True, n=8, size=320, dtype="bf16", graph=False):
     """BASELINE config 5: one train.py video_procedure iteration per step (train.py:288-343) — batch of 8 320x320
     samples per GPU (params.py:8-9) resident in HBM: 3 VGG16 towers + UNetSimple (batch-statistics BN) forward,
     loss, backward through the trainable layers, one RCCL all-reduce of the gradients (DDP), TF-Adam, re-pack.
@@ -475,7 +475,8 @@ def train_bench(dev, steps, warmup, world, rank, threads, cpu=True, n=8, size=32
     cmp_d, bg_d, warped_d, gt_d, fg_d = T(cmp), T(bg - mean), T(warped), T(gt), T(fg)
     np.random.seed(1)
     trn = VideoTrainer(synthetic_vgg16(0), dtype, dev)
-    # forward + loss and backward replayed from HIP graphs (VideoTrainer.capture), DDP exchange + Adam eager
+    # eager launches (the select chains overlap the decoder on side streams); graph: forward + loss and backward
+    # replayed from HIP graphs (VideoTrainer.capture), DDP exchange + Adam eager
     g = trn.capture(cmp_d, bg_d, warped_d, gt_d, fg_d) if graph else None
     for _ in range(warmup):
         if g is not None:
@@ -561,7 +562,6 @@ def train_chain_bench(dev, steps, warmup, n=8, size=320, h=1080, w=1920, dtype="
     np.random.seed(7)
     trn = VideoTrainer(synthetic_vgg16(0), dtype, dev)
     names = ("cmp", "bg", "label", "warped", "fg")
-    tg = [None]
 
     def one(ev=None, wall=None):
         t0 = time.perf_counter()
@@ -576,10 +576,7 @@ def train_chain_bench(dev, steps, warmup, n=8, size=320, h=1080, w=1920, dtype="
         r = vl.compose_batch(samples, (size, size), names, device=dev)
         t2 = time.perf_counter()
         ev and ev.mark()
-        batch = (r["cmp"], r["bg"], r["warped"], r["label"], r["fg"])
-        if tg[0] is None:  # the step's forward / backward as HIP graphs (VideoTrainer.capture), captured once
-            tg[0] = trn.capture(*batch)
-        loss = tg[0].step(*batch)
+        loss = trn.step(r["cmp"], r["bg"], r["warped"], r["label"], r["fg"])
         ev and ev.mark()
         t3 = time.perf_counter()
         if wall is not None:
@@ -704,6 +701,9 @@ def main():
     ap.add_argument("--video-chunk", type=int, default=8, help="frames per HIP graph in the config-4 record")
     ap.add_argument("--option", action="append", default=[], metavar="KEY=VALUE",
                     help="vm_set_option kernel knob before the run (A/B comparisons), repeatable")
+    ap.add_argument("--train-graph", action="store_true",
+                    help="config-5 record from HIP-graph replays (VideoTrainer.capture) instead of eager launches: "
+                         "the step is not host-bound, and the graph runs the side-stream select chains serially")
     ap.add_argument("--only", choices=["train", "train_chain", "temporal"],
                     help="profiling passes: run just this record (rank 0 / N=1) and print it")
     ap.add_argument("--temporal-sizes", default="500x1200,1080x1920", help="config-3 sizes HxW, comma separated")
@@ -724,7 +724,7 @@ def main():
     cpu_model, threads = host_info()
     if args.only:  # one record alone (rocprofv3 passes per record: tools/prof_bench.sh)
         if args.only == "train":
-            rec = train_bench(dev, args.steps, args.warmup, world, rank, threads, cpu=False, graph=not args.no_graph)
+            rec = train_bench(dev, args.steps, args.warmup, world, rank, threads, cpu=False, graph=args.train_graph)
         elif args.only == "train_chain":
             rec = train_chain_bench(dev, args.steps, args.warmup)
         else:
@@ -794,7 +794,7 @@ def main():
     train = None
     if not args.no_train:  # every rank: the DDP all-reduce is part of the step
         train = train_bench(dev, max(args.steps // 4, 10), 3, world, rank, threads, cpu=not args.no_cpu_baseline,
-                            graph=not args.no_graph)
+                            graph=args.train_graph)
         if world == 1:
             train["chained"] = train_chain_bench(dev, 5, 2)
 

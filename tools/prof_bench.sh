@@ -53,7 +53,7 @@ done
 fi
 if ! skip train; then
 run 300 train.log rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/train" -o run \
-    -- python3 "$REPO/bench.py" --only train --steps 20 --warmup 3 "$@"
+    -- python3 "$REPO/bench.py" --only train --steps 20 --warmup 3 "$@"  # eager: side-stream select chains
 cp "$(find "$OUT/train" -name '*kernel_stats.csv' | head -n 1)" "$REPO/profiles/${TAG}_train_kernel_stats.csv"
 tail -n 1 "$OUT/train.log" > "$REPO/profiles/${TAG}_train.json"
 fi

@@ -874,19 +874,30 @@ static WmCfg wgrad_mfma_cfg(int cin, int cout) {
 template <int NCI, int NCO, bool SX, int TH>
 static int launch_wgrad_mfma_t(WgArgs& a, float* dw, hipStream_t st) {
   constexpr int lds = wgrad_mfma_lds<NCI, NCO, SX, TH>();
-  static bool attr = false;
-  if (!attr) {
+  static int attr_dev = -1, resident = 0;  // blocks of this variant resident on the whole chip at once
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (attr_dev != dev) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_mfma_kernel<NCI, NCO, SX, TH>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    if (e != hipSuccess) return fail(VM_EHIP, "hipFuncSetAttribute(wgrad_mfma): %s", hipGetErrorString(e));
-    attr = true;
+    int per_cu = 0, n_cu = 0;
+    if (e == hipSuccess)
+      e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(
+                                                           &wgrad_mfma_kernel<NCI, NCO, SX, TH>), 256, lds);
+    if (e == hipSuccess) e = hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
+    if (e != hipSuccess) return fail(VM_EHIP, "wgrad_mfma setup: %s", hipGetErrorString(e));
+    resident = per_cu * n_cu;
+    attr_dev = dev;
   }
   a.tiles_h = (a.h + TH - 1) / TH;
   a.tiles_w = (a.w + WM_TW - 1) / WM_TW;
   a.ntiles = (long)a.n * a.tiles_h * a.tiles_w;
   if (a.ntiles > 0x7fffffffL) return fail(VM_EUNSUPPORTED, "conv_wgrad: too many pixel tiles");
   const int ncc = (a.cin + NCI * 16 - 1) / (NCI * 16);
-  const long gx = wgrad_mfma_rows(a, NCI * 16);
+  // one round of blocks: the ~1024-block target (the workspace bound) cut to what is resident at once (160-VGPR
+  // variants: 3 blocks per CU), so no block waits for a second round (measured 2 x 72 us per select wgrad)
+  long gx = wgrad_mfma_rows(a, NCI * 16);
+  if (resident >= ncc && gx * ncc > resident) gx = resident / ncc;
   hipLaunchKernelGGL((wgrad_mfma_kernel<NCI, NCO, SX, TH>), dim3((unsigned)gx, ncc), dim3(256), lds, st, a);
   const long S = 9L * a.cin * a.cout;
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((S + 63) / 64)), dim3(1024), 0, st, a.part, (int)gx, S, dw);
