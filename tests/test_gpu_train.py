@@ -184,15 +184,24 @@ def test_bn_backward(mask):
                                          # near the launcher's limits (oh <= 4*ih) and the 1080p level sizes
                                          (3, 5, 12, 20), (7, 9, 25, 31), (68, 120, 135, 240),
                                          (135, 240, 270, 480), (4, 3, 13, 11), (5, 6, 19, 23)])
-def test_resize_backward(ih, iw, oh, ow):
+@pytest.mark.parametrize("c", [6, 8])
+def test_resize_backward(ih, iw, oh, ow, c):
+    """c = 8: the 4-channel vector kernel, bit-identical to the per-channel one (run on a 9-wide view of the same
+    values); both against float64 autograd."""
     from vmatting import ops
     rs = np.random.RandomState(ih)
-    dy = rs.normal(size=(2, oh, ow, 6)).astype(np.float32)
-    dx = torch.empty((2, ih, iw, 6), dtype=torch.float32, device=DEV)
+    dy = rs.normal(size=(2, oh, ow, c)).astype(np.float32)
+    dx = torch.empty((2, ih, iw, c), dtype=torch.float32, device=DEV)
     ops.resize_backward(T(dy), dx)
-    xr = torch.zeros((2, ih, iw, 6), dtype=torch.float64, requires_grad=True)
+    xr = torch.zeros((2, ih, iw, c), dtype=torch.float64, requires_grad=True)
     (tr._resize(xr, oh, ow) * torch.from_numpy(dy.astype(np.float64))).sum().backward()
     assert scaled_err(H(dx), xr.grad.numpy()) <= 1e-5
+    if c % 4 == 0:
+        wide = torch.zeros((2, oh, ow, c + 1), dtype=torch.float32, device=DEV)
+        wide[..., :c] = T(dy)
+        dx1 = torch.empty_like(dx)
+        ops.resize_backward(wide[..., :c], dx1)
+        assert torch.equal(dx1, dx)
 
 
 def test_relu_backward():

@@ -291,7 +291,19 @@ __global__ __launch_bounds__(256) void bn_partial_kernel(View x, double* part, i
   const long M = (long)x.n * x.h * x.w;
   double s = 0.0, ss = 0.0;
   if (c < x.c) {
-    for (long p = ((long)blockIdx.y * 4 + wave) * PPW + lane / CP; p < M; p += (long)nblk * 4 * PPW) {
+    const long stp = (long)nblk * 4 * PPW;
+    long p = ((long)blockIdx.y * 4 + wave) * PPW + lane / CP;
+    for (; p + 3 * stp < M; p += 4 * stp) {  // 4 loads in flight per lane (same summation order)
+      double v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = ldv(x, p + u * stp, c);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        s += v[u];
+        ss += v[u] * v[u];
+      }
+    }
+    for (; p < M; p += stp) {
       const double v = ldv(x, p, c);
       s += v;
       ss += v * v;
@@ -368,7 +380,19 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(View x, View y, const flo
   const float b = beta ? beta[c] : 0.f;
   const float r = 1.0f / sqrtf(v + eps);
   const long step = (long)gridDim.x * (blockDim.x / CP);
-  for (long p = (long)blockIdx.x * (blockDim.x / CP) + threadIdx.x / CP; p < M; p += step) {
+  long p = (long)blockIdx.x * (blockDim.x / CP) + threadIdx.x / CP;
+  for (; p + 3 * step < M; p += 4 * step) {  // 4 loads in flight before the stores (y may alias x: in place)
+    float t[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) t[u] = ldv(x, p + u * step, c);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      float v = (t[u] - m) * r * g + b;
+      v = act == VM_ACT_RELU ? fmaxf(v, 0.f) : act == VM_ACT_SIGMOID ? sigmoid_precise(v) : v;
+      stv(y, p + u * step, c, v);
+    }
+  }
+  for (; p < M; p += step) {
     float t = (ldv(x, p, c) - m) * r * g + b;
     t = act == VM_ACT_RELU ? fmaxf(t, 0.f) : act == VM_ACT_SIGMOID ? sigmoid_precise(t) : t;
     stv(y, p, c, t);

@@ -104,7 +104,27 @@ __global__ __launch_bounds__(256) void bn_bwd_partial(V x, V dy, V y, const floa
   if (c < dy.c) {
     const float m = x.p ? mean[c] : 0.f;
     const float r = x.p ? 1.0f / sqrtf(var[c] + eps) : 0.f;
-    for (long p = ((long)blockIdx.y * 4 + wave) * PPW + lane / CP; p < M; p += (long)nblk * 4 * PPW) {
+    const long stp = (long)nblk * 4 * PPW;
+    long p = ((long)blockIdx.y * 4 + wave) * PPW + lane / CP;
+    // 4 pixels' loads in flight per lane before any is summed (same summation order as one at a time)
+    for (; p + 3 * stp < M; p += 4 * stp) {
+      float g[4], xv[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        g[u] = grad_in<MASK>(dy, y, p + u * stp, c);
+        xv[u] = x.p ? ld(x, p + u * stp, c) : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        s1 += g[u];
+        if (x.p) {
+          const float xh = (xv[u] - m) * r;
+          s2 += (double)g[u] * (double)xh;
+          s3 += (double)xh;
+        }
+      }
+    }
+    for (; p < M; p += stp) {
       const float g = grad_in<MASK>(dy, y, p, c);
       s1 += g;
       if (x.p) {
@@ -194,7 +214,22 @@ __global__ __launch_bounds__(256) void bn_bwd_apply(V x, V dy, V y, const float*
   const float k = (gamma ? gamma[c] : 1.f) * r;
   const float sg = sum_g[c] * invM, sgx = sum_gx[c] * invM;
   const long step = (long)gridDim.x * (blockDim.x / CP);
-  for (long p = (long)blockIdx.x * (blockDim.x / CP) + threadIdx.x / CP; p < M; p += step) {
+  long p = (long)blockIdx.x * (blockDim.x / CP) + threadIdx.x / CP;
+  for (; p + 3 * step < M; p += 4 * step) {  // 4 pixels' loads in flight before the stores
+    float xv[4], g[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      xv[u] = ld(x, p + u * step, c);
+      g[u] = grad_in<MASK>(dy, y, p + u * step, c);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const float v = k * (g[u] - sg - (xv[u] - m) * r * sgx);
+      st(dx, p + u * step, c, v);
+      if (dx2.p) st(dx2, p + u * step, c, v);
+    }
+  }
+  for (; p < M; p += step) {
     const float xh = (ld(x, p, c) - m) * r;
     const float g = grad_in<MASK>(dy, y, p, c);
     const float v = k * (g - sg - xh * sgx);
@@ -209,7 +244,18 @@ __global__ __launch_bounds__(256) void relu_bwd_kernel(V dy, V y, V dx, V dx2) {
   const int c = blockIdx.y * CP + (threadIdx.x & (CP - 1));
   if (c >= dy.c) return;
   const long step = (long)gridDim.x * (blockDim.x / CP);
-  for (long p = (long)blockIdx.x * (blockDim.x / CP) + threadIdx.x / CP; p < M; p += step) {
+  long p = (long)blockIdx.x * (blockDim.x / CP) + threadIdx.x / CP;
+  for (; p + 3 * step < M; p += 4 * step) {  // 4 pixels' loads in flight before the stores
+    float v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = ld(y, p + u * step, c) > 0.f ? ld(dy, p + u * step, c) : 0.f;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      st(dx, p + u * step, c, v[u]);
+      if (dx2.p) st(dx2, p + u * step, c, v[u]);
+    }
+  }
+  for (; p < M; p += step) {
     const float v = ld(y, p, c) > 0.f ? ld(dy, p, c) : 0.f;
     st(dx, p, c, v);
     if (dx2.p) st(dx2, p, c, v);
@@ -279,6 +325,45 @@ __global__ void resize_bwd_kernel(V dy, float* dx, int ih, int iw, float sy, flo
       acc += wy * row;
     }
     dx[i] = acc;
+  }
+}
+
+// the same gather, 4 channels per thread with 16-byte loads / stores (c % 4 == 0, 16-byte aligned dy channel
+// vectors): the taps and weights are computed once per 4 channels; per channel the arithmetic is resize_bwd_kernel's
+__global__ void resize_bwd_kernel4(V dy, float* dx, int ih, int iw, float sy, float sx) {
+  const int C4 = dy.c / 4;
+  const long total = (long)dy.n * ih * iw * C4;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C4) * 4;
+    const long ip = i / C4;
+    const int ix = (int)(ip % iw);
+    const long t = ip / iw;
+    const int iy = (int)(t % ih);
+    const int n = (int)(t / ih);
+    const int r0 = max(0, (int)floorf((iy - 1) / sy) - 1), r1 = min(dy.h - 1, (int)ceilf((iy + 1) / sy) + 1);
+    const int q0 = max(0, (int)floorf((ix - 1) / sx) - 1), q1 = min(dy.w - 1, (int)ceilf((ix + 1) / sx) + 1);
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int oh = r0; oh <= r1; ++oh) {
+      const float wy = tap_w(oh, sy, ih, iy);
+      if (wy == 0.f) continue;
+      float4 row = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int ow = q0; ow <= q1; ++ow) {
+        const float wx = tap_w(ow, sx, iw, ix);
+        if (wx != 0.f) {
+          const float4 v = *reinterpret_cast<const float4*>(
+              reinterpret_cast<const float*>(dy.p) + (((long)n * dy.h + oh) * dy.w + ow) * dy.cs + dy.coff + c);
+          row.x += wx * v.x;
+          row.y += wx * v.y;
+          row.z += wx * v.z;
+          row.w += wx * v.w;
+        }
+      }
+      acc.x += wy * row.x;
+      acc.y += wy * row.y;
+      acc.z += wy * row.z;
+      acc.w += wy * row.w;
+    }
+    *reinterpret_cast<float4*>(dx + ip * dy.c + c) = acc;
   }
 }
 
@@ -1063,6 +1148,12 @@ extern "C" int vm_resize_bilinear_tf1_backward(const vm_tensor* dy, float* dx, i
     return fail(VM_EUNSUPPORTED, "resize_backward: scale %dx%d -> %dx%d outside the upsampling range", ih, iw, dy->h,
                 dy->w);
   const float sy = (float)ih / (float)dy->h, sx = (float)iw / (float)dy->w;
+  if (dy->dtype == VM_F32 && dy->c % 4 == 0 && dy->cstride % 4 == 0 && dy->coff % 4 == 0 &&
+      reinterpret_cast<uintptr_t>(dy->ptr) % 16 == 0 && reinterpret_cast<uintptr_t>(dx) % 16 == 0) {
+    const long n4 = (long)dy->n * ih * iw * (dy->c / 4);
+    hipLaunchKernelGGL(resize_bwd_kernel4, dim3(grid_for(n4, 256)), dim3(256), 0, st, mk(dy), dx, ih, iw, sy, sx);
+    return check_launch("resize_backward");
+  }
   const long n = (long)dy->n * ih * iw * dy->c;
   hipLaunchKernelGGL(resize_bwd_kernel, dim3(grid_for(n, 256)), dim3(256), 0, st, mk(dy), dx, ih, iw, sy, sx);
   return check_launch("resize_backward");

@@ -67,7 +67,9 @@ class UNet:
     # (vm_conv3x3_pair_first_head_nhwc), so conv1_2's 64-channel output never reaches HBM and the head reads only
     # the upconv_4 half; .conv1_2 / .upconv4 are then evaluated on first access
     split_head = True
-    fold_upconv = ("upconv_3", "upconv_4")  # upconv_2 folded would run on the 135x240 grid: slower (measured)
+    # upconv_2 too since its odd phases skip their zero taps (same-box A/B: -0.5 % on the whole forward vs resize +
+    # conv on the rows kernel; without the skip, folding it was slower)
+    fold_upconv = ("upconv_2", "upconv_3", "upconv_4")
 
     def __init__(self, vgg16_npy_path=None, dtype="bf16", device="cuda"):
         self.data_dict = load_vgg16(vgg16_npy_path)
