@@ -384,6 +384,12 @@ int vm_bn_backward_apply_nhwc(const vm_tensor* x, const vm_tensor* dy, const vm_
 int vm_relu_backward_nhwc(const vm_tensor* dy, const vm_tensor* y, vm_tensor* dx, void* stream);
 /* The same with an optional second (e.g. bf16) copy of dx. */
 int vm_relu_backward_ex_nhwc(const vm_tensor* dy, const vm_tensor* y, vm_tensor* dx, vm_tensor* dx2, void* stream);
+/* The same over a decoder level's concat in one pass (upconv_concat, unet_simple.py:30-42): channels [0, split) of
+ * the gradient go to dx_lo [n,h,w,split] (f32: the select convs' already-masked gradients, read densely by their
+ * BN backward), channels [split, c) to dx [n,h,w,c-split] and optionally dx2 (the upconv's).  0 < split < c, or
+ * split 0 with dx_lo NULL (= vm_relu_backward_ex_nhwc). */
+int vm_relu_backward_split_nhwc(const vm_tensor* dy, const vm_tensor* y, int split, vm_tensor* dx_lo, vm_tensor* dx,
+                                vm_tensor* dx2, void* stream);
 
 /* Adjoint of vm_resize_bilinear_tf1_nhwc (tf.image.resize_images, unet_simple.py:33): dy [n,oh,ow,c] (f32 view) ->
  * dx contiguous f32 [n,ih,iw,c] (overwritten). */

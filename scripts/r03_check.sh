@@ -16,18 +16,18 @@ if has smx; then
   [ $rc -eq 0 ] || exit $rc
 fi
 if has ab; then
-  timeout -k 10 300 python tools/ab_unet.py default noskip fold_up2 fold_up2_noskip > gpurun_out/ab.log 2>&1
+  timeout -k 10 300 python tools/ab_unet.py ${AB:-default noskip fold_up2 fold_up2_noskip} > gpurun_out/ab.log 2>&1
   rc=$?; cat gpurun_out/ab.log | grep ms/frame
   [ $rc -eq 0 ] || exit $rc
 fi
 if has train; then
-  timeout -k 10 300 python bench.py --only train --steps 20 --warmup 3 > gpurun_out/train_graph.log 2>&1; rc=$?
-  tail -1 gpurun_out/train_graph.log
+  timeout -k 10 300 python bench.py --only train --steps 20 --warmup 3 > gpurun_out/train_eager.log 2>&1; rc=$?
+  tail -1 gpurun_out/train_eager.log
   [ $rc -eq 0 ] || exit $rc
-  timeout -k 10 300 python bench.py --only train --steps 20 --warmup 3 --no-graph > gpurun_out/train_eager.log 2>&1
-  rc=$?; tail -1 gpurun_out/train_eager.log
+  timeout -k 10 300 python bench.py --only train --steps 20 --warmup 3 --train-graph > gpurun_out/train_graph.log 2>&1
+  rc=$?; tail -1 gpurun_out/train_graph.log
   [ $rc -eq 0 ] || exit $rc
 fi
 if has prof; then
-  SKIP="fwd mfma traffic bench" bash tools/prof_bench.sh r03a || exit $?
+  SKIP="${PROF_SKIP:-fwd mfma traffic bench}" bash tools/prof_bench.sh "${TAG:-r03a}" || exit $?
 fi

@@ -151,9 +151,12 @@ def test_head_kernels_agree(dtype, shape):
 
 
 @pytest.mark.parametrize("case", [(1, 9, 13, 3, 64, "relu"), (2, 11, 70, 7, 64, "relu"), (1, 33, 65, 8, 128, "none"),
-                                  (1, 1, 1, 7, 64, "relu"), (1, 16, 32, 6, 64, "sigmoid")])
+                                  (1, 1, 1, 7, 64, "relu"), (1, 16, 32, 6, 64, "sigmoid"),
+                                  (4, 160, 330, 3, 64, "relu"), (2, 203, 250, 8, 128, "none")])
 def test_first_layer_kernel(case):
-    """cin <= 8 with bf16 output dispatches conv3x3_first (4 taps x 8 channels per MFMA K-step)."""
+    """cin <= 8 with bf16 output dispatches conv3x3_first (4 taps x 8 channels per MFMA K-step).  The last two cases
+    have more tiles than resident blocks: the persistent walk (next patch in flight, weight-slice reload when the
+    output-channel block changes, ragged tiles at both edges)."""
     from vmatting import _lib, ops
     n, h, w, cin, cout, act = case
     rs = np.random.RandomState(cin * 31 + w)

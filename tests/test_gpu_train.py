@@ -214,6 +214,27 @@ def test_relu_backward():
     assert np.array_equal(H(dx), np.where(y > 0, dy, 0).astype(np.float64))
 
 
+@pytest.mark.parametrize("width,split,ys", [(30, 6, 32), (32, 8, 32), (48, 24, 48), (96, 48, 96), (7, 3, 8)])
+def test_relu_backward_split(width, split, ys):
+    """The concat's one-pass split (train.py backward): channels [0, split) to dx_lo, the rest to dx and its bf16
+    copy — each equal to the masked gradient, the bf16 copy equal to the unsplit kernel's."""
+    from vmatting import ops
+    rs = np.random.RandomState(width)
+    n, h, w = 2, 37, 45
+    yb = torch.zeros((n, h, w, ys), dtype=torch.float32, device=DEV)
+    yb[..., :width] = T(np.maximum(rs.normal(size=(n, h, w, width)), 0).astype(np.float32))
+    dy = T(rs.normal(size=(n, h, w, width)).astype(np.float32))
+    ref = np.where(H(yb[..., :width]) > 0, H(dy), 0)
+    lo = torch.empty((n, h, w, split), device=DEV)
+    hi = torch.empty((n, h, w, width - split), device=DEV)
+    g16 = torch.zeros((n, h, w, 32 * ((width - split + 31) // 32)), dtype=torch.bfloat16, device=DEV)
+    ops.relu_backward(dy, yb[..., :width], hi, dx2=g16[..., :width - split], dx_lo=lo)
+    assert np.array_equal(H(lo), ref[..., :split]) and np.array_equal(H(hi), ref[..., split:])
+    full16 = torch.zeros_like(g16)
+    ops.relu_backward(dy[..., split:], yb[..., split:width], torch.empty_like(hi), dx2=full16[..., :width - split])
+    assert torch.equal(g16, full16)
+
+
 def test_loss_backward():
     from vmatting import ops
     rs = np.random.RandomState(9)
@@ -492,12 +513,29 @@ def _bf16(a):
     return torch.from_numpy(np.ascontiguousarray(a, np.float32)).to(torch.bfloat16).float().numpy()
 
 
-@pytest.mark.parametrize("cout", [1, 2, 4, 8, 16, 24, 32, 48])
+@pytest.fixture
+def wgrad_opts():
+    from vmatting import _lib
+    yield _lib.set_option
+    _lib.set_option("wgrad_taps", 1)
+    _lib.set_option("wgrad_variant", 0)
+
+
+# (wgrad_taps, wgrad_variant): taps-in-N kernel for cout <= 8 with 4- and 8-row tiles, and the per-tap kernel
+WGRAD_VARIANTS = [(1, 0), (1, 2), (0, 0)]
+
+
+@pytest.mark.parametrize("variant", WGRAD_VARIANTS)
+@pytest.mark.parametrize("cout", [1, 2, 3, 4, 6, 8, 16, 24, 32, 48])
 @pytest.mark.parametrize("cin,cs", [(9, 16), (30, 32), (64, 72), (192, 192), (70, 80)])
-def test_conv_wgrad_mfma(cin, cs, cout):
+def test_conv_wgrad_mfma(cin, cs, cout, variant, wgrad_opts):
     """vm_conv3x3_wgrad_bf16_nhwc: bf16 x and dy rounded to bf16, f32 sums — against float64 autograd on the same
     bf16-rounded operands (so only the summation order differs): max-abs error <= 1e-4 of scale."""
     from vmatting import ops
+    if cout > 8 and variant != WGRAD_VARIANTS[0]:
+        pytest.skip("the taps option only routes cout <= 8")
+    wgrad_opts("wgrad_taps", variant[0])
+    wgrad_opts("wgrad_variant", variant[1])
     rs = np.random.RandomState(cin * 100 + cout)
     n, h, w = 2, 13, 70
     x = rs.normal(size=(n, h, w, cs)).astype(np.float32)
@@ -525,12 +563,13 @@ def test_conv_wgrad_mfma_wide_cin_accumulates(cin, cout, hw):
     assert scaled_err(H(dw) - 1.0, wr.grad.numpy()) <= 1e-4
 
 
-def test_conv_wgrad_mfma_tower_major_sources():
+@pytest.mark.parametrize("cout", [2, 16])
+def test_conv_wgrad_mfma_tower_major_sources(cout):
     """x read from 3 tower-major sources ([3N,h,w,c] buffer, the batched frozen towers): equals the wgrad of the
     channel concat [tower0 | tower1 | tower2] per pixel (unet_simple.py:153-168)."""
     from vmatting import ops
     rs = np.random.RandomState(5)
-    n, h, w, c, cout = 2, 11, 37, 64, 16
+    n, h, w, c = 2, 11, 37, 64
     feats = rs.normal(size=(3 * n, h, w, c)).astype(np.float32)
     fd = T(feats, torch.bfloat16)
     dy = rs.normal(size=(n, h, w, cout)).astype(np.float32)

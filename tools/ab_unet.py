@@ -14,6 +14,7 @@ from vmatting.weights import synthetic_vgg16  # noqa: E402
 VARIANTS = {
     "default": {},
     "fold_up2": {"fold_upconv": ("upconv_2", "upconv_3", "upconv_4")},
+    "fold3": {"fold_upconv": ("upconv_3", "upconv_4")},  # round-3 default before upconv_2 was folded
     "nosplit": {"split_head": False},
     "noskip": {"_opt": {"up_skip": 0}},  # folded upconvs without the zero-tap skipping
     "fold_up2_noskip": {"fold_upconv": ("upconv_2", "upconv_3", "upconv_4"), "_opt": {"up_skip": 0}},

@@ -1490,105 +1490,137 @@ __global__ __launch_bounds__(512) void conv3x3_pair_persist(ConvArgs a) {
 // ================================================================ first layer: cin <= 8 (conv1_1, unet.py:65-74)
 // One 16-byte chunk per pixel, so a 32-deep MFMA K-step covers 4 taps x 8 channels: lane group q of the pixel
 // fragment reads the patch row shifted by tap 4j+q (taps >= 9 read as zero), matching the tap-major packing
-// k = tap*8 + c.  The 10 x 34 patch (5.4 KB) is loaded once; the 64 x 96 weight slice lives in registers.
-// 8 waves of 32 px x 64 channels; same bf16 slab epilogue as the patch kernel.
-__global__ __launch_bounds__(512) void conv3x3_first(ConvArgs a) {
+// k = tap*8 + c.  The 10 x 34 patch (5.4 KB) is loaded once per tile; the 64 x 96 weight slice sits in LDS (12 KB,
+// one uint4 per MFMA operand lane: in registers it took 48 VGPRs and the persistent loop spilled).
+// 8 waves of 32 px x 64 channels; same bf16 slab epilogue as the patch kernel.  Persistent: a block walks tiles
+// b, b + G, ... (G a multiple of 8, so xcd_tile keeps each block on its XCD's tile range) with the next tile's
+// patch chunk in flight in a register while the current one computes and stores, and reloads its weight slice
+// only when the output-channel block changes.  (One tile per block spent ~10 us of serial load latency per tile
+// at 2 resident blocks per CU: 185 us for the training towers' 2.5 M pixels, 1.7 TB/s of stores.)
+__global__ __launch_bounds__(512, 4) void conv3x3_first(ConvArgs a) {
   using T = uint16_t;
   constexpr int TH = 8, TW = 32, PW = TW + 2, PPIX = (TH + 2) * PW, BM = TH * TW, SR = 64 * 2 + 16;
   __shared__ __attribute__((aligned(16))) uint4 patch[PPIX];
   __shared__ __attribute__((aligned(16))) char stg[BM * SR];
+  __shared__ __attribute__((aligned(16))) uint4 wl[3][4][64];  // the weight slice, one uint4 per (step, fc, lane)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int H = a.H, W = a.W, cs = a.x_cstride;
   const int th = (H + TH - 1) / TH, tw = (W + TW - 1) / TW;
-  const int t = xcd_tile(blockIdx.x, a.tiles_total);
-  const int st = t / a.tiles_n, nt = t - st * a.tiles_n;
-  const int n = st / (th * tw), srem = st - n * th * tw;
-  const int r0 = (srem / tw) * TH, c0 = (srem - (srem / tw) * tw) * TW;
-  const int n0 = nt * 64;
-
-  const T* xb = reinterpret_cast<const T*>(a.x) + a.x_coff + ((long)n * H + r0 - 1) * (long)W * cs;
-  const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<T*>(xb), 0, 0x7ffffff0, 0x00020000);
-  if (tid < PPIX) {
-    const int pr = tid / PW, pc = tid - pr * PW;
-    const int h = r0 - 1 + pr, w = c0 - 1 + pc;
-    const bool ok = (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
-    const int off = ok ? (pr * W + w) * cs * 2 : OOB;
-    patch[tid] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0));
-  }
   const int col = lane & 15, q = lane >> 4;
-  const __amdgpu_buffer_rsrc_t wrs = w_rsrc<T>(a, n0);
-  uint4 wf[3][4];
-#pragma unroll
-  for (int j = 0; j < 3; ++j)
-#pragma unroll
-    for (int fc = 0; fc < 4; ++fc)
-      wf[j][fc] = __builtin_bit_cast(
-          uint4, __builtin_amdgcn_raw_buffer_load_b128(wrs, ((fc * 16 + col) * a.K_pad + j * 32 + q * 8) * 2, 0, 0));
-  __syncthreads();
-
-  f32x4 acc[4][2];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int k = 0; k < 2; ++k) acc[i][k] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int j = 0; j < 3; ++j) {
-    const int tap = 4 * j + q;
-    const int toff = (tap / 3) * PW + tap % 3;
-    uint4 bv[2];
-#pragma unroll
-    for (int fp = 0; fp < 2; ++fp) {
-      const int p = wave * 32 + fp * 16;  // tile pixel of the fragment's first row: one patch row per wave
-      const uint4 v = patch[(p / TW) * PW + (p % TW) + col + (tap < 9 ? toff : 0)];
-      bv[fp] = tap < 9 ? v : make_uint4(0, 0, 0, 0);
+  auto coords = [&](int l, int& n, int& r0, int& c0, int& n0) {
+    const int t = xcd_tile(l, a.tiles_total);
+    const int st = t / a.tiles_n, nt = t - st * a.tiles_n;
+    n = st / (th * tw);
+    const int srem = st - n * th * tw;
+    r0 = (srem / tw) * TH;
+    c0 = (srem - (srem / tw) * tw) * TW;
+    n0 = nt * 64;
+  };
+  auto load_patch = [&](int n, int r0, int c0) {
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (tid < PPIX) {
+      const T* xb = reinterpret_cast<const T*>(a.x) + a.x_coff + ((long)n * H + r0 - 1) * (long)W * cs;
+      const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<T*>(xb), 0, 0x7ffffff0, 0x00020000);
+      const int pr = tid / PW, pc = tid - pr * PW;
+      const int h = r0 - 1 + pr, w = c0 - 1 + pc;
+      const bool ok = (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
+      const int off = ok ? (pr * W + w) * cs * 2 : OOB;
+      v = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0));
     }
+    return v;
+  };
+  const int G = gridDim.x;
+  int l = blockIdx.x;
+  if (l >= a.tiles_total) return;
+  int n, r0, c0, n0, wn0 = -1;
+  coords(l, n, r0, c0, n0);
+  uint4 pv = load_patch(n, r0, c0);
+  for (; l < a.tiles_total; l += G) {
+    if (n0 != wn0) {  // block-uniform; the previous tile's MFMAs are behind its two barriers
+      const __amdgpu_buffer_rsrc_t wrs = w_rsrc<T>(a, n0);
+      for (int e = tid; e < 3 * 4 * 64; e += 512) {
+        const int j = e >> 8, fc = (e >> 6) & 3, ln = e & 63;
+        wl[j][fc][ln] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                      wrs, ((fc * 16 + (ln & 15)) * a.K_pad + j * 32 + (ln >> 4) * 8) * 2,
+                                                      0, 0));
+      }
+      wn0 = n0;
+    }
+    if (tid < PPIX) patch[tid] = pv;
+    __syncthreads();
+    // the next tile's patch chunk: in flight through this tile's MFMAs, epilogue and stores
+    const int cn = n, cr0 = r0, cc0 = c0, cn0 = n0;
+    if (l + G < a.tiles_total) {
+      coords(l + G, n, r0, c0, n0);
+      pv = load_patch(n, r0, c0);
+    }
+
+    f32x4 acc[4][2];
 #pragma unroll
-    for (int fc = 0; fc < 4; ++fc)
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int fp = 0; fp < 2; ++fp) mma16<T>(wf[j][fc], bv[fp], acc[fc][fp]);
-  }
+      for (int k = 0; k < 2; ++k) acc[i][k] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const int tap = 4 * j + q;
+      const int toff = (tap / 3) * PW + tap % 3;
+      uint4 bv[2];
+#pragma unroll
+      for (int fp = 0; fp < 2; ++fp) {
+        const int p = wave * 32 + fp * 16;  // tile pixel of the fragment's first row: one patch row per wave
+        const uint4 v = patch[(p / TW) * PW + (p % TW) + col + (tap < 9 ? toff : 0)];
+        bv[fp] = tap < 9 ? v : make_uint4(0, 0, 0, 0);
+      }
+#pragma unroll
+      for (int fc = 0; fc < 4; ++fc) {
+        const uint4 wv = wl[j][fc][lane];
+#pragma unroll
+        for (int fp = 0; fp < 2; ++fp) mma16<T>(wv, bv[fp], acc[fc][fp]);
+      }
+    }
 
 #pragma unroll
-  for (int fc = 0; fc < 4; ++fc) {
-    const int cc = fc * 16 + 4 * q;
-    float mul[4], add[4];
-#pragma unroll
-    for (int jj = 0; jj < 4; ++jj) {
-      const int co = min(n0 + cc + jj, a.cout - 1);
-      const float sc = a.scale ? a.scale[co] : 1.f;
-      mul[jj] = sc;
-      add[jj] = (a.bias ? a.bias[co] : 0.f) * sc + (a.shift ? a.shift[co] : 0.f);
-    }
-#pragma unroll
-    for (int fp = 0; fp < 2; ++fp) {
-      const int row = wave * 32 + fp * 16 + col;
-      float v[4];
+    for (int fc = 0; fc < 4; ++fc) {
+      const int cc = fc * 16 + 4 * q;
+      float mul[4], add[4];
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj) {
-        v[jj] = fmaf(acc[fc][fp][jj], mul[jj], add[jj]);
-        if (a.act == VM_ACT_RELU) v[jj] = fmaxf(v[jj], 0.f);
-        else if (a.act == VM_ACT_SIGMOID) v[jj] = sigmoid_precise(v[jj]);
+        const int co = min(cn0 + cc + jj, a.cout - 1);
+        const float sc = a.scale ? a.scale[co] : 1.f;
+        mul[jj] = sc;
+        add[jj] = (a.bias ? a.bias[co] : 0.f) * sc + (a.shift ? a.shift[co] : 0.f);
       }
-      uint2 pk;
-      pk.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-      pk.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-      *reinterpret_cast<uint2*>(stg + row * SR + cc * 2) = pk;
-    }
-  }
-  __syncthreads();
-  const int ycs2 = a.y_cstride * 2;
-  T* yb = reinterpret_cast<T*>(a.y) + a.y_coff + (((long)n * H + r0) * W + c0) * (long)a.y_cstride + n0;
-  const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(yb, 0, 0x7ffffff0, 0x00020000);
 #pragma unroll
-  for (int it = 0; it < BM * 8 / 512; ++it) {
-    const int idx = it * 512 + tid;
-    const int rr = idx >> 3, cq = idx & 7;
-    const uint4 d = *reinterpret_cast<const uint4*>(stg + rr * SR + cq * 16);
-    const int pr = rr / TW, pc = rr % TW;
-    const bool ok = r0 + pr < H && c0 + pc < W && n0 + cq * 8 < a.cout;
-    const int off = ok ? (pr * W + pc) * ycs2 + cq * 16 : OOB;
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, d), yrs,
-                                           off, 0, 0);
+      for (int fp = 0; fp < 2; ++fp) {
+        const int row = wave * 32 + fp * 16 + col;
+        float v[4];
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          v[jj] = fmaf(acc[fc][fp][jj], mul[jj], add[jj]);
+          if (a.act == VM_ACT_RELU) v[jj] = fmaxf(v[jj], 0.f);
+          else if (a.act == VM_ACT_SIGMOID) v[jj] = sigmoid_precise(v[jj]);
+        }
+        uint2 pk;
+        pk.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+        pk.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+        *reinterpret_cast<uint2*>(stg + row * SR + cc * 2) = pk;
+      }
+    }
+    __syncthreads();
+    const int ycs2 = a.y_cstride * 2;
+    T* yb = reinterpret_cast<T*>(a.y) + a.y_coff + (((long)cn * H + cr0) * W + cc0) * (long)a.y_cstride + cn0;
+    const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(yb, 0, 0x7ffffff0, 0x00020000);
+#pragma unroll
+    for (int it = 0; it < BM * 8 / 512; ++it) {
+      const int idx = it * 512 + tid;
+      const int rr = idx >> 3, cq = idx & 7;
+      const uint4 d = *reinterpret_cast<const uint4*>(stg + rr * SR + cq * 16);
+      const int pr = rr / TW, pc = rr % TW;
+      const bool ok = cr0 + pr < H && cc0 + pc < W && cn0 + cq * 8 < a.cout;
+      const int off = ok ? (pr * W + pc) * ycs2 + cq * 16 : OOB;
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, d), yrs,
+                                             off, 0, 0);
+    }
   }
 }
 
@@ -3065,7 +3097,22 @@ static int launch_first(ConvArgs& a, hipStream_t st) {
   if (sp * a.tiles_n > 0x7fffffffL) return fail(VM_EUNSUPPORTED, "conv3x3: too many tiles");
   a.tiles_total = (int)(sp * a.tiles_n);
   snprintf(g_last_kernel, sizeof g_last_kernel, "vm::conv3x3_first");
-  hipLaunchKernelGGL(conv3x3_first, dim3(a.tiles_total), dim3(512), 0, st, a);
+  static int attr_dev = -1, resident = 0;  // blocks resident on the whole chip (2 per CU at 98 VGPRs, 41 KB LDS)
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (attr_dev != dev) {
+    int per_cu = 0, n_cu = 0;
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(&conv3x3_first),
+                                                                512, 0);
+    if (e == hipSuccess) e = hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
+    if (e != hipSuccess) return fail(VM_EHIP, "conv3x3_first setup: %s", hipGetErrorString(e));
+    resident = per_cu * n_cu / 8 * 8;
+    attr_dev = dev;
+  }
+  // a multiple of 8 blocks (xcd_tile's XCD ranges stay per block), at most one resident round
+  int grid = resident > 0 && resident < a.tiles_total ? resident : a.tiles_total;
+  if (grid > 8) grid = grid / 8 * 8;
+  hipLaunchKernelGGL(conv3x3_first, dim3(grid), dim3(512), 0, st, a);
   return check_launch("conv3x3_first");
 }
 
@@ -3273,6 +3320,11 @@ extern "C" int vm_set_option(const char* key, long value) {
   if (!strcmp(key, "glds_rb")) {
     if (value != 64 && value != 128) return fail(VM_EINVAL, "glds_rb must be 64 or 128");
     g_glds_rb = value;
+    return VM_OK;
+  }
+  if (!strcmp(key, "bn_blocks")) {
+    if (value < 1 || value > BN_TARGET_MAX) return fail(VM_EINVAL, "set_option: bn_blocks must be 1..%d", BN_TARGET_MAX);
+    g_bn_target = value;
     return VM_OK;
   }
   if (train_set_option(key, value)) return VM_OK;

@@ -278,7 +278,7 @@ __global__ void convert_kernel(View x, View y, const float* scale, const float* 
 // variance over N*H*W.  Pass 1: grid (ceil(C/64), nblk); lane = channel (64 consecutive channels of a
 // pixel per wave -> coalesced), the 4 waves of a block stride over pixels, f64 partial sums,
 // combined across waves in LDS.  Pass 2: one thread per channel folds the nblk partials.
-constexpr int BN_NBLK = 1024;  // pixel blocks (max); launches use min(BN_NBLK, M / 256)
+long g_bn_target = 4096;  // vm_common.h bn_blocks
 
 // CP = lanes per pixel: 64 for c > 32 (a block covers 64 channels of each pixel, blockIdx.x picks the group);
 // for narrow tensors CP = next power of two >= c, so one wave reads 64 / CP pixels per step instead of idling lanes.
@@ -324,34 +324,25 @@ __global__ __launch_bounds__(256) void bn_partial_kernel(View x, double* part, i
   }
 }
 
-// one wave per channel folds the nblk partials (lane-strided, then a shuffle tree)
-__global__ __launch_bounds__(64) void bn_final_kernel(const double* part, int nblk, int C, long M, float* mean,
-                                                      float* var) {
-  const int c = blockIdx.x, lane = threadIdx.x;
-  double s = 0.0, ss = 0.0;
-  for (int b = lane; b < nblk; b += 64) {
-    s += part[(long)b * C + c];
-    ss += part[(long)nblk * C + (long)b * C + c];
-  }
-  for (int o = 32; o > 0; o >>= 1) {
-    s += __shfl_down(s, o);
-    ss += __shfl_down(ss, o);
-  }
-  if (lane == 0) {
-    const double m = s / (double)M;
-    double v = ss / (double)M - m * m;
+// one block per channel folds the nblk partials (vm_common.h fold_columns)
+__global__ __launch_bounds__(256) void bn_final_kernel(const double* part, int nblk, int C, long M, float* mean,
+                                                       float* var) {
+  const int c = blockIdx.x;
+  double r[3];
+  fold_columns(part, nblk, C, c, 2, r);
+  if (threadIdx.x == 0) {
+    const double m = r[0] / (double)M;
+    double v = r[1] / (double)M - m * m;
     if (v < 0.0) v = 0.0;
     mean[c] = (float)m;
     var[c] = (float)v;
   }
 }
 
-static int bn_blocks(long M) { return (int)(M / 256 < 1 ? 1 : M / 256 > BN_NBLK ? BN_NBLK : M / 256); }
-
 template <typename T>
 static int launch_bn_partial(const View& xv, double* part, hipStream_t st) {
   const int C = xv.c;
-  const int nb = bn_blocks((long)xv.n * xv.h * xv.w);
+  const int nb = bn_blocks((long)xv.n * xv.h * xv.w, C);
   const int cp = C > 32 ? 64 : C > 16 ? 32 : C > 8 ? 16 : C > 4 ? 8 : C > 2 ? 4 : C > 1 ? 2 : 1;
   dim3 grid(cp == 64 ? (C + 63) / 64 : 1, nb);
   switch (cp) {
@@ -485,7 +476,7 @@ extern "C" int vm_convert_nhwc(const vm_tensor* x, vm_tensor* y, const float* sc
 
 extern "C" size_t vm_bn_workspace_bytes(const vm_tensor* x) {
   if (!x) return 0;
-  return (size_t)2 * BN_NBLK * x->c * sizeof(double);
+  return (size_t)2 * bn_max_blocks(x->c) * x->c * sizeof(double);
 }
 
 extern "C" int vm_bn_stats_nhwc(const vm_tensor* x, float* mean, float* var, void* work, void* stream) {
@@ -497,7 +488,7 @@ extern "C" int vm_bn_stats_nhwc(const vm_tensor* x, float* mean, float* var, voi
                                      : launch_bn_partial<float>(view(x), part, st);
   int rc = check_launch("bn_partial");
   if (rc) return rc;
-  hipLaunchKernelGGL(bn_final_kernel, dim3(x->c), dim3(64), 0, st, part, nb, x->c, M, mean, var);
+  hipLaunchKernelGGL(bn_final_kernel, dim3(x->c), dim3(256), 0, st, part, nb, x->c, M, mean, var);
   return check_launch("bn_final");
 }
 

@@ -81,7 +81,6 @@ __global__ __launch_bounds__(256) void loss_backward_kernel(const float* __restr
 }
 
 // ---------------------------------------------------------------- batch-norm backward (training statistics)
-constexpr int BN_NBLK = 1024;  // pixel blocks (max); launches use min(BN_NBLK, M / 256)
 
 template <bool MASK>
 __device__ __forceinline__ float grad_in(const V& dy, const V& y, long p, int c) {
@@ -155,27 +154,19 @@ __global__ __launch_bounds__(256) void bn_bwd_partial(V x, V dy, V y, const floa
 // folds the partials; with dbias also the gradient of a bias added before the BN (new_conv's conv bias,
 // unet_simple.py:23-25): sum_p dx = gamma*rstd*(sum g - M*mean g - sum xhat * sum(g*xhat)/M), zero in exact
 // arithmetic (BN removes the bias), evaluated from the same double sums instead of a pass over dx
-__global__ __launch_bounds__(64) void bn_bwd_final(const double* part, int nblk, int C, float* sum_g, float* sum_gx,
-                                                   float* dbias, const float* gamma, const float* var, float eps,
-                                                   long M) {
-  const int c = blockIdx.x, lane = threadIdx.x;
-  double s1 = 0.0, s2 = 0.0, s3 = 0.0;
-  for (int b = lane; b < nblk; b += 64) {
-    s1 += part[(long)b * C + c];
-    s2 += part[(long)nblk * C + (long)b * C + c];
-    if (dbias) s3 += part[2L * nblk * C + (long)b * C + c];
-  }
-  for (int o = 32; o > 0; o >>= 1) {
-    s1 += __shfl_down(s1, o);
-    s2 += __shfl_down(s2, o);
-    s3 += __shfl_down(s3, o);
-  }
-  if (lane == 0) {
+__global__ __launch_bounds__(256) void bn_bwd_final(const double* part, int nblk, int C, float* sum_g, float* sum_gx,
+                                                    float* dbias, const float* gamma, const float* var, float eps,
+                                                    long M) {
+  const int c = blockIdx.x;
+  double r[3];
+  fold_columns(part, nblk, C, c, dbias ? 3 : 2, r);
+  if (threadIdx.x == 0) {
+    const double s1 = r[0], s2 = r[1], s3 = r[2];
     if (sum_g) sum_g[c] = (float)s1;
     if (sum_gx) sum_gx[c] = (float)s2;
     if (dbias) {
-      const double r = 1.0 / sqrt((double)var[c] + (double)eps), g = gamma ? gamma[c] : 1.0;
-      dbias[c] = (float)(g * r * (s1 - (double)M * (s1 / (double)M) - s3 * s2 / (double)M));
+      const double rs = 1.0 / sqrt((double)var[c] + (double)eps), g = gamma ? gamma[c] : 1.0;
+      dbias[c] = (float)(g * rs * (s1 - (double)M * (s1 / (double)M) - s3 * s2 / (double)M));
     }
   }
 }
@@ -238,11 +229,16 @@ __global__ __launch_bounds__(256) void bn_bwd_apply(V x, V dy, V y, const float*
   }
 }
 
+// channels [0, split) go to dxlo at c, [split, C) to dx / dx2 at c - split (split 0: all to dx / dx2)
 template <int CP>
-__global__ __launch_bounds__(256) void relu_bwd_kernel(V dy, V y, V dx, V dx2) {
+__global__ __launch_bounds__(256) void relu_bwd_kernel(V dy, V y, V dx, V dx2, V dxlo, int split) {
   const long M = (long)dy.n * dy.h * dy.w;
   const int c = blockIdx.y * CP + (threadIdx.x & (CP - 1));
   if (c >= dy.c) return;
+  const bool lo = c < split;
+  const V o = lo ? dxlo : dx;
+  const int oc = lo ? c : c - split;
+  const bool two = dx2.p && !lo;
   const long step = (long)gridDim.x * (blockDim.x / CP);
   long p = (long)blockIdx.x * (blockDim.x / CP) + threadIdx.x / CP;
   for (; p + 3 * step < M; p += 4 * step) {  // 4 pixels' loads in flight before the stores
@@ -251,14 +247,14 @@ __global__ __launch_bounds__(256) void relu_bwd_kernel(V dy, V y, V dx, V dx2) {
     for (int u = 0; u < 4; ++u) v[u] = ld(y, p + u * step, c) > 0.f ? ld(dy, p + u * step, c) : 0.f;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      st(dx, p + u * step, c, v[u]);
-      if (dx2.p) st(dx2, p + u * step, c, v[u]);
+      st(o, p + u * step, oc, v[u]);
+      if (two) st(dx2, p + u * step, oc, v[u]);
     }
   }
   for (; p < M; p += step) {
     const float v = ld(y, p, c) > 0.f ? ld(dy, p, c) : 0.f;
-    st(dx, p, c, v);
-    if (dx2.p) st(dx2, p, c, v);
+    st(o, p, oc, v);
+    if (two) st(dx2, p, oc, v);
   }
 }
 
@@ -830,6 +826,210 @@ constexpr int wgrad_mfma_lds() {
   return MAIN > RED ? MAIN : RED;
 }
 
+// Narrow-cout weight gradient with the taps packed into N (select convs, cout <= 8): one GEMM
+//   dW[ci][t*cout + co] = sum_q X[q][ci] * DY[q - off_t][co]
+// whose N axis holds all 9 taps x cout columns (cout 2 -> 18 of 32, 4 -> 36 of 48, 8 -> 72 of 80), so a K-step of 32
+// pixels costs NCI x NT MFMAs (2 x 4 = 8 for cout 2) where wgrad_mfma_kernel's !SX form spends 9 per 16 channels
+// on one 16-wide column block holding cout of them.  The B fragments come from three bf16 planes of the DY patch,
+// plane kw pre-shifted by its tap column (P_kw[r][j] = patch(r, j + 2 - kw)), so every lane's 8 pixels are one
+// aligned 16-byte LDS read: lane (n, g) reads P_kw[row + 2 - kh][8g .. 8g + 7] of channel co, (kh, kw, co) = n's tap.
+// With 32-80 accumulator registers a block holds 64 input channels (one tower source: 128-byte pixel rows) and
+// 8 blocks fit a CU, so ~4x the bytes of X are in flight per CU than with the 160-register variants — the select
+// wgrads read 40-315 MB of tower features each and are bound by that.
+template <int TH>
+constexpr int wt_drows() { return TH + 2; }
+
+template <int NCI, int NT, int TH>
+__global__ __launch_bounds__(256) void wgrad_taps_kernel(WgArgs a) {
+  constexpr int CIB = NCI * 16;
+  constexpr int RBX = NCI == 1 ? 32 : NCI == 2 ? 64 : 128;
+  constexpr int XPIX = TH * WM_TW, XCH = CIB / 8, NXC = XPIX * XCH, XPT = (NXC + 255) / 256;
+  constexpr int DR = wt_drows<TH>();
+  constexpr int COMAX = NT * 16 / 9;                        // the widest cout this NT serves
+  constexpr int NDE = DR * WM_PW * COMAX, DPT = (NDE + 255) / 256;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int c0 = blockIdx.y * CIB;
+  const int cout = a.cout, ndy = DR * WM_PW * cout;
+  char* ximg = smem;
+  uint16_t* dpl = reinterpret_cast<uint16_t*>(smem + XPIX * RBX);  // [3][cout][DR][32]
+
+  f32x4 acc[NCI][NT];
+#pragma unroll
+  for (int i = 0; i < NCI; ++i)
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[i][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // this lane's B column: n = nt * 16 + (lane & 15) -> (tap, co); columns past 9 * cout read a zero slot
+  const int g = lane >> 4;
+  int boff[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int n = t * 16 + (lane & 15);
+    if (n < 9 * cout) {
+      const int tap = n / cout, co = n - tap * cout, kh = tap / 3, kw = tap - kh * 3;
+      boff[t] = ((kw * cout + co) * DR + 2 - kh) * WM_TW + 8 * g;  // + row * 32 per K-step
+    } else {
+      boff[t] = -1;
+    }
+  }
+
+  uint4 xb[XPT];
+  float db[DPT];
+  auto coords = [&](int tile, int& n, int& y0, int& x0) {
+    const int tx = tile % a.tiles_w;
+    const int t2 = tile / a.tiles_w;
+    y0 = (t2 % a.tiles_h) * TH;
+    n = t2 / a.tiles_h;
+    x0 = tx * WM_TW;
+  };
+  auto issue = [&](int tile) {
+    int n, y0, x0;
+    coords(tile, n, y0, x0);
+#pragma unroll
+    for (int k = 0; k < XPT; ++k) {
+      const int e = tid + k * 256;
+      xb[k] = make_uint4(0, 0, 0, 0);
+      if (NXC % 256 == 0 || e < NXC) {
+        const int pe = e / XCH, j = e % XCH;
+        const int gy = y0 + pe / WM_TW, gx = x0 + pe % WM_TW, c = c0 + j * 8;
+        if (gy < a.h && gx < a.w && c < a.cin) {
+          long off = (((long)n * a.h + gy) * a.w + gx) * a.xcs;
+          if (a.x_src_c > 0) off += (long)(c / a.x_src_c) * a.x_src_stride + c % a.x_src_c;
+          else off += c;
+          xb[k] = *reinterpret_cast<const uint4*>(a.x + off);
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < DPT; ++k) {  // the halo patch, (pixel, co) elements in memory order
+      const int e = tid + k * 256;
+      db[k] = 0.f;
+      if (e < ndy) {
+        const int pe = e / cout, co = e - pe * cout;
+        const int gy = y0 - 1 + pe / WM_PW, gx = x0 - 1 + pe % WM_PW;
+        if ((unsigned)gy < (unsigned)a.h && (unsigned)gx < (unsigned)a.w)
+          db[k] = a.dy[(((long)n * a.h + gy) * a.w + gx) * a.dcs + co];
+      }
+    }
+  };
+  auto commit = [&]() {
+#pragma unroll
+    for (int k = 0; k < XPT; ++k) {
+      const int e = tid + k * 256;
+      if (NXC % 256 == 0 || e < NXC) {
+        const int pe = e / XCH, j = e % XCH;
+        uint4 v = xb[k];
+        const int c = c0 + j * 8;
+        if (c + 8 > a.cin) {  // a chunk straddling cin (padded views): zero the lanes past it
+          uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            if (c + 2 * i >= a.cin) w4[i] = 0u;
+            else if (c + 2 * i + 1 >= a.cin) w4[i] &= 0xffffu;
+          }
+          v = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+        }
+        *reinterpret_cast<uint4*>(ximg + wm_off<RBX>(pe, j >> 1) + (j & 1) * 16) = v;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < DPT; ++k) {
+      const int e = tid + k * 256;
+      if (e < ndy) {
+        const int pe = e / cout, co = e - pe * cout;
+        const int r = pe / WM_PW, pc = pe % WM_PW;
+        const uint16_t v = f2bf(db[k]);
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw) {
+          const int j = pc - 2 + kw;
+          if (j >= 0 && j < WM_TW) dpl[((kw * cout + co) * DR + r) * WM_TW + j] = v;
+        }
+      }
+    }
+  };
+
+  const int t_beg = (int)((long)blockIdx.x * a.ntiles / gridDim.x);
+  const int t_end = (int)((long)(blockIdx.x + 1) * a.ntiles / gridDim.x);
+  if (t_beg < t_end) issue(t_beg);
+  for (int tile = t_beg; tile < t_end; ++tile) {
+    commit();
+    __syncthreads();
+    if (tile + 1 < t_end) issue(tile + 1);
+#pragma unroll
+    for (int rr = 0; rr < TH / 4; ++rr) {
+      const int row = wave + 4 * rr;
+      bf16x8 ax[NCI];
+#pragma unroll
+      for (int i = 0; i < NCI; ++i) ax[i] = wm_frag<RBX>(ximg, row * WM_TW + 8 * g, i, lane);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        bf16x8 bd = {};
+        if (boff[t] >= 0) bd = *reinterpret_cast<const bf16x8*>(dpl + boff[t] + row * WM_TW);
+#pragma unroll
+        for (int i = 0; i < NCI; ++i) acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ax[i], bd, acc[i][t], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+  }
+
+  // fold the 4 waves' accumulators (LDS, two rounds), wave 0 stores the block's partial
+  float* red = reinterpret_cast<float*>(smem);
+  constexpr int NA = NCI * NT * 4;
+  auto put = [&](int slot) {
+#pragma unroll
+    for (int i = 0; i < NCI; ++i)
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) red[(slot * NA + (i * NT + t) * 4 + j) * 64 + lane] = acc[i][t][j];
+  };
+  auto add = [&](int slot) {
+#pragma unroll
+    for (int i = 0; i < NCI; ++i)
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][t][j] += red[(slot * NA + (i * NT + t) * 4 + j) * 64 + lane];
+  };
+  if (wave >= 2) put(wave - 2);
+  __syncthreads();
+  if (wave < 2) add(wave);
+  __syncthreads();
+  if (wave == 1) put(0);
+  __syncthreads();
+  if (wave == 0) {
+    add(0);
+    float* part = a.part + (long)blockIdx.x * 9 * a.cin * cout;
+    const int ci_l = 4 * g;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int n = t * 16 + (lane & 15);
+      if (n < 9 * cout) {
+        const int tap = n / cout, co = n - tap * cout;
+#pragma unroll
+        for (int i = 0; i < NCI; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int ci = c0 + i * 16 + ci_l + j;
+            if (ci < a.cin) part[((long)tap * a.cin + ci) * cout + co] = acc[i][t][j];
+          }
+      }
+    }
+  }
+  (void)COMAX;
+}
+
+template <int NCI, int NT, int TH>
+constexpr int wgrad_taps_lds() {
+  constexpr int RBX = NCI == 1 ? 32 : NCI == 2 ? 64 : 128;
+  constexpr int COMAX = NT * 16 / 9;
+  constexpr int MAIN = TH * WM_TW * RBX + 3 * COMAX * wt_drows<TH>() * WM_TW * 2;
+  constexpr int RED = 2 * NCI * NT * 4 * 64 * 4;
+  return MAIN > RED ? MAIN : RED;
+}
+
 // HWIO [3][3][cin][cout] -> the dgrad filter [3][3][cout][cin], spatially flipped
 __global__ void flip_weights_kernel(const float* w, int cin, int cout, float* wt) {
   const long total = 9L * cin * cout;
@@ -857,23 +1057,20 @@ __global__ void adam_kernel(float* var, float* m, float* v, const float* grad, l
 }
 
 // dw[i] += sum over the gx block rows of the partials (fixed order: deterministic).  A block owns 64 columns; its
-// 16 waves stride the rows (independent loads in flight), then fold through LDS.
-__global__ __launch_bounds__(1024) void wgrad_reduce_kernel(const float* part, int rows, long S, float* dw) {
-  __shared__ float sh[16][64];
+// 4 waves stride the rows (independent loads in flight), then fold through LDS.  256-thread blocks: the 1024-thread
+// form waited for whole free CUs behind the side-stream wgrads (up to 120 us for a 14 MB fold).
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* part, int rows, long S, float* dw) {
+  __shared__ float sh[4][64];
   const int col = threadIdx.x & 63, rg = threadIdx.x >> 6;
   const long i = (long)blockIdx.x * 64 + col;
   float s = 0.f;
   if (i < S) {
 #pragma unroll 8
-    for (int b = rg; b < rows; b += 16) s += part[(long)b * S + i];
+    for (int b = rg; b < rows; b += 4) s += part[(long)b * S + i];
   }
   sh[rg][col] = s;
   __syncthreads();
-  if (rg == 0 && i < S) {
-    float t = 0.f;
-    for (int g = 0; g < 16; ++g) t += sh[g][col];
-    dw[i] += t;
-  }
+  if (rg == 0 && i < S) dw[i] += (sh[0][col] + sh[1][col]) + (sh[2][col] + sh[3][col]);
 }
 
 constexpr size_t WG_WS_CAP = 64ull << 20;  // workspace bytes
@@ -901,7 +1098,7 @@ static void launch_wgrad_t(const V& xv, const V& dy, float* dw, float* ws, hipSt
   hipLaunchKernelGGL((wgrad_kernel<CC, CO4, T, XV, DV>), dim3((unsigned)gx, ncc), dim3(WG_NT), 0, st, xv, dy, ws,
                      tiles_h, tiles_w, ntiles);
   const long S = 9L * xv.c * dy.c;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((S + 63) / 64)), dim3(1024), 0, st, ws, (int)gx, S, dw);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((S + 63) / 64)), dim3(256), 0, st, ws, (int)gx, S, dw);
 }
 
 static bool vec_ok(const V& v, int ve) {
@@ -936,6 +1133,7 @@ static void launch_wgrad(const V& xv, const V& dy, float* dw, float* ws, hipStre
 struct WmCfg {
   int nci, nco;
   bool sx;
+  int nt;  // > 0: wgrad_taps_kernel with NT = nt column tiles (cout <= 8)
 };
 
 // operand tiling of the MFMA weight gradient: cout -> NCO 16-wide fragments, the input-channel fragments per block
@@ -948,53 +1146,76 @@ static long wgrad_mfma_rows(const WgArgs& a, int cib) {
 }
 
 // (at most 72-108 accumulator registers: the 144-register tilings spill next to the staging registers)
+// cout <= 8: the taps-in-N kernel, 64 input channels per block (32 for NT 4-5: 80 accumulator registers at most)
 static WmCfg wgrad_mfma_cfg(int cin, int cout) {
   WmCfg c;
   c.nco = cout <= 16 ? 1 : cout <= 32 ? 2 : 3;
   c.nci = (c.nco == 1 && cin > 16) ? 2 : 1;
   c.sx = c.nco >= c.nci;
+  c.nt = cout <= 8 ? (9 * cout + 15) / 16 : 0;
+  if (c.nt) c.nci = cin <= 16 ? 1 : cin <= 32 || c.nt > 3 ? 2 : 4;
   return c;
 }
 
-template <int NCI, int NCO, bool SX, int TH>
-static int launch_wgrad_mfma_t(WgArgs& a, float* dw, hipStream_t st) {
-  constexpr int lds = wgrad_mfma_lds<NCI, NCO, SX, TH>();
-  static int attr_dev = -1, resident = 0;  // blocks of this variant resident on the whole chip at once
+// one round of blocks: the ~1024-block target (the workspace bound) cut to what is resident at once (160-VGPR
+// variants: 3 blocks per CU), so no block waits for a second round (measured 2 x 72 us per select wgrad)
+static int launch_wgrad_grid(const void* kern, int lds, int th, int cib, int& attr_dev, int& resident, WgArgs& a,
+                             float* dw, hipStream_t st, void (*launch)(dim3, int, hipStream_t, const WgArgs&)) {
   int dev = 0;
   (void)hipGetDevice(&dev);
   if (attr_dev != dev) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_mfma_kernel<NCI, NCO, SX, TH>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    hipError_t e = hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     int per_cu = 0, n_cu = 0;
-    if (e == hipSuccess)
-      e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(
-                                                           &wgrad_mfma_kernel<NCI, NCO, SX, TH>), 256, lds);
+    if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, lds);
     if (e == hipSuccess) e = hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
     if (e != hipSuccess) return fail(VM_EHIP, "wgrad_mfma setup: %s", hipGetErrorString(e));
     resident = per_cu * n_cu;
     attr_dev = dev;
   }
-  a.tiles_h = (a.h + TH - 1) / TH;
+  a.tiles_h = (a.h + th - 1) / th;
   a.tiles_w = (a.w + WM_TW - 1) / WM_TW;
   a.ntiles = (long)a.n * a.tiles_h * a.tiles_w;
   if (a.ntiles > 0x7fffffffL) return fail(VM_EUNSUPPORTED, "conv_wgrad: too many pixel tiles");
-  const int ncc = (a.cin + NCI * 16 - 1) / (NCI * 16);
-  // one round of blocks: the ~1024-block target (the workspace bound) cut to what is resident at once (160-VGPR
-  // variants: 3 blocks per CU), so no block waits for a second round (measured 2 x 72 us per select wgrad)
-  long gx = wgrad_mfma_rows(a, NCI * 16);
+  const int ncc = (a.cin + cib - 1) / cib;
+  long gx = wgrad_mfma_rows(a, cib);
   if (resident >= ncc && gx * ncc > resident) gx = resident / ncc;
-  hipLaunchKernelGGL((wgrad_mfma_kernel<NCI, NCO, SX, TH>), dim3((unsigned)gx, ncc), dim3(256), lds, st, a);
+  launch(dim3((unsigned)gx, ncc), lds, st, a);
   const long S = 9L * a.cin * a.cout;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((S + 63) / 64)), dim3(1024), 0, st, a.part, (int)gx, S, dw);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((S + 63) / 64)), dim3(256), 0, st, a.part, (int)gx, S, dw);
   return VM_OK;
 }
 
+template <int NCI, int NCO, bool SX, int TH>
+static int launch_wgrad_mfma_t(WgArgs& a, float* dw, hipStream_t st) {
+  static int attr_dev = -1, resident = 0;  // blocks of this variant resident on the whole chip at once
+  return launch_wgrad_grid(reinterpret_cast<const void*>(&wgrad_mfma_kernel<NCI, NCO, SX, TH>),
+                           wgrad_mfma_lds<NCI, NCO, SX, TH>(), TH, NCI * 16, attr_dev, resident, a, dw, st,
+                           [](dim3 g, int lds, hipStream_t s, const WgArgs& x) {
+                             hipLaunchKernelGGL((wgrad_mfma_kernel<NCI, NCO, SX, TH>), g, dim3(256), lds, s, x);
+                           });
+}
+
+template <int NCI, int NT, int TH>
+static int launch_wgrad_taps_t(WgArgs& a, float* dw, hipStream_t st) {
+  static int attr_dev = -1, resident = 0;
+  return launch_wgrad_grid(reinterpret_cast<const void*>(&wgrad_taps_kernel<NCI, NT, TH>),
+                           wgrad_taps_lds<NCI, NT, TH>(), TH, NCI * 16, attr_dev, resident, a, dw, st,
+                           [](dim3 g, int lds, hipStream_t s, const WgArgs& x) {
+                             hipLaunchKernelGGL((wgrad_taps_kernel<NCI, NT, TH>), g, dim3(256), lds, s, x);
+                           });
+}
+
 static long g_wgrad_variant = 0;  // A/B knob (vm_set_option "wgrad_variant"): 0/1 4-row tiles, 2 8-row tiles
+static long g_wgrad_taps = 1;     // vm_set_option "wgrad_taps": 0 sends cout <= 8 to wgrad_mfma_kernel (A/B)
 }  // namespace trn
 
 int train_set_option(const char* key, long value) {
   if (!strcmp(key, "wgrad_variant")) {
     trn::g_wgrad_variant = value;
+    return 1;
+  }
+  if (!strcmp(key, "wgrad_taps")) {
+    trn::g_wgrad_taps = value;
     return 1;
   }
   return 0;
@@ -1003,8 +1224,24 @@ int train_set_option(const char* key, long value) {
 namespace trn {
 
 static int launch_wgrad_mfma(WgArgs& a, float* dw, hipStream_t st) {
-  const WmCfg c = wgrad_mfma_cfg(a.cin, a.cout);
+  WmCfg c = wgrad_mfma_cfg(a.cin, a.cout);
   const bool th8 = g_wgrad_variant == 2;
+  if (c.nt && g_wgrad_taps) {
+#define VM_WT(NCI, NT) \
+  return th8 ? launch_wgrad_taps_t<NCI, NT, 8>(a, dw, st) : launch_wgrad_taps_t<NCI, NT, 4>(a, dw, st)
+    if (c.nci == 1) {
+      switch (c.nt) { case 1: VM_WT(1, 1); case 2: VM_WT(1, 2); case 3: VM_WT(1, 3); case 4: VM_WT(1, 4); default: VM_WT(1, 5); }
+    } else if (c.nci == 2) {
+      switch (c.nt) { case 1: VM_WT(2, 1); case 2: VM_WT(2, 2); case 3: VM_WT(2, 3); case 4: VM_WT(2, 4); default: VM_WT(2, 5); }
+    } else {
+      switch (c.nt) { case 1: VM_WT(4, 1); case 2: VM_WT(4, 2); default: VM_WT(4, 3); }
+    }
+#undef VM_WT
+  }
+  if (c.nt) {  // the legacy tiling of this shape
+    c.nt = 0;
+    c.nci = a.cin > 16 ? 2 : 1;
+  }
   if (c.nco == 1 && c.nci >= 2)
     return th8 ? launch_wgrad_mfma_t<2, 1, false, 8>(a, dw, st) : launch_wgrad_mfma_t<2, 1, false, 4>(a, dw, st);
   if (c.nci == 1 && c.nco == 1)
@@ -1033,6 +1270,8 @@ extern "C" int vm_bn_backward_ex_nhwc(const vm_tensor* x, const vm_tensor* dy, c
                                       float* dgamma, float* dbeta, float* dbias, void* work, void* stream);
 extern "C" int vm_relu_backward_ex_nhwc(const vm_tensor* dy, const vm_tensor* y, vm_tensor* dx, vm_tensor* dx2,
                                         void* stream);
+extern "C" int vm_relu_backward_split_nhwc(const vm_tensor* dy, const vm_tensor* y, int split, vm_tensor* dx_lo,
+                                           vm_tensor* dx, vm_tensor* dx2, void* stream);
 
 extern "C" int vm_matting_loss_backward(const float* pred, const float* gt, const float* raw_fg, const float* bg,
                                         const float* cmp, long pixels, float* dlogits, void* stream) {
@@ -1045,7 +1284,7 @@ extern "C" int vm_matting_loss_backward(const float* pred, const float* gt, cons
 }
 
 extern "C" size_t vm_bn_backward_workspace_bytes(int channels) {
-  return channels <= 0 ? 0 : (size_t)3 * BN_NBLK * channels * sizeof(double) + (size_t)2 * channels * sizeof(float);
+  return channels <= 0 ? 0 : (size_t)3 * bn_max_blocks(channels) * channels * sizeof(double) + (size_t)2 * channels * sizeof(float);
 }
 
 extern "C" int vm_bn_backward_nhwc(const vm_tensor* x, const vm_tensor* dy, const vm_tensor* y, const float* mean,
@@ -1072,16 +1311,16 @@ extern "C" int vm_bn_backward_ex_nhwc(const vm_tensor* x, const vm_tensor* dy, c
   const int C = dy->c;
   double* part = reinterpret_cast<double*>(work);
   // the two channel sums land in dbeta / dgamma when given, else in the float tail of the workspace
-  float* tail = reinterpret_cast<float*>(part + 3L * BN_NBLK * C);
+  float* tail = reinterpret_cast<float*>(part + 3L * bn_max_blocks(C) * C);
   float* sg = dbeta ? dbeta : tail;
   float* sgx = dgamma ? dgamma : tail + C;
   const long M = (long)dy->n * dy->h * dy->w;
-  const int nb = (int)(M / 256 < 1 ? 1 : M / 256 > BN_NBLK ? BN_NBLK : M / 256);
+  const int nb = bn_blocks(M, C);
   if (y) launch_bn_bwd_partial<true>(xv, dyv, yv, mean, var, eps, part, nb, st);
   else launch_bn_bwd_partial<false>(xv, dyv, yv, mean, var, eps, part, nb, st);
   int rc = check_launch("bn_backward_partial");
   if (rc) return rc;
-  hipLaunchKernelGGL(bn_bwd_final, dim3(C), dim3(64), 0, st, part, nb, C, sg, x ? sgx : nullptr, dbias, gamma, var,
+  hipLaunchKernelGGL(bn_bwd_final, dim3(C), dim3(256), 0, st, part, nb, C, sg, x ? sgx : nullptr, dbias, gamma, var,
                      eps, M);
   rc = check_launch("bn_backward_final");
   if (rc || !dx) return rc;
@@ -1127,15 +1366,25 @@ extern "C" int vm_relu_backward_nhwc(const vm_tensor* dy, const vm_tensor* y, vm
 
 extern "C" int vm_relu_backward_ex_nhwc(const vm_tensor* dy, const vm_tensor* y, vm_tensor* dx, vm_tensor* dx2,
                                         void* stream) {
-  if (!ok_view(dy) || !ok_view(y) || !ok_view(dx) || !same_shape(dy, y) || !same_shape(dy, dx) ||
-      (dx2 && (!ok_view(dx2) || !same_shape(dy, dx2))))
+  return vm_relu_backward_split_nhwc(dy, y, 0, nullptr, dx, dx2, stream);
+}
+
+extern "C" int vm_relu_backward_split_nhwc(const vm_tensor* dy, const vm_tensor* y, int split, vm_tensor* dx_lo,
+                                           vm_tensor* dx, vm_tensor* dx2, void* stream) {
+  if (!ok_view(dy) || !ok_view(y) || !same_shape(dy, y) || split < 0 || split >= dy->c)
     return fail(VM_EINVAL, "relu_backward: bad tensors");
+  auto part_ok = [&](const vm_tensor* t, int c) {
+    return ok_view(t) && t->n == dy->n && t->h == dy->h && t->w == dy->w && t->c == c;
+  };
+  if (!part_ok(dx, dy->c - split) || (dx2 && !part_ok(dx2, dy->c - split)) || (split > 0 && !(dx_lo && part_ok(dx_lo, split))))
+    return fail(VM_EINVAL, "relu_backward: outputs must be [n,h,w,%d] (dx, dx2) and [n,h,w,%d] (dx_lo)",
+                dy->c - split, split);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const long M = (long)dy->n * dy->h * dy->w;
   const int cp = lanes_for(dy->c);
   const dim3 grid = lanes_grid(M, dy->c, cp);
-  const V a = mk(dy), b = mk(y), c = mk(dx), d = dx2 ? mk(dx2) : V{};
-#define VM_RB(CP) hipLaunchKernelGGL((relu_bwd_kernel<CP>), grid, dim3(256), 0, st, a, b, c, d)
+  const V a = mk(dy), b = mk(y), c = mk(dx), d = dx2 ? mk(dx2) : V{}, e = split > 0 ? mk(dx_lo) : V{};
+#define VM_RB(CP) hipLaunchKernelGGL((relu_bwd_kernel<CP>), grid, dim3(256), 0, st, a, b, c, d, e, split)
   VM_CP_SWITCH(cp, VM_RB)
 #undef VM_RB
   return check_launch("relu_backward");

@@ -117,6 +117,59 @@ __device__ __forceinline__ float sigmoid_precise(float v) {
   return e / (1.f + e);
 }
 
+// pixel blocks of the BN partial-sum passes (elementwise.hip bn_partial_kernel, train.hip bn_bwd_partial): about
+// g_bn_target blocks over all channel groups (vm_set_option "bn_blocks"), at least BN_NBLK_MIN per group, at most
+// bn_max_blocks(C), which the workspaces are sized for.  1024 blocks (16 waves per CU) left the narrow full-resolution
+// passes at ~2.5 TB/s; the partial sums are f64, so the block count only moves their rounding far below f32's.
+constexpr int BN_NBLK_MIN = 1024, BN_TARGET_MAX = 8192;
+extern long g_bn_target;
+inline int bn_groups(int C) { return C > 32 ? (C + 63) / 64 : 1; }
+inline int bn_max_blocks(int C) {
+  const int t = BN_TARGET_MAX / bn_groups(C);
+  return t > BN_NBLK_MIN ? t : BN_NBLK_MIN;
+}
+inline int bn_blocks(long M, int C) {
+  long t = g_bn_target / bn_groups(C);
+  if (t < BN_NBLK_MIN) t = BN_NBLK_MIN;
+  if (t > bn_max_blocks(C)) t = bn_max_blocks(C);
+  const long nb = M / 256 < t ? M / 256 : t;
+  return nb < 1 ? 1 : (int)nb;
+}
+
+// column c of k (<= 3) stacked [nblk][C] double tables (table j at part + j * nblk * C), summed by one 256-thread
+// block: 4 rows' loads in flight per thread, then a wave shuffle tree and an LDS fold; the sums land in thread 0
+__device__ __forceinline__ void fold_columns(const double* part, int nblk, int C, int c, int k, double* out) {
+  __shared__ double sh[3][4];
+  double s[3] = {0.0, 0.0, 0.0};
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const long tab = (long)nblk * C;
+  int b = t;
+  for (; b + 3 * 256 < nblk; b += 4 * 256) {
+    double v[3][4];
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[j][u] = j < k ? part[j * tab + (long)(b + u * 256) * C + c] : 0.0;
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) s[j] += v[j][u];
+  }
+  for (; b < nblk; b += 256)
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+      if (j < k) s[j] += part[j * tab + (long)b * C + c];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    for (int o = 32; o > 0; o >>= 1) s[j] += __shfl_down(s[j], o);
+    if (lane == 0) sh[j][wave] = s[j];
+  }
+  __syncthreads();
+  if (t == 0)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) out[j] = sh[j][0] + sh[j][1] + sh[j][2] + sh[j][3];
+}
+
 inline int grid_for(long work, int block, int max_blocks = 256 * 16) {
   long g = (work + block - 1) / block;
   if (g > max_blocks) g = max_blocks;

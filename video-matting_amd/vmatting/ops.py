@@ -731,11 +731,18 @@ def bn_backward_apply(x, dy, y, mean, var, gamma, sum_g, sum_gx, count, dx, eps=
     return dx
 
 
-def relu_backward(dy, y, dx, dx2=None):
+def relu_backward(dy, y, dx, dx2=None, dx_lo=None):
+    """dx = dy * (y > 0) (+ a second copy dx2, e.g. bf16).  ``dx_lo``: its channels k = dx_lo.shape[-1] take the
+    first k channels of the gradient and dx / dx2 the rest (one pass over a decoder level's concat)."""
     dv, yv, xv = nhwc(dy), nhwc(y), nhwc(dx)
     x2 = ctypes.byref(nhwc(dx2)) if dx2 is not None else None
-    check(lib().vm_relu_backward_ex_nhwc(ctypes.byref(dv), ctypes.byref(yv), ctypes.byref(xv), x2, stream_handle()),
-          "relu_backward")
+    if dx_lo is None:
+        check(lib().vm_relu_backward_ex_nhwc(ctypes.byref(dv), ctypes.byref(yv), ctypes.byref(xv), x2,
+                                             stream_handle()), "relu_backward")
+        return dx
+    lv = nhwc(dx_lo)
+    check(lib().vm_relu_backward_split_nhwc(ctypes.byref(dv), ctypes.byref(yv), dx_lo.shape[-1], ctypes.byref(lv),
+                                            ctypes.byref(xv), x2, stream_handle()), "relu_backward")
     return dx
 
 

@@ -180,6 +180,8 @@ class VideoTrainer:
             tb["dcatn_" + up] = F(lv, (width + 3) // 4 * 4)[..., :width]  # conv1's dgrad writes 32 (padded)
             tb["dcat_" + up] = F(lv, width)
             tb["du_" + up] = F(lv, self.model.convs[up].cout)
+            # the select convs' masked gradients, split off the concat's in the same relu-backward pass
+            tb["gsel_" + up] = F(lv, sum(self.model.convs[s].cout for s, _ in sels))
             if up in DGRAD:
                 tb["dr_" + up] = F(lv, self.model.convs[up].cin)
                 tb["dprev_" + up] = F(lv + 1, self.model.convs[up].cin)
@@ -328,20 +330,23 @@ class VideoTrainer:
             self._conv_backward(conv, cn, dout, b[out_key], tb, dgrad_out=tb["dcatn_" + up])
             mean, var = tb["st_" + up]
             self._bn_backward(c, tb["dcatn_" + up], None, mean, var, up, tb["dcat_" + up])
-            dcat, off = tb["dcat_" + up], 0
+            # one relu-backward pass over the concat: the select channels to gsel (dense, so each select's BN
+            # backward reads its 2-16 channels without dragging the whole concat row through), the upconv's to du
+            gsel, off = tb["gsel_" + up], 0
+            g16 = tb.get("g16_" + up)
+            nsel = gsel.shape[-1]
+            du = ops.relu_backward(tb["dcat_" + up], c, tb["du_" + up],
+                                   dx2=None if g16 is None else g16[..., :width - nsel], dx_lo=gsel)
             for i, (s, src) in enumerate(sels):
                 co = m.convs[s].cout
                 if self._side:  # leaves of the backward graph: beside the decoder chain, joined before the update
                     st = self._side[i % len(self._side)]
                     st.wait_stream(main)
                     with torch.cuda.stream(st):
-                        self._conv_backward(s, self._src(b, src), dcat[..., off:off + co], c[..., off:off + co], tb)
+                        self._conv_backward(s, self._src(b, src), gsel[..., off:off + co], None, tb)
                 else:
-                    self._conv_backward(s, self._src(b, src), dcat[..., off:off + co], c[..., off:off + co], tb)
+                    self._conv_backward(s, self._src(b, src), gsel[..., off:off + co], None, tb)
                 off += co
-            g16 = tb.get("g16_" + up)
-            du = ops.relu_backward(dcat[..., off:width], c[..., off:width], tb["du_" + up],
-                                   dx2=None if g16 is None else g16[..., :width - off])
             ops.conv_wgrad(b[RBUF[up]], du, self.G[up, "w"], mfma=self._mfma_wgrad)
             if up in DGRAD:
                 if g16 is not None:
