@@ -846,3 +846,32 @@ def test_unet_video_1080p_bf16_properties(vgg0):
     err = float((af - a2).abs().max())
     print("1080p bf16 vs fp32 alpha max-abs diff: %.3e" % err)
     assert err < 5e-2
+
+
+@pytest.mark.parametrize("xc,yc,ys,odt", [(3, 8, 8, torch.bfloat16), (3, 3, 32, torch.bfloat16), (7, 16, 16, torch.float32),
+                                          (20, 24, 24, torch.bfloat16), (5, 5, 8, torch.float32)])
+@pytest.mark.parametrize("affine", [False, True])
+def test_convert_views(xc, yc, ys, odt, affine):
+    """vm_convert_nhwc (pixel-per-thread form for outputs of <= 16 channels, element form above): x's channels
+    through the optional affine + relu into a channel slice of a wider buffer, extra channels zero, the rest of the
+    buffer untouched."""
+    from vmatting import ops
+    rs = np.random.RandomState(xc * 7 + yc)
+    n, h, w = 2, 19, 37
+    x = rs.normal(size=(n, h, w, xc)).astype(np.float32) * 3
+    sc = (rs.normal(size=xc) + 1).astype(np.float32) if affine else None
+    sh = rs.normal(size=xc).astype(np.float32) if affine else None
+    buf = torch.full((n, h, w, ys), 7.0, dtype=odt, device=DEV)
+    off = ys - yc
+    ops.convert(T(x), buf[..., off:], scale=None if sc is None else T(sc), shift=None if sh is None else T(sh),
+                act="relu" if affine else "none")
+    got = H(buf)
+    if affine:  # x * scale + shift may be one fused multiply-add on the device: within one rounding of the output
+        ref = np.maximum(x.astype(np.float64) * sc + sh, 0)
+        tol = 2.0 ** -7 if odt == torch.bfloat16 else 1e-6
+        assert np.all(np.abs(got[..., off:off + xc] - ref) <= tol * np.abs(ref) + 1e-6)
+    else:
+        ref = torch.from_numpy(x).to(odt).float().numpy()
+        assert np.array_equal(got[..., off:off + xc], ref)
+    assert not got[..., off + xc:].any()
+    assert (got[..., :off] == 7.0).all()

@@ -257,20 +257,29 @@ __global__ __launch_bounds__(256) void resize2x_tf1_rows(View x, View y, int bpr
 }
 
 // ---------------------------------------------------------------- convert / pad / affine
+__device__ __forceinline__ float convert_one(const View& x, long p, int c, const float* scale, const float* shift,
+                                             int act) {
+  float v = ldv(x, p, c);
+  if (scale) v *= scale[c];
+  if (shift) v += shift[c];
+  return act == VM_ACT_RELU ? fmaxf(v, 0.f) : act == VM_ACT_SIGMOID ? sigmoid_precise(v) : v;
+}
+
 __global__ void convert_kernel(View x, View y, const float* scale, const float* shift, int act) {
   const long total = (long)y.n * y.h * y.w * y.c;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
     const int c = (int)(i % y.c);
     const long p = i / y.c;
-    float v = 0.f;
-    if (c < x.c) {
-      v = ldv(x, p, c);
-      if (scale) v *= scale[c];
-      if (shift) v += shift[c];
-      v = act == VM_ACT_RELU ? fmaxf(v, 0.f) : act == VM_ACT_SIGMOID ? sigmoid_precise(v) : v;
-    }
-    stv(y, p, c, v);
+    stv(y, p, c, c < x.c ? convert_one(x, p, c, scale, shift, act) : 0.f);
   }
+}
+
+// narrow outputs (y.c <= 16: the network inputs, pads and channel slices): one thread per pixel walks its channels,
+// so no element index is divided (the 64-bit i / y.c above costs more than the copy)
+__global__ void convert_px_kernel(View x, View y, const float* scale, const float* shift, int act) {
+  const long M = (long)y.n * y.h * y.w;
+  for (long p = blockIdx.x * (long)blockDim.x + threadIdx.x; p < M; p += (long)gridDim.x * blockDim.x)
+    for (int c = 0; c < y.c; ++c) stv(y, p, c, c < x.c ? convert_one(x, p, c, scale, shift, act) : 0.f);
 }
 
 // ---------------------------------------------------------------- batch-norm statistics
@@ -470,7 +479,12 @@ extern "C" int vm_convert_nhwc(const vm_tensor* x, vm_tensor* y, const float* sc
   if (y->n != x->n || y->h != x->h || y->w != x->w || y->c < x->c) return fail(VM_EINVAL, "convert: shape mismatch");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const long work = (long)y->n * y->h * y->w * y->c;
-  hipLaunchKernelGGL(convert_kernel, dim3(grid_for(work, 256)), dim3(256), 0, st, view(x), view(y), scale, shift, act);
+  if (y->c <= 16)
+    hipLaunchKernelGGL(convert_px_kernel, dim3(grid_for(work / y->c, 256)), dim3(256), 0, st, view(x), view(y), scale,
+                       shift, act);
+  else
+    hipLaunchKernelGGL(convert_kernel, dim3(grid_for(work, 256)), dim3(256), 0, st, view(x), view(y), scale, shift,
+                       act);
   return check_launch("convert");
 }
 

@@ -210,17 +210,31 @@ __global__ __launch_bounds__(256) void loss_partial_kernel(const float* __restri
   }
 }
 
-__global__ void loss_final_kernel(const double* part, int nblk, long P, float* out) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+// one 256-thread block folds the nblk partial pairs (a fixed tree: deterministic; a single thread's serial walk of
+// 1024 dependent loads took 47 us)
+__global__ __launch_bounds__(256) void loss_final_kernel(const double* part, int nblk, long P, float* out) {
+  __shared__ double sh[2][256];
   double sa = 0.0, sc = 0.0;
-  for (int b = 0; b < nblk; ++b) {
+  for (int b = threadIdx.x; b < nblk; b += 256) {
     sa += part[2 * b];
     sc += part[2 * b + 1];
   }
-  const double la = sa / (double)P, lc = sc / (3.0 * (double)P);
-  out[0] = (float)(0.5 * la + 0.5 * lc);
-  out[1] = (float)la;
-  out[2] = (float)lc;
+  sh[0][threadIdx.x] = sa;
+  sh[1][threadIdx.x] = sc;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) {
+      sh[0][threadIdx.x] += sh[0][threadIdx.x + s];
+      sh[1][threadIdx.x] += sh[1][threadIdx.x + s];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const double la = sh[0][0] / (double)P, lc = sh[1][0] / (3.0 * (double)P);
+    out[0] = (float)(0.5 * la + 0.5 * lc);
+    out[1] = (float)la;
+    out[2] = (float)lc;
+  }
 }
 
 }  // namespace vm
@@ -308,6 +322,6 @@ extern "C" int vm_matting_loss(const float* pred, const float* gt, const float* 
   hipLaunchKernelGGL(loss_partial_kernel, dim3(nblk), dim3(256), 0, st, pred, gt, raw_fg, bg, cmp, pixels, part);
   int rc = check_launch("loss_partial");
   if (rc) return rc;
-  hipLaunchKernelGGL(loss_final_kernel, dim3(1), dim3(64), 0, st, part, nblk, pixels, out);
+  hipLaunchKernelGGL(loss_final_kernel, dim3(1), dim3(256), 0, st, part, nblk, pixels, out);
   return check_launch("loss_final");
 }
