@@ -875,3 +875,47 @@ def test_convert_views(xc, yc, ys, odt, affine):
         assert np.array_equal(got[..., off:off + xc], ref)
     assert not got[..., off + xc:].any()
     assert (got[..., :off] == 7.0).all()
+
+
+PACK_CASES = [  # n, h, w, cin, cout, mode
+    (3, 20, 20, 64, 64, "plain"), (5, 40, 40, 128, 128, "pool"), (4, 37, 22, 64, 64, "pool"),
+    (3, 19, 21, 64, 128, "plain"), (6, 20, 20, 512, 64, "splitk"), (4, 40, 40, 96, 32, "f32"),
+    (8, 20, 20, 64, 64, "sources"), (2, 9, 50, 64, 64, "plain")]
+
+
+@pytest.mark.parametrize("case", PACK_CASES)
+def test_packed_frames_bit_identical(case):
+    """Packed frames (narrow frames tiled as one virtual image, ConvArgs::vstride): outputs, fused pool, split-K
+    partials, f32 pre-BN output and tower-major split sources equal the per-frame tiling bit for bit, and the
+    oracle within the bf16 bound."""
+    from vmatting import _lib, ops
+    n, h, w, cin, cout, mode = case
+    rs = np.random.RandomState(n * 1000 + w + cout)
+    nsrc = 2 if mode == "sources" else 1
+    x = rs.normal(size=(nsrc * n, h, w, cin)).astype(np.float32)
+    wt = (rs.normal(size=(3, 3, nsrc * cin, cout)) * 0.05).astype(np.float32)
+    b = (rs.normal(size=cout) * 0.1).astype(np.float32)
+    pc = ops.PackedConv(wt, b, torch.bfloat16, DEV)
+    xd = T(x, torch.bfloat16)
+    odt = torch.float32 if mode == "f32" else torch.bfloat16
+
+    def run():
+        out = torch.zeros((n, h, w, cout), dtype=odt, device=DEV)
+        pool = torch.zeros((n, (h + 1) // 2, (w + 1) // 2, cout), dtype=torch.bfloat16, device=DEV)
+        src = ops.SourceConcat(xd, nsrc) if mode == "sources" else xd
+        ops.conv3x3(src, pc, "relu", out=out, pool_out=pool if mode == "pool" else None, splitk=mode == "splitk")
+        return out, pool, _lib.last_conv_kernel()
+
+    try:
+        _lib.set_option("pack_frames", 0)
+        y0, p0, k0 = run()
+        _lib.set_option("pack_frames", 1)
+        y1, p1, k1 = run()
+    finally:
+        _lib.set_option("pack_frames", 1)
+    assert k0 == k1 and k0.startswith("vm::conv3x3_patch"), (k0, k1)
+    assert torch.equal(y0, y1) and torch.equal(p0, p1)
+    xcat = np.concatenate([H(xd[s * n:(s + 1) * n]) for s in range(nsrc)], -1)
+    wb = torch.from_numpy(wt).to(torch.bfloat16).float().numpy().astype(np.float64)
+    ref = np.maximum(oops.conv3x3_same(xcat, wb) + b, 0)
+    assert relerr(H(y1), ref) < 2e-2

@@ -730,12 +730,25 @@ void conv3x3_patch(ConvArgs a) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave % WM, wn = wave / WM;
   const int H = a.H, W = a.W, cs = a.x_cstride;
-  const int th = (H + C::TH - 1) / C::TH, tw = (W + C::TW - 1) / C::TW;
+  const int VW = a.vstride ? a.vW : W;  // packed frames: one virtual image (n = 0), ConvArgs::vstride
+  const int th = (H + C::TH - 1) / C::TH, tw = (VW + C::TW - 1) / C::TW;
   const int t = xcd_tile(blockIdx.x, a.tiles_total);
   const int st = t / a.tiles_n, nt = t - st * a.tiles_n;
   const int n = st / (th * tw), srem = st - n * th * tw;
   const int r0 = (srem / tw) * C::TH, c0 = (srem - (srem / tw) * tw) * C::TW;
   const int n0 = nt * BN;
+  // pixel offset (in pixels, from row r0 of the tile's frame / of frame 0 when packed) of tile pixel (pr, pc) of
+  // the output; ok says whether it is a real output pixel
+  auto out_pix = [&](int pr, int pc, bool& ok) {
+    const int v = c0 + pc;
+    if (a.vstride) {
+      const int f = v / a.vstride, x = v - f * a.vstride;
+      ok = r0 + pr < H && x < W && v < VW;
+      return (f * H + pr) * W + x;
+    }
+    ok = r0 + pr < H && v < W;
+    return pr * W + pc;
+  };
 
   const T* xb = reinterpret_cast<const T*>(a.x) + a.x_coff + ((long)n * H + r0 - 1) * (long)W * cs;
   const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<T*>(xb), 0, 0x7ffffff0, 0x00020000);
@@ -757,8 +770,14 @@ void conv3x3_patch(ConvArgs a) {
       h = min(h, H - 1);
       w = min(w, W - 1);
     }
-    const bool ok = row < C::PPIX && (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
-    xoff[i] = ok ? (((h - r0 + 1) * W + w) * cs + lq * 8) * 2 : OOB;
+    bool ok = row < C::PPIX && (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)VW;
+    int pix = (h - r0 + 1) * W + w;
+    if (a.vstride && ok) {  // virtual column -> (frame, column); the two columns past a frame read as zero
+      const int f = w / a.vstride, x = w - f * a.vstride;
+      ok = x < W;
+      pix = (f * H + h - r0 + 1) * W + x;
+    }
+    xoff[i] = ok ? (pix * cs + lq * 8) * 2 : OOB;
     if (piece < C::XP) ++x_n;
   }
   int woff[WPW];
@@ -985,7 +1004,8 @@ void conv3x3_patch(ConvArgs a) {
   const int ycs2 = a.y_cstride * 2;
   const int YW = a.up ? 2 * W : W;
   T* yb = reinterpret_cast<T*>(a.y) + a.y_coff +
-          (a.up ? (((long)n * 2 * H + 2 * r0) * YW + 2 * c0) : (((long)n * H + r0) * W + c0)) * (long)a.y_cstride;
+          (a.up ? (((long)n * 2 * H + 2 * r0) * YW + 2 * c0) : (((long)n * H + r0) * W + (a.vstride ? 0 : c0))) *
+              (long)a.y_cstride;
   const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(yb, 0, 0x7ffffff0, 0x00020000);
   constexpr int SPW = C::TPN / 64;  // 64-channel slabs per wave column
   const bool splitk = a.ksplit > 1;
@@ -993,8 +1013,9 @@ void conv3x3_patch(ConvArgs a) {
     // f32 output (the training step's pre-BN buffers, unet_simple.py:19-27) or a split-K partial: f32 slab staging,
     // 4 channels per 16-byte store; no fused pool / folded resize on this path (host-checked)
     const int ycs = splitk ? a.cout : a.y_cstride;
-    float* yf = splitk ? a.part + (long)blockIdx.y * a.M * a.cout + (((long)n * H + r0) * W + c0) * (long)ycs
-                       : reinterpret_cast<float*>(a.y) + a.y_coff + (((long)n * H + r0) * W + c0) * (long)ycs;
+    const long pix0 = ((long)n * H + r0) * W + (a.vstride ? 0 : c0);
+    float* yf = splitk ? a.part + (long)blockIdx.y * a.M * a.cout + pix0 * ycs
+                       : reinterpret_cast<float*>(a.y) + a.y_coff + pix0 * ycs;
     const __amdgpu_buffer_rsrc_t yfr = __builtin_amdgcn_make_buffer_rsrc(yf, 0, 0x7ffffff0, 0x00020000);
     const int ycs4 = ycs * 4;
     for (int sl = 0; sl < BN / 64; ++sl) {
@@ -1034,8 +1055,10 @@ void conv3x3_patch(ConvArgs a) {
         const int rr = idx >> 4, cq = idx & 15;
         const uint4 d = *reinterpret_cast<const uint4*>(smem + rr * C::SR32 + cq * 16);
         const int pr = rr / C::TW, pc = rr % C::TW;
-        const bool ok = r0 + pr < H && c0 + pc < W && cb + cq * 4 < a.cout;
-        const int off = ok ? (pr * W + pc) * ycs4 + (cb + cq * 4) * 4 : OOB;
+        bool ok;
+        const int pix = out_pix(pr, pc, ok);
+        ok = ok && cb + cq * 4 < a.cout;
+        const int off = ok ? pix * ycs4 + (cb + cq * 4) * 4 : OOB;
         if (splitk || a.y_vec) {
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, d),
                                                  yfr, off, 0, 0);
@@ -1091,8 +1114,10 @@ void conv3x3_patch(ConvArgs a) {
       const int rr = idx >> 3, cq = idx & 7;
       const uint4 d = *reinterpret_cast<const uint4*>(smem + rr * C::SR + cq * 16);
       const int pr = rr / C::TW, pc = rr % C::TW;
-      const bool ok = r0 + pr < H && c0 + pc < W && cb + cq * 8 < ccap;
-      const int pix = a.up ? (2 * pr + (phase >> 1)) * YW + 2 * pc + (phase & 1) : pr * W + pc;
+      bool ok;
+      int pix = out_pix(pr, pc, ok);
+      ok = ok && cb + cq * 8 < ccap;
+      if (a.up) pix = (2 * pr + (phase >> 1)) * YW + 2 * pc + (phase & 1);
       const int off = ok ? pix * ycs2 + (cb + cq * 8) * 2 : OOB;
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, d), yrs,
                                              off, 0, 0);
@@ -1100,9 +1125,11 @@ void conv3x3_patch(ConvArgs a) {
     if (a.py) {
       // fused tf.nn.max_pool 2x2/2 SAME (unet.py:32-33) of the staged slab: tiles start on even rows/columns,
       // so every window lies inside the tile; taps past the frame edge are skipped (never win)
+      // (packed frames: W even, so frames start on even virtual columns and every window is inside one frame)
       const int PH = (H + 1) >> 1, PW = (W + 1) >> 1;
       const int pr0 = r0 >> 1, pc0 = c0 >> 1;
-      T* pb = reinterpret_cast<T*>(a.py) + a.py_coff + (((long)n * PH + pr0) * PW + pc0) * (long)a.py_cstride + n0;
+      T* pb = reinterpret_cast<T*>(a.py) + a.py_coff +
+              (((long)n * PH + pr0) * PW + (a.vstride ? 0 : pc0)) * (long)a.py_cstride + n0;
       const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(pb, 0, 0x7ffffff0, 0x00020000);
       constexpr int PTW = C::TW / 2, PITEMS = C::BM / 4 * 8;
 #pragma unroll
@@ -1112,7 +1139,10 @@ void conv3x3_patch(ConvArgs a) {
         const int pp = idx >> 3, cq = idx & 7;
         const int pr = pp / PTW, pc = pp % PTW;
         const int rr = 2 * pr * C::TW + 2 * pc;
-        const bool vh = r0 + 2 * pr + 1 < H, vw = c0 + 2 * pc + 1 < W;
+        bool in;
+        const int fpix = out_pix(2 * pr, 2 * pc, in);  // the window's top-left output pixel
+        const int fx = fpix % W;                        // its frame column (even)
+        const bool vh = r0 + 2 * pr + 1 < H, vw = a.vstride ? fx + 1 < W : c0 + 2 * pc + 1 < W;
         float m[8], f[8];
         Chunk<T>::unpack(*reinterpret_cast<const uint4*>(smem + rr * C::SR + cq * 16), m);
         if (vw) {
@@ -1130,8 +1160,14 @@ void conv3x3_patch(ConvArgs a) {
 #pragma unroll
           for (int j = 0; j < 8; ++j) m[j] = fmaxf(m[j], f[j]);
         }
-        const bool ok = pr0 + pr < PH && pc0 + pc < PW && n0 + sl * 64 + cq * 8 < a.cout;
-        const int off = ok ? ((pr * PW + pc) * a.py_cstride + sl * 64 + cq * 8) * 2 : OOB;
+        int ppix = pr * PW + pc;
+        bool ok = pr0 + pr < PH && pc0 + pc < PW;
+        if (a.vstride) {  // pooled pixel (frame, pr0 + pr, fx / 2)
+          ok = in;
+          ppix = ((fpix / W - 2 * pr) / H * PH + pr) * PW + fx / 2;
+        }
+        ok = ok && n0 + sl * 64 + cq * 8 < a.cout;
+        const int off = ok ? (ppix * a.py_cstride + sl * 64 + cq * 8) * 2 : OOB;
         __builtin_amdgcn_raw_buffer_store_b128(
             __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, Chunk<T>::pack(m)), prs, off, 0, 0);
       }
@@ -2861,7 +2897,8 @@ static int launch_patch(ConvArgs& a, hipStream_t st) {
     attr_set = true;
   }
   const long N = a.M / ((long)a.H * a.W);
-  const long sp = N * ((a.H + C::TH - 1) / C::TH) * ((a.W + C::TW - 1) / C::TW);
+  const long sp = a.vstride ? ((a.H + C::TH - 1) / C::TH) * (long)((a.vW + C::TW - 1) / C::TW)
+                            : N * ((a.H + C::TH - 1) / C::TH) * ((a.W + C::TW - 1) / C::TW);
   a.tiles_n = (a.cout + BN - 1) / BN;
   if (sp * a.tiles_n > 0x7fffffffL) return fail(VM_EUNSUPPORTED, "conv3x3: too many tiles");
   a.tiles_total = (int)(sp * a.tiles_n);
@@ -2965,7 +3002,29 @@ static bool patch_ok(const ConvArgs& a, size_t tsize) {
          (a.x_src_c <= 0 || a.x_src_c % 32 == 0);
 }
 
+// packed frames (ConvArgs::vstride): a batch of narrow frames tiled as one virtual image when that saves >= 10 % of
+// the column tiles (8 x 320^2 training crops: the 80 / 40 / 20-wide tower levels, 3 / 2 / 1 tiles per frame -> 2.6
+// / 1.3 / 0.7).  Results are bit-identical (every output keeps its K loop); only which pixels share a block changes.
+// Off for the folded upconvs, odd widths under a fused pool, and where the batch's 32-bit byte offsets would wrap.
+static long g_pack_frames = 1;
+static void plan_packed_frames(ConvArgs& a) {
+  a.vstride = a.vW = 0;
+  const long N = a.M / ((long)a.H * a.W);
+  if (!g_pack_frames || a.up || N < 2 || (a.py && (a.W & 1))) return;
+  const long plain = N * ((a.W + 31) / 32), packed = (N * (a.W + 2) + 31) / 32;
+  if (packed * 10 > plain * 9 || N * (a.W + 2) > 0x7fffffffL) return;
+  const long lim = 0x7ffffff0L;
+  long xspan = a.M * a.x_cstride * 2;
+  if (a.x_src_c > 0) xspan += (long)(a.cin_pad / a.x_src_c - 1) * a.x_src_stride * 2;
+  const long yspan = a.ksplit > 1 ? a.M * a.cout * 4 : a.M * a.y_cstride * (a.y_dtype == VM_F32 ? 4 : 2);
+  const long pspan = a.py ? N * ((a.H + 1) / 2) * ((a.W + 1) / 2) * a.py_cstride * 2 : 0;
+  if (xspan >= lim || yspan >= lim || pspan >= lim) return;
+  a.vstride = a.W + 2;
+  a.vW = (int)(N * (a.W + 2));
+}
+
 static int dispatch_patch(ConvArgs& a, hipStream_t st) {
+  plan_packed_frames(a);
   if (a.ksplit > 1) {  // split-K: the 4 x 32-pixel row-slot config, then the fixed-order reduction
     int rc = launch_patch<64, 4, 1, 2, 4, 2, 9, false, 0, false, 3>(a, st);
     if (rc) return rc;
@@ -3041,7 +3100,7 @@ static int dispatch_patch(ConvArgs& a, hipStream_t st) {
   }
   // row-stationary kernel (conv_rows.hip) on grids of >= g_rows_min_blocks 16 x 32 px x 64 channel blocks (one block
   // per CU: ~4 full rounds); rows_kernel 8 / 16 forces that tile height wherever it is legal
-  if (g_rows_kernel && rows_ok(a)) {
+  if (g_rows_kernel && rows_ok(a) && !a.vstride) {
     if (g_rows_kernel == 8 || g_rows_kernel == 16) return launch_rows(a, st, (int)g_rows_kernel);
     const long N16 = a.M / ((long)a.H * a.W);
     const long blocks16 = N16 * ((a.H + 15) / 16) * ((a.W + 31) / 32) * ((a.cout + 63) / 64);
@@ -3060,7 +3119,7 @@ static int dispatch_patch(ConvArgs& a, hipStream_t st) {
   // of >= ~2 full rounds of blocks, a 3-slot ring for the largest grids, 4 x 32 px tiles for grids under 2 rounds.
   // Same-box A/B of the whole forward (bench.py --option patch_rowslot=0|1): 292.4 -> 306.8 frames/s
   const long N = a.M / ((long)a.H * a.W);
-  const long sp = N * ((a.H + 7) / 8) * ((a.W + 31) / 32);
+  const long sp = a.vstride ? ((a.H + 7) / 8) * (long)((a.vW + 31) / 32) : N * ((a.H + 7) / 8) * ((a.W + 31) / 32);
   const long blocks64 = sp * ((a.cout + 63) / 64);
 #ifdef VM_STUDY
   if (!g_patch_rowslot) {
@@ -3243,6 +3302,11 @@ extern "C" int vm_set_option(const char* key, long value) {
   }
   if (!strcmp(key, "rows_min_blocks")) {
     g_rows_min_blocks = value;
+    return VM_OK;
+  }
+  if (!strcmp(key, "pack_frames")) {
+    if (value < 0 || value > 1) return fail(VM_EINVAL, "pack_frames must be 0 or 1");
+    g_pack_frames = value;
     return VM_OK;
   }
   if (!strcmp(key, "up_skip")) {

@@ -40,6 +40,11 @@ struct ConvArgs {
   float* hd;
   const float* hw;
   int hw_cin, hw_coff, y_skip;
+  // packed frames (patch kernel): vstride > 0 tiles the batch as ONE virtual image of width vW = N * vstride whose
+  // column v is column v % vstride of frame v / vstride; vstride = W + 2, so every frame is followed by two columns
+  // outside it (zero input: the SAME padding of both neighbours; their outputs are never stored).  Narrow frames
+  // (40 or 20 px in 32-px tiles) stop wasting most of their last column tile.
+  int vstride, vW;
 };
 
 // element offset of input channel c (relative to the view's channel 0) under the source split
