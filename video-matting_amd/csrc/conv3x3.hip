@@ -3100,8 +3100,11 @@ static int dispatch_patch(ConvArgs& a, hipStream_t st) {
   }
   // row-stationary kernel (conv_rows.hip) on grids of >= g_rows_min_blocks 16 x 32 px x 64 channel blocks (one block
   // per CU: ~4 full rounds); rows_kernel 8 / 16 forces that tile height wherever it is legal
-  if (g_rows_kernel && rows_ok(a) && !a.vstride) {
-    if (g_rows_kernel == 8 || g_rows_kernel == 16) return launch_rows(a, st, (int)g_rows_kernel);
+  if (g_rows_kernel && rows_ok(a)) {
+    if (g_rows_kernel == 8 || g_rows_kernel == 16) {  // forced: per-frame tiles (the rows kernel does not pack)
+      a.vstride = a.vW = 0;
+      return launch_rows(a, st, (int)g_rows_kernel);
+    }
     const long N16 = a.M / ((long)a.H * a.W);
     const long blocks16 = N16 * ((a.H + 15) / 16) * ((a.W + 31) / 32) * ((a.cout + 63) / 64);
     // measured in the 1080p forward (scripts/opt_ab.sh): a win for cin >= 512 (upconv_2, conv3_4) and for cin 256 on
@@ -3109,7 +3112,7 @@ static int dispatch_patch(ConvArgs& a, hipStream_t st) {
     // ... and only where its 16-row tiles waste no more rows than the patch kernel's 8-row ones (the training
     // towers' 40 x 40 level: 48 of 40 rows vs 40, measured 612 vs ~800 TFLOP/s)
     const bool rows_fit = ((a.H + 15) / 16) * 16 <= ((a.H + 7) / 8) * 8 + a.H / 32;
-    if ((!a.up || g_rows_up) && rows_fit && blocks16 >= g_rows_min_blocks && a.cin_pad >= g_rows_min_cin &&
+    if ((!a.up || g_rows_up) && !a.vstride && rows_fit && blocks16 >= g_rows_min_blocks && a.cin_pad >= g_rows_min_cin &&
         (a.cin_pad >= 2 * g_rows_min_cin || blocks16 >= 2 * g_rows_min_blocks))
       return launch_rows(a, st, 16);
   }
