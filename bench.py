@@ -456,7 +456,8 @@ def train_flops(n, h, w):
     return fwd + head, head + dgrad
 
 
-def train_bench(dev, steps, warmup, world, rank, threads, cpu=True, n=8, size=320, dtype="bf16", graph=False):
+def train_bench(dev, steps, warmup, world, rank, threads, cpu=True, n=8, size=320, dtype="bf16", graph=False,
+                streams=3):
     """BASELINE config 5: one train.py video_procedure iteration per step (train.py:288-343) — batch of 8 320x320
     samples per GPU (params.py:8-9) resident in HBM: 3 VGG16 towers + UNetSimple (batch-statistics BN) forward,
     loss, backward through the trainable layers, one RCCL all-reduce of the gradients (DDP), TF-Adam, re-pack.
@@ -474,7 +475,7 @@ def train_bench(dev, steps, warmup, world, rank, threads, cpu=True, n=8, size=32
     T = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.float32)).to(dev)  # noqa: E731
     cmp_d, bg_d, warped_d, gt_d, fg_d = T(cmp), T(bg - mean), T(warped), T(gt), T(fg)
     np.random.seed(1)
-    trn = VideoTrainer(synthetic_vgg16(0), dtype, dev)
+    trn = VideoTrainer(synthetic_vgg16(0), dtype, dev, streams=streams)
     # eager launches (the select chains overlap the decoder on side streams); graph: forward + loss and backward
     # replayed from HIP graphs (VideoTrainer.capture), DDP exchange + Adam eager
     g = trn.capture(cmp_d, bg_d, warped_d, gt_d, fg_d) if graph else None
@@ -704,6 +705,8 @@ def main():
     ap.add_argument("--train-graph", action="store_true",
                     help="config-5 record from HIP-graph replays (VideoTrainer.capture) instead of eager launches: "
                          "the step is not host-bound, and the graph runs the side-stream select chains serially")
+    ap.add_argument("--train-streams", type=int, default=3,
+                    help="side streams of the config-5 trainer's select chains (0: one stream, for serial profiles)")
     ap.add_argument("--only", choices=["train", "train_chain", "temporal"],
                     help="profiling passes: run just this record (rank 0 / N=1) and print it")
     ap.add_argument("--temporal-sizes", default="500x1200,1080x1920", help="config-3 sizes HxW, comma separated")
@@ -724,7 +727,8 @@ def main():
     cpu_model, threads = host_info()
     if args.only:  # one record alone (rocprofv3 passes per record: tools/prof_bench.sh)
         if args.only == "train":
-            rec = train_bench(dev, args.steps, args.warmup, world, rank, threads, cpu=False, graph=args.train_graph)
+            rec = train_bench(dev, args.steps, args.warmup, world, rank, threads, cpu=False, graph=args.train_graph,
+                              streams=args.train_streams)
         elif args.only == "train_chain":
             rec = train_chain_bench(dev, args.steps, args.warmup)
         else:

@@ -1056,21 +1056,37 @@ __global__ void adam_kernel(float* var, float* m, float* v, const float* grad, l
   }
 }
 
-// dw[i] += sum over the gx block rows of the partials (fixed order: deterministic).  A block owns 64 columns; its
-// 4 waves stride the rows (independent loads in flight), then fold through LDS.  256-thread blocks: the 1024-thread
-// form waited for whole free CUs behind the side-stream wgrads (up to 120 us for a 14 MB fold).
+// dw[i] += sum over the gx block rows of the partials (fixed order: deterministic).  A block owns COLS columns;
+// its 256 / COLS row groups stride the rows (independent loads in flight), then fold through LDS.  64 columns for
+// wide filters; 16 for narrow ones (S = 9 cin cout under 32k: 64-column blocks left a few hundred blocks each
+// walking hundreds of rows).  256-thread blocks: a 1024-thread form waited for whole free CUs behind the
+// side-stream weight gradients.
+template <int COLS>
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* part, int rows, long S, float* dw) {
-  __shared__ float sh[4][64];
-  const int col = threadIdx.x & 63, rg = threadIdx.x >> 6;
-  const long i = (long)blockIdx.x * 64 + col;
+  constexpr int RG = 256 / COLS;
+  __shared__ float sh[RG][COLS];
+  const int col = threadIdx.x % COLS, rg = threadIdx.x / COLS;
+  const long i = (long)blockIdx.x * COLS + col;
   float s = 0.f;
   if (i < S) {
 #pragma unroll 8
-    for (int b = rg; b < rows; b += 4) s += part[(long)b * S + i];
+    for (int b = rg; b < rows; b += RG) s += part[(long)b * S + i];
   }
   sh[rg][col] = s;
   __syncthreads();
-  if (rg == 0 && i < S) dw[i] += (sh[0][col] + sh[1][col]) + (sh[2][col] + sh[3][col]);
+  if (rg == 0 && i < S) {
+    float t = 0.f;
+#pragma unroll
+    for (int g = 0; g < RG; ++g) t += sh[g][col];
+    dw[i] += t;
+  }
+}
+
+static void launch_wgrad_reduce(const float* part, int rows, long S, float* dw, hipStream_t st) {
+  if (S >= 64L * 512)
+    hipLaunchKernelGGL(wgrad_reduce_kernel<64>, dim3((unsigned)((S + 63) / 64)), dim3(256), 0, st, part, rows, S, dw);
+  else
+    hipLaunchKernelGGL(wgrad_reduce_kernel<16>, dim3((unsigned)((S + 15) / 16)), dim3(256), 0, st, part, rows, S, dw);
 }
 
 constexpr size_t WG_WS_CAP = 64ull << 20;  // workspace bytes
@@ -1098,7 +1114,7 @@ static void launch_wgrad_t(const V& xv, const V& dy, float* dw, float* ws, hipSt
   hipLaunchKernelGGL((wgrad_kernel<CC, CO4, T, XV, DV>), dim3((unsigned)gx, ncc), dim3(WG_NT), 0, st, xv, dy, ws,
                      tiles_h, tiles_w, ntiles);
   const long S = 9L * xv.c * dy.c;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((S + 63) / 64)), dim3(256), 0, st, ws, (int)gx, S, dw);
+  launch_wgrad_reduce(ws, (int)gx, S, dw, st);
 }
 
 static bool vec_ok(const V& v, int ve) {
@@ -1181,7 +1197,7 @@ static int launch_wgrad_grid(const void* kern, int lds, int th, int cib, int& at
   if (resident >= ncc && gx * ncc > resident) gx = resident / ncc;
   launch(dim3((unsigned)gx, ncc), lds, st, a);
   const long S = 9L * a.cin * a.cout;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((S + 63) / 64)), dim3(256), 0, st, a.part, (int)gx, S, dw);
+  launch_wgrad_reduce(a.part, (int)gx, S, dw, st);
   return VM_OK;
 }
 
