@@ -93,3 +93,27 @@ def test_thin_conv_matches_generic_kernels():
     finally:
         _lib.set_option("thin_kernel", 1)
     assert _err(y.cpu().numpy(), y0.cpu().numpy()) <= 1e-5
+
+
+@pytest.mark.parametrize("th", [8, 4, 16])
+@pytest.mark.parametrize("n,h,w,cin,cout,splitk", [(8, 160, 160, 384, 4, False), (6, 80, 80, 768, 8, True),
+                                                   (24, 40, 40, 192, 2, False)])
+def test_thin_persistent_walk_bit_identical(th, n, h, w, cin, cout, splitk):
+    """The persistent grid (blocks walk tiles blockIdx.x, +gridDim.x, ... with the next tile's first chunk in flight)
+    equals one block per tile (thin_rounds 0) bit for bit, at sizes with many tiles per block, split-K included."""
+    from vmatting import _lib, ops
+    rs = np.random.RandomState(n + w + th)
+    x = torch.from_numpy(rs.normal(size=(n, h, w, cin)).astype(np.float32)).to(DEV, torch.bfloat16)
+    pc = ops.PackedConv(rs.normal(size=(3, 3, cin, cout)).astype(np.float32) / 40, rs.normal(size=cout).astype(
+        np.float32), "bf16", DEV)
+    outs = []
+    try:
+        _lib.set_option("thin_th", th)
+        for rounds in (1, 0, 2):
+            _lib.set_option("thin_rounds", rounds)
+            outs.append(ops.conv3x3(x, pc, "relu", out_dtype=torch.float32, affine=False, splitk=splitk))
+            assert _lib.last_conv_kernel() == "vm::conv3x3_thin<%d>" % th
+    finally:
+        _lib.set_option("thin_rounds", 1)
+        _lib.set_option("thin_th", 8)
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])

@@ -2694,7 +2694,7 @@ __global__ __launch_bounds__(256) void conv3x3_up2x_border(BorderArgs a) {
 // while this one is consumed.  Output lane l: pixel l % 16, channels 4 (l / 16) .. +3.  ksplit > 1 splits the
 // chunks over gridDim.y into raw f32 partials (splitk_reduce_kernel, fixed order).
 template <int TH>
-__global__ __launch_bounds__(256) void conv3x3_thin(ConvArgs a) {
+__global__ __launch_bounds__(256, TH <= 4 ? 4 : TH <= 8 ? 3 : 2) void conv3x3_thin(ConvArgs a) {
   constexpr int TW = 32, PW = TW + 2, PPIX = (TH + 2) * PW, PIECES = PPIX * 4, PPT = (PIECES + 255) / 256;
   constexpr int RPW = TH / 4;    // patch rows per wave
   constexpr int WPIECES = 9 * 16 * 4, WPT = (WPIECES + 255) / 256;  // the chunk's filter: [tap][k/8][co 16]
@@ -2702,12 +2702,7 @@ __global__ __launch_bounds__(256) void conv3x3_thin(ConvArgs a) {
   __shared__ uint4 ws[WPT * 256];  // tail slots hold clamped duplicates (unconditional stores)
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int tw = (a.W + TW - 1) / TW, th = (a.H + TH - 1) / TH;
-  int t = blockIdx.x;
-  const int tx = t % tw;
-  t /= tw;
-  const int ty = t % th;
-  const int n = t / th;
-  const int r0 = ty * TH, c0 = tx * TW;
+  const int ntiles = a.tiles_total;
   const int nch = a.cin_pad / 32;
   int cb = 0, ce = nch;
   if (a.ksplit > 1) {
@@ -2715,40 +2710,67 @@ __global__ __launch_bounds__(256) void conv3x3_thin(ConvArgs a) {
     cb = blockIdx.y * per;
     ce = min(nch, cb + per);
   }
-  // byte offsets of this thread's patch pieces inside image n (out of the frame: out of range -> the hardware
-  // returns 0, SAME padding); the host guarantees H*W*cstride*2 < 2^31
-  int xoff[PPT];
+  int tile = blockIdx.x;
+  if (cb >= ce || tile >= ntiles) return;
+  // persistent: the block walks tiles blockIdx.x, +gridDim.x, ... and streams (tile, chunk) steps; the next step's
+  // patch and filter pieces (the next tile's first chunk at a tile's end) are in registers while this one computes
+  auto geo = [&](int t, int& n, int& r0, int& c0, int (&xo)[PPT]) {
+    const int tx = t % tw;
+    t /= tw;
+    const int ty = t % th;
+    n = t / th;
+    r0 = ty * TH;
+    c0 = tx * TW;
+    // byte offsets of this thread's patch pieces inside image n (out of the frame: out of range -> the hardware
+    // returns 0, SAME padding); the host guarantees H*W*cstride*2 < 2^31
 #pragma unroll
-  for (int i = 0; i < PPT; ++i) {
-    const int id = tid + i * 256;
-    const int p = id >> 2, q = id & 3;
-    const int pr = p / PW, pc = p - pr * PW;
-    const int yy = r0 - 1 + pr, xx = c0 - 1 + pc;
-    const bool ok = id < PIECES && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W;
-    xoff[i] = ok ? ((yy * a.W + xx) * a.x_cstride + q * 8) * 2 : OOB;
-  }
-  const uint16_t* Xn = reinterpret_cast<const uint16_t*>(a.x) + a.x_coff + (long)n * a.H * a.W * a.x_cstride;
+    for (int i = 0; i < PPT; ++i) {
+      const int id = tid + i * 256;
+      const int p = id >> 2, q = id & 3;
+      const int pr = p / PW, pc = p - pr * PW;
+      const int yy = r0 - 1 + pr, xx = c0 - 1 + pc;
+      const bool ok = id < PIECES && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W;
+      xo[i] = ok ? ((yy * a.W + xx) * a.x_cstride + q * 8) * 2 : OOB;
+    }
+  };
   const __amdgpu_buffer_rsrc_t wrs =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.w), 0, 0x7ffffff0, 0x00020000);  // 16 x K_pad bf16 used
   uint4 xr[PPT], wr[WPT];
-  // the chunk's patch pieces and filter pieces (tap, k/8, co: the A operand's lane order) into registers
-#define VM_THIN_FETCH(CC)                                                                                          \
-  {                                                                                                                \
-    const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(                                          \
-        const_cast<uint16_t*>(Xn + src_chan(a, (CC) * 32)), 0, 0x7ffffff0, 0x00020000);                            \
-    _Pragma("unroll") for (int i = 0; i < PPT; ++i) xr[i] =                                                        \
-        __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xrs, xoff[i], 0, 0));                      \
-    _Pragma("unroll") for (int i = 0; i < WPT; ++i) {                                                              \
-      const int id = min(tid + i * 256, WPIECES - 1);                                                              \
-      wr[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(                                     \
-          wrs, ((id & 15) * a.K_pad + ((CC) * 9 + (id >> 6)) * 32 + ((id >> 4) & 3) * 8) * 2, 0, 0));              \
-    }                                                                                                              \
+  // a chunk's patch pieces and filter pieces (tap, k/8, co: the A operand's lane order) into registers
+  auto fetch = [&](int n, const int (&xo)[PPT], int cc) {
+    const uint16_t* Xn = reinterpret_cast<const uint16_t*>(a.x) + a.x_coff + (long)n * a.H * a.W * a.x_cstride;
+    const __amdgpu_buffer_rsrc_t xrs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(Xn + src_chan(a, cc * 32)), 0, 0x7ffffff0, 0x00020000);
+#pragma unroll
+    for (int i = 0; i < PPT; ++i)
+      xr[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xrs, xo[i], 0, 0));
+#pragma unroll
+    for (int i = 0; i < WPT; ++i) {
+      const int id = min(tid + i * 256, WPIECES - 1);
+      wr[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
+                                            wrs, ((id & 15) * a.K_pad + (cc * 9 + (id >> 6)) * 32 + ((id >> 4) & 3) * 8) * 2,
+                                            0, 0));
+    }
+  };
+  const int co0 = 4 * (lane >> 4);
+  const bool splitk = a.ksplit > 1;
+  float mul[4], add[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int co = min(co0 + j, a.cout - 1);
+    const float sc = (a.scale && !splitk) ? a.scale[co] : 1.f;
+    mul[j] = sc;
+    add[j] = splitk ? 0.f : (a.bias ? a.bias[co] : 0.f) * sc + (a.shift ? a.shift[co] : 0.f);
   }
+
+  int n, r0, c0, xo[PPT];
+  geo(tile, n, r0, c0, xo);
+  fetch(n, xo, cb);
+  int cc = cb;
   f32x4 acc[2 * RPW];
 #pragma unroll
   for (int f = 0; f < 2 * RPW; ++f) acc[f] = f32x4{0.f, 0.f, 0.f, 0.f};
-  if (cb < ce) VM_THIN_FETCH(cb);
-  for (int cc = cb; cc < ce; ++cc) {
+  for (;;) {
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < PPT; ++i) {
@@ -2759,7 +2781,17 @@ __global__ __launch_bounds__(256) void conv3x3_thin(ConvArgs a) {
 #pragma unroll
     for (int i = 0; i < WPT; ++i) ws[tid + i * 256] = wr[i];
     __syncthreads();
-    if (cc + 1 < ce) VM_THIN_FETCH(cc + 1);
+    // the next step: the next chunk of this tile, or the first chunk of the block's next tile
+    const bool last = cc + 1 == ce;
+    const int ntile = last ? tile + (int)gridDim.x : tile;
+    const bool more = ntile < ntiles;
+    int nn = n, nr0 = r0, nc0 = c0, nxo[PPT];
+#pragma unroll
+    for (int i = 0; i < PPT; ++i) nxo[i] = xo[i];
+    if (more) {
+      if (last) geo(ntile, nn, nr0, nc0, nxo);
+      fetch(nn, nxo, last ? cb : cc + 1);
+    }
 #pragma unroll
     for (int tp = 0; tp < 9; ++tp) {
       const uint4 w = ws[tp * 64 + lane];  // A operand: output channel lane % 16, k = 8 (lane / 16) .. +7
@@ -2770,41 +2802,45 @@ __global__ __launch_bounds__(256) void conv3x3_thin(ConvArgs a) {
         const uint4 b = xs[pp * 4 + ((lane >> 4) ^ (((pp >> 2) & 1) << 1))];
         mma16<uint16_t>(w, b, acc[f]);
       }
+      __builtin_amdgcn_sched_barrier(0);  // one tap's fragments live at a time (registers: the prefetch is in flight)
     }
-  }
-  const int co0 = 4 * (lane >> 4);
-  if (co0 >= a.cout) return;
-  const bool splitk = a.ksplit > 1;
-  float mul[4], add[4];
+    if (last) {  // the tile's epilogue, straight from registers (no LDS: the next step's commit may follow)
+      if (co0 < a.cout) {
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int co = min(co0 + j, a.cout - 1);
-    const float sc = (a.scale && !splitk) ? a.scale[co] : 1.f;
-    mul[j] = sc;
-    add[j] = splitk ? 0.f : (a.bias ? a.bias[co] : 0.f) * sc + (a.shift ? a.shift[co] : 0.f);
-  }
+        for (int f = 0; f < 2 * RPW; ++f) {
+          const int row = r0 + wv * RPW + (f >> 1), col = c0 + (f & 1) * 16 + (lane & 15);
+          if (row >= a.H || col >= a.W) continue;
+          const long m = ((long)n * a.H + row) * a.W + col;
+          if (splitk) {
+            float* d = a.part + ((long)blockIdx.y * a.M + m) * a.cout + co0;
 #pragma unroll
-  for (int f = 0; f < 2 * RPW; ++f) {
-    const int row = r0 + wv * RPW + (f >> 1), col = c0 + (f & 1) * 16 + (lane & 15);
-    if (row >= a.H || col >= a.W) continue;
-    const long m = ((long)n * a.H + row) * a.W + col;
-    if (splitk) {
-      float* d = a.part + ((long)blockIdx.y * a.M + m) * a.cout + co0;
+            for (int j = 0; j < 4; ++j)
+              if (co0 + j < a.cout) d[j] = acc[f][j];
+            continue;
+          }
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if (co0 + j < a.cout) d[j] = acc[f][j];
-      continue;
+          for (int j = 0; j < 4; ++j) {
+            if (co0 + j >= a.cout) break;
+            float v = fmaf(acc[f][j], mul[j], add[j]);
+            if (a.act == VM_ACT_RELU) v = fmaxf(v, 0.f);
+            else if (a.act == VM_ACT_SIGMOID) v = sigmoid_precise(v);
+            const long o = m * a.y_cstride + a.y_coff + co0 + j;
+            if (a.y_dtype == VM_BF16) reinterpret_cast<uint16_t*>(a.y)[o] = f2bf(v);
+            else reinterpret_cast<float*>(a.y)[o] = v;
+          }
+        }
+      }
+#pragma unroll
+      for (int f = 0; f < 2 * RPW; ++f) acc[f] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
+    if (!more) break;
+    tile = ntile;
+    cc = last ? cb : cc + 1;
+    n = nn;
+    r0 = nr0;
+    c0 = nc0;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      if (co0 + j >= a.cout) break;
-      float v = fmaf(acc[f][j], mul[j], add[j]);
-      if (a.act == VM_ACT_RELU) v = fmaxf(v, 0.f);
-      else if (a.act == VM_ACT_SIGMOID) v = sigmoid_precise(v);
-      const long o = m * a.y_cstride + a.y_coff + co0 + j;
-      if (a.y_dtype == VM_BF16) reinterpret_cast<uint16_t*>(a.y)[o] = f2bf(v);
-      else reinterpret_cast<float*>(a.y)[o] = v;
-    }
+    for (int i = 0; i < PPT; ++i) xo[i] = nxo[i];
   }
 }
 
@@ -2954,12 +2990,39 @@ static int thin_splitk_plan(long n, int h, int w, int cin_pad) {
   const int per = (nch + ks - 1) / ks;
   return (nch + per - 1) / per;
 }
+// persistent grid: at most g_thin_rounds resident rounds of blocks (0: one block per tile, the r02 launch)
+static long g_thin_rounds = 1;
+template <int TH>
+static int thin_resident() {
+  static int dev_seen = -1, resident = 0;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (dev != dev_seen) {
+    int per_cu = 0, n_cu = 0;
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(&conv3x3_thin<TH>),
+                                                                256, 0);
+    if (e == hipSuccess) e = hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
+    if (e != hipSuccess) return -1;
+    resident = per_cu * n_cu;
+    dev_seen = dev;
+  }
+  return resident;
+}
 static int dispatch_thin(ConvArgs& a, long n, hipStream_t st) {
   const int th = (int)g_thin_th;
   const long tiles = n * ((a.H + th - 1) / th) * ((a.W + 31) / 32);
   if (tiles > 0x7fffffffL) return fail(VM_EUNSUPPORTED, "conv3x3_thin: too many tiles");
+  a.tiles_total = (int)tiles;
+  const int ks = a.ksplit > 1 ? a.ksplit : 1;
+  const int res = th == 16 ? thin_resident<16>() : th == 4 ? thin_resident<4>() : thin_resident<8>();
+  if (res < 0) return fail(VM_EHIP, "conv3x3_thin: occupancy query failed");
+  long gx = tiles;
+  if (g_thin_rounds > 0 && res > 0) {
+    const long cap = g_thin_rounds * (long)res / ks;
+    if (gx > cap) gx = cap < 1 ? 1 : cap;
+  }
   snprintf(g_last_kernel, sizeof g_last_kernel, "vm::conv3x3_thin<%d>", th);
-  const dim3 grid(tiles, a.ksplit > 1 ? a.ksplit : 1);
+  const dim3 grid((unsigned)gx, ks);
   if (th == 16) hipLaunchKernelGGL(conv3x3_thin<16>, grid, dim3(256), 0, st, a);
   else if (th == 4) hipLaunchKernelGGL(conv3x3_thin<4>, grid, dim3(256), 0, st, a);
   else hipLaunchKernelGGL(conv3x3_thin<8>, grid, dim3(256), 0, st, a);
@@ -3305,6 +3368,11 @@ extern "C" int vm_set_option(const char* key, long value) {
   }
   if (!strcmp(key, "rows_min_blocks")) {
     g_rows_min_blocks = value;
+    return VM_OK;
+  }
+  if (!strcmp(key, "thin_rounds")) {
+    if (value < 0 || value > 64) return fail(VM_EINVAL, "thin_rounds must be 0..64");
+    g_thin_rounds = value;
     return VM_OK;
   }
   if (!strcmp(key, "pack_frames")) {
