@@ -207,7 +207,7 @@ def test_conv_fused_maxpool_matches_separate(shape, kernel):
                                    (1, 40, 70, 64)])
 @pytest.mark.parametrize("pool", [False, True])
 @pytest.mark.parametrize("xdtype", ["bf16", "fp32"])
-@pytest.mark.parametrize("pair_kernel", [0, 1])
+@pytest.mark.parametrize("pair_kernel", [0, 1, 2])
 def test_conv_pair_first_bit_exact(shape, pool, xdtype, pair_kernel):
     """vm_conv3x3_pair_first_nhwc (conv1_1 evaluated into LDS, then conv1_2 [+ pool1]) equals the two separate
     kernels bit for bit: same bf16 rounding of the 64-channel intermediate, same accumulation order; an f32 frame is
@@ -224,17 +224,25 @@ def test_conv_pair_first_bit_exact(shape, pool, xdtype, pair_kernel):
     pc2 = ops.PackedConv(w2, (rs.normal(size=cout2) * 0.1).astype(np.float32), torch.bfloat16, DEV)
     cat = torch.full((n, h, w, 2 * cout2), 7.0, dtype=torch.bfloat16, device=DEV)
     pooled = torch.zeros((n, (h + 1) // 2, (w + 1) // 2, cout2), dtype=torch.bfloat16, device=DEV) if pool else None
-    _lib.set_option("pair_kernel", pair_kernel)
+    # pair_kernel 0: the strip-walking kernel (default), 2: the tile-persistent kernel (pair_strip 0), 1: the FIRST
+    # patch kernel
+    _lib.set_option("pair_kernel", 1 if pair_kernel == 1 else 0)
+    _lib.set_option("pair_strip", 1 if pair_kernel == 0 else 0)
     try:
         ops.conv_pair_first(x8[..., :7] if xdtype == "bf16" else xf, pc1, pc2, "relu", out=cat[..., cout2:],
                             pool_out=pooled)
         name = _lib.last_conv_kernel()
     finally:
         _lib.set_option("pair_kernel", 0)
-    persist = pair_kernel == 0 and cout2 == 64
+        _lib.set_option("pair_strip", 1)
     # conv3x3_patch<BN, WM, WN, S, TH, MINB, UNR, PF, ABL, FIRST, G>: the fused pair has FIRST = true
     first = name.split("<", 1)[-1].rstrip(">").split(",")[9].strip() if "<" in name else ""
-    assert name == "vm::conv3x3_pair_persist" if persist else first == "true", name
+    # (the strip kernel fetches >= 2 KB row windows: smaller frames run the tile kernel)
+    strip = pair_kernel == 0 and h * w * (28 if xdtype == "fp32" else 16) >= 2048
+    if cout2 != 64 or pair_kernel == 1:
+        assert first == "true", name
+    else:
+        assert name == ("vm::conv3x3_pair_strip" if strip else "vm::conv3x3_pair_persist"), name
     m = ops.conv3x3(x8[..., :7], pc1, "relu")
     y = ops.conv3x3(m, pc2, "relu")
     assert torch.equal(cat[..., cout2:], y)
@@ -534,6 +542,50 @@ def test_unet_bf16_close_to_reference(vgg0):
     lerr = relerr(H(m.conv1_3), g["logits"])
     print("bf16 UNetVideo 70x90 unit: alpha max-abs err %.3e, logits rel err %.3e" % (err, lerr))
     assert err < 2e-2 and lerr < 5e-2
+
+
+@pytest.mark.parametrize("shape", [(1, 1080, 1920), (3, 67, 101), (1, 541, 97), (2, 3, 45), (2, 8, 17), (5, 64, 64)])
+@pytest.mark.parametrize("xdtype", ["fp32", "bf16"])
+def test_pair_strip_matches_tile_kernel(shape, xdtype):
+    """The strip-walking pair kernel (conv_pair.hip: row ring of conv1_1 in LDS, filters in registers, segments of
+    rows, register epilogue with the DPP pool) against the tile-persistent kernel: conv1_2 output, pool1 and the head
+    split's per-tap partials bit for bit, at 1080p (17 segments of 64 rows), odd sizes (partial last strip, odd
+    height: the last pooled row from one row), small frames (one segment shorter than the halo; row windows clamped
+    at both image ends) and batches."""
+    from vmatting import _lib, ops
+    n, h, w = shape
+    rs = np.random.RandomState(h + 7 * w + n)
+    xf = torch.from_numpy((rs.normal(size=(n, h, w, 7)) * 50).astype(np.float32)).to(DEV)
+    x8 = torch.zeros((n, h, w, 8), dtype=torch.bfloat16, device=DEV)
+    ops.convert(xf, x8)
+    x = xf if xdtype == "fp32" else x8[..., :7]
+    w1 = (rs.normal(size=(3, 3, 7, 64)) * np.sqrt(2.0 / 63)).astype(np.float32)
+    w2 = (rs.normal(size=(3, 3, 64, 64)) * np.sqrt(2.0 / 576)).astype(np.float32)
+    whd = T((rs.normal(size=(3, 3, 128, 1)) * np.sqrt(2.0 / 1152)).astype(np.float32))
+    pc1 = ops.PackedConv(w1, (rs.normal(size=64) * 0.1).astype(np.float32), torch.bfloat16, DEV)
+    pc2 = ops.PackedConv(w2, (rs.normal(size=64) * 0.1).astype(np.float32), torch.bfloat16, DEV)
+    outs = []
+    for strip in (1, 0):
+        _lib.set_option("pair_strip", strip)
+        try:
+            y = torch.full((n, h, w, 64), 7.0, dtype=torch.bfloat16, device=DEV)
+            p = torch.full((n, (h + 1) // 2, (w + 1) // 2, 64), 7.0, dtype=torch.bfloat16, device=DEV)
+            part = torch.full((n, h, w, 12), 3.0, dtype=torch.float32, device=DEV)
+            ops.conv_pair_first_head(x, pc1, pc2, whd, 64, part, "relu", out=y, pool_out=p, store_y=True)
+            name = _lib.last_conv_kernel()
+            y2 = torch.full((n, h, w, 64), 7.0, dtype=torch.bfloat16, device=DEV)
+            p2 = torch.full_like(p, 7.0)
+            ops.conv_pair_first(x, pc1, pc2, "relu", out=y2, pool_out=p2)
+        finally:
+            _lib.set_option("pair_strip", 1)
+        assert name == ("vm::conv3x3_pair_strip" if strip else "vm::conv3x3_pair_persist"), name
+        assert torch.equal(y, y2) and torch.equal(p, p2)
+        outs.append((y, p, part))
+    (ys, ps, qs), (yt, pt, qt) = outs
+    assert torch.equal(ys, yt)
+    assert torch.equal(ps, pt)
+    assert torch.equal(qs[..., :9], qt[..., :9])
+    assert float(qs[..., 9:].abs().max()) == 0.0
 
 
 @pytest.mark.parametrize("shape", [(1, 16, 64), (2, 17, 45), (1, 1, 1), (1, 135, 240), (1, 40, 70)])

@@ -630,6 +630,16 @@ struct PatchCfg {
   static constexpr int LDS = MAIN > EPI ? MAIN : EPI;
   static constexpr int IW = TW + 4, IPIX = (TH + 4) * IW;   // FIRST: 8-channel input patch (16 B per pixel)
   static constexpr int LDS_FIRST = MAIN + IPIX * 16 > EPI ? MAIN + IPIX * 16 : EPI;
+  // register epilogue (vm_set_option "patch_repi"): a wave's pixel fragments must cover 2 whole rows so the fused
+  // 2x2 pool pairs rows inside the wave; 32-pixel waves of 8 x 32 / 4 x 32 tiles (TH == WM) are remapped to 2 rows x
+  // 16 pixels (wave pair 2k, 2k+1 = rows 2k, 2k+1), 64-pixel waves already hold 2 rows x 32 pixels.  Either way every
+  // output pixel keeps its MFMA sequence, so results do not depend on the mapping.
+  static constexpr bool REMAP = TPM == 32 && TW == 32 && WM % 2 == 0 && TH == WM;
+  static constexpr bool REPI_OK = G == 3 && (REMAP || TPM == 64);
+  static constexpr int PSTEP = REMAP ? 1 : 2;  // pixel fragment of the row below fragment fp (pool partner)
+  __device__ static int prow(int wm, int fp) { return REMAP ? 2 * (wm >> 1) + fp : (wm * TPM + fp * 16) / TW; }
+  __device__ static int pcol(int wm, int fp) { return REMAP ? 16 * (wm & 1) : (wm * TPM + fp * 16) % TW; }
+  __device__ static int tpix(int wm, int fp) { return prow(wm, fp) * TW + pcol(wm, fp); }  // first tile pixel
   static_assert(TPN % 64 == 0, "whole 64-channel epilogue slabs per wave column");
   static_assert(TPM % 32 == 0 || TPM == 16, "pixel fragments stay inside one patch row");
   static_assert(G == 1 || G == 3, "a slot holds one tap or one kernel row");
@@ -719,7 +729,7 @@ __device__ __forceinline__ void first_layer_patch(const ConvArgs& a, char* smem,
 template <int BN, int WM, int WN, int S, int TH, int MINB, int UNR, bool PF, int ABL, bool FIRST, int G = 1,
           bool UPSKIP = false>
 __global__ __launch_bounds__(64 * WM * WN)
-__attribute__((amdgpu_waves_per_eu(UPSKIP && MINB * WM * WN < 16 ? 4 : MINB * WM * WN / 4)))  // UPSKIP: <= 128 VGPRs
+__attribute__((amdgpu_waves_per_eu((UPSKIP || G > 1) && MINB * WM * WN < 16 ? 4 : MINB * WM * WN / 4)))  // <= 128 VGPRs
 void conv3x3_patch(ConvArgs a) {
   using C = PatchCfg<BN, WM, WN, S, TH, G>;
   using T = uint16_t;
@@ -822,8 +832,7 @@ void conv3x3_patch(ConvArgs a) {
   for (int f = 0; f < FC; ++f) boff[f] = 2 * C::PB + swz<64>(wn * C::TPN + f * 16 + (lane & 15), lane >> 4);
 #pragma unroll
   for (int f = 0; f < FP; ++f) {
-    const int p = wm * C::TPM + f * 16;
-    abase[f] = (p / C::TW) * C::PW + (p % C::TW) + (lane & 15);
+    abase[f] = C::prow(wm, f) * C::PW + C::pcol(wm, f) + (lane & 15);
   }
   const int ck = lane >> 4;
 
@@ -1036,7 +1045,7 @@ void conv3x3_patch(ConvArgs a) {
           }
 #pragma unroll
           for (int fp = 0; fp < FP; ++fp) {
-            const int row = wm * C::TPM + fp * 16 + (lane & 15);
+            const int row = C::tpix(wm, fp) + (lane & 15);
             float v[4];
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
@@ -1072,6 +1081,91 @@ void conv3x3_patch(ConvArgs a) {
     }
     return;
   }
+  if constexpr (C::REPI_OK) {
+    if (a.repi && !a.vstride) {
+      // register epilogue: bias / affine / act in registers, chunk_pair turns each pair of 16-channel fragments' lane
+      // quads into whole 16-byte chunks stored straight from the lane (no staging, no block barrier); the fused pool
+      // takes the row below from the wave's partner fragment and the column partner through DPP quad_perm [1,0,3,2]
+      const int col = lane & 15, ckq = lane >> 4;
+      const int c16 = (ckq & 1) ? 2 + (ckq >> 1) : ckq >> 1;
+      const int PH = (H + 1) >> 1, PWo = (W + 1) >> 1;
+      T* pb = a.py ? reinterpret_cast<T*>(a.py) + a.py_coff +
+                         (((long)n * PH + (r0 >> 1)) * PWo + (c0 >> 1)) * (long)a.py_cstride + n0
+                   : nullptr;
+      const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(pb, 0, 0x7ffffff0, 0x00020000);
+#pragma unroll
+      for (int g2 = 0; g2 < FC / 2; ++g2) {
+        const int chb = n0 + wn * C::TPN + g2 * 32;  // first block channel of this 32-channel group
+        const int phase = a.up ? chb / a.up_cout : 0;
+        const int cb = chb - phase * a.up_cout;
+        const int ccap = a.up ? a.up_cout : a.cout;
+        float mul[2][4], add[2][4];
+#pragma unroll
+        for (int f = 0; f < 2; ++f)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int co = min(cb + f * 16 + 4 * ckq + j, ccap - 1);
+            const float sc = a.scale ? a.scale[co] : 1.f;
+            mul[f][j] = sc;
+            add[f][j] = (a.bias ? a.bias[co] : 0.f) * sc + (a.shift ? a.shift[co] : 0.f);
+          }
+        float v[FP][2][4];
+#pragma unroll
+        for (int fp = 0; fp < FP; ++fp) {
+          uint2 pk[2];
+#pragma unroll
+          for (int f = 0; f < 2; ++f) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              float t = fmaf(acc[2 * g2 + f][fp][j], mul[f][j], add[f][j]);
+              if (a.act == VM_ACT_RELU) t = fmaxf(t, 0.f);
+              else if (a.act == VM_ACT_SIGMOID) t = sigmoid_precise(t);
+              v[fp][f][j] = t;
+            }
+            pk[f].x = (uint32_t)f2bf(v[fp][f][0]) | ((uint32_t)f2bf(v[fp][f][1]) << 16);
+            pk[f].y = (uint32_t)f2bf(v[fp][f][2]) | ((uint32_t)f2bf(v[fp][f][3]) << 16);
+          }
+          const uint4 d = chunk_pair(pk[0], pk[1]);
+          const int tr = C::prow(wm, fp), tc = C::pcol(wm, fp) + col;
+          const bool ok = r0 + tr < H && c0 + tc < W && cb + c16 * 8 < ccap;
+          const int pix = a.up ? (2 * tr + (phase >> 1)) * YW + 2 * tc + (phase & 1) : tr * W + tc;
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, d),
+                                                 yrs, ok ? pix * ycs2 + (cb + c16 * 8) * 2 : OOB, 0, 0);
+        }
+        if (a.py) {  // tiles start on even rows/columns: every 2x2 window lies inside the tile (host: no a.up)
+#pragma unroll
+          for (int fp = 0; fp < FP; ++fp) {
+            if (C::prow(wm, fp) & 1) continue;  // (compile-time per fp: the top row of each window)
+            const int tr = C::prow(wm, fp), tc = C::pcol(wm, fp) + col;
+            const bool v0 = r0 + tr < H && c0 + tc < W, v1 = r0 + tr + 1 < H && c0 + tc < W;
+            float m[2][4];
+#pragma unroll
+            for (int f = 0; f < 2; ++f)
+#pragma unroll
+              for (int j = 0; j < 4; ++j) {
+                float t = v0 ? v[fp][f][j] : -INFINITY;
+                if (v1) t = fmaxf(t, v[fp + C::PSTEP][f][j]);
+                const float u = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(t), 0xB1, 0xF, 0xF, false));
+                m[f][j] = fmaxf(t, u);
+              }
+            uint2 q2[2];
+#pragma unroll
+            for (int f = 0; f < 2; ++f) {
+              q2[f].x = (uint32_t)f2bf(m[f][0]) | ((uint32_t)f2bf(m[f][1]) << 16);
+              q2[f].y = (uint32_t)f2bf(m[f][2]) | ((uint32_t)f2bf(m[f][3]) << 16);
+            }
+            const uint4 d = chunk_pair(q2[0], q2[1]);
+            const int pr = tr >> 1, pc = tc >> 1;
+            const int chl = wn * C::TPN + g2 * 32 + c16 * 8;  // channel relative to n0
+            const bool pok = (col & 1) == 0 && v0 && (r0 >> 1) + pr < PH && (c0 >> 1) + pc < PWo && n0 + chl < a.cout;
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, d),
+                                                   prs, pok ? ((pr * PWo + pc) * a.py_cstride + chl) * 2 : OOB, 0, 0);
+          }
+        }
+      }
+      return;
+    }
+  }
   for (int sl = 0; sl < BN / 64; ++sl) {
     const int phase = a.up ? (n0 + sl * 64) / a.up_cout : 0;
     const int cb = n0 + sl * 64 - phase * a.up_cout;  // first (per-phase) output channel of the slab
@@ -1092,7 +1186,7 @@ void conv3x3_patch(ConvArgs a) {
         }
 #pragma unroll
         for (int fp = 0; fp < FP; ++fp) {
-          const int row = wm * C::TPM + fp * 16 + (lane & 15);
+          const int row = C::tpix(wm, fp) + (lane & 15);
           float v[4];
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
@@ -1183,7 +1277,7 @@ void conv3x3_patch(ConvArgs a) {
 // input pixels are loaded into registers while the current tile's MFMAs run.
 // The pair kernel's own patch images use a 2-bit chunk swizzle: like swz<64>, conflict-free for the ds_read_b128
 // fragment reads from any start row, and also for ds_write_b128 of 8 consecutive rows (swz<64> is 2-way there)
-__device__ __forceinline__ int swz2(int row, int chunk) { return row * 64 + ((chunk ^ ((row >> 1) & 3)) << 4); }
+// (swz2: conv_common.h)
 
 struct PairCfg {
   static constexpr int TH = 8, TW = 32, BM = TH * TW, PW = TW + 2, PPIX = (TH + 2) * PW;
@@ -2918,6 +3012,7 @@ static int launch_glds(ConvArgs& a, hipStream_t st) {
   return check_launch("conv3x3_glds");
 }
 
+static long g_patch_repi = 0;  // patch kernel: register epilogue (bf16 outputs, no packed frames) where the tiling allows
 template <int BN, int WM, int WN, int S, int TH = 8, int MINB = 1, int UNR = 9, bool PF = false, int ABL = 0,
           bool FIRST = false, int G = 1, bool UPSKIP = false>
 static int launch_patch(ConvArgs& a, hipStream_t st) {
@@ -2936,6 +3031,7 @@ static int launch_patch(ConvArgs& a, hipStream_t st) {
   const long sp = a.vstride ? ((a.H + C::TH - 1) / C::TH) * (long)((a.vW + C::TW - 1) / C::TW)
                             : N * ((a.H + C::TH - 1) / C::TH) * ((a.W + C::TW - 1) / C::TW);
   a.tiles_n = (a.cout + BN - 1) / BN;
+  a.repi = (int)g_patch_repi;
   if (sp * a.tiles_n > 0x7fffffffL) return fail(VM_EUNSUPPORTED, "conv3x3: too many tiles");
   a.tiles_total = (int)(sp * a.tiles_n);
   snprintf(g_last_kernel, sizeof g_last_kernel, "vm::conv3x3_patch<%d, %d, %d, %d, %d, %d, %d, %s, %d, %s, %d, %s>", BN,
@@ -3053,6 +3149,7 @@ static long g_rows_up = 0;            // 1: the folded upconvs too
 static long g_rows_min_cin = 256;      // short K loops: the 2-blocks-per-CU patch kernel hides prologue/epilogue better
 static long g_src_span_limit = 0x7ffffff0L;  // split-source byte span the 32-bit offset kernels take (option
                                               // "src_span_limit" lowers it for the fallback tests)
+static long g_pair_strip = 1;  // vm_conv3x3_pair_first*: 1 = the strip-walking kernel (conv_pair.hip) where it applies
 static long g_pair_kernel = 0;  // vm_conv3x3_pair_first_nhwc: 0 = persistent weights-resident kernel when cout == 64,
                                 // 1 = streaming patch kernel
 
@@ -3434,6 +3531,22 @@ extern "C" int vm_set_option(const char* key, long value) {
     g_pair_xin_wide = value;
     return VM_OK;
   }
+#ifdef VM_STUDY
+  if (!strcmp(key, "pair_strip_abl")) {  // timing-only ablations of the strip pair kernel (garbage results)
+    vm::g_pair_strip_abl = value;
+    return VM_OK;
+  }
+#endif
+  if (!strcmp(key, "patch_repi")) {
+    if (value < 0 || value > 1) return fail(VM_EINVAL, "patch_repi must be 0 or 1");
+    g_patch_repi = value;
+    return VM_OK;
+  }
+  if (!strcmp(key, "pair_strip")) {
+    if (value < 0 || value > 1) return fail(VM_EINVAL, "pair_strip must be 0 or 1");
+    g_pair_strip = value;
+    return VM_OK;
+  }
   if (!strcmp(key, "pair_kernel")) {
 #ifdef VM_STUDY
     if (value < 0 || (value > 1 && value < 10) || value > 18) return fail(VM_EINVAL, "pair_kernel must be 0, 1 or 10..18");
@@ -3680,6 +3793,13 @@ static int pair_first_impl(const vm_tensor* x, const void* packed1, int cin1, co
   a.w1 = packed1; a.bias1 = bias1; a.x_f32 = xf32; a.x_c = cin1;
   if (ypool) { a.py = ypool->ptr; a.py_cstride = ypool->cstride; a.py_coff = ypool->coff; }
   const long sp = (long)x->n * ((x->h + 7) / 8) * ((x->w + 31) / 32);
+  if (partial) {
+    a.hd = partial; a.hw = head_w; a.hw_cin = head_cin; a.hw_coff = head_coff; a.y_skip = store_y ? 0 : 1;
+  }
+  // the strip kernel addresses one image's output / pool with 32-bit byte offsets
+  const bool strip_fits = (long)x->h * x->w * y->cstride * 2 < 0x7ffffff0L &&
+                          (!ypool || (long)ypool->h * ypool->w * ypool->cstride * 2 < 0x7ffffff0L);
+  if (g_pair_strip && g_pair_kernel == 0 && strip_fits && pair_strip_ok(a)) return launch_pair_strip(a, x->n, st);
   if (partial) {  // the head split lives in the persistent pair kernel only
     if (cout2 != 64 || g_pair_kernel != 0 || sp > 0x7fffffffL)
       return fail(VM_EUNSUPPORTED, "conv3x3_pair_first_head: needs the persistent pair kernel (cout2 64)");

@@ -45,6 +45,7 @@ struct ConvArgs {
   // outside it (zero input: the SAME padding of both neighbours; their outputs are never stored).  Narrow frames
   // (40 or 20 px in 32-px tiles) stop wasting most of their last column tile.
   int vstride, vW;
+  int repi;  // patch kernel: 1 = register epilogue where the tiling allows (bf16 output, no split-K, no packed frames)
 };
 
 // element offset of input channel c (relative to the view's channel 0) under the source split
@@ -61,6 +62,10 @@ __device__ __forceinline__ int swz(int row, int chunk) {
   if constexpr (RB == 128) return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4);
   else return row * 64 + ((chunk ^ (((row >> 2) & 1) << 1)) << 4);
 }
+
+// 2-bit chunk swizzle of 64-byte rows (the pair kernels' own patch images): like swz<64>, conflict-free for the
+// ds_read_b128 fragment reads from any start row, and also for ds_write_b128 of 8 consecutive rows
+__device__ __forceinline__ int swz2(int row, int chunk) { return row * 64 + ((chunk ^ ((row >> 1) & 3)) << 4); }
 
 template <typename T>
 __device__ __forceinline__ void mma16(const uint4& a, const uint4& b, f32x4& c);
@@ -156,5 +161,9 @@ extern thread_local char g_last_kernel[128];
 // launchers defined in conv_rows.hip (called from conv3x3.hip's dispatch)
 bool rows_ok(const ConvArgs& a);
 int launch_rows(ConvArgs& a, hipStream_t st, int cfg);
+// launchers defined in conv_pair.hip
+bool pair_strip_ok(const ConvArgs& a);
+int launch_pair_strip(ConvArgs& a, long nimg, hipStream_t st);
+extern long g_pair_strip_abl;
 
 }  // namespace vm
