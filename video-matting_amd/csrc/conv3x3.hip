@@ -3012,7 +3012,7 @@ static int launch_glds(ConvArgs& a, hipStream_t st) {
   return check_launch("conv3x3_glds");
 }
 
-static long g_patch_repi = 0;  // patch kernel: register epilogue (bf16 outputs, no packed frames) where the tiling allows
+static long g_patch_repi = 1;  // patch kernel: register epilogue (bf16 outputs, no packed frames) where the tiling allows
 template <int BN, int WM, int WN, int S, int TH = 8, int MINB = 1, int UNR = 9, bool PF = false, int ABL = 0,
           bool FIRST = false, int G = 1, bool UPSKIP = false>
 static int launch_patch(ConvArgs& a, hipStream_t st) {
