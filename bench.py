@@ -690,6 +690,8 @@ def main():
     ap.add_argument("--no-profile", action="store_true", help="skip per-conv HIP events")
     ap.add_argument("--layers", action="store_true", help="per-conv timing breakdown on stderr")
     ap.add_argument("--no-graph", action="store_true", help="time eager launches instead of the captured HIP graph")
+    ap.add_argument("--no-up-head", action="store_true",
+                    help="upconv_4 stores its output and the head reads it (A/B of the fused up-head)")
     ap.add_argument("--no-split-head", action="store_true",
                     help="conv1_5 over the whole cat1 instead of the pair kernel's head split (A/B)")
     ap.add_argument("--no-loader", action="store_true", help="skip the training-sample loader record (rank 0, N=1)")
@@ -745,6 +747,7 @@ def main():
     np.random.seed(0)
     model = unet.UNetVideo(vgg, dtype=args.dtype, device=dev)
     model.split_head = not args.no_split_head
+    model.fuse_up_head = not args.no_up_head
     model.prepare()
     parallel.broadcast_tensors(model.weights_flat(), src=0)
 

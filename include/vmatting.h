@@ -187,6 +187,24 @@ int vm_conv3x3_up2x_nhwc(const vm_tensor* x, const void* packed_up, const void* 
                          const float* bias, const float* scale, const float* shift, int act, vm_tensor* y,
                          void* stream);
 
+/* The folded upconv with the head split (unet.py:200-205: upconv_4 -> cat1 -> conv1_5): besides y (store_y = 0
+ * leaves it unwritten) the conv writes partial[pixel][12] of its [n,2h,2w] output (f32): taps 0..8 of
+ * sum_c y[pixel][c] * head_w[tap][head_coff + c] over the conv's bf16 outputs (head_w = conv1_5's HWIO f32 filter
+ * [3,3,head_cin,1], bf16-rounded like a packed head; taps 9..11 zero), the frame border included (from the border
+ * pass's values).  cout == 64; VM_EUNSUPPORTED when a kernel-selection option rules out the patch kernel's register
+ * epilogue (the caller then stores y and runs vm_conv3x3_head_partial_nhwc). */
+int vm_conv3x3_up2x_head_nhwc(const vm_tensor* x, const void* packed_up, const void* packed, int cin, int cout,
+                              const float* bias, const float* scale, const float* shift, int act, vm_tensor* y,
+                              const float* head_w, int head_cin, int head_coff, float* partial, int store_y,
+                              void* stream);
+
+/* conv1_5 + sigmoid from two partial sets (unet.py:203-205 with both halves of cat1 taken where they were made,
+ * vm_conv3x3_up2x_head_nhwc and vm_conv3x3_pair_first_head_nhwc): logits[p] = bias[0] + sum_tap (pa[p + off(tap)][tap]
+ * + pb[p + off(tap)][tap]) (zero outside the frame), alpha[p] = sigmoid(logits[p]).  pa, pb: f32 [n*h*w][12];
+ * logits: f32 [n,h,w,1] view or NULL; alpha: contiguous f32 [n*h*w] or NULL. */
+int vm_conv3x3_head_from_partials(const float* pa, const float* pb, int n, int h, int w, const float* bias,
+                                  vm_tensor* logits, float* alpha, void* stream);
+
 /* tf.nn.max_pool(ksize 2, stride 2, 'SAME') — unet.py:32-33, unet_simple.py:95-96, small.py:40,42 */
 int vm_maxpool2x2_same_nhwc(const vm_tensor* x, vm_tensor* y, void* stream);
 

@@ -638,6 +638,55 @@ def test_conv_pair_first_head_partials(shape, store_y):
     assert float((a_split - a_full).abs().max()) < 1e-5
 
 
+@pytest.mark.parametrize("shape", [(1, 17, 23), (2, 8, 16), (1, 68, 120), (1, 540, 960)])
+@pytest.mark.parametrize("store_y", [False, True])
+def test_up2x_head_partials(shape, store_y):
+    """vm_conv3x3_up2x_head_nhwc (upconv_4 with conv1_5's shares of its own half of cat1 taken in the epilogue,
+    unet.py:200-205): y bit-identical to vm_conv3x3_up2x_nhwc (untouched when not stored); the partials
+    partial[p][t] = sum_c y[p][c] * bf16(w)[t][c] of the conv's own bf16 outputs, frame border included (the border
+    pass), within f32 summation order of an f64 restatement; taps 9..11 zero.  Then vm_conv3x3_head_from_partials
+    with the skip half's partials equals the full 128-channel head within f32 summation order."""
+    from vmatting import ops
+    n, h, w = shape
+    rs = np.random.RandomState(h * w + n)
+    x = torch.from_numpy(rs.uniform(0, 2, (n, h, w, 128)).astype(np.float32)).to(DEV).to(torch.bfloat16)
+    pc = ops.PackedConv((rs.normal(size=(3, 3, 128, 64)) * np.sqrt(2.0 / 1152)).astype(np.float32), None,
+                        torch.bfloat16, DEV)
+    wh = (rs.normal(size=(3, 3, 128, 1)) * np.sqrt(2.0 / 1152)).astype(np.float32)
+    whd = T(wh)
+    cat = torch.zeros((n, 2 * h, 2 * w, 128), dtype=torch.bfloat16, device=DEV)
+    ops.upconv3x3(x, pc, "none", out=cat[..., :64])
+    cat[..., 64:] = torch.from_numpy(rs.uniform(0, 2, (n, 2 * h, 2 * w, 64)).astype(np.float32)).to(DEV).to(
+        torch.bfloat16)
+    y = torch.full((n, 2 * h, 2 * w, 64), 7.0, dtype=torch.bfloat16, device=DEV)
+    part = torch.full((n, 2 * h, 2 * w, 12), 3.0, dtype=torch.float32, device=DEV)
+    assert ops.upconv3x3_head(x, pc, whd, 0, part, "none", out=y, store_y=store_y) is not None
+    if store_y:
+        assert torch.equal(y, cat[..., :64])
+    else:
+        assert float((y.float() - 7.0).abs().max()) == 0.0
+    yv = H(cat[..., :64].float()).astype(np.float64)
+    wb = H(whd.to(torch.bfloat16).float()).astype(np.float64).reshape(9, 128)[:, :64]
+    want = np.einsum("nhwc,tc->nhwt", yv, wb)
+    got = H(part)
+    assert np.abs(got[..., 9:]).max() == 0.0
+    assert relerr(got[..., :9], want) < 1e-5, relerr(got[..., :9], want)
+    # the head from the two halves' partials vs the full head over cat1
+    bh = np.array([0.25], np.float32)
+    full = ops.PackedConv(wh, bh, torch.bfloat16, DEV)
+    a_full = torch.empty((n * 4 * h * w,), dtype=torch.float32, device=DEV)
+    l_full = ops.conv_head(cat, full, "none", alpha=a_full)
+    # the skip half's partials in the pair kernel's layout (f64 restatement, rounded to f32)
+    yk = H(cat[..., 64:].float()).astype(np.float64)
+    wk = H(whd.to(torch.bfloat16).float()).astype(np.float64).reshape(9, 128)[:, 64:]
+    pb = np.zeros((n, 2 * h, 2 * w, 12), np.float32)
+    pb[..., :9] = np.einsum("nhwc,tc->nhwt", yk, wk).astype(np.float32)
+    a_sp = torch.empty_like(a_full)
+    l_sp = ops.head_from_partials(part, T(pb), T(bh), alpha=a_sp)
+    assert relerr(H(l_sp), H(l_full)) < 1e-5, relerr(H(l_sp), H(l_full))
+    assert float((a_sp - a_full).abs().max()) < 1e-5
+
+
 def test_unet_bf16_fused_and_unfused_forward_agree(vgg0):
     """bf16 forward: fusing conv1_1->conv1_2 changes nothing (bit for bit, the lazily evaluated .conv1_1 included);
     folding the upconv resizes stays in the bf16 error class of the resize + conv path (logits; alpha of saturated

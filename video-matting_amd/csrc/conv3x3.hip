@@ -1093,22 +1093,54 @@ void conv3x3_patch(ConvArgs a) {
                          (((long)n * PH + (r0 >> 1)) * PWo + (c0 >> 1)) * (long)a.py_cstride + n0
                    : nullptr;
       const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(pb, 0, 0x7ffffff0, 0x00020000);
+      // head split (a.hd, vm_conv3x3_up2x_head_nhwc): the wave holds all 64 channels of its pixels (one phase of the
+      // folded upconv), so conv1_5's per-tap shares of them are 2 MFMAs on the bf16 outputs, as in the pair kernels:
+      // A rows = the 9 taps, k ordered like the lane's output channels (2kk + j/4)*16 + 4q + j%4
+      constexpr bool HEADOK = FC == 4 && BN == 64;
+      // every global load of the epilogue (per-channel constants of all FC fragments, the head filter) is issued
+      // here, before any is used, so the block waits for one round trip instead of one per channel group
+      const int ccap = a.up ? a.up_cout : a.cout;
+      float mul[FC][4], add[FC][4];
+#pragma unroll
+      for (int f = 0; f < FC; ++f) {
+        const int chb = n0 + wn * C::TPN + (f & ~1) * 16;
+        const int cb = chb - (a.up ? chb / a.up_cout : 0) * a.up_cout;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int co = min(cb + (f & 1) * 16 + 4 * ckq + j, ccap - 1);
+          const float sc = a.scale ? a.scale[co] : 1.f;
+          mul[f][j] = sc;
+          add[f][j] = (a.bias ? a.bias[co] : 0.f) * sc + (a.shift ? a.shift[co] : 0.f);  // (as the staged epilogue)
+        }
+      }
+      float hwv[2][8];
+      if (HEADOK && a.hd) {
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const int hc = (2 * kk + j / 4) * 16 + 4 * ckq + j % 4;
+            hwv[kk][j] = col < 9 ? a.hw[col * a.hw_cin + a.hw_coff + hc] : 0.f;
+          }
+      }
+      uint4 hwf[2] = {make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};
+      f32x4 dacc[FP];
+#pragma unroll
+      for (int fp = 0; fp < FP; ++fp) dacc[fp] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (HEADOK && a.hd) {
+        // A fragments of the head filter: rows = taps (9 of 16), k = 8q + j <-> channel (2kk + j/4)*16 + 4q + j%4
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+          hwf[kk] = make_uint4((uint32_t)f2bf(hwv[kk][0]) | ((uint32_t)f2bf(hwv[kk][1]) << 16),
+                               (uint32_t)f2bf(hwv[kk][2]) | ((uint32_t)f2bf(hwv[kk][3]) << 16),
+                               (uint32_t)f2bf(hwv[kk][4]) | ((uint32_t)f2bf(hwv[kk][5]) << 16),
+                               (uint32_t)f2bf(hwv[kk][6]) | ((uint32_t)f2bf(hwv[kk][7]) << 16));
+      }
 #pragma unroll
       for (int g2 = 0; g2 < FC / 2; ++g2) {
         const int chb = n0 + wn * C::TPN + g2 * 32;  // first block channel of this 32-channel group
         const int phase = a.up ? chb / a.up_cout : 0;
         const int cb = chb - phase * a.up_cout;
-        const int ccap = a.up ? a.up_cout : a.cout;
-        float mul[2][4], add[2][4];
-#pragma unroll
-        for (int f = 0; f < 2; ++f)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int co = min(cb + f * 16 + 4 * ckq + j, ccap - 1);
-            const float sc = a.scale ? a.scale[co] : 1.f;
-            mul[f][j] = sc;
-            add[f][j] = (a.bias ? a.bias[co] : 0.f) * sc + (a.shift ? a.shift[co] : 0.f);
-          }
         float v[FP][2][4];
 #pragma unroll
         for (int fp = 0; fp < FP; ++fp) {
@@ -1117,7 +1149,7 @@ void conv3x3_patch(ConvArgs a) {
           for (int f = 0; f < 2; ++f) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-              float t = fmaf(acc[2 * g2 + f][fp][j], mul[f][j], add[f][j]);
+              float t = fmaf(acc[2 * g2 + f][fp][j], mul[2 * g2 + f][j], add[2 * g2 + f][j]);
               if (a.act == VM_ACT_RELU) t = fmaxf(t, 0.f);
               else if (a.act == VM_ACT_SIGMOID) t = sigmoid_precise(t);
               v[fp][f][j] = t;
@@ -1125,12 +1157,18 @@ void conv3x3_patch(ConvArgs a) {
             pk[f].x = (uint32_t)f2bf(v[fp][f][0]) | ((uint32_t)f2bf(v[fp][f][1]) << 16);
             pk[f].y = (uint32_t)f2bf(v[fp][f][2]) | ((uint32_t)f2bf(v[fp][f][3]) << 16);
           }
+          if (HEADOK && a.hd) mma16<T>(hwf[g2], make_uint4(pk[0].x, pk[0].y, pk[1].x, pk[1].y), dacc[fp]);
           const uint4 d = chunk_pair(pk[0], pk[1]);
           const int tr = C::prow(wm, fp), tc = C::pcol(wm, fp) + col;
-          const bool ok = r0 + tr < H && c0 + tc < W && cb + c16 * 8 < ccap;
+          const bool ok = r0 + tr < H && c0 + tc < W && cb + c16 * 8 < ccap && !a.y_skip;
           const int pix = a.up ? (2 * tr + (phase >> 1)) * YW + 2 * tc + (phase & 1) : tr * W + tc;
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, d),
                                                  yrs, ok ? pix * ycs2 + (cb + c16 * 8) * 2 : OOB, 0, 0);
+          if (HEADOK && a.hd && g2 == FC / 2 - 1 && ckq < 3 && r0 + tr < H && c0 + tc < W) {
+            const int YH = a.up ? 2 * H : H;
+            const int yy = a.up ? 2 * (r0 + tr) + (phase >> 1) : r0 + tr, xx = a.up ? 2 * (c0 + tc) + (phase & 1) : c0 + tc;
+            *reinterpret_cast<f32x4*>(a.hd + (((long)n * YH + yy) * YW + xx) * 12 + 4 * ckq) = dacc[fp];
+          }
         }
         if (a.py) {  // tiles start on even rows/columns: every 2x2 window lies inside the tile (host: no a.up)
 #pragma unroll
@@ -2653,6 +2691,9 @@ struct BorderArgs {
   void* y;  // [N,2H,2W,cout] bf16 view
   int y_cstride, y_coff;
   int nb;  // border pixels per frame
+  float* hd;        // head split (cout == 64): per-tap head shares of the border pixels, as the conv's epilogue
+  const float* hw;  // conv1_5 HWIO f32 [3,3,hw_cin,1]
+  int hw_cin, hw_coff, y_skip;
 };
 
 // Border pixels of the folded upconv, computed the unfused way: the 9 resized taps (TF1 legacy bilinear in f32,
@@ -2756,9 +2797,10 @@ __global__ __launch_bounds__(256) void conv3x3_up2x_border(BorderArgs a) {
   __syncthreads();
   const int ep = tid >> 4, cq = (tid & 15) * 4;
   const long b = b0 + ep;
-  if (b >= total) return;
-  int n, ey, ex;
-  decode(b, n, ey, ex);
+  if (b >= total && !a.hd) return;
+  int n = 0, ey = 0, ex = 0;
+  const bool bok = b < total;
+  if (bok) decode(b, n, ey, ex);
   float v[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -2774,7 +2816,76 @@ __global__ __launch_bounds__(256) void conv3x3_up2x_border(BorderArgs a) {
   uint2 pk;
   pk.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
   pk.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-  *reinterpret_cast<uint2*>(yp) = pk;
+  if (!a.y_skip && bok) *reinterpret_cast<uint2*>(yp) = pk;
+  if (a.hd) {  // (uniform: a.hd is a kernel argument; every thread reaches the barriers below)
+    // the border pixel's 64 bf16 outputs -> 9 per-tap shares sum_c bf16(hw[tap][coff + c]) * y[c] (f32, in channel
+    // order); taps 9..11 zero like the MFMA epilogues'
+    float* vals = &red[0][0];     // [16 pixels][64] (the reduction rows were last read above)
+    float* hwl = vals + 16 * 64;  // the head filter's 9 x 64 taps of these channels, bf16-rounded
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 4; ++j) vals[ep * 64 + cq + j] = bf2f(f2bf(v[j]));
+    for (int i = tid; i < 9 * 64; i += 256) hwl[i] = bf2f(f2bf(a.hw[(i >> 6) * a.hw_cin + a.hw_coff + (i & 63)]));
+    __syncthreads();
+    if (tid < 16 * 12) {
+      const int pe = tid / 12, tap = tid - pe * 12;
+      const long bb = b0 + pe;
+      if (bb < total) {
+        int pn, py, px2;
+        decode(bb, pn, py, px2);
+        float acc = 0.f;
+        if (tap < 9)
+#pragma unroll 16
+          for (int c = 0; c < 64; ++c) acc = fmaf(hwl[tap * 64 + c], vals[pe * 64 + c], acc);
+        a.hd[(((long)pn * OH + py) * OW + px2) * 12 + tap] = acc;
+      }
+    }
+  }
+}
+
+// ================================================================ head from per-tap partials (unet.py:203-205)
+// conv1_5 over cat1 = [upconv_4, conv1_2] with both halves' shares taken where they were made (the folded upconv's
+// and the pair kernel's epilogues): logits[p] = bias + sum_tap (pa + pb)[p + off(tap)][tap] (zero outside the
+// frame), alpha = sigmoid(logits).  A block owns 8 x 64 output pixels: the (8+2) x 66 partial rows it needs are
+// contiguous runs of 66 x 48 bytes, staged with 16-byte loads (taps summed over the two halves on the way, taps
+// 9..11 dropped), and each thread then adds its pixels' 9 taps from LDS.
+constexpr int HS_TH = 8, HS_TW = 64, HS_PW = HS_TW + 2, HS_PR = HS_TH + 2;
+__global__ __launch_bounds__(256) void head_from_partials(const float* __restrict__ pa, const float* __restrict__ pb,
+                                                          int N, int H, int W, const float* __restrict__ bias,
+                                                          float* __restrict__ logits, int l_cstride,
+                                                          float* __restrict__ alpha) {
+  __shared__ float sp[HS_PR * HS_PW * 9];
+  const int tw = (W + HS_TW - 1) / HS_TW, th = (H + HS_TH - 1) / HS_TH;
+  const int b = blockIdx.x, n = b / (th * tw), rem = b - n * th * tw;
+  const int y0 = (rem / tw) * HS_TH, x0 = (rem % tw) * HS_TW;
+  const long img = (long)n * H * W;
+  // stage: item i = (row, pixel, float4 group g < 3)
+  for (int i = threadIdx.x; i < HS_PR * HS_PW * 3; i += 256) {
+    const int g = i % 3, px = (i / 3) % HS_PW, row = i / (3 * HS_PW);
+    const int yy = y0 - 1 + row, xx = x0 - 1 + px;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if ((unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W) {
+      const long q = (img + (long)yy * W + xx) * 12 + 4 * g;
+      const float4 u = *reinterpret_cast<const float4*>(pa + q), w = *reinterpret_cast<const float4*>(pb + q);
+      v = make_float4(u.x + w.x, u.y + w.y, u.z + w.z, u.w + w.w);
+    }
+    float* d = sp + (row * HS_PW + px) * 9 + 4 * g;
+    d[0] = v.x;
+    if (g < 2) { d[1] = v.y; d[2] = v.z; d[3] = v.w; }  // (group 2 holds tap 8 and the three zero taps)
+  }
+  __syncthreads();
+  const float b0 = bias ? bias[0] : 0.f;
+  for (int o = threadIdx.x; o < HS_TH * HS_TW; o += 256) {
+    const int ty = o / HS_TW, tx = o % HS_TW;
+    const int y = y0 + ty, x = x0 + tx;
+    if (y >= H || x >= W) continue;
+    float s = b0;
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) s += sp[((ty + tap / 3) * HS_PW + tx + tap % 3) * 9 + tap];
+    const long p = img + (long)y * W + x;
+    if (logits) logits[p * l_cstride] = s;
+    if (alpha) alpha[p] = sigmoid_precise(s);
+  }
 }
 
 // ================================================================ split-K reduction
@@ -3663,6 +3774,16 @@ extern "C" int vm_conv3x3_fold_up2x_weights(const float* w_hwio, int cin, int co
   return check_launch("fold_up2x_weights");
 }
 
+// head split of the folded upconv (vm_conv3x3_up2x_head_nhwc -> vm_conv3x3_up2x_nhwc): per-thread, set only for the
+// duration of that call
+struct UpHead {
+  const float* hw;
+  int hw_cin, hw_coff;
+  float* hd;
+  int y_skip;
+};
+static thread_local UpHead g_up_head = {};
+
 extern "C" int vm_conv3x3_up2x_nhwc(const vm_tensor* x, const void* packed_up, const void* packed, int cin, int cout,
                                     const float* bias, const float* scale, const float* shift, int act, vm_tensor* y,
                                     void* stream) {
@@ -3690,6 +3811,8 @@ extern "C" int vm_conv3x3_up2x_nhwc(const vm_tensor* x, const void* packed_up, c
   a.bias = bias; a.scale = scale; a.shift = shift; a.act = act;
   a.y = y->ptr; a.y_cstride = y->cstride; a.y_coff = y->coff; a.y_dtype = y->dtype; a.y_vec = 1;
   a.up = 1; a.up_cout = cout;
+  a.hd = g_up_head.hd; a.hw = g_up_head.hw; a.hw_cin = g_up_head.hw_cin; a.hw_coff = g_up_head.hw_coff;
+  a.y_skip = g_up_head.y_skip;
   if (!patch_ok(a, 2)) return fail(VM_EUNSUPPORTED, "conv3x3_up2x: shape not supported by the patch kernel");
   int rc = dispatch_patch(a, st);
   if (rc != VM_OK) return rc;
@@ -3698,12 +3821,46 @@ extern "C" int vm_conv3x3_up2x_nhwc(const vm_tensor* x, const void* packed_up, c
   b.w = packed; b.K_pad = g1.K_pad; b.cout = cout; b.nch = g1.cin_pad / 32;
   b.bias = bias; b.scale = scale; b.shift = shift; b.act = act;
   b.y = y->ptr; b.y_cstride = y->cstride; b.y_coff = y->coff;
+  b.hd = g_up_head.hd; b.hw = g_up_head.hw; b.hw_cin = g_up_head.hw_cin; b.hw_coff = g_up_head.hw_coff;
+  b.y_skip = g_up_head.y_skip;
   const int OH = 2 * x->h, OW = 2 * x->w;
   b.nb = 2 * OW + 2 * (OH - 2);
   const long nblk = ((long)x->n * b.nb + 15) / 16;
   if (nblk > 0x7fffffffL) return fail(VM_EUNSUPPORTED, "conv3x3_up2x: too many border pixels");
   hipLaunchKernelGGL(conv3x3_up2x_border, dim3((unsigned)nblk, cout / 64), dim3(256), 0, st, b);
   return check_launch("conv3x3_up2x_border");
+}
+
+extern "C" int vm_conv3x3_up2x_head_nhwc(const vm_tensor* x, const void* packed_up, const void* packed, int cin,
+                                         int cout, const float* bias, const float* scale, const float* shift, int act,
+                                         vm_tensor* y, const float* head_w, int head_cin, int head_coff, float* partial,
+                                         int store_y, void* stream) {
+  if (!head_w || !partial || cout != 64 || head_cin <= 0 || head_coff < 0 || head_coff + cout > head_cin)
+    return fail(VM_EINVAL, "conv3x3_up2x_head: head filter [3,3,%d,1] with the conv's %d channels at %d", head_cin, cout,
+                head_coff);
+  // the partials come from the patch kernel's register epilogue (64-channel row-slot tilings)
+  if (!g_patch_repi || g_patch_cfg || g_rows_up || !g_up_skip)
+    return fail(VM_EUNSUPPORTED, "conv3x3_up2x_head: needs the patch kernel's register epilogue");
+  g_up_head = {head_w, head_cin, head_coff, partial, store_y ? 0 : 1};
+  const int rc = vm_conv3x3_up2x_nhwc(x, packed_up, packed, cin, cout, bias, scale, shift, act, y, stream);
+  g_up_head = {};
+  return rc;
+}
+
+extern "C" int vm_conv3x3_head_from_partials(const float* pa, const float* pb, int n, int h, int w, const float* bias,
+                                             vm_tensor* logits, float* alpha, void* stream) {
+  if (!pa || !pb || n <= 0 || h <= 0 || w <= 0) return fail(VM_EINVAL, "head_from_partials: bad argument");
+  if (logits && (!valid_tensor(logits) || logits->dtype != VM_F32 || logits->n != n || logits->h != h ||
+                 logits->w != w || logits->c != 1))
+    return fail(VM_EINVAL, "head_from_partials: logits must be an f32 [n,h,w,1] view");
+  const long tiles = (long)n * ((h + HS_TH - 1) / HS_TH) * ((w + HS_TW - 1) / HS_TW);
+  if (tiles > 0x7fffffffL || (long)n * h * w * 12 > 0x7fffffffffffL) return fail(VM_EUNSUPPORTED, "head_from_partials");
+  float* lp = logits ? reinterpret_cast<float*>(logits->ptr) + logits->coff : nullptr;
+  hipLaunchKernelGGL(head_from_partials, dim3((unsigned)tiles), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), pa, pb, n, h, w, bias, lp, logits ? logits->cstride : 1,
+                     alpha);
+  snprintf(g_last_kernel, sizeof g_last_kernel, "vm::head_from_partials");
+  return check_launch("head_from_partials");
 }
 
 template <int PABL, int XIN = 2>

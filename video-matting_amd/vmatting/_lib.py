@@ -88,6 +88,10 @@ SIGNATURES = [
     ("vm_conv3x3_fold_up2x_weights", c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p]),
     ("vm_conv3x3_up2x_nhwc", c_int, [P, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, P,
                                      c_void_p]),
+    ("vm_conv3x3_up2x_head_nhwc", c_int, [P, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int,
+                                          P, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p]),
+    ("vm_conv3x3_head_from_partials", c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, P, c_void_p,
+                                              c_void_p]),
     ("vm_maxpool2x2_same_nhwc", c_int, [P, P, c_void_p]),
     ("vm_resize_bilinear_tf1_nhwc", c_int, [P, P, c_void_p]),
     ("vm_convert_nhwc", c_int, [P, P, c_void_p, c_void_p, c_int, c_void_p]),

@@ -396,6 +396,70 @@ def upconv3x3(x, pc, act="none", out=None, size=None, rbuf=None, fold=True):
     return conv3x3(r, pc, act, out=out)
 
 
+def upconv3x3_head(x, pc, head_w, head_coff, partial, act="none", out=None, store_y=False):
+    """upconv3x3 (exact 2x, folded) with the head split (vm_conv3x3_up2x_head_nhwc): besides ``out`` (written only
+    when store_y) the conv writes ``partial`` [n,2h,2w,12] f32 = per-tap shares of the cout == 1 head filter
+    ``head_w`` (device f32 HWIO [3,3,cin_head,1]) over its 64 output channels, which sit at head_coff of the head's
+    input (unet.py:200-205: conv1_5 over cat1 = [upconv_4, conv1_2]).  Returns None when the kernel cannot take the
+    case (the caller runs the unsplit path)."""
+    n, h, w, _ = x.shape
+    up = pc.up2x() if x.dtype == pc.dtype == torch.bfloat16 and pc.cout == 64 else None
+    if up is None:
+        return None
+    if head_w.dtype != torch.float32 or not head_w.is_contiguous() or head_w.dim() != 4 or head_w.shape[3] != 1:
+        raise ValueError("head_w must be a contiguous f32 [3,3,cin,1] filter")
+    if partial.dtype != torch.float32 or not partial.is_contiguous() or tuple(partial.shape) != (n, 2 * h, 2 * w, 12):
+        raise ValueError("partial must be a contiguous f32 [n,2h,2w,12] tensor")
+    _require_gpu(head_w)
+    _require_gpu(partial)
+    if out is None:
+        out = torch.empty((n, 2 * h, 2 * w, pc.cout), dtype=x.dtype, device=x.device)
+    xv, yv = nhwc(x), nhwc(out)
+    prof = _CONV_PROFILE
+    if prof is not None:
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev1 = torch.cuda.Event(enable_timing=True)
+        ev0.record()
+    rc = lib().vm_conv3x3_up2x_head_nhwc(
+        ctypes.byref(xv), _ptr(up), _ptr(pc.packed), pc.cin, pc.cout, _ptr(pc.bias), _ptr(pc.scale), _ptr(pc.shift),
+        _lib.ACT[act], ctypes.byref(yv), _ptr(head_w), int(head_w.shape[2]), head_coff, _ptr(partial),
+        int(bool(store_y)), stream_handle())
+    if rc == _lib.VM_EUNSUPPORTED:
+        return None
+    check(rc, "conv3x3_up2x_head")
+    if prof is not None:
+        ev1.record()
+        prof.append((2 * n * 4 * h * w * 9 * pc.cin * pc.cout, _lib.last_conv_kernel(), ev0, ev1))
+    return out
+
+
+def head_from_partials(pa, pb, bias=None, logits=None, alpha=None):
+    """conv1_5 + sigmoid from the two halves' per-tap partials (vm_conv3x3_head_from_partials): logits =
+    bias + sum_tap (pa + pb)[p + off(tap)][tap], alpha = sigmoid(logits).  pa, pb: contiguous f32 [n,h,w,12]."""
+    n, h, w, k = pa.shape
+    if k != 12 or tuple(pb.shape) != (n, h, w, 12) or pa.dtype != torch.float32 or pb.dtype != torch.float32 \
+            or not pa.is_contiguous() or not pb.is_contiguous():
+        raise ValueError("pa, pb must be contiguous f32 [n,h,w,12] partials")
+    _require_gpu(pa)
+    _require_gpu(pb)
+    if logits is None:
+        logits = torch.empty((n, h, w, 1), dtype=torch.float32, device=pa.device)
+    lv = nhwc(logits)
+    if alpha is not None and (alpha.dtype != torch.float32 or not alpha.is_contiguous() or alpha.numel() != n * h * w):
+        raise ValueError("alpha must be a contiguous f32 tensor of n*h*w values")
+    prof = _CONV_PROFILE
+    if prof is not None:
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev1 = torch.cuda.Event(enable_timing=True)
+        ev0.record()
+    check(lib().vm_conv3x3_head_from_partials(_ptr(pa), _ptr(pb), n, h, w, _ptr(bias), ctypes.byref(lv),
+                                              _ptr(alpha), stream_handle()), "head_from_partials")
+    if prof is not None:  # (the head's own conv FLOPs were made in the two epilogues; listed for its time)
+        ev1.record()
+        prof.append((2 * n * h * w * 9 * 128, _lib.last_conv_kernel(), ev0, ev1))
+    return logits
+
+
 # When a list, conv3x3 appends (algorithmic FLOPs, is_head, start_event, end_event) per launch —
 # HIP events on the launch stream, used by bench.py for the roofline's achieved TFLOP/s.
 _CONV_PROFILE = None

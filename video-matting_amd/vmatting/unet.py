@@ -70,6 +70,9 @@ class UNet:
     # upconv_2 too since its odd phases skip their zero taps (same-box A/B: -0.5 % on the whole forward vs resize +
     # conv on the rows kernel; without the skip, folding it was slower)
     fold_upconv = ("upconv_2", "upconv_3", "upconv_4")
+    # with the head split, upconv_4 takes conv1_5's shares of its own half of cat1 in its epilogue too
+    # (vm_conv3x3_up2x_head_nhwc): cat1 never reaches HBM and the head only sums the two partial sets
+    fuse_up_head = True
 
     def __init__(self, vgg16_npy_path=None, dtype="bf16", device="cuda"):
         self.data_dict = load_vgg16(vgg16_npy_path)
@@ -85,6 +88,7 @@ class UNet:
         self._in8_valid = False
         self._skip_valid = True
         self._head_up = None     # split head: (conv1_5 HWIO f32 on the device, PackedConv of its upconv_4 half)
+        self._up_valid = True    # cat1's upconv_4 half holds this forward's values (False: head split kept it on chip)
 
     # ------------------------------------------------------------------ weights
     def get_conv_filter(self, name):
@@ -157,7 +161,7 @@ class UNet:
         # in8 / c11 (unfused first pair, the lazily evaluated .conv1_1) and the resize targets r1..r4 (unfolded
         # upconvs) are allocated on first use only: the bf16 fused/folded forward never touches in8, c11, r3, r4
         ws = _LazyBuffers(dict(in8=(0, 8), c11=(0, 64), r4=(0, 128), r3=(1, 256), r2=(2, 512), r1=(3, 512),
-                               hpart=(0, 12, torch.float32)), E)
+                               hpart=(0, 12, torch.float32), upart=(0, 12, torch.float32)), E)
         ws.update(
             cat1=E(0, 128),
             p1=E(1, 64), c21=E(1, 128), cat2=E(1, 256), c23=E(1, 128),
@@ -239,9 +243,17 @@ class UNet:
         ops.conv3x3(b["cat3"], C["conv3_4"], "relu", out=b["c34"])
         up(b["c34"], "upconv_3", 1, b["cat2"][..., :128], "r3")
         ops.conv3x3(b["cat2"], C["conv2_3"], "relu", out=b["c23"])
-        up(b["c23"], "upconv_4", 0, b["cat1"][..., :64], "r4")
         alpha = b["out"] if out is None else out
-        if lean:  # conv1_5 + sigmoid over the upconv_4 half + the pair kernel's shares of the conv1_2 half
+        # lean: upconv_4 takes conv1_5's shares of its own half of cat1 in its epilogue too, so neither half of cat1
+        # reaches HBM and the head only sums the two partial sets (.upconv4 is evaluated on first access)
+        self._up_valid = not (lean and self.fuse_up_head and "upconv_4" in self.fold_upconv and ops.upconv3x3_head(
+            b["c23"], C["upconv_4"], self._head_up[0], 0, b["upart"], "none", out=b["cat1"][..., :64],
+            store_y=False) is not None)
+        if self._up_valid:
+            up(b["c23"], "upconv_4", 0, b["cat1"][..., :64], "r4")
+        if lean and not self._up_valid:
+            ops.head_from_partials(b["upart"], b["hpart"], self._head_up[1].bias, logits=b["logits"], alpha=alpha)
+        elif lean:  # conv1_5 + sigmoid over the upconv_4 half + the pair kernel's shares of the conv1_2 half
             ops.conv_head(b["cat1"][..., :64], self._head_up[1], "none", out=b["logits"], alpha=alpha,
                           partial=b["hpart"])
         else:
@@ -282,8 +294,16 @@ class UNet:
 
     @property
     def upconv4(self):
-        """unet.py:200 upconv4 = concat([upconv_4, conv1_2]) (the skip half evaluated on first access)."""
-        return None if self.conv1_2 is None else self._ws["cat1"]
+        """unet.py:200 upconv4 = concat([upconv_4, conv1_2]) (either half evaluated on first access when the head
+        split kept it on chip; bit-identical to the forward's values)."""
+        if self.conv1_2 is None:
+            return None
+        if not self._up_valid:
+            L = _levels(self._ws_key[1], self._ws_key[2])
+            ops.upconv3x3(self._ws["c23"], self.convs["upconv_4"], "none", out=self._ws["cat1"][..., :64], size=L[0],
+                          rbuf=self._ws["r4"], fold="upconv_4" in self.fold_upconv)
+            self._up_valid = True
+        return self._ws["cat1"]
 
     def _publish(self, b):
         self.pool1 = b["p1"]
@@ -375,6 +395,7 @@ class GraphedForward:
         # the buffer set the graph writes stays alive with the graph; so does the forward's host-side state
         self._ws, self._ws_key = model._ws, model._ws_key
         self._skip_valid = model._skip_valid
+        self._up_valid = model._up_valid
 
     def replay(self):
         self.graph.replay()
@@ -383,6 +404,7 @@ class GraphedForward:
             m._ws, m._ws_key = self._ws, self._ws_key
             m._publish(self._ws)
         m._x, m._c11, m._in8_valid, m._skip_valid = self.input, None, False, self._skip_valid
+        m._up_valid = self._up_valid
         m.output = self.output
         return self.output
 
