@@ -1123,19 +1123,7 @@ void conv3x3_patch(ConvArgs a) {
             hwv[kk][j] = col < 9 ? a.hw[col * a.hw_cin + a.hw_coff + hc] : 0.f;
           }
       }
-      uint4 hwf[2] = {make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};
-      f32x4 dacc[FP];
-#pragma unroll
-      for (int fp = 0; fp < FP; ++fp) dacc[fp] = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (HEADOK && a.hd) {
-        // A fragments of the head filter: rows = taps (9 of 16), k = 8q + j <-> channel (2kk + j/4)*16 + 4q + j%4
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk)
-          hwf[kk] = make_uint4((uint32_t)f2bf(hwv[kk][0]) | ((uint32_t)f2bf(hwv[kk][1]) << 16),
-                               (uint32_t)f2bf(hwv[kk][2]) | ((uint32_t)f2bf(hwv[kk][3]) << 16),
-                               (uint32_t)f2bf(hwv[kk][4]) | ((uint32_t)f2bf(hwv[kk][5]) << 16),
-                               (uint32_t)f2bf(hwv[kk][6]) | ((uint32_t)f2bf(hwv[kk][7]) << 16));
-      }
+      uint4 hb[FP][2];  // head split: the B operands (bf16 outputs) of each fragment's 2 head MFMAs, used at the end
 #pragma unroll
       for (int g2 = 0; g2 < FC / 2; ++g2) {
         const int chb = n0 + wn * C::TPN + g2 * 32;  // first block channel of this 32-channel group
@@ -1157,18 +1145,13 @@ void conv3x3_patch(ConvArgs a) {
             pk[f].x = (uint32_t)f2bf(v[fp][f][0]) | ((uint32_t)f2bf(v[fp][f][1]) << 16);
             pk[f].y = (uint32_t)f2bf(v[fp][f][2]) | ((uint32_t)f2bf(v[fp][f][3]) << 16);
           }
-          if (HEADOK && a.hd) mma16<T>(hwf[g2], make_uint4(pk[0].x, pk[0].y, pk[1].x, pk[1].y), dacc[fp]);
+          hb[fp][g2] = make_uint4(pk[0].x, pk[0].y, pk[1].x, pk[1].y);
           const uint4 d = chunk_pair(pk[0], pk[1]);
           const int tr = C::prow(wm, fp), tc = C::pcol(wm, fp) + col;
           const bool ok = r0 + tr < H && c0 + tc < W && cb + c16 * 8 < ccap && !a.y_skip;
           const int pix = a.up ? (2 * tr + (phase >> 1)) * YW + 2 * tc + (phase & 1) : tr * W + tc;
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, d),
                                                  yrs, ok ? pix * ycs2 + (cb + c16 * 8) * 2 : OOB, 0, 0);
-          if (HEADOK && a.hd && g2 == FC / 2 - 1 && ckq < 3 && r0 + tr < H && c0 + tc < W) {
-            const int YH = a.up ? 2 * H : H;
-            const int yy = a.up ? 2 * (r0 + tr) + (phase >> 1) : r0 + tr, xx = a.up ? 2 * (c0 + tc) + (phase & 1) : c0 + tc;
-            *reinterpret_cast<f32x4*>(a.hd + (((long)n * YH + yy) * YW + xx) * 12 + 4 * ckq) = dacc[fp];
-          }
         }
         if (a.py) {  // tiles start on even rows/columns: every 2x2 window lies inside the tile (host: no a.up)
 #pragma unroll
@@ -1198,6 +1181,33 @@ void conv3x3_patch(ConvArgs a) {
             const bool pok = (col & 1) == 0 && v0 && (r0 >> 1) + pr < PH && (c0 >> 1) + pc < PWo && n0 + chl < a.cout;
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, d),
                                                    prs, pok ? ((pr * PWo + pc) * a.py_cstride + chl) * 2 : OOB, 0, 0);
+          }
+        }
+      }
+      if constexpr (HEADOK) {
+        if (a.hd) {
+          // the head's shares, last: the filter loads issued at the top of the epilogue had the whole epilogue to land.
+          // A fragments: rows = taps (9 of 16), k = 8q + j <-> channel (2kk + j/4)*16 + 4q + j%4
+          uint4 hwf[2];
+#pragma unroll
+          for (int kk = 0; kk < 2; ++kk)
+            hwf[kk] = make_uint4((uint32_t)f2bf(hwv[kk][0]) | ((uint32_t)f2bf(hwv[kk][1]) << 16),
+                                 (uint32_t)f2bf(hwv[kk][2]) | ((uint32_t)f2bf(hwv[kk][3]) << 16),
+                                 (uint32_t)f2bf(hwv[kk][4]) | ((uint32_t)f2bf(hwv[kk][5]) << 16),
+                                 (uint32_t)f2bf(hwv[kk][6]) | ((uint32_t)f2bf(hwv[kk][7]) << 16));
+          const int phase = a.up ? (n0 + wn * C::TPN) / a.up_cout : 0;
+          const int YH = a.up ? 2 * H : H;
+#pragma unroll
+          for (int fp = 0; fp < FP; ++fp) {
+            f32x4 d = f32x4{0.f, 0.f, 0.f, 0.f};
+            mma16<T>(hwf[0], hb[fp][0], d);
+            mma16<T>(hwf[1], hb[fp][1], d);
+            const int tr = C::prow(wm, fp), tc = C::pcol(wm, fp) + col;
+            if (ckq < 3 && r0 + tr < H && c0 + tc < W) {
+              const int yy = a.up ? 2 * (r0 + tr) + (phase >> 1) : r0 + tr;
+              const int xx = a.up ? 2 * (c0 + tc) + (phase & 1) : c0 + tc;
+              *reinterpret_cast<f32x4*>(a.hd + (((long)n * YH + yy) * YW + xx) * 12 + 4 * ckq) = d;
+            }
           }
         }
       }
@@ -2698,17 +2708,16 @@ struct BorderArgs {
 
 // Border pixels of the folded upconv, computed the unfused way: the 9 resized taps (TF1 legacy bilinear in f32,
 // rounded to bf16 as vm_resize_bilinear_tf1_nhwc stores them; zero outside the 2H x 2W frame) of 16 pixels are
-// staged per 32-channel granule, and 36 MFMAs (9 taps x 4 groups of 16 output channels) consume them.  The granule
-// loop is spread over the 4 waves (wave w takes granules w, w+4, ...; its own staging buffer, so no block barrier
-// per granule), and the 4 partial sums are added in LDS at the end: the work per block is a few microseconds of
-// latency, so splitting K across waves is what shortens it.
+// staged per 32-channel granule, and wave w runs the 9 MFMAs of its 16 output channels over them.  Every granule is
+// consumed in order by one accumulator chain (granule-major, taps 0..8: the K order of the packed filter), so a
+// border pixel equals the resize + conv3x3 path bit for bit.  The kernel is latency-bound (a few hundred blocks), so
+// the low-res gathers and filter fragments of the granule after next are in flight while this one's are consumed, and the staging is double-buffered (one block barrier per granule).
 __device__ __forceinline__ uint4 sel3(int i, uint4 a, uint4 b, uint4 c) { return i == 0 ? a : (i == 1 ? b : c); }
 
 __global__ __launch_bounds__(256) void conv3x3_up2x_border(BorderArgs a) {
   using T = uint16_t;
-  constexpr int RS = 64 + 4;  // reduction row (f32)
-  __shared__ __attribute__((aligned(16))) char stg[4][9 * 16 * 64];
-  __shared__ __attribute__((aligned(16))) float red[4][16 * RS];
+  __shared__ __attribute__((aligned(16))) char stg[2][9 * 16 * 64];  // [buffer][tap][pixel][32 channels]
+  __shared__ __attribute__((aligned(16))) float red[16 * 64 + 9 * 64];  // head split: values + head filter
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int OH = 2 * a.H, OW = 2 * a.W;
   const long total = (long)a.nframes * a.nb, b0 = (long)blockIdx.x * 16;
@@ -2723,44 +2732,53 @@ __global__ __launch_bounds__(256) void conv3x3_up2x_border(BorderArgs a) {
   };
   const T* xb = reinterpret_cast<const T*>(a.x) + a.x_coff;
   const T* wb = reinterpret_cast<const T*>(a.w);
-  char* my = stg[wave];
-  f32x4 acc[4];
-#pragma unroll
-  for (int g = 0; g < 4; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // lane -> (pixel, 8-channel quarter of the granule); its 9 taps are the 3 x 3 neighbourhood of the border pixel
-  // in the resized frame, which reads at most a 3 x 3 block of the low-res frame: 9 gathers, all in flight at once
-  const int px = (lane >> 2) & 15, q = lane & 3;
-  const bool live = b0 + px < total;
+  // staging role: thread (px, q, dh) builds taps (dh, 0..2) of pixel px for channels 8q..8q+7 of the granule; its
+  // resized row oy + dh - 1 blends low-res rows y0, y1, whose columns x0c .. x0c+2 cover the three taps
+  const int spx = tid & 15, sq = (tid >> 4) & 3, sdh = tid >> 6;  // sdh == 3: no staging work
   int pn = 0, oy = 0, ox = 0;
-  if (live) decode(b0 + px, pn, oy, ox);
-  const int ry0 = max(oy - 1, 0) >> 1, cx0 = max(ox - 1, 0) >> 1;
-  for (int cc = wave; cc < a.nch; cc += 4) {  // wave-uniform trip count: no block barrier inside
-    const T* xr = xb + ((long)pn * a.H) * a.W * (long)a.x_cstride + cc * 32 + q * 8;
-    auto ld = [&](int i, int j) -> uint4 {
-      const int yy = min(ry0 + i, a.H - 1), xx = min(cx0 + j, a.W - 1);
-      return live ? *reinterpret_cast<const uint4*>(xr + ((long)yy * a.W + xx) * a.x_cstride) : make_uint4(0, 0, 0, 0);
-    };
-    const uint4 b00 = ld(0, 0), b01 = ld(0, 1), b02 = ld(0, 2);
-    const uint4 b10 = ld(1, 0), b11 = ld(1, 1), b12 = ld(1, 2);
-    const uint4 b20 = ld(2, 0), b21 = ld(2, 1), b22 = ld(2, 2);
-    auto pick = [=](int i, int j) -> uint4 {  // the 3 x 3 block entry (i, j) for runtime i, j: selects, no indexing
-      return sel3(i, sel3(j, b00, b01, b02), sel3(j, b10, b11, b12), sel3(j, b20, b21, b22));
-    };
+  const bool live = b0 + spx < total && sdh < 3;
+  if (b0 + spx < total) decode(b0 + spx, pn, oy, ox);
+  const int ry = oy + sdh - 1;                  // resized row of this thread's taps
+  const bool rok = live && (unsigned)ry < (unsigned)OH;
+  const float sy = (float)max(ry, 0) * 0.5f;
+  const float fy0 = floorf(sy);
+  const int y0 = (int)fy0, y1 = min(y0 + 1, a.H - 1);
+  const float ly = sy - fy0;
+  const int cx0 = max(ox - 1, 0) >> 1;          // first low-res column any tap reads
+  const T* xr = xb + ((long)pn * a.H) * a.W * (long)a.x_cstride + sq * 8;
+  auto gather = [&](int cc, uint4 (&g)[6]) __attribute__((always_inline)) {
 #pragma unroll
-    for (int tap = 0; tap < 9; ++tap) {
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        const int yy = i ? y1 : y0, xx = min(cx0 + j, a.W - 1);
+        g[i * 3 + j] = rok ? *reinterpret_cast<const uint4*>(xr + ((long)yy * a.W + xx) * a.x_cstride + cc * 32)
+                           : make_uint4(0, 0, 0, 0);
+      }
+  };
+  // filter fragments of this wave's 16 output channels: A rows = channels cob + 16w + (lane & 15), K-step = (cc, tap)
+  const T* wrow = wb + (long)(cob + wave * 16 + (lane & 15)) * a.K_pad + (lane >> 4) * 8;
+  auto wload = [&](int cc, uint4 (&w)[9]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) w[tap] = *reinterpret_cast<const uint4*>(wrow + (cc * 9 + tap) * 32);
+  };
+  auto stage = [&](const uint4 (&g)[6], int buf) __attribute__((always_inline)) {
+    if (sdh >= 3) return;
+#pragma unroll
+    for (int dw = 0; dw < 3; ++dw) {
       float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-      const int yy = oy + tap / 3 - 1, xx = ox + tap % 3 - 1;
-      if (live && (unsigned)yy < (unsigned)OH && (unsigned)xx < (unsigned)OW) {
+      const int rx = ox + dw - 1;
+      if (rok && (unsigned)rx < (unsigned)OW) {
 #pragma clang fp contract(off)
-        const float sy = (float)yy * 0.5f, sx = (float)xx * 0.5f;
-        const float fy0 = floorf(sy), fx0 = floorf(sx);
-        const int y0 = (int)fy0, x0 = (int)fx0, y1 = min(y0 + 1, a.H - 1), x1 = min(x0 + 1, a.W - 1);
-        const float ly = sy - fy0, lx = sx - fx0;
+        const float sx = (float)rx * 0.5f;
+        const float fx0 = floorf(sx);
+        const int x0 = (int)fx0, x1 = min(x0 + 1, a.W - 1);
+        const float lx = sx - fx0;
         float tl[8], tr[8], bl[8], br[8];
-        Chunk<T>::unpack(pick(y0 - ry0, x0 - cx0), tl);
-        Chunk<T>::unpack(pick(y0 - ry0, x1 - cx0), tr);
-        Chunk<T>::unpack(pick(y1 - ry0, x0 - cx0), bl);
-        Chunk<T>::unpack(pick(y1 - ry0, x1 - cx0), br);
+        Chunk<T>::unpack(sel3(x0 - cx0, g[0], g[1], g[2]), tl);
+        Chunk<T>::unpack(sel3(x1 - cx0, g[0], g[1], g[2]), tr);
+        Chunk<T>::unpack(sel3(x0 - cx0, g[3], g[4], g[5]), bl);
+        Chunk<T>::unpack(sel3(x1 - cx0, g[3], g[4], g[5]), br);
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           const float top = tl[e] + (tr[e] - tl[e]) * lx;
@@ -2768,61 +2786,63 @@ __global__ __launch_bounds__(256) void conv3x3_up2x_border(BorderArgs a) {
           o[e] = top + (bot - top) * ly;
         }
       }
-      *reinterpret_cast<uint4*>(my + (tap * 16 + px) * 64 + q * 16) = Chunk<T>::pack(o);
+      *reinterpret_cast<uint4*>(stg[buf] + ((sdh * 3 + dw) * 16 + spx) * 64 + sq * 16) = Chunk<T>::pack(o);
     }
-    // the wave reads what its own lanes wrote: complete the LDS stores before the fragment loads
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  };
+  f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+  // two register sets, A for even and B for odd granules, each refilled right after its use: granule cc+2's gathers
+  // and filter fragments load while cc+1 is consumed (a rotation through one set of registers would make every
+  // copy wait for the load it moves)
+  uint4 gA[6], gB[6], wA[9], wB[9];
+  auto iter = [&](int cc, uint4 (&g)[6], uint4 (&w)[9]) __attribute__((always_inline)) {
+    stage(g, cc & 1);
+    if (cc + 2 < a.nch) gather(cc + 2, g);
+    // LDS-only barrier: __syncthreads would also wait (vmcnt(0)) for the loads in flight for the next granules
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const T* wrow = wb + (long)(cob + g * 16 + (lane & 15)) * a.K_pad + cc * 9 * 32 + (lane >> 4) * 8;
-      uint4 wf[9];
-#pragma unroll
-      for (int tap = 0; tap < 9; ++tap) wf[tap] = *reinterpret_cast<const uint4*>(wrow + tap * 32);
-#pragma unroll
-      for (int tap = 0; tap < 9; ++tap)
-        mma16<T>(wf[tap], *reinterpret_cast<const uint4*>(my + (tap * 16 + (lane & 15)) * 64 + (lane >> 4) * 16),
-                 acc[g]);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (int tap = 0; tap < 9; ++tap)
+      mma16<T>(w[tap], *reinterpret_cast<const uint4*>(stg[cc & 1] + (tap * 16 + (lane & 15)) * 64 + (lane >> 4) * 16),
+               acc);
+    if (cc + 2 < a.nch) wload(cc + 2, w);
+  };
+  gather(0, gA);
+  wload(0, wA);
+  if (a.nch > 1) {
+    gather(1, gB);
+    wload(1, wB);
   }
-  // lane holds output channels cob + g*16 + 4*(lane>>4) + j of border pixel b0 + (lane&15)
-#pragma unroll
-  for (int g = 0; g < 4; ++g)
-    *reinterpret_cast<float4*>(&red[wave][(lane & 15) * RS + g * 16 + 4 * (lane >> 4)]) =
-        make_float4(acc[g][0], acc[g][1], acc[g][2], acc[g][3]);
-  __syncthreads();
-  const int ep = tid >> 4, cq = (tid & 15) * 4;
+  for (int cc = 0; cc < a.nch; cc += 2) {
+    iter(cc, gA, wA);
+    if (cc + 1 < a.nch) iter(cc + 1, gB, wB);
+  }
+  // lane holds output channels cob + 16w + 4q + j (q = lane >> 4) of border pixel b0 + (lane & 15)
+  const int ep = lane & 15, cq = wave * 16 + 4 * (lane >> 4);
   const long b = b0 + ep;
-  if (b >= total && !a.hd) return;
-  int n = 0, ey = 0, ex = 0;
   const bool bok = b < total;
+  int n = 0, ey = 0, ex = 0;
   if (bok) decode(b, n, ey, ex);
   float v[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int co = cob + cq + j;
-    const float sum = ((red[0][ep * RS + cq + j] + red[1][ep * RS + cq + j]) + red[2][ep * RS + cq + j]) +
-                      red[3][ep * RS + cq + j];
     const float sc = a.scale ? a.scale[co] : 1.f;
-    v[j] = fmaf(sum, sc, (a.bias ? a.bias[co] : 0.f) * sc + (a.shift ? a.shift[co] : 0.f));
+    v[j] = fmaf(acc[j], sc, (a.bias ? a.bias[co] : 0.f) * sc + (a.shift ? a.shift[co] : 0.f));
     if (a.act == VM_ACT_RELU) v[j] = fmaxf(v[j], 0.f);
     else if (a.act == VM_ACT_SIGMOID) v[j] = sigmoid_precise(v[j]);
   }
-  T* yp = reinterpret_cast<T*>(a.y) + (((long)n * OH + ey) * OW + ex) * (long)a.y_cstride + a.y_coff + cob + cq;
   uint2 pk;
   pk.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
   pk.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-  if (!a.y_skip && bok) *reinterpret_cast<uint2*>(yp) = pk;
+  if (!a.y_skip && bok)
+    *reinterpret_cast<uint2*>(reinterpret_cast<T*>(a.y) + (((long)n * OH + ey) * OW + ex) * (long)a.y_cstride + a.y_coff +
+                              cob + cq) = pk;
   if (a.hd) {  // (uniform: a.hd is a kernel argument; every thread reaches the barriers below)
     // the border pixel's 64 bf16 outputs -> 9 per-tap shares sum_c bf16(hw[tap][coff + c]) * y[c] (f32, in channel
     // order); taps 9..11 zero like the MFMA epilogues'
-    float* vals = &red[0][0];     // [16 pixels][64] (the reduction rows were last read above)
-    float* hwl = vals + 16 * 64;  // the head filter's 9 x 64 taps of these channels, bf16-rounded
-    __syncthreads();
+    float* vals = red;            // [16 pixels][64]
+    float* hwl = red + 16 * 64;   // the head filter's 9 x 64 taps of these channels, bf16-rounded
 #pragma unroll
     for (int j = 0; j < 4; ++j) vals[ep * 64 + cq + j] = bf2f(f2bf(v[j]));
     for (int i = tid; i < 9 * 64; i += 256) hwl[i] = bf2f(f2bf(a.hw[(i >> 6) * a.hw_cin + a.hw_coff + (i & 63)]));
@@ -2831,13 +2851,13 @@ __global__ __launch_bounds__(256) void conv3x3_up2x_border(BorderArgs a) {
       const int pe = tid / 12, tap = tid - pe * 12;
       const long bb = b0 + pe;
       if (bb < total) {
-        int pn, py, px2;
-        decode(bb, pn, py, px2);
-        float acc = 0.f;
+        int pn2, py, px2;
+        decode(bb, pn2, py, px2);
+        float hacc = 0.f;
         if (tap < 9)
 #pragma unroll 16
-          for (int c = 0; c < 64; ++c) acc = fmaf(hwl[tap * 64 + c], vals[pe * 64 + c], acc);
-        a.hd[(((long)pn * OH + py) * OW + px2) * 12 + tap] = acc;
+          for (int c = 0; c < 64; ++c) hacc = fmaf(hwl[tap * 64 + c], vals[pe * 64 + c], hacc);
+        a.hd[(((long)pn2 * OH + py) * OW + px2) * 12 + tap] = hacc;
       }
     }
   }
