@@ -155,6 +155,14 @@ int vm_conv3x3_pair_first_nhwc(const vm_tensor* x, const void* packed1, int cin1
                                const void* packed2, int cout2, const float* bias2, const float* scale2,
                                const float* shift2, int act2, vm_tensor* y, vm_tensor* ypool, void* stream);
 
+/* The pair with conv1_1's own output kept too (mid: bf16 [n,h,w,64] view, 16-byte aligned channel chunks) — the
+ * training towers (unet_simple.py:60-62), whose select convs read conv1_1 (unet_simple.py:160-168).
+ * VM_EUNSUPPORTED when the strip-walking kernel cannot take the case (the caller runs the two convs). */
+int vm_conv3x3_pair_first_mid_nhwc(const vm_tensor* x, const void* packed1, int cin1, const float* bias1,
+                                   const void* packed2, int cout2, const float* bias2, const float* scale2,
+                                   const float* shift2, int act2, vm_tensor* y, vm_tensor* ypool, vm_tensor* mid,
+                                   void* stream);
+
 /* The pair kernel with the head split (unet.py:170-172 + 203-205): conv1_5 over cat1 = [up, skip] is linear in
  * its input channels, so the skip half's share is taken where conv1_2's output is made.  Besides y/ypool the pair
  * kernel writes partial[pixel][12] (f32, n*h*w*12 floats): taps 0..8 of sum_c y[pixel][c] * head_w[tap][head_coff+c]

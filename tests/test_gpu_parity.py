@@ -588,6 +588,31 @@ def test_pair_strip_matches_tile_kernel(shape, xdtype):
     assert float(qs[..., 9:].abs().max()) == 0.0
 
 
+@pytest.mark.parametrize("shape", [(24, 320, 320), (3, 67, 101), (1, 1, 1)])
+def test_pair_first_keep_mid(shape):
+    """ops.conv_pair_first(keep_mid=True) (vm_conv3x3_pair_first_mid_nhwc on the strip kernel; the two convs where
+    it cannot run): conv1_1's output, conv1_2 and pool1 equal the separate convs bit for bit — the training towers'
+    first pair (unet_simple.py:60-62), whose select convs read conv1_1."""
+    from vmatting import ops
+    n, h, w = shape
+    rs = np.random.RandomState(h + w + n)
+    x8 = torch.zeros((n, h, w, 8), dtype=torch.bfloat16, device=DEV)
+    x8[..., :3] = torch.from_numpy((rs.normal(size=(n, h, w, 3)) * 50).astype(np.float32)).to(DEV).to(torch.bfloat16)
+    pc1 = ops.PackedConv((rs.normal(size=(3, 3, 3, 64)) * 0.2).astype(np.float32), (rs.normal(size=64) * 0.1).astype(
+        np.float32), torch.bfloat16, DEV)
+    pc2 = ops.PackedConv((rs.normal(size=(3, 3, 64, 64)) * 0.06).astype(np.float32), (rs.normal(size=64) * 0.1).astype(
+        np.float32), torch.bfloat16, DEV)
+    mid = torch.full((n, h, w, 64), 7.0, dtype=torch.bfloat16, device=DEV)
+    y = torch.full((n, h, w, 64), 7.0, dtype=torch.bfloat16, device=DEV)
+    p = torch.full((n, (h + 1) // 2, (w + 1) // 2, 64), 7.0, dtype=torch.bfloat16, device=DEV)
+    ops.conv_pair_first(x8[..., :3], pc1, pc2, "relu", out=y, pool_out=p, mid=mid, keep_mid=True)
+    m_ref = ops.conv3x3(x8[..., :3], pc1, "relu")
+    y_ref = ops.conv3x3(m_ref, pc2, "relu")
+    assert torch.equal(mid, m_ref)
+    assert torch.equal(y, y_ref)
+    assert torch.equal(p, ops.maxpool2x2(y_ref))
+
+
 @pytest.mark.parametrize("shape", [(1, 16, 64), (2, 17, 45), (1, 1, 1), (1, 135, 240), (1, 40, 70)])
 @pytest.mark.parametrize("store_y", [False, True])
 def test_conv_pair_first_head_partials(shape, store_y):

@@ -2708,17 +2708,19 @@ struct BorderArgs {
 
 // Border pixels of the folded upconv, computed the unfused way: the 9 resized taps (TF1 legacy bilinear in f32,
 // rounded to bf16 as vm_resize_bilinear_tf1_nhwc stores them; zero outside the 2H x 2W frame) of 16 pixels are
-// staged per 32-channel granule, and wave w runs the 9 MFMAs of its 16 output channels over them.  Every granule is
-// consumed in order by one accumulator chain (granule-major, taps 0..8: the K order of the packed filter), so a
-// border pixel equals the resize + conv3x3 path bit for bit.  The kernel is latency-bound (a few hundred blocks), so
-// the low-res gathers and filter fragments of the granule after next are in flight while this one's are consumed, and the staging is double-buffered (one block barrier per granule).
+// staged per 32-channel granule and consumed by MFMAs.  The pass is latency-bound (a few hundred blocks; each granule
+// costs a round trip for its gathers), so a 1024-thread block splits the granules 4 ways (wave w: output channels
+// 16 (w & 3) .. +15, granules (w >> 2), (w >> 2) + 4, ...: each 4-wave group stages and consumes its own granules,
+// double-buffered, with one LDS-only barrier per step) and adds the 4 partial sums in a fixed order at the end.
 __device__ __forceinline__ uint4 sel3(int i, uint4 a, uint4 b, uint4 c) { return i == 0 ? a : (i == 1 ? b : c); }
 
-__global__ __launch_bounds__(256) void conv3x3_up2x_border(BorderArgs a) {
+template <int BD_KS>  // granule split of the border pass (waves = 4 x BD_KS)
+__global__ __launch_bounds__(256 * BD_KS) void conv3x3_up2x_border(BorderArgs a) {
   using T = uint16_t;
-  __shared__ __attribute__((aligned(16))) char stg[2][9 * 16 * 64];  // [buffer][tap][pixel][32 channels]
-  __shared__ __attribute__((aligned(16))) float red[16 * 64 + 9 * 64];  // head split: values + head filter
+  __shared__ __attribute__((aligned(16))) char stg[BD_KS][2][9 * 16 * 64];  // [split][buffer][tap][pixel][32 ch]
+  __shared__ __attribute__((aligned(16))) float red[BD_KS * 16 * 64];       // [split][pixel][channel] partial sums
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int cg = wave & 3, ks = wave >> 2, gt = tid & 255;  // channel group, granule split, thread in the split group
   const int OH = 2 * a.H, OW = 2 * a.W;
   const long total = (long)a.nframes * a.nb, b0 = (long)blockIdx.x * 16;
   const int cob = blockIdx.y * 64;
@@ -2732,19 +2734,19 @@ __global__ __launch_bounds__(256) void conv3x3_up2x_border(BorderArgs a) {
   };
   const T* xb = reinterpret_cast<const T*>(a.x) + a.x_coff;
   const T* wb = reinterpret_cast<const T*>(a.w);
-  // staging role: thread (px, q, dh) builds taps (dh, 0..2) of pixel px for channels 8q..8q+7 of the granule; its
-  // resized row oy + dh - 1 blends low-res rows y0, y1, whose columns x0c .. x0c+2 cover the three taps
-  const int spx = tid & 15, sq = (tid >> 4) & 3, sdh = tid >> 6;  // sdh == 3: no staging work
+  // staging role inside the split group: thread (px, q, dh) builds taps (dh, 0..2) of pixel px for channels 8q..8q+7
+  // of the granule; its resized row oy + dh - 1 blends low-res rows y0, y1, whose columns x0c .. x0c+2 cover the taps
+  const int spx = gt & 15, sq = (gt >> 4) & 3, sdh = gt >> 6;  // sdh == 3: no staging work
   int pn = 0, oy = 0, ox = 0;
   const bool live = b0 + spx < total && sdh < 3;
   if (b0 + spx < total) decode(b0 + spx, pn, oy, ox);
-  const int ry = oy + sdh - 1;                  // resized row of this thread's taps
+  const int ry = oy + sdh - 1;
   const bool rok = live && (unsigned)ry < (unsigned)OH;
   const float sy = (float)max(ry, 0) * 0.5f;
   const float fy0 = floorf(sy);
   const int y0 = (int)fy0, y1 = min(y0 + 1, a.H - 1);
   const float ly = sy - fy0;
-  const int cx0 = max(ox - 1, 0) >> 1;          // first low-res column any tap reads
+  const int cx0 = max(ox - 1, 0) >> 1;
   const T* xr = xb + ((long)pn * a.H) * a.W * (long)a.x_cstride + sq * 8;
   auto gather = [&](int cc, uint4 (&g)[6]) __attribute__((always_inline)) {
 #pragma unroll
@@ -2752,17 +2754,12 @@ __global__ __launch_bounds__(256) void conv3x3_up2x_border(BorderArgs a) {
 #pragma unroll
       for (int j = 0; j < 3; ++j) {
         const int yy = i ? y1 : y0, xx = min(cx0 + j, a.W - 1);
-        g[i * 3 + j] = rok ? *reinterpret_cast<const uint4*>(xr + ((long)yy * a.W + xx) * a.x_cstride + cc * 32)
+        g[i * 3 + j] = rok && cc < a.nch
+                           ? *reinterpret_cast<const uint4*>(xr + ((long)yy * a.W + xx) * a.x_cstride + cc * 32)
                            : make_uint4(0, 0, 0, 0);
       }
   };
-  // filter fragments of this wave's 16 output channels: A rows = channels cob + 16w + (lane & 15), K-step = (cc, tap)
-  const T* wrow = wb + (long)(cob + wave * 16 + (lane & 15)) * a.K_pad + (lane >> 4) * 8;
-  auto wload = [&](int cc, uint4 (&w)[9]) __attribute__((always_inline)) {
-#pragma unroll
-    for (int tap = 0; tap < 9; ++tap) w[tap] = *reinterpret_cast<const uint4*>(wrow + (cc * 9 + tap) * 32);
-  };
-  auto stage = [&](const uint4 (&g)[6], int buf) __attribute__((always_inline)) {
+  auto stage = [&](const uint4 (&g)[6], char* dst) __attribute__((always_inline)) {
     if (sdh >= 3) return;
 #pragma unroll
     for (int dw = 0; dw < 3; ++dw) {
@@ -2774,78 +2771,91 @@ __global__ __launch_bounds__(256) void conv3x3_up2x_border(BorderArgs a) {
         const float fx0 = floorf(sx);
         const int x0 = (int)fx0, x1 = min(x0 + 1, a.W - 1);
         const float lx = sx - fx0;
-        float tl[8], tr[8], bl[8], br[8];
-        Chunk<T>::unpack(sel3(x0 - cx0, g[0], g[1], g[2]), tl);
-        Chunk<T>::unpack(sel3(x1 - cx0, g[0], g[1], g[2]), tr);
-        Chunk<T>::unpack(sel3(x0 - cx0, g[3], g[4], g[5]), bl);
-        Chunk<T>::unpack(sel3(x1 - cx0, g[3], g[4], g[5]), br);
+        // (top row, then bottom row: fewer values live at once, the same arithmetic)
+        float l8[8], r8[8], top[8];
+        Chunk<T>::unpack(sel3(x0 - cx0, g[0], g[1], g[2]), l8);
+        Chunk<T>::unpack(sel3(x1 - cx0, g[0], g[1], g[2]), r8);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) top[e] = l8[e] + (r8[e] - l8[e]) * lx;
+        Chunk<T>::unpack(sel3(x0 - cx0, g[3], g[4], g[5]), l8);
+        Chunk<T>::unpack(sel3(x1 - cx0, g[3], g[4], g[5]), r8);
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          const float top = tl[e] + (tr[e] - tl[e]) * lx;
-          const float bot = bl[e] + (br[e] - bl[e]) * lx;
-          o[e] = top + (bot - top) * ly;
+          const float bot = l8[e] + (r8[e] - l8[e]) * lx;
+          o[e] = top[e] + (bot - top[e]) * ly;
         }
       }
-      *reinterpret_cast<uint4*>(stg[buf] + ((sdh * 3 + dw) * 16 + spx) * 64 + sq * 16) = Chunk<T>::pack(o);
+      *reinterpret_cast<uint4*>(dst + ((sdh * 3 + dw) * 16 + spx) * 64 + sq * 16) = Chunk<T>::pack(o);
     }
   };
+  // filter fragments of this wave's 16 output channels: A rows = channels cob + 16 cg + (lane & 15)
+  const T* wrow = wb + (long)(cob + cg * 16 + (lane & 15)) * a.K_pad + (lane >> 4) * 8;
   f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-  // two register sets, A for even and B for odd granules, each refilled right after its use: granule cc+2's gathers
-  // and filter fragments load while cc+1 is consumed (a rotation through one set of registers would make every
-  // copy wait for the load it moves)
-  uint4 gA[6], gB[6], wA[9], wB[9];
-  auto iter = [&](int cc, uint4 (&g)[6], uint4 (&w)[9]) __attribute__((always_inline)) {
-    stage(g, cc & 1);
-    if (cc + 2 < a.nch) gather(cc + 2, g);
-    // LDS-only barrier: __syncthreads would also wait (vmcnt(0)) for the loads in flight for the next granules
+  const int steps = (a.nch + BD_KS - 1) / BD_KS;  // every group runs the same number of steps (uniform barriers)
+  uint4 g[6];
+  gather(ks, g);
+  for (int i = 0; i < steps; ++i) {
+    const int cc = ks + i * BD_KS;
+    char* buf = stg[ks][i & 1];
+    stage(g, buf);
+    gather(cc + BD_KS, g);  // the group's next granule goes in flight under this one's barrier and MFMAs
+    uint4 w[9];
+    if (cc < a.nch) {
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) w[tap] = *reinterpret_cast<const uint4*>(wrow + (cc * 9 + tap) * 32);
+    }
+    // LDS-only barrier: __syncthreads would also wait (vmcnt(0)) for the gathers in flight
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
+    if (cc < a.nch) {
 #pragma unroll
-    for (int tap = 0; tap < 9; ++tap)
-      mma16<T>(w[tap], *reinterpret_cast<const uint4*>(stg[cc & 1] + (tap * 16 + (lane & 15)) * 64 + (lane >> 4) * 16),
-               acc);
-    if (cc + 2 < a.nch) wload(cc + 2, w);
-  };
-  gather(0, gA);
-  wload(0, wA);
-  if (a.nch > 1) {
-    gather(1, gB);
-    wload(1, wB);
+      for (int tap = 0; tap < 9; ++tap)
+        mma16<T>(w[tap], *reinterpret_cast<const uint4*>(buf + (tap * 16 + (lane & 15)) * 64 + (lane >> 4) * 16), acc);
+    }
   }
-  for (int cc = 0; cc < a.nch; cc += 2) {
-    iter(cc, gA, wA);
-    if (cc + 1 < a.nch) iter(cc + 1, gB, wB);
-  }
-  // lane holds output channels cob + 16w + 4q + j (q = lane >> 4) of border pixel b0 + (lane & 15)
-  const int ep = lane & 15, cq = wave * 16 + 4 * (lane >> 4);
+  // partial sums: lane holds channels 16 cg + 4 (lane >> 4) + j of pixel lane & 15
+#pragma unroll
+  for (int j = 0; j < 4; ++j) red[(ks * 16 + (lane & 15)) * 64 + cg * 16 + 4 * (lane >> 4) + j] = acc[j];
+  __syncthreads();
+  // one thread per (pixel, 4 channels): the splits added in order, then bias / affine / act
+  const bool ew = tid < 256;
+  const int ep = tid >> 4, cq = (tid & 15) * 4;
   const long b = b0 + ep;
-  const bool bok = b < total;
+  const bool bok = ew && b < total;
   int n = 0, ey = 0, ex = 0;
   if (bok) decode(b, n, ey, ex);
-  float v[4];
+  float v[4] = {0.f, 0.f, 0.f, 0.f};
+  uint2 pk = make_uint2(0, 0);
+  if (ew) {
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int co = cob + cq + j;
-    const float sc = a.scale ? a.scale[co] : 1.f;
-    v[j] = fmaf(acc[j], sc, (a.bias ? a.bias[co] : 0.f) * sc + (a.shift ? a.shift[co] : 0.f));
-    if (a.act == VM_ACT_RELU) v[j] = fmaxf(v[j], 0.f);
-    else if (a.act == VM_ACT_SIGMOID) v[j] = sigmoid_precise(v[j]);
+    for (int j = 0; j < 4; ++j) {
+      float sum = red[(0 * 16 + ep) * 64 + cq + j];
+#pragma unroll
+      for (int k = 1; k < BD_KS; ++k) sum += red[(k * 16 + ep) * 64 + cq + j];
+      const int co = cob + cq + j;
+      const float sc = a.scale ? a.scale[co] : 1.f;
+      v[j] = fmaf(sum, sc, (a.bias ? a.bias[co] : 0.f) * sc + (a.shift ? a.shift[co] : 0.f));
+      if (a.act == VM_ACT_RELU) v[j] = fmaxf(v[j], 0.f);
+      else if (a.act == VM_ACT_SIGMOID) v[j] = sigmoid_precise(v[j]);
+    }
+    pk.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+    pk.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+    if (!a.y_skip && bok)
+      *reinterpret_cast<uint2*>(reinterpret_cast<T*>(a.y) + (((long)n * OH + ey) * OW + ex) * (long)a.y_cstride +
+                                a.y_coff + cob + cq) = pk;
   }
-  uint2 pk;
-  pk.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-  pk.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-  if (!a.y_skip && bok)
-    *reinterpret_cast<uint2*>(reinterpret_cast<T*>(a.y) + (((long)n * OH + ey) * OW + ex) * (long)a.y_cstride + a.y_coff +
-                              cob + cq) = pk;
   if (a.hd) {  // (uniform: a.hd is a kernel argument; every thread reaches the barriers below)
     // the border pixel's 64 bf16 outputs -> 9 per-tap shares sum_c bf16(hw[tap][coff + c]) * y[c] (f32, in channel
     // order); taps 9..11 zero like the MFMA epilogues'
-    float* vals = red;            // [16 pixels][64]
-    float* hwl = red + 16 * 64;   // the head filter's 9 x 64 taps of these channels, bf16-rounded
+    float* vals = reinterpret_cast<float*>(&stg[0][0][0]);  // [16 pixels][64]
+    float* hwl = vals + 16 * 64;                              // the head filter's 9 x 64 taps, bf16-rounded
+    __syncthreads();
+    if (ew) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) vals[ep * 64 + cq + j] = bf2f(f2bf(v[j]));
-    for (int i = tid; i < 9 * 64; i += 256) hwl[i] = bf2f(f2bf(a.hw[(i >> 6) * a.hw_cin + a.hw_coff + (i & 63)]));
+      for (int j = 0; j < 4; ++j) vals[ep * 64 + cq + j] = bf2f(f2bf(v[j]));
+    }
+    for (int i = tid; i < 9 * 64; i += 256 * BD_KS) hwl[i] = bf2f(f2bf(a.hw[(i >> 6) * a.hw_cin + a.hw_coff + (i & 63)]));
     __syncthreads();
     if (tid < 16 * 12) {
       const int pe = tid / 12, tap = tid - pe * 12;
@@ -3143,6 +3153,7 @@ static int launch_glds(ConvArgs& a, hipStream_t st) {
   return check_launch("conv3x3_glds");
 }
 
+static long g_border_ks = 1;  // folded-upconv border pass: granule split (1, 2 or 4 wave groups per block)
 static long g_patch_repi = 1;  // patch kernel: register epilogue (bf16 outputs, no packed frames) where the tiling allows
 template <int BN, int WM, int WN, int S, int TH = 8, int MINB = 1, int UNR = 9, bool PF = false, int ABL = 0,
           bool FIRST = false, int G = 1, bool UPSKIP = false>
@@ -3668,6 +3679,11 @@ extern "C" int vm_set_option(const char* key, long value) {
     return VM_OK;
   }
 #endif
+  if (!strcmp(key, "border_ks")) {
+    if (value != 1 && value != 2 && value != 4) return fail(VM_EINVAL, "border_ks must be 1, 2 or 4");
+    g_border_ks = value;
+    return VM_OK;
+  }
   if (!strcmp(key, "patch_repi")) {
     if (value < 0 || value > 1) return fail(VM_EINVAL, "patch_repi must be 0 or 1");
     g_patch_repi = value;
@@ -3847,7 +3863,12 @@ extern "C" int vm_conv3x3_up2x_nhwc(const vm_tensor* x, const void* packed_up, c
   b.nb = 2 * OW + 2 * (OH - 2);
   const long nblk = ((long)x->n * b.nb + 15) / 16;
   if (nblk > 0x7fffffffL) return fail(VM_EUNSUPPORTED, "conv3x3_up2x: too many border pixels");
-  hipLaunchKernelGGL(conv3x3_up2x_border, dim3((unsigned)nblk, cout / 64), dim3(256), 0, st, b);
+  if (g_border_ks == 4)
+    hipLaunchKernelGGL(conv3x3_up2x_border<4>, dim3((unsigned)nblk, cout / 64), dim3(1024), 0, st, b);
+  else if (g_border_ks == 2)
+    hipLaunchKernelGGL(conv3x3_up2x_border<2>, dim3((unsigned)nblk, cout / 64), dim3(512), 0, st, b);
+  else
+    hipLaunchKernelGGL(conv3x3_up2x_border<1>, dim3((unsigned)nblk, cout / 64), dim3(256), 0, st, b);
   return check_launch("conv3x3_up2x_border");
 }
 
@@ -3908,7 +3929,18 @@ static int launch_pair_persist(ConvArgs& a, long sp, hipStream_t st) {
 static int pair_first_impl(const vm_tensor* x, const void* packed1, int cin1, const float* bias1, const void* packed2,
                            int cout2, const float* bias2, const float* scale2, const float* shift2, int act2,
                            vm_tensor* y, vm_tensor* ypool, const float* head_w, int head_cin, int head_coff,
-                           float* partial, int store_y, void* stream);
+                           float* partial, int store_y, void* stream, vm_tensor* mid = nullptr);
+
+extern "C" int vm_conv3x3_pair_first_mid_nhwc(const vm_tensor* x, const void* packed1, int cin1, const float* bias1,
+                                              const void* packed2, int cout2, const float* bias2, const float* scale2,
+                                              const float* shift2, int act2, vm_tensor* y, vm_tensor* ypool,
+                                              vm_tensor* mid, void* stream) {
+  if (!valid_tensor(mid) || mid->dtype != VM_BF16 || mid->c != 64 || !x || mid->n != x->n || mid->h != x->h ||
+      mid->w != x->w || reinterpret_cast<uintptr_t>(mid->ptr) % 16 || mid->cstride % 8 || mid->coff % 8)
+    return fail(VM_EINVAL, "conv3x3_pair_first_mid: mid must be a 16-byte aligned bf16 [n,h,w,64] view");
+  return pair_first_impl(x, packed1, cin1, bias1, packed2, cout2, bias2, scale2, shift2, act2, y, ypool, nullptr, 0, 0,
+                         nullptr, 1, stream, mid);
+}
 
 extern "C" int vm_conv3x3_pair_first_nhwc(const vm_tensor* x, const void* packed1, int cin1, const float* bias1,
                                           const void* packed2, int cout2, const float* bias2, const float* scale2,
@@ -3939,7 +3971,7 @@ extern "C" int vm_conv3x3_head_partial_nhwc(const vm_tensor* x, const void* pack
 static int pair_first_impl(const vm_tensor* x, const void* packed1, int cin1, const float* bias1, const void* packed2,
                            int cout2, const float* bias2, const float* scale2, const float* shift2, int act2,
                            vm_tensor* y, vm_tensor* ypool, const float* head_w, int head_cin, int head_coff,
-                           float* partial, int store_y, void* stream) {
+                           float* partial, int store_y, void* stream, vm_tensor* mid) {
   if (!valid_tensor(x) || !valid_tensor(y) || !packed1 || !packed2)
     return fail(VM_EINVAL, "conv3x3_pair_first: invalid tensor/weights");
   if (cin1 <= 0 || cin1 > 8 || x->c != cin1 || cout2 <= 0 || y->c != cout2)
@@ -3976,6 +4008,12 @@ static int pair_first_impl(const vm_tensor* x, const void* packed1, int cin1, co
   // the strip kernel addresses one image's output / pool with 32-bit byte offsets
   const bool strip_fits = (long)x->h * x->w * y->cstride * 2 < 0x7ffffff0L &&
                           (!ypool || (long)ypool->h * ypool->w * ypool->cstride * 2 < 0x7ffffff0L);
+  if (mid) {  // conv1_1's output too: the strip kernel only (the caller otherwise runs the two convs)
+    if (!(g_pair_strip && g_pair_kernel == 0 && strip_fits && pair_strip_ok(a) &&
+          (long)mid->h * mid->w * mid->cstride * 2 < 0x7ffffff0L))
+      return fail(VM_EUNSUPPORTED, "conv3x3_pair_first_mid: needs the strip pair kernel");
+    a.y1 = mid->ptr; a.y1_cstride = mid->cstride; a.y1_coff = mid->coff;
+  }
   if (g_pair_strip && g_pair_kernel == 0 && strip_fits && pair_strip_ok(a)) return launch_pair_strip(a, x->n, st);
   if (partial) {  // the head split lives in the persistent pair kernel only
     if (cout2 != 64 || g_pair_kernel != 0 || sp > 0x7fffffffL)

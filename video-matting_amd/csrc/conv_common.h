@@ -46,6 +46,9 @@ struct ConvArgs {
   // (40 or 20 px in 32-px tiles) stop wasting most of their last column tile.
   int vstride, vW;
   int repi;  // patch kernel: 1 = register epilogue where the tiling allows (bf16 output, no split-K, no packed frames)
+  // strip pair kernel: optional bf16 output of the FIRST conv (conv1_1 + bias + relu), [N,H,W,64] view
+  void* y1;
+  int y1_cstride, y1_coff;
 };
 
 // element offset of input channel c (relative to the view's channel 0) under the source split

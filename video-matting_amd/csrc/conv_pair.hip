@@ -144,6 +144,8 @@ void conv3x3_pair_strip(ConvArgs a, int seg, int nseg, int nstrip) {
   };
 
   // ---- conv1_1 row jr (+ bias + relu; zero outside the frame = conv1_2's SAME padding) -> this wave's plane, slot jr&3
+  T* y1b = a.y1 ? reinterpret_cast<T*>(a.y1) + a.y1_coff + ((long)n * H) * W * (long)a.y1_cstride : nullptr;
+  const __amdgpu_buffer_rsrc_t y1rs = __builtin_amdgcn_make_buffer_rsrc(y1b, 0, 0x7ffffff0, 0x00020000);
   auto conv1 = [&](int jr) __attribute__((always_inline)) {
     // lane-derived addresses are recomputed per call (an opaque copy of the lane id): hoisted out of the row loop they
     // would hold a dozen registers the filters need
@@ -207,7 +209,14 @@ void conv3x3_pair_strip(ConvArgs a, int seg, int nseg, int nstrip) {
         }
       }
       // swz2(16 fr + cl, c) = 1024 fr + swz2(cl, c): ((16 fr + cl) >> 1) & 3 == (cl >> 1) & 3
-      *reinterpret_cast<uint4*>(dst + fr * 1024) = chunk_pair(pk[0], pk[1]);
+      const uint4 ck = chunk_pair(pk[0], pk[1]);
+      *reinterpret_cast<uint4*>(dst + fr * 1024) = ck;
+      if (a.y1) {  // conv1_1 itself (the training towers' select convs read it): this segment's rows, own columns
+        const int c = c0 + rc - 1;
+        const bool ok = jr >= s0 && jr < s1 && rc >= 1 && rc <= C::SW && c < W;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, ck), y1rs,
+                                               ok ? ((jr * W + c) * a.y1_cstride + 32 * wave + 8 * cq16) * 2 : OOB, 0, 0);
+      }
     }
   };
 

@@ -80,6 +80,8 @@ SIGNATURES = [
                                      c_void_p]),
     ("vm_conv3x3_pair_first_nhwc", c_int, [P, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p,
                                            c_void_p, c_int, P, P, c_void_p]),
+    ("vm_conv3x3_pair_first_mid_nhwc", c_int, [P, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p,
+                                               c_void_p, c_int, P, P, P, c_void_p]),
     ("vm_conv3x3_pair_first_head_nhwc", c_int, [P, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p,
                                                 c_void_p, c_int, P, P, c_void_p, c_int, c_int, c_void_p, c_int,
                                                 c_void_p]),

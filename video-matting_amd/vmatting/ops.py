@@ -330,10 +330,11 @@ def conv_pair_first_head(x, pc1, pc2, head_w, head_coff, partial, act2="relu", o
     return out
 
 
-def conv_pair_first(x, pc1, pc2, act2="relu", out=None, pool_out=None, mid=None):
+def conv_pair_first(x, pc1, pc2, act2="relu", out=None, pool_out=None, mid=None, keep_mid=False):
     """conv3x3(relu(conv3x3(x, pc1)), pc2) (+ 2x2 SAME max-pool into pool_out): unet.py:170-172, conv1_1 -> conv1_2
     (-> pool1).  bf16 runs ONE kernel whose 64-channel intermediate stays in LDS (vm_conv3x3_pair_first_nhwc); any
-    other case runs the two convs through ``mid`` (the intermediate, allocated when None)."""
+    other case runs the two convs through ``mid`` (the intermediate, allocated when None).  ``keep_mid``: ``mid``
+    receives conv1_1's output in every case (the fused kernel writes it too, vm_conv3x3_pair_first_mid_nhwc)."""
     n, h, w, _ = x.shape
     if out is None:
         out = torch.empty((n, h, w, pc2.cout), dtype=x.dtype, device=x.device)
@@ -346,10 +347,20 @@ def conv_pair_first(x, pc1, pc2, act2="relu", out=None, pool_out=None, mid=None)
             ev0 = torch.cuda.Event(enable_timing=True)
             ev1 = torch.cuda.Event(enable_timing=True)
             ev0.record()
-        rc = lib().vm_conv3x3_pair_first_nhwc(ctypes.byref(xv), _ptr(pc1.packed), pc1.cin, _ptr(pc1.bias),
-                                              _ptr(pc2.packed), pc2.cout, _ptr(pc2.bias), _ptr(pc2.scale),
-                                              _ptr(pc2.shift), _lib.ACT[act2], ctypes.byref(yv),
-                                              ctypes.byref(pv) if pv is not None else None, stream_handle())
+        if keep_mid:
+            if mid is None or mid.dtype != torch.bfloat16:
+                raise ValueError("keep_mid needs a bf16 mid buffer")
+            mv = nhwc(mid)
+            rc = lib().vm_conv3x3_pair_first_mid_nhwc(ctypes.byref(xv), _ptr(pc1.packed), pc1.cin, _ptr(pc1.bias),
+                                                      _ptr(pc2.packed), pc2.cout, _ptr(pc2.bias), _ptr(pc2.scale),
+                                                      _ptr(pc2.shift), _lib.ACT[act2], ctypes.byref(yv),
+                                                      ctypes.byref(pv) if pv is not None else None, ctypes.byref(mv),
+                                                      stream_handle())
+        else:
+            rc = lib().vm_conv3x3_pair_first_nhwc(ctypes.byref(xv), _ptr(pc1.packed), pc1.cin, _ptr(pc1.bias),
+                                                  _ptr(pc2.packed), pc2.cout, _ptr(pc2.bias), _ptr(pc2.scale),
+                                                  _ptr(pc2.shift), _lib.ACT[act2], ctypes.byref(yv),
+                                                  ctypes.byref(pv) if pv is not None else None, stream_handle())
         if rc != _lib.VM_EUNSUPPORTED:
             check(rc, "conv3x3_pair_first")
             if prof is not None:

@@ -128,8 +128,9 @@ class UNetSimple:
         batch-invariant."""
         V = self.vgg.convs
         t = lambda k: b["t_" + k]  # noqa: E731
-        ops.conv3x3(b["tin"][..., :3], V["conv1_1"], "relu", out=t("conv1_1"))
-        ops.conv3x3(t("conv1_1"), V["conv1_2"], "relu", out=t("conv1_2"), pool_out=b["tpool1"])
+        # conv1_1 -> conv1_2 -> pool1 as one strip-walking kernel that also writes conv1_1 (select1_2 reads it)
+        ops.conv_pair_first(b["tin"][..., :3], V["conv1_1"], V["conv1_2"], "relu", out=t("conv1_2"),
+                            pool_out=b["tpool1"], mid=t("conv1_1"), keep_mid=True)
         ops.conv3x3(b["tpool1"], V["conv2_1"], "relu", out=t("conv2_1"))
         ops.conv3x3(t("conv2_1"), V["conv2_2"], "relu", out=t("conv2_2"), pool_out=b["tpool2"])
         ops.conv3x3(b["tpool2"], V["conv3_1"], "relu", out=t("conv3_1"))
