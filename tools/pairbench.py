@@ -24,12 +24,15 @@ def main():
     ap.add_argument("--xin-wide", type=int, default=1)
     ap.add_argument("--pair-strip", type=int, default=1)
     ap.add_argument("--abl", type=int, default=0)
+    ap.add_argument("--pin", type=int, default=1)
     ap.add_argument("--head", type=int, default=1, help="head split partials + no conv1_2 store (the UNetVideo path)")
     a = ap.parse_args()
     _lib.set_option("pair_xin_wide", a.xin_wide)
     h, w = (int(v) for v in a.hw.split("x"))
     _lib.set_option("pair_kernel", a.pair_kernel)
     _lib.set_option("pair_strip", a.pair_strip)
+    if a.pin != 1:
+        _lib.set_option("pair_strip_pin", a.pin)
     if a.abl:  # timing-only ablations: the study build (VM_LIB_PATH=video-matting_amd/study/libvmatting_study.so)
         _lib.set_option("pair_strip_abl", a.abl)
     rs = np.random.RandomState(0)

@@ -3689,6 +3689,11 @@ extern "C" int vm_set_option(const char* key, long value) {
     g_patch_repi = value;
     return VM_OK;
   }
+  if (!strcmp(key, "pair_strip_pin")) {
+    if (value < 0 || value > 1) return fail(VM_EINVAL, "pair_strip_pin must be 0 or 1");
+    vm::g_pair_strip_pin = value;
+    return VM_OK;
+  }
   if (!strcmp(key, "pair_strip")) {
     if (value < 0 || value > 1) return fail(VM_EINVAL, "pair_strip must be 0 or 1");
     g_pair_strip = value;

@@ -167,6 +167,6 @@ int launch_rows(ConvArgs& a, hipStream_t st, int cfg);
 // launchers defined in conv_pair.hip
 bool pair_strip_ok(const ConvArgs& a);
 int launch_pair_strip(ConvArgs& a, long nimg, hipStream_t st);
-extern long g_pair_strip_abl;
+extern long g_pair_strip_abl, g_pair_strip_pin;
 
 }  // namespace vm

@@ -47,7 +47,7 @@ struct StripCfg {
 // XIN: 0 = bf16 frame of 8-channel pixels, 2 = f32 frame with x_c <= 8 channels (cstride <= 8)
 // ACT: the epilogue's activation as a compile-time constant (a runtime switch per element made hipcc emit a branch
 // tree per value, and this kernel is issue-bound, not MFMA-bound)
-template <int XIN, int ACT, int ABL = 0>
+template <int XIN, int ACT, int ABL = 0, int PIN = 1>
 __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2)))
 void conv3x3_pair_strip(ConvArgs a, int seg, int nseg, int nstrip) {
   using C = StripCfg;
@@ -167,46 +167,33 @@ void conv3x3_pair_strip(ConvArgs a, int seg, int nseg, int nstrip) {
       const int tap = min(4 * j + ql, 8), dh = tap / 3, dw = tap - 3 * dh;
       ib[j] = C::I_OFF + (((jr - 1 + dh) & 7) * C::IW + cl + dw) * 16;
     }
-    // every ring column inside the frame (a uniform test): no per-element masking
-    const bool interior = rin && c0 >= 1 && c0 + C::SW < W;
+    // branch-free (one basic block with conv1_2's loop, so the two can interleave): rows outside the frame read the
+    // input ring's zero rows and are masked to zero like columns outside it
 #pragma unroll
     for (int fr = 0; fr < C::RC / 16; ++fr) {
       const int rc = fr * 16 + cl;  // ring column: strip column rc - 1
       f32x4 acc1[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
-      if (rin) {
 #pragma unroll
-        for (int j = 0; j < 3; ++j) {
-          // unconditional: taps 9..11 (K-step 2, q > 0) read tap 8's pixel, whose finite values meet zero weights
-          // (the products are zeros, as with a zero operand)
-          const uint4 bv = *reinterpret_cast<const uint4*>(smem + ib[j] + fr * 256);
+      for (int j = 0; j < 3; ++j) {
+        // unconditional: taps 9..11 (K-step 2, q > 0) read tap 8's pixel, whose finite values meet zero weights
+        // (the products are zeros, as with a zero operand)
+        const uint4 bv = *reinterpret_cast<const uint4*>(smem + ib[j] + fr * 256);
 #pragma unroll
-          for (int f = 0; f < 2; ++f) {
-            if constexpr (ABL & 1) asm volatile("" ::"v"(bv.x), "v"(w1f[j][f].x));
-            else mma16<T>(w1f[j][f], bv, acc1[f]);
-          }
+        for (int f = 0; f < 2; ++f) {
+          if constexpr (ABL & 1) asm volatile("" ::"v"(bv.x), "v"(w1f[j][f].x));
+          else mma16<T>(w1f[j][f], bv, acc1[f]);
         }
       }
+      const int cc = c0 - 1 + rc;
+      const bool inside = rin && (unsigned)cc < (unsigned)W;
       uint2 pk[2];
-      if (interior) {
 #pragma unroll
-        for (int f = 0; f < 2; ++f) {
-          float v[4];
+      for (int f = 0; f < 2; ++f) {
+        float v[4];
 #pragma unroll
-          for (int jj = 0; jj < 4; ++jj) v[jj] = fmaxf(acc1[f][jj] + b1[f][jj], 0.f);
-          pk[f].x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-          pk[f].y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-        }
-      } else {
-        const int cc = c0 - 1 + rc;
-        const bool inside = rin && (unsigned)cc < (unsigned)W;
-#pragma unroll
-        for (int f = 0; f < 2; ++f) {
-          float v[4];
-#pragma unroll
-          for (int jj = 0; jj < 4; ++jj) v[jj] = inside ? fmaxf(acc1[f][jj] + b1[f][jj], 0.f) : 0.f;
-          pk[f].x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-          pk[f].y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-        }
+        for (int jj = 0; jj < 4; ++jj) v[jj] = inside ? fmaxf(acc1[f][jj] + b1[f][jj], 0.f) : 0.f;
+        pk[f].x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+        pk[f].y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
       }
       // swz2(16 fr + cl, c) = 1024 fr + swz2(cl, c): ((16 fr + cl) >> 1) & 3 == (cl >> 1) & 3
       const uint4 ck = chunk_pair(pk[0], pk[1]);
@@ -281,11 +268,13 @@ void conv3x3_pair_strip(ConvArgs a, int seg, int nseg, int nstrip) {
         }
     }
     // pin the order: step s+1's 2 reads ahead of step s's 4 MFMAs
-    __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+    if constexpr (PIN) {
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
 #pragma unroll
-    for (int s = 0; s < 18; ++s) {
-      if (s + 1 < 18) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-      __builtin_amdgcn_sched_group_barrier(0x8, 4, 0);
+      for (int s = 0; s < 18; ++s) {
+        if (s + 1 < 18) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+        __builtin_amdgcn_sched_group_barrier(0x8, 4, 0);
+      }
     }
 
     if constexpr ((ABL & 16) != 0) {
@@ -427,7 +416,7 @@ void conv3x3_pair_strip(ConvArgs a, int seg, int nseg, int nstrip) {
       if constexpr (!(ABL & 8)) dma_row(r + 5, r & 1);
       nst = (a.y_skip ? 0 : 2) + (a.py && ((r & 1) || r + 1 == H) ? 2 : 0);
     }
-    if (r + 2 <= s1) conv1(r + 2);
+    conv1(r + 2);  // (row s1 + 1 at a segment's last row: computed into a ring slot nothing reads)
     conv2(r);
     if (wave == 0) {  // nst is 0, 2 or 4
       if ((ABL & 8) || nst == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -453,14 +442,19 @@ bool pair_strip_ok(const ConvArgs& a) {
 long g_pair_strip_abl = 0;  // study build: timing-only ablations (1 no conv1_1 MFMAs, 2 no conv1_2 MFMAs, 4 no row
                             // barrier, 8 no input DMA, 16 no conv1_2 epilogue; garbage results)
 
-template <int ACT, int ABL>
+long g_pair_strip_pin = 1;  // 1: conv1_2's LDS reads pinned 2 ahead of its MFMAs; 0: left to the scheduler (A/B)
+
+template <int ACT, int ABL, int PIN = 1>
 static void launch_strip_act(ConvArgs& a, long grid, int seg, int nseg, int nstrip, hipStream_t st) {
+  if constexpr (PIN) {
+    if (!g_pair_strip_pin) return launch_strip_act<ACT, ABL, 0>(a, grid, seg, nseg, nstrip, st);
+  }
   if (a.x_f32)
-    hipLaunchKernelGGL((conv3x3_pair_strip<2, ACT, ABL>), dim3((unsigned)grid), dim3(128), StripCfg::LDS, st, a, seg, nseg,
-                       nstrip);
+    hipLaunchKernelGGL((conv3x3_pair_strip<2, ACT, ABL, PIN>), dim3((unsigned)grid), dim3(128), StripCfg::LDS, st, a, seg,
+                       nseg, nstrip);
   else
-    hipLaunchKernelGGL((conv3x3_pair_strip<0, ACT, ABL>), dim3((unsigned)grid), dim3(128), StripCfg::LDS, st, a, seg, nseg,
-                       nstrip);
+    hipLaunchKernelGGL((conv3x3_pair_strip<0, ACT, ABL, PIN>), dim3((unsigned)grid), dim3(128), StripCfg::LDS, st, a, seg,
+                       nseg, nstrip);
 }
 template <int ABL>
 static void launch_strip_abl(ConvArgs& a, long grid, int seg, int nseg, int nstrip, hipStream_t st) {
