@@ -663,6 +663,57 @@ def test_conv_pair_first_head_partials(shape, store_y):
     assert float((a_split - a_full).abs().max()) < 1e-5
 
 
+PERSIST_CASES = [(1, 68, 120, 128, 64, "relu", True), (2, 37, 45, 64, 128, "relu", True),
+                 (1, 135, 240, 256, 128, "none", False), (1, 17, 30, 512, 512, "relu", False),
+                 (3, 9, 70, 32, 64, "sigmoid", True), (1, 540, 960, 64, 128, "relu", True),
+                 (1, 4, 16, 64, 64, "relu", True), (1, 33, 97, 96, 192, "relu", False)]
+
+
+@pytest.mark.parametrize("case", PERSIST_CASES)
+def test_patch_persist_bit_identical(case):
+    """The persistent row-slot patch kernel (vm_set_option patch_persist 1: resident grid, tile loop inside the
+    kernel, the DMA stream running across tiles) writes exactly the streaming kernel's outputs: conv + bias + act
+    (+ fused pool) into a channel slice of a wider buffer, and the folded 2x upconv, with and without the head split."""
+    from vmatting import _lib, ops
+    n, h, w, cin, cout, act, pool = case
+    rs = np.random.RandomState(h * w + cin)
+    x = torch.from_numpy(rs.normal(size=(n, h, w, cin)).astype(np.float32)).to(torch.bfloat16).to(DEV)
+    wt = (rs.normal(size=(3, 3, cin, cout)) * np.sqrt(2.0 / (9 * cin))).astype(np.float32)
+    pc = ops.PackedConv(wt, (rs.normal(size=cout) * 0.1).astype(np.float32), torch.bfloat16, DEV)
+    res, names = [], []
+    try:
+        _lib.set_option("persist_rounds", 0)  # (any grid: the small cases take the persistent kernel too)
+        _lib.set_option("persist_up_rounds", 0)
+        for persist in (0, 1):
+            _lib.set_option("patch_persist", persist)
+            cat = torch.full((n, h, w, cout + 32), 7.0, dtype=torch.bfloat16, device=DEV)
+            po = torch.full((n, (h + 1) // 2, (w + 1) // 2, cout), 5.0, dtype=torch.bfloat16, device=DEV) if pool else None
+            ops.conv3x3(x, pc, act, out=cat[..., 16:16 + cout], pool_out=po)
+            names.append(_lib.last_conv_kernel())
+            outs = [cat, po]
+            if cout == 64 or cout == 128:
+                up = ops.upconv3x3(x, pc, "relu")
+                names.append(_lib.last_conv_kernel())
+                outs.append(up)
+            if cout == 64:
+                whd = T((rs.normal(size=(3, 3, 128, 1)) * 0.05).astype(np.float32)) if persist == 0 else whd
+                y = torch.full((n, 2 * h, 2 * w, 64), 7.0, dtype=torch.bfloat16, device=DEV)
+                part = torch.full((n, 2 * h, 2 * w, 12), 3.0, dtype=torch.float32, device=DEV)
+                assert ops.upconv3x3_head(x, pc, whd, 64, part, "relu", out=y, store_y=True) is not None
+                outs += [y, part]
+            res.append(outs)
+    finally:
+        _lib.set_option("patch_persist", 1)
+        _lib.set_option("persist_rounds", 2)
+        _lib.set_option("persist_up_rounds", 6)
+    for a, b in zip(res[0], res[1]):
+        if a is not None:
+            assert torch.equal(a, b)
+    assert all("persist" not in nm for nm in names[:len(names) // 2]), names
+    if n * h * w >= 8 * 8 * 32 * 2:  # enough pixel tiles for the resident grid (frames not packed): persistent
+        assert "conv3x3_patch_persist" in names[len(names) // 2], names
+
+
 @pytest.mark.parametrize("shape", [(1, 17, 23), (2, 8, 16), (1, 68, 120), (1, 540, 960)])
 @pytest.mark.parametrize("store_y", [False, True])
 def test_up2x_head_partials(shape, store_y):

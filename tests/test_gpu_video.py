@@ -104,8 +104,12 @@ def _world2_worker(rank, world, port, q, n_frames, h, w, chunk):
         ok_w = all(float(s[0]) == float(sums[0][0]) for s in sums) and float(sums[1][1]) != float(sums[0][1])
         ok_shape = tuple(got.shape) == (n_frames, h, w, 1)
         allf = video.synthetic_frames(n_frames, h, w, first=0, device="cuda:0")
-        bad = [i for i in range(n_frames)
-               if not torch.equal(model.forward(allf[i:i + 1].clone())[0], got[i])]
+        bad = []
+        for i in range(n_frames):
+            ref = model.forward(allf[i:i + 1].clone())[0]
+            if not torch.equal(ref, got[i]):  # (frame, max |diff|, differing pixels, first one) for the report
+                d = (ref.float() - got[i].float()).abs()
+                bad.append((i, float(d.max()), int((d > 0).sum()), tuple(int(v) for v in (d > 0).nonzero()[0])))
         q.put((rank, ok_w, ok_shape, bad, len(vm.spans)))
     except Exception as e:  # report instead of hanging the parent
         import traceback

@@ -1317,6 +1317,340 @@ void conv3x3_patch(ConvArgs a) {
   }
 }
 
+// ================================================================ persistent row-slot patch kernel
+// The G = 3 patch pipeline above with the tile loop inside the kernel (vm_set_option "patch_persist"): a resident
+// grid of 8 x J blocks; block b lives on XCD b % 8 and walks the (pixel tile, 64-channel output tile) items of its
+// XCD's band of pixel tiles [lo, hi): round `it` hands walker j the item it*J + j, so the walkers of a round cover
+// all output tiles of adjacent pixel tiles (the input patch is fetched from HBM about once per XCD) and, J being a
+// multiple of the output tile count, each walker keeps one output tile.  A folded upconv's phases run 9 / 6 / 6 / 4
+// taps, so there (ConvArgs::prot) walker j takes item it*J + (j + it) % J instead and cycles through the phases:
+// a fixed phase per walker leaves the 9-tap walkers as the tail.  The DMA stream (input granules, weight row slots) runs on
+// across tile boundaries: the next item's first granule and weight rows are issued during the current one's last
+// steps and land while it finishes its MFMAs and its register epilogue, so an item pays no prologue latency.  The
+// per-channel affine of every output channel and the head filter fragments are staged in LDS once per block (the
+// epilogue then has no global load, whose vmcnt wait would drain the prefetch).  Every output pixel keeps the
+// non-persistent kernel's MFMA sequence and epilogue arithmetic: results are bit-identical.
+template <int BN, int WM, int WN, int S, int TH, int MINB, bool UPSKIP>
+__global__ __launch_bounds__(64 * WM * WN)
+__attribute__((amdgpu_waves_per_eu(MINB * WM * WN < 16 ? 4 : MINB * WM * WN / 4)))  // <= 128 VGPRs
+void conv3x3_patch_persist(ConvArgs a) {
+  using C = PatchCfg<BN, WM, WN, S, TH, 3>;
+  using T = uint16_t;
+  static_assert(BN == 64 && WN == 1 && C::REPI_OK && C::FC == 4, "64-channel output tiles");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int NW = C::NW, NT = C::NT, FP = C::FP, FC = C::FC, XPW = C::XPW, WPW = C::WPW, R = 3, G = 3;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave;
+  const int H = a.H, W = a.W, cs = a.x_cstride;
+  const int th = (H + C::TH - 1) / C::TH, tw = (W + C::TW - 1) / C::TW;
+  const int tn = a.tiles_n, sp = a.tiles_total / tn, CT = tn * BN;
+  const int xcd = blockIdx.x & 7, jw = blockIdx.x >> 3, J = (int)(gridDim.x >> 3);
+  const int lo = (int)((long)xcd * sp / 8), hi = (int)((long)(xcd + 1) * sp / 8);
+  const int nitem = (hi - lo) * tn;
+  int it = 0, q = jw;
+  if (q >= nitem) return;  // (before any barrier: the block has no work)
+
+  // per-block constants in LDS: mul[CT], add[CT] (f32, output channel order), then the head A fragments [lane][2]
+  char* kc = smem + C::MAIN;
+  const int ccap = a.up ? a.up_cout : a.cout;
+  for (int c = tid; c < CT; c += NT) {
+    const int chb = c & ~31;  // (the register epilogue's 32-channel group base and phase)
+    const int cb = chb - (a.up ? chb / a.up_cout : 0) * a.up_cout;
+    const int co = min(cb + (c & 31), ccap - 1);
+    const float sc = a.scale ? a.scale[co] : 1.f;
+    reinterpret_cast<float*>(kc)[c] = sc;
+    reinterpret_cast<float*>(kc)[CT + c] = (a.bias ? a.bias[co] : 0.f) * sc + (a.shift ? a.shift[co] : 0.f);
+  }
+  char* kh = kc + CT * 8;
+  const int col = lane & 15, ckq = lane >> 4;
+  if (a.hd && tid < 64) {
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      float hv[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int hc = (2 * kk + j / 4) * 16 + 4 * ckq + j % 4;
+        hv[j] = col < 9 ? a.hw[col * a.hw_cin + a.hw_coff + hc] : 0.f;
+      }
+      *reinterpret_cast<uint4*>(kh + (lane * 2 + kk) * 16) =
+          make_uint4((uint32_t)f2bf(hv[0]) | ((uint32_t)f2bf(hv[1]) << 16),
+                     (uint32_t)f2bf(hv[2]) | ((uint32_t)f2bf(hv[3]) << 16),
+                     (uint32_t)f2bf(hv[4]) | ((uint32_t)f2bf(hv[5]) << 16),
+                     (uint32_t)f2bf(hv[6]) | ((uint32_t)f2bf(hv[7]) << 16));
+    }
+  }
+  __syncthreads();
+
+  const __amdgpu_buffer_rsrc_t wrs = w_rsrc<T>(a, 0);  // (item weights at n0 * K_pad * 2 bytes: host-checked)
+  const int lrow = lane >> 2, lpos = lane & 3;
+  int woff[WPW];
+  int w_n = 0;
+#pragma unroll
+  for (int i = 0; i < WPW; ++i) {
+    const int piece = wave + i * NW;
+    const int row = piece * 16 + lrow;
+    const int lq = (swz<64>(row, lpos) - row * 64) >> 4;
+    woff[i] = (row * a.K_pad + lq * 8) * 2;
+    if (piece < C::WP) ++w_n;
+  }
+  int x_n = 0;
+#pragma unroll
+  for (int i = 0; i < XPW; ++i)
+    if (wave + i * NW < C::XP) ++x_n;
+
+  // input DMA state of the tile whose granules are being fetched (switches to the next tile at the last granule)
+  __amdgpu_buffer_rsrc_t xrs;
+  int xoff[XPW];
+  auto set_xtile = [&](int s) {
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    const int lrow = ln >> 2, lpos = ln & 3;
+    const int n = s / (th * tw), srem = s - n * th * tw;
+    const int r0 = (srem / tw) * C::TH, c0 = (srem - (srem / tw) * tw) * C::TW;
+    const T* xb = reinterpret_cast<const T*>(a.x) + a.x_coff + ((long)n * H + r0 - 1) * (long)W * cs;
+    xrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<T*>(xb), 0, 0x7ffffff0, 0x00020000);
+#pragma unroll
+    for (int i = 0; i < XPW; ++i) {
+      const int row = (wave + i * NW) * 16 + lrow;
+      const int lq = (swz<64>(row, lpos) - row * 64) >> 4;
+      const int pr = row / C::PW, pc = row - pr * C::PW;
+      int h = r0 - 1 + pr, w = c0 - 1 + pc;
+      if (a.up) {  // folded 2x resize: the low-res frame's edge is replicated (as conv3x3_patch)
+        h = min(h, H - 1);
+        w = min(w, W - 1);
+      }
+      const bool ok = row < C::PPIX && (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
+      xoff[i] = ok ? (((h - r0 + 1) * W + w) * cs + lq * 8) * 2 : OOB;
+    }
+  };
+  const int nch = a.cin_pad / 32, nsr = nch * R;
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr(smem));
+  const uint32_t wring = lds0 + 2 * C::PB;
+  auto issue_x = [&](int cc, int buf, bool real) {
+#pragma unroll
+    for (int i = 0; i < XPW; ++i)
+      if (wave + i * NW < C::XP)
+        glds16(xrs, lds0 + buf * C::PB + (wave + i * NW) * 1024, real ? xoff[i] + (int)src_chan(a, cc * 32) * 2 : OOB);
+  };
+  auto issue_w = [&](int s, int slot, bool real, int wb) {  // wb: the item's weight byte offset
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+      for (int i = 0; i < WPW; ++i)
+        if (wave + i * NW < C::WP)
+          glds16(wrs, wring + (slot * G + g) * C::WSLOT + (wave + i * NW) * 1024,
+                 real ? woff[i] + wb + (s * G + g) * 64 : OOB);
+  };
+
+  int boff[FC], abase[FP];
+#pragma unroll
+  for (int f = 0; f < FC; ++f) boff[f] = 2 * C::PB + swz<64>(f * 16 + (lane & 15), lane >> 4);
+#pragma unroll
+  for (int f = 0; f < FP; ++f) abase[f] = C::prow(wm, f) * C::PW + C::pcol(wm, f) + (lane & 15);
+  const int ck = lane >> 4;
+  auto frags = [&](uint4 (&av)[FC], uint4 (&bv)[FP], int slot, int buf, int tap) {
+    const char* wp = smem + (slot * G + tap % G) * C::WSLOT;
+    const char* xp = smem + buf * C::PB;
+#pragma unroll
+    for (int f = 0; f < FC; ++f) av[f] = *reinterpret_cast<const uint4*>(wp + boff[f]);
+    const int toff = (tap / 3) * C::PW + tap % 3;
+#pragma unroll
+    for (int f = 0; f < FP; ++f) bv[f] = *reinterpret_cast<const uint4*>(xp + swz<64>(abase[f] + toff, ck));
+  };
+  auto sync = [&](int n) {
+    wait_vm(n);
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+
+  // stores of one epilogue (counted into the first waits of the next tile: they are younger than the weight rows
+  // issued before it); the head's conditional stores are not counted (waiting longer is safe)
+  int e_st = 2 * FP;
+  if (a.py) {
+#pragma unroll
+    for (int fp = 0; fp < FP; ++fp) e_st += (C::prow(wm, fp) & 1) ? 0 : 2;
+  }
+
+  const int ycs2 = a.y_cstride * 2;
+  const int YW = a.up ? 2 * W : W;
+  const int PH = (H + 1) >> 1, PWo = (W + 1) >> 1;
+  auto epilogue = [&](const f32x4 (&acc)[FC][FP], int s, int n0) {
+    // lane-derived values from an opaque copy of the lane id: recomputed per tile instead of held across the loop
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    const int col = ln & 15, ckq = ln >> 4;
+    const int n = s / (th * tw), srem = s - n * th * tw;
+    const int r0 = (srem / tw) * C::TH, c0 = (srem - (srem / tw) * tw) * C::TW;
+    T* yb = reinterpret_cast<T*>(a.y) + a.y_coff +
+            (a.up ? (((long)n * 2 * H + 2 * r0) * YW + 2 * c0) : (((long)n * H + r0) * W + c0)) * (long)a.y_cstride;
+    const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(yb, 0, 0x7ffffff0, 0x00020000);
+    const int c16 = (ckq & 1) ? 2 + (ckq >> 1) : ckq >> 1;
+    T* pb = a.py ? reinterpret_cast<T*>(a.py) + a.py_coff +
+                       (((long)n * PH + (r0 >> 1)) * PWo + (c0 >> 1)) * (long)a.py_cstride + n0
+                 : nullptr;
+    const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(pb, 0, 0x7ffffff0, 0x00020000);
+    f32x4 dh[FP];  // head split: conv1_5's per-tap partials, accumulated over the two 32-channel groups
+#pragma unroll
+    for (int fp = 0; fp < FP; ++fp) dh[fp] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int g2 = 0; g2 < FC / 2; ++g2) {
+      const int chb = n0 + g2 * 32;
+      const int phase = a.up ? chb / a.up_cout : 0;
+      const int cb = chb - phase * a.up_cout;
+      float v[FP][2][4];
+#pragma unroll
+      for (int f = 0; f < 2; ++f) {
+        const float4 m4 = *reinterpret_cast<const float4*>(kc + (n0 + (2 * g2 + f) * 16 + 4 * ckq) * 4);
+        const float4 a4 = *reinterpret_cast<const float4*>(kc + (CT + n0 + (2 * g2 + f) * 16 + 4 * ckq) * 4);
+        const float mul[4] = {m4.x, m4.y, m4.z, m4.w}, add[4] = {a4.x, a4.y, a4.z, a4.w};
+#pragma unroll
+        for (int fp = 0; fp < FP; ++fp)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            float t = fmaf(acc[2 * g2 + f][fp][j], mul[j], add[j]);
+            if (a.act == VM_ACT_RELU) t = fmaxf(t, 0.f);
+            else if (a.act == VM_ACT_SIGMOID) t = sigmoid_precise(t);
+            v[fp][f][j] = t;
+          }
+      }
+#pragma unroll
+      for (int fp = 0; fp < FP; ++fp) {
+        uint2 pk[2];
+#pragma unroll
+        for (int f = 0; f < 2; ++f) {
+          pk[f].x = (uint32_t)f2bf(v[fp][f][0]) | ((uint32_t)f2bf(v[fp][f][1]) << 16);
+          pk[f].y = (uint32_t)f2bf(v[fp][f][2]) | ((uint32_t)f2bf(v[fp][f][3]) << 16);
+        }
+        if (a.hd)  // (the same two MFMAs, in the same order, as the register epilogue's head split)
+          mma16<T>(*reinterpret_cast<const uint4*>(kh + (ln * 2 + g2) * 16),
+                   make_uint4(pk[0].x, pk[0].y, pk[1].x, pk[1].y), dh[fp]);
+        const uint4 d = chunk_pair(pk[0], pk[1]);
+        const int tr = C::prow(wm, fp), tc = C::pcol(wm, fp) + col;
+        const bool ok = r0 + tr < H && c0 + tc < W && cb + c16 * 8 < ccap && !a.y_skip;
+        const int pix = a.up ? (2 * tr + (phase >> 1)) * YW + 2 * tc + (phase & 1) : tr * W + tc;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, d), yrs,
+                                               ok ? pix * ycs2 + (cb + c16 * 8) * 2 : OOB, 0, 0);
+      }
+      if (a.py) {
+#pragma unroll
+        for (int fp = 0; fp < FP; ++fp) {
+          if (C::prow(wm, fp) & 1) continue;
+          const int tr = C::prow(wm, fp), tc = C::pcol(wm, fp) + col;
+          const bool v0 = r0 + tr < H && c0 + tc < W, v1 = r0 + tr + 1 < H && c0 + tc < W;
+          float m[2][4];
+#pragma unroll
+          for (int f = 0; f < 2; ++f)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              float t = v0 ? v[fp][f][j] : -INFINITY;
+              if (v1) t = fmaxf(t, v[fp + C::PSTEP][f][j]);
+              const float u = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(t), 0xB1, 0xF, 0xF, false));
+              m[f][j] = fmaxf(t, u);
+            }
+          uint2 q2[2];
+#pragma unroll
+          for (int f = 0; f < 2; ++f) {
+            q2[f].x = (uint32_t)f2bf(m[f][0]) | ((uint32_t)f2bf(m[f][1]) << 16);
+            q2[f].y = (uint32_t)f2bf(m[f][2]) | ((uint32_t)f2bf(m[f][3]) << 16);
+          }
+          const uint4 d = chunk_pair(q2[0], q2[1]);
+          const int pr = tr >> 1, pc = tc >> 1;
+          const int chl = g2 * 32 + c16 * 8;
+          const bool pok = (col & 1) == 0 && v0 && (r0 >> 1) + pr < PH && (c0 >> 1) + pc < PWo && n0 + chl < a.cout;
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, d),
+                                                 prs, pok ? ((pr * PWo + pc) * a.py_cstride + chl) * 2 : OOB, 0, 0);
+        }
+      }
+    }
+    if (a.hd) {
+      const int phase = a.up ? n0 / a.up_cout : 0;
+      const int YH = a.up ? 2 * H : H;
+#pragma unroll
+      for (int fp = 0; fp < FP; ++fp) {
+        const f32x4 d = dh[fp];
+        const int tr = C::prow(wm, fp), tc = C::pcol(wm, fp) + col;
+        if (ckq < 3 && r0 + tr < H && c0 + tc < W) {
+          const int yy = a.up ? 2 * (r0 + tr) + (phase >> 1) : r0 + tr;
+          const int xx = a.up ? 2 * (c0 + tc) + (phase & 1) : c0 + tc;
+          *reinterpret_cast<f32x4*>(a.hd + (((long)n * YH + yy) * YW + xx) * 12 + 4 * ckq) = d;
+        }
+      }
+    }
+  };
+
+  const int wstep = a.K_pad * 2 * BN;  // weight bytes of one output tile
+  int st = lo + q / tn, n0 = (q % tn) * BN;
+  set_xtile(st);
+  int gcnt = 0;  // granules issued so far (input buffer parity)
+  issue_x(0, 0, true);
+#pragma unroll
+  for (int j = 0; j < S - 1; ++j) issue_w(j, j, j < nsr, (q % tn) * wstep);
+  int slot = 0;
+  bool first = true;
+  for (;;) {
+    const int qn = (it + 1) * J + (a.prot ? (jw + it + 1) % J : jw);
+    const bool more = qn < nitem;
+    const int stn = lo + qn / tn, wbn = more ? (qn % tn) * wstep : 0, wb = (n0 / BN) * wstep;
+    const int up_phase = UPSKIP && a.up && n0 / a.up_cout == (n0 + BN - 1) / a.up_cout ? n0 / a.up_cout : 0;
+    const bool skip_r0 = (up_phase >> 1) != 0, skip_c0 = (up_phase & 1) != 0;
+    f32x4 acc[FC][FP];
+#pragma unroll
+    for (int i = 0; i < FC; ++i)
+#pragma unroll
+      for (int j = 0; j < FP; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int cc = 0; cc < nch; ++cc) {
+      const int buf = gcnt & 1;
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int k = cc * R + r;
+        int nw = (S - 2) * G * w_n + ((r >= 1 && r <= S - 2) ? x_n : 0);
+        if (!first && k < S - 1) nw += e_st;
+        sync(nw);
+        if (r == 0) {
+          if (cc + 1 < nch) {
+            issue_x(cc + 1, buf ^ 1, true);
+          } else {  // the next item's first granule (a dummy past the walk's end)
+            if (more && stn != st) set_xtile(stn);
+            issue_x(0, buf ^ 1, more);
+          }
+        }
+        int ws = k + S - 1;
+        if (ws < nsr) {
+          issue_w(ws, slot + S - 1 - (slot + S - 1 >= S ? S : 0), true, wb);
+        } else {
+          issue_w(ws - nsr, slot + S - 1 - (slot + S - 1 >= S ? S : 0), more, wbn);
+        }
+        if (!(UPSKIP && skip_r0 && r == 0)) {
+          uint4 av[2][FC], bv[2][FP];
+          frags(av[0], bv[0], slot, buf, r * G);
+#pragma unroll
+          for (int g = 0; g < G; ++g) {
+            if (g + 1 < G) frags(av[(g + 1) & 1], bv[(g + 1) & 1], slot, buf, r * G + g + 1);
+            if (!(UPSKIP && skip_c0 && g == 0)) {
+#pragma unroll
+              for (int fc = 0; fc < FC; ++fc)
+#pragma unroll
+                for (int fp = 0; fp < FP; ++fp) mma16<T>(av[g & 1][fc], bv[g & 1][fp], acc[fc][fp]);
+            }
+          }
+        }
+        slot = slot + 1 == S ? 0 : slot + 1;
+      }
+      ++gcnt;
+    }
+    epilogue(acc, st, n0);
+    if (!more) break;
+    ++it;
+    q = qn;
+    st = stn;
+    n0 = (qn % tn) * BN;
+    first = false;
+  }
+}
+
 // ================================================================ persistent first pair (conv1_1 -> conv1_2 [-> pool1])
 // unet.py:170-172 at full resolution.  conv1_2 has only 2 channel granules (18 K-steps), so in the streaming patch
 // kernel the per-tile fixed costs (input latency, the first conv, the epilogue) dominate.  Here ONE 512-thread block
@@ -3185,6 +3519,59 @@ static int launch_patch(ConvArgs& a, hipStream_t st) {
 
 static long g_up_skip = 1;  // vm_set_option "up_skip": 0 runs the folded upconvs without the zero-tap skipping (A/B)
 
+// persistent row-slot patch kernel (conv3x3_patch_persist): a resident grid of 8 XCD bands x J walkers, on grids of
+// >= g_persist_rounds full rounds of items (a shorter walk gains no prologue overlap and its last round is ragged);
+// the callers check persist_ok, then persist_launch returns 1 when the grid is too small (the caller falls back)
+static long g_patch_persist = 1;
+static long g_persist_rounds = 2;
+static long g_persist_up_rounds = 6;
+static bool persist_ok(const ConvArgs& a) {
+  return g_patch_persist && g_patch_repi && a.ksplit <= 1 && !a.vstride && a.y_dtype == VM_BF16 &&
+         (!a.up || a.up_cout % 32 == 0) && (long)a.cout_pad * a.K_pad * 2 < 0x7fff0000L;
+}
+template <int BN, int WM, int WN, int S, int TH, int MINB, bool UPSKIP>
+static int launch_patch_persist(ConvArgs& a, hipStream_t st) {
+  using C = PatchCfg<BN, WM, WN, S, TH, 3>;
+  const int tn = (a.cout + BN - 1) / BN;
+  const int lds = C::MAIN + tn * BN * 8 + 2048;  // + per-channel affine of every output tile + head fragments
+  constexpr int lds_max = 160 * 1024 / (160 * 1024 / C::MAIN);  // as many blocks per CU as the streaming kernel
+  if (lds > lds_max) return 1;
+  const void* fn = reinterpret_cast<const void*>(&conv3x3_patch_persist<BN, WM, WN, S, TH, MINB, UPSKIP>);
+  static int dev_seen = -1, per_cu = 0, n_cu = 0;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (dev != dev_seen) {
+    hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max);
+    if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, C::NT, lds_max);
+    if (e == hipSuccess) e = hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
+    if (e != hipSuccess) return fail(VM_EHIP, "conv3x3_patch_persist: %s", hipGetErrorString(e));
+    dev_seen = dev;
+  }
+  const long N = a.M / ((long)a.H * a.W);
+  const long sp = N * ((a.H + C::TH - 1) / C::TH) * ((a.W + C::TW - 1) / C::TW);
+  const long resident = (long)per_cu * n_cu;
+  // where it pays (same-box A/B per layer of the 1080p forward, 2 blocks per CU = 512 resident): a folded upconv
+  // (phases of 9 / 6 / 6 / 4 taps, rotated over the walkers) needs >= g_persist_up_rounds rounds of items to even
+  // out (upconv_3 / upconv_4, 8 / 16 rounds: -3 % / -18 %; upconv_2, 4 rounds: +13 %); a plain conv gains on grids of
+  // 2..3 rounds (conv4_x, conv5 of 1024 / 512 channels: -2..-3 %) and on the 2-granule K loop (conv2_1: -9 %), and
+  // loses a little on 4..8 rounds of 4..8 granules (conv2_2, conv3_2, conv3_3: +2..+3 %)
+  const long items = sp * tn;
+  bool use;
+  if (a.up) use = items >= g_persist_up_rounds * resident;
+  else use = items >= g_persist_rounds * resident && (items < 3 * resident || a.cin_pad <= 64 || g_persist_rounds == 0);
+  if (sp < 8 || resident < 8 || !use || items > 0x7fffffffL) return 1;
+  a.tiles_n = tn;
+  a.prot = a.up ? 1 : 0;
+  a.repi = 1;
+  a.tiles_total = (int)(sp * tn);
+  const long J = resident / 8;  // walkers per XCD band (every band has >= 2 rounds of items)
+  snprintf(g_last_kernel, sizeof g_last_kernel, "vm::conv3x3_patch_persist<%d, %d, %d, %d, %d, %d, %s>", BN, WM, WN, S,
+           TH, MINB, UPSKIP ? "true" : "false");
+  hipLaunchKernelGGL((conv3x3_patch_persist<BN, WM, WN, S, TH, MINB, UPSKIP>), dim3((unsigned)(8 * J)), dim3(C::NT), lds,
+                     st, a);
+  return check_launch("conv3x3_patch_persist");
+}
+
 // a shipped tiling: the folded-upconv instantiation (zero phase taps skipped, row-slot pipeline G = 3) for a.up,
 // else the plain one
 template <int BN, int WM, int WN, int S, int TH = 8, int MINB = 1, int UNR = 9, bool PF = false, int ABL = 0,
@@ -3437,6 +3824,15 @@ static int dispatch_patch(ConvArgs& a, hipStream_t st) {
   // (a folded upconv takes the row-slot configs below, whose instantiation skips its phases' zero taps)
   if (!(a.up && g_up_skip) && a.cout >= 128 && a.cin_pad >= 512 && sp * ((a.cout + 127) / 128) >= 1000)
     return launch_patch_up<128, 4, 2, 3, 8, 2>(a, st);  // 64 px x 64 channel waves, 4 per SIMD (r02: -5% vs 4x1)
+  if (persist_ok(a)) {  // the same tilings, persistent (2-slot ring: the LDS also holds the block's constants)
+    const bool sk = a.up && g_up_skip;
+    int rc = 1;
+    if (blocks64 >= 512)
+      rc = sk ? launch_patch_persist<64, 8, 1, 2, 8, 1, true>(a, st) : launch_patch_persist<64, 8, 1, 2, 8, 1, false>(a, st);
+    else
+      rc = sk ? launch_patch_persist<64, 4, 1, 2, 4, 2, true>(a, st) : launch_patch_persist<64, 4, 1, 2, 4, 2, false>(a, st);
+    if (rc != 1) return rc;
+  }
   if (blocks64 >= 8000) return launch_patch_up<64, 8, 1, 3, 8, 1, 9, false, 0, false, 3>(a, st);
   if (blocks64 < 512) return launch_patch_up<64, 4, 1, 2, 4, 2, 9, false, 0, false, 3>(a, st);  // L5: 4 x 32 px tiles
   return launch_patch_up<64, 8, 1, 2, 8, 1, 9, false, 0, false, 3>(a, st);
@@ -3687,6 +4083,16 @@ extern "C" int vm_set_option(const char* key, long value) {
   if (!strcmp(key, "patch_repi")) {
     if (value < 0 || value > 1) return fail(VM_EINVAL, "patch_repi must be 0 or 1");
     g_patch_repi = value;
+    return VM_OK;
+  }
+  if (!strcmp(key, "persist_rounds") || !strcmp(key, "persist_up_rounds")) {
+    if (value < 0 || value > 64) return fail(VM_EINVAL, "%s must be in 0..64 (0: any grid)", key);
+    (key[8] == 'u' ? g_persist_up_rounds : g_persist_rounds) = value;
+    return VM_OK;
+  }
+  if (!strcmp(key, "patch_persist")) {
+    if (value < 0 || value > 1) return fail(VM_EINVAL, "patch_persist must be 0 or 1");
+    g_patch_persist = value;
     return VM_OK;
   }
   if (!strcmp(key, "pair_strip_pin")) {

@@ -46,6 +46,7 @@ struct ConvArgs {
   // (40 or 20 px in 32-px tiles) stop wasting most of their last column tile.
   int vstride, vW;
   int repi;  // patch kernel: 1 = register epilogue where the tiling allows (bf16 output, no split-K, no packed frames)
+  int prot;  // persistent patch kernel: 1 = walkers rotate through the output tiles (folded-upconv phases)
   // strip pair kernel: optional bf16 output of the FIRST conv (conv1_1 + bias + relu), [N,H,W,64] view
   void* y1;
   int y1_cstride, y1_coff;
