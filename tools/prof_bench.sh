@@ -26,7 +26,7 @@ if ! skip fwd; then
 run 300 stats.log rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/stats" -o run \
     -- python3 "$REPO/bench.py" --steps 50 --warmup 5 $FWD "$@"
 cp "$(find "$OUT/stats" -name '*kernel_stats.csv' | head -n 1)" "$REPO/profiles/${TAG}_kernel_stats.csv"
-tail -n 1 "$OUT/stats.log" > "$REPO/profiles/${TAG}_stats_bench.json"
+grep "^{\"metric\"" "$OUT/stats.log" | tail -n 1 > "$REPO/profiles/${TAG}_stats_bench.json"
 fi
 if ! skip mfma; then
 run 300 mfma.log timeout -s KILL 240 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace \
