@@ -3525,6 +3525,8 @@ static long g_up_skip = 1;  // vm_set_option "up_skip": 0 runs the folded upconv
 static long g_patch_persist = 1;
 static long g_persist_rounds = 2;
 static long g_persist_up_rounds = 6;
+static long g_persist_all = 0;  // (A/B) every plain grid of >= persist_rounds rounds
+static long g_persist_rot = 0;  // (A/B) walker rotation: 0 = folded upconvs only, 1 = all, 2 = none
 static bool persist_ok(const ConvArgs& a) {
   return g_patch_persist && g_patch_repi && a.ksplit <= 1 && !a.vstride && a.y_dtype == VM_BF16 &&
          (!a.up || a.up_cout % 32 == 0) && (long)a.cout_pad * a.K_pad * 2 < 0x7fff0000L;
@@ -3558,10 +3560,11 @@ static int launch_patch_persist(ConvArgs& a, hipStream_t st) {
   const long items = sp * tn;
   bool use;
   if (a.up) use = items >= g_persist_up_rounds * resident;
-  else use = items >= g_persist_rounds * resident && (items < 3 * resident || a.cin_pad <= 64 || g_persist_rounds == 0);
+  else use = items >= g_persist_rounds * resident && (items < 3 * resident || a.cin_pad <= 64 || g_persist_rounds == 0 ||
+                                                        g_persist_all);
   if (sp < 8 || resident < 8 || !use || items > 0x7fffffffL) return 1;
   a.tiles_n = tn;
-  a.prot = a.up ? 1 : 0;
+  a.prot = g_persist_rot == 0 ? (a.up ? 1 : 0) : g_persist_rot == 1 ? 1 : 0;
   a.repi = 1;
   a.tiles_total = (int)(sp * tn);
   const long J = resident / 8;  // walkers per XCD band (every band has >= 2 rounds of items)
@@ -3673,9 +3676,9 @@ static long g_patch_rowslot = 1;  // 0 = the per-tap-barrier dispatch of r01 (A/
 static long g_patch_ablate = 0;
 #endif
 static long g_rows_kernel = 1;        // conv_rows.hip: 0 = off, 1 = auto (grid size), 8 / 16 = forced tile height
-static long g_rows_min_blocks = 900;
+static long g_rows_min_blocks = 400;
 static long g_rows_up = 0;            // 1: the folded upconvs too
-static long g_rows_min_cin = 256;      // short K loops: the 2-blocks-per-CU patch kernel hides prologue/epilogue better
+static long g_rows_min_cin = 128;      // shorter K loops: the 2-blocks-per-CU patch kernel hides prologue/epilogue better
 static long g_src_span_limit = 0x7ffffff0L;  // split-source byte span the 32-bit offset kernels take (option
                                               // "src_span_limit" lowers it for the fallback tests)
 static long g_pair_strip = 1;  // vm_conv3x3_pair_first*: 1 = the strip-walking kernel (conv_pair.hip) where it applies
@@ -3796,8 +3799,10 @@ static int dispatch_patch(ConvArgs& a, hipStream_t st) {
     }
     const long N16 = a.M / ((long)a.H * a.W);
     const long blocks16 = N16 * ((a.H + 15) / 16) * ((a.W + 31) / 32) * ((a.cout + 63) / 64);
-    // measured in the 1080p forward (scripts/opt_ab.sh): a win for cin >= 512 (upconv_2, conv3_4) and for cin 256 on
-    // >= 2 x 900 blocks (conv2_3); a loss for the folded upconvs (8-byte phase-scattered stores) and shorter K loops
+    // measured in the 1080p forward (scripts/opt_ab.sh, bench.py --layers --option rows_min_*): a win for cin >= 256
+    // on >= 400 blocks (conv3_4, conv2_3, conv3_2, conv3_3: -3..-4 %) and for cin 128 on >= 800 blocks (conv2_2,
+    // conv3_1: -2..-3 %; r03: whole forward +1.0 % same-box); a loss for the folded upconvs (8-byte phase-scattered
+    // stores), cin 64 (conv2_1: the persistent patch kernel is faster)
     // ... and only where its 16-row tiles waste no more rows than the patch kernel's 8-row ones (the training
     // towers' 40 x 40 level: 48 of 40 rows vs 40, measured 612 vs ~800 TFLOP/s)
     const bool rows_fit = ((a.H + 15) / 16) * 16 <= ((a.H + 7) / 8) * 8 + a.H / 32;
@@ -4088,6 +4093,11 @@ extern "C" int vm_set_option(const char* key, long value) {
   if (!strcmp(key, "persist_rounds") || !strcmp(key, "persist_up_rounds")) {
     if (value < 0 || value > 64) return fail(VM_EINVAL, "%s must be in 0..64 (0: any grid)", key);
     (key[8] == 'u' ? g_persist_up_rounds : g_persist_rounds) = value;
+    return VM_OK;
+  }
+  if (!strcmp(key, "persist_all") || !strcmp(key, "persist_rot")) {
+    if (value < 0 || value > 2) return fail(VM_EINVAL, "%s must be 0, 1 or 2", key);
+    (key[8] == 'a' ? g_persist_all : g_persist_rot) = value;
     return VM_OK;
   }
   if (!strcmp(key, "patch_persist")) {
