@@ -2476,7 +2476,7 @@ __global__ __launch_bounds__(512, 4) void conv3x3_first_softmax_strip(ConvArgs a
 // offsets are staged once per block ([step][lane] records: one ds_read_b128 for the 4 cout fragments + one offset);
 // the next strip's pixels are prefetched into registers.  Softmax + per-wave LDS transpose + whole-pixel nontemporal
 // stores as in conv3x3_first_softmax.
-template <int CIN>
+template <int CIN, int ABL = 0>  // ABL (study builds only, results are garbage): 1 = no softmax / store, 2 = no MFMA
 __global__ __launch_bounds__(512, 4) void conv3x3_first_softmax_f32(ConvArgs a) {
   constexpr int NS = (9 * CIN + 3) / 4;
   constexpr int TH = 8, TW = 32, PW = TW + 2, SP = 3 * PW;  // strip patch: 3 rows x 34 px
@@ -2567,6 +2567,10 @@ __global__ __launch_bounds__(512, 4) void conv3x3_first_softmax_f32(ConvArgs a) 
       const f32x4 w4 = wl[s * 64 + lane];
       const int po = pl[s * 4 + q];
       const float b0 = P[po + col], b1 = P[po + 16 + col];
+      if constexpr (ABL & 2) {
+        asm volatile("" ::"v"(w4[0]), "v"(w4[3]), "v"(b0), "v"(b1));
+        continue;
+      }
 #pragma unroll
       for (int fc = 0; fc < 4; ++fc) {
         acc[fc][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(w4[fc], b0, acc[fc][0], 0, 0, 0);
@@ -2574,6 +2578,11 @@ __global__ __launch_bounds__(512, 4) void conv3x3_first_softmax_f32(ConvArgs a) 
       }
     }
 
+    if constexpr (ABL & 1) {
+#pragma unroll
+      for (int fc = 0; fc < 4; ++fc) asm volatile("" ::"v"(acc[fc][0][0]), "v"(acc[fc][1][3]));
+      continue;
+    }
     float* yb = reinterpret_cast<float*>(a.y) + a.y_coff + (((long)n * H + r) * W + c0) * (long)a.y_cstride;
     if (aff) softmax_store_strip<true>(acc, rmul, stg + wave * 16 * SRF, yb, a.y_cstride, W - c0, lane);
     else softmax_store_strip<false>(acc, rmul, stg + wave * 16 * SRF, yb, a.y_cstride, W - c0, lane);
@@ -3672,6 +3681,7 @@ static long g_head_kernel = 0;
 static long g_head_th = 16;  // conv3x3_head_mfma tile height for the bf16 128-channel head (8 or 16)
 static long g_patch_cfg = 0;
 #ifdef VM_STUDY
+static long g_softmax_abl = 0;  // conv3x3_first_softmax_f32 timing ablations
 static long g_patch_rowslot = 1;  // 0 = the per-tap-barrier dispatch of r01 (A/B runs)
 static long g_patch_ablate = 0;
 #endif
@@ -3930,6 +3940,15 @@ static int launch_first_softmax_f32(ConvArgs& a, int cin, hipStream_t st) {
     snprintf(g_last_kernel, sizeof g_last_kernel, "vm::conv3x3_first_softmax_f32<%d>", C); \
     hipLaunchKernelGGL(conv3x3_first_softmax_f32<C>, dim3(grid), dim3(512), 0, st, a);      \
     break;
+#ifdef VM_STUDY
+  if (cin == 5 && g_softmax_abl) {  // timing ablations of the f32 refine kernel (results are garbage)
+    snprintf(g_last_kernel, sizeof g_last_kernel, "vm::conv3x3_first_softmax_f32<5, %ld>", g_softmax_abl);
+    if (g_softmax_abl == 1) hipLaunchKernelGGL((conv3x3_first_softmax_f32<5, 1>), dim3(grid), dim3(512), 0, st, a);
+    else if (g_softmax_abl == 2) hipLaunchKernelGGL((conv3x3_first_softmax_f32<5, 2>), dim3(grid), dim3(512), 0, st, a);
+    else hipLaunchKernelGGL((conv3x3_first_softmax_f32<5, 3>), dim3(grid), dim3(512), 0, st, a);
+    return check_launch("conv3x3_first_softmax_f32");
+  }
+#endif
   switch (cin) {
     VM_SMF(1) VM_SMF(2) VM_SMF(3) VM_SMF(4) VM_SMF(5) VM_SMF(6) VM_SMF(7) VM_SMF(8)
     default: return fail(VM_EINVAL, "conv3x3_first_softmax_f32: cin %d", cin);
@@ -4061,6 +4080,10 @@ extern "C" int vm_set_option(const char* key, long value) {
 #ifdef VM_STUDY
   if (!strcmp(key, "patch_ablate")) {  // timing-only ablations: garbage results
     g_patch_ablate = value;
+    return VM_OK;
+  }
+  if (!strcmp(key, "softmax_abl")) {  // timing-only ablations of the f32 refine kernel: garbage results
+    g_softmax_abl = value;
     return VM_OK;
   }
   if (!strcmp(key, "patch_rowslot")) {
