@@ -3848,7 +3848,10 @@ static int dispatch_patch(ConvArgs& a, hipStream_t st) {
       rc = sk ? launch_patch_persist<64, 4, 1, 2, 4, 2, true>(a, st) : launch_patch_persist<64, 4, 1, 2, 4, 2, false>(a, st);
     if (rc != 1) return rc;
   }
-  if (blocks64 >= 8000) return launch_patch_up<64, 8, 1, 3, 8, 1, 9, false, 0, false, 3>(a, st);
+  // the 3-slot ring for the largest grids and for the folded upconvs the persistent kernel leaves (upconv_2: its
+  // zero-tap phases are latency-bound on the ring, a deeper prefetch measured -2 %)
+  if (blocks64 >= 8000 || (a.up && g_up_skip && blocks64 >= 512))
+    return launch_patch_up<64, 8, 1, 3, 8, 1, 9, false, 0, false, 3>(a, st);
   if (blocks64 < 512) return launch_patch_up<64, 4, 1, 2, 4, 2, 9, false, 0, false, 3>(a, st);  // L5: 4 x 32 px tiles
   return launch_patch_up<64, 8, 1, 2, 8, 1, 9, false, 0, false, 3>(a, st);
 }
