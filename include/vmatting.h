@@ -80,7 +80,19 @@ const char* vm_last_error(void);
  *                    strips, no per-tile block barrier (default); f32: any value but 0 = conv3x3_first_softmax_f32
  *   "softmax_blocks" persistent grid of the conv3x3_first_softmax kernels (default 2048)
  *   "pair_xin_wide"  pair kernel, f32 frames with 4..8 channels: 1 = two 16-byte loads per pixel (default),
- *                    0 = one dword load per channel */
+ *                    0 = one dword load per channel
+ *   "pair_strip"     first pair: 1 = strip-walking kernel where it applies (default), 0 = tile kernels
+ *   "patch_repi"     patch kernel register epilogue: 1 (default) / 0 = LDS-staged epilogue
+ *   "patch_persist"  1 = persistent row-slot patch kernel where the round policy says it pays (default), 0 = off
+ *   "persist_rounds", "persist_up_rounds"  its minimum rounds of items for plain convs (default 2) and folded
+ *                    upconvs (default 6); 0 = any grid (tests)
+ *   "persist_all"    1 = every plain grid of >= persist_rounds rounds (A/B); "persist_rot" 0 = walkers rotate
+ *                    through the output tiles for folded upconvs only (default), 1 = always, 2 = never
+ *   "rows_kernel", "rows_min_blocks", "rows_min_cin", "rows_up"  row-stationary kernel dispatch (1, 400, 128, 0)
+ *   "border_ks"      folded-upconv border pass granule split: 1 (default), 2 or 4
+ *   The patch / row-stationary / persistent / strip choices and "up_skip" are bit-identical (every output keeps its
+ *   MFMA sequence); "conv_kernel", "head_kernel" and "softmax_kernel" pick kernels with another f32 summation order
+ *   (within the stated tolerances). */
 int vm_set_option(const char* key, long value);
 /* Name of the conv kernel the calling thread's last vm_conv3x3_nhwc launched, spelled the way
  * rocprofv3 reports it (e.g. "vm::conv3x3_mfma<unsigned short, 128, 128>"); "" before the first call.
