@@ -524,7 +524,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_glds(ConvArgs a) {
   for (int kt = 0; kt < nk; ++kt) {
     // stage kt has landed once only the min(S-2, nk-1-kt) younger stages are still in flight
     wait_vm(min(S - 2, nk - 1 - kt) * lps);
-    asm volatile("" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (fragment reads of the slot refilled below: see conv3x3_patch)
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     if (kt + S - 1 < nk) {
@@ -855,9 +855,13 @@ void conv3x3_patch(ConvArgs a) {
       bv[f] = *reinterpret_cast<const uint4*>(xp + swz<64>(row, ck));
     }
   };
+  // counted DMA wait, then lgkmcnt(0): this wave's fragment reads of the ring slot / patch buffer that the DMAs
+  // issued right after the barrier refill must have returned before the barrier — the MFMAs consuming them may be
+  // scheduled past it (seen in the 4 x 32 folded-upconv instantiation: under a second process on the GPU the refill
+  // overtook a queued ds_read about once per 100 frames)
   auto sync = [&](int n) {
     wait_vm(n);
-    asm volatile("" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
   };
@@ -869,7 +873,7 @@ void conv3x3_patch(ConvArgs a) {
   // latency-bound on that ring, and a variant that also dropped the zero rows from the ring (shorter prefetch cover)
   // measured 1.3 % slower on the whole forward, this one 0.3 % faster (same-box A/B, tools/ab_unet.py).
   const int up_phase = UPSKIP && a.up && n0 / a.up_cout == (n0 + BN - 1) / a.up_cout ? n0 / a.up_cout : 0;
-  const bool skip_r0 = (up_phase >> 1) != 0, skip_c0 = (up_phase & 1) != 0;
+  const bool skip_r0 = (up_phase >> 1) != 0 && (a.upmask & 1), skip_c0 = (up_phase & 1) != 0 && (a.upmask & 2);
 
   if constexpr (G > 1) {
     // one ring slot = one kernel row (G = 3 taps): one barrier per row; inside the row the fragments of tap g+1 are
@@ -1459,9 +1463,13 @@ void conv3x3_patch_persist(ConvArgs a) {
 #pragma unroll
     for (int f = 0; f < FP; ++f) bv[f] = *reinterpret_cast<const uint4*>(xp + swz<64>(abase[f] + toff, ck));
   };
+  // counted DMA wait, then lgkmcnt(0): this wave's fragment reads of the ring slot / patch buffer that the DMAs
+  // issued right after the barrier refill must have returned before the barrier — the MFMAs consuming them may be
+  // scheduled past it (seen in the 4 x 32 folded-upconv instantiation: under a second process on the GPU the refill
+  // overtook a queued ds_read about once per 100 frames)
   auto sync = [&](int n) {
     wait_vm(n);
-    asm volatile("" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
   };
@@ -1595,7 +1603,7 @@ void conv3x3_patch_persist(ConvArgs a) {
     const bool more = qn < nitem;
     const int stn = lo + qn / tn, wbn = more ? (qn % tn) * wstep : 0, wb = (n0 / BN) * wstep;
     const int up_phase = UPSKIP && a.up && n0 / a.up_cout == (n0 + BN - 1) / a.up_cout ? n0 / a.up_cout : 0;
-    const bool skip_r0 = (up_phase >> 1) != 0, skip_c0 = (up_phase & 1) != 0;
+    const bool skip_r0 = (up_phase >> 1) != 0 && (a.upmask & 1), skip_c0 = (up_phase & 1) != 0 && (a.upmask & 2);
     f32x4 acc[FC][FP];
 #pragma unroll
     for (int i = 0; i < FC; ++i)
@@ -3497,6 +3505,7 @@ static int launch_glds(ConvArgs& a, hipStream_t st) {
 }
 
 static long g_border_ks = 1;  // folded-upconv border pass: granule split (1, 2 or 4 wave groups per block)
+static long g_up_skip_mask = 3;  // folded upconvs: which zero taps are skipped (1 = kernel row, 2 = column, 3 = both)
 static long g_patch_repi = 1;  // patch kernel: register epilogue (bf16 outputs, no packed frames) where the tiling allows
 template <int BN, int WM, int WN, int S, int TH = 8, int MINB = 1, int UNR = 9, bool PF = false, int ABL = 0,
           bool FIRST = false, int G = 1, bool UPSKIP = false>
@@ -3517,6 +3526,7 @@ static int launch_patch(ConvArgs& a, hipStream_t st) {
                             : N * ((a.H + C::TH - 1) / C::TH) * ((a.W + C::TW - 1) / C::TW);
   a.tiles_n = (a.cout + BN - 1) / BN;
   a.repi = (int)g_patch_repi;
+  a.upmask = (int)g_up_skip_mask;
   if (sp * a.tiles_n > 0x7fffffffL) return fail(VM_EUNSUPPORTED, "conv3x3: too many tiles");
   a.tiles_total = (int)(sp * a.tiles_n);
   snprintf(g_last_kernel, sizeof g_last_kernel, "vm::conv3x3_patch<%d, %d, %d, %d, %d, %d, %d, %s, %d, %s, %d, %s>", BN,
@@ -3575,6 +3585,7 @@ static int launch_patch_persist(ConvArgs& a, hipStream_t st) {
   a.tiles_n = tn;
   a.prot = g_persist_rot == 0 ? (a.up ? 1 : 0) : g_persist_rot == 1 ? 1 : 0;
   a.repi = 1;
+  a.upmask = (int)g_up_skip_mask;
   a.tiles_total = (int)(sp * tn);
   const long J = resident / 8;  // walkers per XCD band (every band has >= 2 rounds of items)
   snprintf(g_last_kernel, sizeof g_last_kernel, "vm::conv3x3_patch_persist<%d, %d, %d, %d, %d, %d, %s>", BN, WM, WN, S,
@@ -4124,6 +4135,11 @@ extern "C" int vm_set_option(const char* key, long value) {
   if (!strcmp(key, "persist_all") || !strcmp(key, "persist_rot")) {
     if (value < 0 || value > 2) return fail(VM_EINVAL, "%s must be 0, 1 or 2", key);
     (key[8] == 'a' ? g_persist_all : g_persist_rot) = value;
+    return VM_OK;
+  }
+  if (!strcmp(key, "up_skip_mask")) {
+    if (value < 0 || value > 3) return fail(VM_EINVAL, "up_skip_mask must be 0..3");
+    g_up_skip_mask = value;
     return VM_OK;
   }
   if (!strcmp(key, "patch_persist")) {

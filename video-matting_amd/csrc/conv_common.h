@@ -47,6 +47,7 @@ struct ConvArgs {
   int vstride, vW;
   int repi;  // patch kernel: 1 = register epilogue where the tiling allows (bf16 output, no split-K, no packed frames)
   int prot;  // persistent patch kernel: 1 = walkers rotate through the output tiles (folded-upconv phases)
+  int upmask;  // folded upconvs: bit 0 = skip the zero kernel row, bit 1 = the zero kernel column (3 = both)
   // strip pair kernel: optional bf16 output of the FIRST conv (conv1_1 + bias + relu), [N,H,W,64] view
   void* y1;
   int y1_cstride, y1_coff;
