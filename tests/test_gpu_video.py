@@ -138,3 +138,49 @@ def test_frame_parallel_world2_real_model():
     for rank, ok_w, ok_shape, bad, spans in res:
         assert ok_w and ok_shape and bad == [], (rank, ok_w, ok_shape, bad)
     assert [r[4] for r in res] == [2, 2]  # 4 frames -> 2 chunks of 2; 3 frames -> 2 + 1
+
+
+def _contention_worker(rank, q, seconds, h, w):
+    """One of two processes sharing cuda:0: chunked graph replay (video.matte_video) vs standalone forward() of the
+    same frames, over and over, with the 4 x 32-pixel patch tiling forced on every patch-kernel layer."""
+    import time
+    try:
+        from vmatting import _lib, unet, video
+        from vmatting.weights import synthetic_vgg16
+        torch.cuda.set_device(0)
+        _lib.set_option("patch_cfg", 25)
+        np.random.seed(100)
+        model = unet.UNetVideo(synthetic_vgg16(0), dtype="bf16", device="cuda:0").prepare()
+        frames = video.synthetic_frames(4, h, w, first=4 * rank, device="cuda:0")
+        t0, it, bad = time.time(), 0, []
+        while time.time() - t0 < seconds:
+            full, _ = video.matte_video(model, frames, 4, chunk=2)
+            torch.cuda.synchronize()
+            got = full.clone()
+            for i in range(4):
+                ref = model.forward(frames[i:i + 1].clone())[0]
+                if not torch.equal(ref, got[i]):
+                    bad.append((it, i, float((ref - got[i]).abs().max())))
+            it += 1
+        q.put((rank, it, bad[:5], len(bad)))
+    except Exception as e:  # report instead of hanging the parent
+        import traceback
+        q.put((rank, 0, [repr(e), traceback.format_exc()[-800:]], -1))
+
+
+def test_graph_vs_eager_under_contention():
+    """Two processes on the one GPU, each replaying chunked HIP graphs and the eager forward of the same frames for
+    ~20 s: every matte bit-identical.  Regression test for the LDS race fixed in r03 (a ring slot's refill DMA could
+    overtake a queued fragment read when the consuming MFMAs were scheduled past the slot-release barrier; with a
+    second process on the GPU about 1 % of the frames differed, with the 4 x 32 tiling several per second)."""
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_contention_worker, args=(r, q, 20.0, 270, 480)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=115) for _ in procs)
+    for p in procs:
+        p.join(30)
+    for rank, iters, bad, nbad in res:
+        assert nbad == 0 and iters > 50, (rank, iters, nbad, bad)
