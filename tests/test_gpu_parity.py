@@ -11,7 +11,9 @@ import numpy as np
 import pytest
 import torch
 
+from bf16check import abs_conv_at, check_bf16
 from conftest import golden, gpu_available
+from oracle import bf16 as ob
 from oracle import flow as oflow
 from oracle import models as om
 from oracle import ops as oops
@@ -88,10 +90,11 @@ def test_patch_kernel_configs(case, cfg):
         _lib.set_option("conv_kernel", 0)
         _lib.set_option("patch_cfg", 0)
     assert name.startswith("vm::conv3x3_patch<"), name
-    ref = oops.conv3x3_same(x.float().numpy().astype(np.float64), wt.astype(np.float64)) + b
+    x64 = x.float().numpy().astype(np.float64)
+    ref = oops.conv3x3_same(x64, wt.astype(np.float64)) + b
     ref = {"relu": oops.relu, "sigmoid": oops.sigmoid}.get(act, lambda v: v)(ref)
-    err = np.abs(y.float().cpu().numpy() - ref).max() / max(1.0, np.abs(ref).max())
-    assert err < 1e-2, err
+    # the bf16 rounding bound: >= 99.99 % within 1 ulp, all within 2 ulp or the f32 summation bound
+    check_bf16("patch cfg %d" % cfg, H(y), ref, 9 * cin, lambda idx: abs_conv_at(x64, wt, b, idx, ref.shape))
 
 
 @pytest.mark.parametrize("dtype", ["fp32", "bf16"])
@@ -169,10 +172,10 @@ def test_first_layer_kernel(case):
     buf[..., :cin] = x.to(DEV)
     y = ops.conv3x3(buf[..., :cin], pc, act)
     assert _lib.last_conv_kernel() == "vm::conv3x3_first"
-    ref = oops.conv3x3_same(x.float().numpy().astype(np.float64), wt.astype(np.float64)) + b
+    x64 = x.float().numpy().astype(np.float64)
+    ref = oops.conv3x3_same(x64, wt.astype(np.float64)) + b
     ref = {"relu": oops.relu, "sigmoid": oops.sigmoid}.get(act, lambda v: v)(ref)
-    err = np.abs(y.float().cpu().numpy() - ref).max() / max(1.0, np.abs(ref).max())
-    assert err < 1e-2, err
+    check_bf16("first", H(y), ref, 9 * cin, lambda idx: abs_conv_at(x64, wt, b, idx, ref.shape))
 
 
 @pytest.mark.parametrize("shape", [(1, 16, 64, 64, 64), (2, 17, 45, 64, 128), (1, 9, 33, 256, 256),
@@ -308,10 +311,10 @@ def test_rows_kernel(case, th):
         outs.append(cat[..., 8:8 + cout].clone())
         pools.append(pool)
     assert names[0] == "vm::conv3x3_rows<%d>" % th and names[1].startswith("vm::conv3x3_patch<"), names
-    ref = oops.conv3x3_same(x.float().numpy().astype(np.float64), wt.astype(np.float64)) + b
+    x64 = x.float().numpy().astype(np.float64)
+    ref = oops.conv3x3_same(x64, wt.astype(np.float64)) + b
     ref = {"relu": oops.relu, "sigmoid": oops.sigmoid}.get(act, lambda v: v)(ref)
-    y = outs[0].float().cpu().numpy()
-    assert np.abs(y - ref).max() / max(1.0, np.abs(ref).max()) < 1e-2
+    check_bf16("rows<%d>" % th, H(outs[0]), ref, 9 * cin, lambda idx: abs_conv_at(x64, wt, b, idx, ref.shape))
     assert torch.equal(outs[0], outs[1])
     assert torch.equal(pools[0], pools[1])
     assert np.array_equal(H(pools[0]), oops.max_pool_2x2_same(H(outs[0])))
@@ -373,6 +376,11 @@ def test_upconv_folded_resize(case, cfg):
     ref = oops.relu(oops.conv3x3_same(r, wt.astype(np.float64)) + b)
     err = np.abs(y - ref).max() / max(1.0, np.abs(ref).max())
     assert err < 1e-2, err
+    # the kernel's own arithmetic (bf16 folded phase filters, unfused bf16 border) to the bf16 rounding bound
+    x64 = x.float().cpu().numpy().astype(np.float64)
+    refk = oops.relu(ob.upconv2x_folded(x64, wt, round_w=True) + b)
+    absk = ob.upconv2x_folded(np.abs(x64), np.abs(wt), round_w=False) + np.abs(b)
+    check_bf16("up2x cfg %d" % cfg, y, refk, 9 * cin, lambda idx: 1.01 * absk.reshape(-1)[idx])
     unfused = ops.upconv3x3(x, pc, "relu", fold=False).float().cpu().numpy()
     assert np.abs(y - unfused).max() / max(1.0, np.abs(unfused).max()) < 1e-2
     # border pixels take the unfused arithmetic (bf16 resized taps, plain filter)
