@@ -429,6 +429,13 @@ int vm_relu_backward_ex_nhwc(const vm_tensor* dy, const vm_tensor* y, vm_tensor*
 int vm_relu_backward_split_nhwc(const vm_tensor* dy, const vm_tensor* y, int split, vm_tensor* dx_lo, vm_tensor* dx,
                                 vm_tensor* dx2, void* stream);
 
+/* Adjoint of vm_maxpool2x2_same_nhwc (tf.nn.max_pool 2x2/2 SAME: small.py:40,42; unet.py:32-33): x is the pool's
+ * input [n,h,w,c] (any dtype), dy its output gradient [n,ceil(h/2),ceil(w/2),c]; dx [n,h,w,c] (f32 or bf16)
+ * = add + the window gradient at the window's first maximum in row-major order (TF MaxPoolGrad's tie rule), 0
+ * elsewhere.  add (optional, may alias dx): a gradient reaching x by another path (small.py:20's skip concat). */
+int vm_maxpool2x2_backward_nhwc(const vm_tensor* x, const vm_tensor* dy, const vm_tensor* add, vm_tensor* dx,
+                                void* stream);
+
 /* Adjoint of vm_resize_bilinear_tf1_nhwc (tf.image.resize_images, unet_simple.py:33): dy [n,oh,ow,c] (f32 view) ->
  * dx contiguous f32 [n,ih,iw,c] (overwritten). */
 int vm_resize_bilinear_tf1_backward(const vm_tensor* dy, float* dx, int ih, int iw, void* stream);

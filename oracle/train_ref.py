@@ -5,6 +5,12 @@ cpu_baseline may use it; the product never does).
                     create_model(cmp, bg, warped, phase=True) (unet_simple.py:145-171) with the frozen VGG towers
                     taken from the numpy oracle (models.vgg16_tower), then UNetSimple restated in torch float64 so
                     that autograd gives d loss / d every variable of 'model/simple_unet' (train.py:289)
+  small_step_grads  one iteration of small_train.py's small_training (small_train.py:34-88, entry train() at
+                    :91-112): UNetSmall(concat(cmp, bg), phase=True) (small.py:37-50) restated in torch float64, the
+                    same loss (small_train.py:39-44), autograd over ALL its variables (small_train.py:47-48: Adam on
+                    every trainable variable — conv weights / biases and BN gamma / beta; the upconvs' drawn biases
+                    feed nothing and get no gradient).  max_pool's gradient goes to each window's first maximum in
+                    row-major order (TF MaxPoolGrad's strict '>' scan; parity unpinned, TF is absent)
   adam_tf           tf.train.AdamOptimizer's ApplyAdam (train.py:302-304) in numpy float32, including TF's f32
                     beta-power variables and lr_t = lr*sqrt(1-beta2^t)/(1-beta1^t)
 
@@ -128,6 +134,70 @@ def train_step_grads(cmp, bg, warped, gt, raw_fg, vgg, params, bn=None, towers=N
     grads = {k: v.grad.cpu().numpy().copy() for k, v in V.items()}
     terms = (float(loss), float(la.mean()), float(lc.mean()))
     return terms, alpha.detach().cpu().numpy(), grads
+
+
+def _pool(x):
+    """tf.nn.max_pool 2x2/2 SAME (small.py:40,42): pad past odd edges with -inf; torch.max over the row-major window
+    returns (and back-propagates to) the first maximum, TF's tie rule."""
+    n, h, w, c = x.shape
+    oh, ow = (h + 1) // 2, (w + 1) // 2
+    xp = F.pad(x, (0, 0, 0, 2 * ow - w, 0, 2 * oh - h), value=float("-inf"))
+    win = xp.reshape(n, oh, 2, ow, 2, c).permute(0, 1, 3, 5, 2, 4).reshape(n, oh, ow, c, 4)
+    return win.max(dim=-1).values
+
+
+SMALL_BN_WIDTH = {"upconv1": 32, "upconv2": 16}
+
+
+def small_step_grads(cmp, bg, gt, raw_fg, params, bn=None, device="cpu"):
+    """-> (loss terms, alpha, grads {(scope, kind): ndarray}, forward dict) for small_train.py's step on
+    input = concat(cmp, bg) (small_train.py:95).  params: models.unet_small_params (cin 6); bn: {scope: (gamma,
+    beta)} or fresh (1, 0)."""
+    f64 = lambda a: np.asarray(a, np.float64)  # noqa: E731
+    T = lambda a: torch.from_numpy(f64(a)).to(device)  # noqa: E731
+    x = torch.cat([T(cmp), T(bg)], -1)
+    V = {}
+    for scope, (w, b) in params.items():
+        V[scope, "w"] = torch.tensor(f64(w), requires_grad=True, device=device)
+        if not scope.startswith("upconv"):
+            V[scope, "b"] = torch.tensor(f64(b), requires_grad=True, device=device)
+        c = SMALL_BN_WIDTH.get(scope, w.shape[3])
+        g, be = (np.ones(c), np.zeros(c)) if bn is None or scope not in bn else bn[scope]
+        V[scope, "gamma"] = torch.tensor(f64(g), requires_grad=True, device=device)
+        V[scope, "beta"] = torch.tensor(f64(be), requires_grad=True, device=device)
+
+    def new_conv(t, s):  # small.py:26-34
+        return _bn(_conv(t, V[s, "w"], V[s, "b"]), V[s, "gamma"], V[s, "beta"])
+
+    def upconv_concat(prev_layer, down, s):  # small.py:13-23: resize -> conv (no bias) -> relu -> [skip, up] -> BN
+        h, w = prev_layer.shape[1:3]
+        up = torch.relu(_conv(_resize(down, h, w), V[s, "w"]))
+        return _bn(torch.cat([prev_layer, up], -1), V[s, "gamma"], V[s, "beta"])
+
+    r = {}
+    r["conv1_1"] = torch.relu(new_conv(x, "conv1_1"))
+    r["pool1"] = _pool(r["conv1_1"])
+    r["conv2_1"] = torch.relu(new_conv(r["pool1"], "conv2_1"))
+    r["pool2"] = _pool(r["conv2_1"])
+    r["conv3_1"] = torch.relu(new_conv(r["pool2"], "conv3_1"))
+    r["conv3_2"] = torch.relu(new_conv(r["conv3_1"], "conv3_2"))
+    r["upconv1"] = upconv_concat(r["conv2_1"], r["conv3_2"], "upconv1")
+    r["conv2_2"] = torch.relu(new_conv(r["upconv1"], "conv2_2"))
+    r["upconv2"] = upconv_concat(r["conv1_1"], r["conv2_2"], "upconv2")
+    r["conv1_2"] = torch.relu(new_conv(r["upconv2"], "conv1_2"))
+    r["conv1_3"] = new_conv(r["conv1_2"], "conv1_3")
+    alpha = torch.sigmoid(r["conv1_3"])
+    gt_t, fg_t, bg_t, cmp_t = (T(a) for a in (gt, raw_fg, bg, cmp))
+    eps2 = np.float64(np.float32(1e-6) ** 2)
+    la = torch.sqrt((alpha - gt_t) ** 2 + eps2)
+    lc = torch.sqrt((alpha * fg_t + (1 - alpha) * bg_t - cmp_t) ** 2 + eps2)
+    loss = (0.5 * la + 0.5 * lc).mean()
+    loss.backward()
+    grads = {k: v.grad.cpu().numpy().copy() for k, v in V.items() if v.grad is not None}
+    terms = (float(loss.detach()), float(la.mean().detach()), float(lc.mean().detach()))
+    fwd = {k: v.detach().cpu().numpy() for k, v in r.items()}
+    fwd["output"] = alpha.detach().cpu().numpy()
+    return terms, fwd["output"], grads, fwd
 
 
 def adam_tf(var, m, v, grad, t, lr=1e-3, beta1=0.9, beta2=0.999, eps=1e-8):

@@ -107,3 +107,50 @@ def test_gradient_allreduce_gloo_world2():
     for p in procs:
         p.join(60)
     assert sorted(r for r, _ in res) == [0, 1] and all(ok for _, ok in res), res
+
+
+# ---------------------------------------------------------------------------- small_train.py (UNetSmall, all variables)
+
+def _small_case(n=2, h=18, w=22, seed=6):
+    rs = np.random.RandomState(seed)
+    mean = np.array([103.939, 116.779, 123.68])
+    fg = rs.uniform(0, 255, (n, h, w, 3))
+    bg = rs.uniform(0, 255, (n, h, w, 3))
+    gt = rs.uniform(0, 1, (n, h, w, 1))
+    return gt * fg + (1 - gt) * bg - mean, bg - mean, gt, fg
+
+
+def test_small_restatement_forward_and_layout():
+    """small_step_grads' forward equals the numpy oracle (pinned by the small_70x90_train golden), and its gradient
+    keys are exactly SmallTrainer's flat layout: every variable of small.py except the upconvs' unused biases."""
+    from vmatting.small_train import param_layout as small_layout
+    cmp, bg, gt, fg = _small_case()
+    p = om.unet_small_params(np.random.RandomState(1), cin=6)
+    terms, alpha, grads, _ = tr.small_step_grads(cmp, bg, gt, fg, p)
+    ref = om.unet_small_forward(np.concatenate([cmp, bg], -1), True, p)
+    assert np.abs(alpha - ref["output"]).max() <= 1e-10
+    np.testing.assert_allclose(terms, oops.matting_loss(ref["output"], gt, fg, bg, cmp), rtol=1e-9)
+    layout, total = small_layout(6)
+    assert set(grads) == {(s, k) for s, k, _, _ in layout}
+    assert total == sum(int(np.prod(g.shape)) for g in grads.values())
+
+
+def test_small_restatement_gradient_finite_difference():
+    """Central differences through the max-pools, the [skip, up] concats' BN and the first (6-channel) conv."""
+    cmp, bg, gt, fg = _small_case(h=14, w=15, seed=8)
+    p = om.unet_small_params(np.random.RandomState(2), cin=6)
+    _, _, grads, _ = tr.small_step_grads(cmp, bg, gt, fg, p)
+    for scope, idx in (("conv1_1", (0, 2, 5, 3)), ("conv2_1", (1, 1, 4, 9)), ("upconv1", (2, 0, 7, 5)),
+                       ("conv1_3", (1, 2, 6, 0))):
+        h = 1e-5
+        w = p[scope][0].astype(np.float64)
+        vals = []
+        for s in (h, -h):
+            q = dict(p)
+            w2 = w.copy()
+            w2[idx] += s
+            q[scope] = (w2, p[scope][1])
+            vals.append(tr.small_step_grads(cmp, bg, gt, fg, q)[0][0])
+        fd = (vals[0] - vals[1]) / (2 * h)
+        g = grads[scope, "w"][idx]
+        assert abs(fd - g) <= 1e-5 * max(1e-6, abs(g)) + 1e-9, (scope, fd, g)

@@ -16,6 +16,7 @@
 //   conv dgrad      the forward conv kernels on flipped, transposed weights (flip_weights here)
 //   resize_backward adjoint of the TF-1 legacy bilinear resize, gathered per input element (no atomics)
 //   relu_backward   dy * (y > 0)
+//   maxpool_bwd     tf.nn.max_pool 2x2/2 SAME adjoint: the window's gradient to its first maximum (small.py:40,42)
 //   adam            TF ApplyAdam: m += (g-m)(1-b1); v += (g^2-v)(1-b2); var -= m*lr_t/(sqrt(v)+eps)
 
 #include <cstring>
@@ -276,6 +277,41 @@ static dim3 lanes_grid(long M, int C, int cp) {
     case 32: CALL(32); break;   \
     default: CALL(64); break;   \
   }
+
+// ---------------------------------------------------------------- max-pool backward (small.py:40,42)
+// Adjoint of tf.nn.max_pool 2x2/2 SAME (vm_maxpool2x2_same_nhwc): an input element receives its window's gradient
+// iff it is the window's FIRST maximum in row-major order — TF's MaxPoolGrad scans the window with a strict '>'
+// (taps past an odd edge are not in the window).  dx = add + that share (add optional; it may alias dx: each lane
+// reads its own element before writing it).  CP lanes per input pixel as the other elementwise passes; a lane
+// re-reads its window's other three values (L1/L2 hits) instead of a stored argmax.
+template <int CP>
+__global__ __launch_bounds__(256) void maxpool_bwd_kernel(V x, V dy, V add, V dx) {
+  const long HW = (long)x.h * x.w, M = (long)x.n * HW;
+  const int c = blockIdx.y * CP + (threadIdx.x & (CP - 1));
+  if (c >= x.c) return;
+  const int oh = dy.h, ow = dy.w;
+  const long step = (long)gridDim.x * (blockDim.x / CP);
+  for (long p = (long)blockIdx.x * (blockDim.x / CP) + threadIdx.x / CP; p < M; p += step) {
+    const int n = (int)(p / HW);
+    const int r = (int)(p - (long)n * HW);
+    const int iy = r / x.w, ix = r - iy * x.w;
+    const int y0 = iy & ~1, x0 = ix & ~1;
+    const long base = (long)n * HW;
+    float best = 0.f;
+    int win = -1;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int yy = y0 + (k >> 1), xx = x0 + (k & 1);
+      if (yy < x.h && xx < x.w) {
+        const float v = ld(x, base + (long)yy * x.w + xx, c);
+        if (win < 0 || v > best) { best = v; win = k; }
+      }
+    }
+    float g = win == ((iy - y0) << 1) + (ix - x0) ? ld(dy, ((long)n * oh + (iy >> 1)) * ow + (ix >> 1), c) : 0.f;
+    if (add.p) g += ld(add, p, c);
+    st(dx, p, c, g);
+  }
+}
 
 // ---------------------------------------------------------------- resize backward (adjoint of resize_tf1)
 __device__ __forceinline__ void tf1c(int i, float scale, int in, int& lo, int& hi, float& lerp) {
@@ -1404,6 +1440,23 @@ extern "C" int vm_relu_backward_split_nhwc(const vm_tensor* dy, const vm_tensor*
   VM_CP_SWITCH(cp, VM_RB)
 #undef VM_RB
   return check_launch("relu_backward");
+}
+
+extern "C" int vm_maxpool2x2_backward_nhwc(const vm_tensor* x, const vm_tensor* dy, const vm_tensor* add, vm_tensor* dx,
+                                           void* stream) {
+  if (!ok_view(x) || !ok_view(dy) || !ok_view(dx) || !same_shape(x, dx) || (add && (!ok_view(add) || !same_shape(add, x))))
+    return fail(VM_EINVAL, "maxpool_backward: bad tensors");
+  if (dy->n != x->n || dy->h != (x->h + 1) / 2 || dy->w != (x->w + 1) / 2 || dy->c != x->c)
+    return fail(VM_EINVAL, "maxpool_backward: dy must be [%d,%d,%d,%d]", x->n, (x->h + 1) / 2, (x->w + 1) / 2, x->c);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const long M = (long)x->n * x->h * x->w;
+  const int cp = lanes_for(x->c);
+  const dim3 grid = lanes_grid(M, x->c, cp);
+  const V a = mk(x), b = mk(dy), c = add ? mk(add) : V{}, d = mk(dx);
+#define VM_MPB(CP) hipLaunchKernelGGL((maxpool_bwd_kernel<CP>), grid, dim3(256), 0, st, a, b, c, d)
+  VM_CP_SWITCH(cp, VM_MPB)
+#undef VM_MPB
+  return check_launch("maxpool_backward");
 }
 
 extern "C" int vm_resize_bilinear_tf1_backward(const vm_tensor* dy, float* dx, int ih, int iw, void* stream) {

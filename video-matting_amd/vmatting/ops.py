@@ -821,6 +821,16 @@ def relu_backward(dy, y, dx, dx2=None, dx_lo=None):
     return dx
 
 
+def maxpool_backward(x, dy, dx, add=None):
+    """Adjoint of maxpool2x2 (tf.nn.max_pool 2x2/2 SAME): dx = add + dy routed to each window's first maximum of x
+    (TF MaxPoolGrad's tie rule).  ``add`` may be dx itself."""
+    xv, dv, ov = nhwc(x), nhwc(dy), nhwc(dx)
+    av = ctypes.byref(nhwc(add)) if add is not None else None
+    check(lib().vm_maxpool2x2_backward_nhwc(ctypes.byref(xv), ctypes.byref(dv), av, ctypes.byref(ov),
+                                            stream_handle()), "maxpool_backward")
+    return dx
+
+
 def resize_backward(dy, dx):
     """Adjoint of resize_bilinear: dy [n,oh,ow,c] -> dx contiguous f32 [n,ih,iw,c] (overwritten)."""
     _f32(dx)

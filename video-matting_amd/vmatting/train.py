@@ -65,7 +65,101 @@ def param_layout():
     return out, off
 
 
-class VideoTrainer:
+class TrainerBase:
+    """What the training steps of train.py (video_procedure / simple_procedure) and small_train.py
+    (small_training) share: the flat f32 parameter / gradient / Adam-slot buffers, batch statistics with optional
+    SyncBN, the BN backward, the DDP exchange and tf.train.AdamOptimizer's update."""
+
+    def _init_flat(self, layout, n, lr, beta1, beta2, epsilon, sync_bn):
+        self.lr, self.beta1, self.beta2, self.epsilon = lr, beta1, beta2, epsilon
+        # SyncBN: batch statistics (and their gradient sums) over every replica's batch, as the single-device
+        # reference normalises its whole batch; one small all-reduce per BN layer in the forward and one in the
+        # backward.  Off: per-replica statistics (plain DDP)
+        self.sync_bn = bool(sync_bn) and parallel.world_size() > 1
+        self.layout = layout
+        dev = self.device
+        self.flat = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.grad = torch.zeros_like(self.flat)
+        self.m = torch.zeros_like(self.flat)
+        self.v = torch.zeros_like(self.flat)
+        self.P, self.G = {}, {}
+        for scope, kind, off, shape in layout:
+            self.P[scope, kind] = self.flat[off:off + int(np.prod(shape))].view(shape)
+            self.G[scope, kind] = self.grad[off:off + int(np.prod(shape))].view(shape)
+        self.t = 0
+        self._b1p = np.float32(1.0)
+        self._b2p = np.float32(1.0)
+        self._gbatch = {}
+
+    def _global_batch(self, n, h, w):
+        """SyncBN: the frames of the global batch (sum of every replica's n, made once per batch shape on the host so
+        the backward's pixel counts need no device read); replicas must share the frame size."""
+        key = (n, h, w)
+        if key not in self._gbatch:
+            t = torch.tensor([float(n), float(h), float(w), -float(h), -float(w)], dtype=torch.float64,
+                             device=self.device)
+            s = t[:1].clone()
+            parallel.allreduce_sum(s)
+            mx = t[1:].clone()
+            if torch.distributed.is_initialized():
+                torch.distributed.all_reduce(mx, op=torch.distributed.ReduceOp.MAX)
+            mx = mx.cpu().numpy()
+            if mx[0] != -mx[2] or mx[1] != -mx[3]:
+                raise ValueError("SyncBN: every replica must train on the same frame size")
+            self._gbatch[key] = int(round(float(s.item())))
+        return self._gbatch[key]
+
+    def _stats(self, x, mean, var):
+        """Batch mean / biased variance of x's channels; SyncBN: over every replica's pixels (count-weighted, the
+        second moment combined in float64 so the per-replica variances do not cancel)."""
+        ops.bn_stats(x, mean, var)
+        if self.sync_bn:
+            m = float(x.shape[0] * x.shape[1] * x.shape[2])
+            md = mean.double()
+            t = torch.stack([md * m, (var.double() + md * md) * m, torch.full_like(md, m)])
+            parallel.allreduce_sum(t)
+            gm = t[0] / t[2]
+            mean.copy_(gm)
+            var.copy_((t[1] / t[2] - gm * gm).clamp_min(0.0))
+
+    def _bn_backward(self, x, dy, mask, mean, var, scope, dx, dx2=None, dbias=None):
+        """BN(+relu mask) backward: dx, dgamma / dbeta (local sums, DDP averages them) and optionally the conv-bias
+        gradient.  SyncBN: the local channel sums are all-reduced and the input gradient uses the global ones over
+        the global pixel count — the same count the forward's statistics were weighted by (replicas may hold
+        different batch sizes, e.g. an uneven last shard)."""
+        gamma, dgamma, dbeta = self.P[scope, "gamma"], self.G[scope, "gamma"], self.G[scope, "beta"]
+        if not self.sync_bn:
+            return ops.bn_backward(x, dy, mask, mean, var, gamma, EPS, dx=dx, dgamma=dgamma, dbeta=dbeta, dx2=dx2,
+                                   dbias=dbias)
+        ops.bn_backward(x, dy, mask, mean, var, gamma, EPS, dgamma=dgamma, dbeta=dbeta)
+        sums = torch.cat([dbeta, dgamma])
+        parallel.allreduce_sum(sums)
+        c = dbeta.numel()
+        n, h, w = x.shape[0], x.shape[1], x.shape[2]
+        count = self._global_batch_for(n) * h * w
+        ops.bn_backward_apply(x, dy, mask, mean, var, gamma, sums[:c], sums[c:], count, dx, EPS, dx2=dx2)
+        if dbias is not None:  # the conv bias's gradient = channel sum of this replica's dx
+            ops.bn_backward(None, dx, None, None, None, None, EPS, dbeta=dbias)
+        return dx
+
+    def _global_batch_for(self, n):
+        """The global batch of the shape this replica's current step runs (set by forward via _global_batch)."""
+        return self._cur_gbatch if getattr(self, "_cur_gbatch", None) is not None else n * parallel.world_size()
+
+    def apply_gradients(self):
+        """DDP gradient all-reduce + tf.train.AdamOptimizer step over the flat buffer, then re-pack the filters."""
+        scale = parallel.allreduce_grads(self.grad)
+        self.t += 1
+        # TF keeps beta1_power / beta2_power as f32 variables multiplied once per step (adam.py _finish)
+        self._b1p = np.float32(self._b1p * np.float32(self.beta1))
+        self._b2p = np.float32(self._b2p * np.float32(self.beta2))
+        one = np.float32(1.0)
+        lr_t = np.float32(np.float32(self.lr) * np.sqrt(one - self._b2p) / (one - self._b1p))
+        ops.adam_tf(self.flat, self.m, self.v, self.grad, lr_t, self.beta1, self.beta2, self.epsilon, scale)
+        self._refresh_packs()
+
+
+class VideoTrainer(TrainerBase):
     """train.video_procedure's iteration on device (also simple_procedure's: pass diff = cmp - bg as ``warped``)."""
 
     def __init__(self, vgg16_npy_path=None, dtype="fp32", device="cuda", params=None, bn=None, lr=1e-3,
@@ -73,11 +167,9 @@ class VideoTrainer:
         self.vgg = vgg16_npy_path if isinstance(vgg16_npy_path, Vgg16) else Vgg16(vgg16_npy_path, dtype, device)
         self.model = UNetSimple(self.vgg, True, dtype, device, params)
         self.device = self.model.device
-        self.lr, self.beta1, self.beta2, self.epsilon = lr, beta1, beta2, epsilon
-        # SyncBN: batch statistics (and their gradient sums) over every replica's batch, as the single-device
-        # reference normalises its whole batch (unet_simple.py:25,41; params.py:8); one small all-reduce per BN
-        # layer in the forward and one in the backward.  Off: per-replica statistics (plain DDP)
-        self.sync_bn = bool(sync_bn) and parallel.world_size() > 1
+        layout, n = param_layout()
+        # (SyncBN = the single-device reference's statistics over its whole batch: unet_simple.py:25,41; params.py:8)
+        self._init_flat(layout, n, lr, beta1, beta2, epsilon, sync_bn)
         # the select convs (unet_simple.py:120-139) read only the frozen towers' features and feed only their
         # level's concat: their chains (conv -> BN forward; BN backward -> filter gradient) run on `streams` side
         # streams beside the decoder chain, whose small deep-level kernels leave most of the chip idle.  Same
@@ -86,16 +178,7 @@ class VideoTrainer:
         dev_ = torch.device(device)
         self._side = [] if self.sync_bn or streams < 1 or dev_.type != "cuda" else \
             [torch.cuda.Stream(device=dev_) for _ in range(int(streams))]
-        self.layout, n = param_layout()
         dev = self.device
-        self.flat = torch.zeros(n, dtype=torch.float32, device=dev)
-        self.grad = torch.zeros_like(self.flat)
-        self.m = torch.zeros_like(self.flat)
-        self.v = torch.zeros_like(self.flat)
-        self.P, self.G = {}, {}
-        for scope, kind, off, shape in self.layout:
-            self.P[scope, kind] = self.flat[off:off + int(np.prod(shape))].view(shape)
-            self.G[scope, kind] = self.grad[off:off + int(np.prod(shape))].view(shape)
         # move the freshly drawn variables into the flat buffer and alias every consumer onto it
         for scope, pc in self.model.convs.items():
             self.P[scope, "w"].copy_(pc.w_hwio)
@@ -148,9 +231,6 @@ class VideoTrainer:
             self._refresh_packs()
         # filter gradients: bf16 operands on MFMA in the bf16 path, the exact-f32 kernel in the fp32 (parity) path
         self._mfma_wgrad = self.model.dtype == torch.bfloat16
-        self.t = 0
-        self._b1p = np.float32(1.0)
-        self._b2p = np.float32(1.0)
         self._tb, self._key = None, None
 
     # ------------------------------------------------------------------------------------------- buffers
@@ -226,6 +306,7 @@ class VideoTrainer:
               for t in (cmp, bg, warped)]
         xs = [t.to(self.device, torch.float32) for t in xs]
         n, h, w, _ = xs[0].shape
+        self._cur_gbatch = self._global_batch(n, h, w) if self.sync_bn else None
         b = m._buffers(n, h, w)
         tb = self._train_buffers(n, h, w)
         L = _levels(h, w)
@@ -272,35 +353,6 @@ class VideoTrainer:
         self.output = tb["alpha"]
         return self.output
 
-    def _stats(self, x, mean, var):
-        """Batch mean / biased variance of x's channels; SyncBN: over every replica's pixels (count-weighted, the
-        second moment combined in float64 so the per-replica variances do not cancel)."""
-        ops.bn_stats(x, mean, var)
-        if self.sync_bn:
-            m = float(x.shape[0] * x.shape[1] * x.shape[2])
-            md = mean.double()
-            t = torch.stack([md * m, (var.double() + md * md) * m, torch.full_like(md, m)])
-            parallel.allreduce_sum(t)
-            gm = t[0] / t[2]
-            mean.copy_(gm)
-            var.copy_((t[1] / t[2] - gm * gm).clamp_min(0.0))
-
-    def _bn_backward(self, x, dy, mask, mean, var, scope, dx, dx2=None, dbias=None):
-        """BN(+relu mask) backward: dx, dgamma / dbeta (local sums, DDP averages them) and optionally the conv-bias
-        gradient.  SyncBN: the local channel sums are all-reduced and the input gradient uses the global ones."""
-        gamma, dgamma, dbeta = self.P[scope, "gamma"], self.G[scope, "gamma"], self.G[scope, "beta"]
-        if not self.sync_bn:
-            return ops.bn_backward(x, dy, mask, mean, var, gamma, EPS, dx=dx, dgamma=dgamma, dbeta=dbeta, dx2=dx2,
-                                   dbias=dbias)
-        ops.bn_backward(x, dy, mask, mean, var, gamma, EPS, dgamma=dgamma, dbeta=dbeta)
-        sums = torch.cat([dbeta, dgamma])
-        parallel.allreduce_sum(sums)
-        c = dbeta.numel()
-        count = x.shape[0] * x.shape[1] * x.shape[2] * parallel.world_size()
-        ops.bn_backward_apply(x, dy, mask, mean, var, gamma, sums[:c], sums[c:], count, dx, EPS, dx2=dx2)
-        if dbias is not None:  # the conv bias's gradient = channel sum of this replica's dx
-            ops.bn_backward(None, dx, None, None, None, None, EPS, dbeta=dbias)
-        return dx
 
     # ------------------------------------------------------------------------------------------- backward
     def _conv_backward(self, scope, x_in, dy, mask, tb, dgrad_out=None):
@@ -358,17 +410,6 @@ class VideoTrainer:
             main.wait_stream(st)
 
     # ------------------------------------------------------------------------------------------- update
-    def apply_gradients(self):
-        """DDP gradient all-reduce + tf.train.AdamOptimizer step over the flat buffer, then re-pack the filters."""
-        scale = parallel.allreduce_grads(self.grad)
-        self.t += 1
-        # TF keeps beta1_power / beta2_power as f32 variables multiplied once per step (adam.py _finish)
-        self._b1p = np.float32(self._b1p * np.float32(self.beta1))
-        self._b2p = np.float32(self._b2p * np.float32(self.beta2))
-        one = np.float32(1.0)
-        lr_t = np.float32(np.float32(self.lr) * np.sqrt(one - self._b2p) / (one - self._b1p))
-        ops.adam_tf(self.flat, self.m, self.v, self.grad, lr_t, self.beta1, self.beta2, self.epsilon, scale)
-        self._refresh_packs()
 
     def _refresh_packs(self):
         """Re-make every kernel-layout copy of the flat parameters (forward, data-gradient and channel-padded packs,
