@@ -283,6 +283,13 @@ def cpu_baseline(x_host, params, frames, threads, model_name, flops_per_frame):
            "threads_def": "cores = BLAS pool threads the oracle ran on (numpy's OpenBLAS, OMP_NUM_THREADS on the box); "
                           "affinity_cpus = CPUs in this process's affinity mask; the loader / augment / train / "
                           "temporal CPU legs use the same thread count",
+           # BASELINE.md's plan sets the pool to the affinity mask; on this pool a 1-GPU job's CPU share is
+           # OMP_NUM_THREADS (16) of a host whose whole mask (256) is shared with the other GPUs' jobs, so the
+           # measurement keeps that share, and the linear scaling to the full mask is given as an upper bound
+           "threads_subset_reason": "the pool gives each GPU job OMP_NUM_THREADS=%s of the %d host CPUs in the "
+                                    "affinity mask (shared with the other GPUs' jobs); the baseline runs on that share"
+                                    % (os.environ.get("OMP_NUM_THREADS", "?"), len(os.sched_getaffinity(0))),
+           "upper_bound_at_affinity_cpus": round(len(os.sched_getaffinity(0)) / max(1, threads) / med, 4),
            "sample": "oracle/models.py numpy-f32 UNetVideo forward (the reference's op sequence) on the timed "
                      "1920x1080 frame: 1 warm-up (270x480), median of %d full frames (%s s)"
                      % (frames, ", ".join("%.1f" % t for t in times))}

@@ -74,7 +74,18 @@ def _resize(x, oh, ow):
     return top + (bot - top) * fy
 
 
-def train_step_grads(cmp, bg, warped, gt, raw_fg, vgg, params, bn=None, towers=None, device="cpu"):
+def _loss(la, lc, sample_weights):
+    """mean(0.5*L_alpha + 0.5*L_cmp) (train.py:294-298); with per-sample weights w: sum_i w_i * (sample i's mean) —
+    e.g. the objective data-parallel replicas jointly minimise, the sum of each replica's batch-mean loss."""
+    s = 0.5 * la + 0.5 * lc
+    if sample_weights is None:
+        return s.mean()
+    w = torch.as_tensor(np.asarray(sample_weights, np.float64), device=s.device)
+    return (s.mean(dim=(1, 2, 3)) * w).sum()
+
+
+def train_step_grads(cmp, bg, warped, gt, raw_fg, vgg, params, bn=None, towers=None, device="cpu",
+                     sample_weights=None):
     """-> (loss terms (loss, alpha_loss, cmp_loss), alpha, grads {(scope, kind): ndarray})
 
     device: where the float64 autograd runs ("cpu"; a GPU only for large test shapes — float64 there too, the
@@ -129,7 +140,7 @@ def train_step_grads(cmp, bg, warped, gt, raw_fg, vgg, params, bn=None, towers=N
     eps2 = np.float64(np.float32(1e-6) ** 2)
     la = torch.sqrt((alpha - gt_t) ** 2 + eps2)
     lc = torch.sqrt((alpha * fg_t + (1 - alpha) * bg_t - cmp_t) ** 2 + eps2)
-    loss = (0.5 * la + 0.5 * lc).mean()
+    loss = _loss(la, lc, sample_weights)
     loss.backward()
     grads = {k: v.grad.cpu().numpy().copy() for k, v in V.items()}
     terms = (float(loss), float(la.mean()), float(lc.mean()))
@@ -149,7 +160,7 @@ def _pool(x):
 SMALL_BN_WIDTH = {"upconv1": 32, "upconv2": 16}
 
 
-def small_step_grads(cmp, bg, gt, raw_fg, params, bn=None, device="cpu"):
+def small_step_grads(cmp, bg, gt, raw_fg, params, bn=None, device="cpu", sample_weights=None):
     """-> (loss terms, alpha, grads {(scope, kind): ndarray}, forward dict) for small_train.py's step on
     input = concat(cmp, bg) (small_train.py:95).  params: models.unet_small_params (cin 6); bn: {scope: (gamma,
     beta)} or fresh (1, 0)."""
@@ -191,7 +202,7 @@ def small_step_grads(cmp, bg, gt, raw_fg, params, bn=None, device="cpu"):
     eps2 = np.float64(np.float32(1e-6) ** 2)
     la = torch.sqrt((alpha - gt_t) ** 2 + eps2)
     lc = torch.sqrt((alpha * fg_t + (1 - alpha) * bg_t - cmp_t) ** 2 + eps2)
-    loss = (0.5 * la + 0.5 * lc).mean()
+    loss = _loss(la, lc, sample_weights)
     loss.backward()
     grads = {k: v.grad.cpu().numpy().copy() for k, v in V.items() if v.grad is not None}
     terms = (float(loss.detach()), float(la.mean().detach()), float(lc.mean().detach()))

@@ -246,12 +246,12 @@ def _worker(rank, world, port, q, kind, sizes, sync_bn, seed_base):
             trn.backward(T(gt), T(fg), T(bg), T(cmp))
         torch.cuda.synchronize()
         local = trn.grad.cpu().numpy().copy()
-        trn.apply_gradients()  # DDP all-reduce + Adam
+        trn.apply_gradients()  # DDP all-reduce (in place: trn.grad is the replicas' sum) + Adam
         torch.cuda.synchronize()
-        q.put((rank, p0, local, trn.flat.cpu().numpy(), None))
+        q.put((rank, p0, local, trn.flat.cpu().numpy(), trn.grad.cpu().numpy().copy(), None))
     except Exception:  # report instead of hanging the parent
         import traceback
-        q.put((rank, None, None, None, traceback.format_exc()[-2000:]))
+        q.put((rank, None, None, None, None, traceback.format_exc()[-2000:]))
     finally:
         if dist.is_initialized():
             dist.destroy_process_group()
@@ -267,7 +267,7 @@ def _run_world2(kind, sizes, sync_bn, seed_base=100):
     res = sorted((q.get(timeout=110) for _ in procs), key=lambda r: r[0])
     for p in procs:
         p.join(30)
-    assert all(r[4] is None for r in res), [r[4] for r in res]
+    assert all(r[5] is None for r in res), [r[5] for r in res]
     return res
 
 
@@ -281,39 +281,44 @@ def test_small_ddp_replicas_start_and_stay_identical():
 
 
 @pytest.mark.parametrize("kind", ["small", "video"])
-def test_syncbn_unequal_batches_match_single_replica(kind):
+def test_syncbn_unequal_batches_match_single_device(kind):
     """SyncBN with unequal per-rank batches (1 and 2 samples; ADVICE r03: the backward must use the forward's global
-    pixel count): the batch-weighted combination of the replicas' local gradients, (n0 g0 + n1 g1) / N — the
-    gradient of the mean loss over the whole batch — equals one replica's gradient on all 3 samples."""
+    pixel count).  The replicas jointly minimise the sum of their batch-mean losses, S = l_0 + (l_1 + l_2) / 2, with
+    batch statistics over all 3 samples; the all-reduced gradient must equal dS/dW of the float64 restatement on the
+    whole batch with those per-sample weights (a wrong count in the BN backward moves every gradient upstream of a
+    BN by O(1))."""
     sizes = (1, 2)
     res = _run_world2(kind, sizes, True)
-    g = (sizes[0] * res[0][2].astype(np.float64) + sizes[1] * res[1][2].astype(np.float64)) / sum(sizes)
+    np.testing.assert_array_equal(res[0][4], res[1][4])  # the all-reduced gradient is the same on both ranks
+    g = res[0][4].astype(np.float64)
+    wts = [1.0 / sizes[0]] * sizes[0] + [1.0 / sizes[1]] * sizes[1]
     if kind == "small":
-        from vmatting.small_train import SmallTrainer
+        from vmatting.small_train import param_layout as lay
         np.random.seed(100)  # rank 0's draws: the replicas run on them after the broadcast
-        ref = SmallTrainer(6, "fp32", DEV)
+        from vmatting.small import NEW_CONVS
+        from vmatting.weights import init_conv
+        params = {}
+        for name, ci, co in NEW_CONVS:
+            w, b = init_conv(6 if ci is None else ci, co)
+            params[name] = (w, None if name.startswith("upconv") else b)
         cmp, bg, gt, fg = _small_batch(3, 32, 40, seed=13)
-        ref.forward(cmp, bg)
-        ref.grad.zero_()
-        ref.backward(T(gt), T(fg), T(bg), T(cmp))
+        _, _, grads, _ = tr.small_step_grads(cmp, bg, gt, fg, params, sample_weights=wts)
+        layout = lay(6)[0]
     else:
         from test_gpu_train import _batch
-        from vmatting.train import VideoTrainer
+        from vmatting.train import param_layout as lay
         from vmatting.weights import synthetic_vgg16
-        ref = VideoTrainer(synthetic_vgg16(0), "fp32", DEV, params=om.unet_simple_params(np.random.RandomState(1)))
+        params = om.unet_simple_params(np.random.RandomState(1))
         cmp, bg, warped, gt, fg = _batch(3, 48, 64, seed=13)
-        ref.forward(cmp, bg, warped)
-        ref.grad.zero_()
-        ref.backward(T(gt), T(fg), T(bg), T(cmp))
-    torch.cuda.synchronize()
-    g_ref = H(ref.grad)
+        _, _, grads = tr.train_step_grads(cmp, bg, warped, gt, fg, synthetic_vgg16(0), params, sample_weights=wts)
+        layout = lay()[0]
     bad = []
-    for scope, k, off, shape in ref.layout:
+    for scope, k, off, shape in layout:
         if k == "b":  # conv biases: zero in exact arithmetic (BN removes them)
             continue
         n = int(np.prod(shape))
-        a, b = g[off:off + n], g_ref[off:off + n]
+        a, b = g[off:off + n], grads[scope, k].reshape(-1)
         l2 = np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30)
-        if l2 > 1e-3:
+        if l2 > 2e-3:
             bad.append((scope, k, float(l2)))
     assert not bad, bad

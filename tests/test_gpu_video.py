@@ -55,6 +55,32 @@ def test_video_batch_eager_equals_graph(model_bf16):
     assert torch.equal(g, e)
 
 
+def test_shape_switch_after_dropped_graph(vgg0):
+    """a captured forward's buffer set is allocated on the warm-up side stream and replayed on the
+    caller's stream (GraphedForward records that use).  Capture at one shape, replay, drop the graph, switch the model
+    to other shapes (the old set is freed and its memory handed out again) and back: every output equals a fresh
+    model's eager forward bit for bit."""
+    import gc
+    from vmatting import unet, video
+    np.random.seed(0)
+    m = unet.UNetVideo(vgg0, dtype="bf16", device="cuda").prepare()
+    np.random.seed(0)
+    ref = unet.UNetVideo(vgg0, dtype="bf16", device="cuda").prepare()
+    fa = video.synthetic_frames(2, 136, 250, first=3)
+    fb = video.synthetic_frames(1, 70, 90, first=4)
+    g = m.capture(fa)
+    for _ in range(3):
+        g.replay()
+    got_a = g.output.clone()
+    del g
+    gc.collect()
+    outs = [m.forward(fb).clone(), m.forward(video.synthetic_frames(3, 40, 64, first=5)).clone(), m.forward(fa).clone()]
+    torch.cuda.synchronize()
+    assert torch.equal(got_a, ref.forward(fa))
+    assert torch.equal(outs[0], ref.forward(fb))
+    assert torch.equal(outs[2], got_a)
+
+
 @pytest.mark.slow
 def test_video_batch_fp32_frame_vs_oracle(vgg0):
     """One sampled 1080p frame of the config-4 path in fp32 against the oracle: alpha within 1e-4."""

@@ -75,7 +75,10 @@ def gather_frames(local, n_frames, out=None):
     if out is None:
         out = torch.empty((world * mx,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
     if dist.get_backend() == "gloo":  # gloo's collective is the list form (host-staged for device tensors)
-        dist.all_gather(list(out.view((world, mx) + tuple(local.shape[1:])).unbind(0)), pad)
+        recv = out if out.is_contiguous() else torch.empty(out.shape, dtype=out.dtype, device=out.device)
+        dist.all_gather(list(recv.view((world, mx) + tuple(local.shape[1:])).unbind(0)), pad)
+        if recv is not out:
+            out.copy_(recv)
     else:
         dist.all_gather_into_tensor(out, pad)
     if all(b - a == mx for a, b in sizes):

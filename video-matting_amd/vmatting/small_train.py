@@ -151,7 +151,8 @@ class SmallTrainer(TrainerBase):
                 b["z_" + name] = b["zfull_" + name][..., :co]
             else:
                 b["z_" + name] = F(lv[name], co)
-            b["dz_" + name] = F(lv[name], co)
+            # (the fp32 data-gradient conv reads dz: a narrow one keeps an 8-channel row, zero padded)
+            b["dz_" + name] = F(lv[name], co) if co % 8 == 0 else F(lv[name], 8)[..., :co]
         # bf16 copies of the gradients the data-gradient convs read, channels zero-padded to 32
         if self.dtype == torch.bfloat16:
             for name in DGRAD:

@@ -387,8 +387,14 @@ class GraphedForward:
         side.wait_stream(torch.cuda.current_stream(self.input.device))
         with torch.cuda.stream(side):  # lazily built kernels/weights (folded filters, attributes) before capture
             model.forward(self.input, out)
-        torch.cuda.current_stream(self.input.device).wait_stream(side)
+        main = torch.cuda.current_stream(self.input.device)
+        main.wait_stream(side)
         torch.cuda.synchronize(self.input.device)
+        # the buffer set (and any lazily allocated entry) was allocated on the side stream but the graph replays on
+        # the caller's: tell the caching allocator, so a set freed later (the model moved to another shape and this
+        # graph was dropped) is not handed out again while replays queued on that stream may still use it
+        for t in model._ws.values():
+            t.record_stream(main)
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
             self.output = model.forward(self.input, out)
