@@ -548,6 +548,116 @@ def train_bench(dev, steps, warmup, world, rank, threads, cpu=True, n=8, size=32
     return rec
 
 
+def small_train_traffic(n, h, w, dtype_bytes=2):
+    """Algorithmic HBM bytes of one small_train.py step (8 x 320^2): every tensor the step materialises written once
+    and read once per consumer — activations in the compute dtype, pre-BN outputs and gradients in f32 — plus the
+    parameters, gradients and Adam slots once (the roofline of a step whose convs are 1-32 channels wide)."""
+    from vmatting.small_train import param_layout
+    L = [(h, w), ((h + 1) // 2, (w + 1) // 2)]
+    L.append(((L[1][0] + 1) // 2, (L[1][1] + 1) // 2))
+    px = [n * a * b for a, b in L]
+    T, F = dtype_bytes, 4
+    # (level, channels, bytes per element, reads) of each tensor of the forward and backward (small.py:37-50)
+    fwd = [(0, 6, F, 1), (0, 8, T, 1),                      # input, its bf16 copy
+           (0, 8, F, 2), (0, 8, T, 3), (1, 8, T, 2),          # conv1_1 z, act, pool1
+           (1, 16, F, 2), (1, 16, T, 3), (2, 16, T, 2),       # conv2_1 z, act, pool2
+           (2, 32, F, 2), (2, 32, T, 2), (2, 32, F, 2), (2, 32, T, 2),   # conv3_1, conv3_2
+           (1, 32, T, 1), (1, 16, T, 3), (1, 32, T, 2),       # resize, upconv1, BN(cat1)
+           (1, 16, F, 2), (1, 16, T, 2), (0, 16, T, 1), (0, 8, T, 3), (0, 16, T, 2),  # conv2_2, resize, upconv2, BN
+           (0, 8, F, 2), (0, 8, T, 2), (0, 1, F, 2), (0, 1, F, 2)]                   # conv1_2, conv1_3, alpha
+    bwd = [(0, 1, F, 2), (0, 8, F, 3), (0, 16, F, 2), (0, 16, F, 2), (0, 8, F, 1), (0, 8, F, 2), (0, 16, F, 1),
+           (1, 16, F, 2), (1, 32, F, 2), (1, 32, F, 2), (1, 16, F, 1), (1, 16, F, 2), (1, 32, F, 1), (2, 32, F, 2),
+           (2, 32, F, 2), (2, 16, F, 1), (1, 16, F, 2), (1, 8, F, 1), (0, 8, F, 2)]
+    act = sum(px[lv] * c * b * (1 + r) for lv, c, b, r in fwd + bwd)
+    nparam = param_layout(6)[1]
+    return act + nparam * 4 * (1 + 1 + 2 + 2)  # params read+write, gradients, Adam m / v read+write
+
+
+def train_small_bench(dev, steps, warmup, world, rank, threads, cpu=True, n=8, size=320, dtype="bf16", graph=True):
+    """small_train.py's step (small_train.py:34-88 with train()'s graph, :91-112): UNetSmall(concat(cmp, bg),
+    phase=True) forward, the loss, backward through EVERY variable (max-pool, BN and resize adjoints, filter and data
+    gradients), DDP all-reduce, TF-Adam at lr 1e-5, re-pack — batch 8 x 320^2 per GPU (params.py:8-9) resident in
+    HBM.  Forward + loss and backward are replayed from HIP graphs (the step is ~110 tiny launches)."""
+    from vmatting.small_train import SmallTrainer
+    rs = np.random.RandomState(200 + rank)
+    mean = np.array(VGG_MEAN)
+    fg = rs.uniform(0, 255, (n, size, size, 3))
+    bg = rs.uniform(0, 255, (n, size, size, 3))
+    yy, xx = np.mgrid[:size, :size]
+    gt = np.clip(1.2 - np.hypot((yy - size / 2) / (size / 3), (xx - size / 2) / (size / 4)), 0, 1)
+    gt = np.repeat(gt[None, :, :, None], n, 0)
+    cmp = gt * fg + (1 - gt) * bg - mean
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.float32)).to(dev)  # noqa: E731
+    cmp_d, bg_d, gt_d, fg_d = T(cmp), T(bg - mean), T(gt), T(fg)
+    np.random.seed(2)
+    trn = SmallTrainer(6, dtype, dev)
+    g = trn.capture(cmp_d, bg_d, gt_d, fg_d) if graph else None
+    for _ in range(warmup):
+        if g is not None:
+            g.step()
+        else:
+            trn.step(cmp_d, bg_d, gt_d, fg_d)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    ev = Events()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        ev.mark()
+        if g is not None:
+            g.g_fwd.replay()
+        else:
+            trn.forward(cmp_d, bg_d)
+            trn._b["loss"].copy_(ops.matting_loss(trn._b["alpha"], gt_d, fg_d, bg_d, cmp_d))
+        ev.mark()
+        if g is not None:
+            g.g_bwd.replay()
+        else:
+            trn.grad.zero_()
+            trn.backward(gt_d, fg_d, bg_d, cmp_d)
+        ev.mark()
+        trn.apply_gradients()
+        ev.mark()
+    torch.cuda.synchronize()
+    wall = torch.tensor([(time.perf_counter() - t0) / steps], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(wall, op=dist.ReduceOp.MAX)
+    wall = float(wall)
+    e = ev.e
+    ph = [sum(ms(e[4 * i + k], e[4 * i + k + 1]) for i in range(steps)) / steps for k in range(3)]
+    dev_ms = sum(ph)
+    nbytes = small_train_traffic(n, size, size, 2 if dtype == "bf16" else 4)
+    rec = {"workload": "small_train.py step: %d x %dx%d per GPU, UNetSmall(concat(cmp, bg)) fwd/bwd over all "
+                       "variables, loss, DDP all-reduce, TF-Adam" % (n, size, size),
+           "dtype": dtype + " forward, f32 gradients/optimizer", "n_gpus": world,
+           "launch": "hip-graph replay of forward+loss and of backward, eager all-reduce + Adam + re-pack" if graph
+                     else "eager",
+           "samples_per_s": round(n * world / wall, 1), "ms_per_step": round(1000 * wall, 4),
+           "device_ms": {"forward_loss": round(ph[0], 4), "backward": round(ph[1], 4),
+                         "allreduce_adam_repack": round(ph[2], 4)},
+           "roofline": {"bound": "hbm", "algorithmic_bytes": int(nbytes),
+                        "achieved_gbps": round(nbytes / (dev_ms * 1e-3) / 1e9, 1), "peak_gbps": PEAK_HBM_GBPS,
+                        "frac": round(nbytes / (dev_ms * 1e-3) / 1e9 / PEAK_HBM_GBPS, 4),
+                        "def": "bench.small_train_traffic: every tensor of the step written once and read once per "
+                               "consumer + parameters / gradients / Adam slots, over the step's device time"},
+           "loss_last": [round(float(v), 5) for v in trn._b["loss"].cpu()]}
+    if cpu and world == 1:
+        from oracle import models as om  # the CPU-baseline leg only
+        from oracle import train_ref as tr
+        p = om.unet_small_params(np.random.RandomState(1), cin=6)
+        sl = lambda a: np.asarray(a[:2], np.float64)  # noqa: E731
+        best = None
+        for _ in range(2):
+            t0 = time.perf_counter()
+            tr.small_step_grads(sl(cmp), sl(bg - mean), sl(gt), sl(fg), p)
+            dt = time.perf_counter() - t0
+            best = dt if best is None else min(best, dt)
+        rec["cpu_baseline"] = {"value": round(2.0 / best, 3), "unit": "samples/s", "cores": threads, "kind": "port",
+                               "sample": "oracle/train_ref.py small_step_grads (torch-f64 autograd of UNetSmall) on 2 "
+                                         "of the %dx%d samples, best of 2" % (size, size)}
+    return rec
+
+
 def train_chain_bench(dev, steps, warmup, n=8, size=320, h=1080, w=1920, dtype="bf16"):
     """BASELINE config 5 as ONE pipeline per step (rank 0, N=1): augmentation.augment makes frame t of each of n
     1080p source samples resident in HBM (augmentation.py:102-135, host np.random draws + TPS solve + one stats
@@ -716,7 +826,7 @@ def main():
                          "the step is not host-bound, and the graph runs the side-stream select chains serially")
     ap.add_argument("--train-streams", type=int, default=3,
                     help="side streams of the config-5 trainer's select chains (0: one stream, for serial profiles)")
-    ap.add_argument("--only", choices=["train", "train_chain", "temporal"],
+    ap.add_argument("--only", choices=["train", "train_chain", "train_small", "temporal"],
                     help="profiling passes: run just this record (rank 0 / N=1) and print it")
     ap.add_argument("--temporal-sizes", default="500x1200,1080x1920", help="config-3 sizes HxW, comma separated")
     ap.add_argument("--temporal-dtypes", default="fp32,bf16", help="config-3 compute dtypes, comma separated")
@@ -740,6 +850,8 @@ def main():
                               streams=args.train_streams)
         elif args.only == "train_chain":
             rec = train_chain_bench(dev, args.steps, args.warmup)
+        elif args.only == "train_small":
+            rec = train_small_bench(dev, args.steps, args.warmup, world, rank, threads, cpu=False)
         else:
             rec = temporal_bench(dev, args.steps, t_dtypes, t_sizes, False, threads)
         if rank == 0:
@@ -811,6 +923,8 @@ def main():
                             graph=args.train_graph)
         if world == 1:
             train["chained"] = train_chain_bench(dev, 5, 2)
+        train_small = train_small_bench(dev, max(args.steps // 4, 10), 3, world, rank, threads,
+                                        cpu=not args.no_cpu_baseline)
 
     roofline = conv_roofline(prof, args) if prof else None
     if rank == 0:
@@ -872,6 +986,7 @@ def main():
             rec["temporal"] = temporal_bench(dev, 20, t_dtypes, t_sizes, not args.no_cpu_baseline, threads)
         if train:
             rec["train"] = train
+            rec["train_small"] = train_small
         if world == 1 and not args.no_loader:
             rec["loader"] = loader_bench(dev, max(args.steps // 4, 10), threads, cpu=not args.no_cpu_baseline)
         if world == 1 and not args.no_augment:

@@ -1104,3 +1104,35 @@ def test_packed_frames_bit_identical(case):
     wb = torch.from_numpy(wt).to(torch.bfloat16).float().numpy().astype(np.float64)
     ref = np.maximum(oops.conv3x3_same(xcat, wb) + b, 0)
     assert relerr(H(y1), ref) < 2e-2
+
+
+@pytest.mark.parametrize("case", [(1, 17, 30, 256, 512, True), (1, 9, 33, 512, 512, False), (2, 5, 40, 128, 1024, False)])
+def test_channel_banded_tiles_bit_identical(case):
+    """The channel-banded block -> tile order of the streaming patch kernel (ConvArgs::cband: XCD b % 8 keeps its
+    64-channel weight slices L2-resident over every pixel tile; an option, off by default: measured slower) changes
+    only which block computes a tile: outputs bit-identical to the pixel-banded order, for folded
+    upconvs and plain convs (threshold lowered so these small shapes take it)."""
+    from vmatting import _lib, ops
+    n, h, w, cin, cout, up = case
+    rs = np.random.RandomState(h + cin)
+    x = torch.from_numpy(rs.normal(size=(n, h, w, cin)).astype(np.float32)).to(torch.bfloat16).to(DEV)
+    wt = (rs.normal(size=(3, 3, cin, cout)) * np.sqrt(2.0 / (9 * cin))).astype(np.float32)
+    pc = ops.PackedConv(wt, (rs.normal(size=cout) * 0.1).astype(np.float32), torch.bfloat16, DEV)
+    outs = []
+    try:
+        _lib.set_option("patch_persist", 0)
+        _lib.set_option("rows_kernel", 0)
+        _lib.set_option("cband_bytes", 0)
+        for band in (0, 2):
+            _lib.set_option("cband", band)
+            if up:
+                outs.append(ops.upconv3x3(x, pc, "relu"))
+            else:
+                outs.append(ops.conv3x3(x, pc, "relu"))
+            assert _lib.last_conv_kernel().startswith("vm::conv3x3_patch<"), _lib.last_conv_kernel()
+    finally:
+        _lib.set_option("cband", 0)
+        _lib.set_option("cband_bytes", 4 << 20)
+        _lib.set_option("patch_persist", 1)
+        _lib.set_option("rows_kernel", 1)
+    assert torch.equal(outs[0], outs[1])

@@ -742,8 +742,16 @@ void conv3x3_patch(ConvArgs a) {
   const int H = a.H, W = a.W, cs = a.x_cstride;
   const int VW = a.vstride ? a.vW : W;  // packed frames: one virtual image (n = 0), ConvArgs::vstride
   const int th = (H + C::TH - 1) / C::TH, tw = (VW + C::TW - 1) / C::TW;
-  const int t = xcd_tile(blockIdx.x, a.tiles_total);
-  const int st = t / a.tiles_n, nt = t - st * a.tiles_n;
+  int st, nt;
+  if (a.cband) {  // channel-banded: XCD b % 8 owns output tiles [xcd * cband, +cband) over every pixel tile
+    const int i = blockIdx.x >> 3;
+    st = i / a.cband;
+    nt = (blockIdx.x & 7) * a.cband + (i - st * a.cband);
+  } else {
+    const int t = xcd_tile(blockIdx.x, a.tiles_total);
+    st = t / a.tiles_n;
+    nt = t - st * a.tiles_n;
+  }
   const int n = st / (th * tw), srem = st - n * th * tw;
   const int r0 = (srem / tw) * C::TH, c0 = (srem - (srem / tw) * tw) * C::TW;
   const int n0 = nt * BN;
@@ -3507,6 +3515,12 @@ static int launch_glds(ConvArgs& a, hipStream_t st) {
 static long g_border_ks = 1;  // folded-upconv border pass: granule split (1, 2 or 4 wave groups per block)
 static long g_up_skip_mask = 3;  // folded upconvs: which zero taps are skipped (1 = kernel row, 2 = column, 3 = both)
 static long g_patch_repi = 1;  // patch kernel: register epilogue (bf16 outputs, no packed frames) where the tiling allows
+// channel-banded patch tiles (ConvArgs::cband): 0 off, 1 folded upconvs, 2 all.  Off: measured on upconv_2 (9.4 MB
+// folded filter) 0.261 -> 0.312 ms and on the L5 convs 0.053 -> 0.057 ms (same box, bench.py --option cband=0|1|2):
+// every XCD then reads the whole input from the Infinity Cache, which costs more than the weight stream it saves
+static long g_cband = 0;
+static long g_cband_bytes = 4L << 20;   // ... for filters of at least this many bytes (an XCD's L2)
+
 template <int BN, int WM, int WN, int S, int TH = 8, int MINB = 1, int UNR = 9, bool PF = false, int ABL = 0,
           bool FIRST = false, int G = 1, bool UPSKIP = false>
 static int launch_patch(ConvArgs& a, hipStream_t st) {
@@ -3529,6 +3543,11 @@ static int launch_patch(ConvArgs& a, hipStream_t st) {
   a.upmask = (int)g_up_skip_mask;
   if (sp * a.tiles_n > 0x7fffffffL) return fail(VM_EUNSUPPORTED, "conv3x3: too many tiles");
   a.tiles_total = (int)(sp * a.tiles_n);
+  // channel-banded tile order (ConvArgs::cband) for weight-heavy layers: the whole filter exceeds an XCD's 4 MB L2
+  // and its output tiles split evenly over the 8 XCDs.  cband option: 0 off, 1 folded upconvs, 2 any such layer
+  const long wbytes = (long)a.cout_pad * a.K_pad * 2;
+  a.cband = (g_cband >= (a.up ? 1 : 2)) && !FIRST && BN == 64 && a.tiles_n % 8 == 0 && wbytes >= g_cband_bytes
+                ? a.tiles_n / 8 : 0;
   snprintf(g_last_kernel, sizeof g_last_kernel, "vm::conv3x3_patch<%d, %d, %d, %d, %d, %d, %d, %s, %d, %s, %d, %s>", BN,
            WM, WN, S, TH, MINB, UNR, PF ? "true" : "false", ABL, FIRST ? "true" : "false", G, UPSKIP ? "true" : "false");
   hipLaunchKernelGGL((conv3x3_patch<BN, WM, WN, S, TH, MINB, UNR, PF, ABL, FIRST, G, UPSKIP>),
@@ -4024,6 +4043,15 @@ extern "C" int vm_set_option(const char* key, long value) {
   if (!strcmp(key, "head_th")) {
     if (value != 8 && value != 16) return fail(VM_EINVAL, "head_th must be 8 or 16");
     g_head_th = value;
+    return VM_OK;
+  }
+  if (!strcmp(key, "cband")) {
+    if (value < 0 || value > 2) return fail(VM_EINVAL, "cband must be 0, 1 or 2");
+    g_cband = value;
+    return VM_OK;
+  }
+  if (!strcmp(key, "cband_bytes")) {
+    g_cband_bytes = value;
     return VM_OK;
   }
   if (!strcmp(key, "rows_kernel")) {

@@ -48,6 +48,10 @@ struct ConvArgs {
   int repi;  // patch kernel: 1 = register epilogue where the tiling allows (bf16 output, no split-K, no packed frames)
   int prot;  // persistent patch kernel: 1 = walkers rotate through the output tiles (folded-upconv phases)
   int upmask;  // folded upconvs: bit 0 = skip the zero kernel row, bit 1 = the zero kernel column (3 = both)
+  // streaming patch kernel: cband > 0 maps block b to output tile (b & 7) * cband + (b >> 3) % cband of pixel tile
+  // (b >> 3) / cband, so XCD b % 8 keeps its cband 64-channel weight slices L2-resident over every pixel tile (weight-
+  // heavy layers: upconv_2's 9.4 MB folded filter, which the pixel-banded order re-streams per resident round)
+  int cband;
   // strip pair kernel: optional bf16 output of the FIRST conv (conv1_1 + bias + relu), [N,H,W,64] view
   void* y1;
   int y1_cstride, y1_coff;

@@ -165,12 +165,13 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
   // DMA of granule g of tile tt into buffer buf.  Every wave issues exactly XPW patch and WPW weight pieces (pieces past
   // the patch / weight slot land in the junk slot), so the vmcnt counts below are compile-time constants; real ==
   // false (steps past the end) turns every piece into an out-of-range (zero) load with the same count.
-  auto issue_x = [&](const RowTile& tt, bool real, int g, int buf) __attribute__((always_inline)) {
+  auto issue_x = [&](const RowTile& tt, bool real, int g, int buf, auto i0c, auto i1c) __attribute__((always_inline)) {
+    constexpr int i0 = decltype(i0c)::value, i1 = decltype(i1c)::value;
     const T* xb = uniform_ptr(reinterpret_cast<const T*>(a.x) + a.x_coff + (long)tt.n * H * W * cs);
     const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<T*>(xb), 0, 0x7ffffff0, 0x00020000);
     const int coff = (int)src_chan(a, g * 32) * 2;
 #pragma unroll
-    for (int i = 0; i < XPW; ++i) {
+    for (int i = i0; i < i1; ++i) {
       const bool piece_ok = wave + i * 8 < C::XP;
       int h = tt.r0 - 1 + (xgeo[i] >> 16), w = tt.c0 - 1 + ((xgeo[i] >> 8) & 255);
       if (a.up) {  // folded 2x resize: past the bottom/right edge the low-res frame is replicated (TF1 clamp)
@@ -182,12 +183,13 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
              ok ? ((h * W + w) * cs + (xgeo[i] & 255) * 8) * 2 + coff : OOB);
     }
   };
-  auto issue_w = [&](int n0, bool real, int g, int buf) __attribute__((always_inline)) {
+  auto issue_w = [&](int n0, bool real, int g, int buf, auto i0c, auto i1c) __attribute__((always_inline)) {
+    constexpr int i0 = decltype(i0c)::value, i1 = decltype(i1c)::value;
     const T* wb = uniform_ptr(reinterpret_cast<const T*>(a.w) + (long)n0 * a.K_pad);
     const uint32_t wbytes = __builtin_amdgcn_readfirstlane((uint32_t)((long)(a.cout_pad - n0) * a.K_pad * 2));
     const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<T*>(wb), 0, wbytes, 0x00020000);
 #pragma unroll
-    for (int i = 0; i < WPW; ++i) {
+    for (int i = i0; i < i1; ++i) {
       const bool piece_ok = wave + i * 8 < C::WP;
       glds16(wrs, __builtin_amdgcn_readfirstlane(lds0 + (piece_ok ? buf * C::WB + (wave + i * 8) * 1024 : C::JUNK)),
              real && piece_ok ? woff[i] + g * 576 : OOB);
@@ -372,36 +374,29 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
   using Z = std::integral_constant<int, 0>;
   using NX = std::integral_constant<int, XPW>;
   using NW = std::integral_constant<int, WPW>;
-  // DMA of step s + d (d = 1, 2): its tile is k + (g + d) / nch (at most k + 2)
-  auto issue_step = [&](int d, bool wts, int buf) __attribute__((always_inline)) {
-    int gg = g + d, dk = 0;
-    if (gg >= nch) {
-      gg -= nch;
-      dk = 1;
-      if (gg >= nch) {
-        gg -= nch;
-        dk = 2;
-      }
-    }
+  // DMA of step s + d (d = 1, 2): its tile is k + (g + d) / nch (at most k + 2).  Branch-free (scalar selects of
+  // the candidate tiles' fields), so the pieces can sit among the MFMAs of one basic block; pieces [i0, i1) only
+  auto issue_step = [&](int d, bool wts, int buf, auto i0, auto i1) __attribute__((always_inline)) {
+    const int gd = g + d;
+    const int dk = (gd >= nch ? 1 : 0) + (gd >= 2 * nch ? 1 : 0);
+    const int gg = gd - dk * nch;
+    // (arithmetic, not a select between the tile structs: that one demoted the register arrays to scratch)
+    const int m1 = dk >= 1, m2 = dk >= 2;
+    RowTile tt;
+    tt.n = t0.n + m1 * (t1.n - t0.n) + m2 * (t2.n - t1.n);
+    tt.r0 = t0.r0 + m1 * (t1.r0 - t0.r0) + m2 * (t2.r0 - t1.r0);
+    tt.c0 = t0.c0 + m1 * (t1.c0 - t0.c0) + m2 * (t2.c0 - t1.c0);
+    tt.n0 = t0.n0 + m1 * (t1.n0 - t0.n0) + m2 * (t2.n0 - t1.n0);
     const bool real = k + dk < ntile;
-    // uniform branches, one per candidate tile (a select between the tiles would put them in scratch)
-    if (dk == 0) {
-      if (wts) issue_w(t0.n0, real, gg, buf);
-      else issue_x(t0, real, gg, buf);
-    } else if (dk == 1) {
-      if (wts) issue_w(t1.n0, real, gg, buf);
-      else issue_x(t1, real, gg, buf);
-    } else {
-      if (wts) issue_w(t2.n0, real, gg, buf);
-      else issue_x(t2, real, gg, buf);
-    }
+    if (wts) issue_w(tt.n0, real, gg, buf, i0, i1);
+    else issue_x(tt, real, gg, buf, i0, i1);
   };
   // prologue: step 0 in, then step 1's DMA in flight
-  issue_w(t0.n0, true, 0, 0);
-  issue_x(t0, true, 0, 0);
+  using I = std::integral_constant<int, 0>;
+  issue_w(t0.n0, true, 0, 0, I{}, NW{});
+  issue_x(t0, true, 0, 0, I{}, NX{});
   sync(Z{});
-  issue_step(1, true, 1);
-  issue_step(1, false, 1);
+  issue_step(1, true, 1, I{}, NW{});  // W(1); X(1) goes out at the start of step 0, among its MFMAs
   ldw(w0, 0, 0);
   ldw(w1, 0, 1);
   ldw(w2, 0, 2);
@@ -414,33 +409,38 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
     static_assert(R == 4, "the row schedule below is written for 4-row waves");
     WRow& k2 = b == 0 ? w2 : w3;  // this step's kernel row 2
     WRow& n2 = b == 0 ? w3 : w2;  // the next step's
-    const bool more = s + 1 < S;
     XRow xa, xb;
+    // X(s+1) into X(s-1)'s buffer (every wave retired its reads of it at B'(s)), its pieces among rows 0..2's MFMAs;
+    // steps past the end issue the same number of zero pieces, so barriers and vmcnt counts stay uniform
     ldx(xa, b, 0);
     ldx(xb, b, 1);
+    issue_step(1, false, b ^ 1, I{}, std::integral_constant<int, 2>{});
     row_mma(0, xa, k2);
     ldx(xa, b, 2);
+    issue_step(1, false, b ^ 1, std::integral_constant<int, 2>{}, std::integral_constant<int, 4>{});
     row_mma(1, xb, k2);
     ldx(xb, b, 3);
+    issue_step(1, false, b ^ 1, std::integral_constant<int, 4>{}, NX{});
     row_mma(2, xa, k2);
     ldx(xa, b, 4);
     row_mma(3, xb, k2);
     sched_rows<FC, 12, 6, 6, 6, 0>();
-    if (more) {
-      sync(NX{});               // B(s+1): W(s+1) landed, X(s+1) may still fly
-      issue_step(2, true, b);   // W(s) lives in registers: its buffer takes W(s+2)
-    }
+    __builtin_amdgcn_sched_barrier(0);
+    sync(NX{});  // B(s+1): W(s+1) landed, X(s+1) may still fly
+    __builtin_amdgcn_sched_barrier(0);
+    // W(s) lives in registers: its buffer takes W(s+2), pieces among rows 4, 5's MFMAs
     ldx(xb, b, 5);
+    issue_step(2, true, b, I{}, std::integral_constant<int, 2>{});
     ldw(w0, b ^ 1, 0);  // kernel row 0 is dead after input row 3 (read anyway on the last step: unused)
+    issue_step(2, true, b, std::integral_constant<int, 2>{}, std::integral_constant<int, 4>{});
     ldw(n2, b ^ 1, 2);
     row_mma(4, xa, k2);
+    issue_step(2, true, b, std::integral_constant<int, 4>{}, NW{});
     ldw(w1, b ^ 1, 1);  // kernel row 1 is dead after input row 4
     row_mma(5, xb, k2);
     sched_tail<FC>();
-    if (more) {
-      sync(NW{});               // B'(s+1): X(s+1) landed, W(s+2) may still fly
-      issue_step(2, false, b);  // every wave is done with X(s)
-    }
+    __builtin_amdgcn_sched_barrier(0);
+    sync(NW{});  // B'(s+1): X(s+1) landed, W(s+2) may still fly
     if (g == nch - 1) {  // last granule of the tile: write it out, restart the accumulators
       epilogue(t0);
 #pragma unroll

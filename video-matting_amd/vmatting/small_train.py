@@ -270,9 +270,67 @@ class SmallTrainer(TrainerBase):
         self.apply_gradients()
         return b["loss"].clone()
 
+    def capture(self, cmp, bg, gt, raw_fg):
+        """Record one step's forward + loss and its backward as two HIP graphs (torch.cuda.CUDAGraph over the same
+        C-ABI launches) -> SmallTrainGraph; its step() replays both and runs the DDP exchange + Adam + re-pack eagerly
+        (TF's bias correction changes every step).  The graphs read the trainer's parameters, packs and buffers in
+        place.  A tiny UNetSmall step is ~110 launches of a few microseconds each: replay removes their host cost."""
+        return SmallTrainGraph(self, cmp, bg, gt, raw_fg)
+
     def params_numpy(self):
         """{scope: (w, b|None)} and {scope: (gamma, beta)} on the host (checkpoint / small.UNetSmall hand-off)."""
         conv = {s: (self.P[s, "w"].cpu().numpy(), self.P[s, "b"].cpu().numpy() if (s, "b") in self.P else None)
                 for s, _, _ in NEW_CONVS}
         bn = {s: (self.P[s, "gamma"].cpu().numpy(), self.P[s, "beta"].cpu().numpy()) for s, _, _ in NEW_CONVS}
         return conv, bn
+
+
+class SmallTrainGraph:
+    """SmallTrainer.capture's result: ``step(cmp, bg, gt, raw_fg)`` = SmallTrainer.step on graph replays."""
+
+    def __init__(self, trn, *batch):
+        if trn.sync_bn and torch.distributed.get_backend() != "nccl":
+            raise NotImplementedError("capture with sync_bn needs the nccl (RCCL) backend")
+        dev = trn.device
+        self.trn = trn
+        self.inputs = [(t if isinstance(t, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(t, np.float32)))
+                       .to(dev, torch.float32).contiguous().clone() for t in batch]
+        side = torch.cuda.Stream(device=dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):  # buffers, workspaces and the SyncBN batch count before capture
+            self._forward()
+            self._backward()
+        main = torch.cuda.current_stream(dev)
+        main.wait_stream(side)
+        torch.cuda.synchronize(dev)
+        for t in trn._b.values():  # allocated on the side stream, replayed on this one
+            for u in (t if isinstance(t, tuple) else (t,)):
+                u.record_stream(main)
+        self.g_fwd, self.g_bwd = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.g_fwd):
+            self._forward()
+        with torch.cuda.graph(self.g_bwd):
+            self._backward()
+
+    def _forward(self):
+        cmp, bg, gt, fg = self.inputs
+        t = self.trn
+        t.forward(cmp, bg)
+        t._b["loss"].copy_(ops.matting_loss(t._b["alpha"], gt, fg, bg, cmp))
+
+    def _backward(self):
+        cmp, bg, gt, fg = self.inputs
+        self.trn.grad.zero_()
+        self.trn.backward(gt, fg, bg, cmp)
+
+    def load(self, *batch):
+        for dst, src in zip(self.inputs, batch):
+            dst.copy_(src if isinstance(src, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(src, np.float32)))
+
+    def step(self, *batch):
+        if batch:
+            self.load(*batch)
+        self.g_fwd.replay()
+        self.g_bwd.replay()
+        self.trn.apply_gradients()
+        return self.trn._b["loss"].clone()
