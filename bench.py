@@ -749,7 +749,7 @@ def conv_roofline(prof, args):
     (2*H*W*9*cin*cout of each launch) / its average launch duration from HIP events on
     the launch stream, recorded over a K-step pass identical to the timed region (run right after it)."""
     per = {}
-    for fl, name, e0, e1 in prof:
+    for fl, name, e0, e1, *_ in prof:
         d = per.setdefault(name, [0, 0.0, 0])
         d[0] += fl
         d[1] += ms(e0, e1)
@@ -767,7 +767,7 @@ def conv_roofline(prof, args):
         per_step = len(prof) // max(1, args.steps)
         for i in range(per_step):
             rows = prof[i::per_step]
-            t_ms = sum(ms(e0, e1) for _, _, e0, e1 in rows) / len(rows)
+            t_ms = sum(ms(r[2], r[3]) for r in rows) / len(rows)
             log("  conv #%2d %-55s %.3f ms  %.1f TFLOP/s" % (i, rows[0][1], t_ms, rows[0][0] / (t_ms * 1e-3) / 1e12))
     for k, (f, tt, c) in sorted(per.items(), key=lambda kv: -kv[1][1]):
         log("%-58s %3d launches %.3f ms/step %.1f TFLOP/s" % (k, c, tt / args.steps, f / (tt * 1e-3) / 1e12))

@@ -1136,3 +1136,47 @@ def test_channel_banded_tiles_bit_identical(case):
         _lib.set_option("patch_persist", 1)
         _lib.set_option("rows_kernel", 1)
     assert torch.equal(outs[0], outs[1])
+
+
+THIN_CASES = [  # n, h, w, cin (per source x nsrc), cout, nsrc, out dtype, splitk
+    (8, 40, 40, 512, 16, 3, "f32", True), (8, 80, 80, 256, 8, 3, "f32", True), (8, 160, 160, 128, 4, 3, "f32", False),
+    (8, 320, 320, 64, 2, 3, "f32", False), (3, 37, 45, 96, 8, 1, "bf16", False), (2, 17, 70, 64, 2, 1, "bf16", True),
+    (1, 9, 5, 32, 16, 2, "f32", False)]
+
+
+@pytest.mark.parametrize("case", THIN_CASES)
+def test_thin_dma_bit_identical(case):
+    """The LDS-DMA narrow-cout kernel (conv3x3_thin_dma, 4 ring / tile configs) against conv3x3_thin: the same MFMA
+    order and epilogue, so bit-identical outputs (tower-major split sources, split-K partials, f32 and bf16 outputs,
+    ragged tiles, the training step's select shapes); and the oracle within the bf16 bound."""
+    from vmatting import _lib, ops
+    n, h, w, cin, cout, nsrc, od, splitk = case
+    rs = np.random.RandomState(n * 7 + h + cin + cout)
+    xd = T(rs.normal(size=(nsrc * n, h, w, cin)).astype(np.float32), torch.bfloat16)
+    wt = (rs.normal(size=(3, 3, nsrc * cin, cout)) * 0.05).astype(np.float32)
+    b = (rs.normal(size=cout) * 0.1).astype(np.float32)
+    pc = ops.PackedConv(wt, b, torch.bfloat16, DEV)
+    odt = torch.float32 if od == "f32" else torch.bfloat16
+
+    def run(cfg):
+        _lib.set_option("thin_dma", cfg)
+        out = torch.zeros((n, h, w, cout), dtype=odt, device=DEV)
+        src = ops.SourceConcat(xd, nsrc) if nsrc > 1 else xd
+        ops.conv3x3(src, pc, "none", out=out, splitk=splitk)
+        return out, _lib.last_conv_kernel()
+
+    try:
+        y0, k0 = run(0)
+        assert k0.startswith("vm::conv3x3_thin<"), k0
+        for cfg in (1, 2, 3, 4):
+            y1, k1 = run(cfg)
+            assert k1.startswith("vm::conv3x3_thin_dma<"), k1
+            assert torch.equal(y0, y1), (cfg, k1, (y0 - y1).abs().max().item())
+    finally:
+        _lib.set_option("thin_dma", 0)
+    if n * h * w > 200000:
+        return  # the oracle at the select shapes would take minutes; bit identity carries it from the small cases
+    xcat = np.concatenate([H(xd[s * n:(s + 1) * n]) for s in range(nsrc)], -1).astype(np.float64)
+    wb = torch.from_numpy(wt).to(torch.bfloat16).float().numpy().astype(np.float64)
+    ref = oops.conv3x3_same(xcat, wb) + b
+    assert relerr(H(y0), ref) < (1e-4 if od == "f32" else 1e-2)

@@ -197,15 +197,25 @@ def test_refine_softmax_f32_kernel(n, h, w, cin):
     xd = T(x)[..., :cin]
     try:
         got = ops.conv3x3(xd, pc, "softmax").clone()
-        assert _lib.last_conv_kernel() == "vm::conv3x3_first_softmax_f32<%d>" % cin, _lib.last_conv_kernel()
+        want = "vm::conv3x3_first_softmax_f32p<%d, 2, false, 0, 18>" % cin
+        assert _lib.last_conv_kernel() == want, _lib.last_conv_kernel()
         _lib.set_option("softmax_blocks", 3)
         assert torch.equal(ops.conv3x3(xd, pc, "softmax"), got)  # persistent walk, partial last round
+        # the pipelined kernel (next strip's MFMAs under this strip's softmax, direct stores) computes every output
+        # exactly as the r03 one (same K order, same softmax expression); also its 4-waves-per-SIMD build
+        _lib.set_option("softmax_blocks", 2048)
+        for v in (0, 1, 2, 3, 5):  # 0: the r03 kernel; 1..5 the pipelined one (3..5: store variants, cin 5)
+            _lib.set_option("softmax_f32p", v)
+            assert torch.equal(ops.conv3x3(xd, pc, "softmax"), got), v
+            assert ("softmax_f32p" in _lib.last_conv_kernel()) == (v > 0)
+        _lib.set_option("softmax_f32p", 4)
         _lib.set_option("softmax_kernel", 0)
         gen = ops.conv3x3(xd, pc, "softmax").clone()
         assert "first_softmax" not in _lib.last_conv_kernel()
     finally:
         _lib.set_option("softmax_kernel", 6)
         _lib.set_option("softmax_blocks", 2048)
+        _lib.set_option("softmax_f32p", 4)
     ref = oops.softmax_lastdim(oops.conv3x3_same(x[..., :cin].astype(np.float64), wt.astype(np.float64),
                                                  b.astype(np.float64)))
     g = got.cpu().numpy()

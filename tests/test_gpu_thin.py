@@ -112,8 +112,32 @@ def test_thin_persistent_walk_bit_identical(th, n, h, w, cin, cout, splitk):
         for rounds in (1, 0, 2):
             _lib.set_option("thin_rounds", rounds)
             outs.append(ops.conv3x3(x, pc, "relu", out_dtype=torch.float32, affine=False, splitk=splitk))
-            assert _lib.last_conv_kernel() == "vm::conv3x3_thin<%d>" % th
+            assert _lib.last_conv_kernel() == "vm::conv3x3_thin<%d, true>" % th
     finally:
         _lib.set_option("thin_rounds", 1)
         _lib.set_option("thin_th", 8)
     assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+
+
+@pytest.mark.parametrize("th", [8, 4, 16])
+@pytest.mark.parametrize("n,h,w,cin,cout,splitk", [(8, 80, 80, 768, 8, False), (3, 37, 45, 96, 2, True),
+                                                   (2, 40, 40, 1536, 16, True)])
+def test_thin_row_reuse_bit_identical(th, n, h, w, cin, cout, splitk):
+    """r04: thin_chunk reads each patch row's pixel fragments once for all the output rows they reach; per
+    accumulator the MFMAs still run taps 0..8 in order, so the outputs equal the tap-major loop's bit for bit."""
+    from vmatting import _lib, ops
+    rs = np.random.RandomState(n + cin + th)
+    x = torch.from_numpy(rs.normal(size=(n, h, w, cin)).astype(np.float32)).to(DEV, torch.bfloat16)
+    pc = ops.PackedConv(rs.normal(size=(3, 3, cin, cout)).astype(np.float32) / 40, rs.normal(size=cout).astype(
+        np.float32), "bf16", DEV)
+    outs = []
+    try:
+        _lib.set_option("thin_th", th)
+        for rr in (0, 1):
+            _lib.set_option("thin_rowreuse", rr)
+            outs.append(ops.conv3x3(x, pc, "none", out_dtype=torch.float32, affine=False, splitk=splitk))
+            assert _lib.last_conv_kernel() == "vm::conv3x3_thin<%d, %s>" % (th, "true" if rr else "false")
+    finally:
+        _lib.set_option("thin_rowreuse", 1)
+        _lib.set_option("thin_th", 8)
+    assert torch.equal(outs[0], outs[1])

@@ -763,6 +763,31 @@ def test_train_graph_step_equals_eager(dtype):
 
 
 @pytest.mark.slow
+def test_side_streams_bit_identical_bench_shape():
+    """the select chains write channel slices of the concat rows on side streams while the main stream's
+    upconv writes the neighbouring channels.  Every epilogue on this path (patch / thin / split-K reduce / bn_apply)
+    stores only inside its channel view: a whole 16-byte chunk only when the view is 16-byte aligned and the chunk
+    lies inside [coff, coff + c) (conv3x3.hip: y_vec && co + 8 <= cout), element-wise otherwise (upconv1 at channel
+    6 of its concat, the 2..16-channel selects) -- no read-modify-write of a neighbour's bytes.  Checked at the bench's 8 x 320^2 bf16 batch, where the kernels do overlap in time: three steps
+    with side streams and three on one stream leave bit-identical losses and variables."""
+    from vmatting.train import VideoTrainer
+    from vmatting.weights import synthetic_vgg16
+    vgg = synthetic_vgg16(0)
+    params = om.unet_simple_params(np.random.RandomState(1))
+    batches = [_batch(8, 320, 320, seed=20 + i) for i in range(3)]
+    res = []
+    for streams in (3, 0):
+        trn = VideoTrainer(vgg, "bf16", DEV, params=params, streams=streams)
+        assert bool(trn._side) == (streams > 0)
+        losses = [H(trn.step(*b)) for b in batches]
+        torch.cuda.synchronize()
+        res.append((losses, trn.flat.clone()))
+        del trn
+    assert all(np.array_equal(a, b) for a, b in zip(res[0][0], res[1][0])), (res[0][0], res[1][0])
+    assert torch.equal(res[0][1], res[1][1])
+
+
+@pytest.mark.slow
 def test_train_step_bf16_gradients_bench_shape():
     """the bf16 step's gradients at the bench's 8 x 320^2 batch, where the BN statistics run over
     many pixels per channel, against float64 autograd (run on the GPU: test infrastructure) on the trainer's own bf16

@@ -5,8 +5,9 @@
 #   3. --pmc FETCH_SIZE, 4. --pmc WRITE_SIZE (own passes)                                 -> profiles/<tag>_traffic.json
 #   5. --kernel-trace --stats of the config-3 record, one pass per (dtype, size)            -> profiles/<tag>_temporal_<dtype>_<HxW>_kernel_stats.csv
 #   6. --kernel-trace --stats of the config-5 training step alone (8 x 320^2, bf16)        -> profiles/<tag>_train_kernel_stats.csv
-#   7. the full bench (reads the profiles of 2-4)                                         -> gpurun_out/<tag>_bench.json
-# SKIP="fwd mfma traffic temporal train bench" skips passes.
+#   7. --kernel-trace --stats of the small_train.py step alone (8 x 320^2, bf16, graphs)   -> profiles/<tag>_train_small_kernel_stats.csv
+#   8. the full bench (reads the profiles of 2-4)                                         -> gpurun_out/<tag>_bench.json
+# SKIP="fwd mfma traffic temporal train train_small bench" skips passes.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 REPO=$(pwd)
 TAG=$1; shift
@@ -56,6 +57,12 @@ run 300 train.log rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/
     -- python3 "$REPO/bench.py" --only train --steps 20 --warmup 3 "$@"  # eager: side-stream select chains
 cp "$(find "$OUT/train" -name '*kernel_stats.csv' | head -n 1)" "$REPO/profiles/${TAG}_train_kernel_stats.csv"
 tail -n 1 "$OUT/train.log" > "$REPO/profiles/${TAG}_train.json"
+fi
+if ! skip train_small; then
+run 300 train_small.log rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/train_small" -o run \
+    -- python3 "$REPO/bench.py" --only train_small --steps 20 --warmup 3 "$@"
+cp "$(find "$OUT/train_small" -name '*kernel_stats.csv' | head -n 1)" "$REPO/profiles/${TAG}_train_small_kernel_stats.csv"
+tail -n 1 "$OUT/train_small.log" > "$REPO/profiles/${TAG}_train_small.json"
 fi
 cp "$REPO"/profiles/${TAG}_* "$REPO/gpurun_out/"
 skip bench && exit 0

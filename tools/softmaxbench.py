@@ -20,11 +20,14 @@ wt, bias = (rs.normal(size=(3, 3, 5, 64)) * 0.3).astype(np.float32), rs.normal(s
 pcs = {"bf16": ops.PackedConv(wt, bias, "bf16"), "fp32": ops.PackedConv(wt, bias, "fp32")}
 xs = {"bf16": xf.to(torch.bfloat16), "fp32": xf}
 out = torch.empty((1, h, w, 64), dtype=torch.float32, device="cuda")
-CFGS = [("bf16", 4, 1024), ("bf16", 5, 1024), ("bf16", 6, 1024), ("bf16", 6, 2048), ("bf16", 6, 4096),
-        ("fp32", 0, 1024), ("fp32", 6, 1024), ("fp32", 6, 2048), ("fp32", 6, 4096), ("bf16", 6, 2048)]
-for dt, k, blocks in CFGS:
+CFGS = [("bf16", 6, 2048, 0), ("fp32", 0, 1024, 0)] + [("fp32", 6, b, 0) for b in (1024, 2048, 4096)] + \
+    [("fp32", 6, 2048, p) for p in (1, 2, 3, 4, 5)]  # pipelined f32 kernel: one resident round whatever softmax_blocks
+if len(sys.argv) > 3 and sys.argv[3] == "fp32":
+    CFGS = CFGS[2:]
+for dt, k, blocks, f32p in CFGS:
     _lib.set_option("softmax_kernel", k)
     _lib.set_option("softmax_blocks", blocks)
+    _lib.set_option("softmax_f32p", f32p)
     x, pc = xs[dt], pcs[dt]
     nbytes = h * w * ((16 if dt == "bf16" else 32) + 256)
     fn = lambda: ops.conv3x3(x[..., :5], pc, "softmax", out=out)  # noqa: E731
@@ -42,3 +45,4 @@ for dt, k, blocks in CFGS:
         dt, k, blocks, _lib.last_conv_kernel(), ms * 1e3, nbytes / ms / 1e9), flush=True)
 _lib.set_option("softmax_kernel", 6)
 _lib.set_option("softmax_blocks", 2048)
+_lib.set_option("softmax_f32p", 4)

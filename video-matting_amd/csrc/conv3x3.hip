@@ -2152,6 +2152,25 @@ __global__ __launch_bounds__(512, 4) void conv3x3_first(ConvArgs a) {
   }
 }
 
+// {x[l], x[l ^ 16]} and {x[l], x[l ^ 32]} in VALU (v_permlane16/32_swap of x with itself) instead of ds_bpermute:
+// max and + of the pair are commutative, so the results equal fmaxf / + with __shfl_xor bit for bit
+__device__ __forceinline__ float max_xor16(float x) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float max_xor32(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float add_xor16(float x) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float add_xor32(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
 // ================================================================ refine conv4 + softmax (refine.py:27-32)
 // RefineNet's only live layer: a cin <= 8 -> 64 3x3 conv whose 64 logits per pixel go straight into
 // tf.nn.softmax and out as f32.  The conv is conv3x3_first's (one 16-byte chunk per pixel, 4 taps x 8 channels
@@ -2264,8 +2283,7 @@ __global__ __launch_bounds__(512, WL ? 4 : 2) void conv3x3_first_softmax(ConvArg
           mx = fmaxf(mx, v[fc][jj]);
         }
       }
-      mx = fmaxf(mx, __shfl_xor(mx, 16));
-      mx = fmaxf(mx, __shfl_xor(mx, 32));
+      mx = max_xor32(max_xor16(mx));
       float sum = 0.f;
 #pragma unroll
       for (int fc = 0; fc < 4; ++fc)
@@ -2274,8 +2292,7 @@ __global__ __launch_bounds__(512, WL ? 4 : 2) void conv3x3_first_softmax(ConvArg
           v[fc][jj] = expf(v[fc][jj] - mx);
           sum += v[fc][jj];
         }
-      sum += __shfl_xor(sum, 16);
-      sum += __shfl_xor(sum, 32);
+      sum = add_xor32(add_xor16(sum));
       const float inv = 1.f / sum;
       if constexpr (STG) {
         float* ws = stg + wave * 16 * SRF;
@@ -2359,8 +2376,7 @@ __device__ __forceinline__ void softmax_store_strip(const f32x4 (&acc)[4][2], co
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj) mx = fmaxf(mx, v[fc][jj]);
     }
-    mx = fmaxf(mx, __shfl_xor(mx, 16));
-    mx = fmaxf(mx, __shfl_xor(mx, 32));
+    mx = max_xor32(max_xor16(mx));
     float sum = 0.f;
 #pragma unroll
     for (int fc = 0; fc < 4; ++fc)
@@ -2369,8 +2385,7 @@ __device__ __forceinline__ void softmax_store_strip(const f32x4 (&acc)[4][2], co
         v[fc][jj] = __expf(v[fc][jj] - mx);
         sum += v[fc][jj];
       }
-    sum += __shfl_xor(sum, 16);
-    sum += __shfl_xor(sum, 32);
+    sum = add_xor32(add_xor16(sum));
     const float inv = 1.f / sum;
 #pragma unroll
     for (int fc = 0; fc < 4; ++fc)
@@ -2555,6 +2570,9 @@ __global__ __launch_bounds__(512, 4) void conv3x3_first_softmax_f32(ConvArgs a) 
   }
   const bool aff = a.scale || a.shift;  // else the accumulators start at the bias and hold the logits
   __syncthreads();  // the only block-wide barrier: the staged tables
+  int poff[NS];  // this lane's patch offset of every K step in registers (no dependent LDS load per step)
+#pragma unroll
+  for (int s = 0; s < NS; ++s) poff[s] = pl[s * 4 + q] + col;
   int i = blockIdx.x;
   float4 nv[2][2];
   if (i < ntiles) load_strip(tile_of(i), nv);
@@ -2581,8 +2599,7 @@ __global__ __launch_bounds__(512, 4) void conv3x3_first_softmax_f32(ConvArgs a) 
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
       const f32x4 w4 = wl[s * 64 + lane];
-      const int po = pl[s * 4 + q];
-      const float b0 = P[po + col], b1 = P[po + 16 + col];
+      const float b0 = P[poff[s]], b1 = P[poff[s] + 16];
       if constexpr (ABL & 2) {
         asm volatile("" ::"v"(w4[0]), "v"(w4[3]), "v"(b0), "v"(b1));
         continue;
@@ -2602,6 +2619,340 @@ __global__ __launch_bounds__(512, 4) void conv3x3_first_softmax_f32(ConvArgs a) 
     float* yb = reinterpret_cast<float*>(a.y) + a.y_coff + (((long)n * H + r) * W + c0) * (long)a.y_cstride;
     if (aff) softmax_store_strip<true>(acc, rmul, stg + wave * 16 * SRF, yb, a.y_cstride, W - c0, lane);
     else softmax_store_strip<false>(acc, rmul, stg + wave * 16 * SRF, yb, a.y_cstride, W - c0, lane);
+  }
+}
+
+// Pipelined form of conv3x3_first_softmax_f32 (r04): a wave computes strip i+1's MFMAs (accumulator set N) in the same
+// basic block as strip i's softmax + stores (set C), so the matrix pipe runs under the VALU-bound softmax instead of
+// beside it only when another wave happens to be in the other phase (ablations: the two phases of the non-pipelined
+// kernel overlapped by ~0.02 ms).  What makes one basic block possible: the per-wave patch is double-buffered, the
+// output is written straight from the accumulator lanes (per (16-pixel fragment, 16-channel group) one store of 16
+// pixels x 64 contiguous bytes: the four stores of a fragment fill its 16 whole pixels) through a buffer descriptor
+// whose out-of-range offsets drop the pixels past the frame — no LDS transpose, no wave barrier, no branch; the next
+// strip's global loads are clamped the same way.  Arithmetic per output is the non-pipelined kernel's (same K order,
+// same softmax expression), so results are bit-identical to it.
+template <int I, int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<I + 1, N>(f);
+  }
+}
+
+// The strip softmax of softmax_store_strip cut into 10 chunks, one per K step of the next strip's MFMAs, computed in
+// place in the accumulators C (acc[fc][fp]: pixel fp*16 + col, channels fc*16 + 4q .. +3); same operations in the same
+// order as softmax_store_strip (max over fc, jj; exp and the sum fc-major), so the probabilities are bit-identical.
+// Chunks: 0, 1 affine + row max of fragment 0 / 1; 2 the max across the 4 lane groups; 3..6 exp + partial sums (half a
+// fragment each); 7 the sums across lanes and their reciprocals; 8, 9 the scaled stores of fragment 0 / 1, straight
+// from the lanes (per 16-channel group one store of 16 pixels x 64 contiguous bytes; pixels past `valid` dropped by
+// the buffer descriptor's range check).
+// AUX: the stores' cache policy (0: through L2, where the four 64-byte pieces of a pixel's 256-byte row meet before
+// write-back; 2: non-temporal, each piece its own partial-line write)
+// AUX & 16: the scaled fragment goes through a wave-private LDS slab (16 pixels x 68 floats) and leaves as 4 stores
+// of 4 whole pixels (1 KB contiguous for a dense 64-channel output), with cache policy AUX & 15.
+template <bool AFF, int S, int ABL = 0, int AUX = 0>  // ABL (study build, timing only): 1 no stores, 4 no softmax math
+__device__ __forceinline__ void softmax_chunk(f32x4 (&C)[4][2], float (&mx)[2], float (&sm)[2], const float* rmul,
+                                              __amdgpu_buffer_rsrc_t yrs, int ycs, int valid, int lane,
+                                              float* slab = nullptr) {
+  const int col = lane & 15, q = lane >> 4;
+  if constexpr ((ABL & 4) && S < 8) {
+    return;
+  } else if constexpr (S == 0 || S == 1) {
+    constexpr int fp = S;
+    float m = -INFINITY;
+#pragma unroll
+    for (int fc = 0; fc < 4; ++fc) {
+      if constexpr (AFF) {
+        const float4 m4 = *reinterpret_cast<const float4*>(rmul + fc * 16 + 4 * q);
+        const float4 a4 = *reinterpret_cast<const float4*>(rmul + 64 + fc * 16 + 4 * q);
+        const float mul[4] = {m4.x, m4.y, m4.z, m4.w}, add[4] = {a4.x, a4.y, a4.z, a4.w};
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) C[fc][fp][jj] = fmaf(C[fc][fp][jj], mul[jj], add[jj]);
+      }
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) m = fmaxf(m, C[fc][fp][jj]);
+    }
+    mx[fp] = m;
+  } else if constexpr (S == 2) {
+#pragma unroll
+    for (int fp = 0; fp < 2; ++fp) mx[fp] = max_xor32(max_xor16(mx[fp]));
+  } else if constexpr (S >= 3 && S <= 6) {
+    constexpr int fp = (S - 3) / 2, h = (S - 3) % 2;
+    float t = h ? sm[fp] : 0.f;
+#pragma unroll
+    for (int fc = 2 * h; fc < 2 * h + 2; ++fc)
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        C[fc][fp][jj] = __expf(C[fc][fp][jj] - mx[fp]);
+        t += C[fc][fp][jj];
+      }
+    sm[fp] = t;
+  } else if constexpr (S == 7) {
+#pragma unroll
+    for (int fp = 0; fp < 2; ++fp) sm[fp] = 1.f / add_xor32(add_xor16(sm[fp]));
+  } else if constexpr ((S == 8 || S == 9) && (AUX & 16)) {
+    constexpr int fp = S - 8, SRF = 68;
+    const float inv = sm[fp];
+#pragma unroll
+    for (int fc = 0; fc < 4; ++fc)
+      *reinterpret_cast<f32x4*>(slab + col * SRF + fc * 16 + 4 * q) =
+          f32x4{C[fc][fp][0] * inv, C[fc][fp][1] * inv, C[fc][fp][2] * inv, C[fc][fp][3] * inv};
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {  // lane l: pixel 4 it + l / 16, channels 4 (l % 16) .. +3
+      const int px = 4 * it + (lane >> 4), ch = 4 * (lane & 15);
+      const f32x4 o = *reinterpret_cast<const f32x4*>(slab + px * SRF + ch);
+      const int pc = fp * 16 + px;
+      if constexpr (ABL & 1) {
+        asm volatile("" ::"v"(o[0]), "v"(o[3]));
+        continue;
+      }
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, o), yrs,
+                                             pc < valid ? (pc * ycs + ch) * 4 : OOB, 0, AUX & 15);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the slab's reads retire before fragment 1 rewrites it
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  } else if constexpr (S == 8 || S == 9) {
+    constexpr int fp = S - 8;
+    const float inv = sm[fp];
+    const int pc = fp * 16 + col;
+#pragma unroll
+    for (int fc = 0; fc < 4; ++fc) {
+      const f32x4 o = f32x4{C[fc][fp][0] * inv, C[fc][fp][1] * inv, C[fc][fp][2] * inv, C[fc][fp][3] * inv};
+      if constexpr (ABL & 1) {
+        asm volatile("" ::"v"(o[0]), "v"(o[3]));
+        continue;
+      }
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, o), yrs,
+                                             pc < valid ? (pc * ycs + fc * 16 + 4 * q) * 4 : OOB, 0, AUX);
+    }
+  }
+}
+
+template <int CIN, int MINW = 2, bool AFF = false, int ABL = 0, int AUX = 0>  // MINW: min waves per SIMD; AFF: a
+                                                                               // scale / shift epilogue; AUX: stores
+__global__ __launch_bounds__(512, MINW) void conv3x3_first_softmax_f32p(ConvArgs a) {  // epilogue; ABL: study only
+  constexpr int NS = (9 * CIN + 3) / 4;
+  constexpr int TH = 8, TW = 32, PW = TW + 2, SP = 3 * PW;
+  constexpr int WPF = (CIN * SP + 32 + 3) / 4 * 4;
+  constexpr int ZERO = CIN * SP;
+  __shared__ __attribute__((aligned(16))) f32x4 wl[NS * 64];
+  __shared__ int pl[NS * 4];
+  __shared__ __attribute__((aligned(16))) float rmul[2 * 64];
+  __shared__ __attribute__((aligned(16))) float pat[8 * 2 * WPF];
+  __shared__ __attribute__((aligned(16))) float stg[(AUX & 16) ? 8 * 16 * 68 : 4];  // AUX & 16: the store slabs
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  float* const slab = stg + ((AUX & 16) ? wave * 16 * 68 : 0);
+  const int H = a.H, W = a.W, cs = a.x_cstride;
+  const int th = (H + TH - 1) / TH, tw = (W + TW - 1) / TW;
+  const int ntiles = a.tiles_total;
+  const int G = (int)gridDim.x;
+  auto tile_of = [&](int i) {
+    const int base = (i / a.tiles_n) * a.tiles_n;
+    return base + a.tiles_n <= ntiles ? base + xcd_tile(i - base, a.tiles_n) : i;
+  };
+  // strip i of this wave: frame n, row r, first column c0 (i past the end: a zero strip below every frame)
+  auto strip = [&](int i, int& n, int& r, int& c0) __attribute__((always_inline)) {
+    const bool real = i < ntiles;
+    const int t = tile_of(real ? i : 0);
+    n = t / (th * tw);
+    const int srem = t - n * th * tw;
+    r = real ? (srem / tw) * TH + wave : H;
+    c0 = (srem - (srem / tw) * tw) * TW;
+  };
+  // strip coordinates are decoded outside the interleaved region (the decode's integer divisions expand with
+  // branches, which would split the basic block the schedule below needs)
+  struct SC {
+    int n, r, c0;
+  };
+  auto coords = [&](int i) __attribute__((always_inline)) {
+    SC c;
+    strip(i, c.n, c.r, c.c0);
+    return c;
+  };
+  auto load_strip = [&](const SC& sc, float4 (&v)[2][2]) __attribute__((always_inline)) {
+    const int n = sc.n, r = sc.r, c0 = sc.c0;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int e = lane + 64 * k;
+      const int pr = e / PW, pc = e - pr * PW;
+      const int h = r - 1 + pr, w = c0 - 1 + pc;
+      const bool ok = e < SP && (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
+      const float* xp = reinterpret_cast<const float*>(a.x) + a.x_coff + ((long)n * H + (ok ? h : 0)) * (long)W * cs +
+                        (long)(ok ? w : 0) * cs;
+      v[k][0] = ok ? *reinterpret_cast<const float4*>(xp) : make_float4(0.f, 0.f, 0.f, 0.f);
+      v[k][1] = ok && CIN > 4 ? *reinterpret_cast<const float4*>(xp + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  const int col = lane & 15, q = lane >> 4;
+  const float* Wt = reinterpret_cast<const float*>(a.w);
+  for (int e = tid; e < NS * 64; e += 512) {
+    const int st = e >> 6, l = e & 63;
+    const int kk = 4 * st + (l >> 4), co = l & 15;
+    const int tap = kk / CIN, c = kk - tap * CIN;
+    f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (kk < 9 * CIN)
+#pragma unroll
+      for (int fc = 0; fc < 4; ++fc) v[fc] = Wt[(long)(fc * 16 + co) * a.K_pad + tap * 8 + c];
+    wl[e] = v;
+  }
+  if (tid < NS * 4) {
+    const int kk = tid;
+    const int tap = kk / CIN, c = kk - tap * CIN;
+    pl[tid] = kk < 9 * CIN ? c * SP + (tap / 3) * PW + tap % 3 : ZERO;
+  }
+  float* P0 = pat + wave * 2 * WPF;
+  float* P1 = P0 + WPF;
+  if (lane < 32) {
+    P0[ZERO + lane] = 0.f;
+    P1[ZERO + lane] = 0.f;
+  }
+  if (tid < 64) {
+    const float sc = a.scale ? a.scale[tid] : 1.f;
+    rmul[tid] = sc;
+    rmul[64 + tid] = (a.bias ? a.bias[tid] : 0.f) * sc + (a.shift ? a.shift[tid] : 0.f);
+  }
+  constexpr bool aff = AFF;
+  __syncthreads();  // the only block-wide barrier: the staged tables
+  auto stage = [&](float* P, const float4 (&v)[2][2]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int e = lane + 64 * k;
+      const float vv[8] = {v[k][0].x, v[k][0].y, v[k][0].z, v[k][0].w, v[k][1].x, v[k][1].y, v[k][1].z, v[k][1].w};
+      if (e < SP)
+#pragma unroll
+        for (int c = 0; c < CIN; ++c) P[c * SP + e] = vv[c];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  };
+  // the MFMAs of strip P into N; with C, the 10 softmax chunks of the previous strip, one per K step: each step is its
+  // own scheduling region (sched_barrier), so the chunk's VALU work issues between that step's MFMAs, and the next
+  // step's fragments are read under them
+  // this lane's patch offsets of every K step (the pl table's entry for its k-slot q, plus its pixel column), held
+  // in registers: read from LDS inside the step they made each step's fragment reads wait on a dependent LDS load
+  int poff[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) poff[s] = pl[s * 4 + q] + col;
+  auto mma = [&](const float* P, f32x4 (&N)[4][2], f32x4* Cp, const __amdgpu_buffer_rsrc_t& yrs, int valid)
+      __attribute__((always_inline)) {
+    init_strip_acc(N, rmul, aff, q);
+    float mx[2] = {0.f, 0.f}, sm[2] = {0.f, 0.f};
+    f32x4 w4 = wl[lane];
+    float b0 = P[poff[0]], b1 = P[poff[0] + 16];
+    static_for<0, NS>([&](auto sc) __attribute__((always_inline)) {
+      constexpr int s = decltype(sc)::value;
+      f32x4 w4n = w4;
+      float b0n = b0, b1n = b1;
+      if constexpr (s + 1 < NS) {
+        w4n = wl[(s + 1) * 64 + lane];
+        b0n = P[poff[s + 1]];
+        b1n = P[poff[s + 1] + 16];
+      }
+      if constexpr (ABL & 2) {
+        asm volatile("" ::"v"(w4[0]), "v"(w4[3]), "v"(b0), "v"(b1));
+      } else {
+#pragma unroll
+        for (int fc = 0; fc < 4; ++fc) {
+          N[fc][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(w4[fc], b0, N[fc][0], 0, 0, 0);
+          N[fc][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(w4[fc], b1, N[fc][1], 0, 0, 0);
+        }
+      }
+      if (Cp) {
+        if constexpr (s < 10)
+          softmax_chunk<AFF, s, ABL, AUX>(*reinterpret_cast<f32x4(*)[4][2]>(Cp), mx, sm, rmul, yrs, a.y_cstride, valid,
+                                          lane, slab);
+      }
+      // the next step's fragment reads first (else hipcc sinks them to the step's end and the next step's first
+      // MFMA waits a whole LDS latency), then one MFMA per 3 VALU of the softmax chunk
+      if constexpr (s + 1 < NS) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+      if constexpr (s + 1 >= NS) __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      w4 = w4n;
+      b0 = b0n;
+      b1 = b1n;
+    });
+    if (Cp) {  // a short K loop (CIN < 4): the chunks left over
+      static_for<NS, 10>([&](auto sc) __attribute__((always_inline)) {
+        softmax_chunk<AFF, decltype(sc)::value, ABL, AUX>(*reinterpret_cast<f32x4(*)[4][2]>(Cp), mx, sm, rmul, yrs,
+                                                           a.y_cstride, valid, lane, slab);
+      });
+    }
+  };
+  auto yrs_of = [&](const SC& sc, int& valid) __attribute__((always_inline)) {
+    float* yb = reinterpret_cast<float*>(a.y) + a.y_coff +
+                (((long)sc.n * H + (sc.r < H ? sc.r : 0)) * W + sc.c0) * (long)a.y_cstride;
+    valid = sc.r < H ? W - sc.c0 : 0;
+    return __builtin_amdgcn_make_buffer_rsrc(uniform_ptr(yb), 0, 0x7ffffff0, 0x00020000);
+  };
+  // the last strip's softmax alone (no MFMAs left to hide it under)
+  auto store = [&](const SC& sc, f32x4 (&C)[4][2]) __attribute__((always_inline)) {
+    int valid;
+    const __amdgpu_buffer_rsrc_t yrs = yrs_of(sc, valid);
+    float mx[2] = {0.f, 0.f}, sm[2] = {0.f, 0.f};
+    static_for<0, 10>([&](auto sc2) __attribute__((always_inline)) {
+      softmax_chunk<AFF, decltype(sc2)::value, ABL, AUX>(C, mx, sm, rmul, yrs, a.y_cstride, valid, lane, slab);
+    });
+  };
+  int cur = blockIdx.x;
+  if (cur >= ntiles) return;
+  float4 nv[2][2];
+  SC s0 = coords(cur), s1 = coords(cur + G), s2;  // strips cur (accumulators C), cur + G (patch in flight)
+  load_strip(s0, nv);
+  stage(P0, nv);
+  load_strip(s1, nv);
+  f32x4 acc0[4][2], acc1[4][2];
+  {
+    int v0;
+    mma(P0, acc0, nullptr, yrs_of(s0, v0), 0);
+  }
+  // one step: strip cur's accumulators are in C; stage strip cur+G into buffer B and compute it into N while C's
+  // softmax and stores go out between its MFMAs
+  auto step = [&](auto bconst, f32x4 (&C)[4][2], f32x4 (&N)[4][2]) __attribute__((always_inline)) {
+    constexpr int b = decltype(bconst)::value;
+    float* Pn = b ? P1 : P0;
+    stage(Pn, nv);
+    s2 = coords(cur + 2 * G);
+    int valid;
+    const __amdgpu_buffer_rsrc_t yrs = yrs_of(s0, valid);
+    load_strip(s2, nv);
+    mma(Pn, N, &C[0][0], yrs, valid);
+    s0 = s1;
+    s1 = s2;
+    cur += G;
+  };
+  while (true) {
+    if (cur + G >= ntiles) {
+      store(s0, acc0);
+      break;
+    }
+    step(std::integral_constant<int, 1>{}, acc0, acc1);
+    if (cur + G >= ntiles) {
+      store(s0, acc1);
+      break;
+    }
+    step(std::integral_constant<int, 0>{}, acc1, acc0);
   }
 }
 
@@ -3287,7 +3638,35 @@ __global__ __launch_bounds__(256) void head_from_partials(const float* __restric
 // 32-channel chunk staged in LDS (swizzled 64-byte pixel rows), the next chunk's patch and filter held in registers
 // while this one is consumed.  Output lane l: pixel l % 16, channels 4 (l / 16) .. +3.  ksplit > 1 splits the
 // chunks over gridDim.y into raw f32 partials (splitk_reduce_kernel, fixed order).
-template <int TH>
+// One chunk of the narrow conv for a wave's RPW output rows: the chunk's 9 filter fragments are read once, and each
+// patch row's 6 pixel fragments (3 column shifts x 2 halves) once, each feeding the MFMAs of every output row it
+// reaches (kernel row kh = patch row - output row).  Per accumulator the MFMAs still run taps 0..8 in order (patch
+// rows ascend with kh), so the sums are those of the tap-major loop bit for bit, with (RPW + 2) * 6 fragment reads
+// per chunk instead of RPW * 18.
+template <int RPW, int PW>
+__device__ __forceinline__ void thin_chunk(const uint4* xs, const uint4* ws, int wv, int lane, f32x4 (&acc)[2 * RPW]) {
+  uint4 w[9];
+#pragma unroll
+  for (int tp = 0; tp < 9; ++tp) w[tp] = ws[tp * 64 + lane];  // A operand: co lane % 16, k = 8 (lane / 16) .. +7
+#pragma unroll
+  for (int pr = 0; pr < RPW + 2; ++pr) {
+#pragma unroll
+    for (int kw = 0; kw < 3; ++kw) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int pp = (wv * RPW + pr) * PW + h * 16 + (lane & 15) + kw;
+        const uint4 b = xs[pp * 4 + ((lane >> 4) ^ (((pp >> 2) & 1) << 1))];
+#pragma unroll
+        for (int r = 0; r < RPW; ++r) {
+          const int kh = pr - r;
+          if (kh >= 0 && kh < 3) mma16<uint16_t>(w[kh * 3 + kw], b, acc[2 * r + h]);
+        }
+      }
+    }
+  }
+}
+
+template <int TH, bool RR = true>  // RR: thin_chunk's row reuse (false: the r03 tap-major loop, for A/B)
 __global__ __launch_bounds__(256, TH <= 4 ? 4 : TH <= 8 ? 3 : 2) void conv3x3_thin(ConvArgs a) {
   constexpr int TW = 32, PW = TW + 2, PPIX = (TH + 2) * PW, PIECES = PPIX * 4, PPT = (PIECES + 255) / 256;
   constexpr int RPW = TH / 4;    // patch rows per wave
@@ -3386,17 +3765,21 @@ __global__ __launch_bounds__(256, TH <= 4 ? 4 : TH <= 8 ? 3 : 2) void conv3x3_th
       if (last) geo(ntile, nn, nr0, nc0, nxo);
       fetch(nn, nxo, last ? cb : cc + 1);
     }
+    if constexpr (RR) {
+      thin_chunk<RPW, PW>(xs, ws, wv, lane, acc);
+    } else {
 #pragma unroll
-    for (int tp = 0; tp < 9; ++tp) {
-      const uint4 w = ws[tp * 64 + lane];  // A operand: output channel lane % 16, k = 8 (lane / 16) .. +7
+      for (int tp = 0; tp < 9; ++tp) {
+        const uint4 w = ws[tp * 64 + lane];  // A operand: output channel lane % 16, k = 8 (lane / 16) .. +7
 #pragma unroll
-      for (int f = 0; f < 2 * RPW; ++f) {
-        const int rr = wv * RPW + (f >> 1), c = (f & 1) * 16 + (lane & 15);
-        const int pp = (rr + tp / 3) * PW + c + tp % 3;
-        const uint4 b = xs[pp * 4 + ((lane >> 4) ^ (((pp >> 2) & 1) << 1))];
-        mma16<uint16_t>(w, b, acc[f]);
+        for (int f = 0; f < 2 * RPW; ++f) {
+          const int rr = wv * RPW + (f >> 1), c = (f & 1) * 16 + (lane & 15);
+          const int pp = (rr + tp / 3) * PW + c + tp % 3;
+          const uint4 b = xs[pp * 4 + ((lane >> 4) ^ (((pp >> 2) & 1) << 1))];
+          mma16<uint16_t>(w, b, acc[f]);
+        }
+        __builtin_amdgcn_sched_barrier(0);  // one tap's fragments live at a time (registers: the prefetch in flight)
       }
-      __builtin_amdgcn_sched_barrier(0);  // one tap's fragments live at a time (registers: the prefetch is in flight)
     }
     if (last) {  // the tile's epilogue, straight from registers (no LDS: the next step's commit may follow)
       if (co0 < a.cout) {
@@ -3436,6 +3819,147 @@ __global__ __launch_bounds__(256, TH <= 4 ? 4 : TH <= 8 ? 3 : 2) void conv3x3_th
 #pragma unroll
     for (int i = 0; i < PPT; ++i) xo[i] = nxo[i];
   }
+}
+
+// LDS-DMA form of conv3x3_thin (r04).  The select convs are a stream over 192..1536-channel tower features (1.3 GB
+// per training step) and conv3x3_thin ran them at 1.1-2.8 TB/s: one chunk in flight per block, its patch and filter
+// held in registers from the end of one chunk's compute to the start of the next, so every chunk exposed most of
+// the load latency.  Here chunk t+S-1's patch and filter are DMA'd (buffer_load ... lds) into an S-slot LDS ring
+// while chunk t computes: S-1 chunks in flight per block, no registers held.  One raw barrier per chunk, after the
+// wave's own DMAs of chunk t have landed (counted vmcnt: every thread issues exactly PPT + WPT pieces per step;
+// steps past the end load out-of-range zeros) and its fragment reads of chunk t-1 have retired (lgkmcnt(0): the
+// slot the next DMA overwrites).  The patch swizzle is applied on the source side (LDS position p*4 + q holds
+// piece (p, q ^ swz(p))); MFMA order and epilogue are conv3x3_thin's, so results are bit-identical to it.
+template <int TH, int S>
+__global__ __launch_bounds__(256, 1) void conv3x3_thin_dma(ConvArgs a) {
+  constexpr int TW = 32, PW = TW + 2, PPIX = (TH + 2) * PW, PIECES = PPIX * 4, PPT = (PIECES + 255) / 256;
+  constexpr int RPW = TH / 4;
+  constexpr int WPIECES = 9 * 16 * 4, WPT = (WPIECES + 255) / 256;
+  constexpr int XS = PPT * 256 * 16, WS = WPT * 256 * 16, SLOT = XS + WS, NP = PPT + WPT;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int tw = (a.W + TW - 1) / TW, th = (a.H + TH - 1) / TH;
+  const int ntiles = a.tiles_total;
+  const int nch = a.cin_pad / 32;
+  int cb = 0, ce = nch;
+  if (a.ksplit > 1) {
+    const int per = (nch + a.ksplit - 1) / a.ksplit;
+    cb = blockIdx.y * per;
+    ce = min(nch, cb + per);
+  }
+  if (cb >= ce || (int)blockIdx.x >= ntiles) return;
+  const int nsteps_per_tile = ce - cb;
+  // step j of this block: tile blockIdx.x + (j / nsteps) * gridDim.x, chunk cb + j % nsteps
+  const int ntile_blk = (ntiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
+  const int nsteps = ntile_blk * nsteps_per_tile;
+  const __amdgpu_buffer_rsrc_t wrs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.w), 0, 0x7ffffff0, 0x00020000);
+  const uint32_t lds0 = lds_addr(smem);
+  // DMA of step j into slot j % S (j >= nsteps: out-of-range zeros, so every step issues NP pieces)
+  auto issue = [&](int j) __attribute__((always_inline)) {
+    const bool real = j < nsteps;
+    const int jj = real ? j : 0;
+    const int t = (int)blockIdx.x + (jj / nsteps_per_tile) * (int)gridDim.x;
+    const int cc = cb + jj % nsteps_per_tile;
+    int tt = t;
+    const int tx = tt % tw;
+    tt /= tw;
+    const int ty = tt % th;
+    const int n = tt / th;
+    const int r0 = ty * TH, c0 = tx * TW;
+    const uint16_t* Xn = reinterpret_cast<const uint16_t*>(a.x) + a.x_coff + (long)n * a.H * a.W * a.x_cstride +
+                         src_chan(a, cc * 32);
+    const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(uniform_ptr(const_cast<uint16_t*>(Xn)), 0,
+                                                                         0x7ffffff0, 0x00020000);
+    const uint32_t slot = __builtin_amdgcn_readfirstlane(lds0 + (uint32_t)((j % S) * SLOT));
+#pragma unroll
+    for (int i = 0; i < PPT; ++i) {
+      const int id = tid + i * 256;
+      const int p = id >> 2, qq = id & 3;
+      const int q = qq ^ (((p >> 2) & 1) << 1);  // the piece whose swizzled home is LDS position id
+      const int pr = p / PW, pc = p - pr * PW;
+      const int yy = r0 - 1 + pr, xx = c0 - 1 + pc;
+      const bool ok = real & (id < PIECES) & ((unsigned)yy < (unsigned)a.H) & ((unsigned)xx < (unsigned)a.W);
+      const int off = ((yy * a.W + xx) * a.x_cstride + q * 8) * 2;  // (32-bit: checked by the host)
+      glds16(xrs, slot + (uint32_t)((i * 256 + wv * 64) * 16), ok ? off : OOB);
+    }
+#pragma unroll
+    for (int i = 0; i < WPT; ++i) {
+      const int id = tid + i * 256;
+      const bool ok = real & (id < WPIECES);
+      const int off = ((id & 15) * a.K_pad + (cc * 9 + (id >> 6)) * 32 + ((id >> 4) & 3) * 8) * 2;
+      glds16(wrs, slot + (uint32_t)(XS + (i * 256 + wv * 64) * 16), ok ? off : OOB);
+    }
+  };
+  const int co0 = 4 * (lane >> 4);
+  const bool splitk = a.ksplit > 1;
+  float mul[4], add[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int co = min(co0 + j, a.cout - 1);
+    const float sc = (a.scale && !splitk) ? a.scale[co] : 1.f;
+    mul[j] = sc;
+    add[j] = splitk ? 0.f : (a.bias ? a.bias[co] : 0.f) * sc + (a.shift ? a.shift[co] : 0.f);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the epilogue constants: nothing older in the DMA counts
+#pragma unroll
+  for (int j = 0; j < S - 1; ++j) issue(j);
+  f32x4 acc[2 * RPW];
+#pragma unroll
+  for (int f = 0; f < 2 * RPW; ++f) acc[f] = f32x4{0.f, 0.f, 0.f, 0.f};
+  int tile = blockIdx.x;
+  for (int j = 0; j < nsteps; ++j) {
+    // chunk j landed (the S-2 younger steps may stay in flight); this wave's reads of slot (j-1) % S retired
+    if constexpr (S == 2) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    else wait_vm((S - 2) * NP);
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    issue(j + S - 1);  // into slot (j - 1) % S, free since the barrier
+    const uint4* xs = reinterpret_cast<const uint4*>(smem + (j % S) * SLOT);
+    const uint4* ws = reinterpret_cast<const uint4*>(smem + (j % S) * SLOT + XS);
+    thin_chunk<RPW, PW>(xs, ws, wv, lane, acc);
+    if ((j + 1) % nsteps_per_tile == 0) {  // the tile's epilogue (conv3x3_thin's), straight from registers
+      int t = tile;
+      const int tx = t % tw;
+      t /= tw;
+      const int ty = t % th;
+      const int n = t / th;
+      const int r0 = ty * TH, c0 = tx * TW;
+      if (co0 < a.cout) {
+#pragma unroll
+        for (int f = 0; f < 2 * RPW; ++f) {
+          const int row = r0 + wv * RPW + (f >> 1), col = c0 + (f & 1) * 16 + (lane & 15);
+          if (row >= a.H || col >= a.W) continue;
+          const long m = ((long)n * a.H + row) * a.W + col;
+          if (splitk) {
+            float* d = a.part + ((long)blockIdx.y * a.M + m) * a.cout + co0;
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj)
+              if (co0 + jj < a.cout) d[jj] = acc[f][jj];
+            continue;
+          }
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) {
+            if (co0 + jj >= a.cout) break;
+            float v = fmaf(acc[f][jj], mul[jj], add[jj]);
+            if (a.act == VM_ACT_RELU) v = fmaxf(v, 0.f);
+            else if (a.act == VM_ACT_SIGMOID) v = sigmoid_precise(v);
+            const long o = m * a.y_cstride + a.y_coff + co0 + jj;
+            if (a.y_dtype == VM_BF16) reinterpret_cast<uint16_t*>(a.y)[o] = f2bf(v);
+            else reinterpret_cast<float*>(a.y)[o] = v;
+          }
+        }
+      }
+#pragma unroll
+      for (int f = 0; f < 2 * RPW; ++f) acc[f] = f32x4{0.f, 0.f, 0.f, 0.f};
+      tile += gridDim.x;
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing zero-fill DMAs land before the block exits
+}
+template <int TH, int S>
+constexpr int thin_dma_lds() {
+  constexpr int PPT = ((TH + 2) * 34 * 4 + 255) / 256, WPT = (9 * 16 * 4 + 255) / 256;
+  return S * (PPT + WPT) * 256 * 16;
 }
 
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ part, int ks, long M, int cout,
@@ -3666,14 +4190,51 @@ static int thin_resident() {
   (void)hipGetDevice(&dev);
   if (dev != dev_seen) {
     int per_cu = 0, n_cu = 0;
-    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(&conv3x3_thin<TH>),
-                                                                256, 0);
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &per_cu, reinterpret_cast<const void*>(&conv3x3_thin<TH, true>), 256, 0);
     if (e == hipSuccess) e = hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
     if (e != hipSuccess) return -1;
     resident = per_cu * n_cu;
     dev_seen = dev;
   }
   return resident;
+}
+// the LDS-DMA thin kernel (conv3x3_thin_dma): 0 off; 1 = 8-row tiles, 3-slot ring; 2 = 4-row tiles, 4 slots;
+// 3 = 4-row tiles, 3 slots; 4 = 8-row tiles, 2 slots.  A resident grid of thin_dma_rounds x blocks per CU x CUs
+static long g_thin_dma = 0, g_thin_dma_rounds = 1;
+static long g_thin_rowreuse = 1;  // conv3x3_thin: thin_chunk's row reuse (0: the r03 tap-major loop)
+template <int TH, int S>
+static int launch_thin_dma_cfg(ConvArgs& a, long n, int ks, hipStream_t st) {
+  constexpr int lds = thin_dma_lds<TH, S>();
+  static int dev_seen = -1, resident = 0;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (dev != dev_seen) {
+    const void* fn = reinterpret_cast<const void*>(&conv3x3_thin_dma<TH, S>);
+    int per_cu = 0, n_cu = 0;
+    hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 256, lds);
+    if (e == hipSuccess) e = hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
+    if (e != hipSuccess) return fail(VM_EHIP, "conv3x3_thin_dma: %s", hipGetErrorString(e));
+    resident = per_cu * n_cu;
+    dev_seen = dev;
+  }
+  long gx = n * ((a.H + TH - 1) / TH) * (long)((a.W + 31) / 32);
+  if (gx > 0x7fffffffL) return fail(VM_EUNSUPPORTED, "conv3x3_thin_dma: too many tiles");
+  a.tiles_total = (int)gx;
+  const long cap = g_thin_dma_rounds * (long)resident / ks;
+  if (gx > cap) gx = cap < 1 ? 1 : cap;
+  snprintf(g_last_kernel, sizeof g_last_kernel, "vm::conv3x3_thin_dma<%d, %d>", TH, S);
+  hipLaunchKernelGGL((conv3x3_thin_dma<TH, S>), dim3((unsigned)gx, ks), dim3(256), lds, st, a);
+  return check_launch("conv3x3_thin_dma");
+}
+static int launch_thin_dma(ConvArgs& a, long n, int ks, hipStream_t st) {
+  switch (g_thin_dma) {
+    case 2: return launch_thin_dma_cfg<4, 4>(a, n, ks, st);
+    case 3: return launch_thin_dma_cfg<4, 3>(a, n, ks, st);
+    case 4: return launch_thin_dma_cfg<8, 2>(a, n, ks, st);
+    default: return launch_thin_dma_cfg<8, 3>(a, n, ks, st);
+  }
 }
 static int dispatch_thin(ConvArgs& a, long n, hipStream_t st) {
   const int th = (int)g_thin_th;
@@ -3688,11 +4249,27 @@ static int dispatch_thin(ConvArgs& a, long n, hipStream_t st) {
     const long cap = g_thin_rounds * (long)res / ks;
     if (gx > cap) gx = cap < 1 ? 1 : cap;
   }
-  snprintf(g_last_kernel, sizeof g_last_kernel, "vm::conv3x3_thin<%d>", th);
+  if (g_thin_dma) {
+    const int rc = launch_thin_dma(a, n, ks, st);
+    if (rc) return rc;
+    if (a.ksplit <= 1) return VM_OK;
+    const long work = a.M * ((a.cout + 3) / 4);
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(grid_for(work, 256)), dim3(256), 0, st, a.part, a.ksplit, a.M,
+                       a.cout, a.bias, a.scale, a.shift, a.act, a.y, a.y_dtype, a.y_cstride, a.y_coff);
+    return check_launch("splitk_reduce");
+  }
   const dim3 grid((unsigned)gx, ks);
-  if (th == 16) hipLaunchKernelGGL(conv3x3_thin<16>, grid, dim3(256), 0, st, a);
-  else if (th == 4) hipLaunchKernelGGL(conv3x3_thin<4>, grid, dim3(256), 0, st, a);
-  else hipLaunchKernelGGL(conv3x3_thin<8>, grid, dim3(256), 0, st, a);
+  if (!g_thin_rowreuse) {
+    snprintf(g_last_kernel, sizeof g_last_kernel, "vm::conv3x3_thin<%d, false>", th);
+    if (th == 16) hipLaunchKernelGGL((conv3x3_thin<16, false>), grid, dim3(256), 0, st, a);
+    else if (th == 4) hipLaunchKernelGGL((conv3x3_thin<4, false>), grid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((conv3x3_thin<8, false>), grid, dim3(256), 0, st, a);
+  } else {
+    snprintf(g_last_kernel, sizeof g_last_kernel, "vm::conv3x3_thin<%d, true>", th);
+    if (th == 16) hipLaunchKernelGGL((conv3x3_thin<16, true>), grid, dim3(256), 0, st, a);
+    else if (th == 4) hipLaunchKernelGGL((conv3x3_thin<4, true>), grid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((conv3x3_thin<8, true>), grid, dim3(256), 0, st, a);
+  }
   int rc = check_launch("conv3x3_thin");
   if (rc || a.ksplit <= 1) return rc;
   const long work = a.M * ((a.cout + 3) / 4);
@@ -3961,6 +4538,8 @@ static int launch_first_softmax(ConvArgs& a, hipStream_t st) {
   return check_launch("conv3x3_first_softmax");
 }
 
+static long g_softmax_f32p = 4;  // the pipelined f32 refine kernel's variant (softmax_f32p option); 0: the r03 one
+
 static int launch_first_softmax_f32(ConvArgs& a, int cin, hipStream_t st) {
   const long N = a.M / ((long)a.H * a.W);
   const long sp = N * ((a.H + 7) / 8) * ((a.W + 31) / 32);
@@ -3968,6 +4547,69 @@ static int launch_first_softmax_f32(ConvArgs& a, int cin, hipStream_t st) {
   a.tiles_total = (int)sp;
   const int grid = (int)std::min<long>(sp, g_softmax_blocks);
   a.tiles_n = grid;
+  if (g_softmax_f32p && !a.scale && !a.shift) {  // (a scale / shift epilogue: the r03 kernel below)
+    // one resident round (2 waves per SIMD: one 512-thread block per CU); softmax_blocks caps it for tests
+    static int n_cu = 0;
+    if (!n_cu) {
+      int dev = 0;
+      (void)hipGetDevice(&dev);
+      if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0)
+        return fail(VM_EHIP, "conv3x3_first_softmax_f32p: CU count query failed");
+    }
+    const int gp = (int)std::min<long>(std::min<long>(sp, n_cu), g_softmax_blocks);
+    a.tiles_n = gp;
+#define VM_SMP(C)                                                                             \
+  case C:                                                                                    \
+    snprintf(g_last_kernel, sizeof g_last_kernel, "vm::conv3x3_first_softmax_f32p<%d, 2, false, 0, 18>", C); \
+    hipLaunchKernelGGL((conv3x3_first_softmax_f32p<C, 2, false, 0, 18>), dim3(gp), dim3(512), 0, st, a);     \
+    break;
+#ifdef VM_STUDY
+    if (cin == 5 && g_softmax_abl) {  // timing ablations (garbage results): 1 no stores, 2 no MFMA, 4 no softmax
+      snprintf(g_last_kernel, sizeof g_last_kernel, "vm::conv3x3_first_softmax_f32p<5, 2, false, %ld>", g_softmax_abl);
+      switch (g_softmax_abl) {
+        case 1: hipLaunchKernelGGL((conv3x3_first_softmax_f32p<5, 2, false, 1>), dim3(gp), dim3(512), 0, st, a); break;
+        case 2: hipLaunchKernelGGL((conv3x3_first_softmax_f32p<5, 2, false, 2>), dim3(gp), dim3(512), 0, st, a); break;
+        case 3: hipLaunchKernelGGL((conv3x3_first_softmax_f32p<5, 2, false, 3>), dim3(gp), dim3(512), 0, st, a); break;
+        case 4: hipLaunchKernelGGL((conv3x3_first_softmax_f32p<5, 2, false, 4>), dim3(gp), dim3(512), 0, st, a); break;
+        case 5: hipLaunchKernelGGL((conv3x3_first_softmax_f32p<5, 2, false, 5>), dim3(gp), dim3(512), 0, st, a); break;
+        case 6: hipLaunchKernelGGL((conv3x3_first_softmax_f32p<5, 2, false, 6>), dim3(gp), dim3(512), 0, st, a); break;
+        default: hipLaunchKernelGGL((conv3x3_first_softmax_f32p<5, 2, false, 7>), dim3(gp), dim3(512), 0, st, a); break;
+      }
+      return check_launch("conv3x3_first_softmax_f32p");
+    }
+#endif
+    if (cin == 5 && g_softmax_f32p == 2) {
+      snprintf(g_last_kernel, sizeof g_last_kernel, "vm::conv3x3_first_softmax_f32p<5, 4>");
+      hipLaunchKernelGGL((conv3x3_first_softmax_f32p<5, 4>), dim3(gp), dim3(512), 0, st, a);
+      return check_launch("conv3x3_first_softmax_f32p");
+    }
+    if (cin == 5 && g_softmax_f32p >= 4) {  // LDS-transposed whole-pixel stores: 4 non-temporal, 5 through L2
+      if (g_softmax_f32p == 4) {
+        snprintf(g_last_kernel, sizeof g_last_kernel, "vm::conv3x3_first_softmax_f32p<5, 2, false, 0, 18>");
+        hipLaunchKernelGGL((conv3x3_first_softmax_f32p<5, 2, false, 0, 18>), dim3(gp), dim3(512), 0, st, a);
+      } else {
+        snprintf(g_last_kernel, sizeof g_last_kernel, "vm::conv3x3_first_softmax_f32p<5, 2, false, 0, 16>");
+        hipLaunchKernelGGL((conv3x3_first_softmax_f32p<5, 2, false, 0, 16>), dim3(gp), dim3(512), 0, st, a);
+      }
+      return check_launch("conv3x3_first_softmax_f32p");
+    }
+    if (cin == 5 && g_softmax_f32p == 1) {  // stores straight from the accumulator lanes through L2 (A/B)
+      snprintf(g_last_kernel, sizeof g_last_kernel, "vm::conv3x3_first_softmax_f32p<5>");
+      hipLaunchKernelGGL((conv3x3_first_softmax_f32p<5>), dim3(gp), dim3(512), 0, st, a);
+      return check_launch("conv3x3_first_softmax_f32p");
+    }
+    if (cin == 5 && g_softmax_f32p == 3) {  // non-temporal stores (A/B)
+      snprintf(g_last_kernel, sizeof g_last_kernel, "vm::conv3x3_first_softmax_f32p<5, 2, false, 0, 2>");
+      hipLaunchKernelGGL((conv3x3_first_softmax_f32p<5, 2, false, 0, 2>), dim3(gp), dim3(512), 0, st, a);
+      return check_launch("conv3x3_first_softmax_f32p");
+    }
+    switch (cin) {
+      VM_SMP(1) VM_SMP(2) VM_SMP(3) VM_SMP(4) VM_SMP(5) VM_SMP(6) VM_SMP(7) VM_SMP(8)
+      default: return fail(VM_EINVAL, "conv3x3_first_softmax_f32p: cin %d", cin);
+    }
+#undef VM_SMP
+    return check_launch("conv3x3_first_softmax_f32p");
+  }
 #define VM_SMF(C)                                                                            \
   case C:                                                                                   \
     snprintf(g_last_kernel, sizeof g_last_kernel, "vm::conv3x3_first_softmax_f32<%d>", C); \
@@ -4045,6 +4687,12 @@ extern "C" int vm_set_option(const char* key, long value) {
     g_head_th = value;
     return VM_OK;
   }
+  if (!strcmp(key, "softmax_f32p")) {  // 0 the r03 kernel; 1 pipelined; 2 its 4-waves-per-SIMD build; 3 NT stores;
+                                       // 4 / 5 LDS-transposed whole-pixel stores, NT / through L2
+    if (value < 0 || value > 5) return fail(VM_EINVAL, "softmax_f32p must be 0..5");
+    g_softmax_f32p = value;
+    return VM_OK;
+  }
   if (!strcmp(key, "cband")) {
     if (value < 0 || value > 2) return fail(VM_EINVAL, "cband must be 0, 1 or 2");
     g_cband = value;
@@ -4098,6 +4746,21 @@ extern "C" int vm_set_option(const char* key, long value) {
   if (!strcmp(key, "thin_th")) {
     if (value != 4 && value != 8 && value != 16) return fail(VM_EINVAL, "thin_th must be 4, 8 or 16");
     g_thin_th = value;
+    return VM_OK;
+  }
+  if (!strcmp(key, "thin_rowreuse")) {
+    if (value < 0 || value > 1) return fail(VM_EINVAL, "thin_rowreuse must be 0 or 1");
+    g_thin_rowreuse = value;
+    return VM_OK;
+  }
+  if (!strcmp(key, "thin_dma")) {  // 0: conv3x3_thin; 1..4: conv3x3_thin_dma configs (launch_thin_dma)
+    if (value < 0 || value > 4) return fail(VM_EINVAL, "thin_dma must be 0..4");
+    g_thin_dma = value;
+    return VM_OK;
+  }
+  if (!strcmp(key, "thin_dma_rounds")) {
+    if (value < 1 || value > 64) return fail(VM_EINVAL, "thin_dma_rounds must be 1..64");
+    g_thin_dma_rounds = value;
     return VM_OK;
   }
   if (!strcmp(key, "thin_kernel")) {

@@ -57,6 +57,14 @@ struct ConvArgs {
   int y1_cstride, y1_coff;
 };
 
+// a pointer every lane holds the same value of, moved to SGPRs (buffer descriptors must be scalar)
+template <typename P>
+__device__ __forceinline__ P* uniform_ptr(P* p) {
+  const uint64_t v = reinterpret_cast<uint64_t>(p);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return reinterpret_cast<P*>(((uint64_t)hi << 32) | lo);
+}
+
 // element offset of input channel c (relative to the view's channel 0) under the source split
 __device__ __forceinline__ long src_chan(const ConvArgs& a, int c) {
   if (a.x_src_c <= 0) return c;

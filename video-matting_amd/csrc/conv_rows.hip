@@ -85,14 +85,6 @@ __device__ __forceinline__ void sched_tail() {
   sched_spread<row_mfmas<FC>(5), 3 * FC>();
 }
 
-// a pointer every lane holds the same value of, moved to SGPRs (buffer descriptors must be scalar)
-template <typename P>
-__device__ __forceinline__ P* uniform_ptr(P* p) {
-  const uint64_t v = reinterpret_cast<uint64_t>(p);
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
-  return reinterpret_cast<P*>(((uint64_t)hi << 32) | lo);
-}
-
 struct RowTile {
   int n, r0, c0, n0;
 };

@@ -226,7 +226,8 @@ def conv3x3(x, pc, act="none", out=None, out_dtype=None, affine=None, pool_out=N
         check(rc, "conv3x3")
         if prof is not None:
             ev1.record()
-            prof.append((2 * n * h * w * 9 * pc.cin * pc.cout, _lib.last_conv_kernel(), ev0, ev1))
+            prof.append((2 * n * h * w * 9 * pc.cin * pc.cout, _lib.last_conv_kernel(), ev0, ev1,
+                         (n, h, w, pc.cin, pc.cout)))
         return out
     xv, yv = nhwc(x), nhwc(out)
     prof = _CONV_PROFILE
@@ -248,7 +249,8 @@ def conv3x3(x, pc, act="none", out=None, out_dtype=None, affine=None, pool_out=N
                                     _ptr(shift), _lib.ACT[act], ctypes.byref(yv), stream_handle()), "conv3x3")
     if prof is not None:
         ev1.record()
-        prof.append((2 * n * h * w * 9 * pc.cin * pc.cout, _lib.last_conv_kernel(), ev0, ev1))
+        prof.append((2 * n * h * w * 9 * pc.cin * pc.cout, _lib.last_conv_kernel(), ev0, ev1,
+                     (n, h, w, pc.cin, pc.cout)))
     if pool_out is not None and not fused:
         maxpool2x2(out, out=pool_out)
     return out
