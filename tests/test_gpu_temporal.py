@@ -204,10 +204,11 @@ def test_refine_softmax_f32_kernel(n, h, w, cin):
         # the pipelined kernel (next strip's MFMAs under this strip's softmax, direct stores) computes every output
         # exactly as the r03 one (same K order, same softmax expression); also its 4-waves-per-SIMD build
         _lib.set_option("softmax_blocks", 2048)
-        for v in (0, 1, 2, 3, 5):  # 0: the r03 kernel; 1..5 the pipelined one (3..5: store variants, cin 5)
-            _lib.set_option("softmax_f32p", v)
-            assert torch.equal(ops.conv3x3(xd, pc, "softmax"), got), v
-            assert ("softmax_f32p" in _lib.last_conv_kernel()) == (v > 0)
+        for v in (0, 1, 2, 3, 5, 6):  # 0: the r03 kernel; 1..5 the pipelined one (3..5: store variants, cin 5);
+            _lib.set_option("softmax_f32p", v)  # 6: its row-ring form
+            assert torch.equal(ops.conv3x3(xd, pc, "softmax"), got), (v, _lib.last_conv_kernel())
+            k = _lib.last_conv_kernel()
+            assert ("softmax_f32p" in k) == (0 < v < 6) and ("softmax_f32r" in k) == (v == 6), (v, k)
         _lib.set_option("softmax_f32p", 4)
         _lib.set_option("softmax_kernel", 0)
         gen = ops.conv3x3(xd, pc, "softmax").clone()

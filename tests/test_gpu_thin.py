@@ -141,3 +141,24 @@ def test_thin_row_reuse_bit_identical(th, n, h, w, cin, cout, splitk):
         _lib.set_option("thin_rowreuse", 1)
         _lib.set_option("thin_th", 8)
     assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("n,h,w,cin,cout,splitk", [(8, 320, 320, 192, 2, False), (8, 80, 80, 768, 8, True),
+                                                   (3, 37, 45, 96, 4, False)])
+def test_thin_xcd_walk_bit_identical(n, h, w, cin, cout, splitk):
+    """r04: the XCD-banded tile walk (each XCD's blocks take a contiguous eighth of the tiles) computes every tile
+    exactly as the round-robin walk: bit-identical outputs."""
+    from vmatting import _lib, ops
+    rs = np.random.RandomState(n + cin + w)
+    x = torch.from_numpy(rs.normal(size=(n, h, w, cin)).astype(np.float32)).to(DEV, torch.bfloat16)
+    pc = ops.PackedConv(rs.normal(size=(3, 3, cin, cout)).astype(np.float32) / 40, rs.normal(size=cout).astype(
+        np.float32), "bf16", DEV)
+    outs = []
+    try:
+        for tw in (0, 1):
+            _lib.set_option("thin_twalk", tw)
+            outs.append(ops.conv3x3(x, pc, "none", out_dtype=torch.float32, affine=False, splitk=splitk))
+            assert _lib.last_conv_kernel().startswith("vm::conv3x3_thin<")
+    finally:
+        _lib.set_option("thin_twalk", 1)
+    assert torch.equal(outs[0], outs[1])

@@ -21,7 +21,7 @@ pcs = {"bf16": ops.PackedConv(wt, bias, "bf16"), "fp32": ops.PackedConv(wt, bias
 xs = {"bf16": xf.to(torch.bfloat16), "fp32": xf}
 out = torch.empty((1, h, w, 64), dtype=torch.float32, device="cuda")
 CFGS = [("bf16", 6, 2048, 0), ("fp32", 0, 1024, 0)] + [("fp32", 6, b, 0) for b in (1024, 2048, 4096)] + \
-    [("fp32", 6, 2048, p) for p in (1, 2, 3, 4, 5)]  # pipelined f32 kernel: one resident round whatever softmax_blocks
+    [("fp32", 6, 2048, p) for p in (1, 2, 3, 4, 5, 6, 4, 6)]  # pipelined f32 kernel: one resident round whatever softmax_blocks
 if len(sys.argv) > 3 and sys.argv[3] == "fp32":
     CFGS = CFGS[2:]
 for dt, k, blocks, f32p in CFGS:

@@ -738,6 +738,7 @@ void conv3x3_patch(ConvArgs a) {
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  if (a.prio && NW == 8 && wave >= 4) __builtin_amdgcn_s_setprio(1);
   const int wm = wave % WM, wn = wave / WM;
   const int H = a.H, W = a.W, cs = a.x_cstride;
   const int VW = a.vstride ? a.vW : W;  // packed frames: one virtual image (n = 0), ConvArgs::vstride
@@ -1354,6 +1355,7 @@ void conv3x3_patch_persist(ConvArgs a) {
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  if (a.prio && wave >= 4) __builtin_amdgcn_s_setprio(1);
   const int wm = wave;
   const int H = a.H, W = a.W, cs = a.x_cstride;
   const int th = (H + C::TH - 1) / C::TH, tw = (W + C::TW - 1) / C::TW;
@@ -2956,6 +2958,236 @@ __global__ __launch_bounds__(512, MINW) void conv3x3_first_softmax_f32p(ConvArgs
   }
 }
 
+// Row-ring form of conv3x3_first_softmax_f32p (r04): a wave walks a column band of 32 pixels down a segment of
+// a.seg rows instead of taking one row of an 8-row tile, so each strip stages ONE new input row (its window's bottom
+// row) instead of three: the per-wave patch is a ring of 4 row slots, and the rows in slots 0 and 1 are written
+// twice (slots 4 and 5 too), so the 3-row window of every strip is contiguous at slot base (strip - first) % 4 and
+// the per-step patch offsets stay fixed registers (the window base moves the pointer, not the offsets).  Staging
+// alone was 0.048 of the pipelined kernel's 0.167 ms (smxabl abl 7): 3 input rows read per output row.  The MFMA
+// order, softmax chunks and stores are the pipelined kernel's, so results are bit-identical to it.
+template <int CIN, int AUX = 18>
+__global__ __launch_bounds__(512, 2) void conv3x3_first_softmax_f32r(ConvArgs a) {
+  constexpr int NS = (9 * CIN + 3) / 4;
+  constexpr int TW = 32, PW = TW + 2, SP = 6 * PW;  // 6 row slots: ring of 4 + copies of slots 0 and 1
+  constexpr int ZERO = CIN * SP;                     // 32 + 3 * PW zeros: the padded k-slots read at any base
+  constexpr int WPF = (ZERO + 32 + 3 * PW + 3) / 4 * 4;
+  constexpr bool AFF = false;
+  __shared__ __attribute__((aligned(16))) f32x4 wl[NS * 64];
+  __shared__ int pl[NS * 4];
+  __shared__ __attribute__((aligned(16))) float rmul[2 * 64];
+  __shared__ __attribute__((aligned(16))) float pat[8 * WPF];
+  __shared__ __attribute__((aligned(16))) float stg[(AUX & 16) ? 8 * 16 * 68 : 4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  float* const slab = stg + ((AUX & 16) ? wave * 16 * 68 : 0);
+  const int H = a.H, W = a.W, cs = a.x_cstride;
+  const int tw = (W + TW - 1) / TW, RS = a.seg, nseg = (H + RS - 1) / RS;
+  const int nitems = a.tiles_total;  // frames x segments x bands
+  const int gw = blockIdx.x * 8 + wave, GW = (int)gridDim.x * 8;
+  // strip = (item, row); the walk: rows r0 .. rend-1 of item gw, then of gw + GW, ...
+  struct SC {
+    int n, r, c0, rend, item;
+  };
+  auto item_start = [&](int item) __attribute__((always_inline)) {
+    SC c;
+    c.item = item;
+    if (item >= nitems) {
+      c.n = 0; c.r = H; c.c0 = 0; c.rend = H;
+      return c;
+    }
+    const int band = item % tw, t = item / tw;
+    const int seg = t % nseg;
+    c.n = t / nseg;
+    c.c0 = band * TW;
+    c.r = seg * RS;
+    c.rend = min(H, c.r + RS);
+    return c;
+  };
+  auto next_strip = [&](const SC& c) __attribute__((always_inline)) {
+    if (c.item < nitems && c.r + 1 < c.rend) {
+      SC d = c;
+      d.r += 1;
+      return d;
+    }
+    return item_start(c.item + GW);
+  };
+  const int col = lane & 15, q = lane >> 4;
+  const float* Wt = reinterpret_cast<const float*>(a.w);
+  for (int e = tid; e < NS * 64; e += 512) {
+    const int st = e >> 6, l = e & 63;
+    const int kk = 4 * st + (l >> 4), co = l & 15;
+    const int tap = kk / CIN, c = kk - tap * CIN;
+    f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (kk < 9 * CIN)
+#pragma unroll
+      for (int fc = 0; fc < 4; ++fc) v[fc] = Wt[(long)(fc * 16 + co) * a.K_pad + tap * 8 + c];
+    wl[e] = v;
+  }
+  if (tid < NS * 4) {
+    const int kk = tid;
+    const int tap = kk / CIN, c = kk - tap * CIN;
+    pl[tid] = kk < 9 * CIN ? c * SP + (tap / 3) * PW + tap % 3 : ZERO;
+  }
+  float* const P = pat + wave * WPF;
+  for (int e = lane; e < 32 + 3 * PW; e += 64) P[ZERO + e] = 0.f;
+  if (tid < 64) {
+    rmul[tid] = 1.f;
+    rmul[64 + tid] = a.bias ? a.bias[tid] : 0.f;
+  }
+  __syncthreads();  // the only block-wide barrier: the staged tables
+  int poff[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) poff[s] = pl[s * 4 + q] + col;
+  // input rows of a strip: its whole 3-row window when it starts an item (first), else the window's bottom row
+  auto load_rows = [&](const SC& sc, bool first, float4 (&v)[2][2]) __attribute__((always_inline)) {
+    const int n = sc.n, c0 = sc.c0;
+    const int rlo = first ? sc.r - 1 : sc.r + 1;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int e = lane + 64 * k;
+      const int pr = e / PW, pc = e - pr * PW;
+      const int h = rlo + pr, w = c0 - 1 + pc;
+      const bool ok = e < (first ? 3 * PW : PW) && sc.r < H && (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
+      const float* xp = reinterpret_cast<const float*>(a.x) + a.x_coff + ((long)n * H + (ok ? h : 0)) * (long)W * cs +
+                        (long)(ok ? w : 0) * cs;
+      v[k][0] = ok ? *reinterpret_cast<const float4*>(xp) : make_float4(0.f, 0.f, 0.f, 0.f);
+      v[k][1] = ok && CIN > 4 ? *reinterpret_cast<const float4*>(xp + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  // ring slot of the window's first row for strip row r of an item starting at r0
+  auto base_of = [&](const SC& sc) __attribute__((always_inline)) {
+    return (sc.r - (sc.r / RS) * RS) & 3;
+  };
+  auto stage = [&](const SC& sc, bool first, const float4 (&v)[2][2]) __attribute__((always_inline)) {
+    const int j = base_of(sc);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int e = lane + 64 * k;
+      const float vv[8] = {v[k][0].x, v[k][0].y, v[k][0].z, v[k][0].w, v[k][1].x, v[k][1].y, v[k][1].z, v[k][1].w};
+      const int pr = e / PW, pc = e - pr * PW;
+      const int slot = first ? pr : (j + 2) & 3;  // first: window base 0
+      if (e < (first ? 3 * PW : PW)) {
+#pragma unroll
+        for (int c = 0; c < CIN; ++c) {
+          P[c * SP + slot * PW + pc] = vv[c];
+          if (slot < 2) P[c * SP + (slot + 4) * PW + pc] = vv[c];
+        }
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  };
+  auto mma = [&](const float* Pw, f32x4 (&N)[4][2], f32x4* Cp, const __amdgpu_buffer_rsrc_t& yrs, int valid)
+      __attribute__((always_inline)) {
+    init_strip_acc(N, rmul, false, q);
+    float mx[2] = {0.f, 0.f}, sm[2] = {0.f, 0.f};
+    f32x4 w4 = wl[lane];
+    float b0 = Pw[poff[0]], b1 = Pw[poff[0] + 16];
+    static_for<0, NS>([&](auto sc) __attribute__((always_inline)) {
+      constexpr int s = decltype(sc)::value;
+      f32x4 w4n = w4;
+      float b0n = b0, b1n = b1;
+      if constexpr (s + 1 < NS) {
+        w4n = wl[(s + 1) * 64 + lane];
+        b0n = Pw[poff[s + 1]];
+        b1n = Pw[poff[s + 1] + 16];
+      }
+#pragma unroll
+      for (int fc = 0; fc < 4; ++fc) {
+        N[fc][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(w4[fc], b0, N[fc][0], 0, 0, 0);
+        N[fc][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(w4[fc], b1, N[fc][1], 0, 0, 0);
+      }
+      if (Cp) {
+        if constexpr (s < 10)
+          softmax_chunk<AFF, s, 0, AUX>(*reinterpret_cast<f32x4(*)[4][2]>(Cp), mx, sm, rmul, yrs, a.y_cstride, valid,
+                                        lane, slab);
+      }
+      if constexpr (s + 1 < NS) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+      if constexpr (s + 1 >= NS) __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      w4 = w4n;
+      b0 = b0n;
+      b1 = b1n;
+    });
+    if (Cp) {
+      static_for<NS, 10>([&](auto sc) __attribute__((always_inline)) {
+        softmax_chunk<AFF, decltype(sc)::value, 0, AUX>(*reinterpret_cast<f32x4(*)[4][2]>(Cp), mx, sm, rmul, yrs,
+                                                         a.y_cstride, valid, lane, slab);
+      });
+    }
+  };
+  auto yrs_of = [&](const SC& sc, int& valid) __attribute__((always_inline)) {
+    float* yb = reinterpret_cast<float*>(a.y) + a.y_coff +
+                (((long)sc.n * H + (sc.r < H ? sc.r : 0)) * W + sc.c0) * (long)a.y_cstride;
+    valid = sc.r < H ? W - sc.c0 : 0;
+    return __builtin_amdgcn_make_buffer_rsrc(uniform_ptr(yb), 0, 0x7ffffff0, 0x00020000);
+  };
+  auto store = [&](const SC& sc, f32x4 (&C)[4][2]) __attribute__((always_inline)) {
+    int valid;
+    const __amdgpu_buffer_rsrc_t yrs = yrs_of(sc, valid);
+    float mx[2] = {0.f, 0.f}, sm[2] = {0.f, 0.f};
+    static_for<0, 10>([&](auto sc2) __attribute__((always_inline)) {
+      softmax_chunk<AFF, decltype(sc2)::value, 0, AUX>(C, mx, sm, rmul, yrs, a.y_cstride, valid, lane, slab);
+    });
+  };
+  SC s0 = item_start(gw);
+  if (s0.item >= nitems) return;  // (wave-uniform; the block barrier above is behind every wave)
+  float4 nv[2][2];
+  load_rows(s0, true, nv);
+  stage(s0, true, nv);
+  SC s1 = next_strip(s0);
+  bool f1 = s1.item != s0.item;
+  load_rows(s1, f1, nv);
+  f32x4 acc0[4][2], acc1[4][2];
+  {
+    int v0;
+    mma(P + base_of(s0) * PW, acc0, nullptr, yrs_of(s0, v0), 0);
+  }
+  // one step: strip s0's accumulators are in C; stage strip s1 and compute it into N while C's softmax and stores go
+  // out between its MFMAs
+  auto step = [&](f32x4 (&C)[4][2], f32x4 (&N)[4][2]) __attribute__((always_inline)) {
+    stage(s1, f1, nv);
+    const SC s2 = next_strip(s1);
+    const bool f2 = s2.item != s1.item;
+    int valid;
+    const __amdgpu_buffer_rsrc_t yrs = yrs_of(s0, valid);
+    load_rows(s2, f2, nv);
+    mma(P + base_of(s1) * PW, N, &C[0][0], yrs, valid);
+    s0 = s1;
+    s1 = s2;
+    f1 = f2;
+  };
+  while (true) {
+    if (s1.item >= nitems) {
+      store(s0, acc0);
+      break;
+    }
+    step(acc0, acc1);
+    if (s1.item >= nitems) {
+      store(s0, acc1);
+      break;
+    }
+    step(acc1, acc0);
+  }
+}
+
 // ================================================================ Cout == 1 head (conv1_5 + sigmoid)
 // unet.py:203-205 / unet_simple.py:142 / small.py:49-50: a 1-channel 3x3 conv over <=128 channels at full
 // resolution is a memory-bound dot product: 16 lanes per pixel, each lane one 16-byte channel chunk per
@@ -3683,9 +3915,19 @@ __global__ __launch_bounds__(256, TH <= 4 ? 4 : TH <= 8 ? 3 : 2) void conv3x3_th
     cb = blockIdx.y * per;
     ce = min(nch, cb + per);
   }
-  int tile = blockIdx.x;
-  if (cb >= ce || tile >= ntiles) return;
-  // persistent: the block walks tiles blockIdx.x, +gridDim.x, ... and streams (tile, chunk) steps; the next step's
+  // persistent: the block walks tiles blockIdx.x, +gridDim.x, ...; with a.twalk (r04) XCD x = blockIdx.x % 8 takes
+  // the contiguous eighth [lo, hi) of the tile list and its gridDim.x / 8 blocks every (gridDim.x / 8)-th tile of it,
+  // so the tiles resident at once on one XCD are neighbours whose patches share halo rows and 128-byte lines in that
+  // XCD's L2 (round-robin placement put horizontally adjacent tiles on different XCDs: FETCH_SIZE 1.8x the input)
+  int tile = blockIdx.x, tstep = (int)gridDim.x, tend = ntiles;
+  if (a.twalk && (gridDim.x & 7) == 0) {
+    const int xcd = blockIdx.x & 7;
+    tile = (int)((long)xcd * ntiles / 8) + (int)(blockIdx.x >> 3);
+    tstep = (int)(gridDim.x >> 3);
+    tend = (int)((long)(xcd + 1) * ntiles / 8);
+  }
+  if (cb >= ce || tile >= tend) return;
+  // the block streams (tile, chunk) steps; the next step's
   // patch and filter pieces (the next tile's first chunk at a tile's end) are in registers while this one computes
   auto geo = [&](int t, int& n, int& r0, int& c0, int (&xo)[PPT]) {
     const int tx = t % tw;
@@ -3756,8 +3998,8 @@ __global__ __launch_bounds__(256, TH <= 4 ? 4 : TH <= 8 ? 3 : 2) void conv3x3_th
     __syncthreads();
     // the next step: the next chunk of this tile, or the first chunk of the block's next tile
     const bool last = cc + 1 == ce;
-    const int ntile = last ? tile + (int)gridDim.x : tile;
-    const bool more = ntile < ntiles;
+    const int ntile = last ? tile + tstep : tile;
+    const bool more = ntile < tend;
     int nn = n, nr0 = r0, nc0 = c0, nxo[PPT];
 #pragma unroll
     for (int i = 0; i < PPT; ++i) nxo[i] = xo[i];
@@ -4065,6 +4307,7 @@ static int launch_patch(ConvArgs& a, hipStream_t st) {
   a.tiles_n = (a.cout + BN - 1) / BN;
   a.repi = (int)g_patch_repi;
   a.upmask = (int)g_up_skip_mask;
+  a.prio = (int)g_conv_prio;
   if (sp * a.tiles_n > 0x7fffffffL) return fail(VM_EUNSUPPORTED, "conv3x3: too many tiles");
   a.tiles_total = (int)(sp * a.tiles_n);
   // channel-banded tile order (ConvArgs::cband) for weight-heavy layers: the whole filter exceeds an XCD's 4 MB L2
@@ -4128,6 +4371,7 @@ static int launch_patch_persist(ConvArgs& a, hipStream_t st) {
   a.tiles_n = tn;
   a.prot = g_persist_rot == 0 ? (a.up ? 1 : 0) : g_persist_rot == 1 ? 1 : 0;
   a.repi = 1;
+  a.prio = (int)g_conv_prio;
   a.upmask = (int)g_up_skip_mask;
   a.tiles_total = (int)(sp * tn);
   const long J = resident / 8;  // walkers per XCD band (every band has >= 2 rounds of items)
@@ -4202,7 +4446,9 @@ static int thin_resident() {
 // the LDS-DMA thin kernel (conv3x3_thin_dma): 0 off; 1 = 8-row tiles, 3-slot ring; 2 = 4-row tiles, 4 slots;
 // 3 = 4-row tiles, 3 slots; 4 = 8-row tiles, 2 slots.  A resident grid of thin_dma_rounds x blocks per CU x CUs
 static long g_thin_dma = 0, g_thin_dma_rounds = 1;
+long g_conv_prio = 0;  // ConvArgs::prio (conv_common.h)
 static long g_thin_rowreuse = 1;  // conv3x3_thin: thin_chunk's row reuse (0: the r03 tap-major loop)
+static long g_thin_twalk = 1;     // conv3x3_thin: XCD-banded tile walk (ConvArgs::twalk; 0: round-robin)
 template <int TH, int S>
 static int launch_thin_dma_cfg(ConvArgs& a, long n, int ks, hipStream_t st) {
   constexpr int lds = thin_dma_lds<TH, S>();
@@ -4259,6 +4505,7 @@ static int dispatch_thin(ConvArgs& a, long n, hipStream_t st) {
     return check_launch("splitk_reduce");
   }
   const dim3 grid((unsigned)gx, ks);
+  a.twalk = (int)g_thin_twalk;
   if (!g_thin_rowreuse) {
     snprintf(g_last_kernel, sizeof g_last_kernel, "vm::conv3x3_thin<%d, false>", th);
     if (th == 16) hipLaunchKernelGGL((conv3x3_thin<16, false>), grid, dim3(256), 0, st, a);
@@ -4563,17 +4810,39 @@ static int launch_first_softmax_f32(ConvArgs& a, int cin, hipStream_t st) {
     snprintf(g_last_kernel, sizeof g_last_kernel, "vm::conv3x3_first_softmax_f32p<%d, 2, false, 0, 18>", C); \
     hipLaunchKernelGGL((conv3x3_first_softmax_f32p<C, 2, false, 0, 18>), dim3(gp), dim3(512), 0, st, a);     \
     break;
+    if (g_softmax_f32p == 6) {  // the row-ring form: segments of a.seg rows x 32-pixel bands, one per wave
+      const long nimg = N, bands = (a.W + 31) / 32;
+      const long waves = (long)gp * 8;
+      long seg = (nimg * bands * a.H + waves - 1) / waves;  // rows per segment for about one item per wave
+      if (seg < 4) seg = 4;
+      const long items = nimg * bands * ((a.H + seg - 1) / seg);
+      if (items > 0x7fffffffL) return fail(VM_EUNSUPPORTED, "conv3x3_first_softmax_f32r: too many items");
+      a.seg = (int)seg;
+      a.tiles_total = (int)items;
+      switch (cin) {
+#define VM_SMR(C)                                                                                              \
+  case C:                                                                                                      \
+    snprintf(g_last_kernel, sizeof g_last_kernel, "vm::conv3x3_first_softmax_f32r<%d>", C);                   \
+    hipLaunchKernelGGL((conv3x3_first_softmax_f32r<C>), dim3((unsigned)std::min<long>(gp, (items + 7) / 8)),  \
+                       dim3(512), 0, st, a);                                                                   \
+    break;
+        VM_SMR(1) VM_SMR(2) VM_SMR(3) VM_SMR(4) VM_SMR(5) VM_SMR(6) VM_SMR(7) VM_SMR(8)
+#undef VM_SMR
+        default: return fail(VM_EINVAL, "conv3x3_first_softmax_f32r: cin %d", cin);
+      }
+      return check_launch("conv3x3_first_softmax_f32r");
+    }
 #ifdef VM_STUDY
     if (cin == 5 && g_softmax_abl) {  // timing ablations (garbage results): 1 no stores, 2 no MFMA, 4 no softmax
-      snprintf(g_last_kernel, sizeof g_last_kernel, "vm::conv3x3_first_softmax_f32p<5, 2, false, %ld>", g_softmax_abl);
+      snprintf(g_last_kernel, sizeof g_last_kernel, "vm::conv3x3_first_softmax_f32p<5, 2, false, %ld, 18>", g_softmax_abl);
       switch (g_softmax_abl) {
-        case 1: hipLaunchKernelGGL((conv3x3_first_softmax_f32p<5, 2, false, 1>), dim3(gp), dim3(512), 0, st, a); break;
-        case 2: hipLaunchKernelGGL((conv3x3_first_softmax_f32p<5, 2, false, 2>), dim3(gp), dim3(512), 0, st, a); break;
-        case 3: hipLaunchKernelGGL((conv3x3_first_softmax_f32p<5, 2, false, 3>), dim3(gp), dim3(512), 0, st, a); break;
-        case 4: hipLaunchKernelGGL((conv3x3_first_softmax_f32p<5, 2, false, 4>), dim3(gp), dim3(512), 0, st, a); break;
-        case 5: hipLaunchKernelGGL((conv3x3_first_softmax_f32p<5, 2, false, 5>), dim3(gp), dim3(512), 0, st, a); break;
-        case 6: hipLaunchKernelGGL((conv3x3_first_softmax_f32p<5, 2, false, 6>), dim3(gp), dim3(512), 0, st, a); break;
-        default: hipLaunchKernelGGL((conv3x3_first_softmax_f32p<5, 2, false, 7>), dim3(gp), dim3(512), 0, st, a); break;
+        case 1: hipLaunchKernelGGL((conv3x3_first_softmax_f32p<5, 2, false, 1, 18>), dim3(gp), dim3(512), 0, st, a); break;
+        case 2: hipLaunchKernelGGL((conv3x3_first_softmax_f32p<5, 2, false, 2, 18>), dim3(gp), dim3(512), 0, st, a); break;
+        case 3: hipLaunchKernelGGL((conv3x3_first_softmax_f32p<5, 2, false, 3, 18>), dim3(gp), dim3(512), 0, st, a); break;
+        case 4: hipLaunchKernelGGL((conv3x3_first_softmax_f32p<5, 2, false, 4, 18>), dim3(gp), dim3(512), 0, st, a); break;
+        case 5: hipLaunchKernelGGL((conv3x3_first_softmax_f32p<5, 2, false, 5, 18>), dim3(gp), dim3(512), 0, st, a); break;
+        case 6: hipLaunchKernelGGL((conv3x3_first_softmax_f32p<5, 2, false, 6, 18>), dim3(gp), dim3(512), 0, st, a); break;
+        default: hipLaunchKernelGGL((conv3x3_first_softmax_f32p<5, 2, false, 7, 18>), dim3(gp), dim3(512), 0, st, a); break;
       }
       return check_launch("conv3x3_first_softmax_f32p");
     }
@@ -4688,8 +4957,9 @@ extern "C" int vm_set_option(const char* key, long value) {
     return VM_OK;
   }
   if (!strcmp(key, "softmax_f32p")) {  // 0 the r03 kernel; 1 pipelined; 2 its 4-waves-per-SIMD build; 3 NT stores;
-                                       // 4 / 5 LDS-transposed whole-pixel stores, NT / through L2
-    if (value < 0 || value > 5) return fail(VM_EINVAL, "softmax_f32p must be 0..5");
+                                       // 4 / 5 LDS-transposed whole-pixel stores, NT / through L2;
+                                       // 6 the row-ring form (conv3x3_first_softmax_f32r)
+    if (value < 0 || value > 6) return fail(VM_EINVAL, "softmax_f32p must be 0..6");
     g_softmax_f32p = value;
     return VM_OK;
   }
@@ -4746,6 +5016,16 @@ extern "C" int vm_set_option(const char* key, long value) {
   if (!strcmp(key, "thin_th")) {
     if (value != 4 && value != 8 && value != 16) return fail(VM_EINVAL, "thin_th must be 4, 8 or 16");
     g_thin_th = value;
+    return VM_OK;
+  }
+  if (!strcmp(key, "conv_prio")) {
+    if (value < 0 || value > 1) return fail(VM_EINVAL, "conv_prio must be 0 or 1");
+    g_conv_prio = value;
+    return VM_OK;
+  }
+  if (!strcmp(key, "thin_twalk")) {
+    if (value < 0 || value > 1) return fail(VM_EINVAL, "thin_twalk must be 0 or 1");
+    g_thin_twalk = value;
     return VM_OK;
   }
   if (!strcmp(key, "thin_rowreuse")) {

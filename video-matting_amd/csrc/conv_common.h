@@ -52,6 +52,9 @@ struct ConvArgs {
   // (b >> 3) / cband, so XCD b % 8 keeps its cband 64-channel weight slices L2-resident over every pixel tile (weight-
   // heavy layers: upconv_2's 9.4 MB folded filter, which the pixel-banded order re-streams per resident round)
   int cband;
+  int twalk;  // conv3x3_thin: XCD-banded tile walk
+  int seg;    // conv3x3_first_softmax_f32r: rows per wave segment
+  int prio;  // 1: waves 4..7 of an 8-wave block run at s_setprio 1 (static priority for the arbitration loser)
   // strip pair kernel: optional bf16 output of the FIRST conv (conv1_1 + bias + relu), [N,H,W,64] view
   void* y1;
   int y1_cstride, y1_coff;
@@ -175,6 +178,8 @@ __device__ __forceinline__ uint4 chunk_pair(uint2 lo, uint2 hi) {
 // name of the kernel the last conv call on this thread launched, spelled as rocprofv3 reports it (conv3x3.hip)
 extern thread_local char g_last_kernel[128];
 
+// vm_set_option "conv_prio": ConvArgs::prio for the 8-wave conv kernels (patch, persistent patch, row-stationary)
+extern long g_conv_prio;
 // launchers defined in conv_rows.hip (called from conv3x3.hip's dispatch)
 bool rows_ok(const ConvArgs& a);
 int launch_rows(ConvArgs& a, hipStream_t st, int cfg);

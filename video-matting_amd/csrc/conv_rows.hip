@@ -98,6 +98,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  if (a.prio && wave >= 4) __builtin_amdgcn_s_setprio(1);
   const int rg = wave % C::RG, cg = wave / C::RG;
   const int H = a.H, W = a.W, cs = a.x_cstride;
   const int th = (H + TH - 1) / TH, tw = (W + C::TW - 1) / C::TW;
@@ -492,6 +493,7 @@ static int launch_th(ConvArgs& a, hipStream_t st) {
   a.tiles_n = (a.cout + C::BN - 1) / C::BN;
   if (sp * a.tiles_n > 0x7fffffffL) return fail(VM_EUNSUPPORTED, "conv3x3: too many tiles");
   a.tiles_total = (int)(sp * a.tiles_n);
+  a.prio = (int)g_conv_prio;
   // persistent: one block per CU (LDS-limited), a multiple of 8 so every XCD gets the same number of blocks
   long grid = g_num_cu < a.tiles_total ? g_num_cu : a.tiles_total;
   grid = (grid + 7) / 8 * 8;
