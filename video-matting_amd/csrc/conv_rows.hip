@@ -153,6 +153,15 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
   }
   // LDS: weight buffers [0, 2 WB), patch buffers [2 WB, 2 WB + 2 PB)
   const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr(smem));
+  // per-channel epilogue constants (mul, add) of every output channel, staged in LDS once per block (r04): read from
+  // global memory inside the epilogue they made hipcc wait vmcnt(0) there, draining the next granules' DMA at every
+  // tile end; published by the prologue's barrier
+  const int ccap = a.up ? a.up_cout : a.cout;
+  float2* const ctab = reinterpret_cast<float2*>(smem + C::LDS);
+  for (int c = tid; c < ccap; c += 512) {
+    const float sc = a.scale ? a.scale[c] : 1.f;
+    ctab[c] = make_float2(sc, (a.bias ? a.bias[c] : 0.f) * sc + (a.shift ? a.shift[c] : 0.f));
+  }
   // DMA of granule g of local tile k into buffer buf; k >= ntile issues the same number of out-of-range (zero) pieces,
   // so every wave's vmcnt bookkeeping stays uniform
   // DMA of granule g of tile tt into buffer buf.  Every wave issues exactly XPW patch and WPW weight pieces (pieces past
@@ -266,7 +275,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
   auto epilogue = [&](const RowTile& tt) __attribute__((always_inline)) {
     const int phase = a.up ? tt.n0 / a.up_cout : 0;
     const int cb = tt.n0 - phase * a.up_cout;  // first (per-phase) output channel of the tile
-    const int ccap = a.up ? a.up_cout : a.cout;
     const int YH = a.up ? 2 * H : H, YW = a.up ? 2 * W : W;
     T* yb = uniform_ptr(reinterpret_cast<T*>(a.y) + a.y_coff + (long)tt.n * YH * YW * a.y_cstride);
     const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(yb, 0, 0x7ffffff0, 0x00020000);
@@ -278,10 +286,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
     for (int f = 0; f < FC; ++f)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int co = min(cb + cg * C::CW + f * 16 + 4 * ck + j, ccap - 1);
-        const float sc = a.scale ? a.scale[co] : 1.f;
-        mul[f][j] = sc;
-        add[f][j] = (a.bias ? a.bias[co] : 0.f) * sc + (a.shift ? a.shift[co] : 0.f);
+        const float2 t = ctab[min(cb + cg * C::CW + f * 16 + 4 * ck + j, ccap - 1)];
+        mul[f][j] = t.x;
+        add[f][j] = t.y;
       }
     auto pack4 = [](const float (&v)[4]) __attribute__((always_inline)) {
       return make_uint2((uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16), (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16));
@@ -467,7 +474,8 @@ bool rows_ok(const ConvArgs& a) {
   return a.chunk_major && a.cin_pad % 32 == 0 && a.y_dtype == VM_BF16 && a.y_vec && (a.cout & 7) == 0 &&
          a.act != VM_ACT_SOFTMAX && a.ksplit <= 1 && (a.x_src_c <= 0 || a.x_src_c % 32 == 0) &&
          (!a.up || a.up_cout % 64 == 0) && img_in < 0x7ffffff0L && img_out < 0x7ffffff0L &&
-         (!a.py || (a.py_cstride % 8 == 0 && a.py_coff % 8 == 0));
+         (!a.py || (a.py_cstride % 8 == 0 && a.py_coff % 8 == 0)) &&
+         RowsCfg<16>::LDS + 8 * (a.up ? a.up_cout : a.cout) <= 163840;  // + the epilogue constants table
 }
 
 static int g_num_cu = 0;
@@ -475,10 +483,12 @@ static int g_num_cu = 0;
 template <int TH>
 static int launch_th(ConvArgs& a, hipStream_t st) {
   using C = RowsCfg<TH>;
+  const int lds = C::LDS + 8 * (a.up ? a.up_cout : a.cout);  // + the epilogue constants table
+  if (lds > 163840) return fail(VM_EUNSUPPORTED, "conv3x3_rows: %d output channels overflow LDS", a.cout);
   static bool attr_set = false;  // idempotent; benign race
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3_rows<TH>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
     if (e != hipSuccess) return fail(VM_EHIP, "hipFuncSetAttribute(rows): %s", hipGetErrorString(e));
     attr_set = true;
   }
@@ -498,7 +508,7 @@ static int launch_th(ConvArgs& a, hipStream_t st) {
   long grid = g_num_cu < a.tiles_total ? g_num_cu : a.tiles_total;
   grid = (grid + 7) / 8 * 8;
   snprintf(g_last_kernel, sizeof g_last_kernel, "vm::conv3x3_rows<%d>", TH);
-  hipLaunchKernelGGL((conv3x3_rows<TH>), dim3(grid), dim3(512), C::LDS, st, a);
+  hipLaunchKernelGGL((conv3x3_rows<TH>), dim3(grid), dim3(512), lds, st, a);
   return check_launch("conv3x3_rows");
 }
 
