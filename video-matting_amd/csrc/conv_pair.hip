@@ -215,6 +215,8 @@ void conv3x3_pair_strip(ConvArgs a, int seg, int nseg, int nstrip) {
   const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(prow0, 0, 0x7ffffff0, 0x00020000);
   uint2 prev[2][2];  // the even row's bf16 outputs [fp][f] (pool partner)
 
+  const __amdgpu_buffer_rsrc_t hrs = __builtin_amdgcn_make_buffer_rsrc(
+      uniform_ptr(a.hd ? a.hd + (long)n * H * W * 12 : nullptr), 0, 0x7ffffff0, 0x00020000);
   auto head_finish = [&](int r) __attribute__((always_inline)) {  // wave 0: row r's partials (wave 1's half via LDS)
     const uint4 ha0 = *reinterpret_cast<const uint4*>(smem + C::H_OFF + lane * 16);
     const uint4 ha1 = *reinterpret_cast<const uint4*>(smem + C::H_OFF + (64 + lane) * 16);
@@ -226,7 +228,10 @@ void conv3x3_pair_strip(ConvArgs a, int seg, int nseg, int nstrip) {
       mma16<T>(ha0, hb0, d);
       mma16<T>(ha1, hb1, d);
       const int p = fp * 16 + col, c = c0 + p;
-      if (q < 3 && p < C::SW && c < W) *reinterpret_cast<f32x4*>(a.hd + (((long)n * H + r) * W + c) * 12 + 4 * q) = d;
+      // a buffer store per fragment whatever the lane mask (out-of-range offsets drop the rest), so the loop's
+      // counted vmcnt knows exactly how many stores follow the row's DMA
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, d), hrs,
+                                             q < 3 && p < C::SW && c < W ? ((r * W + c) * 12 + 4 * q) * 4 : OOB, 0, 0);
     }
   };
 
@@ -412,16 +417,20 @@ void conv3x3_pair_strip(ConvArgs a, int seg, int nseg, int nstrip) {
     int nst = 0;  // wave 0: vector-memory ops issued after this row's DMA (counted vmcnt before the barrier)
     if (wave == 0) {
       if constexpr (!(ABL & 8)) convert_row(r + 4, (r - 1) & 1);  // read from iteration r + 1 on, after the barrier
-      if (a.hd && r > s0) head_finish(r - 1);
       if constexpr (!(ABL & 8)) dma_row(r + 5, r & 1);
-      nst = (a.y_skip ? 0 : 2) + (a.py && ((r & 1) || r + 1 == H) ? 2 : 0);
+      // the previous row's head partials after the DMA (r04): the barrier's counted wait then leaves them in flight
+      // (issued before the DMA, in-order counting made every row wait for their write-back too)
+      const bool hf = a.hd && r > s0;
+      if (hf) head_finish(r - 1);
+      nst = (hf ? 2 : 0) + (a.y_skip ? 0 : 2) + (a.py && ((r & 1) || r + 1 == H) ? 2 : 0);
     }
     conv1(r + 2);  // (row s1 + 1 at a segment's last row: computed into a ring slot nothing reads)
     conv2(r);
-    if (wave == 0) {  // nst is 0, 2 or 4
+    if (wave == 0) {  // nst is 0, 2, 4 or 6
       if ((ABL & 8) || nst == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       else if (nst == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else if (nst == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // LDS-only barrier: global stores stay in flight
     if constexpr (!(ABL & 4)) __builtin_amdgcn_s_barrier();
