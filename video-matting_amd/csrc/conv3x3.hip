@@ -265,8 +265,8 @@ __global__ __launch_bounds__(256, 2) void conv3x3_mfma(ConvArgs a) {
           else if (a.act == VM_ACT_SIGMOID) v[j] = sigmoid_precise(v[j]);
         }
         uint2 pk;
-        pk.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-        pk.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+        pk.x = bf16x2_bits(v[0], v[1]);
+        pk.y = bf16x2_bits(v[2], v[3]);
         *reinterpret_cast<uint2*>(smem + row * SR16 + col * 2) = pk;
       }
     }
@@ -711,8 +711,8 @@ __device__ __forceinline__ void first_layer_patch(const ConvArgs& a, char* smem,
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj) v[jj] = inside ? fmaxf(acc[fc][jj] + b1[fc][jj], 0.f) : 0.f;
         uint2 pk;
-        pk.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-        pk.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+        pk.x = bf16x2_bits(v[0], v[1]);
+        pk.y = bf16x2_bits(v[2], v[3]);
         // channel fc*16 + 4q: granule fc/2, 16-byte chunk (fc&1)*2 + q/2, half q&1
         *reinterpret_cast<uint2*>(smem + (fc >> 1) * pb + swz<64>(p, (fc & 1) * 2 + (q >> 1)) + (q & 1) * 8) = pk;
       }
@@ -1155,8 +1155,8 @@ void conv3x3_patch(ConvArgs a) {
               else if (a.act == VM_ACT_SIGMOID) t = sigmoid_precise(t);
               v[fp][f][j] = t;
             }
-            pk[f].x = (uint32_t)f2bf(v[fp][f][0]) | ((uint32_t)f2bf(v[fp][f][1]) << 16);
-            pk[f].y = (uint32_t)f2bf(v[fp][f][2]) | ((uint32_t)f2bf(v[fp][f][3]) << 16);
+            pk[f].x = bf16x2_bits(v[fp][f][0], v[fp][f][1]);
+            pk[f].y = bf16x2_bits(v[fp][f][2], v[fp][f][3]);
           }
           hb[fp][g2] = make_uint4(pk[0].x, pk[0].y, pk[1].x, pk[1].y);
           const uint4 d = chunk_pair(pk[0], pk[1]);
@@ -1185,8 +1185,8 @@ void conv3x3_patch(ConvArgs a) {
             uint2 q2[2];
 #pragma unroll
             for (int f = 0; f < 2; ++f) {
-              q2[f].x = (uint32_t)f2bf(m[f][0]) | ((uint32_t)f2bf(m[f][1]) << 16);
-              q2[f].y = (uint32_t)f2bf(m[f][2]) | ((uint32_t)f2bf(m[f][3]) << 16);
+              q2[f].x = bf16x2_bits(m[f][0], m[f][1]);
+              q2[f].y = bf16x2_bits(m[f][2], m[f][3]);
             }
             const uint4 d = chunk_pair(q2[0], q2[1]);
             const int pr = tr >> 1, pc = tc >> 1;
@@ -1204,10 +1204,10 @@ void conv3x3_patch(ConvArgs a) {
           uint4 hwf[2];
 #pragma unroll
           for (int kk = 0; kk < 2; ++kk)
-            hwf[kk] = make_uint4((uint32_t)f2bf(hwv[kk][0]) | ((uint32_t)f2bf(hwv[kk][1]) << 16),
-                                 (uint32_t)f2bf(hwv[kk][2]) | ((uint32_t)f2bf(hwv[kk][3]) << 16),
-                                 (uint32_t)f2bf(hwv[kk][4]) | ((uint32_t)f2bf(hwv[kk][5]) << 16),
-                                 (uint32_t)f2bf(hwv[kk][6]) | ((uint32_t)f2bf(hwv[kk][7]) << 16));
+            hwf[kk] = make_uint4(bf16x2_bits(hwv[kk][0], hwv[kk][1]),
+                                 bf16x2_bits(hwv[kk][2], hwv[kk][3]),
+                                 bf16x2_bits(hwv[kk][4], hwv[kk][5]),
+                                 bf16x2_bits(hwv[kk][6], hwv[kk][7]));
           const int phase = a.up ? (n0 + wn * C::TPN) / a.up_cout : 0;
           const int YH = a.up ? 2 * H : H;
 #pragma unroll
@@ -1256,8 +1256,8 @@ void conv3x3_patch(ConvArgs a) {
             else if (a.act == VM_ACT_SIGMOID) v[j] = sigmoid_precise(v[j]);
           }
           uint2 pk;
-          pk.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-          pk.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+          pk.x = bf16x2_bits(v[0], v[1]);
+          pk.y = bf16x2_bits(v[2], v[3]);
           *reinterpret_cast<uint2*>(smem + row * C::SR + col * 2) = pk;
         }
       }
@@ -1389,10 +1389,10 @@ void conv3x3_patch_persist(ConvArgs a) {
         hv[j] = col < 9 ? a.hw[col * a.hw_cin + a.hw_coff + hc] : 0.f;
       }
       *reinterpret_cast<uint4*>(kh + (lane * 2 + kk) * 16) =
-          make_uint4((uint32_t)f2bf(hv[0]) | ((uint32_t)f2bf(hv[1]) << 16),
-                     (uint32_t)f2bf(hv[2]) | ((uint32_t)f2bf(hv[3]) << 16),
-                     (uint32_t)f2bf(hv[4]) | ((uint32_t)f2bf(hv[5]) << 16),
-                     (uint32_t)f2bf(hv[6]) | ((uint32_t)f2bf(hv[7]) << 16));
+          make_uint4(bf16x2_bits(hv[0], hv[1]),
+                     bf16x2_bits(hv[2], hv[3]),
+                     bf16x2_bits(hv[4], hv[5]),
+                     bf16x2_bits(hv[6], hv[7]));
     }
   }
   __syncthreads();
@@ -1539,8 +1539,8 @@ void conv3x3_patch_persist(ConvArgs a) {
         uint2 pk[2];
 #pragma unroll
         for (int f = 0; f < 2; ++f) {
-          pk[f].x = (uint32_t)f2bf(v[fp][f][0]) | ((uint32_t)f2bf(v[fp][f][1]) << 16);
-          pk[f].y = (uint32_t)f2bf(v[fp][f][2]) | ((uint32_t)f2bf(v[fp][f][3]) << 16);
+          pk[f].x = bf16x2_bits(v[fp][f][0], v[fp][f][1]);
+          pk[f].y = bf16x2_bits(v[fp][f][2], v[fp][f][3]);
         }
         if (a.hd)  // (the same two MFMAs, in the same order, as the register epilogue's head split)
           mma16<T>(*reinterpret_cast<const uint4*>(kh + (ln * 2 + g2) * 16),
@@ -1571,8 +1571,8 @@ void conv3x3_patch_persist(ConvArgs a) {
           uint2 q2[2];
 #pragma unroll
           for (int f = 0; f < 2; ++f) {
-            q2[f].x = (uint32_t)f2bf(m[f][0]) | ((uint32_t)f2bf(m[f][1]) << 16);
-            q2[f].y = (uint32_t)f2bf(m[f][2]) | ((uint32_t)f2bf(m[f][3]) << 16);
+            q2[f].x = bf16x2_bits(m[f][0], m[f][1]);
+            q2[f].y = bf16x2_bits(m[f][2], m[f][3]);
           }
           const uint4 d = chunk_pair(q2[0], q2[1]);
           const int pr = tr >> 1, pc = tc >> 1;
@@ -1759,7 +1759,7 @@ __global__ __launch_bounds__(512) void conv3x3_pair_persist(ConvArgs a) {
         const int c0 = (2 * kk + j0 / 4) * 16 + 4 * q + j0 % 4, c1 = (2 * kk + j1 / 4) * 16 + 4 * q + j1 % 4;
         const float w0 = col < 9 ? a.hw[col * a.hw_cin + a.hw_coff + c0] : 0.f;
         const float w1 = col < 9 ? a.hw[col * a.hw_cin + a.hw_coff + c1] : 0.f;
-        u[jp] = (uint32_t)f2bf(w0) | ((uint32_t)f2bf(w1) << 16);
+        u[jp] = bf16x2_bits(w0, w1);
       }
       hwf[kk] = make_uint4(u[0], u[1], u[2], u[3]);
     }
@@ -1859,8 +1859,8 @@ __global__ __launch_bounds__(512) void conv3x3_pair_persist(ConvArgs a) {
         float v[4];
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj) v[jj] = inside ? fmaxf(acc1[fc][jj] + b1[jj], 0.f) : 0.f;
-        pk[fc].x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-        pk[fc].y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+        pk[fc].x = bf16x2_bits(v[0], v[1]);
+        pk[fc].y = bf16x2_bits(v[2], v[3]);
       }
       // whole 16-byte chunks per lane (conflict-free ds_write_b128 under swz2) instead of 8-byte halves
 #pragma unroll
@@ -1942,8 +1942,8 @@ __global__ __launch_bounds__(512) void conv3x3_pair_persist(ConvArgs a) {
           if (a.act == VM_ACT_RELU) v[j] = fmaxf(v[j], 0.f);
           else if (a.act == VM_ACT_SIGMOID) v[j] = sigmoid_precise(v[j]);
         }
-        pk[fc].x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-        pk[fc].y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+        pk[fc].x = bf16x2_bits(v[0], v[1]);
+        pk[fc].y = bf16x2_bits(v[2], v[3]);
       }
       if (a.hd) {  // the skip half's head partials of this lane's pixel: 2 MFMAs on the bf16 outputs just made
         f32x4 dacc = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -2131,8 +2131,8 @@ __global__ __launch_bounds__(512, 4) void conv3x3_first(ConvArgs a) {
           else if (a.act == VM_ACT_SIGMOID) v[jj] = sigmoid_precise(v[jj]);
         }
         uint2 pk;
-        pk.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-        pk.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+        pk.x = bf16x2_bits(v[0], v[1]);
+        pk.y = bf16x2_bits(v[2], v[3]);
         *reinterpret_cast<uint2*>(stg + row * SR + cc * 2) = pk;
       }
     }
@@ -3781,8 +3781,8 @@ __global__ __launch_bounds__(256 * BD_KS) void conv3x3_up2x_border(BorderArgs a)
       if (a.act == VM_ACT_RELU) v[j] = fmaxf(v[j], 0.f);
       else if (a.act == VM_ACT_SIGMOID) v[j] = sigmoid_precise(v[j]);
     }
-    pk.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-    pk.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+    pk.x = bf16x2_bits(v[0], v[1]);
+    pk.y = bf16x2_bits(v[2], v[3]);
     if (!a.y_skip && bok)
       *reinterpret_cast<uint2*>(reinterpret_cast<T*>(a.y) + (((long)n * OH + ey) * OW + ex) * (long)a.y_cstride +
                                 a.y_coff + cob + cq) = pk;

@@ -95,7 +95,7 @@ void conv3x3_pair_strip(ConvArgs a, int seg, int nseg, int nstrip) {
         const int ch0 = (2 * kk + j0 / 4) * 16 + 4 * q + j0 % 4, ch1 = (2 * kk + j1 / 4) * 16 + 4 * q + j1 % 4;
         const float h0 = col < 9 ? a.hw[col * a.hw_cin + a.hw_coff + ch0] : 0.f;
         const float h1 = col < 9 ? a.hw[col * a.hw_cin + a.hw_coff + ch1] : 0.f;
-        u[jp] = (uint32_t)f2bf(h0) | ((uint32_t)f2bf(h1) << 16);
+        u[jp] = bf16x2_bits(h0, h1);
       }
       *reinterpret_cast<uint4*>(smem + C::H_OFF + (kk * 64 + lane) * 16) = make_uint4(u[0], u[1], u[2], u[3]);
     }
@@ -161,12 +161,14 @@ void conv3x3_pair_strip(ConvArgs a, int seg, int nseg, int nstrip) {
       const float4 bb = *reinterpret_cast<const float4*>(rk + 128 + 32 * wave + 16 * f + 4 * ql);
       b1[f][0] = bb.x; b1[f][1] = bb.y; b1[f][2] = bb.z; b1[f][3] = bb.w;
     }
-    int ib[3];  // input-ring byte offset of K-step j's tap (4j + ql) for ring column cl
+    // input-ring byte offset of K-step j's tap (4j + ql, taps 9..11 -> 8) for ring column cl: the three input-row
+    // offsets are uniform (scalar), the lane picks one (j = 0: tap ql, j = 1: tap 4 + ql, j = 2: tap 8)
+    int ro[3];
 #pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      const int tap = min(4 * j + ql, 8), dh = tap / 3, dw = tap - 3 * dh;
-      ib[j] = C::I_OFF + (((jr - 1 + dh) & 7) * C::IW + cl + dw) * 16;
-    }
+    for (int d = 0; d < 3; ++d) ro[d] = C::I_OFF + ((jr - 1 + d) & 7) * (C::IW * 16);
+    const bool q3 = ql == 3, q01 = ql < 2;
+    const int ib[3] = {(q3 ? ro[1] : ro[0]) + (cl + (q3 ? 0 : ql)) * 16,
+                       (q01 ? ro[1] : ro[2]) + (cl + (q01 ? 1 + ql : ql - 2)) * 16, ro[2] + (cl + 2) * 16};
     // branch-free (one basic block with conv1_2's loop, so the two can interleave): rows outside the frame read the
     // input ring's zero rows and are masked to zero like columns outside it
 #pragma unroll
@@ -191,9 +193,10 @@ void conv3x3_pair_strip(ConvArgs a, int seg, int nseg, int nstrip) {
       for (int f = 0; f < 2; ++f) {
         float v[4];
 #pragma unroll
-        for (int jj = 0; jj < 4; ++jj) v[jj] = inside ? fmaxf(acc1[f][jj] + b1[f][jj], 0.f) : 0.f;
-        pk[f].x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-        pk[f].y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+        for (int jj = 0; jj < 4; ++jj) v[jj] = fmaxf(acc1[f][jj] + b1[f][jj], 0.f);
+        // outside the frame: +0 (masked on the packed pairs, the bits a +0 float converts to)
+        pk[f].x = inside ? bf16x2_bits(v[0], v[1]) : 0u;
+        pk[f].y = inside ? bf16x2_bits(v[2], v[3]) : 0u;
       }
       // swz2(16 fr + cl, c) = 1024 fr + swz2(cl, c): ((16 fr + cl) >> 1) & 3 == (cl >> 1) & 3
       const uint4 ck = chunk_pair(pk[0], pk[1]);
@@ -316,8 +319,8 @@ void conv3x3_pair_strip(ConvArgs a, int seg, int nseg, int nstrip) {
           else if constexpr (ACT == VM_ACT_SIGMOID) t = sigmoid_precise(t);
           v[f][j] = t;
         }
-        pk[f].x = (uint32_t)f2bf(v[f][0]) | ((uint32_t)f2bf(v[f][1]) << 16);
-        pk[f].y = (uint32_t)f2bf(v[f][2]) | ((uint32_t)f2bf(v[f][3]) << 16);
+        pk[f].x = bf16x2_bits(v[f][0], v[f][1]);
+        pk[f].y = bf16x2_bits(v[f][2], v[f][3]);
       }
       if (!a.y_skip) {
         const uint4 d = chunk_pair(pk[0], pk[1]);
@@ -373,8 +376,8 @@ void conv3x3_pair_strip(ConvArgs a, int seg, int nseg, int nstrip) {
               const float u = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(t), 0xB1, 0xF, 0xF, false));
               m[j] = fmaxf(t, u);
             }
-            m2[f].x = (uint32_t)f2bf(m[0]) | ((uint32_t)f2bf(m[1]) << 16);
-            m2[f].y = (uint32_t)f2bf(m[2]) | ((uint32_t)f2bf(m[3]) << 16);
+            m2[f].x = bf16x2_bits(m[0], m[1]);
+            m2[f].y = bf16x2_bits(m[2], m[3]);
           }
           }
           const uint4 d = chunk_pair(m2[0], m2[1]);

@@ -291,7 +291,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
         add[f][j] = t.y;
       }
     auto pack4 = [](const float (&v)[4]) __attribute__((always_inline)) {
-      return make_uint2((uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16), (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16));
+      return make_uint2(bf16x2_bits(v[0], v[1]), bf16x2_bits(v[2], v[3]));
     };
     // FC == 2: the two 16-channel fragments form one 32-channel group, and chunk_pair turns the lanes' 4-channel quads
     // into whole 16-byte chunks (chunk c16 of the group): one 16-byte store per pixel row instead of two 8-byte ones

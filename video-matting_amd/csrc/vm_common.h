@@ -57,6 +57,15 @@ __device__ __forceinline__ uint16_t f2bf(float f) {
   return __builtin_bit_cast(uint16_t, b);
 }
 
+// two floats -> packed bf16 pair (lo in bits 0..15): ONE v_cvt_pk_bf16_f32 with both operands, the same RNE rounding
+// as f2bf.  Spelled as two f2bf calls, hipcc emits two conversions (second operand 0), a shift and an or.
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t bf16x2_bits(float lo, float hi) {
+  const f32x2_t v = {lo, hi};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2_t));
+}
+
 template <typename T>
 __device__ __forceinline__ float ld_elem(const T* p);
 template <>
@@ -99,7 +108,7 @@ struct Chunk<uint16_t> {
   __device__ static uint4 pack(const float* f) {
     uint32_t w[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) w[i] = uint32_t(f2bf(f[2 * i])) | (uint32_t(f2bf(f[2 * i + 1])) << 16);
+    for (int i = 0; i < 4; ++i) w[i] = bf16x2_bits(f[2 * i], f[2 * i + 1]);
     return make_uint4(w[0], w[1], w[2], w[3]);
   }
 };
