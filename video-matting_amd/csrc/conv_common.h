@@ -126,6 +126,10 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t w_rsrc(const ConvArgs& a, int 
 }
 
 constexpr int OOB = (int)0x80000000;
+// the same for the issue-bound strip pair kernel: the bit pattern of -4.0f, an inline constant, so a select of it needs
+// no v_bfrev to materialise 0x80000000 first (every descriptor here has num_records <= 0x7ffffff0).  Kept out of the
+// MFMA-bound kernels, whose schedules measured 1 % slower with it (code placement, not the instruction count).
+constexpr int OOB_INL = (int)0xC0800000;
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 

@@ -47,7 +47,9 @@ struct StripCfg {
 // XIN: 0 = bf16 frame of 8-channel pixels, 2 = f32 frame with x_c <= 8 channels (cstride <= 8)
 // ACT: the epilogue's activation as a compile-time constant (a runtime switch per element made hipcc emit a branch
 // tree per value, and this kernel is issue-bound, not MFMA-bound)
-template <int XIN, int ACT, int ABL = 0, int PIN = 1>
+// XC: the f32 frame's channel count when known at compile time (7: the video path's cmp / bg / trimap frame), 0 =
+// a.x_c at run time (a per-channel branch with its own LDS-load wait)
+template <int XIN, int ACT, int ABL = 0, int PIN = 1, int XC = 0>
 __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2)))
 void conv3x3_pair_strip(ConvArgs a, int seg, int nseg, int nstrip) {
   using C = StripCfg;
@@ -107,7 +109,7 @@ void conv3x3_pair_strip(ConvArgs a, int seg, int nseg, int nstrip) {
   // 8-row input ring.  The descriptor covers ONE image, and the fetched bytes [ws, ws + nd KB) are clamped inside it
   // (ws = the window's first byte, moved right at the image start and left at its end), so no 16-byte piece ever
   // straddles the image bounds: every needed byte is fetched, none outside the tensor.  Rows outside the frame fetch
-  // nothing (OOB offsets read as zeros).
+  // nothing (out-of-range offsets read as zeros).
   const int es = XIN == 2 ? 4 : 2, cs = a.x_cstride;
   const int pxb = cs * es, imgb = H * W * pxb;  // host: imgb >= 2 KB and < 2 GB
   const char* ximg = reinterpret_cast<const char*>(a.x) + ((long)a.x_coff + (long)n * H * W * cs) * es;
@@ -122,8 +124,8 @@ void conv3x3_pair_strip(ConvArgs a, int seg, int nseg, int nstrip) {
     const bool ok = (unsigned)ir < (unsigned)H;
     const int base = wstart(ir) + lane * 16;
     const uint32_t dst = __builtin_amdgcn_readfirstlane(raw0 + slot * C::RSZ);
-    glds16(xrs, dst, ok ? base : OOB);
-    if (nd > 1) glds16(xrs, dst + 1024, ok ? base + 1024 : OOB);
+    glds16(xrs, dst, ok ? base : OOB_INL);
+    if (nd > 1) glds16(xrs, dst + 1024, ok ? base + 1024 : OOB_INL);
   };
   auto convert_row = [&](int ir, int slot) __attribute__((always_inline)) {  // wave 0, lanes 0..35
     if (lane < C::IW) {
@@ -134,7 +136,8 @@ void conv3x3_pair_strip(ConvArgs a, int seg, int nseg, int nstrip) {
       if constexpr (XIN == 2) {
         float xz[8];
 #pragma unroll
-        for (int c = 0; c < 8; ++c) xz[c] = c < a.x_c ? *reinterpret_cast<const float*>(rp + 4 * c) : 0.f;
+        for (int c = 0; c < 8; ++c)
+          xz[c] = c < (XC ? XC : a.x_c) ? *reinterpret_cast<const float*>(rp + 4 * c) : 0.f;
         v = Chunk<T>::pack(xz);
       } else {
         v = *reinterpret_cast<const uint4*>(rp);
@@ -205,7 +208,7 @@ void conv3x3_pair_strip(ConvArgs a, int seg, int nseg, int nstrip) {
         const int c = c0 + rc - 1;
         const bool ok = jr >= s0 && jr < s1 && rc >= 1 && rc <= C::SW && c < W;
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, ck), y1rs,
-                                               ok ? ((jr * W + c) * a.y1_cstride + 32 * wave + 8 * cq16) * 2 : OOB, 0, 0);
+                                               ok ? ((int)__umul24(jr * W + c, a.y1_cstride) + 32 * wave + 8 * cq16) * 2 : OOB_INL, 0, 0);
       }
     }
   };
@@ -234,7 +237,7 @@ void conv3x3_pair_strip(ConvArgs a, int seg, int nseg, int nstrip) {
       // a buffer store per fragment whatever the lane mask (out-of-range offsets drop the rest), so the loop's
       // counted vmcnt knows exactly how many stores follow the row's DMA
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, d), hrs,
-                                             q < 3 && p < C::SW && c < W ? ((r * W + c) * 12 + 4 * q) * 4 : OOB, 0, 0);
+                                             q < 3 && p < C::SW && c < W ? ((r * W + c) * 12 + 4 * q) * 4 : OOB_INL, 0, 0);
     }
   };
 
@@ -324,7 +327,7 @@ void conv3x3_pair_strip(ConvArgs a, int seg, int nseg, int nstrip) {
       }
       if (!a.y_skip) {
         const uint4 d = chunk_pair(pk[0], pk[1]);
-        const int off = cok ? ((r * W + c) * ycs2 + (32 * wave + 8 * cq16) * 2) : OOB;
+        const int off = cok ? ((int)__umul24(r * W + c, ycs2) + (32 * wave + 8 * cq16) * 2) : OOB_INL;
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, d), yrs,
                                                off, 0, 0);
       }
@@ -383,7 +386,7 @@ void conv3x3_pair_strip(ConvArgs a, int seg, int nseg, int nstrip) {
           const uint4 d = chunk_pair(m2[0], m2[1]);
           const int pr = r >> 1, pc = c >> 1;
           const bool pok = (cl & 1) == 0 && cok && pc < PWd;
-          const int off = pok ? ((pr * PWd + pc) * a.py_cstride + 32 * wave + 8 * cq16) * 2 : OOB;
+          const int off = pok ? ((int)__umul24(pr * PWd + pc, a.py_cstride) + 32 * wave + 8 * cq16) * 2 : OOB_INL;
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, d),
                                                  prs, off, 0, 0);
         }
@@ -447,8 +450,9 @@ bool pair_strip_ok(const ConvArgs& a) {
   // (and an image holds at least the 2 KB a row fetch may span)
   const int es = a.x_f32 ? 4 : 2;
   const long imgb = (long)a.H * a.W * a.x_cstride * es;
+  // (pixel indices of a frame < 2^24: the output offsets use the full-rate 24-bit multiply)
   return a.cout == 64 && a.x_c <= 8 && (a.x_f32 ? a.x_cstride <= 8 : a.x_cstride == 8) && imgb < 0x7ffffff0L - 4096 &&
-         imgb >= 2048 && a.W > 0 && a.H > 0;
+         imgb >= 2048 && a.W > 0 && a.H > 0 && (long)a.H * a.W < (1L << 24);
 }
 
 long g_pair_strip_abl = 0;  // study build: timing-only ablations (1 no conv1_1 MFMAs, 2 no conv1_2 MFMAs, 4 no row
@@ -461,7 +465,10 @@ static void launch_strip_act(ConvArgs& a, long grid, int seg, int nseg, int nstr
   if constexpr (PIN) {
     if (!g_pair_strip_pin) return launch_strip_act<ACT, ABL, 0>(a, grid, seg, nseg, nstrip, st);
   }
-  if (a.x_f32)
+  if (a.x_f32 && a.x_c == 7)
+    hipLaunchKernelGGL((conv3x3_pair_strip<2, ACT, ABL, PIN, 7>), dim3((unsigned)grid), dim3(128), StripCfg::LDS, st, a,
+                       seg, nseg, nstrip);
+  else if (a.x_f32)
     hipLaunchKernelGGL((conv3x3_pair_strip<2, ACT, ABL, PIN>), dim3((unsigned)grid), dim3(128), StripCfg::LDS, st, a, seg,
                        nseg, nstrip);
   else
