@@ -27,6 +27,9 @@ UNET_1080 = [("conv1_1", 1080, 1920, 7, 64), ("conv1_2", 1080, 1920, 64, 64), ("
              ("upconv_4", 1080, 1920, 128, 64)]
 
 
+SPLITK = False
+
+
 def run(name, h, w, cin, cout, dtype, iters, n=1):
     tdt = ops.TORCH_DTYPE[dtype]
     cpad = (cin + 7) // 8 * 8
@@ -35,12 +38,12 @@ def run(name, h, w, cin, cout, dtype, iters, n=1):
     pc = ops.PackedConv(wt, np.zeros(cout, np.float32), tdt)
     y = torch.empty(n, h, w, cout, dtype=tdt, device="cuda")
     for _ in range(3):
-        ops.conv3x3(x, pc, "relu", out=y)
+        ops.conv3x3(x, pc, "relu", out=y, splitk=SPLITK)
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(iters):
-        ops.conv3x3(x, pc, "relu", out=y)
+        ops.conv3x3(x, pc, "relu", out=y, splitk=SPLITK)
     e1.record()
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / iters
@@ -63,7 +66,10 @@ def main():
     ap.add_argument("--option", action="append", default=[], help="extra vm_set_option key=value")
     ap.add_argument("--ab", default="", help="key=v1,v2,...: time every value per shape, interleaved in rounds")
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--splitk", action="store_true", help="allow split-K (a workspace; the training path's setting)")
     args = ap.parse_args()
+    global SPLITK
+    SPLITK = args.splitk
     for kv in args.option:
         k, v = kv.split("=")
         _lib.set_option(k, int(v))

@@ -48,7 +48,7 @@ for dt in fp32 bf16; do
         -- python3 "$REPO/bench.py" --only temporal --steps 20 --temporal-dtypes $dt --temporal-sizes $hw "$@"
     cp "$(find "$OUT/temporal_${dt}_${hw}" -name '*kernel_stats.csv' | head -n 1)" \
        "$REPO/profiles/${TAG}_temporal_${dt}_${hw}_kernel_stats.csv"
-    tail -n 1 "$OUT/temporal_${dt}_${hw}.log" > "$REPO/profiles/${TAG}_temporal_${dt}_${hw}.json"
+    grep "^{" "$OUT/temporal_${dt}_${hw}.log" | tail -n 1 > "$REPO/profiles/${TAG}_temporal_${dt}_${hw}.json"
   done
 done
 fi
@@ -56,13 +56,13 @@ if ! skip train; then
 run 300 train.log rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/train" -o run \
     -- python3 "$REPO/bench.py" --only train --steps 20 --warmup 3 "$@"  # eager: side-stream select chains
 cp "$(find "$OUT/train" -name '*kernel_stats.csv' | head -n 1)" "$REPO/profiles/${TAG}_train_kernel_stats.csv"
-tail -n 1 "$OUT/train.log" > "$REPO/profiles/${TAG}_train.json"
+grep "^{" "$OUT/train.log" | tail -n 1 > "$REPO/profiles/${TAG}_train.json"
 fi
 if ! skip train_small; then
 run 300 train_small.log rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/train_small" -o run \
     -- python3 "$REPO/bench.py" --only train_small --steps 20 --warmup 3 "$@"
 cp "$(find "$OUT/train_small" -name '*kernel_stats.csv' | head -n 1)" "$REPO/profiles/${TAG}_train_small_kernel_stats.csv"
-tail -n 1 "$OUT/train_small.log" > "$REPO/profiles/${TAG}_train_small.json"
+grep "^{" "$OUT/train_small.log" | tail -n 1 > "$REPO/profiles/${TAG}_train_small.json"
 fi
 cp "$REPO"/profiles/${TAG}_* "$REPO/gpurun_out/"
 skip bench && exit 0
