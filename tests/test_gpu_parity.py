@@ -1033,11 +1033,13 @@ def test_unet_video_1080p_bf16_properties(vgg0):
     assert err < 5e-2
 
 
-@pytest.mark.parametrize("xc,yc,ys,odt", [(3, 8, 8, torch.bfloat16), (3, 3, 32, torch.bfloat16), (7, 16, 16, torch.float32),
+@pytest.mark.parametrize("xc,yc,ys,odt", [(3, 8, 8, torch.bfloat16), (8, 8, 16, torch.bfloat16), (3, 3, 32, torch.bfloat16),
+                                          (7, 16, 16, torch.float32),
                                           (20, 24, 24, torch.bfloat16), (5, 5, 8, torch.float32)])
 @pytest.mark.parametrize("affine", [False, True])
 def test_convert_views(xc, yc, ys, odt, affine):
-    """vm_convert_nhwc (pixel-per-thread form for outputs of <= 16 channels, element form above): x's channels
+    """vm_convert_nhwc (one 16-byte store per pixel for an aligned 8-channel bf16 output, pixel-per-thread form for
+    other outputs of <= 16 channels, element form above): x's channels
     through the optional affine + relu into a channel slice of a wider buffer, extra channels zero, the rest of the
     buffer untouched."""
     from vmatting import ops

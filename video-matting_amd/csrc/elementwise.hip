@@ -282,6 +282,18 @@ __global__ void convert_px_kernel(View x, View y, const float* scale, const floa
     for (int c = 0; c < y.c; ++c) stv(y, p, c, c < x.c ? convert_one(x, p, c, scale, shift, act) : 0.f);
 }
 
+// one 16-byte chunk of 8 bf16 channels per pixel (the training towers' 8-channel input frames, loader outputs): the
+// per-channel 2-byte stores of convert_px_kernel ran these at ~0.7 TB/s
+__global__ void convert_px8_bf16_kernel(View x, View y, const float* scale, const float* shift, int act) {
+  const long M = (long)y.n * y.h * y.w;
+  for (long p = blockIdx.x * (long)blockDim.x + threadIdx.x; p < M; p += (long)gridDim.x * blockDim.x) {
+    float f[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) f[c] = c < x.c ? convert_one(x, p, c, scale, shift, act) : 0.f;
+    *reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(y.p) + p * y.cs + y.coff) = Chunk<uint16_t>::pack(f);
+  }
+}
+
 // ---------------------------------------------------------------- batch-norm statistics
 // tf.contrib.layers.batch_norm(is_training=True) (unet_simple.py:25): per-channel mean and biased
 // variance over N*H*W.  Pass 1: grid (ceil(C/64), nblk); lane = channel (64 consecutive channels of a
@@ -479,7 +491,10 @@ extern "C" int vm_convert_nhwc(const vm_tensor* x, vm_tensor* y, const float* sc
   if (y->n != x->n || y->h != x->h || y->w != x->w || y->c < x->c) return fail(VM_EINVAL, "convert: shape mismatch");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const long work = (long)y->n * y->h * y->w * y->c;
-  if (y->c <= 16)
+  if (y->dtype == VM_BF16 && y->c == 8 && vec16_ok(y))
+    hipLaunchKernelGGL(convert_px8_bf16_kernel, dim3(grid_for(work / 8, 256)), dim3(256), 0, st, view(x), view(y), scale,
+                       shift, act);
+  else if (y->c <= 16)
     hipLaunchKernelGGL(convert_px_kernel, dim3(grid_for(work / y->c, 256)), dim3(256), 0, st, view(x), view(y), scale,
                        shift, act);
   else
