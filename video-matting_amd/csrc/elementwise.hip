@@ -340,8 +340,8 @@ __global__ __launch_bounds__(256) void bn_partial_kernel(View x, double* part, i
         s += sh[0][w][k * CP + threadIdx.x];
         ss += sh[1][w][k * CP + threadIdx.x];
       }
-    part[(long)blockIdx.y * x.c + c] = s;
-    part[(long)nblk * x.c + (long)blockIdx.y * x.c + c] = ss;
+    part[(long)c * nblk + blockIdx.y] = s;  // channel-major [k][C][nblk]: the fold reads each channel's run
+    part[(long)nblk * x.c + (long)c * nblk + blockIdx.y] = ss;
   }
 }
 

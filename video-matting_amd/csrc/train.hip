@@ -146,9 +146,9 @@ __global__ __launch_bounds__(256) void bn_bwd_partial(V x, V dy, V y, const floa
         s2 += sh[1][w][k * CP + threadIdx.x];
         s3 += sh[2][w][k * CP + threadIdx.x];
       }
-    part[(long)blockIdx.y * dy.c + c] = s1;
-    part[(long)nblk * dy.c + (long)blockIdx.y * dy.c + c] = s2;
-    part[2L * nblk * dy.c + (long)blockIdx.y * dy.c + c] = s3;
+    part[(long)c * nblk + blockIdx.y] = s1;  // channel-major [k][C][nblk] (vm_common.h fold_columns)
+    part[(long)nblk * dy.c + (long)c * nblk + blockIdx.y] = s2;
+    part[2L * nblk * dy.c + (long)c * nblk + blockIdx.y] = s3;
   }
 }
 

@@ -145,8 +145,10 @@ inline int bn_blocks(long M, int C) {
   return nb < 1 ? 1 : (int)nb;
 }
 
-// column c of k (<= 3) stacked [nblk][C] double tables (table j at part + j * nblk * C), summed by one 256-thread
-// block: 4 rows' loads in flight per thread, then a wave shuffle tree and an LDS fold; the sums land in thread 0
+// channel c of k (<= 3) stacked channel-major [C][nblk] double tables (table j at part + j * nblk * C), summed by one
+// 256-thread block: 4 partials' loads in flight per thread, then a wave shuffle tree and an LDS fold; the sums land
+// in thread 0.  (r04: the tables were [nblk][C], so every load of the fold touched its own cache line — C * 8 bytes
+// apart; channel-major they are one contiguous run per channel, the same values summed in the same order)
 __device__ __forceinline__ void fold_columns(const double* part, int nblk, int C, int c, int k, double* out) {
   __shared__ double sh[3][4];
   double s[3] = {0.0, 0.0, 0.0};
@@ -158,7 +160,7 @@ __device__ __forceinline__ void fold_columns(const double* part, int nblk, int C
 #pragma unroll
     for (int j = 0; j < 3; ++j)
 #pragma unroll
-      for (int u = 0; u < 4; ++u) v[j][u] = j < k ? part[j * tab + (long)(b + u * 256) * C + c] : 0.0;
+      for (int u = 0; u < 4; ++u) v[j][u] = j < k ? part[j * tab + (long)c * nblk + b + u * 256] : 0.0;
 #pragma unroll
     for (int j = 0; j < 3; ++j)
 #pragma unroll
@@ -167,7 +169,7 @@ __device__ __forceinline__ void fold_columns(const double* part, int nblk, int C
   for (; b < nblk; b += 256)
 #pragma unroll
     for (int j = 0; j < 3; ++j)
-      if (j < k) s[j] += part[j * tab + (long)b * C + c];
+      if (j < k) s[j] += part[j * tab + (long)c * nblk + b];
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
     for (int o = 32; o > 0; o >>= 1) s[j] += __shfl_down(s[j], o);
