@@ -530,7 +530,7 @@ _ws_cache = {}
 
 
 def _workspace(nbytes, device):
-    key = (str(device), torch.cuda.current_stream(device).cuda_stream)
+    key = (str(device), _lib.current_raw_stream(device.index if isinstance(device, torch.device) else None))
     buf = _ws_cache.get(key)
     if buf is None or buf.numel() < nbytes:
         buf = torch.empty(max(nbytes, 1 << 16), dtype=torch.uint8, device=device)
