@@ -230,6 +230,39 @@ __global__ __launch_bounds__(256) void bn_bwd_apply(V x, V dy, V y, const float*
   }
 }
 
+// the unmasked 2-channel f32 case (the training step's select1_* convs) one pixel per thread with 8-byte loads and
+// stores: at their 32-byte pixel stride the 2-lanes-per-pixel form above ran at ~0.5 TB/s, its per-element dtype
+// branches and 64-bit index products the bound.  Per element the same expression as bn_bwd_apply, so the same values.
+__global__ __launch_bounds__(256) void bn_bwd_apply2_f32(const float* x, int xcs, const float* dy, int dycs, float* dx,
+                                                         int dxcs, long M, const float* mean, const float* var,
+                                                         const float* gamma, float eps, const float* sum_g,
+                                                         const float* sum_gx) {
+  const float invM = 1.0f / (float)M;
+  float r[2], m[2], k[2], sg[2], sgx[2];
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    r[c] = 1.0f / sqrtf(var[c] + eps);
+    m[c] = mean[c];
+    k[c] = (gamma ? gamma[c] : 1.f) * r[c];
+    sg[c] = sum_g[c] * invM;
+    sgx[c] = sum_gx[c] * invM;
+  }
+  for (long p = blockIdx.x * (long)blockDim.x + threadIdx.x; p < M; p += (long)gridDim.x * blockDim.x) {
+    const float2 x2 = *reinterpret_cast<const float2*>(x + p * xcs);
+    const float2 g2 = *reinterpret_cast<const float2*>(dy + p * dycs);
+    const float xv[2] = {x2.x, x2.y}, g[2] = {g2.x, g2.y};
+    float v[2];
+#pragma unroll
+    for (int c = 0; c < 2; ++c) v[c] = k[c] * (g[c] - sg[c] - (xv[c] - m[c]) * r[c] * sgx[c]);
+    *reinterpret_cast<float2*>(dx + p * dxcs) = make_float2(v[0], v[1]);
+  }
+}
+
+static bool f32_pair(const vm_tensor* t) {  // 2 f32 channels at an 8-byte aligned offset of every pixel
+  return t->dtype == VM_F32 && t->c == 2 && t->cstride % 2 == 0 && t->coff % 2 == 0 &&
+         reinterpret_cast<uintptr_t>(t->ptr) % 8 == 0;
+}
+
 // channels [0, split) go to dxlo at c, [split, C) to dx / dx2 at c - split (split 0: all to dx / dx2)
 template <int CP>
 __global__ __launch_bounds__(256) void relu_bwd_kernel(V dy, V y, V dx, V dx2, V dxlo, int split) {
@@ -1376,6 +1409,13 @@ extern "C" int vm_bn_backward_ex_nhwc(const vm_tensor* x, const vm_tensor* dy, c
                      eps, M);
   rc = check_launch("bn_backward_final");
   if (rc || !dx) return rc;
+  if (!y && !dx2 && f32_pair(x) && f32_pair(dy) && f32_pair(dx) && x->cstride > 0) {
+    hipLaunchKernelGGL(bn_bwd_apply2_f32, dim3(grid_for(M, 256)), dim3(256), 0, st,
+                       reinterpret_cast<const float*>(x->ptr) + x->coff, x->cstride,
+                       reinterpret_cast<const float*>(dy->ptr) + dy->coff, dy->cstride,
+                       reinterpret_cast<float*>(dx->ptr) + dx->coff, dx->cstride, M, mean, var, gamma, eps, sg, sgx);
+    return check_launch("bn_backward_apply");
+  }
   const int cp = lanes_for(C);
   const dim3 grid = lanes_grid(M, C, cp);
   const V dxv = mk(dx), dx2v = dx2 ? mk(dx2) : V{};
