@@ -1,8 +1,12 @@
 """Benchmark: alpha-mattes/sec of unet.UNetVideo at 1920x1080 (BASELINE.json configs[1]; configs[3] at N>1).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--dtype bf16|fp32]
-    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
-        --master-port P bench.py --gpus N --steps K --warmup W
+    python bench.py --gpus N --dist-selftest      # CPU-only (gloo) check of the N-rank launcher and collectives
+
+With --gpus N > 1 bench.py starts its own N ranks (one child process per GPU, RANK / LOCAL_RANK / WORLD_SIZE /
+MASTER_ADDR=127.0.0.1 / MASTER_PORT in their environment) before anything touches a GPU, waits for them and exits
+with rank 0's code (the first failing rank's, if any fails).  Launched by torchrun instead (WORLD_SIZE already set),
+it is one of those ranks.  Either way a run whose initialised world differs from --gpus exits non-zero.
 
 A step = one UNetVideo forward over B synthetic 1080p 7-channel frames per GPU (inputs resident
 in HBM before timing).  Frame-parallel: every rank runs its own frames, no collective in the data
@@ -18,7 +22,9 @@ import argparse
 import json
 import os
 import platform
+import socket
 import statistics
+import subprocess
 import sys
 import time
 
@@ -791,6 +797,74 @@ def conv_roofline(prof, args):
     return rec
 
 
+# ------------------------------------------------------------------------------------------------ launcher
+
+def _free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def launch_ranks(n, argv):
+    """One child process of this script per rank (BASELINE metric at 1/2/4/8 GPUs), with torchrun's
+    environment contract.  The parent never touches a GPU (no HIP call, no torch.cuda initialisation) and never
+    re-execs itself: it only waits.  When a rank fails the others are stopped (they would block in a collective).
+    Returns rank 0's exit code, or the first failing rank's."""
+    port = int(os.environ.get("MASTER_PORT") or _free_port())
+    procs = []
+    try:
+        for r in range(n):
+            env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                       GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+            procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+        rcs = [None] * n
+        while any(rc is None for rc in rcs):
+            for r, p in enumerate(procs):
+                if rcs[r] is None:
+                    rcs[r] = p.poll()
+            failed = [r for r in range(n) if rcs[r] not in (None, 0)]
+            if failed:
+                log("bench launcher: rank %d exited with %d; stopping the other ranks" % (failed[0], rcs[failed[0]]))
+                for p in procs:
+                    if p.poll() is None:
+                        p.terminate()
+                for p in procs:
+                    try:
+                        p.wait(30)
+                    except subprocess.TimeoutExpired:
+                        p.kill()
+                        p.wait()
+                return rcs[failed[0]]
+            time.sleep(0.2)
+        return rcs[0]
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+
+
+def dist_selftest(rank, world):
+    """CPU-only (gloo) check of what the multi-GPU run relies on, through the same launcher: the weight broadcast
+    from rank 0 (parallel.broadcast_tensors) and the matte all-gather of an uneven frame split
+    (parallel.gather_frames, config 4).  Rank 0 prints one JSON line."""
+    n_frames = 2 * world + 1  # uneven: the first ranks get 2 frames, the last 3
+    wts = [torch.arange(64, dtype=torch.float32) * (rank + 1), torch.full((3, 5), float(rank), dtype=torch.float64)]
+    parallel.broadcast_tensors(wts, src=0)
+    ok_b = torch.equal(wts[0], torch.arange(64, dtype=torch.float32)) and bool((wts[1] == 0).all())
+    a, b = parallel.shard_range(n_frames, rank, world)
+    local = torch.arange(a, b, dtype=torch.float32).view(-1, 1, 1, 1).expand(b - a, 4, 6, 1).contiguous()
+    full = parallel.gather_frames(local, n_frames)
+    ok_g = tuple(full.shape) == (n_frames, 4, 6, 1) and all(bool((full[i] == i).all()) for i in range(n_frames))
+    ok = torch.tensor([1 if ok_b and ok_g else 0], dtype=torch.int64)
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    if rank == 0:
+        print(json.dumps({"selftest": "dist", "n_gpus": world, "backend": dist.get_backend(), "frames": n_frames,
+                          "split": [list(parallel.shard_range(n_frames, r, world)) for r in range(world)],
+                          "broadcast_ok": ok_b, "gather_ok": ok_g, "ok": bool(ok.item())}), flush=True)
+    return 0 if ok.item() else 1
+
+
 # ------------------------------------------------------------------------------------------------ main
 
 def main():
@@ -830,13 +904,35 @@ def main():
                     help="profiling passes: run just this record (rank 0 / N=1) and print it")
     ap.add_argument("--temporal-sizes", default="500x1200,1080x1920", help="config-3 sizes HxW, comma separated")
     ap.add_argument("--temporal-dtypes", default="fp32,bf16", help="config-3 compute dtypes, comma separated")
+    ap.add_argument("--dist-selftest", action="store_true",
+                    help="CPU-only: the N-rank launcher + gloo broadcast / uneven all-gather, no GPU")
     args = ap.parse_args()
     t_sizes = [tuple(int(v) for v in hw.split("x")) for hw in args.temporal_sizes.split(",")]
     t_dtypes = args.temporal_dtypes.split(",")
 
-    rank, world, local = parallel.init_from_env("nccl")
+    if args.gpus < 1:
+        log("bench: --gpus must be >= 1")
+        return 2
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # this process is the launcher: start the N ranks before anything touches a GPU
+        if not args.dist_selftest and torch.cuda.device_count() < args.gpus:  # device_count does not init HIP
+            log("bench: --gpus %d but %d GPU(s) visible" % (args.gpus, torch.cuda.device_count()))
+            return 2
+        return launch_ranks(args.gpus, sys.argv[1:])
+
+    rank, world, local = parallel.init_from_env("gloo" if args.dist_selftest else "nccl")
     if world != args.gpus:
-        log("warning: --gpus %d but WORLD_SIZE %d; using WORLD_SIZE" % (args.gpus, world))
+        log("bench: --gpus %d but the initialised world has %d rank(s)" % (args.gpus, world))
+        if dist.is_initialized():
+            dist.destroy_process_group()
+        return 2
+    if args.dist_selftest:
+        rc = dist_selftest(rank, world) if world > 1 else 0
+        if world == 1:
+            print(json.dumps({"selftest": "dist", "n_gpus": 1, "ok": True}), flush=True)
+        if dist.is_initialized():
+            dist.destroy_process_group()
+        return rc
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     for kv in args.option:
@@ -858,7 +954,7 @@ def main():
             print(json.dumps({"only": args.only, "record": rec}), flush=True)
         if world > 1:
             dist.destroy_process_group()
-        return
+        return 0
 
     # identical weights everywhere: every rank draws from the same seeds, then rank 0's packed
     # buffers are broadcast (one RCCL collective) so replicas are bit-identical by construction
@@ -994,7 +1090,8 @@ def main():
         print(json.dumps(rec), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -69,3 +69,33 @@ def test_ops_refuse_cpu_tensors():
     from vmatting import ops
     with pytest.raises(TypeError):
         ops.maxpool2x2(torch.zeros(1, 4, 4, 8))
+
+
+def test_raw_stream_falls_back_to_public_getter(monkeypatch):
+    """if a torch release drops the private stream getters, every launch still gets the current stream's
+    handle, from torch.cuda.current_stream(d).cuda_stream (no GPU needed: the public call is stubbed)."""
+    import torch
+    from vmatting import _lib
+
+    class FakeStream:
+        cuda_stream = 0x1234
+
+    seen = []
+    monkeypatch.setattr(_lib, "_GET_RAW_STREAM", None)
+    monkeypatch.setattr(torch.cuda, "current_stream", lambda d=None: seen.append(d) or FakeStream())
+    assert _lib.current_raw_stream() == 0x1234
+    assert _lib.current_raw_stream(3) == 0x1234
+    assert seen == [None, 3]
+
+
+@pytest.mark.gpu
+def test_raw_stream_matches_public_getter():
+    """The private getters return torch.cuda.current_stream().cuda_stream, outside and inside a stream context."""
+    import torch
+    from vmatting import _lib
+    assert _lib.current_raw_stream() == torch.cuda.current_stream().cuda_stream
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        assert _lib.current_raw_stream() == s.cuda_stream == torch.cuda.current_stream().cuda_stream
+        assert _lib.current_raw_stream(torch.cuda.current_device()) == s.cuda_stream
+    assert _lib.current_raw_stream() == torch.cuda.current_stream().cuda_stream != s.cuda_stream

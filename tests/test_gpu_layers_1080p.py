@@ -215,3 +215,28 @@ def test_head_logits_alpha(timed):
     ae = oops.sigmoid(e)
     tol = 0.25 * np.abs(d["logits"] - e) + 2e-7
     assert (np.abs(d["out"] - ae) <= tol).all()
+
+
+def test_timed_graph_replay_equals_pinned_eager_pass(timed):
+    """bench.py times HIP-graph replays of this forward (`model.capture(x)`, bench.py's timed
+    loop), while the layer checks above pin the eager pass.  The replays on the timed frame must equal that eager
+    pass bit for bit — alpha and logits — so the pinned numbers are the timed ones (first replay and the 3rd)."""
+    from vmatting import unet, video
+    from vmatting.weights import synthetic_vgg16
+    np.random.seed(0)
+    m = unet.UNetVideo(synthetic_vgg16(0), dtype="bf16", device=DEV)
+    m.split_head = True
+    m.fuse_up_head = True
+    m.prepare()
+    x = video.synthetic_frames(1, H, W, first=0, device=DEV)
+    g = m.capture(x)
+    for i in range(3):
+        g.replay()
+        torch.cuda.synchronize()
+        if i in (0, 2):
+            alpha = g.output.float().cpu().numpy()
+            logits = m.conv1_3.float().cpu().numpy()
+            assert np.array_equal(alpha, timed["out"]), (i, np.abs(alpha - timed["out"]).max())
+            assert np.array_equal(logits, timed["logits"]), (i, np.abs(logits - timed["logits"]).max())
+    del g, m
+    torch.cuda.empty_cache()

@@ -216,32 +216,34 @@ def test_small_bf16_steps_run():
 
 # ------------------------------------------------------------------------------------------- world 2 (gloo)
 
-def _worker(rank, world, port, q, kind, sizes, sync_bn, seed_base, dtype="fp32"):
+def _worker(rank, world, port, q, kind, sizes, sync_bn, seed_base, dtype="fp32", pre=()):
+    """One forward + backward per rank on its slice of a batch split ``sizes``, then the DDP exchange + Adam.
+    ``pre``: earlier splits run first (forward + backward, no update) — a batch size that changes between steps."""
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
     try:
         from vmatting import parallel
         parallel.init_from_env(backend="gloo")  # gloo moves the cuda tensors; both ranks share cuda:0
         torch.cuda.set_device(0)
-        a, b = sum(sizes[:rank]), sum(sizes[:rank + 1])
         if kind == "small":
             from vmatting.small_train import SmallTrainer
             np.random.seed(seed_base + rank)  # different draws per rank: the broadcast must make them identical
             trn = SmallTrainer(6, dtype, "cuda:0", sync_bn=sync_bn)
-            cmp, bg, gt, fg = (x[a:b] for x in _small_batch(sum(sizes), 32, 40, seed=13))
-            p0 = trn.flat.cpu().numpy()
-            trn.forward(cmp, bg)
-            trn.grad.zero_()
-            trn.backward(T(gt), T(fg), T(bg), T(cmp))
         else:
             from vmatting.train import VideoTrainer
             from vmatting.weights import synthetic_vgg16
             params = om.unet_simple_params(np.random.RandomState(1))
             trn = VideoTrainer(synthetic_vgg16(0), dtype, "cuda:0", params=params, sync_bn=sync_bn)
-            from test_gpu_train import _batch
-            cmp, bg, warped, gt, fg = (x[a:b] for x in _batch(sum(sizes), 48, 64, seed=13))
-            p0 = trn.flat.cpu().numpy()
-            trn.forward(cmp, bg, warped)
+        p0 = trn.flat.cpu().numpy()
+        for sz in tuple(pre) + (sizes,):
+            a, b = sum(sz[:rank]), sum(sz[:rank + 1])
+            if kind == "small":
+                cmp, bg, gt, fg = (x[a:b] for x in _small_batch(sum(sz), 32, 40, seed=13))
+                trn.forward(cmp, bg)
+            else:
+                from test_gpu_train import _batch
+                cmp, bg, warped, gt, fg = (x[a:b] for x in _batch(sum(sz), 48, 64, seed=13))
+                trn.forward(cmp, bg, warped)
             trn.grad.zero_()
             trn.backward(T(gt), T(fg), T(bg), T(cmp))
         torch.cuda.synchronize()
@@ -257,12 +259,12 @@ def _worker(rank, world, port, q, kind, sizes, sync_bn, seed_base, dtype="fp32")
             dist.destroy_process_group()
 
 
-def _run_world2(kind, sizes, sync_bn, seed_base=100, dtype="fp32"):
+def _run_world2(kind, sizes, sync_bn, seed_base=100, dtype="fp32", pre=()):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = 29500 + (os.getpid() % 97) + (7 if sync_bn else 0) + (3 if kind == "small" else 0) + \
-        (11 if dtype == "bf16" else 0)
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, kind, sizes, sync_bn, seed_base, dtype))
+        (11 if dtype == "bf16" else 0) + (17 if pre else 0)
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, kind, sizes, sync_bn, seed_base, dtype, pre))
              for r in range(2)]
     for p in procs:
         p.start()
@@ -282,15 +284,17 @@ def test_small_ddp_replicas_start_and_stay_identical():
     assert not np.array_equal(res[0][2], res[1][2])  # different data -> different local gradients
 
 
-@pytest.mark.parametrize("kind", ["small", "video"])
-def test_syncbn_unequal_batches_match_single_device(kind):
-    """SyncBN with unequal per-rank batches (1 and 2 samples; ADVICE r03: the backward must use the forward's global
-    pixel count).  The replicas jointly minimise the sum of their batch-mean losses, S = l_0 + (l_1 + l_2) / 2, with
-    batch statistics over all 3 samples; the all-reduced gradient must equal dS/dW of the float64 restatement on the
-    whole batch with those per-sample weights (a wrong count in the BN backward moves every gradient upstream of a
-    BN by O(1))."""
-    sizes = (1, 2)
-    res = _run_world2(kind, sizes, True)
+@pytest.mark.parametrize("kind,pre,sizes", [("small", (), (1, 2)), ("video", (), (1, 2)),
+                                             ("small", ((2, 2),), (2, 1)), ("video", ((2, 2),), (2, 1))])
+def test_syncbn_unequal_batches_match_single_device(kind, pre, sizes):
+    """SyncBN with unequal per-rank batches (the backward must use the forward's global pixel count).
+    The replicas jointly minimise the sum of their batch-mean losses, e.g. S = l_0 + (l_1 + l_2) / 2 for sizes (1, 2),
+    with batch statistics over the whole batch; the all-reduced gradient must equal dS/dW of the float64 restatement
+    on the whole batch with those per-sample weights (a wrong count in the BN backward moves every gradient upstream
+    of a BN by O(1)).  ``pre``: a (2, 2) step first, then (2, 1) — an uneven last shard after full
+    steps, where only rank 1's batch changes; every rank must still run the same collectives and use this step's
+    global count."""
+    res = _run_world2(kind, sizes, True, pre=pre)
     np.testing.assert_array_equal(res[0][4], res[1][4])  # the all-reduced gradient is the same on both ranks
     g = res[0][4].astype(np.float64)
     wts = [1.0 / sizes[0]] * sizes[0] + [1.0 / sizes[1]] * sizes[1]
@@ -303,7 +307,7 @@ def test_syncbn_unequal_batches_match_single_device(kind):
         for name, ci, co in NEW_CONVS:
             w, b = init_conv(6 if ci is None else ci, co)
             params[name] = (w, None if name.startswith("upconv") else b)
-        cmp, bg, gt, fg = _small_batch(3, 32, 40, seed=13)
+        cmp, bg, gt, fg = _small_batch(sum(sizes), 32, 40, seed=13)
         _, _, grads, _ = tr.small_step_grads(cmp, bg, gt, fg, params, sample_weights=wts)
         layout = lay(6)[0]
     else:
@@ -311,7 +315,7 @@ def test_syncbn_unequal_batches_match_single_device(kind):
         from vmatting.train import param_layout as lay
         from vmatting.weights import synthetic_vgg16
         params = om.unet_simple_params(np.random.RandomState(1))
-        cmp, bg, warped, gt, fg = _batch(3, 48, 64, seed=13)
+        cmp, bg, warped, gt, fg = _batch(sum(sizes), 48, 64, seed=13)
         _, _, grads = tr.train_step_grads(cmp, bg, warped, gt, fg, synthetic_vgg16(0), params, sample_weights=wts)
         layout = lay()[0]
     bad, worst = [], 0.0

@@ -189,3 +189,38 @@ def test_load_vgg16_explicit_npy_is_not_redirected(tmp_path):
         weights.load_vgg16(str(tmp_path / "vgg16.npy"))
     got = weights.load_vgg16(str(tmp_path / "vgg16.npz"))
     assert list(got) == ["conv1_1"] and np.array_equal(got["conv1_1"][0], d["conv1_1"][0])
+
+
+def _bench(*args, env=None):
+    import json
+    import subprocess
+    import sys
+    from conftest import REPO
+    e = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
+        e.pop(k, None)
+    e.update(env or {})
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py")] + list(args), env=e, capture_output=True,
+                       text=True, timeout=150)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    return r.returncode, [json.loads(ln) for ln in lines], r.stderr
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_bench_launches_its_own_ranks(n):
+    """`bench.py --gpus N` without torchrun starts N ranks itself (the same launcher the GPU run
+    uses) — here with --dist-selftest: gloo on the CPU, rank 0's broadcast and the uneven matte all-gather."""
+    rc, recs, err = _bench("--gpus", str(n), "--dist-selftest")
+    assert rc == 0, err[-2000:]
+    assert len(recs) == 1, recs  # only rank 0 prints
+    r = recs[0]
+    assert r["n_gpus"] == n and r["backend"] == "gloo" and r["ok"] and r["broadcast_ok"] and r["gather_ok"]
+    assert r["frames"] == 2 * n + 1 and r["split"][-1][1] == 2 * n + 1
+
+
+def test_bench_refuses_a_world_other_than_gpus():
+    """A run whose initialised world differs from --gpus (here: a torchrun-style env of world 1) exits non-zero
+    instead of reporting a one-GPU number as N GPUs."""
+    rc, recs, err = _bench("--gpus", "2", "--dist-selftest", env={"WORLD_SIZE": "1", "RANK": "0"})
+    assert rc != 0 and not recs
+    assert "initialised world" in err

@@ -197,14 +197,22 @@ def last_conv_kernel():
     return lib().vm_conv3x3_last_kernel().decode()
 
 
+# torch's private C getters behind torch.cuda.current_stream(d).cuda_stream, looked up once; if a torch release
+# renames or drops them, current_raw_stream falls back to the public call (same handle, ~6 us more per launch)
+_GET_RAW_STREAM = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+_GET_DEVICE = getattr(torch._C, "_cuda_getDevice", None)
+
+
 def current_raw_stream(device_index=None):
     """The current stream's raw hipStream_t (as an int) on ``device_index`` (default: the current device).  The same
     handle as torch.cuda.current_stream(d).cuda_stream, from the two C-level getters that call wraps: that call
     builds a Stream object and resolves the device through several Python layers, ~6 us per call, and every
     kernel launch asks for it (profiled: ~230 calls = ~1.4 ms of host time per training step)."""
+    if _GET_RAW_STREAM is None or _GET_DEVICE is None:
+        return torch.cuda.current_stream(device_index).cuda_stream
     if not torch.cuda.is_initialized():
         torch.cuda.init()
-    return torch._C._cuda_getCurrentRawStream(torch._C._cuda_getDevice() if device_index is None else device_index)
+    return _GET_RAW_STREAM(_GET_DEVICE() if device_index is None else device_index)
 
 
 def stream_handle(stream=None):

@@ -186,7 +186,6 @@ class SmallTrainer(TrainerBase):
         n, h, w, c = cmp.shape
         if self.cin != 2 * c or tuple(bg.shape) != (n, h, w, c):
             raise ValueError("SmallTrainer(cin=%d) expects cmp, bg of %d channels each" % (self.cin, self.cin // 2))
-        self._cur_gbatch = self._global_batch(n, h, w) if self.sync_bn else None
         b = self._buffers(n, h, w)
         b["in6"][..., :c].copy_(cmp)  # small_train.py:95 input = concat([in_cmp, in_bg], -1)
         b["in6"][..., c:].copy_(bg)

@@ -89,25 +89,8 @@ class TrainerBase:
         self.t = 0
         self._b1p = np.float32(1.0)
         self._b2p = np.float32(1.0)
-        self._gbatch = {}
-
-    def _global_batch(self, n, h, w):
-        """SyncBN: the frames of the global batch (sum of every replica's n, made once per batch shape on the host so
-        the backward's pixel counts need no device read); replicas must share the frame size."""
-        key = (n, h, w)
-        if key not in self._gbatch:
-            t = torch.tensor([float(n), float(h), float(w), -float(h), -float(w)], dtype=torch.float64,
-                             device=self.device)
-            s = t[:1].clone()
-            parallel.allreduce_sum(s)
-            mx = t[1:].clone()
-            if torch.distributed.is_initialized():
-                torch.distributed.all_reduce(mx, op=torch.distributed.ReduceOp.MAX)
-            mx = mx.cpu().numpy()
-            if mx[0] != -mx[2] or mx[1] != -mx[3]:
-                raise ValueError("SyncBN: every replica must train on the same frame size")
-            self._gbatch[key] = int(round(float(s.item())))
-        return self._gbatch[key]
+        # SyncBN: every BN layer's global pixel count from its forward all-reduce (device f64), by mean buffer
+        self._gcount = {}
 
     def _stats(self, x, mean, var):
         """Batch mean / biased variance of x's channels; SyncBN: over every replica's pixels (count-weighted, the
@@ -121,12 +104,16 @@ class TrainerBase:
             gm = t[0] / t[2]
             mean.copy_(gm)
             var.copy_((t[1] / t[2] - gm * gm).clamp_min(0.0))
+            # every replica's pixels, summed by the same collective: the count the backward divides by.  Taken per
+            # step and per layer from this all-reduce (never cached on a local key: replicas may change their batch
+            # independently, e.g. an uneven last shard), and kept on the device (no host sync, capturable)
+            self._gcount[mean.data_ptr()] = t[2, :1]
 
     def _bn_backward(self, x, dy, mask, mean, var, scope, dx, dx2=None, dbias=None):
         """BN(+relu mask) backward: dx, dgamma / dbeta (local sums, DDP averages them) and optionally the conv-bias
         gradient.  SyncBN: the local channel sums are all-reduced and the input gradient uses the global ones over
-        the global pixel count — the same count the forward's statistics were weighted by (replicas may hold
-        different batch sizes, e.g. an uneven last shard)."""
+        the global pixel count — the count the forward's statistics all-reduce summed for this layer (replicas may
+        hold different batch sizes or frame sizes, e.g. an uneven last shard)."""
         gamma, dgamma, dbeta = self.P[scope, "gamma"], self.G[scope, "gamma"], self.G[scope, "beta"]
         if not self.sync_bn:
             return ops.bn_backward(x, dy, mask, mean, var, gamma, EPS, dx=dx, dgamma=dgamma, dbeta=dbeta, dx2=dx2,
@@ -135,16 +122,12 @@ class TrainerBase:
         sums = torch.cat([dbeta, dgamma])
         parallel.allreduce_sum(sums)
         c = dbeta.numel()
-        n, h, w = x.shape[0], x.shape[1], x.shape[2]
-        count = self._global_batch_for(n) * h * w
-        ops.bn_backward_apply(x, dy, mask, mean, var, gamma, sums[:c], sums[c:], count, dx, EPS, dx2=dx2)
+        # the global sums as means over the global count (device division: the kernel then divides by 1)
+        means = (sums.double() / self._gcount[mean.data_ptr()]).float()
+        ops.bn_backward_apply(x, dy, mask, mean, var, gamma, means[:c], means[c:], 1, dx, EPS, dx2=dx2)
         if dbias is not None:  # the conv bias's gradient = channel sum of this replica's dx
             ops.bn_backward(None, dx, None, None, None, None, EPS, dbeta=dbias)
         return dx
-
-    def _global_batch_for(self, n):
-        """The global batch of the shape this replica's current step runs (set by forward via _global_batch)."""
-        return self._cur_gbatch if getattr(self, "_cur_gbatch", None) is not None else n * parallel.world_size()
 
     def apply_gradients(self):
         """DDP gradient all-reduce + tf.train.AdamOptimizer step over the flat buffer, then re-pack the filters."""
@@ -306,7 +289,6 @@ class VideoTrainer(TrainerBase):
               for t in (cmp, bg, warped)]
         xs = [t.to(self.device, torch.float32) for t in xs]
         n, h, w, _ = xs[0].shape
-        self._cur_gbatch = self._global_batch(n, h, w) if self.sync_bn else None
         b = m._buffers(n, h, w)
         tb = self._train_buffers(n, h, w)
         L = _levels(h, w)
