@@ -11,6 +11,12 @@ cpu_baseline may use it; the product never does).
                     every trainable variable — conv weights / biases and BN gamma / beta; the upconvs' drawn biases
                     feed nothing and get no gradient).  max_pool's gradient goes to each window's first maximum in
                     row-major order (TF MaxPoolGrad's strict '>' scan; parity unpinned, TF is absent)
+  image_step_grads  one iteration of train.py's training_procedure (train.py:37-109, entry train() at :112-135):
+                    unet.UNetImage.build(x = concat(cmp, bg)) (unet.py:86-148: 12 VGG convs, 4 SAME max-pools, 4
+                    upconv_concat = resize -> conv (no bias, no relu) -> [up, skip], conv1_5 + sigmoid) restated in
+                    torch float64, the same loss (train.py:41-47), autograd over EVERY variable (train.py:51-52:
+                    minimize() with the default var_list — the VGG filters and biases, UNetImage's halved conv1_1
+                    and the fresh convs; the upconvs' drawn biases feed nothing and get no gradient)
   adam_tf           tf.train.AdamOptimizer's ApplyAdam (train.py:302-304) in numpy float32, including TF's f32
                     beta-power variables and lr_t = lr*sqrt(1-beta2^t)/(1-beta1^t)
 
@@ -205,6 +211,70 @@ def small_step_grads(cmp, bg, gt, raw_fg, params, bn=None, device="cpu", sample_
     loss = _loss(la, lc, sample_weights)
     loss.backward()
     grads = {k: v.grad.cpu().numpy().copy() for k, v in V.items() if v.grad is not None}
+    terms = (float(loss.detach()), float(la.mean().detach()), float(lc.mean().detach()))
+    fwd = {k: v.detach().cpu().numpy() for k, v in r.items()}
+    fwd["output"] = alpha.detach().cpu().numpy()
+    return terms, fwd["output"], grads, fwd
+
+
+IMAGE_LAYERS = ("conv1_1", "conv1_2", "conv2_1", "conv2_2", "conv3_1", "conv3_2", "conv3_3", "conv4_1", "conv4_2",
+                "conv4_3", "conv5_1", "conv5_2", "upconv_1", "conv4_4", "upconv_2", "conv3_4", "upconv_3", "conv2_3",
+                "upconv_4", "conv1_5")
+
+
+def image_step_grads(cmp, bg, gt, raw_fg, params, device="cpu", sample_weights=None):
+    """-> (loss terms (loss, alpha_loss, cmp_loss), alpha, grads {(scope, kind): ndarray}, forward dict) for
+    train.py's training_procedure on x = concat(cmp, bg) (train.py:41: in_cmp, in_bg = split(x, [3, 3])).
+    params: {scope: (w_hwio, bias|None)} of UNetImage (models.unet_params(video=False)); kinds 'w' and 'b'.
+    The forward is models.unet_forward's op sequence (a test checks the two agree)."""
+    f64 = lambda a: np.asarray(a, np.float64)  # noqa: E731
+    T = lambda a: torch.from_numpy(f64(a)).to(device)  # noqa: E731
+    x = torch.cat([T(cmp), T(bg)], -1)
+    V = {}
+    for scope in IMAGE_LAYERS:
+        w, b = params[scope]
+        V[scope, "w"] = torch.tensor(f64(w), requires_grad=True, device=device)
+        if b is not None:
+            V[scope, "b"] = torch.tensor(f64(b), requires_grad=True, device=device)
+    cv = lambda t, s: _conv(t, V[s, "w"], V.get((s, "b")))  # noqa: E731
+
+    def upconv_concat(a, skip, s):  # unet.py:44-63
+        h, w = skip.shape[1:3]
+        return torch.cat([cv(_resize(a, h, w), s), skip], -1)
+
+    r = {}
+    r["conv1_1"] = torch.relu(cv(x, "conv1_1"))
+    r["conv1_2"] = torch.relu(cv(r["conv1_1"], "conv1_2"))
+    r["pool1"] = _pool(r["conv1_2"])
+    r["conv2_1"] = torch.relu(cv(r["pool1"], "conv2_1"))
+    r["conv2_2"] = torch.relu(cv(r["conv2_1"], "conv2_2"))
+    r["pool2"] = _pool(r["conv2_2"])
+    r["conv3_1"] = torch.relu(cv(r["pool2"], "conv3_1"))
+    r["conv3_2"] = torch.relu(cv(r["conv3_1"], "conv3_2"))
+    r["conv3_3"] = torch.relu(cv(r["conv3_2"], "conv3_3"))
+    r["pool3"] = _pool(r["conv3_3"])
+    r["conv4_1"] = torch.relu(cv(r["pool3"], "conv4_1"))
+    r["conv4_2"] = torch.relu(cv(r["conv4_1"], "conv4_2"))
+    r["conv4_3"] = torch.relu(cv(r["conv4_2"], "conv4_3"))
+    r["pool4"] = _pool(r["conv4_3"])
+    r["conv5_1"] = torch.relu(cv(r["pool4"], "conv5_1"))
+    r["conv5_2"] = torch.relu(cv(r["conv5_1"], "conv5_2"))
+    r["upconv1"] = upconv_concat(r["conv5_2"], r["conv4_3"], "upconv_1")
+    r["conv4_4"] = torch.relu(cv(r["upconv1"], "conv4_4"))
+    r["upconv2"] = upconv_concat(r["conv4_4"], r["conv3_3"], "upconv_2")
+    r["conv3_4"] = torch.relu(cv(r["upconv2"], "conv3_4"))
+    r["upconv3"] = upconv_concat(r["conv3_4"], r["conv2_2"], "upconv_3")
+    r["conv2_3"] = torch.relu(cv(r["upconv3"], "conv2_3"))
+    r["upconv4"] = upconv_concat(r["conv2_3"], r["conv1_2"], "upconv_4")
+    r["conv1_3"] = cv(r["upconv4"], "conv1_5")
+    alpha = torch.sigmoid(r["conv1_3"])
+    gt_t, fg_t, bg_t, cmp_t = (T(a) for a in (gt, raw_fg, bg, cmp))
+    eps2 = np.float64(np.float32(1e-6) ** 2)
+    la = torch.sqrt((alpha - gt_t) ** 2 + eps2)
+    lc = torch.sqrt((alpha * fg_t + (1 - alpha) * bg_t - cmp_t) ** 2 + eps2)
+    loss = _loss(la, lc, sample_weights)
+    loss.backward()
+    grads = {k: v.grad.cpu().numpy().copy() for k, v in V.items()}
     terms = (float(loss.detach()), float(la.mean().detach()), float(lc.mean().detach()))
     fwd = {k: v.detach().cpu().numpy() for k, v in r.items()}
     fwd["output"] = alpha.detach().cpu().numpy()

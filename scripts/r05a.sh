@@ -16,4 +16,6 @@ guard() {  # guard <limit> <logfile> cmd...
 PT="python -u -m pytest -v --timeout 300 --timeout-method thread -rf"
 guard 600 r5a_syncbn.log $PT tests/test_capi.py tests/test_gpu_small_train.py tests/test_gpu_train.py -m gpu -k "syncbn or raw_stream or ddp"
 guard 400 r5a_graph1080.log $PT tests/test_gpu_layers_1080p.py -m gpu -k "graph_replay or timed_kernels or head_logits"
+guard 600 r5a_wide.log $PT tests/test_gpu_train.py -m gpu -k "wgrad"
+guard 900 r5a_image.log $PT tests/test_gpu_image_train.py -m gpu
 guard 600 r5a_probe.log python -u tools/capture_probe.py

@@ -1,0 +1,208 @@
+"""train.py's UNetImage training step (training_procedure, /root/reference/train.py:37-109; entry train() at :112-135)
+on the GPU against oracle/train_ref.py::image_step_grads — torch-float64 autograd of unet.UNetImage (unet.py:86-148)
+on the same op sequence as oracle/models.unet_forward, whose forward the reference's own builders pin
+(tests/golden/unet_image_70x90.npz; test_train_host.py checks the two forwards agree).
+
+  fp32 step   loss terms within 1e-5 relative, every variable's gradient (20 filters, 16 biases — the VGG ones
+              included: train.py:51-52 trains every variable) within 2e-3 relative L2, at 2x64x64 and 2x37x45
+  bf16 step   at the bench's 8 x 320^2 batch: per-tensor relative L2 within 3x the float64 sensitivity to bf16-sized
+              filter noise + 1e-2, whole-gradient cosine >= 0.999
+  Adam        the updated flat variables against oracle/train_ref.adam_tf
+  graphs      forward + loss and backward replayed from HIP graphs leave bit-identical variables to eager steps
+  DDP         two gloo replicas drawing different weights start from rank 0's and stay identical; the all-reduced
+              gradient is the sum of the replicas' local gradients
+
+Gradients are parity unpinned against real TF 1.x (absent): autograd on the golden-pinned forward is the oracle.
+"""
+
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from conftest import gpu_available
+from oracle import models as om
+from oracle import train_ref as tr
+
+pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not gpu_available(), reason="needs a ROCm GPU")]
+
+DEV = "cuda"
+MEAN = np.array([103.939, 116.779, 123.68])
+
+
+def T(a, dtype=torch.float32):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(DEV, dtype)
+
+
+def H(t):
+    return t.detach().float().cpu().numpy().astype(np.float64)
+
+
+def _batch(n, h, w, seed=11):
+    """loader.get_batch-shaped inputs (train.py:79): cmp / bg minus VGG_MEAN, gt alpha, raw fg in 0..255."""
+    rs = np.random.RandomState(seed)
+    fg = rs.uniform(0, 255, (n, h, w, 3))
+    bg = rs.uniform(0, 255, (n, h, w, 3))
+    yy, xx = np.mgrid[:h, :w]
+    gt = np.clip(1.2 - np.hypot((yy - h / 2) / (h / 3), (xx - w / 2) / (w / 3)), 0, 1)[None, :, :, None]
+    gt = np.repeat(gt, n, 0)
+    cmp = gt * fg + (1 - gt) * bg - MEAN
+    f = lambda a: a.astype(np.float32)  # noqa: E731
+    return f(cmp), f(bg - MEAN), f(gt), f(fg)
+
+
+def _params(seed=3, scale=1.0):
+    return om.unet_params(om.synthetic_vgg16(0, scale=scale), np.random.RandomState(seed), video=False)
+
+
+def _trainer(params, dtype, **kw):
+    from vmatting.image_train import ImageTrainer
+    return ImageTrainer(om.synthetic_vgg16(0), dtype, DEV, params=params, **kw)
+
+
+def _grad_errors(trn, grads):
+    out = {}
+    for (scope, kind), g_ref in grads.items():
+        g = H(trn.G[scope, kind])
+        out[scope, kind] = np.linalg.norm(g - g_ref) / max(np.linalg.norm(g_ref), 1e-30)
+    return out
+
+
+@pytest.mark.parametrize("n,h,w", [(2, 64, 64), (2, 37, 45)])
+def test_image_step_fp32_matches_f64_autograd(n, h, w):
+    params = _params()
+    cmp, bg, gt, fg = _batch(n, h, w)
+    trn = _trainer(params, "fp32")
+    trn.forward(cmp, bg)
+    from vmatting import ops
+    loss = H(ops.matting_loss(trn.model.output, T(gt), T(fg), T(bg), T(cmp)))
+    trn.grad.zero_()
+    trn.backward(T(gt), T(fg), T(bg), T(cmp))
+    torch.cuda.synchronize()
+    terms, alpha, grads, _ = tr.image_step_grads(cmp, bg, gt, fg, params)
+    assert np.abs(H(trn.model.output) - alpha).max() <= 1e-4
+    for a, b in zip(loss, terms):
+        assert abs(a - b) <= 1e-5 * abs(b), (loss, terms)
+    assert len(grads) == 36 and set(grads) == set((s, k) for s, k, _, _ in trn.layout)
+    errs = _grad_errors(trn, grads)
+    bad = {k: v for k, v in errs.items() if not v <= 2e-3}
+    print("fp32 image step %dx%dx%d worst rel L2 %.3g" % (n, h, w, max(errs.values())))
+    assert not bad, bad
+
+
+def test_image_step_fp32_adam_update():
+    """One whole step: the flat variables after TF-Adam (lr 1e-5, train.py:49-52) against oracle adam_tf applied to
+    the step's own gradient (left in trn.grad), and that gradient against float64 autograd."""
+    params = _params()
+    cmp, bg, gt, fg = _batch(2, 40, 48, seed=5)
+    trn = _trainer(params, "fp32")
+    p0 = H(trn.flat).astype(np.float32)
+    trn.step(cmp, bg, gt, fg)
+    torch.cuda.synchronize()
+    g = H(trn.grad).astype(np.float32)
+    z = np.zeros_like(p0)
+    ref, _, _ = tr.adam_tf(p0, z, z.copy(), g, 1, lr=1e-5)
+    got = H(trn.flat)
+    assert np.abs(got - ref).max() <= 1e-6 * max(1.0, np.abs(ref).max()), np.abs(got - ref).max()
+    assert np.abs(got - p0).max() > 5e-6  # it moved (~lr per variable with a gradient)
+    _, _, grads, _ = tr.image_step_grads(cmp, bg, gt, fg, params)
+    errs = _grad_errors(trn, grads)
+    assert max(errs.values()) <= 2e-3, errs
+
+
+def test_image_step_bf16_bench_shape():
+    """The bf16 step at the bench's 8 x 320^2 batch (params.py BATCH_SIZE / INPUT_SIZE) against float64 autograd run
+    on the GPU (test infrastructure) on the same bf16-rounded filters, bound self-calibrated by the float64
+    sensitivity to bf16-sized (2^-9) filter noise."""
+    params = _params()
+    n, h, w = 8, 320, 320
+    cmp, bg, gt, fg = _batch(n, h, w, seed=17)
+    trn = _trainer(params, "bf16")
+    trn.forward(cmp, bg)
+    trn.grad.zero_()
+    trn.backward(T(gt), T(fg), T(bg), T(cmp))
+    torch.cuda.synchronize()
+    pb = {k: (np.asarray(torch.from_numpy(w_).bfloat16().float().numpy()), b_) for k, (w_, b_) in params.items()}
+    _, _, grads, _ = tr.image_step_grads(cmp, bg, gt, fg, pb, device=DEV)
+    rs = np.random.RandomState(7)
+    p2 = {k: (w_ * (1 + 2.0 ** -9 * rs.normal(size=w_.shape)).astype(np.float32), b_) for k, (w_, b_) in pb.items()}
+    _, _, g2, _ = tr.image_step_grads(cmp, bg, gt, fg, p2, device=DEV)
+    bad, got_all, ref_all, rows = [], [], [], []
+    for (scope, kind), g_ref in grads.items():
+        g = H(trn.G[scope, kind])
+        nrm = max(np.linalg.norm(g_ref), 1e-30)
+        l2 = np.linalg.norm(g - g_ref) / nrm
+        sens = np.linalg.norm(g2[scope, kind] - g_ref) / nrm
+        got_all.append(g.ravel())
+        ref_all.append(g_ref.ravel())
+        rows.append("%s/%s %.3e (sens %.3e)" % (scope, kind, l2, sens))
+        if not l2 <= 3 * sens + 1e-2:
+            bad.append((scope, kind, round(float(l2), 4), round(float(sens), 4)))
+    a, b_ = np.concatenate(got_all), np.concatenate(ref_all)
+    cos = float(a @ b_ / (np.linalg.norm(a) * np.linalg.norm(b_)))
+    print("bf16 image step 8x320^2: gradient cosine %.6f\n  %s" % (cos, "\n  ".join(rows)))
+    assert not bad, bad
+    assert cos >= 0.999
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_image_graph_step_equals_eager(dtype):
+    """ImageTrainer.capture: two steps replayed from the forward / backward HIP graphs (new batches copied in, Adam
+    eager in between) leave bit-identical variables and losses to two eager steps."""
+    params = _params()
+    b1, b2 = _batch(2, 48, 64, seed=3), _batch(2, 48, 64, seed=4)
+    eager = _trainer(params, dtype, lr=1e-3)
+    le = [H(eager.step(*b)) for b in (b1, b2)]
+    graphed = _trainer(params, dtype, lr=1e-3)
+    g = graphed.capture(*b1)
+    lg = [H(g.step(*b)) for b in (b1, b2)]
+    torch.cuda.synchronize()
+    assert all(np.array_equal(a, b) for a, b in zip(le, lg)), (le, lg)
+    assert torch.equal(eager.flat, graphed.flat)
+
+
+def _ddp_worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    try:
+        from vmatting import parallel
+        from vmatting.image_train import ImageTrainer
+        parallel.init_from_env(backend="gloo")
+        torch.cuda.set_device(0)
+        np.random.seed(50 + rank)  # different init_conv draws per rank: the broadcast must make them identical
+        trn = ImageTrainer(om.synthetic_vgg16(0), "bf16", "cuda:0")
+        cmp, bg, gt, fg = (x[rank:rank + 1] for x in _batch(2, 40, 56, seed=21))
+        p0 = trn.flat.cpu().numpy()
+        trn.forward(cmp, bg)
+        trn.grad.zero_()
+        trn.backward(T(gt), T(fg), T(bg), T(cmp))
+        torch.cuda.synchronize()
+        local = trn.grad.cpu().numpy().copy()
+        trn.apply_gradients()
+        torch.cuda.synchronize()
+        q.put((rank, p0, local, trn.flat.cpu().numpy(), trn.grad.cpu().numpy().copy(), None))
+    except Exception:
+        import traceback
+        q.put((rank, None, None, None, None, traceback.format_exc()[-2000:]))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def test_image_ddp_world2_replicas_identical():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29600 + (os.getpid() % 97)
+    procs = [ctx.Process(target=_ddp_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted((q.get(timeout=150) for _ in procs), key=lambda r: r[0])
+    for p in procs:
+        p.join(30)
+    assert all(r[5] is None for r in res), [r[5] for r in res]
+    np.testing.assert_array_equal(res[0][1], res[1][1])  # rank 0's variables everywhere
+    np.testing.assert_array_equal(res[0][3], res[1][3])  # identical after the all-reduced Adam step
+    assert not np.array_equal(res[0][2], res[1][2])      # different data -> different local gradients
+    np.testing.assert_allclose(res[0][4], res[0][2] + res[1][2], rtol=1e-6, atol=1e-12)

@@ -90,11 +90,44 @@ def test_conv_wgrad_accumulates_and_large_cin():
     assert scaled_err(H(dw) - 1.0, wr.grad.numpy()) <= 1e-4
 
 
-def test_conv_wgrad_rejects_wide_cout():
+@pytest.mark.parametrize("cin,cout,n,h,w,mode", [(6, 64, 2, 37, 45, "bf16"), (64, 64, 2, 33, 70, "bf16"),
+                                                  (200, 128, 1, 9, 40, "bf16"), (512, 512, 2, 20, 20, "bf16"),
+                                                  (1024, 64, 1, 7, 33, "bf16"), (128, 256, 3, 5, 3, "bf16"),
+                                                  (6, 64, 2, 37, 45, "f32"), (200, 128, 1, 9, 40, "f32"),
+                                                  (512, 96, 2, 11, 13, "f32")])
+def test_conv_wgrad_wide(cin, cout, n, h, w, mode):
+    """The wide weight gradients of UNetImage's convs (cout > 48; train.py:37-109): the bf16 MFMA kernel (x bf16, dy
+    bf16 or f32, both tried; cin not a multiple of 64 and odd frames) against float64 on the same bf16 operands
+    within the f32 summation bound, and the exact-f32 FMA kernel within 1e-5 of float64.  dw accumulates."""
     from vmatting import ops
-    x = torch.zeros((1, 4, 4, 8), device=DEV)
+    rs = np.random.RandomState(cin + cout + h)
+    x = rs.normal(size=(n, h, w, (cin + 7) // 8 * 8)).astype(np.float32)
+    dy = rs.normal(size=(n, h, w, cout)).astype(np.float32)
+    tdt = torch.bfloat16 if mode == "bf16" else torch.float32
+    xd = T(x, tdt)[..., :cin]
+    dys = [T(dy, tdt)] + ([T(dy)] if mode == "bf16" else [])
+    xr = torch.from_numpy(H(xd))
+    dr = torch.from_numpy(H(dys[0]))
+    wr = torch.zeros((3, 3, cin, cout), dtype=torch.float64, requires_grad=True)
+    (tr._conv(xr, wr) * dr).sum().backward()
+    wa = torch.zeros((3, 3, cin, cout), dtype=torch.float64, requires_grad=True)
+    (tr._conv(xr.abs(), wa) * dr.abs()).sum().backward()
+    bound = n * h * w * 2.0 ** -23 * wa.grad.numpy() + 1e-30
+    for d in dys:
+        dw = torch.ones((3, 3, cin, cout), dtype=torch.float32, device=DEV)
+        ops.conv_wgrad(xd, d, dw, mfma=mode == "bf16")
+        err = np.abs(H(dw) - 1.0 - wr.grad.numpy())
+        assert (err <= bound + 1e-6).all(), (float(err.max()), float((err / bound).max()))
+        if mode == "f32":
+            assert scaled_err(H(dw) - 1.0, wr.grad.numpy()) <= 1e-5
+
+
+def test_conv_wgrad_wide_rejects_split_sources():
+    from vmatting import ops
+    x = torch.zeros((2, 4, 4, 16), dtype=torch.bfloat16, device=DEV)
     with pytest.raises(NotImplementedError):
-        ops.conv_wgrad(x, torch.zeros((1, 4, 4, 64), device=DEV), torch.zeros((3, 3, 8, 64), device=DEV))
+        ops.conv_wgrad(x[:1], torch.zeros((1, 4, 4, 64), device=DEV), torch.zeros((3, 3, 32, 64), device=DEV),
+                       mfma=True, sources=(2, 4 * 4 * 16))
 
 
 @pytest.mark.parametrize("cin,cout", [(1, 32), (24, 48), (32, 24), (48, 96)])

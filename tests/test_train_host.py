@@ -154,3 +154,22 @@ def test_small_restatement_gradient_finite_difference():
         fd = (vals[0] - vals[1]) / (2 * h)
         g = grads[scope, "w"][idx]
         assert abs(fd - g) <= 1e-5 * max(1e-6, abs(g)) + 1e-9, (scope, fd, g)
+
+
+def test_image_step_oracle_forward_matches_numpy_oracle():
+    """oracle/train_ref.image_step_grads (the UNetImage training step's autograd oracle, train.py:37-109) runs the
+    same forward as oracle/models.unet_forward, which the reference's builders pin (unet_image_70x90 golden), and
+    yields a gradient for every variable train.py:51-52 trains: 20 filters + 16 biases (no upconv biases)."""
+    vgg = om.synthetic_vgg16(0)
+    p = om.unet_params(vgg, np.random.RandomState(3), video=False)
+    rs = np.random.RandomState(1)
+    n, h, w = 1, 21, 27
+    cmp, bg = rs.uniform(-100, 100, (n, h, w, 3)), rs.uniform(-100, 100, (n, h, w, 3))
+    gt, fg = rs.uniform(0, 1, (n, h, w, 1)), rs.uniform(0, 255, (n, h, w, 3))
+    terms, alpha, grads, fwd = tr.image_step_grads(cmp, bg, gt, fg, p)
+    r = om.unet_forward(np.concatenate([cmp, bg], -1), p)
+    for k in ("conv1_2", "pool2", "conv4_3", "conv5_2", "upconv1", "upconv4", "conv1_3", "output"):
+        assert np.abs(r[k] - fwd[k]).max() <= 1e-12 * max(1.0, np.abs(r[k]).max()), k
+    assert len(grads) == 36
+    assert not any(s.startswith("upconv") for s, k in grads if k == "b")
+    assert all(np.isfinite(g).all() for g in grads.values())

@@ -1099,6 +1099,264 @@ constexpr int wgrad_taps_lds() {
   return MAIN > RED ? MAIN : RED;
 }
 
+// ---------------------------------------------------------------- wide conv weight gradient (UNetImage training)
+// train.py's training_procedure (train.py:37-109) back-propagates through every conv of unet.UNetImage
+// (unet.py:86-148): cin 6 ... 1024, cout 64 ... 512.  dW_t[ci][co] = sum_p X[p + off_t][ci] * DY[p][co] as 9 GEMMs
+// with K = the pixels, v_mfma_f32_16x16x32_bf16 (A = X^T: 16 input channels x 32 pixels, B = DY: 32 pixels x 16
+// output channels, f32 accumulation), both operands read k-major from their natural NHWC LDS images with
+// ds_read_b64_tr_b16 (wm_frag), like wgrad_mfma_kernel.  The narrow kernel above runs every output channel in one
+// block and splits its K-steps over the waves (cout <= 48); here a block owns a 64 x 64 (ci x co) tile of all 9
+// taps and the 4 waves split the OUTPUT: wave (wi, wj) holds ci 32wi..+31 x co 32wj..+31 x 9 taps (144 f32
+// accumulators) and walks every pixel row of the tile, so no cross-wave reduction is needed.  Per 32-pixel row a
+// wave reads 2 DY fragments (reused by 9 taps x 2 ci pieces) and 18 X fragments (each reused by 2 co pieces):
+// 20 fragment reads per 36 MFMAs.
+// Grid: gx K-split blocks (contiguous tile ranges, one partial filter gradient each, summed in fixed order by
+// wgrad_reduce_kernel: deterministic) x the 64-channel blocks of cin and cout, as ONE dimension whose order is
+// XCD-aware: the blocks that share a pixel range (every channel block of it) are dispatched to the same XCD, so
+// its X patch and DY tile are fetched from HBM once per XCD and re-read from that XCD's L2.
+// DY is bf16 (the bf16 gradient copy the relu / BN backward writes for the data-gradient conv) or f32 (rounded
+// to bf16 when staged); X is the bf16 conv input, channels past cin (UNetImage's 6-channel conv1_1) read as 0.
+struct WwArgs {
+  const uint16_t* x;  // bf16 input view base (pixel 0, coff applied)
+  int n, h, w, cin, xcs;
+  const void* dy;     // bf16 / f32 output-gradient view base (coff applied)
+  int cout, dcs;
+  float* part;        // [gx][9][cin][cout]
+  int tiles_h, tiles_w;
+  long ntiles;
+  int gx, ncin, ncout;
+};
+
+constexpr int WW_TH = 4;
+constexpr int WW_TARGET_BLOCKS = 512;  // ~2 resident blocks per CU: one round; the partials stay <= 75 MB
+
+template <int TH, bool DYF32>
+__global__ __launch_bounds__(256, 2) void wgrad_wide_kernel(WwArgs a) {
+  constexpr int XPIX = wm_ppix<TH>(), DPIX = TH * WM_TW;
+  constexpr int XBYTES = wm_prows<TH>() * 128;
+  constexpr int NXC = XPIX * 8, NDC = DPIX * 8;                 // 16-byte chunks (8 channels) of each image
+  constexpr int XPT = (NXC + 255) / 256, DPT = (NDC + 255) / 256;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* ximg = smem;
+  char* dimg = smem + XBYTES;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wi = wave & 1, wj = wave >> 1;
+  const int nb = gridDim.x, lin = blockIdx.x;
+  // consecutive work ids on one XCD (workgroups are dealt to the 8 XCDs round-robin)
+  const int wid = (nb % 8 == 0) ? (lin % 8) * (nb / 8) + lin / 8 : lin;
+  const int nch = a.ncin * a.ncout;
+  const int kx = wid / nch, cb = wid - kx * nch;
+  const int c0 = (cb % a.ncin) * 64, o0 = (cb / a.ncin) * 64;
+
+  f32x4 acc[9][2][2];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int o = 0; o < 2; ++o) acc[t][i][o] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  uint4 xb[XPT];
+  uint4 db[DPT];
+  float4 df[DYF32 ? DPT : 1][2];
+  auto issue = [&](int tile) {
+    const int tx = tile % a.tiles_w;
+    const int t2 = tile / a.tiles_w;
+    const int y0 = (t2 % a.tiles_h) * TH, n = t2 / a.tiles_h, x0 = tx * WM_TW;
+#pragma unroll
+    for (int k = 0; k < XPT; ++k) {
+      const int e = tid + k * 256;
+      xb[k] = make_uint4(0, 0, 0, 0);
+      if (NXC % 256 == 0 || e < NXC) {
+        const int pe = e >> 3, j = e & 7;
+        const int gy = y0 - 1 + pe / WM_PW, gx = x0 - 1 + pe % WM_PW;
+        const int c = c0 + j * 8;
+        if ((unsigned)gy < (unsigned)a.h && (unsigned)gx < (unsigned)a.w && c < a.cin)
+          xb[k] = *reinterpret_cast<const uint4*>(a.x + (((long)n * a.h + gy) * a.w + gx) * a.xcs + c);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < DPT; ++k) {
+      const int e = tid + k * 256;
+      const int pe = e >> 3, j = e & 7;
+      const int gy = y0 + pe / WM_TW, gx = x0 + pe % WM_TW;
+      const bool in = (NDC % 256 == 0 || e < NDC) && (unsigned)gy < (unsigned)a.h && (unsigned)gx < (unsigned)a.w;
+      const long off = (((long)n * a.h + gy) * a.w + gx) * a.dcs + o0 + j * 8;
+      if constexpr (DYF32) {
+        df[k][0] = df[k][1] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (in) {
+          const float* src = reinterpret_cast<const float*>(a.dy) + off;
+          df[k][0] = *reinterpret_cast<const float4*>(src);
+          df[k][1] = *reinterpret_cast<const float4*>(src + 4);
+        }
+      } else {
+        db[k] = make_uint4(0, 0, 0, 0);
+        if (in) db[k] = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(a.dy) + off);
+      }
+    }
+  };
+  auto commit = [&]() {
+#pragma unroll
+    for (int k = 0; k < XPT; ++k) {
+      const int e = tid + k * 256;
+      if (NXC % 256 == 0 || e < NXC) {
+        const int pe = e >> 3, j = e & 7;
+        uint4 v = xb[k];
+        const int c = c0 + j * 8;
+        if (c + 8 > a.cin) {  // a chunk straddling cin: zero the channels past it
+          uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            if (c + 2 * i >= a.cin) w4[i] = 0u;
+            else if (c + 2 * i + 1 >= a.cin) w4[i] &= 0xffffu;
+          }
+          v = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+        }
+        *reinterpret_cast<uint4*>(ximg + wm_off<128>(pe, j >> 1) + (j & 1) * 16) = v;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < DPT; ++k) {
+      const int e = tid + k * 256;
+      if (NDC % 256 == 0 || e < NDC) {
+        const int pe = e >> 3, j = e & 7;
+        uint4 v;
+        if constexpr (DYF32) {
+          const float f[8] = {df[k][0].x, df[k][0].y, df[k][0].z, df[k][0].w,
+                              df[k][1].x, df[k][1].y, df[k][1].z, df[k][1].w};
+          v = Chunk<uint16_t>::pack(f);
+        } else {
+          v = db[k];
+        }
+        *reinterpret_cast<uint4*>(dimg + wm_off<128>(pe, j >> 1) + (j & 1) * 16) = v;
+      }
+    }
+  };
+
+  const int g = lane >> 4;
+  const int t_beg = (int)((long)kx * a.ntiles / a.gx);
+  const int t_end = (int)((long)(kx + 1) * a.ntiles / a.gx);
+  if (t_beg < t_end) issue(t_beg);
+  for (int tile = t_beg; tile < t_end; ++tile) {
+    commit();
+    __syncthreads();
+    if (tile + 1 < t_end) issue(tile + 1);
+#pragma unroll 1
+    for (int row = 0; row < TH; ++row) {
+      bf16x8 bd[2];
+#pragma unroll
+      for (int o = 0; o < 2; ++o) bd[o] = wm_frag<128>(dimg, row * WM_TW + 8 * g, 2 * wj + o, lane);
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int r0 = (row + t / 3) * WM_PW + t % 3 + 8 * g;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const bf16x8 ax = wm_frag<128>(ximg, r0, 2 * wi + i, lane);
+#pragma unroll
+          for (int o = 0; o < 2; ++o)
+            acc[t][i][o] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ax, bd[o], acc[t][i][o], 0, 0, 0);
+        }
+      }
+    }
+    __syncthreads();
+  }
+
+  // this block's partial of its 64 x 64 x 9 tile (lanes: co = lane & 15, ci = 4 * (lane >> 4) + j)
+  float* part = a.part + (long)kx * 9 * a.cin * a.cout;
+  const int co_l = lane & 15, ci_l = 4 * g;
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int o = 0; o < 2; ++o) {
+        const int co = o0 + 32 * wj + 16 * o + co_l;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int ci = c0 + 32 * wi + 16 * i + ci_l + j;
+          if (ci < a.cin) part[((long)t * a.cin + ci) * a.cout + co] = acc[t][i][o][j];
+        }
+      }
+}
+
+template <int TH>
+constexpr int wgrad_wide_lds() { return wm_prows<TH>() * 128 + TH * WM_TW * 128; }
+
+// The exact-f32 wide weight gradient of the fp32 (parity) training path: a plain FMA GEMM per tap.  Block = 256
+// threads on one (tap, 32 input channels, 64 output channels) tile; per 32-pixel K chunk the shifted X rows and
+// the DY rows are staged in LDS, each thread accumulates 2 ci x 4 co in f32 over its block's contiguous pixel
+// range (fixed order), and wgrad_reduce_kernel sums the gx partials in fixed order: deterministic.
+struct WfArgs {
+  const float* x;
+  int n, h, w, cin, xcs;
+  const float* dy;
+  int cout, dcs;
+  float* part;  // [gx][9][cin][cout]
+  long npix;
+  int gx, ncin, ncout;
+};
+
+__global__ __launch_bounds__(256) void wgrad_wide_f32_kernel(WfArgs a) {
+  __shared__ float xs[32][33];
+  __shared__ float ds[32][65];
+  const int tid = threadIdx.x;
+  int b = blockIdx.y;
+  const int t = b % 9;
+  b /= 9;
+  const int c0 = (b % a.ncin) * 32, o0 = (b / a.ncin) * 64;
+  const int kh = t / 3 - 1, kw = t % 3 - 1;
+  const int kx = blockIdx.x;
+  const long p_beg = kx * a.npix / a.gx, p_end = (kx + 1) * a.npix / a.gx;
+  const int tc = tid / 16, to = tid % 16;  // thread: ci 2tc, 2tc+1; co 4to .. 4to+3
+  float acc[2][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+  for (long p0 = p_beg; p0 < p_end; p0 += 32) {
+    // stage X[p + off_t][c0 .. c0+31] and DY[p][o0 .. o0+63] for 32 pixels
+    for (int e = tid; e < 32 * 32; e += 256) {
+      const int pk = e / 32, c = e % 32;
+      const long p = p0 + pk;
+      float v = 0.f;
+      if (p < p_end && c0 + c < a.cin) {
+        const int xx = (int)(p % a.w);
+        const long r = p / a.w;
+        const int yy = (int)(r % a.h), nn = (int)(r / a.h);
+        const int gy = yy + kh, gx = xx + kw;
+        if ((unsigned)gy < (unsigned)a.h && (unsigned)gx < (unsigned)a.w)
+          v = a.x[(((long)nn * a.h + gy) * a.w + gx) * a.xcs + c0 + c];
+      }
+      xs[pk][c] = v;
+    }
+    for (int e = tid; e < 32 * 64; e += 256) {
+      const int pk = e / 64, c = e % 64;
+      const long p = p0 + pk;
+      ds[pk][c] = (p < p_end && o0 + c < a.cout) ? a.dy[p * a.dcs + o0 + c] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll 8
+    for (int k = 0; k < 32; ++k) {
+      const float x0 = xs[k][2 * tc], x1 = xs[k][2 * tc + 1];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float d = ds[k][4 * to + j];
+        acc[0][j] = fmaf(x0, d, acc[0][j]);
+        acc[1][j] = fmaf(x1, d, acc[1][j]);
+      }
+    }
+    __syncthreads();
+  }
+  float* part = a.part + (long)kx * 9 * a.cin * a.cout;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int ci = c0 + 2 * tc + i;
+    if (ci >= a.cin) continue;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int co = o0 + 4 * to + j;
+      if (co < a.cout) part[((long)t * a.cin + ci) * a.cout + co] = acc[i][j];
+    }
+  }
+}
+
 // HWIO [3][3][cin][cout] -> the dgrad filter [3][3][cout][cin], spatially flipped
 __global__ void flip_weights_kernel(const float* w, int cin, int cout, float* wt) {
   const long total = 9L * cin * cout;
@@ -1338,6 +1596,90 @@ static int launch_wgrad_mfma(WgArgs& a, float* dw, hipStream_t st) {
   return th8 ? launch_wgrad_mfma_t<1, 3, true, 8>(a, dw, st) : launch_wgrad_mfma_t<1, 3, true, 4>(a, dw, st);
 }
 
+// K-split of the wide weight gradients: WW_TARGET_BLOCKS blocks in all (one resident round), at most one per pixel
+// tile (bf16) / 32-pixel chunk (f32), and partials of at most WW_WS_CAP bytes
+constexpr size_t WW_WS_CAP = 128ull << 20;
+
+static long wgrad_wide_gx(int n, int h, int w, int cin, int cout, bool f32) {
+  long units, nch;
+  if (f32) {
+    units = ((long)n * h * w + 31) / 32;
+    nch = 9L * ((cin + 31) / 32) * ((cout + 63) / 64);
+  } else {
+    units = (long)n * ((h + WW_TH - 1) / WW_TH) * ((w + WM_TW - 1) / WM_TW);
+    nch = (long)((cin + 63) / 64) * (cout / 64);
+  }
+  long gx = (WW_TARGET_BLOCKS + nch - 1) / nch;
+  const long cap = (long)(WW_WS_CAP / (9ull * cin * cout * sizeof(float)));
+  if (gx > cap) gx = cap;
+  if (gx > units) gx = units;
+  return gx < 1 ? 1 : gx;
+}
+
+static int launch_wgrad_wide(const vm_tensor* x, const vm_tensor* dy, float* dw, void* work, hipStream_t st) {
+  WwArgs a{};
+  a.x = reinterpret_cast<const uint16_t*>(x->ptr) + x->coff;
+  a.n = x->n; a.h = x->h; a.w = x->w; a.cin = x->c; a.xcs = x->cstride;
+  const bool f32 = dy->dtype == VM_F32;
+  a.dy = f32 ? static_cast<const void*>(reinterpret_cast<const float*>(dy->ptr) + dy->coff)
+             : static_cast<const void*>(reinterpret_cast<const uint16_t*>(dy->ptr) + dy->coff);
+  a.cout = dy->c; a.dcs = dy->cstride;
+  a.part = reinterpret_cast<float*>(work);
+  a.tiles_h = (a.h + WW_TH - 1) / WW_TH;
+  a.tiles_w = (a.w + WM_TW - 1) / WM_TW;
+  a.ntiles = (long)a.n * a.tiles_h * a.tiles_w;
+  if (a.ntiles > 0x7fffffffL) return fail(VM_EUNSUPPORTED, "conv_wgrad: too many pixel tiles");
+  a.ncin = (a.cin + 63) / 64;
+  a.ncout = a.cout / 64;
+  a.gx = (int)wgrad_wide_gx(a.n, a.h, a.w, a.cin, a.cout, false);
+  const long nb = (long)a.gx * a.ncin * a.ncout;
+  if (nb > 0x7fffffffL) return fail(VM_EUNSUPPORTED, "conv_wgrad: grid too large");
+  constexpr int lds = wgrad_wide_lds<WW_TH>();
+  if (f32) {
+    static int attr = -1;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (attr != dev) {
+      hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_wide_kernel<WW_TH, true>),
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+      if (e != hipSuccess) return fail(VM_EHIP, "wgrad_wide setup: %s", hipGetErrorString(e));
+      attr = dev;
+    }
+    hipLaunchKernelGGL((wgrad_wide_kernel<WW_TH, true>), dim3((unsigned)nb), dim3(256), lds, st, a);
+  } else {
+    static int attr = -1;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (attr != dev) {
+      hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_wide_kernel<WW_TH, false>),
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+      if (e != hipSuccess) return fail(VM_EHIP, "wgrad_wide setup: %s", hipGetErrorString(e));
+      attr = dev;
+    }
+    hipLaunchKernelGGL((wgrad_wide_kernel<WW_TH, false>), dim3((unsigned)nb), dim3(256), lds, st, a);
+  }
+  launch_wgrad_reduce(a.part, a.gx, 9L * a.cin * a.cout, dw, st);
+  return VM_OK;
+}
+
+static int launch_wgrad_wide_f32(const vm_tensor* x, const vm_tensor* dy, float* dw, void* work, hipStream_t st) {
+  WfArgs a{};
+  a.x = reinterpret_cast<const float*>(x->ptr) + x->coff;
+  a.n = x->n; a.h = x->h; a.w = x->w; a.cin = x->c; a.xcs = x->cstride;
+  a.dy = reinterpret_cast<const float*>(dy->ptr) + dy->coff;
+  a.cout = dy->c; a.dcs = dy->cstride;
+  a.part = reinterpret_cast<float*>(work);
+  a.npix = (long)a.n * a.h * a.w;
+  a.ncin = (a.cin + 31) / 32;
+  a.ncout = (a.cout + 63) / 64;
+  a.gx = (int)wgrad_wide_gx(a.n, a.h, a.w, a.cin, a.cout, true);
+  const long ny = 9L * a.ncin * a.ncout;
+  if (ny > 65535) return fail(VM_EUNSUPPORTED, "conv_wgrad: too many channel blocks");
+  hipLaunchKernelGGL(wgrad_wide_f32_kernel, dim3((unsigned)a.gx, (unsigned)ny), dim3(256), 0, st, a);
+  launch_wgrad_reduce(a.part, a.gx, 9L * a.cin * a.cout, dw, st);
+  return VM_OK;
+}
+
 static bool ok_view(const vm_tensor* t) { return valid_tensor(t); }
 
 static bool same_shape(const vm_tensor* a, const vm_tensor* b) {
@@ -1547,7 +1889,9 @@ extern "C" int vm_conv3x3_wgrad_nhwc(const vm_tensor* x, const vm_tensor* dy, fl
 }
 
 extern "C" size_t vm_conv3x3_wgrad_ex_workspace_bytes(int n, int h, int w, int cin, int cout, int mode) {
-  if (n <= 0 || h <= 0 || w <= 0 || cin <= 0 || cout <= 0 || cout > 48) return 0;
+  if (n <= 0 || h <= 0 || w <= 0 || cin <= 0 || cout <= 0) return 0;
+  if (cout > 48)  // the wide kernels (UNetImage training)
+    return (size_t)wgrad_wide_gx(n, h, w, cin, cout, mode != 1) * 9 * cin * cout * sizeof(float);
   if (mode != 1) return (size_t)wgrad_rows(n, h, w, cin, cout, wgrad_cc(cout)) * 9 * cin * cout * sizeof(float);
   const WmCfg c = wgrad_mfma_cfg(cin, cout);
   return (size_t)wgrad_rows(n, h, w, cin, cout, c.nci * 16) * 9 * cin * cout * sizeof(float);
@@ -1557,11 +1901,28 @@ extern "C" int vm_conv3x3_wgrad_ex_nhwc(const vm_tensor* x, int x_src_c, long x_
                                         float* dw, void* work, int mode, void* stream) {
   vm_tensor xs = x ? *x : vm_tensor{};
   if (x_src_c > 0) xs.c = x_src_c;  // the view of source 0 must be valid; the others follow at x_src_stride
-  if (!x || !ok_view(&xs) || !ok_view(dy) || !dw || !work || dy->dtype != VM_F32 || dy->n != x->n || dy->h != x->h ||
+  if (!x || !ok_view(&xs) || !ok_view(dy) || !dw || !work || (dy->dtype != VM_F32 && !(dy->dtype == VM_BF16 && dy->c > 48)) || dy->n != x->n || dy->h != x->h ||
       dy->w != x->w || x_src_c < 0 || (x_src_c > 0 && (x_src_stride <= 0 || x->c % x_src_c)) ||
       (mode != 0 && mode != 1))
     return fail(VM_EINVAL, "conv3x3_wgrad_ex: bad argument");
-  if (dy->c > 48) return fail(VM_EUNSUPPORTED, "conv3x3_wgrad_ex: cout %d > 48", dy->c);
+  if (dy->c > 48) {  // the wide weight gradients of UNetImage's convs (train.py:37-109)
+    if (x_src_c > 0) return fail(VM_EUNSUPPORTED, "conv3x3_wgrad_ex: split sources need cout <= 48");
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    if (mode == 0) {
+      if (x->dtype != VM_F32 || dy->dtype != VM_F32)
+        return fail(VM_EUNSUPPORTED, "conv3x3_wgrad_ex: the exact mode with cout > 48 needs f32 x and dy");
+      int rc = launch_wgrad_wide_f32(x, dy, dw, work, st);
+      return rc ? rc : check_launch("conv3x3_wgrad_ex");
+    }
+    const int dch = dy->dtype == VM_F32 ? 4 : 8;  // elements per 16 bytes
+    if (x->dtype != VM_BF16 || reinterpret_cast<uintptr_t>(x->ptr) % 16 || x->coff % 8 || x->cstride % 8 ||
+        x->coff + (x->c + 7) / 8 * 8 > x->cstride || dy->c % 64 || (dy->dtype != VM_F32 && dy->dtype != VM_BF16) ||
+        reinterpret_cast<uintptr_t>(dy->ptr) % 16 || dy->coff % dch || dy->cstride % dch)
+      return fail(VM_EUNSUPPORTED, "conv3x3_wgrad_ex: the wide MFMA mode needs a bf16 x of 16-byte channel chunks "
+                                   "and a 16-byte aligned dy of a multiple of 64 channels");
+    int rc = launch_wgrad_wide(x, dy, dw, work, st);
+    return rc ? rc : check_launch("conv3x3_wgrad_ex");
+  }
   if (mode == 0) {  // exact f32 FMA kernel, optionally over split sources
     V xv = mk(x), dv = mk(dy);
     xv.sc = x_src_c;
