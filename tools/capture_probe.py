@@ -92,6 +92,40 @@ def case_fork_prio_nested():
     return _expect(x, outs, 3) and torch.equal(outs[3], outs[0] + 1)
 
 
+def _nested(mid, inner):
+    x, outs = _bufs()
+
+    def fn():
+        cur = torch.cuda.current_stream()
+        mid.wait_stream(cur)
+        with torch.cuda.stream(mid):
+            _work(x, outs, inner)
+            torch.add(outs[0], 1, out=outs[3])
+        cur.wait_stream(mid)
+    g = _capture(fn)
+    for o in outs:
+        o.zero_()
+    g.replay()
+    torch.cuda.synchronize()
+    return _expect(x, outs, len(inner)) and torch.equal(outs[3], outs[0] + 1)
+
+
+def case_nested_default():
+    """capture stream -> default-priority stream -> 3 default-priority side streams -> joined back: the nested fork
+    alone, no stream priority."""
+    return _nested(torch.cuda.Stream(), [torch.cuda.Stream() for _ in range(3)])
+
+
+def case_nested_default_single():
+    """capture stream -> default-priority stream -> ONE default-priority stream -> joined back."""
+    return _nested(torch.cuda.Stream(), [torch.cuda.Stream()])
+
+
+def case_prio_nested_single():
+    """capture stream -> high-priority stream -> ONE default-priority stream -> joined back."""
+    return _nested(torch.cuda.Stream(priority=torch.cuda.Stream.priority_range()[1]), [torch.cuda.Stream()])
+
+
 def case_capture_on_prio_stream():
     """the capture itself begun while a high-priority stream is current (caller-level priority)."""
     x, outs = _bufs()
@@ -175,11 +209,14 @@ CASES = ["fork_default", "fork_prio", "fork_prio_nested", "capture_on_prio_strea
 
 
 def main():
-    if len(sys.argv) > 1:
+    cases = CASES
+    if len(sys.argv) > 2 and sys.argv[1] == "--cases":
+        cases = sys.argv[2].split(",")
+    elif len(sys.argv) > 1:
         ok = globals()["case_" + sys.argv[1]]()
         print("%s %s" % (sys.argv[1], "ok" if ok else "MISMATCH"), flush=True)
         return 0 if ok else 1
-    for c in CASES:
+    for c in cases:
         try:
             r = subprocess.run([sys.executable, os.path.abspath(__file__), c], timeout=240)
             rc = r.returncode

@@ -845,7 +845,8 @@ def resize_backward(dy, dx):
 
 
 def conv_wgrad(x, dy, dw, mfma=False, sources=None):
-    """dw[3,3,cin,cout] += 3x3 SAME conv weight gradient of input view x and f32 output-gradient view dy.
+    """dw[3,3,cin,cout] += 3x3 SAME conv weight gradient of input view x and output-gradient view dy (f32; bf16 too
+    for the wide MFMA kernel, cout > 48).
 
     ``mfma``: bf16 x only — the MFMA kernel with dy rounded to bf16 (the bf16 training path); else the exact-f32
     FMA kernel.  ``sources`` = (number of sources, element stride between sources): x is the [n,h,w,c] view of
@@ -861,7 +862,7 @@ def conv_wgrad(x, dy, dw, mfma=False, sources=None):
     if tuple(dy.shape[:3]) != (n, h, w) or dw.numel() != 9 * cin * cout:
         raise ValueError("conv_wgrad: x %s, dy %s, dw %s" % (tuple(x.shape), tuple(dy.shape), tuple(dw.shape)))
     dv = nhwc(dy)
-    if mfma or sources is not None:
+    if mfma or sources is not None or cout > 48:  # (cout > 48: the wide kernels, UNetImage training)
         xv = nhwc(x)
         xv.c = cin
         src_c, stride = (src_c, int(sources[1])) if sources is not None else (0, 0)
