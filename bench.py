@@ -436,14 +436,12 @@ def augment_bench(dev, steps, threads, cpu=True, h=1080, w=1920):
            "achieved_gbps": round(algo / (dev_ms * 1e-3) / 1e9, 1), "peak_gbps": PEAK_HBM_GBPS}
     if cpu:
         from oracle import augment as oa  # the CPU-baseline leg only
-        sh, sw = h // 2, w // 2
-        args = (fg_h[:sh, :sw].copy(), bg_h[:sh, :sw].copy(), alpha_h[::2, ::2].copy())
         np.random.seed(0)
-        rate = _pool_rate(lambda _: oa.augment(*args), list(range(threads)), threads) * (sh * sw) / float(h * w)
+        rate = _pool_rate(lambda _: oa.augment(fg_h, bg_h, alpha_h), list(range(threads)), threads)
         rec["cpu_baseline"] = {"value": round(rate, 3), "unit": "samples/s", "cores": threads, "kind": "port",
                                "sample": "oracle/augment.py (numpy, scipy-order TPS + OpenCV restatement): %d "
-                                         "%dx%d samples on a pool of %d host threads, scaled x%d to %dx%d by pixel "
-                                         "count" % (threads, sw, sh, threads, (h * w) // (sh * sw), w, h)}
+                                         "%dx%d samples (the config's size, not scaled) on a pool of %d host threads"
+                                         % (threads, w, h, threads)}
     return rec
 
 
@@ -540,17 +538,15 @@ def train_bench(dev, steps, warmup, world, rank, threads, cpu=True, n=8, size=32
     if cpu and world == 1:
         from oracle import models as om  # the CPU-baseline leg only
         from oracle import train_ref as tr
-        sh = 128
         p = om.unet_simple_params(np.random.RandomState(1))
-        sl = lambda a: np.asarray(a[:1, :sh, :sh], np.float64)  # noqa: E731
+        sl = lambda a: np.asarray(a[:1], np.float64)  # noqa: E731
         t0 = time.perf_counter()
         tr.train_step_grads(sl(cmp), sl(bg - mean), sl(warped), sl(gt), sl(fg), synthetic_vgg16(0), p)
-        dt = (time.perf_counter() - t0) * (size * size) / float(sh * sh)
+        dt = time.perf_counter() - t0
         rec["cpu_baseline"] = {"value": round(1.0 / dt, 4), "unit": "samples/s", "cores": threads,
                                "kind": "port",
                                "sample": "oracle/train_ref.py (numpy-f64 VGG towers + torch-f64 autograd head) on one "
-                                         "%dx%d sample, scaled x%.2f to %dx%d by pixel count" %
-                                         (sh, sh, (size * size) / float(sh * sh), size, size)}
+                                         "%dx%d sample (the config's sample size, timed, not scaled)" % (size, size)}
     return rec
 
 
@@ -661,6 +657,96 @@ def train_small_bench(dev, steps, warmup, world, rank, threads, cpu=True, n=8, s
         rec["cpu_baseline"] = {"value": round(2.0 / best, 3), "unit": "samples/s", "cores": threads, "kind": "port",
                                "sample": "oracle/train_ref.py small_step_grads (torch-f64 autograd of UNetSmall) on 2 "
                                          "of the %dx%d samples, best of 2" % (size, size)}
+    return rec
+
+
+def train_image_bench(dev, steps, warmup, world, rank, threads, cpu=True, n=8, size=320, dtype="bf16", graph=True):
+    """train.py's training_procedure step (train.py:37-109 with train()'s graph, :112-135):
+    unet.UNetImage(x = [cmp, bg]) forward (the 20 convs, pools, TF-1 resizes, concats), the loss, backward through
+    EVERY variable (VGG filters and biases included: wide MFMA filter gradients, data gradients on the forward conv
+    kernels over flipped filters, pool / resize adjoints), DDP all-reduce, TF-Adam at lr 1e-5, re-pack — batch 8 x
+    320^2 per GPU (params.py BATCH_SIZE / INPUT_SIZE) resident in HBM.  Forward + loss and backward replayed from
+    HIP graphs; roofline: the step's algorithmic conv FLOPs over its device time at the bf16 dense MFMA peak."""
+    from vmatting.image_train import ImageTrainer
+    from vmatting.weights import synthetic_vgg16 as svgg
+    rs = np.random.RandomState(300 + rank)
+    mean = np.array(VGG_MEAN)
+    fg = rs.uniform(0, 255, (n, size, size, 3))
+    bg = rs.uniform(0, 255, (n, size, size, 3))
+    yy, xx = np.mgrid[:size, :size]
+    gt = np.clip(1.2 - np.hypot((yy - size / 2) / (size / 3), (xx - size / 2) / (size / 4)), 0, 1)
+    gt = np.repeat(gt[None, :, :, None], n, 0)
+    cmp = gt * fg + (1 - gt) * bg - mean
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.float32)).to(dev)  # noqa: E731
+    cmp_d, bg_d, gt_d, fg_d = T(cmp), T(bg - mean), T(gt), T(fg)
+    np.random.seed(4)
+    trn = ImageTrainer(svgg(0), dtype, dev)
+    g = trn.capture(cmp_d, bg_d, gt_d, fg_d) if graph else None
+    for _ in range(warmup):
+        if g is not None:
+            g.step()
+        else:
+            trn.step(cmp_d, bg_d, gt_d, fg_d)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    ev = Events()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        ev.mark()
+        if g is not None:
+            g.g_fwd.replay()
+        else:
+            trn.forward(cmp_d, bg_d)
+            trn._g["loss"].copy_(ops.matting_loss(trn.model.output, gt_d, fg_d, bg_d, cmp_d))
+        ev.mark()
+        if g is not None:
+            g.g_bwd.replay()
+        else:
+            trn.grad.zero_()
+            trn.backward(gt_d, fg_d, bg_d, cmp_d)
+        ev.mark()
+        trn.apply_gradients()
+        ev.mark()
+    torch.cuda.synchronize()
+    wall = torch.tensor([(time.perf_counter() - t0) / steps], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(wall, op=dist.ReduceOp.MAX)
+    wall = float(wall)
+    e = ev.e
+    ph = [sum(ms(e[4 * i + k], e[4 * i + k + 1]) for i in range(steps)) / steps for k in range(3)]
+    dev_ms = sum(ph)
+    fwd_f, bwd_f = trn.conv_flops(n, size, size)
+    pk = PEAK_TFLOPS[dtype]
+    tf = (fwd_f + bwd_f) / (dev_ms * 1e-3) / 1e12
+    rec = {"workload": "train.py training_procedure step: %d x %dx%d per GPU, unet.UNetImage([cmp, bg]) fwd/bwd over "
+                       "all variables (VGG included), loss, DDP all-reduce, TF-Adam" % (n, size, size),
+           "dtype": dtype + " forward / MFMA gradients, f32 gradients/optimizer", "n_gpus": world,
+           "launch": "hip-graph replay of forward+loss and of backward, eager all-reduce + Adam + re-pack" if graph
+                     else "eager",
+           "samples_per_s": round(n * world / wall, 1), "ms_per_step": round(1000 * wall, 4),
+           "device_ms": {"forward_loss": round(ph[0], 4), "backward": round(ph[1], 4),
+                         "allreduce_adam_repack": round(ph[2], 4)},
+           "flops_per_step_per_gpu": {"forward": fwd_f, "backward": bwd_f},
+           "roofline": {"bound": "mfma", "achieved": round(tf, 2), "peak": pk, "unit": "TFLOP/s",
+                        "frac": round(tf / pk, 4),
+                        "def": "algorithmic conv FLOPs of the step (forward 20 convs + 20 filter gradients + 19 data "
+                               "gradients, 2*H*W*9*cin*cout each) over the step's device time (HIP events)"},
+           "loss_last": [round(float(v), 5) for v in trn._g["loss"].cpu()]}
+    if cpu and world == 1:
+        from oracle import models as om  # the CPU-baseline leg only
+        from oracle import train_ref as tr
+        p = om.unet_params(om.synthetic_vgg16(0), np.random.RandomState(4), video=False)
+        sl = lambda a: np.asarray(a[:1], np.float64)  # noqa: E731
+        best = None
+        for _ in range(2):
+            t0 = time.perf_counter()
+            tr.image_step_grads(sl(cmp), sl(bg - mean), sl(gt), sl(fg), p)
+            dt = time.perf_counter() - t0
+            best = dt if best is None else min(best, dt)
+        rec["cpu_baseline"] = {"value": round(1.0 / best, 4), "unit": "samples/s", "cores": threads, "kind": "port",
+                               "sample": "oracle/train_ref.py image_step_grads (torch-f64 autograd of UNetImage) on "
+                                         "one %dx%d sample (the config's sample size), best of 2" % (size, size)}
     return rec
 
 
@@ -789,7 +875,9 @@ def conv_roofline(prof, args):
         # GRBM_GUI_ACTIVE / 8: the launch's GPU cycles (summed over the 8 XCDs by rocprofv3)
         cyc = mk["GRBM_GUI_ACTIVE"] / 8.0
         rec["mfma_util"] = round(mk["SQ_VALU_MFMA_BUSY_CYCLES"] / (N_SIMD * cyc), 4)
-        rec["mfma_counters"] = {"source": src_m, "SQ_VALU_MFMA_BUSY_CYCLES": mk["SQ_VALU_MFMA_BUSY_CYCLES"],
+        rec["mfma_counters"] = {"source": src_m, "measured_in_this_run": False,
+                                "note": "copied from the committed rocprofv3 --pmc pass over the same workload "
+                                        "(tools/prof_bench.sh), not measured by this process", "SQ_VALU_MFMA_BUSY_CYCLES": mk["SQ_VALU_MFMA_BUSY_CYCLES"],
                                 "GRBM_GUI_ACTIVE": mk["GRBM_GUI_ACTIVE"], "SQ_BUSY_CYCLES": mk.get("SQ_BUSY_CYCLES"),
                                 "effective_clock_ghz": round(cyc / (t / n * 1e-3) / 1e9, 3),
                                 "def": "mfma_util = SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE/8): "
@@ -900,7 +988,7 @@ def main():
                          "the step is not host-bound, and the graph runs the side-stream select chains serially")
     ap.add_argument("--train-streams", type=int, default=3,
                     help="side streams of the config-5 trainer's select chains (0: one stream, for serial profiles)")
-    ap.add_argument("--only", choices=["train", "train_chain", "train_small", "temporal"],
+    ap.add_argument("--only", choices=["train", "train_chain", "train_small", "train_image", "temporal"],
                     help="profiling passes: run just this record (rank 0 / N=1) and print it")
     ap.add_argument("--temporal-sizes", default="500x1200,1080x1920", help="config-3 sizes HxW, comma separated")
     ap.add_argument("--temporal-dtypes", default="fp32,bf16", help="config-3 compute dtypes, comma separated")
@@ -948,6 +1036,8 @@ def main():
             rec = train_chain_bench(dev, args.steps, args.warmup)
         elif args.only == "train_small":
             rec = train_small_bench(dev, args.steps, args.warmup, world, rank, threads, cpu=False)
+        elif args.only == "train_image":
+            rec = train_image_bench(dev, args.steps, args.warmup, world, rank, threads, cpu=False)
         else:
             rec = temporal_bench(dev, args.steps, t_dtypes, t_sizes, False, threads)
         if rank == 0:
@@ -1021,6 +1111,8 @@ def main():
             train["chained"] = train_chain_bench(dev, 5, 2)
         train_small = train_small_bench(dev, max(args.steps // 4, 10), 3, world, rank, threads,
                                         cpu=not args.no_cpu_baseline)
+        train_image = train_image_bench(dev, max(args.steps // 4, 10), 3, world, rank, threads,
+                                        cpu=not args.no_cpu_baseline)
 
     roofline = conv_roofline(prof, args) if prof else None
     if rank == 0:
@@ -1083,6 +1175,7 @@ def main():
         if train:
             rec["train"] = train
             rec["train_small"] = train_small
+            rec["train_image"] = train_image
         if world == 1 and not args.no_loader:
             rec["loader"] = loader_bench(dev, max(args.steps // 4, 10), threads, cpu=not args.no_cpu_baseline)
         if world == 1 and not args.no_augment:

@@ -235,6 +235,14 @@ int vm_resize_bilinear_tf1_nhwc(const vm_tensor* x, vm_tensor* y, void* stream);
  * (packs the caller's f32 [N,H,W,7] frame into the compute layout; loader.py:76-78 mean/shift
  * can be folded in via shift).  Channels >= x->c of y are zero-filled. */
 int vm_convert_nhwc(const vm_tensor* x, vm_tensor* y, const float* scale, const float* shift, int act, void* stream);
+/* Split-bf16 x6 operand of an f32 activation (no reference counterpart: the operand format of the split-bf16 conv
+ * path, which evaluates unet.py's tf.nn.conv2d (unet.py:39,60,70) at f32 accuracy on bf16 MFMA).  x (f32 view,
+ * x.c channels) -> three bf16 parts h = bf16(x), m = bf16(x - h), l = bf16(x - h - m), written as six slabs
+ * [l, m, h, m, h, h] at channel p*S + y.coff + c of y (bf16, S = y.cstride / 6; y.c >= x.c, the extra channels 0).
+ * A conv over the 6*S channels with the filter parts [h, m, l, h, m, h] stacked along cin is the sum of the six
+ * cross products down to 2^-16 of the leading one.  y_pool (optional, same layout at ceil(h/2) x ceil(w/2)): the
+ * split of tf.nn.max_pool 2x2 SAME (unet.py:33) of x, from the same pass. */
+int vm_split6_nhwc(const vm_tensor* x, vm_tensor* y, vm_tensor* y_pool, void* stream);
 
 /* tf.contrib.layers.batch_norm(is_training=True): batch mean / biased variance over N,H,W
  * (unet_simple.py:25,41; small.py:22,32).  work: vm_bn_workspace_bytes(x) bytes of device scratch. */

@@ -149,7 +149,7 @@ def train_step_grads(cmp, bg, warped, gt, raw_fg, vgg, params, bn=None, towers=N
     loss = _loss(la, lc, sample_weights)
     loss.backward()
     grads = {k: v.grad.cpu().numpy().copy() for k, v in V.items()}
-    terms = (float(loss), float(la.mean()), float(lc.mean()))
+    terms = (float(loss.detach()), float(la.mean().detach()), float(lc.mean().detach()))
     return terms, alpha.detach().cpu().numpy(), grads
 
 

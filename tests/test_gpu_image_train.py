@@ -81,14 +81,21 @@ def test_image_step_fp32_matches_f64_autograd(n, h, w):
     trn.grad.zero_()
     trn.backward(T(gt), T(fg), T(bg), T(cmp))
     torch.cuda.synchronize()
-    terms, alpha, grads, _ = tr.image_step_grads(cmp, bg, gt, fg, params)
+    terms, alpha, grads, fwd = tr.image_step_grads(cmp, bg, gt, fg, params)
     assert np.abs(H(trn.model.output) - alpha).max() <= 1e-4
     for a, b in zip(loss, terms):
         assert abs(a - b) <= 1e-5 * abs(b), (loss, terms)
     assert len(grads) == 36 and set(grads) == set((s, k) for s, k, _, _ in trn.layout)
     errs = _grad_errors(trn, grads)
-    bad = {k: v for k, v in errs.items() if not v <= 2e-3}
-    print("fp32 image step %dx%dx%d worst rel L2 %.3g" % (n, h, w, max(errs.values())))
+    # conv1_1 reads the raw +-128 input: a pre-activation within f32 rounding of 0 can take the other side of the
+    # relu than in float64, and ONE such mask flip moves conv1_1's filter gradient by ~2e-3 relative L2 (its 54
+    # entries of one output channel, each a ~60-pixel-deep sum, shift by ~1/60).  Counted, and allowed per flip.
+    flips = int(np.count_nonzero((H(trn.model.conv1_1) > 0) != (fwd["conv1_1"] > 0)))
+    tol = {k: 2e-3 + (5e-3 * flips if k == ("conv1_1", "w") else 0.0) for k in errs}
+    bad = {k: v for k, v in errs.items() if not v <= tol[k]}
+    print("fp32 image step %dx%dx%d worst rel L2 %.3g, conv1_1 relu-mask flips vs f64: %d"
+          % (n, h, w, max(errs.values()), flips))
+    assert flips <= 3
     assert not bad, bad
 
 

@@ -795,6 +795,67 @@ def test_train_graph_step_equals_eager(dtype):
     assert torch.equal(eager.flat, single.flat)
 
 
+def test_train_graph_under_high_priority_caller_stream():
+    """a capture made while the caller's current stream is a high-priority stream (the measured
+    -1 % configuration) is a single-level fork of the select chains from the capture's origin: it
+    captures, and its replayed step is bit-identical to the eager step."""
+    from vmatting.train import VideoTrainer
+    from vmatting.weights import synthetic_vgg16
+    vgg = synthetic_vgg16(0)
+    params = om.unet_simple_params(np.random.RandomState(1))
+    b1 = _batch(2, 48, 64, seed=3)
+    eager = VideoTrainer(vgg, "bf16", DEV, params=params)
+    le = H(eager.step(*b1))
+    hp = torch.cuda.Stream(priority=torch.cuda.Stream.priority_range()[1])
+    with torch.cuda.stream(hp):
+        graphed = VideoTrainer(vgg, "bf16", DEV, params=params)
+        g = graphed.capture(*b1)
+        lg = H(g.step())
+    torch.cuda.synchronize()
+    assert np.array_equal(le, lg), (le, lg)
+    assert torch.equal(eager.flat, graphed.flat)
+
+
+def test_train_capture_refuses_nested_fork():
+    """VERDICT r04 item 2 (gpurun_out/c17t.log: SIGSEGV in torch/cuda/graphs.py capture_end).  Cause, isolated by
+    tools/capture_probe.py on MI355X: a stream forked inside a HIP graph capture that forks again (capture -> s1 ->
+    s2, all joined back) crashes hipStreamEndCapture, with or without stream priorities; a single-level fork is
+    fine.  The dropped r04 variant moved each pass onto a trainer-owned high-priority stream, so the select chains
+    forked from that stream: a nested fork.  The trainer now refuses it with a RuntimeError before the inner fork
+    (the outer fork here is joined back in a finally, so the capture ends cleanly)."""
+    from vmatting.train import VideoTrainer
+    from vmatting.weights import synthetic_vgg16
+
+    class PassOnOwnStream(VideoTrainer):
+        def __init__(self, *a, **k):
+            super().__init__(*a, **k)
+            self._hp = torch.cuda.Stream(priority=torch.cuda.Stream.priority_range()[1])
+
+        def _fork(self, fn, *a):
+            cur = torch.cuda.current_stream()
+            self._hp.wait_stream(cur)
+            try:
+                with torch.cuda.stream(self._hp):
+                    return fn(*a)
+            finally:
+                cur.wait_stream(self._hp)
+
+        def forward(self, *a):
+            return self._fork(super().forward, *a)
+
+        def backward(self, *a):
+            return self._fork(super().backward, *a)
+
+    params = om.unet_simple_params(np.random.RandomState(1))
+    b1 = _batch(2, 48, 64, seed=3)
+    trn = PassOnOwnStream(synthetic_vgg16(0), "bf16", DEV, params=params)
+    H(trn.step(*b1))  # eager: the nested fork is fine outside a capture
+    with pytest.raises(RuntimeError, match="nested fork"):
+        trn.capture(*b1)
+    torch.cuda.synchronize()
+    H(trn.step(*b1))  # the trainer and the device are still usable
+
+
 @pytest.mark.slow
 def test_side_streams_bit_identical_bench_shape():
     """the select chains write channel slices of the concat rows on side streams while the main stream's

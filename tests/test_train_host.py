@@ -173,3 +173,22 @@ def test_image_step_oracle_forward_matches_numpy_oracle():
     assert len(grads) == 36
     assert not any(s.startswith("upconv") for s, k in grads if k == "b")
     assert all(np.isfinite(g).all() for g in grads.values())
+
+
+def test_split6_filter_parts_reconstruct_the_filter():
+    """vmatting/split6.py: the filter's three bf16 parts (h, m, l) sum back to the f32 filter to within 2^-24 of
+    each weight, each part is exactly representable in bf16, and the stack follows the slab order [h, m, l, h, m, h]
+    with zero padding rows past cin."""
+    from vmatting.split6 import split6_filter, W_PARTS
+    rs = np.random.RandomState(0)
+    w = (rs.normal(size=(3, 3, 5, 7)) * np.logspace(-3, 2, 7)).astype(np.float32)
+    s = split6_filter(w, 8, 7).numpy().astype(np.float64)
+    assert s.shape == (3, 3, 48, 7)
+    parts = [s[:, :, p * 8:p * 8 + 5] for p in range(3)]
+    assert np.all(np.abs(parts[0] + parts[1] + parts[2] - w) <= 2.0 ** -24 * np.abs(w))
+    for p in range(6):
+        blk = s[:, :, p * 8:(p + 1) * 8]
+        assert not blk[:, :, 5:].any()
+        assert np.array_equal(blk[:, :, :5], parts[W_PARTS[p]])
+        t = torch.from_numpy(blk.astype(np.float32))
+        assert torch.equal(t.bfloat16().float(), t)

@@ -1,0 +1,47 @@
+"""1080p forward time of the split-bf16 x6 path against fp32 and bf16 (graph replay), plus its per-conv kernels:
+    python tools/x6bench.py [steps]"""
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.path.join(REPO, "video-matting_amd")]
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from vmatting import ops, unet, video  # noqa: E402
+from vmatting.weights import synthetic_vgg16  # noqa: E402
+
+steps = int(sys.argv[1]) if len(sys.argv) > 1 else 10
+x = video.synthetic_frames(1, 1080, 1920, first=0, device="cuda")
+res = {}
+for dt in ("bf16x6", "fp32", "bf16"):
+    np.random.seed(0)
+    m = unet.UNetVideo(synthetic_vgg16(0), dtype=dt)
+    m.prepare()
+    g = m.capture(x)
+    for _ in range(2):
+        g.replay()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        g.replay()
+    torch.cuda.synchronize()
+    ms = 1e3 * (time.perf_counter() - t0) / steps
+    res[dt] = (ms, g.output.clone())
+    print("%-7s %.3f ms/frame" % (dt, ms), flush=True)
+    if dt == "bf16x6":
+        prof = ops.conv_profile(True)
+        m.forward(x)
+        torch.cuda.synchronize()
+        ops.conv_profile(False)
+        tot = 0.0
+        for fl, name, e0, e1, *shape in prof:
+            t = e0.elapsed_time(e1)
+            tot += t
+            print("  %-70s %7.3f ms %7.1f TFLOP/s (x6 products)" % (name[:70], t, fl / (t * 1e-3) / 1e12))
+        print("  conv total %.3f ms" % tot)
+    del m, g
+    torch.cuda.empty_cache()
+print("bf16x6 vs fp32 alpha max-abs %.3e" % float((res["bf16x6"][1] - res["fp32"][1]).abs().max()))

@@ -518,6 +518,125 @@ extern "C" int vm_resize_bilinear_tf1_nhwc(const vm_tensor* x, vm_tensor* y, voi
   return check_launch("resize_tf1");
 }
 
+
+// ---------------------------------------------------------------- split-bf16 x6 operands (unet.py forward at f32 accuracy)
+// An f32 activation x is held as three bf16 parts x = h + m + l (h = bf16(x), m = bf16(x - h), l = bf16(x - h - m):
+// both differences are exact in f32, so the parts carry x's 24 significant bits).  A conv over such an input is a
+// bf16 MFMA conv over 6 channel slabs with exact bf16 x bf16 products and f32 sums: the slabs [l, m, h, m, h, h] meet
+// the filter parts [h, m, l, h, m, h] packed along K, i.e. l*Wh + m*Wm + h*Wl + m*Wh + h*Wm + h*Wh — every product
+// down to 2^-16 of the leading one, smallest first (the MFMA K loop sums granules in order, so the 2^-16 terms are
+// summed while the accumulator is still small).  Layout of the split buffer: slab p of channel c at p*S + coff + c,
+// S = cstride / 6 (the channel count of the whole concat this view is a segment of).
+// POOL: the tile's 2x2 SAME max-pool of x (f32, before the split) is split into a second view of the same layout.
+__device__ __forceinline__ void split3(float x, uint16_t& h, uint16_t& m, uint16_t& l) {
+  h = f2bf(x);
+  const float r1 = x - bf2f(h);
+  m = f2bf(r1);
+  l = f2bf(r1 - bf2f(m));
+}
+
+__device__ __forceinline__ void store_split6(uint16_t* base, long S, const float* v) {
+  uint32_t wh[4], wm[4], wl[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    uint16_t h0, m0, l0, h1, m1, l1;
+    split3(v[2 * i], h0, m0, l0);
+    split3(v[2 * i + 1], h1, m1, l1);
+    wh[i] = (uint32_t)h0 | ((uint32_t)h1 << 16);
+    wm[i] = (uint32_t)m0 | ((uint32_t)m1 << 16);
+    wl[i] = (uint32_t)l0 | ((uint32_t)l1 << 16);
+  }
+  const uint4 H = make_uint4(wh[0], wh[1], wh[2], wh[3]), M = make_uint4(wm[0], wm[1], wm[2], wm[3]),
+              L = make_uint4(wl[0], wl[1], wl[2], wl[3]);
+  *reinterpret_cast<uint4*>(base) = L;
+  *reinterpret_cast<uint4*>(base + S) = M;
+  *reinterpret_cast<uint4*>(base + 2 * S) = H;
+  *reinterpret_cast<uint4*>(base + 3 * S) = M;
+  *reinterpret_cast<uint4*>(base + 4 * S) = H;
+  *reinterpret_cast<uint4*>(base + 5 * S) = H;
+}
+
+// one thread = one 8-channel chunk of one output pixel (POOL: of one pooled pixel and the 2x2 window under it)
+template <bool POOL>
+__global__ __launch_bounds__(256) void split6_kernel(View x, View y, View yp) {
+  const int cpp = (y.c + 7) / 8;
+  const long S = y.cs / 6;
+  const int on = POOL ? yp.n : y.n, oh = POOL ? yp.h : y.h, ow = POOL ? yp.w : y.w;
+  const long total = (long)on * oh * ow * cpp;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int cc = (int)(i % cpp);
+    const long op = i / cpp;
+    const int c = cc * 8;
+    auto load = [&](long pix, float* f) {
+      const float* src = reinterpret_cast<const float*>(x.p) + pix * x.cs + x.coff + c;
+      if (c + 8 <= x.c && ((x.cs | x.coff) & 3) == 0 && (reinterpret_cast<uintptr_t>(x.p) & 15) == 0) {
+        const float4 a = *reinterpret_cast<const float4*>(src), b = *reinterpret_cast<const float4*>(src + 4);
+        f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w; f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] = c + j < x.c ? src[j] : 0.f;  // channels past x.c: zero padding
+      }
+    };
+    auto out = [&](const View& v, long pix) {
+      return reinterpret_cast<uint16_t*>(v.p) + pix * v.cs + v.coff + c;
+    };
+    if constexpr (!POOL) {
+      float f[8];
+      load(op, f);
+      store_split6(out(y, op), S, f);
+    } else {
+      const int pw = (int)(op % yp.w);
+      const long t = op / yp.w;
+      const int ph = (int)(t % yp.h), n = (int)(t / yp.h);
+      const int iy = 2 * ph, ix = 2 * pw;
+      const bool hasr = ix + 1 < x.w, hasd = iy + 1 < x.h;
+      const long p00 = ((long)n * x.h + iy) * x.w + ix;
+      float f[8], m[8];
+      load(p00, f);
+      store_split6(out(y, p00), S, f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) m[j] = f[j];
+      auto tap = [&](long pix) {
+        load(pix, f);
+        store_split6(out(y, pix), S, f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) m[j] = fmaxf(m[j], f[j]);
+      };
+      if (hasr) tap(p00 + 1);
+      if (hasd) tap(p00 + x.w);
+      if (hasr && hasd) tap(p00 + x.w + 1);
+      store_split6(out(yp, op), yp.cs / 6, m);
+    }
+  }
+}
+
+
+static bool split6_view_ok(const vm_tensor* y, const vm_tensor* x) {
+  return y->dtype == VM_BF16 && y->cstride % 48 == 0 && y->coff % 8 == 0 && y->c % 8 == 0 && y->c >= x->c &&
+         y->coff + y->c <= y->cstride / 6 && reinterpret_cast<uintptr_t>(y->ptr) % 16 == 0;
+}
+
+extern "C" int vm_split6_nhwc(const vm_tensor* x, vm_tensor* y, vm_tensor* y_pool, void* stream) {
+  if (!valid_tensor(x) || !valid_tensor(y) || (y_pool && !valid_tensor(y_pool)) || x->dtype != VM_F32)
+    return fail(VM_EINVAL, "split6: x must be an f32 view");
+  if (y->n != x->n || y->h != x->h || y->w != x->w) return fail(VM_EINVAL, "split6: shape mismatch");
+  if (!split6_view_ok(y, x) || (y_pool && !split6_view_ok(y_pool, x)))
+    return fail(VM_EUNSUPPORTED, "split6: the split view must be bf16, 16-byte aligned, c and coff multiples of 8, "
+                                 "cstride = 6 x a multiple of 8 channels");
+  if (y_pool && (y_pool->n != x->n || y_pool->h != (x->h + 1) / 2 || y_pool->w != (x->w + 1) / 2 ||
+                 y_pool->c != y->c))
+    return fail(VM_EINVAL, "split6: pool view shape mismatch");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const vm_tensor* o = y_pool ? y_pool : y;
+  const long work = (long)o->n * o->h * o->w * ((y->c + 7) / 8);
+  if (y_pool)
+    hipLaunchKernelGGL(split6_kernel<true>, dim3(grid_for(work, 256)), dim3(256), 0, st, view(x), view(y),
+                       view(y_pool));
+  else
+    hipLaunchKernelGGL(split6_kernel<false>, dim3(grid_for(work, 256)), dim3(256), 0, st, view(x), view(y), view(y));
+  return check_launch("split6");
+}
+
 extern "C" int vm_convert_nhwc(const vm_tensor* x, vm_tensor* y, const float* scale, const float* shift, int act,
                                void* stream) {
   if (!valid_tensor(x) || !valid_tensor(y)) return fail(VM_EINVAL, "convert: invalid tensor");

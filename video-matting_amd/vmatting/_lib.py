@@ -97,6 +97,7 @@ SIGNATURES = [
     ("vm_maxpool2x2_same_nhwc", c_int, [P, P, c_void_p]),
     ("vm_resize_bilinear_tf1_nhwc", c_int, [P, P, c_void_p]),
     ("vm_convert_nhwc", c_int, [P, P, c_void_p, c_void_p, c_int, c_void_p]),
+    ("vm_split6_nhwc", c_int, [P, P, P, c_void_p]),
     ("vm_bn_workspace_bytes", c_size_t, [P]),
     ("vm_bn_stats_nhwc", c_int, [P, c_void_p, c_void_p, c_void_p, c_void_p]),
     ("vm_bn_apply_nhwc", c_int, [P, P, c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_int, c_void_p]),

@@ -161,6 +161,7 @@ class VideoTrainer(TrainerBase):
         dev_ = torch.device(device)
         self._side = [] if self.sync_bn or streams < 1 or dev_.type != "cuda" else \
             [torch.cuda.Stream(device=dev_) for _ in range(int(streams))]
+        self._capture_origin = None  # the stream a TrainGraph capture began on (see _check_capture_fork)
         dev = self.device
         # move the freshly drawn variables into the flat buffer and alias every consumer onto it
         for scope, pc in self.model.convs.items():
@@ -283,7 +284,23 @@ class VideoTrainer(TrainerBase):
         bnl = self.model.bn[scope]
         ops.bn_apply(z, mean, var, bnl.gamma, bnl.beta, EPS, act, out=out)
 
+    def _check_capture_fork(self):
+        """The side-stream fork of forward / backward is legal inside a HIP graph capture only from the stream the
+        capture began on.  Forking from a stream that was itself forked inside the capture (e.g. a pass moved onto
+        its own high-priority stream) is a nested fork, and ROCm 7's hipStreamEndCapture segfaults on a captured
+        nested fork (tools/capture_probe.py: capture -> s1 -> s2 -> joined back dies in capture_end with SIGSEGV,
+        with or without stream priorities; a single-level fork is fine).  That was the r04 segfault under
+        test_train_graph_step_equals_eager.  Refused here with an exception instead: capture through
+        VideoTrainer.capture() (which records the origin), or build the trainer with streams=0."""
+        if not self._side or not torch.cuda.is_current_stream_capturing():
+            return
+        if self._capture_origin is None or torch.cuda.current_stream(self.device) != self._capture_origin:
+            raise RuntimeError("VideoTrainer: side-stream fork inside a HIP graph capture from a stream other than "
+                               "the capture's origin (a nested fork, which segfaults hipStreamEndCapture on ROCm); "
+                               "capture with VideoTrainer.capture() on the caller's stream, or use streams=0")
+
     def forward(self, cmp, bg, warped):
+        self._check_capture_fork()
         m = self.model
         xs = [t if isinstance(t, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(t, np.float32))
               for t in (cmp, bg, warped)]
@@ -353,6 +370,7 @@ class VideoTrainer(TrainerBase):
         return dz
 
     def backward(self, gt, raw_fg, bg, cmp):
+        self._check_capture_fork()
         m, tb = self.model, self._tb
         b = m._ws
         main = torch.cuda.current_stream(self.device) if self._side else None
@@ -450,11 +468,20 @@ class TrainGraph:
             self._backward()
         torch.cuda.current_stream(dev).wait_stream(side)
         torch.cuda.synchronize(dev)
+        for t in trn._tb.values():  # allocated on the side stream, replayed on the caller's
+            for u in (t if isinstance(t, tuple) else (t,)):
+                if isinstance(u, torch.Tensor):
+                    u.record_stream(torch.cuda.current_stream(dev))
         self.g_fwd, self.g_bwd = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.g_fwd):
-            self._forward()
-        with torch.cuda.graph(self.g_bwd):
-            self._backward()
+        try:
+            with torch.cuda.graph(self.g_fwd):
+                trn._capture_origin = torch.cuda.current_stream(dev)
+                self._forward()
+            with torch.cuda.graph(self.g_bwd):
+                trn._capture_origin = torch.cuda.current_stream(dev)
+                self._backward()
+        finally:
+            trn._capture_origin = None
 
     def _forward(self):
         cmp, bg, warped, gt, fg = self.inputs

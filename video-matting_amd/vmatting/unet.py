@@ -76,7 +76,10 @@ class UNet:
 
     def __init__(self, vgg16_npy_path=None, dtype="bf16", device="cuda"):
         self.data_dict = load_vgg16(vgg16_npy_path)
-        self.dtype = ops.TORCH_DTYPE[dtype] if isinstance(dtype, str) else dtype
+        # "bf16x6": the split-bf16 x6 path (vmatting/split6.py) — f32 accuracy on the bf16 MFMA kernels
+        self.x6mode = dtype == "bf16x6"
+        self._x6 = None
+        self.dtype = torch.bfloat16 if self.x6mode else (ops.TORCH_DTYPE[dtype] if isinstance(dtype, str) else dtype)
         self.device = torch.device(device)
         self.params = None       # name -> (w_hwio f32 np, bias f32 np | None)
         self.convs = None        # name -> ops.PackedConv
@@ -120,6 +123,12 @@ class UNet:
         return self
 
     def _pack(self):
+        if self.x6mode:
+            from .split6 import Split6Forward
+            self._x6 = Split6Forward(self)
+            self.convs = self._x6.convs
+            self._head_up = None
+            return
         self.convs = {k: ops.PackedConv(w, b, self.dtype, self.device) for k, (w, b) in self.params.items()}
         self._head_up = None
         if self._lean():
@@ -128,10 +137,12 @@ class UNet:
                              ops.PackedConv(np.ascontiguousarray(w[:, :, :64, :]), b, self.dtype, self.device))
 
     def _lean(self):
-        return self.split_head and self.fuse_first and self.dtype == torch.bfloat16
+        return not self.x6mode and self.split_head and self.fuse_first and self.dtype == torch.bfloat16
 
     def weights_flat(self):
         """All packed weights as one list of tensors (for an RCCL broadcast from rank 0)."""
+        if self._x6 is not None:
+            return self._x6.weights_flat()
         out = []
         for k in sorted(self.convs):
             pc = self.convs[k]
@@ -198,6 +209,11 @@ class UNet:
                                           input.dtype == torch.float32) else input
         if self.convs is None:
             raise RuntimeError("call build() first")
+        if self._x6 is not None:  # split-bf16 x6: only .output and .conv1_3 (the logits) are kept
+            alpha = self._x6.forward(x, out)
+            self._x, self._ws, self._ws_key = x, self._x6._b, self._x6._key
+            self.conv1_3, self.output = self._x6.logits, alpha
+            return alpha
         n, h, w, c = x.shape
         b = self._buffers(n, h, w)
         L = _levels(h, w)
