@@ -374,6 +374,13 @@ int vm_tps_sample(const vm_tps_map* map, const void* img, int ih, int iw, int cn
  * VM_U8 (15-bit fixed-point weights), VM_F32 or VM_F64 (float table weights). */
 int vm_warp_affine(const void* src, int ih, int iw, int cn, int dtype, const double* m, void* dst, int h, int w,
                    void* stream);
+/* augmentation.warp_image without its TPS part (augmentation.py:59-63): cv2.warpAffine by the integer translation
+ * [[1,0,tu],[0,1,tv]] to (w, h), then cv2.warpAffine by m (the forward getRotationMatrix2D, inverted as warpAffine
+ * does) to (w, h) — fused into one pass, bit-identical to the two vm_warp_affine calls (the translation's fixed-point
+ * fraction is zero, so its output is src shifted with zero fill).  lut (optional, u8 BGR only): then
+ * change_illumination (augmentation.py:86-98, 133-134) with that S/V map, as vm_change_illumination_u8. */
+int vm_warp_image(const void* src, int ih, int iw, int cn, int dtype, int tu, int tv, const double* m,
+                  const uint8_t* lut, void* dst, int h, int w, void* stream);
 
 /* augmentation.change_illumination (augmentation.py:86-98): cvtColor BGR2HSV (uint8, hrange 180), S and V through
  * lut (HOST, 256 bytes: lut[u] = uint8(255 * clip(a * (u/255.)**b + c, 0, 1)), built by the caller with the

@@ -291,3 +291,47 @@ def test_composite_image_matches_numpy(shape, cn, idt, adt):
     assert np.array_equal(H(out), ref)
     out32 = reader.create_composite_image(dev(fg), dev(bg), dev(alpha), out_dtype=torch.float32)
     assert np.array_equal(H(out32), ref.astype(np.float32))
+
+
+@pytest.mark.parametrize("kind", ["u8x3", "u8x3_lut", "f64", "f32x2"])
+def test_warp_image_fused_equals_two_warps(kind):
+    """vm_warp_image (augmentation.warp_image's translate + warpAffine pair in one pass, + the illumination change)
+    is bit-identical to the two vm_warp_affine passes (+ vm_change_illumination_u8), incl. translations that push
+    the image off the canvas and a source larger than the output (the TPS output is (h+1) x (w+1))."""
+    from vmatting import augmentation as va
+    from vmatting import ops
+    rs = np.random.RandomState(len(kind))
+    h, w = 41, 67
+    shp = {"u8x3": (h + 1, w + 1, 3), "u8x3_lut": (h + 1, w + 1, 3), "f64": (h + 1, w + 1), "f32x2": (h, w, 2)}[kind]
+    src = rs.rand(*shp) * 255
+    src = src.astype(np.uint8) if kind.startswith("u8") else src.astype(np.float64 if kind == "f64" else np.float32)
+    d = torch.from_numpy(src).cuda()
+    lut = va.illumination_lut(1.03, 0.81, -0.05) if kind == "u8x3_lut" else None
+    for tu, tv in [(0, 0), (5, -3), (-20, 11), (70, 0), (0, -45)]:
+        for center, rot, scale in [((w // 2, h // 2), 0.0, 1.07), ((30, 17), -8.5, 1.12), ((3, 40), 9.9, 1.0)]:
+            M = va.rotation_matrix(center, rot, scale)
+            got = ops.warp_image(d, tu, tv, M, (w, h), lut)
+            t = ops.warp_affine(d, np.float32([[1, 0, tu], [0, 1, tv]]), (w, h))
+            want = ops.warp_affine(t, M, (w, h))
+            if lut is not None:
+                want = ops.change_illumination(want, lut)
+            assert torch.equal(got, want), (tu, tv, center, rot, scale)
+
+
+def test_augment_many_equals_sequential_augment():
+    """augment_many (one statistics readback, one landmark upload, fused warps) draws like consecutive augment calls
+    and returns bit-identical samples."""
+    from vmatting import augmentation as va
+    g = golden("augment")
+    triples = [(g["fg%d" % i], g["bg%d" % i], g["alpha%d" % i]) for i in (0, 1)] * 2
+    np.random.seed(11)
+    many = va.augment_many([tuple(torch.from_numpy(np.ascontiguousarray(a)).cuda() for a in t) for t in triples])
+    nxt = np.random.randint(0, 1 << 30)
+    np.random.seed(11)
+    seq = [va.augment(*t) for t in triples]
+    assert np.random.randint(0, 1 << 30) == nxt
+    for (a, b, c), (x, y, z) in zip(many, seq):
+        assert np.array_equal(H(a), x) and np.array_equal(H(b), y) and np.array_equal(H(c), z)
+    st = va.StatsPrefetch([torch.from_numpy(np.ascontiguousarray(t[2])).cuda() for t in triples]).result()
+    assert st == va.nonzero_stats_many([torch.from_numpy(np.ascontiguousarray(t[2])).cuda() for t in triples])
+    assert st[0][0] == int(np.count_nonzero(triples[0][2]))

@@ -232,63 +232,126 @@ struct Lut256 {
 // augmentation.change_illumination (augmentation.py:86-98): cvtColor BGR2HSV (RGB2HSV_b, hsv_shift 12, hrange
 // 180), S and V through the host-built map lut[u] = uint8(255 * clip(a * (u/255)^b + c, 0, 1)), cvtColor HSV2BGR
 // (HSV2RGB_b: float32 HSV2RGB_f, then cvRound(x * 255) saturated).  The division tables live in LDS.
-__global__ void __launch_bounds__(256) illumination_kernel(const uint8_t* __restrict__ bgr, long pixels, Lut256 lut,
-                                                           uint8_t* __restrict__ out) {
-  __shared__ int sdiv[256], hdiv[256];
-  {
-    const int t = threadIdx.x;
+// HSV round trip of one BGR pixel with S, V through lut (the division tables sdiv / hdiv in LDS)
+__device__ __forceinline__ void illum_px(int b, int g, int r, const Lut256& lut, const int* sdiv, const int* hdiv,
+                                         uint8_t* o) {
+  const float hscale = 6.f / 180.f;
+  const float inv255 = 1.f / 255.f;
+  int v = b > g ? b : g;
+  v = v > r ? v : r;
+  int vmin = b < g ? b : g;
+  vmin = vmin < r ? vmin : r;
+  const int diff = v - vmin;
+  const int vr = v == r ? -1 : 0, vg = v == g ? -1 : 0;
+  const int s = (diff * sdiv[v] + (1 << 11)) >> 12;
+  int hh = (vr & (g - b)) + (~vr & ((vg & (b - r + 2 * diff)) + ((~vg) & (r - g + 4 * diff))));
+  hh = (hh * hdiv[diff] + (1 << 11)) >> 12;
+  hh += hh < 0 ? 180 : 0;
+  // new_hsv = (h, lut[s], lut[v]) -> HSV2RGB_b
+  float hf = (float)(uint8_t)hh;
+  const float sf = (float)lut.t[s] * inv255;
+  const float vf = (float)lut.t[v] * inv255;
+  float ob, og, orr;
+  if (sf == 0.f) {
+    ob = og = orr = vf;
+  } else {
+    hf *= hscale;
+    while (hf < 0.f) hf += 6.f;
+    while (hf >= 6.f) hf -= 6.f;
+    int sector = (int)floorf(hf);
+    hf -= (float)sector;
+    if ((unsigned)sector >= 6u) {
+      sector = 0;
+      hf = 0.f;
+    }
+    float tab[4];
+    tab[0] = vf;
+    tab[1] = vf * (1.f - sf);
+    tab[2] = vf * (1.f - sf * hf);
+    tab[3] = vf * (1.f - sf * (1.f - hf));
+    const int sd[6][3] = {{1, 3, 0}, {1, 0, 2}, {3, 0, 1}, {0, 2, 1}, {0, 1, 3}, {2, 1, 0}};
+    ob = tab[sd[sector][0]];
+    og = tab[sd[sector][1]];
+    orr = tab[sd[sector][2]];
+  }
+  auto sat = [](float x) -> uint8_t {
+    const int q = (int)rintf(x * 255.f);
+    return (uint8_t)(q < 0 ? 0 : (q > 255 ? 255 : q));
+  };
+  o[0] = sat(ob);
+  o[1] = sat(og);
+  o[2] = sat(orr);
+}
+
+__device__ __forceinline__ void illum_tables(int* sdiv, int* hdiv) {
+  for (int t = threadIdx.x; t < 256; t += blockDim.x) {
     sdiv[t] = t ? (int)rint((double)(255 << 12) / (1.0 * t)) : 0;
     hdiv[t] = t ? (int)rint((double)(180 << 12) / (6.0 * t)) : 0;
   }
   __syncthreads();
-  const float hscale = 6.f / 180.f;
-  const float inv255 = 1.f / 255.f;
+}
+
+__global__ void __launch_bounds__(256) illumination_kernel(const uint8_t* __restrict__ bgr, long pixels, Lut256 lut,
+                                                           uint8_t* __restrict__ out) {
+  __shared__ int sdiv[256], hdiv[256];
+  illum_tables(sdiv, hdiv);
   for_pixels(pixels, 3, out, [&](long i, uint8_t* o) {
-    const int b = bgr[3 * i], g = bgr[3 * i + 1], r = bgr[3 * i + 2];
-    int v = b > g ? b : g;
-    v = v > r ? v : r;
-    int vmin = b < g ? b : g;
-    vmin = vmin < r ? vmin : r;
-    const int diff = v - vmin;
-    const int vr = v == r ? -1 : 0, vg = v == g ? -1 : 0;
-    const int s = (diff * sdiv[v] + (1 << 11)) >> 12;
-    int hh = (vr & (g - b)) + (~vr & ((vg & (b - r + 2 * diff)) + ((~vg) & (r - g + 4 * diff))));
-    hh = (hh * hdiv[diff] + (1 << 11)) >> 12;
-    hh += hh < 0 ? 180 : 0;
-    // new_hsv = (h, lut[s], lut[v]) -> HSV2RGB_b
-    float hf = (float)(uint8_t)hh;
-    const float sf = (float)lut.t[s] * inv255;
-    const float vf = (float)lut.t[v] * inv255;
-    float ob, og, orr;
-    if (sf == 0.f) {
-      ob = og = orr = vf;
-    } else {
-      hf *= hscale;
-      while (hf < 0.f) hf += 6.f;
-      while (hf >= 6.f) hf -= 6.f;
-      int sector = (int)floorf(hf);
-      hf -= (float)sector;
-      if ((unsigned)sector >= 6u) {
-        sector = 0;
-        hf = 0.f;
-      }
-      float tab[4];
-      tab[0] = vf;
-      tab[1] = vf * (1.f - sf);
-      tab[2] = vf * (1.f - sf * hf);
-      tab[3] = vf * (1.f - sf * (1.f - hf));
-      const int sd[6][3] = {{1, 3, 0}, {1, 0, 2}, {3, 0, 1}, {0, 2, 1}, {0, 1, 3}, {2, 1, 0}};
-      ob = tab[sd[sector][0]];
-      og = tab[sd[sector][1]];
-      orr = tab[sd[sector][2]];
-    }
-    auto sat = [](float x) -> uint8_t {
-      const int q = (int)rintf(x * 255.f);
-      return (uint8_t)(q < 0 ? 0 : (q > 255 ? 255 : q));
+    illum_px(bgr[3 * i], bgr[3 * i + 1], bgr[3 * i + 2], lut, sdiv, hdiv, o);
+  });
+}
+
+// augmentation.warp_image without the TPS part (augmentation.py:59-63) in ONE pass, optionally followed by
+// change_illumination (augmentation.py:133-134, u8 BGR only).  The first cv2.warpAffine is the integer translation
+// [[1, 0, tu], [0, 1, tv]]: its fixed-point coordinates have zero fraction, so translated(y, x) = src(y - tv, x - tu)
+// inside src, else 0, exactly (u8: (v*32768 + 2^14) >> 15 = v; float: v*1 + 0 + 0 + 0).  The second warpAffine
+// (getRotationMatrix2D, inverted on the host side as warpAffine does) then gathers its 4 taps from that virtual
+// translated image (size h x w, zero outside) — no intermediate image in HBM.
+template <typename T, bool ILLUM>
+__global__ void __launch_bounds__(256) warp_image_kernel(const T* __restrict__ src, int ih, int iw, int cn, int tu,
+                                                         int tv, Affine a, Lut256 lut, T* __restrict__ dst, int h,
+                                                         int w) {
+  __shared__ int sdiv[256], hdiv[256];
+  if constexpr (ILLUM) illum_tables(sdiv, hdiv);
+  const long total = (long)h * w;
+  for_pixels(total, cn, dst, [&](long i, T* o) {
+    const int y = row_of(i, w), x = (int)(i - (long)y * w);
+    const int adelta = cv_round(a.m[0] * (double)x * 1024.0);
+    const int bdelta = cv_round(a.m[3] * (double)x * 1024.0);
+    const int X0 = cv_round((a.m[1] * (double)y + a.m[2]) * 1024.0) + 16;
+    const int Y0 = cv_round((a.m[4] * (double)y + a.m[5]) * 1024.0) + 16;
+    const int X = (X0 + adelta) >> 5, Y = (Y0 + bdelta) >> 5;
+    int sx = X >> 5, sy = Y >> 5;
+    sx = sx < -32768 ? -32768 : (sx > 32767 ? 32767 : sx);
+    sy = sy < -32768 ? -32768 : (sy > 32767 ? 32767 : sy);
+    const int ax = X & 31, ay = Y & 31;
+    // a tap (ty, tx) of the translated image: inside it AND its source pixel inside src
+    auto ok = [&](int ty, int tx) {
+      return (unsigned)ty < (unsigned)h && (unsigned)tx < (unsigned)w && (unsigned)(ty - tv) < (unsigned)ih &&
+             (unsigned)(tx - tu) < (unsigned)iw;
     };
-    o[0] = sat(ob);
-    o[1] = sat(og);
-    o[2] = sat(orr);
+    const bool k0 = ok(sy, sx), k1 = ok(sy, sx + 1), k2 = ok(sy + 1, sx), k3 = ok(sy + 1, sx + 1);
+    const T* p = src + ((long)(sy - tv) * iw + (sx - tu)) * cn;
+    uint8_t px[8];
+    for (int k = 0; k < cn; ++k) {
+      const T v0 = k0 ? p[k] : T(0);
+      const T v1 = k1 ? p[cn + k] : T(0);
+      const T v2 = k2 ? p[(long)iw * cn + k] : T(0);
+      const T v3 = k3 ? p[((long)iw + 1) * cn + k] : T(0);
+      if constexpr (sizeof(T) == 1) {
+        const int s = (int)v0 * ((32 - ay) * (32 - ax) * 32) + (int)v1 * ((32 - ay) * ax * 32) +
+                      (int)v2 * (ay * (32 - ax) * 32) + (int)v3 * (ay * ax * 32);
+        const int r = (s + (1 << 14)) >> 15;
+        const T q = (T)(r < 0 ? 0 : (r > 255 ? 255 : r));
+        if constexpr (ILLUM) px[k] = q;
+        else o[k] = q;
+      } else {
+        const float wy0 = 1.f - (float)ay * (1.f / 32.f), wy1 = (float)ay * (1.f / 32.f);
+        const float wx0 = 1.f - (float)ax * (1.f / 32.f), wx1 = (float)ax * (1.f / 32.f);
+        const T w0 = (T)(wy0 * wx0), w1 = (T)(wy0 * wx1), w2 = (T)(wy1 * wx0), w3 = (T)(wy1 * wx1);
+        o[k] = v0 * w0 + v1 * w1 + v2 * w2 + v3 * w3;
+      }
+    }
+    if constexpr (ILLUM) illum_px(px[0], px[1], px[2], lut, sdiv, hdiv, reinterpret_cast<uint8_t*>(o));
   });
 }
 
@@ -439,13 +502,8 @@ extern "C" int vm_tps_sample(const vm_tps_map* map, const void* img, int ih, int
   return check_launch("tps_sample");
 }
 
-extern "C" int vm_warp_affine(const void* src, int ih, int iw, int cn, int dtype, const double* m, void* dst, int h,
-                              int w, void* stream) {
-  if (!src || !dst || !m || ih <= 0 || iw <= 0 || cn <= 0 || h <= 0 || w <= 0)
-    return fail(VM_EINVAL, "warp_affine: bad argument");
-  if (dtype == VM_U8 && cn > 8) return fail(VM_EUNSUPPORTED, "warp_affine: uint8 images with more than 8 channels");
-  if ((long)h * w >= (1L << 31)) return fail(VM_EUNSUPPORTED, "warp_affine: more than 2^31 pixels");
-  // warpAffine without WARP_INVERSE_MAP inverts the forward matrix in double (imgwarp.cpp)
+// warpAffine without WARP_INVERSE_MAP inverts the forward matrix in double (imgwarp.cpp)
+static Affine invert_affine(const double* m) {
   Affine a;
   for (int i = 0; i < 6; ++i) a.m[i] = m[i];
   double d = a.m[0] * a.m[4] - a.m[1] * a.m[3];
@@ -459,6 +517,52 @@ extern "C" int vm_warp_affine(const void* src, int ih, int iw, int cn, int dtype
   const double b2 = -a.m[3] * a.m[2] - a.m[4] * a.m[5];
   a.m[2] = b1;
   a.m[5] = b2;
+  return a;
+}
+
+extern "C" int vm_warp_image(const void* src, int ih, int iw, int cn, int dtype, int tu, int tv, const double* m,
+                             const uint8_t* lut, void* dst, int h, int w, void* stream) {
+  if (!src || !dst || !m || ih <= 0 || iw <= 0 || cn <= 0 || h <= 0 || w <= 0)
+    return fail(VM_EINVAL, "warp_image: bad argument");
+  if (dtype == VM_U8 && cn > 8) return fail(VM_EUNSUPPORTED, "warp_image: uint8 images with more than 8 channels");
+  if (lut && (dtype != VM_U8 || cn != 3)) return fail(VM_EINVAL, "warp_image: the illumination change needs u8 BGR");
+  if ((long)h * w >= (1L << 31) || (long)ih * iw >= (1L << 31))
+    return fail(VM_EUNSUPPORTED, "warp_image: more than 2^31 pixels");
+  const Affine a = invert_affine(m);
+  Lut256 l{};
+  if (lut)
+    for (int i = 0; i < 256; ++i) l.t[i] = lut[i];
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const dim3 g(grid_for((long)h * w, 256)), b(256);
+  switch (dtype) {
+    case VM_U8:
+      if (lut)
+        hipLaunchKernelGGL((warp_image_kernel<uint8_t, true>), g, b, 0, st, static_cast<const uint8_t*>(src), ih, iw,
+                           cn, tu, tv, a, l, static_cast<uint8_t*>(dst), h, w);
+      else
+        hipLaunchKernelGGL((warp_image_kernel<uint8_t, false>), g, b, 0, st, static_cast<const uint8_t*>(src), ih, iw,
+                           cn, tu, tv, a, l, static_cast<uint8_t*>(dst), h, w);
+      break;
+    case VM_F32:
+      hipLaunchKernelGGL((warp_image_kernel<float, false>), g, b, 0, st, static_cast<const float*>(src), ih, iw, cn,
+                         tu, tv, a, l, static_cast<float*>(dst), h, w);
+      break;
+    case VM_F64:
+      hipLaunchKernelGGL((warp_image_kernel<double, false>), g, b, 0, st, static_cast<const double*>(src), ih, iw, cn,
+                         tu, tv, a, l, static_cast<double*>(dst), h, w);
+      break;
+    default: return fail(VM_EUNSUPPORTED, "warp_image: dtype %d", dtype);
+  }
+  return check_launch("warp_image");
+}
+
+extern "C" int vm_warp_affine(const void* src, int ih, int iw, int cn, int dtype, const double* m, void* dst, int h,
+                              int w, void* stream) {
+  if (!src || !dst || !m || ih <= 0 || iw <= 0 || cn <= 0 || h <= 0 || w <= 0)
+    return fail(VM_EINVAL, "warp_affine: bad argument");
+  if (dtype == VM_U8 && cn > 8) return fail(VM_EUNSUPPORTED, "warp_affine: uint8 images with more than 8 channels");
+  if ((long)h * w >= (1L << 31)) return fail(VM_EUNSUPPORTED, "warp_affine: more than 2^31 pixels");
+  const Affine a = invert_affine(m);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const dim3 g(grid_for((long)h * w, 256)), b(256);
   switch (dtype) {

@@ -122,6 +122,8 @@ SIGNATURES = [
                               c_void_p]),
     ("vm_warp_affine", c_int, [c_void_p, c_int, c_int, c_int, c_int, ctypes.POINTER(ctypes.c_double), c_void_p,
                                c_int, c_int, c_void_p]),
+    ("vm_warp_image", c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, ctypes.POINTER(ctypes.c_double),
+                              ctypes.POINTER(ctypes.c_uint8), c_void_p, c_int, c_int, c_void_p]),
     ("vm_change_illumination_u8", c_int, [c_void_p, c_long, ctypes.POINTER(ctypes.c_uint8), c_void_p, c_void_p]),
     ("vm_nonzero_stats", c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
     ("vm_trimap_from_matte", c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),

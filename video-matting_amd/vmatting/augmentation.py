@@ -64,9 +64,8 @@ def _warp_image_dev(img, params, inv=None):
         img = inv.sample(img, 1)
         if img.shape[2] == 1:
             img = img[:, :, 0]
-    mt = np.float32([[1, 0, tu], [0, 1, tv]])
-    translated = ops.warp_affine(img, mt, (w, h))
-    return ops.warp_affine(translated, rotation_matrix(center, rot, scale), (w, h))
+    # cv2.warpAffine by [[1, 0, tu], [0, 1, tv]] then by getRotationMatrix2D(center, rot, scale), one fused pass
+    return ops.warp_image(img, tu, tv, rotation_matrix(center, rot, scale), (w, h))
 
 
 def warp_image(img, params, thin=None):
@@ -111,37 +110,110 @@ def change_illumination(bgr, a, b, c):
 def augment(fg, bg, alpha):
     """augmentation.augment (augmentation.py:101-135): camera motion on bg, TPS + similarity motion on fg and
     alpha, one illumination change for both.  Returns (new_fg u8, new_bg u8, new_alpha f64)."""
+    nfg, nbg, nal = augment_many([(fg, bg, alpha)])[0]
+    return _out(nfg, fg), _out(nbg, bg), _out(nal, alpha)
+
+
+def nonzero_stats_many(alphas):
+    """(count, row sum, column sum) of every alpha's nonzero pixels (object_size / fg_center) with ONE host sync:
+    one vm_nonzero_stats launch per alpha into one [n, 3] device buffer, read back once."""
+    st = torch.empty((len(alphas), 3), dtype=torch.int64, device=alphas[0].device)
+    for i, a in enumerate(alphas):
+        ops.nonzero_stats(a, out=st[i])
+    return [tuple(int(v) for v in row) for row in st.cpu().tolist()]
+
+
+class StatsPrefetch:
+    """nonzero_stats_many launched ahead on a side stream: it waits only for the work queued on the caller's stream
+    so far (e.g. the upload of the next batch's sources), not for what is queued after (the current training step),
+    and ``result()`` blocks only until those few launches are done."""
+
+    def __init__(self, alphas):
+        dev = alphas[0].device
+        cur = torch.cuda.current_stream(dev)
+        self.stream = torch.cuda.Stream(device=dev)
+        self.stream.wait_stream(cur)
+        with torch.cuda.stream(self.stream):
+            st = torch.empty((len(alphas), 3), dtype=torch.int64, device=dev)
+            for i, a in enumerate(alphas):
+                a.record_stream(self.stream)
+                ops.nonzero_stats(a, out=st[i])
+            self.host = torch.empty((len(alphas), 3), dtype=torch.int64, pin_memory=True)
+            self.host.copy_(st, non_blocking=True)
+            self.done = torch.cuda.Event()
+            self.done.record(self.stream)
+        self._st = st
+
+    def result(self):
+        self.done.synchronize()
+        return [tuple(int(v) for v in row) for row in self.host.tolist()]
+
+
+def _upload_f64(arrays, device):
+    """Small host float64 arrays -> device views, through ONE pinned buffer and one asynchronous copy (the caching
+    pinned allocator keeps the buffer until the copy has run)."""
+    flat = [np.ascontiguousarray(a, np.float64).ravel() for a in arrays]
+    host = torch.empty(sum(f.size for f in flat), dtype=torch.float64, pin_memory=True)
+    hn = host.numpy()
+    off, spans = 0, []
+    for f in flat:
+        hn[off:off + f.size] = f
+        spans.append((off, f.size))
+        off += f.size
+    dev = host.to(device, non_blocking=True)
+    return [dev[o:o + n].view(np.shape(a)) for (o, n), a in zip(spans, arrays)]
+
+
+def augment_many(triples, stats=None):
+    """augment() over several (fg, bg, alpha) samples as one device pipeline: the foreground statistics of every
+    sample with one readback (or ``stats`` already read, e.g. by a StatsPrefetch), then every sample's host draws in
+    augment's order (sample by sample, so a seeded global RandomState gives the per-call draws), the TPS solves, one
+    upload of all landmarks / coefficients, and per sample: the TPS lattice, fg / alpha TPS resampling, and the fused
+    translate + similarity warps with the illumination change (vm_warp_image).  No host sync after the statistics.
+    Returns [(new_fg u8, new_bg u8, new_alpha f64)] as device tensors."""
     bound_translate, bound_rotate, bound_scale = 0.05, 10, 0.15
-    dfg, dbg, dal = _device(fg), _device(bg), _device(alpha)
-    h, w = dfg.shape[:2]
-    cnt, sr, sc = _stats(dal)
-    fg_size = np.sqrt(cnt)
-    # camera motion (bg)
-    tu_bg = int(np.random.uniform(-w * bound_translate, w * bound_translate))
-    tv_bg = int(np.random.uniform(-h * bound_translate, h * bound_translate))
-    rot_bg = 0.
-    scale_bg = np.random.uniform(1., 1. + bound_scale)
-    new_bg = _warp_image_dev(dbg, ((tu_bg, tv_bg), rot_bg, scale_bg, (w // 2, h // 2)))
-    # object motion (fg): TPS deformation + similarity
-    grid, def_grid = deform_grid(h, w)
-    tu_fg = int(np.random.uniform(-fg_size * bound_translate, fg_size * bound_translate))
-    tv_fg = int(np.random.uniform(-fg_size * bound_translate, fg_size * bound_translate))
-    rot_fg = np.random.uniform(-bound_rotate, bound_rotate)
-    scale_fg = np.random.uniform(1., 1. + bound_scale)
-    if cnt == 0:
-        raise ValueError("cannot convert float NaN to integer")
-    params_fg = (tu_fg, tv_fg), rot_fg, scale_fg, (int(sc / cnt), int(sr / cnt))
-    # one TPS map serves fg and alpha (the reference evaluates the same map twice)
-    inv = tps.InverseWarp(grid, def_grid, (0, 0, h, w), 2, dfg.device)
-    new_fg = _warp_image_dev(dfg, params_fg, inv)
-    new_alpha = _warp_image_dev(dal, params_fg, inv)
-    a = np.random.uniform(1. - 0.05, 1. + 0.05)
-    b = np.random.uniform(1. - 0.3, 1. + 0.3)
-    c = np.random.uniform(-0.07, 0.07)
-    lut = illumination_lut(a, b, c)
-    new_fg = ops.change_illumination(new_fg, lut)
-    new_bg = ops.change_illumination(new_bg, lut)
-    return _out(new_fg, fg), _out(new_bg, bg), _out(new_alpha, alpha)
+    devs = [(_device(fg), _device(bg), _device(al)) for fg, bg, al in triples]
+    if stats is None:
+        stats = nonzero_stats_many([d[2] for d in devs])
+    plans, uploads = [], []
+    for (dfg, dbg, dal), (cnt, sr, sc) in zip(devs, stats):
+        h, w = dfg.shape[:2]
+        fg_size = np.sqrt(cnt)
+        # camera motion (bg)
+        tu_bg = int(np.random.uniform(-w * bound_translate, w * bound_translate))
+        tv_bg = int(np.random.uniform(-h * bound_translate, h * bound_translate))
+        scale_bg = np.random.uniform(1., 1. + bound_scale)
+        # object motion (fg): TPS deformation + similarity
+        grid, def_grid = deform_grid(h, w)
+        tu_fg = int(np.random.uniform(-fg_size * bound_translate, fg_size * bound_translate))
+        tv_fg = int(np.random.uniform(-fg_size * bound_translate, fg_size * bound_translate))
+        rot_fg = np.random.uniform(-bound_rotate, bound_rotate)
+        scale_fg = np.random.uniform(1., 1. + bound_scale)
+        if cnt == 0:
+            raise ValueError("cannot convert float NaN to integer")
+        center = (int(sc / cnt), int(sr / cnt))
+        a = np.random.uniform(1. - 0.05, 1. + 0.05)
+        b = np.random.uniform(1. - 0.3, 1. + 0.3)
+        c = np.random.uniform(-0.07, 0.07)
+        # one TPS map serves fg and alpha (the reference evaluates the same map twice): the reverse transform
+        # def_grid -> grid (tps.py:50-51), solved on the host like the reference
+        uploads += [def_grid, tps._coefficients(def_grid, grid)]
+        plans.append((h, w, grid, def_grid, (tu_bg, tv_bg, scale_bg), (tu_fg, tv_fg, rot_fg, scale_fg, center),
+                      illumination_lut(a, b, c)))
+    dev_arrays = _upload_f64(uploads, devs[0][0].device) if uploads else []
+    out = []
+    for k, ((dfg, dbg, dal), (h, w, grid, def_grid, pbg, pfg, lut)) in enumerate(zip(devs, plans)):
+        tu_bg, tv_bg, scale_bg = pbg
+        new_bg = ops.warp_image(dbg, tu_bg, tv_bg, rotation_matrix((w // 2, h // 2), 0., scale_bg), (w, h), lut)
+        inv = tps.InverseWarp(grid, def_grid, (0, 0, h, w), 2, dfg.device,
+                              solved=(dev_arrays[2 * k], dev_arrays[2 * k + 1]))
+        tu_fg, tv_fg, rot_fg, scale_fg, center = pfg
+        m = rotation_matrix(center, rot_fg, scale_fg)
+        new_fg = ops.warp_image(inv.sample(dfg, 1), tu_fg, tv_fg, m, (w, h), lut)
+        tal = inv.sample(dal, 1)
+        new_alpha = ops.warp_image(tal[:, :, 0] if tal.dim() == 3 else tal, tu_fg, tv_fg, m, (w, h))
+        out.append((new_fg, new_bg, new_alpha))
+    return out
 
 
 def bgra(fg, alpha):
@@ -158,6 +230,13 @@ def video_sample(fg, bg, alpha, flow):
     BGRA with its augmented background.  ``flow`` is the entry's .flo (the reference computes it offline with an
     optical-flow estimator between the two frames; any [h, w, 2] f32).  Returns the dict loader.compose_batch takes
     (fg, bg, prev, flow; add "plan" = loader.plan_crop(...)), all on the device."""
-    nfg, nbg, nal = augment(_device(fg), _device(bg), _device(alpha))
-    return {"fg": bgra(nfg, nal), "bg": nbg, "prev": bgra(_device(fg), _device(alpha)), "flow": _device(flow)}
+    return video_samples([(fg, bg, alpha)], flow)[0]
 
+
+def video_samples(sources, flow, stats=None):
+    """video_sample over several (fg, bg, alpha) sources as one augment_many pipeline (one statistics readback, or
+    none with ``stats`` from a StatsPrefetch)."""
+    aug = augment_many([(_device(fg), _device(bg), _device(al)) for fg, bg, al in sources], stats=stats)
+    d_flow = _device(flow)
+    return [{"fg": bgra(nfg, nal), "bg": nbg, "prev": bgra(_device(fg), _device(al)), "flow": d_flow}
+            for (nfg, nbg, nal), (fg, bg, al) in zip(aug, sources)]

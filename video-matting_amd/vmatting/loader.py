@@ -118,13 +118,47 @@ def _dev(a, dtype, device):
     return torch.from_numpy(np.ascontiguousarray(a)).to(device=device, dtype=dtype)
 
 
+class _PinnedDescRing:
+    """Pinned host memory for the per-batch sample descriptors vm_loader_compose copies to the device: a copy from
+    pageable memory would make hipMemcpyAsync wait for the stream (the previous training step); from pinned memory
+    it stays asynchronous.  A slot is reused only after the event recorded behind its copy has completed."""
+
+    def __init__(self, slots=4):
+        self.slots = [[None, None] for _ in range(slots)]
+        self.i = 0
+
+    def take(self, n):
+        slot = self.slots[self.i]
+        self.i = (self.i + 1) % len(self.slots)
+        buf, ev = slot
+        if ev is not None:
+            ev.synchronize()
+        nbytes = n * ctypes.sizeof(_lib.VmLoaderSample)
+        if buf is None or buf.numel() < nbytes:
+            buf = torch.empty(max(nbytes, 4096), dtype=torch.uint8, pin_memory=True)
+            slot[0] = buf
+        desc = (_lib.VmLoaderSample * n).from_address(buf.data_ptr())
+        ctypes.memset(buf.data_ptr(), 0, nbytes)
+        return desc, slot
+
+    @staticmethod
+    def issued(slot):
+        ev = torch.cuda.Event()
+        ev.record()
+        slot[1] = ev
+
+
+_DESC = _PinnedDescRing()
+
+
 def compose_batch(samples, input_size, outputs=("cmp", "bg", "label", "fg"), mirror=None, dtype=torch.float32,
-                  device="cuda"):
+                  device="cuda", out=None):
     """Run vm_loader_compose on decoded samples.
 
     samples: list of dicts with fg (u8 BGRA [h,w,4]), bg (u8 BGR), plan (from plan_crop) and, for
     video samples, prev (u8 BGRA) + flow (f32 [h,w,2]); numpy arrays or device tensors.
     outputs: names from cmp, bg, label, warped, fg and input (= cmp | bg, get_batch's layout).
+    out: optional {name: contiguous tensor} to write into (e.g. a captured training graph's static inputs).
     Returns {name: tensor [n, input_size[1], input_size[0], C]}."""
     if dtype not in (torch.float32, torch.float64):
         raise ValueError("loader outputs are float32 or float64")
@@ -135,7 +169,7 @@ def compose_batch(samples, input_size, outputs=("cmp", "bg", "label", "fg"), mir
         raise ValueError("'input' already holds cmp and bg (channels 0-2 / 3-5)")
     ow, oh = int(input_size[0]), int(input_size[1])
     keep = []
-    desc = (_lib.VmLoaderSample * n)()
+    desc, slot = _DESC.take(n)
     for i, s in enumerate(samples):
         fg = _dev(s["fg"], torch.uint8, device)
         bg = _dev(s["bg"], torch.uint8, device)
@@ -156,7 +190,13 @@ def compose_batch(samples, input_size, outputs=("cmp", "bg", "label", "fg"), mir
         d.fg_rows, d.fg_cols = _lib.VmCropAxis(*fr), _lib.VmCropAxis(*fc)
         d.bg_rows, d.bg_cols = _lib.VmCropAxis(*br), _lib.VmCropAxis(*bc)
         d.mirror = int(bool(mirror[i])) if mirror is not None else 0
-    res = {k: torch.empty((n, oh, ow, _OUT_CH[k]), dtype=dtype, device=device) for k in outputs}
+    res = {}
+    for k in outputs:
+        shape = (n, oh, ow, _OUT_CH[k])
+        t = None if out is None else out.get(k)
+        if t is not None and (tuple(t.shape) != shape or t.dtype != dtype or not t.is_contiguous()):
+            raise ValueError("compose_batch: out[%r] must be a contiguous %s tensor of shape %s" % (k, dtype, shape))
+        res[k] = t if t is not None else torch.empty(shape, dtype=dtype, device=device)
     o = _lib.VmLoaderOutputs()
     esz = 8 if dtype == torch.float64 else 4
     for k, t in res.items():
@@ -171,6 +211,7 @@ def compose_batch(samples, input_size, outputs=("cmp", "bg", "label", "fg"), mir
         _lib.check(lib.vm_loader_compose(desc, n, oh, ow, _lib.VM_F64 if dtype == torch.float64 else _lib.VM_F32,
                                          ctypes.byref(o), ctypes.c_void_p(work.data_ptr()), _lib.stream_handle()),
                    "loader_compose")
+        _DESC.issued(slot)
     return res
 
 

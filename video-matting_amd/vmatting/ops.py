@@ -726,6 +726,29 @@ def warp_affine(src, M, dsize, out=None):
     return out
 
 
+def warp_image(src, tu, tv, M, dsize, lut=None, out=None):
+    """vm_warp_image: augmentation.warp_image's translate + warpAffine pair (augmentation.py:59-63) in one pass,
+    optionally followed by change_illumination with the S/V map ``lut`` (u8 BGR)."""
+    _require_gpu(src)
+    src = src.contiguous()
+    two_d = src.dim() == 2
+    ih, iw = src.shape[:2]
+    cn = 1 if two_d else src.shape[2]
+    w, h = int(dsize[0]), int(dsize[1])
+    m = (ctypes.c_double * 6)(*[float(v) for v in np.asarray(M, np.float64).reshape(6)])
+    lp = None
+    if lut is not None:
+        lut = np.ascontiguousarray(lut, np.uint8)
+        if lut.shape != (256,):
+            raise ValueError("warp_image: lut must have 256 entries")
+        lp = lut.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))
+    if out is None:
+        out = torch.empty((h, w) if two_d else (h, w, cn), dtype=src.dtype, device=src.device)
+    check(lib().vm_warp_image(_ptr(src), ih, iw, cn, _dtype_code(src, "warp_image"), int(tu), int(tv), m, lp,
+                              _ptr(out), h, w, stream_handle()), "warp_image")
+    return out
+
+
 def change_illumination(bgr, lut, out=None):
     """vm_change_illumination_u8: BGR u8 -> HSV -> (h, lut[s], lut[v]) -> BGR u8."""
     _require_gpu(bgr)

@@ -66,7 +66,9 @@ class InverseWarp:
     approximate grid ([2, nx, ny] f64), plus the upsampling parameters of tps.py:55-74 (None when
     approximate_grid == 1)."""
 
-    def __init__(self, from_points, to_points, output_region, approximate_grid, device="cuda"):
+    def __init__(self, from_points, to_points, output_region, approximate_grid, device="cuda", solved=None):
+        """solved: (to_points, coefficients) already on the device (augmentation.augment_many uploads every
+        sample's in one copy); else they are solved here and uploaded."""
         x_min, y_min, x_max, y_max = output_region
         if approximate_grid is None:
             approximate_grid = 1
@@ -74,10 +76,13 @@ class InverseWarp:
         y_steps = (y_max - y_min) / approximate_grid
         nx, xstep = _mgrid_axis(x_min, x_max, x_steps)
         ny, ystep = _mgrid_axis(y_min, y_max, y_steps)
-        # the reverse transform (to -> from), because images are resampled backwards (tps.py:50-51)
-        coeffs = _coefficients(to_points, from_points)
-        pts = torch.from_numpy(np.ascontiguousarray(np.asarray(to_points, np.float64))).to(device)
-        co = torch.from_numpy(np.ascontiguousarray(coeffs, np.float64)).to(device)
+        if solved is None:
+            # the reverse transform (to -> from), because images are resampled backwards (tps.py:50-51)
+            coeffs = _coefficients(to_points, from_points)
+            pts = torch.from_numpy(np.ascontiguousarray(np.asarray(to_points, np.float64))).to(device)
+            co = torch.from_numpy(np.ascontiguousarray(coeffs, np.float64)).to(device)
+        else:
+            pts, co = solved
         self.grid = ops.tps_grid(pts, co, nx, ny, x_min, xstep, y_min, ystep)
         self.upsample = None if approximate_grid == 1 else (x_steps, x_max - x_min, y_steps, y_max - y_min)
         self.shape = (nx, ny) if self.upsample is None else (x_max - x_min + 1, y_max - y_min + 1)
