@@ -155,6 +155,12 @@ int vm_conv3x3_pool_nhwc(const vm_tensor* x, const void* packed, int cin, int co
 int vm_conv3x3_head_nhwc(const vm_tensor* x, const void* packed, int cin, const float* bias, const float* scale,
                          const float* shift, int act, vm_tensor* y, float* alpha, void* stream);
 
+/* The same cout == 1 head over one channel chunk of its input, adding y_acc (f32, contiguous [n*h*w], e.g. the
+ * previous chunk's y) to the pre-activation: a head over more channels than one MFMA head tile holds, chunk by chunk
+ * (the split-bf16 x6 path's conv1_5 over 6 x 128 channels, unet.py:203-205).  cin <= 256 (bf16). */
+int vm_conv3x3_head_acc_nhwc(const vm_tensor* x, const void* packed, int cin, const float* bias, const float* y_acc,
+                             vm_tensor* y, float* alpha, void* stream);
+
 /* Two chained convs whose 64-channel intermediate never leaves the chip: y = act2(conv3x3(relu(conv3x3(x, w1) + bias1),
  * w2) + bias2 ...), optionally with the fused 2x2 SAME max-pool of y into ypool (NULL = none) — replaces
  * unet.py:170-172 (conv1_1 -> conv1_2 -> pool1; conv_layer at :65-74) and the VGG towers' first pair

@@ -22,3 +22,4 @@ import sys; sys.argv=['bench.py']; import bench, torch, json
 dev=torch.device('cuda',0); torch.cuda.set_device(dev)
 print(json.dumps(bench.augment_bench(dev, 20, 16, cpu=False)))
 "
+guard 300 r5d_tlayers.log python -u tools/train_layers.py --steps 3

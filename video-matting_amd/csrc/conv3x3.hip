@@ -3207,6 +3207,7 @@ struct HeadArgs {
   int y_cstride, y_coff, y_dtype;
   float* y2;  // optional: sigmoid of the pre-activation value, f32 [M] (unet.py:204-205 output beside conv1_3)
   const float* part;  // optional: per-tap partials [M][12] of the channels x does not carry (the pair kernel's hd)
+  const float* yacc;  // optional: f32 [M] added to the pre-activation (a head over channel chunks, split-bf16 x6)
 };
 
 template <typename T>
@@ -3507,6 +3508,7 @@ __global__ __launch_bounds__(256) void conv3x3_head_mfma(HeadArgs a) {
     float sum = 0.f;
 #pragma unroll
     for (int t = 0; t < 9; ++t) sum += ys[((orow + t / 3) * IW + ocol + t % 3) * 9 + t];
+    if (a.yacc) sum += a.yacc[((long)n * H + h) * W + w];
     float v = (sum + bias) * sc + sh;
     if (a.y2) a.y2[((long)n * H + h) * W + w] = sigmoid_precise(v);
     if (a.act == VM_ACT_RELU) v = v > 0.f ? v : 0.f;
@@ -5212,7 +5214,7 @@ extern "C" int vm_conv3x3_pack_weights_batch(int njobs, const vm_pack_job* jobs,
 static int conv_impl(const vm_tensor* x, const void* packed, int cin, int cout, const float* bias, const float* scale,
                      const float* shift, int act, vm_tensor* y, const vm_tensor* yp, void* stream,
                      float* y2 = nullptr, int nsrc = 0, long src_stride = 0, void* work = nullptr,
-                     size_t work_bytes = 0, const float* head_part = nullptr);
+                     size_t work_bytes = 0, const float* head_part = nullptr, const float* y_acc = nullptr);
 
 extern "C" int vm_conv3x3_nhwc(const vm_tensor* x, const void* packed, int cin, int cout, const float* bias,
                                const float* scale, const float* shift, int act, vm_tensor* y, void* stream) {
@@ -5395,6 +5397,13 @@ extern "C" int vm_conv3x3_pair_first_head_nhwc(const vm_tensor* x, const void* p
                          head_cin, head_coff, partial, store_y, stream);
 }
 
+extern "C" int vm_conv3x3_head_acc_nhwc(const vm_tensor* x, const void* packed, int cin, const float* bias,
+                                        const float* y_acc, vm_tensor* y, float* alpha, void* stream) {
+  if (!y_acc) return fail(VM_EINVAL, "conv3x3_head_acc: y_acc is NULL");
+  return conv_impl(x, packed, cin, 1, bias, nullptr, nullptr, VM_ACT_NONE, y, nullptr, stream, alpha, 0, 0, nullptr, 0,
+                   nullptr, y_acc);
+}
+
 extern "C" int vm_conv3x3_head_partial_nhwc(const vm_tensor* x, const void* packed, int cin, const float* bias,
                                             const float* scale, const float* shift, int act, vm_tensor* y,
                                             float* alpha, const float* partial, void* stream) {
@@ -5480,8 +5489,9 @@ extern "C" int vm_conv3x3_head_nhwc(const vm_tensor* x, const void* packed, int 
 
 static int conv_impl(const vm_tensor* x, const void* packed, int cin, int cout, const float* bias, const float* scale,
                      const float* shift, int act, vm_tensor* y, const vm_tensor* yp, void* stream, float* y2, int nsrc,
-                     long src_stride, void* work, size_t work_bytes, const float* head_part) {
+                     long src_stride, void* work, size_t work_bytes, const float* head_part, const float* y_acc) {
   if (!valid_tensor(x) || !valid_tensor(y) || !packed) return fail(VM_EINVAL, "conv3x3: invalid tensor/weights");
+  if (y_acc && cout != 1) return fail(VM_EINVAL, "conv3x3: an accumulated pre-activation needs cout == 1");
   if (head_part && cout != 1) return fail(VM_EINVAL, "conv3x3: head partials need cout == 1");
   const int xc = nsrc > 1 ? nsrc * x->c : x->c;  // sources: x is the view of source 0
   if (cin <= 0 || cout <= 0 || xc != cin || y->c != cout)
@@ -5511,8 +5521,9 @@ static int conv_impl(const vm_tensor* x, const void* packed, int cin, int cout, 
     h.w = packed; h.bias = bias; h.scale = scale; h.shift = shift; h.act = act;
     h.y = y->ptr; h.y_cstride = y->cstride; h.y_coff = y->coff; h.y_dtype = y->dtype; h.y2 = y2;
     h.part = head_part;
-    if (head_part && (g_head_kernel != 0 || (g.cin_pad + 4 * ce - 1) / (4 * ce) > 8))
-      return fail(VM_EUNSUPPORTED, "conv3x3 head: partials need the MFMA head kernel");
+    h.yacc = y_acc;
+    if ((head_part || y_acc) && (g_head_kernel != 0 || (g.cin_pad + 4 * ce - 1) / (4 * ce) > 8))
+      return fail(VM_EUNSUPPORTED, "conv3x3 head: partials / accumulation need the MFMA head kernel (cin <= 256)");
     const int nks = (g.cin_pad + 4 * ce - 1) / (4 * ce);
     if (g_head_kernel == 0 && nks <= 8) {
       constexpr int TW = 64;

@@ -78,6 +78,7 @@ SIGNATURES = [
                                      c_void_p]),
     ("vm_conv3x3_head_nhwc", c_int, [P, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, P, c_void_p,
                                      c_void_p]),
+    ("vm_conv3x3_head_acc_nhwc", c_int, [P, c_void_p, c_int, c_void_p, c_void_p, P, c_void_p, c_void_p]),
     ("vm_conv3x3_pair_first_nhwc", c_int, [P, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p,
                                            c_void_p, c_int, P, P, c_void_p]),
     ("vm_conv3x3_pair_first_mid_nhwc", c_int, [P, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p,

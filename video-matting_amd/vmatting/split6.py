@@ -29,7 +29,7 @@ from . import ops
 W_PARTS = (0, 1, 2, 0, 1, 0)  # index into (wh, wm, wl)
 
 # (conv scope, input channels of its split input (the concat width), output channels)
-LAYERS = (("conv1_1", 8, 64), ("conv1_2", 64, 64), ("conv2_1", 64, 128), ("conv2_2", 128, 128),
+LAYERS = (("conv1_1", 16, 64), ("conv1_2", 64, 64), ("conv2_1", 64, 128), ("conv2_2", 128, 128),
           ("conv3_1", 128, 256), ("conv3_2", 256, 256), ("conv3_3", 256, 256), ("conv4_1", 256, 512),
           ("conv4_2", 512, 512), ("conv4_3", 512, 512), ("conv5_1", 512, 512), ("conv5_2", 512, 512),
           ("upconv_1", 512, 512), ("conv4_4", 1024, 512), ("upconv_2", 512, 256), ("conv3_4", 512, 256),
@@ -92,21 +92,25 @@ class Split6Forward:
         for name, cin, cout in LAYERS:
             w, b = model.params[name]
             if name == "conv1_1":
-                cin = 8
-            bias = b
+                cin = 16  # 6 slabs of 16 (8 live): 96 channels, whole 32-channel granules for the patch kernel
             if name == "conv1_5":
-                bias = np.zeros(8, np.float32)
-                bias[0] = b[0]
-            pc = ops.PackedConv(split6_filter(w, cin, cout), bias, "bf16", self.dev)
+                # the cout-1 head over 6 x 128 channels as three 256-channel MFMA-head chunks [l m | h m | h h],
+                # the smallest first, each adding the previous chunk's logits (vm_conv3x3_head_acc_nhwc)
+                wf = split6_filter(w, cin, 1)
+                self.head = [ops.PackedConv(wf[:, :, 256 * k:256 * (k + 1)].contiguous(), b if k == 0 else None,
+                                            "bf16", self.dev) for k in range(3)]
+                self.convs[name] = self.head[0]
+                continue
+            pc = ops.PackedConv(split6_filter(w, cin, cout), b, "bf16", self.dev)
             self.convs[name] = pc
         self._b, self._key = None, None
 
     def weights_flat(self):
         out = []
-        for k in sorted(self.convs):
-            out.append(self.convs[k].packed)
-            if self.convs[k].bias is not None:
-                out.append(self.convs[k].bias)
+        for pc in [self.convs[k] for k in sorted(self.convs) if k != "conv1_5"] + self.head:
+            out.append(pc.packed)
+            if pc.bias is not None:
+                out.append(pc.bias)
         return out
 
     def _buffers(self, n, h, w):
@@ -117,14 +121,15 @@ class Split6Forward:
         dev = self.dev
         S = lambda lv, c: torch.empty((n, L[lv][0], L[lv][1], 6 * c), dtype=torch.bfloat16, device=dev)  # noqa
         F = lambda lv, c: torch.empty((n, L[lv][0], L[lv][1], c), dtype=torch.float32, device=dev)  # noqa
-        b = {"x": S(0, 8), "s11": S(0, 64), "cat1": S(0, 128), "r4": S(0, 128),
+        b = {"x": torch.zeros((n, L[0][0], L[0][1], 6 * 16), dtype=torch.bfloat16, device=dev), "s11": S(0, 64), "cat1": S(0, 128), "r4": S(0, 128),
              "p1": S(1, 64), "s21": S(1, 128), "cat2": S(1, 256), "r3": S(1, 256),
              "p2": S(2, 128), "s31": S(2, 256), "s32": S(2, 256), "cat3": S(2, 512), "r2": S(2, 512),
              "p3": S(3, 256), "s41": S(3, 512), "s42": S(3, 512), "cat4": S(3, 1024), "r1": S(3, 512),
              "p4": S(4, 512), "s51": S(4, 512),
              "f0": F(0, 128), "f1": F(1, 256), "f2": F(2, 512), "f3": F(3, 512), "f4": F(4, 512),
              "rr0": F(0, 128), "rr1": F(1, 256), "rr2": F(2, 512), "rr3": F(3, 512),
-             "h8": F(0, 8), "out": F(0, 1)}
+             "lg": [F(0, 1) for _ in range(3)], "zero": torch.zeros((n, L[0][0], L[0][1], 1), device=dev),
+             "out": F(0, 1)}
         self._b, self._key = b, (n, h, w)
         return b
 
@@ -135,7 +140,7 @@ class Split6Forward:
         b = self._buffers(n, h, w)
         L = _levels(h, w)
         C = self.convs
-        split6(x, b["x"][..., :8])
+        split6(x, b["x"][..., :8])  # 6 slabs of 16 channels, 8 written (the rest stay zero)
 
         def conv(src, name, dst_f32, act="relu"):
             return ops.conv3x3(src, C[name], act, out=dst_f32, affine=False, splitk=True)
@@ -170,9 +175,16 @@ class Split6Forward:
         y23 = conv(b["cat2"], "conv2_3", f1[..., :128])
         resize_split(y23, 0, b["rr0"], whole(b["r4"]))
         split6(conv(b["r4"], "upconv_4", f0[..., :64], act="none"), seg(b["cat1"], 0, 64))
-        # conv1_5 + sigmoid (unet.py:203-205): 8 padded output channels, logits in channel 0
-        conv(b["cat1"], "conv1_5", b["h8"], act="none")
+        # conv1_5 + sigmoid (unet.py:203-205): three 256-channel chunks of the split cat1, logits accumulated,
+        # the sigmoid from the last
         alpha = b["out"] if out is None else out
-        ops.convert(b["h8"][..., :1], alpha, act="sigmoid")
-        self.logits = b["h8"][..., :1]
+        lg = b["lg"]
+        for k in range(3):
+            xv, yv = ops.nhwc(b["cat1"][..., 256 * k:256 * (k + 1)]), ops.nhwc(lg[k])
+            pc = self.head[k]
+            ops.check(ops.lib().vm_conv3x3_head_acc_nhwc(
+                ops.ctypes.byref(xv), ops._ptr(pc.packed), 256, ops._ptr(pc.bias),
+                ops._ptr(lg[k - 1] if k else b["zero"]), ops.ctypes.byref(yv),
+                ops._ptr(alpha if k == 2 else None), ops.stream_handle()), "conv3x3_head_acc")
+        self.logits = lg[2]
         return alpha
