@@ -14,7 +14,7 @@ guard() {  # guard <limit> <logfile> cmd...
   fi
 }
 PT="python -u -m pytest -v --timeout 300 --timeout-method thread -rf"
-guard 600 r5d_tests.log $PT tests/test_gpu_augment.py tests/test_gpu_loader.py tests/test_gpu_train.py -m gpu -k "augment or warp or loader or compose or config5 or tps or illumination or statistics"
+guard 600 r5d_tests.log $PT tests/test_gpu_augment.py tests/test_gpu_loader.py tests/test_gpu_train.py tests/test_gpu_split6.py -m gpu -k "augment or warp or loader or compose or config5 or tps or illumination or statistics or split6 or bf16x6"
 guard 300 r5d_chain.log python -u bench.py --only train_chain --steps 10 --warmup 3
 guard 300 r5d_timage.log python -u bench.py --only train_image --steps 10 --warmup 3
 guard 300 r5d_aug.log python -u -c "
@@ -23,3 +23,4 @@ dev=torch.device('cuda',0); torch.cuda.set_device(dev)
 print(json.dumps(bench.augment_bench(dev, 20, 16, cpu=False)))
 "
 guard 300 r5d_tlayers.log python -u tools/train_layers.py --steps 3
+guard 300 r5d_x6bench.log python -u tools/x6bench.py 10

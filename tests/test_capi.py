@@ -89,6 +89,7 @@ def test_raw_stream_falls_back_to_public_getter(monkeypatch):
 
 
 @pytest.mark.gpu
+@pytest.mark.skipif(not __import__("conftest").gpu_available(), reason="needs a ROCm GPU")
 def test_raw_stream_matches_public_getter():
     """The private getters return torch.cuda.current_stream().cuda_stream, outside and inside a stream context."""
     import torch
