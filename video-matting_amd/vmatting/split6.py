@@ -128,7 +128,7 @@ class Split6Forward:
              "p4": S(4, 512), "s51": S(4, 512),
              "f0": F(0, 128), "f1": F(1, 256), "f2": F(2, 512), "f3": F(3, 512), "f4": F(4, 512),
              "rr0": F(0, 128), "rr1": F(1, 256), "rr2": F(2, 512), "rr3": F(3, 512),
-             "lg": [F(0, 1) for _ in range(3)], "zero": torch.zeros((n, L[0][0], L[0][1], 1), device=dev),
+             "lg0": F(0, 1), "lg1": F(0, 1), "lg2": F(0, 1), "zero": torch.zeros((n, L[0][0], L[0][1], 1), device=dev),
              "out": F(0, 1)}
         self._b, self._key = b, (n, h, w)
         return b
@@ -178,7 +178,7 @@ class Split6Forward:
         # conv1_5 + sigmoid (unet.py:203-205): three 256-channel chunks of the split cat1, logits accumulated,
         # the sigmoid from the last
         alpha = b["out"] if out is None else out
-        lg = b["lg"]
+        lg = [b["lg0"], b["lg1"], b["lg2"]]
         for k in range(3):
             xv, yv = ops.nhwc(b["cat1"][..., 256 * k:256 * (k + 1)]), ops.nhwc(lg[k])
             pc = self.head[k]
