@@ -457,6 +457,16 @@ int vm_relu_backward_split_nhwc(const vm_tensor* dy, const vm_tensor* y, int spl
 int vm_maxpool2x2_backward_nhwc(const vm_tensor* x, const vm_tensor* dy, const vm_tensor* add, vm_tensor* dx,
                                 void* stream);
 
+/* The front end of a relu conv's backward (train.py training_procedure through unet.py's y = relu(conv(x) + b),
+ * :35-42,65-74): dz = (y > 0) * g written as dz (e.g. the bf16 copy the filter / data-gradient convs read) and the
+ * bias gradient dbias[c] = sum_p dz (f64 partials, fixed-order fold) from one pass.  g = dy (+ add) when dy is y's
+ * shape; when dy is the 2x2 SAME pool's shape, g = add (optional) + tf.nn.max_pool's adjoint of dy (the window's
+ * first maximum of y in row-major order, TF MaxPoolGrad) — the skip half of an [up, skip] concat (unet.py:62) and its
+ * pool in one pass.  dy / add f32; y any dtype; work = vm_relu_backward_bias_workspace_bytes(c). */
+size_t vm_relu_backward_bias_workspace_bytes(int channels);
+int vm_relu_backward_bias_nhwc(const vm_tensor* dy, const vm_tensor* y, const vm_tensor* add, vm_tensor* dz,
+                               float* dbias, void* work, void* stream);
+
 /* Adjoint of vm_resize_bilinear_tf1_nhwc (tf.image.resize_images, unet_simple.py:33): dy [n,oh,ow,c] (f32 view) ->
  * dx contiguous f32 [n,ih,iw,c] (overwritten). */
 int vm_resize_bilinear_tf1_backward(const vm_tensor* dy, float* dx, int ih, int iw, void* stream);

@@ -14,5 +14,5 @@ guard() {  # guard <limit> <logfile> cmd...
   fi
 }
 PT="python -u -m pytest -v --timeout 300 --timeout-method thread -rf -s"
-guard 600 r5c_tests.log $PT tests/test_gpu_train.py tests/test_gpu_image_train.py tests/test_gpu_split6.py -m gpu -k "nested_fork or high_priority or graph_step or fp32_matches or split6 or bf16x6"
+guard 600 r5c_tests.log $PT tests/test_gpu_train.py tests/test_gpu_image_train.py tests/test_gpu_split6.py -m gpu -k "nested_fork"
 guard 300 r5c_x6bench.log python -u tools/x6bench.py 10

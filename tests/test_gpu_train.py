@@ -925,3 +925,45 @@ def test_train_step_bf16_gradients_bench_shape():
     print("bf16 step 8x320^2: gradient cosine %.5f\n  %s" % (cos, "\n  ".join(rows)))
     assert not bad, bad
     assert cos >= 0.99
+
+
+@pytest.mark.parametrize("pool", [False, True])
+@pytest.mark.parametrize("c,ydt,dzdt", [(64, "bf16", "bf16"), (512, "bf16", "bf16"), (24, "f32", "f32")])
+def test_relu_backward_bias(pool, c, ydt, dzdt):
+    """vm_relu_backward_bias_nhwc (the UNetImage backward's per-conv front end): dz = (y > 0) * (dy (+ add)) or, with a
+    pooled dy, (y > 0) * (add + maxpool adjoint of dy) with TF MaxPoolGrad's first-maximum rule (ties included, odd
+    edges), written in dz's dtype, and the bias gradient = channel sums of dz (float64 partials)."""
+    from vmatting import ops
+    rs = np.random.RandomState(c + pool)
+    n, h, w = 2, 9, 13
+    y = np.maximum(rs.normal(size=(n, h, w, c)), 0).astype(np.float32)
+    y[:, ::3, ::2] = np.round(y[:, ::3, ::2])  # exact ties inside windows
+    if ydt == "bf16":
+        y = torch.from_numpy(y).bfloat16().float().numpy()
+    ph, pw = (h + 1) // 2, (w + 1) // 2
+    dy = rs.normal(size=(n, ph, pw, c) if pool else (n, h, w, c)).astype(np.float32)
+    add = rs.normal(size=(n, h, w, c)).astype(np.float32)
+    tdt = {"bf16": torch.bfloat16, "f32": torch.float32}
+    yd = T(y, tdt[ydt])
+    dz = torch.zeros((n, h, w, c), dtype=tdt[dzdt], device=DEV)
+    db = torch.zeros(c, device=DEV)
+    ops.relu_backward_bias(T(dy), yd, dz, db, add=T(add))
+    g = add.astype(np.float64).copy()
+    if pool:
+        for b_ in range(n):
+            for i in range(ph):
+                for j in range(pw):
+                    win = [(2 * i + a, 2 * j + bb) for a in (0, 1) for bb in (0, 1) if 2 * i + a < h and 2 * j + bb < w]
+                    for ch in range(c):
+                        vals = [y[b_, r, q, ch] for r, q in win]
+                        k = int(np.argmax(vals))  # first maximum
+                        g[b_, win[k][0], win[k][1], ch] += dy[b_, i, j, ch]
+    else:
+        g += dy
+    ref = np.where(y > 0, g, 0.0)
+    got = H(dz)
+    if dzdt == "bf16":
+        assert np.array_equal(got, torch.from_numpy(ref.astype(np.float32)).bfloat16().double().numpy())
+    else:
+        assert np.abs(got - ref).max() <= 1e-6 * np.abs(ref).max()
+    assert np.abs(H(db) - ref.astype(np.float32).astype(np.float64).sum((0, 1, 2))).max() <= 1e-5 * np.abs(ref).sum() / c

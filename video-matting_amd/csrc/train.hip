@@ -346,6 +346,84 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(V x, V dy, V add, V dx
   }
 }
 
+// ---------------------------------------------------------------- relu conv backward front end (UNetImage training)
+// For y = relu(conv(x) + b) (unet.py:35-42,65-74), one pass from the incoming gradient to what the conv's filter /
+// data gradients read: dz = (y > 0) * g, written ONLY as the bf16 copy those MFMA convs read (no f32 dz), with the
+// bias gradient sum_p dz from the same pass (f64 partials per block, folded in fixed order: deterministic).
+//   plain: g = dy (+ add)                                 dy, add, y, dz all [n,h,w,c]
+//   POOL : g = add + the 2x2 SAME max-pool adjoint of dy   dy [n,ceil(h/2),ceil(w/2),c], y / add / dz [n,h,w,c]
+//          (tf.nn.max_pool's gradient to the window's first maximum of y in row-major order, TF MaxPoolGrad; the
+//          skip half of an [up, skip] concat carries `add`, unet.py:62, so pool adjoint + concat gradient + relu
+//          mask + bias sum are one pass instead of three)
+// One lane per channel (CP lanes per pixel / window), a block's 4 waves stride over pixels (windows).
+template <bool POOL, int CP>
+__global__ __launch_bounds__(256) void relu_bwd_bias_kernel(V dy, V y, V add, V dz, double* part, int nblk) {
+  constexpr int PPW = 64 / CP;
+  __shared__ double sh[4][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c = blockIdx.x * CP + (lane % CP);
+  double s = 0.0;
+  if (c < y.c) {
+    const long units = POOL ? (long)dy.n * dy.h * dy.w : (long)y.n * y.h * y.w;
+    const long stp = (long)nblk * 4 * PPW;
+    for (long u = ((long)blockIdx.y * 4 + wave) * PPW + lane / CP; u < units; u += stp) {
+      if constexpr (!POOL) {
+        float g = ld(dy, u, c);
+        if (add.p) g += ld(add, u, c);
+        const float z = ld(y, u, c) > 0.f ? g : 0.f;
+        st(dz, u, c, z);
+        s += (double)z;
+      } else {
+        const long hw = (long)dy.h * dy.w;
+        const int n = (int)(u / hw);
+        const int r = (int)(u - (long)n * hw);
+        const int oy = r / dy.w, ox = r - oy * dy.w;
+        const long base = (long)n * y.h * y.w;
+        const float gp = ld(dy, u, c);
+        float yv[4];
+        long pix[4];
+        bool in[4];
+        float best = 0.f;
+        int win = -1;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int yy = 2 * oy + (k >> 1), xx = 2 * ox + (k & 1);
+          in[k] = yy < y.h && xx < y.w;
+          pix[k] = base + (long)yy * y.w + xx;
+          yv[k] = in[k] ? ld(y, pix[k], c) : 0.f;
+          if (in[k] && (win < 0 || yv[k] > best)) {
+            best = yv[k];
+            win = k;
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          if (!in[k]) continue;
+          float g = k == win ? gp : 0.f;
+          if (add.p) g += ld(add, pix[k], c);
+          const float z = yv[k] > 0.f ? g : 0.f;
+          st(dz, pix[k], c, z);
+          s += (double)z;
+        }
+      }
+    }
+  }
+  sh[wave][lane] = s;
+  __syncthreads();
+  if ((int)threadIdx.x < CP && c < y.c) {
+    s = 0.0;
+    for (int w = 0; w < 4; ++w)
+      for (int k = 0; k < PPW; ++k) s += sh[w][k * CP + threadIdx.x];
+    part[(long)c * nblk + blockIdx.y] = s;  // channel-major [C][nblk] (vm_common.h fold_columns)
+  }
+}
+
+__global__ __launch_bounds__(256) void fold_sum_kernel(const double* part, int nblk, int C, float* out) {
+  double r[3];
+  fold_columns(part, nblk, C, blockIdx.x, 1, r);
+  if (threadIdx.x == 0) out[blockIdx.x] = (float)r[0];
+}
+
 // ---------------------------------------------------------------- resize backward (adjoint of resize_tf1)
 __device__ __forceinline__ void tf1c(int i, float scale, int in, int& lo, int& hi, float& lerp) {
 #pragma clang fp contract(off)
@@ -1106,10 +1184,11 @@ constexpr int wgrad_taps_lds() {
 // output channels, f32 accumulation), both operands read k-major from their natural NHWC LDS images with
 // ds_read_b64_tr_b16 (wm_frag), like wgrad_mfma_kernel.  The narrow kernel above runs every output channel in one
 // block and splits its K-steps over the waves (cout <= 48); here a block owns a 64 x 64 (ci x co) tile of all 9
-// taps and the 4 waves split the OUTPUT: wave (wi, wj) holds ci 32wi..+31 x co 32wj..+31 x 9 taps (144 f32
-// accumulators) and walks every pixel row of the tile, so no cross-wave reduction is needed.  Per 32-pixel row a
-// wave reads 2 DY fragments (reused by 9 taps x 2 ci pieces) and 18 X fragments (each reused by 2 co pieces):
-// 20 fragment reads per 36 MFMAs.
+// taps and the 4 waves split the OUTPUT: wave w holds ci 16w..16w+15 x all 64 co x 9 taps (144 f32 accumulators)
+// and walks every pixel row of the tile, so no cross-wave reduction is needed.  Per 32-pixel row a wave reads 4 DY
+// fragments (reused by the 9 taps) and 9 X fragments (each reused by the 4 co pieces): 13 fragment reads per 36
+// MFMAs, i.e. ~370 B of LDS reads per MFMA — inside the CU's LDS bandwidth at the matrix pipes' rate (a 32 x 32
+// split read 20 fragments per 36 MFMAs, ~570 B, above it).
 // Grid: gx K-split blocks (contiguous tile ranges, one partial filter gradient each, summed in fixed order by
 // wgrad_reduce_kernel: deterministic) x the 64-channel blocks of cin and cout, as ONE dimension whose order is
 // XCD-aware: the blocks that share a pixel range (every channel block of it) are dispatched to the same XCD, so
@@ -1131,7 +1210,7 @@ constexpr int WW_TH = 4;
 constexpr int WW_TARGET_BLOCKS = 512;  // ~2 resident blocks per CU: one round; the partials stay <= 75 MB
 
 template <int TH, bool DYF32>
-__global__ __launch_bounds__(256, 2) void wgrad_wide_kernel(WwArgs a) {
+__global__ __launch_bounds__(256, 1) void wgrad_wide_kernel(WwArgs a) {
   constexpr int XPIX = wm_ppix<TH>(), DPIX = TH * WM_TW;
   constexpr int XBYTES = wm_prows<TH>() * 128;
   constexpr int NXC = XPIX * 8, NDC = DPIX * 8;                 // 16-byte chunks (8 channels) of each image
@@ -1140,8 +1219,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_wide_kernel(WwArgs a) {
   char* ximg = smem;
   char* dimg = smem + XBYTES;
   const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wi = wave & 1, wj = wave >> 1;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // = the 16-channel piece of ci this wave owns
   const int nb = gridDim.x, lin = blockIdx.x;
   // consecutive work ids on one XCD (workgroups are dealt to the 8 XCDs round-robin)
   const int wid = (nb % 8 == 0) ? (lin % 8) * (nb / 8) + lin / 8 : lin;
@@ -1149,13 +1227,11 @@ __global__ __launch_bounds__(256, 2) void wgrad_wide_kernel(WwArgs a) {
   const int kx = wid / nch, cb = wid - kx * nch;
   const int c0 = (cb % a.ncin) * 64, o0 = (cb / a.ncin) * 64;
 
-  f32x4 acc[9][2][2];
+  f32x4 acc[9][4];
 #pragma unroll
   for (int t = 0; t < 9; ++t)
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int o = 0; o < 2; ++o) acc[t][i][o] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int o = 0; o < 4; ++o) acc[t][o] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   uint4 xb[XPT];
   uint4 db[DPT];
@@ -1244,19 +1320,15 @@ __global__ __launch_bounds__(256, 2) void wgrad_wide_kernel(WwArgs a) {
     if (tile + 1 < t_end) issue(tile + 1);
 #pragma unroll 1
     for (int row = 0; row < TH; ++row) {
-      bf16x8 bd[2];
+      bf16x8 bd[4];
 #pragma unroll
-      for (int o = 0; o < 2; ++o) bd[o] = wm_frag<128>(dimg, row * WM_TW + 8 * g, 2 * wj + o, lane);
+      for (int o = 0; o < 4; ++o) bd[o] = wm_frag<128>(dimg, row * WM_TW + 8 * g, o, lane);
 #pragma unroll
       for (int t = 0; t < 9; ++t) {
         const int r0 = (row + t / 3) * WM_PW + t % 3 + 8 * g;
+        const bf16x8 ax = wm_frag<128>(ximg, r0, wave, lane);
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          const bf16x8 ax = wm_frag<128>(ximg, r0, 2 * wi + i, lane);
-#pragma unroll
-          for (int o = 0; o < 2; ++o)
-            acc[t][i][o] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ax, bd[o], acc[t][i][o], 0, 0, 0);
-        }
+        for (int o = 0; o < 4; ++o) acc[t][o] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ax, bd[o], acc[t][o], 0, 0, 0);
       }
     }
     __syncthreads();
@@ -1268,16 +1340,14 @@ __global__ __launch_bounds__(256, 2) void wgrad_wide_kernel(WwArgs a) {
 #pragma unroll
   for (int t = 0; t < 9; ++t)
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int o = 0; o < 4; ++o) {
+      const int co = o0 + 16 * o + co_l;
 #pragma unroll
-      for (int o = 0; o < 2; ++o) {
-        const int co = o0 + 32 * wj + 16 * o + co_l;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int ci = c0 + 32 * wi + 16 * i + ci_l + j;
-          if (ci < a.cin) part[((long)t * a.cin + ci) * a.cout + co] = acc[t][i][o][j];
-        }
+      for (int j = 0; j < 4; ++j) {
+        const int ci = c0 + 16 * wave + ci_l + j;
+        if (ci < a.cin) part[((long)t * a.cin + ci) * a.cout + co] = acc[t][o][j];
       }
+    }
 }
 
 template <int TH>
@@ -1839,6 +1909,40 @@ extern "C" int vm_maxpool2x2_backward_nhwc(const vm_tensor* x, const vm_tensor* 
   VM_CP_SWITCH(cp, VM_MPB)
 #undef VM_MPB
   return check_launch("maxpool_backward");
+}
+
+
+extern "C" size_t vm_relu_backward_bias_workspace_bytes(int channels) {
+  return channels <= 0 ? 0 : (size_t)bn_max_blocks(channels) * channels * sizeof(double);
+}
+
+extern "C" int vm_relu_backward_bias_nhwc(const vm_tensor* dy, const vm_tensor* y, const vm_tensor* add,
+                                          vm_tensor* dz, float* dbias, void* work, void* stream) {
+  if (!ok_view(dy) || !ok_view(y) || !ok_view(dz) || (add && !ok_view(add)) || !dbias || !work)
+    return fail(VM_EINVAL, "relu_backward_bias: bad argument");
+  if (dy->dtype != VM_F32 || (add && add->dtype != VM_F32) || !same_shape(dz, y) || (add && !same_shape(add, y)) ||
+      dy->n != y->n || dy->c != y->c)
+    return fail(VM_EINVAL, "relu_backward_bias: dy / add f32, dz and add shaped like y");
+  const bool pool = !(dy->h == y->h && dy->w == y->w);
+  if (pool && (dy->h != (y->h + 1) / 2 || dy->w != (y->w + 1) / 2))
+    return fail(VM_EINVAL, "relu_backward_bias: dy must be y's shape or its 2x2 SAME pool's");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int C = y->c;
+  const long units = pool ? (long)dy->n * dy->h * dy->w : (long)y->n * y->h * y->w;
+  const int nb = bn_blocks(pool ? 4 * units : units, C);
+  const int cp = C > 32 ? 64 : C > 16 ? 32 : C > 8 ? 16 : C > 4 ? 8 : C > 2 ? 4 : C > 1 ? 2 : 1;
+  const dim3 grid(cp == 64 ? (C + 63) / 64 : 1, nb);
+  V a = mk(dy), b = mk(y), c = add ? mk(add) : V{}, d = mk(dz);
+  double* part = reinterpret_cast<double*>(work);
+#define VM_RBB(CP)                                                                                           \
+  if (pool) hipLaunchKernelGGL((relu_bwd_bias_kernel<true, CP>), grid, dim3(256), 0, st, a, b, c, d, part, nb); \
+  else hipLaunchKernelGGL((relu_bwd_bias_kernel<false, CP>), grid, dim3(256), 0, st, a, b, c, d, part, nb)
+  VM_CP_SWITCH(cp, VM_RBB)
+#undef VM_RBB
+  int rc = check_launch("relu_backward_bias");
+  if (rc) return rc;
+  hipLaunchKernelGGL(fold_sum_kernel, dim3(C), dim3(256), 0, st, part, nb, C, dbias);
+  return check_launch("relu_backward_bias fold");
 }
 
 extern "C" int vm_resize_bilinear_tf1_backward(const vm_tensor* dy, float* dx, int ih, int iw, void* stream) {

@@ -14,11 +14,12 @@
   backward  through EVERY variable (train.py:51-52: minimize() with the default var_list): the VGG filters and
             biases (tf.Variable, unet.py:76-77,157), the fresh convs' weights and biases; the upconvs' drawn biases
             (unet.py:59) feed nothing and get no gradient, so Adam skips them — here they are not parameters.
-            Per relu conv: relu backward (f32 dz + its bf16 copy), bias = channel sum, the filter gradient
-            (ops.conv_wgrad: the wide MFMA kernel for cout >= 64), the data gradient (forward conv kernels on the
-            flipped filter); the [up, skip] concat gradient splits by channel view; the skip half gets the max-pool
-            adjoint added in place (TF MaxPoolGrad's first-maximum rule); the upconv half goes through its conv's
-            data gradient and the TF-1 resize adjoint
+            Per relu conv one pass (vm_relu_backward_bias_nhwc) gives the masked gradient as the bf16 operand of
+            the filter gradient (ops.conv_wgrad: the wide MFMA kernel for cout >= 64) and of the data gradient
+            (forward conv kernels on the flipped filter) plus the bias gradient; the [up, skip] concat gradient
+            splits by channel view: the skip conv's pass also takes its max-pool's adjoint (TF MaxPoolGrad's
+            first-maximum rule) and adds the concat half; the upconv half goes through its conv's data gradient and
+            the TF-1 resize adjoint
   exchange  DDP: one all-reduce of the flat gradient buffer (UNetImage has no BN, so nothing else is exchanged)
   update    tf.train.AdamOptimizer(1e-5, 0.9, 0.999, 1e-8) over the flat buffer in one launch, then re-packs
 """
@@ -104,16 +105,18 @@ class ImageTrainer(TrainerBase):
         L = _levels(h, w)
         dev = self.device
         F = lambda lv, c: torch.zeros((n, L[lv][0], L[lv][1], c), dtype=torch.float32, device=dev)  # noqa: E731
+        bf16 = self.dtype == torch.bfloat16
+        Z = (lambda lv, c: None) if bf16 else F  # noqa: E731  (f32 dz: the fp32 path only)
         g = {"dlogit": F(0, 1), "dlog8": F(0, 8), "loss": torch.zeros(3, dtype=torch.float32, device=dev),
              "in6": torch.empty((n, h, w, 6), dtype=torch.float32, device=dev),
-             "dcat1": F(0, 128), "dr4": F(0, 128), "dz12": F(0, 64), "dc11": F(0, 64), "dz11": F(0, 64),
-             "dcat2": F(1, 256), "dc23": F(1, 128), "dz23": F(1, 128), "dr3": F(1, 256), "dz22": F(1, 128),
-             "dc21": F(1, 128), "dz21": F(1, 128), "dp1": F(1, 64),
-             "dcat3": F(2, 512), "dc34": F(2, 256), "dz34": F(2, 256), "dr2": F(2, 512), "dz33": F(2, 256),
-             "dc32": F(2, 256), "dz32": F(2, 256), "dc31": F(2, 256), "dz31": F(2, 256), "dp2": F(2, 128),
-             "dcat4": F(3, 1024), "dc44": F(3, 512), "dz44": F(3, 512), "dr1": F(3, 512), "dz43": F(3, 512),
-             "dc42": F(3, 512), "dz42": F(3, 512), "dc41": F(3, 512), "dz41": F(3, 512), "dp3": F(3, 256),
-             "dc52": F(4, 512), "dz52": F(4, 512), "dc51": F(4, 512), "dz51": F(4, 512), "dp4": F(4, 512)}
+             "dcat1": F(0, 128), "dr4": F(0, 128), "dz12": Z(0, 64), "dc11": F(0, 64), "dz11": Z(0, 64),
+             "dcat2": F(1, 256), "dc23": F(1, 128), "dz23": Z(1, 128), "dr3": F(1, 256), "dz22": Z(1, 128),
+             "dc21": F(1, 128), "dz21": Z(1, 128), "dp1": F(1, 64),
+             "dcat3": F(2, 512), "dc34": F(2, 256), "dz34": Z(2, 256), "dr2": F(2, 512), "dz33": Z(2, 256),
+             "dc32": F(2, 256), "dz32": Z(2, 256), "dc31": F(2, 256), "dz31": Z(2, 256), "dp2": F(2, 128),
+             "dcat4": F(3, 1024), "dc44": F(3, 512), "dz44": Z(3, 512), "dr1": F(3, 512), "dz43": Z(3, 512),
+             "dc42": F(3, 512), "dz42": Z(3, 512), "dc41": F(3, 512), "dz41": Z(3, 512), "dp3": F(3, 256),
+             "dc52": F(4, 512), "dz52": Z(4, 512), "dc51": F(4, 512), "dz51": Z(4, 512), "dp4": F(4, 512)}
         if self.dtype == torch.bfloat16:
             B = lambda lv, c: torch.zeros((n, L[lv][0], L[lv][1], c), dtype=torch.bfloat16, device=dev)  # noqa: E731
             for k, (lv, c) in {"dlog16": (0, 32), "du4": (0, 64), "dz12": (0, 64), "dz11": (0, 64),
@@ -122,6 +125,7 @@ class ImageTrainer(TrainerBase):
                                "dz31": (2, 256), "dz44": (3, 512), "du1": (3, 512), "dz43": (3, 512),
                                "dz42": (3, 512), "dz41": (3, 512), "dz52": (4, 512), "dz51": (4, 512)}.items():
                 g["h_" + k] = B(lv, c)
+        g = {k: v for k, v in g.items() if v is not None}
         self._g, self._key = g, (n, h, w)
         return g
 
@@ -144,13 +148,14 @@ class ImageTrainer(TrainerBase):
     def _bf16(self):
         return self.dtype == torch.bfloat16
 
-    def _relu_conv_backward(self, name, dy, y, x_in, dz_key, dx_out=None):
-        """y = relu(conv(x_in) + b): dz = dy * (y > 0), the bias and filter gradients, optionally x_in's gradient."""
+    def _relu_conv_backward(self, name, dy, y, x_in, dz_key, dx_out=None, add=None):
+        """y = relu(conv(x_in) + b): dz = (y > 0) * (dy (+ add)) — or, when dy is the 2x2 pool's gradient, the pool
+        adjoint of dy plus ``add`` — and the bias gradient from ONE pass (vm_relu_backward_bias_nhwc; the bf16 path
+        writes only the bf16 dz its MFMA convs read), then the filter gradient and optionally x_in's gradient."""
         g = self._g
-        dz = g[dz_key]
         h16 = g.get("h_" + dz_key)
-        ops.relu_backward(dy, y, dz, dx2=h16)
-        ops.bn_backward(None, dz, None, None, None, None, dbeta=self.G[name, "b"])  # bias: channel sums
+        dz = h16 if h16 is not None else g[dz_key]
+        ops.relu_backward_bias(dy, y, dz, self.G[name, "b"], add=add)
         self._wgrad_dgrad(name, x_in, dz, h16, dx_out)
 
     def _wgrad_dgrad(self, name, x_in, dz, h16, dx_out):
@@ -195,26 +200,22 @@ class ImageTrainer(TrainerBase):
         self._upconv_backward("upconv_2", g["dcat3"][..., :256], b["r2"], "du2", g["dr2"], g["dc44"])
         self._relu_conv_backward("conv4_4", g["dc44"], b["c44"], b["cat4"], "dz44", g["dcat4"])
         self._upconv_backward("upconv_1", g["dcat4"][..., :512], b["r1"], "du1", g["dr1"], g["dc52"])
-        # encoder, bottom up; each skip half of a concat receives its pool's adjoint in place
+        # encoder, bottom up; each skip conv's gradient = its concat half + its pool's adjoint, in the same pass
         self._relu_conv_backward("conv5_2", g["dc52"], b["c52"], b["c51"], "dz52", g["dc51"])
         self._relu_conv_backward("conv5_1", g["dc51"], b["c51"], b["p4"], "dz51", g["dp4"])
-        d43 = g["dcat4"][..., 512:]
-        ops.maxpool_backward(b["cat4"][..., 512:], g["dp4"], d43, add=d43)
-        self._relu_conv_backward("conv4_3", d43, b["cat4"][..., 512:], b["c42"], "dz43", g["dc42"])
+        self._relu_conv_backward("conv4_3", g["dp4"], b["cat4"][..., 512:], b["c42"], "dz43", g["dc42"],
+                                 add=g["dcat4"][..., 512:])
         self._relu_conv_backward("conv4_2", g["dc42"], b["c42"], b["c41"], "dz42", g["dc41"])
         self._relu_conv_backward("conv4_1", g["dc41"], b["c41"], b["p3"], "dz41", g["dp3"])
-        d33 = g["dcat3"][..., 256:]
-        ops.maxpool_backward(b["cat3"][..., 256:], g["dp3"], d33, add=d33)
-        self._relu_conv_backward("conv3_3", d33, b["cat3"][..., 256:], b["c32"], "dz33", g["dc32"])
+        self._relu_conv_backward("conv3_3", g["dp3"], b["cat3"][..., 256:], b["c32"], "dz33", g["dc32"],
+                                 add=g["dcat3"][..., 256:])
         self._relu_conv_backward("conv3_2", g["dc32"], b["c32"], b["c31"], "dz32", g["dc31"])
         self._relu_conv_backward("conv3_1", g["dc31"], b["c31"], b["p2"], "dz31", g["dp2"])
-        d22 = g["dcat2"][..., 128:]
-        ops.maxpool_backward(b["cat2"][..., 128:], g["dp2"], d22, add=d22)
-        self._relu_conv_backward("conv2_2", d22, b["cat2"][..., 128:], b["c21"], "dz22", g["dc21"])
+        self._relu_conv_backward("conv2_2", g["dp2"], b["cat2"][..., 128:], b["c21"], "dz22", g["dc21"],
+                                 add=g["dcat2"][..., 128:])
         self._relu_conv_backward("conv2_1", g["dc21"], b["c21"], b["p1"], "dz21", g["dp1"])
-        d12 = g["dcat1"][..., 64:]
-        ops.maxpool_backward(b["cat1"][..., 64:], g["dp1"], d12, add=d12)
-        self._relu_conv_backward("conv1_2", d12, b["cat1"][..., 64:], b["c11"], "dz12", g["dc11"])
+        self._relu_conv_backward("conv1_2", g["dp1"], b["cat1"][..., 64:], b["c11"], "dz12", g["dc11"],
+                                 add=g["dcat1"][..., 64:])
         self._relu_conv_backward("conv1_1", g["dc11"], b["c11"], b["in8"][..., :6], "dz11")
 
     # ------------------------------------------------------------------------------------------- step

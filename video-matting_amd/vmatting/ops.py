@@ -856,6 +856,18 @@ def maxpool_backward(x, dy, dx, add=None):
     return dx
 
 
+def relu_backward_bias(dy, y, dz, dbias, add=None):
+    """vm_relu_backward_bias_nhwc: dz = (y > 0) * g and dbias = channel sums of dz in one pass; g = dy (+ add), or —
+    when dy has the 2x2 SAME pool's shape — add + the max-pool adjoint of dy (TF MaxPoolGrad's first maximum)."""
+    _f32(dbias)
+    views = [nhwc(dy), nhwc(y), None if add is None else nhwc(add), nhwc(dz)]
+    ref = lambda v: None if v is None else ctypes.byref(v)  # noqa: E731
+    ws = _workspace(lib().vm_relu_backward_bias_workspace_bytes(y.shape[-1]), y.device)
+    check(lib().vm_relu_backward_bias_nhwc(ref(views[0]), ref(views[1]), ref(views[2]), ref(views[3]), _ptr(dbias),
+                                           _ptr(ws), stream_handle()), "relu_backward_bias")
+    return dz
+
+
 def resize_backward(dy, dx):
     """Adjoint of resize_bilinear: dy [n,oh,ow,c] -> dx contiguous f32 [n,ih,iw,c] (overwritten)."""
     _f32(dx)
