@@ -781,7 +781,7 @@ def train_image_bench(dev, steps, warmup, world, rank, threads, cpu=True, n=8, s
     return rec
 
 
-def train_chain_bench(dev, steps, warmup, n=8, size=320, h=1080, w=1920, dtype="bf16"):
+def train_chain_bench(dev, steps, warmup, n=8, size=320, h=1080, w=1920, dtype="bf16", graph=False):
     """BASELINE config 5 as ONE pipeline per step (rank 0, N=1): augmentation.augment makes frame t of each of n
     1080p source samples resident in HBM (augmentation.py:102-135: host np.random draws + TPS solves, the device
     statistics / TPS lattice / resampling / fused warps + illumination — augment_many, one landmark upload, no sync),
@@ -789,7 +789,9 @@ def train_chain_bench(dev, steps, warmup, n=8, size=320, h=1080, w=1920, dtype="
     n x size^2 batch (loader.py:285-330, host crop draws) written straight into the captured training step's input
     buffers, then the step (train.py:318-332) replays from its HIP graphs.  Pipelined: the next batch's foreground
     statistics are launched on a side stream before this step, so the host's only wait (their readback) overlaps the
-    training step, and the next batch's draws / TPS solves / launches happen while it runs.  No decoding: the source
+    training step, and the next batch's draws / TPS solves / launches happen while it runs.  graph=False: the step's
+    eager launches with the select chains on side streams (HIP graph replay runs those branches one after another:
+    slower when the host keeps ahead, as it does here).  No decoding: the source
     images are synthetic device tensors (PNG/JPEG decode is host I/O outside the path).  Wall ms per phase and device
     ms per phase (HIP events on the launch stream)."""
     from vmatting import augmentation as va
@@ -816,8 +818,12 @@ def train_chain_bench(dev, steps, warmup, n=8, size=320, h=1080, w=1920, dtype="
         return samples
 
     r = vl.compose_batch(batch(va.StatsPrefetch(alphas).result()), (size, size), names, device=dev)
-    g = trn.capture(r["cmp"], r["bg"], r["warped"], r["label"], r["fg"])
-    outs = dict(zip(("cmp", "bg", "warped", "label", "fg"), g.inputs))
+    if graph:
+        g = trn.capture(r["cmp"], r["bg"], r["warped"], r["label"], r["fg"])
+        ins = g.inputs
+    else:
+        g, ins = None, [r["cmp"], r["bg"], r["warped"], r["label"], r["fg"]]
+    outs = dict(zip(("cmp", "bg", "warped", "label", "fg"), ins))
     state = {"pending": va.StatsPrefetch(alphas)}
 
     def one(ev=None, wall=None):
@@ -830,7 +836,7 @@ def train_chain_bench(dev, steps, warmup, n=8, size=320, h=1080, w=1920, dtype="
         state["pending"] = va.StatsPrefetch(alphas)  # the next batch's statistics, ahead of this step
         t2 = time.perf_counter()
         ev and ev.mark()
-        loss = g.step()
+        loss = g.step() if g is not None else trn.step(*ins)
         ev and ev.mark()
         t3 = time.perf_counter()
         if wall is not None:
@@ -856,9 +862,10 @@ def train_chain_bench(dev, steps, warmup, n=8, size=320, h=1080, w=1920, dtype="
                           "train_step": round(dev_ms[2], 3)},
             "host_issue_ms": {"augment_stats_wait_draws_tps_solve_launch": round(host_ms[0], 3),
                               "loader_crop_draws_launch_next_stats": round(host_ms[1], 3),
-                              "train_step_graph_replay_adam": round(host_ms[2], 3)},
+                              "train_step_launches_adam": round(host_ms[2], 3)},
             "launch": "augment + loader eager (one statistics readback per batch, prefetched on a side stream), "
-                      "training step replayed from HIP graphs",
+                      "training step %s" % ("replayed from HIP graphs" if graph else
+                                            "eager with the select chains on side streams"),
             "decode": "none: synthetic source images resident in HBM (PNG/JPEG decoding is host I/O outside the path)",
             "loss_last": [round(float(v), 5) for v in loss.cpu()]}
 
@@ -1079,7 +1086,7 @@ def main():
             rec = train_bench(dev, args.steps, args.warmup, world, rank, threads, cpu=False, graph=args.train_graph,
                               streams=args.train_streams)
         elif args.only == "train_chain":
-            rec = train_chain_bench(dev, args.steps, args.warmup)
+            rec = train_chain_bench(dev, args.steps, args.warmup, graph=args.train_graph)
         elif args.only == "train_small":
             rec = train_small_bench(dev, args.steps, args.warmup, world, rank, threads, cpu=False)
         elif args.only == "train_image":

@@ -397,6 +397,10 @@ int vm_change_illumination_u8(const uint8_t* bgr, long pixels, const uint8_t* lu
  * alpha pixels, sum of their row indices, sum of their column indices.  alpha [h, w] VM_F64 / VM_F32 / VM_U8. */
 int vm_nonzero_stats(const void* alpha, int h, int w, int dtype, long long* stats, void* stream);
 
+/* augmentation.augmentation's BGRA frame (augmentation.py:154-155, 162-163): out[p] = [fg B, G, R,
+ * uint8(255. * alpha[p])] (the product in the alpha's precision, f64 / f32, truncated like numpy's astype). */
+int vm_bgra_u8(const uint8_t* fg, const void* alpha, int alpha_dtype, long pixels, uint8_t* out, void* stream);
+
 /* data.trimap_from_matte (data.py:37-67; the reference uses dilate 1, crop 3): trimap u8 [h, w] from a float64
  * matte [h, w] (device), 255 / 0 where the matte is exactly 1 / 0, 128 elsewhere and — reproducing the reference's
  * raster-order overwrites — on 1-pixels (0-pixels) with a non-0/1 pixel later in raster order within crop (dilate)

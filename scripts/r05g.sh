@@ -20,6 +20,8 @@ for v in base cur lb2 base cur lb2; do
 done
 grep -E "==|total" gpurun_out/r5g_ww.log
 PT="python -u -m pytest -v --timeout 300 --timeout-method thread -rf -s"
-guard 600 r5g_tests.log $PT tests/test_gpu_train.py tests/test_gpu_image_train.py tests/test_gpu_split6.py -m gpu -k "relu_backward_bias or wgrad_wide or image or bf16x6_graph"
+guard 600 r5g_tests.log $PT tests/test_gpu_train.py tests/test_gpu_image_train.py tests/test_gpu_split6.py tests/test_gpu_augment.py -m gpu -k "relu_backward_bias or wgrad_wide or image or bf16x6_graph or bgra or augment_many or config5"
 guard 300 r5g_timage.log python -u bench.py --only train_image --steps 10 --warmup 3
 guard 300 r5g_x6.log python -u tools/x6bench.py 10
+guard 300 r5g_chain.log python -u bench.py --only train_chain --steps 10 --warmup 3
+guard 300 r5g_chain_g.log python -u bench.py --only train_chain --steps 10 --warmup 3 --train-graph

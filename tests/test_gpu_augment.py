@@ -335,3 +335,16 @@ def test_augment_many_equals_sequential_augment():
     st = va.StatsPrefetch([torch.from_numpy(np.ascontiguousarray(t[2])).cuda() for t in triples]).result()
     assert st == va.nonzero_stats_many([torch.from_numpy(np.ascontiguousarray(t[2])).cuda() for t in triples])
     assert st[0][0] == int(np.count_nonzero(triples[0][2]))
+
+
+@pytest.mark.parametrize("adt", [np.float64, np.float32])
+def test_bgra_matches_numpy(adt):
+    """vm_bgra_u8 == np.concatenate((fg, (255. * alpha[..., None]).astype(np.uint8)), 2) (augmentation.py:154-155)."""
+    from vmatting import ops
+    rs = np.random.RandomState(2)
+    fg = (rs.rand(37, 53, 3) * 255).astype(np.uint8)
+    al = rs.rand(37, 53).astype(adt)
+    al[0, :4] = [0.0, 1.0, 254.5 / 255, 1 / 255.]
+    got = H(ops.bgra(torch.from_numpy(fg).cuda(), torch.from_numpy(al).cuda()))
+    want = np.concatenate((fg, (255. * al.reshape(37, 53, 1)).astype(np.uint8)), axis=2)
+    assert np.array_equal(got, want)

@@ -355,6 +355,17 @@ __global__ void __launch_bounds__(256) warp_image_kernel(const T* __restrict__ s
   });
 }
 
+// augmentation.augmentation's BGRA frame (augmentation.py:154-155, 162-163): concat(fg u8 BGR, (255. * alpha)
+// .astype(uint8)) — the product in the alpha's precision (f64 like numpy), truncated — one 4-byte store per pixel.
+template <typename TA>
+__global__ void __launch_bounds__(256) bgra_kernel(const uint8_t* __restrict__ fg, const TA* __restrict__ alpha,
+                                                   long pixels, uint32_t* __restrict__ out) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < pixels; i += (long)gridDim.x * blockDim.x) {
+    const uint32_t a8 = (uint32_t)(uint8_t)(int)(255.0 * (double)alpha[i]);
+    out[i] = (uint32_t)fg[3 * i] | ((uint32_t)fg[3 * i + 1] << 8) | ((uint32_t)fg[3 * i + 2] << 16) | (a8 << 24);
+  }
+}
+
 // augmentation.object_size / fg_center (augmentation.py:10-20): count, row-index sum and column-index sum of the
 // nonzero alpha pixels (exact integers; the host forms sqrt(count) and int(sum / count) like numpy).
 template <typename T>
@@ -612,6 +623,24 @@ extern "C" int vm_nonzero_stats(const void* alpha, int h, int w, int dtype, long
     default: return fail(VM_EUNSUPPORTED, "nonzero_stats: dtype %d", dtype);
   }
   return check_launch("nonzero_stats");
+}
+
+
+extern "C" int vm_bgra_u8(const uint8_t* fg, const void* alpha, int alpha_dtype, long pixels, uint8_t* out,
+                          void* stream) {
+  if (!fg || !alpha || !out || pixels <= 0 || reinterpret_cast<uintptr_t>(out) % 4)
+    return fail(VM_EINVAL, "bgra: bad argument");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const dim3 g(grid_for(pixels, 256)), b(256);
+  uint32_t* o = reinterpret_cast<uint32_t*>(out);
+  switch (alpha_dtype) {
+    case VM_F64: hipLaunchKernelGGL(bgra_kernel<double>, g, b, 0, st, fg, static_cast<const double*>(alpha), pixels, o);
+      break;
+    case VM_F32: hipLaunchKernelGGL(bgra_kernel<float>, g, b, 0, st, fg, static_cast<const float*>(alpha), pixels, o);
+      break;
+    default: return fail(VM_EUNSUPPORTED, "bgra: alpha dtype %d", alpha_dtype);
+  }
+  return check_launch("bgra");
 }
 
 extern "C" int vm_trimap_from_matte(const double* matte, int h, int w, int dilate, int crop, uint8_t* trimap,

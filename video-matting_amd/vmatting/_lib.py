@@ -127,6 +127,7 @@ SIGNATURES = [
                               ctypes.POINTER(ctypes.c_uint8), c_void_p, c_int, c_int, c_void_p]),
     ("vm_change_illumination_u8", c_int, [c_void_p, c_long, ctypes.POINTER(ctypes.c_uint8), c_void_p, c_void_p]),
     ("vm_nonzero_stats", c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
+    ("vm_bgra_u8", c_int, [c_void_p, c_void_p, c_int, c_long, c_void_p, c_void_p]),
     ("vm_trimap_from_matte", c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
     ("vm_matting_loss_backward", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_void_p,
                                          c_void_p]),

@@ -220,8 +220,7 @@ def bgra(fg, alpha):
     """The BGRA image augmentation.augmentation writes for a (fg, alpha) pair (augmentation.py:152-153,163-164):
     concat(fg u8, (255. * alpha).astype(uint8)) — on the device for device tensors (float64 product, truncation)."""
     dfg, dal = _device(fg), _device(alpha)
-    a8 = (255.0 * dal.to(torch.float64)).to(torch.uint8)
-    return _out(torch.cat([dfg, a8.reshape(dal.shape[0], dal.shape[1], 1)], 2), fg)
+    return _out(ops.bgra(dfg, dal), fg)
 
 
 def video_sample(fg, bg, alpha, flow):

@@ -766,6 +766,21 @@ def change_illumination(bgr, lut, out=None):
     return out
 
 
+def bgra(fg, alpha, out=None):
+    """vm_bgra_u8: concat(fg u8 [h, w, 3], uint8(255. * alpha [h, w] f64 / f32)) -> u8 [h, w, 4]."""
+    _require_gpu(fg)
+    _require_gpu(alpha)
+    fg, alpha = fg.contiguous(), alpha.contiguous()
+    h, w = fg.shape[:2]
+    if fg.dtype != torch.uint8 or tuple(fg.shape) != (h, w, 3) or alpha.numel() != h * w:
+        raise ValueError("bgra: fg u8 [h, w, 3] and alpha [h, w]")
+    if out is None:
+        out = torch.empty((h, w, 4), dtype=torch.uint8, device=fg.device)
+    check(lib().vm_bgra_u8(_ptr(fg), _ptr(alpha), _dtype_code(alpha, "bgra"), h * w, _ptr(out), stream_handle()),
+          "bgra")
+    return out
+
+
 def nonzero_stats(alpha, out=None):
     """vm_nonzero_stats: (count, row-index sum, column-index sum) of alpha != 0, int64[3] on the device."""
     _require_gpu(alpha)
