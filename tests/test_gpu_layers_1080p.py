@@ -34,7 +34,7 @@ H, W = 1080, 1920
 # conv launch order of the lean bf16 forward (unet.py:170-205) and the kernel each one must run on
 TIMED = [
     ("conv1_1+conv1_2+pool1", r"vm::conv3x3_pair_strip"),
-    ("conv2_1", r"vm::conv3x3_patch_persist<64, 8, 1, 2, 8, 1, false>"),
+    ("conv2_1", r"vm::conv3x3_rows<16>"),
     ("conv2_2", r"vm::conv3x3_rows<16>"),
     ("conv3_1", r"vm::conv3x3_rows<16>"),
     ("conv3_2", r"vm::conv3x3_rows<16>"),

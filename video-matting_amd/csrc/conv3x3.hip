@@ -4544,7 +4544,8 @@ static long g_patch_ablate = 0;
 static long g_rows_kernel = 1;        // conv_rows.hip: 0 = off, 1 = auto (grid size), 8 / 16 = forced tile height
 static long g_rows_min_blocks = 400;
 static long g_rows_up = 0;            // 1: the folded upconvs too
-static long g_rows_min_cin = 128;      // shorter K loops: the 2-blocks-per-CU patch kernel hides prologue/epilogue better
+static long g_rows_min_cin = 64;       // r04 A/B: conv2_1 (cin 64, 2040 blocks) +0.3 % on rows<16>; below 64 the
+                                       // 2-blocks-per-CU patch kernel hides prologue/epilogue better
 static long g_src_span_limit = 0x7ffffff0L;  // split-source byte span the 32-bit offset kernels take (option
                                               // "src_span_limit" lowers it for the fallback tests)
 static long g_pair_strip = 1;  // vm_conv3x3_pair_first*: 1 = the strip-walking kernel (conv_pair.hip) where it applies

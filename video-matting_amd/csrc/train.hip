@@ -1210,7 +1210,8 @@ constexpr int WW_TH = 4;
 constexpr int WW_TARGET_BLOCKS = 512;  // ~2 resident blocks per CU: one round; the partials stay <= 75 MB
 
 template <int TH, bool DYF32>
-__global__ __launch_bounds__(256, 1) void wgrad_wide_kernel(WwArgs a) {
+__global__ __launch_bounds__(256, 2) void wgrad_wide_kernel(WwArgs a) {  // A/B (scripts/build_variant.sh):
+                                                                           // (256,2) 2.58 ms vs (256,1) 2.87 ms
   constexpr int XPIX = wm_ppix<TH>(), DPIX = TH * WM_TW;
   constexpr int XBYTES = wm_prows<TH>() * 128;
   constexpr int NXC = XPIX * 8, NDC = DPIX * 8;                 // 16-byte chunks (8 channels) of each image
