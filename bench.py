@@ -781,7 +781,7 @@ def train_image_bench(dev, steps, warmup, world, rank, threads, cpu=True, n=8, s
     return rec
 
 
-def train_chain_bench(dev, steps, warmup, n=8, size=320, h=1080, w=1920, dtype="bf16", graph=False):
+def train_chain_bench(dev, steps, warmup, n=8, size=320, h=1080, w=1920, dtype="bf16", graph=False, overlap=True):
     """BASELINE config 5 as ONE pipeline per step (rank 0, N=1): augmentation.augment makes frame t of each of n
     1080p source samples resident in HBM (augmentation.py:102-135: host np.random draws + TPS solves, the device
     statistics / TPS lattice / resampling / fused warps + illumination — augment_many, one landmark upload, no sync),
@@ -817,6 +817,8 @@ def train_chain_bench(dev, steps, warmup, n=8, size=320, h=1080, w=1920, dtype="
             smp["plan"] = vl.plan_crop((h, w), (h, w))
         return samples
 
+    if overlap:
+        return _train_chain_overlap(dev, steps, warmup, trn, batch, alphas, n, size, names, dtype, graph)
     r = vl.compose_batch(batch(va.StatsPrefetch(alphas).result()), (size, size), names, device=dev)
     if graph:
         g = trn.capture(r["cmp"], r["bg"], r["warped"], r["label"], r["fg"])
@@ -866,6 +868,103 @@ def train_chain_bench(dev, steps, warmup, n=8, size=320, h=1080, w=1920, dtype="
             "launch": "augment + loader eager (one statistics readback per batch, prefetched on a side stream), "
                       "training step %s" % ("replayed from HIP graphs" if graph else
                                             "eager with the select chains on side streams"),
+            "decode": "none: synthetic source images resident in HBM (PNG/JPEG decoding is host I/O outside the path)",
+            "loss_last": [round(float(v), 5) for v in loss.cpu()]}
+
+
+def _train_chain_overlap(dev, steps, warmup, trn, batch, alphas, n, size, names, dtype, graph):
+    """train_chain_bench's pipelined form: batch k+1's augment + loader run on a producer stream while step k runs
+    on the caller's stream (the data pipeline of a training job overlapping its step, as a prefetching loader
+    does).  Two batch slots: the producer fills slot (k+1) % 2 after the step that read it has finished (event),
+    the step waits for its slot's ready event.  Same batches, same order, same step: only the overlap differs
+    from the serial form.  Host per step: the step's launches (graph: two replays), then batch k+1's draws / TPS
+    solves / launches."""
+    from vmatting import augmentation as va
+    from vmatting import loader as vl
+    main = torch.cuda.current_stream(dev)
+    prod = torch.cuda.Stream(device=dev)
+    ready = [torch.cuda.Event(), torch.cuda.Event()]
+    freed = [torch.cuda.Event(), torch.cuda.Event()]
+    slots = [None, None]
+    pev = {}  # producer-stream timing events of the timed steps
+
+    def produce(k, stats, timed):
+        s = k % 2
+        with torch.cuda.stream(prod):
+            prod.wait_event(freed[s])  # the step that read this slot is done (never-recorded events: no wait)
+            e0 = torch.cuda.Event(enable_timing=True) if timed else None
+            e0 and e0.record()
+            samples = batch(stats)
+            e1 = torch.cuda.Event(enable_timing=True) if timed else None
+            e1 and e1.record()
+            slots[s] = vl.compose_batch(samples, (size, size), names, device=dev, out=slots[s])
+            ready[s].record(prod)
+            if timed:
+                e2 = torch.cuda.Event(enable_timing=True)
+                e2.record()
+                pev[k] = (e0, e1, e2)
+            # the next batch's foreground statistics, behind this batch on the producer stream
+            return va.StatsPrefetch(alphas)
+
+    # batch 0 = the serial form's first batch: it sizes the slots (and is what a graph is captured on), the steps
+    # start at batch 1 in both forms
+    pending = produce(0, va.StatsPrefetch(alphas).result(), False)
+    main.wait_event(ready[0])
+    g = None
+    if graph:
+        r = slots[0]
+        g = trn.capture(r["cmp"], r["bg"], r["warped"], r["label"], r["fg"])
+    freed[0].record(main)
+    pending = produce(1, pending.result(), False)
+
+    def one(k, timed, sev=None):
+        s = k % 2
+        r = slots[s]
+        main.wait_event(ready[s])
+        if sev is not None:
+            sev.append(torch.cuda.Event(enable_timing=True))
+            sev[-1].record(main)
+        ins = (r["cmp"], r["bg"], r["warped"], r["label"], r["fg"])
+        if g is not None:
+            g.load(*ins)  # the graph's static inputs (on the caller's stream), then the slot is free again
+            freed[s].record(main)
+            loss = g.step()
+        else:
+            loss = trn.step(*ins)
+            freed[s].record(main)
+        if sev is not None:
+            sev.append(torch.cuda.Event(enable_timing=True))
+            sev[-1].record(main)
+        return loss, produce(k + 1, pending_box[0].result(), timed)
+
+    pending_box = [pending]
+    k = 1
+    for _ in range(warmup):
+        loss, pending_box[0] = one(k, False)
+        k += 1
+    torch.cuda.synchronize()
+    sev = []
+    k0 = k
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        loss, pending_box[0] = one(k, True, sev)
+        k += 1
+    # both streams drained: the timed region also holds the batch produced behind the last step (the first timed
+    # step's batch was produced before it), so it is one full pipeline period per step
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    step_ms = sum(ms(sev[2 * i], sev[2 * i + 1]) for i in range(steps)) / steps
+    aug_ms = sum(ms(pev[k][0], pev[k][1]) for k in range(k0 + 1, k0 + steps + 1)) / steps
+    ldr_ms = sum(ms(pev[k][1], pev[k][2]) for k in range(k0 + 1, k0 + steps + 1)) / steps
+    return {"workload": "config 5 chained: augmentation.augment on %d 1080p sources -> loader video_batch per-pixel "
+                        "work -> %dx%d -> VideoTrainer step (%s forward, f32 gradients / Adam)" % (n, size, size, dtype),
+            "samples_per_s": round(n / dt, 1), "ms_per_step": round(1e3 * dt, 3),
+            "device_ms": {"augment": round(aug_ms, 3), "loader": round(ldr_ms, 3), "train_step": round(step_ms, 3)},
+            "device_ms_def": "HIP events on each phase's own stream; augment + loader of batch k+1 (producer stream) "
+                             "run concurrently with step k (training stream), so the phases overlap",
+            "launch": "pipelined: augment + loader of the next batch on a producer stream (two batch slots, events) "
+                      "beside the training step %s" % ("replayed from HIP graphs" if graph else
+                                                       "(eager, select chains on side streams)"),
             "decode": "none: synthetic source images resident in HBM (PNG/JPEG decoding is host I/O outside the path)",
             "loss_last": [round(float(v), 5) for v in loss.cpu()]}
 
@@ -1039,6 +1138,8 @@ def main():
     ap.add_argument("--train-graph", action="store_true",
                     help="config-5 record from HIP-graph replays (VideoTrainer.capture) instead of eager launches: "
                          "the step is not host-bound, and the graph runs the side-stream select chains serially")
+    ap.add_argument("--chain-serial", action="store_true",
+                    help="config-5 chained record without the producer-stream overlap (augment, loader, step in turn)")
     ap.add_argument("--train-streams", type=int, default=3,
                     help="side streams of the config-5 trainer's select chains (0: one stream, for serial profiles)")
     ap.add_argument("--only", choices=["train", "train_chain", "train_small", "train_image", "temporal"],
@@ -1086,7 +1187,7 @@ def main():
             rec = train_bench(dev, args.steps, args.warmup, world, rank, threads, cpu=False, graph=args.train_graph,
                               streams=args.train_streams)
         elif args.only == "train_chain":
-            rec = train_chain_bench(dev, args.steps, args.warmup, graph=args.train_graph)
+            rec = train_chain_bench(dev, args.steps, args.warmup, graph=args.train_graph, overlap=not args.chain_serial)
         elif args.only == "train_small":
             rec = train_small_bench(dev, args.steps, args.warmup, world, rank, threads, cpu=False)
         elif args.only == "train_image":
@@ -1161,7 +1262,7 @@ def main():
         train = train_bench(dev, max(args.steps // 4, 10), 3, world, rank, threads, cpu=not args.no_cpu_baseline,
                             graph=args.train_graph)
         if world == 1:
-            train["chained"] = train_chain_bench(dev, 5, 2)
+            train["chained"] = train_chain_bench(dev, 5, 2, graph=args.train_graph, overlap=not args.chain_serial)
         train_small = train_small_bench(dev, max(args.steps // 4, 10), 3, world, rank, threads,
                                         cpu=not args.no_cpu_baseline)
         train_image = train_image_bench(dev, max(args.steps // 4, 10), 3, world, rank, threads,

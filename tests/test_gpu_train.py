@@ -704,6 +704,19 @@ def test_config5_chain_augment_loader_step():
     assert np.isfinite(loss).all() and loss[0] > 0
 
 
+@pytest.mark.parametrize("graph", [False, True])
+def test_chain_overlap_equals_serial(graph):
+    """bench.py's pipelined config-5 chain (batch k+1's augment + loader on a producer stream beside step k, two
+    batch slots) trains on the same batches in the same order as the serial chain: the last step's loss terms are
+    bit-identical (fp32 step; graph replay of the step too)."""
+    import bench
+    kw = dict(n=2, size=64, h=120, w=160, dtype="fp32")
+    ser = bench.train_chain_bench(DEV, 2, 2, overlap=False, **kw)
+    ovl = bench.train_chain_bench(DEV, 2, 2, overlap=True, graph=graph, **kw)
+    assert ovl["loss_last"] == ser["loss_last"], (ovl["loss_last"], ser["loss_last"])
+    assert np.isfinite(ovl["loss_last"]).all()
+
+
 def _syncbn_worker(rank, world, port, q):
     import os
     import torch.distributed as dist

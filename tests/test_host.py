@@ -224,3 +224,56 @@ def test_bench_refuses_a_world_other_than_gpus():
     rc, recs, err = _bench("--gpus", "2", "--dist-selftest", env={"WORLD_SIZE": "1", "RANK": "0"})
     assert rc != 0 and not recs
     assert "initialised world" in err
+
+
+@pytest.mark.parametrize("h,w,n,fact", [(1080, 1920, 5, 0.05), (37, 51, 5, 0.05), (64, 64, 4, 0.1), (9, 300, 6, 0.2)])
+def test_deform_grid_draws_match_the_reference_loop(h, w, n, fact):
+    """tps.deform_grid draws its landmark offsets as one array; the reference (tps.py:127-143, restated in
+    oracle/augment.py) draws one scalar per interior coordinate, x before y: same grids, bit for bit, and the
+    same global RNG state after."""
+    from oracle import augment as oa
+    from vmatting import tps
+    for seed in range(5):
+        np.random.seed(seed)
+        g1, d1 = tps.deform_grid(h, w, n, fact)
+        after1 = np.random.rand()
+        np.random.seed(seed)
+        g2, d2 = oa.deform_grid(h, w, n, fact)
+        after2 = np.random.rand()
+        assert np.array_equal(g1, g2) and np.array_equal(d1, d2) and after1 == after2
+
+
+def test_training_procedures_follow_the_reference_loop(tmp_path):
+    """vmatting.procedures: per epoch the lists are copied and shuffled (train first), batches popped off the end
+    until fewer than a batch remain, each fed to one step; training_procedure's validation over the test list."""
+    import random
+    from vmatting import procedures
+    seen = []
+
+    class FakeTrainer:
+        device = "cpu"
+
+        def step(self, *batch):
+            seen.append(batch[0])
+            return len(seen)
+
+    made = []
+
+    def make(batch_list):
+        made.append(list(batch_list))
+        return (tuple(batch_list),)
+
+    files = ["f%d" % i for i in range(11)]
+    random.seed(3)
+    steps = []
+    procedures._loop(FakeTrainer(), files, files[:5], make, 2, 4, False,
+                     lambda e, it, loss: steps.append((e, it, loss)), None)
+    random.seed(3)
+    want = []
+    for _ in range(2):
+        tl, vl = list(files), list(files[:5])
+        random.shuffle(tl)
+        random.shuffle(vl)
+        while len(tl) >= 4:
+            want.append([tl.pop() for _ in range(4)])
+    assert made == want and [s[1] for s in steps] == list(range(4)) and files == ["f%d" % i for i in range(11)]

@@ -196,7 +196,8 @@ def augment_many(triples, stats=None):
         b = np.random.uniform(1. - 0.3, 1. + 0.3)
         c = np.random.uniform(-0.07, 0.07)
         # one TPS map serves fg and alpha (the reference evaluates the same map twice): the reverse transform
-        # def_grid -> grid (tps.py:50-51), solved on the host like the reference
+        # def_grid -> grid (tps.py:50-51), solved on the host like the reference (numpy's pinv: L is numerically
+        # singular, cond ~1e16, so pinv's cut of the small singular values IS the map — no faster LU solve)
         uploads += [def_grid, tps._coefficients(def_grid, grid)]
         plans.append((h, w, grid, def_grid, (tu_bg, tv_bg, scale_bg), (tu_fg, tv_fg, rot_fg, scale_fg, center),
                       illumination_lut(a, b, c)))

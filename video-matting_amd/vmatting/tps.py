@@ -137,14 +137,15 @@ def deform_grid(h, w, n=5, fact=0.05):
     vec1 = (h / (n - 1)) * np.arange(n)
     vec2 = (w / (n - 1)) * np.arange(n)
     grid = np.transpose([np.repeat(vec1, n), np.tile(vec2, n)])
-    new_grid = np.zeros_like(grid)
-    for i in range(n * n):
-        y, x = grid[i, 0], grid[i, 1]
-        new_grid[i] = grid[i]
-        if 0. < x < w:
-            new_grid[i, 1] += np.random.uniform(-bound, bound)
-        if 0. < y < h:
-            new_grid[i, 0] += np.random.uniform(-bound, bound)
+    # the reference's loop draws one np.random.uniform(-bound, bound) per interior coordinate, point by point, x
+    # before y; the legacy RandomState gives the same doubles drawn as one array in that order (off + scale * u
+    # each), so the draws are made at once and scattered (~10x less host time per sample)
+    inner = np.stack([(grid[:, 1] > 0.) & (grid[:, 1] < w), (grid[:, 0] > 0.) & (grid[:, 0] < h)], axis=1).ravel()
+    d = np.zeros(2 * n * n)
+    d[inner] = np.random.uniform(-bound, bound, size=int(inner.sum()))
+    new_grid = grid.copy()
+    new_grid[:, 1] += d[0::2]  # + 0.0 where no draw: the coordinate unchanged
+    new_grid[:, 0] += d[1::2]
     return grid, new_grid
 
 
