@@ -781,7 +781,8 @@ def train_image_bench(dev, steps, warmup, world, rank, threads, cpu=True, n=8, s
     return rec
 
 
-def train_chain_bench(dev, steps, warmup, n=8, size=320, h=1080, w=1920, dtype="bf16", graph=False, overlap=True):
+def train_chain_bench(dev, steps, warmup, n=8, size=320, h=1080, w=1920, dtype="bf16", graph=False, overlap=True,
+                      profiler=None):
     """BASELINE config 5 as ONE pipeline per step (rank 0, N=1): augmentation.augment makes frame t of each of n
     1080p source samples resident in HBM (augmentation.py:102-135: host np.random draws + TPS solves, the device
     statistics / TPS lattice / resampling / fused warps + illumination — augment_many, one landmark upload, no sync),
@@ -818,7 +819,7 @@ def train_chain_bench(dev, steps, warmup, n=8, size=320, h=1080, w=1920, dtype="
         return samples
 
     if overlap:
-        return _train_chain_overlap(dev, steps, warmup, trn, batch, alphas, n, size, names, dtype, graph)
+        return _train_chain_overlap(dev, steps, warmup, trn, batch, alphas, n, size, names, dtype, graph, profiler)
     r = vl.compose_batch(batch(va.StatsPrefetch(alphas).result()), (size, size), names, device=dev)
     if graph:
         g = trn.capture(r["cmp"], r["bg"], r["warped"], r["label"], r["fg"])
@@ -849,11 +850,13 @@ def train_chain_bench(dev, steps, warmup, n=8, size=320, h=1080, w=1920, dtype="
         one()
     torch.cuda.synchronize()
     ev, wall = Events(), []
+    profiler and profiler.enable()
     t0 = time.perf_counter()
     for _ in range(steps):
         loss = one(ev, wall)
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / steps
+    profiler and profiler.disable()
     e = ev.e
     dev_ms = [sum(ms(e[4 * i + k], e[4 * i + k + 1]) for i in range(steps)) / steps for k in range(3)]
     host_ms = [1e3 * sum(wl[k] for wl in wall) / steps for k in range(3)]
@@ -872,7 +875,7 @@ def train_chain_bench(dev, steps, warmup, n=8, size=320, h=1080, w=1920, dtype="
             "loss_last": [round(float(v), 5) for v in loss.cpu()]}
 
 
-def _train_chain_overlap(dev, steps, warmup, trn, batch, alphas, n, size, names, dtype, graph):
+def _train_chain_overlap(dev, steps, warmup, trn, batch, alphas, n, size, names, dtype, graph, profiler=None):
     """train_chain_bench's pipelined form: batch k+1's augment + loader run on a producer stream while step k runs
     on the caller's stream (the data pipeline of a training job overlapping its step, as a prefetching loader
     does).  Two batch slots: the producer fills slot (k+1) % 2 after the step that read it has finished (event),
@@ -945,6 +948,7 @@ def _train_chain_overlap(dev, steps, warmup, trn, batch, alphas, n, size, names,
     torch.cuda.synchronize()
     sev = []
     k0 = k
+    profiler and profiler.enable()
     t0 = time.perf_counter()
     for _ in range(steps):
         loss, pending_box[0] = one(k, True, sev)
@@ -953,6 +957,7 @@ def _train_chain_overlap(dev, steps, warmup, trn, batch, alphas, n, size, names,
     # step's batch was produced before it), so it is one full pipeline period per step
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / steps
+    profiler and profiler.disable()
     step_ms = sum(ms(sev[2 * i], sev[2 * i + 1]) for i in range(steps)) / steps
     aug_ms = sum(ms(pev[k][0], pev[k][1]) for k in range(k0 + 1, k0 + steps + 1)) / steps
     ldr_ms = sum(ms(pev[k][1], pev[k][2]) for k in range(k0 + 1, k0 + steps + 1)) / steps

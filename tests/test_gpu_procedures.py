@@ -28,8 +28,9 @@ def _files(tmp_path, video, n=5):
     return out
 
 
-def _reference_loop(trainer, files, tests, make, epochs, bs):
-    """train.py:64-79 as the reference writes it (summaries aside)."""
+def _reference_loop(trainer, files, tests, make, epochs, bs, validate=False):
+    """train.py:64-95 as the reference writes it (summaries aside); validate: training_procedure's validation
+    batches (their loader draws; the forward leaves the model as it is)."""
     from vmatting import loader
     losses = []
     for _ in range(epochs):
@@ -38,6 +39,8 @@ def _reference_loop(trainer, files, tests, make, epochs, bs):
         random.shuffle(test_list)
         while not loader.epoch_is_over(training_list, bs):
             losses.append(trainer.step(*make(loader.get_batch_list(training_list, bs))).cpu().numpy())
+        while validate and not loader.epoch_is_over(test_list, bs):
+            make(loader.get_batch_list(test_list, bs))
     return losses
 
 
@@ -80,7 +83,7 @@ def _run(kind, tmp_path, graph):
     t2 = trainer()
     random.seed(5)
     np.random.seed(6)
-    want = _reference_loop(t2, files, tests, make, 2, 2)
+    want = _reference_loop(t2, files, tests, make, 2, 2, validate=kind == "image")
     return got, want, vals
 
 

@@ -552,23 +552,28 @@ def wgrad_opts():
     yield _lib.set_option
     _lib.set_option("wgrad_taps", 1)
     _lib.set_option("wgrad_variant", 0)
+    _lib.set_option("wgrad_dma", 1)
 
 
-# (wgrad_taps, wgrad_variant): taps-in-N kernel for cout <= 8 with 4- and 8-row tiles, and the per-tap kernel
-WGRAD_VARIANTS = [(1, 0), (1, 2), (0, 0)]
+# (wgrad_taps, wgrad_variant, wgrad_dma): the LDS-DMA narrow kernel (cout <= 16, cin % 8 == 0; the default), the
+# register-staged taps-in-N kernel for cout <= 8 with 4- and 8-row tiles, and the per-tap kernel
+WGRAD_VARIANTS = [(1, 0, 1), (1, 0, 0), (1, 2, 0), (0, 0, 0)]
 
 
 @pytest.mark.parametrize("variant", WGRAD_VARIANTS)
 @pytest.mark.parametrize("cout", [1, 2, 3, 4, 6, 8, 16, 24, 32, 48])
-@pytest.mark.parametrize("cin,cs", [(9, 16), (30, 32), (64, 72), (192, 192), (70, 80)])
+@pytest.mark.parametrize("cin,cs", [(9, 16), (30, 32), (64, 72), (192, 192), (70, 80), (40, 40)])
 def test_conv_wgrad_mfma(cin, cs, cout, variant, wgrad_opts):
     """vm_conv3x3_wgrad_bf16_nhwc: bf16 x and dy rounded to bf16, f32 sums — against float64 autograd on the same
     bf16-rounded operands (so only the summation order differs): max-abs error <= 1e-4 of scale."""
     from vmatting import ops
-    if cout > 8 and variant != WGRAD_VARIANTS[0]:
+    if cout > 16 and variant != WGRAD_VARIANTS[0]:
+        pytest.skip("the options only route cout <= 16")
+    if cout > 8 and variant[2] == 0 and variant != WGRAD_VARIANTS[1]:
         pytest.skip("the taps option only routes cout <= 8")
     wgrad_opts("wgrad_taps", variant[0])
     wgrad_opts("wgrad_variant", variant[1])
+    wgrad_opts("wgrad_dma", variant[2])
     rs = np.random.RandomState(cin * 100 + cout)
     n, h, w = 2, 13, 70
     x = rs.normal(size=(n, h, w, cs)).astype(np.float32)
@@ -594,6 +599,24 @@ def test_conv_wgrad_mfma_wide_cin_accumulates(cin, cout, hw):
     wr = torch.zeros((3, 3, cin, cout), dtype=torch.float64, requires_grad=True)
     (tr._conv(torch.from_numpy(H(xd)), wr) * torch.from_numpy(_bf16(dy).astype(np.float64))).sum().backward()
     assert scaled_err(H(dw) - 1.0, wr.grad.numpy()) <= 1e-4
+
+
+@pytest.mark.parametrize("n,hw,c,cout", [(2, (320, 320), 64, 2), (2, (160, 160), 128, 4), (4, (80, 80), 256, 8),
+                                         (8, (40, 40), 512, 16), (2, (37, 301), 64, 3)])
+def test_conv_wgrad_dma_matches_register_staged(n, hw, c, cout, wgrad_opts):
+    """The select convs' weight gradients at their training shapes (tower-major sources, many tiles per block): the
+    LDS-DMA kernel against the register-staged one (same GEMM, other K-split): 1e-5 of scale."""
+    from vmatting import ops
+    torch.manual_seed(cout)
+    base = torch.randn(3 * n, hw[0], hw[1], c, device=DEV).to(torch.bfloat16)
+    dy = torch.randn(n, hw[0], hw[1], cout, device=DEV)
+    out = []
+    for dma in (1, 0):
+        wgrad_opts("wgrad_dma", dma)
+        dw = torch.zeros((3, 3, 3 * c, cout), dtype=torch.float32, device=DEV)
+        ops.conv_wgrad(ops.SourceConcat(base, 3), dy, dw, mfma=True)
+        out.append(H(dw).astype(np.float64))
+    assert scaled_err(out[0], out[1]) <= 1e-5
 
 
 @pytest.mark.parametrize("cout", [2, 16])

@@ -164,6 +164,10 @@ __device__ __forceinline__ void wait_vm(int n) {
   switch (n) {
     VM_W(0) VM_W(1) VM_W(2) VM_W(3) VM_W(4) VM_W(5) VM_W(6) VM_W(7) VM_W(8) VM_W(9) VM_W(10) VM_W(11) VM_W(12)
     VM_W(13) VM_W(14) VM_W(15) VM_W(16) VM_W(17) VM_W(18) VM_W(19) VM_W(20) VM_W(21) VM_W(22) VM_W(23) VM_W(24)
+    VM_W(25) VM_W(26) VM_W(27) VM_W(28) VM_W(29) VM_W(30) VM_W(31) VM_W(32) VM_W(33) VM_W(34) VM_W(35) VM_W(36)
+    VM_W(37) VM_W(38) VM_W(39) VM_W(40) VM_W(41) VM_W(42) VM_W(43) VM_W(44) VM_W(45) VM_W(46) VM_W(47) VM_W(48)
+    VM_W(49) VM_W(50) VM_W(51) VM_W(52) VM_W(53) VM_W(54) VM_W(55) VM_W(56) VM_W(57) VM_W(58) VM_W(59) VM_W(60)
+    VM_W(61) VM_W(62) VM_W(63)
     default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
 #undef VM_W

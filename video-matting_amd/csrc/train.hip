@@ -21,6 +21,7 @@
 
 #include <cstring>
 
+#include "conv_common.h"
 #include "vm_common.h"
 
 namespace vm {
@@ -1177,6 +1178,210 @@ constexpr int wgrad_taps_lds() {
   return MAIN > RED ? MAIN : RED;
 }
 
+// ---------------------------------------------------------------- narrow weight gradient, LDS-DMA stream (r05)
+// The select convs' weight gradients (unet_simple.py:120-139 through train.py:288-304's minimize) read 39-315 MB of
+// tower features each for a few GFLOP: a stream.  wgrad_taps_kernel stages one 4 x 32-pixel tile per block in
+// registers and exposes its load latency every step (2.0 TB/s at 320^2, 0.4 TB/s at 40^2 on MI355X; 1.0 ms of the
+// 4.9 ms step).  Here the X tiles and the f32 DY halo patches are DMA'd (buffer_load ... lds) into an S-slot LDS
+// ring, S-1 tiles in flight per block and no staging registers, so two blocks per CU keep ~100 KB in flight.  Same
+// GEMM as wgrad_taps_kernel (taps in N, B from the three pre-shifted bf16 DY planes, built from the landed f32 patch
+// after the ring barrier), same tiles per block and the same MFMA order: the partials are bit-identical to it.
+// The X image keeps wm_off's swizzle by permuting the SOURCE chunk of each LDS position (the DMA writes lane-linear).
+// cout <= 16 (NT <= 9 column tiles); cin a multiple of 8, the block's 16 NCI channels inside one source.
+template <int RB>
+__device__ __forceinline__ void wm_src(int e, int& pe, int& j) {  // LDS chunk e of the X image -> (pixel, chunk)
+  if constexpr (RB == 32) {
+    const int r = e >> 1;
+    pe = r ^ (((r >> 3) & 1) << 2);
+    j = e & 1;
+  } else if constexpr (RB == 64) {
+    const int r = e >> 2, s = e & 3;
+    pe = r;
+    j = 2 * ((s >> 1) ^ ((r >> 3) & 1)) + (s & 1);
+  } else {
+    const int r = e >> 3, s = e & 7;
+    pe = r;
+    j = 2 * ((s >> 1) ^ ((r >> 1) & 1) ^ (((r >> 3) & 1) << 1)) + (s & 1);
+  }
+}
+
+// one 4-byte-per-lane LDS-DMA (buffer_load_dword ... offen lds): lane l writes lds_dst + 4 l (see glds16)
+__device__ __forceinline__ void glds4(__amdgpu_buffer_rsrc_t rsrc, uint32_t lds_dst, int voffset) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dword %1, %3, 0 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voffset), "s"(lds_dst), "s"(rsrc)
+      : "memory");
+}
+
+template <int NCI, int NT, int TH_>
+struct WtDma {
+  static constexpr int TH = TH_, CIB = NCI * 16, RBX = NCI == 1 ? 32 : NCI == 2 ? 64 : 128;
+  static constexpr int XPIX = TH * WM_TW, XCH = CIB / 8, NXC = XPIX * XCH, XPT = (NXC + 255) / 256;
+  static constexpr int DR = TH + 2, COMAX = NT * 16 / 9, NDE = DR * WM_PW * COMAX, DPT = (NDE + 255) / 256;
+  static constexpr int XS = XPT * 256 * 16, DS = DPT * 256 * 4, SLOT = XS + DS, NP = XPT + DPT;
+  static constexpr int PLANES = 3 * COMAX * DR * WM_TW * 2;
+  static constexpr int RED = 2 * NCI * NT * 4 * 64 * 4;
+  template <int S>
+  static constexpr int lds() { return S * SLOT + PLANES > RED ? S * SLOT + PLANES : RED; }
+};
+
+template <int NCI, int NT, int TH_, int S>
+__global__ __launch_bounds__(256, 2) void wgrad_taps_dma_kernel(WgArgs a) {
+  using C = WtDma<NCI, NT, TH_>;
+  constexpr int TH = C::TH, RBX = C::RBX, XPT = C::XPT, DPT = C::DPT, DR = C::DR, NP = C::NP;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int c0 = blockIdx.y * C::CIB;
+  const int cout = a.cout, ndy = DR * WM_PW * cout;
+  uint16_t* dpl = reinterpret_cast<uint16_t*>(smem + S * C::SLOT);  // [3][cout][DR][32]
+  const uint32_t lds0 = lds_addr(smem);
+
+  f32x4 acc[NCI][NT];
+#pragma unroll
+  for (int i = 0; i < NCI; ++i)
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[i][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int g = lane >> 4;
+  int boff[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int n = t * 16 + (lane & 15);
+    if (n < 9 * cout) {
+      const int tap = n / cout, co = n - tap * cout, kh = tap / 3, kw = tap - kh * 3;
+      boff[t] = ((kw * cout + co) * DR + 2 - kh) * WM_TW + 8 * g;
+    } else {
+      boff[t] = -1;
+    }
+  }
+  // this block's channel slice inside its source (the host checks it does not straddle two)
+  const long xsrc = a.x_src_c > 0 ? (long)(c0 / a.x_src_c) * a.x_src_stride + c0 % a.x_src_c : (long)c0;
+  const int t_beg = (int)((long)blockIdx.x * a.ntiles / gridDim.x);
+  const int t_end = (int)((long)(blockIdx.x + 1) * a.ntiles / gridDim.x);
+  const int nsteps = t_end - t_beg;
+  // DMA of step j (tile t_beg + j) into slot j % S; steps past the end load out-of-range zeros, so every thread
+  // issues exactly NP pieces per step and the counted waits stay uniform
+  auto issue = [&](int j) __attribute__((always_inline)) {
+    const bool real = j < nsteps;
+    const int tile = t_beg + (real ? j : 0);
+    const int tx = tile % a.tiles_w, t2 = tile / a.tiles_w;
+    const int y0 = (t2 % a.tiles_h) * TH, n = t2 / a.tiles_h, x0 = tx * WM_TW;
+    const uint16_t* Xn = a.x + (long)n * a.h * a.w * a.xcs + xsrc;
+    const float* Dn = a.dy + (long)n * a.h * a.w * a.dcs;
+    const __amdgpu_buffer_rsrc_t xrs =
+        __builtin_amdgcn_make_buffer_rsrc(uniform_ptr(const_cast<uint16_t*>(Xn)), 0, 0x7ffffff0, 0x00020000);
+    const __amdgpu_buffer_rsrc_t drs =
+        __builtin_amdgcn_make_buffer_rsrc(uniform_ptr(const_cast<float*>(Dn)), 0, 0x7ffffff0, 0x00020000);
+    const uint32_t slot = __builtin_amdgcn_readfirstlane(lds0 + (uint32_t)((j % S) * C::SLOT));
+#pragma unroll
+    for (int k = 0; k < XPT; ++k) {
+      const int e = tid + k * 256;
+      int pe, jj;
+      wm_src<RBX>(e, pe, jj);
+      const int gy = y0 + pe / WM_TW, gx = x0 + pe % WM_TW, c = c0 + jj * 8;
+      const bool ok = real & (e < C::NXC) & (gy < a.h) & (gx < a.w) & (c < a.cin);
+      glds16(xrs, slot + (uint32_t)((k * 256 + wave * 64) * 16), ok ? ((gy * a.w + gx) * a.xcs + jj * 8) * 2 : OOB);
+    }
+#pragma unroll
+    for (int k = 0; k < DPT; ++k) {  // the halo patch, (pixel, co) elements in memory order
+      const int e = tid + k * 256;
+      const int pe = e / cout, co = e - pe * cout;
+      const int gy = y0 - 1 + pe / WM_PW, gx = x0 - 1 + pe % WM_PW;
+      const bool ok = real & (e < ndy) & ((unsigned)gy < (unsigned)a.h) & ((unsigned)gx < (unsigned)a.w);
+      glds4(drs, slot + (uint32_t)(C::XS + (k * 256 + wave * 64) * 4), ok ? ((gy * a.w + gx) * a.dcs + co) * 4 : OOB);
+    }
+  };
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // nothing older in the DMA counts
+#pragma unroll
+  for (int j = 0; j < S - 1; ++j) issue(j);
+  for (int j = 0; j < nsteps; ++j) {
+    // step j landed (this wave's own DMAs; the S-2 younger steps may fly), then everyone's, and every wave's reads
+    // of step j-1 (slot (j-1) % S and the planes) retired
+    wait_vm((S - 2) * NP);
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    issue(j + S - 1);  // into slot (j - 1) % S
+    const char* ximg = smem + (j % S) * C::SLOT;
+    const float* dys = reinterpret_cast<const float*>(ximg + C::XS);
+    for (int e = tid; e < ndy; e += 256) {  // the three pre-shifted bf16 DY planes (wgrad_taps_kernel's commit)
+      const int pe = e / cout, co = e - pe * cout;
+      const int r = pe / WM_PW, pc = pe % WM_PW;
+      const uint16_t v = f2bf(dys[e]);
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        const int jx = pc - 2 + kw;
+        if (jx >= 0 && jx < WM_TW) dpl[((kw * cout + co) * DR + r) * WM_TW + jx] = v;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int rr = 0; rr < TH / 4; ++rr) {  // K-steps: tile rows wave, wave + 4 (wgrad_taps_kernel's order)
+      const int row = wave + 4 * rr;
+      bf16x8 ax[NCI];
+#pragma unroll
+      for (int i = 0; i < NCI; ++i) ax[i] = wm_frag<RBX>(ximg, row * WM_TW + 8 * g, i, lane);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        bf16x8 bd = {};
+        if (boff[t] >= 0) bd = *reinterpret_cast<const bf16x8*>(dpl + boff[t] + row * WM_TW);
+#pragma unroll
+        for (int i = 0; i < NCI; ++i)
+          acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ax[i], bd, acc[i][t], 0, 0, 0);
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // ring drained: LDS reused
+
+  float* red = reinterpret_cast<float*>(smem);
+  constexpr int NA = NCI * NT * 4;
+  auto put = [&](int sl) {
+#pragma unroll
+    for (int i = 0; i < NCI; ++i)
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) red[(sl * NA + (i * NT + t) * 4 + q) * 64 + lane] = acc[i][t][q];
+  };
+  auto add = [&](int sl) {
+#pragma unroll
+    for (int i = 0; i < NCI; ++i)
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[i][t][q] += red[(sl * NA + (i * NT + t) * 4 + q) * 64 + lane];
+  };
+  if (wave >= 2) put(wave - 2);
+  __syncthreads();
+  if (wave < 2) add(wave);
+  __syncthreads();
+  if (wave == 1) put(0);
+  __syncthreads();
+  if (wave == 0) {
+    add(0);
+    float* part = a.part + (long)blockIdx.x * 9 * a.cin * cout;
+    const int ci_l = 4 * g;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int n = t * 16 + (lane & 15);
+      if (n < 9 * cout) {
+        const int tap = n / cout, co = n - tap * cout;
+#pragma unroll
+        for (int i = 0; i < NCI; ++i)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int ci = c0 + i * 16 + ci_l + q;
+            if (ci < a.cin) part[((long)tap * a.cin + ci) * cout + co] = acc[i][t][q];
+          }
+      }
+    }
+  }
+}
+
 // ---------------------------------------------------------------- wide conv weight gradient (UNetImage training)
 // train.py's training_procedure (train.py:37-109) back-propagates through every conv of unet.UNetImage
 // (unet.py:86-148): cin 6 ... 1024, cout 64 ... 512.  dW_t[ci][co] = sum_p X[p + off_t][ci] * DY[p][co] as 9 GEMMs
@@ -1621,6 +1826,61 @@ static int launch_wgrad_taps_t(WgArgs& a, float* dw, hipStream_t st) {
 
 static long g_wgrad_variant = 0;  // A/B knob (vm_set_option "wgrad_variant"): 0/1 4-row tiles, 2 8-row tiles
 static long g_wgrad_taps = 1;     // vm_set_option "wgrad_taps": 0 sends cout <= 8 to wgrad_mfma_kernel (A/B)
+static long g_wgrad_dma = 1;      // vm_set_option "wgrad_dma": 0 = the register-staged narrow kernels (A/B)
+
+// the LDS-DMA narrow weight gradient: cout <= 16, 8-channel chunks, the block's channels inside one source, 32-bit
+// byte offsets inside one image
+static bool wgrad_dma_ok(const WgArgs& a, int cib) {
+  return g_wgrad_dma && a.cout >= 1 && a.cout <= 16 && a.cin % 8 == 0 && a.xcs % 8 == 0 &&
+         reinterpret_cast<uintptr_t>(a.x) % 16 == 0 && (a.x_src_c <= 0 || (a.x_src_c % cib == 0 && a.x_src_stride % 8 == 0)) &&
+         (long)a.h * a.w * a.xcs * 2 < 0x7ff00000L && (long)a.h * a.w * a.dcs * 4 < 0x7ff00000L;
+}
+
+static long g_wgrad_dma_cfg = 0;  // vm_set_option "wgrad_dma_cfg" (A/B): 0 auto, 1 = 8-row tiles, 2 = 4 rows x 6 slots
+
+template <int NCI, int NT, int TH, int S>
+static int launch_wgrad_taps_dma_s(WgArgs& a, float* dw, hipStream_t st) {
+  using C = WtDma<NCI, NT, TH>;
+  static int attr_dev = -1, resident = 0;
+  return launch_wgrad_grid(reinterpret_cast<const void*>(&wgrad_taps_dma_kernel<NCI, NT, TH, S>),
+                           C::template lds<S>(), TH, C::CIB, attr_dev, resident, a, dw, st,
+                           [](dim3 g, int lds, hipStream_t s, const WgArgs& x) {
+                             hipLaunchKernelGGL((wgrad_taps_dma_kernel<NCI, NT, TH, S>), g, dim3(256), lds, s, x);
+                           });
+}
+
+template <int NCI, int NT>
+static int launch_wgrad_taps_dma_t(WgArgs& a, float* dw, hipStream_t st) {
+  // 4 ring slots where two blocks still fit a CU's 160 KB, else 3
+  constexpr int S4 = WtDma<NCI, NT, 4>::template lds<4>() <= 80 * 1024 ? 4 : 3;
+  if (g_wgrad_dma_cfg == 1) return launch_wgrad_taps_dma_s<NCI, NT, 8, 3>(a, dw, st);
+  if (g_wgrad_dma_cfg == 2) return launch_wgrad_taps_dma_s<NCI, NT, 4, 6>(a, dw, st);
+  return launch_wgrad_taps_dma_s<NCI, NT, 4, S4>(a, dw, st);
+}
+
+static int launch_wgrad_taps_dma(WgArgs& a, float* dw, hipStream_t st) {
+  const int nt = (9 * a.cout + 15) / 16;
+  if (nt <= 5 && a.cin > 32) {
+    switch (nt) {
+      case 1: return launch_wgrad_taps_dma_t<4, 1>(a, dw, st);
+      case 2: return launch_wgrad_taps_dma_t<4, 2>(a, dw, st);
+      case 3: return launch_wgrad_taps_dma_t<4, 3>(a, dw, st);
+      case 4: return launch_wgrad_taps_dma_t<4, 4>(a, dw, st);
+      default: return launch_wgrad_taps_dma_t<4, 5>(a, dw, st);
+    }
+  }
+  switch (nt) {
+    case 1: return launch_wgrad_taps_dma_t<2, 1>(a, dw, st);
+    case 2: return launch_wgrad_taps_dma_t<2, 2>(a, dw, st);
+    case 3: return launch_wgrad_taps_dma_t<2, 3>(a, dw, st);
+    case 4: return launch_wgrad_taps_dma_t<2, 4>(a, dw, st);
+    case 5: return launch_wgrad_taps_dma_t<2, 5>(a, dw, st);
+    case 6: return launch_wgrad_taps_dma_t<2, 6>(a, dw, st);
+    case 7: return launch_wgrad_taps_dma_t<2, 7>(a, dw, st);
+    case 8: return launch_wgrad_taps_dma_t<2, 8>(a, dw, st);
+    default: return launch_wgrad_taps_dma_t<2, 9>(a, dw, st);
+  }
+}
 }  // namespace trn
 
 int train_set_option(const char* key, long value) {
@@ -1632,6 +1892,14 @@ int train_set_option(const char* key, long value) {
     trn::g_wgrad_taps = value;
     return 1;
   }
+  if (!strcmp(key, "wgrad_dma")) {
+    trn::g_wgrad_dma = value;
+    return 1;
+  }
+  if (!strcmp(key, "wgrad_dma_cfg")) {
+    trn::g_wgrad_dma_cfg = value;
+    return 1;
+  }
   return 0;
 }
 
@@ -1640,6 +1908,7 @@ namespace trn {
 static int launch_wgrad_mfma(WgArgs& a, float* dw, hipStream_t st) {
   WmCfg c = wgrad_mfma_cfg(a.cin, a.cout);
   const bool th8 = g_wgrad_variant == 2;
+  if (wgrad_dma_ok(a, (9 * a.cout + 15) / 16 <= 5 && a.cin > 32 ? 64 : 32)) return launch_wgrad_taps_dma(a, dw, st);
   if (c.nt && g_wgrad_taps) {
 #define VM_WT(NCI, NT) \
   return th8 ? launch_wgrad_taps_t<NCI, NT, 8>(a, dw, st) : launch_wgrad_taps_t<NCI, NT, 4>(a, dw, st)
@@ -1999,7 +2268,12 @@ extern "C" size_t vm_conv3x3_wgrad_ex_workspace_bytes(int n, int h, int w, int c
     return (size_t)wgrad_wide_gx(n, h, w, cin, cout, mode != 1) * 9 * cin * cout * sizeof(float);
   if (mode != 1) return (size_t)wgrad_rows(n, h, w, cin, cout, wgrad_cc(cout)) * 9 * cin * cout * sizeof(float);
   const WmCfg c = wgrad_mfma_cfg(cin, cout);
-  return (size_t)wgrad_rows(n, h, w, cin, cout, c.nci * 16) * 9 * cin * cout * sizeof(float);
+  long rows = wgrad_rows(n, h, w, cin, cout, c.nci * 16);
+  if (cout <= 16) {  // the LDS-DMA narrow kernel may take 64-channel blocks (fewer of them, more rows each)
+    const long r64 = wgrad_rows(n, h, w, cin, cout, 64);
+    if (r64 > rows) rows = r64;
+  }
+  return (size_t)rows * 9 * cin * cout * sizeof(float);
 }
 
 extern "C" int vm_conv3x3_wgrad_ex_nhwc(const vm_tensor* x, int x_src_c, long x_src_stride, const vm_tensor* dy,
