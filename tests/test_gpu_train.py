@@ -552,12 +552,12 @@ def wgrad_opts():
     yield _lib.set_option
     _lib.set_option("wgrad_taps", 1)
     _lib.set_option("wgrad_variant", 0)
-    _lib.set_option("wgrad_dma", 1)
+    _lib.set_option("wgrad_dma", 0)
 
 
-# (wgrad_taps, wgrad_variant, wgrad_dma): the LDS-DMA narrow kernel (cout <= 16, cin % 8 == 0; the default), the
-# register-staged taps-in-N kernel for cout <= 8 with 4- and 8-row tiles, and the per-tap kernel
-WGRAD_VARIANTS = [(1, 0, 1), (1, 0, 0), (1, 2, 0), (0, 0, 0)]
+# (wgrad_taps, wgrad_variant, wgrad_dma): the register-staged taps-in-N kernel for cout <= 8 (the default), the LDS-DMA
+# narrow kernel (an A/B option: cout <= 16, cin % 8 == 0), the taps kernel with 8-row tiles, and the per-tap kernel
+WGRAD_VARIANTS = [(1, 0, 0), (1, 0, 1), (1, 2, 0), (0, 0, 0)]
 
 
 @pytest.mark.parametrize("variant", WGRAD_VARIANTS)
@@ -569,7 +569,7 @@ def test_conv_wgrad_mfma(cin, cs, cout, variant, wgrad_opts):
     from vmatting import ops
     if cout > 16 and variant != WGRAD_VARIANTS[0]:
         pytest.skip("the options only route cout <= 16")
-    if cout > 8 and variant[2] == 0 and variant != WGRAD_VARIANTS[1]:
+    if cout > 8 and variant[2] == 0 and variant != WGRAD_VARIANTS[0]:
         pytest.skip("the taps option only routes cout <= 8")
     wgrad_opts("wgrad_taps", variant[0])
     wgrad_opts("wgrad_variant", variant[1])

@@ -20,6 +20,7 @@ def main():
     cfgs = [tuple(int(v) for v in a.split(":")) for a in sys.argv[2:]] or [(0, 0), (1, 0)]
     n = 8
     tot = {c: 0.0 for c in cfgs}
+    flush = None if os.environ.get("NO_FLUSH") else torch.empty(256 << 20, device="cuda")  # 1 GiB
     for name, s, c, cout in SHAPES:
         base = torch.randn(3 * n, s, s, c, device="cuda").to(torch.bfloat16)
         x = ops.SourceConcat(base, 3)
@@ -31,13 +32,17 @@ def main():
             _lib.set_option("wgrad_dma_cfg", cfg[1])
             for _ in range(3):
                 ops.conv_wgrad(x, dy, dw, mfma=True)
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
+            ev = []
             for _ in range(iters):
+                if flush is not None:  # evict L2 / MALL: x streams from HBM, as inside the training step
+                    flush.fill_(1.0)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
                 ops.conv_wgrad(x, dy, dw, mfma=True)
-            e1.record()
+                e1.record()
+                ev.append((e0, e1))
             torch.cuda.synchronize()
-            ms = e0.elapsed_time(e1) / iters
+            ms = sum(a.elapsed_time(b) for a, b in ev) / iters
             tot[cfg] += ms
             line.append("dma%d:cfg%d %.4f ms %6.0f GB/s" % (cfg[0], cfg[1], ms, base.numel() * 2 / ms / 1e6))
         print("%-10s %3d^2 %4d->%-2d  %s" % (name, s, 3 * c, cout, " | ".join(line)), flush=True)

@@ -1826,7 +1826,10 @@ static int launch_wgrad_taps_t(WgArgs& a, float* dw, hipStream_t st) {
 
 static long g_wgrad_variant = 0;  // A/B knob (vm_set_option "wgrad_variant"): 0/1 4-row tiles, 2 8-row tiles
 static long g_wgrad_taps = 1;     // vm_set_option "wgrad_taps": 0 sends cout <= 8 to wgrad_mfma_kernel (A/B)
-static long g_wgrad_dma = 1;      // vm_set_option "wgrad_dma": 0 = the register-staged narrow kernels (A/B)
+// vm_set_option "wgrad_dma": 1 = the LDS-DMA narrow kernel.  Off: measured at the config-5 select shapes with L2 /
+// MALL flushed between calls (tools/selectwgrad_bench.py, MI355X) it streams x no faster than the register-staged
+// kernels (select1 136 vs 128 us, 2.3-2.5 TB/s; select4 150 vs 42 us: its f32 DY patch outweighs the 40^2 X tile)
+static long g_wgrad_dma = 0;
 
 // the LDS-DMA narrow weight gradient: cout <= 16, 8-channel chunks, the block's channels inside one source, 32-bit
 // byte offsets inside one image
