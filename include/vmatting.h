@@ -401,6 +401,38 @@ int vm_nonzero_stats(const void* alpha, int h, int w, int dtype, long long* stat
  * uint8(255. * alpha[p])] (the product in the alpha's precision, f64 / f32, truncated like numpy's astype). */
 int vm_bgra_u8(const uint8_t* fg, const void* alpha, int alpha_dtype, long pixels, uint8_t* out, void* stream);
 
+/* augmentation.augment (augmentation.py:101-135) for a batch of samples in four launches per 4 samples (the
+ * config-5 pipeline, vmatting.augmentation.augment_many): per sample the TPS lattice of tps._make_inverse_warp
+ * (output region (0, 0, h, w), approximate_grid 2), ONE resampling pass for the fg planes and the alpha through its
+ * upsampled map (tps.warp_images, order 1), the fused translate + similarity warps (vm_warp_image) of the background
+ * (its own size, camera motion) and of the resampled fg / alpha (object motion), and change_illumination with the
+ * sample's S/V map on fg and bg.  Bit-identical to the per-sample entry points.  The np.random draws, the TPS solve
+ * and the maps stay on the host (the caller's), as in vm_tps_grid / vm_warp_image. */
+typedef struct vm_augment_job {
+  const uint8_t* fg;        /* [h, w, 3] u8 BGR (device) */
+  const uint8_t* bg;        /* [bg_h, bg_w, 3] u8 BGR */
+  const double* alpha;      /* [h, w] f64 */
+  const double* tps_points; /* [npts, 2] f64 (device): the deformed landmarks, the reverse map's from-points */
+  const double* tps_coeffs; /* [npts + 3, 2] f64 (device): their solve, tps._make_warp (pinv(L) @ [landmarks; 0]) */
+  void* scratch;            /* vm_augment_scratch_bytes(h, w) device bytes (lattice, resampled fg and alpha) */
+  uint8_t* new_fg;          /* [h, w, 3] u8 */
+  uint8_t* new_bg;          /* [bg_h, bg_w, 3] u8 */
+  double* new_alpha;        /* [h, w] f64 */
+  int32_t h, w, bg_h, bg_w, npts;
+  int32_t tu_bg, tv_bg, tu_fg, tv_fg;
+  int32_t reserved;
+  double m_bg[6];           /* the forward getRotationMatrix2D matrices (host values), inverted as warpAffine does */
+  double m_fg[6];
+  uint8_t lut[256];         /* change_illumination's S/V map (augmentation.py:89-95), shared by fg and bg */
+} vm_augment_job;
+size_t vm_augment_scratch_bytes(int h, int w);
+int vm_augment_batch(const vm_augment_job* jobs, int n, void* stream);
+
+/* vm_nonzero_stats for n f64 alphas (host arrays of device pointers and sizes) in one launch per 8: stats is device
+ * int64 [n][3] (count, row-index sum, column-index sum per alpha). */
+int vm_nonzero_stats_batch(const double* const* alphas, const int* h, const int* w, int n, long long* stats,
+                           void* stream);
+
 /* data.trimap_from_matte (data.py:37-67; the reference uses dilate 1, crop 3): trimap u8 [h, w] from a float64
  * matte [h, w] (device), 255 / 0 where the matte is exactly 1 / 0, 128 elsewhere and — reproducing the reference's
  * raster-order overwrites — on 1-pixels (0-pixels) with a non-0/1 pixel later in raster order within crop (dilate)

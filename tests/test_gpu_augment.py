@@ -337,6 +337,36 @@ def test_augment_many_equals_sequential_augment():
     assert st[0][0] == int(np.count_nonzero(triples[0][2]))
 
 
+@pytest.mark.parametrize("shapes", [[(1080, 1920)] * 5, [(37, 51), (64, 64), (120, 160), (9, 300)]])
+def test_augment_batch_equals_per_sample_kernels(shapes, monkeypatch):
+    """vm_augment_batch (TPS lattice, the shared fg + alpha resampling pass and the fused warps, 4 samples per launch)
+    returns what the per-sample entry points (vm_tps_grid / vm_tps_sample / vm_warp_image) return, bit for bit, for
+    batches of 5 1080p samples and of mixed small sizes; and vm_nonzero_stats_batch the per-alpha statistics."""
+    from vmatting import augmentation as va
+    rs = np.random.RandomState(len(shapes))
+    triples = []
+    for h, w in shapes:
+        yy, xx = np.mgrid[0:h, 0:w]
+        al = np.clip(1.3 - np.hypot((yy - 0.45 * h) / (0.3 * h), (xx - 0.5 * w) / (0.25 * w)), 0, 1)
+        triples.append(tuple(torch.from_numpy(np.ascontiguousarray(a)).cuda() for a in
+                             ((rs.rand(h, w, 3) * 255).astype(np.uint8), (rs.rand(h, w, 3) * 255).astype(np.uint8),
+                              al)))
+    np.random.seed(3)
+    got = va.augment_many(triples)
+    monkeypatch.setattr(va, "_BATCH", False)
+    np.random.seed(3)
+    want = va.augment_many(triples)
+    torch.cuda.synchronize()
+    for a, b in zip(got, want):
+        for x, y in zip(a, b):
+            assert x.shape == y.shape and torch.equal(x, y)
+    st = torch.empty((len(triples), 3), dtype=torch.int64, device="cuda")
+    va._stats_into([t[2] for t in triples], st)
+    for i, t in enumerate(triples):
+        from vmatting import ops
+        assert torch.equal(st[i], ops.nonzero_stats(t[2]))
+
+
 @pytest.mark.parametrize("adt", [np.float64, np.float32])
 def test_bgra_matches_numpy(adt):
     """vm_bgra_u8 == np.concatenate((fg, (255. * alpha[..., None]).astype(np.uint8)), 2) (augmentation.py:154-155)."""

@@ -53,9 +53,9 @@ __device__ __forceinline__ void for_pixels(long total, int cn, T* __restrict__ o
 // x_i = i*x_step + x_lo (np.mgrid), f = a1 + ax*x + ay*y + sum_k w_k * U(r_k), U(r) = (r*r)*log(r), 0 below
 // 1e-100 (tps.py:80-81).  Both coordinates share the distance evaluation; each keeps its own accumulator in the
 // reference's order.
-__global__ void tps_grid_kernel(const double* __restrict__ pts, const double* __restrict__ coef, int npts, int nx,
-                                int ny, double x_lo, double x_step, double y_lo, double y_step,
-                                double* __restrict__ grid) {
+__device__ __forceinline__ void tps_grid_body(const double* __restrict__ pts, const double* __restrict__ coef,
+                                              int npts, int nx, int ny, double x_lo, double x_step, double y_lo,
+                                              double y_step, double* __restrict__ grid) {
   const long total = (long)nx * ny;
   const double a1x = coef[2 * npts], a1y = coef[2 * npts + 1];
   const double axx = coef[2 * npts + 2], axy = coef[2 * npts + 3];
@@ -75,6 +75,12 @@ __global__ void tps_grid_kernel(const double* __restrict__ pts, const double* __
     grid[i] = a1x + axx * x + ayx * y + sx;
     grid[total + i] = a1y + axy * x + ayy * y + sy;
   }
+}
+
+__global__ void tps_grid_kernel(const double* __restrict__ pts, const double* __restrict__ coef, int npts, int nx,
+                                int ny, double x_lo, double x_step, double y_lo, double y_step,
+                                double* __restrict__ grid) {
+  tps_grid_body(pts, coef, npts, nx, ny, x_lo, x_step, y_lo, y_step, grid);
 }
 
 // One axis of the grid upsampling (tps.py:55-63): frac, idx = modf((steps - 1) * u / span); idx1 =
@@ -404,6 +410,217 @@ __global__ void __launch_bounds__(256) nonzero_stats_kernel(const T* __restrict_
 }
 
 
+// ---------------------------------------------------------------------------------------------------- batches
+// augmentation.augment over a batch of samples (augment_many: the config-5 pipeline) in a handful of launches: every
+// launch takes up to kAugJobs samples' parameters by value (grid.y = the sample), so a batch of 8 costs 2 x 4
+// launches where the per-sample calls cost 8 x 6 (their ~25 us of host issue each bounded the chained step).  Per
+// pixel the arithmetic is the per-sample kernels' own (tps_grid_body, the UP / order-1 path of tps_sample_kernel,
+// warp_image_kernel): outputs bit-identical.  The fg and alpha TPS resamplings share one map, so they are ONE pass
+// here (one upsampled coordinate per pixel, then the 3 u8 and the f64 taps).
+constexpr int kAugJobs = 4;
+
+struct AugGridJobs {
+  const double* pts[kAugJobs];
+  const double* coef[kAugJobs];
+  double* grid[kAugJobs];
+  int npts[kAugJobs], nx[kAugJobs], ny[kAugJobs];
+  double xstep[kAugJobs], ystep[kAugJobs];
+};
+
+__global__ void __launch_bounds__(256) tps_grid_batch_kernel(AugGridJobs J) {
+  const int j = blockIdx.y;
+  tps_grid_body(J.pts[j], J.coef[j], J.npts[j], J.nx[j], J.ny[j], 0.0, J.xstep[j], 0.0, J.ystep[j], J.grid[j]);
+}
+
+struct AugSampleJobs {
+  const double* grid[kAugJobs];
+  const uint8_t* fg[kAugJobs];
+  const double* al[kAugJobs];
+  uint8_t* fg_t[kAugJobs];
+  double* al_t[kAugJobs];
+  int h[kAugJobs], w[kAugJobs], nx[kAugJobs], ny[kAugJobs];
+  double xsteps[kAugJobs], ysteps[kAugJobs];
+};
+
+// tps.warp_images' resampling of the fg planes (u8) and of the alpha plane (f64) through the same upsampled map
+// (tps.py:55-74, output (h+1) x (w+1)): tps_sample_kernel<uint8_t, 1, true> and <double, 1, true> in one pass
+__global__ void __launch_bounds__(256) tps_sample_pair_kernel(AugSampleJobs J) {
+  const int j = blockIdx.y;
+  const int ih = J.h[j], iw = J.w[j], oh = ih + 1, ow = iw + 1, nx = J.nx[j], ny = J.ny[j];
+  const double* __restrict__ grid = J.grid[j];
+  const uint8_t* __restrict__ img = J.fg[j];
+  const double* __restrict__ al = J.al[j];
+  double* __restrict__ alt = J.al_t[j];
+  const long total = (long)oh * ow, gsz = (long)nx * ny;
+  const double xsteps = J.xsteps[j], ysteps = J.ysteps[j];
+  for_pixels(total, 3, J.fg_t[j], [&](long i, uint8_t* o) {
+    const int oy = row_of(i, ow), ox = (int)(i - (long)oy * ow);
+    const UpAxis ax = up_axis(oy, xsteps, ih);
+    const UpAxis ay = up_axis(ox, ysteps, iw);
+    const long a00 = (long)ax.i0 * ny + ay.i0, a01 = (long)ax.i0 * ny + ay.i1;
+    const long a10 = (long)ax.i1 * ny + ay.i0, a11 = (long)ax.i1 * ny + ay.i1;
+    const double tr = grid[a00] * ax.f1 * ay.f1 + grid[a01] * ax.f1 * ay.f + grid[a10] * ax.f * ay.f1 +
+                      grid[a11] * ax.f * ay.f;
+    const double tc = grid[gsz + a00] * ax.f1 * ay.f1 + grid[gsz + a01] * ax.f1 * ay.f +
+                      grid[gsz + a10] * ax.f * ay.f1 + grid[gsz + a11] * ax.f * ay.f;
+    const bool inside = tr >= 0.0 && tr <= (double)(ih - 1) && tc >= 0.0 && tc <= (double)(iw - 1);
+    if (!inside) {
+      o[0] = o[1] = o[2] = 0;
+      alt[i] = 0.0;
+      return;
+    }
+    const double fr0 = floor(tr), fc0 = floor(tc);
+    const int r0 = (int)fr0, c0 = (int)fc0;
+    const double fr = tr - fr0, fc = tc - fc0;
+    const double wr0 = 1.0 - fr, wr1 = 1.0 - wr0, wc0 = 1.0 - fc, wc1 = 1.0 - wc0;
+    const bool r1ok = r0 + 1 < ih, c1ok = c0 + 1 < iw;
+    const uint8_t* p00 = img + ((long)r0 * iw + c0) * 3;
+    for (int k = 0; k < 3; ++k) {
+      const double v00 = (double)p00[k];
+      const double v01 = c1ok ? (double)p00[3 + k] : 0.0;
+      const double v10 = r1ok ? (double)p00[(long)iw * 3 + k] : 0.0;
+      const double v11 = (r1ok && c1ok) ? (double)p00[((long)iw + 1) * 3 + k] : 0.0;
+      double t = 0.0;
+      t += (v00 * wr0) * wc0;
+      t += (v01 * wr0) * wc1;
+      t += (v10 * wr1) * wc0;
+      t += (v11 * wr1) * wc1;
+      o[k] = from_f64<uint8_t>(t);
+    }
+    const double* q00 = al + (long)r0 * iw + c0;
+    const double v00 = q00[0];
+    const double v01 = c1ok ? q00[1] : 0.0;
+    const double v10 = r1ok ? q00[iw] : 0.0;
+    const double v11 = (r1ok && c1ok) ? q00[iw + 1] : 0.0;
+    double t = 0.0;
+    t += (v00 * wr0) * wc0;
+    t += (v01 * wr0) * wc1;
+    t += (v10 * wr1) * wc0;
+    t += (v11 * wr1) * wc1;
+    alt[i] = t;
+  });
+}
+
+// warp_image_kernel's per-pixel work, one job per blockIdx.y
+template <typename T, bool ILLUM>
+__device__ __forceinline__ void warp_image_body(const T* __restrict__ src, int ih, int iw, int cn, int tu, int tv,
+                                                const Affine& a, const Lut256& lut, const int* sdiv, const int* hdiv,
+                                                T* __restrict__ dst, int h, int w) {
+  const long total = (long)h * w;
+  for_pixels(total, cn, dst, [&](long i, T* o) {
+    const int y = row_of(i, w), x = (int)(i - (long)y * w);
+    const int adelta = cv_round(a.m[0] * (double)x * 1024.0);
+    const int bdelta = cv_round(a.m[3] * (double)x * 1024.0);
+    const int X0 = cv_round((a.m[1] * (double)y + a.m[2]) * 1024.0) + 16;
+    const int Y0 = cv_round((a.m[4] * (double)y + a.m[5]) * 1024.0) + 16;
+    const int X = (X0 + adelta) >> 5, Y = (Y0 + bdelta) >> 5;
+    int sx = X >> 5, sy = Y >> 5;
+    sx = sx < -32768 ? -32768 : (sx > 32767 ? 32767 : sx);
+    sy = sy < -32768 ? -32768 : (sy > 32767 ? 32767 : sy);
+    const int ax = X & 31, ay = Y & 31;
+    auto ok = [&](int ty, int tx) {
+      return (unsigned)ty < (unsigned)h && (unsigned)tx < (unsigned)w && (unsigned)(ty - tv) < (unsigned)ih &&
+             (unsigned)(tx - tu) < (unsigned)iw;
+    };
+    const bool k0 = ok(sy, sx), k1 = ok(sy, sx + 1), k2 = ok(sy + 1, sx), k3 = ok(sy + 1, sx + 1);
+    const T* p = src + ((long)(sy - tv) * iw + (sx - tu)) * cn;
+    uint8_t px[8];
+    for (int k = 0; k < cn; ++k) {
+      const T v0 = k0 ? p[k] : T(0);
+      const T v1 = k1 ? p[cn + k] : T(0);
+      const T v2 = k2 ? p[(long)iw * cn + k] : T(0);
+      const T v3 = k3 ? p[((long)iw + 1) * cn + k] : T(0);
+      if constexpr (sizeof(T) == 1) {
+        const int s = (int)v0 * ((32 - ay) * (32 - ax) * 32) + (int)v1 * ((32 - ay) * ax * 32) +
+                      (int)v2 * (ay * (32 - ax) * 32) + (int)v3 * (ay * ax * 32);
+        const int r = (s + (1 << 14)) >> 15;
+        const T q = (T)(r < 0 ? 0 : (r > 255 ? 255 : r));
+        if constexpr (ILLUM) px[k] = q;
+        else o[k] = q;
+      } else {
+        const float wy0 = 1.f - (float)ay * (1.f / 32.f), wy1 = (float)ay * (1.f / 32.f);
+        const float wx0 = 1.f - (float)ax * (1.f / 32.f), wx1 = (float)ax * (1.f / 32.f);
+        const T w0 = (T)(wy0 * wx0), w1 = (T)(wy0 * wx1), w2 = (T)(wy1 * wx0), w3 = (T)(wy1 * wx1);
+        o[k] = v0 * w0 + v1 * w1 + v2 * w2 + v3 * w3;
+      }
+    }
+    if constexpr (ILLUM) illum_px(px[0], px[1], px[2], lut, sdiv, hdiv, reinterpret_cast<uint8_t*>(o));
+  });
+}
+
+// the u8 BGR warps + illumination of a batch: job 2s = sample s's background (camera motion), 2s + 1 its TPS-resampled
+// foreground (object motion); both through sample s's S/V map (augmentation.py:127-134)
+struct AugWarpU8Jobs {
+  const uint8_t* src[2 * kAugJobs];
+  uint8_t* dst[2 * kAugJobs];
+  int ih[2 * kAugJobs], iw[2 * kAugJobs], h[2 * kAugJobs], w[2 * kAugJobs], tu[2 * kAugJobs], tv[2 * kAugJobs];
+  Affine a[2 * kAugJobs];
+  Lut256 lut[kAugJobs];
+};
+
+__global__ void __launch_bounds__(256) warp_u8_illum_batch_kernel(AugWarpU8Jobs J) {
+  __shared__ int sdiv[256], hdiv[256];
+  illum_tables(sdiv, hdiv);
+  const int j = blockIdx.y;
+  warp_image_body<uint8_t, true>(J.src[j], J.ih[j], J.iw[j], 3, J.tu[j], J.tv[j], J.a[j], J.lut[j >> 1], sdiv, hdiv,
+                                 J.dst[j], J.h[j], J.w[j]);
+}
+
+struct AugWarpF64Jobs {
+  const double* src[kAugJobs];
+  double* dst[kAugJobs];
+  int ih[kAugJobs], iw[kAugJobs], h[kAugJobs], w[kAugJobs], tu[kAugJobs], tv[kAugJobs];
+  Affine a[kAugJobs];
+};
+
+__global__ void __launch_bounds__(256) warp_f64_batch_kernel(AugWarpF64Jobs J) {
+  const int j = blockIdx.y;
+  const Lut256 none{};
+  warp_image_body<double, false>(J.src[j], J.ih[j], J.iw[j], 1, J.tu[j], J.tv[j], J.a[j], none, nullptr, nullptr,
+                                 J.dst[j], J.h[j], J.w[j]);
+}
+
+// the foreground statistics of a batch of alphas, one launch (grid.y = the alpha)
+struct AugStatsJobs {
+  const double* a[2 * kAugJobs];
+  int h[2 * kAugJobs], w[2 * kAugJobs];
+};
+
+__global__ void __launch_bounds__(256) nonzero_stats_batch_kernel(AugStatsJobs J, unsigned long long* __restrict__ stats) {
+  const int j = blockIdx.y;
+  const int h = J.h[j], w = J.w[j];
+  const double* a = J.a[j];
+  unsigned long long cnt = 0, sr = 0, sc = 0;
+  for (int r = blockIdx.x; r < h; r += gridDim.x) {
+    const double* row = a + (long)r * w;
+    for (int c = threadIdx.x; c < w; c += blockDim.x) {
+      if (row[c] != 0.0) {
+        ++cnt;
+        sr += (unsigned long long)r;
+        sc += (unsigned long long)c;
+      }
+    }
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    cnt += __shfl_xor(cnt, off, 64);
+    sr += __shfl_xor(sr, off, 64);
+    sc += __shfl_xor(sc, off, 64);
+  }
+  __shared__ unsigned long long part[3][4];
+  const int wv = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    part[0][wv] = cnt;
+    part[1][wv] = sr;
+    part[2][wv] = sc;
+  }
+  __syncthreads();
+  if (threadIdx.x < 3) {
+    unsigned long long v = 0;
+    for (int k = 0; k < (int)(blockDim.x >> 6); ++k) v += part[threadIdx.x][k];
+    if (v) atomicAdd(&stats[3 * j + threadIdx.x], v);
+  }
+}
+
 // ---------------------------------------------------------------------------------------------------- data.py
 
 // data.trimap_from_matte (data.py:37-67).  The reference's raster loop lets a known pixel's own assignment (255 for
@@ -653,4 +870,138 @@ extern "C" int vm_trimap_from_matte(const double* matte, int h, int w, int dilat
   const dim3 g((w + kTriW - 1) / kTriW, (h + kTriH - 1) / kTriH), b(256);
   hipLaunchKernelGGL(trimap_kernel, g, b, 0, st, matte, h, w, dilate, crop, trimap);
   return check_launch("trimap_from_matte");
+}
+
+// ---------------------------------------------------------------------------------------------------- batches (C ABI)
+// scratch of one sample: the TPS lattice [2][h/2][w/2] f64, the resampled fg [(h+1)(w+1)][3] u8 and alpha f64
+static void aug_lattice(int h, int w, int& nx, int& ny, double& xstep, double& ystep, double& xsteps, double& ysteps) {
+  // tps._make_inverse_warp with output_region (0, 0, h, w), approximate_grid 2 (augmentation.py:49-54): x_steps =
+  // h / 2 (a float), np.mgrid[0:h:x_steps*1j] -> int(x_steps) points, step h / (count - 1) (tps.py:46-51, 55-63)
+  xsteps = (double)h / 2.0;
+  ysteps = (double)w / 2.0;
+  nx = (int)xsteps;
+  ny = (int)ysteps;
+  xstep = nx > 1 ? (double)h / (double)(nx - 1) : 1.0;
+  ystep = ny > 1 ? (double)w / (double)(ny - 1) : 1.0;
+}
+
+static size_t al16(size_t b) { return (b + 255) & ~(size_t)255; }
+
+extern "C" size_t vm_augment_scratch_bytes(int h, int w) {
+  if (h <= 0 || w <= 0) return 0;
+  int nx, ny;
+  double a, b, c, d;
+  aug_lattice(h, w, nx, ny, a, b, c, d);
+  const size_t px = (size_t)(h + 1) * (w + 1);
+  return al16(2 * (size_t)nx * ny * 8) + al16(px * 3) + al16(px * 8);
+}
+
+extern "C" int vm_augment_batch(const vm_augment_job* jobs, int n, void* stream) {
+  if (!jobs || n <= 0) return fail(VM_EINVAL, "augment_batch: bad argument");
+  for (int i = 0; i < n; ++i) {
+    const vm_augment_job& q = jobs[i];
+    if (!q.fg || !q.bg || !q.alpha || !q.tps_points || !q.tps_coeffs || !q.scratch || !q.new_fg || !q.new_bg ||
+        !q.new_alpha || q.h < 4 || q.w < 4 || q.bg_h <= 0 || q.bg_w <= 0 || q.npts <= 0)
+      return fail(VM_EINVAL, "augment_batch: job %d: bad argument", i);
+    if ((long)(q.h + 1) * (q.w + 1) >= (1L << 31) || (long)q.bg_h * q.bg_w >= (1L << 31))
+      return fail(VM_EUNSUPPORTED, "augment_batch: job %d: more than 2^31 pixels", i);
+  }
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  for (int b0 = 0; b0 < n; b0 += kAugJobs) {
+    const int m = n - b0 < kAugJobs ? n - b0 : kAugJobs;
+    AugGridJobs G{};
+    AugSampleJobs S{};
+    AugWarpU8Jobs U{};
+    AugWarpF64Jobs F{};
+    long gmax = 1, pmax = 1, wmax = 1;
+    for (int k = 0; k < m; ++k) {
+      const vm_augment_job& q = jobs[b0 + k];
+      int nx, ny;
+      double xstep, ystep, xsteps, ysteps;
+      aug_lattice(q.h, q.w, nx, ny, xstep, ystep, xsteps, ysteps);
+      char* sc = static_cast<char*>(q.scratch);
+      double* grid = reinterpret_cast<double*>(sc);
+      const size_t px = (size_t)(q.h + 1) * (q.w + 1);
+      uint8_t* fg_t = reinterpret_cast<uint8_t*>(sc + al16(2 * (size_t)nx * ny * 8));
+      double* al_t = reinterpret_cast<double*>(sc + al16(2 * (size_t)nx * ny * 8) + al16(px * 3));
+      G.pts[k] = q.tps_points;
+      G.coef[k] = q.tps_coeffs;
+      G.grid[k] = grid;
+      G.npts[k] = q.npts;
+      G.nx[k] = nx;
+      G.ny[k] = ny;
+      G.xstep[k] = xstep;
+      G.ystep[k] = ystep;
+      gmax = gmax > (long)nx * ny ? gmax : (long)nx * ny;
+      S.grid[k] = grid;
+      S.fg[k] = q.fg;
+      S.al[k] = q.alpha;
+      S.fg_t[k] = fg_t;
+      S.al_t[k] = al_t;
+      S.h[k] = q.h;
+      S.w[k] = q.w;
+      S.nx[k] = nx;
+      S.ny[k] = ny;
+      S.xsteps[k] = xsteps;
+      S.ysteps[k] = ysteps;
+      pmax = pmax > (long)px ? pmax : (long)px;
+      // camera motion on the background (its own size), object motion on the resampled foreground
+      U.src[2 * k] = q.bg;
+      U.dst[2 * k] = q.new_bg;
+      U.ih[2 * k] = U.h[2 * k] = q.bg_h;
+      U.iw[2 * k] = U.w[2 * k] = q.bg_w;
+      U.tu[2 * k] = q.tu_bg;
+      U.tv[2 * k] = q.tv_bg;
+      U.a[2 * k] = invert_affine(q.m_bg);
+      U.src[2 * k + 1] = fg_t;
+      U.dst[2 * k + 1] = q.new_fg;
+      U.ih[2 * k + 1] = q.h + 1;
+      U.iw[2 * k + 1] = q.w + 1;
+      U.h[2 * k + 1] = q.h;
+      U.w[2 * k + 1] = q.w;
+      U.tu[2 * k + 1] = q.tu_fg;
+      U.tv[2 * k + 1] = q.tv_fg;
+      U.a[2 * k + 1] = invert_affine(q.m_fg);
+      for (int i = 0; i < 256; ++i) U.lut[k].t[i] = q.lut[i];
+      const long wpx = (long)q.h * q.w > (long)q.bg_h * q.bg_w ? (long)q.h * q.w : (long)q.bg_h * q.bg_w;
+      wmax = wmax > wpx ? wmax : wpx;
+      F.src[k] = al_t;
+      F.dst[k] = q.new_alpha;
+      F.ih[k] = q.h + 1;
+      F.iw[k] = q.w + 1;
+      F.h[k] = q.h;
+      F.w[k] = q.w;
+      F.tu[k] = q.tu_fg;
+      F.tv[k] = q.tv_fg;
+      F.a[k] = U.a[2 * k + 1];
+    }
+    hipLaunchKernelGGL(tps_grid_batch_kernel, dim3(grid_for(gmax, 256, 1024), m), dim3(256), 0, st, G);
+    hipLaunchKernelGGL(tps_sample_pair_kernel, dim3(grid_for(pmax, 256, 1024), m), dim3(256), 0, st, S);
+    hipLaunchKernelGGL(warp_u8_illum_batch_kernel, dim3(grid_for(wmax, 256, 1024), 2 * m), dim3(256), 0, st, U);
+    hipLaunchKernelGGL(warp_f64_batch_kernel, dim3(grid_for(wmax, 256, 1024), m), dim3(256), 0, st, F);
+  }
+  return check_launch("augment_batch");
+}
+
+extern "C" int vm_nonzero_stats_batch(const double* const* alphas, const int* h, const int* w, int n,
+                                      long long* stats, void* stream) {
+  if (!alphas || !h || !w || !stats || n <= 0) return fail(VM_EINVAL, "nonzero_stats_batch: bad argument");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (hipMemsetAsync(stats, 0, 3 * sizeof(long long) * (size_t)n, st) != hipSuccess)
+    return fail(VM_EHIP, "nonzero_stats_batch: memset");
+  for (int b0 = 0; b0 < n; b0 += 2 * kAugJobs) {
+    const int m = n - b0 < 2 * kAugJobs ? n - b0 : 2 * kAugJobs;
+    AugStatsJobs J{};
+    int hmax = 1;
+    for (int k = 0; k < m; ++k) {
+      if (!alphas[b0 + k] || h[b0 + k] <= 0 || w[b0 + k] <= 0) return fail(VM_EINVAL, "nonzero_stats_batch: job %d", b0 + k);
+      J.a[k] = alphas[b0 + k];
+      J.h[k] = h[b0 + k];
+      J.w[k] = w[b0 + k];
+      hmax = hmax > h[b0 + k] ? hmax : h[b0 + k];
+    }
+    hipLaunchKernelGGL(nonzero_stats_batch_kernel, dim3(hmax < 1024 ? hmax : 1024, m), dim3(256), 0, st, J,
+                       reinterpret_cast<unsigned long long*>(stats + 3 * (long)b0));
+  }
+  return check_launch("nonzero_stats_batch");
 }

@@ -63,6 +63,16 @@ class VmTpsMap(ctypes.Structure):
                 ("x_steps", ctypes.c_double), ("y_steps", ctypes.c_double)]
 
 
+class VmAugmentJob(ctypes.Structure):
+    _fields_ = [("fg", c_void_p), ("bg", c_void_p), ("alpha", c_void_p), ("tps_points", c_void_p),
+                ("tps_coeffs", c_void_p), ("scratch", c_void_p), ("new_fg", c_void_p), ("new_bg", c_void_p),
+                ("new_alpha", c_void_p), ("h", ctypes.c_int32), ("w", ctypes.c_int32), ("bg_h", ctypes.c_int32),
+                ("bg_w", ctypes.c_int32), ("npts", ctypes.c_int32), ("tu_bg", ctypes.c_int32),
+                ("tv_bg", ctypes.c_int32), ("tu_fg", ctypes.c_int32), ("tv_fg", ctypes.c_int32),
+                ("reserved", ctypes.c_int32), ("m_bg", ctypes.c_double * 6), ("m_fg", ctypes.c_double * 6),
+                ("lut", ctypes.c_uint8 * 256)]
+
+
 LOADER_PLANES = {"cmp": 0, "bg": 1, "label": 2, "warped": 3, "fg": 4}
 
 # (name, restype, argtypes) — one row per declaration in include/vmatting.h
@@ -128,6 +138,10 @@ SIGNATURES = [
     ("vm_change_illumination_u8", c_int, [c_void_p, c_long, ctypes.POINTER(ctypes.c_uint8), c_void_p, c_void_p]),
     ("vm_nonzero_stats", c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
     ("vm_bgra_u8", c_int, [c_void_p, c_void_p, c_int, c_long, c_void_p, c_void_p]),
+    ("vm_augment_scratch_bytes", ctypes.c_size_t, [c_int, c_int]),
+    ("vm_augment_batch", c_int, [ctypes.POINTER(VmAugmentJob), c_int, c_void_p]),
+    ("vm_nonzero_stats_batch", c_int, [ctypes.POINTER(c_void_p), ctypes.POINTER(c_int), ctypes.POINTER(c_int), c_int,
+                                       c_void_p, c_void_p]),
     ("vm_trimap_from_matte", c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
     ("vm_matting_loss_backward", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_void_p,
                                          c_void_p]),

@@ -9,12 +9,13 @@ arithmetic).  numpy in -> numpy out; torch device tensors stay on the device.  T
 augmentation() (file listing, imread/imwrite, progress bar) is I/O and out of scope.
 """
 
+import ctypes
 import math
 
 import numpy as np
 import torch
 
-from . import ops
+from . import _lib, ops
 from . import tps
 from .tps import deform_grid  # noqa: F401  (augmentation.deform_grid, augmentation.py:23-39)
 
@@ -114,12 +115,28 @@ def augment(fg, bg, alpha):
     return _out(nfg, fg), _out(nbg, bg), _out(nal, alpha)
 
 
+def _stats_into(alphas, st):
+    """Every alpha's (count, row sum, column sum) into the device [n, 3] buffer st: one vm_nonzero_stats_batch launch
+    per 8 f64 alphas (the augment pipeline's), else one vm_nonzero_stats per alpha."""
+    al = [a.contiguous() for a in alphas]
+    if all(a.dtype == torch.float64 and a.dim() == 2 for a in al):
+        n = len(al)
+        ptrs = (ctypes.c_void_p * n)(*[a.data_ptr() for a in al])
+        hs = (ctypes.c_int * n)(*[a.shape[0] for a in al])
+        ws = (ctypes.c_int * n)(*[a.shape[1] for a in al])
+        ops.check(ops.lib().vm_nonzero_stats_batch(ptrs, hs, ws, n, ops._ptr(st), ops.stream_handle()),
+                  "nonzero_stats_batch")
+        return al
+    for i, a in enumerate(al):
+        ops.nonzero_stats(a, out=st[i])
+    return al
+
+
 def nonzero_stats_many(alphas):
     """(count, row sum, column sum) of every alpha's nonzero pixels (object_size / fg_center) with ONE host sync:
-    one vm_nonzero_stats launch per alpha into one [n, 3] device buffer, read back once."""
+    one batched launch into one [n, 3] device buffer, read back once."""
     st = torch.empty((len(alphas), 3), dtype=torch.int64, device=alphas[0].device)
-    for i, a in enumerate(alphas):
-        ops.nonzero_stats(a, out=st[i])
+    _stats_into(alphas, st)
     return [tuple(int(v) for v in row) for row in st.cpu().tolist()]
 
 
@@ -135,9 +152,9 @@ class StatsPrefetch:
         self.stream.wait_stream(cur)
         with torch.cuda.stream(self.stream):
             st = torch.empty((len(alphas), 3), dtype=torch.int64, device=dev)
-            for i, a in enumerate(alphas):
+            for a in alphas:
                 a.record_stream(self.stream)
-                ops.nonzero_stats(a, out=st[i])
+            _stats_into(alphas, st)
             self.host = torch.empty((len(alphas), 3), dtype=torch.int64, pin_memory=True)
             self.host.copy_(st, non_blocking=True)
             self.done = torch.cuda.Event()
@@ -202,10 +219,17 @@ def augment_many(triples, stats=None):
         plans.append((h, w, grid, def_grid, (tu_bg, tv_bg, scale_bg), (tu_fg, tv_fg, rot_fg, scale_fg, center),
                       illumination_lut(a, b, c)))
     dev_arrays = _upload_f64(uploads, devs[0][0].device) if uploads else []
+    batched = _BATCH and all(dfg.dtype == torch.uint8 and dfg.dim() == 3 and dfg.shape[2] == 3 and dbg.dtype == torch.uint8 and
+                  dbg.dim() == 3 and dbg.shape[2] == 3 and dal.dtype == torch.float64 and dal.dim() == 2 and
+                  tuple(dal.shape) == tuple(dfg.shape[:2]) and min(dfg.shape[:2]) >= 4 for dfg, dbg, dal in devs)
+    if batched:
+        return _augment_batch(devs, plans, dev_arrays)
     out = []
     for k, ((dfg, dbg, dal), (h, w, grid, def_grid, pbg, pfg, lut)) in enumerate(zip(devs, plans)):
         tu_bg, tv_bg, scale_bg = pbg
-        new_bg = ops.warp_image(dbg, tu_bg, tv_bg, rotation_matrix((w // 2, h // 2), 0., scale_bg), (w, h), lut)
+        # the camera motion warps the background to its own size (augmentation.py:56-63 with h, w = bg's)
+        new_bg = ops.warp_image(dbg, tu_bg, tv_bg, rotation_matrix((w // 2, h // 2), 0., scale_bg),
+                                (dbg.shape[1], dbg.shape[0]), lut)
         inv = tps.InverseWarp(grid, def_grid, (0, 0, h, w), 2, dfg.device,
                               solved=(dev_arrays[2 * k], dev_arrays[2 * k + 1]))
         tu_fg, tv_fg, rot_fg, scale_fg, center = pfg
@@ -214,6 +238,41 @@ def augment_many(triples, stats=None):
         tal = inv.sample(dal, 1)
         new_alpha = ops.warp_image(tal[:, :, 0] if tal.dim() == 3 else tal, tu_fg, tv_fg, m, (w, h))
         out.append((new_fg, new_bg, new_alpha))
+    return out
+
+
+_BATCH = True  # False: the per-sample launches (the batched kernels' bit-identity test)
+
+
+def _augment_batch(devs, plans, dev_arrays):
+    """augment_many's device work for u8 BGR fg / bg and f64 alpha samples: vm_augment_batch (the TPS lattice, one
+    fg + alpha resampling pass, the fused warps with the illumination change; four launches per 4 samples)."""
+    lib = ops.lib()
+    n = len(devs)
+    jobs = (_lib.VmAugmentJob * n)()
+    out, keep = [], []
+    for k, ((dfg, dbg, dal), (h, w, grid, def_grid, pbg, pfg, lut)) in enumerate(zip(devs, plans)):
+        dfg, dbg, dal = dfg.contiguous(), dbg.contiguous(), dal.contiguous()
+        dev = dfg.device
+        scratch = torch.empty(lib.vm_augment_scratch_bytes(h, w), dtype=torch.uint8, device=dev)
+        new_fg = torch.empty((h, w, 3), dtype=torch.uint8, device=dev)
+        new_bg = torch.empty(dbg.shape, dtype=torch.uint8, device=dev)
+        new_alpha = torch.empty((h, w), dtype=torch.float64, device=dev)
+        pts, co = dev_arrays[2 * k], dev_arrays[2 * k + 1]
+        tu_bg, tv_bg, scale_bg = pbg
+        tu_fg, tv_fg, rot_fg, scale_fg, center = pfg
+        j = jobs[k]
+        j.fg, j.bg, j.alpha = dfg.data_ptr(), dbg.data_ptr(), dal.data_ptr()
+        j.tps_points, j.tps_coeffs, j.scratch = pts.data_ptr(), co.data_ptr(), scratch.data_ptr()
+        j.new_fg, j.new_bg, j.new_alpha = new_fg.data_ptr(), new_bg.data_ptr(), new_alpha.data_ptr()
+        j.h, j.w, j.bg_h, j.bg_w, j.npts = h, w, dbg.shape[0], dbg.shape[1], pts.shape[0]
+        j.tu_bg, j.tv_bg, j.tu_fg, j.tv_fg = int(tu_bg), int(tv_bg), int(tu_fg), int(tv_fg)
+        j.m_bg[:] = [float(v) for v in rotation_matrix((w // 2, h // 2), 0., scale_bg).reshape(6)]
+        j.m_fg[:] = [float(v) for v in rotation_matrix(center, rot_fg, scale_fg).reshape(6)]
+        ctypes.memmove(j.lut, np.ascontiguousarray(lut, np.uint8).ctypes.data, 256)
+        keep += [dfg, dbg, dal, scratch]
+        out.append((new_fg, new_bg, new_alpha))
+    ops.check(lib.vm_augment_batch(jobs, n, ops.stream_handle()), "augment_batch")
     return out
 
 
