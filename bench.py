@@ -782,7 +782,7 @@ def train_image_bench(dev, steps, warmup, world, rank, threads, cpu=True, n=8, s
 
 
 def train_chain_bench(dev, steps, warmup, n=8, size=320, h=1080, w=1920, dtype="bf16", graph=False, overlap=True,
-                      profiler=None):
+                      profiler=None, prio=False):
     """BASELINE config 5 as ONE pipeline per step (rank 0, N=1): augmentation.augment makes frame t of each of n
     1080p source samples resident in HBM (augmentation.py:102-135: host np.random draws + TPS solves, the device
     statistics / TPS lattice / resampling / fused warps + illumination — augment_many, one landmark upload, no sync),
@@ -809,7 +809,10 @@ def train_chain_bench(dev, steps, warmup, n=8, size=320, h=1080, w=1920, dtype="
     alphas = [t[2] for t in src]
     flow = torch.from_numpy(synthetic_flow(h, w, 11, amp=12.0)).to(dev)
     np.random.seed(7)
-    trn = VideoTrainer(synthetic_vgg16(0), dtype, dev)
+    # (prio: the step's streams at the greatest priority, the producer at 0 — measured on MI355X: the step at high
+    # queue priority ran 9.4 ms against 5.6, so the overlap keeps every stream at the default priority)
+    hi = torch.cuda.Stream.priority_range()[1] if (overlap and prio) else 0
+    trn = VideoTrainer(synthetic_vgg16(0), dtype, dev, stream_priority=hi)
     names = ("cmp", "bg", "label", "warped", "fg")
 
     def batch(stats, out=None):
@@ -819,6 +822,12 @@ def train_chain_bench(dev, steps, warmup, n=8, size=320, h=1080, w=1920, dtype="
         return samples
 
     if overlap:
+        if hi != 0:
+            with torch.cuda.stream(torch.cuda.Stream(device=dev, priority=hi)):
+                rec = _train_chain_overlap(dev, steps, warmup, trn, batch, alphas, n, size, names, dtype, graph,
+                                           profiler)
+            rec["launch"] += "; step streams at priority %d, producer at 0" % hi
+            return rec
         return _train_chain_overlap(dev, steps, warmup, trn, batch, alphas, n, size, names, dtype, graph, profiler)
     r = vl.compose_batch(batch(va.StatsPrefetch(alphas).result()), (size, size), names, device=dev)
     if graph:
@@ -1143,6 +1152,8 @@ def main():
     ap.add_argument("--train-graph", action="store_true",
                     help="config-5 record from HIP-graph replays (VideoTrainer.capture) instead of eager launches: "
                          "the step is not host-bound, and the graph runs the side-stream select chains serially")
+    ap.add_argument("--chain-prio", action="store_true",
+                    help="config-5 chained record: the step's streams at the greatest priority (A/B; slower)")
     ap.add_argument("--chain-serial", action="store_true",
                     help="config-5 chained record without the producer-stream overlap (augment, loader, step in turn)")
     ap.add_argument("--train-streams", type=int, default=3,
@@ -1192,7 +1203,8 @@ def main():
             rec = train_bench(dev, args.steps, args.warmup, world, rank, threads, cpu=False, graph=args.train_graph,
                               streams=args.train_streams)
         elif args.only == "train_chain":
-            rec = train_chain_bench(dev, args.steps, args.warmup, graph=args.train_graph, overlap=not args.chain_serial)
+            rec = train_chain_bench(dev, args.steps, args.warmup, graph=args.train_graph, overlap=not args.chain_serial,
+                                    prio=args.chain_prio)
         elif args.only == "train_small":
             rec = train_small_bench(dev, args.steps, args.warmup, world, rank, threads, cpu=False)
         elif args.only == "train_image":
@@ -1267,7 +1279,8 @@ def main():
         train = train_bench(dev, max(args.steps // 4, 10), 3, world, rank, threads, cpu=not args.no_cpu_baseline,
                             graph=args.train_graph)
         if world == 1:
-            train["chained"] = train_chain_bench(dev, 5, 2, graph=args.train_graph, overlap=not args.chain_serial)
+            train["chained"] = train_chain_bench(dev, 5, 2, graph=args.train_graph, overlap=not args.chain_serial,
+                                                 prio=args.chain_prio)
         train_small = train_small_bench(dev, max(args.steps // 4, 10), 3, world, rank, threads,
                                         cpu=not args.no_cpu_baseline)
         train_image = train_image_bench(dev, max(args.steps // 4, 10), 3, world, rank, threads,

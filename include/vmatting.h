@@ -406,7 +406,8 @@ int vm_bgra_u8(const uint8_t* fg, const void* alpha, int alpha_dtype, long pixel
  * (output region (0, 0, h, w), approximate_grid 2), ONE resampling pass for the fg planes and the alpha through its
  * upsampled map (tps.warp_images, order 1), the fused translate + similarity warps (vm_warp_image) of the background
  * (its own size, camera motion) and of the resampled fg / alpha (object motion), and change_illumination with the
- * sample's S/V map on fg and bg.  Bit-identical to the per-sample entry points.  The np.random draws, the TPS solve
+ * sample's S/V map on fg and bg (the fg and alpha object-motion warps share one pass, which can also write the
+ * BGRA frame).  Bit-identical to the per-sample entry points.  The np.random draws, the TPS solve
  * and the maps stay on the host (the caller's), as in vm_tps_grid / vm_warp_image. */
 typedef struct vm_augment_job {
   const uint8_t* fg;        /* [h, w, 3] u8 BGR (device) */
@@ -418,6 +419,8 @@ typedef struct vm_augment_job {
   uint8_t* new_fg;          /* [h, w, 3] u8 */
   uint8_t* new_bg;          /* [bg_h, bg_w, 3] u8 */
   double* new_alpha;        /* [h, w] f64 */
+  uint8_t* new_bgra;        /* optional [h, w, 4] u8: the augmented frame as augmentation.augmentation writes it
+                             * (augmentation.py:162-163, vm_bgra_u8 of new_fg and new_alpha); NULL: not written */
   int32_t h, w, bg_h, bg_w, npts;
   int32_t tu_bg, tv_bg, tu_fg, tv_fg;
   int32_t reserved;
@@ -427,6 +430,10 @@ typedef struct vm_augment_job {
 } vm_augment_job;
 size_t vm_augment_scratch_bytes(int h, int w);
 int vm_augment_batch(const vm_augment_job* jobs, int n, void* stream);
+
+/* vm_bgra_u8 for n (fg u8 [px, 3], f64 alpha [px]) pairs (host arrays of device pointers) in one launch per 8. */
+int vm_bgra_u8_batch(const uint8_t* const* fg, const double* const* alpha, const long* pixels, uint8_t* const* out,
+                     int n, void* stream);
 
 /* vm_nonzero_stats for n f64 alphas (host arrays of device pointers and sizes) in one launch per 8: stats is device
  * int64 [n][3] (count, row-index sum, column-index sum per alpha). */

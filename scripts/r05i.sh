@@ -19,3 +19,7 @@ guard 300 r5i_chain.log python -u bench.py --only train_chain --steps 10 --warmu
 guard 300 r5i_chain.log python -u bench.py --only train_chain --steps 10 --warmup 3 --train-graph
 guard 300 r5i_chain.log python -u bench.py --only train_chain --steps 10 --warmup 3 --chain-serial
 grep -h '"only"' gpurun_out/r5i_chain.log | cut -c1-420
+for v in 0 2 0 2; do
+  guard 300 r5i_wv.log python -u bench.py --only train --steps 20 --warmup 3 --option wgrad_variant=$v
+done
+grep -h '"only"' gpurun_out/r5i_wv.log | cut -c1-300

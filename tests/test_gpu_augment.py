@@ -339,9 +339,10 @@ def test_augment_many_equals_sequential_augment():
 
 @pytest.mark.parametrize("shapes", [[(1080, 1920)] * 5, [(37, 51), (64, 64), (120, 160), (9, 300)]])
 def test_augment_batch_equals_per_sample_kernels(shapes, monkeypatch):
-    """vm_augment_batch (TPS lattice, the shared fg + alpha resampling pass and the fused warps, 4 samples per launch)
-    returns what the per-sample entry points (vm_tps_grid / vm_tps_sample / vm_warp_image) return, bit for bit, for
-    batches of 5 1080p samples and of mixed small sizes; and vm_nonzero_stats_batch the per-alpha statistics."""
+    """vm_augment_batch (TPS lattice, the shared fg + alpha resampling pass, the bg warp and the fused fg + alpha + BGRA
+    object-motion pass, 4 samples per launch) returns what the per-sample entry points (vm_tps_grid / vm_tps_sample /
+    vm_warp_image / vm_bgra_u8) return, bit for bit, for batches of 5 1080p samples and of mixed small sizes; and
+    vm_nonzero_stats_batch / vm_bgra_u8_batch the per-alpha results."""
     from vmatting import augmentation as va
     rs = np.random.RandomState(len(shapes))
     triples = []
@@ -351,20 +352,23 @@ def test_augment_batch_equals_per_sample_kernels(shapes, monkeypatch):
         triples.append(tuple(torch.from_numpy(np.ascontiguousarray(a)).cuda() for a in
                              ((rs.rand(h, w, 3) * 255).astype(np.uint8), (rs.rand(h, w, 3) * 255).astype(np.uint8),
                               al)))
+    from vmatting import ops
     np.random.seed(3)
-    got = va.augment_many(triples)
+    got = va._augment_many(triples, bgra=True)  # + the BGRA frame written by the fused object-motion pass
     monkeypatch.setattr(va, "_BATCH", False)
     np.random.seed(3)
-    want = va.augment_many(triples)
+    want = va._augment_many(triples, bgra=True)
     torch.cuda.synchronize()
     for a, b in zip(got, want):
+        assert len(a) == len(b) == 4
         for x, y in zip(a, b):
             assert x.shape == y.shape and torch.equal(x, y)
     st = torch.empty((len(triples), 3), dtype=torch.int64, device="cuda")
     va._stats_into([t[2] for t in triples], st)
+    prev = va.bgra_many([(t[0], t[2]) for t in triples])
     for i, t in enumerate(triples):
-        from vmatting import ops
         assert torch.equal(st[i], ops.nonzero_stats(t[2]))
+        assert torch.equal(prev[i], ops.bgra(t[0], t[2]))
 
 
 @pytest.mark.parametrize("adt", [np.float64, np.float32])

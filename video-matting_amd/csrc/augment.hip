@@ -66,9 +66,13 @@ __device__ __forceinline__ void tps_grid_body(const double* __restrict__ pts, co
     const double y = (double)iy * y_step + y_lo;
     double sx = 0.0, sy = 0.0;
     for (int k = 0; k < npts; ++k) {
+      // U(r) = r^2 log r as d2 * log(d2) / 2 (d2 = r^2): one log and no sqrt per term (the f64 lattice is
+      // compute-bound: 13M terms per 1080p sample), contracted to FMAs here only; a few ulp from the reference's
+      // sqrt-then-log, far inside the 1e-9 px the map is held to (tests/test_gpu_augment.py)
+#pragma clang fp contract(fast)
       const double dx = x - pts[2 * k], dy = y - pts[2 * k + 1];
-      const double r = sqrt(dx * dx + dy * dy);
-      const double u = (r * r) * (r < 1e-100 ? 0.0 : log(r));
+      const double d2 = dx * dx + dy * dy;
+      const double u = d2 < 1e-200 ? 0.0 : 0.5 * d2 * log(d2);  // r < 1e-100 -> 0 (tps.py:80-81)
       sx += coef[2 * k] * u;
       sy += coef[2 * k + 1] * u;
     }
@@ -423,17 +427,24 @@ struct AugGridJobs {
   const double* pts[kAugJobs];
   const double* coef[kAugJobs];
   double* grid[kAugJobs];
-  int npts[kAugJobs], nx[kAugJobs], ny[kAugJobs];
-  double xstep[kAugJobs], ystep[kAugJobs];
+  UpAxis* axes[kAugJobs];  // the upsampling's per-row ([h+1]) then per-column ([w+1]) terms
+  int npts[kAugJobs], nx[kAugJobs], ny[kAugJobs], h[kAugJobs], w[kAugJobs];
+  double xstep[kAugJobs], ystep[kAugJobs], xsteps[kAugJobs], ysteps[kAugJobs];
 };
 
+// the lattice, and the resampling's up_axis terms of every output row and column (each an f64 division): formed
+// once per sample here instead of twice per output pixel
 __global__ void __launch_bounds__(256) tps_grid_batch_kernel(AugGridJobs J) {
   const int j = blockIdx.y;
   tps_grid_body(J.pts[j], J.coef[j], J.npts[j], J.nx[j], J.ny[j], 0.0, J.xstep[j], 0.0, J.ystep[j], J.grid[j]);
+  const int h = J.h[j], w = J.w[j];
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < h + w + 2; i += gridDim.x * blockDim.x)
+    J.axes[j][i] = i <= h ? up_axis(i, J.xsteps[j], h) : up_axis(i - h - 1, J.ysteps[j], w);
 }
 
 struct AugSampleJobs {
   const double* grid[kAugJobs];
+  const UpAxis* axes[kAugJobs];
   const uint8_t* fg[kAugJobs];
   const double* al[kAugJobs];
   uint8_t* fg_t[kAugJobs];
@@ -452,11 +463,13 @@ __global__ void __launch_bounds__(256) tps_sample_pair_kernel(AugSampleJobs J) {
   const double* __restrict__ al = J.al[j];
   double* __restrict__ alt = J.al_t[j];
   const long total = (long)oh * ow, gsz = (long)nx * ny;
-  const double xsteps = J.xsteps[j], ysteps = J.ysteps[j];
+  const UpAxis* __restrict__ axes = J.axes[j];
+  (void)J.xsteps[j];
+  (void)J.ysteps[j];
   for_pixels(total, 3, J.fg_t[j], [&](long i, uint8_t* o) {
     const int oy = row_of(i, ow), ox = (int)(i - (long)oy * ow);
-    const UpAxis ax = up_axis(oy, xsteps, ih);
-    const UpAxis ay = up_axis(ox, ysteps, iw);
+    const UpAxis ax = axes[oy];            // == up_axis(oy, xsteps, ih)
+    const UpAxis ay = axes[oh + ox];       // == up_axis(ox, ysteps, iw)
     const long a00 = (long)ax.i0 * ny + ay.i0, a01 = (long)ax.i0 * ny + ay.i1;
     const long a10 = (long)ax.i1 * ny + ay.i0, a11 = (long)ax.i1 * ny + ay.i1;
     const double tr = grid[a00] * ax.f1 * ay.f1 + grid[a01] * ax.f1 * ay.f + grid[a10] * ax.f * ay.f1 +
@@ -548,36 +561,110 @@ __device__ __forceinline__ void warp_image_body(const T* __restrict__ src, int i
   });
 }
 
-// the u8 BGR warps + illumination of a batch: job 2s = sample s's background (camera motion), 2s + 1 its TPS-resampled
-// foreground (object motion); both through sample s's S/V map (augmentation.py:127-134)
+// the camera motion of a batch: each sample's background through its translation + scale and its S/V map
+// (augmentation.py:113-116, 133-134)
 struct AugWarpU8Jobs {
-  const uint8_t* src[2 * kAugJobs];
-  uint8_t* dst[2 * kAugJobs];
-  int ih[2 * kAugJobs], iw[2 * kAugJobs], h[2 * kAugJobs], w[2 * kAugJobs], tu[2 * kAugJobs], tv[2 * kAugJobs];
-  Affine a[2 * kAugJobs];
+  const uint8_t* src[kAugJobs];
+  uint8_t* dst[kAugJobs];
+  int ih[kAugJobs], iw[kAugJobs], h[kAugJobs], w[kAugJobs], tu[kAugJobs], tv[kAugJobs];
+  Affine a[kAugJobs];
   Lut256 lut[kAugJobs];
 };
 
-__global__ void __launch_bounds__(256) warp_u8_illum_batch_kernel(AugWarpU8Jobs J) {
+__global__ void __launch_bounds__(256) warp_bg_batch_kernel(AugWarpU8Jobs J) {
   __shared__ int sdiv[256], hdiv[256];
   illum_tables(sdiv, hdiv);
   const int j = blockIdx.y;
-  warp_image_body<uint8_t, true>(J.src[j], J.ih[j], J.iw[j], 3, J.tu[j], J.tv[j], J.a[j], J.lut[j >> 1], sdiv, hdiv,
+  warp_image_body<uint8_t, true>(J.src[j], J.ih[j], J.iw[j], 3, J.tu[j], J.tv[j], J.a[j], J.lut[j], sdiv, hdiv,
                                  J.dst[j], J.h[j], J.w[j]);
 }
 
-struct AugWarpF64Jobs {
-  const double* src[kAugJobs];
-  double* dst[kAugJobs];
+// the object motion of a batch: the TPS-resampled fg (u8 BGR, then the illumination change) and alpha (f64) go through
+// the SAME translation and similarity (augmentation.py:121-129), so one pass forms each pixel's fixed-point source
+// coordinate once and gathers both images' taps; optionally it also writes the sample's BGRA frame (vm_bgra_u8 of the
+// two outputs, augmentation.py:162-163).  Per image, warp_image_body's arithmetic: bit-identical.
+struct AugWarpObjJobs {
+  const uint8_t* fg[kAugJobs];
+  const double* al[kAugJobs];
+  uint8_t* dfg[kAugJobs];
+  double* dal[kAugJobs];
+  uint32_t* bgra[kAugJobs];
   int ih[kAugJobs], iw[kAugJobs], h[kAugJobs], w[kAugJobs], tu[kAugJobs], tv[kAugJobs];
   Affine a[kAugJobs];
+  Lut256 lut[kAugJobs];
 };
 
-__global__ void __launch_bounds__(256) warp_f64_batch_kernel(AugWarpF64Jobs J) {
+__global__ void __launch_bounds__(256) warp_object_batch_kernel(AugWarpObjJobs J) {
+  __shared__ int sdiv[256], hdiv[256];
+  illum_tables(sdiv, hdiv);
   const int j = blockIdx.y;
-  const Lut256 none{};
-  warp_image_body<double, false>(J.src[j], J.ih[j], J.iw[j], 1, J.tu[j], J.tv[j], J.a[j], none, nullptr, nullptr,
-                                 J.dst[j], J.h[j], J.w[j]);
+  const int ih = J.ih[j], iw = J.iw[j], h = J.h[j], w = J.w[j], tu = J.tu[j], tv = J.tv[j];
+  const Affine a = J.a[j];
+  const uint8_t* __restrict__ src = J.fg[j];
+  const double* __restrict__ asrc = J.al[j];
+  double* __restrict__ dal = J.dal[j];
+  uint32_t* __restrict__ bgra = J.bgra[j];
+  const long total = (long)h * w;
+  for_pixels(total, 3, J.dfg[j], [&](long i, uint8_t* o) {
+    const int y = row_of(i, w), x = (int)(i - (long)y * w);
+    const int adelta = cv_round(a.m[0] * (double)x * 1024.0);
+    const int bdelta = cv_round(a.m[3] * (double)x * 1024.0);
+    const int X0 = cv_round((a.m[1] * (double)y + a.m[2]) * 1024.0) + 16;
+    const int Y0 = cv_round((a.m[4] * (double)y + a.m[5]) * 1024.0) + 16;
+    const int X = (X0 + adelta) >> 5, Y = (Y0 + bdelta) >> 5;
+    int sx = X >> 5, sy = Y >> 5;
+    sx = sx < -32768 ? -32768 : (sx > 32767 ? 32767 : sx);
+    sy = sy < -32768 ? -32768 : (sy > 32767 ? 32767 : sy);
+    const int ax = X & 31, ay = Y & 31;
+    auto ok = [&](int ty, int tx) {
+      return (unsigned)ty < (unsigned)h && (unsigned)tx < (unsigned)w && (unsigned)(ty - tv) < (unsigned)ih &&
+             (unsigned)(tx - tu) < (unsigned)iw;
+    };
+    const bool k0 = ok(sy, sx), k1 = ok(sy, sx + 1), k2 = ok(sy + 1, sx), k3 = ok(sy + 1, sx + 1);
+    const long base = (long)(sy - tv) * iw + (sx - tu);
+    const uint8_t* p = src + base * 3;
+    uint8_t px[3];
+    for (int k = 0; k < 3; ++k) {
+      const int v0 = k0 ? p[k] : 0, v1 = k1 ? p[3 + k] : 0;
+      const int v2 = k2 ? p[(long)iw * 3 + k] : 0, v3 = k3 ? p[((long)iw + 1) * 3 + k] : 0;
+      const int s = v0 * ((32 - ay) * (32 - ax) * 32) + v1 * ((32 - ay) * ax * 32) + v2 * (ay * (32 - ax) * 32) +
+                    v3 * (ay * ax * 32);
+      const int r = (s + (1 << 14)) >> 15;
+      px[k] = (uint8_t)(r < 0 ? 0 : (r > 255 ? 255 : r));
+    }
+    illum_px(px[0], px[1], px[2], J.lut[j], sdiv, hdiv, o);
+    const double* q = asrc + base;
+    const double v0 = k0 ? q[0] : 0.0, v1 = k1 ? q[1] : 0.0, v2 = k2 ? q[iw] : 0.0, v3 = k3 ? q[iw + 1] : 0.0;
+    const float wy0 = 1.f - (float)ay * (1.f / 32.f), wy1 = (float)ay * (1.f / 32.f);
+    const float wx0 = 1.f - (float)ax * (1.f / 32.f), wx1 = (float)ax * (1.f / 32.f);
+    const double w0 = (double)(wy0 * wx0), w1 = (double)(wy0 * wx1), w2 = (double)(wy1 * wx0), w3 = (double)(wy1 * wx1);
+    const double al = v0 * w0 + v1 * w1 + v2 * w2 + v3 * w3;
+    dal[i] = al;
+    if (bgra) {
+      const uint32_t a8 = (uint32_t)(uint8_t)(int)(255.0 * al);
+      bgra[i] = (uint32_t)o[0] | ((uint32_t)o[1] << 8) | ((uint32_t)o[2] << 16) | (a8 << 24);
+    }
+  });
+}
+
+// augmentation.augmentation's BGRA frames of a batch (vm_bgra_u8 per job, f64 alpha), grid.y = the job
+struct AugBgraJobs {
+  const uint8_t* fg[2 * kAugJobs];
+  const double* al[2 * kAugJobs];
+  uint32_t* out[2 * kAugJobs];
+  long px[2 * kAugJobs];
+};
+
+__global__ void __launch_bounds__(256) bgra_batch_kernel(AugBgraJobs J) {
+  const int j = blockIdx.y;
+  const uint8_t* __restrict__ fg = J.fg[j];
+  const double* __restrict__ alpha = J.al[j];
+  uint32_t* __restrict__ out = J.out[j];
+  const long pixels = J.px[j];
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < pixels; i += (long)gridDim.x * blockDim.x) {
+    const uint32_t a8 = (uint32_t)(uint8_t)(int)(255.0 * alpha[i]);
+    out[i] = (uint32_t)fg[3 * i] | ((uint32_t)fg[3 * i + 1] << 8) | ((uint32_t)fg[3 * i + 2] << 16) | (a8 << 24);
+  }
 }
 
 // the foreground statistics of a batch of alphas, one launch (grid.y = the alpha)
@@ -893,7 +980,7 @@ extern "C" size_t vm_augment_scratch_bytes(int h, int w) {
   double a, b, c, d;
   aug_lattice(h, w, nx, ny, a, b, c, d);
   const size_t px = (size_t)(h + 1) * (w + 1);
-  return al16(2 * (size_t)nx * ny * 8) + al16(px * 3) + al16(px * 8);
+  return al16(2 * (size_t)nx * ny * 8) + al16(px * 3) + al16(px * 8) + al16((size_t)(h + w + 2) * sizeof(UpAxis));
 }
 
 extern "C" int vm_augment_batch(const vm_augment_job* jobs, int n, void* stream) {
@@ -901,7 +988,8 @@ extern "C" int vm_augment_batch(const vm_augment_job* jobs, int n, void* stream)
   for (int i = 0; i < n; ++i) {
     const vm_augment_job& q = jobs[i];
     if (!q.fg || !q.bg || !q.alpha || !q.tps_points || !q.tps_coeffs || !q.scratch || !q.new_fg || !q.new_bg ||
-        !q.new_alpha || q.h < 4 || q.w < 4 || q.bg_h <= 0 || q.bg_w <= 0 || q.npts <= 0)
+        !q.new_alpha || q.h < 4 || q.w < 4 || q.bg_h <= 0 || q.bg_w <= 0 || q.npts <= 0 ||
+        reinterpret_cast<uintptr_t>(q.new_bgra) % 4)
       return fail(VM_EINVAL, "augment_batch: job %d: bad argument", i);
     if ((long)(q.h + 1) * (q.w + 1) >= (1L << 31) || (long)q.bg_h * q.bg_w >= (1L << 31))
       return fail(VM_EUNSUPPORTED, "augment_batch: job %d: more than 2^31 pixels", i);
@@ -912,8 +1000,8 @@ extern "C" int vm_augment_batch(const vm_augment_job* jobs, int n, void* stream)
     AugGridJobs G{};
     AugSampleJobs S{};
     AugWarpU8Jobs U{};
-    AugWarpF64Jobs F{};
-    long gmax = 1, pmax = 1, wmax = 1;
+    AugWarpObjJobs O{};
+    long gmax = 1, pmax = 1, wmax = 1, bmax = 1;
     for (int k = 0; k < m; ++k) {
       const vm_augment_job& q = jobs[b0 + k];
       int nx, ny;
@@ -924,6 +1012,7 @@ extern "C" int vm_augment_batch(const vm_augment_job* jobs, int n, void* stream)
       const size_t px = (size_t)(q.h + 1) * (q.w + 1);
       uint8_t* fg_t = reinterpret_cast<uint8_t*>(sc + al16(2 * (size_t)nx * ny * 8));
       double* al_t = reinterpret_cast<double*>(sc + al16(2 * (size_t)nx * ny * 8) + al16(px * 3));
+      UpAxis* axes = reinterpret_cast<UpAxis*>(sc + al16(2 * (size_t)nx * ny * 8) + al16(px * 3) + al16(px * 8));
       G.pts[k] = q.tps_points;
       G.coef[k] = q.tps_coeffs;
       G.grid[k] = grid;
@@ -932,6 +1021,12 @@ extern "C" int vm_augment_batch(const vm_augment_job* jobs, int n, void* stream)
       G.ny[k] = ny;
       G.xstep[k] = xstep;
       G.ystep[k] = ystep;
+      G.axes[k] = axes;
+      G.h[k] = q.h;
+      G.w[k] = q.w;
+      G.xsteps[k] = xsteps;
+      G.ysteps[k] = ysteps;
+      S.axes[k] = axes;
       gmax = gmax > (long)nx * ny ? gmax : (long)nx * ny;
       S.grid[k] = grid;
       S.fg[k] = q.fg;
@@ -945,40 +1040,34 @@ extern "C" int vm_augment_batch(const vm_augment_job* jobs, int n, void* stream)
       S.xsteps[k] = xsteps;
       S.ysteps[k] = ysteps;
       pmax = pmax > (long)px ? pmax : (long)px;
-      // camera motion on the background (its own size), object motion on the resampled foreground
-      U.src[2 * k] = q.bg;
-      U.dst[2 * k] = q.new_bg;
-      U.ih[2 * k] = U.h[2 * k] = q.bg_h;
-      U.iw[2 * k] = U.w[2 * k] = q.bg_w;
-      U.tu[2 * k] = q.tu_bg;
-      U.tv[2 * k] = q.tv_bg;
-      U.a[2 * k] = invert_affine(q.m_bg);
-      U.src[2 * k + 1] = fg_t;
-      U.dst[2 * k + 1] = q.new_fg;
-      U.ih[2 * k + 1] = q.h + 1;
-      U.iw[2 * k + 1] = q.w + 1;
-      U.h[2 * k + 1] = q.h;
-      U.w[2 * k + 1] = q.w;
-      U.tu[2 * k + 1] = q.tu_fg;
-      U.tv[2 * k + 1] = q.tv_fg;
-      U.a[2 * k + 1] = invert_affine(q.m_fg);
-      for (int i = 0; i < 256; ++i) U.lut[k].t[i] = q.lut[i];
-      const long wpx = (long)q.h * q.w > (long)q.bg_h * q.bg_w ? (long)q.h * q.w : (long)q.bg_h * q.bg_w;
-      wmax = wmax > wpx ? wmax : wpx;
-      F.src[k] = al_t;
-      F.dst[k] = q.new_alpha;
-      F.ih[k] = q.h + 1;
-      F.iw[k] = q.w + 1;
-      F.h[k] = q.h;
-      F.w[k] = q.w;
-      F.tu[k] = q.tu_fg;
-      F.tv[k] = q.tv_fg;
-      F.a[k] = U.a[2 * k + 1];
+      // camera motion on the background (its own size); object motion on the resampled fg and alpha, one pass
+      U.src[k] = q.bg;
+      U.dst[k] = q.new_bg;
+      U.ih[k] = U.h[k] = q.bg_h;
+      U.iw[k] = U.w[k] = q.bg_w;
+      U.tu[k] = q.tu_bg;
+      U.tv[k] = q.tv_bg;
+      U.a[k] = invert_affine(q.m_bg);
+      for (int i = 0; i < 256; ++i) U.lut[k].t[i] = O.lut[k].t[i] = q.lut[i];
+      bmax = bmax > (long)q.bg_h * q.bg_w ? bmax : (long)q.bg_h * q.bg_w;
+      O.fg[k] = fg_t;
+      O.al[k] = al_t;
+      O.dfg[k] = q.new_fg;
+      O.dal[k] = q.new_alpha;
+      O.bgra[k] = reinterpret_cast<uint32_t*>(q.new_bgra);
+      O.ih[k] = q.h + 1;
+      O.iw[k] = q.w + 1;
+      O.h[k] = q.h;
+      O.w[k] = q.w;
+      O.tu[k] = q.tu_fg;
+      O.tv[k] = q.tv_fg;
+      O.a[k] = invert_affine(q.m_fg);
+      wmax = wmax > (long)q.h * q.w ? wmax : (long)q.h * q.w;
     }
     hipLaunchKernelGGL(tps_grid_batch_kernel, dim3(grid_for(gmax, 256, 1024), m), dim3(256), 0, st, G);
     hipLaunchKernelGGL(tps_sample_pair_kernel, dim3(grid_for(pmax, 256, 1024), m), dim3(256), 0, st, S);
-    hipLaunchKernelGGL(warp_u8_illum_batch_kernel, dim3(grid_for(wmax, 256, 1024), 2 * m), dim3(256), 0, st, U);
-    hipLaunchKernelGGL(warp_f64_batch_kernel, dim3(grid_for(wmax, 256, 1024), m), dim3(256), 0, st, F);
+    hipLaunchKernelGGL(warp_bg_batch_kernel, dim3(grid_for(bmax, 256, 1024), m), dim3(256), 0, st, U);
+    hipLaunchKernelGGL(warp_object_batch_kernel, dim3(grid_for(wmax, 256, 1024), m), dim3(256), 0, st, O);
   }
   return check_launch("augment_batch");
 }
@@ -1004,4 +1093,27 @@ extern "C" int vm_nonzero_stats_batch(const double* const* alphas, const int* h,
                        reinterpret_cast<unsigned long long*>(stats + 3 * (long)b0));
   }
   return check_launch("nonzero_stats_batch");
+}
+
+extern "C" int vm_bgra_u8_batch(const uint8_t* const* fg, const double* const* alpha, const long* pixels,
+                                uint8_t* const* out, int n, void* stream) {
+  if (!fg || !alpha || !pixels || !out || n <= 0) return fail(VM_EINVAL, "bgra_batch: bad argument");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  for (int b0 = 0; b0 < n; b0 += 2 * kAugJobs) {
+    const int m = n - b0 < 2 * kAugJobs ? n - b0 : 2 * kAugJobs;
+    AugBgraJobs J{};
+    long pmax = 1;
+    for (int k = 0; k < m; ++k) {
+      const int i = b0 + k;
+      if (!fg[i] || !alpha[i] || !out[i] || pixels[i] <= 0 || reinterpret_cast<uintptr_t>(out[i]) % 4)
+        return fail(VM_EINVAL, "bgra_batch: job %d", i);
+      J.fg[k] = fg[i];
+      J.al[k] = alpha[i];
+      J.out[k] = reinterpret_cast<uint32_t*>(out[i]);
+      J.px[k] = pixels[i];
+      pmax = pmax > pixels[i] ? pmax : pixels[i];
+    }
+    hipLaunchKernelGGL(bgra_batch_kernel, dim3(grid_for(pmax, 256, 1024), m), dim3(256), 0, st, J);
+  }
+  return check_launch("bgra_batch");
 }

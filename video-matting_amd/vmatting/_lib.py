@@ -66,7 +66,7 @@ class VmTpsMap(ctypes.Structure):
 class VmAugmentJob(ctypes.Structure):
     _fields_ = [("fg", c_void_p), ("bg", c_void_p), ("alpha", c_void_p), ("tps_points", c_void_p),
                 ("tps_coeffs", c_void_p), ("scratch", c_void_p), ("new_fg", c_void_p), ("new_bg", c_void_p),
-                ("new_alpha", c_void_p), ("h", ctypes.c_int32), ("w", ctypes.c_int32), ("bg_h", ctypes.c_int32),
+                ("new_alpha", c_void_p), ("new_bgra", c_void_p), ("h", ctypes.c_int32), ("w", ctypes.c_int32), ("bg_h", ctypes.c_int32),
                 ("bg_w", ctypes.c_int32), ("npts", ctypes.c_int32), ("tu_bg", ctypes.c_int32),
                 ("tv_bg", ctypes.c_int32), ("tu_fg", ctypes.c_int32), ("tv_fg", ctypes.c_int32),
                 ("reserved", ctypes.c_int32), ("m_bg", ctypes.c_double * 6), ("m_fg", ctypes.c_double * 6),
@@ -139,6 +139,8 @@ SIGNATURES = [
     ("vm_nonzero_stats", c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
     ("vm_bgra_u8", c_int, [c_void_p, c_void_p, c_int, c_long, c_void_p, c_void_p]),
     ("vm_augment_scratch_bytes", ctypes.c_size_t, [c_int, c_int]),
+    ("vm_bgra_u8_batch", c_int, [ctypes.POINTER(c_void_p), ctypes.POINTER(c_void_p), ctypes.POINTER(c_long),
+                                 ctypes.POINTER(c_void_p), c_int, c_void_p]),
     ("vm_augment_batch", c_int, [ctypes.POINTER(VmAugmentJob), c_int, c_void_p]),
     ("vm_nonzero_stats_batch", c_int, [ctypes.POINTER(c_void_p), ctypes.POINTER(c_int), ctypes.POINTER(c_int), c_int,
                                        c_void_p, c_void_p]),

@@ -182,12 +182,18 @@ def _upload_f64(arrays, device):
 
 
 def augment_many(triples, stats=None):
+    """augment() over several samples: see _augment_many.  Returns [(new_fg u8, new_bg u8, new_alpha f64)]."""
+    return [r[:3] for r in _augment_many(triples, stats)]
+
+
+def _augment_many(triples, stats=None, bgra=False):
     """augment() over several (fg, bg, alpha) samples as one device pipeline: the foreground statistics of every
     sample with one readback (or ``stats`` already read, e.g. by a StatsPrefetch), then every sample's host draws in
     augment's order (sample by sample, so a seeded global RandomState gives the per-call draws), the TPS solves, one
     upload of all landmarks / coefficients, and per sample: the TPS lattice, fg / alpha TPS resampling, and the fused
     translate + similarity warps with the illumination change (vm_warp_image).  No host sync after the statistics.
-    Returns [(new_fg u8, new_bg u8, new_alpha f64)] as device tensors."""
+    Returns [(new_fg u8, new_bg u8, new_alpha f64, new BGRA frame u8 or None)] as device tensors (the BGRA frame,
+    augmentation.augmentation's frame t, only with bgra=True)."""
     bound_translate, bound_rotate, bound_scale = 0.05, 10, 0.15
     devs = [(_device(fg), _device(bg), _device(al)) for fg, bg, al in triples]
     if stats is None:
@@ -223,7 +229,7 @@ def augment_many(triples, stats=None):
                   dbg.dim() == 3 and dbg.shape[2] == 3 and dal.dtype == torch.float64 and dal.dim() == 2 and
                   tuple(dal.shape) == tuple(dfg.shape[:2]) and min(dfg.shape[:2]) >= 4 for dfg, dbg, dal in devs)
     if batched:
-        return _augment_batch(devs, plans, dev_arrays)
+        return _augment_batch(devs, plans, dev_arrays, bgra)
     out = []
     for k, ((dfg, dbg, dal), (h, w, grid, def_grid, pbg, pfg, lut)) in enumerate(zip(devs, plans)):
         tu_bg, tv_bg, scale_bg = pbg
@@ -237,14 +243,14 @@ def augment_many(triples, stats=None):
         new_fg = ops.warp_image(inv.sample(dfg, 1), tu_fg, tv_fg, m, (w, h), lut)
         tal = inv.sample(dal, 1)
         new_alpha = ops.warp_image(tal[:, :, 0] if tal.dim() == 3 else tal, tu_fg, tv_fg, m, (w, h))
-        out.append((new_fg, new_bg, new_alpha))
+        out.append((new_fg, new_bg, new_alpha, ops.bgra(new_fg, new_alpha) if bgra else None))
     return out
 
 
 _BATCH = True  # False: the per-sample launches (the batched kernels' bit-identity test)
 
 
-def _augment_batch(devs, plans, dev_arrays):
+def _augment_batch(devs, plans, dev_arrays, bgra=False):
     """augment_many's device work for u8 BGR fg / bg and f64 alpha samples: vm_augment_batch (the TPS lattice, one
     fg + alpha resampling pass, the fused warps with the illumination change; four launches per 4 samples)."""
     lib = ops.lib()
@@ -258,6 +264,7 @@ def _augment_batch(devs, plans, dev_arrays):
         new_fg = torch.empty((h, w, 3), dtype=torch.uint8, device=dev)
         new_bg = torch.empty(dbg.shape, dtype=torch.uint8, device=dev)
         new_alpha = torch.empty((h, w), dtype=torch.float64, device=dev)
+        new_bgra = torch.empty((h, w, 4), dtype=torch.uint8, device=dev) if bgra else None
         pts, co = dev_arrays[2 * k], dev_arrays[2 * k + 1]
         tu_bg, tv_bg, scale_bg = pbg
         tu_fg, tv_fg, rot_fg, scale_fg, center = pfg
@@ -265,13 +272,14 @@ def _augment_batch(devs, plans, dev_arrays):
         j.fg, j.bg, j.alpha = dfg.data_ptr(), dbg.data_ptr(), dal.data_ptr()
         j.tps_points, j.tps_coeffs, j.scratch = pts.data_ptr(), co.data_ptr(), scratch.data_ptr()
         j.new_fg, j.new_bg, j.new_alpha = new_fg.data_ptr(), new_bg.data_ptr(), new_alpha.data_ptr()
+        j.new_bgra = new_bgra.data_ptr() if bgra else None
         j.h, j.w, j.bg_h, j.bg_w, j.npts = h, w, dbg.shape[0], dbg.shape[1], pts.shape[0]
         j.tu_bg, j.tv_bg, j.tu_fg, j.tv_fg = int(tu_bg), int(tv_bg), int(tu_fg), int(tv_fg)
         j.m_bg[:] = [float(v) for v in rotation_matrix((w // 2, h // 2), 0., scale_bg).reshape(6)]
         j.m_fg[:] = [float(v) for v in rotation_matrix(center, rot_fg, scale_fg).reshape(6)]
         ctypes.memmove(j.lut, np.ascontiguousarray(lut, np.uint8).ctypes.data, 256)
         keep += [dfg, dbg, dal, scratch]
-        out.append((new_fg, new_bg, new_alpha))
+        out.append((new_fg, new_bg, new_alpha, new_bgra))
     ops.check(lib.vm_augment_batch(jobs, n, ops.stream_handle()), "augment_batch")
     return out
 
@@ -281,6 +289,21 @@ def bgra(fg, alpha):
     concat(fg u8, (255. * alpha).astype(uint8)) — on the device for device tensors (float64 product, truncation)."""
     dfg, dal = _device(fg), _device(alpha)
     return _out(ops.bgra(dfg, dal), fg)
+
+
+def bgra_many(pairs):
+    """bgra() of several (fg u8 [h, w, 3], alpha f64 [h, w]) device pairs: one vm_bgra_u8_batch launch per 8."""
+    pairs = [(f.contiguous(), a.contiguous()) for f, a in pairs]
+    if not all(f.dtype == torch.uint8 and a.dtype == torch.float64 and f.dim() == 3 and f.shape[2] == 3 and
+               a.numel() == f.shape[0] * f.shape[1] for f, a in pairs):
+        return [ops.bgra(f, a) for f, a in pairs]
+    n = len(pairs)
+    outs = [torch.empty((f.shape[0], f.shape[1], 4), dtype=torch.uint8, device=f.device) for f, _ in pairs]
+    P = ctypes.c_void_p * n
+    ops.check(ops.lib().vm_bgra_u8_batch(P(*[f.data_ptr() for f, _ in pairs]), P(*[a.data_ptr() for _, a in pairs]),
+                                         (ctypes.c_long * n)(*[a.numel() for _, a in pairs]),
+                                         P(*[o.data_ptr() for o in outs]), n, ops.stream_handle()), "bgra_batch")
+    return outs
 
 
 def video_sample(fg, bg, alpha, flow):
@@ -295,7 +318,8 @@ def video_sample(fg, bg, alpha, flow):
 def video_samples(sources, flow, stats=None):
     """video_sample over several (fg, bg, alpha) sources as one augment_many pipeline (one statistics readback, or
     none with ``stats`` from a StatsPrefetch)."""
-    aug = augment_many([(_device(fg), _device(bg), _device(al)) for fg, bg, al in sources], stats=stats)
+    devs = [(_device(fg), _device(bg), _device(al)) for fg, bg, al in sources]
+    aug = _augment_many(devs, stats=stats, bgra=True)  # frame t's BGRA written by the object-motion pass
+    prev = bgra_many([(d[0], d[2]) for d in devs])      # frame t-1: the source itself
     d_flow = _device(flow)
-    return [{"fg": bgra(nfg, nal), "bg": nbg, "prev": bgra(_device(fg), _device(al)), "flow": d_flow}
-            for (nfg, nbg, nal), (fg, bg, al) in zip(aug, sources)]
+    return [{"fg": a[3], "bg": a[1], "prev": p, "flow": d_flow} for a, p in zip(aug, prev)]

@@ -146,7 +146,7 @@ class VideoTrainer(TrainerBase):
     """train.video_procedure's iteration on device (also simple_procedure's: pass diff = cmp - bg as ``warped``)."""
 
     def __init__(self, vgg16_npy_path=None, dtype="fp32", device="cuda", params=None, bn=None, lr=1e-3,
-                 beta1=0.9, beta2=0.999, epsilon=1e-8, sync_bn=False, streams=3):
+                 beta1=0.9, beta2=0.999, epsilon=1e-8, sync_bn=False, streams=3, stream_priority=0):
         self.vgg = vgg16_npy_path if isinstance(vgg16_npy_path, Vgg16) else Vgg16(vgg16_npy_path, dtype, device)
         self.model = UNetSimple(self.vgg, True, dtype, device, params)
         self.device = self.model.device
@@ -160,7 +160,7 @@ class VideoTrainer(TrainerBase):
         # one stream (its collectives stay in one issue order)
         dev_ = torch.device(device)
         self._side = [] if self.sync_bn or streams < 1 or dev_.type != "cuda" else \
-            [torch.cuda.Stream(device=dev_) for _ in range(int(streams))]
+            [torch.cuda.Stream(device=dev_, priority=stream_priority) for _ in range(int(streams))]
         self._capture_origin = None  # the stream a TrainGraph capture began on (see _check_capture_fork)
         dev = self.device
         # move the freshly drawn variables into the flat buffer and alias every consumer onto it
