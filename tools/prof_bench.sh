@@ -6,8 +6,10 @@
 #   5. --kernel-trace --stats of the config-3 record, one pass per (dtype, size)            -> profiles/<tag>_temporal_<dtype>_<HxW>_kernel_stats.csv
 #   6. --kernel-trace --stats of the config-5 training step alone (8 x 320^2, bf16)        -> profiles/<tag>_train_kernel_stats.csv
 #   7. --kernel-trace --stats of the small_train.py step alone (8 x 320^2, bf16, graphs)   -> profiles/<tag>_train_small_kernel_stats.csv
-#   8. the full bench (reads the profiles of 2-4)                                         -> gpurun_out/<tag>_bench.json
-# SKIP="fwd mfma traffic temporal train train_small bench" skips passes.
+#   8. --kernel-trace --stats of train_image, train_chain, augment (batched), loader records and the bf16x6 forward
+#                                                                                         -> profiles/<tag>_<record>_kernel_stats.csv
+#   9. the full bench (reads the profiles of 2-4)                                         -> gpurun_out/<tag>_bench.json
+# SKIP="fwd mfma traffic temporal train train_small train_image train_chain augment loader x6 bench" skips passes.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 REPO=$(pwd)
 TAG=$1; shift
@@ -63,6 +65,21 @@ run 300 train_small.log rocprofv3 --kernel-trace --stats --output-format csv -d 
     -- python3 "$REPO/bench.py" --only train_small --steps 20 --warmup 3 "$@"
 cp "$(find "$OUT/train_small" -name '*kernel_stats.csv' | head -n 1)" "$REPO/profiles/${TAG}_train_small_kernel_stats.csv"
 grep "^{" "$OUT/train_small.log" | tail -n 1 > "$REPO/profiles/${TAG}_train_small.json"
+fi
+# 9-13. (r05) the UNetImage step, the chained config-5 pipeline, the batched augment, the loader, the bf16x6 forward
+for rec in train_image train_chain augment loader; do
+  if ! skip $rec; then
+    run 300 $rec.log rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/$rec" -o run \
+        -- python3 "$REPO/bench.py" --only $rec --steps 20 --warmup 3 "$@"
+    cp "$(find "$OUT/$rec" -name '*kernel_stats.csv' | head -n 1)" "$REPO/profiles/${TAG}_${rec}_kernel_stats.csv"
+    grep "^{" "$OUT/$rec.log" | tail -n 1 > "$REPO/profiles/${TAG}_${rec}.json"
+  fi
+done
+if ! skip x6; then
+run 300 x6.log rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/x6" -o run \
+    -- python3 "$REPO/tools/x6bench.py" 10
+cp "$(find "$OUT/x6" -name '*kernel_stats.csv' | head -n 1)" "$REPO/profiles/${TAG}_x6_kernel_stats.csv"
+grep -v "amdgpu.ids" "$OUT/x6.log" | grep -v "^[EW]20" > "$REPO/profiles/${TAG}_x6.log" || true
 fi
 cp "$REPO"/profiles/${TAG}_* "$REPO/gpurun_out/"
 skip bench && exit 0
