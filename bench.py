@@ -452,14 +452,17 @@ def augment_bench(dev, steps, threads, cpu=True, h=1080, w=1920, batch=8):
         va.augment_many(triples)
     torch.cuda.synchronize()
     ev = Events()
+    va._EVENTS = kev = []  # the device pipeline's own time: events around each vm_augment_batch launch
     t0 = time.perf_counter()
     ev.mark()
     for _ in range(steps):
         va.augment_many(triples)
     ev.mark()
     torch.cuda.synchronize()
+    va._EVENTS = None
     wall = (time.perf_counter() - t0) / steps / batch
-    dev_ms = ms(*ev.e) / steps / batch
+    span_ms = ms(*ev.e) / steps / batch
+    dev_ms = sum(ms(a, b) for a, b in kev) / steps / batch
     # algorithmic bytes per sample (per pixel): alpha stats 8; bg 2 warps 2*(3+3); TPS grid (h/2)(w/2)*16 = 4;
     # fg TPS 3+3, alpha TPS 8+8; fg 2 warps 2*(3+3); alpha 2 warps 2*(8+8); illumination fg+bg 2*(3+3)
     algo = h * w * (8 + 12 + 4 + 6 + 16 + 12 + 32 + 12)
@@ -468,8 +471,13 @@ def augment_bench(dev, steps, threads, cpu=True, h=1080, w=1920, batch=8):
            "algorithmic_bytes_def": "the reference's passes (stats, two warpAffine per image, TPS lattice + resampling, "
                                     "illumination), each image read and written once per pass",
            "samples_per_s": round(1.0 / wall, 1), "ms_per_sample": round(1000 * wall, 4),
-           "device_ms_per_sample": round(dev_ms, 4), "algorithmic_bytes_per_sample": int(algo),
-           "achieved_gbps": round(algo / (dev_ms * 1e-3) / 1e9, 1), "peak_gbps": PEAK_HBM_GBPS}
+           "device_ms_per_sample": round(dev_ms, 4),
+           "device_ms_def": "HIP events around each vm_augment_batch launch (the per-pixel pipeline); the stream span "
+                            "per sample, host draws / TPS solves / statistics readback included, is stream_ms_per_sample",
+           "stream_ms_per_sample": round(span_ms, 4), "algorithmic_bytes_per_sample": int(algo),
+           "achieved_gbps": round(algo / (dev_ms * 1e-3) / 1e9, 1), "peak_gbps": PEAK_HBM_GBPS,
+           "roofline": {"bound": "hbm", "achieved": round(algo / (dev_ms * 1e-3) / 1e9, 1), "peak": PEAK_HBM_GBPS,
+                        "unit": "GB/s", "frac": round(algo / (dev_ms * 1e-3) / 1e9 / PEAK_HBM_GBPS, 4)}}
     if cpu:
         from oracle import augment as oa  # the CPU-baseline leg only
         np.random.seed(0)

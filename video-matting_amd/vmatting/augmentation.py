@@ -248,6 +248,7 @@ def _augment_many(triples, stats=None, bgra=False):
 
 
 _BATCH = True  # False: the per-sample launches (the batched kernels' bit-identity test)
+_EVENTS = None  # a list: HIP events around every vm_augment_batch launch are appended (bench.py's kernel time)
 
 
 def _augment_batch(devs, plans, dev_arrays, bgra=False):
@@ -280,7 +281,11 @@ def _augment_batch(devs, plans, dev_arrays, bgra=False):
         ctypes.memmove(j.lut, np.ascontiguousarray(lut, np.uint8).ctypes.data, 256)
         keep += [dfg, dbg, dal, scratch]
         out.append((new_fg, new_bg, new_alpha, new_bgra))
+    ev = _EVENTS is not None and (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+    ev and ev[0].record()
     ops.check(lib.vm_augment_batch(jobs, n, ops.stream_handle()), "augment_batch")
+    ev and ev[1].record()
+    ev and _EVENTS.append(ev)
     return out
 
 
