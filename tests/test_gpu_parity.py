@@ -674,7 +674,8 @@ def test_conv_pair_first_head_partials(shape, store_y):
 PERSIST_CASES = [(1, 68, 120, 128, 64, "relu", True), (2, 37, 45, 64, 128, "relu", True),
                  (1, 135, 240, 256, 128, "none", False), (1, 17, 30, 512, 512, "relu", False),
                  (3, 9, 70, 32, 64, "sigmoid", True), (1, 540, 960, 64, 128, "relu", True),
-                 (1, 4, 16, 64, 64, "relu", True), (1, 33, 97, 96, 192, "relu", False)]
+                 (1, 4, 16, 64, 64, "relu", True), (1, 33, 97, 96, 192, "relu", False),
+                 (1, 135, 240, 512, 512, "relu", True), (2, 24, 80, 64, 64, "relu", True)]
 
 
 @pytest.mark.parametrize("case", PERSIST_CASES)
@@ -692,6 +693,7 @@ def test_patch_persist_bit_identical(case):
     try:
         _lib.set_option("persist_rounds", 0)  # (any grid: the small cases take the persistent kernel too)
         _lib.set_option("persist_up_rounds", 0)
+        _lib.set_option("rows_kernel", 0)  # (the row-stationary kernel would take the cin >= 64 1080p-level grids)
         for persist in (0, 1):
             _lib.set_option("patch_persist", persist)
             cat = torch.full((n, h, w, cout + 32), 7.0, dtype=torch.bfloat16, device=DEV)
@@ -714,6 +716,7 @@ def test_patch_persist_bit_identical(case):
         _lib.set_option("patch_persist", 1)
         _lib.set_option("persist_rounds", 2)
         _lib.set_option("persist_up_rounds", 6)
+        _lib.set_option("rows_kernel", 1)
     for a, b in zip(res[0], res[1]):
         if a is not None:
             assert torch.equal(a, b)

@@ -1365,6 +1365,25 @@ void conv3x3_patch_persist(ConvArgs a) {
   const int nitem = (hi - lo) * tn;
   int it = 0, q = jw;
   if (q >= nitem) return;  // (before any barrier: the block has no work)
+  // band-local pixel tile i -> pixel tile; with halfskip the band's last-column tiles (s % tw == tw - 1; [0, s) holds
+  // s / tw of them) come after its other tiles, in order
+  const int nhalf = a.halfskip ? hi / tw - lo / tw : 0, nfull = hi - lo - nhalf;
+  auto band_tile = [&](int i) __attribute__((always_inline)) {
+    if (!a.halfskip) return lo + i;
+    if (i < nfull) {
+      const int g = lo - lo / tw + i;  // the g-th tile off the last column
+      return g + g / (tw - 1);
+    }
+    return (lo / tw + i - nfull) * tw + tw - 1;
+  };
+  // round r's item of walker jw: prot 1 rotates the walkers over the output tiles, prot 2 reverses the order of the
+  // walker groups (tn walkers, one per output tile) in odd rounds, so the walkers that end a round late start the
+  // next one early (each walker keeps its output tile)
+  auto item_of = [&](int r) __attribute__((always_inline)) {
+    if (a.prot == 1) return r * J + (jw + r) % J;
+    if (a.prot == 2 && (r & 1)) return r * J + J - tn - jw + 2 * (jw % tn);
+    return r * J + jw;
+  };
 
   // per-block constants in LDS: mul[CT], add[CT] (f32, output channel order), then the head A fragments [lane][2]
   char* kc = smem + C::MAIN;
@@ -1600,7 +1619,7 @@ void conv3x3_patch_persist(ConvArgs a) {
   };
 
   const int wstep = a.K_pad * 2 * BN;  // weight bytes of one output tile
-  int st = lo + q / tn, n0 = (q % tn) * BN;
+  int st = band_tile(q / tn), n0 = (q % tn) * BN;
   set_xtile(st);
   int gcnt = 0;  // granules issued so far (input buffer parity)
   issue_x(0, 0, true);
@@ -1609,9 +1628,11 @@ void conv3x3_patch_persist(ConvArgs a) {
   int slot = 0;
   bool first = true;
   for (;;) {
-    const int qn = (it + 1) * J + (a.prot ? (jw + it + 1) % J : jw);
+    const int qn = item_of(it + 1);
     const bool more = qn < nitem;
-    const int stn = lo + qn / tn, wbn = more ? (qn % tn) * wstep : 0, wb = (n0 / BN) * wstep;
+    const int stn = more ? band_tile(qn / tn) : st, wbn = more ? (qn % tn) * wstep : 0, wb = (n0 / BN) * wstep;
+    // a last-column tile of a halfskip frame: the right-half waves' pixels are all outside it (stores masked as ever)
+    const bool idle = a.halfskip && (wm & 1) && st % tw == tw - 1;
     const int up_phase = UPSKIP && a.up && n0 / a.up_cout == (n0 + BN - 1) / a.up_cout ? n0 / a.up_cout : 0;
     const bool skip_r0 = (up_phase >> 1) != 0 && (a.upmask & 1), skip_c0 = (up_phase & 1) != 0 && (a.upmask & 2);
     f32x4 acc[FC][FP];
@@ -1641,7 +1662,7 @@ void conv3x3_patch_persist(ConvArgs a) {
         } else {
           issue_w(ws - nsr, slot + S - 1 - (slot + S - 1 >= S ? S : 0), more, wbn);
         }
-        if (!(UPSKIP && skip_r0 && r == 0)) {
+        if (!(UPSKIP && skip_r0 && r == 0) && !idle) {
           uint4 av[2][FC], bv[2][FP];
           frags(av[0], bv[0], slot, buf, r * G);
 #pragma unroll
@@ -4334,6 +4355,7 @@ static long g_persist_rounds = 2;
 static long g_persist_up_rounds = 6;
 static long g_persist_all = 0;  // (A/B) every plain grid of >= persist_rounds rounds
 static long g_persist_rot = 0;  // (A/B) walker rotation: 0 = folded upconvs only, 1 = all, 2 = none
+static long g_persist_half = 1;  // (A/B) halfskip walk for frames whose last tile column is <= 16 px (ConvArgs::halfskip)
 static bool persist_ok(const ConvArgs& a) {
   return g_patch_persist && g_patch_repi && a.ksplit <= 1 && !a.vstride && a.y_dtype == VM_BF16 &&
          (!a.up || a.up_cout % 32 == 0) && (long)a.cout_pad * a.K_pad * 2 < 0x7fff0000L;
@@ -4372,6 +4394,11 @@ static int launch_patch_persist(ConvArgs& a, hipStream_t st) {
   if (sp < 8 || resident < 8 || !use || items > 0x7fffffffL) return 1;
   a.tiles_n = tn;
   a.prot = g_persist_rot == 0 ? (a.up ? 1 : 0) : g_persist_rot == 1 ? 1 : 0;
+  // a last tile column of <= 16 frame columns (135 x 240: 7.5 tiles) costs half a tile: walk those tiles last and
+  // serpentine the rounds, so the 2.125 rounds of items of the conv4 level end after ~2.2 tile times instead of 3
+  const long J_ = resident / 8;
+  a.halfskip = g_persist_half && C::REMAP && a.W % C::TW != 0 && a.W % C::TW <= 16 && a.W > C::TW;
+  if (a.halfskip && !a.prot && J_ % tn == 0) a.prot = 2;
   a.repi = 1;
   a.prio = (int)g_conv_prio;
   a.upmask = (int)g_up_skip_mask;
@@ -4978,6 +5005,10 @@ extern "C" int vm_set_option(const char* key, long value) {
   if (!strcmp(key, "rows_kernel")) {
     if (value != 0 && value != 1 && value != 8 && value != 16) return fail(VM_EINVAL, "rows_kernel must be 0, 1, 8 or 16");
     g_rows_kernel = value;
+    return VM_OK;
+  }
+  if (!strcmp(key, "persist_half")) {
+    g_persist_half = value;
     return VM_OK;
   }
   if (!strcmp(key, "rows_up")) {

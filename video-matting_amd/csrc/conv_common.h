@@ -58,6 +58,11 @@ struct ConvArgs {
   // strip pair kernel: optional bf16 output of the FIRST conv (conv1_1 + bias + relu), [N,H,W,64] view
   void* y1;
   int y1_cstride, y1_coff;
+  // persistent patch kernel, frames whose last 32-px tile column holds <= 16 frame columns (the conv4 level's 240):
+  // the odd (right-half) waves of those tiles hold no frame pixel and skip their MFMAs, and each XCD band walks its
+  // last-column tiles after the others (with prot == 2's serpentine rounds the half-cost items pair up on the walkers
+  // that hold the band's third round)
+  int halfskip;
 };
 
 // a pointer every lane holds the same value of, moved to SGPRs (buffer descriptors must be scalar)
