@@ -224,3 +224,36 @@ def test_refine_softmax_f32_kernel(n, h, w, cin):
     assert np.abs(g - gen.cpu().numpy()).max() <= 5e-5
     assert np.abs(g - ref).max() <= 1e-4, np.abs(g - ref).max()
     np.testing.assert_allclose(g.sum(-1), 1.0, atol=1e-5)
+
+
+@pytest.mark.parametrize("cin", [1, 3, 5])
+@pytest.mark.parametrize("n,h,w", [(1, 37, 70), (2, 8, 32), (1, 1, 1), (1, 135, 240)])
+def test_refine_softmax_x6_kernel(n, h, w, cin):
+    """The split-bf16 x6 form of the fp32 refine kernel (softmax_f32p 7: each f32 input / filter value split exactly
+    into three bf16 parts, six products per term on the bf16 MFMA, f32 sums) at f32 accuracy: within 5e-5 of the
+    exact-f32 MFMA kernel and 1e-4 (north_star's bound) of float64, rows sum to 1; ragged tiles, partial rounds."""
+    from oracle import ops as oops
+    from vmatting import _lib, ops
+    rs = np.random.RandomState(h * 11 + w + cin)
+    x = np.zeros((n, h, w, 8), np.float32)
+    x[..., :cin] = rs.uniform(-30, 30, size=(n, h, w, cin))
+    wt = (rs.normal(size=(3, 3, cin, 64)) * 0.3).astype(np.float32)
+    b = rs.normal(size=64).astype(np.float32)
+    pc = ops.PackedConv(wt, b, "fp32")
+    xd = T(x)[..., :cin]
+    try:
+        f32 = ops.conv3x3(xd, pc, "softmax").clone()
+        _lib.set_option("softmax_f32p", 7)
+        got = ops.conv3x3(xd, pc, "softmax").clone()
+        assert _lib.last_conv_kernel() == "vm::conv3x3_first_softmax_f32p<%d, 2, false, 0, 18, true>" % cin
+        _lib.set_option("softmax_blocks", 3)
+        assert torch.equal(ops.conv3x3(xd, pc, "softmax"), got)  # persistent walk, partial last round
+    finally:
+        _lib.set_option("softmax_blocks", 2048)
+        _lib.set_option("softmax_f32p", 4)
+    ref = oops.softmax_lastdim(oops.conv3x3_same(x[..., :cin].astype(np.float64), wt.astype(np.float64),
+                                                 b.astype(np.float64)))
+    g = got.cpu().numpy()
+    assert np.abs(g - f32.cpu().numpy()).max() <= 5e-5, np.abs(g - f32.cpu().numpy()).max()
+    assert np.abs(g - ref).max() <= 1e-4, np.abs(g - ref).max()
+    np.testing.assert_allclose(g.sum(-1), 1.0, atol=1e-5)

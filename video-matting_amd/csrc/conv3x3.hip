@@ -2755,17 +2755,36 @@ __device__ __forceinline__ void softmax_chunk(f32x4 (&C)[4][2], float (&mx)[2], 
   }
 }
 
-template <int CIN, int MINW = 2, bool AFF = false, int ABL = 0, int AUX = 0>  // MINW: min waves per SIMD; AFF: a
-                                                                               // scale / shift epilogue; AUX: stores
+// X6 (CIN <= 5): the same conv at f32 accuracy on the bf16 MFMA (v_mfma_f32_16x16x32_bf16, 16x the f32 rate).  Each
+// f32 input x and filter tap w is split exactly into three bf16 parts (h + m + l, as split6_kernel in elementwise.hip),
+// and one 32-deep K step per tap carries the six products l*Wh + m*Wm + h*Wl + m*Wh + h*Wm + h*Wh of every channel
+// (the parts' 24 significant bits; the dropped m*Wl, l*Wm, l*Wl terms are below 2^-24 of h*Wh): the per-wave patch
+// holds a 64-byte record [l, m, h, m, h, h] (CIN channels each, zero padded) per pixel in 4 chunk planes, the weight
+// table the matching [Wh, Wm, Wl, Wh, Wm, Wh] fragments.  9 steps of 8 bf16 MFMAs replace 12 of 8 f32 ones at a
+// quarter of the cycles each, which leaves the kernel bound by its softmax and its 256-byte-per-pixel output stores.
+// Single-buffered patch (the LDS budget: 36 KB of weight fragments + 8 x 6.5 KB of records + the store slabs; a wave's
+// LDS reads and writes stay in program order, so restaging over the previous strip's records is safe).
+__device__ __forceinline__ void split3_bf16(float x, uint32_t& h, uint32_t& m, uint32_t& l) {
+  h = f2bf(x);
+  const float r1 = x - bf2f((uint16_t)h);
+  m = f2bf(r1);
+  l = f2bf(r1 - bf2f((uint16_t)m));
+}
+
+template <int CIN, int MINW = 2, bool AFF = false, int ABL = 0, int AUX = 0, bool X6 = false>  // MINW: min waves per
+                                                                      // SIMD; AFF: a scale / shift epilogue; AUX: stores
 __global__ __launch_bounds__(512, MINW) void conv3x3_first_softmax_f32p(ConvArgs a) {  // epilogue; ABL: study only
-  constexpr int NS = (9 * CIN + 3) / 4;
+  static_assert(!X6 || CIN * 6 <= 32, "x6: six parts of every channel in one 32-deep K step");
+  constexpr int NS = X6 ? 9 : (9 * CIN + 3) / 4;
   constexpr int TH = 8, TW = 32, PW = TW + 2, SP = 3 * PW;
-  constexpr int WPF = (CIN * SP + 32 + 3) / 4 * 4;
+  constexpr int WPF = X6 ? 4 * SP * 4 : (CIN * SP + 32 + 3) / 4 * 4;  // per-wave patch floats (x6: 4 chunk planes)
+  constexpr int NBUF = X6 ? 1 : 2;
   constexpr int ZERO = CIN * SP;
-  __shared__ __attribute__((aligned(16))) f32x4 wl[NS * 64];
-  __shared__ int pl[NS * 4];
+  __shared__ __attribute__((aligned(16))) f32x4 wl[X6 ? 1 : NS * 64];
+  __shared__ __attribute__((aligned(16))) uint4 wx[X6 ? 9 * 4 * 64 : 1];  // x6: [tap][fc][lane] A fragments
+  __shared__ int pl[X6 ? 1 : NS * 4];
   __shared__ __attribute__((aligned(16))) float rmul[2 * 64];
-  __shared__ __attribute__((aligned(16))) float pat[8 * 2 * WPF];
+  __shared__ __attribute__((aligned(16))) float pat[8 * NBUF * WPF];
   __shared__ __attribute__((aligned(16))) float stg[(AUX & 16) ? 8 * 16 * 68 : 4];  // AUX & 16: the store slabs
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   float* const slab = stg + ((AUX & 16) ? wave * 16 * 68 : 0);
@@ -2812,24 +2831,42 @@ __global__ __launch_bounds__(512, MINW) void conv3x3_first_softmax_f32p(ConvArgs
   };
   const int col = lane & 15, q = lane >> 4;
   const float* Wt = reinterpret_cast<const float*>(a.w);
-  for (int e = tid; e < NS * 64; e += 512) {
-    const int st = e >> 6, l = e & 63;
-    const int kk = 4 * st + (l >> 4), co = l & 15;
-    const int tap = kk / CIN, c = kk - tap * CIN;
-    f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (kk < 9 * CIN)
+  if constexpr (X6) {
+    // k slot kk of a tap: part group g = kk / CIN (record [l, m, h, m, h, h] against filter parts [h, m, l, h, m, h]),
+    // channel kk % CIN; slots past 6 * CIN are zero
+    for (int e = tid; e < 9 * 4 * 64; e += 512) {
+      const int tap = e >> 8, fc = (e >> 6) & 3, l = e & 63;
+      const int co = fc * 16 + (l & 15);
+      uint32_t v[8];
 #pragma unroll
-      for (int fc = 0; fc < 4; ++fc) v[fc] = Wt[(long)(fc * 16 + co) * a.K_pad + tap * 8 + c];
-    wl[e] = v;
+      for (int j = 0; j < 8; ++j) {
+        const int kk = 8 * (l >> 4) + j, g = kk / CIN, c = kk - g * CIN;
+        uint32_t h = 0, m = 0, lo = 0;
+        if (kk < 6 * CIN) split3_bf16(Wt[(long)co * a.K_pad + tap * 8 + c], h, m, lo);
+        v[j] = g == 0 || g == 3 || g == 5 ? h : g == 1 || g == 4 ? m : g == 2 ? lo : 0u;
+      }
+      wx[e] = make_uint4(v[0] | v[1] << 16, v[2] | v[3] << 16, v[4] | v[5] << 16, v[6] | v[7] << 16);
+    }
+  } else {
+    for (int e = tid; e < NS * 64; e += 512) {
+      const int st = e >> 6, l = e & 63;
+      const int kk = 4 * st + (l >> 4), co = l & 15;
+      const int tap = kk / CIN, c = kk - tap * CIN;
+      f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (kk < 9 * CIN)
+#pragma unroll
+        for (int fc = 0; fc < 4; ++fc) v[fc] = Wt[(long)(fc * 16 + co) * a.K_pad + tap * 8 + c];
+      wl[e] = v;
+    }
+    if (tid < NS * 4) {
+      const int kk = tid;
+      const int tap = kk / CIN, c = kk - tap * CIN;
+      pl[tid] = kk < 9 * CIN ? c * SP + (tap / 3) * PW + tap % 3 : ZERO;
+    }
   }
-  if (tid < NS * 4) {
-    const int kk = tid;
-    const int tap = kk / CIN, c = kk - tap * CIN;
-    pl[tid] = kk < 9 * CIN ? c * SP + (tap / 3) * PW + tap % 3 : ZERO;
-  }
-  float* P0 = pat + wave * 2 * WPF;
-  float* P1 = P0 + WPF;
-  if (lane < 32) {
+  float* P0 = pat + wave * NBUF * WPF;
+  float* P1 = P0 + (NBUF - 1) * WPF;
+  if (!X6 && lane < 32) {
     P0[ZERO + lane] = 0.f;
     P1[ZERO + lane] = 0.f;
   }
@@ -2845,9 +2882,25 @@ __global__ __launch_bounds__(512, MINW) void conv3x3_first_softmax_f32p(ConvArgs
     for (int k = 0; k < 2; ++k) {
       const int e = lane + 64 * k;
       const float vv[8] = {v[k][0].x, v[k][0].y, v[k][0].z, v[k][0].w, v[k][1].x, v[k][1].y, v[k][1].z, v[k][1].w};
-      if (e < SP)
+      if constexpr (X6) {  // the pixel's 32-slot record [l, m, h, m, h, h] as 4 chunk planes of SP x 16 bytes
+        uint32_t h[CIN], m[CIN], lo[CIN], r[32];
+#pragma unroll
+        for (int c = 0; c < CIN; ++c) split3_bf16(vv[c], h[c], m[c], lo[c]);
+#pragma unroll
+        for (int kk = 0; kk < 32; ++kk) {
+          const int g = kk / CIN, c = kk % CIN;
+          r[kk] = kk >= 6 * CIN ? 0u : g == 0 ? lo[c] : (g == 1 || g == 3) ? m[c] : h[c];
+        }
+        if (e < SP)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            reinterpret_cast<uint4*>(P)[j * SP + e] =
+                make_uint4(r[8 * j] | r[8 * j + 1] << 16, r[8 * j + 2] | r[8 * j + 3] << 16,
+                           r[8 * j + 4] | r[8 * j + 5] << 16, r[8 * j + 6] | r[8 * j + 7] << 16);
+      } else if (e < SP) {
 #pragma unroll
         for (int c = 0; c < CIN; ++c) P[c * SP + e] = vv[c];
+      }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -2858,69 +2911,140 @@ __global__ __launch_bounds__(512, MINW) void conv3x3_first_softmax_f32p(ConvArgs
   // step's fragments are read under them
   // this lane's patch offsets of every K step (the pl table's entry for its k-slot q, plus its pixel column), held
   // in registers: read from LDS inside the step they made each step's fragment reads wait on a dependent LDS load
-  int poff[NS];
+  int poff[X6 ? 1 : NS];
+  if constexpr (!X6) {
 #pragma unroll
-  for (int s = 0; s < NS; ++s) poff[s] = pl[s * 4 + q] + col;
-  auto mma = [&](const float* P, f32x4 (&N)[4][2], f32x4* Cp, const __amdgpu_buffer_rsrc_t& yrs, int valid)
+    for (int s = 0; s < NS; ++s) poff[s] = pl[s * 4 + q] + col;
+  }
+  // x6: step s = tap s; A = the 4 cout fragments of the tap, B = chunk q of the records of pixels col, col + 16
+  auto mma_x6 = [&](const float* P, f32x4 (&N)[4][2], f32x4* Cp, const __amdgpu_buffer_rsrc_t& yrs, int valid)
       __attribute__((always_inline)) {
     init_strip_acc(N, rmul, aff, q);
     float mx[2] = {0.f, 0.f}, sm[2] = {0.f, 0.f};
-    f32x4 w4 = wl[lane];
-    float b0 = P[poff[0]], b1 = P[poff[0] + 16];
-    static_for<0, NS>([&](auto sc) __attribute__((always_inline)) {
+    const uint4* R = reinterpret_cast<const uint4*>(P) + q * SP + col;
+    uint4 av[4], bv[2];
+#pragma unroll
+    for (int fc = 0; fc < 4; ++fc) av[fc] = wx[fc * 64 + lane];
+    bv[0] = R[0];
+    bv[1] = R[16];
+    static_for<0, 9>([&](auto sc) __attribute__((always_inline)) {
       constexpr int s = decltype(sc)::value;
-      f32x4 w4n = w4;
-      float b0n = b0, b1n = b1;
-      if constexpr (s + 1 < NS) {
-        w4n = wl[(s + 1) * 64 + lane];
-        b0n = P[poff[s + 1]];
-        b1n = P[poff[s + 1] + 16];
+      uint4 an[4], bn[2];
+      if constexpr (s + 1 < 9) {
+        constexpr int toff = ((s + 1) / 3) * PW + (s + 1) % 3;
+#pragma unroll
+        for (int fc = 0; fc < 4; ++fc) an[fc] = wx[((s + 1) * 4 + fc) * 64 + lane];
+        bn[0] = R[toff];
+        bn[1] = R[toff + 16];
       }
-      if constexpr (ABL & 2) {
-        asm volatile("" ::"v"(w4[0]), "v"(w4[3]), "v"(b0), "v"(b1));
-      } else {
+      if constexpr (!(ABL & 2)) {
 #pragma unroll
         for (int fc = 0; fc < 4; ++fc) {
-          N[fc][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(w4[fc], b0, N[fc][0], 0, 0, 0);
-          N[fc][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(w4[fc], b1, N[fc][1], 0, 0, 0);
+          mma16<uint16_t>(av[fc], bv[0], N[fc][0]);
+          mma16<uint16_t>(av[fc], bv[1], N[fc][1]);
         }
       }
       if (Cp) {
-        if constexpr (s < 10)
-          softmax_chunk<AFF, s, ABL, AUX>(*reinterpret_cast<f32x4(*)[4][2]>(Cp), mx, sm, rmul, yrs, a.y_cstride, valid,
-                                          lane, slab);
+        softmax_chunk<AFF, s, ABL, AUX>(*reinterpret_cast<f32x4(*)[4][2]>(Cp), mx, sm, rmul, yrs, a.y_cstride, valid,
+                                        lane, slab);
       }
-      // the next step's fragment reads first (else hipcc sinks them to the step's end and the next step's first
-      // MFMA waits a whole LDS latency), then one MFMA per 3 VALU of the softmax chunk
-      if constexpr (s + 1 < NS) {
+      if constexpr (s + 1 < 9) {
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
         __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
+      } else {
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
       }
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
-      if constexpr (s + 1 >= NS) __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
       __builtin_amdgcn_sched_barrier(0);
-      w4 = w4n;
-      b0 = b0n;
-      b1 = b1n;
+      if constexpr (s + 1 < 9) {
+#pragma unroll
+        for (int fc = 0; fc < 4; ++fc) av[fc] = an[fc];
+        bv[0] = bn[0];
+        bv[1] = bn[1];
+      }
     });
-    if (Cp) {  // a short K loop (CIN < 4): the chunks left over
-      static_for<NS, 10>([&](auto sc) __attribute__((always_inline)) {
-        softmax_chunk<AFF, decltype(sc)::value, ABL, AUX>(*reinterpret_cast<f32x4(*)[4][2]>(Cp), mx, sm, rmul, yrs,
-                                                           a.y_cstride, valid, lane, slab);
+    if (Cp) {  // the 10th chunk
+      softmax_chunk<AFF, 9, ABL, AUX>(*reinterpret_cast<f32x4(*)[4][2]>(Cp), mx, sm, rmul, yrs, a.y_cstride, valid,
+                                      lane, slab);
+    }
+  };
+  auto mma = [&](const float* P, f32x4 (&N)[4][2], f32x4* Cp, const __amdgpu_buffer_rsrc_t& yrs, int valid)
+      __attribute__((always_inline)) {
+    if constexpr (X6) {
+      mma_x6(P, N, Cp, yrs, valid);
+    } else {
+      init_strip_acc(N, rmul, aff, q);
+      float mx[2] = {0.f, 0.f}, sm[2] = {0.f, 0.f};
+      f32x4 w4 = wl[lane];
+      float b0 = P[poff[0]], b1 = P[poff[0] + 16];
+      static_for<0, NS>([&](auto sc) __attribute__((always_inline)) {
+        constexpr int s = decltype(sc)::value;
+        f32x4 w4n = w4;
+        float b0n = b0, b1n = b1;
+        if constexpr (s + 1 < NS) {
+          w4n = wl[(s + 1) * 64 + lane];
+          b0n = P[poff[s + 1]];
+          b1n = P[poff[s + 1] + 16];
+        }
+        if constexpr (ABL & 2) {
+          asm volatile("" ::"v"(w4[0]), "v"(w4[3]), "v"(b0), "v"(b1));
+        } else {
+  #pragma unroll
+          for (int fc = 0; fc < 4; ++fc) {
+            N[fc][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(w4[fc], b0, N[fc][0], 0, 0, 0);
+            N[fc][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(w4[fc], b1, N[fc][1], 0, 0, 0);
+          }
+        }
+        if (Cp) {
+          if constexpr (s < 10)
+            softmax_chunk<AFF, s, ABL, AUX>(*reinterpret_cast<f32x4(*)[4][2]>(Cp), mx, sm, rmul, yrs, a.y_cstride, valid,
+                                            lane, slab);
+        }
+        // the next step's fragment reads first (else hipcc sinks them to the step's end and the next step's first
+        // MFMA waits a whole LDS latency), then one MFMA per 3 VALU of the softmax chunk
+        if constexpr (s + 1 < NS) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+        if constexpr (s + 1 >= NS) __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        w4 = w4n;
+        b0 = b0n;
+        b1 = b1n;
       });
+      if (Cp) {  // a short K loop (CIN < 4): the chunks left over
+        static_for<NS, 10>([&](auto sc) __attribute__((always_inline)) {
+          softmax_chunk<AFF, decltype(sc)::value, ABL, AUX>(*reinterpret_cast<f32x4(*)[4][2]>(Cp), mx, sm, rmul, yrs,
+                                                             a.y_cstride, valid, lane, slab);
+        });
+      }
     }
   };
   auto yrs_of = [&](const SC& sc, int& valid) __attribute__((always_inline)) {
@@ -4877,6 +5001,19 @@ static int launch_first_softmax_f32(ConvArgs& a, int cin, hipStream_t st) {
       return check_launch("conv3x3_first_softmax_f32p");
     }
 #endif
+    if (cin <= 5 && g_softmax_f32p == 7) {  // split-bf16 x6 on the bf16 MFMA (f32 accuracy; X6 above)
+      switch (cin) {
+#define VM_SMX(C)                                                                                        \
+  case C:                                                                                                \
+    snprintf(g_last_kernel, sizeof g_last_kernel, "vm::conv3x3_first_softmax_f32p<%d, 2, false, 0, 18, true>", C); \
+    hipLaunchKernelGGL((conv3x3_first_softmax_f32p<C, 2, false, 0, 18, true>), dim3(gp), dim3(512), 0, st, a);     \
+    break;
+        VM_SMX(1) VM_SMX(2) VM_SMX(3) VM_SMX(4) VM_SMX(5)
+#undef VM_SMX
+        default: break;
+      }
+      return check_launch("conv3x3_first_softmax_f32p");
+    }
     if (cin == 5 && g_softmax_f32p == 2) {
       snprintf(g_last_kernel, sizeof g_last_kernel, "vm::conv3x3_first_softmax_f32p<5, 4>");
       hipLaunchKernelGGL((conv3x3_first_softmax_f32p<5, 4>), dim3(gp), dim3(512), 0, st, a);
@@ -4988,8 +5125,8 @@ extern "C" int vm_set_option(const char* key, long value) {
   }
   if (!strcmp(key, "softmax_f32p")) {  // 0 the r03 kernel; 1 pipelined; 2 its 4-waves-per-SIMD build; 3 NT stores;
                                        // 4 / 5 LDS-transposed whole-pixel stores, NT / through L2;
-                                       // 6 the row-ring form (conv3x3_first_softmax_f32r)
-    if (value < 0 || value > 6) return fail(VM_EINVAL, "softmax_f32p must be 0..6");
+                                       // 6 the row-ring form (conv3x3_first_softmax_f32r); 7 split-bf16 x6
+    if (value < 0 || value > 7) return fail(VM_EINVAL, "softmax_f32p must be 0..7");
     g_softmax_f32p = value;
     return VM_OK;
   }
