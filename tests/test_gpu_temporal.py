@@ -133,6 +133,14 @@ def test_temporal_index_error():
     tp = temporal.TemporalRefiner(dtype="fp32")
     with pytest.raises(IndexError):
         tp(T(prev), T(cur), T(cmp), T(bw), T(fw))
+    # the error flag is not re-zeroed per call: after the raise, an unchecked call over the bad flow and a checked
+    # call over a good one must not report it; a checked call over the bad flow raises again
+    _, _, _, bw_ok, _, _ = _case(16, 20)
+    tp(T(prev), T(cur), T(cmp), T(bw_ok), T(fw))
+    tp(T(prev), T(cur), T(cmp), T(bw), T(fw), check_index=False)
+    tp(T(prev), T(cur), T(cmp), T(bw_ok), T(fw))
+    with pytest.raises(IndexError):
+        tp(T(prev), T(cur), T(cmp), T(bw), T(fw))
 
 
 @pytest.mark.parametrize("n,h,w", [(1, 37, 70), (2, 8, 32), (1, 1, 1), (1, 135, 240), (1, 17, 33)])

@@ -46,6 +46,9 @@ class TemporalRefiner:
         self.promote = 0 if promote == "numpy1" else 1
         self.thresh = float(thresh)
         self._bufs = {}
+        # the IndexError flag is zeroed when allocated and after a raised error; a call that does not read it
+        # (check_index=False) leaves it unknown, and the next checked call zeroes it first (no fill launch per call)
+        self._err_dirty = set()
 
     def _buffers(self, h, w):
         b = self._bufs.get((h, w))
@@ -67,12 +70,17 @@ class TemporalRefiner:
         backward = _f32c(backward, (h, w, 2), "backward")
         forward = _f32c(forward, (h, w, 2), "forward")
         b = self._buffers(h, w)
-        b["err"].zero_()
+        if check_index and (h, w) in self._err_dirty:
+            b["err"].zero_()
+            self._err_dirty.discard((h, w))
         P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
         check(lib().vm_temporal_refine_input(P(prev_alpha), P(backward), P(forward), P(cmp), P(alpha), h, w,
                                              self.thresh, self.promote, P(b["xin"]), ops._DT[self.dtype],
                                              P(b["warped"]), P(b["err"]), stream_handle()), "temporal_refine_input")
-        if check_index and int(b["err"].item()) != 0:
+        if not check_index:
+            self._err_dirty.add((h, w))
+        elif int(b["err"].item()) != 0:
+            b["err"].zero_()
             raise IndexError("correct_alpha: a backward-flow target lies more than one frame outside the image "
                              "(the reference's numpy IndexError, flow.py:46)")
         self.warped = b["warped"]
