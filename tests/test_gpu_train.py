@@ -122,6 +122,37 @@ def test_conv_wgrad_wide(cin, cout, n, h, w, mode):
             assert scaled_err(H(dw) - 1.0, wr.grad.numpy()) <= 1e-5
 
 
+@pytest.mark.parametrize("cin,cout,n,h,w", [(6, 64, 2, 37, 45), (64, 64, 2, 33, 70), (200, 128, 1, 9, 40),
+                                            (512, 512, 2, 20, 20), (128, 64, 8, 40, 40)])
+@pytest.mark.parametrize("dyf32", [False, True])
+def test_conv_wgrad_wide_pipelined_bit_identical(cin, cout, n, h, w, dyf32):
+    """wgrad_wide_kernel's pipelined inner loop (wgrad_wide_pipe 1: unrolled rows, per-lane fragment bases, the next
+    tap's fragments read under the current MFMAs, one block per CU) against the plain loop at the same K-split
+    (wgrad_wide_target): every accumulator sees the same MFMAs in the same order, so the gradients are bit-identical;
+    then the default split of each (256 / 512 blocks) within the f32 summation bound of each other."""
+    from vmatting import _lib, ops
+    rs = np.random.RandomState(cin * 3 + h)
+    x = rs.normal(size=(n, h, w, (cin + 7) // 8 * 8)).astype(np.float32)
+    dy = rs.normal(size=(n, h, w, cout)).astype(np.float32)
+    xd = T(x, torch.bfloat16)[..., :cin]
+    d = T(dy) if dyf32 else T(dy, torch.bfloat16)
+    out = {}
+    try:
+        for target in (256, 0):
+            _lib.set_option("wgrad_wide_target", target)
+            for pipe in (0, 1):
+                _lib.set_option("wgrad_wide_pipe", pipe)
+                dw = torch.zeros((3, 3, cin, cout), dtype=torch.float32, device=DEV)
+                ops.conv_wgrad(xd, d, dw, mfma=True)
+                out[target, pipe] = dw
+    finally:
+        _lib.set_option("wgrad_wide_pipe", 1)
+        _lib.set_option("wgrad_wide_target", 0)
+    assert torch.equal(out[256, 0], out[256, 1])
+    a, b = H(out[0, 0]), H(out[0, 1])
+    assert np.abs(a - b).max() <= 1e-5 * max(1.0, float(np.abs(a).max())), np.abs(a - b).max()
+
+
 def test_conv_wgrad_wide_rejects_split_sources():
     from vmatting import ops
     x = torch.zeros((2, 4, 4, 16), dtype=torch.bfloat16, device=DEV)
@@ -558,6 +589,32 @@ def wgrad_opts():
 # (wgrad_taps, wgrad_variant, wgrad_dma): the register-staged taps-in-N kernel for cout <= 8 (the default), the LDS-DMA
 # narrow kernel (an A/B option: cout <= 16, cin % 8 == 0), the taps kernel with 8-row tiles, and the per-tap kernel
 WGRAD_VARIANTS = [(1, 0, 0), (1, 0, 1), (1, 2, 0), (0, 0, 0)]
+
+
+@pytest.mark.parametrize("th8", [0, 2])
+@pytest.mark.parametrize("cin,cout", [(9, 16), (30, 16), (64, 16), (30, 24), (40, 32), (70, 48), (192, 16),
+                                      (16, 32)])
+def test_conv_wgrad_mfma_pipelined_bit_identical(cin, cout, th8, wgrad_opts):
+    """wgrad_mfma_kernel's pipelined form (wgrad_mfma_pipe 1: fragment addresses computed once per kernel, a row's
+    fragments read up front) writes exactly the plain loop's gradients: same MFMAs per accumulator, same order; 4- and
+    8-row tiles, the shifted-x and shifted-dy forms (cout 16 with cin > 16 shifts dy)."""
+    from vmatting import ops
+    rs = np.random.RandomState(cin * 7 + cout)
+    n, h, w = 2, 21, 45
+    xd = T(rs.normal(size=(n, h, w, (cin + 7) // 8 * 8)).astype(np.float32), torch.bfloat16)[..., :cin]
+    dy = T(rs.normal(size=(n, h, w, cout)).astype(np.float32))
+    out = []
+    try:
+        wgrad_opts("wgrad_taps", 0)  # (cout <= 8 would take the taps-in-N kernel)
+        wgrad_opts("wgrad_variant", th8)
+        for pipe in (0, 1):
+            wgrad_opts("wgrad_mfma_pipe", pipe)
+            dw = torch.zeros((3, 3, cin, cout), dtype=torch.float32, device=DEV)
+            ops.conv_wgrad(xd, dy, dw, mfma=True)
+            out.append(dw)
+    finally:
+        wgrad_opts("wgrad_mfma_pipe", 1)
+    assert torch.equal(out[0], out[1])
 
 
 @pytest.mark.parametrize("variant", WGRAD_VARIANTS)

@@ -2654,13 +2654,6 @@ __global__ __launch_bounds__(512, 4) void conv3x3_first_softmax_f32(ConvArgs a) 
 // whose out-of-range offsets drop the pixels past the frame — no LDS transpose, no wave barrier, no branch; the next
 // strip's global loads are clamped the same way.  Arithmetic per output is the non-pipelined kernel's (same K order,
 // same softmax expression), so results are bit-identical to it.
-template <int I, int N, typename F>
-__device__ __forceinline__ void static_for(F&& f) {
-  if constexpr (I < N) {
-    f(std::integral_constant<int, I>{});
-    static_for<I + 1, N>(f);
-  }
-}
 
 // The strip softmax of softmax_store_strip cut into 10 chunks, one per K step of the next strip's MFMAs, computed in
 // place in the accumulators C (acc[fc][fp]: pixel fp*16 + col, channels fc*16 + 4q .. +3); same operations in the same

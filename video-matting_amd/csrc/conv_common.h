@@ -1,6 +1,8 @@
 // Conv argument block and device helpers shared by the 3x3 conv kernels (conv3x3.hip, conv_rows.hip).
 #pragma once
 
+#include <type_traits>
+
 #include "vm_common.h"
 
 namespace vm {
@@ -64,6 +66,15 @@ struct ConvArgs {
   // that hold the band's third round)
   int halfskip;
 };
+
+// compile-time loop: f(std::integral_constant<int, I>) for I in [I, N)
+template <int I, int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<I + 1, N>(f);
+  }
+}
 
 // a pointer every lane holds the same value of, moved to SGPRs (buffer descriptors must be scalar)
 template <typename P>

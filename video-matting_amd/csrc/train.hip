@@ -736,7 +736,11 @@ __device__ __forceinline__ bf16x8 wm_frag(const char* img, int r0, int c, int la
   return __builtin_bit_cast(bf16x8, v);
 }
 
-template <int NCI, int NCO, bool SX, int TH>
+// PIPE (r05): every fragment address is computed once per kernel (the LDS images keep their layout from tile to
+// tile) and the next tap's fragments are read while the current tap's MFMAs run (the plain loop let hipcc recompute
+// the swizzled addresses and wait lgkmcnt(0) in front of every tap's MFMAs).  Same MFMAs per accumulator in the same
+// order: bit-identical.
+template <int NCI, int NCO, bool SX, int TH, bool PIPE = true>
 __global__ __launch_bounds__(256, 2) void wgrad_mfma_kernel(WgArgs a) {
   constexpr int WM_TH = TH, WM_PPIX = wm_ppix<TH>(), WM_PROWS = wm_prows<TH>();
   constexpr int CIB = NCI * 16, COP = NCO * 16;
@@ -867,6 +871,69 @@ __global__ __launch_bounds__(256, 2) void wgrad_mfma_kernel(WgArgs a) {
   // gridDim-strided walk jumps megabytes per step and pays TLB misses on every one)
   const int t_beg = (int)((long)blockIdx.x * a.ntiles / gridDim.x);
   const int t_end = (int)((long)(blockIdx.x + 1) * a.ntiles / gridDim.x);
+  if constexpr (PIPE) {
+    constexpr int RR = TH / 4, NTX = SX ? 9 : 1, NTD = SX ? 1 : 9;
+    const int q = (lane >> 2) & 3, p = lane & 3;
+    int xa[RR][NTX][NCI][2], da[RR][NTD][NCO][2];  // byte offsets of the lo / hi reads of every fragment
+#pragma unroll
+    for (int rr = 0; rr < RR; ++rr) {
+      const int row = wave + 4 * rr;
+#pragma unroll
+      for (int tt = 0; tt < NTX; ++tt) {
+        const int r0 = SX ? (row + tt / 3) * WM_PW + tt % 3 + 8 * g : row * WM_TW + 8 * g;
+#pragma unroll
+        for (int i = 0; i < NCI; ++i)
+#pragma unroll
+          for (int h = 0; h < 2; ++h) xa[rr][tt][i][h] = wm_off<RBX>(r0 + 4 * h + q, i) + 8 * p;
+      }
+#pragma unroll
+      for (int tt = 0; tt < NTD; ++tt) {
+        const int r0 = SX ? row * WM_TW + 8 * g : (row + 2 - tt / 3) * WM_PW + 2 - tt % 3 + 8 * g;
+#pragma unroll
+        for (int o = 0; o < NCO; ++o)
+#pragma unroll
+          for (int h = 0; h < 2; ++h) da[rr][tt][o][h] = wm_off<RBD>(r0 + 4 * h + q, o) + 8 * p;
+      }
+    }
+    auto frag = [&](const char* img, const int (&ad)[2]) __attribute__((always_inline)) {
+      typedef __attribute__((address_space(3))) v4s* lp;
+      const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(img + ad[0]));
+      const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(img + ad[1]));
+      v4s v[2] = {lo, hi};
+      return __builtin_bit_cast(bf16x8, v);
+    };
+    constexpr int NP = SX ? NCI : NCO;  // fragments read per tap (the shifted operand)
+    if (t_beg < t_end) issue(t_beg);
+    for (int tile = t_beg; tile < t_end; ++tile) {
+      commit();
+      __syncthreads();
+      if (tile + 1 < t_end) issue(tile + 1);
+      // (a row's 9 taps carry only 9 x NCI x NCO MFMAs, too few to hide a read one tap ahead: all of the row's
+      // fragments are read up front and the MFMAs wait for them in order)
+      static_for<0, RR>([&](auto rc) __attribute__((always_inline)) {
+        constexpr int rr = decltype(rc)::value;
+        bf16x8 fix[SX ? NCO : NCI], sh[9][NP];  // the per-row operand, the per-tap one
+#pragma unroll
+        for (int k = 0; k < (SX ? NCO : NCI); ++k) fix[k] = SX ? frag(dimg, da[rr][0][k]) : frag(ximg, xa[rr][0][k]);
+#pragma unroll
+        for (int t = 0; t < 9; ++t)
+#pragma unroll
+          for (int k = 0; k < NP; ++k) sh[t][k] = SX ? frag(ximg, xa[rr][SX ? t : 0][k]) : frag(dimg, da[rr][SX ? 0 : t][k]);
+#pragma unroll
+        for (int t = 0; t < 9; ++t)
+#pragma unroll
+          for (int i = 0; i < NCI; ++i)
+#pragma unroll
+            for (int o = 0; o < NCO; ++o)
+              acc[t][i][o] = SX ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(sh[t][i], fix[o], acc[t][i][o], 0, 0, 0)
+                                : __builtin_amdgcn_mfma_f32_16x16x32_bf16(fix[i], sh[t][o], acc[t][i][o], 0, 0, 0);
+        // (pinned: left alone, hipcc sinks each tap's reads to just before its MFMAs to keep 3 waves per SIMD)
+        __builtin_amdgcn_sched_group_barrier(0x100, 2 * ((SX ? NCO : NCI) + 9 * NP), 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 9 * NCI * NCO, 0);
+      });
+      __syncthreads();
+    }
+  } else {
   if (t_beg < t_end) issue(t_beg);
   for (int tile = t_beg; tile < t_end; ++tile) {
     commit();
@@ -910,6 +977,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_mfma_kernel(WgArgs a) {
       }
     }
     __syncthreads();
+  }
   }
 
   // fold the 4 waves' accumulators (LDS, two rounds), wave 0 stores the block's partial
@@ -1414,8 +1482,31 @@ struct WwArgs {
 constexpr int WW_TH = 4;
 constexpr int WW_TARGET_BLOCKS = 512;  // ~2 resident blocks per CU: one round; the partials stay <= 75 MB
 
-template <int TH, bool DYF32>
-__global__ __launch_bounds__(256, 2) void wgrad_wide_kernel(WwArgs a) {  // A/B (scripts/build_variant.sh):
+// Pipelined fragment reads (PIPE, r05).  The plain loop below left hipcc a per-tap chain of ~12 VALU for the
+// swizzled row address, two ds_read_b64_tr_b16 and an lgkmcnt(0) wait in front of every 4 MFMAs, so each tap paid
+// the whole LDS latency.  The row loop is unrolled and every fragment address is a per-lane base register plus an
+// immediate: wm_off<128>(C + u, c) = 128 C + [128 u + 32 (c ^ x((C + u) mod 16))] for the lane's u = 8g + q, so 16
+// bases per X piece (C mod 16) and 2 per DY piece cover every (row, tap); the next tap's X fragment (and, over the
+// last two taps of a row, the next row's DY fragments and first X fragment) is read while the current tap's MFMAs
+// run.  Each accumulator sees the same MFMAs in the same order: bit-identical to the plain loop.
+template <int RB>
+__device__ __forceinline__ int wm_base(int u, int c, int p) {  // wm_off<RB>(u, c) + 8p, RB = 128
+  static_assert(RB == 128, "the 128-byte image rows of wgrad_wide_kernel");
+  return 128 * u + 32 * (c ^ ((u >> 1) & 1) ^ (((u >> 3) & 1) << 1)) + 8 * p;
+}
+
+template <int C>  // fragment whose k rows are image rows C + u (lo) and C + 4 + u (hi), bases per C mod 16
+__device__ __forceinline__ bf16x8 wm_frag_b(const char* img, const int (&b)[16]) {
+  typedef __attribute__((address_space(3))) v4s* lp;
+  const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(img + 128 * C + b[C & 15]));
+  const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(img + 128 * (C + 4) + b[(C + 4) & 15]));
+  v4s v[2] = {lo, hi};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+// PIPE: one block per CU (the unrolled rows, the bases and the next tile's staging registers need > 256 VGPRs)
+template <int TH, bool DYF32, bool PIPE = true>
+__global__ __launch_bounds__(256, PIPE ? 1 : 2) void wgrad_wide_kernel(WwArgs a) {  // A/B (scripts/build_variant.sh):
                                                                            // (256,2) 2.58 ms vs (256,1) 2.87 ms
   constexpr int XPIX = wm_ppix<TH>(), DPIX = TH * WM_TW;
   constexpr int XBYTES = wm_prows<TH>() * 128;
@@ -1519,6 +1610,53 @@ __global__ __launch_bounds__(256, 2) void wgrad_wide_kernel(WwArgs a) {  // A/B 
   const int g = lane >> 4;
   const int t_beg = (int)((long)kx * a.ntiles / a.gx);
   const int t_end = (int)((long)(kx + 1) * a.ntiles / a.gx);
+  if constexpr (PIPE) {
+    // per-lane fragment bases: X piece `wave` for every C mod 16, DY piece o for C mod 16 in {0, 4} (C = 32 row)
+    const int u = 8 * g + ((lane >> 2) & 3), p = lane & 3;
+    int bx[16], bdy[4][16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) bx[k] = wm_base<128>(k + u, wave, p) - 128 * k;
+#pragma unroll
+    for (int o = 0; o < 4; ++o)
+#pragma unroll
+      for (int k = 0; k < 16; ++k) bdy[o][k] = (k == 0 || k == 4) ? wm_base<128>(k + u, o, p) - 128 * k : 0;
+    if (t_beg < t_end) issue(t_beg);
+    for (int tile = t_beg; tile < t_end; ++tile) {
+      commit();
+      __syncthreads();
+      if (tile + 1 < t_end) issue(tile + 1);
+      bf16x8 bd[2][4], ax[2];
+#pragma unroll
+      for (int o = 0; o < 4; ++o) bd[0][o] = wm_frag_b<0>(dimg, bdy[o]);
+      ax[0] = wm_frag_b<0>(ximg, bx);
+      static_for<0, TH>([&](auto rc) __attribute__((always_inline)) {
+        constexpr int row = decltype(rc)::value, cb = row & 1;
+        static_for<0, 9>([&](auto tc) __attribute__((always_inline)) {
+          constexpr int t = decltype(tc)::value;
+          constexpr int gi = row * 9 + t;  // X fragments alternate between two slots over the tile's rows x taps
+          if constexpr (t + 1 < 9) {
+            constexpr int C = (row + (t + 1) / 3) * WM_PW + (t + 1) % 3;
+            ax[(gi + 1) & 1] = wm_frag_b<C>(ximg, bx);
+          } else if constexpr (row + 1 < TH) {
+            constexpr int C = (row + 1) * WM_PW;  // the next row's tap 0
+            ax[(gi + 1) & 1] = wm_frag_b<C>(ximg, bx);
+          }
+          if constexpr (t == 7 && row + 1 < TH) {
+#pragma unroll
+            for (int o = 0; o < 4; ++o) bd[cb ^ 1][o] = wm_frag_b<(row + 1) * WM_TW>(dimg, bdy[o]);
+          }
+#pragma unroll
+          for (int o = 0; o < 4; ++o)
+            acc[t][o] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ax[gi & 1], bd[cb][o], acc[t][o], 0, 0, 0);
+          // the reads issued above go out ahead of this tap's MFMAs
+          if constexpr (t == 7 && row + 1 < TH) __builtin_amdgcn_sched_group_barrier(0x100, 10, 0);
+          else if constexpr (t + 1 < 9 || row + 1 < TH) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+        });
+      });
+      __syncthreads();
+    }
+  } else {
   if (t_beg < t_end) issue(t_beg);
   for (int tile = t_beg; tile < t_end; ++tile) {
     commit();
@@ -1538,6 +1676,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_wide_kernel(WwArgs a) {  // A/B 
       }
     }
     __syncthreads();
+  }
   }
 
   // this block's partial of its 64 x 64 x 9 tile (lanes: co = lane & 15, ci = 4 * (lane >> 4) + j)
@@ -1804,14 +1943,20 @@ static int launch_wgrad_grid(const void* kern, int lds, int th, int cib, int& at
   return VM_OK;
 }
 
-template <int NCI, int NCO, bool SX, int TH>
-static int launch_wgrad_mfma_t(WgArgs& a, float* dw, hipStream_t st) {
+static long g_wgrad_mfma_pipe = 1;  // vm_set_option "wgrad_mfma_pipe": 0 = wgrad_mfma_kernel's plain loop (A/B)
+template <int NCI, int NCO, bool SX, int TH, bool PIPE>
+static int launch_wgrad_mfma_p(WgArgs& a, float* dw, hipStream_t st) {
   static int attr_dev = -1, resident = 0;  // blocks of this variant resident on the whole chip at once
-  return launch_wgrad_grid(reinterpret_cast<const void*>(&wgrad_mfma_kernel<NCI, NCO, SX, TH>),
+  return launch_wgrad_grid(reinterpret_cast<const void*>(&wgrad_mfma_kernel<NCI, NCO, SX, TH, PIPE>),
                            wgrad_mfma_lds<NCI, NCO, SX, TH>(), TH, NCI * 16, attr_dev, resident, a, dw, st,
                            [](dim3 g, int lds, hipStream_t s, const WgArgs& x) {
-                             hipLaunchKernelGGL((wgrad_mfma_kernel<NCI, NCO, SX, TH>), g, dim3(256), lds, s, x);
+                             hipLaunchKernelGGL((wgrad_mfma_kernel<NCI, NCO, SX, TH, PIPE>), g, dim3(256), lds, s, x);
                            });
+}
+template <int NCI, int NCO, bool SX, int TH>
+static int launch_wgrad_mfma_t(WgArgs& a, float* dw, hipStream_t st) {
+  return g_wgrad_mfma_pipe ? launch_wgrad_mfma_p<NCI, NCO, SX, TH, true>(a, dw, st)
+                           : launch_wgrad_mfma_p<NCI, NCO, SX, TH, false>(a, dw, st);
 }
 
 template <int NCI, int NT, int TH>
@@ -1838,6 +1983,9 @@ static bool wgrad_dma_ok(const WgArgs& a, int cib) {
          reinterpret_cast<uintptr_t>(a.x) % 16 == 0 && (a.x_src_c <= 0 || (a.x_src_c % cib == 0 && a.x_src_stride % 8 == 0)) &&
          (long)a.h * a.w * a.xcs * 2 < 0x7ff00000L && (long)a.h * a.w * a.dcs * 4 < 0x7ff00000L;
 }
+
+static long g_wgrad_wide_pipe = 1;  // vm_set_option "wgrad_wide_pipe": 0 = the plain-loop kernel at 2 blocks per CU (A/B)
+static long g_wgrad_wide_target = 0;  // vm_set_option "wgrad_wide_target": > 0 overrides the K-split's block target
 
 static long g_wgrad_dma_cfg = 0;  // vm_set_option "wgrad_dma_cfg" (A/B): 0 auto, 1 = 8-row tiles, 2 = 4 rows x 6 slots
 
@@ -1899,6 +2047,18 @@ int train_set_option(const char* key, long value) {
     trn::g_wgrad_dma = value;
     return 1;
   }
+  if (!strcmp(key, "wgrad_mfma_pipe")) {
+    trn::g_wgrad_mfma_pipe = value;
+    return 1;
+  }
+  if (!strcmp(key, "wgrad_wide_pipe")) {
+    trn::g_wgrad_wide_pipe = value;
+    return 1;
+  }
+  if (!strcmp(key, "wgrad_wide_target")) {  // (<= WW_TARGET_BLOCKS: the workspace query's bound)
+    trn::g_wgrad_wide_target = value;
+    return 1;
+  }
   if (!strcmp(key, "wgrad_dma_cfg")) {
     trn::g_wgrad_dma_cfg = value;
     return 1;
@@ -1943,7 +2103,7 @@ static int launch_wgrad_mfma(WgArgs& a, float* dw, hipStream_t st) {
 // tile (bf16) / 32-pixel chunk (f32), and partials of at most WW_WS_CAP bytes
 constexpr size_t WW_WS_CAP = 128ull << 20;
 
-static long wgrad_wide_gx(int n, int h, int w, int cin, int cout, bool f32) {
+static long wgrad_wide_gx(int n, int h, int w, int cin, int cout, bool f32, long target = WW_TARGET_BLOCKS) {
   long units, nch;
   if (f32) {
     units = ((long)n * h * w + 31) / 32;
@@ -1952,7 +2112,7 @@ static long wgrad_wide_gx(int n, int h, int w, int cin, int cout, bool f32) {
     units = (long)n * ((h + WW_TH - 1) / WW_TH) * ((w + WM_TW - 1) / WM_TW);
     nch = (long)((cin + 63) / 64) * (cout / 64);
   }
-  long gx = (WW_TARGET_BLOCKS + nch - 1) / nch;
+  long gx = (target + nch - 1) / nch;
   const long cap = (long)(WW_WS_CAP / (9ull * cin * cout * sizeof(float)));
   if (gx > cap) gx = cap;
   if (gx > units) gx = units;
@@ -1974,7 +2134,11 @@ static int launch_wgrad_wide(const vm_tensor* x, const vm_tensor* dy, float* dw,
   if (a.ntiles > 0x7fffffffL) return fail(VM_EUNSUPPORTED, "conv_wgrad: too many pixel tiles");
   a.ncin = (a.cin + 63) / 64;
   a.ncout = a.cout / 64;
-  a.gx = (int)wgrad_wide_gx(a.n, a.h, a.w, a.cin, a.cout, false);
+  // the pipelined kernel runs one block per CU: one resident round of WW_TARGET_BLOCKS / 2 blocks (half the partials)
+  const bool pipe = g_wgrad_wide_pipe != 0;
+  long target = pipe ? WW_TARGET_BLOCKS / 2 : WW_TARGET_BLOCKS;
+  if (g_wgrad_wide_target > 0 && g_wgrad_wide_target <= WW_TARGET_BLOCKS) target = g_wgrad_wide_target;
+  a.gx = (int)wgrad_wide_gx(a.n, a.h, a.w, a.cin, a.cout, false, target);
   const long nb = (long)a.gx * a.ncin * a.ncout;
   if (nb > 0x7fffffffL) return fail(VM_EUNSUPPORTED, "conv_wgrad: grid too large");
   constexpr int lds = wgrad_wide_lds<WW_TH>();
@@ -1985,10 +2149,14 @@ static int launch_wgrad_wide(const vm_tensor* x, const vm_tensor* dy, float* dw,
     if (attr != dev) {
       hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_wide_kernel<WW_TH, true>),
                                          hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+      if (e == hipSuccess)
+        e = hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_wide_kernel<WW_TH, true, false>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, lds);
       if (e != hipSuccess) return fail(VM_EHIP, "wgrad_wide setup: %s", hipGetErrorString(e));
       attr = dev;
     }
-    hipLaunchKernelGGL((wgrad_wide_kernel<WW_TH, true>), dim3((unsigned)nb), dim3(256), lds, st, a);
+    if (pipe) hipLaunchKernelGGL((wgrad_wide_kernel<WW_TH, true>), dim3((unsigned)nb), dim3(256), lds, st, a);
+    else hipLaunchKernelGGL((wgrad_wide_kernel<WW_TH, true, false>), dim3((unsigned)nb), dim3(256), lds, st, a);
   } else {
     static int attr = -1;
     int dev = 0;
@@ -1996,10 +2164,14 @@ static int launch_wgrad_wide(const vm_tensor* x, const vm_tensor* dy, float* dw,
     if (attr != dev) {
       hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_wide_kernel<WW_TH, false>),
                                          hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+      if (e == hipSuccess)
+        e = hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_wide_kernel<WW_TH, false, false>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, lds);
       if (e != hipSuccess) return fail(VM_EHIP, "wgrad_wide setup: %s", hipGetErrorString(e));
       attr = dev;
     }
-    hipLaunchKernelGGL((wgrad_wide_kernel<WW_TH, false>), dim3((unsigned)nb), dim3(256), lds, st, a);
+    if (pipe) hipLaunchKernelGGL((wgrad_wide_kernel<WW_TH, false>), dim3((unsigned)nb), dim3(256), lds, st, a);
+    else hipLaunchKernelGGL((wgrad_wide_kernel<WW_TH, false, false>), dim3((unsigned)nb), dim3(256), lds, st, a);
   }
   launch_wgrad_reduce(a.part, a.gx, 9L * a.cin * a.cout, dw, st);
   return VM_OK;
