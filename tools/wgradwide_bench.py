@@ -1,5 +1,6 @@
 """The wide weight gradients of the UNetImage training step (8 x 320^2, bf16 x and bf16 dy, every conv but conv1_5):
-per-layer ms / TFLOP/s and the total.   python tools/wgradwide_bench.py [iters]   (VM_LIB_PATH for an A/B build)"""
+per-layer ms / TFLOP/s and the total.   python tools/wgradwide_bench.py [iters] [key=value ...]   (vm_set_option
+A/B knobs, e.g. wgrad_wide_pipe=0; VM_LIB_PATH for an A/B build)"""
 import os
 import sys
 
@@ -8,7 +9,7 @@ sys.path[:0] = [REPO, os.path.join(REPO, "video-matting_amd")]
 
 import torch  # noqa: E402
 
-from vmatting import ops  # noqa: E402
+from vmatting import _lib, ops  # noqa: E402
 
 # (name, side, cin, cout) at 8 x 320^2 (unet.py:96-143)
 SHAPES = [("upconv_4", 320, 128, 64), ("conv2_3", 160, 256, 128), ("upconv_3", 160, 256, 128),
@@ -21,6 +22,9 @@ SHAPES = [("upconv_4", 320, 128, 64), ("conv2_3", 160, 256, 128), ("upconv_3", 1
 
 def main():
     iters = int(sys.argv[1]) if len(sys.argv) > 1 else 10
+    for kv in sys.argv[2:]:
+        k, v = kv.split("=")
+        _lib.set_option(k, int(v))
     tot_ms, tot_fl = 0.0, 0.0
     for name, s, cin, cout in SHAPES:
         cs = (cin + 7) // 8 * 8
