@@ -1021,6 +1021,37 @@ def test_train_step_bf16_gradients_bench_shape():
 
 
 @pytest.mark.parametrize("pool", [False, True])
+@pytest.mark.parametrize("with_add", [False, True])
+@pytest.mark.parametrize("c", [8, 64, 128, 512])
+def test_relu_backward_bias_vectorised_bit_identical(pool, with_add, c):
+    """The 8-channels-per-lane form of vm_relu_backward_bias_nhwc (relu_bias_vec 1, bf16 y / dz) writes exactly the
+    per-element form's dz (same arithmetic per element, first-maximum pool adjoint, odd edges), and the bias gradient
+    within f64-partial rounding of it."""
+    from vmatting import _lib, ops
+    rs = np.random.RandomState(c + 2 * pool + with_add)
+    n, h, w = 2, 17, 23
+    y = np.maximum(rs.normal(size=(n, h, w, c)), 0).astype(np.float32)
+    y[:, ::3, ::2] = np.round(y[:, ::3, ::2])  # exact ties inside windows
+    yd = T(y, torch.bfloat16)
+    ph, pw = (h + 1) // 2, (w + 1) // 2
+    dy = T(rs.normal(size=(n, ph, pw, c) if pool else (n, h, w, c)).astype(np.float32))
+    add = T(rs.normal(size=(n, h, w, c)).astype(np.float32)) if with_add else None
+    out = []
+    try:
+        for vec in (0, 1):
+            _lib.set_option("relu_bias_vec", vec)
+            dz = torch.zeros((n, h, w, c), dtype=torch.bfloat16, device=DEV)
+            db = torch.zeros(c, device=DEV)
+            ops.relu_backward_bias(dy, yd, dz, db, add=add)
+            out.append((dz, db))
+    finally:
+        _lib.set_option("relu_bias_vec", 1)
+    assert torch.equal(out[0][0], out[1][0])
+    a, b = H(out[0][1]), H(out[1][1])
+    assert np.abs(a - b).max() <= 1e-6 * max(1.0, float(np.abs(a).max()))
+
+
+@pytest.mark.parametrize("pool", [False, True])
 @pytest.mark.parametrize("c,ydt,dzdt", [(64, "bf16", "bf16"), (512, "bf16", "bf16"), (24, "f32", "f32")])
 def test_relu_backward_bias(pool, c, ydt, dzdt):
     """vm_relu_backward_bias_nhwc (the UNetImage backward's per-conv front end): dz = (y > 0) * (dy (+ add)) or, with a

@@ -419,6 +419,119 @@ __global__ __launch_bounds__(256) void relu_bwd_bias_kernel(V dy, V y, V add, V 
   }
 }
 
+// Vectorised form for the bf16 path (bf16 y and dz, f32 dy / add; C % 8 == 0, C <= 512): a lane takes 8 channels of
+// a pixel — one 16-byte y chunk, two f32x4 of dy and of add, one 16-byte dz store — where the per-element form above
+// issued a 2- to 4-byte access per channel (~2.5 TB/s).  Per element the same arithmetic (g = dy, g += add in f32;
+// the first-maximum pool adjoint; z rounded to bf16 as st() does), so dz is bit-identical; the channel sums are f64
+// partials per block in another partition of the pixels, folded in fixed order by fold_sum_kernel as before.
+template <bool POOL, bool ADD, int TPG>  // TPG: lanes per pixel (a power of two >= C / 8)
+__global__ __launch_bounds__(256) void relu_bwd_bias8_kernel(const float* __restrict__ dy, int dycs,
+                                                             const uint16_t* __restrict__ y, int ycs,
+                                                             const float* __restrict__ add, int acs,
+                                                             uint16_t* __restrict__ dz, int zcs, int N, int H, int W,
+                                                             int DH, int DW, int C, double* part, int nblk) {
+  constexpr int PPB = 256 / TPG;
+  __shared__ double sh[8][256];
+  const int t = threadIdx.x, j = t % TPG, pl = t / TPG;
+  const int c0 = 8 * j;
+  double s[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+  auto ld8f = [&](const float* p, float (&v)[8]) __attribute__((always_inline)) {
+    const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  };
+  auto ld8y = [&](const uint16_t* p, float (&v)[8]) __attribute__((always_inline)) {
+    const uint4 q = *reinterpret_cast<const uint4*>(p);
+    const uint32_t w4[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      v[2 * k] = bf2f((uint16_t)(w4[k] & 0xffffu));
+      v[2 * k + 1] = bf2f((uint16_t)(w4[k] >> 16));
+    }
+  };
+  auto st8 = [&](uint16_t* p, const float (&z)[8]) __attribute__((always_inline)) {
+    uint32_t w4[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) w4[k] = (uint32_t)f2bf(z[2 * k]) | ((uint32_t)f2bf(z[2 * k + 1]) << 16);
+    *reinterpret_cast<uint4*>(p) = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+  };
+  if (c0 < C) {
+    const long units = POOL ? (long)N * DH * DW : (long)N * H * W;
+    for (long u = (long)blockIdx.x * PPB + pl; u < units; u += (long)gridDim.x * PPB) {
+      if constexpr (!POOL) {
+        float g[8], yv[8], z[8];
+        ld8f(dy + u * dycs + c0, g);
+        if constexpr (ADD) {
+          float a8[8];
+          ld8f(add + u * acs + c0, a8);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) g[k] += a8[k];
+        }
+        ld8y(y + u * ycs + c0, yv);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          z[k] = yv[k] > 0.f ? g[k] : 0.f;
+          s[k] += (double)z[k];
+        }
+        st8(dz + u * zcs + c0, z);
+      } else {
+        const long hw = (long)DH * DW;
+        const int n = (int)(u / hw);
+        const int r = (int)(u - (long)n * hw);
+        const int oy = r / DW, ox = r - oy * DW;
+        float gp[8], yv[4][8];
+        ld8f(dy + u * dycs + c0, gp);
+        long pix[4];
+        bool in[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int yy = 2 * oy + (q >> 1), xx = 2 * ox + (q & 1);
+          in[q] = yy < H && xx < W;
+          pix[q] = ((long)n * H + yy) * W + xx;
+          if (in[q]) ld8y(y + pix[q] * ycs + c0, yv[q]);
+          else
+#pragma unroll
+            for (int k = 0; k < 8; ++k) yv[q][k] = 0.f;
+        }
+        int win[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {  // TF MaxPoolGrad: the window's first maximum
+          float best = 0.f;
+          win[k] = -1;
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            if (in[q] && (win[k] < 0 || yv[q][k] > best)) {
+              best = yv[q][k];
+              win[k] = q;
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          if (!in[q]) continue;
+          float a8[8], z[8];
+          if constexpr (ADD) ld8f(add + pix[q] * acs + c0, a8);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            float g = k < 8 && win[k] == q ? gp[k] : 0.f;
+            if constexpr (ADD) g += a8[k];
+            z[k] = yv[q][k] > 0.f ? g : 0.f;
+            s[k] += (double)z[k];
+          }
+          st8(dz + pix[q] * zcs + c0, z);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) sh[k][t] = s[k];
+  __syncthreads();
+  for (int c = t; c < C; c += 256) {
+    const int jj = c >> 3, k = c & 7;
+    double r = 0.0;
+    for (int q = 0; q < PPB; ++q) r += sh[k][q * TPG + jj];
+    part[(long)c * nblk + blockIdx.x] = r;  // channel-major [C][nblk], as relu_bwd_bias_kernel
+  }
+}
+
 __global__ __launch_bounds__(256) void fold_sum_kernel(const double* part, int nblk, int C, float* out) {
   double r[3];
   fold_columns(part, nblk, C, blockIdx.x, 1, r);
@@ -1943,6 +2056,7 @@ static int launch_wgrad_grid(const void* kern, int lds, int th, int cib, int& at
   return VM_OK;
 }
 
+static long g_relu_bias_vec = 1;  // vm_set_option "relu_bias_vec": 0 = the per-element relu / bias backward (A/B)
 static long g_wgrad_mfma_pipe = 1;  // vm_set_option "wgrad_mfma_pipe": 0 = wgrad_mfma_kernel's plain loop (A/B)
 template <int NCI, int NCO, bool SX, int TH, bool PIPE>
 static int launch_wgrad_mfma_p(WgArgs& a, float* dw, hipStream_t st) {
@@ -2045,6 +2159,10 @@ int train_set_option(const char* key, long value) {
   }
   if (!strcmp(key, "wgrad_dma")) {
     trn::g_wgrad_dma = value;
+    return 1;
+  }
+  if (!strcmp(key, "relu_bias_vec")) {
+    trn::g_relu_bias_vec = value;
     return 1;
   }
   if (!strcmp(key, "wgrad_mfma_pipe")) {
@@ -2375,6 +2493,39 @@ extern "C" int vm_relu_backward_bias_nhwc(const vm_tensor* dy, const vm_tensor* 
   const int C = y->c;
   const long units = pool ? (long)dy->n * dy->h * dy->w : (long)y->n * y->h * y->w;
   const int nb = bn_blocks(pool ? 4 * units : units, C);
+  auto al16 = [](const vm_tensor* t, int es) {  // every 8-channel run of the view 16-byte aligned
+    return t->cstride % 8 == 0 && t->coff % 8 == 0 && reinterpret_cast<uintptr_t>(t->ptr) % 16 == 0 && es > 0;
+  };
+  if (g_relu_bias_vec && y->dtype == VM_BF16 && dz->dtype == VM_BF16 && C % 8 == 0 && C <= 512 && al16(y, 2) &&
+      al16(dz, 2) && al16(dy, 4) && (!add || al16(add, 4))) {
+    const int tpg = C / 8 > 32 ? 64 : C / 8 > 16 ? 32 : C / 8 > 8 ? 16 : C / 8 > 4 ? 8 : C / 8 > 2 ? 4 : C / 8 > 1 ? 2 : 1;
+    const float* dyp = reinterpret_cast<const float*>(dy->ptr) + dy->coff;
+    const uint16_t* yp = reinterpret_cast<const uint16_t*>(y->ptr) + y->coff;
+    const float* ap = add ? reinterpret_cast<const float*>(add->ptr) + add->coff : nullptr;
+    uint16_t* zp = reinterpret_cast<uint16_t*>(dz->ptr) + dz->coff;
+    double* part = reinterpret_cast<double*>(work);
+#define VM_RB8(TPG)                                                                                                    \
+  case TPG:                                                                                                            \
+    if (pool && add)                                                                                                   \
+      hipLaunchKernelGGL((relu_bwd_bias8_kernel<true, true, TPG>), dim3(nb), dim3(256), 0, st, dyp, dy->cstride, yp,   \
+                         y->cstride, ap, add->cstride, zp, dz->cstride, y->n, y->h, y->w, dy->h, dy->w, C, part, nb);  \
+    else if (pool)                                                                                                     \
+      hipLaunchKernelGGL((relu_bwd_bias8_kernel<true, false, TPG>), dim3(nb), dim3(256), 0, st, dyp, dy->cstride, yp,  \
+                         y->cstride, ap, 0, zp, dz->cstride, y->n, y->h, y->w, dy->h, dy->w, C, part, nb);             \
+    else if (add)                                                                                                      \
+      hipLaunchKernelGGL((relu_bwd_bias8_kernel<false, true, TPG>), dim3(nb), dim3(256), 0, st, dyp, dy->cstride, yp,  \
+                         y->cstride, ap, add->cstride, zp, dz->cstride, y->n, y->h, y->w, dy->h, dy->w, C, part, nb);  \
+    else                                                                                                               \
+      hipLaunchKernelGGL((relu_bwd_bias8_kernel<false, false, TPG>), dim3(nb), dim3(256), 0, st, dyp, dy->cstride, yp, \
+                         y->cstride, ap, 0, zp, dz->cstride, y->n, y->h, y->w, dy->h, dy->w, C, part, nb);             \
+    break;
+    switch (tpg) { VM_RB8(1) VM_RB8(2) VM_RB8(4) VM_RB8(8) VM_RB8(16) VM_RB8(32) VM_RB8(64) }
+#undef VM_RB8
+    int rc = check_launch("relu_backward_bias");
+    if (rc) return rc;
+    hipLaunchKernelGGL(fold_sum_kernel, dim3(C), dim3(256), 0, st, part, nb, C, dbias);
+    return check_launch("relu_backward_bias fold");
+  }
   const int cp = C > 32 ? 64 : C > 16 ? 32 : C > 8 ? 16 : C > 4 ? 8 : C > 2 ? 4 : C > 1 ? 2 : 1;
   const dim3 grid(cp == 64 ? (C + 63) / 64 : 1, nb);
   V a = mk(dy), b = mk(y), c = add ? mk(add) : V{}, d = mk(dz);
