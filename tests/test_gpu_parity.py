@@ -1038,7 +1038,9 @@ def test_unet_video_1080p_bf16_properties(vgg0):
 
 @pytest.mark.parametrize("xc,yc,ys,odt", [(3, 8, 8, torch.bfloat16), (8, 8, 16, torch.bfloat16), (3, 3, 32, torch.bfloat16),
                                           (7, 16, 16, torch.float32),
-                                          (20, 24, 24, torch.bfloat16), (5, 5, 8, torch.float32)])
+                                          (20, 24, 24, torch.bfloat16), (5, 5, 8, torch.float32),
+                                          # whole 8-channel runs f32 -> bf16 (the vectorised form when not affine)
+                                          (16, 16, 24, torch.bfloat16), (64, 64, 128, torch.bfloat16)])
 @pytest.mark.parametrize("affine", [False, True])
 def test_convert_views(xc, yc, ys, odt, affine):
     """vm_convert_nhwc (one 16-byte store per pixel for an aligned 8-channel bf16 output, pixel-per-thread form for
