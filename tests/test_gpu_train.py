@@ -186,7 +186,9 @@ def test_pack_weights_batch_matches_single_packs():
     from vmatting import ops
     rs = np.random.RandomState(11)
     cases = []
-    for cin, cout, dt in [(64, 64, "bf16"), (30, 2, "bf16"), (9, 16, "fp32"), (96, 30, "bf16"), (30, 24, "fp32")]:
+    # (chunk-major bf16 forward packs take the tiled transpose, the rest the element-wise kernel)
+    for cin, cout, dt in [(64, 64, "bf16"), (30, 2, "bf16"), (9, 16, "fp32"), (96, 30, "bf16"), (30, 24, "fp32"),
+                          (512, 512, "bf16"), (1024, 64, "bf16"), (6, 64, "bf16"), (256, 100, "bf16")]:
         cases.append((T(rs.normal(size=(3, 3, cin, cout)).astype(np.float32)), cin, cout, dt))
     convs, refs = [], []
     for w, cin, cout, dt in cases:

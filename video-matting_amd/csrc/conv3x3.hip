@@ -3715,6 +3715,39 @@ __global__ void pack_weights_batch(PackBatch b) {
   }
 }
 
+// the forward packs of chunk-major bf16 filters (every conv of the UNetImage / UNetVideo training re-pack): a block
+// transposes one (granule, 64-output-channel) tile through LDS, so the source filter is read along cout (256-byte
+// runs; pack_weights_batch's one element per thread read it with a w_cout stride) and each packed row receives 64
+// contiguous bytes; zero padding (cin / cout past the filter, the K_pad tail granule) as pack_weights_batch, and the
+// same RNE rounding: bit-identical
+__global__ __launch_bounds__(256) void pack_weights_tiled(PackBatch b) {
+  const int jb = blockIdx.y;
+  const vm_pack_job& j = b.j[jb];
+  const int K_pad = b.K_pad[jb], ngr = K_pad / 32, ng = 9 * b.cin_pad[jb] / 32, ncot = b.cout_pad[jb] / 64;
+  const int t = blockIdx.x;
+  if (t >= ngr * ncot) return;
+  const int gr = t % ngr, co0 = (t / ngr) * 64;
+  __shared__ float tile[32][65];
+  const int tid = threadIdx.x;
+  if (gr < ng) {
+    const int cc = gr / 9, tap = gr - cc * 9;
+    for (int e = tid; e < 32 * 64; e += 256) {
+      const int ci = e >> 6, coj = e & 63;
+      const int c = cc * 32 + ci, co = co0 + coj;
+      float v = 0.f;
+      if (co < j.cout && c < j.cin && co < j.w_cout && c < j.w_cin) v = j.w[((long)tap * j.w_cin + c) * j.w_cout + co];
+      tile[ci][coj] = v;
+    }
+  }
+  __syncthreads();
+  const int coj = tid >> 2, ch = tid & 3;
+  float f[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) f[k] = gr < ng ? tile[ch * 8 + k][coj] : 0.f;
+  *reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(j.packed) + (long)(co0 + coj) * K_pad + gr * 32 + ch * 8) =
+      Chunk<uint16_t>::pack(f);
+}
+
 struct PackGeom {
   int cin_pad, ge, K9, K_pad, cout_pad, chunk_major, ng;
 };
@@ -4462,6 +4495,7 @@ static int launch_patch(ConvArgs& a, hipStream_t st) {
   return check_launch("conv3x3_patch");
 }
 
+static long g_pack_tiled = 1;  // vm_set_option "pack_tiled": 0 = every job on the element-wise pack_weights_batch (A/B)
 static long g_up_skip = 1;  // vm_set_option "up_skip": 0 runs the folded upconvs without the zero-tap skipping (A/B)
 
 // persistent row-slot patch kernel (conv3x3_patch_persist): a resident grid of 8 XCD bands x J walkers, on grids of
@@ -5137,6 +5171,10 @@ extern "C" int vm_set_option(const char* key, long value) {
     g_rows_kernel = value;
     return VM_OK;
   }
+  if (!strcmp(key, "pack_tiled")) {
+    g_pack_tiled = value;
+    return VM_OK;
+  }
   if (!strcmp(key, "persist_half")) {
     g_persist_half = value;
     return VM_OK;
@@ -5349,25 +5387,44 @@ extern "C" int vm_conv3x3_pack_weights(const float* w_hwio, int cin, int cout, i
 extern "C" int vm_conv3x3_pack_weights_batch(int njobs, const vm_pack_job* jobs, void* stream) {
   if (njobs < 0 || (njobs > 0 && !jobs)) return fail(VM_EINVAL, "pack_weights_batch: bad argument");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  for (int base = 0; base < njobs; base += PACK_MAX_JOBS) {
+  for (int i = 0; i < njobs; ++i) {
+    const vm_pack_job& j = jobs[i];
+    if (!j.w || !j.packed || j.cin <= 0 || j.cout <= 0 || j.w_cin <= 0 || j.w_cout <= 0 ||
+        (j.dtype != VM_F32 && j.dtype != VM_BF16))
+      return fail(VM_EINVAL, "pack_weights_batch: bad job %d", i);
+  }
+  // chunk-major bf16 forward packs go to the tiled transpose (pack_weights_tiled), the rest element-wise
+  for (int tiled = 0; tiled < 2; ++tiled) {
     PackBatch b{};
-    b.n = njobs - base < PACK_MAX_JOBS ? njobs - base : PACK_MAX_JOBS;
     long mx = 1;
-    for (int i = 0; i < b.n; ++i) {
-      const vm_pack_job& j = jobs[base + i];
-      if (!j.w || !j.packed || j.cin <= 0 || j.cout <= 0 || j.w_cin <= 0 || j.w_cout <= 0 ||
-          (j.dtype != VM_F32 && j.dtype != VM_BF16))
-        return fail(VM_EINVAL, "pack_weights_batch: bad job %d", base + i);
-      b.j[i] = j;
+    auto flush = [&]() -> int {
+      if (!b.n) return VM_OK;
+      if (tiled)
+        hipLaunchKernelGGL(pack_weights_tiled, dim3((unsigned)mx, b.n), dim3(256), 0, st, b);
+      else
+        hipLaunchKernelGGL(pack_weights_batch, dim3(grid_for(mx, 256, 256), b.n), dim3(256), 0, st, b);
+      const int rc = check_launch("pack_weights_batch");
+      b.n = 0;
+      mx = 1;
+      return rc;
+    };
+    for (int i = 0; i < njobs; ++i) {
+      const vm_pack_job& j = jobs[i];
       const PackGeom g = geom(j.cin, j.cout, j.dtype);
-      b.K_pad[i] = g.K_pad;
-      b.cout_pad[i] = g.cout_pad;
-      b.cin_pad[i] = g.cin_pad;
-      const long t = (long)g.cout_pad * g.K_pad;
+      const bool tj = g_pack_tiled && j.dtype == VM_BF16 && !j.flip && g.chunk_major;
+      if (tj != (tiled != 0)) continue;
+      b.j[b.n] = j;
+      b.K_pad[b.n] = g.K_pad;
+      b.cout_pad[b.n] = g.cout_pad;
+      b.cin_pad[b.n] = g.cin_pad;
+      const long t = tiled ? (long)(g.K_pad / 32) * (g.cout_pad / 64) : (long)g.cout_pad * g.K_pad;
       if (t > mx) mx = t;
+      if (++b.n == PACK_MAX_JOBS) {
+        const int rc = flush();
+        if (rc) return rc;
+      }
     }
-    hipLaunchKernelGGL(pack_weights_batch, dim3(grid_for(mx, 256, 256), b.n), dim3(256), 0, st, b);
-    int rc = check_launch("pack_weights_batch");
+    const int rc = flush();
     if (rc) return rc;
   }
   return VM_OK;
