@@ -246,6 +246,43 @@ def test_bn_backward(mask):
     assert scaled_err(H(s), dy.astype(np.float64).sum(axis=(0, 1, 2))) <= 1e-5
 
 
+@pytest.mark.parametrize("c", [8, 32, 48, 64])
+@pytest.mark.parametrize("mask", [False, True])
+@pytest.mark.parametrize("with_dx2", [False, True])
+def test_bn_backward_vectorised_matches(c, mask, with_dx2):
+    """The 8-channels-per-lane BN backward (bn_vec 1: f32 x / dy / dx, bf16 relu mask and bf16 copy) against the
+    per-channel forms: the same per-element expressions and f64 channel sums over another partition of the pixels,
+    so dx within a couple of f32 roundings, the bf16 copy equal to dx's rounding, the sums within f64 rounding."""
+    from vmatting import _lib, ops
+    rs = np.random.RandomState(c + 2 * mask + with_dx2)
+    n, h, w = 2, 19, 33
+    x = T((rs.normal(size=(n, h, w, c)) * 3 + 1).astype(np.float32))
+    dy = T(rs.normal(size=(n, h, w, c)).astype(np.float32))
+    gamma = T(rs.uniform(0.5, 1.5, c).astype(np.float32))
+    mean, var = ops.bn_stats(x)
+    y = T(np.maximum(rs.normal(size=(n, h, w, c)), 0).astype(np.float32), torch.bfloat16) if mask else None
+    out = []
+    try:
+        for vec in (0, 1):
+            _lib.set_option("bn_vec", vec)
+            dx = torch.empty_like(x)
+            dx2 = torch.zeros((n, h, w, c), dtype=torch.bfloat16, device=DEV) if with_dx2 else None
+            dg = torch.empty(c, device=DEV)
+            db = torch.empty(c, device=DEV)
+            dbias = torch.empty(c, device=DEV)
+            ops.bn_backward(x, dy, y, mean, var, gamma, 1e-3, dx=dx, dgamma=dg, dbeta=db, dx2=dx2, dbias=dbias)
+            out.append((dx, dx2, dg, db, dbias))
+    finally:
+        _lib.set_option("bn_vec", 1)
+    a, b = H(out[0][0]), H(out[1][0])
+    assert np.abs(a - b).max() <= 4e-7 * max(1.0, float(np.abs(a).max())), np.abs(a - b).max()
+    if with_dx2:  # each copy is its own dx rounded to bf16
+        assert torch.equal(out[1][1], out[1][0].to(torch.bfloat16))
+    for k in (2, 3, 4):
+        a, b = H(out[0][k]), H(out[1][k])
+        assert np.abs(a - b).max() <= 1e-6 * max(1.0, float(np.abs(a).max())), (k, np.abs(a - b).max())
+
+
 @pytest.mark.parametrize("ih,iw,oh,ow", [(5, 7, 10, 14), (3, 4, 5, 7), (17, 30, 34, 60), (8, 8, 8, 8),
                                          # near the launcher's limits (oh <= 4*ih) and the 1080p level sizes
                                          (3, 5, 12, 20), (7, 9, 25, 31), (68, 120, 135, 240),

@@ -190,6 +190,121 @@ static void launch_bn_bwd_partial(const V& x, const V& dy, const V& y, const flo
   }
 }
 
+// Vectorised BN backward for whole 8-channel runs (f32 x / dy / dx, an optional bf16 relu mask y and bf16 copy dx2;
+// every view 16-byte aligned, C % 8 == 0, C <= 512): a lane takes 8 channels of a pixel — two f32x4 of x and of dy,
+// one 16-byte y chunk — where the per-channel forms above issue a 4-byte access per element (~3.5 TB/s on the 32-
+// channel full-resolution layers of the config-5 step).  Per element the same expressions, summed in f64 per block
+// into the same [3][C][nblk] tables (another partition of the pixels; bn_bwd_final folds them as before).
+__device__ __forceinline__ void ld8f32(const float* p, float (&v)[8]) {
+  const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+__device__ __forceinline__ void ld8bf(const uint16_t* p, float (&v)[8]) {
+  const uint4 q = *reinterpret_cast<const uint4*>(p);
+  const uint32_t w4[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    v[2 * k] = bf2f((uint16_t)(w4[k] & 0xffffu));
+    v[2 * k + 1] = bf2f((uint16_t)(w4[k] >> 16));
+  }
+}
+struct Bn8 {
+  const float* x;
+  const float* dy;
+  const uint16_t* y;  // bf16 relu output (mask) or nullptr
+  float* dx;
+  uint16_t* dx2;      // bf16 copy or nullptr
+  int xcs, dycs, ycs, dxcs, dx2cs, C;
+  long M;
+};
+
+template <bool MASK, int TPG>
+__global__ __launch_bounds__(256) void bn_bwd_partial8(Bn8 a, const float* mean, const float* var, float eps,
+                                                       double* part, int nblk) {
+  constexpr int PPB = 256 / TPG;
+  __shared__ double sh[8][256];
+  const int t = threadIdx.x, j = t % TPG, pl = t / TPG, c0 = 8 * j;
+  double s1[8], s2[8], s3[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) s1[k] = s2[k] = s3[k] = 0.0;
+  if (c0 < a.C) {
+    float m[8], r[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      m[k] = mean[c0 + k];
+      r[k] = 1.0f / sqrtf(var[c0 + k] + eps);
+    }
+    for (long p = (long)blockIdx.x * PPB + pl; p < a.M; p += (long)nblk * PPB) {
+      float g[8], xv[8];
+      ld8f32(a.dy + p * a.dycs + c0, g);
+      ld8f32(a.x + p * a.xcs + c0, xv);
+      if constexpr (MASK) {
+        float yv[8];
+        ld8bf(a.y + p * a.ycs + c0, yv);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) g[k] = yv[k] > 0.f ? g[k] : 0.f;
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        s1[k] += g[k];
+        const float xh = (xv[k] - m[k]) * r[k];
+        s2[k] += (double)g[k] * (double)xh;
+        s3[k] += (double)xh;
+      }
+    }
+  }
+  // three tables through one 16 KB staging buffer
+#pragma unroll
+  for (int tab = 0; tab < 3; ++tab) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) sh[k][t] = tab == 0 ? s1[k] : tab == 1 ? s2[k] : s3[k];
+    __syncthreads();
+    for (int c = t; c < a.C; c += 256) {
+      const int jj = c >> 3, k = c & 7;
+      double v = 0.0;
+      for (int q = 0; q < PPB; ++q) v += sh[k][q * TPG + jj];
+      part[(long)tab * nblk * a.C + (long)c * nblk + blockIdx.x] = v;
+    }
+    __syncthreads();
+  }
+}
+
+template <bool MASK, bool DX2, int TPG>
+__global__ __launch_bounds__(256) void bn_bwd_apply8(Bn8 a, const float* mean, const float* var, const float* gamma,
+                                                     float eps, const float* sum_g, const float* sum_gx) {
+  constexpr int PPB = 256 / TPG;
+  const int t = threadIdx.x, j = t % TPG, pl = t / TPG, c0 = 8 * j;
+  if (c0 >= a.C) return;
+  const float invM = 1.0f / (float)a.M;
+  float m[8], r[8], kk[8], sg[8], sgx[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int c = c0 + k;
+    r[k] = 1.0f / sqrtf(var[c] + eps);
+    m[k] = mean[c];
+    kk[k] = (gamma ? gamma[c] : 1.f) * r[k];
+    sg[k] = sum_g[c] * invM;
+    sgx[k] = sum_gx[c] * invM;
+  }
+  for (long p = (long)blockIdx.x * PPB + pl; p < a.M; p += (long)gridDim.x * PPB) {
+    float g[8], xv[8], v[8];
+    ld8f32(a.dy + p * a.dycs + c0, g);
+    ld8f32(a.x + p * a.xcs + c0, xv);
+    if constexpr (MASK) {
+      float yv[8];
+      ld8bf(a.y + p * a.ycs + c0, yv);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) g[k] = yv[k] > 0.f ? g[k] : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = kk[k] * (g[k] - sg[k] - (xv[k] - m[k]) * r[k] * sgx[k]);
+    float* o = a.dx + p * a.dxcs + c0;
+    *reinterpret_cast<float4*>(o) = make_float4(v[0], v[1], v[2], v[3]);
+    *reinterpret_cast<float4*>(o + 4) = make_float4(v[4], v[5], v[6], v[7]);
+    if constexpr (DX2) *reinterpret_cast<uint4*>(a.dx2 + p * a.dx2cs + c0) = Chunk<uint16_t>::pack(v);
+  }
+}
+
 // elementwise passes over [M pixels x C channels]: CP (power of two >= C, at most 64) lanes per pixel, channel
 // block blockIdx.y, so a lane keeps one channel (its per-channel constants in registers) and no element index is
 // ever divided
@@ -2056,6 +2171,7 @@ static int launch_wgrad_grid(const void* kern, int lds, int th, int cib, int& at
   return VM_OK;
 }
 
+static long g_bn_vec = 1;  // vm_set_option "bn_vec": 0 = the per-channel BN backward forms (A/B)
 static long g_relu_bias_vec = 1;  // vm_set_option "relu_bias_vec": 0 = the per-element relu / bias backward (A/B)
 static long g_wgrad_mfma_pipe = 1;  // vm_set_option "wgrad_mfma_pipe": 0 = wgrad_mfma_kernel's plain loop (A/B)
 template <int NCI, int NCO, bool SX, int TH, bool PIPE>
@@ -2159,6 +2275,10 @@ int train_set_option(const char* key, long value) {
   }
   if (!strcmp(key, "wgrad_dma")) {
     trn::g_wgrad_dma = value;
+    return 1;
+  }
+  if (!strcmp(key, "bn_vec")) {
+    trn::g_bn_vec = value;
     return 1;
   }
   if (!strcmp(key, "relu_bias_vec")) {
@@ -2376,14 +2496,60 @@ extern "C" int vm_bn_backward_ex_nhwc(const vm_tensor* x, const vm_tensor* dy, c
   float* sgx = dgamma ? dgamma : tail + C;
   const long M = (long)dy->n * dy->h * dy->w;
   const int nb = bn_blocks(M, C);
-  if (y) launch_bn_bwd_partial<true>(xv, dyv, yv, mean, var, eps, part, nb, st);
-  else launch_bn_bwd_partial<false>(xv, dyv, yv, mean, var, eps, part, nb, st);
+  auto v16 = [](const vm_tensor* t) {
+    return t->cstride % 8 == 0 && t->coff % 8 == 0 && reinterpret_cast<uintptr_t>(t->ptr) % 16 == 0;
+  };
+  const bool vec = g_bn_vec && x && x->dtype == VM_F32 && C % 8 == 0 && C <= 512 && v16(x) && v16(dy) &&
+                   (!y || (y->dtype == VM_BF16 && v16(y))) && (!dx || v16(dx)) &&
+                   (!dx2 || (dx2->dtype == VM_BF16 && v16(dx2)));
+  Bn8 b8{};
+  int tpg = 1;
+  if (vec) {
+    b8.x = reinterpret_cast<const float*>(x->ptr) + x->coff;
+    b8.dy = reinterpret_cast<const float*>(dy->ptr) + dy->coff;
+    b8.y = y ? reinterpret_cast<const uint16_t*>(y->ptr) + y->coff : nullptr;
+    b8.dx = dx ? reinterpret_cast<float*>(dx->ptr) + dx->coff : nullptr;
+    b8.dx2 = dx2 ? reinterpret_cast<uint16_t*>(dx2->ptr) + dx2->coff : nullptr;
+    b8.xcs = x->cstride; b8.dycs = dy->cstride; b8.ycs = y ? y->cstride : 0;
+    b8.dxcs = dx ? dx->cstride : 0; b8.dx2cs = dx2 ? dx2->cstride : 0;
+    b8.C = C; b8.M = M;
+    tpg = C / 8 > 32 ? 64 : C / 8 > 16 ? 32 : C / 8 > 8 ? 16 : C / 8 > 4 ? 8 : C / 8 > 2 ? 4 : C / 8 > 1 ? 2 : 1;
+#define VM_BP8(TPG)                                                                                                   \
+  case TPG:                                                                                                           \
+    if (y) hipLaunchKernelGGL((bn_bwd_partial8<true, TPG>), dim3(nb), dim3(256), 0, st, b8, mean, var, eps, part, nb); \
+    else hipLaunchKernelGGL((bn_bwd_partial8<false, TPG>), dim3(nb), dim3(256), 0, st, b8, mean, var, eps, part, nb); \
+    break;
+    switch (tpg) { VM_BP8(1) VM_BP8(2) VM_BP8(4) VM_BP8(8) VM_BP8(16) VM_BP8(32) VM_BP8(64) }
+#undef VM_BP8
+  } else if (y) {
+    launch_bn_bwd_partial<true>(xv, dyv, yv, mean, var, eps, part, nb, st);
+  } else {
+    launch_bn_bwd_partial<false>(xv, dyv, yv, mean, var, eps, part, nb, st);
+  }
   int rc = check_launch("bn_backward_partial");
   if (rc) return rc;
   hipLaunchKernelGGL(bn_bwd_final, dim3(C), dim3(256), 0, st, part, nb, C, sg, x ? sgx : nullptr, dbias, gamma, var,
                      eps, M);
   rc = check_launch("bn_backward_final");
   if (rc || !dx) return rc;
+  if (vec) {
+    const long px = (M + 256 / tpg - 1) / (256 / tpg);
+    const dim3 g8((unsigned)(px < 4096 ? px : 4096));
+#define VM_BA8(TPG)                                                                                                  \
+  case TPG:                                                                                                          \
+    if (y && dx2) hipLaunchKernelGGL((bn_bwd_apply8<true, true, TPG>), g8, dim3(256), 0, st, b8, mean, var, gamma,   \
+                                     eps, sg, sgx);                                                                  \
+    else if (y) hipLaunchKernelGGL((bn_bwd_apply8<true, false, TPG>), g8, dim3(256), 0, st, b8, mean, var, gamma,    \
+                                   eps, sg, sgx);                                                                    \
+    else if (dx2) hipLaunchKernelGGL((bn_bwd_apply8<false, true, TPG>), g8, dim3(256), 0, st, b8, mean, var, gamma,  \
+                                     eps, sg, sgx);                                                                  \
+    else hipLaunchKernelGGL((bn_bwd_apply8<false, false, TPG>), g8, dim3(256), 0, st, b8, mean, var, gamma, eps, sg, \
+                            sgx);                                                                                    \
+    break;
+    switch (tpg) { VM_BA8(1) VM_BA8(2) VM_BA8(4) VM_BA8(8) VM_BA8(16) VM_BA8(32) VM_BA8(64) }
+#undef VM_BA8
+    return check_launch("bn_backward_apply");
+  }
   if (!y && !dx2 && f32_pair(x) && f32_pair(dy) && f32_pair(dx) && x->cstride > 0) {
     hipLaunchKernelGGL(bn_bwd_apply2_f32, dim3(grid_for(M, 256)), dim3(256), 0, st,
                        reinterpret_cast<const float*>(x->ptr) + x->coff, x->cstride,
