@@ -246,6 +246,42 @@ def test_bn_backward(mask):
     assert scaled_err(H(s), dy.astype(np.float64).sum(axis=(0, 1, 2))) <= 1e-5
 
 
+@pytest.mark.parametrize("c,xdt,ydt", [(8, "f32", "bf16"), (32, "f32", "bf16"), (48, "f32", "f32"),
+                                        (96, "bf16", "bf16"), (64, "bf16", "f32")])
+@pytest.mark.parametrize("act", ["none", "relu"])
+def test_bn_forward_vectorised_matches(c, xdt, ydt, act):
+    """The 8-channels-per-lane batch statistics and BN apply (bn_vec_fwd 1, an A/B option) against the per-channel
+    forms (the default): the same
+    f64 sums over another partition of the pixels (mean / var within f32 rounding) and the same per-element
+    expression (the output within one rounding of its dtype)."""
+    from vmatting import _lib, ops
+    rs = np.random.RandomState(c + len(act))
+    n, h, w = 2, 21, 35
+    tdt = {"f32": torch.float32, "bf16": torch.bfloat16}
+    x = T((rs.normal(size=(n, h, w, c)) * 3 + 1).astype(np.float32), tdt[xdt])
+    gamma = T(rs.uniform(0.5, 1.5, c).astype(np.float32))
+    beta = T(rs.normal(size=c).astype(np.float32))
+    out = []
+    try:
+        for vec in (0, 1):
+            _lib.set_option("bn_vec_fwd", vec)
+            mean, var = ops.bn_stats(x)
+            y = torch.empty((n, h, w, c), dtype=tdt[ydt], device=DEV)
+            ops.bn_apply(x, mean, var, gamma, beta, 1e-3, act, out=y)
+            out.append((mean, var, y))
+    finally:
+        _lib.set_option("bn_vec_fwd", 0)
+    for k in (0, 1):
+        a, b = H(out[0][k]), H(out[1][k])
+        assert np.abs(a - b).max() <= 2e-7 * max(1.0, float(np.abs(a).max())), (k, np.abs(a - b).max())
+    # the apply on the same statistics is the same expression
+    y1 = torch.empty_like(out[1][2])
+    ops.bn_apply(x, out[1][0], out[1][1], gamma, beta, 1e-3, act, out=y1)  # (the default: per-channel forms)
+    a, b = H(y1), H(out[1][2])
+    tol = 2.0 ** -7 if ydt == "bf16" else 1e-6
+    assert np.all(np.abs(a - b) <= tol * np.abs(a) + 1e-6)
+
+
 @pytest.mark.parametrize("c", [8, 32, 48, 64])
 @pytest.mark.parametrize("mask", [False, True])
 @pytest.mark.parametrize("with_dx2", [False, True])

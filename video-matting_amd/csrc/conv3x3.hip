@@ -5353,6 +5353,10 @@ extern "C" int vm_set_option(const char* key, long value) {
     g_glds_rb = value;
     return VM_OK;
   }
+  if (!strcmp(key, "bn_vec_fwd")) {
+    g_bn_vec_fwd = value;
+    return VM_OK;
+  }
   if (!strcmp(key, "bn_blocks")) {
     if (value < 1 || value > BN_TARGET_MAX) return fail(VM_EINVAL, "set_option: bn_blocks must be 1..%d", BN_TARGET_MAX);
     g_bn_target = value;

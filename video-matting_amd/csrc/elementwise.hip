@@ -426,6 +426,106 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(View x, View y, const flo
   }
 }
 
+// Whole 8-channel runs (C % 8 == 0, C <= 512, 16-byte aligned views): a lane takes 8 channels of a pixel, one or two
+// 16-byte accesses per side where the per-channel forms issue one 2- / 4-byte access per element.  bn_partial8: the
+// same f64 sums per channel over another partition of the pixels ([2][C][nblk] tables, bn_final_kernel folds them);
+// bn_apply8: the same expression per element (y may alias x).
+template <typename T>
+__device__ __forceinline__ void ld8v(const T* p, float (&v)[8]) {
+  if constexpr (sizeof(T) == 4) {
+    const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  } else {
+    Chunk<uint16_t>::unpack(*reinterpret_cast<const uint4*>(p), v);
+  }
+}
+template <typename T>
+__device__ __forceinline__ void st8v(T* p, const float (&v)[8]) {
+  if constexpr (sizeof(T) == 4) {
+    *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+    *reinterpret_cast<float4*>(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
+  } else {
+    *reinterpret_cast<uint4*>(p) = Chunk<uint16_t>::pack(v);
+  }
+}
+
+template <typename T, int TPG>
+__global__ __launch_bounds__(256) void bn_partial8_kernel(const T* x, int xcs, long M, int C, double* part, int nblk) {
+  constexpr int PPB = 256 / TPG;
+  __shared__ double sh[8][256];
+  const int t = threadIdx.x, j = t % TPG, pl = t / TPG, c0 = 8 * j;
+  double s[8], ss[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) s[k] = ss[k] = 0.0;
+  if (c0 < C) {
+    for (long p = (long)blockIdx.x * PPB + pl; p < M; p += (long)nblk * PPB) {
+      float v[8];
+      ld8v(x + p * xcs + c0, v);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const double d = v[k];
+        s[k] += d;
+        ss[k] += d * d;
+      }
+    }
+  }
+#pragma unroll
+  for (int tab = 0; tab < 2; ++tab) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) sh[k][t] = tab ? ss[k] : s[k];
+    __syncthreads();
+    for (int c = t; c < C; c += 256) {
+      const int jj = c >> 3, k = c & 7;
+      double r = 0.0;
+      for (int q = 0; q < PPB; ++q) r += sh[k][q * TPG + jj];
+      part[(long)tab * nblk * C + (long)c * nblk + blockIdx.x] = r;  // channel-major, as bn_partial_kernel
+    }
+    __syncthreads();
+  }
+}
+
+template <typename TX, typename TY, int TPG>
+__global__ __launch_bounds__(256) void bn_apply8_kernel(const TX* x, int xcs, TY* y, int ycs, long M, int C,
+                                                        const float* mean, const float* var, const float* gamma,
+                                                        const float* beta, float eps, int act) {
+  constexpr int PPB = 256 / TPG;
+  const int t = threadIdx.x, j = t % TPG, pl = t / TPG, c0 = 8 * j;
+  if (c0 >= C) return;
+  float m[8], r[8], g[8], b[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int c = c0 + k;
+    m[k] = mean ? mean[c] : 0.f;
+    const float v = var ? var[c] : 1.f;
+    g[k] = gamma ? gamma[c] : 1.f;
+    b[k] = beta ? beta[c] : 0.f;
+    r[k] = 1.0f / sqrtf(v + eps);
+  }
+  for (long p = (long)blockIdx.x * PPB + pl; p < M; p += (long)gridDim.x * PPB) {
+    float v[8];
+    ld8v(x + p * xcs + c0, v);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      float u = (v[k] - m[k]) * r[k] * g[k] + b[k];
+      v[k] = act == VM_ACT_RELU ? fmaxf(u, 0.f) : act == VM_ACT_SIGMOID ? sigmoid_precise(u) : u;
+    }
+    st8v(y + p * ycs + c0, v);
+  }
+}
+
+// vm_set_option "bn_vec_fwd" (A/B, off): the 8-channel forms measured no faster in the config-5 step (4.75-4.76 vs
+// 4.77-4.79 ms, same box: these passes run beside the select chains, where their 16 KB reduction buffer costs
+// occupancy), unlike the backward's (train.hip bn_bwd_partial8 / apply8: -2 %)
+long g_bn_vec_fwd = 0;
+
+static bool vec8_view(const vm_tensor* t) {
+  return t->cstride % 8 == 0 && t->coff % 8 == 0 && reinterpret_cast<uintptr_t>(t->ptr) % 16 == 0 && t->c % 8 == 0 &&
+         t->c <= 512;
+}
+static int tpg8(int C) {
+  return C / 8 > 32 ? 64 : C / 8 > 16 ? 32 : C / 8 > 8 ? 16 : C / 8 > 4 ? 8 : C / 8 > 2 ? 4 : C / 8 > 1 ? 2 : 1;
+}
+
 // two f32 channels per pixel, one pixel per thread, one 8-byte load and store each (the 2-channel select convs of the
 // training step: at a 32-byte pixel stride the 2-lanes-per-pixel form above spent a dtype branch and a 64-bit index
 // product per 4-byte element, ~0.8 TB/s).  Per element the same expression, so the same values.
@@ -686,8 +786,25 @@ extern "C" int vm_bn_stats_nhwc(const vm_tensor* x, float* mean, float* var, voi
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const long M = (long)x->n * x->h * x->w;
   double* part = reinterpret_cast<double*>(work);
-  const int nb = x->dtype == VM_BF16 ? launch_bn_partial<uint16_t>(view(x), part, st)
-                                     : launch_bn_partial<float>(view(x), part, st);
+  int nb;
+  if (g_bn_vec_fwd && vec8_view(x)) {
+    nb = bn_blocks(M, x->c);
+    const int C = x->c, tp = tpg8(C);
+#define VM_BP8(TPG)                                                                                                 \
+  case TPG:                                                                                                         \
+    if (x->dtype == VM_BF16)                                                                                        \
+      hipLaunchKernelGGL((bn_partial8_kernel<uint16_t, TPG>), dim3(nb), dim3(256), 0, st,                           \
+                         reinterpret_cast<const uint16_t*>(x->ptr) + x->coff, x->cstride, M, C, part, nb);          \
+    else                                                                                                            \
+      hipLaunchKernelGGL((bn_partial8_kernel<float, TPG>), dim3(nb), dim3(256), 0, st,                              \
+                         reinterpret_cast<const float*>(x->ptr) + x->coff, x->cstride, M, C, part, nb);             \
+    break;
+    switch (tp) { VM_BP8(1) VM_BP8(2) VM_BP8(4) VM_BP8(8) VM_BP8(16) VM_BP8(32) VM_BP8(64) }
+#undef VM_BP8
+  } else {
+    nb = x->dtype == VM_BF16 ? launch_bn_partial<uint16_t>(view(x), part, st)
+                             : launch_bn_partial<float>(view(x), part, st);
+  }
   int rc = check_launch("bn_partial");
   if (rc) return rc;
   hipLaunchKernelGGL(bn_final_kernel, dim3(x->c), dim3(256), 0, st, part, nb, x->c, M, mean, var);
@@ -704,6 +821,36 @@ extern "C" int vm_bn_apply_nhwc(const vm_tensor* x, vm_tensor* y, const float* m
   const int cp = C > 32 ? 64 : C > 16 ? 32 : C > 8 ? 16 : C > 4 ? 8 : C > 2 ? 4 : C > 1 ? 2 : 1;
   const long px = (M + 256 / cp - 1) / (256 / cp);
   const dim3 grid((unsigned)(px < 4096 ? px : 4096), (unsigned)((C + cp - 1) / cp));
+  if (g_bn_vec_fwd && vec8_view(x) && vec8_view(y)) {
+    const int tp = tpg8(C);
+    const long px8 = (M + 256 / tp - 1) / (256 / tp);
+    const dim3 g8((unsigned)(px8 < 4096 ? px8 : 4096));
+    const bool xf = x->dtype == VM_F32, yf = y->dtype == VM_F32;
+#define VM_BA8(TPG)                                                                                                 \
+  case TPG:                                                                                                         \
+    if (xf && yf)                                                                                                   \
+      hipLaunchKernelGGL((bn_apply8_kernel<float, float, TPG>), g8, dim3(256), 0, st,                               \
+                         reinterpret_cast<const float*>(x->ptr) + x->coff, x->cstride,                              \
+                         reinterpret_cast<float*>(y->ptr) + y->coff, y->cstride, M, C, mean, var, gamma, beta, eps, act); \
+    else if (xf)                                                                                                    \
+      hipLaunchKernelGGL((bn_apply8_kernel<float, uint16_t, TPG>), g8, dim3(256), 0, st,                            \
+                         reinterpret_cast<const float*>(x->ptr) + x->coff, x->cstride,                              \
+                         reinterpret_cast<uint16_t*>(y->ptr) + y->coff, y->cstride, M, C, mean, var, gamma, beta, eps, \
+                         act);                                                                                      \
+    else if (yf)                                                                                                    \
+      hipLaunchKernelGGL((bn_apply8_kernel<uint16_t, float, TPG>), g8, dim3(256), 0, st,                            \
+                         reinterpret_cast<const uint16_t*>(x->ptr) + x->coff, x->cstride,                           \
+                         reinterpret_cast<float*>(y->ptr) + y->coff, y->cstride, M, C, mean, var, gamma, beta, eps, act); \
+    else                                                                                                            \
+      hipLaunchKernelGGL((bn_apply8_kernel<uint16_t, uint16_t, TPG>), g8, dim3(256), 0, st,                         \
+                         reinterpret_cast<const uint16_t*>(x->ptr) + x->coff, x->cstride,                           \
+                         reinterpret_cast<uint16_t*>(y->ptr) + y->coff, y->cstride, M, C, mean, var, gamma, beta, eps, \
+                         act);                                                                                      \
+    break;
+    switch (tp) { VM_BA8(1) VM_BA8(2) VM_BA8(4) VM_BA8(8) VM_BA8(16) VM_BA8(32) VM_BA8(64) }
+#undef VM_BA8
+    return check_launch("bn_apply");
+  }
   if (f32_pair_view(x) && f32_pair_view(y)) {
     hipLaunchKernelGGL(bn_apply2_f32_kernel, dim3(grid_for(M, 256)), dim3(256), 0, st,
                        reinterpret_cast<const float*>(x->ptr) + x->coff, x->cstride,

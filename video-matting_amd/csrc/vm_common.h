@@ -132,6 +132,7 @@ __device__ __forceinline__ float sigmoid_precise(float v) {
 // passes at ~2.5 TB/s; the partial sums are f64, so the block count only moves their rounding far below f32's.
 constexpr int BN_NBLK_MIN = 1024, BN_TARGET_MAX = 8192;
 extern long g_bn_target;
+extern long g_bn_vec_fwd;  // elementwise.hip: the 8-channel forward BN forms (vm_set_option "bn_vec_fwd")
 inline int bn_groups(int C) { return C > 32 ? (C + 63) / 64 : 1; }
 inline int bn_max_blocks(int C) {
   const int t = BN_TARGET_MAX / bn_groups(C);
