@@ -105,6 +105,27 @@ def test_loader_batch_1080p_sources_bit_exact(size):
         assert np.array_equal(H(got32[k]), want[k].astype(np.float32)), k
 
 
+def test_loader_batch_beyond_kernarg_descriptors():
+    """Batches of up to 8 samples pass their descriptors in the kernel arguments, larger ones upload them to the
+    workspace: a 10-sample batch equals the oracle exactly, and its first 5 samples equal a 5-sample batch."""
+    from vmatting import loader as vl
+    np.random.seed(23)
+    samples, mirror = [], []
+    for i in range(10):
+        fg, bg, prev, flow = ol.synthetic_entry(700 + i, (120 + 8 * i, 150), (140, 170 + 4 * i))
+        s = {"fg": fg, "bg": bg, "prev": prev, "flow": flow, "plan": vl.plan_crop(fg.shape[:2], bg.shape[:2])}
+        samples.append(s)
+        mirror.append(i % 3 == 0)
+    names = ("cmp", "bg", "label", "warped")
+    want = _oracle_batch(samples, (64, 64), mirror)
+    got = vl.compose_batch(samples, (64, 64), names, mirror, dtype=torch.float64)
+    part = vl.compose_batch(samples[:5], (64, 64), names, mirror[:5], dtype=torch.float64)
+    torch.cuda.synchronize()
+    for k in names:
+        assert np.array_equal(H(got[k]), want[k]), k
+        assert torch.equal(got[k][:5], part[k]), k
+
+
 def test_loader_device_resident_inputs_and_input_layout():
     """Inputs already in HBM (device tensors) and get_batch's 6-channel input layout."""
     from vmatting import loader as vl

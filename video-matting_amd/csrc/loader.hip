@@ -16,6 +16,8 @@
 
 #include <cfloat>
 
+#include <type_traits>
+
 #include "vm_common.h"
 
 namespace vm {
@@ -123,10 +125,18 @@ __device__ __forceinline__ void put(void* base, long pix, int stride, int k, dou
   reinterpret_cast<T*>(base)[pix * stride + k] = (T)v;
 }
 
-template <typename T>
-__global__ __launch_bounds__(256) void loader_compose_kernel(const vm_loader_sample* __restrict__ samples, int oh,
-                                                             int ow, vm_loader_outputs out) {
-  const vm_loader_sample& s = samples[blockIdx.y];
+// up to kLoaderJobs descriptors travel by value in the kernel arguments (no upload copy per batch)
+constexpr int kLoaderJobs = 8;
+struct LoaderJobs {
+  vm_loader_sample s[kLoaderJobs];
+};
+
+template <typename T, typename SRC>
+__global__ __launch_bounds__(256) void loader_compose_kernel(SRC samples, int oh, int ow, vm_loader_outputs out) {
+  const vm_loader_sample& s = [&]() -> const vm_loader_sample& {
+    if constexpr (std::is_same_v<SRC, LoaderJobs>) return samples.s[blockIdx.y];
+    else return samples[blockIdx.y];
+  }();
   const int p = blockIdx.x * 256 + threadIdx.x;
   if (p >= oh * ow) return;
   const int dy = p / ow, dxo = p - dy * ow;
@@ -210,13 +220,24 @@ extern "C" int vm_loader_compose(const vm_loader_sample* samples, int n, int out
       return fail(VM_EINVAL, "loader_compose: sample %d: crop window outside the image", i);
   }
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const dim3 grid((out_h * out_w + 255) / 256, n);
+  if (n <= kLoaderJobs) {  // the descriptors by value: one launch, no upload
+    LoaderJobs J{};
+    for (int i = 0; i < n; ++i) J.s[i] = samples[i];
+    if (dtype == VM_F32)
+      hipLaunchKernelGGL((loader_compose_kernel<float, LoaderJobs>), grid, dim3(256), 0, st, J, out_h, out_w, *out);
+    else
+      hipLaunchKernelGGL((loader_compose_kernel<double, LoaderJobs>), grid, dim3(256), 0, st, J, out_h, out_w, *out);
+    return check_launch("loader_compose");
+  }
   hipError_t e = hipMemcpyAsync(work, samples, (size_t)n * sizeof(vm_loader_sample), hipMemcpyHostToDevice, st);
   if (e != hipSuccess) return fail(VM_EHIP, "loader_compose: descriptor upload: %s", hipGetErrorString(e));
   const auto* dev = reinterpret_cast<const vm_loader_sample*>(work);
-  const dim3 grid((out_h * out_w + 255) / 256, n);
   if (dtype == VM_F32)
-    hipLaunchKernelGGL(loader_compose_kernel<float>, grid, dim3(256), 0, st, dev, out_h, out_w, *out);
+    hipLaunchKernelGGL((loader_compose_kernel<float, const vm_loader_sample*>), grid, dim3(256), 0, st, dev, out_h,
+                       out_w, *out);
   else
-    hipLaunchKernelGGL(loader_compose_kernel<double>, grid, dim3(256), 0, st, dev, out_h, out_w, *out);
+    hipLaunchKernelGGL((loader_compose_kernel<double, const vm_loader_sample*>), grid, dim3(256), 0, st, dev, out_h,
+                       out_w, *out);
   return check_launch("loader_compose");
 }
