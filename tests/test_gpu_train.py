@@ -341,6 +341,12 @@ def test_resize_backward(ih, iw, oh, ow, c):
         dx1 = torch.empty_like(dx)
         ops.resize_backward(wide[..., :c], dx1)
         assert torch.equal(dx1, dx)
+    # bf16 dy (the bf16 training path's data gradients) == the f32 run on the same bf16-rounded values
+    dyb = T(dy, torch.bfloat16)
+    dxb, dxf = torch.empty_like(dx), torch.empty_like(dx)
+    ops.resize_backward(dyb, dxb)
+    ops.resize_backward(dyb.float(), dxf)
+    assert torch.equal(dxb, dxf)
 
 
 def test_relu_backward():
@@ -1098,19 +1104,24 @@ def test_train_step_bf16_gradients_bench_shape():
 @pytest.mark.parametrize("pool", [False, True])
 @pytest.mark.parametrize("with_add", [False, True])
 @pytest.mark.parametrize("c", [8, 64, 128, 512])
-def test_relu_backward_bias_vectorised_bit_identical(pool, with_add, c):
+@pytest.mark.parametrize("gdt", ["f32", "bf16", "mixed"])
+def test_relu_backward_bias_vectorised_bit_identical(pool, with_add, c, gdt):
     """The 8-channels-per-lane form of vm_relu_backward_bias_nhwc (relu_bias_vec 1, bf16 y / dz) writes exactly the
     per-element form's dz (same arithmetic per element, first-maximum pool adjoint, odd edges), and the bias gradient
-    within f64-partial rounding of it."""
+    within f64-partial rounding of it — for f32 or bf16 dy / add (gdt; mixed = bf16 dy, f32 add)."""
     from vmatting import _lib, ops
+    if gdt != "f32" and c == 8 and not with_add:
+        pytest.skip("covered by the c = 64 cases")
     rs = np.random.RandomState(c + 2 * pool + with_add)
     n, h, w = 2, 17, 23
     y = np.maximum(rs.normal(size=(n, h, w, c)), 0).astype(np.float32)
     y[:, ::3, ::2] = np.round(y[:, ::3, ::2])  # exact ties inside windows
     yd = T(y, torch.bfloat16)
     ph, pw = (h + 1) // 2, (w + 1) // 2
-    dy = T(rs.normal(size=(n, ph, pw, c) if pool else (n, h, w, c)).astype(np.float32))
-    add = T(rs.normal(size=(n, h, w, c)).astype(np.float32)) if with_add else None
+    dyt = torch.float32 if gdt == "f32" else torch.bfloat16
+    at = torch.bfloat16 if gdt == "bf16" else torch.float32
+    dy = T(rs.normal(size=(n, ph, pw, c) if pool else (n, h, w, c)).astype(np.float32), dyt)
+    add = T(rs.normal(size=(n, h, w, c)).astype(np.float32), at) if with_add else None
     out = []
     try:
         for vec in (0, 1):

@@ -539,10 +539,12 @@ __global__ __launch_bounds__(256) void relu_bwd_bias_kernel(V dy, V y, V add, V 
 // issued a 2- to 4-byte access per channel (~2.5 TB/s).  Per element the same arithmetic (g = dy, g += add in f32;
 // the first-maximum pool adjoint; z rounded to bf16 as st() does), so dz is bit-identical; the channel sums are f64
 // partials per block in another partition of the pixels, folded in fixed order by fold_sum_kernel as before.
-template <bool POOL, bool ADD, int TPG>  // TPG: lanes per pixel (a power of two >= C / 8)
-__global__ __launch_bounds__(256) void relu_bwd_bias8_kernel(const float* __restrict__ dy, int dycs,
+// TPG: lanes per pixel (a power of two >= C / 8).  TD / TA: f32 or bf16 dy / add (the bf16 training path hands its
+// data gradients over as bf16; a bf16 chunk widens exactly to f32, so the arithmetic after the load is the same).
+template <bool POOL, bool ADD, int TPG, typename TD = float, typename TA = float>
+__global__ __launch_bounds__(256) void relu_bwd_bias8_kernel(const TD* __restrict__ dy, int dycs,
                                                              const uint16_t* __restrict__ y, int ycs,
-                                                             const float* __restrict__ add, int acs,
+                                                             const TA* __restrict__ add, int acs,
                                                              uint16_t* __restrict__ dz, int zcs, int N, int H, int W,
                                                              int DH, int DW, int C, double* part, int nblk) {
   constexpr int PPB = 256 / TPG;
@@ -550,10 +552,6 @@ __global__ __launch_bounds__(256) void relu_bwd_bias8_kernel(const float* __rest
   const int t = threadIdx.x, j = t % TPG, pl = t / TPG;
   const int c0 = 8 * j;
   double s[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-  auto ld8f = [&](const float* p, float (&v)[8]) __attribute__((always_inline)) {
-    const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
-    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
-  };
   auto ld8y = [&](const uint16_t* p, float (&v)[8]) __attribute__((always_inline)) {
     const uint4 q = *reinterpret_cast<const uint4*>(p);
     const uint32_t w4[4] = {q.x, q.y, q.z, q.w};
@@ -561,6 +559,14 @@ __global__ __launch_bounds__(256) void relu_bwd_bias8_kernel(const float* __rest
     for (int k = 0; k < 4; ++k) {
       v[2 * k] = bf2f((uint16_t)(w4[k] & 0xffffu));
       v[2 * k + 1] = bf2f((uint16_t)(w4[k] >> 16));
+    }
+  };
+  auto ld8f = [&](const auto* p, float (&v)[8]) __attribute__((always_inline)) {
+    if constexpr (sizeof(*p) == 4) {
+      const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+      v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+    } else {
+      ld8y(reinterpret_cast<const uint16_t*>(p), v);
     }
   };
   auto st8 = [&](uint16_t* p, const float (&z)[8]) __attribute__((always_inline)) {
@@ -702,6 +708,7 @@ __global__ void resize_bwd_kernel(V dy, float* dx, int ih, int iw, float sy, flo
 
 // the same gather, 4 channels per thread with 16-byte loads / stores (c % 4 == 0, 16-byte aligned dy channel
 // vectors): the taps and weights are computed once per 4 channels; per channel the arithmetic is resize_bwd_kernel's
+template <typename TD>  // dy f32 (16-byte loads) or bf16 (8-byte loads: the bf16 training path's data gradients)
 __global__ void resize_bwd_kernel4(V dy, float* dx, int ih, int iw, float sy, float sx) {
   const int C4 = dy.c / 4;
   const long total = (long)dy.n * ih * iw * C4;
@@ -722,8 +729,16 @@ __global__ void resize_bwd_kernel4(V dy, float* dx, int ih, int iw, float sy, fl
       for (int ow = q0; ow <= q1; ++ow) {
         const float wx = tap_w(ow, sx, iw, ix);
         if (wx != 0.f) {
-          const float4 v = *reinterpret_cast<const float4*>(
-              reinterpret_cast<const float*>(dy.p) + (((long)n * dy.h + oh) * dy.w + ow) * dy.cs + dy.coff + c);
+          float4 v;
+          if constexpr (sizeof(TD) == 4) {
+            v = *reinterpret_cast<const float4*>(
+                reinterpret_cast<const float*>(dy.p) + (((long)n * dy.h + oh) * dy.w + ow) * dy.cs + dy.coff + c);
+          } else {
+            const uint2 u = *reinterpret_cast<const uint2*>(
+                reinterpret_cast<const uint16_t*>(dy.p) + (((long)n * dy.h + oh) * dy.w + ow) * dy.cs + dy.coff + c);
+            v = make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
+                            __uint_as_float(u.y & 0xffff0000u));
+          }
           row.x += wx * v.x;
           row.y += wx * v.y;
           row.z += wx * v.z;
@@ -2649,9 +2664,8 @@ extern "C" int vm_relu_backward_bias_nhwc(const vm_tensor* dy, const vm_tensor* 
                                           vm_tensor* dz, float* dbias, void* work, void* stream) {
   if (!ok_view(dy) || !ok_view(y) || !ok_view(dz) || (add && !ok_view(add)) || !dbias || !work)
     return fail(VM_EINVAL, "relu_backward_bias: bad argument");
-  if (dy->dtype != VM_F32 || (add && add->dtype != VM_F32) || !same_shape(dz, y) || (add && !same_shape(add, y)) ||
-      dy->n != y->n || dy->c != y->c)
-    return fail(VM_EINVAL, "relu_backward_bias: dy / add f32, dz and add shaped like y");
+  if (!same_shape(dz, y) || (add && !same_shape(add, y)) || dy->n != y->n || dy->c != y->c)
+    return fail(VM_EINVAL, "relu_backward_bias: dz and add shaped like y");
   const bool pool = !(dy->h == y->h && dy->w == y->w);
   if (pool && (dy->h != (y->h + 1) / 2 || dy->w != (y->w + 1) / 2))
     return fail(VM_EINVAL, "relu_backward_bias: dy must be y's shape or its 2x2 SAME pool's");
@@ -2665,28 +2679,42 @@ extern "C" int vm_relu_backward_bias_nhwc(const vm_tensor* dy, const vm_tensor* 
   if (g_relu_bias_vec && y->dtype == VM_BF16 && dz->dtype == VM_BF16 && C % 8 == 0 && C <= 512 && al16(y, 2) &&
       al16(dz, 2) && al16(dy, 4) && (!add || al16(add, 4))) {
     const int tpg = C / 8 > 32 ? 64 : C / 8 > 16 ? 32 : C / 8 > 8 ? 16 : C / 8 > 4 ? 8 : C / 8 > 2 ? 4 : C / 8 > 1 ? 2 : 1;
-    const float* dyp = reinterpret_cast<const float*>(dy->ptr) + dy->coff;
     const uint16_t* yp = reinterpret_cast<const uint16_t*>(y->ptr) + y->coff;
-    const float* ap = add ? reinterpret_cast<const float*>(add->ptr) + add->coff : nullptr;
     uint16_t* zp = reinterpret_cast<uint16_t*>(dz->ptr) + dz->coff;
     double* part = reinterpret_cast<double*>(work);
-#define VM_RB8(TPG)                                                                                                    \
-  case TPG:                                                                                                            \
-    if (pool && add)                                                                                                   \
-      hipLaunchKernelGGL((relu_bwd_bias8_kernel<true, true, TPG>), dim3(nb), dim3(256), 0, st, dyp, dy->cstride, yp,   \
-                         y->cstride, ap, add->cstride, zp, dz->cstride, y->n, y->h, y->w, dy->h, dy->w, C, part, nb);  \
-    else if (pool)                                                                                                     \
-      hipLaunchKernelGGL((relu_bwd_bias8_kernel<true, false, TPG>), dim3(nb), dim3(256), 0, st, dyp, dy->cstride, yp,  \
-                         y->cstride, ap, 0, zp, dz->cstride, y->n, y->h, y->w, dy->h, dy->w, C, part, nb);             \
-    else if (add)                                                                                                      \
-      hipLaunchKernelGGL((relu_bwd_bias8_kernel<false, true, TPG>), dim3(nb), dim3(256), 0, st, dyp, dy->cstride, yp,  \
-                         y->cstride, ap, add->cstride, zp, dz->cstride, y->n, y->h, y->w, dy->h, dy->w, C, part, nb);  \
-    else                                                                                                               \
-      hipLaunchKernelGGL((relu_bwd_bias8_kernel<false, false, TPG>), dim3(nb), dim3(256), 0, st, dyp, dy->cstride, yp, \
-                         y->cstride, ap, 0, zp, dz->cstride, y->n, y->h, y->w, dy->h, dy->w, C, part, nb);             \
+    auto go = [&](auto dyt, auto at) {  // dy / add element types
+      using TD = decltype(dyt);
+      using TA = decltype(at);
+      const TD* dyp = reinterpret_cast<const TD*>(dy->ptr) + dy->coff;
+      const TA* ap = add ? reinterpret_cast<const TA*>(add->ptr) + add->coff : nullptr;
+      const int acs = add ? add->cstride : 0;
+#define VM_RB8(TPG)                                                                                                  \
+  case TPG:                                                                                                          \
+    if (pool && add)                                                                                                 \
+      hipLaunchKernelGGL((relu_bwd_bias8_kernel<true, true, TPG, TD, TA>), dim3(nb), dim3(256), 0, st, dyp,          \
+                         dy->cstride, yp, y->cstride, ap, acs, zp, dz->cstride, y->n, y->h, y->w, dy->h, dy->w, C,   \
+                         part, nb);                                                                                  \
+    else if (pool)                                                                                                   \
+      hipLaunchKernelGGL((relu_bwd_bias8_kernel<true, false, TPG, TD, TA>), dim3(nb), dim3(256), 0, st, dyp,         \
+                         dy->cstride, yp, y->cstride, ap, acs, zp, dz->cstride, y->n, y->h, y->w, dy->h, dy->w, C,   \
+                         part, nb);                                                                                  \
+    else if (add)                                                                                                    \
+      hipLaunchKernelGGL((relu_bwd_bias8_kernel<false, true, TPG, TD, TA>), dim3(nb), dim3(256), 0, st, dyp,         \
+                         dy->cstride, yp, y->cstride, ap, acs, zp, dz->cstride, y->n, y->h, y->w, dy->h, dy->w, C,   \
+                         part, nb);                                                                                  \
+    else                                                                                                             \
+      hipLaunchKernelGGL((relu_bwd_bias8_kernel<false, false, TPG, TD, TA>), dim3(nb), dim3(256), 0, st, dyp,        \
+                         dy->cstride, yp, y->cstride, ap, acs, zp, dz->cstride, y->n, y->h, y->w, dy->h, dy->w, C,   \
+                         part, nb);                                                                                  \
     break;
-    switch (tpg) { VM_RB8(1) VM_RB8(2) VM_RB8(4) VM_RB8(8) VM_RB8(16) VM_RB8(32) VM_RB8(64) }
+      switch (tpg) { VM_RB8(1) VM_RB8(2) VM_RB8(4) VM_RB8(8) VM_RB8(16) VM_RB8(32) VM_RB8(64) }
 #undef VM_RB8
+    };
+    const bool dyb = dy->dtype == VM_BF16, ab = add && add->dtype == VM_BF16;
+    if (dyb && ab) go(uint16_t{}, uint16_t{});
+    else if (dyb) go(uint16_t{}, float{});
+    else if (ab) go(float{}, uint16_t{});
+    else go(float{}, float{});
     int rc = check_launch("relu_backward_bias");
     if (rc) return rc;
     hipLaunchKernelGGL(fold_sum_kernel, dim3(C), dim3(256), 0, st, part, nb, C, dbias);
@@ -2714,10 +2742,15 @@ extern "C" int vm_resize_bilinear_tf1_backward(const vm_tensor* dy, float* dx, i
     return fail(VM_EUNSUPPORTED, "resize_backward: scale %dx%d -> %dx%d outside the upsampling range", ih, iw, dy->h,
                 dy->w);
   const float sy = (float)ih / (float)dy->h, sx = (float)iw / (float)dy->w;
-  if (dy->dtype == VM_F32 && dy->c % 4 == 0 && dy->cstride % 4 == 0 && dy->coff % 4 == 0 &&
-      reinterpret_cast<uintptr_t>(dy->ptr) % 16 == 0 && reinterpret_cast<uintptr_t>(dx) % 16 == 0) {
+  if (dy->c % 4 == 0 && dy->cstride % 4 == 0 && dy->coff % 4 == 0 && reinterpret_cast<uintptr_t>(dy->ptr) % 16 == 0 &&
+      reinterpret_cast<uintptr_t>(dx) % 16 == 0) {
     const long n4 = (long)dy->n * ih * iw * (dy->c / 4);
-    hipLaunchKernelGGL(resize_bwd_kernel4, dim3(grid_for(n4, 256)), dim3(256), 0, st, mk(dy), dx, ih, iw, sy, sx);
+    if (dy->dtype == VM_F32)
+      hipLaunchKernelGGL(resize_bwd_kernel4<float>, dim3(grid_for(n4, 256)), dim3(256), 0, st, mk(dy), dx, ih, iw, sy,
+                         sx);
+    else
+      hipLaunchKernelGGL(resize_bwd_kernel4<uint16_t>, dim3(grid_for(n4, 256)), dim3(256), 0, st, mk(dy), dx, ih, iw,
+                         sy, sx);
     return check_launch("resize_backward");
   }
   const long n = (long)dy->n * ih * iw * dy->c;

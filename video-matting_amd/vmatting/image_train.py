@@ -53,6 +53,8 @@ def param_layout(shapes):
 class ImageTrainer(TrainerBase):
     """train.training_procedure's iteration on device (unet.UNetImage, all variables trainable)."""
 
+    bf16_dgrad = True  # bf16 path: data gradients held in bf16 (see _grad_buffers); False = f32 as the fp32 path
+
     def __init__(self, vgg16_npy_path=None, dtype="fp32", device="cuda", params=None, lr=1e-5, beta1=0.9,
                  beta2=0.999, epsilon=1e-8):
         m = UNetImage(vgg16_npy_path, dtype, device)
@@ -106,24 +108,32 @@ class ImageTrainer(TrainerBase):
         dev = self.device
         F = lambda lv, c: torch.zeros((n, L[lv][0], L[lv][1], c), dtype=torch.float32, device=dev)  # noqa: E731
         bf16 = self.dtype == torch.bfloat16
+        B = lambda lv, c: torch.zeros((n, L[lv][0], L[lv][1], c), dtype=torch.bfloat16, device=dev)  # noqa: E731
         Z = (lambda lv, c: None) if bf16 else F  # noqa: E731  (f32 dz: the fp32 path only)
+        # D: the data gradients the dgrad convs write.  The bf16 path keeps them bf16 (bf16_dgrad): their only
+        # readers round to bf16 anyway (the MFMA convs' operands) or widen exactly (the relu / resize adjoints), so
+        # the convs write half the bytes and the upconv gradient needs no f32 -> bf16 convert.  The resize adjoint's
+        # outputs (dc23, dc34, dc44, dc52) stay f32: it accumulates.
+        D = B if bf16 and self.bf16_dgrad else F
         g = {"dlogit": F(0, 1), "dlog8": F(0, 8), "loss": torch.zeros(3, dtype=torch.float32, device=dev),
              "in6": torch.empty((n, h, w, 6), dtype=torch.float32, device=dev),
-             "dcat1": F(0, 128), "dr4": F(0, 128), "dz12": Z(0, 64), "dc11": F(0, 64), "dz11": Z(0, 64),
-             "dcat2": F(1, 256), "dc23": F(1, 128), "dz23": Z(1, 128), "dr3": F(1, 256), "dz22": Z(1, 128),
-             "dc21": F(1, 128), "dz21": Z(1, 128), "dp1": F(1, 64),
-             "dcat3": F(2, 512), "dc34": F(2, 256), "dz34": Z(2, 256), "dr2": F(2, 512), "dz33": Z(2, 256),
-             "dc32": F(2, 256), "dz32": Z(2, 256), "dc31": F(2, 256), "dz31": Z(2, 256), "dp2": F(2, 128),
-             "dcat4": F(3, 1024), "dc44": F(3, 512), "dz44": Z(3, 512), "dr1": F(3, 512), "dz43": Z(3, 512),
-             "dc42": F(3, 512), "dz42": Z(3, 512), "dc41": F(3, 512), "dz41": Z(3, 512), "dp3": F(3, 256),
-             "dc52": F(4, 512), "dz52": Z(4, 512), "dc51": F(4, 512), "dz51": Z(4, 512), "dp4": F(4, 512)}
-        if self.dtype == torch.bfloat16:
-            B = lambda lv, c: torch.zeros((n, L[lv][0], L[lv][1], c), dtype=torch.bfloat16, device=dev)  # noqa: E731
-            for k, (lv, c) in {"dlog16": (0, 32), "du4": (0, 64), "dz12": (0, 64), "dz11": (0, 64),
-                               "dz23": (1, 128), "du3": (1, 128), "dz22": (1, 128), "dz21": (1, 128),
-                               "dz34": (2, 256), "du2": (2, 256), "dz33": (2, 256), "dz32": (2, 256),
-                               "dz31": (2, 256), "dz44": (3, 512), "du1": (3, 512), "dz43": (3, 512),
-                               "dz42": (3, 512), "dz41": (3, 512), "dz52": (4, 512), "dz51": (4, 512)}.items():
+             "dcat1": D(0, 128), "dr4": D(0, 128), "dz12": Z(0, 64), "dc11": D(0, 64), "dz11": Z(0, 64),
+             "dcat2": D(1, 256), "dc23": F(1, 128), "dz23": Z(1, 128), "dr3": D(1, 256), "dz22": Z(1, 128),
+             "dc21": D(1, 128), "dz21": Z(1, 128), "dp1": D(1, 64),
+             "dcat3": D(2, 512), "dc34": F(2, 256), "dz34": Z(2, 256), "dr2": D(2, 512), "dz33": Z(2, 256),
+             "dc32": D(2, 256), "dz32": Z(2, 256), "dc31": D(2, 256), "dz31": Z(2, 256), "dp2": D(2, 128),
+             "dcat4": D(3, 1024), "dc44": F(3, 512), "dz44": Z(3, 512), "dr1": D(3, 512), "dz43": Z(3, 512),
+             "dc42": D(3, 512), "dz42": Z(3, 512), "dc41": D(3, 512), "dz41": Z(3, 512), "dp3": D(3, 256),
+             "dc52": F(4, 512), "dz52": Z(4, 512), "dc51": D(4, 512), "dz51": Z(4, 512), "dp4": D(4, 512)}
+        if bf16:
+            hb = {"dlog16": (0, 32), "dz12": (0, 64), "dz11": (0, 64),
+                  "dz23": (1, 128), "dz22": (1, 128), "dz21": (1, 128),
+                  "dz34": (2, 256), "dz33": (2, 256), "dz32": (2, 256), "dz31": (2, 256),
+                  "dz44": (3, 512), "dz43": (3, 512), "dz42": (3, 512), "dz41": (3, 512),
+                  "dz52": (4, 512), "dz51": (4, 512)}
+            if not self.bf16_dgrad:  # dense bf16 copies of the upconv gradients
+                hb.update({"du4": (0, 64), "du3": (1, 128), "du2": (2, 256), "du1": (3, 512)})
+            for k, (lv, c) in hb.items():
                 g["h_" + k] = B(lv, c)
         g = {k: v for k, v in g.items() if v is not None}
         self._g, self._key = g, (n, h, w)
@@ -174,6 +184,8 @@ class ImageTrainer(TrainerBase):
         h16 = self._g.get("h_" + up_key)
         if h16 is not None:
             ops.convert(dup, h16)
+        elif dup.dtype == torch.bfloat16:  # bf16_dgrad: the bf16 slice of dcat is the MFMA operand itself
+            h16 = dup
         self._wgrad_dgrad(name, rbuf, dup, h16, dr)
         ops.resize_backward(dr, dprev)
 
