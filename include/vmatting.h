@@ -510,9 +510,11 @@ size_t vm_relu_backward_bias_workspace_bytes(int channels);
 int vm_relu_backward_bias_nhwc(const vm_tensor* dy, const vm_tensor* y, const vm_tensor* add, vm_tensor* dz,
                                float* dbias, void* work, void* stream);
 
-/* Adjoint of vm_resize_bilinear_tf1_nhwc (tf.image.resize_images, unet_simple.py:33): dy [n,oh,ow,c] (f32 view) ->
- * dx contiguous f32 [n,ih,iw,c] (overwritten). */
+/* Adjoint of vm_resize_bilinear_tf1_nhwc (tf.image.resize_images, unet_simple.py:33): dy [n,oh,ow,c] (f32 or bf16
+ * view) -> dx contiguous f32 [n,ih,iw,c] (overwritten). */
 int vm_resize_bilinear_tf1_backward(const vm_tensor* dy, float* dx, int ih, int iw, void* stream);
+/* The same with dx a dense view [n,ih,iw,c]: f32, or bf16 (c % 4 == 0; each f32 sum rounded once to nearest even). */
+int vm_resize_bilinear_tf1_backward_nhwc(const vm_tensor* dy, vm_tensor* dx, void* stream);
 
 /* Workspace of vm_conv3x3_wgrad_nhwc (per-block partial filter gradients, <= 64 MiB). */
 size_t vm_conv3x3_wgrad_workspace_bytes(int n, int h, int w, int cin, int cout);

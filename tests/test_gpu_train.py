@@ -347,6 +347,37 @@ def test_resize_backward(ih, iw, oh, ow, c):
     ops.resize_backward(dyb, dxb)
     ops.resize_backward(dyb.float(), dxf)
     assert torch.equal(dxb, dxf)
+    if c % 4 == 0:  # bf16 dx (vm_resize_bilinear_tf1_backward_nhwc): the f32 sums rounded once to nearest even
+        for src in (T(dy), dyb):
+            ref = torch.empty_like(dx)
+            ops.resize_backward(src, ref)
+            d16 = torch.empty(dx.shape, dtype=torch.bfloat16, device=DEV)
+            ops.resize_backward(src, d16)
+            assert torch.equal(d16, ref.bfloat16())
+
+
+@pytest.mark.parametrize("ih,iw", [(5, 7), (1, 1), (20, 20), (40, 33), (160, 160)])
+@pytest.mark.parametrize("c", [8, 64, 512])
+def test_resize_backward_2x_matches_windowed(ih, iw, c):
+    """The exact-2x adjoint (resize2x_bwd_kernel8: closed-form taps) equals the windowed-search kernels bit for bit, for
+    f32 / bf16 dy and f32 / bf16 dx (option resize_bwd_2x 0 = the windowed form)."""
+    from vmatting import _lib, ops
+    if ih * iw * c > 160 * 160 * 64:
+        pytest.skip("size")
+    rs = np.random.RandomState(ih * 7 + c)
+    dy = rs.normal(size=(2, 2 * ih, 2 * iw, c)).astype(np.float32)
+    for ddt in (torch.float32, torch.bfloat16):
+        for xdt in (torch.float32, torch.bfloat16):
+            out = []
+            try:
+                for fast in (0, 1):
+                    _lib.set_option("resize_bwd_2x", fast)
+                    dx = torch.empty((2, ih, iw, c), dtype=xdt, device=DEV)
+                    ops.resize_backward(T(dy, ddt), dx)
+                    out.append(dx)
+            finally:
+                _lib.set_option("resize_bwd_2x", 1)
+            assert torch.equal(out[0], out[1]), (ddt, xdt)
 
 
 def test_relu_backward():
@@ -1105,15 +1136,18 @@ def test_train_step_bf16_gradients_bench_shape():
 @pytest.mark.parametrize("with_add", [False, True])
 @pytest.mark.parametrize("c", [8, 64, 128, 512])
 @pytest.mark.parametrize("gdt", ["f32", "bf16", "mixed"])
-def test_relu_backward_bias_vectorised_bit_identical(pool, with_add, c, gdt):
+@pytest.mark.parametrize("nhw", [(2, 17, 23), (8, 40, 40)])
+def test_relu_backward_bias_vectorised_bit_identical(pool, with_add, c, gdt, nhw):
     """The 8-channels-per-lane form of vm_relu_backward_bias_nhwc (relu_bias_vec 1, bf16 y / dz) writes exactly the
     per-element form's dz (same arithmetic per element, first-maximum pool adjoint, odd edges), and the bias gradient
     within f64-partial rounding of it — for f32 or bf16 dy / add (gdt; mixed = bf16 dy, f32 add)."""
     from vmatting import _lib, ops
     if gdt != "f32" and c == 8 and not with_add:
         pytest.skip("covered by the c = 64 cases")
+    if nhw[0] == 8 and (gdt == "mixed" or c < 128):
+        pytest.skip("the UNetImage level-3 shape: 128 / 512 channels")
     rs = np.random.RandomState(c + 2 * pool + with_add)
-    n, h, w = 2, 17, 23
+    n, h, w = nhw
     y = np.maximum(rs.normal(size=(n, h, w, c)), 0).astype(np.float32)
     y[:, ::3, ::2] = np.round(y[:, ::3, ::2])  # exact ties inside windows
     yd = T(y, torch.bfloat16)

@@ -19,6 +19,7 @@
 //   maxpool_bwd     tf.nn.max_pool 2x2/2 SAME adjoint: the window's gradient to its first maximum (small.py:40,42)
 //   adam            TF ApplyAdam: m += (g-m)(1-b1); v += (g^2-v)(1-b2); var -= m*lr_t/(sqrt(v)+eps)
 
+#include <algorithm>
 #include <cstring>
 
 #include "conv_common.h"
@@ -708,8 +709,10 @@ __global__ void resize_bwd_kernel(V dy, float* dx, int ih, int iw, float sy, flo
 
 // the same gather, 4 channels per thread with 16-byte loads / stores (c % 4 == 0, 16-byte aligned dy channel
 // vectors): the taps and weights are computed once per 4 channels; per channel the arithmetic is resize_bwd_kernel's
-template <typename TD>  // dy f32 (16-byte loads) or bf16 (8-byte loads: the bf16 training path's data gradients)
-__global__ void resize_bwd_kernel4(V dy, float* dx, int ih, int iw, float sy, float sx) {
+// TD: dy f32 (16-byte loads) or bf16 (8-byte loads: the bf16 training path's data gradients); TX: dx f32, or bf16
+// (each f32 sum rounded to nearest even once, as a bf16 store of the f32 result would)
+template <typename TD, typename TX = float>
+__global__ void resize_bwd_kernel4(V dy, TX* dx, int ih, int iw, float sy, float sx) {
   const int C4 = dy.c / 4;
   const long total = (long)dy.n * ih * iw * C4;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
@@ -750,7 +753,13 @@ __global__ void resize_bwd_kernel4(V dy, float* dx, int ih, int iw, float sy, fl
       acc.z += wy * row.z;
       acc.w += wy * row.w;
     }
-    *reinterpret_cast<float4*>(dx + ip * dy.c + c) = acc;
+    if constexpr (sizeof(TX) == 4) {
+      *reinterpret_cast<float4*>(dx + ip * dy.c + c) = acc;
+    } else {
+      const uint2 u = make_uint2((uint32_t)f2bf(acc.x) | ((uint32_t)f2bf(acc.y) << 16),
+                                 (uint32_t)f2bf(acc.z) | ((uint32_t)f2bf(acc.w) << 16));
+      *reinterpret_cast<uint2*>(dx + ip * dy.c + c) = u;
+    }
   }
 }
 
@@ -2187,7 +2196,10 @@ static int launch_wgrad_grid(const void* kern, int lds, int th, int cib, int& at
 }
 
 static long g_bn_vec = 1;  // vm_set_option "bn_vec": 0 = the per-channel BN backward forms (A/B)
+static long g_resize_bwd_2x = 1;  // vm_set_option "resize_bwd_2x": 0 = the windowed-search kernels for 2x too (A/B)
 static long g_relu_bias_vec = 1;  // vm_set_option "relu_bias_vec": 0 = the per-element relu / bias backward (A/B)
+static long g_relu_bias_iters = 8;  // vm_set_option "relu_bias_iters": pixel iterations per thread of the 8-channel
+                                    // form's grid (0 = bn_blocks' rule)
 static long g_wgrad_mfma_pipe = 1;  // vm_set_option "wgrad_mfma_pipe": 0 = wgrad_mfma_kernel's plain loop (A/B)
 template <int NCI, int NCO, bool SX, int TH, bool PIPE>
 static int launch_wgrad_mfma_p(WgArgs& a, float* dw, hipStream_t st) {
@@ -2298,6 +2310,14 @@ int train_set_option(const char* key, long value) {
   }
   if (!strcmp(key, "relu_bias_vec")) {
     trn::g_relu_bias_vec = value;
+    return 1;
+  }
+  if (!strcmp(key, "resize_bwd_2x")) {
+    trn::g_resize_bwd_2x = value;
+    return 1;
+  }
+  if (!strcmp(key, "relu_bias_iters")) {
+    trn::g_relu_bias_iters = value;
     return 1;
   }
   if (!strcmp(key, "wgrad_mfma_pipe")) {
@@ -2672,13 +2692,19 @@ extern "C" int vm_relu_backward_bias_nhwc(const vm_tensor* dy, const vm_tensor* 
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int C = y->c;
   const long units = pool ? (long)dy->n * dy->h * dy->w : (long)y->n * y->h * y->w;
-  const int nb = bn_blocks(pool ? 4 * units : units, C);
   auto al16 = [](const vm_tensor* t, int es) {  // every 8-channel run of the view 16-byte aligned
     return t->cstride % 8 == 0 && t->coff % 8 == 0 && reinterpret_cast<uintptr_t>(t->ptr) % 16 == 0 && es > 0;
   };
   if (g_relu_bias_vec && y->dtype == VM_BF16 && dz->dtype == VM_BF16 && C % 8 == 0 && C <= 512 && al16(y, 2) &&
       al16(dz, 2) && al16(dy, 4) && (!add || al16(add, 4))) {
     const int tpg = C / 8 > 32 ? 64 : C / 8 > 16 ? 32 : C / 8 > 8 ? 16 : C / 8 > 4 ? 8 : C / 8 > 2 ? 4 : C / 8 > 1 ? 2 : 1;
+    // every block covers all C channels of 256 / tpg pixels per iteration: size the grid for ~g_relu_bias_iters
+    // iterations per thread (bn_blocks' per-channel-group rule left the 512-channel levels at 12-50 blocks)
+    int nb = bn_blocks(pool ? 4 * units : units, C);
+    if (g_relu_bias_iters > 0) {
+      const long want = (pool ? 4 * units : units) / ((256 / tpg) * g_relu_bias_iters);
+      nb = (int)std::max(1L, std::min<long>(want, bn_max_blocks(C)));
+    }
     const uint16_t* yp = reinterpret_cast<const uint16_t*>(y->ptr) + y->coff;
     uint16_t* zp = reinterpret_cast<uint16_t*>(dz->ptr) + dz->coff;
     double* part = reinterpret_cast<double*>(work);
@@ -2720,6 +2746,7 @@ extern "C" int vm_relu_backward_bias_nhwc(const vm_tensor* dy, const vm_tensor* 
     hipLaunchKernelGGL(fold_sum_kernel, dim3(C), dim3(256), 0, st, part, nb, C, dbias);
     return check_launch("relu_backward_bias fold");
   }
+  const int nb = bn_blocks(pool ? 4 * units : units, C);
   const int cp = C > 32 ? 64 : C > 16 ? 32 : C > 8 ? 16 : C > 4 ? 8 : C > 2 ? 4 : C > 1 ? 2 : 1;
   const dim3 grid(cp == 64 ? (C + 63) / 64 : 1, nb);
   V a = mk(dy), b = mk(y), c = add ? mk(add) : V{}, d = mk(dz);
@@ -2735,6 +2762,88 @@ extern "C" int vm_relu_backward_bias_nhwc(const vm_tensor* dy, const vm_tensor* 
   return check_launch("relu_backward_bias fold");
 }
 
+// Exact 2x upsampling (oh = 2 ih, ow = 2 iw: scale 0.5, the UNet decoders' every resize): the TF-1 taps are known in
+// closed form — output o takes input o/2 with weight 1 when o is even; lo = (o-1)/2 and hi = min(lo + 1, in - 1) with
+// 0.5 each when odd (1.0 on the last input, where hi = lo) — so input i collects output rows 2i-1, 2i, 2i+1 (weights
+// 0.5, 1, 0.5 or 1 on the last) and the same columns.  Only resize_bwd_kernel's nonzero terms, in its order (rows
+// ascending, columns ascending within a row, row = sum of wx * v from 0, acc = sum of wy * row from 0), and every
+// product is exact (weights 0.5 / 1), so the sums are bit-identical to the windowed search's.  A lane takes 8 channels
+// of one input pixel: 9 16-byte (bf16) or 2x16-byte (f32) loads, one 16-byte / 2x16-byte store.
+template <typename TD, typename TX>
+__global__ __launch_bounds__(256) void resize2x_bwd_kernel8(V dy, TX* __restrict__ dx, int ih, int iw) {
+  const int C8 = dy.c / 8;
+  const long total = (long)dy.n * ih * iw * C8;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C8) * 8;
+    const long ip = i / C8;
+    const int ix = (int)(ip % iw);
+    const long t = ip / iw;
+    const int iy = (int)(t % ih);
+    const int n = (int)(t / ih);
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      const int oh = 2 * iy - 1 + r;
+      if (oh < 0) continue;
+      const float wy = r == 1 ? 1.f : (r == 2 && iy == ih - 1) ? 1.f : 0.5f;
+      float row[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        const int ow = 2 * ix - 1 + q;
+        if (ow < 0) continue;
+        const float wx = q == 1 ? 1.f : (q == 2 && ix == iw - 1) ? 1.f : 0.5f;
+        const long off = (((long)n * dy.h + oh) * dy.w + ow) * dy.cs + dy.coff + c;
+        float v[8];
+        if constexpr (sizeof(TD) == 4) {
+          const float4 a = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(dy.p) + off);
+          const float4 b = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(dy.p) + off + 4);
+          v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+        } else {
+          const uint4 u = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(dy.p) + off);
+          const uint32_t w4[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            v[2 * k] = __uint_as_float(w4[k] << 16);
+            v[2 * k + 1] = __uint_as_float(w4[k] & 0xffff0000u);
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) row[k] += wx * v[k];
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[k] += wy * row[k];
+    }
+    TX* o = dx + ip * dy.c + c;
+    if constexpr (sizeof(TX) == 4) {
+      *reinterpret_cast<float4*>(o) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+      *reinterpret_cast<float4*>(o + 4) = make_float4(acc[4], acc[5], acc[6], acc[7]);
+    } else {
+      uint32_t w4[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) w4[k] = (uint32_t)f2bf(acc[2 * k]) | ((uint32_t)f2bf(acc[2 * k + 1]) << 16);
+      *reinterpret_cast<uint4*>(o) = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+    }
+  }
+}
+
+// the exact-2x form when it applies (dy 2x dx, c % 8 == 0, 16-byte aligned); false = not launched
+static bool resize2x_bwd(const vm_tensor* dy, void* dx, bool dx_bf16, int ih, int iw, hipStream_t st) {
+  if (!g_resize_bwd_2x || dy->h != 2 * ih || dy->w != 2 * iw || dy->c % 8 || dy->cstride % 8 || dy->coff % 8 ||
+      reinterpret_cast<uintptr_t>(dy->ptr) % 16 || reinterpret_cast<uintptr_t>(dx) % 16)
+    return false;
+  const long n8 = (long)dy->n * ih * iw * (dy->c / 8);
+  const dim3 g(grid_for(n8, 256, 256 * 64)), b(256);
+  if (dy->dtype == VM_F32 && !dx_bf16)
+    hipLaunchKernelGGL((resize2x_bwd_kernel8<float, float>), g, b, 0, st, mk(dy), (float*)dx, ih, iw);
+  else if (dy->dtype == VM_F32)
+    hipLaunchKernelGGL((resize2x_bwd_kernel8<float, uint16_t>), g, b, 0, st, mk(dy), (uint16_t*)dx, ih, iw);
+  else if (!dx_bf16)
+    hipLaunchKernelGGL((resize2x_bwd_kernel8<uint16_t, float>), g, b, 0, st, mk(dy), (float*)dx, ih, iw);
+  else
+    hipLaunchKernelGGL((resize2x_bwd_kernel8<uint16_t, uint16_t>), g, b, 0, st, mk(dy), (uint16_t*)dx, ih, iw);
+  return true;
+}
+
 extern "C" int vm_resize_bilinear_tf1_backward(const vm_tensor* dy, float* dx, int ih, int iw, void* stream) {
   if (!ok_view(dy) || !dx || ih <= 0 || iw <= 0) return fail(VM_EINVAL, "resize_backward: bad argument");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
@@ -2742,6 +2851,7 @@ extern "C" int vm_resize_bilinear_tf1_backward(const vm_tensor* dy, float* dx, i
     return fail(VM_EUNSUPPORTED, "resize_backward: scale %dx%d -> %dx%d outside the upsampling range", ih, iw, dy->h,
                 dy->w);
   const float sy = (float)ih / (float)dy->h, sx = (float)iw / (float)dy->w;
+  if (resize2x_bwd(dy, dx, false, ih, iw, st)) return check_launch("resize_backward");
   if (dy->c % 4 == 0 && dy->cstride % 4 == 0 && dy->coff % 4 == 0 && reinterpret_cast<uintptr_t>(dy->ptr) % 16 == 0 &&
       reinterpret_cast<uintptr_t>(dx) % 16 == 0) {
     const long n4 = (long)dy->n * ih * iw * (dy->c / 4);
@@ -2755,6 +2865,35 @@ extern "C" int vm_resize_bilinear_tf1_backward(const vm_tensor* dy, float* dx, i
   }
   const long n = (long)dy->n * ih * iw * dy->c;
   hipLaunchKernelGGL(resize_bwd_kernel, dim3(grid_for(n, 256)), dim3(256), 0, st, mk(dy), dx, ih, iw, sy, sx);
+  return check_launch("resize_backward");
+}
+
+// dx as a view: f32 as above, or dense bf16 with c % 4 == 0 and 8-byte aligned (the bf16 training path's relu
+// gradients: the relu backward rounds dz to bf16 anyway, so a bf16 dx changes no dz where no `add` joins it)
+extern "C" int vm_resize_bilinear_tf1_backward_nhwc(const vm_tensor* dy, vm_tensor* dx, void* stream) {
+  if (!ok_view(dy) || !ok_view(dx) || dx->n != dy->n || dx->c != dy->c)
+    return fail(VM_EINVAL, "resize_backward: dx [n,ih,iw,c] with dy's n and c");
+  if (dx->cstride != dx->c || dx->coff != 0) return fail(VM_EUNSUPPORTED, "resize_backward: dx must be dense");
+  if (dx->dtype == VM_F32) return vm_resize_bilinear_tf1_backward(dy, reinterpret_cast<float*>(dx->ptr), dx->h, dx->w,
+                                                                  stream);
+  const int ih = dx->h, iw = dx->w;
+  if (dy->h > 4 * ih || dy->w > 4 * iw || ih > 2 * dy->h || iw > 2 * dy->w)
+    return fail(VM_EUNSUPPORTED, "resize_backward: scale %dx%d -> %dx%d outside the upsampling range", ih, iw, dy->h,
+                dy->w);
+  if (dy->c % 4 || dy->cstride % 4 || dy->coff % 4 || reinterpret_cast<uintptr_t>(dy->ptr) % 16 ||
+      reinterpret_cast<uintptr_t>(dx->ptr) % 8)
+    return fail(VM_EUNSUPPORTED, "resize_backward: bf16 dx needs c %% 4 == 0 and aligned views");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (resize2x_bwd(dy, dx->ptr, true, ih, iw, st)) return check_launch("resize_backward");
+  const float sy = (float)ih / (float)dy->h, sx = (float)iw / (float)dy->w;
+  const long n4 = (long)dy->n * ih * iw * (dy->c / 4);
+  uint16_t* d = reinterpret_cast<uint16_t*>(dx->ptr);
+  if (dy->dtype == VM_F32)
+    hipLaunchKernelGGL((resize_bwd_kernel4<float, uint16_t>), dim3(grid_for(n4, 256)), dim3(256), 0, st, mk(dy), d, ih,
+                       iw, sy, sx);
+  else
+    hipLaunchKernelGGL((resize_bwd_kernel4<uint16_t, uint16_t>), dim3(grid_for(n4, 256)), dim3(256), 0, st, mk(dy), d,
+                       ih, iw, sy, sx);
   return check_launch("resize_backward");
 }
 

@@ -161,6 +161,7 @@ SIGNATURES = [
     ("vm_relu_backward_bias_workspace_bytes", c_size_t, [c_int]),
     ("vm_relu_backward_bias_nhwc", c_int, [P, P, P, P, c_void_p, c_void_p, c_void_p]),
     ("vm_resize_bilinear_tf1_backward", c_int, [P, c_void_p, c_int, c_int, c_void_p]),
+    ("vm_resize_bilinear_tf1_backward_nhwc", c_int, [P, P, c_void_p]),
     ("vm_conv3x3_wgrad_workspace_bytes", c_size_t, [c_int, c_int, c_int, c_int, c_int]),
     ("vm_conv3x3_wgrad_nhwc", c_int, [P, P, c_void_p, c_void_p, c_void_p]),
     ("vm_conv3x3_workspace_bytes", c_size_t, [P, c_int, c_int]),

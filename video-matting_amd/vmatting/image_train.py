@@ -113,18 +113,19 @@ class ImageTrainer(TrainerBase):
         # D: the data gradients the dgrad convs write.  The bf16 path keeps them bf16 (bf16_dgrad): their only
         # readers round to bf16 anyway (the MFMA convs' operands) or widen exactly (the relu / resize adjoints), so
         # the convs write half the bytes and the upconv gradient needs no f32 -> bf16 convert.  The resize adjoint's
-        # outputs (dc23, dc34, dc44, dc52) stay f32: it accumulates.
+        # outputs (dc23, dc34, dc44, dc52) too: it sums in f32 and rounds once, and their only reader is a relu
+        # backward with no `add`, whose bf16 dz = mask * bf16(dy) is then the same value either way.
         D = B if bf16 and self.bf16_dgrad else F
         g = {"dlogit": F(0, 1), "dlog8": F(0, 8), "loss": torch.zeros(3, dtype=torch.float32, device=dev),
              "in6": torch.empty((n, h, w, 6), dtype=torch.float32, device=dev),
              "dcat1": D(0, 128), "dr4": D(0, 128), "dz12": Z(0, 64), "dc11": D(0, 64), "dz11": Z(0, 64),
-             "dcat2": D(1, 256), "dc23": F(1, 128), "dz23": Z(1, 128), "dr3": D(1, 256), "dz22": Z(1, 128),
+             "dcat2": D(1, 256), "dc23": D(1, 128), "dz23": Z(1, 128), "dr3": D(1, 256), "dz22": Z(1, 128),
              "dc21": D(1, 128), "dz21": Z(1, 128), "dp1": D(1, 64),
-             "dcat3": D(2, 512), "dc34": F(2, 256), "dz34": Z(2, 256), "dr2": D(2, 512), "dz33": Z(2, 256),
+             "dcat3": D(2, 512), "dc34": D(2, 256), "dz34": Z(2, 256), "dr2": D(2, 512), "dz33": Z(2, 256),
              "dc32": D(2, 256), "dz32": Z(2, 256), "dc31": D(2, 256), "dz31": Z(2, 256), "dp2": D(2, 128),
-             "dcat4": D(3, 1024), "dc44": F(3, 512), "dz44": Z(3, 512), "dr1": D(3, 512), "dz43": Z(3, 512),
+             "dcat4": D(3, 1024), "dc44": D(3, 512), "dz44": Z(3, 512), "dr1": D(3, 512), "dz43": Z(3, 512),
              "dc42": D(3, 512), "dz42": Z(3, 512), "dc41": D(3, 512), "dz41": Z(3, 512), "dp3": D(3, 256),
-             "dc52": F(4, 512), "dz52": Z(4, 512), "dc51": D(4, 512), "dz51": Z(4, 512), "dp4": D(4, 512)}
+             "dc52": D(4, 512), "dz52": Z(4, 512), "dc51": D(4, 512), "dz51": Z(4, 512), "dp4": D(4, 512)}
         if bf16:
             hb = {"dlog16": (0, 32), "dz12": (0, 64), "dz11": (0, 64),
                   "dz23": (1, 128), "dz22": (1, 128), "dz21": (1, 128),

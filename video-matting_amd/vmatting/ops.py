@@ -884,11 +884,17 @@ def relu_backward_bias(dy, y, dz, dbias, add=None):
 
 
 def resize_backward(dy, dx):
-    """Adjoint of resize_bilinear: dy [n,oh,ow,c] -> dx contiguous f32 [n,ih,iw,c] (overwritten)."""
-    _f32(dx)
+    """Adjoint of resize_bilinear: dy [n,oh,ow,c] -> dx contiguous f32 (or bf16, c % 4 == 0) [n,ih,iw,c]
+    (overwritten)."""
     if dx.shape[0] != dy.shape[0] or dx.shape[3] != dy.shape[3]:
         raise ValueError("resize_backward: batch/channel mismatch")
     dv = nhwc(dy)
+    if dx.dtype == torch.bfloat16:
+        xv = nhwc(dx)
+        check(lib().vm_resize_bilinear_tf1_backward_nhwc(ctypes.byref(dv), ctypes.byref(xv), stream_handle()),
+              "resize_backward")
+        return dx
+    _f32(dx)
     check(lib().vm_resize_bilinear_tf1_backward(ctypes.byref(dv), _ptr(dx), dx.shape[1], dx.shape[2],
                                                 stream_handle()), "resize_backward")
     return dx
