@@ -512,7 +512,7 @@ def train_flops(n, h, w):
 
 
 def train_bench(dev, steps, warmup, world, rank, threads, cpu=True, n=8, size=320, dtype="bf16", graph=False,
-                streams=3):
+                streams=3, wgrad_stream=True):
     """BASELINE config 5: one train.py video_procedure iteration per step (train.py:288-343) — batch of 8 320x320
     samples per GPU (params.py:8-9) resident in HBM: 3 VGG16 towers + UNetSimple (batch-statistics BN) forward,
     loss, backward through the trainable layers, one RCCL all-reduce of the gradients (DDP), TF-Adam, re-pack.
@@ -530,7 +530,7 @@ def train_bench(dev, steps, warmup, world, rank, threads, cpu=True, n=8, size=32
     T = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.float32)).to(dev)  # noqa: E731
     cmp_d, bg_d, warped_d, gt_d, fg_d = T(cmp), T(bg - mean), T(warped), T(gt), T(fg)
     np.random.seed(1)
-    trn = VideoTrainer(synthetic_vgg16(0), dtype, dev, streams=streams)
+    trn = VideoTrainer(synthetic_vgg16(0), dtype, dev, streams=streams, wgrad_stream=wgrad_stream)
     # eager launches (the select chains overlap the decoder on side streams); graph: forward + loss and backward
     # replayed from HIP graphs (VideoTrainer.capture), DDP exchange + Adam eager
     g = trn.capture(cmp_d, bg_d, warped_d, gt_d, fg_d) if graph else None
@@ -571,8 +571,8 @@ def train_bench(dev, steps, warmup, world, rank, threads, cpu=True, n=8, size=32
     rec = {"workload": "train.py video_procedure step (config 5): %d x %dx%d per GPU, 3 VGG16 towers + UNetSimple "
                        "fwd/bwd, loss, DDP all-reduce, TF-Adam" % (n, size, size),
            "dtype": dtype + " forward, f32 gradients/optimizer", "n_gpus": world,
-           "launch": "hip-graph replay of forward+loss and of backward, eager all-reduce + Adam + re-pack" if graph
-                     else "eager",
+           "launch": ("hip-graph replay of forward+loss and of backward, eager all-reduce + Adam + re-pack" if graph
+                      else "eager") + ("; filter gradients on a side stream" if streams else ""),
            "samples_per_s": round(n * world / wall, 1), "ms_per_step": round(1000 * wall, 3),
            "device_ms": {"forward_loss": round(ph[0], 3), "backward": round(ph[1], 3),
                          "allreduce_adam_repack": round(ph[2], 3)},
@@ -704,13 +704,16 @@ def train_small_bench(dev, steps, warmup, world, rank, threads, cpu=True, n=8, s
     return rec
 
 
-def train_image_bench(dev, steps, warmup, world, rank, threads, cpu=True, n=8, size=320, dtype="bf16", graph=True):
+def train_image_bench(dev, steps, warmup, world, rank, threads, cpu=True, n=8, size=320, dtype="bf16", graph=False,
+                      streams=1):
     """train.py's training_procedure step (train.py:37-109 with train()'s graph, :112-135):
     unet.UNetImage(x = [cmp, bg]) forward (the 20 convs, pools, TF-1 resizes, concats), the loss, backward through
     EVERY variable (VGG filters and biases included: wide MFMA filter gradients, data gradients on the forward conv
     kernels over flipped filters, pool / resize adjoints), DDP all-reduce, TF-Adam at lr 1e-5, re-pack — batch 8 x
-    320^2 per GPU (params.py BATCH_SIZE / INPUT_SIZE) resident in HBM.  Forward + loss and backward replayed from
-    HIP graphs; roofline: the step's algorithmic conv FLOPs over its device time at the bf16 dense MFMA peak."""
+    320^2 per GPU (params.py BATCH_SIZE / INPUT_SIZE) resident in HBM.  Eager launches with the filter gradients on
+    a side stream beside the data-gradient chain (6.0 ms against 6.5 on one stream; a HIP-graph replay runs the
+    captured fork's branches serially, 6.7 — so ``graph`` captures without the side stream); roofline: the step's
+    algorithmic conv FLOPs over its device time at the bf16 dense MFMA peak."""
     from vmatting.image_train import ImageTrainer
     from vmatting.weights import synthetic_vgg16 as svgg
     rs = np.random.RandomState(300 + rank)
@@ -724,7 +727,7 @@ def train_image_bench(dev, steps, warmup, world, rank, threads, cpu=True, n=8, s
     T = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.float32)).to(dev)  # noqa: E731
     cmp_d, bg_d, gt_d, fg_d = T(cmp), T(bg - mean), T(gt), T(fg)
     np.random.seed(4)
-    trn = ImageTrainer(svgg(0), dtype, dev)
+    trn = ImageTrainer(svgg(0), dtype, dev, streams=streams)
     g = trn.capture(cmp_d, bg_d, gt_d, fg_d) if graph else None
     for _ in range(warmup):
         if g is not None:
@@ -1171,6 +1174,12 @@ def main():
                     help="config-5 chained record without the producer-stream overlap (augment, loader, step in turn)")
     ap.add_argument("--train-streams", type=int, default=3,
                     help="side streams of the config-5 trainer's select chains (0: one stream, for serial profiles)")
+    ap.add_argument("--train-wgrad-stream", type=int, default=1,
+                    help="config-5 trainer: 1 = the decoder chain's filter gradients on their own side stream")
+    ap.add_argument("--image-graph", action="store_true",
+                    help="train_image record from HIP-graph replays (one stream) instead of eager launches")
+    ap.add_argument("--image-streams", type=int, default=1,
+                    help="train_image: 1 = filter gradients on a side stream beside the data-gradient chain, 0 = one")
     ap.add_argument("--only", choices=["train", "train_chain", "train_small", "train_image", "temporal", "augment",
                                        "loader"],
                     help="profiling passes: run just this record (rank 0 / N=1) and print it")
@@ -1215,14 +1224,15 @@ def main():
     if args.only:  # one record alone (rocprofv3 passes per record: tools/prof_bench.sh)
         if args.only == "train":
             rec = train_bench(dev, args.steps, args.warmup, world, rank, threads, cpu=False, graph=args.train_graph,
-                              streams=args.train_streams)
+                              streams=args.train_streams, wgrad_stream=bool(args.train_wgrad_stream))
         elif args.only == "train_chain":
             rec = train_chain_bench(dev, args.steps, args.warmup, graph=args.train_graph, overlap=not args.chain_serial,
                                     prio=args.chain_prio)
         elif args.only == "train_small":
             rec = train_small_bench(dev, args.steps, args.warmup, world, rank, threads, cpu=False)
         elif args.only == "train_image":
-            rec = train_image_bench(dev, args.steps, args.warmup, world, rank, threads, cpu=False)
+            rec = train_image_bench(dev, args.steps, args.warmup, world, rank, threads, cpu=False,
+                                    graph=args.image_graph, streams=args.image_streams)
         elif args.only == "augment":
             rec = augment_bench(dev, args.steps, threads, cpu=False)
         elif args.only == "loader":
@@ -1295,14 +1305,16 @@ def main():
     train = None
     if not args.no_train:  # every rank: the DDP all-reduce is part of the step
         train = train_bench(dev, max(args.steps // 4, 10), 3, world, rank, threads, cpu=not args.no_cpu_baseline,
-                            graph=args.train_graph)
+                            graph=args.train_graph, streams=args.train_streams,
+                            wgrad_stream=bool(args.train_wgrad_stream))
         if world == 1:
             train["chained"] = train_chain_bench(dev, 5, 2, graph=args.train_graph, overlap=not args.chain_serial,
                                                  prio=args.chain_prio)
         train_small = train_small_bench(dev, max(args.steps // 4, 10), 3, world, rank, threads,
                                         cpu=not args.no_cpu_baseline)
         train_image = train_image_bench(dev, max(args.steps // 4, 10), 3, world, rank, threads,
-                                        cpu=not args.no_cpu_baseline)
+                                        cpu=not args.no_cpu_baseline, graph=args.image_graph,
+                                        streams=args.image_streams)
 
     roofline = conv_roofline(prof, args) if prof else None
     if rank == 0:

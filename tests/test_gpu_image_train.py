@@ -170,6 +170,22 @@ def test_image_graph_step_equals_eager(dtype):
     assert torch.equal(eager.flat, graphed.flat)
 
 
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_image_side_stream_step_equals_single_stream(dtype):
+    """The filter gradients on the side stream (streams=1, the default) beside the data-gradient chain: two steps
+    leave bit-identical variables and losses to the one-stream trainer (same kernels; per-stream workspaces)."""
+    params = _params()
+    b1, b2 = _batch(2, 48, 64, seed=5), _batch(2, 48, 64, seed=6)
+    out = []
+    for streams in (0, 1):
+        trn = _trainer(params, dtype, lr=1e-3, streams=streams)
+        assert (trn._side is not None) == bool(streams)
+        out.append(([H(trn.step(*b)) for b in (b1, b2)], trn.flat))
+    torch.cuda.synchronize()
+    assert all(np.array_equal(a, b) for a, b in zip(out[0][0], out[1][0]))
+    assert torch.equal(out[0][1], out[1][1])
+
+
 def _ddp_worker(rank, world, port, q):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))

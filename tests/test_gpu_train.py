@@ -994,6 +994,7 @@ def test_train_graph_step_equals_eager(dtype):
     # the select chains on side streams (default) vs everything on one stream: the same kernels, bit-identical
     single = VideoTrainer(vgg, dtype, DEV, params=params, streams=0)
     assert not single._side and eager._side
+    assert single._wside is None and eager._wside is not None  # the decoder chain's filter gradients too
     ls = [H(single.step(*b)) for b in (b1, b2)]
     torch.cuda.synchronize()
     assert all(np.array_equal(a, b) for a, b in zip(le, ls)), (le, ls)

@@ -146,7 +146,8 @@ class VideoTrainer(TrainerBase):
     """train.video_procedure's iteration on device (also simple_procedure's: pass diff = cmp - bg as ``warped``)."""
 
     def __init__(self, vgg16_npy_path=None, dtype="fp32", device="cuda", params=None, bn=None, lr=1e-3,
-                 beta1=0.9, beta2=0.999, epsilon=1e-8, sync_bn=False, streams=3, stream_priority=0):
+                 beta1=0.9, beta2=0.999, epsilon=1e-8, sync_bn=False, streams=3, stream_priority=0,
+                 wgrad_stream=True):
         self.vgg = vgg16_npy_path if isinstance(vgg16_npy_path, Vgg16) else Vgg16(vgg16_npy_path, dtype, device)
         self.model = UNetSimple(self.vgg, True, dtype, device, params)
         self.device = self.model.device
@@ -161,6 +162,10 @@ class VideoTrainer(TrainerBase):
         dev_ = torch.device(device)
         self._side = [] if self.sync_bn or streams < 1 or dev_.type != "cuda" else \
             [torch.cuda.Stream(device=dev_, priority=stream_priority) for _ in range(int(streams))]
+        # the decoder chain's own filter gradients (output, conv*, upconv*) are leaves too: with side streams they run
+        # on one more, beside the chain's BN backward -> data-gradient convs, joined before the update
+        self._wside = torch.cuda.Stream(device=dev_, priority=stream_priority) if self._side and wgrad_stream \
+            else None
         self._capture_origin = None  # the stream a TrainGraph capture began on (see _check_capture_fork)
         dev = self.device
         # move the freshly drawn variables into the flat buffer and alias every consumer onto it
@@ -354,13 +359,24 @@ class VideoTrainer(TrainerBase):
 
 
     # ------------------------------------------------------------------------------------------- backward
+    def _chain_wgrad(self, x_in, dz, dw):
+        if self._wside is None:
+            ops.conv_wgrad(x_in, dz, dw, mfma=self._mfma_wgrad)
+            return
+        self._wside.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(self._wside):
+            ops.conv_wgrad(x_in, dz, dw, mfma=self._mfma_wgrad)
+
     def _conv_backward(self, scope, x_in, dy, mask, tb, dgrad_out=None):
         """BN(+relu) backward into dz, then bias / filter gradients, optionally the data gradient of x_in."""
         z, dz, (mean, var) = tb["z_" + scope], tb["dz_" + scope], tb["st_" + scope]
         g16 = tb["g16_" + scope] if dgrad_out is not None and scope in self.dconv16 else None
         self._bn_backward(z, dy, mask, mean, var, scope, dz, dx2=None if g16 is None else g16[..., :dz.shape[-1]],
                           dbias=self.G[scope, "b"])
-        ops.conv_wgrad(x_in, dz, self.G[scope, "w"], mfma=self._mfma_wgrad)
+        if dgrad_out is not None:  # the decoder chain (the select chains, on their side streams, pass None)
+            self._chain_wgrad(x_in, dz, self.G[scope, "w"])
+        else:
+            ops.conv_wgrad(x_in, dz, self.G[scope, "w"], mfma=self._mfma_wgrad)
         if dgrad_out is not None:
             if g16 is not None:
                 pc = self.dconv16[scope]
@@ -399,15 +415,15 @@ class VideoTrainer(TrainerBase):
                 else:
                     self._conv_backward(s, self._src(b, src), gsel[..., off:off + co], None, tb)
                 off += co
-            ops.conv_wgrad(b[RBUF[up]], du, self.G[up, "w"], mfma=self._mfma_wgrad)
+            self._chain_wgrad(b[RBUF[up]], du, self.G[up, "w"])
             if up in DGRAD:
                 if g16 is not None:
                     ops.conv3x3(g16, self.dconv16[up], "none", out=tb["dr_" + up], affine=False)
                 else:
                     ops.conv3x3(du, self.dconv[up], "none", out=tb["dr_" + up], affine=False)
                 dout = ops.resize_backward(tb["dr_" + up], tb["dprev_" + up])
-        for st in self._side:  # every gradient is in place before the all-reduce / Adam that read them
-            main.wait_stream(st)
+        for st in self._side + ([self._wside] if self._wside is not None else []):
+            main.wait_stream(st)  # every gradient is in place before the all-reduce / Adam that read them
 
     # ------------------------------------------------------------------------------------------- update
 
