@@ -149,6 +149,13 @@ def test_conv_wgrad_wide_pipelined_bit_identical(cin, cout, n, h, w, dyf32):
         _lib.set_option("wgrad_wide_pipe", 1)
         _lib.set_option("wgrad_wide_target", 0)
     assert torch.equal(out[256, 0], out[256, 1])
+    try:  # the pipelined kernel with one LDS image buffer (two barriers per tile) against the default two
+        _lib.set_option("wgrad_wide_dbuf", 0)
+        dw = torch.zeros((3, 3, cin, cout), dtype=torch.float32, device=DEV)
+        ops.conv_wgrad(xd, d, dw, mfma=True)
+    finally:
+        _lib.set_option("wgrad_wide_dbuf", 1)
+    assert torch.equal(dw, out[0, 1])
     a, b = H(out[0, 0]), H(out[0, 1])
     assert np.abs(a - b).max() <= 1e-5 * max(1.0, float(np.abs(a).max())), np.abs(a - b).max()
 

@@ -1729,6 +1729,7 @@ struct WwArgs {
   int tiles_h, tiles_w;
   long ntiles;
   int gx, ncin, ncout;
+  int dbuf;           // PIPE: two LDS image buffers, tile t in buffer t & 1 (one barrier per tile)
 };
 
 constexpr int WW_TH = 4;
@@ -1872,8 +1873,14 @@ __global__ __launch_bounds__(256, PIPE ? 1 : 2) void wgrad_wide_kernel(WwArgs a)
     for (int o = 0; o < 4; ++o)
 #pragma unroll
       for (int k = 0; k < 16; ++k) bdy[o][k] = (k == 0 || k == 4) ? wm_base<128>(k + u, o, p) - 128 * k : 0;
+    // dbuf: tile t's images go to buffer t & 1.  Buffer (t + 1) & 1 was last read by tile t - 1's MFMAs, which every
+    // wave finished before the barrier after tile t's commit, so the trailing barrier is not needed: a wave that is
+    // done with tile t commits tile t + 1 while the others still compute.
+    const int bstride = a.dbuf ? XBYTES + DPIX * 128 : 0;
     if (t_beg < t_end) issue(t_beg);
     for (int tile = t_beg; tile < t_end; ++tile) {
+      ximg = smem + ((tile - t_beg) & 1) * bstride;
+      dimg = ximg + XBYTES;
       commit();
       __syncthreads();
       if (tile + 1 < t_end) issue(tile + 1);
@@ -1906,7 +1913,7 @@ __global__ __launch_bounds__(256, PIPE ? 1 : 2) void wgrad_wide_kernel(WwArgs a)
           __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
         });
       });
-      __syncthreads();
+      if (!a.dbuf) __syncthreads();
     }
   } else {
   if (t_beg < t_end) issue(t_beg);
@@ -2242,6 +2249,7 @@ static bool wgrad_dma_ok(const WgArgs& a, int cib) {
 }
 
 static long g_wgrad_wide_pipe = 1;  // vm_set_option "wgrad_wide_pipe": 0 = the plain-loop kernel at 2 blocks per CU (A/B)
+static long g_wgrad_wide_dbuf = 1;  // vm_set_option "wgrad_wide_dbuf": 0 = one LDS image buffer, two barriers per tile
 static long g_wgrad_wide_target = 0;  // vm_set_option "wgrad_wide_target": > 0 overrides the K-split's block target
 
 static long g_wgrad_dma_cfg = 0;  // vm_set_option "wgrad_dma_cfg" (A/B): 0 auto, 1 = 8-row tiles, 2 = 4 rows x 6 slots
@@ -2332,6 +2340,10 @@ int train_set_option(const char* key, long value) {
     trn::g_wgrad_wide_target = value;
     return 1;
   }
+  if (!strcmp(key, "wgrad_wide_dbuf")) {
+    trn::g_wgrad_wide_dbuf = value;
+    return 1;
+  }
   if (!strcmp(key, "wgrad_dma_cfg")) {
     trn::g_wgrad_dma_cfg = value;
     return 1;
@@ -2414,17 +2426,19 @@ static int launch_wgrad_wide(const vm_tensor* x, const vm_tensor* dy, float* dw,
   a.gx = (int)wgrad_wide_gx(a.n, a.h, a.w, a.cin, a.cout, false, target);
   const long nb = (long)a.gx * a.ncin * a.ncout;
   if (nb > 0x7fffffffL) return fail(VM_EUNSUPPORTED, "conv_wgrad: grid too large");
-  constexpr int lds = wgrad_wide_lds<WW_TH>();
+  a.dbuf = pipe && g_wgrad_wide_dbuf ? 1 : 0;
+  const int lds = wgrad_wide_lds<WW_TH>() * (a.dbuf ? 2 : 1);
+  constexpr int lds_max = 2 * wgrad_wide_lds<WW_TH>();
   if (f32) {
     static int attr = -1;
     int dev = 0;
     (void)hipGetDevice(&dev);
     if (attr != dev) {
       hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_wide_kernel<WW_TH, true>),
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, lds_max);
       if (e == hipSuccess)
         e = hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_wide_kernel<WW_TH, true, false>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+                                hipFuncAttributeMaxDynamicSharedMemorySize, lds_max);
       if (e != hipSuccess) return fail(VM_EHIP, "wgrad_wide setup: %s", hipGetErrorString(e));
       attr = dev;
     }
@@ -2436,10 +2450,10 @@ static int launch_wgrad_wide(const vm_tensor* x, const vm_tensor* dy, float* dw,
     (void)hipGetDevice(&dev);
     if (attr != dev) {
       hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_wide_kernel<WW_TH, false>),
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, lds_max);
       if (e == hipSuccess)
         e = hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_wide_kernel<WW_TH, false, false>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+                                hipFuncAttributeMaxDynamicSharedMemorySize, lds_max);
       if (e != hipSuccess) return fail(VM_EHIP, "wgrad_wide setup: %s", hipGetErrorString(e));
       attr = dev;
     }
