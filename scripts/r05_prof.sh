@@ -8,7 +8,7 @@ for rec in train train_image train_chain; do
   timeout -k 10 300 python -u bench.py --only $rec --steps $steps --warmup 5 > gpurun_out/prof5/$rec.log 2>&1 || { tail -20 gpurun_out/prof5/$rec.log; exit 1; }
   tail -n 1 gpurun_out/prof5/$rec.log > gpurun_out/prof5/r05_$rec.json
   echo "$rec: $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/prof5/r05_$rec.json | head -1)"
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof5/rp_$rec -o run -- python bench.py --only $rec --steps 10 --warmup 3 > gpurun_out/prof5/rp_$rec.log 2>&1 || { tail -20 gpurun_out/prof5/rp_$rec.log; exit 1; }
-  cp "$(find gpurun_out/prof5/rp_$rec -name '*kernel_stats.csv' | head -n 1)" gpurun_out/prof5/r05_${rec}_kernel_stats.csv
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof5/rp_$rec -o run -- python bench.py --only $rec --steps 10 --warmup 3 > gpurun_out/prof5/rp_$rec.log 2>&1 || { tail -20 gpurun_out/prof5/rp_$rec.log; exit 1; }
+  f=$(find gpurun_out/prof5/rp_$rec -name '*kernel_stats.csv' | head -n 1); [ -n "$f" ] && cp "$f" gpurun_out/prof5/r05_${rec}_kernel_stats.csv
 done
 ls gpurun_out/prof5
