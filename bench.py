@@ -572,7 +572,9 @@ def train_bench(dev, steps, warmup, world, rank, threads, cpu=True, n=8, size=32
                        "fwd/bwd, loss, DDP all-reduce, TF-Adam" % (n, size, size),
            "dtype": dtype + " forward, f32 gradients/optimizer", "n_gpus": world,
            "launch": ("hip-graph replay of forward+loss and of backward, eager all-reduce + Adam + re-pack" if graph
-                      else "eager") + ("; filter gradients on a side stream" if streams else ""),
+                      else "eager") + ("; select chains on %d side streams%s" % (
+                          streams, ", decoder filter gradients on one more" if wgrad_stream else "") if streams
+                                       else ""),
            "samples_per_s": round(n * world / wall, 1), "ms_per_step": round(1000 * wall, 3),
            "device_ms": {"forward_loss": round(ph[0], 3), "backward": round(ph[1], 3),
                          "allreduce_adam_repack": round(ph[2], 3)},
@@ -676,8 +678,8 @@ def train_small_bench(dev, steps, warmup, world, rank, threads, cpu=True, n=8, s
     rec = {"workload": "small_train.py step: %d x %dx%d per GPU, UNetSmall(concat(cmp, bg)) fwd/bwd over all "
                        "variables, loss, DDP all-reduce, TF-Adam" % (n, size, size),
            "dtype": dtype + " forward, f32 gradients/optimizer", "n_gpus": world,
-           "launch": "hip-graph replay of forward+loss and of backward, eager all-reduce + Adam + re-pack" if graph
-                     else "eager",
+           "launch": "hip-graph replay of forward+loss and of backward (one stream), eager all-reduce + Adam + "
+                     "re-pack" if graph else "eager" + ("; filter gradients on a side stream" if streams else ""),
            "samples_per_s": round(n * world / wall, 1), "ms_per_step": round(1000 * wall, 4),
            "device_ms": {"forward_loss": round(ph[0], 4), "backward": round(ph[1], 4),
                          "allreduce_adam_repack": round(ph[2], 4)},
@@ -1312,7 +1314,7 @@ def main():
                                                  prio=args.chain_prio)
         train_small = train_small_bench(dev, max(args.steps // 4, 10), 3, world, rank, threads,
                                         cpu=not args.no_cpu_baseline)
-        train_image = train_image_bench(dev, max(args.steps // 4, 10), 3, world, rank, threads,
+        train_image = train_image_bench(dev, max(args.steps // 4, 10), 5, world, rank, threads,
                                         cpu=not args.no_cpu_baseline, graph=args.image_graph,
                                         streams=args.image_streams)
 
