@@ -160,6 +160,29 @@ def test_conv_wgrad_wide_pipelined_bit_identical(cin, cout, n, h, w, dyf32):
     assert np.abs(a - b).max() <= 1e-5 * max(1.0, float(np.abs(a).max())), np.abs(a - b).max()
 
 
+@pytest.mark.parametrize("cin,cout,n,h,w", [(6, 64, 8, 40, 48), (16, 128, 2, 33, 70), (3, 64, 2, 9, 40)])
+def test_wgrad_wide_channel_split_bit_identical(cin, cout, n, h, w):
+    """cin <= 16 (UNetImage's 6-channel conv1_1): the output-channel wave split (wgrad_wide_cs 1) runs each
+    accumulator's MFMAs on the same fragments in the same order as the default split: bit-identical."""
+    from vmatting import _lib, ops
+    rs = np.random.RandomState(cin * 5 + h)
+    x = rs.normal(size=(n, h, w, (cin + 7) // 8 * 8)).astype(np.float32)
+    dy = rs.normal(size=(n, h, w, cout)).astype(np.float32)
+    xd = T(x, torch.bfloat16)[..., :cin]
+    d = T(dy, torch.bfloat16)
+    out = []
+    try:
+        for cs in (0, 1):
+            _lib.set_option("wgrad_wide_cs", cs)
+            dw = torch.zeros((3, 3, cin, cout), dtype=torch.float32, device=DEV)
+            ops.conv_wgrad(xd, d, dw, mfma=True)
+            out.append(dw)
+    finally:
+        _lib.set_option("wgrad_wide_cs", 1)
+    assert torch.equal(out[0], out[1])
+    assert float(out[1].abs().max()) > 0
+
+
 def test_conv_wgrad_wide_rejects_split_sources():
     from vmatting import ops
     x = torch.zeros((2, 4, 4, 16), dtype=torch.bfloat16, device=DEV)

@@ -1758,7 +1758,11 @@ __device__ __forceinline__ bf16x8 wm_frag_b(const char* img, const int (&b)[16])
 }
 
 // PIPE: one block per CU (the unrolled rows, the bases and the next tile's staging registers need > 256 VGPRs)
-template <int TH, bool DYF32, bool PIPE = true>
+// CS (cin <= 16, plain loop): the 4 waves split the OUTPUT channels instead — wave w takes ci 0..15 x co 16w..16w+15
+// x 9 taps — so UNetImage's 6-channel conv1_1 does not leave 3 of 4 waves multiplying zero input channels.  Each
+// accumulator (ci piece 0, co piece w) sees the same MFMAs on the same fragments in the same order as wave 0's
+// accumulator o = w in the default split: bit-identical.
+template <int TH, bool DYF32, bool PIPE = true, bool CS = false>
 __global__ __launch_bounds__(256, PIPE ? 1 : 2) void wgrad_wide_kernel(WwArgs a) {  // A/B (scripts/build_variant.sh):
                                                                            // (256,2) 2.58 ms vs (256,1) 2.87 ms
   constexpr int XPIX = wm_ppix<TH>(), DPIX = TH * WM_TW;
@@ -1923,6 +1927,16 @@ __global__ __launch_bounds__(256, PIPE ? 1 : 2) void wgrad_wide_kernel(WwArgs a)
     if (tile + 1 < t_end) issue(tile + 1);
 #pragma unroll 1
     for (int row = 0; row < TH; ++row) {
+      if constexpr (CS) {
+        const bf16x8 bdw = wm_frag<128>(dimg, row * WM_TW + 8 * g, wave, lane);
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+          const int r0 = (row + t / 3) * WM_PW + t % 3 + 8 * g;
+          const bf16x8 ax = wm_frag<128>(ximg, r0, 0, lane);
+          acc[t][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ax, bdw, acc[t][0], 0, 0, 0);
+        }
+        continue;
+      }
       bf16x8 bd[4];
 #pragma unroll
       for (int o = 0; o < 4; ++o) bd[o] = wm_frag<128>(dimg, row * WM_TW + 8 * g, o, lane);
@@ -1941,6 +1955,18 @@ __global__ __launch_bounds__(256, PIPE ? 1 : 2) void wgrad_wide_kernel(WwArgs a)
   // this block's partial of its 64 x 64 x 9 tile (lanes: co = lane & 15, ci = 4 * (lane >> 4) + j)
   float* part = a.part + (long)kx * 9 * a.cin * a.cout;
   const int co_l = lane & 15, ci_l = 4 * g;
+  if constexpr (CS) {
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int co = o0 + 16 * wave + co_l;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int ci = c0 + ci_l + j;
+        if (ci < a.cin) part[((long)t * a.cin + ci) * a.cout + co] = acc[t][0][j];
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int t = 0; t < 9; ++t)
 #pragma unroll
@@ -2249,6 +2275,7 @@ static bool wgrad_dma_ok(const WgArgs& a, int cib) {
 }
 
 static long g_wgrad_wide_pipe = 1;  // vm_set_option "wgrad_wide_pipe": 0 = the plain-loop kernel at 2 blocks per CU (A/B)
+static long g_wgrad_wide_cs = 1;  // vm_set_option "wgrad_wide_cs": 0 = the input-channel wave split for cin <= 16 too
 static long g_wgrad_wide_dbuf = 1;  // vm_set_option "wgrad_wide_dbuf": 0 = one LDS image buffer, two barriers per tile
 static long g_wgrad_wide_target = 0;  // vm_set_option "wgrad_wide_target": > 0 overrides the K-split's block target
 
@@ -2338,6 +2365,10 @@ int train_set_option(const char* key, long value) {
   }
   if (!strcmp(key, "wgrad_wide_target")) {  // (<= WW_TARGET_BLOCKS: the workspace query's bound)
     trn::g_wgrad_wide_target = value;
+    return 1;
+  }
+  if (!strcmp(key, "wgrad_wide_cs")) {
+    trn::g_wgrad_wide_cs = value;
     return 1;
   }
   if (!strcmp(key, "wgrad_wide_dbuf")) {
@@ -2444,6 +2475,18 @@ static int launch_wgrad_wide(const vm_tensor* x, const vm_tensor* dy, float* dw,
     }
     if (pipe) hipLaunchKernelGGL((wgrad_wide_kernel<WW_TH, true>), dim3((unsigned)nb), dim3(256), lds, st, a);
     else hipLaunchKernelGGL((wgrad_wide_kernel<WW_TH, true, false>), dim3((unsigned)nb), dim3(256), lds, st, a);
+  } else if (a.cin <= 16 && g_wgrad_wide_cs) {  // (the 6-channel conv1_1: output-channel wave split)
+    static int attr = -1;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    constexpr int lds1 = wgrad_wide_lds<WW_TH>();
+    if (attr != dev) {
+      hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_wide_kernel<WW_TH, false, false, true>),
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, lds1);
+      if (e != hipSuccess) return fail(VM_EHIP, "wgrad_wide setup: %s", hipGetErrorString(e));
+      attr = dev;
+    }
+    hipLaunchKernelGGL((wgrad_wide_kernel<WW_TH, false, false, true>), dim3((unsigned)nb), dim3(256), lds1, st, a);
   } else {
     static int attr = -1;
     int dev = 0;
