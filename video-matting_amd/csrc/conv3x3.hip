@@ -3748,6 +3748,32 @@ __global__ __launch_bounds__(256) void pack_weights_tiled(PackBatch b) {
       Chunk<uint16_t>::pack(f);
 }
 
+// the flipped (data-gradient) packs of chunk-major bf16 filters: a lane fills one 16-byte run of 8 packed channels,
+// whose sources w[8 - tap][co][c .. c + 7] are 8 consecutive floats (the filter's contiguous cout axis), where
+// pack_weights_batch decoded and stored one element per thread; same zero padding, same RNE rounding: bit-identical
+__global__ __launch_bounds__(256) void pack_weights_flip8(PackBatch b) {
+  const int jb = blockIdx.y;
+  const vm_pack_job& j = b.j[jb];
+  const int K_pad = b.K_pad[jb], ng = 9 * b.cin_pad[jb] / 32, kq8 = K_pad / 8;
+  const long total = (long)b.cout_pad[jb] * kq8;
+  for (long q = blockIdx.x * 256L + threadIdx.x; q < total; q += (long)gridDim.x * 256) {
+    const int co = (int)(q / kq8), kq = (int)(q - (long)co * kq8);
+    const int gr = kq >> 2, c0 = (kq & 3) * 8;
+    float f[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (gr < ng && co < j.cout && co < j.w_cin) {
+      const int cc = gr / 9, tap = gr - cc * 9;
+      const float* src = j.w + ((long)(8 - tap) * j.w_cin + co) * j.w_cout;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int c = cc * 32 + c0 + k;
+        if (c < j.cin && c < j.w_cout) f[k] = src[c];
+      }
+    }
+    *reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(j.packed) + (long)co * K_pad + kq * 8) =
+        Chunk<uint16_t>::pack(f);
+  }
+}
+
 struct PackGeom {
   int cin_pad, ge, K9, K_pad, cout_pad, chunk_major, ng;
 };
@@ -5397,14 +5423,17 @@ extern "C" int vm_conv3x3_pack_weights_batch(int njobs, const vm_pack_job* jobs,
         (j.dtype != VM_F32 && j.dtype != VM_BF16))
       return fail(VM_EINVAL, "pack_weights_batch: bad job %d", i);
   }
-  // chunk-major bf16 forward packs go to the tiled transpose (pack_weights_tiled), the rest element-wise
-  for (int tiled = 0; tiled < 2; ++tiled) {
+  // chunk-major bf16 packs: forward ones to the tiled transpose (pack_weights_tiled), flipped ones 8 channels per
+  // lane (pack_weights_flip8); the rest element-wise.  kind 0 element-wise, 1 tiled, 2 flip8
+  for (int tiled = 0; tiled < 3; ++tiled) {
     PackBatch b{};
     long mx = 1;
     auto flush = [&]() -> int {
       if (!b.n) return VM_OK;
-      if (tiled)
+      if (tiled == 1)
         hipLaunchKernelGGL(pack_weights_tiled, dim3((unsigned)mx, b.n), dim3(256), 0, st, b);
+      else if (tiled == 2)
+        hipLaunchKernelGGL(pack_weights_flip8, dim3(grid_for(mx, 256, 1024), b.n), dim3(256), 0, st, b);
       else
         hipLaunchKernelGGL(pack_weights_batch, dim3(grid_for(mx, 256, 256), b.n), dim3(256), 0, st, b);
       const int rc = check_launch("pack_weights_batch");
@@ -5415,13 +5444,16 @@ extern "C" int vm_conv3x3_pack_weights_batch(int njobs, const vm_pack_job* jobs,
     for (int i = 0; i < njobs; ++i) {
       const vm_pack_job& j = jobs[i];
       const PackGeom g = geom(j.cin, j.cout, j.dtype);
-      const bool tj = g_pack_tiled && j.dtype == VM_BF16 && !j.flip && g.chunk_major;
-      if (tj != (tiled != 0)) continue;
+      const bool vec = g_pack_tiled && j.dtype == VM_BF16 && g.chunk_major &&
+                       reinterpret_cast<uintptr_t>(j.packed) % 16 == 0;
+      const int kind = !vec ? 0 : j.flip ? 2 : 1;
+      if (kind != tiled) continue;
       b.j[b.n] = j;
       b.K_pad[b.n] = g.K_pad;
       b.cout_pad[b.n] = g.cout_pad;
       b.cin_pad[b.n] = g.cin_pad;
-      const long t = tiled ? (long)(g.K_pad / 32) * (g.cout_pad / 64) : (long)g.cout_pad * g.K_pad;
+      const long t = tiled == 1 ? (long)(g.K_pad / 32) * (g.cout_pad / 64)
+                     : tiled == 2 ? (long)g.cout_pad * (g.K_pad / 8) : (long)g.cout_pad * g.K_pad;
       if (t > mx) mx = t;
       if (++b.n == PACK_MAX_JOBS) {
         const int rc = flush();
