@@ -289,6 +289,8 @@ class VideoTrainer(TrainerBase):
         bnl = self.model.bn[scope]
         ops.bn_apply(z, mean, var, bnl.gamma, bnl.beta, EPS, act, out=out)
 
+    in9_side = True  # the 9-channel input concat converted on a side stream beside the towers (A/B: False)
+
     def _check_capture_fork(self):
         """The side-stream fork of forward / backward is legal inside a HIP graph capture only from the stream the
         capture began on.  Forking from a stream that was itself forked inside the capture (e.g. a pass moved onto
@@ -314,9 +316,22 @@ class VideoTrainer(TrainerBase):
         b = m._buffers(n, h, w)
         tb = self._train_buffers(n, h, w)
         L = _levels(h, w)
-        m.load_inputs(b, xs)
-        m._towers(b)
         main = torch.cuda.current_stream(self.device) if self._side else None
+        ev_in9 = None
+        if self._side and self.in9_side:
+            # the 9-channel concat is first read by the level-0 select convs, after the towers: its three converts
+            # (~85 us of strided 3-channel writes) run on a side stream beside the towers instead of ahead of them
+            self._side[0].wait_stream(main)
+            with torch.cuda.stream(self._side[0]):
+                m.load_in9(b, xs)
+            ev_in9 = torch.cuda.Event()
+            ev_in9.record(self._side[0])
+            m.load_towers(b, xs)
+        else:
+            m.load_inputs(b, xs)
+        m._towers(b)
+        if ev_in9 is not None:
+            main.wait_event(ev_in9)
         done = {}
         if self._side:  # every level's select chains, queued on the side streams right after the towers
             for st in self._side:

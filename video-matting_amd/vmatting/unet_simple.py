@@ -146,9 +146,18 @@ class UNetSimple:
     def load_inputs(self, b, xs):
         """cmp / bg / diff (f32 device tensors) into the towers' batch (tower t = frames t*n..) and into the 9-channel
         layers['conv1'][0] = concat(cmp, bg, diff) (unet_simple.py:148-152)."""
+        self.load_towers(b, xs)
+        self.load_in9(b, xs)
+
+    def load_towers(self, b, xs):
+        """cmp / bg / diff into the towers' batch only."""
         n = xs[0].shape[0]
         for t in range(3):
             ops.convert(xs[t], b["tin"][t * n:(t + 1) * n])
+
+    def load_in9(self, b, xs):
+        """cmp / bg / diff into the 9-channel concat only (read first by the level-0 select convs)."""
+        for t in range(3):
             ops.convert(xs[t], b["in9"][..., 3 * t:3 * t + 3])
 
     def forward(self, cmp, bg, diff, phase=None):
