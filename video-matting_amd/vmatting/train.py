@@ -446,8 +446,9 @@ class VideoTrainer(TrainerBase):
         """Re-make every kernel-layout copy of the flat parameters (forward, data-gradient and channel-padded packs,
         the padded biases) after the flat buffer changed: the optimizer step, or rank 0's DDP broadcast."""
         self._repack()
-        for scope, (pc, bp, cout) in self._padconv.items():
-            bp[:cout].copy_(self.P[scope, "b"])
+        if self._padconv:  # the padded biases: one multi-tensor copy launch instead of one copy per conv
+            torch._foreach_copy_([bp[:cout] for _, bp, cout in self._padconv.values()],
+                                 [self.P[scope, "b"] for scope in self._padconv])
 
     def step(self, cmp, bg, warped, gt, raw_fg):
         """One training iteration; returns a new device tensor [loss, alpha_loss, compositional_loss] (pre-update),
