@@ -290,6 +290,7 @@ class VideoTrainer(TrainerBase):
         ops.bn_apply(z, mean, var, bnl.gamma, bnl.beta, EPS, act, out=out)
 
     in9_side = True  # the 9-channel input concat converted on a side stream beside the towers (A/B: False)
+    interleave_issue = True  # forward: queue level k+1's select chains after level k's upconv (A/B: False)
 
     def _check_capture_fork(self):
         """The side-stream fork of forward / backward is legal inside a HIP graph capture only from the stream the
@@ -333,21 +334,31 @@ class VideoTrainer(TrainerBase):
         if ev_in9 is not None:
             main.wait_event(ev_in9)
         done = {}
-        if self._side:  # every level's select chains, queued on the side streams right after the towers
+
+        def queue_selects(lv, cat, width, sels):  # one level's select chains on the side streams
+            c, off, done[lv] = b[cat][..., :width], 0, []
+            for i, (s, src) in enumerate(sels):
+                co = m.convs[s].cout
+                st = self._side[i % len(self._side)]
+                with torch.cuda.stream(st):
+                    self._new_conv(self._src(b, src), s, "relu", c[..., off:off + co], tb)
+                ev = torch.cuda.Event()
+                ev.record(st)
+                done[lv].append(ev)
+                off += co
+
+        # the select chains go on the side streams right after the towers.  interleave_issue: the host queues level
+        # k+1's chains after the decoder's level-k resize + upconv instead of all levels' chains first, so the main
+        # stream has work queued while the host issues the ~40 side launches (~0.4 ms of host time after the towers
+        # with the decoder idle)
+        ahead = self._side and self.interleave_issue
+        if self._side:
             for st in self._side:
                 st.wait_stream(main)
-            for lv, cat, width, sels, up, prev, conv, out_key in LEVELS:
-                c, off, done[lv] = b[cat][..., :width], 0, []
-                for i, (s, src) in enumerate(sels):
-                    co = m.convs[s].cout
-                    st = self._side[i % len(self._side)]
-                    with torch.cuda.stream(st):
-                        self._new_conv(self._src(b, src), s, "relu", c[..., off:off + co], tb)
-                    ev = torch.cuda.Event()
-                    ev.record(st)
-                    done[lv].append(ev)
-                    off += co
-        for lv, cat, width, sels, up, prev, conv, out_key in LEVELS:
+            for k, (lv, cat, width, sels, *_rest) in enumerate(LEVELS):
+                if not ahead or k == 0:
+                    queue_selects(lv, cat, width, sels)
+        for k, (lv, cat, width, sels, up, prev, conv, out_key) in enumerate(LEVELS):
             c, off = b[cat][..., :width], 0
             for s, src in sels:
                 co = m.convs[s].cout
@@ -362,6 +373,9 @@ class VideoTrainer(TrainerBase):
                 ops.resize_bilinear(b[prev], L[lv], out=r)
             pc, rx = m.conv(up, r)
             ops.conv3x3(rx, pc, "relu", out=c[..., off:width], affine=False, splitk=True)
+            if ahead and k + 1 < len(LEVELS):
+                nlv, ncat, nwidth, nsels = LEVELS[k + 1][:4]
+                queue_selects(nlv, ncat, nwidth, nsels)
             for ev in done.get(lv, ()):
                 main.wait_event(ev)
             mean, var = tb["st_" + up]
@@ -420,23 +434,39 @@ class VideoTrainer(TrainerBase):
             nsel = gsel.shape[-1]
             du = ops.relu_backward(tb["dcat_" + up], c, tb["du_" + up],
                                    dx2=None if g16 is None else g16[..., :width - nsel], dx_lo=gsel)
+            split = None
+            if self._side:
+                split = torch.cuda.Event()
+                split.record(main)
+
+            def chain_next(up=up, du=du, g16=g16):  # the decoder chain's next step: the upconv's data gradient
+                if g16 is not None:
+                    ops.conv3x3(g16, self.dconv16[up], "none", out=tb["dr_" + up], affine=False)
+                else:
+                    ops.conv3x3(du, self.dconv[up], "none", out=tb["dr_" + up], affine=False)
+                return ops.resize_backward(tb["dr_" + up], tb["dprev_" + up])
+
+            # interleave_issue: the host queues the upconv's filter gradient (its own stream) and the decoder chain's
+            # next step before the select chains, so neither waits behind the ~15 select launches' host time
+            first = self._wside is not None and self.interleave_issue
+            if first:
+                self._chain_wgrad(b[RBUF[up]], du, self.G[up, "w"])
+                if up in DGRAD:
+                    dout = chain_next()
             for i, (s, src) in enumerate(sels):
                 co = m.convs[s].cout
                 if self._side:  # leaves of the backward graph: beside the decoder chain, joined before the update
                     st = self._side[i % len(self._side)]
-                    st.wait_stream(main)
+                    st.wait_event(split)
                     with torch.cuda.stream(st):
                         self._conv_backward(s, self._src(b, src), gsel[..., off:off + co], None, tb)
                 else:
                     self._conv_backward(s, self._src(b, src), gsel[..., off:off + co], None, tb)
                 off += co
-            self._chain_wgrad(b[RBUF[up]], du, self.G[up, "w"])
-            if up in DGRAD:
-                if g16 is not None:
-                    ops.conv3x3(g16, self.dconv16[up], "none", out=tb["dr_" + up], affine=False)
-                else:
-                    ops.conv3x3(du, self.dconv[up], "none", out=tb["dr_" + up], affine=False)
-                dout = ops.resize_backward(tb["dr_" + up], tb["dprev_" + up])
+            if not first:
+                self._chain_wgrad(b[RBUF[up]], du, self.G[up, "w"])
+                if up in DGRAD:
+                    dout = chain_next()
         for st in self._side + ([self._wside] if self._wside is not None else []):
             main.wait_stream(st)  # every gradient is in place before the all-reduce / Adam that read them
 
