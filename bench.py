@@ -678,8 +678,8 @@ def train_small_bench(dev, steps, warmup, world, rank, threads, cpu=True, n=8, s
     rec = {"workload": "small_train.py step: %d x %dx%d per GPU, UNetSmall(concat(cmp, bg)) fwd/bwd over all "
                        "variables, loss, DDP all-reduce, TF-Adam" % (n, size, size),
            "dtype": dtype + " forward, f32 gradients/optimizer", "n_gpus": world,
-           "launch": "hip-graph replay of forward+loss and of backward (one stream), eager all-reduce + Adam + "
-                     "re-pack" if graph else "eager" + ("; filter gradients on a side stream" if streams else ""),
+           "launch": "hip-graph replay of forward+loss and of backward, eager all-reduce + Adam + re-pack" if graph
+                     else "eager",
            "samples_per_s": round(n * world / wall, 1), "ms_per_step": round(1000 * wall, 4),
            "device_ms": {"forward_loss": round(ph[0], 4), "backward": round(ph[1], 4),
                          "allreduce_adam_repack": round(ph[2], 4)},
@@ -771,8 +771,8 @@ def train_image_bench(dev, steps, warmup, world, rank, threads, cpu=True, n=8, s
     rec = {"workload": "train.py training_procedure step: %d x %dx%d per GPU, unet.UNetImage([cmp, bg]) fwd/bwd over "
                        "all variables (VGG included), loss, DDP all-reduce, TF-Adam" % (n, size, size),
            "dtype": dtype + " forward / MFMA gradients, f32 gradients/optimizer", "n_gpus": world,
-           "launch": "hip-graph replay of forward+loss and of backward, eager all-reduce + Adam + re-pack" if graph
-                     else "eager",
+           "launch": "hip-graph replay of forward+loss and of backward (one stream), eager all-reduce + Adam + "
+                     "re-pack" if graph else "eager" + ("; filter gradients on a side stream" if streams else ""),
            "samples_per_s": round(n * world / wall, 1), "ms_per_step": round(1000 * wall, 4),
            "device_ms": {"forward_loss": round(ph[0], 4), "backward": round(ph[1], 4),
                          "allreduce_adam_repack": round(ph[2], 4)},
