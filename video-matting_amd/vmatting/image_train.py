@@ -54,6 +54,9 @@ class ImageTrainer(TrainerBase):
     """train.training_procedure's iteration on device (unet.UNetImage, all variables trainable)."""
 
     bf16_dgrad = True  # bf16 path: data gradients held in bf16 (see _grad_buffers); False = f32 as the fp32 path
+    # filter gradients kept on the caller's stream: conv1_1's is the backward's last work and the data-gradient chain
+    # (no dgrad for conv1_1) is idle by then, while the side stream still has the earlier layers' queued
+    main_wgrad = ("conv1_1",)
 
     def __init__(self, vgg16_npy_path=None, dtype="fp32", device="cuda", params=None, lr=1e-5, beta1=0.9,
                  beta2=0.999, epsilon=1e-8, streams=1):
@@ -176,8 +179,8 @@ class ImageTrainer(TrainerBase):
         ops.relu_backward_bias(dy, y, dz, self.G[name, "b"], add=add)
         self._wgrad_dgrad(name, x_in, dz, h16, dx_out)
 
-    def _wgrad(self, x_in, dz, dw, mfma):
-        if self._main is None:
+    def _wgrad(self, x_in, dz, dw, mfma, main=False):
+        if self._main is None or main:
             ops.conv_wgrad(x_in, dz, dw, mfma=mfma)
             return
         self._side.wait_stream(self._main)
@@ -186,11 +189,11 @@ class ImageTrainer(TrainerBase):
 
     def _wgrad_dgrad(self, name, x_in, dz, h16, dx_out):
         if h16 is not None:  # bf16 path: the bf16 copy feeds both MFMA convs
-            self._wgrad(x_in, h16, self.G[name, "w"], True)
+            self._wgrad(x_in, h16, self.G[name, "w"], True, name in self.main_wgrad)
             if dx_out is not None:
                 ops.conv3x3(h16, self.dconv[name], "none", out=dx_out, affine=False, splitk=True)
         else:
-            self._wgrad(x_in, dz, self.G[name, "w"], False)
+            self._wgrad(x_in, dz, self.G[name, "w"], False, name in self.main_wgrad)
             if dx_out is not None:
                 ops.conv3x3(dz, self.dconv[name], "none", out=dx_out, affine=False, splitk=True)
 
