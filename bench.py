@@ -1197,11 +1197,15 @@ def main():
         log("bench: --gpus must be >= 1")
         return 2
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
-        # this process is the launcher: start the N ranks before anything touches a GPU
-        if not args.dist_selftest and torch.cuda.device_count() < args.gpus:  # device_count does not init HIP
-            log("bench: --gpus %d but %d GPU(s) visible" % (args.gpus, torch.cuda.device_count()))
-            return 2
+        # this process is the launcher: it starts the N ranks and makes no torch.cuda / HIP call at all (on ROCm
+        # torch.cuda.device_count() can fall back to a HIP-initialising query; a child started from a GPU-initialised
+        # parent is the pattern this pool forbids) — each rank checks the visible GPUs itself
         return launch_ranks(args.gpus, sys.argv[1:])
+    if not args.dist_selftest:
+        need = int(os.environ.get("WORLD_SIZE", args.gpus))
+        if torch.cuda.device_count() < need:  # a rank process (or the N=1 run): checked before any GPU work
+            log("bench: %d rank(s) need %d GPU(s), %d visible" % (need, need, torch.cuda.device_count()))
+            return 2
 
     rank, world, local = parallel.init_from_env("gloo" if args.dist_selftest else "nccl")
     if world != args.gpus:

@@ -33,7 +33,13 @@ extern "C" {
 
 #define VM_ABI_VERSION 1
 
-enum vm_dtype { VM_F32 = 0, VM_BF16 = 1, VM_U8 = 2, VM_F64 = 3 /* loader outputs only */ };
+enum vm_dtype {
+  VM_F32 = 0,
+  VM_BF16 = 1,
+  VM_U8 = 2,
+  VM_F64 = 3, /* loader outputs only */
+  VM_F16 = 4  /* IEEE half: the split-fp16 x3 conv operands only (vm_split3h_nhwc, vm_conv3x3_ex_nhwc, head_acc) */
+};
 
 enum vm_act {
   VM_ACT_NONE = 0,
@@ -160,6 +166,11 @@ int vm_conv3x3_head_nhwc(const vm_tensor* x, const void* packed, int cin, const 
  * (the split-bf16 x6 path's conv1_5 over 6 x 128 channels, unet.py:203-205).  cin <= 256 (bf16). */
 int vm_conv3x3_head_acc_nhwc(const vm_tensor* x, const void* packed, int cin, const float* bias, const float* y_acc,
                              vm_tensor* y, float* alpha, void* stream);
+/* The same with the per-channel affine of vm_conv3x3_nhwc: pre-activation = (conv + y_acc + bias) * scale + shift
+ * (y_acc may be NULL) — the split-fp16 x3 path's conv1_5, whose fp16 filter parts are pre-scaled by a power of two
+ * that the last chunk's scale undoes (exactly) before the sigmoid (unet.py:203-205).  x may be VM_F16 (cin <= 256). */
+int vm_conv3x3_head_acc_ex_nhwc(const vm_tensor* x, const void* packed, int cin, const float* bias, const float* scale,
+                                const float* shift, const float* y_acc, vm_tensor* y, float* alpha, void* stream);
 
 /* Two chained convs whose 64-channel intermediate never leaves the chip: y = act2(conv3x3(relu(conv3x3(x, w1) + bias1),
  * w2) + bias2 ...), optionally with the fused 2x2 SAME max-pool of y into ypool (NULL = none) — replaces
@@ -249,6 +260,14 @@ int vm_convert_nhwc(const vm_tensor* x, vm_tensor* y, const float* scale, const 
  * cross products down to 2^-16 of the leading one.  y_pool (optional, same layout at ceil(h/2) x ceil(w/2)): the
  * split of tf.nn.max_pool 2x2 SAME (unet.py:33) of x, from the same pass. */
 int vm_split6_nhwc(const vm_tensor* x, vm_tensor* y, vm_tensor* y_pool, void* stream);
+/* Split-fp16 x3 operand of an f32 activation (no reference counterpart: the operand format of the split-fp16 conv path,
+ * which evaluates unet.py's tf.nn.conv2d (unet.py:39,60,70) at f32 accuracy in three fp16 MFMA products).  x (f32
+ * view) -> h = fp16(x), l = fp16(x - h) (RNE; 22 significant bits), written as three slabs [l, h, h] at channel
+ * p*S + y.coff + c of y (VM_F16; S = slab, or y.cstride / 3 when slab <= 0; y.c >= x.c, the extra channels 0).  A conv
+ * over those channels with the filter parts [Wh, Wl, Wh] stacked along cin is l*Wh + h*Wl + h*Wh.  y_pool (optional,
+ * same layout at ceil(h/2) x ceil(w/2)): the split of tf.nn.max_pool 2x2 SAME (unet.py:33) of x from the same pass.
+ * overflow (device int, may be NULL): set to 1 when some |x| >= 65520 (fp16's range; the split is then invalid). */
+int vm_split3h_nhwc(const vm_tensor* x, vm_tensor* y, vm_tensor* y_pool, int slab, int* overflow, void* stream);
 
 /* tf.contrib.layers.batch_norm(is_training=True): batch mean / biased variance over N,H,W
  * (unet_simple.py:25,41; small.py:22,32).  work: vm_bn_workspace_bytes(x) bytes of device scratch. */

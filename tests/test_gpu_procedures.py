@@ -28,9 +28,10 @@ def _files(tmp_path, video, n=5):
     return out
 
 
-def _reference_loop(trainer, files, tests, make, epochs, bs, validate=False):
-    """train.py:64-95 as the reference writes it (summaries aside); validate: training_procedure's validation
-    batches (their loader draws; the forward leaves the model as it is)."""
+def _reference_loop(trainer, files, tests, make, epochs, bs, validate=False, examples=False):
+    """train.py:64-109 as the reference writes it (summaries aside); validate: training_procedure's validation
+    batches (their loader draws; the forward leaves the model as it is); examples: the epoch-end example summary's
+    draws (train.py:102-104: 5 np.random.randint picks of the test list, then the loader call over them)."""
     from vmatting import loader
     losses = []
     for _ in range(epochs):
@@ -41,6 +42,8 @@ def _reference_loop(trainer, files, tests, make, epochs, bs, validate=False):
             losses.append(trainer.step(*make(loader.get_batch_list(training_list, bs))).cpu().numpy())
         while validate and not loader.epoch_is_over(test_list, bs):
             make(loader.get_batch_list(test_list, bs))
+        if examples:
+            make([tests[np.random.randint(0, len(tests))] for _ in range(5)])
     return losses
 
 
@@ -83,7 +86,8 @@ def _run(kind, tmp_path, graph):
     t2 = trainer()
     random.seed(5)
     np.random.seed(6)
-    want = _reference_loop(t2, files, tests, make, 2, 2, validate=kind == "image")
+    # the epoch-end example draws of train.py (small_train.py makes them every 1000 iterations: none here)
+    want = _reference_loop(t2, files, tests, make, 2, 2, validate=kind == "image", examples=kind != "small")
     return got, want, vals
 
 

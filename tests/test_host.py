@@ -218,6 +218,39 @@ def test_bench_launches_its_own_ranks(n):
     assert r["frames"] == 2 * n + 1 and r["split"][-1][1] == 2 * n + 1
 
 
+@pytest.mark.parametrize("selftest", [True, False])
+def test_bench_launcher_parent_stays_gpu_free(selftest):
+    """the `--gpus N` launcher parent makes no torch.cuda / HIP call before (or after) it starts
+    its ranks.  The parent runs with every device query patched to raise; the ranks are ordinary children.  With
+    --dist-selftest the run succeeds; without it (no GPU here) each rank reports the missing GPUs itself and the
+    launcher returns that non-zero code — the parent never raised."""
+    import subprocess
+    import sys
+    from conftest import REPO
+    bench = os.path.join(REPO, "bench.py")
+    argv = ["--gpus", "2"] + (["--dist-selftest"] if selftest else [])
+    code = ("import sys, runpy, torch\n"
+            "def boom(*a, **k):\n"
+            "    raise SystemExit('PARENT TOUCHED THE GPU')\n"
+            "torch.cuda.device_count = boom\n"
+            "torch.cuda.is_available = boom\n"
+            "torch.cuda.init = boom\n"
+            "torch._C._cuda_getDeviceCount = boom\n"
+            "sys.argv = [%r] + %r\n"
+            "runpy.run_path(%r, run_name='__main__')\n" % (bench, argv, bench))
+    e = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
+        e.pop(k, None)
+    r = subprocess.run([sys.executable, "-c", code], env=e, capture_output=True, text=True, timeout=150)
+    assert "PARENT TOUCHED THE GPU" not in r.stderr + r.stdout
+    if selftest:
+        assert r.returncode == 0, r.stderr[-2000:]
+        assert '"ok": true' in r.stdout
+    else:
+        assert r.returncode == 2, r.stderr[-2000:]
+        assert "need 2 GPU(s)" in r.stderr
+
+
 def test_bench_refuses_a_world_other_than_gpus():
     """A run whose initialised world differs from --gpus (here: a torchrun-style env of world 1) exits non-zero
     instead of reporting a one-GPU number as N GPUs."""
@@ -277,3 +310,70 @@ def test_training_procedures_follow_the_reference_loop(tmp_path):
         while len(tl) >= 4:
             want.append([tl.pop() for _ in range(4)])
     assert made == want and [s[1] for s in steps] == list(range(4)) and files == ["f%d" % i for i in range(11)]
+
+
+def test_training_procedures_example_draws_and_graph_shape_guard():
+    """the loops make the reference's example-summary draws (train.py:102-104: 5 np.random.randint picks
+    of the test list + the loader call, every epoch; small_train.py:78-82: every 1000 iterations), so np.random stays
+    on the reference's stream after epoch 1; and a HIP-graph loop refuses a batch of another shape instead of an
+    eager step under the captured graph's buffers."""
+    from vmatting import procedures
+
+    class FakeTrainer:
+        device = "cpu"
+
+        def step(self, *batch):
+            return 0
+
+        def capture(self, *batch):
+            return self
+
+    made = []
+
+    def make(batch_list):
+        made.append(list(batch_list))
+        np.random.rand()  # stands for the loader's own draws
+        return (np.zeros((len(batch_list), 2)),)
+
+    files = ["f%d" % i for i in range(9)]
+    np.random.seed(4)
+    procedures._loop(FakeTrainer(), files, files[:5], make, 2, 4, False, None, None, examples=make)
+    after = np.random.rand()
+    np.random.seed(4)
+    for _ in range(2):
+        for _ in range(2):
+            np.random.rand()  # two training batches of 4 per epoch
+        [np.random.randint(0, 5) for _ in range(5)]
+        np.random.rand()
+    assert after == np.random.rand()
+    assert [len(m) for m in made] == [4, 4, 5, 4, 4, 5]
+    # small_train.py's cadence: draws whenever (iteration + 1) % every == 0
+    made.clear()
+    procedures._loop(FakeTrainer(), files, files[:5], make, 1, 1, False, None, None, examples=make, example_every=3)
+    assert [len(m) for m in made] == [1, 1, 5, 1, 1, 1, 5, 1, 1, 1, 5, 1]
+    # graph loop: one batch shape
+    st = procedures._Stepper(FakeTrainer(), True)
+    st(np.zeros((4, 2)))
+    st(np.zeros((4, 2)))
+    with pytest.raises(ValueError, match="one batch shape"):
+        st(np.zeros((3, 2)))
+
+
+def test_entry_points_without_arguments_name_what_is_missing(tmp_path, monkeypatch):
+    """train(), simple_train(), video_train() and small_train.train() take no arguments, like the
+    reference (train.py:112,241,346; small_train.py:91); without the reference's dataset (params.py:3-6, 12-15) they
+    raise a ValueError naming it instead of a TypeError / open(None)."""
+    from vmatting import params, procedures
+    monkeypatch.chdir(tmp_path)
+    monkeypatch.setattr(params, "SYNTHETIC_DATASET", None)
+    for fn, what in ((procedures.train, "SYNTHETIC_DATASET"), (procedures.simple_train, "SYNTHETIC_DATASET"),
+                     (procedures.small_train, "SYNTHETIC_DATASET"), (procedures.video_train, "TRAIN_AUGMENTED")):
+        with pytest.raises(ValueError, match=what):
+            fn()
+    monkeypatch.setattr(params, "SYNTHETIC_DATASET", str(tmp_path))
+    with pytest.raises(ValueError, match="dataset/train.txt"):
+        procedures.train()
+    (tmp_path / "dataset").mkdir()
+    (tmp_path / "dataset" / "train.txt").write_text("a b c\n")
+    with pytest.raises(ValueError, match="dataset/valid.txt"):
+        procedures.small_train()

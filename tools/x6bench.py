@@ -1,5 +1,6 @@
-"""1080p forward time of the split-bf16 x6 path against fp32 and bf16 (graph replay), plus its per-conv kernels:
-    python tools/x6bench.py [steps]"""
+"""1080p forward time of the split paths (f16x3, bf16x6) against fp32 and bf16 (graph replay), plus the split
+paths' per-conv kernels:
+    python tools/x6bench.py [steps] [dtype ...]"""
 import os
 import sys
 import time
@@ -14,9 +15,10 @@ from vmatting import ops, unet, video  # noqa: E402
 from vmatting.weights import synthetic_vgg16  # noqa: E402
 
 steps = int(sys.argv[1]) if len(sys.argv) > 1 else 10
+dts = sys.argv[2:] or ["f16x3", "bf16x6", "fp32", "bf16"]
 x = video.synthetic_frames(1, 1080, 1920, first=0, device="cuda")
 res = {}
-for dt in ("bf16x6", "fp32", "bf16"):
+for dt in dts:
     np.random.seed(0)
     m = unet.UNetVideo(synthetic_vgg16(0), dtype=dt)
     m.prepare()
@@ -31,7 +33,7 @@ for dt in ("bf16x6", "fp32", "bf16"):
     ms = 1e3 * (time.perf_counter() - t0) / steps
     res[dt] = (ms, g.output.clone())
     print("%-7s %.3f ms/frame" % (dt, ms), flush=True)
-    if dt == "bf16x6":
+    if dt in ("bf16x6", "f16x3"):
         prof = ops.conv_profile(True)
         m.forward(x)
         torch.cuda.synchronize()
@@ -40,8 +42,10 @@ for dt in ("bf16x6", "fp32", "bf16"):
         for fl, name, e0, e1, *shape in prof:
             t = e0.elapsed_time(e1)
             tot += t
-            print("  %-70s %7.3f ms %7.1f TFLOP/s (x6 products)" % (name[:70], t, fl / (t * 1e-3) / 1e12))
+            print("  %-70s %7.3f ms %7.1f TFLOP/s (executed products)" % (name[:70], t, fl / (t * 1e-3) / 1e12))
         print("  conv total %.3f ms" % tot)
     del m, g
     torch.cuda.empty_cache()
-print("bf16x6 vs fp32 alpha max-abs %.3e" % float((res["bf16x6"][1] - res["fp32"][1]).abs().max()))
+for dt in res:
+    if dt != "fp32" and "fp32" in res:
+        print("%s vs fp32 alpha max-abs %.3e" % (dt, float((res[dt][1] - res["fp32"][1]).abs().max())))

@@ -726,8 +726,9 @@ __device__ __forceinline__ void first_layer_patch(const ConvArgs& a, char* smem,
 // granule buffers (zero outside the frame = the second conv's SAME padding), so the 64-channel activation never
 // touches HBM; the main loop then streams only weights.
 // UPSKIP: the folded-upconv instantiation (vm_conv3x3_up2x_nhwc), which skips its phase filters' zero taps
+// MT: the MFMA operand type (uint16_t = bf16; f16_t = the split-fp16 forward's fp16 parts, same data path)
 template <int BN, int WM, int WN, int S, int TH, int MINB, int UNR, bool PF, int ABL, bool FIRST, int G = 1,
-          bool UPSKIP = false>
+          bool UPSKIP = false, typename MT = uint16_t>
 __global__ __launch_bounds__(64 * WM * WN)
 __attribute__((amdgpu_waves_per_eu((UPSKIP || G > 1) && MINB * WM * WN < 16 ? 4 : MINB * WM * WN / 4)))  // <= 128 VGPRs
 void conv3x3_patch(ConvArgs a) {
@@ -928,7 +929,7 @@ void conv3x3_patch(ConvArgs a) {
 #pragma unroll
               for (int fc = 0; fc < FC; ++fc)
 #pragma unroll
-                for (int fp = 0; fp < FP; ++fp) mma16<T>(av[g & 1][fc], bv[g & 1][fp], acc[fc][fp]);
+                for (int fp = 0; fp < FP; ++fp) mma16<MT>(av[g & 1][fc], bv[g & 1][fp], acc[fc][fp]);
             }
           }
         }
@@ -971,7 +972,7 @@ void conv3x3_patch(ConvArgs a) {
 #pragma unroll
         for (int fc = 0; fc < FC; ++fc)
 #pragma unroll
-          for (int fp = 0; fp < FP; ++fp) mma16<T>(av[fc], bv[fp], acc[fc][fp]);
+          for (int fp = 0; fp < FP; ++fp) mma16<MT>(av[fc], bv[fp], acc[fc][fp]);
         if (s + 1 < nsteps) {
           // in flight after W(s+1): S-2 younger weight steps, plus the patch issued at the end of the last chunk
           sync((S - 2) * w_n + ((tap <= S - 2 && cc >= 1) ? x_n : 0));
@@ -1006,7 +1007,7 @@ void conv3x3_patch(ConvArgs a) {
 #pragma unroll
           for (int fc = 0; fc < FC; ++fc)
 #pragma unroll
-            for (int fp = 0; fp < FP; ++fp) mma16<T>(av[fc], bv[fp], acc[fc][fp]);
+            for (int fp = 0; fp < FP; ++fp) mma16<MT>(av[fc], bv[fp], acc[fc][fp]);
         } else {  // keep the fragment reads alive without the MFMAs
 #pragma unroll
           for (int fc = 0; fc < FC; ++fc) asm volatile("" ::"v"(av[fc].x), "v"(av[fc].w));
@@ -4492,13 +4493,19 @@ static int launch_patch(ConvArgs& a, hipStream_t st) {
   using C = PatchCfg<BN, WM, WN, S, TH, G>;
   static_assert(!(FIRST && PF), "FIRST uses the plain pipeline");
   constexpr int lds = FIRST ? C::LDS_FIRST : C::LDS;
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute(
-        reinterpret_cast<const void*>(&conv3x3_patch<BN, WM, WN, S, TH, MINB, UNR, PF, ABL, FIRST, G, UPSKIP>),
-        hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  // fp16 operands (ConvArgs::f16, the split-fp16 forward): the same tiling on v_mfma_f32_16x16x32_f16
+  constexpr bool F16_OK = !FIRST && !UPSKIP && ABL == 0;
+  const bool f16 = F16_OK && a.f16;
+  if (a.f16 && !F16_OK) return fail(VM_EUNSUPPORTED, "conv3x3_patch: no fp16 instantiation of this tiling");
+  static bool attr_set = false, attr16_set = false;
+  if (!(f16 ? attr16_set : attr_set)) {
+    const void* fn = f16 ? reinterpret_cast<const void*>(
+                               &conv3x3_patch<BN, WM, WN, S, TH, MINB, UNR, PF, ABL, FIRST, G, UPSKIP, f16_t>)
+                         : reinterpret_cast<const void*>(
+                               &conv3x3_patch<BN, WM, WN, S, TH, MINB, UNR, PF, ABL, FIRST, G, UPSKIP>);
+    hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (e != hipSuccess) return fail(VM_EHIP, "hipFuncSetAttribute(patch): %s", hipGetErrorString(e));
-    attr_set = true;
+    (f16 ? attr16_set : attr_set) = true;
   }
   const long N = a.M / ((long)a.H * a.W);
   const long sp = a.vstride ? ((a.H + C::TH - 1) / C::TH) * (long)((a.vW + C::TW - 1) / C::TW)
@@ -4514,10 +4521,19 @@ static int launch_patch(ConvArgs& a, hipStream_t st) {
   const long wbytes = (long)a.cout_pad * a.K_pad * 2;
   a.cband = (g_cband >= (a.up ? 1 : 2)) && !FIRST && BN == 64 && a.tiles_n % 8 == 0 && wbytes >= g_cband_bytes
                 ? a.tiles_n / 8 : 0;
-  snprintf(g_last_kernel, sizeof g_last_kernel, "vm::conv3x3_patch<%d, %d, %d, %d, %d, %d, %d, %s, %d, %s, %d, %s>", BN,
-           WM, WN, S, TH, MINB, UNR, PF ? "true" : "false", ABL, FIRST ? "true" : "false", G, UPSKIP ? "true" : "false");
-  hipLaunchKernelGGL((conv3x3_patch<BN, WM, WN, S, TH, MINB, UNR, PF, ABL, FIRST, G, UPSKIP>),
-                     dim3(a.tiles_total, a.ksplit > 1 ? a.ksplit : 1), dim3(C::NT), lds, st, a);
+  snprintf(g_last_kernel, sizeof g_last_kernel, "vm::conv3x3_patch<%d, %d, %d, %d, %d, %d, %d, %s, %d, %s, %d, %s%s>",
+           BN, WM, WN, S, TH, MINB, UNR, PF ? "true" : "false", ABL, FIRST ? "true" : "false", G,
+           UPSKIP ? "true" : "false", f16 ? ", vm::f16_t" : "");
+  const dim3 grid(a.tiles_total, a.ksplit > 1 ? a.ksplit : 1);
+  if constexpr (F16_OK) {
+    if (f16) {
+      hipLaunchKernelGGL((conv3x3_patch<BN, WM, WN, S, TH, MINB, UNR, PF, ABL, FIRST, G, UPSKIP, f16_t>), grid,
+                         dim3(C::NT), lds, st, a);
+      return check_launch("conv3x3_patch");
+    }
+  }
+  hipLaunchKernelGGL((conv3x3_patch<BN, WM, WN, S, TH, MINB, UNR, PF, ABL, FIRST, G, UPSKIP>), grid, dim3(C::NT), lds,
+                     st, a);
   return check_launch("conv3x3_patch");
 }
 
@@ -5395,14 +5411,14 @@ extern "C" int vm_set_option(const char* key, long value) {
 extern "C" const char* vm_conv3x3_last_kernel(void) { return g_last_kernel; }
 
 extern "C" size_t vm_conv3x3_packed_bytes(int cin, int cout, int dtype) {
-  if (cin <= 0 || cout <= 0 || (dtype != VM_F32 && dtype != VM_BF16)) return 0;
+  if (cin <= 0 || cout <= 0 || (dtype != VM_F32 && dtype != VM_BF16 && dtype != VM_F16)) return 0;
   PackGeom g = geom(cin, cout, dtype);
   return (size_t)g.cout_pad * g.K_pad * elem_bytes(dtype);
 }
 
 extern "C" int vm_conv3x3_pack_weights(const float* w_hwio, int cin, int cout, int dtype, void* packed, void* stream) {
   if (!w_hwio || !packed || cin <= 0 || cout <= 0) return fail(VM_EINVAL, "pack_weights: bad argument");
-  if (dtype != VM_F32 && dtype != VM_BF16) return fail(VM_EINVAL, "pack_weights: dtype %d", dtype);
+  if (dtype != VM_F32 && dtype != VM_BF16 && dtype != VM_F16) return fail(VM_EINVAL, "pack_weights: dtype %d", dtype);
   PackGeom g = geom(cin, cout, dtype);
   ConvArgs a{};
   fill_geom(a, g);
@@ -5410,6 +5426,7 @@ extern "C" int vm_conv3x3_pack_weights(const float* w_hwio, int cin, int cout, i
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int grid = grid_for((long)g.cout_pad * g.K_pad, 256);
   if (dtype == VM_BF16) hipLaunchKernelGGL(pack_weights<uint16_t>, dim3(grid), dim3(256), 0, st, w_hwio, cin, cout, a);
+  else if (dtype == VM_F16) hipLaunchKernelGGL(pack_weights<f16_t>, dim3(grid), dim3(256), 0, st, w_hwio, cin, cout, a);
   else hipLaunchKernelGGL(pack_weights<float>, dim3(grid), dim3(256), 0, st, w_hwio, cin, cout, a);
   return check_launch("pack_weights");
 }
@@ -5659,6 +5676,13 @@ extern "C" int vm_conv3x3_head_acc_nhwc(const vm_tensor* x, const void* packed, 
                    nullptr, y_acc);
 }
 
+extern "C" int vm_conv3x3_head_acc_ex_nhwc(const vm_tensor* x, const void* packed, int cin, const float* bias,
+                                           const float* scale, const float* shift, const float* y_acc, vm_tensor* y,
+                                           float* alpha, void* stream) {
+  return conv_impl(x, packed, cin, 1, bias, scale, shift, VM_ACT_NONE, y, nullptr, stream, alpha, 0, 0, nullptr, 0,
+                   nullptr, y_acc);
+}
+
 extern "C" int vm_conv3x3_head_partial_nhwc(const vm_tensor* x, const void* packed, int cin, const float* bias,
                                             const float* scale, const float* shift, int act, vm_tensor* y,
                                             float* alpha, const float* partial, void* stream) {
@@ -5745,7 +5769,12 @@ extern "C" int vm_conv3x3_head_nhwc(const vm_tensor* x, const void* packed, int 
 static int conv_impl(const vm_tensor* x, const void* packed, int cin, int cout, const float* bias, const float* scale,
                      const float* shift, int act, vm_tensor* y, const vm_tensor* yp, void* stream, float* y2, int nsrc,
                      long src_stride, void* work, size_t work_bytes, const float* head_part, const float* y_acc) {
-  if (!valid_tensor(x) || !valid_tensor(y) || !packed) return fail(VM_EINVAL, "conv3x3: invalid tensor/weights");
+  if (!valid_tensor(x, true) || !valid_tensor(y) || !packed) return fail(VM_EINVAL, "conv3x3: invalid tensor/weights");
+  // fp16 operands (the split-fp16 forward, vmatting/split3.py): f32 outputs of the patch kernel (any cout % 4 == 0)
+  // or the MFMA head (cout == 1, <= 256 channels per call); no pooling, split sources or softmax
+  const bool f16 = x->dtype == VM_F16;
+  if (f16 && (y->dtype != VM_F32 || yp || nsrc > 1 || act == VM_ACT_SOFTMAX || head_part))
+    return fail(VM_EUNSUPPORTED, "conv3x3: fp16 operands need an f32 output without pool / sources / softmax");
   if (y_acc && cout != 1) return fail(VM_EINVAL, "conv3x3: an accumulated pre-activation needs cout == 1");
   if (head_part && cout != 1) return fail(VM_EINVAL, "conv3x3: head partials need cout == 1");
   const int xc = nsrc > 1 ? nsrc * x->c : x->c;  // sources: x is the view of source 0
@@ -5777,8 +5806,8 @@ static int conv_impl(const vm_tensor* x, const void* packed, int cin, int cout, 
     h.y = y->ptr; h.y_cstride = y->cstride; h.y_coff = y->coff; h.y_dtype = y->dtype; h.y2 = y2;
     h.part = head_part;
     h.yacc = y_acc;
-    if ((head_part || y_acc) && (g_head_kernel != 0 || (g.cin_pad + 4 * ce - 1) / (4 * ce) > 8))
-      return fail(VM_EUNSUPPORTED, "conv3x3 head: partials / accumulation need the MFMA head kernel (cin <= 256)");
+    if ((head_part || y_acc || f16) && (g_head_kernel != 0 || (g.cin_pad + 4 * ce - 1) / (4 * ce) > 8))
+      return fail(VM_EUNSUPPORTED, "conv3x3 head: partials / accumulation / fp16 need the MFMA head kernel (cin <= 256)");
     const int nks = (g.cin_pad + 4 * ce - 1) / (4 * ce);
     if (g_head_kernel == 0 && nks <= 8) {
       constexpr int TW = 64;
@@ -5793,7 +5822,11 @@ static int conv_impl(const vm_tensor* x, const void* packed, int cin, int cout, 
                dt == VM_BF16 ? "unsigned short" : "float", TH, TW, nk);
 #define VM_HEAD_MFMA(TT, NK) \
   hipLaunchKernelGGL((conv3x3_head_mfma<TT, 8, TW, NK>), dim3(tiles), dim3(256), lds, st, h)
-      if (TH == 16 && nk == 2) {  // the split head's 64-channel half
+      if (f16) {
+        snprintf(g_last_kernel, sizeof g_last_kernel, "vm::conv3x3_head_mfma<vm::f16_t, 8, %d, %d>", TW, nk);
+        if (nk == 1) VM_HEAD_MFMA(f16_t, 1); else if (nk == 2) VM_HEAD_MFMA(f16_t, 2);
+        else if (nk == 4) VM_HEAD_MFMA(f16_t, 4); else VM_HEAD_MFMA(f16_t, 8);
+      } else if (TH == 16 && nk == 2) {  // the split head's 64-channel half
         hipLaunchKernelGGL((conv3x3_head_mfma<uint16_t, 16, TW, 2>), dim3(tiles), dim3(256), lds, st, h);
       } else if (TH == 16) {
         hipLaunchKernelGGL((conv3x3_head_mfma<uint16_t, 16, TW, 4>), dim3(tiles), dim3(256), lds, st, h);
@@ -5854,6 +5887,20 @@ static int conv_impl(const vm_tensor* x, const void* packed, int cin, int cout, 
     a.py_coff = yp->coff;
     return dispatch_patch(a, st);
   }
+  if (f16) {  // the patch kernel's fp16 form (+ split-K on small grids with a workspace)
+    a.f16 = 1;
+    if (!patch_ok(a, 2)) return fail(VM_EUNSUPPORTED, "conv3x3: fp16 operands need the patch kernel (cin %% 32 == 0)");
+    a.py = nullptr;
+    a.up = 0;
+    if (work && (cout & 3) == 0) {
+      const int ks = splitk_plan(x->n, x->h, x->w, a.cin_pad, cout);
+      if (ks > 1 && work_bytes >= (size_t)ks * M * cout * sizeof(float)) {
+        a.ksplit = ks;
+        a.part = reinterpret_cast<float*>(work);
+      }
+    }
+    return dispatch_patch(a, st);
+  }
   if (g_conv_kernel == 0 && thin_ok(dt, g, cout, a.x_src_c, act, x)) {
     const int ks = work ? thin_splitk_plan(x->n, x->h, x->w, a.cin_pad) : 1;
     if (ks > 1 && work_bytes >= (size_t)ks * M * cout * sizeof(float)) {
@@ -5885,9 +5932,9 @@ static int conv_impl(const vm_tensor* x, const void* packed, int cin, int cout, 
 
 // workspace of vm_conv3x3_ex_nhwc: the split-K partial sums of a small-grid bf16 conv, else 0
 extern "C" size_t vm_conv3x3_workspace_bytes(const vm_tensor* x, int cin, int cout) {
-  if (!x || x->dtype != VM_BF16 || cin <= 0 || cout <= 0) return 0;
+  if (!x || (x->dtype != VM_BF16 && x->dtype != VM_F16) || cin <= 0 || cout <= 0) return 0;
   const PackGeom g = geom(cin, cout, VM_BF16);
-  if (g_conv_kernel == 0 && thin_ok(VM_BF16, g, cout, cin == x->c ? 0 : x->c, VM_ACT_NONE, x)) {
+  if (x->dtype == VM_BF16 && g_conv_kernel == 0 && thin_ok(VM_BF16, g, cout, cin == x->c ? 0 : x->c, VM_ACT_NONE, x)) {
     const int ks = thin_splitk_plan(x->n, x->h, x->w, g.cin_pad);
     return ks > 1 ? (size_t)ks * x->n * x->h * x->w * cout * sizeof(float) : 0;
   }

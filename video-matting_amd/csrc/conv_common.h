@@ -65,6 +65,8 @@ struct ConvArgs {
   // last-column tiles after the others (with prot == 2's serpentine rounds the half-cost items pair up on the walkers
   // that hold the band's third round)
   int halfskip;
+  // fp16 operands (VM_F16 input view and filter pack: the split-fp16 forward): the patch kernel's fp16 MFMA form
+  int f16;
 };
 
 // compile-time loop: f(std::integral_constant<int, I>) for I in [I, N)
@@ -110,6 +112,13 @@ template <>
 __device__ __forceinline__ void mma16<uint16_t>(const uint4& a, const uint4& b, f32x4& c) {
   c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0, 0,
                                                0);
+}
+
+// fp16 operands (the split-fp16 x3 forward, vmatting/split3.py): 16-bit storage like bf16, so every bf16 data path
+// (LDS-DMA, fragments, packing geometry) carries them unchanged; only the MFMA differs
+template <>
+__device__ __forceinline__ void mma16<f16_t>(const uint4& a, const uint4& b, f32x4& c) {
+  c = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
 }
 
 template <>

@@ -752,6 +752,119 @@ extern "C" int vm_split6_nhwc(const vm_tensor* x, vm_tensor* y, vm_tensor* y_poo
   return check_launch("split6");
 }
 
+// ---------------------------------------------------------------- split-fp16 x3 operands (vmatting/split3.py)
+// x = h + l with h = fp16(x), l = fp16(x - h) (the difference is exact in f32): 22 significant bits where the two
+// bf16 parts of a bf16 x3 split hold 16, so three fp16 products l*Wh + h*Wl + h*Wh (the filter likewise cut in two
+// fp16 parts, pre-scaled by a power of two into fp16's normal range) carry an f32-class conv.  Slabs [l, h, h] at
+// p*S + coff + c meet the filter parts [Wh, Wl, Wh] packed along K: the two 2^-11 terms first, h*Wh last.
+// |x| >= 65520 rounds h to inf: *overflow is set (the caller checks it and falls back for that frame).
+typedef _Float16 f16x2_t __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ uint32_t f16x2_bits(float lo, float hi) {
+  const f32x2_t v = {lo, hi};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, f16x2_t));  // RNE
+}
+
+__device__ __forceinline__ bool store_split3h(uint16_t* base, long S, const float* v) {
+  uint32_t wh[4], wl[4];
+  bool ovf = false;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    wh[i] = f16x2_bits(v[2 * i], v[2 * i + 1]);
+    const f16x2_t h = __builtin_bit_cast(f16x2_t, wh[i]);
+    wl[i] = f16x2_bits(v[2 * i] - (float)h[0], v[2 * i + 1] - (float)h[1]);
+    ovf |= !(fabsf(v[2 * i]) < 65520.f) || !(fabsf(v[2 * i + 1]) < 65520.f);  // (NaN counts too)
+  }
+  const uint4 H = make_uint4(wh[0], wh[1], wh[2], wh[3]), L = make_uint4(wl[0], wl[1], wl[2], wl[3]);
+  *reinterpret_cast<uint4*>(base) = L;
+  *reinterpret_cast<uint4*>(base + S) = H;
+  *reinterpret_cast<uint4*>(base + 2 * S) = H;
+  return ovf;
+}
+
+// one thread = one 8-channel chunk of one output pixel (POOL: of one pooled pixel and the 2x2 window under it)
+template <bool POOL>
+__global__ __launch_bounds__(256) void split3h_kernel(View x, View y, View yp, long S, long Sp, int* overflow) {
+  const int cpp = (y.c + 7) / 8;
+  const int on = POOL ? yp.n : y.n, oh = POOL ? yp.h : y.h, ow = POOL ? yp.w : y.w;
+  const long total = (long)on * oh * ow * cpp;
+  bool ovf = false;
+  const bool vec = ((x.cs | x.coff) & 3) == 0 && (reinterpret_cast<uintptr_t>(x.p) & 15) == 0;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int cc = (int)(i % cpp);
+    const long op = i / cpp;
+    const int c = cc * 8;
+    auto load = [&](long pix, float* f) {
+      const float* src = reinterpret_cast<const float*>(x.p) + pix * x.cs + x.coff + c;
+      if (c + 8 <= x.c && vec) {
+        const float4 a = *reinterpret_cast<const float4*>(src), b = *reinterpret_cast<const float4*>(src + 4);
+        f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w; f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] = c + j < x.c ? src[j] : 0.f;  // channels past x.c: zero padding
+      }
+    };
+    auto out = [&](const View& v, long pix) { return reinterpret_cast<uint16_t*>(v.p) + pix * v.cs + v.coff + c; };
+    if constexpr (!POOL) {
+      float f[8];
+      load(op, f);
+      ovf |= store_split3h(out(y, op), S, f);
+    } else {
+      const int pw = (int)(op % yp.w);
+      const long t = op / yp.w;
+      const int ph = (int)(t % yp.h), n = (int)(t / yp.h);
+      const int iy = 2 * ph, ix = 2 * pw;
+      const bool hasr = ix + 1 < x.w, hasd = iy + 1 < x.h;
+      const long p00 = ((long)n * x.h + iy) * x.w + ix;
+      float f[8], m[8];
+      load(p00, f);
+      ovf |= store_split3h(out(y, p00), S, f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) m[j] = f[j];
+      auto tap = [&](long pix) {
+        load(pix, f);
+        ovf |= store_split3h(out(y, pix), S, f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) m[j] = fmaxf(m[j], f[j]);
+      };
+      if (hasr) tap(p00 + 1);
+      if (hasd) tap(p00 + x.w);
+      if (hasr && hasd) tap(p00 + x.w + 1);
+      store_split3h(out(yp, op), Sp, m);
+    }
+  }
+  if (ovf && overflow) *overflow = 1;  // a plain vector store: any writer's 1 is the answer
+}
+
+static bool split3h_view_ok(const vm_tensor* y, const vm_tensor* x, long S) {
+  return y->dtype == VM_F16 && S % 8 == 0 && 3 * S <= y->cstride && y->coff % 8 == 0 && y->c % 8 == 0 &&
+         y->c >= x->c && y->coff + y->c <= S && y->cstride % 8 == 0 && reinterpret_cast<uintptr_t>(y->ptr) % 16 == 0;
+}
+
+extern "C" int vm_split3h_nhwc(const vm_tensor* x, vm_tensor* y, vm_tensor* y_pool, int slab, int* overflow,
+                               void* stream) {
+  if (!valid_tensor(x) || !valid_tensor(y, true) || (y_pool && !valid_tensor(y_pool, true)) || x->dtype != VM_F32)
+    return fail(VM_EINVAL, "split3h: x must be an f32 view");
+  if (y->n != x->n || y->h != x->h || y->w != x->w) return fail(VM_EINVAL, "split3h: shape mismatch");
+  const long S = slab > 0 ? slab : y->cstride / 3, Sp = y_pool ? (slab > 0 ? slab : y_pool->cstride / 3) : S;
+  if (!split3h_view_ok(y, x, S) || (y_pool && !split3h_view_ok(y_pool, x, Sp)))
+    return fail(VM_EUNSUPPORTED, "split3h: the split view must be fp16, 16-byte aligned, c and coff multiples of 8, "
+                                 "three slabs of S (a multiple of 8) channels inside the pixel row");
+  if (y_pool && (y_pool->n != x->n || y_pool->h != (x->h + 1) / 2 || y_pool->w != (x->w + 1) / 2 ||
+                 y_pool->c != y->c))
+    return fail(VM_EINVAL, "split3h: pool view shape mismatch");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const vm_tensor* o = y_pool ? y_pool : y;
+  const long work = (long)o->n * o->h * o->w * ((y->c + 7) / 8);
+  if (y_pool)
+    hipLaunchKernelGGL(split3h_kernel<true>, dim3(grid_for(work, 256)), dim3(256), 0, st, view(x), view(y),
+                       view(y_pool), S, Sp, overflow);
+  else
+    hipLaunchKernelGGL(split3h_kernel<false>, dim3(grid_for(work, 256)), dim3(256), 0, st, view(x), view(y), view(y),
+                       S, Sp, overflow);
+  return check_launch("split3h");
+}
+
 extern "C" int vm_convert_nhwc(const vm_tensor* x, vm_tensor* y, const float* scale, const float* shift, int act,
                                void* stream) {
   if (!valid_tensor(x) || !valid_tensor(y)) return fail(VM_EINVAL, "convert: invalid tensor");

@@ -33,11 +33,12 @@ inline int check_launch(const char* what) {
   return VM_OK;
 }
 
-inline int elem_bytes(int dtype) { return dtype == VM_F32 ? 4 : dtype == VM_BF16 ? 2 : 1; }
+inline int elem_bytes(int dtype) { return dtype == VM_F32 ? 4 : (dtype == VM_BF16 || dtype == VM_F16) ? 2 : 1; }
 
-inline bool valid_tensor(const vm_tensor* t) {
+// allow_f16: the conv input of the split-fp16 forward (vm_conv3x3_ex_nhwc / head_acc); every other op takes f32 / bf16
+inline bool valid_tensor(const vm_tensor* t, bool allow_f16 = false) {
   return t && t->ptr && t->n > 0 && t->h > 0 && t->w > 0 && t->c > 0 && t->coff >= 0 &&
-         t->coff + t->c <= t->cstride && (t->dtype == VM_F32 || t->dtype == VM_BF16);
+         t->coff + t->c <= t->cstride && (t->dtype == VM_F32 || t->dtype == VM_BF16 || (allow_f16 && t->dtype == VM_F16));
 }
 
 inline bool vec16_ok(const vm_tensor* t, int extra_elems_multiple = 1) {
@@ -48,7 +49,13 @@ inline bool vec16_ok(const vm_tensor* t, int extra_elems_multiple = 1) {
 
 // ---------------------------------------------------------------- device helpers
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// an IEEE fp16 element (VM_F16): 16-bit storage, a distinct type so templates pick the fp16 MFMA / conversions
+struct f16_t {
+  uint16_t v;
+};
 
 __device__ __forceinline__ float bf2f(uint16_t b) { return __uint_as_float(static_cast<uint32_t>(b) << 16); }
 
@@ -79,6 +86,10 @@ template <>
 __device__ __forceinline__ void st_elem<float>(float* p, float v) { *p = v; }
 template <>
 __device__ __forceinline__ void st_elem<uint16_t>(uint16_t* p, float v) { *p = f2bf(v); }
+template <>
+__device__ __forceinline__ void st_elem<f16_t>(f16_t* p, float v) {
+  p->v = __builtin_bit_cast(uint16_t, static_cast<_Float16>(v));  // RNE
+}
 
 // 16-byte chunk <-> floats (4 f32 or 8 bf16)
 template <typename T>

@@ -17,7 +17,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 # VM_LIB_PATH: an alternative build of the same library (same-box A/B timing runs); never a fallback
 LIB_PATH = os.environ.get("VM_LIB_PATH") or os.path.join(HERE, "libvmatting.so")
 
-VM_F32, VM_BF16, VM_U8, VM_F64 = 0, 1, 2, 3
+VM_F32, VM_BF16, VM_U8, VM_F64, VM_F16 = 0, 1, 2, 3, 4
 ACT = {"none": 0, "relu": 1, "sigmoid": 2, "softmax": 3}
 VM_OK, VM_EINVAL, VM_EUNSUPPORTED, VM_EHIP, VM_EINDEX = 0, -1, -2, -3, -4
 ABI_VERSION = 1
@@ -89,6 +89,8 @@ SIGNATURES = [
     ("vm_conv3x3_head_nhwc", c_int, [P, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, P, c_void_p,
                                      c_void_p]),
     ("vm_conv3x3_head_acc_nhwc", c_int, [P, c_void_p, c_int, c_void_p, c_void_p, P, c_void_p, c_void_p]),
+    ("vm_conv3x3_head_acc_ex_nhwc", c_int, [P, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, P, c_void_p,
+                                            c_void_p]),
     ("vm_conv3x3_pair_first_nhwc", c_int, [P, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p,
                                            c_void_p, c_int, P, P, c_void_p]),
     ("vm_conv3x3_pair_first_mid_nhwc", c_int, [P, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p,
@@ -109,6 +111,7 @@ SIGNATURES = [
     ("vm_resize_bilinear_tf1_nhwc", c_int, [P, P, c_void_p]),
     ("vm_convert_nhwc", c_int, [P, P, c_void_p, c_void_p, c_int, c_void_p]),
     ("vm_split6_nhwc", c_int, [P, P, P, c_void_p]),
+    ("vm_split3h_nhwc", c_int, [P, P, P, c_int, c_void_p, c_void_p]),
     ("vm_bn_workspace_bytes", c_size_t, [P]),
     ("vm_bn_stats_nhwc", c_int, [P, c_void_p, c_void_p, c_void_p, c_void_p]),
     ("vm_bn_apply_nhwc", c_int, [P, P, c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_int, c_void_p]),

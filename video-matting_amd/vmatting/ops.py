@@ -15,9 +15,10 @@ import torch
 from . import _lib
 from ._lib import VmTensor, check, lib, stream_handle
 
-_DT = {torch.float32: _lib.VM_F32, torch.bfloat16: _lib.VM_BF16, torch.uint8: _lib.VM_U8}
+_DT = {torch.float32: _lib.VM_F32, torch.bfloat16: _lib.VM_BF16, torch.uint8: _lib.VM_U8,
+       torch.float16: _lib.VM_F16}  # (fp16: the split-fp16 x3 conv operands only, vmatting/split3.py)
 TORCH_DTYPE = {"fp32": torch.float32, "f32": torch.float32, "float32": torch.float32,
-               "bf16": torch.bfloat16, "bfloat16": torch.bfloat16}
+               "bf16": torch.bfloat16, "bfloat16": torch.bfloat16, "f16": torch.float16}
 
 
 def _require_gpu(t):

@@ -1,0 +1,222 @@
+"""unet.py's forward at f32 accuracy in three fp16 MFMA products per conv: the split-fp16 x3 path
+(``UNetVideo(dtype="f16x3")``).
+
+north_star asks for alpha within 1e-4 of the reference's CPU forward (unet.py:161-205).  The split-bf16 x6 path
+(split6.py) gets there with SIX bf16 products per conv, because a bf16 part holds 8 significant bits and two parts
+(16 bits; x3 = hh + hl + lh) leave alpha 7.3e-4 off on the timed frame.  An fp16 part holds 11 bits, so two parts
+hold 22:
+
+    x = h + l,  h = fp16(x), l = fp16(x - h)          (the difference is exact in f32)
+    W * 2^t = Wh + Wl                                  (t per filter: max |W * 2^t| just under 2^12)
+    y = (l*Wh + h*Wl + h*Wh) * 2^-t                    (exact fp16 x fp16 products, f32 accumulation)
+
+The dropped l*Wl term and the parts' residuals are ~2^-22 of h*Wh, 64x below bf16 x3's.  A float64 emulation of the
+whole 1080p forward on the bench's frame and weights (tools/split_emulate.py) puts alpha 1.9e-5 from the exact
+forward (logits 4.0e-7 relative), bf16 x3 7.3e-4.  The filter scale keeps the small parts Wl in fp16's normal range
+(He-normal filters are ~0.01-0.1, so their unscaled low parts would be subnormal); it is a power of two, so the
+epilogue's ``* 2^-t`` is exact (the conv's per-channel scale; the bias rides in the shift).  Activations stay
+unscaled: |x| on this network is ~2e3 against fp16's 65504; a split that meets |x| >= 65520 sets an overflow flag
+(``overflowed()``), and ``UNet.build`` then re-runs the frames on the bf16x6 path.
+
+Cost: 3x the MFMA work of the bf16 forward (x6: 6x) on the same patch kernels (their fp16 MFMA form,
+v_mfma_f32_16x16x32_f16), plus one split pass per activation.  Layout: a split buffer holds slabs [l, h, h] of its
+S channels at p*S + c (S = the concat width), so the [up, skip] concats are channel ranges written by their own
+producers, as in split6.py.  conv1_1's 7-channel frame is split into slabs of 16 (64 channels, the 4th slab zero:
+two whole 32-channel granules).  conv1_5 (cout 1) is two MFMA-head chunks [l | h] (256 channels) and [h] (128), the
+second adding the first's logits and undoing the filter scale before the sigmoid.
+"""
+
+import numpy as np
+import torch
+
+from . import ops
+
+# slab order of the activations and the filter parts they meet: l*Wh, h*Wl, h*Wh
+W_PARTS = (0, 1, 0)  # index into (Wh, Wl)
+WTOP = 12  # filter scale: max |W * 2^t| in (2^11, 2^12]
+
+# (conv scope, channels of its split input (the concat width), output channels)
+LAYERS = (("conv1_1", 16, 64), ("conv1_2", 64, 64), ("conv2_1", 64, 128), ("conv2_2", 128, 128),
+          ("conv3_1", 128, 256), ("conv3_2", 256, 256), ("conv3_3", 256, 256), ("conv4_1", 256, 512),
+          ("conv4_2", 512, 512), ("conv4_3", 512, 512), ("conv5_1", 512, 512), ("conv5_2", 512, 512),
+          ("upconv_1", 512, 512), ("conv4_4", 1024, 512), ("upconv_2", 512, 256), ("conv3_4", 512, 256),
+          ("upconv_3", 256, 128), ("conv2_3", 256, 128), ("upconv_4", 128, 64), ("conv1_5", 128, 1))
+
+
+def filter_scale(w):
+    """2^t putting max |w * 2^t| in (2^(WTOP-1), 2^WTOP] (1 for an all-zero filter)."""
+    m = float(np.abs(np.asarray(w, np.float64)).max())
+    if m == 0.0:
+        return 1.0
+    return 2.0 ** (WTOP - int(np.ceil(np.log2(m))))
+
+
+def split2h(w):
+    """f32 -> (h, l): h = fp16(w), l = fp16(w - h) (RNE), returned as f32 holding fp16 values exactly."""
+    w = torch.as_tensor(w, dtype=torch.float32)
+    h = w.half().float()
+    lo = (w - h).half().float()
+    return h, lo
+
+
+def split3_filter(w_hwio, cin, cout, t):
+    """[3,3,ci,co] f32 filter, scale 2^t -> the [3,3,3*cin,cout] stack of the parts of w * 2^t in slab order (zero rows
+    past ci, zero columns past co)."""
+    w = torch.as_tensor(np.asarray(w_hwio, np.float32), dtype=torch.float32) * float(t)  # exact: a power of two
+    ci, co = int(w.shape[2]), int(w.shape[3])
+    parts = split2h(w)
+    out = torch.zeros((3, 3, 3 * cin, cout), dtype=torch.float32)
+    for p, k in enumerate(W_PARTS):
+        out[:, :, p * cin:p * cin + ci, :co] = parts[k]
+    return out
+
+
+def split3h(x, y, pool=None, slab=0, overflow=None):
+    """vm_split3h_nhwc: f32 view x -> its [l, h, h] slabs in the fp16 view y (a channel range of a 3*S-wide buffer,
+    S = ``slab`` or y's concat width), optionally the split of its 2x2 SAME max-pool into ``pool``; ``overflow`` (a
+    device int32) is set to 1 where |x| >= 65520."""
+    xv, yv = ops.nhwc(x), ops.nhwc(y)
+    pv = ops.nhwc(pool) if pool is not None else None
+    ref = (lambda v: None if v is None else ops.ctypes.byref(v))
+    ops.check(ops.lib().vm_split3h_nhwc(ref(xv), ref(yv), ref(pv), int(slab), ops._ptr(overflow),
+                                        ops.stream_handle()), "split3h")
+    return y
+
+
+def whole(buf):
+    """The split-layout view of all channels of a 3*S-wide split buffer."""
+    return buf[..., :buf.shape[-1] // 3]
+
+
+def seg(buf, off, c):
+    """Channels [off, off + c) of a 3*S-wide split buffer (split3h writes the 3 slabs at p*S + off)."""
+    return buf[..., off:off + c]
+
+
+class Split3Forward:
+    """The split-fp16 x3 forward of a UNet (unet.UNetVideo / UNetImage) with its parameters."""
+
+    def __init__(self, model):
+        self.m = model
+        self.dev = model.device
+        self.convs = {}
+        self.scales = {}
+        for name, cin, cout in LAYERS:
+            w, b = model.params[name]
+            t = filter_scale(w)
+            self.scales[name] = t
+            if name == "conv1_5":
+                # [l | h] against [Wh | Wl] (256 channels), then [h] against [Wh] adding the first chunk's logits
+                wf = split3_filter(w, cin, 1, t)
+                self.head = [ops.PackedConv(wf[:, :, :256].contiguous(), None, "f16", self.dev),
+                             ops.PackedConv(wf[:, :, 256:].contiguous(), None, "f16", self.dev,
+                                            scale=np.full(1, 1.0 / t, np.float32),
+                                            shift=np.zeros(1, np.float32) if b is None else b)]
+                self.convs[name] = self.head[1]
+                continue
+            cp = cin
+            if name == "conv1_1":
+                cp = 16  # slabs of 16 (8 live) + a zero 4th slab: 64 channels, two whole 32-channel granules
+            wf = split3_filter(w, cp, cout, t)
+            if name == "conv1_1":
+                wf = torch.cat([wf, torch.zeros((3, 3, 16, cout))], 2)
+            # epilogue (acc * 2^-t) + b: exact descale, then the bias (unet.py:41,73)
+            self.convs[name] = ops.PackedConv(wf, None, "f16", self.dev, scale=np.full(cout, 1.0 / t, np.float32),
+                                              shift=np.zeros(cout, np.float32) if b is None else b)
+        self.overflow = torch.zeros(1, dtype=torch.int32, device=self.dev)
+        self._b, self._key = None, None
+        self.logits = None
+
+    def weights_flat(self):
+        out = []
+        for pc in [self.convs[k] for k in sorted(self.convs) if k != "conv1_5"] + self.head:
+            out.append(pc.packed)
+            for t in (pc.bias, pc.scale, pc.shift):
+                if t is not None:
+                    out.append(t)
+        return out
+
+    def _buffers(self, n, h, w):
+        if self._key == (n, h, w):
+            return self._b
+        from .unet import _levels
+        L = _levels(h, w)
+        dev = self.dev
+        S = lambda lv, c: torch.empty((n, L[lv][0], L[lv][1], 3 * c), dtype=torch.float16, device=dev)  # noqa
+        F = lambda lv, c: torch.empty((n, L[lv][0], L[lv][1], c), dtype=torch.float32, device=dev)  # noqa
+        b = {"x": torch.zeros((n, L[0][0], L[0][1], 64), dtype=torch.float16, device=dev),
+             "s11": S(0, 64), "cat1": S(0, 128), "r4": S(0, 128),
+             "p1": S(1, 64), "s21": S(1, 128), "cat2": S(1, 256), "r3": S(1, 256),
+             "p2": S(2, 128), "s31": S(2, 256), "s32": S(2, 256), "cat3": S(2, 512), "r2": S(2, 512),
+             "p3": S(3, 256), "s41": S(3, 512), "s42": S(3, 512), "cat4": S(3, 1024), "r1": S(3, 512),
+             "p4": S(4, 512), "s51": S(4, 512),
+             "f0": F(0, 128), "f1": F(1, 256), "f2": F(2, 512), "f3": F(3, 512), "f4": F(4, 512),
+             "rr0": F(0, 128), "rr1": F(1, 256), "rr2": F(2, 512), "rr3": F(3, 512),
+             "lg0": F(0, 1), "out": F(0, 1)}
+        self._b, self._key = b, (n, h, w)
+        return b
+
+    def overflowed(self):
+        """True when a split of the last forward(s) since reset met |x| >= 65520 (synchronises)."""
+        return bool(self.overflow.item())
+
+    def forward(self, x, out=None):
+        """x: [N,H,W,C] f32 frames (C = 7 video / 6 image) -> alpha [N,H,W,1] f32 (``out`` if given)."""
+        from .unet import _levels
+        n, h, w, c = x.shape
+        b = self._buffers(n, h, w)
+        L = _levels(h, w)
+        C = self.convs
+        ovf = self.overflow
+        ovf.zero_()
+        split3h(x, b["x"][..., :8], slab=16, overflow=ovf)  # slabs [l, h, h] of 16 channels, 8 written
+
+        def conv(src, name, dst_f32, act="relu"):
+            return ops.conv3x3(src, C[name], act, out=dst_f32, splitk=True)
+
+        def sp(f, y, pool=None):
+            return split3h(f, y, pool, overflow=ovf)
+
+        def resize_split(f_src, lv, rr_f32, r_split):
+            ops.resize_bilinear(f_src, L[lv], out=rr_f32)
+            sp(rr_f32, r_split)
+
+        f0, f1, f2, f3, f4 = b["f0"], b["f1"], b["f2"], b["f3"], b["f4"]
+        # encoder (unet.py:170-189)
+        sp(conv(b["x"], "conv1_1", f0[..., :64]), whole(b["s11"]))
+        sp(conv(b["s11"], "conv1_2", f0[..., :64]), seg(b["cat1"], 64, 64), pool=whole(b["p1"]))
+        sp(conv(b["p1"], "conv2_1", f1[..., :128]), whole(b["s21"]))
+        sp(conv(b["s21"], "conv2_2", f1[..., :128]), seg(b["cat2"], 128, 128), pool=whole(b["p2"]))
+        sp(conv(b["p2"], "conv3_1", f2[..., :256]), whole(b["s31"]))
+        sp(conv(b["s31"], "conv3_2", f2[..., :256]), whole(b["s32"]))
+        sp(conv(b["s32"], "conv3_3", f2[..., :256]), seg(b["cat3"], 256, 256), pool=whole(b["p3"]))
+        sp(conv(b["p3"], "conv4_1", f3), whole(b["s41"]))
+        sp(conv(b["s41"], "conv4_2", f3), whole(b["s42"]))
+        sp(conv(b["s42"], "conv4_3", f3), seg(b["cat4"], 512, 512), pool=whole(b["p4"]))
+        sp(conv(b["p4"], "conv5_1", f4), whole(b["s51"]))
+        y52 = conv(b["s51"], "conv5_2", f4)
+        # decoder: resize (f32) -> split -> conv (no bias, no relu) into the concat's up range (unet.py:191-200)
+        resize_split(y52, 3, b["rr3"], whole(b["r1"]))
+        sp(conv(b["r1"], "upconv_1", f3, act="none"), seg(b["cat4"], 0, 512))
+        y44 = conv(b["cat4"], "conv4_4", f3)
+        resize_split(y44, 2, b["rr2"], whole(b["r2"]))
+        sp(conv(b["r2"], "upconv_2", f2[..., :256], act="none"), seg(b["cat3"], 0, 256))
+        y34 = conv(b["cat3"], "conv3_4", f2[..., :256])
+        resize_split(y34, 1, b["rr1"], whole(b["r3"]))
+        sp(conv(b["r3"], "upconv_3", f1[..., :128], act="none"), seg(b["cat2"], 0, 128))
+        y23 = conv(b["cat2"], "conv2_3", f1[..., :128])
+        resize_split(y23, 0, b["rr0"], whole(b["r4"]))
+        sp(conv(b["r4"], "upconv_4", f0[..., :64], act="none"), seg(b["cat1"], 0, 64))
+        # conv1_5 + sigmoid (unet.py:203-205): [l | h] x [Wh | Wl], then [h] x [Wh] + those logits, * 2^-t + bias
+        alpha = b["out"] if out is None else out
+        lg0 = b["lg0"]
+        logits = f0[..., :1]
+        for k, (xs, yv, acc) in enumerate(((b["cat1"][..., :256], lg0, None), (b["cat1"][..., 256:], logits, lg0))):
+            pc = self.head[k]
+            xv, yvv = ops.nhwc(xs), ops.nhwc(yv)
+            ops.check(ops.lib().vm_conv3x3_head_acc_ex_nhwc(
+                ops.ctypes.byref(xv), ops._ptr(pc.packed), xs.shape[-1], None, ops._ptr(pc.scale),
+                ops._ptr(pc.shift), ops._ptr(acc), ops.ctypes.byref(yvv), ops._ptr(alpha if k == 1 else None),
+                ops.stream_handle()), "conv3x3_head_acc_ex")
+        self.logits = logits
+        return alpha

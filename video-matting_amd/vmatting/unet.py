@@ -76,10 +76,13 @@ class UNet:
 
     def __init__(self, vgg16_npy_path=None, dtype="bf16", device="cuda"):
         self.data_dict = load_vgg16(vgg16_npy_path)
-        # "bf16x6": the split-bf16 x6 path (vmatting/split6.py) — f32 accuracy on the bf16 MFMA kernels
-        self.x6mode = dtype == "bf16x6"
+        # split-operand paths at f32 accuracy on the 16-bit MFMA kernels: "bf16x6" (vmatting/split6.py, six bf16
+        # products per conv) and "f16x3" (vmatting/split3.py, three fp16 products per conv)
+        self.split_mode = dtype if dtype in ("bf16x6", "f16x3") else None
+        self.x6mode = self.split_mode is not None
         self._x6 = None
-        self.dtype = torch.bfloat16 if self.x6mode else (ops.TORCH_DTYPE[dtype] if isinstance(dtype, str) else dtype)
+        self.dtype = ({"bf16x6": torch.bfloat16, "f16x3": torch.float16}[dtype] if self.x6mode else
+                      (ops.TORCH_DTYPE[dtype] if isinstance(dtype, str) else dtype))
         self.device = torch.device(device)
         self.params = None       # name -> (w_hwio f32 np, bias f32 np | None)
         self.convs = None        # name -> ops.PackedConv
@@ -124,8 +127,12 @@ class UNet:
 
     def _pack(self):
         if self.x6mode:
-            from .split6 import Split6Forward
-            self._x6 = Split6Forward(self)
+            if self.split_mode == "f16x3":
+                from .split3 import Split3Forward
+                self._x6 = Split3Forward(self)
+            else:
+                from .split6 import Split6Forward
+                self._x6 = Split6Forward(self)
             self.convs = self._x6.convs
             self._head_up = None
             return
@@ -190,8 +197,20 @@ class UNet:
         x = self._as_input(input)
         self.prepare()
         self.forward(x)
+        if self.split_mode == "f16x3" and self._x6.overflowed():
+            # an activation left fp16's range (|x| >= 65520): these frames take the bf16x6 path (f32 range)
+            from .split6 import Split6Forward
+            self.split_mode, self.dtype = "bf16x6", torch.bfloat16
+            self._x6 = Split6Forward(self)
+            self.convs = self._x6.convs
+            self.forward(x)
         self.data_dict = None  # unet.py:147,207
         return self.output
+
+    def overflowed(self):
+        """f16x3: whether a split since the last forward began met |x| >= 65520 (its alpha is then invalid and the
+        frames belong on the bf16x6 path); synchronises.  False on the other paths."""
+        return self.split_mode == "f16x3" and self._x6 is not None and self._x6.overflowed()
 
     def _as_input(self, input):
         x = input if isinstance(input, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(input, np.float32))
@@ -209,7 +228,7 @@ class UNet:
                                           input.dtype == torch.float32) else input
         if self.convs is None:
             raise RuntimeError("call build() first")
-        if self._x6 is not None:  # split-bf16 x6: only .output and .conv1_3 (the logits) are kept
+        if self._x6 is not None:  # split paths (bf16x6 / f16x3): only .output and .conv1_3 (the logits) are kept
             alpha = self._x6.forward(x, out)
             self._x, self._ws, self._ws_key = x, self._x6._b, self._x6._key
             self.conv1_3, self.output = self._x6.logits, alpha
@@ -418,13 +437,17 @@ class GraphedForward:
         self._ws, self._ws_key = model._ws, model._ws_key
         self._skip_valid = model._skip_valid
         self._up_valid = model._up_valid
+        self._logits = model.conv1_3 if model._x6 is not None else None
 
     def replay(self):
         self.graph.replay()
         m = self.model
         if m._ws is not self._ws:  # the model ran another shape since: its attributes follow this replay
             m._ws, m._ws_key = self._ws, self._ws_key
-            m._publish(self._ws)
+            if m._x6 is None:
+                m._publish(self._ws)
+        if m._x6 is not None:
+            m.conv1_3 = self._logits
         m._x, m._c11, m._in8_valid, m._skip_valid = self.input, None, False, self._skip_valid
         m._up_valid = self._up_valid
         m.output = self.output
