@@ -330,12 +330,24 @@ def fp32_record(model, x, steps, vgg, params):
     return rec, m32
 
 
-def x6_record(x, steps, vgg, params):
-    """The split-bf16 x6 path (vmatting/split6.py: every conv operand as three bf16 parts, the six cross products
-    on the bf16 MFMA kernels with f32 epilogues) at 1080p: the path that meets north_star's 1e-4 alpha bound faster
-    than exact-f32 MFMA.  Graph-replayed forward over `steps` frames; roofline over the 6x products it issues."""
-    m6 = unet.UNetVideo(vgg, dtype="bf16x6", device=x.device).load_params(params).prepare()
-    g = m6.capture(x)
+SPLIT_DESC = {
+    "bf16x6": ("split-bf16 x6 (three bf16 parts per operand, 6 cross products on v_mfma_f32_16x16x32_bf16, f32 sums)",
+               6),
+    "f16x3": ("split-fp16 x3 (two fp16 parts per operand, the filter pre-scaled by a power of two; l*Wh + h*Wl + h*Wh "
+              "on v_mfma_f32_16x16x32_f16, f32 sums)", 3),
+}
+
+
+def split_record(x, steps, vgg, params, mode):
+    """A split-operand path (vmatting/split6.py "bf16x6", vmatting/split3.py "f16x3": conv operands carried as
+    16-bit parts whose cross products are exact, f32 epilogues) at 1080p — the paths that meet north_star's 1e-4
+    alpha bound on the 16-bit MFMA pipes.  Graph-replayed forward over `steps` frames.  roofline: the ALGORITHMIC
+    conv FLOPs (2*H*W*9*cin*cout, 3.233 TFLOP per frame) over the whole forward's time at the bf16 dense peak
+    (what the path delivers); executed_products: the products the MFMA pipes run (k x those FLOPs) over the convs'
+    own launch time (how busy the pipes are)."""
+    desc, k = SPLIT_DESC[mode]
+    m = unet.UNetVideo(vgg, dtype=mode, device=x.device).load_params(params).prepare()
+    g = m.capture(x)
     g.replay()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -344,21 +356,28 @@ def x6_record(x, steps, vgg, params):
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / steps
     prof = ops.conv_profile(True)
-    m6.forward(x)
+    m.forward(x)
     torch.cuda.synchronize()
     ops.conv_profile(False)
     fl = sum(p[0] for p in prof)
     t = sum(ms(p[2], p[3]) for p in prof)
-    flops = m6.conv_flops(x.shape[0], x.shape[1], x.shape[2])
-    rec = {"workload": "unet.UNetVideo forward, split-bf16 x6 (three bf16 parts per operand, 6 cross products on "
-                       "v_mfma_f32_16x16x32_bf16, f32 sums), 1920x1080, hip-graph replay",
+    flops = m.conv_flops(x.shape[0], x.shape[1], x.shape[2])
+    pk = PEAK_TFLOPS["bf16"]
+    algo = flops / dt / 1e12
+    rec = {"workload": "unet.UNetVideo forward, %s, 1920x1080, hip-graph replay" % desc,
            "frames_per_s": round(x.shape[0] / dt, 3), "ms_per_frame": round(1e3 * dt / x.shape[0], 3),
-           "tflops_whole_forward": round(flops / dt / 1e12, 2),
-           "roofline": {"bound": "mfma", "achieved": round(fl / (t * 1e-3) / 1e12, 2), "peak": PEAK_TFLOPS["bf16"],
-                        "unit": "TFLOP/s", "frac": round(fl / (t * 1e-3) / 1e12 / PEAK_TFLOPS["bf16"], 4),
-                        "scope": "all convs of one forward (HIP events per launch), counting the 6x products "
-                                 "(the conv over 6 stacked channel slabs) the MFMA pipes execute"}}
-    return rec, m6
+           "tflops_whole_forward": round(algo, 2),
+           "roofline": {"bound": "mfma", "achieved": round(algo, 2), "peak": pk, "unit": "TFLOP/s",
+                        "frac": round(algo / pk, 4),
+                        "scope": "algorithmic conv FLOPs of the forward (3.233 TFLOP per 1080p frame) over the whole "
+                                 "forward's time (graph replay) at the bf16 dense peak"},
+           "executed_products": {"tflops": round(fl / (t * 1e-3) / 1e12, 2), "frac": round(fl / (t * 1e-3) / 1e12 / pk, 4),
+                                 "conv_ms": round(t, 3), "products_per_algorithmic_flop": k,
+                                 "scope": "the %dx products the MFMA pipes execute (the conv over %d stacked operand "
+                                          "slabs) over the convs' own launch time (HIP events per launch)" % (k, k)}}
+    if mode == "f16x3":
+        rec["overflow"] = m.overflowed()  # an activation past fp16's range would void the frame (bf16x6 fallback)
+    return rec, m
 
 
 # ------------------------------------------------------------------------------------------------ loader / augment
@@ -465,7 +484,7 @@ def augment_bench(dev, steps, threads, cpu=True, h=1080, w=1920, batch=8):
     dev_ms = sum(ms(a, b) for a, b in kev) / steps / batch
     # algorithmic bytes per sample (per pixel): alpha stats 8; bg 2 warps 2*(3+3); TPS grid (h/2)(w/2)*16 = 4;
     # fg TPS 3+3, alpha TPS 8+8; fg 2 warps 2*(3+3); alpha 2 warps 2*(8+8); illumination fg+bg 2*(3+3)
-    algo = h * w * (8 + 12 + 4 + 6 + 16 + 12 + 32 + 12)
+    algo = augment_bytes(h, w)
     rec = {"workload": "augmentation.augment: %dx%d samples (u8 fg/bg, f64 alpha), %d per augment_many call, inputs in "
                        "HBM; per-sample figures" % (w, h, batch),
            "algorithmic_bytes_def": "the reference's passes (stats, two warpAffine per image, TPS lattice + resampling, "
@@ -509,6 +528,57 @@ def train_flops(n, h, w):
     head = sum(f(lvl[s], ci, co) for s, ci, co in NEW_CONVS)
     dgrad = sum(f(lvl[s], ci, co) for s, ci, co in NEW_CONVS if s in DGRAD)
     return fwd + head, head + dgrad
+
+
+def train_step_traffic(n, h, w, dtype_bytes=2):
+    """Algorithmic HBM bytes of the memory-bound part of one config-5 step (unet_simple.py:116-142 at phase=True,
+    train.py:288-304), the way small_train_traffic counts small_train.py's: the select convs read every tower
+    feature level twice (forward, and again for their filter gradients) — the concat of the three towers, in the
+    compute dtype; every decoder tensor (1-96 channels: select / upconv / conv pre-BN outputs in f32, BN'd
+    activations and resized inputs in the compute dtype) written once and read once per consumer, and their f32
+    gradients likewise; the trainable parameters, gradients and Adam slots once.  The tower convs themselves (their
+    activations included) are the MFMA-bound part, priced by train_flops."""
+    from vmatting.train import param_layout
+    from vmatting.unet_simple import _levels
+    L = _levels(h, w)
+    px = [n * a * b for a, b in L]
+    T, F = dtype_bytes, 4
+    # tower features the select convs read (unet_simple.py:153-168: cmp | bg | diff per level; in9 = the 9-channel
+    # input concat at L0), and conv5_3's concat that upconv4 resizes
+    feats = [(0, 9 + 3 * 64 + 3 * 64), (1, 3 * 128 * 2), (2, 3 * 256 * 3), (3, 3 * 512 * 3), (4, 3 * 512)]
+    tower = sum(px[lv] * c * T * 2 for lv, c in feats)
+    # per level (selects k x nsel, upconv cout u, concat width W, conv cout c, the upconv's input width ci at lv+1)
+    lvls = [(3, 48, 48, 96, 48, None), (2, 24, 24, 48, 24, 48), (1, 8, 24, 32, 32, 24), (0, 6, 24, 30, 32, 32)]
+    dec = 0
+    for lv, sel, u, W, c, ci in lvls:
+        ent = [(lv, sel, F, 2), (lv, u, F, 2),             # select / upconv pre-BN outputs (stats + apply)
+               (lv, W, T, 1 + 1),                          # BN'd concat: conv input + its filter gradient
+               (lv, c, F, 2), (lv, c, T, 2)]               # conv pre-BN output, its BN'd relu activation
+        if ci is not None:
+            ent.append((lv, ci, T, 2))                     # the resized upconv input (conv + filter gradient)
+        grads = [(lv, W, F, 2), (lv, c, F, 2), (lv, u, F, 1), (lv, sel, F, 1)]  # dconcat, dconv, dupconv, dselect
+        reread = [(lv, sel + u + c, F, 1)]                 # the BN backward re-reads its pre-BN inputs
+        dec += sum(px[l] * ch * b * (1 + r) for l, ch, b, r in ent + grads) + sum(px[l] * ch * b for l, ch, b, _ in
+                                                                                     reread)
+    dec += px[0] * (1 * F * 3 + 1 * F * 2 + 3 * 4 * 3 + 1 * 4 * 2)  # output conv, alpha, the loss's inputs, dalpha
+    nparam = param_layout()[1]
+    return tower + dec + nparam * 4 * (1 + 1 + 2 + 2)
+
+
+def step_roofline(flops, nbytes, dev_ms, peak_tflops):
+    """Two-part roofline of a step: its MFMA-bound convs at the dense peak plus its memory-bound work at the HBM peak
+    (dependent phases: the sum is the bound), over the measured device time."""
+    t_mfma = flops / (peak_tflops * 1e12) * 1e3
+    t_hbm = nbytes / (PEAK_HBM_GBPS * 1e9) * 1e3
+    rl = t_mfma + t_hbm
+    return {"bound": "mfma+hbm", "roofline_ms": round(rl, 4), "measured_device_ms": round(dev_ms, 4),
+            "frac": round(rl / dev_ms, 4), "mfma_ms": round(t_mfma, 4), "hbm_ms": round(t_hbm, 4),
+            "flops": int(flops), "algorithmic_bytes": int(nbytes), "peak_tflops": peak_tflops,
+            "peak_gbps": PEAK_HBM_GBPS, "achieved_tflops": round(flops / (dev_ms * 1e-3) / 1e12, 2),
+            "frac_max": round(max(t_mfma, t_hbm) / dev_ms, 4),
+            "def": "roofline_ms = algorithmic conv FLOPs / dense MFMA peak + algorithmic bytes of the memory-bound work "
+                   "/ 8 TB/s (phases in sequence); frac = roofline_ms / measured device ms; frac_max uses the larger "
+                   "of the two instead (perfect overlap)"}
 
 
 def train_bench(dev, steps, warmup, world, rank, threads, cpu=True, n=8, size=320, dtype="bf16", graph=False,
@@ -580,6 +650,8 @@ def train_bench(dev, steps, warmup, world, rank, threads, cpu=True, n=8, size=32
                          "allreduce_adam_repack": round(ph[2], 3)},
            "flops_per_step_per_gpu": {"forward": fwd_f, "backward": bwd_f},
            "achieved_tflops_per_gpu": round((fwd_f + bwd_f) / wall / 1e12, 1),
+           "roofline": step_roofline(fwd_f + bwd_f, train_step_traffic(n, size, size, 2 if dtype == "bf16" else 4),
+                                     sum(ph), PEAK_TFLOPS[dtype]),
            "loss_last": [round(float(v), 5) for v in trn._tb["loss"].cpu()]}
     if cpu and world == 1:
         from oracle import models as om  # the CPU-baseline leg only
@@ -900,6 +972,72 @@ def train_chain_bench(dev, steps, warmup, n=8, size=320, h=1080, w=1920, dtype="
                                             "eager with the select chains on side streams"),
             "decode": "none: synthetic source images resident in HBM (PNG/JPEG decoding is host I/O outside the path)",
             "loss_last": [round(float(v), 5) for v in loss.cpu()]}
+
+
+def augment_bytes(h, w):
+    """augment_bench's algorithmic bytes of one augmentation.augment sample (per pixel: alpha stats 8; bg two warps
+    2*(3+3); TPS grid (h/2)(w/2)*16 = 4; fg TPS 3+3, alpha TPS 8+8; fg two warps 2*(3+3); alpha two warps 2*(8+8);
+    illumination fg+bg 2*(3+3))."""
+    return h * w * (8 + 12 + 4 + 6 + 16 + 12 + 32 + 12)
+
+
+def chain_roofline_and_baseline(rec, n, size, h, w, dtype, threads, cpu):
+    """train.chained's roofline and CPU baseline: the pipeline's algorithmic work per batch —
+    augment of n 1080p sources + the loader's per-pixel work + one config-5 step (its MFMA FLOPs and memory-bound
+    bytes) — at the MFMA / HBM peaks, over the measured wall time per step (the phases overlap on two streams, so
+    wall, not a phase sum, is what the roofline is compared with).  CPU baseline: the oracle's augment of one 1080p
+    source, the oracle loader on one 1080p video entry and oracle/train_ref's step on one 320^2 sample, in turn."""
+    fwd_f, bwd_f = train_flops(n, size, size)
+    nbytes = (n * augment_bytes(h, w) + n * size * size * 13 * 4 + n * 4 * size * size * (4 + 8 + 4 + 3)
+              + train_step_traffic(n, size, size, 2 if dtype == "bf16" else 4))
+    rl = step_roofline(fwd_f + bwd_f, nbytes, rec["ms_per_step"], PEAK_TFLOPS[dtype])
+    rl["def"] = ("roofline_ms = the step's algorithmic conv FLOPs / dense MFMA peak + (augment of %d 1080p sources + "
+                 "loader per-pixel bytes + the step's memory-bound bytes) / 8 TB/s; frac = roofline_ms / measured "
+                 "wall ms per step (augment + loader of batch k+1 overlap step k)" % n)
+    rl.pop("measured_device_ms")
+    rl["measured_wall_ms"] = rec["ms_per_step"]
+    rec["roofline"] = rl
+    if not cpu:
+        return rec
+    from oracle import augment as oa  # the CPU-baseline leg only
+    from oracle import loader as ol
+    from oracle import models as om
+    from oracle import train_ref as tr
+    rs = np.random.RandomState(13)
+    yy, xx = np.mgrid[0:h, 0:w]
+    al = np.clip(1.2 - np.sqrt(((yy - 0.4 * h) / (0.28 * h)) ** 2 + ((xx - 0.47 * w) / (0.21 * w)) ** 2), 0, 1)
+    fg = (rs.rand(h, w, 3) * 255).astype(np.uint8)
+    bg = (rs.rand(h, w, 3) * 255).astype(np.uint8)
+    np.random.seed(0)
+    t0 = time.perf_counter()
+    oa.augment(fg, bg, al)
+    t_aug = time.perf_counter() - t0
+    ent = loader_inputs(1, h, w)[0]
+    np.random.seed(0)
+    from vmatting import loader as vl
+    plan = vl.plan_crop((h, w), (h, w))
+    t0 = time.perf_counter()
+    fr, fc, br, bc = (ol.Axis(*a) for a in plan)
+    srcs = ol.crop_sources(ent["fg"], ent["bg"], fr, fc, br, bc, ent["prev"], ent["flow"])
+    ol.compose(srcs[0], srcs[1], srcs[3], (size, size), srcs[2])
+    t_ldr = time.perf_counter() - t0
+    mean = np.array(VGG_MEAN)
+    rs = np.random.RandomState(100)
+    f1 = rs.uniform(0, 255, (1, size, size, 3))
+    b1 = rs.uniform(0, 255, (1, size, size, 3))
+    g1 = rs.uniform(0, 1, (1, size, size, 1))
+    c1 = g1 * f1 + (1 - g1) * b1 - mean
+    p = om.unet_simple_params(np.random.RandomState(1))
+    t0 = time.perf_counter()
+    tr.train_step_grads(c1, b1 - mean, np.repeat(g1, 3, -1), g1, f1, synthetic_vgg16(0), p)
+    t_step = time.perf_counter() - t0
+    tot = t_aug + t_ldr + t_step
+    rec["cpu_baseline"] = {"value": round(1.0 / tot, 5), "unit": "samples/s", "cores": threads, "kind": "port",
+                           "sample": "one sample through the oracle chain in turn: oracle/augment.py augment of one "
+                                     "%dx%d source (%.2f s), oracle/loader.py crop + warp + resize + composite of one "
+                                     "%dx%d video entry to %dx%d (%.2f s), oracle/train_ref.py step of one %dx%d "
+                                     "sample (%.2f s)" % (w, h, t_aug, w, h, size, size, t_ldr, size, size, t_step)}
+    return rec
 
 
 def _train_chain_overlap(dev, steps, warmup, trn, batch, alphas, n, size, names, dtype, graph, profiler=None):
@@ -1232,8 +1370,9 @@ def main():
             rec = train_bench(dev, args.steps, args.warmup, world, rank, threads, cpu=False, graph=args.train_graph,
                               streams=args.train_streams, wgrad_stream=bool(args.train_wgrad_stream))
         elif args.only == "train_chain":
-            rec = train_chain_bench(dev, args.steps, args.warmup, graph=args.train_graph, overlap=not args.chain_serial,
-                                    prio=args.chain_prio)
+            rec = chain_roofline_and_baseline(
+                train_chain_bench(dev, args.steps, args.warmup, graph=args.train_graph, overlap=not args.chain_serial,
+                                  prio=args.chain_prio), 8, 320, 1080, 1920, "bf16", threads, False)
         elif args.only == "train_small":
             rec = train_small_bench(dev, args.steps, args.warmup, world, rank, threads, cpu=False)
         elif args.only == "train_image":
@@ -1314,8 +1453,9 @@ def main():
                             graph=args.train_graph, streams=args.train_streams,
                             wgrad_stream=bool(args.train_wgrad_stream))
         if world == 1:
-            train["chained"] = train_chain_bench(dev, 5, 2, graph=args.train_graph, overlap=not args.chain_serial,
-                                                 prio=args.chain_prio)
+            train["chained"] = chain_roofline_and_baseline(
+                train_chain_bench(dev, 5, 2, graph=args.train_graph, overlap=not args.chain_serial,
+                                  prio=args.chain_prio), 8, 320, 1080, 1920, "bf16", threads, not args.no_cpu_baseline)
         train_small = train_small_bench(dev, max(args.steps // 4, 10), 3, world, rank, threads,
                                         cpu=not args.no_cpu_baseline)
         train_image = train_image_bench(dev, max(args.steps // 4, 10), 5, world, rank, threads,
@@ -1351,7 +1491,11 @@ def main():
             a32 = m32.output.clone()
             l32 = m32.conv1_3.clone()
             del m32
-            x6, m6 = x6_record(x, 10, vgg, params)
+            x3, m3 = split_record(x, 10, vgg, params, "f16x3")
+            rec["f16x3"] = x3
+            a3 = m3.output.clone()
+            del m3
+            x6, m6 = split_record(x, 10, vgg, params, "bf16x6")
             rec["bf16x6"] = x6
             a6 = m6.output.clone()
             del m6
@@ -1378,6 +1522,8 @@ def main():
                 par["bf16_vs_oracle_alpha_maxabs"] = float(np.abs(alpha_timed[:1].cpu().numpy()
                                                                   - ref["output"]).max())
                 par["bf16x6_vs_oracle_alpha_maxabs"] = float(np.abs(a6[:1].cpu().numpy() - ref["output"]).max())
+                par["f16x3_vs_oracle_alpha_maxabs"] = float(np.abs(a3[:1].cpu().numpy() - ref["output"]).max())
+                par["f16x3_meets_bound"] = par["f16x3_vs_oracle_alpha_maxabs"] <= 1e-4
                 par["fp32_meets_bound"] = par["fp32_vs_oracle_alpha_maxabs"] <= 1e-4
                 par["bf16_meets_bound"] = par["bf16_vs_oracle_alpha_maxabs"] <= 1e-4
                 par["bf16x6_meets_bound"] = par["bf16x6_vs_oracle_alpha_maxabs"] <= 1e-4

@@ -262,12 +262,30 @@ int vm_convert_nhwc(const vm_tensor* x, vm_tensor* y, const float* scale, const 
 int vm_split6_nhwc(const vm_tensor* x, vm_tensor* y, vm_tensor* y_pool, void* stream);
 /* Split-fp16 x3 operand of an f32 activation (no reference counterpart: the operand format of the split-fp16 conv path,
  * which evaluates unet.py's tf.nn.conv2d (unet.py:39,60,70) at f32 accuracy in three fp16 MFMA products).  x (f32
- * view) -> h = fp16(x), l = fp16(x - h) (RNE; 22 significant bits), written as three slabs [l, h, h] at channel
- * p*S + y.coff + c of y (VM_F16; S = slab, or y.cstride / 3 when slab <= 0; y.c >= x.c, the extra channels 0).  A conv
- * over those channels with the filter parts [Wh, Wl, Wh] stacked along cin is l*Wh + h*Wl + h*Wh.  y_pool (optional,
- * same layout at ceil(h/2) x ceil(w/2)): the split of tf.nn.max_pool 2x2 SAME (unet.py:33) of x from the same pass.
- * overflow (device int, may be NULL): set to 1 when some |x| >= 65520 (fp16's range; the split is then invalid). */
+ * view) -> h = fp16(x), l = fp16(x - h) (RNE; 22 significant bits), written as slabs [l, h] at channel p*S + y.coff + c
+ * of y (VM_F16; S = slab, or y.cstride / 2 when slab <= 0; y.c >= x.c, the extra channels 0), and a third slab [h]
+ * at 2*S + y.coff + c when the pixel row holds it (3*S <= y.cstride).  A conv over [l, h, h] with the filter parts
+ * [Wh, Wl, Wh] stacked along cin is l*Wh + h*Wl + h*Wh; vm_conv3x3_ex_nhwc / split3 read a two-slab view (x.c = 2S,
+ * cin = 3S, S % 32 == 0) as [l, h, h], so h is stored once.  y_pool (optional, same layout at ceil(h/2) x ceil(w/2)):
+ * the split of tf.nn.max_pool 2x2 SAME (unet.py:33) of x from the same pass.  overflow (device int, may be NULL): set
+ * to 1 when some |x| >= 65520 (fp16's range; the split is then invalid). */
 int vm_split3h_nhwc(const vm_tensor* x, vm_tensor* y, vm_tensor* y_pool, int slab, int* overflow, void* stream);
+/* tf.image.resize_images(x, [y.h, y.w]) TF-1 legacy bilinear (unet.py:58) of an f32 activation, written as its
+ * split-fp16 x3 operand (the vm_split3h_nhwc layout of y, slab / overflow as there) without the f32 resized tensor;
+ * the same float32 arithmetic as vm_resize_bilinear_tf1_nhwc, so bit-identical to that resize followed by the split.
+ * 16-byte aligned views, c % 8 == 0 (the split-fp16 path's upconv_concat inputs, unet.py:44-63). */
+int vm_resize_split3h_nhwc(const vm_tensor* x, vm_tensor* y, int slab, int* overflow, void* stream);
+/* The split-fp16 x3 conv with the split of its output fused into the epilogue (no f32 round trip): x is an fp16 split
+ * input (slabs [l, h] read as [l, h, h], or three stored slabs; cin = 3 x its channels) and packed its fp16 filter
+ * parts; y = act((conv + bias) * scale + shift) is computed in f32 as vm_conv3x3_nhwc does, then written split as
+ * vm_split3h_nhwc writes it: slabs [l, h] (+ [h] where 3 * y_slab <= y.cstride) of y (VM_F16, cout % 8 == 0 channels
+ * at y.coff inside the first slab) at slab distance y_slab (<= 0: y.cstride / 2);
+ * ypool (optional, same layout, pool_slab) receives the split of tf.nn.max_pool 2x2 SAME (unet.py:33) of y.  overflow
+ * (device int, may be NULL) is set when some |y| >= 65520.  work / work_bytes: vm_conv3x3_workspace_bytes (split-K on
+ * small grids; not with ypool). */
+int vm_conv3x3_split3_nhwc(const vm_tensor* x, const void* packed, int cin, int cout, const float* bias,
+                           const float* scale, const float* shift, int act, vm_tensor* y, int y_slab, vm_tensor* ypool,
+                           int pool_slab, int* overflow, void* work, size_t work_bytes, void* stream);
 
 /* tf.contrib.layers.batch_norm(is_training=True): batch mean / biased variance over N,H,W
  * (unet_simple.py:25,41; small.py:22,32).  work: vm_bn_workspace_bytes(x) bytes of device scratch. */

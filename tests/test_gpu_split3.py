@@ -35,15 +35,19 @@ def _split_ref(x):
     return [lo, h, h]
 
 
-@pytest.mark.parametrize("n,h,w,c,S,off,slab", [(2, 7, 9, 7, 16, 0, 16), (1, 16, 33, 64, 64, 0, 0),
-                                                (1, 5, 6, 128, 256, 128, 0), (2, 3, 5, 24, 40, 16, 0)])
+@pytest.mark.parametrize("n,h,w,c,S,off,width", [(2, 7, 9, 7, 16, 0, 64), (1, 16, 33, 64, 64, 0, 128),
+                                                 (1, 5, 6, 128, 256, 128, 512), (2, 3, 5, 24, 40, 16, 120),
+                                                 (1, 9, 17, 64, 64, 0, 192)])
 @pytest.mark.parametrize("pool", [False, True])
-def test_split3h_kernel_bit_exact(n, h, w, c, S, off, slab, pool):
+def test_split3h_kernel_bit_exact(n, h, w, c, S, off, width, pool):
+    """slabs [l, h] (and the third, [h] again, where the row holds 3 * S channels: the conv1_1 input's 4 x 16 layout,
+    the 3 * 64 case) at p * S + off."""
     from vmatting.split3 import split3h
     torch.manual_seed(c + h)
     x = (torch.randn(n, h, w, c + 3) * torch.logspace(-9, 4, c + 3)).float()
     xd = x.to(DEV)[..., 1:1 + c]  # a channel-slice f32 view
-    width = 4 * S if slab else 3 * S
+    slab = S
+    nsl = 3 if 3 * S <= width else 2
     buf = torch.zeros((n, h, w, width), dtype=torch.float16, device=DEV)
     cc = (c + 7) // 8 * 8
     pb = None
@@ -57,10 +61,9 @@ def test_split3h_kernel_bit_exact(n, h, w, c, S, off, slab, pool):
     xp = torch.zeros((n, h, w, cc))
     xp[..., :c] = xs
     got = buf.cpu()
-    for p, ref in enumerate(_split_ref(xp)):
+    for p, ref in enumerate(_split_ref(xp)[:nsl]):
         assert torch.equal(got[..., p * S + off:p * S + off + cc].view(torch.int16), ref.view(torch.int16)), p
-    if slab:
-        assert not got[..., 3 * S:].any()  # past the three slabs: untouched
+    assert not got[..., nsl * S:].any()  # past the written slabs: untouched
     # h + l carries x to 2^-22 relative (normal range) / 2^-25 absolute (the fp16 subnormal spacing of l)
     parts = [got[..., p * S + off:p * S + off + c].double() for p in range(2)]
     xd64 = xs.double()
@@ -71,14 +74,14 @@ def test_split3h_kernel_bit_exact(n, h, w, c, S, off, slab, pool):
         xx[:, :h, :w] = xp
         mx = xx.view(n, ph, 2, pw, 2, cc).amax(dim=(2, 4))
         gp = pb.cpu()
-        for p, ref in enumerate(_split_ref(mx)):
+        for p, ref in enumerate(_split_ref(mx)[:nsl]):
             assert torch.equal(gp[..., p * S + off:p * S + off + cc].view(torch.int16), ref.view(torch.int16)), p
 
 
 def test_split3h_overflow_flag():
     from vmatting.split3 import split3h
     x = torch.full((1, 4, 4, 8), 1000.0, device=DEV)
-    y = torch.zeros((1, 4, 4, 24), dtype=torch.float16, device=DEV)
+    y = torch.zeros((1, 4, 4, 16), dtype=torch.float16, device=DEV)
     ovf = torch.zeros(1, dtype=torch.int32, device=DEV)
     split3h(x, y[..., :8], overflow=ovf)
     assert int(ovf.item()) == 0
@@ -104,10 +107,11 @@ def test_f16x3_conv_matches_float64(n, h, w, cin, cout, splitk):
     t = filter_scale(wt)
     pc = ops.PackedConv(split3_filter(wt, cin, cout, t), None, "f16", DEV, scale=np.full(cout, 1.0 / t, np.float32),
                         shift=b)
-    xs = torch.zeros((n, h, w, 3 * cin), dtype=torch.float16, device=DEV)
+    xs = torch.zeros((n, h, w, 2 * cin), dtype=torch.float16, device=DEV)  # [l, h], read as [l, h, h]
     split3h(torch.from_numpy(x).to(DEV), xs[..., :cin])
     y = torch.empty((n, h, w, cout), dtype=torch.float32, device=DEV)
-    ops.conv3x3(xs, pc, "none", out=y, splitk=splitk)
+    from vmatting.split3 import conv_f32
+    conv_f32(xs, pc, y, "none", splitk=splitk)
     torch.cuda.synchronize()
     ref = oo.conv3x3_same(x.astype(np.float64), wt.astype(np.float64), b.astype(np.float64))
     got = H(y)
@@ -115,6 +119,25 @@ def test_f16x3_conv_matches_float64(n, h, w, cin, cout, splitk):
     err = np.abs(got - ref).max() / scale
     print("f16x3 conv %s: max err %.3e of max |y|" % ((n, h, w, cin, cout), err))
     assert err <= 2e-6  # f32 accumulation over 27 * cin products (the exact-f32 MFMA path: ~1e-6 here)
+
+
+@pytest.mark.parametrize("n,h,w", [(1, 72, 100), (2, 35, 61)])
+def test_f16x3_fused_split_equals_unfused(n, h, w, vgg0):
+    """vm_conv3x3_split3_nhwc (split + pool split in the conv epilogue, split-K reduction included) against the f32
+    output + vm_split3h_nhwc round trip: the same forward, bit for bit."""
+    from vmatting import unet
+    np.random.seed(0)
+    m = unet.UNetVideo(vgg0, dtype="f16x3")
+    m.prepare()
+    x = torch.randn(n, h, w, 7, device=DEV) * 60
+    m._x6.fuse_split = False
+    a0 = m.forward(x).clone()
+    l0 = m.conv1_3.clone()
+    m._x6.fuse_split = True
+    a1 = m.forward(x).clone()
+    torch.cuda.synchronize()
+    assert torch.equal(a0, a1)
+    assert torch.equal(l0, m.conv1_3)
 
 
 @pytest.mark.parametrize("case", ["unet_video_70x90", "unet_video_64x96", "unet_image_70x90"])

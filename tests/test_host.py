@@ -377,3 +377,27 @@ def test_entry_points_without_arguments_name_what_is_missing(tmp_path, monkeypat
     (tmp_path / "dataset" / "train.txt").write_text("a b c\n")
     with pytest.raises(ValueError, match="dataset/valid.txt"):
         procedures.small_train()
+
+
+def test_split3_filter_parts_carry_the_scaled_filter():
+    """vmatting.split3: the fp16 filter parts of w * 2^t (t from filter_scale: max |w * 2^t| in (2^11, 2^12]) sum back
+    to it within 2^-22 relative (the two-part fp16 residual) and sit in slab order [Wh, Wl, Wh]; the scale is an
+    exact power of two, so the epilogue's 2^-t undoes it exactly."""
+    import torch
+    from vmatting.split3 import filter_scale, split3_filter
+    rs = np.random.RandomState(5)
+    for cin, cout, std in ((7, 64, 0.2), (64, 128, 0.06), (512, 8, 0.02)):
+        w = (rs.randn(3, 3, cin, cout) * std).astype(np.float32)
+        t = filter_scale(w)
+        assert t == 2.0 ** round(np.log2(t)) and 2 ** 11 < np.abs(w).max() * t <= 2 ** 12
+        f = split3_filter(w, cin, cout, t).double().numpy()
+        wh, wl, wh2 = f[:, :, :cin], f[:, :, cin:2 * cin], f[:, :, 2 * cin:]
+        assert np.array_equal(wh, wh2)
+        assert np.array_equal(wh, wh.astype(np.float16).astype(np.float64))  # exact fp16 values
+        assert np.array_equal(wl, wl.astype(np.float16).astype(np.float64))
+        ws = w.astype(np.float64) * t
+        assert np.all(np.abs(wh + wl - ws) <= 2.0 ** -22 * np.abs(ws) + 2.0 ** -24)
+        # wider slabs: zero rows past the filter's channels
+        f2 = split3_filter(w, cin + 8, cout, t).numpy()
+        assert not f2[:, :, cin:cin + 8].any() and np.array_equal(f2[:, :, cin + 8:2 * cin + 8], f[:, :, cin:2 * cin])
+    assert torch.float16 is not None

@@ -1041,6 +1041,11 @@ void conv3x3_patch(ConvArgs a) {
                        : reinterpret_cast<float*>(a.y) + a.y_coff + pix0 * ycs;
     const __amdgpu_buffer_rsrc_t yfr = __builtin_amdgcn_make_buffer_rsrc(yf, 0, 0x7ffffff0, 0x00020000);
     const int ycs4 = ycs * 4;
+    // split-fp16 x3 output (ConvArgs::ysplit): the same f32 staging, then 8 channels per thread split into [l, h, h]
+    const bool ysp = a.ysplit > 0 && !splitk;
+    uint16_t* ys = reinterpret_cast<uint16_t*>(a.y) + a.y_coff + pix0 * (long)a.y_cstride;
+    const __amdgpu_buffer_rsrc_t ysr = __builtin_amdgcn_make_buffer_rsrc(ys, 0, 0x7ffffff0, 0x00020000);
+    bool ovf = false;
     for (int sl = 0; sl < BN / 64; ++sl) {
       const int cb = n0 + sl * 64;
       __syncthreads();
@@ -1072,6 +1077,92 @@ void conv3x3_patch(ConvArgs a) {
         }
       }
       __syncthreads();
+      if (ysp) {
+        const int S2 = a.ysplit * 2;
+        const bool y3 = 3 * a.ysplit <= a.y_cstride;  // the third slab [h again] where the pixel row holds it
+#pragma unroll
+        for (int it = 0; it < C::BM * 8 / NT; ++it) {
+          const int idx = it * NT + tid;
+          const int rr = idx >> 3, cq = idx & 7;
+          const float4 d0 = *reinterpret_cast<const float4*>(smem + rr * C::SR32 + cq * 32);
+          const float4 d1 = *reinterpret_cast<const float4*>(smem + rr * C::SR32 + cq * 32 + 16);
+          const float v[8] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w};
+          const int pr = rr / C::TW, pc = rr % C::TW;
+          bool ok;
+          const int pix = out_pix(pr, pc, ok);
+          ok = ok && cb + cq * 8 < a.cout;
+          uint4 hv, lv;
+          const bool o = split3h_chunk(v, hv, lv);
+          ovf |= ok && o;
+          const int off = ok ? pix * ycs2 + (cb + cq * 8) * 2 : OOB;
+          const int off1 = ok ? off + S2 : OOB, off2 = ok ? off + 2 * S2 : OOB;
+          typedef __attribute__((ext_vector_type(4))) unsigned u4_t;
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4_t, lv), ysr, off, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4_t, hv), ysr, off1, 0, 0);
+          if (y3) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4_t, hv), ysr, off2, 0, 0);
+        }
+        if (a.py) {
+          // the split of the fused 2x2 SAME max-pool (unet.py:32-33) of the staged f32 slab, as the bf16 path's
+          // pool: tiles start on even rows / columns, taps past the frame edge never win
+          const int PH = (H + 1) >> 1, PW = (W + 1) >> 1;
+          const int pr0 = r0 >> 1, pc0 = c0 >> 1;
+          uint16_t* pbs = reinterpret_cast<uint16_t*>(a.py) + a.py_coff +
+                          (((long)n * PH + pr0) * PW + (a.vstride ? 0 : pc0)) * (long)a.py_cstride + n0;
+          const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(pbs, 0, 0x7ffffff0, 0x00020000);
+          const int P2 = a.psplit * 2;
+          constexpr int PTW = C::TW / 2, PITEMS = C::BM / 4 * 8;
+#pragma unroll
+          for (int it = 0; it < (PITEMS + NT - 1) / NT; ++it) {
+            const int idx = it * NT + tid;
+            if (idx >= PITEMS) break;
+            const int pp = idx >> 3, cq = idx & 7;
+            const int pr = pp / PTW, pc = pp % PTW;
+            const int rr = 2 * pr * C::TW + 2 * pc;
+            bool in;
+            const int fpix = out_pix(2 * pr, 2 * pc, in);
+            const int fx = fpix % W;
+            const bool vh = r0 + 2 * pr + 1 < H, vw = a.vstride ? fx + 1 < W : c0 + 2 * pc + 1 < W;
+            auto ld8 = [&](int r, float* f) {
+              const float4 q0 = *reinterpret_cast<const float4*>(smem + r * C::SR32 + cq * 32);
+              const float4 q1 = *reinterpret_cast<const float4*>(smem + r * C::SR32 + cq * 32 + 16);
+              f[0] = q0.x; f[1] = q0.y; f[2] = q0.z; f[3] = q0.w; f[4] = q1.x; f[5] = q1.y; f[6] = q1.z; f[7] = q1.w;
+            };
+            float m[8], f[8];
+            ld8(rr, m);
+            if (vw) {
+              ld8(rr + 1, f);
+#pragma unroll
+              for (int j = 0; j < 8; ++j) m[j] = fmaxf(m[j], f[j]);
+            }
+            if (vh) {
+              ld8(rr + C::TW, f);
+#pragma unroll
+              for (int j = 0; j < 8; ++j) m[j] = fmaxf(m[j], f[j]);
+            }
+            if (vh && vw) {
+              ld8(rr + C::TW + 1, f);
+#pragma unroll
+              for (int j = 0; j < 8; ++j) m[j] = fmaxf(m[j], f[j]);
+            }
+            int ppix = pr * PW + pc;
+            bool ok = pr0 + pr < PH && pc0 + pc < PW;
+            if (a.vstride) {
+              ok = in;
+              ppix = ((fpix / W - 2 * pr) / H * PH + pr) * PW + fx / 2;
+            }
+            ok = ok && n0 + sl * 64 + cq * 8 < a.cout;
+            uint4 hv, lv;
+            split3h_chunk(m, hv, lv);
+            const int off = ok ? (ppix * a.py_cstride + sl * 64 + cq * 8) * 2 : OOB;
+            typedef __attribute__((ext_vector_type(4))) unsigned u4_t;
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4_t, lv), prs, off, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4_t, hv), prs, ok ? off + P2 : OOB, 0, 0);
+            if (3 * a.psplit <= a.py_cstride)
+              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4_t, hv), prs, ok ? off + 2 * P2 : OOB, 0, 0);
+          }
+        }
+        continue;
+      }
 #pragma unroll
       for (int it = 0; it < C::BM * 16 / NT; ++it) {
         const int idx = it * NT + tid;
@@ -1093,6 +1184,7 @@ void conv3x3_patch(ConvArgs a) {
         }
       }
     }
+    if (ovf && a.ovf) *a.ovf = 1;  // a plain vector store: any writer's 1 is the answer
     return;
   }
   if constexpr (C::REPI_OK) {
@@ -4406,7 +4498,8 @@ constexpr int thin_dma_lds() {
 
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ part, int ks, long M, int cout,
                                                             const float* bias, const float* scale, const float* shift,
-                                                            int act, void* y, int y_dtype, int ycs, int ycoff) {
+                                                            int act, void* y, int y_dtype, int ycs, int ycoff,
+                                                            int ysplit = 0, int* ovf = nullptr) {
   const int c4 = (cout + 3) / 4;
   const long total = M * c4;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
@@ -4426,8 +4519,19 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
       if (act == VM_ACT_RELU) t = fmaxf(t, 0.f);
       else if (act == VM_ACT_SIGMOID) t = sigmoid_precise(t);
       const long o = p * ycs + ycoff + c + j;
-      if (y_dtype == VM_F32) reinterpret_cast<float*>(y)[o] = t;
-      else reinterpret_cast<uint16_t*>(y)[o] = f2bf(t);
+      if (ysplit > 0) {  // split-fp16 x3 output (ConvArgs::ysplit): [l, h, h] at 0, ysplit, 2 * ysplit
+        const _Float16 h = (_Float16)t;
+        const _Float16 l = (_Float16)(t - (float)h);
+        uint16_t* yo = reinterpret_cast<uint16_t*>(y) + o;
+        yo[0] = __builtin_bit_cast(uint16_t, l);
+        yo[ysplit] = __builtin_bit_cast(uint16_t, h);
+        if (3 * ysplit <= ycs) yo[2 * ysplit] = __builtin_bit_cast(uint16_t, h);
+        if (!(fabsf(t) < 65520.f) && ovf) *ovf = 1;
+      } else if (y_dtype == VM_F32) {
+        reinterpret_cast<float*>(y)[o] = t;
+      } else {
+        reinterpret_cast<uint16_t*>(y)[o] = f2bf(t);
+      }
     }
   }
 }
@@ -4776,7 +4880,7 @@ static bool patch_ok(const ConvArgs& a, size_t tsize) {
   // bf16 output (16-byte aligned view), or f32 output without the fused pool / folded resize (cout multiple of 4;
   // dword stores when the view is not 16-byte aligned)
   const bool yok = a.y_dtype == VM_BF16 ? (a.cout & 7) == 0 && a.y_vec
-                                        : (a.y_dtype == VM_F32 && !a.py && !a.up && (a.cout & 3) == 0);
+                                        : (a.y_dtype == VM_F32 && (!a.py || a.ysplit) && !a.up && (a.cout & 3) == 0);
   return tsize == 2 && a.chunk_major && a.cin_pad % 32 == 0 && yok && a.act != VM_ACT_SOFTMAX &&
          (a.x_src_c <= 0 || a.x_src_c % 32 == 0);
 }
@@ -4809,7 +4913,7 @@ static int dispatch_patch(ConvArgs& a, hipStream_t st) {
     if (rc) return rc;
     const long work = a.M * ((a.cout + 3) / 4);
     hipLaunchKernelGGL(splitk_reduce_kernel, dim3(grid_for(work, 256)), dim3(256), 0, st, a.part, a.ksplit, a.M,
-                       a.cout, a.bias, a.scale, a.shift, a.act, a.y, a.y_dtype, a.y_cstride, a.y_coff);
+                       a.cout, a.bias, a.scale, a.shift, a.act, a.y, a.y_dtype, a.y_cstride, a.y_coff, a.ysplit, a.ovf);
     return check_launch("splitk_reduce");
   }
 #ifdef VM_STUDY
@@ -5483,10 +5587,17 @@ extern "C" int vm_conv3x3_pack_weights_batch(int njobs, const vm_pack_job* jobs,
   return VM_OK;
 }
 
+// split-fp16 x3 output of vm_conv3x3_split3_nhwc (ConvArgs::ysplit / psplit / ovf)
+struct SplitOut {
+  int yslab, pslab;
+  int* ovf;
+};
+
 static int conv_impl(const vm_tensor* x, const void* packed, int cin, int cout, const float* bias, const float* scale,
                      const float* shift, int act, vm_tensor* y, const vm_tensor* yp, void* stream,
                      float* y2 = nullptr, int nsrc = 0, long src_stride = 0, void* work = nullptr,
-                     size_t work_bytes = 0, const float* head_part = nullptr, const float* y_acc = nullptr);
+                     size_t work_bytes = 0, const float* head_part = nullptr, const float* y_acc = nullptr,
+                     const SplitOut* so = nullptr);
 
 extern "C" int vm_conv3x3_nhwc(const vm_tensor* x, const void* packed, int cin, int cout, const float* bias,
                                const float* scale, const float* shift, int act, vm_tensor* y, void* stream) {
@@ -5683,6 +5794,31 @@ extern "C" int vm_conv3x3_head_acc_ex_nhwc(const vm_tensor* x, const void* packe
                    nullptr, y_acc);
 }
 
+static bool split3_view_ok(const vm_tensor* t, int slab, int c) {
+  return t->dtype == VM_F16 && slab > 0 && slab % 8 == 0 && t->coff % 8 == 0 && t->cstride % 8 == 0 &&
+         t->coff + c <= slab && 2 * slab <= t->cstride && reinterpret_cast<uintptr_t>(t->ptr) % 16 == 0;
+}
+
+extern "C" int vm_conv3x3_split3_nhwc(const vm_tensor* x, const void* packed, int cin, int cout, const float* bias,
+                                      const float* scale, const float* shift, int act, vm_tensor* y, int y_slab,
+                                      vm_tensor* ypool, int pool_slab, int* overflow, void* work, size_t work_bytes,
+                                      void* stream) {
+  if (!x || !y || !valid_tensor(y, true) || (ypool && !valid_tensor(ypool, true)))
+    return fail(VM_EINVAL, "conv3x3_split3: invalid tensor");
+  SplitOut so{y_slab > 0 ? y_slab : y->cstride / 2, 0, overflow};
+  if (cout % 8 || !split3_view_ok(y, so.yslab, cout))
+    return fail(VM_EUNSUPPORTED, "conv3x3_split3: y must be an fp16 view of cout %% 8 == 0 channels inside the first "
+                                 "of two (or three) slabs of S %% 8 == 0 channels, 16-byte aligned");
+  if (ypool) {
+    so.pslab = pool_slab > 0 ? pool_slab : ypool->cstride / 2;
+    if (!split3_view_ok(ypool, so.pslab, cout) || ypool->n != y->n || ypool->h != (y->h + 1) / 2 ||
+        ypool->w != (y->w + 1) / 2 || ypool->c != cout)
+      return fail(VM_EINVAL, "conv3x3_split3: pool view must be [n, ceil(h/2), ceil(w/2), cout] in the split layout");
+  }
+  return conv_impl(x, packed, cin, cout, bias, scale, shift, act, y, ypool, stream, nullptr, 0, 0, work, work_bytes,
+                   nullptr, nullptr, &so);
+}
+
 extern "C" int vm_conv3x3_head_partial_nhwc(const vm_tensor* x, const void* packed, int cin, const float* bias,
                                             const float* scale, const float* shift, int act, vm_tensor* y,
                                             float* alpha, const float* partial, void* stream) {
@@ -5768,16 +5904,28 @@ extern "C" int vm_conv3x3_head_nhwc(const vm_tensor* x, const void* packed, int 
 
 static int conv_impl(const vm_tensor* x, const void* packed, int cin, int cout, const float* bias, const float* scale,
                      const float* shift, int act, vm_tensor* y, const vm_tensor* yp, void* stream, float* y2, int nsrc,
-                     long src_stride, void* work, size_t work_bytes, const float* head_part, const float* y_acc) {
-  if (!valid_tensor(x, true) || !valid_tensor(y) || !packed) return fail(VM_EINVAL, "conv3x3: invalid tensor/weights");
+                     long src_stride, void* work, size_t work_bytes, const float* head_part, const float* y_acc,
+                     const SplitOut* so) {
+  if (!valid_tensor(x, true) || !valid_tensor(y, so != nullptr) || !packed)
+    return fail(VM_EINVAL, "conv3x3: invalid tensor/weights");
   // fp16 operands (the split-fp16 forward, vmatting/split3.py): f32 outputs of the patch kernel (any cout % 4 == 0)
-  // or the MFMA head (cout == 1, <= 256 channels per call); no pooling, split sources or softmax
+  // or the MFMA head (cout == 1, <= 256 channels per call), or (so) the split-fp16 output with its fused pool; no
+  // split sources or softmax
   const bool f16 = x->dtype == VM_F16;
-  if (f16 && (y->dtype != VM_F32 || yp || nsrc > 1 || act == VM_ACT_SOFTMAX || head_part))
-    return fail(VM_EUNSUPPORTED, "conv3x3: fp16 operands need an f32 output without pool / sources / softmax");
+  if (so && (!f16 || y->dtype != VM_F16 || cout == 1))
+    return fail(VM_EINVAL, "conv3x3_split3: fp16 input and fp16 split output views, cout > 1");
+  if (f16 && ((!so && (y->dtype != VM_F32 || yp)) || nsrc > 1 || act == VM_ACT_SOFTMAX || head_part))
+    return fail(VM_EUNSUPPORTED, "conv3x3: fp16 operands need an f32 (or split) output without sources / softmax");
   if (y_acc && cout != 1) return fail(VM_EINVAL, "conv3x3: an accumulated pre-activation needs cout == 1");
   if (head_part && cout != 1) return fail(VM_EINVAL, "conv3x3: head partials need cout == 1");
-  const int xc = nsrc > 1 ? nsrc * x->c : x->c;  // sources: x is the view of source 0
+  int xc = nsrc > 1 ? nsrc * x->c : x->c;  // sources: x is the view of source 0
+  // split-fp16 input stored as two slabs [l, h] (x->c = 2S) for a filter over [l, h, h] (cin = 3S): the third slab is
+  // read from the second (ConvArgs::xalias)
+  int xalias = 0;
+  if (x->dtype == VM_F16 && nsrc <= 1 && 2 * cin == 3 * x->c && x->c % 64 == 0) {
+    xalias = x->c / 2;
+    xc = cin;
+  }
   if (cin <= 0 || cout <= 0 || xc != cin || y->c != cout)
     return fail(VM_EINVAL, "conv3x3: channel mismatch x.c=%d cin=%d y.c=%d cout=%d", xc, cin, y->c, cout);
   if (nsrc > 1 && (cout == 1 || yp || x->c % (x->dtype == VM_BF16 ? 32 : 16) || src_stride % 8))
@@ -5789,7 +5937,7 @@ static int conv_impl(const vm_tensor* x, const void* packed, int cin, int cout, 
   PackGeom g = geom(cin, cout, dt);
   const int ce = 16 / elem_bytes(dt);
   if (reinterpret_cast<uintptr_t>(x->ptr) % 16 || x->cstride % ce || x->coff % ce ||
-      x->coff + (nsrc > 1 ? x->c : g.cin_pad) > x->cstride)
+      x->coff + (nsrc > 1 || xalias ? x->c : g.cin_pad) > x->cstride)
     return fail(VM_EUNSUPPORTED,
                 "conv3x3: input view must be 16-byte aligned with channel padding to %d (coff=%d cstride=%d)",
                 g.cin_pad, x->coff, x->cstride);
@@ -5889,10 +6037,23 @@ static int conv_impl(const vm_tensor* x, const void* packed, int cin, int cout, 
   }
   if (f16) {  // the patch kernel's fp16 form (+ split-K on small grids with a workspace)
     a.f16 = 1;
-    if (!patch_ok(a, 2)) return fail(VM_EUNSUPPORTED, "conv3x3: fp16 operands need the patch kernel (cin %% 32 == 0)");
+    a.xalias = xalias;
     a.py = nullptr;
     a.up = 0;
-    if (work && (cout & 3) == 0) {
+    if (so) {  // split output: staged like an f32 output, stored as fp16 slabs (y_cstride stays in fp16 elements)
+      a.y_dtype = VM_F32;
+      a.y_vec = 1;
+      a.ysplit = so->yslab;
+      a.ovf = so->ovf;
+      if (yp) {
+        a.py = yp->ptr;
+        a.py_cstride = yp->cstride;
+        a.py_coff = yp->coff;
+        a.psplit = so->pslab;
+      }
+    }
+    if (!patch_ok(a, 2)) return fail(VM_EUNSUPPORTED, "conv3x3: fp16 operands need the patch kernel (cin %% 32 == 0)");
+    if (work && (cout & 3) == 0 && !yp) {
       const int ks = splitk_plan(x->n, x->h, x->w, a.cin_pad, cout);
       if (ks > 1 && work_bytes >= (size_t)ks * M * cout * sizeof(float)) {
         a.ksplit = ks;

@@ -67,6 +67,15 @@ struct ConvArgs {
   int halfskip;
   // fp16 operands (VM_F16 input view and filter pack: the split-fp16 forward): the patch kernel's fp16 MFMA form
   int f16;
+  // split-fp16 x3 output (vm_conv3x3_split3_nhwc; patch kernel f32-staged epilogue and the split-K reduction): y is
+  // an fp16 view and each output value v (after bias / affine / act, in f32) is written as h = fp16(v), l =
+  // fp16(v - h) into the slabs [l, h, h] at channel offsets 0, ysplit, 2 * ysplit; the fused pool likewise at
+  // psplit.  ovf (device int, may be null) is set where |v| >= 65520 (the split would be invalid)
+  int ysplit, psplit;
+  int* ovf;
+  // split-fp16 input stored as two slabs [l, h] of xalias channels (K = 3 * xalias: [l, h, h]): input channels
+  // [2 * xalias, 3 * xalias) are read from [xalias, 2 * xalias) (src_chan), so h is stored once
+  int xalias;
 };
 
 // compile-time loop: f(std::integral_constant<int, I>) for I in [I, N)
@@ -88,6 +97,7 @@ __device__ __forceinline__ P* uniform_ptr(P* p) {
 
 // element offset of input channel c (relative to the view's channel 0) under the source split
 __device__ __forceinline__ long src_chan(const ConvArgs& a, int c) {
+  if (a.xalias > 0 && c >= 2 * a.xalias) c -= a.xalias;  // split-fp16 input: the third slab re-reads the second
   if (a.x_src_c <= 0) return c;
   const int s = c / a.x_src_c;
   return (long)s * a.x_src_stride + (c - s * a.x_src_c);
@@ -128,6 +138,27 @@ __device__ __forceinline__ void mma16<float>(const uint4& a, const uint4& b, f32
   c = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.y), __uint_as_float(b.y), c, 0, 0, 0);
   c = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.z), __uint_as_float(b.z), c, 0, 0, 0);
   c = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.w), __uint_as_float(b.w), c, 0, 0, 0);
+}
+
+// split-fp16 x3 parts of 8 f32 values: h = fp16(v) (RNE), l = fp16(v - h) (the difference is exact in f32), as
+// two 16-byte chunks; returns whether some |v| >= 65520 (h = inf: the split is invalid) or v is NaN
+__device__ __forceinline__ bool split3h_chunk(const float* v, uint4& H, uint4& L) {
+  typedef _Float16 h2_t __attribute__((ext_vector_type(2)));
+  typedef float f2_t __attribute__((ext_vector_type(2)));
+  uint32_t wh[4], wl[4];
+  bool ovf = false;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const f2_t x = {v[2 * i], v[2 * i + 1]};
+    const h2_t h = __builtin_convertvector(x, h2_t);
+    wh[i] = __builtin_bit_cast(uint32_t, h);
+    const f2_t r = {v[2 * i] - (float)h[0], v[2 * i + 1] - (float)h[1]};
+    wl[i] = __builtin_bit_cast(uint32_t, __builtin_convertvector(r, h2_t));
+    ovf |= !(fabsf(v[2 * i]) < 65520.f) || !(fabsf(v[2 * i + 1]) < 65520.f);
+  }
+  H = make_uint4(wh[0], wh[1], wh[2], wh[3]);
+  L = make_uint4(wl[0], wl[1], wl[2], wl[3]);
+  return ovf;
 }
 
 // XCD-aware bijective remap: blocks b and b+8 share an XCD -> each XCD gets a contiguous tile range

@@ -765,7 +765,7 @@ __device__ __forceinline__ uint32_t f16x2_bits(float lo, float hi) {
   return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, f16x2_t));  // RNE
 }
 
-__device__ __forceinline__ bool store_split3h(uint16_t* base, long S, const float* v) {
+__device__ __forceinline__ bool store_split3h(uint16_t* base, long S, const float* v, bool three) {
   uint32_t wh[4], wl[4];
   bool ovf = false;
 #pragma unroll
@@ -778,7 +778,7 @@ __device__ __forceinline__ bool store_split3h(uint16_t* base, long S, const floa
   const uint4 H = make_uint4(wh[0], wh[1], wh[2], wh[3]), L = make_uint4(wl[0], wl[1], wl[2], wl[3]);
   *reinterpret_cast<uint4*>(base) = L;
   *reinterpret_cast<uint4*>(base + S) = H;
-  *reinterpret_cast<uint4*>(base + 2 * S) = H;
+  if (three) *reinterpret_cast<uint4*>(base + 2 * S) = H;
   return ovf;
 }
 
@@ -790,6 +790,7 @@ __global__ __launch_bounds__(256) void split3h_kernel(View x, View y, View yp, l
   const long total = (long)on * oh * ow * cpp;
   bool ovf = false;
   const bool vec = ((x.cs | x.coff) & 3) == 0 && (reinterpret_cast<uintptr_t>(x.p) & 15) == 0;
+  const bool y3 = 3 * S <= y.cs;  // the third slab [h again] where the pixel row holds it (else [l, h] only)
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
     const int cc = (int)(i % cpp);
     const long op = i / cpp;
@@ -808,7 +809,7 @@ __global__ __launch_bounds__(256) void split3h_kernel(View x, View y, View yp, l
     if constexpr (!POOL) {
       float f[8];
       load(op, f);
-      ovf |= store_split3h(out(y, op), S, f);
+      ovf |= store_split3h(out(y, op), S, f, y3);
     } else {
       const int pw = (int)(op % yp.w);
       const long t = op / yp.w;
@@ -818,26 +819,111 @@ __global__ __launch_bounds__(256) void split3h_kernel(View x, View y, View yp, l
       const long p00 = ((long)n * x.h + iy) * x.w + ix;
       float f[8], m[8];
       load(p00, f);
-      ovf |= store_split3h(out(y, p00), S, f);
+      ovf |= store_split3h(out(y, p00), S, f, y3);
 #pragma unroll
       for (int j = 0; j < 8; ++j) m[j] = f[j];
       auto tap = [&](long pix) {
         load(pix, f);
-        ovf |= store_split3h(out(y, pix), S, f);
+        ovf |= store_split3h(out(y, pix), S, f, y3);
 #pragma unroll
         for (int j = 0; j < 8; ++j) m[j] = fmaxf(m[j], f[j]);
       };
       if (hasr) tap(p00 + 1);
       if (hasd) tap(p00 + x.w);
       if (hasr && hasd) tap(p00 + x.w + 1);
-      store_split3h(out(yp, op), Sp, m);
+      store_split3h(out(yp, op), Sp, m, 3 * Sp <= yp.cs);
     }
   }
   if (ovf && overflow) *overflow = 1;  // a plain vector store: any writer's 1 is the answer
 }
 
+// tf.image.resize_images (unet.py:58) of an f32 activation written straight as its split-fp16 x3 operand: the
+// resize's float32 arithmetic of resize_tf1_kernel / resize2x_tf1_rows (bit-identical values), then the split of
+// split3h_kernel — no f32 resized tensor.  One thread = 8 channels; TWO: the exact-2x quad form (one thread loads
+// the 2x2 low-res taps of low-res pixel (i, j) once and writes the 4 output pixels of its quad).
+__device__ __forceinline__ void ld8f(const View& x, long pix, int c, float* f) {
+  const float* src = reinterpret_cast<const float*>(x.p) + pix * x.cs + x.coff + c;
+  const float4 a = *reinterpret_cast<const float4*>(src), b = *reinterpret_cast<const float4*>(src + 4);
+  f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w; f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
+}
+
+template <bool TWO>
+__global__ __launch_bounds__(256) void resize_split3h_kernel(View x, View y, long S, float sy, float sx,
+                                                             int* overflow) {
+  const int cpp = y.c / 8;
+  const bool y3 = 3 * S <= y.cs;
+  const int oh_n = TWO ? x.h : y.h, ow_n = TWO ? x.w : y.w;
+  const long total = (long)y.n * oh_n * ow_n * cpp;
+  bool ovf = false;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int cc = (int)(i % cpp);
+    const long op = i / cpp;
+    const int ow = (int)(op % ow_n);
+    const long t = op / ow_n;
+    const int oh = (int)(t % oh_n), n = (int)(t / oh_n);
+    const int c = cc * 8;
+    const long rb = (long)n * x.h;
+    if constexpr (TWO) {  // (oh, ow) = low-res pixel (i, j)
+      const int i1 = min(oh + 1, x.h - 1), j1 = min(ow + 1, x.w - 1);
+      float a00[8], a01[8], a10[8], a11[8];
+      ld8f(x, (rb + oh) * x.w + ow, c, a00);
+      ld8f(x, (rb + oh) * x.w + j1, c, a01);
+      ld8f(x, (rb + i1) * x.w + ow, c, a10);
+      ld8f(x, (rb + i1) * x.w + j1, c, a11);
+#pragma unroll
+      for (int dy = 0; dy < 2; ++dy) {
+        const int oy = 2 * oh + dy;
+        if (oy >= y.h) break;
+#pragma unroll
+        for (int dx = 0; dx < 2; ++dx) {
+          const int ox = 2 * ow + dx;
+          if (ox >= y.w) break;
+          int ly0, ly1, lx0, lx1;
+          float fy, fx;
+          tf1_coord(oy, 0.5f, x.h, ly0, ly1, fy);
+          tf1_coord(ox, 0.5f, x.w, lx0, lx1, fx);
+          const float* tl = a00;
+          const float* tr = (lx1 == lx0) ? a00 : a01;
+          const float* bl = (ly1 == ly0) ? a00 : a10;
+          const float* br = (ly1 == ly0) ? tr : ((lx1 == lx0) ? a10 : a11);
+          float o[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+#pragma clang fp contract(off)
+            const float top = tl[e] + (tr[e] - tl[e]) * fx;
+            const float bot = bl[e] + (br[e] - bl[e]) * fx;
+            o[e] = top + (bot - top) * fy;
+          }
+          uint16_t* yo = reinterpret_cast<uint16_t*>(y.p) + (((long)n * y.h + oy) * y.w + ox) * y.cs + y.coff + c;
+          ovf |= store_split3h(yo, S, o, y3);
+        }
+      }
+    } else {
+      int y0, y1, x0, x1;
+      float yl, xl;
+      tf1_coord(oh, sy, x.h, y0, y1, yl);
+      tf1_coord(ow, sx, x.w, x0, x1, xl);
+      float tl[8], tr[8], bl[8], br[8], o[8];
+      ld8f(x, (rb + y0) * x.w + x0, c, tl);
+      ld8f(x, (rb + y0) * x.w + x1, c, tr);
+      ld8f(x, (rb + y1) * x.w + x0, c, bl);
+      ld8f(x, (rb + y1) * x.w + x1, c, br);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+#pragma clang fp contract(off)
+        const float top = tl[e] + (tr[e] - tl[e]) * xl;
+        const float bot = bl[e] + (br[e] - bl[e]) * xl;
+        o[e] = top + (bot - top) * yl;
+      }
+      uint16_t* yo = reinterpret_cast<uint16_t*>(y.p) + op * y.cs + y.coff + c;
+      ovf |= store_split3h(yo, S, o, y3);
+    }
+  }
+  if (ovf && overflow) *overflow = 1;
+}
+
 static bool split3h_view_ok(const vm_tensor* y, const vm_tensor* x, long S) {
-  return y->dtype == VM_F16 && S % 8 == 0 && 3 * S <= y->cstride && y->coff % 8 == 0 && y->c % 8 == 0 &&
+  return y->dtype == VM_F16 && S % 8 == 0 && 2 * S <= y->cstride && y->coff % 8 == 0 && y->c % 8 == 0 &&
          y->c >= x->c && y->coff + y->c <= S && y->cstride % 8 == 0 && reinterpret_cast<uintptr_t>(y->ptr) % 16 == 0;
 }
 
@@ -846,7 +932,7 @@ extern "C" int vm_split3h_nhwc(const vm_tensor* x, vm_tensor* y, vm_tensor* y_po
   if (!valid_tensor(x) || !valid_tensor(y, true) || (y_pool && !valid_tensor(y_pool, true)) || x->dtype != VM_F32)
     return fail(VM_EINVAL, "split3h: x must be an f32 view");
   if (y->n != x->n || y->h != x->h || y->w != x->w) return fail(VM_EINVAL, "split3h: shape mismatch");
-  const long S = slab > 0 ? slab : y->cstride / 3, Sp = y_pool ? (slab > 0 ? slab : y_pool->cstride / 3) : S;
+  const long S = slab > 0 ? slab : y->cstride / 2, Sp = y_pool ? (slab > 0 ? slab : y_pool->cstride / 2) : S;
   if (!split3h_view_ok(y, x, S) || (y_pool && !split3h_view_ok(y_pool, x, Sp)))
     return fail(VM_EUNSUPPORTED, "split3h: the split view must be fp16, 16-byte aligned, c and coff multiples of 8, "
                                  "three slabs of S (a multiple of 8) channels inside the pixel row");
@@ -863,6 +949,28 @@ extern "C" int vm_split3h_nhwc(const vm_tensor* x, vm_tensor* y, vm_tensor* y_po
     hipLaunchKernelGGL(split3h_kernel<false>, dim3(grid_for(work, 256)), dim3(256), 0, st, view(x), view(y), view(y),
                        S, Sp, overflow);
   return check_launch("split3h");
+}
+
+extern "C" int vm_resize_split3h_nhwc(const vm_tensor* x, vm_tensor* y, int slab, int* overflow, void* stream) {
+  if (!valid_tensor(x) || !valid_tensor(y, true) || x->dtype != VM_F32)
+    return fail(VM_EINVAL, "resize_split3h: x must be an f32 view");
+  if (y->n != x->n || y->c != x->c) return fail(VM_EINVAL, "resize_split3h: batch/channel mismatch");
+  const long S = slab > 0 ? slab : y->cstride / 2;
+  if (!split3h_view_ok(y, x, S) || x->c % 8 || x->cstride % 4 || x->coff % 4 ||
+      reinterpret_cast<uintptr_t>(x->ptr) % 16)
+    return fail(VM_EUNSUPPORTED, "resize_split3h: 16-byte aligned views of c %% 8 == 0 channels, the split layout of "
+                                 "vm_split3h_nhwc");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const bool two = y->h == 2 * x->h && y->w == 2 * x->w;
+  const long work = (long)y->n * (two ? (long)x->h * x->w : (long)y->h * y->w) * (y->c / 8);
+  const float sy = (float)x->h / (float)y->h, sx = (float)x->w / (float)y->w;
+  if (two)
+    hipLaunchKernelGGL(resize_split3h_kernel<true>, dim3(grid_for(work, 256)), dim3(256), 0, st, view(x), view(y), S,
+                       sy, sx, overflow);
+  else
+    hipLaunchKernelGGL(resize_split3h_kernel<false>, dim3(grid_for(work, 256)), dim3(256), 0, st, view(x), view(y), S,
+                       sy, sx, overflow);
+  return check_launch("resize_split3h");
 }
 
 extern "C" int vm_convert_nhwc(const vm_tensor* x, vm_tensor* y, const float* scale, const float* shift, int act,

@@ -51,7 +51,12 @@ def param_layout(shapes):
 
 
 class ImageTrainer(TrainerBase):
-    """train.training_procedure's iteration on device (unet.UNetImage, all variables trainable)."""
+    """train.training_procedure's iteration on device (unet.UNetImage, all variables trainable).
+
+    ``streams=1`` runs the filter gradients on a side stream (``_side``) beside the data-gradient chain.  capture()
+    (ImageTrainGraph) clears ``_side`` for the duration of the capture, so the graph is recorded on one stream, and
+    restores it afterwards (also when the capture raises).  A trainer is not thread-safe: another thread's eager
+    step during a capture would run single-stream."""
 
     bf16_dgrad = True  # bf16 path: data gradients held in bf16 (see _grad_buffers); False = f32 as the fp32 path
     # filter gradients kept on the caller's stream: conv1_1's is the backward's last work and the data-gradient chain

@@ -19,9 +19,12 @@ unscaled: |x| on this network is ~2e3 against fp16's 65504; a split that meets |
 (``overflowed()``), and ``UNet.build`` then re-runs the frames on the bf16x6 path.
 
 Cost: 3x the MFMA work of the bf16 forward (x6: 6x) on the same patch kernels (their fp16 MFMA form,
-v_mfma_f32_16x16x32_f16), plus one split pass per activation.  Layout: a split buffer holds slabs [l, h, h] of its
-S channels at p*S + c (S = the concat width), so the [up, skip] concats are channel ranges written by their own
-producers, as in split6.py.  conv1_1's 7-channel frame is split into slabs of 16 (64 channels, the 4th slab zero:
+v_mfma_f32_16x16x32_f16); the conv's epilogue writes its output split (vm_conv3x3_split3_nhwc, and the split of the
+fused 2x2 pool), so activations never round-trip through f32 except where a resize follows (conv5_2, conv4_4,
+conv3_4, conv2_3 feed the TF-1 resizes, which run in f32).  Layout: a split buffer holds slabs [l, h] of its S
+channels at p*S + c (S = the concat width, so the [up, skip] concats are channel ranges written by their own
+producers, as in split6.py); the convs read it as [l, h, h] (the kernel re-reads slab h for the third K range,
+ConvArgs::xalias), so h is stored once.  conv1_1's 7-channel frame is split into slabs of 16 (64 channels, the 4th slab zero:
 two whole 32-channel granules).  conv1_5 (cout 1) is two MFMA-head chunks [l | h] (256 channels) and [h] (128), the
 second adding the first's logits and undoing the filter scale before the sigmoid.
 """
@@ -83,18 +86,79 @@ def split3h(x, y, pool=None, slab=0, overflow=None):
     return y
 
 
+def resize_split3h(x, y, slab=0, overflow=None):
+    """vm_resize_split3h_nhwc: TF-1 legacy bilinear resize (unet.py:58) of the f32 view x to y's size, written split
+    into the fp16 view y (bit-identical to ops.resize_bilinear + split3h)."""
+    xv, yv = ops.nhwc(x), ops.nhwc(y)
+    ops.check(ops.lib().vm_resize_split3h_nhwc(ops.ctypes.byref(xv), ops.ctypes.byref(yv), int(slab),
+                                               ops._ptr(overflow), ops.stream_handle()), "resize_split3h")
+    return y
+
+
+def _prof_begin():
+    prof = ops._CONV_PROFILE
+    if prof is None:
+        return None
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record()
+    return prof, ev0, ev1
+
+
+def _prof_end(p, x, pc):
+    if p is not None:
+        prof, ev0, ev1 = p
+        ev1.record()
+        n, h, w, _ = x.shape
+        prof.append((2 * n * h * w * 9 * pc.cin * pc.cout, ops._lib.last_conv_kernel(), ev0, ev1,
+                     (n, h, w, pc.cin, pc.cout)))
+
+
+def conv_f32(x, pc, y, act="relu", splitk=True):
+    """The fp16 conv of split input x (a two-slab [l, h] view read as [l, h, h], or a plain fp16 view of pc.cin
+    channels) into the f32 view y (vm_conv3x3_ex_nhwc; split-K on small grids)."""
+    xv, yv = ops.nhwc(x), ops.nhwc(y)
+    wsz = ops.lib().vm_conv3x3_workspace_bytes(ops.ctypes.byref(xv), pc.cin, pc.cout) if splitk else 0
+    ws = ops._workspace(wsz, x.device) if wsz else None
+    p = _prof_begin()
+    ops.check(ops.lib().vm_conv3x3_ex_nhwc(ops.ctypes.byref(xv), 1, 0, ops._ptr(pc.packed), pc.cin, pc.cout,
+                                           ops._ptr(pc.bias), ops._ptr(pc.scale), ops._ptr(pc.shift), ops._lib.ACT[act],
+                                           ops.ctypes.byref(yv), ops._ptr(ws), wsz, ops.stream_handle()), "conv3x3(f16)")
+    _prof_end(p, x, pc)
+    return y
+
+
+def conv_split(x, pc, y, act="relu", pool=None, overflow=None, y_slab=0, pool_slab=0, splitk=True):
+    """vm_conv3x3_split3_nhwc: the fp16 conv of split input x with its output written split into the fp16 view y
+    (and the split of its 2x2 SAME max-pool into ``pool``) from the conv's epilogue — no f32 round trip."""
+    xv, yv = ops.nhwc(x), ops.nhwc(y)
+    pv = ops.nhwc(pool) if pool is not None else None
+    wsz = ops.lib().vm_conv3x3_workspace_bytes(ops.ctypes.byref(xv), pc.cin, pc.cout) if (splitk and pool is None) else 0
+    ws = ops._workspace(wsz, x.device) if wsz else None
+    ref = (lambda v: None if v is None else ops.ctypes.byref(v))
+    p = _prof_begin()
+    ops.check(ops.lib().vm_conv3x3_split3_nhwc(
+        ref(xv), ops._ptr(pc.packed), pc.cin, pc.cout, ops._ptr(pc.bias), ops._ptr(pc.scale), ops._ptr(pc.shift),
+        ops._lib.ACT[act], ref(yv), int(y_slab), ref(pv), int(pool_slab), ops._ptr(overflow), ops._ptr(ws), wsz,
+        ops.stream_handle()), "conv3x3_split3")
+    _prof_end(p, x, pc)
+    return y
+
+
 def whole(buf):
-    """The split-layout view of all channels of a 3*S-wide split buffer."""
-    return buf[..., :buf.shape[-1] // 3]
+    """The split-layout view of all channels of a 2*S-wide split buffer [l, h]."""
+    return buf[..., :buf.shape[-1] // 2]
 
 
 def seg(buf, off, c):
-    """Channels [off, off + c) of a 3*S-wide split buffer (split3h writes the 3 slabs at p*S + off)."""
+    """Channels [off, off + c) of a 2*S-wide split buffer (the writers put the slabs at p*S + off)."""
     return buf[..., off:off + c]
 
 
 class Split3Forward:
     """The split-fp16 x3 forward of a UNet (unet.UNetVideo / UNetImage) with its parameters."""
+
+    # conv -> split in the conv's epilogue (vm_conv3x3_split3_nhwc); False: f32 output + vm_split3h_nhwc (A/B)
+    fuse_split = True
 
     def __init__(self, model):
         self.m = model
@@ -142,7 +206,7 @@ class Split3Forward:
         from .unet import _levels
         L = _levels(h, w)
         dev = self.dev
-        S = lambda lv, c: torch.empty((n, L[lv][0], L[lv][1], 3 * c), dtype=torch.float16, device=dev)  # noqa
+        S = lambda lv, c: torch.empty((n, L[lv][0], L[lv][1], 2 * c), dtype=torch.float16, device=dev)  # noqa
         F = lambda lv, c: torch.empty((n, L[lv][0], L[lv][1], c), dtype=torch.float32, device=dev)  # noqa
         b = {"x": torch.zeros((n, L[0][0], L[0][1], 64), dtype=torch.float16, device=dev),
              "s11": S(0, 64), "cat1": S(0, 128), "r4": S(0, 128),
@@ -151,7 +215,6 @@ class Split3Forward:
              "p3": S(3, 256), "s41": S(3, 512), "s42": S(3, 512), "cat4": S(3, 1024), "r1": S(3, 512),
              "p4": S(4, 512), "s51": S(4, 512),
              "f0": F(0, 128), "f1": F(1, 256), "f2": F(2, 512), "f3": F(3, 512), "f4": F(4, 512),
-             "rr0": F(0, 128), "rr1": F(1, 256), "rr2": F(2, 512), "rr3": F(3, 512),
              "lg0": F(0, 1), "out": F(0, 1)}
         self._b, self._key = b, (n, h, w)
         return b
@@ -171,47 +234,57 @@ class Split3Forward:
         ovf.zero_()
         split3h(x, b["x"][..., :8], slab=16, overflow=ovf)  # slabs [l, h, h] of 16 channels, 8 written
 
-        def conv(src, name, dst_f32, act="relu"):
-            return ops.conv3x3(src, C[name], act, out=dst_f32, splitk=True)
+        def conv(src, name, dst_f32, act="relu", splitk=True):
+            return conv_f32(src, C[name], dst_f32, act, splitk)
 
         def sp(f, y, pool=None):
             return split3h(f, y, pool, overflow=ovf)
 
-        def resize_split(f_src, lv, rr_f32, r_split):
-            ops.resize_bilinear(f_src, L[lv], out=rr_f32)
-            sp(rr_f32, r_split)
+        def cs(src, name, dst_f32, y, pool=None, act="relu"):
+            """conv -> split (-> pool split): fused, or the f32 round trip"""
+            if self.fuse_split:
+                return conv_split(src, C[name], y, act, pool, ovf)
+            # (no split-K under a pool, as the fused form: the same sums, bit for bit)
+            return sp(conv(src, name, dst_f32, act, splitk=pool is None), y, pool)
+
+        def resize_split(f_src, lv, r_split):
+            if self.fuse_split:  # the resize written split, no f32 resized tensor
+                return resize_split3h(f_src, r_split, overflow=ovf)
+            rr = torch.empty((n, L[lv][0], L[lv][1], f_src.shape[-1]), dtype=torch.float32, device=x.device)
+            ops.resize_bilinear(f_src, L[lv], out=rr)
+            sp(rr, r_split)
 
         f0, f1, f2, f3, f4 = b["f0"], b["f1"], b["f2"], b["f3"], b["f4"]
         # encoder (unet.py:170-189)
-        sp(conv(b["x"], "conv1_1", f0[..., :64]), whole(b["s11"]))
-        sp(conv(b["s11"], "conv1_2", f0[..., :64]), seg(b["cat1"], 64, 64), pool=whole(b["p1"]))
-        sp(conv(b["p1"], "conv2_1", f1[..., :128]), whole(b["s21"]))
-        sp(conv(b["s21"], "conv2_2", f1[..., :128]), seg(b["cat2"], 128, 128), pool=whole(b["p2"]))
-        sp(conv(b["p2"], "conv3_1", f2[..., :256]), whole(b["s31"]))
-        sp(conv(b["s31"], "conv3_2", f2[..., :256]), whole(b["s32"]))
-        sp(conv(b["s32"], "conv3_3", f2[..., :256]), seg(b["cat3"], 256, 256), pool=whole(b["p3"]))
-        sp(conv(b["p3"], "conv4_1", f3), whole(b["s41"]))
-        sp(conv(b["s41"], "conv4_2", f3), whole(b["s42"]))
-        sp(conv(b["s42"], "conv4_3", f3), seg(b["cat4"], 512, 512), pool=whole(b["p4"]))
-        sp(conv(b["p4"], "conv5_1", f4), whole(b["s51"]))
+        cs(b["x"], "conv1_1", f0[..., :64], whole(b["s11"]))
+        cs(b["s11"], "conv1_2", f0[..., :64], seg(b["cat1"], 64, 64), pool=whole(b["p1"]))
+        cs(b["p1"], "conv2_1", f1[..., :128], whole(b["s21"]))
+        cs(b["s21"], "conv2_2", f1[..., :128], seg(b["cat2"], 128, 128), pool=whole(b["p2"]))
+        cs(b["p2"], "conv3_1", f2[..., :256], whole(b["s31"]))
+        cs(b["s31"], "conv3_2", f2[..., :256], whole(b["s32"]))
+        cs(b["s32"], "conv3_3", f2[..., :256], seg(b["cat3"], 256, 256), pool=whole(b["p3"]))
+        cs(b["p3"], "conv4_1", f3, whole(b["s41"]))
+        cs(b["s41"], "conv4_2", f3, whole(b["s42"]))
+        cs(b["s42"], "conv4_3", f3, seg(b["cat4"], 512, 512), pool=whole(b["p4"]))
+        cs(b["p4"], "conv5_1", f4, whole(b["s51"]))
         y52 = conv(b["s51"], "conv5_2", f4)
         # decoder: resize (f32) -> split -> conv (no bias, no relu) into the concat's up range (unet.py:191-200)
-        resize_split(y52, 3, b["rr3"], whole(b["r1"]))
-        sp(conv(b["r1"], "upconv_1", f3, act="none"), seg(b["cat4"], 0, 512))
+        resize_split(y52, 3, whole(b["r1"]))
+        cs(b["r1"], "upconv_1", f3, seg(b["cat4"], 0, 512), act="none")
         y44 = conv(b["cat4"], "conv4_4", f3)
-        resize_split(y44, 2, b["rr2"], whole(b["r2"]))
-        sp(conv(b["r2"], "upconv_2", f2[..., :256], act="none"), seg(b["cat3"], 0, 256))
+        resize_split(y44, 2, whole(b["r2"]))
+        cs(b["r2"], "upconv_2", f2[..., :256], seg(b["cat3"], 0, 256), act="none")
         y34 = conv(b["cat3"], "conv3_4", f2[..., :256])
-        resize_split(y34, 1, b["rr1"], whole(b["r3"]))
-        sp(conv(b["r3"], "upconv_3", f1[..., :128], act="none"), seg(b["cat2"], 0, 128))
+        resize_split(y34, 1, whole(b["r3"]))
+        cs(b["r3"], "upconv_3", f1[..., :128], seg(b["cat2"], 0, 128), act="none")
         y23 = conv(b["cat2"], "conv2_3", f1[..., :128])
-        resize_split(y23, 0, b["rr0"], whole(b["r4"]))
-        sp(conv(b["r4"], "upconv_4", f0[..., :64], act="none"), seg(b["cat1"], 0, 64))
+        resize_split(y23, 0, whole(b["r4"]))
+        cs(b["r4"], "upconv_4", f0[..., :64], seg(b["cat1"], 0, 64), act="none")
         # conv1_5 + sigmoid (unet.py:203-205): [l | h] x [Wh | Wl], then [h] x [Wh] + those logits, * 2^-t + bias
         alpha = b["out"] if out is None else out
         lg0 = b["lg0"]
         logits = f0[..., :1]
-        for k, (xs, yv, acc) in enumerate(((b["cat1"][..., :256], lg0, None), (b["cat1"][..., 256:], logits, lg0))):
+        for k, (xs, yv, acc) in enumerate(((b["cat1"], lg0, None), (b["cat1"][..., 128:], logits, lg0))):
             pc = self.head[k]
             xv, yvv = ops.nhwc(xs), ops.nhwc(yv)
             ops.check(ops.lib().vm_conv3x3_head_acc_ex_nhwc(
