@@ -6,10 +6,11 @@
 #   5. --kernel-trace --stats of the config-3 record, one pass per (dtype, size)            -> profiles/<tag>_temporal_<dtype>_<HxW>_kernel_stats.csv
 #   6. --kernel-trace --stats of the config-5 training step alone (8 x 320^2, bf16)        -> profiles/<tag>_train_kernel_stats.csv
 #   7. --kernel-trace --stats of the small_train.py step alone (8 x 320^2, bf16, graphs)   -> profiles/<tag>_train_small_kernel_stats.csv
-#   8. --kernel-trace --stats of train_image, train_chain, augment (batched), loader records and the bf16x6 forward
+#   8. --kernel-trace --stats of train_image, train_chain, augment (batched), loader records and the split forwards
+#      (f16x3 -> <tag>_x3_*, bf16x6 -> <tag>_x6_*)
 #                                                                                         -> profiles/<tag>_<record>_kernel_stats.csv
 #   9. the full bench (reads the profiles of 2-4)                                         -> gpurun_out/<tag>_bench.json
-# SKIP="fwd mfma traffic temporal train train_small train_image train_chain augment loader x6 bench" skips passes.
+# SKIP="fwd mfma traffic temporal train train_small train_image train_chain augment loader x3 x6 bench" skips passes.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 REPO=$(pwd)
 TAG=$1; shift
@@ -75,12 +76,16 @@ for rec in train_image train_chain augment loader; do
     grep "^{" "$OUT/$rec.log" | tail -n 1 > "$REPO/profiles/${TAG}_${rec}.json"
   fi
 done
-if ! skip x6; then
-run 300 x6.log rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/x6" -o run \
-    -- python3 "$REPO/tools/x6bench.py" 10
-cp "$(find "$OUT/x6" -name '*kernel_stats.csv' | head -n 1)" "$REPO/profiles/${TAG}_x6_kernel_stats.csv"
-grep -v "amdgpu.ids" "$OUT/x6.log" | grep -v "^[EW]20" > "$REPO/profiles/${TAG}_x6.log" || true
-fi
+# (r06) the split paths one at a time: f16x3 (x3) and bf16x6 (x6), each its forward alone
+for sp in x3:f16x3 x6:bf16x6; do
+  key=${sp%%:*}; dt=${sp##*:}
+  if ! skip $key; then
+    run 300 $key.log rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/$key" -o run \
+        -- python3 "$REPO/tools/x6bench.py" 10 $dt
+    cp "$(find "$OUT/$key" -name '*kernel_stats.csv' | head -n 1)" "$REPO/profiles/${TAG}_${key}_kernel_stats.csv"
+    grep -v "amdgpu.ids" "$OUT/$key.log" | grep -v "^[EW]20" > "$REPO/profiles/${TAG}_${key}.log" || true
+  fi
+done
 cp "$REPO"/profiles/${TAG}_* "$REPO/gpurun_out/"
 skip bench && exit 0
 run 600 bench.log python3 "$REPO/bench.py" --layers "$@"

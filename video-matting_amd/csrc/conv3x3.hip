@@ -6026,7 +6026,7 @@ static int conv_impl(const vm_tensor* x, const void* packed, int cin, int cout, 
   a.y = y->ptr; a.y_cstride = y->cstride; a.y_coff = y->coff; a.y_dtype = y->dtype;
   const int yve = 16 / elem_bytes(y->dtype);
   a.y_vec = (reinterpret_cast<uintptr_t>(y->ptr) % 16 == 0) && (y->cstride % yve == 0) && (y->coff % yve == 0);
-  if (yp) {
+  if (yp && !f16) {
     const bool pvec = reinterpret_cast<uintptr_t>(yp->ptr) % 16 == 0 && yp->cstride % 8 == 0 && yp->coff % 8 == 0;
     if (cout == 1 || dt != VM_BF16 || !pvec || !patch_ok(a, 2) || g_conv_kernel == 1 || g_conv_kernel == 2)
       return fail(VM_EUNSUPPORTED, "conv3x3_pool: fused pooling needs the bf16 patch kernel");

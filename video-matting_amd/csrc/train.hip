@@ -2109,7 +2109,47 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* part, in
   }
 }
 
+// The same fixed-order sum, 4 columns per lane (16-byte loads) and 16 row groups per block (r06): the 64-column form
+// kept one 256-byte run per row group in flight and read the partials at ~0.8 TB/s (UNetImage step: 18 reductions,
+// 45 us each, profiles/r05_train_image_kernel_stats.csv).  Each column's rows are summed in the order b = rg, rg + 16,
+// ... per group, then the 16 groups in order: deterministic (another order than wgrad_reduce_kernel's).
+__global__ __launch_bounds__(256) void wgrad_reduce4_kernel(const float* __restrict__ part, int rows, long S,
+                                                            float* __restrict__ dw) {
+  constexpr int RG = 16, CQ = 256 / RG;
+  __shared__ float4 sh[RG][CQ];
+  const int cq = threadIdx.x % CQ, rg = threadIdx.x / CQ;
+  const long i = ((long)blockIdx.x * CQ + cq) * 4;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (i < S) {
+#pragma unroll 4
+    for (int b = rg; b < rows; b += RG) {
+      const float4 v = *reinterpret_cast<const float4*>(part + (long)b * S + i);
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+  }
+  sh[rg][cq] = s;
+  __syncthreads();
+  if (rg == 0 && i < S) {
+    float4 t = sh[0][cq];
+#pragma unroll
+    for (int g = 1; g < RG; ++g) {
+      const float4 v = sh[g][cq];
+      t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
+    }
+    float4 d = *reinterpret_cast<float4*>(dw + i);
+    d.x += t.x; d.y += t.y; d.z += t.z; d.w += t.w;
+    *reinterpret_cast<float4*>(dw + i) = d;
+  }
+}
+
+static long g_wgrad_reduce4 = 1;  // vm_set_option "wgrad_reduce4": 0 = the r05 scalar-column reduction (A/B)
+
 static void launch_wgrad_reduce(const float* part, int rows, long S, float* dw, hipStream_t st) {
+  if (g_wgrad_reduce4 && S % 4 == 0 && reinterpret_cast<uintptr_t>(dw) % 16 == 0 &&
+      reinterpret_cast<uintptr_t>(part) % 16 == 0 && rows > 1) {
+    hipLaunchKernelGGL(wgrad_reduce4_kernel, dim3((unsigned)((S / 4 + 15) / 16)), dim3(256), 0, st, part, rows, S, dw);
+    return;
+  }
   if (S >= 64L * 512)
     hipLaunchKernelGGL(wgrad_reduce_kernel<64>, dim3((unsigned)((S + 63) / 64)), dim3(256), 0, st, part, rows, S, dw);
   else
@@ -2327,6 +2367,10 @@ static int launch_wgrad_taps_dma(WgArgs& a, float* dw, hipStream_t st) {
 }  // namespace trn
 
 int train_set_option(const char* key, long value) {
+  if (!strcmp(key, "wgrad_reduce4")) {
+    trn::g_wgrad_reduce4 = value;
+    return 1;
+  }
   if (!strcmp(key, "wgrad_variant")) {
     trn::g_wgrad_variant = value;
     return 1;
