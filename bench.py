@@ -1325,6 +1325,9 @@ def main():
                     help="profiling passes: run just this record (rank 0 / N=1) and print it")
     ap.add_argument("--temporal-sizes", default="500x1200,1080x1920", help="config-3 sizes HxW, comma separated")
     ap.add_argument("--temporal-dtypes", default="fp32,bf16", help="config-3 compute dtypes, comma separated")
+    ap.add_argument("--dummy-streams", type=int, default=0,
+                    help="(study) create this many idle HIP streams first: how the trainers' side streams map onto "
+                         "the hardware queues when a process already holds streams")
     ap.add_argument("--dist-selftest", action="store_true",
                     help="CPU-only: the N-rank launcher + gloo broadcast / uneven all-gather, no GPU")
     args = ap.parse_args()
@@ -1365,6 +1368,7 @@ def main():
         from vmatting import _lib
         _lib.set_option(k, int(v))
     cpu_model, threads = host_info()
+    _dummy = [torch.cuda.Stream(device=dev) for _ in range(args.dummy_streams)]  # noqa: F841 (study knob)
     if args.only:  # one record alone (rocprofv3 passes per record: tools/prof_bench.sh)
         if args.only == "train":
             rec = train_bench(dev, args.steps, args.warmup, world, rank, threads, cpu=False, graph=args.train_graph,

@@ -230,6 +230,14 @@ int vm_conv3x3_up2x_nhwc(const vm_tensor* x, const void* packed_up, const void* 
  * [3,3,head_cin,1], bf16-rounded like a packed head; taps 9..11 zero), the frame border included (from the border
  * pass's values).  cout == 64; VM_EUNSUPPORTED when a kernel-selection option rules out the patch kernel's register
  * epilogue (the caller then stores y and runs vm_conv3x3_head_partial_nhwc). */
+/* The folded upconv of the split-fp16 x3 path (unet.py:44-63 at f32 accuracy): x is the low-res split input [l, h]
+ * (VM_F16, S = x.c / 2 channels per slab, S % 32 == 0), packed_up the fp16 parts [Wh', Wl', Wh'] (cin = 3 S) of the
+ * folded filter of vm_conv3x3_fold_up2x_weights (pre-scaled by 2^t), packed the plain filter's parts at the same
+ * scale (the border pass: the resize of x = h + l in f32, split again); y = act((conv + bias) * scale + shift) in f32,
+ * written split as vm_conv3x3_split3_nhwc writes it ([n, 2h, 2w, cout], cout % 64 == 0, slab y_slab). */
+int vm_conv3x3_up2x_split3_nhwc(const vm_tensor* x, const void* packed_up, const void* packed, int cin, int cout,
+                                const float* bias, const float* scale, const float* shift, int act, vm_tensor* y,
+                                int y_slab, int* overflow, void* stream);
 int vm_conv3x3_up2x_head_nhwc(const vm_tensor* x, const void* packed_up, const void* packed, int cin, int cout,
                               const float* bias, const float* scale, const float* shift, int act, vm_tensor* y,
                               const float* head_w, int head_cin, int head_coff, float* partial, int store_y,

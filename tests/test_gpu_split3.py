@@ -140,6 +140,27 @@ def test_f16x3_fused_split_equals_unfused(n, h, w, vgg0):
     assert torch.equal(l0, m.conv1_3)
 
 
+@pytest.mark.parametrize("n,h,w", [(1, 72, 100), (2, 35, 61), (1, 64, 96)])
+def test_f16x3_folded_upconvs_match_the_resize_path(n, h, w, vgg0):
+    """The exact-2x upconvs on the folded filter (vm_conv3x3_up2x_split3_nhwc: interior phase filters + the split
+    border pass) against resize -> split -> conv: the same forward to f32 accumulation order (logits within 1e-6 of
+    their max), on odd sizes (the L2..L4 levels of 35 x 61: 18 x 31 ... where only some upconvs are exact 2x)."""
+    from vmatting import unet
+    np.random.seed(0)
+    m = unet.UNetVideo(vgg0, dtype="f16x3")
+    m.prepare()
+    x = torch.randn(n, h, w, 7, device=DEV) * 60
+    m._x6.fold_up = False
+    m.forward(x)
+    l0 = H(m.conv1_3)
+    m._x6.fold_up = True
+    m.forward(x)
+    l1 = H(m.conv1_3)
+    err = np.abs(l1 - l0).max() / np.abs(l0).max()
+    print("folded vs resize path: logits rel %.3e" % err)
+    assert err <= 1e-6
+
+
 @pytest.mark.parametrize("case", ["unet_video_70x90", "unet_video_64x96", "unet_image_70x90"])
 def test_unet_f16x3_matches_reference_golden(case, vgg0):
     from vmatting import unet

@@ -401,3 +401,21 @@ def test_split3_filter_parts_carry_the_scaled_filter():
         f2 = split3_filter(w, cin + 8, cout, t).numpy()
         assert not f2[:, :, cin:cin + 8].any() and np.array_equal(f2[:, :, cin + 8:2 * cin + 8], f[:, :, cin:2 * cin])
     assert torch.float16 is not None
+
+
+def test_split3_fold_up2x_is_resize_then_conv_inside_the_frame():
+    """vmatting.split3.fold_up2x: the phase filters of conv3x3(resize2x(x), W) (TF-1 legacy bilinear, unet.py:58-60)
+    reproduce it exactly away from the frame border, with the low-res frame replicated past its bottom / right edge
+    (the folded kernel's loads); the border rows / columns are the border pass's (tests/test_gpu_split3.py)."""
+    from oracle import ops as oo
+    from vmatting.split3 import fold_up2x
+    rs = np.random.RandomState(0)
+    for h, w, ci, co in ((6, 7, 5, 4), (9, 4, 3, 2)):
+        wt, x = rs.randn(3, 3, ci, co), rs.randn(2, h, w, ci)
+        ref = oo.conv3x3_same(oo.resize_bilinear_tf1(x, 2 * h, 2 * w), wt)
+        xp = np.pad(x, ((0, 0), (0, 1), (0, 1), (0, 0)), mode="edge")
+        y = oo.conv3x3_same(xp, fold_up2x(wt))[:, :h, :w]
+        got = np.zeros_like(ref)
+        for p in range(4):
+            got[:, p >> 1::2, p & 1::2] = y[..., p * co:(p + 1) * co]
+        assert np.abs(got - ref)[:, 1:-1, 1:-1].max() <= 1e-12 * np.abs(ref).max()

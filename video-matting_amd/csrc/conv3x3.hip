@@ -1043,7 +1043,9 @@ void conv3x3_patch(ConvArgs a) {
     const int ycs4 = ycs * 4;
     // split-fp16 x3 output (ConvArgs::ysplit): the same f32 staging, then 8 channels per thread split into [l, h, h]
     const bool ysp = a.ysplit > 0 && !splitk;
-    uint16_t* ys = reinterpret_cast<uint16_t*>(a.y) + a.y_coff + pix0 * (long)a.y_cstride;
+    // (a folded upconv's split output: [N, 2H, 2W] pixels from (2 r0, 2 c0), as the bf16 epilogues' yb)
+    uint16_t* ys = reinterpret_cast<uint16_t*>(a.y) + a.y_coff +
+                   (a.up ? ((long)n * 2 * H + 2 * r0) * YW + 2 * c0 : pix0) * (long)a.y_cstride;
     const __amdgpu_buffer_rsrc_t ysr = __builtin_amdgcn_make_buffer_rsrc(ys, 0, 0x7ffffff0, 0x00020000);
     bool ovf = false;
     for (int sl = 0; sl < BN / 64; ++sl) {
@@ -1054,10 +1056,13 @@ void conv3x3_patch(ConvArgs a) {
         for (int fc = 0; fc < FC; ++fc) {
           if (fc / 4 != sl % SPW) continue;
           const int col = (fc % 4) * 16 + 4 * (lane >> 4);
+          // (a folded upconv, split output only: the slab is one phase of up_cout channels, ConvArgs::up)
+          const int uph = a.up ? cb / a.up_cout : 0;
+          const int cbp = cb - uph * a.up_cout, ccap = a.up ? a.up_cout : a.cout;
           float mul[4], add[4];
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            const int co = min(cb + col + j, a.cout - 1);
+            const int co = min(cbp + col + j, ccap - 1);
             const float sc = (a.scale && !splitk) ? a.scale[co] : 1.f;
             mul[j] = sc;
             add[j] = splitk ? 0.f : (a.bias ? a.bias[co] : 0.f) * sc + (a.shift ? a.shift[co] : 0.f);
@@ -1089,12 +1094,15 @@ void conv3x3_patch(ConvArgs a) {
           const float v[8] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w};
           const int pr = rr / C::TW, pc = rr % C::TW;
           bool ok;
-          const int pix = out_pix(pr, pc, ok);
-          ok = ok && cb + cq * 8 < a.cout;
+          int pix = out_pix(pr, pc, ok);
+          const int uph = a.up ? cb / a.up_cout : 0;
+          const int cbp = cb - uph * a.up_cout;  // (the phase's own channel, a.up)
+          ok = ok && cbp + cq * 8 < (a.up ? a.up_cout : a.cout);
+          if (a.up) pix = (2 * pr + (uph >> 1)) * YW + 2 * pc + (uph & 1);
           uint4 hv, lv;
           const bool o = split3h_chunk(v, hv, lv);
           ovf |= ok && o;
-          const int off = ok ? pix * ycs2 + (cb + cq * 8) * 2 : OOB;
+          const int off = ok ? pix * ycs2 + (cbp + cq * 8) * 2 : OOB;
           const int off1 = ok ? off + S2 : OOB, off2 = ok ? off + 2 * S2 : OOB;
           typedef __attribute__((ext_vector_type(4))) unsigned u4_t;
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4_t, lv), ysr, off, 0, 0);
@@ -3938,7 +3946,21 @@ struct BorderArgs {
   float* hd;        // head split (cout == 64): per-tap head shares of the border pixels, as the conv's epilogue
   const float* hw;  // conv1_5 HWIO f32 [3,3,hw_cin,1]
   int hw_cin, hw_coff, y_skip;
+  // SPL (split-fp16 x3, vm_conv3x3_up2x_split3_nhwc): x is the low-res split input [l, h] (xs channels per slab; the
+  // K granules run over [l, h, h], nch = 3 xs / 32); y the split output (slab ysplit); ovf as ConvArgs::ovf
+  int xs, ysplit;
+  int* ovf;
 };
+
+// 8 fp16 values of a 16-byte chunk -> f32
+__device__ __forceinline__ void unpack_f16x8(uint4 u, float* f) {
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f[2 * i] = (float)__builtin_bit_cast(_Float16, (uint16_t)(w[i] & 0xffffu));
+    f[2 * i + 1] = (float)__builtin_bit_cast(_Float16, (uint16_t)(w[i] >> 16));
+  }
+}
 
 // Border pixels of the folded upconv, computed the unfused way: the 9 resized taps (TF1 legacy bilinear in f32,
 // rounded to bf16 as vm_resize_bilinear_tf1_nhwc stores them; zero outside the 2H x 2W frame) of 16 pixels are
@@ -3948,9 +3970,13 @@ struct BorderArgs {
 // double-buffered, with one LDS-only barrier per step) and adds the 4 partial sums in a fixed order at the end.
 __device__ __forceinline__ uint4 sel3(int i, uint4 a, uint4 b, uint4 c) { return i == 0 ? a : (i == 1 ? b : c); }
 
-template <int BD_KS>  // granule split of the border pass (waves = 4 x BD_KS)
+// SPL: the split-fp16 x3 form (the folded upconvs of vmatting/split3.py): each staged value is the resize of the f32
+// activation x = h + l (exact in f32), split again into fp16 (h', l'); K granule cc stages l' (slab 0) or h' (slabs 1,
+// 2) for the fp16 filter parts [Wh, Wl, Wh]; the output is written split (ConvArgs::ysplit's layout)
+template <int BD_KS, bool SPL = false>  // granule split of the border pass (waves = 4 x BD_KS)
 __global__ __launch_bounds__(256 * BD_KS) void conv3x3_up2x_border(BorderArgs a) {
   using T = uint16_t;
+  using MT = std::conditional_t<SPL, f16_t, uint16_t>;
   __shared__ __attribute__((aligned(16))) char stg[BD_KS][2][9 * 16 * 64];  // [split][buffer][tap][pixel][32 ch]
   __shared__ __attribute__((aligned(16))) float red[BD_KS * 16 * 64];       // [split][pixel][channel] partial sums
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -3982,19 +4008,35 @@ __global__ __launch_bounds__(256 * BD_KS) void conv3x3_up2x_border(BorderArgs a)
   const float ly = sy - fy0;
   const int cx0 = max(ox - 1, 0) >> 1;
   const T* xr = xb + ((long)pn * a.H) * a.W * (long)a.x_cstride + sq * 8;
-  auto gather = [&](int cc, uint4 (&g)[6]) __attribute__((always_inline)) {
+  // SPL: granule cc of [l, h, h] reads input channels (cc mod xs/32) * 32 of both stored slabs (l at 0, h at xs)
+  const int sg = SPL ? a.xs / 32 : 1;
+  auto gather = [&](int cc, uint4 (&g)[SPL ? 12 : 6]) __attribute__((always_inline)) {
+    const int cin0 = SPL ? (cc % sg) * 32 : cc * 32;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int j = 0; j < 3; ++j) {
         const int yy = i ? y1 : y0, xx = min(cx0 + j, a.W - 1);
-        g[i * 3 + j] = rok && cc < a.nch
-                           ? *reinterpret_cast<const uint4*>(xr + ((long)yy * a.W + xx) * a.x_cstride + cc * 32)
-                           : make_uint4(0, 0, 0, 0);
+        const T* p = xr + ((long)yy * a.W + xx) * a.x_cstride + cin0;
+        const bool ok = rok && cc < a.nch;
+        g[i * 3 + j] = ok ? *reinterpret_cast<const uint4*>(p) : make_uint4(0, 0, 0, 0);
+        if constexpr (SPL) g[6 + i * 3 + j] = ok ? *reinterpret_cast<const uint4*>(p + a.xs) : make_uint4(0, 0, 0, 0);
       }
   };
-  auto stage = [&](const uint4 (&g)[6], char* dst) __attribute__((always_inline)) {
+  auto stage = [&](const uint4 (&g)[SPL ? 12 : 6], char* dst, int cc) __attribute__((always_inline)) {
     if (sdh >= 3) return;
+    // SPL: the tap's f32 value x = h + l (exact), unpacked from both slabs
+    auto unp = [&](int k, float* f) __attribute__((always_inline)) {
+      if constexpr (SPL) {
+        float fl[8];
+        unpack_f16x8(k < 3 ? sel3(k, g[6], g[7], g[8]) : sel3(k - 3, g[9], g[10], g[11]), f);
+        unpack_f16x8(k < 3 ? sel3(k, g[0], g[1], g[2]) : sel3(k - 3, g[3], g[4], g[5]), fl);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) f[e] += fl[e];
+      } else {
+        Chunk<T>::unpack(k < 3 ? sel3(k, g[0], g[1], g[2]) : sel3(k - 3, g[3], g[4], g[5]), f);
+      }
+    };
 #pragma unroll
     for (int dw = 0; dw < 3; ++dw) {
       float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -4007,31 +4049,39 @@ __global__ __launch_bounds__(256 * BD_KS) void conv3x3_up2x_border(BorderArgs a)
         const float lx = sx - fx0;
         // (top row, then bottom row: fewer values live at once, the same arithmetic)
         float l8[8], r8[8], top[8];
-        Chunk<T>::unpack(sel3(x0 - cx0, g[0], g[1], g[2]), l8);
-        Chunk<T>::unpack(sel3(x1 - cx0, g[0], g[1], g[2]), r8);
+        unp(x0 - cx0, l8);
+        unp(x1 - cx0, r8);
 #pragma unroll
         for (int e = 0; e < 8; ++e) top[e] = l8[e] + (r8[e] - l8[e]) * lx;
-        Chunk<T>::unpack(sel3(x0 - cx0, g[3], g[4], g[5]), l8);
-        Chunk<T>::unpack(sel3(x1 - cx0, g[3], g[4], g[5]), r8);
+        unp(3 + x0 - cx0, l8);
+        unp(3 + x1 - cx0, r8);
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           const float bot = l8[e] + (r8[e] - l8[e]) * lx;
           o[e] = top[e] + (bot - top[e]) * ly;
         }
       }
-      *reinterpret_cast<uint4*>(dst + ((sdh * 3 + dw) * 16 + spx) * 64 + sq * 16) = Chunk<T>::pack(o);
+      uint4 q;
+      if constexpr (SPL) {
+        uint4 hq, lq;
+        split3h_chunk(o, hq, lq);
+        q = cc / sg == 0 ? lq : hq;
+      } else {
+        q = Chunk<T>::pack(o);
+      }
+      *reinterpret_cast<uint4*>(dst + ((sdh * 3 + dw) * 16 + spx) * 64 + sq * 16) = q;
     }
   };
   // filter fragments of this wave's 16 output channels: A rows = channels cob + 16 cg + (lane & 15)
   const T* wrow = wb + (long)(cob + cg * 16 + (lane & 15)) * a.K_pad + (lane >> 4) * 8;
   f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
   const int steps = (a.nch + BD_KS - 1) / BD_KS;  // every group runs the same number of steps (uniform barriers)
-  uint4 g[6];
+  uint4 g[SPL ? 12 : 6];
   gather(ks, g);
   for (int i = 0; i < steps; ++i) {
     const int cc = ks + i * BD_KS;
     char* buf = stg[ks][i & 1];
-    stage(g, buf);
+    stage(g, buf, cc);
     gather(cc + BD_KS, g);  // the group's next granule goes in flight under this one's barrier and MFMAs
     uint4 w[9];
     if (cc < a.nch) {
@@ -4045,7 +4095,7 @@ __global__ __launch_bounds__(256 * BD_KS) void conv3x3_up2x_border(BorderArgs a)
     if (cc < a.nch) {
 #pragma unroll
       for (int tap = 0; tap < 9; ++tap)
-        mma16<T>(w[tap], *reinterpret_cast<const uint4*>(buf + (tap * 16 + (lane & 15)) * 64 + (lane >> 4) * 16), acc);
+        mma16<MT>(w[tap], *reinterpret_cast<const uint4*>(buf + (tap * 16 + (lane & 15)) * 64 + (lane >> 4) * 16), acc);
     }
   }
   // partial sums: lane holds channels 16 cg + 4 (lane >> 4) + j of pixel lane & 15
@@ -4073,13 +4123,34 @@ __global__ __launch_bounds__(256 * BD_KS) void conv3x3_up2x_border(BorderArgs a)
       if (a.act == VM_ACT_RELU) v[j] = fmaxf(v[j], 0.f);
       else if (a.act == VM_ACT_SIGMOID) v[j] = sigmoid_precise(v[j]);
     }
-    pk.x = bf16x2_bits(v[0], v[1]);
-    pk.y = bf16x2_bits(v[2], v[3]);
-    if (!a.y_skip && bok)
-      *reinterpret_cast<uint2*>(reinterpret_cast<T*>(a.y) + (((long)n * OH + ey) * OW + ex) * (long)a.y_cstride +
-                                a.y_coff + cob + cq) = pk;
+    if constexpr (SPL) {  // [l, h(, h)] of the 4 channels
+      typedef _Float16 h2_t __attribute__((ext_vector_type(2)));
+      uint32_t hw2[2], lw2[2];
+      bool o = false;
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const h2_t hh = {(_Float16)v[2 * k], (_Float16)v[2 * k + 1]};
+        const h2_t ll = {(_Float16)(v[2 * k] - (float)hh[0]), (_Float16)(v[2 * k + 1] - (float)hh[1])};
+        hw2[k] = __builtin_bit_cast(uint32_t, hh);
+        lw2[k] = __builtin_bit_cast(uint32_t, ll);
+        o |= !(fabsf(v[2 * k]) < 65520.f) || !(fabsf(v[2 * k + 1]) < 65520.f);
+      }
+      if (bok) {
+        T* yo = reinterpret_cast<T*>(a.y) + (((long)n * OH + ey) * OW + ex) * (long)a.y_cstride + a.y_coff + cob + cq;
+        *reinterpret_cast<uint2*>(yo) = make_uint2(lw2[0], lw2[1]);
+        *reinterpret_cast<uint2*>(yo + a.ysplit) = make_uint2(hw2[0], hw2[1]);
+        if (3 * a.ysplit <= a.y_cstride) *reinterpret_cast<uint2*>(yo + 2 * a.ysplit) = make_uint2(hw2[0], hw2[1]);
+        if (o && a.ovf) *a.ovf = 1;
+      }
+    } else {
+      pk.x = bf16x2_bits(v[0], v[1]);
+      pk.y = bf16x2_bits(v[2], v[3]);
+      if (!a.y_skip && bok)
+        *reinterpret_cast<uint2*>(reinterpret_cast<T*>(a.y) + (((long)n * OH + ey) * OW + ex) * (long)a.y_cstride +
+                                  a.y_coff + cob + cq) = pk;
+    }
   }
-  if (a.hd) {  // (uniform: a.hd is a kernel argument; every thread reaches the barriers below)
+  if (!SPL && a.hd) {  // (uniform: a.hd is a kernel argument; every thread reaches the barriers below)
     // the border pixel's 64 bf16 outputs -> 9 per-tap shares sum_c bf16(hw[tap][coff + c]) * y[c] (f32, in channel
     // order); taps 9..11 zero like the MFMA epilogues'
     float* vals = reinterpret_cast<float*>(&stg[0][0][0]);  // [16 pixels][64]
@@ -4598,7 +4669,7 @@ static int launch_patch(ConvArgs& a, hipStream_t st) {
   static_assert(!(FIRST && PF), "FIRST uses the plain pipeline");
   constexpr int lds = FIRST ? C::LDS_FIRST : C::LDS;
   // fp16 operands (ConvArgs::f16, the split-fp16 forward): the same tiling on v_mfma_f32_16x16x32_f16
-  constexpr bool F16_OK = !FIRST && !UPSKIP && ABL == 0;
+  constexpr bool F16_OK = !FIRST && ABL == 0;
   const bool f16 = F16_OK && a.f16;
   if (a.f16 && !F16_OK) return fail(VM_EUNSUPPORTED, "conv3x3_patch: no fp16 instantiation of this tiling");
   static bool attr_set = false, attr16_set = false;
@@ -5691,6 +5762,62 @@ extern "C" int vm_conv3x3_up2x_nhwc(const vm_tensor* x, const void* packed_up, c
   return check_launch("conv3x3_up2x_border");
 }
 
+static bool split3_view_ok(const vm_tensor* t, int slab, int c) {
+  return t->dtype == VM_F16 && slab > 0 && slab % 8 == 0 && t->coff % 8 == 0 && t->cstride % 8 == 0 &&
+         t->coff + c <= slab && 2 * slab <= t->cstride && reinterpret_cast<uintptr_t>(t->ptr) % 16 == 0;
+}
+
+extern "C" int vm_conv3x3_up2x_split3_nhwc(const vm_tensor* x, const void* packed_up, const void* packed, int cin,
+                                           int cout, const float* bias, const float* scale, const float* shift, int act,
+                                           vm_tensor* y, int y_slab, int* overflow, void* stream) {
+  if (!valid_tensor(x, true) || !valid_tensor(y, true) || !packed_up || !packed)
+    return fail(VM_EINVAL, "conv3x3_up2x_split3: invalid tensor/weights");
+  const int S = x->c / 2;
+  if (x->dtype != VM_F16 || y->dtype != VM_F16 || x->c % 64 || cin != 3 * S || y->c != cout)
+    return fail(VM_EINVAL, "conv3x3_up2x_split3: fp16 views, x = [l, h] slabs of S %% 32 == 0 channels, cin = 3 S "
+                           "(x.c=%d cin=%d y.c=%d cout=%d)", x->c, cin, y->c, cout);
+  if (y->n != x->n || y->h != 2 * x->h || y->w != 2 * x->w)
+    return fail(VM_EINVAL, "conv3x3_up2x_split3: output must be [%d,%d,%d,%d]", x->n, 2 * x->h, 2 * x->w, cout);
+  if (act < VM_ACT_NONE || act >= VM_ACT_SOFTMAX) return fail(VM_EINVAL, "conv3x3_up2x_split3: act %d", act);
+  const int ys = y_slab > 0 ? y_slab : y->cstride / 2;
+  const PackGeom g = geom(cin, 4 * cout, VM_F16), g1 = geom(cin, cout, VM_F16);
+  const bool xvec = reinterpret_cast<uintptr_t>(x->ptr) % 16 == 0 && x->cstride % 8 == 0 && x->coff % 8 == 0 &&
+                    x->coff + x->c <= x->cstride;
+  if (cout % 64 || !xvec || !split3_view_ok(y, ys, cout) || !g_up_skip || g_conv_kernel == 1 || g_conv_kernel == 2)
+    return fail(VM_EUNSUPPORTED, "conv3x3_up2x_split3: cout %% 64 == 0, 16-byte channel views, the split layout");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  ConvArgs a{};
+  a.x = x->ptr; a.x_cstride = x->cstride; a.x_coff = x->coff; a.H = x->h; a.W = x->w;
+  a.M = (long)x->n * x->h * x->w;
+  fill_geom(a, g);
+  a.w = packed_up; a.cout = 4 * cout;
+  a.bias = bias; a.scale = scale; a.shift = shift; a.act = act;
+  a.y = y->ptr; a.y_cstride = y->cstride; a.y_coff = y->coff;
+  a.y_dtype = VM_F32;  // f32 staging, split stores (ConvArgs::ysplit)
+  a.y_vec = 1;
+  a.ysplit = ys;
+  a.ovf = overflow;
+  a.f16 = 1;
+  a.xalias = S;
+  a.up = 1; a.up_cout = cout;
+  a.ksplit = 1;
+  if (!patch_ok(a, 2)) return fail(VM_EUNSUPPORTED, "conv3x3_up2x_split3: shape not supported by the patch kernel");
+  int rc = dispatch_patch(a, st);
+  if (rc != VM_OK) return rc;
+  BorderArgs b{};
+  b.x = x->ptr; b.x_cstride = x->cstride; b.x_coff = x->coff; b.H = x->h; b.W = x->w; b.nframes = x->n;
+  b.w = packed; b.K_pad = g1.K_pad; b.cout = cout; b.nch = g1.cin_pad / 32;
+  b.bias = bias; b.scale = scale; b.shift = shift; b.act = act;
+  b.y = y->ptr; b.y_cstride = y->cstride; b.y_coff = y->coff;
+  b.xs = S; b.ysplit = ys; b.ovf = overflow;
+  const int OH = 2 * x->h, OW = 2 * x->w;
+  b.nb = 2 * OW + 2 * (OH - 2);
+  const long nblk = ((long)x->n * b.nb + 15) / 16;
+  if (nblk > 0x7fffffffL) return fail(VM_EUNSUPPORTED, "conv3x3_up2x_split3: too many border pixels");
+  hipLaunchKernelGGL((conv3x3_up2x_border<4, true>), dim3((unsigned)nblk, cout / 64), dim3(1024), 0, st, b);
+  return check_launch("conv3x3_up2x_border(split)");
+}
+
 extern "C" int vm_conv3x3_up2x_head_nhwc(const vm_tensor* x, const void* packed_up, const void* packed, int cin,
                                          int cout, const float* bias, const float* scale, const float* shift, int act,
                                          vm_tensor* y, const float* head_w, int head_cin, int head_coff, float* partial,
@@ -5794,10 +5921,6 @@ extern "C" int vm_conv3x3_head_acc_ex_nhwc(const vm_tensor* x, const void* packe
                    nullptr, y_acc);
 }
 
-static bool split3_view_ok(const vm_tensor* t, int slab, int c) {
-  return t->dtype == VM_F16 && slab > 0 && slab % 8 == 0 && t->coff % 8 == 0 && t->cstride % 8 == 0 &&
-         t->coff + c <= slab && 2 * slab <= t->cstride && reinterpret_cast<uintptr_t>(t->ptr) % 16 == 0;
-}
 
 extern "C" int vm_conv3x3_split3_nhwc(const vm_tensor* x, const void* packed, int cin, int cout, const float* bias,
                                       const float* scale, const float* shift, int act, vm_tensor* y, int y_slab,

@@ -113,6 +113,8 @@ SIGNATURES = [
     ("vm_split6_nhwc", c_int, [P, P, P, c_void_p]),
     ("vm_split3h_nhwc", c_int, [P, P, P, c_int, c_void_p, c_void_p]),
     ("vm_resize_split3h_nhwc", c_int, [P, P, c_int, c_void_p, c_void_p]),
+    ("vm_conv3x3_up2x_split3_nhwc", c_int, [P, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int,
+                                            P, c_int, c_void_p, c_void_p]),
     ("vm_conv3x3_split3_nhwc", c_int, [P, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, P, c_int, P,
                                        c_int, c_void_p, c_void_p, c_size_t, c_void_p]),
     ("vm_bn_workspace_bytes", c_size_t, [P]),

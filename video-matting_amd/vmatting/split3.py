@@ -63,15 +63,39 @@ def split2h(w):
 
 
 def split3_filter(w_hwio, cin, cout, t):
-    """[3,3,ci,co] f32 filter, scale 2^t -> the [3,3,3*cin,cout] stack of the parts of w * 2^t in slab order (zero rows
-    past ci, zero columns past co)."""
-    w = torch.as_tensor(np.asarray(w_hwio, np.float32), dtype=torch.float32) * float(t)  # exact: a power of two
+    """[3,3,ci,co] filter (f32, or f64 for a folded one), scale 2^t -> the [3,3,3*cin,cout] f32 stack of the fp16 parts
+    of w * 2^t in slab order (zero rows past ci, zero columns past co).  Split in float64: h = fp16(w * 2^t), l =
+    fp16(w * 2^t - h) (for an f32 w the same parts as in f32, whose difference is exact)."""
+    w = torch.from_numpy(np.asarray(w_hwio, np.float64) * float(t))  # exact: a power of two
     ci, co = int(w.shape[2]), int(w.shape[3])
-    parts = split2h(w)
+    h = w.half().double()
+    parts = (h.float(), (w - h).half().float())
     out = torch.zeros((3, 3, 3 * cin, cout), dtype=torch.float32)
     for p, k in enumerate(W_PARTS):
         out[:, :, p * cin:p * cin + ci, :co] = parts[k]
     return out
+
+
+# TF-1 legacy bilinear 2x (scale 0.5) as a phase filter: resized row 2i + a blends low-res rows by R[a] (rows: the
+# low-res tap u = offset u - 1, columns: the 3x3 kernel row kh), the same table as csrc/conv3x3.hip fold_up2x_weights
+_R = np.array([[[.5, 0., 0.], [.5, 1., .5], [0., 0., .5]], [[0., 0., 0.], [1., .5, 0.], [0., .5, 1.]]])
+
+
+def fold_up2x(w_hwio):
+    """conv3x3(resize2x(x), w) = conv3x3(x, W') away from the frame border: W' [3,3,cin,4*cout] (channel p*cout + co =
+    phase p = 2a + b of output channel co, pixel (2i + a, 2j + b)), in float64 (vm_conv3x3_fold_up2x_weights rounds it
+    to f32; here the fp16 parts are cut from the exact sum)."""
+    w = np.asarray(w_hwio, np.float64)
+    co = w.shape[3]
+    out = np.zeros((3, 3, w.shape[2], 4 * co))
+    for p in range(4):
+        out[..., p * co:(p + 1) * co] = np.einsum("uk,vl,klio->uvio", _R[p >> 1], _R[p & 1], w)
+    return out
+
+
+# upconvs whose resize is an exact 2x (unet.py:191-200 at 1080p: upconv_2..4; upconv_1's 68 -> 135 is not): the resize
+# folded into the filter (vm_conv3x3_up2x_split3_nhwc), zero phase taps skipped (25 of 36), no resized tensor
+FOLD = ("upconv_2", "upconv_3", "upconv_4")
 
 
 def split3h(x, y, pool=None, slab=0, overflow=None):
@@ -144,6 +168,24 @@ def conv_split(x, pc, y, act="relu", pool=None, overflow=None, y_slab=0, pool_sl
     return y
 
 
+def up_split(x, pc_up, pc, y, overflow=None, act="none", y_slab=0):
+    """vm_conv3x3_up2x_split3_nhwc: the folded 2x upconv of the low-res split input x ([l, h]) into the full-res split
+    view y (pc_up: the folded filter's parts, pc: the plain filter's, for the border pass; same scale)."""
+    xv, yv = ops.nhwc(x), ops.nhwc(y)
+    p = _prof_begin()
+    ops.check(ops.lib().vm_conv3x3_up2x_split3_nhwc(
+        ops.ctypes.byref(xv), ops._ptr(pc_up.packed), ops._ptr(pc.packed), pc.cin, pc.cout, ops._ptr(pc.bias),
+        ops._ptr(pc.scale), ops._ptr(pc.shift), ops._lib.ACT[act], ops.ctypes.byref(yv), int(y_slab),
+        ops._ptr(overflow), ops.stream_handle()), "conv3x3_up2x_split3")
+    if p is not None:  # FLOPs of the unfolded conv it stands for (its output pixels)
+        prof, ev0, ev1 = p
+        ev1.record()
+        n, h, w, _ = y.shape
+        prof.append((2 * n * h * w * 9 * pc.cin * pc.cout, ops._lib.last_conv_kernel(), ev0, ev1,
+                     (n, h, w, pc.cin, pc.cout)))
+    return y
+
+
 def whole(buf):
     """The split-layout view of all channels of a 2*S-wide split buffer [l, h]."""
     return buf[..., :buf.shape[-1] // 2]
@@ -159,12 +201,15 @@ class Split3Forward:
 
     # conv -> split in the conv's epilogue (vm_conv3x3_split3_nhwc); False: f32 output + vm_split3h_nhwc (A/B)
     fuse_split = True
+    # the exact-2x upconvs on the folded filter (fuse_split only); False: resize -> split -> conv (A/B)
+    fold_up = True
 
     def __init__(self, model):
         self.m = model
         self.dev = model.device
         self.convs = {}
         self.scales = {}
+        self.up = {}  # folded upconv filters (FOLD)
         for name, cin, cout in LAYERS:
             w, b = model.params[name]
             t = filter_scale(w)
@@ -181,6 +226,13 @@ class Split3Forward:
             cp = cin
             if name == "conv1_1":
                 cp = 16  # slabs of 16 (8 live) + a zero 4th slab: 64 channels, two whole 32-channel granules
+            if name in FOLD:  # one scale for the folded filter and the plain one (its border pass)
+                wu = fold_up2x(w)
+                t = min(t, filter_scale(wu))  # max |W' * 2^t| and max |W * 2^t| both <= 2^12
+                self.scales[name] = t
+                self.up[name] = ops.PackedConv(split3_filter(wu, cin, 4 * cout, t), None, "f16", self.dev,
+                                               scale=np.full(cout, 1.0 / t, np.float32),
+                                               shift=np.zeros(cout, np.float32))
             wf = split3_filter(w, cp, cout, t)
             if name == "conv1_1":
                 wf = torch.cat([wf, torch.zeros((3, 3, 16, cout))], 2)
@@ -193,7 +245,8 @@ class Split3Forward:
 
     def weights_flat(self):
         out = []
-        for pc in [self.convs[k] for k in sorted(self.convs) if k != "conv1_5"] + self.head:
+        for pc in [self.convs[k] for k in sorted(self.convs) if k != "conv1_5"] + self.head + [self.up[k] for k in
+                                                                                             sorted(self.up)]:
             out.append(pc.packed)
             for t in (pc.bias, pc.scale, pc.shift):
                 if t is not None:
@@ -214,6 +267,7 @@ class Split3Forward:
              "p2": S(2, 128), "s31": S(2, 256), "s32": S(2, 256), "cat3": S(2, 512), "r2": S(2, 512),
              "p3": S(3, 256), "s41": S(3, 512), "s42": S(3, 512), "cat4": S(3, 1024), "r1": S(3, 512),
              "p4": S(4, 512), "s51": S(4, 512),
+             "c44s": S(3, 512), "c34s": S(2, 256), "c23s": S(1, 128),  # the folded upconvs' low-res inputs
              "f0": F(0, 128), "f1": F(1, 256), "f2": F(2, 512), "f3": F(3, 512), "f4": F(4, 512),
              "lg0": F(0, 1), "out": F(0, 1)}
         self._b, self._key = b, (n, h, w)
@@ -271,15 +325,23 @@ class Split3Forward:
         # decoder: resize (f32) -> split -> conv (no bias, no relu) into the concat's up range (unet.py:191-200)
         resize_split(y52, 3, whole(b["r1"]))
         cs(b["r1"], "upconv_1", f3, seg(b["cat4"], 0, 512), act="none")
-        y44 = conv(b["cat4"], "conv4_4", f3)
-        resize_split(y44, 2, whole(b["r2"]))
-        cs(b["r2"], "upconv_2", f2[..., :256], seg(b["cat3"], 0, 256), act="none")
-        y34 = conv(b["cat3"], "conv3_4", f2[..., :256])
-        resize_split(y34, 1, whole(b["r3"]))
-        cs(b["r3"], "upconv_3", f1[..., :128], seg(b["cat2"], 0, 128), act="none")
-        y23 = conv(b["cat2"], "conv2_3", f1[..., :128])
-        resize_split(y23, 0, whole(b["r4"]))
-        cs(b["r4"], "upconv_4", f0[..., :64], seg(b["cat1"], 0, 64), act="none")
+        fold = self.fold_up and self.fuse_split
+
+        def level(src_cat, conv_name, f_dst, s_name, lv, r_name, up_name, y):
+            """conv (relu) over the concat -> upconv (no bias, no relu) into the next concat's up range: the folded
+            2x upconv on its split low-res output where the resize is an exact 2x, else f32 -> resize -> split ->
+            conv (unet.py:192-200)"""
+            if fold and L[lv] == (2 * L[lv + 1][0], 2 * L[lv + 1][1]):
+                cs(b[src_cat], conv_name, f_dst, whole(b[s_name]))
+                up_split(b[s_name], self.up[up_name], C[up_name], y, ovf)
+            else:
+                f = conv(b[src_cat], conv_name, f_dst)
+                resize_split(f, lv, whole(b[r_name]))
+                cs(b[r_name], up_name, f_dst, y, act="none")
+
+        level("cat4", "conv4_4", f3, "c44s", 2, "r2", "upconv_2", seg(b["cat3"], 0, 256))
+        level("cat3", "conv3_4", f2[..., :256], "c34s", 1, "r3", "upconv_3", seg(b["cat2"], 0, 128))
+        level("cat2", "conv2_3", f1[..., :128], "c23s", 0, "r4", "upconv_4", seg(b["cat1"], 0, 64))
         # conv1_5 + sigmoid (unet.py:203-205): [l | h] x [Wh | Wl], then [h] x [Wh] + those logits, * 2^-t + bias
         alpha = b["out"] if out is None else out
         lg0 = b["lg0"]
