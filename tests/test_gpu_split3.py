@@ -123,13 +123,15 @@ def test_f16x3_conv_matches_float64(n, h, w, cin, cout, splitk):
 
 @pytest.mark.parametrize("n,h,w", [(1, 72, 100), (2, 35, 61)])
 def test_f16x3_fused_split_equals_unfused(n, h, w, vgg0):
-    """vm_conv3x3_split3_nhwc (split + pool split in the conv epilogue, split-K reduction included) against the f32
-    output + vm_split3h_nhwc round trip: the same forward, bit for bit."""
+    """vm_conv3x3_split3_nhwc (split + pool split in the conv epilogue — the patch kernel's staged epilogue, the
+    row-stationary kernel's register one, the split-K reduction) and the fused resize + split against the f32 output
+    + vm_split3h_nhwc round trip: the same forward, bit for bit."""
     from vmatting import unet
     np.random.seed(0)
     m = unet.UNetVideo(vgg0, dtype="f16x3")
     m.prepare()
     x = torch.randn(n, h, w, 7, device=DEV) * 60
+    m._x6.fold_up = False  # (the folded upconvs are another arithmetic: test_f16x3_folded_upconvs_match_...)
     m._x6.fuse_split = False
     a0 = m.forward(x).clone()
     l0 = m.conv1_3.clone()

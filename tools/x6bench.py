@@ -14,6 +14,11 @@ import torch  # noqa: E402
 from vmatting import ops, unet, video  # noqa: E402
 from vmatting.weights import synthetic_vgg16  # noqa: E402
 
+# VM_OPT="key=value,key=value": vm_set_option knobs first (A/B runs)
+for kv in filter(None, os.environ.get("VM_OPT", "").split(",")):
+    k, v = kv.split("=")
+    from vmatting import _lib
+    _lib.set_option(k, int(v))
 steps = int(sys.argv[1]) if len(sys.argv) > 1 else 10
 dts = sys.argv[2:] or ["f16x3", "bf16x6", "fp32", "bf16"]
 x = video.synthetic_frames(1, 1080, 1920, first=0, device="cuda")

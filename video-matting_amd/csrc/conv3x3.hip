@@ -4951,7 +4951,8 @@ static bool patch_ok(const ConvArgs& a, size_t tsize) {
   // bf16 output (16-byte aligned view), or f32 output without the fused pool / folded resize (cout multiple of 4;
   // dword stores when the view is not 16-byte aligned)
   const bool yok = a.y_dtype == VM_BF16 ? (a.cout & 7) == 0 && a.y_vec
-                                        : (a.y_dtype == VM_F32 && (!a.py || a.ysplit) && !a.up && (a.cout & 3) == 0);
+                                        : (a.y_dtype == VM_F32 && (!a.py || a.ysplit) && (!a.up || a.ysplit) &&
+                                           (a.cout & 3) == 0);
   return tsize == 2 && a.chunk_major && a.cin_pad % 32 == 0 && yok && a.act != VM_ACT_SOFTMAX &&
          (a.x_src_c <= 0 || a.x_src_c % 32 == 0);
 }

@@ -89,10 +89,26 @@ struct RowTile {
   int n, r0, c0, n0;
 };
 
-template <int TH>
+// split-fp16 x3 output of 4 channels: h = fp16(v), l = fp16(v - h) as two 8-byte quads; true if some |v| >= 65520
+__device__ __forceinline__ bool split4h(const float (&v)[4], uint2& h, uint2& l) {
+  typedef _Float16 h2_t __attribute__((ext_vector_type(2)));
+  typedef float f2_t __attribute__((ext_vector_type(2)));
+  const f2_t a = {v[0], v[1]}, b = {v[2], v[3]};
+  const h2_t ha = __builtin_convertvector(a, h2_t), hb = __builtin_convertvector(b, h2_t);
+  const f2_t ra = {v[0] - (float)ha[0], v[1] - (float)ha[1]}, rb = {v[2] - (float)hb[0], v[3] - (float)hb[1]};
+  h = make_uint2(__builtin_bit_cast(uint32_t, ha), __builtin_bit_cast(uint32_t, hb));
+  l = make_uint2(__builtin_bit_cast(uint32_t, __builtin_convertvector(ra, h2_t)),
+                 __builtin_bit_cast(uint32_t, __builtin_convertvector(rb, h2_t)));
+  return !(fabsf(v[0]) < 65520.f) || !(fabsf(v[1]) < 65520.f) || !(fabsf(v[2]) < 65520.f) || !(fabsf(v[3]) < 65520.f);
+}
+
+// SPL: the split-fp16 x3 form (vmatting/split3.py): fp16 operands (v_mfma_f32_16x16x32_f16) and the output written
+// split as [l, h(, h)] slabs (ConvArgs::ysplit / psplit / ovf) from the same register epilogue
+template <int TH, bool SPL = false>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void conv3x3_rows(ConvArgs a) {
   using C = RowsCfg<TH>;
   using T = uint16_t;
+  using MT = std::conditional_t<SPL, f16_t, uint16_t>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int R = C::R, FC = C::FC, XPW = C::XPW, WPW = C::WPW, PW = C::PW;
 
@@ -263,7 +279,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
 #pragma unroll
           for (int pf = 0; pf < 2; ++pf) {
             const uint4& wv = kh == 0 ? w0[kw][f] : (kh == 1 ? w1[kw][f] : k2[kw][f]);
-            mma16<T>(wv, x[kw][pf], acc[o][f][pf]);
+            mma16<MT>(wv, x[kw][pf], acc[o][f][pf]);
           }
       }
   };
@@ -272,6 +288,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
   // of pixel (r0 + rg*R + o, c0 + pf*16 + col).  bias / inference-BN affine / act, bf16, one 8-byte store each;
   // a.up scatters phase (n0 / up_cout) to pixel (2h + p/2, 2w + p%2); a.py gets the 2x2 SAME max-pool (rows o, o+1
   // in this lane, columns col, col+1 in the neighbouring lane; positions past the frame never win)
+  bool ovf = false;  // SPL: some output left fp16's range
   auto epilogue = [&](const RowTile& tt) __attribute__((always_inline)) {
     const int phase = a.up ? tt.n0 / a.up_cout : 0;
     const int cb = tt.n0 - phase * a.up_cout;  // first (per-phase) output channel of the tile
@@ -313,7 +330,37 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
             v[o][f][j] = t;
           }
         const int pix = a.up ? (2 * r + (phase >> 1)) * YW + 2 * c + (phase & 1) : r * W + c;
-        if constexpr (FC == 2) {
+        if constexpr (SPL) {  // [l, h(, h)]: slab distance ysplit, the third where the pixel row holds it
+          typedef __attribute__((ext_vector_type(4))) unsigned u4_t;
+          typedef __attribute__((ext_vector_type(2))) unsigned u2_t;
+          const int S2 = a.ysplit * 2;
+          const bool y3 = 3 * a.ysplit <= a.y_cstride;
+          uint2 hq[FC], lq[FC];
+          bool o2 = false;
+#pragma unroll
+          for (int f = 0; f < FC; ++f) o2 |= split4h(v[o][f], hq[f], lq[f]);
+          if constexpr (FC == 2) {
+            const int chan = cb + cg * C::CW + c16 * 8;
+            const bool ok = r < H && c < W && chan < ccap;
+            ovf |= ok && o2;
+            const int off = ok ? (pix * a.y_cstride + chan) * 2 : OOB;
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4_t, chunk_pair(lq[0], lq[1])), yrs, off, 0, 0);
+            const uint4 dh = chunk_pair(hq[0], hq[1]);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4_t, dh), yrs, ok ? off + S2 : OOB, 0, 0);
+            if (y3) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4_t, dh), yrs, ok ? off + 2 * S2 : OOB, 0, 0);
+          } else {
+#pragma unroll
+            for (int f = 0; f < FC; ++f) {
+              const int chan = cb + cg * C::CW + f * 16 + 4 * ck;
+              const bool ok = r < H && c < W && chan < ccap;
+              ovf |= ok && o2;
+              const int off = ok ? (pix * a.y_cstride + chan) * 2 : OOB;
+              __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2_t, lq[f]), yrs, off, 0, 0);
+              __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2_t, hq[f]), yrs, ok ? off + S2 : OOB, 0, 0);
+              if (y3) __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2_t, hq[f]), yrs, ok ? off + 2 * S2 : OOB, 0, 0);
+            }
+          }
+        } else if constexpr (FC == 2) {
           const int chan = cb + cg * C::CW + c16 * 8;
           const uint4 d = chunk_pair(pack4(v[o][0]), pack4(v[o][1]));
           const bool ok = r < H && c < W && chan < ccap;
@@ -348,7 +395,36 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
             }
           const int pr = r >> 1, pc = c >> 1;
           const bool pok = (col & 1) == 0 && pr < PH && pc < PWo;
-          if constexpr (FC == 2) {
+          if constexpr (SPL) {
+            typedef __attribute__((ext_vector_type(4))) unsigned u4_t;
+            typedef __attribute__((ext_vector_type(2))) unsigned u2_t;
+            const int P2 = a.psplit * 2;
+            const bool p3 = 3 * a.psplit <= a.py_cstride;
+            uint2 hq[FC], lq[FC];
+#pragma unroll
+            for (int f = 0; f < FC; ++f) split4h(m[f], hq[f], lq[f]);
+            if constexpr (FC == 2) {
+              const int chan = tt.n0 + cg * C::CW + c16 * 8;
+              const int off = pok && chan < a.cout ? ((pr * PWo + pc) * a.py_cstride + chan) * 2 : OOB;
+              const uint4 dh = chunk_pair(hq[0], hq[1]);
+              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4_t, chunk_pair(lq[0], lq[1])), prs, off, 0, 0);
+              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4_t, dh), prs, off == OOB ? OOB : off + P2, 0, 0);
+              if (p3)
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4_t, dh), prs, off == OOB ? OOB : off + 2 * P2, 0,
+                                                       0);
+            } else {
+#pragma unroll
+              for (int f = 0; f < FC; ++f) {
+                const int chan = tt.n0 + cg * C::CW + f * 16 + 4 * ck;
+                const int off = pok && chan < a.cout ? ((pr * PWo + pc) * a.py_cstride + chan) * 2 : OOB;
+                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2_t, lq[f]), prs, off, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2_t, hq[f]), prs, off == OOB ? OOB : off + P2, 0, 0);
+                if (p3)
+                  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2_t, hq[f]), prs, off == OOB ? OOB : off + 2 * P2,
+                                                        0, 0);
+              }
+            }
+          } else if constexpr (FC == 2) {
             const int chan = tt.n0 + cg * C::CW + c16 * 8;
             const uint4 d = chunk_pair(pack4(m[0]), pack4(m[1]));
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, d),
@@ -464,6 +540,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
     if (s < S) step(std::integral_constant<int, 1>{});
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // dummy DMAs past the end must land before the block exits
+  if (SPL && ovf && a.ovf) *a.ovf = 1;  // a plain vector store: any writer's 1 is the answer
 }
 
 // the row-stationary kernel takes: bf16 in / bf16 out (16-byte aligned views), chunk-major 32-channel granules, no
@@ -471,7 +548,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
 bool rows_ok(const ConvArgs& a) {
   const long img_in = (long)a.H * a.W * a.x_cstride * 2;
   const long img_out = (long)(a.up ? 4 : 1) * a.H * a.W * a.y_cstride * 2;
-  return a.chunk_major && a.cin_pad % 32 == 0 && a.y_dtype == VM_BF16 && a.y_vec && (a.cout & 7) == 0 &&
+  // (SPL: fp16 operands with the split output, ConvArgs::ysplit; plain f16 with an f32 output stays on the patch kernel)
+  const bool yok = a.f16 ? a.ysplit > 0 : a.y_dtype == VM_BF16;
+  return a.chunk_major && a.cin_pad % 32 == 0 && yok && a.y_vec && (a.cout & 7) == 0 &&
          a.act != VM_ACT_SOFTMAX && a.ksplit <= 1 && (a.x_src_c <= 0 || a.x_src_c % 32 == 0) &&
          (!a.up || a.up_cout % 64 == 0) && img_in < 0x7ffffff0L && img_out < 0x7ffffff0L &&
          (!a.py || (a.py_cstride % 8 == 0 && a.py_coff % 8 == 0)) &&
@@ -480,14 +559,14 @@ bool rows_ok(const ConvArgs& a) {
 
 static int g_num_cu = 0;
 
-template <int TH>
+template <int TH, bool SPL>
 static int launch_th(ConvArgs& a, hipStream_t st) {
   using C = RowsCfg<TH>;
   const int lds = C::LDS + 8 * (a.up ? a.up_cout : a.cout);  // + the epilogue constants table
   if (lds > 163840) return fail(VM_EUNSUPPORTED, "conv3x3_rows: %d output channels overflow LDS", a.cout);
   static bool attr_set = false;  // idempotent; benign race
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3_rows<TH>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3_rows<TH, SPL>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
     if (e != hipSuccess) return fail(VM_EHIP, "hipFuncSetAttribute(rows): %s", hipGetErrorString(e));
     attr_set = true;
@@ -507,15 +586,19 @@ static int launch_th(ConvArgs& a, hipStream_t st) {
   // persistent: one block per CU (LDS-limited), a multiple of 8 so every XCD gets the same number of blocks
   long grid = g_num_cu < a.tiles_total ? g_num_cu : a.tiles_total;
   grid = (grid + 7) / 8 * 8;
-  snprintf(g_last_kernel, sizeof g_last_kernel, "vm::conv3x3_rows<%d>", TH);
-  hipLaunchKernelGGL((conv3x3_rows<TH>), dim3(grid), dim3(512), lds, st, a);
+  snprintf(g_last_kernel, sizeof g_last_kernel, SPL ? "vm::conv3x3_rows<%d, true>" : "vm::conv3x3_rows<%d>", TH);
+  hipLaunchKernelGGL((conv3x3_rows<TH, SPL>), dim3(grid), dim3(512), lds, st, a);
   return check_launch("conv3x3_rows");
 }
 
 // cfg: 16 or 8 = tile height (TH 8: 2 row groups x 4 channel groups of 16)
 int launch_rows(ConvArgs& a, hipStream_t st, int cfg) {
-  if (cfg == 8) return launch_th<8>(a, st);
-  return launch_th<16>(a, st);
+  if (a.f16) {
+    if (a.ysplit <= 0) return fail(VM_EUNSUPPORTED, "conv3x3_rows: fp16 operands need the split output");
+    return cfg == 8 ? launch_th<8, true>(a, st) : launch_th<16, true>(a, st);
+  }
+  if (cfg == 8) return launch_th<8, false>(a, st);
+  return launch_th<16, false>(a, st);
 }
 
 }  // namespace vm

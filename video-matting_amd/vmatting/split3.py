@@ -24,8 +24,8 @@ fused 2x2 pool), so activations never round-trip through f32 except where a resi
 conv3_4, conv2_3 feed the TF-1 resizes, which run in f32).  Layout: a split buffer holds slabs [l, h] of its S
 channels at p*S + c (S = the concat width, so the [up, skip] concats are channel ranges written by their own
 producers, as in split6.py); the convs read it as [l, h, h] (the kernel re-reads slab h for the third K range,
-ConvArgs::xalias), so h is stored once.  conv1_1's 7-channel frame is split into slabs of 16 (64 channels, the 4th slab zero:
-two whole 32-channel granules).  conv1_5 (cout 1) is two MFMA-head chunks [l | h] (256 channels) and [h] (128), the
+ConvArgs::xalias), so h is stored once.  conv1_1's 7-channel frame is split into three stored slabs of 8 (32 channels with a zero 4th
+slab: one whole 32-channel granule).  conv1_5 (cout 1) is two MFMA-head chunks [l | h] (256 channels) and [h] (128), the
 second adding the first's logits and undoing the filter scale before the sigmoid.
 """
 
@@ -39,7 +39,7 @@ W_PARTS = (0, 1, 0)  # index into (Wh, Wl)
 WTOP = 12  # filter scale: max |W * 2^t| in (2^11, 2^12]
 
 # (conv scope, channels of its split input (the concat width), output channels)
-LAYERS = (("conv1_1", 16, 64), ("conv1_2", 64, 64), ("conv2_1", 64, 128), ("conv2_2", 128, 128),
+LAYERS = (("conv1_1", 8, 64), ("conv1_2", 64, 64), ("conv2_1", 64, 128), ("conv2_2", 128, 128),
           ("conv3_1", 128, 256), ("conv3_2", 256, 256), ("conv3_3", 256, 256), ("conv4_1", 256, 512),
           ("conv4_2", 512, 512), ("conv4_3", 512, 512), ("conv5_1", 512, 512), ("conv5_2", 512, 512),
           ("upconv_1", 512, 512), ("conv4_4", 1024, 512), ("upconv_2", 512, 256), ("conv3_4", 512, 256),
@@ -225,7 +225,7 @@ class Split3Forward:
                 continue
             cp = cin
             if name == "conv1_1":
-                cp = 16  # slabs of 16 (8 live) + a zero 4th slab: 64 channels, two whole 32-channel granules
+                cp = 8  # slabs [l, h, h] of 8 (7 or 6 live) + a zero 4th slab: 32 channels, one whole granule
             if name in FOLD:  # one scale for the folded filter and the plain one (its border pass)
                 wu = fold_up2x(w)
                 t = min(t, filter_scale(wu))  # max |W' * 2^t| and max |W * 2^t| both <= 2^12
@@ -235,7 +235,7 @@ class Split3Forward:
                                                shift=np.zeros(cout, np.float32))
             wf = split3_filter(w, cp, cout, t)
             if name == "conv1_1":
-                wf = torch.cat([wf, torch.zeros((3, 3, 16, cout))], 2)
+                wf = torch.cat([wf, torch.zeros((3, 3, 8, cout))], 2)
             # epilogue (acc * 2^-t) + b: exact descale, then the bias (unet.py:41,73)
             self.convs[name] = ops.PackedConv(wf, None, "f16", self.dev, scale=np.full(cout, 1.0 / t, np.float32),
                                               shift=np.zeros(cout, np.float32) if b is None else b)
@@ -261,7 +261,7 @@ class Split3Forward:
         dev = self.dev
         S = lambda lv, c: torch.empty((n, L[lv][0], L[lv][1], 2 * c), dtype=torch.float16, device=dev)  # noqa
         F = lambda lv, c: torch.empty((n, L[lv][0], L[lv][1], c), dtype=torch.float32, device=dev)  # noqa
-        b = {"x": torch.zeros((n, L[0][0], L[0][1], 64), dtype=torch.float16, device=dev),
+        b = {"x": torch.zeros((n, L[0][0], L[0][1], 32), dtype=torch.float16, device=dev),
              "s11": S(0, 64), "cat1": S(0, 128), "r4": S(0, 128),
              "p1": S(1, 64), "s21": S(1, 128), "cat2": S(1, 256), "r3": S(1, 256),
              "p2": S(2, 128), "s31": S(2, 256), "s32": S(2, 256), "cat3": S(2, 512), "r2": S(2, 512),
@@ -286,7 +286,7 @@ class Split3Forward:
         C = self.convs
         ovf = self.overflow
         ovf.zero_()
-        split3h(x, b["x"][..., :8], slab=16, overflow=ovf)  # slabs [l, h, h] of 16 channels, 8 written
+        split3h(x, b["x"][..., :8], slab=8, overflow=ovf)  # slabs [l, h, h] of 8 channels (the 4th stays zero)
 
         def conv(src, name, dst_f32, act="relu", splitk=True):
             return conv_f32(src, C[name], dst_f32, act, splitk)
@@ -327,7 +327,7 @@ class Split3Forward:
         cs(b["r1"], "upconv_1", f3, seg(b["cat4"], 0, 512), act="none")
         fold = self.fold_up and self.fuse_split
 
-        def level(src_cat, conv_name, f_dst, s_name, lv, r_name, up_name, y):
+        def level(src_cat, conv_name, f_dst, s_name, lv, r_name, up_name, up_f32, y):
             """conv (relu) over the concat -> upconv (no bias, no relu) into the next concat's up range: the folded
             2x upconv on its split low-res output where the resize is an exact 2x, else f32 -> resize -> split ->
             conv (unet.py:192-200)"""
@@ -337,11 +337,11 @@ class Split3Forward:
             else:
                 f = conv(b[src_cat], conv_name, f_dst)
                 resize_split(f, lv, whole(b[r_name]))
-                cs(b[r_name], up_name, f_dst, y, act="none")
+                cs(b[r_name], up_name, up_f32, y, act="none")
 
-        level("cat4", "conv4_4", f3, "c44s", 2, "r2", "upconv_2", seg(b["cat3"], 0, 256))
-        level("cat3", "conv3_4", f2[..., :256], "c34s", 1, "r3", "upconv_3", seg(b["cat2"], 0, 128))
-        level("cat2", "conv2_3", f1[..., :128], "c23s", 0, "r4", "upconv_4", seg(b["cat1"], 0, 64))
+        level("cat4", "conv4_4", f3, "c44s", 2, "r2", "upconv_2", f2[..., :256], seg(b["cat3"], 0, 256))
+        level("cat3", "conv3_4", f2[..., :256], "c34s", 1, "r3", "upconv_3", f1[..., :128], seg(b["cat2"], 0, 128))
+        level("cat2", "conv2_3", f1[..., :128], "c23s", 0, "r4", "upconv_4", f0[..., :64], seg(b["cat1"], 0, 64))
         # conv1_5 + sigmoid (unet.py:203-205): [l | h] x [Wh | Wl], then [h] x [Wh] + those logits, * 2^-t + bias
         alpha = b["out"] if out is None else out
         lg0 = b["lg0"]
