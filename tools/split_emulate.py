@@ -12,9 +12,11 @@ the representation error of a scheme, before the f32 accumulation order every f3
   f16x3w   the filter scale only (activations unscaled: max |x| stays far below fp16's 65504 on this net)
   f16x3u   the same without scales
   bf16     y = bf16(x) * bf16(W)
+  f16x2a   x3 without l*Wh (the activation rounded to fp16), f16x2w without h*Wl (the filter rounded), f16 h*Wh only
 
     python tools/split_emulate.py --size 1080x1920 --scheme f16x3 bf16x3
     python tools/split_emulate.py --size 540x960 --scheme f16x3 --only conv1_2     # one layer split, the rest exact
+    python tools/split_emulate.py --scheme f16x2a --per-layer --rest f16x3         # per-layer sensitivity on x3
 """
 
 import argparse
@@ -73,13 +75,20 @@ def parts(x, w, scheme):
         xl, wl = _hf(xs - xh), _hf(ws - wh)
         assert torch.isfinite(xh).all() and torch.isfinite(wh).all()
         return [(xl, wh), (xh, wl), (xh, wh)], 1.0 / (s * t)
+    if scheme in ("f16x2a", "f16x2w", "f16"):  # x3 minus a cross term: the activation (a) or filter (w) fp16-rounded
+        t = _p2(w.abs().max().item(), WMAX)
+        ws = w * t
+        xh, wh = _hf(x), _hf(ws)
+        xl, wl = _hf(x - xh), _hf(ws - wh)
+        pr = {"f16x2a": [(xh, wl), (xh, wh)], "f16x2w": [(xl, wh), (xh, wh)], "f16": [(xh, wh)]}[scheme]
+        return pr, 1.0 / t
     raise ValueError(scheme)
 
 
 class Emu:
-    def __init__(self, params, scheme, only=None):
+    def __init__(self, params, scheme, only=None, rest="exact"):
         self.p = params
-        self.scheme, self.only = scheme, only
+        self.scheme, self.only, self.rest = scheme, only, rest
         self.amax = {}
 
     def conv(self, x, name, exact=False):
@@ -87,7 +96,7 @@ class Emu:
         w, b = self.p[name]
         wt = torch.from_numpy(np.asarray(w, np.float64)).permute(3, 2, 0, 1).contiguous()
         self.amax[name] = max(self.amax.get(name, 0.0), x.abs().max().item())
-        sch = "exact" if exact or (self.only is not None and name not in self.only) else self.scheme
+        sch = "exact" if exact else self.rest if (self.only is not None and name not in self.only) else self.scheme
         pr, sc = parts(x, wt, sch)
         y = None
         for xa, wa in pr:
@@ -140,22 +149,34 @@ def main():
     ap.add_argument("--scheme", nargs="+", default=["f16x3", "bf16x3"])
     ap.add_argument("--only", nargs="*", default=None, help="split only these convs (the rest exact)")
     ap.add_argument("--per-layer", action="store_true", help="one run per conv, that conv split, the rest exact")
+    ap.add_argument("--golden", default=None, help="a tests/golden case: its frame and weights (size ignored)")
+    ap.add_argument("--rest", default="exact", help="the scheme of the convs --only / --per-layer leave out")
     ap.add_argument("--threads", type=int, default=8)
     args = ap.parse_args()
     torch.set_num_threads(args.threads)
     h, w = map(int, args.size.split("x"))
-    np.random.seed(0)
-    params = om.unet_params(om.synthetic_vgg16(0), np.random.mtrand._rand, video=True)
-    x = frame(h, w).permute(0, 3, 1, 2).double().contiguous()
+    g = None
+    if args.golden:
+        g = np.load(os.path.join(os.path.dirname(__file__), "..", "tests", "golden", args.golden + ".npz"))
+        params = om.unet_params(om.synthetic_vgg16(0), np.random.RandomState(int(g["weight_seed"])),
+                                video=bool(g["video"]))
+        x = torch.from_numpy(np.asarray(g["x"], np.float64)).permute(0, 3, 1, 2).contiguous()
+    else:
+        np.random.seed(0)
+        params = om.unet_params(om.synthetic_vgg16(0), np.random.mtrand._rand, video=True)
+        x = frame(h, w).permute(0, 3, 1, 2).double().contiguous()
     t0 = time.time()
     ex = Emu(params, "exact").forward(x, exact=True)
     print("exact forward %.1f s; max |logit| %.4g" % (time.time() - t0, ex["logits"].abs().max().item()), flush=True)
+    if g is not None:
+        ga = torch.from_numpy(np.asarray(g["output"], np.float64)).permute(0, 3, 1, 2)
+        print("golden alpha vs exact: max-abs %.3e" % (ga - ex["alpha"]).abs().max().item(), flush=True)
     names = [n for n, _, _ in om.VGG_LAYERS[:12]] + [n for n, _, _, _ in om.UNET_NEW_CONVS]
     for sch in args.scheme:
         runs = [[n] for n in names] if args.per_layer else [args.only]
         for only in runs:
             t0 = time.time()
-            e = Emu(params, sch, only)
+            e = Emu(params, sch, only, args.rest)
             r = e.forward(x)
             da = (r["alpha"] - ex["alpha"]).abs().max().item()
             dl = (r["logits"] - ex["logits"]).abs().max().item() / ex["logits"].abs().max().item()

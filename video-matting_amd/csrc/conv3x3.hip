@@ -4426,6 +4426,125 @@ __global__ __launch_bounds__(256, TH <= 4 ? 4 : TH <= 8 ? 3 : 2) void conv3x3_th
   }
 }
 
+// ---------------------------------------------------------------- narrow-input convs (cin <= 16, cout <= 32)
+// UNetSmall's encoder and decoder convs (small.py:39-48: 6 -> 8, 8 -> 16, 16 -> 32, 16 -> 8) hold 8 or 16 channels per
+// pixel, so there is no 32-channel granule: K runs tap-major (k = tap * cin_pad + c, the generic packing) and one
+// MFMA K-step of 32 takes 4 (tap, 8-channel group) pieces, each a 16-byte LDS read of one patch pixel.  One 8 x 32
+// tile per block: its 10 x 34 patch in LDS (G pieces per pixel), the filter (NS K-steps x NT 16-channel tiles) in
+// registers.  Output lane l: pixel l % 16, channels 4 (l / 16) .. +3 of the tile.  The MFMAs chain k in ascending
+// 32-blocks and the epilogue is conv3x3_mfma's (fmaf form for bf16 outputs, (acc + b) * s + t for f32), so the
+// results are bit-identical to the generic kernel's (which spent a 256 x 64 tile and 64-K steps on these).
+template <int G, int NT>
+__global__ __launch_bounds__(256) void conv3x3_narrowin(ConvArgs a) {
+  constexpr int TH = 8, TW = 32, PW = TW + 2, PPIX = (TH + 2) * PW, PIECES = PPIX * G, PPT = (PIECES + 255) / 256;
+  constexpr int NQ = 9 * G, NS = (NQ + 3) / 4, RPW = TH / 4;
+  __shared__ uint4 xs[PIECES];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int tw = (a.W + TW - 1) / TW, th = (a.H + TH - 1) / TH;
+  int t = blockIdx.x;
+  const int tx = t % tw;
+  t /= tw;
+  const int ty = t % th, n = t / th;
+  const int r0 = ty * TH, c0 = tx * TW;
+  const uint16_t* Xn = reinterpret_cast<const uint16_t*>(a.x) + a.x_coff + (long)n * a.H * a.W * a.x_cstride;
+  const __amdgpu_buffer_rsrc_t xrs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(Xn), 0, 0x7ffffff0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.w), 0, 0x7ffffff0, 0x00020000);
+  uint4 xr[PPT], w[NT][NS];
+#pragma unroll
+  for (int i = 0; i < PPT; ++i) {  // patch pieces: pixel id / G, channel group id % G (out of frame: zeros)
+    const int id = tid + i * 256;
+    const int p = id / G, q = id - p * G;
+    const int pr = p / PW, pc = p - pr * PW;
+    const int yy = r0 - 1 + pr, xx = c0 - 1 + pc;
+    const bool ok = id < PIECES && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W;
+    xr[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
+                                          xrs, ok ? ((yy * a.W + xx) * a.x_cstride + q * 8) * 2 : OOB, 0, 0));
+  }
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt)  // A operand: output channel nt * 16 + lane % 16, k = 32 s + 8 (lane / 16) .. +7
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+      w[nt][s] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
+                                               wrs, ((nt * 16 + (lane & 15)) * a.K_pad + 32 * s + 8 * (lane >> 4)) * 2,
+                                               0, 0));
+#pragma unroll
+  for (int i = 0; i < PPT; ++i) {
+    const int id = tid + i * 256;
+    if (id < PIECES) xs[id] = xr[i];
+  }
+  __syncthreads();
+  f32x4 acc[NT][2 * RPW];
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+    for (int f = 0; f < 2 * RPW; ++f) acc[nt][f] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    const int q = 4 * s + (lane >> 4);
+    const bool kv = q < NQ;  // K padding past tap 8: zero pieces (the packed filter is zero there too)
+    const int tap = kv ? q / G : 0, g = q - (q / G) * G;
+    const int kh = tap / 3, kw = tap - kh * 3;
+#pragma unroll
+    for (int f = 0; f < 2 * RPW; ++f) {
+      const int pp = (wv * RPW + (f >> 1) + kh) * PW + (f & 1) * 16 + (lane & 15) + kw;
+      uint4 b = xs[pp * G + (kv ? g : 0)];
+      if (!kv) b = uint4{0u, 0u, 0u, 0u};
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) mma16<uint16_t>(w[nt][s], b, acc[nt][f]);
+    }
+  }
+  const bool f32o = a.y_dtype == VM_F32;
+  const bool fma_form = !f32o && a.y_vec && (a.cout & 7) == 0;  // conv3x3_mfma's fast bf16 epilogue, else its general one
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) {
+    const int co0 = nt * 16 + 4 * (lane >> 4);
+    if (co0 >= a.cout) continue;
+    float bs[4], sc[4], sh[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int co = min(co0 + j, a.cout - 1);
+      bs[j] = a.bias ? a.bias[co] : 0.f;
+      sc[j] = a.scale ? a.scale[co] : 1.f;
+      sh[j] = a.shift ? a.shift[co] : 0.f;
+    }
+    const bool full = co0 + 4 <= a.cout && a.y_vec;
+#pragma unroll
+    for (int f = 0; f < 2 * RPW; ++f) {
+      const int row = r0 + wv * RPW + (f >> 1), col = c0 + (f & 1) * 16 + (lane & 15);
+      if (row >= a.H || col >= a.W) continue;
+      const long o = (((long)n * a.H + row) * a.W + col) * a.y_cstride + a.y_coff + co0;
+      float v[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float tv = fma_form ? fmaf(acc[nt][f][j], sc[j], bs[j] * sc[j] + sh[j]) : (acc[nt][f][j] + bs[j]) * sc[j] + sh[j];
+        if (a.act == VM_ACT_RELU) tv = fma_form ? fmaxf(tv, 0.f) : (tv > 0.f ? tv : 0.f);
+        else if (a.act == VM_ACT_SIGMOID) tv = sigmoid_precise(tv);
+        v[j] = tv;
+      }
+      if (f32o) {
+        float* Y = reinterpret_cast<float*>(a.y) + o;
+        if (full) {
+          *reinterpret_cast<float4*>(Y) = make_float4(v[0], v[1], v[2], v[3]);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (co0 + j < a.cout) Y[j] = v[j];
+        }
+      } else {
+        uint16_t* Y = reinterpret_cast<uint16_t*>(a.y) + o;
+        if (full) {
+          *reinterpret_cast<uint2*>(Y) = uint2{bf16x2_bits(v[0], v[1]), bf16x2_bits(v[2], v[3])};
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (co0 + j < a.cout) Y[j] = f2bf(v[j]);
+        }
+      }
+    }
+  }
+}
+
 // LDS-DMA form of conv3x3_thin (r04).  The select convs are a stream over 192..1536-channel tower features (1.3 GB
 // per training step) and conv3x3_thin ran them at 1.1-2.8 TB/s: one chunk in flight per block, its patch and filter
 // held in registers from the end of one chunk's compute to the start of the next, so every chunk exposed most of
@@ -4809,6 +4928,25 @@ static bool thin_ok(int dt, const PackGeom& g, int cout, int x_src_c, int act, c
   return g_thin_kernel && dt == VM_BF16 && cout >= 2 && cout <= 16 && g.chunk_major && g.cin_pad % 32 == 0 &&
          (x_src_c <= 0 || x_src_c % 32 == 0) && act != VM_ACT_SOFTMAX &&
          (long)x->h * x->w * x->cstride * 2 < 0x7ffffff0L;  // 32-bit byte offsets inside one image
+}
+// narrow-input convs (conv3x3_narrowin): bf16, 8 or 16 tap-major input channels, <= 32 outputs, one source
+static long g_narrowin = 1;
+static bool narrowin_ok(const ConvArgs& a, const PackGeom& g, int cout, int act, const vm_tensor* x, const vm_tensor* y) {
+  return g_narrowin && !g.chunk_major && (g.cin_pad == 8 || g.cin_pad == 16) && cout <= 32 && a.x_src_c <= 0 &&
+         act != VM_ACT_SOFTMAX && (y->dtype == VM_F32 || y->dtype == VM_BF16) && g.K_pad >= 32 * ((9 * g.cin_pad / 8 + 3) / 4) &&
+         (long)x->h * x->w * x->cstride * 2 < 0x7ffffff0L;
+}
+static int launch_narrowin(ConvArgs& a, long n, const PackGeom& g, hipStream_t st) {
+  const long tiles = n * ((a.H + 7) / 8) * (long)((a.W + 31) / 32);
+  if (tiles > 0x7fffffffL) return fail(VM_EUNSUPPORTED, "conv3x3_narrowin: too many tiles");
+  const int G = g.cin_pad / 8, NT = a.cout > 16 ? 2 : 1;
+  snprintf(g_last_kernel, sizeof g_last_kernel, "vm::conv3x3_narrowin<%d, %d>", G, NT);
+  const dim3 grid((unsigned)tiles);
+  if (G == 1 && NT == 1) hipLaunchKernelGGL((conv3x3_narrowin<1, 1>), grid, dim3(256), 0, st, a);
+  else if (G == 1) hipLaunchKernelGGL((conv3x3_narrowin<1, 2>), grid, dim3(256), 0, st, a);
+  else if (NT == 1) hipLaunchKernelGGL((conv3x3_narrowin<2, 1>), grid, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((conv3x3_narrowin<2, 2>), grid, dim3(256), 0, st, a);
+  return check_launch("conv3x3_narrowin");
 }
 // split-K plan: below 1024 blocks of 8 x 32 pixels, split the 32-channel chunks over ~thin_blocks (512) blocks
 static long g_thin_th = 8, g_thin_blocks = 512;
@@ -5461,6 +5599,11 @@ extern "C" int vm_set_option(const char* key, long value) {
   if (!strcmp(key, "thin_dma_rounds")) {
     if (value < 1 || value > 64) return fail(VM_EINVAL, "thin_dma_rounds must be 1..64");
     g_thin_dma_rounds = value;
+    return VM_OK;
+  }
+  if (!strcmp(key, "narrowin_kernel")) {
+    if (value < 0 || value > 1) return fail(VM_EINVAL, "narrowin_kernel must be 0 or 1");
+    g_narrowin = value;
     return VM_OK;
   }
   if (!strcmp(key, "thin_kernel")) {
@@ -6211,6 +6354,7 @@ static int conv_impl(const vm_tensor* x, const void* packed, int cin, int cout, 
       return dispatch_patch(a, st);
     }
   }
+  if (dt == VM_BF16 && g_conv_kernel == 0 && narrowin_ok(a, g, cout, act, x, y)) return launch_narrowin(a, x->n, g, st);
   if (dt == VM_BF16) return dispatch_mfma<uint16_t>(a, st);
   return dispatch_mfma<float>(a, st, cin);
 }

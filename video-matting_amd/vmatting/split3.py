@@ -93,8 +93,9 @@ def fold_up2x(w_hwio):
     return out
 
 
-# upconvs whose resize is an exact 2x (unet.py:191-200 at 1080p: upconv_2..4; upconv_1's 68 -> 135 is not): the resize
-# folded into the filter (vm_conv3x3_up2x_split3_nhwc), zero phase taps skipped (25 of 36), no resized tensor
+# upconvs whose resize is an exact 2x (unet.py:191-200 at 1080p: upconv_2..4; upconv_1's 68 -> 135 is not): with
+# Split3Forward.fold_up the resize is folded into the filter (vm_conv3x3_up2x_split3_nhwc), zero phase taps skipped
+# (25 of 36), no resized tensor
 FOLD = ("upconv_2", "upconv_3", "upconv_4")
 
 
@@ -201,8 +202,12 @@ class Split3Forward:
 
     # conv -> split in the conv's epilogue (vm_conv3x3_split3_nhwc); False: f32 output + vm_split3h_nhwc (A/B)
     fuse_split = True
-    # the exact-2x upconvs on the folded filter (fuse_split only); False: resize -> split -> conv (A/B)
-    fold_up = True
+    # the exact-2x upconvs on the folded filter (fuse_split only) — measured slower here (1080p: upconv_2 / _3 / _4
+    # 1.49 / 1.06 / 0.92 ms folded with their split border pass, against 0.75 / 0.82 / 0.85 resized; the 12-step split
+    # border pass is latency-bound) and ~2x the f32 accumulation error (the 64x96 golden 1.4e-4): off, kept for A/B
+    fold_up = False
+    # conv1_1's input slab width: 8 (three slabs + a zero 4th in one 32-channel granule) or 32 (three granules, A/B)
+    first_slab = 8
 
     def __init__(self, model):
         self.m = model
@@ -225,7 +230,7 @@ class Split3Forward:
                 continue
             cp = cin
             if name == "conv1_1":
-                cp = 8  # slabs [l, h, h] of 8 (7 or 6 live) + a zero 4th slab: 32 channels, one whole granule
+                cp = self.first_slab  # slabs [l, h, h] of 8 (7 or 6 live) + a zero 4th slab: one whole granule
             if name in FOLD:  # one scale for the folded filter and the plain one (its border pass)
                 wu = fold_up2x(w)
                 t = min(t, filter_scale(wu))  # max |W' * 2^t| and max |W * 2^t| both <= 2^12
@@ -234,7 +239,7 @@ class Split3Forward:
                                                scale=np.full(cout, 1.0 / t, np.float32),
                                                shift=np.zeros(cout, np.float32))
             wf = split3_filter(w, cp, cout, t)
-            if name == "conv1_1":
+            if name == "conv1_1" and cp == 8:
                 wf = torch.cat([wf, torch.zeros((3, 3, 8, cout))], 2)
             # epilogue (acc * 2^-t) + b: exact descale, then the bias (unet.py:41,73)
             self.convs[name] = ops.PackedConv(wf, None, "f16", self.dev, scale=np.full(cout, 1.0 / t, np.float32),
@@ -261,7 +266,8 @@ class Split3Forward:
         dev = self.dev
         S = lambda lv, c: torch.empty((n, L[lv][0], L[lv][1], 2 * c), dtype=torch.float16, device=dev)  # noqa
         F = lambda lv, c: torch.empty((n, L[lv][0], L[lv][1], c), dtype=torch.float32, device=dev)  # noqa
-        b = {"x": torch.zeros((n, L[0][0], L[0][1], 32), dtype=torch.float16, device=dev),
+        fs = self.first_slab
+        b = {"x": torch.zeros((n, L[0][0], L[0][1], 32 if fs == 8 else 3 * fs), dtype=torch.float16, device=dev),
              "s11": S(0, 64), "cat1": S(0, 128), "r4": S(0, 128),
              "p1": S(1, 64), "s21": S(1, 128), "cat2": S(1, 256), "r3": S(1, 256),
              "p2": S(2, 128), "s31": S(2, 256), "s32": S(2, 256), "cat3": S(2, 512), "r2": S(2, 512),
@@ -286,7 +292,8 @@ class Split3Forward:
         C = self.convs
         ovf = self.overflow
         ovf.zero_()
-        split3h(x, b["x"][..., :8], slab=8, overflow=ovf)  # slabs [l, h, h] of 8 channels (the 4th stays zero)
+        fs = self.first_slab
+        split3h(x, b["x"][..., :fs], slab=fs, overflow=ovf)  # slabs [l, h, h] of fs channels (a 4th stays zero)
 
         def conv(src, name, dst_f32, act="relu", splitk=True):
             return conv_f32(src, C[name], dst_f32, act, splitk)
