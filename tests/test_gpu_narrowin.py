@@ -91,3 +91,27 @@ def test_narrowin_conv_into_concat_view():
     assert torch.all(cats[0][..., :8] == 5.0)
     want = _ref(x.float().cpu().numpy(), wt, 0.0, "relu")
     assert np.abs(cats[0][..., 8:].float().cpu().numpy() - want).max() <= 2 ** -8 * np.abs(want).max() + 1e-6
+
+
+@pytest.mark.parametrize("ngroup", [2, 4])
+def test_patch_grouped_tile_order_bit_identical(ngroup):
+    """ConvArgs::ngroup (the patch kernel's grouped output-tile order) only reorders the blocks: the bf16 UNetVideo
+    forward equals the default order's bit for bit, with the grouping forced onto every patch launch."""
+    from oracle.models import synthetic_vgg16
+    from vmatting import _lib, unet
+    rs = np.random.RandomState(1)
+    x = rs.uniform(-100, 100, (1, 72, 100, 7)).astype(np.float32)
+    outs = []
+    for ng, cb in ((0, 4 << 20), (ngroup, 0)):
+        _lib.set_option("ngroup", ng)
+        _lib.set_option("cband_bytes", cb)
+        try:
+            np.random.seed(0)
+            m = unet.UNetVideo(synthetic_vgg16(0), dtype="bf16")
+            m.build(x)
+            torch.cuda.synchronize()
+            outs.append(m.conv1_3.float().clone())
+        finally:
+            _lib.set_option("ngroup", 0)
+            _lib.set_option("cband_bytes", 4 << 20)
+    assert torch.equal(outs[0], outs[1])

@@ -18,7 +18,13 @@ VARIANTS = {
     "nosplit": {"split_head": False},
     "noskip": {"_opt": {"up_skip": 0}},  # folded upconvs without the zero-tap skipping
     "fold_up2_noskip": {"fold_upconv": ("upconv_2", "upconv_3", "upconv_4"), "_opt": {"up_skip": 0}},
+    # r06: grouped patch tile order (ConvArgs::ngroup) for filters >= cband_bytes
+    "ng2": {"_opt": {"ngroup": 2}},
+    "ng4": {"_opt": {"ngroup": 4}},
+    "ng8": {"_opt": {"ngroup": 8}},
+    "ng4_1m": {"_opt": {"ngroup": 4, "cband_bytes": 1 << 20}},
 }
+DEFAULT_OPT = {"up_skip": 1, "cband_bytes": 4 << 20}
 
 
 def run(name, steps=100):
@@ -42,7 +48,7 @@ def run(name, steps=100):
     torch.cuda.synchronize()
     ms = 1000 * (time.perf_counter() - t0) / steps
     for k in opts:
-        _lib.set_option(k, {"up_skip": 1}.get(k, 0))
+        _lib.set_option(k, DEFAULT_OPT.get(k, 0))
     return ms
 
 

@@ -18,7 +18,7 @@ from oracle import models as om  # noqa: E402
 from vmatting import _lib, split3, unet  # noqa: E402
 
 
-def run(case, dtype, opts=(), first_slab=8):
+def run(case, dtype, opts=(), first_slab=32):
     g = golden(case)
     cls = unet.UNetVideo if int(g["video"]) else unet.UNetImage
     for k, v in opts:
@@ -32,7 +32,7 @@ def run(case, dtype, opts=(), first_slab=8):
         a = m.output.float().cpu().numpy()
         lg = m.conv1_3.float().cpu().numpy()
     finally:
-        split3.Split3Forward.first_slab = 8
+        split3.Split3Forward.first_slab = 32
     da = np.abs(a - g["output"])
     dl = np.abs(lg - g["logits"])
     i = np.unravel_index(np.argmax(da), da.shape)
@@ -41,10 +41,10 @@ def run(case, dtype, opts=(), first_slab=8):
 
 def main():
     cases = sys.argv[1:] or ["unet_video_64x96", "unet_image_70x90"]
-    variants = [("fp32", "fp32", (), 8), ("bf16x6", "bf16x6", (), 8), ("f16x3", "f16x3", (), 8),
-                ("f16x3 rows off", "f16x3", (("rows_kernel", 0),), 8),
-                ("f16x3 slab32", "f16x3", (), 32),
-                ("f16x3 rows off slab32", "f16x3", (("rows_kernel", 0),), 32)]
+    variants = [("fp32", "fp32", (), 32), ("bf16x6", "bf16x6", (), 32), ("f16x3", "f16x3", (), 32),
+                ("f16x3 rows off", "f16x3", (("rows_kernel", 0),), 32),
+                ("f16x3 slab8", "f16x3", (), 8),
+                ("f16x3 rows off slab8", "f16x3", (("rows_kernel", 0),), 8)]
     for case in cases:
         for name, dt, opts, fs in variants:
             try:

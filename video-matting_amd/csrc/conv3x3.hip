@@ -749,6 +749,11 @@ void conv3x3_patch(ConvArgs a) {
     const int i = blockIdx.x >> 3;
     st = i / a.cband;
     nt = (blockIdx.x & 7) * a.cband + (i - st * a.cband);
+  } else if (a.ngroup) {  // grouped: ngroup output tiles x every pixel tile, group after group (XCD ranges within)
+    const int t = xcd_tile(blockIdx.x, a.tiles_total);
+    const int per = (a.tiles_total / a.tiles_n) * a.ngroup, gi = t / per, r = t - gi * per;
+    st = r / a.ngroup;
+    nt = gi * a.ngroup + (r - st * a.ngroup);
   } else {
     const int t = xcd_tile(blockIdx.x, a.tiles_total);
     st = t / a.tiles_n;
@@ -4780,6 +4785,9 @@ static long g_patch_repi = 1;  // patch kernel: register epilogue (bf16 outputs,
 // every XCD then reads the whole input from the Infinity Cache, which costs more than the weight stream it saves
 static long g_cband = 0;
 static long g_cband_bytes = 4L << 20;   // ... for filters of at least this many bytes (an XCD's L2)
+// grouped tile order (ConvArgs::ngroup): this many output tiles per group for filters of >= cband_bytes (0: off) —
+// the XCD working set is ngroup filter slices instead of the whole filter; the input is read tiles_n / ngroup times
+static long g_ngroup = 0;
 
 template <int BN, int WM, int WN, int S, int TH = 8, int MINB = 1, int UNR = 9, bool PF = false, int ABL = 0,
           bool FIRST = false, int G = 1, bool UPSKIP = false>
@@ -4815,6 +4823,8 @@ static int launch_patch(ConvArgs& a, hipStream_t st) {
   const long wbytes = (long)a.cout_pad * a.K_pad * 2;
   a.cband = (g_cband >= (a.up ? 1 : 2)) && !FIRST && BN == 64 && a.tiles_n % 8 == 0 && wbytes >= g_cband_bytes
                 ? a.tiles_n / 8 : 0;
+  a.ngroup = !a.cband && g_ngroup > 0 && a.tiles_n > g_ngroup && a.tiles_n % g_ngroup == 0 && wbytes >= g_cband_bytes
+                 ? (int)g_ngroup : 0;
   snprintf(g_last_kernel, sizeof g_last_kernel, "vm::conv3x3_patch<%d, %d, %d, %d, %d, %d, %d, %s, %d, %s, %d, %s%s>",
            BN, WM, WN, S, TH, MINB, UNR, PF ? "true" : "false", ABL, FIRST ? "true" : "false", G,
            UPSKIP ? "true" : "false", f16 ? ", vm::f16_t" : "");
@@ -5516,6 +5526,11 @@ extern "C" int vm_set_option(const char* key, long value) {
   if (!strcmp(key, "cband")) {
     if (value < 0 || value > 2) return fail(VM_EINVAL, "cband must be 0, 1 or 2");
     g_cband = value;
+    return VM_OK;
+  }
+  if (!strcmp(key, "ngroup")) {
+    if (value < 0 || value > 64) return fail(VM_EINVAL, "ngroup must be 0..64");
+    g_ngroup = value;
     return VM_OK;
   }
   if (!strcmp(key, "cband_bytes")) {

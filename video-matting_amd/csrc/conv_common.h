@@ -54,6 +54,7 @@ struct ConvArgs {
   // (b >> 3) / cband, so XCD b % 8 keeps its cband 64-channel weight slices L2-resident over every pixel tile (weight-
   // heavy layers: upconv_2's 9.4 MB folded filter, which the pixel-banded order re-streams per resident round)
   int cband;
+  int ngroup;  // patch kernel: output-channel tiles per group of the tile order (0: all of a pixel tile's together)
   int twalk;  // conv3x3_thin: XCD-banded tile walk
   int seg;    // conv3x3_first_softmax_f32r: rows per wave segment
   int prio;  // 1: waves 4..7 of an 8-wave block run at s_setprio 1 (static priority for the arbitration loser)

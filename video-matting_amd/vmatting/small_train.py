@@ -98,14 +98,14 @@ class SmallTrainer(TrainerBase):
                 self.convs[name] = ops.PackedConv.from_source(w, w.shape[2], co, self.dtype, bias=bias)
         self._refresh_bias()
         # data-gradient convs: flipped / transposed filters; bf16 packs take the gradient's bf16 copy with its
-        # channels zero-padded to 32 (the patch-reuse kernel's granule)
+        # channels zero-padded to 8 or 16 (conv3x3_narrowin's tap-major pieces), wider ones to 32 (the granule)
         self.dconv = {}
         for name in DGRAD:
             w = self.P[name, "w"]
             ci, co = int(w.shape[2]), int(w.shape[3])
             if bf16:
-                self.dconv[name] = ops.PackedConv.from_source(w, (co + 31) // 32 * 32, (ci + 3) // 4 * 4, "bf16",
-                                                              flip=True)
+                cg = (co + 7) // 8 * 8 if co <= 16 else (co + 31) // 32 * 32
+                self.dconv[name] = ops.PackedConv.from_source(w, cg, (ci + 3) // 4 * 4, "bf16", flip=True)
             else:
                 self.dconv[name] = ops.PackedConv.from_source(w, co, ci, "fp32", flip=True)
         self._repack = ops.PackBatch(list(self.convs.values()) + list(self.dconv.values()))

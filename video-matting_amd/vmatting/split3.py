@@ -24,8 +24,8 @@ fused 2x2 pool), so activations never round-trip through f32 except where a resi
 conv3_4, conv2_3 feed the TF-1 resizes, which run in f32).  Layout: a split buffer holds slabs [l, h] of its S
 channels at p*S + c (S = the concat width, so the [up, skip] concats are channel ranges written by their own
 producers, as in split6.py); the convs read it as [l, h, h] (the kernel re-reads slab h for the third K range,
-ConvArgs::xalias), so h is stored once.  conv1_1's 7-channel frame is split into three stored slabs of 8 (32 channels with a zero 4th
-slab: one whole 32-channel granule).  conv1_5 (cout 1) is two MFMA-head chunks [l | h] (256 channels) and [h] (128), the
+ConvArgs::xalias), so h is stored once.  conv1_1's 7-channel frame is split into three stored slabs of 32 (one granule each;
+Split3Forward.first_slab).  conv1_5 (cout 1) is two MFMA-head chunks [l | h] (256 channels) and [h] (128), the
 second adding the first's logits and undoing the filter scale before the sigmoid.
 """
 
@@ -206,8 +206,10 @@ class Split3Forward:
     # 1.49 / 1.06 / 0.92 ms folded with their split border pass, against 0.75 / 0.82 / 0.85 resized; the 12-step split
     # border pass is latency-bound) and ~2x the f32 accumulation error (the 64x96 golden 1.4e-4): off, kept for A/B
     fold_up = False
-    # conv1_1's input slab width: 8 (three slabs + a zero 4th in one 32-channel granule) or 32 (three granules, A/B)
-    first_slab = 8
+    # conv1_1's input slab width: 32 (three granules: the l*Wh and h*Wl sums run before h*Wh joins them) or 8 (three
+    # slabs + a zero 4th in ONE granule, 0.03 ms faster at 1080p, but every MFMA mixes the small and the large products:
+    # the 64x96 golden's alpha 1.01e-4 against 7.8e-5 with 32, fp32 4.1e-5 — tools/x3_golden_study.py)
+    first_slab = 32
 
     def __init__(self, model):
         self.m = model
