@@ -1325,6 +1325,8 @@ def main():
                     help="profiling passes: run just this record (rank 0 / N=1) and print it")
     ap.add_argument("--temporal-sizes", default="500x1200,1080x1920", help="config-3 sizes HxW, comma separated")
     ap.add_argument("--temporal-dtypes", default="fp32,bf16", help="config-3 compute dtypes, comma separated")
+    ap.add_argument("--cooldown", type=float, default=5.0,
+                    help="seconds of GPU idle before each training record (outside the timed regions)")
     ap.add_argument("--dummy-streams", type=int, default=0,
                     help="(study) create this many idle HIP streams first: how the trainers' side streams map onto "
                          "the hardware queues when a process already holds streams")
@@ -1451,17 +1453,29 @@ def main():
     if args.video_frames > 0:
         vrec = video_batch(model, args.video_frames, H, W, rank, world, dev, args.video_chunk)
 
+    # each training / config-3 / loader / augment record starts from an idle GPU: measured (tools/img_interference.py, profiles/r06i_img_
+    # interference.log), the UNetImage step right after another heavy record runs 6.70 ms against 6.03 after a 5 s
+    # pause or alone (the card's clock / power state, not the code); the pause is outside every timed region
+    def cool():
+        if args.cooldown > 0:
+            torch.cuda.synchronize()
+            time.sleep(args.cooldown)
+
     train = None
     if not args.no_train:  # every rank: the DDP all-reduce is part of the step
+        cool()
         train = train_bench(dev, max(args.steps // 4, 10), 3, world, rank, threads, cpu=not args.no_cpu_baseline,
                             graph=args.train_graph, streams=args.train_streams,
                             wgrad_stream=bool(args.train_wgrad_stream))
         if world == 1:
+            cool()
             train["chained"] = chain_roofline_and_baseline(
                 train_chain_bench(dev, 5, 2, graph=args.train_graph, overlap=not args.chain_serial,
                                   prio=args.chain_prio), 8, 320, 1080, 1920, "bf16", threads, not args.no_cpu_baseline)
+        cool()
         train_small = train_small_bench(dev, max(args.steps // 4, 10), 3, world, rank, threads,
                                         cpu=not args.no_cpu_baseline)
+        cool()
         train_image = train_image_bench(dev, max(args.steps // 4, 10), 5, world, rank, threads,
                                         cpu=not args.no_cpu_baseline, graph=args.image_graph,
                                         streams=args.image_streams)
@@ -1535,14 +1549,19 @@ def main():
         if vrec:
             rec["video_batch"] = vrec
         if world == 1 and not args.no_temporal:
+            cool()
             rec["temporal"] = temporal_bench(dev, 20, t_dtypes, t_sizes, not args.no_cpu_baseline, threads)
         if train:
             rec["train"] = train
             rec["train_small"] = train_small
             rec["train_image"] = train_image
+            for r in (train, train_small, train_image):
+                r["idle_before_s"] = args.cooldown
         if world == 1 and not args.no_loader:
+            cool()
             rec["loader"] = loader_bench(dev, max(args.steps // 4, 10), threads, cpu=not args.no_cpu_baseline)
         if world == 1 and not args.no_augment:
+            cool()
             rec["augment"] = augment_bench(dev, max(args.steps // 4, 10), threads, cpu=not args.no_cpu_baseline)
         print(json.dumps(rec), flush=True)
     if world > 1:
