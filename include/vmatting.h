@@ -168,7 +168,8 @@ int vm_conv3x3_head_acc_nhwc(const vm_tensor* x, const void* packed, int cin, co
                              vm_tensor* y, float* alpha, void* stream);
 /* The same with the per-channel affine of vm_conv3x3_nhwc: pre-activation = (conv + y_acc + bias) * scale + shift
  * (y_acc may be NULL) — the split-fp16 x3 path's conv1_5, whose fp16 filter parts are pre-scaled by a power of two
- * that the last chunk's scale undoes (exactly) before the sigmoid (unet.py:203-205).  x may be VM_F16 (cin <= 256). */
+ * that the last chunk's scale undoes (exactly) before the sigmoid (unet.py:203-205).  x may be VM_F16 (cin <= 256), or a two-slab
+ * split-fp16 view [l, h] of 128-channel slabs with cin 384 (read as [l, h, h]; conv1_5 of the f16x3 forward). */
 int vm_conv3x3_head_acc_ex_nhwc(const vm_tensor* x, const void* packed, int cin, const float* bias, const float* scale,
                                 const float* shift, const float* y_acc, vm_tensor* y, float* alpha, void* stream);
 

@@ -234,3 +234,25 @@ def test_unet_f16x3_1080p_timed_frame_vs_oracle():
     print("1080p f16x3 alpha max-abs vs oracle %.3e, logits rel %.3e" % (err, lrel))
     assert err <= 1e-4
     assert lrel <= 1e-5
+
+
+def test_f16x3_fused_head_matches_two_chunk_head(vgg0):
+    """conv1_5 in one aliased 12-step MFMA-head call (Split3Forward.head_fused) against the two-call form ([l | h] x
+    [Wh | Wl], then [h] x [Wh] adding the first's logits): the same products in another f32 summation order — logits
+    within 1e-6 of their max (a 1e-3 logit near alpha 0.5 moves it 2.5e-4; measured 4.7e-6), alpha within 2e-5."""
+    from vmatting import split3, unet
+    x = torch.from_numpy(np.random.RandomState(5).uniform(-120, 120, (1, 72, 100, 7)).astype(np.float32)).to(DEV)
+    outs = []
+    for fused in (True, False):
+        split3.Split3Forward.head_fused = fused
+        try:
+            np.random.seed(0)
+            m = unet.UNetVideo(vgg0, dtype="f16x3")
+            m.build(x)
+            torch.cuda.synchronize()
+            outs.append((H(m.output), H(m.conv1_3)))
+        finally:
+            split3.Split3Forward.head_fused = True
+    (a0, l0), (a1, l1) = outs
+    assert np.abs(l0 - l1).max() <= 1e-6 * np.abs(l1).max()
+    assert np.abs(a0 - a1).max() <= 2e-5

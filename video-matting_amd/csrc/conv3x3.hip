@@ -3653,7 +3653,10 @@ __global__ __launch_bounds__(256) void conv3x3_head_strip(HeadArgs a) {
 // Y[p][t] = sum_c X[p][c] * W[t][c] for every pixel p of the (TH+2) x (TW+2) input window (MFMA: 16 pixels x
 // 16 tap-columns, 9 used), parks Y in LDS, then out(r,c) = sum_t Y[(r+dh_t, c+dw_t)][t].  Every input pixel is
 // read once per tile (plus the halo) straight into MFMA A-fragments; no 3x3 re-reads, no VALU dot products.
-template <typename T, int TH, int TW, int NKS>
+// ALIAS (split-fp16 x3, vmatting/split3.py): x holds two slabs [l, h] of S = cin / 3 channels and the filter runs over
+// [l, h, h] (cin = 3S): the k-steps of the third range reuse the second range's fragments (no extra loads), so one
+// call does conv1_5's three products, the small ones first in each tap's chain
+template <typename T, int TH, int TW, int NKS, bool ALIAS = false>
 __global__ __launch_bounds__(256) void conv3x3_head_mfma(HeadArgs a) {
   constexpr int CE = 16 / sizeof(T);
   constexpr int KS = 4 * CE;  // channels per MFMA k-step
@@ -3721,6 +3724,7 @@ __global__ __launch_bounds__(256) void conv3x3_head_mfma(HeadArgs a) {
       const int pix = (lr * W + ww) * cs;
 #pragma unroll
       for (int s = 0; s < NKS; ++s) {
+        if (ALIAS && s >= 2 * (NKS / 3)) break;  // the third range: the second's fragments
         const int c = s * KS + ks * CE;
         const int off = (ok && c < cin) ? (pix + c) * (int)sizeof(T) : OOB;
         xa[u][s] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
@@ -3732,7 +3736,8 @@ __global__ __launch_bounds__(256) void conv3x3_head_mfma(HeadArgs a) {
       if (g0 + u >= NG) break;
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int s = 0; s < NKS; ++s) mma16<T>(xa[u][s], wf[s], acc);
+      for (int s = 0; s < NKS; ++s)
+        mma16<T>(ALIAS && s >= 2 * (NKS / 3) ? xa[u][s - NKS / 3] : xa[u][s], wf[s], acc);
       if (col < 9) {
         const int p = (g0 + u) * 16 + 4 * ks;
 #pragma unroll
@@ -6238,9 +6243,20 @@ static int conv_impl(const vm_tensor* x, const void* packed, int cin, int cout, 
     h.y = y->ptr; h.y_cstride = y->cstride; h.y_coff = y->coff; h.y_dtype = y->dtype; h.y2 = y2;
     h.part = head_part;
     h.yacc = y_acc;
-    if ((head_part || y_acc || f16) && (g_head_kernel != 0 || (g.cin_pad + 4 * ce - 1) / (4 * ce) > 8))
-      return fail(VM_EUNSUPPORTED, "conv3x3 head: partials / accumulation / fp16 need the MFMA head kernel (cin <= 256)");
     const int nks = (g.cin_pad + 4 * ce - 1) / (4 * ce);
+    // the split-fp16 x3 head over a two-slab [l, h] view of 128-channel slabs (cin 384 as [l, h, h]): one call
+    if (f16 && xalias == 128 && nks == 12 && g_head_kernel == 0) {
+      constexpr int TW = 64;
+      const long tiles = (long)x->n * ((x->h + 7) / 8) * ((x->w + TW - 1) / TW);
+      if (tiles > 0x7fffffffL) return fail(VM_EUNSUPPORTED, "conv3x3 head: too many tiles");
+      snprintf(g_last_kernel, sizeof g_last_kernel, "vm::conv3x3_head_mfma<vm::f16_t, 8, %d, 12, true>", TW);
+      hipLaunchKernelGGL((conv3x3_head_mfma<f16_t, 8, TW, 12, true>), dim3(tiles), dim3(256),
+                         (size_t)9 * g.cin_pad * 2, st, h);
+      return check_launch("conv3x3_head_mfma");
+    }
+    if ((head_part || y_acc || f16) && (g_head_kernel != 0 || nks > 8))
+      return fail(VM_EUNSUPPORTED, "conv3x3 head: partials / accumulation / fp16 need the MFMA head kernel (cin <= 256, "
+                                   "or 384 as a two-slab split-fp16 view)");
     if (g_head_kernel == 0 && nks <= 8) {
       constexpr int TW = 64;
       // 16-row tiles for the bf16 128-channel head (cat1 of UNetVideo): input window 18 x 66 per 16 x 64 outputs

@@ -783,17 +783,19 @@ __device__ __forceinline__ bool store_split3h(uint16_t* base, long S, const floa
 }
 
 // one thread = one 8-channel chunk of one output pixel (POOL: of one pooled pixel and the 2x2 window under it)
-template <bool POOL>
+// I: the index type (int when the work fits: 32-bit divisions instead of 64-bit ones, which cost more than the
+// element's loads and stores)
+template <bool POOL, typename I>
 __global__ __launch_bounds__(256) void split3h_kernel(View x, View y, View yp, long S, long Sp, int* overflow) {
   const int cpp = (y.c + 7) / 8;
   const int on = POOL ? yp.n : y.n, oh = POOL ? yp.h : y.h, ow = POOL ? yp.w : y.w;
-  const long total = (long)on * oh * ow * cpp;
+  const I total = (I)on * oh * ow * cpp;
   bool ovf = false;
   const bool vec = ((x.cs | x.coff) & 3) == 0 && (reinterpret_cast<uintptr_t>(x.p) & 15) == 0;
   const bool y3 = 3 * S <= y.cs;  // the third slab [h again] where the pixel row holds it (else [l, h] only)
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+  for (I i = blockIdx.x * (I)blockDim.x + threadIdx.x; i < total; i += (I)gridDim.x * blockDim.x) {
     const int cc = (int)(i % cpp);
-    const long op = i / cpp;
+    const long op = (long)(i / cpp);
     const int c = cc * 8;
     auto load = [&](long pix, float* f) {
       const float* src = reinterpret_cast<const float*>(x.p) + pix * x.cs + x.coff + c;
@@ -847,19 +849,19 @@ __device__ __forceinline__ void ld8f(const View& x, long pix, int c, float* f) {
   f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w; f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
 }
 
-template <bool TWO>
+template <bool TWO, typename I>
 __global__ __launch_bounds__(256) void resize_split3h_kernel(View x, View y, long S, float sy, float sx,
                                                              int* overflow) {
   const int cpp = y.c / 8;
   const bool y3 = 3 * S <= y.cs;
   const int oh_n = TWO ? x.h : y.h, ow_n = TWO ? x.w : y.w;
-  const long total = (long)y.n * oh_n * ow_n * cpp;
+  const I total = (I)y.n * oh_n * ow_n * cpp;
   bool ovf = false;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+  for (I i = blockIdx.x * (I)blockDim.x + threadIdx.x; i < total; i += (I)gridDim.x * blockDim.x) {
     const int cc = (int)(i % cpp);
-    const long op = i / cpp;
+    const I op = i / cpp;
     const int ow = (int)(op % ow_n);
-    const long t = op / ow_n;
+    const I t = op / ow_n;
     const int oh = (int)(t % oh_n), n = (int)(t / oh_n);
     const int c = cc * 8;
     const long rb = (long)n * x.h;
@@ -915,7 +917,7 @@ __global__ __launch_bounds__(256) void resize_split3h_kernel(View x, View y, lon
         const float bot = bl[e] + (br[e] - bl[e]) * xl;
         o[e] = top + (bot - top) * yl;
       }
-      uint16_t* yo = reinterpret_cast<uint16_t*>(y.p) + op * y.cs + y.coff + c;
+      uint16_t* yo = reinterpret_cast<uint16_t*>(y.p) + (long)op * y.cs + y.coff + c;
       ovf |= store_split3h(yo, S, o, y3);
     }
   }
@@ -942,12 +944,19 @@ extern "C" int vm_split3h_nhwc(const vm_tensor* x, vm_tensor* y, vm_tensor* y_po
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const vm_tensor* o = y_pool ? y_pool : y;
   const long work = (long)o->n * o->h * o->w * ((y->c + 7) / 8);
-  if (y_pool)
-    hipLaunchKernelGGL(split3h_kernel<true>, dim3(grid_for(work, 256)), dim3(256), 0, st, view(x), view(y),
+  const bool i32 = work + 256L * 4096 < 0x7fffffffL;  // (the grid-stride index stays below 2^31)
+  if (y_pool && i32)
+    hipLaunchKernelGGL((split3h_kernel<true, int>), dim3(grid_for(work, 256)), dim3(256), 0, st, view(x), view(y),
                        view(y_pool), S, Sp, overflow);
+  else if (y_pool)
+    hipLaunchKernelGGL((split3h_kernel<true, long>), dim3(grid_for(work, 256)), dim3(256), 0, st, view(x), view(y),
+                       view(y_pool), S, Sp, overflow);
+  else if (i32)
+    hipLaunchKernelGGL((split3h_kernel<false, int>), dim3(grid_for(work, 256)), dim3(256), 0, st, view(x), view(y),
+                       view(y), S, Sp, overflow);
   else
-    hipLaunchKernelGGL(split3h_kernel<false>, dim3(grid_for(work, 256)), dim3(256), 0, st, view(x), view(y), view(y),
-                       S, Sp, overflow);
+    hipLaunchKernelGGL((split3h_kernel<false, long>), dim3(grid_for(work, 256)), dim3(256), 0, st, view(x), view(y),
+                       view(y), S, Sp, overflow);
   return check_launch("split3h");
 }
 
@@ -964,12 +973,19 @@ extern "C" int vm_resize_split3h_nhwc(const vm_tensor* x, vm_tensor* y, int slab
   const bool two = y->h == 2 * x->h && y->w == 2 * x->w;
   const long work = (long)y->n * (two ? (long)x->h * x->w : (long)y->h * y->w) * (y->c / 8);
   const float sy = (float)x->h / (float)y->h, sx = (float)x->w / (float)y->w;
-  if (two)
-    hipLaunchKernelGGL(resize_split3h_kernel<true>, dim3(grid_for(work, 256)), dim3(256), 0, st, view(x), view(y), S,
-                       sy, sx, overflow);
+  const bool i32 = work + 256L * 4096 < 0x7fffffffL;
+  const dim3 grid(grid_for(work, 256));
+  if (two && i32)
+    hipLaunchKernelGGL((resize_split3h_kernel<true, int>), grid, dim3(256), 0, st, view(x), view(y), S, sy, sx, overflow);
+  else if (two)
+    hipLaunchKernelGGL((resize_split3h_kernel<true, long>), grid, dim3(256), 0, st, view(x), view(y), S, sy, sx,
+                       overflow);
+  else if (i32)
+    hipLaunchKernelGGL((resize_split3h_kernel<false, int>), grid, dim3(256), 0, st, view(x), view(y), S, sy, sx,
+                       overflow);
   else
-    hipLaunchKernelGGL(resize_split3h_kernel<false>, dim3(grid_for(work, 256)), dim3(256), 0, st, view(x), view(y), S,
-                       sy, sx, overflow);
+    hipLaunchKernelGGL((resize_split3h_kernel<false, long>), grid, dim3(256), 0, st, view(x), view(y), S, sy, sx,
+                       overflow);
   return check_launch("resize_split3h");
 }
 

@@ -24,9 +24,9 @@ fused 2x2 pool), so activations never round-trip through f32 except where a resi
 conv3_4, conv2_3 feed the TF-1 resizes, which run in f32).  Layout: a split buffer holds slabs [l, h] of its S
 channels at p*S + c (S = the concat width, so the [up, skip] concats are channel ranges written by their own
 producers, as in split6.py); the convs read it as [l, h, h] (the kernel re-reads slab h for the third K range,
-ConvArgs::xalias), so h is stored once.  conv1_1's 7-channel frame is split into three stored slabs of 32 (one granule each;
-Split3Forward.first_slab).  conv1_5 (cout 1) is two MFMA-head chunks [l | h] (256 channels) and [h] (128), the
-second adding the first's logits and undoing the filter scale before the sigmoid.
+ConvArgs::xalias), so h is stored once.  conv1_1's 7-channel frame is split into two stored slabs [l, h] of 32 channels, read as
+[l, h, h] (Split3Forward.first_slab).  conv1_5 (cout 1) is one MFMA-head call over cat1's [l, h] read as [l, h, h] (12 k-steps, the third
+range's fragments reused), undoing the filter scale before the sigmoid (Split3Forward.head_fused).
 """
 
 import numpy as np
@@ -210,6 +210,9 @@ class Split3Forward:
     # slabs + a zero 4th in ONE granule, 0.03 ms faster at 1080p, but every MFMA mixes the small and the large products:
     # the 64x96 golden's alpha 1.01e-4 against 7.8e-5 with 32, fp32 4.1e-5 — tools/x3_golden_study.py)
     first_slab = 32
+    # conv1_5 in one MFMA-head call over cat1's [l, h] read as [l, h, h] (12 k-steps, the third range's fragments
+    # reused); False: two calls, [l | h] x [Wh | Wl] then [h] x [Wh] adding the first's logits (A/B)
+    head_fused = True
 
     def __init__(self, model):
         self.m = model
@@ -222,8 +225,13 @@ class Split3Forward:
             t = filter_scale(w)
             self.scales[name] = t
             if name == "conv1_5":
-                # [l | h] against [Wh | Wl] (256 channels), then [h] against [Wh] adding the first chunk's logits
                 wf = split3_filter(w, cin, 1, t)
+                if self.head_fused:  # [l, h, h] x [Wh, Wl, Wh], descaled + bias in the epilogue
+                    self.head = [ops.PackedConv(wf, None, "f16", self.dev, scale=np.full(1, 1.0 / t, np.float32),
+                                                shift=np.zeros(1, np.float32) if b is None else b)]
+                    self.convs[name] = self.head[0]
+                    continue
+                # [l | h] against [Wh | Wl] (256 channels), then [h] against [Wh] adding the first chunk's logits
                 self.head = [ops.PackedConv(wf[:, :, :256].contiguous(), None, "f16", self.dev),
                              ops.PackedConv(wf[:, :, 256:].contiguous(), None, "f16", self.dev,
                                             scale=np.full(1, 1.0 / t, np.float32),
@@ -232,7 +240,7 @@ class Split3Forward:
                 continue
             cp = cin
             if name == "conv1_1":
-                cp = self.first_slab  # slabs [l, h, h] of 8 (7 or 6 live) + a zero 4th slab: one whole granule
+                cp = self.first_slab  # slab width (7 or 6 live channels): see first_slab
             if name in FOLD:  # one scale for the folded filter and the plain one (its border pass)
                 wu = fold_up2x(w)
                 t = min(t, filter_scale(wu))  # max |W' * 2^t| and max |W * 2^t| both <= 2^12
@@ -269,7 +277,8 @@ class Split3Forward:
         S = lambda lv, c: torch.empty((n, L[lv][0], L[lv][1], 2 * c), dtype=torch.float16, device=dev)  # noqa
         F = lambda lv, c: torch.empty((n, L[lv][0], L[lv][1], c), dtype=torch.float32, device=dev)  # noqa
         fs = self.first_slab
-        b = {"x": torch.zeros((n, L[0][0], L[0][1], 32 if fs == 8 else 3 * fs), dtype=torch.float16, device=dev),
+        # (slab 8: [l, h, h] + a zero 4th slab in one granule; wider: the two stored slabs [l, h], read as [l, h, h])
+        b = {"x": torch.zeros((n, L[0][0], L[0][1], 32 if fs == 8 else 2 * fs), dtype=torch.float16, device=dev),
              "s11": S(0, 64), "cat1": S(0, 128), "r4": S(0, 128),
              "p1": S(1, 64), "s21": S(1, 128), "cat2": S(1, 256), "r3": S(1, 256),
              "p2": S(2, 128), "s31": S(2, 256), "s32": S(2, 256), "cat3": S(2, 512), "r2": S(2, 512),
@@ -295,7 +304,8 @@ class Split3Forward:
         ovf = self.overflow
         ovf.zero_()
         fs = self.first_slab
-        split3h(x, b["x"][..., :fs], slab=fs, overflow=ovf)  # slabs [l, h, h] of fs channels (a 4th stays zero)
+        # channels 0..7 of each slab (the frame's 7 or 6 and zeros); the rest of the slabs stay zero from allocation
+        split3h(x, b["x"][..., :8], slab=fs, overflow=ovf)
 
         def conv(src, name, dst_f32, act="relu", splitk=True):
             return conv_f32(src, C[name], dst_f32, act, splitk)
@@ -355,12 +365,14 @@ class Split3Forward:
         alpha = b["out"] if out is None else out
         lg0 = b["lg0"]
         logits = f0[..., :1]
-        for k, (xs, yv, acc) in enumerate(((b["cat1"], lg0, None), (b["cat1"][..., 128:], logits, lg0))):
+        chunks = (((b["cat1"], logits, None),) if self.head_fused else
+                  ((b["cat1"], lg0, None), (b["cat1"][..., 128:], logits, lg0)))
+        for k, (xs, yv, acc) in enumerate(chunks):
             pc = self.head[k]
             xv, yvv = ops.nhwc(xs), ops.nhwc(yv)
             ops.check(ops.lib().vm_conv3x3_head_acc_ex_nhwc(
-                ops.ctypes.byref(xv), ops._ptr(pc.packed), xs.shape[-1], None, ops._ptr(pc.scale),
-                ops._ptr(pc.shift), ops._ptr(acc), ops.ctypes.byref(yvv), ops._ptr(alpha if k == 1 else None),
-                ops.stream_handle()), "conv3x3_head_acc_ex")
+                ops.ctypes.byref(xv), ops._ptr(pc.packed), pc.cin, None, ops._ptr(pc.scale),
+                ops._ptr(pc.shift), ops._ptr(acc), ops.ctypes.byref(yvv),
+                ops._ptr(alpha if k == len(chunks) - 1 else None), ops.stream_handle()), "conv3x3_head_acc_ex")
         self.logits = logits
         return alpha
