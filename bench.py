@@ -837,6 +837,7 @@ def train_image_bench(dev, steps, warmup, world, rank, threads, cpu=True, n=8, s
     e = ev.e
     ph = [sum(ms(e[4 * i + k], e[4 * i + k + 1]) for i in range(steps)) / steps for k in range(3)]
     dev_ms = sum(ph)
+    per_step = sorted(ms(e[4 * i], e[4 * i + 3]) for i in range(steps))
     fwd_f, bwd_f = trn.conv_flops(n, size, size)
     pk = PEAK_TFLOPS[dtype]
     tf = (fwd_f + bwd_f) / (dev_ms * 1e-3) / 1e12
@@ -848,6 +849,8 @@ def train_image_bench(dev, steps, warmup, world, rank, threads, cpu=True, n=8, s
            "samples_per_s": round(n * world / wall, 1), "ms_per_step": round(1000 * wall, 4),
            "device_ms": {"forward_loss": round(ph[0], 4), "backward": round(ph[1], 4),
                          "allreduce_adam_repack": round(ph[2], 4)},
+           "device_ms_per_step": {"min": round(per_step[0], 4), "median": round(per_step[len(per_step) // 2], 4),
+                                  "max": round(per_step[-1], 4)},
            "flops_per_step_per_gpu": {"forward": fwd_f, "backward": bwd_f},
            "roofline": {"bound": "mfma", "achieved": round(tf, 2), "peak": pk, "unit": "TFLOP/s",
                         "frac": round(tf / pk, 4),

@@ -5245,8 +5245,12 @@ static int dispatch_patch(ConvArgs& a, hipStream_t st) {
   }
 #endif
   // (a folded upconv takes the row-slot configs below, whose instantiation skips its phases' zero taps)
-  if (!(a.up && g_up_skip) && a.cout >= 128 && a.cin_pad >= 512 && sp * ((a.cout + 127) / 128) >= 1000)
+  if (!(a.up && g_up_skip) && a.cout >= 128 && a.cin_pad >= 512 && sp * ((a.cout + 127) / 128) >= 1000) {
+    // fp16 operands (the split x3 forward's upconv_2 / _3, K = 3 x cin): the 3-slot 64-channel ring measured faster
+    // (same box, patch_cfg 19 vs auto: 0.759 / 0.803 -> 0.732 / 0.754 ms, profiles/r06k_f16x3_patch_cfg_ab.log)
+    if (a.f16) return launch_patch_up<64, 8, 1, 3, 8, 1, 9, false, 0, false, 3>(a, st);
     return launch_patch_up<128, 4, 2, 3, 8, 2>(a, st);  // 64 px x 64 channel waves, 4 per SIMD (r02: -5% vs 4x1)
+  }
   if (persist_ok(a)) {  // the same tilings, persistent (2-slot ring: the LDS also holds the block's constants)
     const bool sk = a.up && g_up_skip;
     int rc = 1;
