@@ -1456,9 +1456,9 @@ def main():
     if args.video_frames > 0:
         vrec = video_batch(model, args.video_frames, H, W, rank, world, dev, args.video_chunk)
 
-    # each training / config-3 / loader / augment record starts from an idle GPU: measured (tools/img_interference.py, profiles/r06i_img_
-    # interference.log), the UNetImage step right after another heavy record runs 6.70 ms against 6.03 after a 5 s
-    # pause or alone (the card's clock / power state, not the code); the pause is outside every timed region
+    # each training / config-3 / loader / augment record starts from an idle GPU (no record inherits its predecessor's
+    # queued work); the pause is outside every timed region.  (It does not decide the UNetImage step's slow mode:
+    # DESIGN §3.9, profiles/r06m_img_trainer_instances.log)
     def cool():
         if args.cooldown > 0:
             torch.cuda.synchronize()
