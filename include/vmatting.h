@@ -261,6 +261,14 @@ int vm_resize_bilinear_tf1_nhwc(const vm_tensor* x, vm_tensor* y, void* stream);
  * (packs the caller's f32 [N,H,W,7] frame into the compute layout; loader.py:76-78 mean/shift
  * can be folded in via shift).  Channels >= x->c of y are zero-filled. */
 int vm_convert_nhwc(const vm_tensor* x, vm_tensor* y, const float* scale, const float* shift, int act, void* stream);
+/* A HIP stream created with a full CU mask (hipExtStreamCreateWithCUMask), for the trainers' side streams (the
+ * filter gradients beside the data-gradient chain, train.py:37-52 / 288-304): a plain stream shares one of the
+ * process's hardware queues, possibly the caller's, which serialises the two.  vm_stream_destroy releases it. */
+int vm_stream_create_masked(void** stream);
+int vm_stream_destroy(void* stream);
+/* One wave spinning for `microseconds` of the device wall clock on `stream`: the trainers' probe for a side stream
+ * that runs beside theirs (a plain stream may share the caller's hardware queue). */
+int vm_spin(int microseconds, void* stream);
 /* Split-bf16 x6 operand of an f32 activation (no reference counterpart: the operand format of the split-bf16 conv
  * path, which evaluates unet.py's tf.nn.conv2d (unet.py:39,60,70) at f32 accuracy on bf16 MFMA).  x (f32 view,
  * x.c channels) -> three bf16 parts h = bf16(x), m = bf16(x - h), l = bf16(x - h - m), written as six slabs

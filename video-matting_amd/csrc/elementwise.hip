@@ -1169,3 +1169,52 @@ extern "C" int vm_composite_image(const void* fg, const void* bg, int img_dtype,
   else launch_composite_a<double>(fg, bg, alpha, alpha_dtype, elems, cn, out, out_dtype, st);
   return check_launch("composite");
 }
+
+// A stream created with a full CU mask (hipExtStreamCreateWithCUMask).  A plain hipStream shares one of the process's
+// GPU_MAX_HW_QUEUES hardware queues, and which one it gets is not under the caller's control: kernel traces
+// (profiles/r06o_imgtrace_queues.txt) caught UNetImage trainers whose side stream sat on the caller's queue, which
+// serialises the filter gradients behind the data-gradient chain (backward 4.8 ms instead of 4.1).  A CU-masked
+// stream gets a queue of its own, but measured slower still (8.3 ms per step): kept for A/B, the trainers probe a
+// pooled stream instead (vm_spin below, ops.concurrent_stream).
+extern "C" int vm_stream_create_masked(void** stream) {
+  if (!stream) return vm::fail(VM_EINVAL, "stream_create_masked: NULL");
+  int dev = 0, ncu = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e == hipSuccess) e = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  if (e != hipSuccess || ncu <= 0) return vm::fail(VM_EHIP, "stream_create_masked: %s", hipGetErrorString(e));
+  uint32_t mask[64];
+  const int words = (ncu + 31) / 32;
+  if (words > 64) return vm::fail(VM_EUNSUPPORTED, "stream_create_masked: %d CUs", ncu);
+  for (int i = 0; i < words; ++i) mask[i] = 0xffffffffu;
+  hipStream_t s = nullptr;
+  e = hipExtStreamCreateWithCUMask(&s, (uint32_t)words, mask);
+  if (e != hipSuccess) return vm::fail(VM_EHIP, "hipExtStreamCreateWithCUMask: %s", hipGetErrorString(e));
+  *stream = reinterpret_cast<void*>(s);
+  return VM_OK;
+}
+
+extern "C" int vm_stream_destroy(void* stream) {
+  if (!stream) return vm::fail(VM_EINVAL, "stream_destroy: NULL");
+  const hipError_t e = hipStreamDestroy(reinterpret_cast<hipStream_t>(stream));
+  return e == hipSuccess ? VM_OK : vm::fail(VM_EHIP, "hipStreamDestroy: %s", hipGetErrorString(e));
+}
+
+// A kernel that holds one wave busy for `us` microseconds of the device's constant-rate wall clock: the probe that
+// tells whether a second stream runs beside the caller's (ops.concurrent_stream) — a short kernel queued on that
+// stream finishes while this one still spins only if the two streams sit on different hardware queues
+__global__ void spin_kernel(long long ticks) {
+  const long long t0 = wall_clock64();
+  while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+}
+
+extern "C" int vm_spin(int microseconds, void* stream) {
+  if (microseconds < 0 || microseconds > 1000000) return vm::fail(VM_EINVAL, "spin: %d us", microseconds);
+  int dev = 0, khz = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e == hipSuccess) e = hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev);
+  if (e != hipSuccess || khz <= 0) return vm::fail(VM_EHIP, "spin: wall clock rate: %s", hipGetErrorString(e));
+  hipLaunchKernelGGL(spin_kernel, dim3(1), dim3(64), 0, reinterpret_cast<hipStream_t>(stream),
+                     (long long)microseconds * khz / 1000);
+  return check_launch("spin");
+}
+

@@ -110,6 +110,9 @@ SIGNATURES = [
     ("vm_maxpool2x2_same_nhwc", c_int, [P, P, c_void_p]),
     ("vm_resize_bilinear_tf1_nhwc", c_int, [P, P, c_void_p]),
     ("vm_convert_nhwc", c_int, [P, P, c_void_p, c_void_p, c_int, c_void_p]),
+    ("vm_stream_create_masked", c_int, [ctypes.POINTER(c_void_p)]),
+    ("vm_stream_destroy", c_int, [c_void_p]),
+    ("vm_spin", c_int, [c_int, c_void_p]),
     ("vm_split6_nhwc", c_int, [P, P, P, c_void_p]),
     ("vm_split3h_nhwc", c_int, [P, P, P, c_int, c_void_p, c_void_p]),
     ("vm_resize_split3h_nhwc", c_int, [P, P, c_int, c_void_p, c_void_p]),

@@ -62,6 +62,11 @@ class ImageTrainer(TrainerBase):
     # filter gradients kept on the caller's stream: conv1_1's is the backward's last work and the data-gradient chain
     # (no dgrad for conv1_1) is idle by then, while the side stream still has the earlier layers' queued
     main_wgrad = ("conv1_1",)
+    # the side stream: "probe" (ops.concurrent_stream: a pooled stream checked to run beside the caller's; a plain one
+    # landed on the caller's hardware queue for 2 of 9 trainers, backward 4.8 ms instead of 4.1), or for A/B "pool"
+    # (the r05 form), "high" (high priority: 8.3 ms when it gets the high-priority queue), "masked" (a CU-masked
+    # stream: its own queue, 8.3 ms) — kernel traces in profiles/r06o_imgtrace_queues.txt
+    side_kind = "probe"
 
     def __init__(self, vgg16_npy_path=None, dtype="fp32", device="cuda", params=None, lr=1e-5, beta1=0.9,
                  beta2=0.999, epsilon=1e-8, streams=1):
@@ -108,7 +113,14 @@ class ImageTrainer(TrainerBase):
         # backward -> dgrad conv -> next layer), joined before the update.  Same kernels, same arithmetic; per-stream
         # workspaces (ops._workspace)
         dev_ = torch.device(device)
-        self._side = torch.cuda.Stream(device=dev_) if streams and dev_.type == "cuda" else None
+        self._side = None
+        if streams and dev_.type == "cuda":
+            if self.side_kind == "probe":  # a pooled stream probed to run beside the caller's (ops.concurrent_stream)
+                self._side = ops.concurrent_stream(dev_)
+            elif self.side_kind == "masked":  # (A/B) a CU-masked stream (ops.side_stream)
+                self._side = ops.side_stream(dev_)
+            else:  # (A/B) "pool": a torch pool stream (the r05 form); "high": a high-priority one
+                self._side = torch.cuda.Stream(device=dev_, priority=-1 if self.side_kind == "high" else 0)
         self._main = None
 
     def _refresh_packs(self):

@@ -528,6 +528,64 @@ def convert(x, out, scale=None, shift=None, act="none"):
 
 
 _ws_cache = {}
+_masked_streams = {}
+
+
+_beside = {}
+
+
+def _runs_beside(main, side, spin_us=1500):
+    """True when a short kernel queued on ``side`` finishes while one queued before it on ``main`` still spins."""
+    torch.cuda.synchronize(main.device)
+    check(lib().vm_spin(spin_us, ctypes.c_void_p(main.cuda_stream)), "spin")
+    e_main = torch.cuda.Event()
+    e_main.record(main)
+    check(lib().vm_spin(1, ctypes.c_void_p(side.cuda_stream)), "spin")
+    e_side = torch.cuda.Event()
+    e_side.record(side)
+    beside = False
+    while not e_main.query():
+        if e_side.query():
+            beside = True
+            break
+    torch.cuda.synchronize(main.device)
+    return beside
+
+
+def concurrent_stream(device, tries=8):
+    """A pooled torch stream that runs beside the caller's current stream of ``device``: a plain stream takes one of
+    the process's hardware queues (GPU_MAX_HW_QUEUES) with no say in which, and on the caller's own queue a side
+    stream's work is serialised behind the caller's (kernel traces).  Probed once per (device, current
+    stream) with vm_spin; the chosen stream is cached and shared."""
+    dev = torch.device(device)
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    main = torch.cuda.current_stream(idx)
+    key = (idx, main.cuda_stream)
+    s = _beside.get(key)
+    if s is None:
+        for _ in range(tries):
+            s = torch.cuda.Stream(device=torch.device("cuda", idx))
+            if _runs_beside(main, s):
+                break
+        _beside[key] = s  # (after `tries` misses: the last one; the step is then only slower, never wrong)
+    return s
+
+
+def side_stream(device, slot=0):
+    """A CU-masked side stream of ``device`` (vm_stream_create_masked), one per ``slot``, created once per process and
+    shared by the trainers that ask for that slot.  A plain torch stream takes one of the process's hardware queues
+    without a say in which: a kernel trace caught a UNetImage trainer whose side stream sat on the caller's queue,
+    serialising its filter gradients behind the data-gradient chain."""
+    dev = torch.device(device)
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    s = _masked_streams.get((idx, slot))
+    if s is None:
+        ptr = ctypes.c_void_p()
+        with torch.cuda.device(idx):
+            check(lib().vm_stream_create_masked(ctypes.byref(ptr)), "stream_create_masked")
+        s = torch.cuda.ExternalStream(ptr.value, device=torch.device("cuda", idx))
+        _masked_streams[(idx, slot)] = s
+    return s
 
 
 def _workspace(nbytes, device):
