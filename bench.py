@@ -581,6 +581,13 @@ def step_roofline(flops, nbytes, dev_ms, peak_tflops):
                    "of the two instead (perfect overlap)"}
 
 
+def set_train_side(kind):
+    """--train-side: the config-5 trainer's side-stream kind (VideoTrainer.side_kind), set in the ranks only."""
+    if kind:
+        from vmatting.train import VideoTrainer
+        VideoTrainer.side_kind = kind
+
+
 def train_bench(dev, steps, warmup, world, rank, threads, cpu=True, n=8, size=320, dtype="bf16", graph=False,
                 streams=3, wgrad_stream=True):
     """BASELINE config 5: one train.py video_procedure iteration per step (train.py:288-343) — batch of 8 320x320
@@ -1328,6 +1335,9 @@ def main():
                     help="profiling passes: run just this record (rank 0 / N=1) and print it")
     ap.add_argument("--temporal-sizes", default="500x1200,1080x1920", help="config-3 sizes HxW, comma separated")
     ap.add_argument("--temporal-dtypes", default="fp32,bf16", help="config-3 compute dtypes, comma separated")
+    ap.add_argument("--train-side", default=None, choices=["pool", "probe"],
+                    help="config-5 trainer side streams: torch pool streams, or pool streams probed to run beside the "
+                         "caller's (VideoTrainer.side_kind; default: the class default)")
     ap.add_argument("--cooldown", type=float, default=5.0,
                     help="seconds of GPU idle before each training record (outside the timed regions)")
     ap.add_argument("--dummy-streams", type=int, default=0,
@@ -1376,6 +1386,7 @@ def main():
     _dummy = [torch.cuda.Stream(device=dev) for _ in range(args.dummy_streams)]  # noqa: F841 (study knob)
     if args.only:  # one record alone (rocprofv3 passes per record: tools/prof_bench.sh)
         if args.only == "train":
+            set_train_side(args.train_side)
             rec = train_bench(dev, args.steps, args.warmup, world, rank, threads, cpu=False, graph=args.train_graph,
                               streams=args.train_streams, wgrad_stream=bool(args.train_wgrad_stream))
         elif args.only == "train_chain":
@@ -1467,6 +1478,7 @@ def main():
     train = None
     if not args.no_train:  # every rank: the DDP all-reduce is part of the step
         cool()
+        set_train_side(args.train_side)
         train = train_bench(dev, max(args.steps // 4, 10), 3, world, rank, threads, cpu=not args.no_cpu_baseline,
                             graph=args.train_graph, streams=args.train_streams,
                             wgrad_stream=bool(args.train_wgrad_stream))

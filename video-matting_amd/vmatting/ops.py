@@ -552,6 +552,28 @@ def _runs_beside(main, side, spin_us=1500):
     return beside
 
 
+def concurrent_streams(device, n, tries=16):
+    """``n`` distinct pooled streams that each run beside the caller's current stream (as concurrent_stream; the
+    candidates that share the caller's hardware queue are skipped), cached per (device, caller stream, n)."""
+    dev = torch.device(device)
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    main = torch.cuda.current_stream(idx)
+    key = (idx, main.cuda_stream, "n", n)
+    got = _beside.get(key)
+    if got is None:
+        got, last = [], None
+        for _ in range(tries):
+            last = torch.cuda.Stream(device=torch.device("cuda", idx))
+            if _runs_beside(main, last):
+                got.append(last)
+                if len(got) == n:
+                    break
+        while len(got) < n:  # (the probe kept failing: plain pool streams, slower at worst, never wrong)
+            got.append(torch.cuda.Stream(device=torch.device("cuda", idx)))
+        _beside[key] = got
+    return list(got)
+
+
 def concurrent_stream(device, tries=8):
     """A pooled torch stream that runs beside the caller's current stream of ``device``: a plain stream takes one of
     the process's hardware queues (GPU_MAX_HW_QUEUES) with no say in which, and on the caller's own queue a side

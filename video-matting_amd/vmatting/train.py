@@ -145,6 +145,10 @@ class TrainerBase:
 class VideoTrainer(TrainerBase):
     """train.video_procedure's iteration on device (also simple_procedure's: pass diff = cmp - bg as ``warped``)."""
 
+    # the side streams: "pool" (torch pool streams, whatever hardware queue HIP gives them) or "probe" (pool streams
+    # checked to run beside the caller's stream, ops.concurrent_streams; A/B)
+    side_kind = "pool"
+
     def __init__(self, vgg16_npy_path=None, dtype="fp32", device="cuda", params=None, bn=None, lr=1e-3,
                  beta1=0.9, beta2=0.999, epsilon=1e-8, sync_bn=False, streams=3, stream_priority=0,
                  wgrad_stream=True):
@@ -160,12 +164,16 @@ class VideoTrainer(TrainerBase):
         # kernels, same arithmetic (bit-identical); events order them, also inside a captured graph.  SyncBN keeps
         # one stream (its collectives stay in one issue order)
         dev_ = torch.device(device)
-        self._side = [] if self.sync_bn or streams < 1 or dev_.type != "cuda" else \
-            [torch.cuda.Stream(device=dev_, priority=stream_priority) for _ in range(int(streams))]
+        probe = self.side_kind == "probe" and stream_priority == 0
+        nside = 0 if self.sync_bn or streams < 1 or dev_.type != "cuda" else int(streams)
+        pool = ops.concurrent_streams(dev_, nside + (1 if nside and wgrad_stream else 0)) if probe and nside else None
+        self._side = pool[:nside] if pool else \
+            [torch.cuda.Stream(device=dev_, priority=stream_priority) for _ in range(nside)]
         # the decoder chain's own filter gradients (output, conv*, upconv*) are leaves too: with side streams they run
         # on one more, beside the chain's BN backward -> data-gradient convs, joined before the update
-        self._wside = torch.cuda.Stream(device=dev_, priority=stream_priority) if self._side and wgrad_stream \
-            else None
+        self._wside = None
+        if self._side and wgrad_stream:
+            self._wside = pool[nside] if pool else torch.cuda.Stream(device=dev_, priority=stream_priority)
         self._capture_origin = None  # the stream a TrainGraph capture began on (see _check_capture_fork)
         dev = self.device
         # move the freshly drawn variables into the flat buffer and alias every consumer onto it
