@@ -3667,20 +3667,31 @@ __global__ __launch_bounds__(256) void conv3x3_head_mfma(HeadArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   T* sw = reinterpret_cast<T*>(smem);  // [9][cin_pad] tap-major
   const T* Wt = reinterpret_cast<const T*>(a.w);
-  for (int k = threadIdx.x; k < a.K_pad; k += 256) {
-    int tap, c;
-    if (a.chunk_major) {
-      const int g = k / GE;
-      if (g >= a.ng) continue;
-      const int cc = g / 9;
-      tap = g - cc * 9;
-      c = cc * GE + (k - g * GE);
-    } else {
-      if (k >= a.K9) continue;
-      tap = k / a.cin_pad;
-      c = k - tap * a.cin_pad;
+  if (sizeof(T) == 2 && a.chunk_major) {
+    // 16-byte pieces: 8 consecutive k of a granule are 8 consecutive channels of one tap (the element loop below
+    // issued 14 dependent 2-byte loads per thread for a 384-channel head before any pixel load)
+    const int nvec = a.ng * GE / 8;
+    for (int v = threadIdx.x; v < nvec; v += 256) {
+      const int k = v * 8, g = k / GE, cc = g / 9, tap = g - cc * 9;
+      *reinterpret_cast<uint4*>(sw + tap * a.cin_pad + cc * GE + (k - g * GE)) =
+          *reinterpret_cast<const uint4*>(Wt + k);
     }
-    sw[tap * a.cin_pad + c] = Wt[k];
+  } else {
+    for (int k = threadIdx.x; k < a.K_pad; k += 256) {
+      int tap, c;
+      if (a.chunk_major) {
+        const int g = k / GE;
+        if (g >= a.ng) continue;
+        const int cc = g / 9;
+        tap = g - cc * 9;
+        c = cc * GE + (k - g * GE);
+      } else {
+        if (k >= a.K9) continue;
+        tap = k / a.cin_pad;
+        c = k - tap * a.cin_pad;
+      }
+      sw[tap * a.cin_pad + c] = Wt[k];
+    }
   }
   __syncthreads();
 
