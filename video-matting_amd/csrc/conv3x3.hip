@@ -6261,12 +6261,19 @@ static int conv_impl(const vm_tensor* x, const void* packed, int cin, int cout, 
     const int nks = (g.cin_pad + 4 * ce - 1) / (4 * ce);
     // the split-fp16 x3 head over a two-slab [l, h] view of 128-channel slabs (cin 384 as [l, h, h]): one call
     if (f16 && xalias == 128 && nks == 12 && g_head_kernel == 0) {
+      // 16-row tiles: an 18 x 66 input window per 16 x 64 outputs (1.16x the tile's pixels, 1.29x for 8 rows); the
+      // per-pixel tap sums and the 9-tap epilogue are the same arithmetic whatever the tile: bit-identical
       constexpr int TW = 64;
-      const long tiles = (long)x->n * ((x->h + 7) / 8) * ((x->w + TW - 1) / TW);
+      const int th16 = g_head_th == 16 ? 16 : 8;
+      const long tiles = (long)x->n * ((x->h + th16 - 1) / th16) * ((x->w + TW - 1) / TW);
       if (tiles > 0x7fffffffL) return fail(VM_EUNSUPPORTED, "conv3x3 head: too many tiles");
-      snprintf(g_last_kernel, sizeof g_last_kernel, "vm::conv3x3_head_mfma<vm::f16_t, 8, %d, 12, true>", TW);
-      hipLaunchKernelGGL((conv3x3_head_mfma<f16_t, 8, TW, 12, true>), dim3(tiles), dim3(256),
-                         (size_t)9 * g.cin_pad * 2, st, h);
+      snprintf(g_last_kernel, sizeof g_last_kernel, "vm::conv3x3_head_mfma<vm::f16_t, %d, %d, 12, true>", th16, TW);
+      if (th16 == 16)
+        hipLaunchKernelGGL((conv3x3_head_mfma<f16_t, 16, TW, 12, true>), dim3(tiles), dim3(256),
+                           (size_t)9 * g.cin_pad * 2, st, h);
+      else
+        hipLaunchKernelGGL((conv3x3_head_mfma<f16_t, 8, TW, 12, true>), dim3(tiles), dim3(256),
+                           (size_t)9 * g.cin_pad * 2, st, h);
       return check_launch("conv3x3_head_mfma");
     }
     if ((head_part || y_acc || f16) && (g_head_kernel != 0 || nks > 8))
