@@ -3662,7 +3662,10 @@ __global__ __launch_bounds__(256) void conv3x3_head_mfma(HeadArgs a) {
   constexpr int KS = 4 * CE;  // channels per MFMA k-step
   constexpr int GE = 64 / sizeof(T);
   constexpr int IW = TW + 2, NPIX = (TH + 2) * IW, NG = (NPIX + 15) / 16;
-  constexpr int GB = 3;  // pixel groups whose loads are in flight together
+  // pixel groups whose loads are in flight together (ALIAS: 8 of the 12 k-steps' fragments are loaded, so the
+  // registers hold 4 groups)
+  constexpr int GB = ALIAS ? 4 : 3;
+  constexpr int NL = ALIAS ? 2 * (NKS / 3) : NKS;  // fragments loaded per pixel group
   __shared__ float ys[NG * 16 * 9];
   extern __shared__ __attribute__((aligned(16))) char smem[];
   T* sw = reinterpret_cast<T*>(smem);  // [9][cin_pad] tap-major
@@ -3713,7 +3716,7 @@ __global__ __launch_bounds__(256) void conv3x3_head_mfma(HeadArgs a) {
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<T*>(base), 0, 0x7ffffff0, 0x00020000);
 
   for (int g0 = wave * GB; g0 < NG; g0 += 4 * GB) {
-    uint4 xa[GB][NKS];
+    uint4 xa[GB][NL];
     float pv[GB][4];  // head split: the partials this lane adds (issued with the input loads, used after the MFMAs)
 #pragma unroll
     for (int u = 0; u < GB; ++u) {
@@ -3734,8 +3737,7 @@ __global__ __launch_bounds__(256) void conv3x3_head_mfma(HeadArgs a) {
       const bool ok = g0 + u < NG && j < NPIX && (unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W;
       const int pix = (lr * W + ww) * cs;
 #pragma unroll
-      for (int s = 0; s < NKS; ++s) {
-        if (ALIAS && s >= 2 * (NKS / 3)) break;  // the third range: the second's fragments
+      for (int s = 0; s < NL; ++s) {  // (ALIAS: the third range reuses the second's fragments)
         const int c = s * KS + ks * CE;
         const int off = (ok && c < cin) ? (pix + c) * (int)sizeof(T) : OOB;
         xa[u][s] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
@@ -3747,8 +3749,7 @@ __global__ __launch_bounds__(256) void conv3x3_head_mfma(HeadArgs a) {
       if (g0 + u >= NG) break;
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int s = 0; s < NKS; ++s)
-        mma16<T>(ALIAS && s >= 2 * (NKS / 3) ? xa[u][s - NKS / 3] : xa[u][s], wf[s], acc);
+      for (int s = 0; s < NKS; ++s) mma16<T>(xa[u][s < NL ? s : s - NKS / 3], wf[s], acc);
       if (col < 9) {
         const int p = (g0 + u) * 16 + 4 * ks;
 #pragma unroll
